@@ -1,0 +1,852 @@
+// C ABI implementation (include/dcp.h): context management, the one-off
+// mesh/DoF upload (patterns, colouring, scatter maps) and the hot-path calls.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/dcp.h"
+#include "context.h"
+#include "fe_tables.h"
+#include "mesh.h"
+#include "prm.h"
+
+using namespace dcp;
+
+struct dcp_ctx : Ctx {};
+
+namespace dcp {
+Ctx::~Ctx() {
+  free_workspaces(*this);
+  if (hpinned) (void)hipHostFree(hpinned);
+  ev_total.destroy();
+  ev_schur.destroy();
+  if (stream) (void)hipStreamDestroy(stream);
+}
+}  // namespace dcp
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
+template <class F>
+int guarded(dcp_ctx* ctx, F&& f) {
+  try {
+    return f();
+  } catch (const ApiError& e) {
+    if (ctx) ctx->err = e.msg;
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const DeviceError& e) {
+    std::string m = std::string("HIP error ") + hipGetErrorString(e.code) + " in " + e.what_expr +
+                    " (" + e.file + ":" + std::to_string(e.line) + ")";
+    if (ctx) ctx->err = m;
+    g_last_error = m;
+    return DCP_ERR_DEVICE;
+  } catch (const std::exception& e) {
+    if (ctx) ctx->err = e.what();
+    g_last_error = e.what();
+    return DCP_ERR_INVALID;
+  }
+}
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw ApiError{code, msg}; }
+
+void require(bool ok, int code, const std::string& msg) {
+  if (!ok) fail(code, msg);
+}
+
+// Sorted, de-duplicated union pattern: row r collects the `cols` entries of
+// every cell in which r appears among the `rows` entries.
+void union_pattern(int n_rows, int n_cells, const int32_t* rows, int kr, const int32_t* cols, int kc,
+                   std::vector<int32_t>& ptr, std::vector<int32_t>& col) {
+  std::vector<int64_t> cnt(size_t(n_rows) + 1, 0);
+  for (size_t i = 0; i < size_t(n_cells) * kr; ++i) cnt[rows[i] + 1] += kc;
+  for (int r = 0; r < n_rows; ++r) cnt[r + 1] += cnt[r];
+  std::vector<int32_t> tmp(static_cast<size_t>(cnt[n_rows]));
+  std::vector<int64_t> fillp(cnt.begin(), cnt.end() - 1);
+  for (int c = 0; c < n_cells; ++c)
+    for (int a = 0; a < kr; ++a) {
+      const int r = rows[size_t(c) * kr + a];
+      std::memcpy(&tmp[fillp[r]], &cols[size_t(c) * kc], kc * sizeof(int32_t));
+      fillp[r] += kc;
+    }
+  ptr.assign(size_t(n_rows) + 1, 0);
+  std::vector<int32_t> len(n_rows);
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (int r = 0; r < n_rows; ++r) {
+    auto b = tmp.begin() + cnt[r], e = tmp.begin() + cnt[r + 1];
+    std::sort(b, e);
+    len[r] = int32_t(std::unique(b, e) - b);
+  }
+  for (int r = 0; r < n_rows; ++r) ptr[r + 1] = ptr[r] + len[r];
+  col.resize(size_t(ptr[n_rows]));
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (int r = 0; r < n_rows; ++r)
+    std::copy(tmp.begin() + cnt[r], tmp.begin() + cnt[r] + len[r], col.begin() + ptr[r]);
+}
+
+void set_physics_dev(Ctx& c) {
+  const dcp_physics& p = c.hph;
+  c.ph.dt = p.time_step;
+  c.ph.nu_sys = p.time_step * p.one_over_reynolds;
+  c.ph.nu_pre = p.time_step * p.one_over_reynolds;
+  c.ph.beta = p.expansion_coefficient;
+  c.ph.T_ref = p.temperature_ref;
+  c.ph.grav_scale = p.gravity_scale;
+  c.ph.g = p.gravity_constant;
+  c.ph.coriolis_z = p.cuboid ? p.coriolis_scale * p.omega : 0.0;
+  c.ph.one_over_peclet = p.one_over_peclet;
+  c.ph.dt_T = p.time_step / p.nse_solver_interval;
+  c.ph.cuboid = p.cuboid;
+}
+
+double* field_ptr(Ctx& c, int field, size_t& n) {
+  switch (field) {
+    case DCP_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.nse_sol.p;
+    case DCP_OLD_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.old_nse.p;
+    case DCP_T_SOLUTION: n = size_t(c.n_T); return c.T_sol.p;
+    case DCP_OLD_T_SOLUTION: n = size_t(c.n_T); return c.old_T.p;
+    case DCP_NSE_RHS: n = size_t(c.n_u + c.n_p); return c.nse_rhs.p;
+    case DCP_T_RHS: n = size_t(c.n_T); return c.T_rhs.p;
+    default: fail(DCP_ERR_INVALID, "unknown state field " + std::to_string(field));
+  }
+}
+
+struct PhaseTimer {
+  Ctx& c;
+  double* out;
+  explicit PhaseTimer(Ctx& ctx, double* o) : c(ctx), out(o) {
+    DCP_HIP_CHECK(hipEventRecord(c.ev_total.a, c.stream));
+  }
+  void stop() {
+    DCP_HIP_CHECK(hipEventRecord(c.ev_total.b, c.stream));
+    DCP_HIP_CHECK(hipEventSynchronize(c.ev_total.b));
+    float ms = 0;
+    DCP_HIP_CHECK(hipEventElapsedTime(&ms, c.ev_total.a, c.ev_total.b));
+    *out = ms;
+  }
+};
+
+void need_ready(Ctx& c) {
+  require(c.have_physics, DCP_ERR_STATE, "dcp_set_physics has not been called");
+  require(c.have_mesh, DCP_ERR_STATE, "dcp_mesh_upload has not been called");
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcp_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* dcp_last_error(const dcp_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_last_error.c_str();
+}
+
+int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
+  return guarded(nullptr, [&] {
+    require(out != nullptr, DCP_ERR_INVALID, "out is NULL");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+      fail(DCP_ERR_DEVICE, "no HIP device available: the dcp hot path runs on MI355X only");
+    std::unique_ptr<dcp_ctx> c(new dcp_ctx());
+    if (cfg) c->cfg = *cfg;
+    if (c->cfg.world_size <= 0) c->cfg.world_size = 1;
+    require(c->cfg.world_size == 1, DCP_ERR_UNSUPPORTED,
+            "world_size > 1 needs the RCCL halo path (not built in this library version)");
+    require(c->cfg.device >= 0 && c->cfg.device < ndev, DCP_ERR_INVALID, "device ordinal out of range");
+    DCP_HIP_CHECK(hipSetDevice(c->cfg.device));
+    DCP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->ev_total.init();
+    c->ev_schur.init();
+    ensure_workspaces(*c);
+    *out = c.release();
+    return DCP_OK;
+  });
+}
+
+void dcp_ctx_destroy(dcp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->cfg.device);
+  delete ctx;
+}
+
+int dcp_set_physics(dcp_ctx* ctx, const dcp_physics* ph) {
+  return guarded(ctx, [&] {
+    require(ctx && ph, DCP_ERR_INVALID, "NULL argument");
+    require(ph->temperature_degree == 1, DCP_ERR_UNSUPPORTED,
+            "device temperature path implements FE_Q(1) (classic shell configuration)");
+    require(ph->nse_solver_interval >= 1, DCP_ERR_INVALID, "NSE solver interval must be >= 1");
+    ctx->hph = *ph;
+    set_physics_dev(*ctx);
+    ctx->have_physics = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_set_time_step(dcp_ctx* ctx, double dt) {
+  return guarded(ctx, [&] {
+    require(ctx && ctx->have_physics, DCP_ERR_STATE, "physics not set");
+    ctx->hph.time_step = dt;
+    set_physics_dev(*ctx);
+    return DCP_OK;
+  });
+}
+
+int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
+                    const int32_t* cell_T_dofs, const double* cell_geometry,
+                    const double* cell_diameter, int n_u, int n_p, int n_T,
+                    const dcp_constraints* nse_c, const dcp_constraints* T_c) {
+  return guarded(ctx, [&] {
+    require(ctx && cell_nse_dofs && cell_T_dofs && cell_geometry && cell_diameter, DCP_ERR_INVALID,
+            "NULL argument");
+    require(n_cells > 0 && n_u > 0 && n_u % 3 == 0 && n_p > 0 && n_T > 0, DCP_ERR_INVALID,
+            "invalid sizes");
+    Ctx& c = *ctx;
+    DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
+    const int nv = n_u / 3;
+    // ---- FESystem cell dofs -> node map (velocity dofs must be 3*node + comp)
+    std::vector<int32_t> q2(size_t(n_cells) * 27), pd(size_t(n_cells) * 8), td(size_t(n_cells) * 8);
+    std::vector<double> xyz(size_t(nv) * 3, 0.0);
+    std::vector<char> seen(nv, 0);
+    for (int cell = 0; cell < n_cells; ++cell) {
+      const int32_t* d = cell_nse_dofs + size_t(cell) * kNseDofs;
+      for (int i = 0; i < kNseDofs; ++i) {
+        const SysDof s = system_dof(i);
+        if (s.comp < 3) {
+          require(d[i] >= 0 && d[i] < n_u && d[i] % 3 == s.comp, DCP_ERR_UNSUPPORTED,
+                  "velocity dofs must be node-interleaved (3*node + component), as after "
+                  "DoFRenumbering::component_wise({0,0,0,1})");
+          const int node = d[i] / 3;
+          if (s.comp == 0) {
+            q2[size_t(cell) * 27 + s.lex] = node;
+            if (!seen[node]) {
+              seen[node] = 1;
+              for (int k = 0; k < 3; ++k)
+                xyz[3 * size_t(node) + k] = cell_geometry[(size_t(cell) * 27 + s.lex) * 3 + k];
+            }
+          } else {
+            require(q2[size_t(cell) * 27 + s.lex] == node, DCP_ERR_UNSUPPORTED,
+                    "velocity components of one support point must share a node");
+          }
+        } else {
+          require(d[i] >= n_u && d[i] < n_u + n_p, DCP_ERR_INVALID, "pressure dof out of range");
+          pd[size_t(cell) * 8 + s.lex] = d[i] - n_u;
+        }
+      }
+      for (int v = 0; v < 8; ++v) {
+        const int t = cell_T_dofs[size_t(cell) * 8 + v];
+        require(t >= 0 && t < n_T, DCP_ERR_INVALID, "temperature dof out of range");
+        td[size_t(cell) * 8 + v] = t;
+      }
+    }
+    for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
+    // ---- constraints -> node-local form
+    std::vector<NodeConstraint> vc(nv, NodeConstraint{{0, 0, 0}, 0, -1});
+    std::vector<int> fixed_count(nv, 0);
+    if (nse_c) {
+      for (int l = 0; l < nse_c->n_lines; ++l) {
+        const int dof = nse_c->line_dof[l];
+        require(dof >= 0 && dof < n_u, DCP_ERR_UNSUPPORTED, "pressure constraints are not supported");
+        require(nse_c->inhomogeneity[l] == 0.0, DCP_ERR_UNSUPPORTED,
+                "inhomogeneous velocity constraints are not supported");
+        const int node = dof / 3, comp = dof % 3;
+        const int b = nse_c->entry_ptr[l], e = nse_c->entry_ptr[l + 1];
+        if (b == e) {
+          fixed_count[node]++;
+          continue;
+        }
+        require(vc[node].type == 0, DCP_ERR_UNSUPPORTED, "two constraint lines on one node");
+        vc[node].type = 2;
+        vc[node].k = comp;
+        for (int k = b; k < e; ++k) {
+          const int t = nse_c->entry_dof[k];
+          require(t / 3 == node && t % 3 != comp, DCP_ERR_UNSUPPORTED,
+                  "constraint couples dofs of different support points (periodic / hanging "
+                  "nodes are not supported by the device path)");
+          vc[node].w[t % 3] = nse_c->entry_w[k];
+        }
+      }
+      for (int k = 0; k < nv; ++k) {
+        if (fixed_count[k] == 0) continue;
+        if (fixed_count[k] == 3 && vc[k].type == 0) {
+          vc[k].type = 1;
+        } else if (fixed_count[k] == 1 && vc[k].type == 0) {
+          fail(DCP_ERR_UNSUPPORTED, "single fixed velocity component (not a no-slip node)");
+        } else {
+          fail(DCP_ERR_UNSUPPORTED, "mixed velocity constraints on one node");
+        }
+      }
+    }
+    std::vector<uint8_t> Tfix(n_T, 0);
+    std::vector<double> Tbc(n_T, 0.0);
+    if (T_c)
+      for (int l = 0; l < T_c->n_lines; ++l) {
+        const int dof = T_c->line_dof[l];
+        require(dof >= 0 && dof < n_T, DCP_ERR_INVALID, "temperature constraint out of range");
+        require(T_c->entry_ptr[l] == T_c->entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
+                "temperature constraints must be Dirichlet lines");
+        Tfix[dof] = 1;
+        Tbc[dof] = T_c->inhomogeneity[l];
+      }
+    // ---- colouring (greedy over vertex-sharing cells; tree order)
+    std::vector<int32_t> vptr, vcells;
+    {
+      std::vector<int32_t> cnt(size_t(n_p) + 1, 0);
+      for (size_t i = 0; i < pd.size(); ++i) cnt[pd[i] + 1]++;
+      for (int v = 0; v < n_p; ++v) cnt[v + 1] += cnt[v];
+      vcells.resize(pd.size());
+      std::vector<int32_t> f(cnt.begin(), cnt.end() - 1);
+      for (int cell = 0; cell < n_cells; ++cell)
+        for (int v = 0; v < 8; ++v) vcells[f[pd[size_t(cell) * 8 + v]]++] = cell;
+      vptr.swap(cnt);
+    }
+    std::vector<int> color(n_cells, -1);
+    int n_colors = 0;
+    for (int cell = 0; cell < n_cells; ++cell) {
+      uint64_t used = 0;
+      for (int v = 0; v < 8; ++v) {
+        const int p = pd[size_t(cell) * 8 + v];
+        for (int k = vptr[p]; k < vptr[p + 1]; ++k) {
+          const int o = vcells[k];
+          if (color[o] >= 0) used |= (uint64_t(1) << color[o]);
+        }
+      }
+      int col = 0;
+      while (col < 64 && (used >> col) & 1) ++col;
+      require(col < 64, DCP_ERR_UNSUPPORTED, "cell colouring needs more than 64 colours");
+      color[cell] = col;
+      n_colors = std::max(n_colors, col + 1);
+    }
+    c.color_ptr.assign(n_colors + 1, 0);
+    for (int cell = 0; cell < n_cells; ++cell) c.color_ptr[color[cell] + 1]++;
+    for (int k = 0; k < n_colors; ++k) c.color_ptr[k + 1] += c.color_ptr[k];
+    std::vector<int32_t> ccells(n_cells);
+    {
+      std::vector<int> f(c.color_ptr.begin(), c.color_ptr.end() - 1);
+      for (int cell = 0; cell < n_cells; ++cell) ccells[f[color[cell]]++] = cell;
+    }
+    // ---- patterns
+    std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc;
+    union_pattern(nv, n_cells, q2.data(), 27, q2.data(), 27, Ap, Ac);
+    union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, Btp, Btc);
+    union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, Bp, Bc);
+    union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, Tp, Tc);
+    // ---- upload
+    c.n_cells = n_cells;
+    c.n_u = n_u;
+    c.n_p = n_p;
+    c.n_T = n_T;
+    c.n_vnodes = nv;
+    c.cell_q2.upload(q2);
+    c.cell_p.upload(pd);
+    c.cell_T.upload(td);
+    c.xyz.upload(xyz);
+    c.diameter.upload(std::vector<double>(cell_diameter, cell_diameter + n_cells));
+    c.vcon.upload(vc);
+    c.T_fixed.upload(Tfix);
+    c.T_bc.upload(Tbc);
+    c.color_cells.upload(ccells);
+    c.A_ptr.upload(Ap);
+    c.A_col.upload(Ac);
+    c.Bt_ptr.upload(Btp);
+    c.Bt_col.upload(Btc);
+    c.B_ptr.upload(Bp);
+    c.B_col.upload(Bc);
+    c.T_ptr.upload(Tp);
+    c.T_col.upload(Tc);
+    c.A_val.alloc(Ac.size() * 9);
+    c.Bt_val.alloc(Btc.size() * 3);
+    c.B_val.alloc(Bc.size() * 3);
+    c.Tmass.alloc(Tc.size());
+    c.Tstiff.alloc(Tc.size());
+    c.Tmat.alloc(Tc.size());
+    c.posA.alloc(size_t(n_cells) * 729);
+    c.posBt.alloc(size_t(n_cells) * 216);
+    c.posB.alloc(size_t(n_cells) * 216);
+    c.posT.alloc(size_t(n_cells) * 64);
+    launch_build_scatter_maps(c.cd(), c.A_ptr.p, c.A_col.p, c.Bt_ptr.p, c.Bt_col.p, c.B_ptr.p,
+                              c.B_col.p, c.T_ptr.p, c.T_col.p, c.posA.p, c.posBt.p, c.posB.p,
+                              c.posT.p, c.stream);
+    const size_t nn = size_t(n_u + n_p);
+    c.nse_sol.alloc(nn);
+    c.old_nse.alloc(nn);
+    c.nse_rhs.alloc(nn);
+    c.T_sol.alloc(n_T);
+    c.old_T.alloc(n_T);
+    c.T_rhs.alloc(n_T);
+    for (auto* b : {&c.nse_sol, &c.old_nse, &c.nse_rhs, &c.T_sol, &c.old_T, &c.T_rhs}) b->zero(c.stream);
+    c.A_diag.alloc(n_u);
+    c.Mp_diag.alloc(n_p);
+    c.A_inv.alloc(n_u);
+    c.Mp_inv.alloc(n_p);
+    c.T_inv.alloc(n_T);
+    c.schur_tmp1.alloc(n_u);
+    c.schur_tmp2.alloc(n_u);
+    c.utmp.alloc(n_u);
+    c.fg_aux.alloc(nn);
+    free_workspaces(c);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.have_mesh = true;
+    c.nse_assembled = c.precond_built = c.T_matrix_ok = c.T_rhs_ok = false;
+    return DCP_OK;
+  });
+}
+
+int dcp_state_set(dcp_ctx* ctx, int field, const double* host, size_t n) {
+  return guarded(ctx, [&] {
+    require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
+    size_t want = 0;
+    double* p = field_ptr(*ctx, field, want);
+    require(n == want, DCP_ERR_INVALID, "state size mismatch");
+    DCP_HIP_CHECK(hipMemcpyAsync(p, host, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_state_get(dcp_ctx* ctx, int field, double* host, size_t n) {
+  return guarded(ctx, [&] {
+    require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
+    size_t want = 0;
+    double* p = field_ptr(*ctx, field, want);
+    require(n == want, DCP_ERR_INVALID, "state size mismatch");
+    DCP_HIP_CHECK(hipMemcpyAsync(host, p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_state_copy(dcp_ctx* ctx, int dst_field, int src_field) {
+  return guarded(ctx, [&] {
+    require(ctx && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
+    size_t nd = 0, ns = 0;
+    double* d = field_ptr(*ctx, dst_field, nd);
+    double* s = field_ptr(*ctx, src_field, ns);
+    require(nd == ns, DCP_ERR_INVALID, "state size mismatch");
+    copy(int(nd), s, d, ctx->stream);
+    return DCP_OK;
+  });
+}
+
+double* dcp_state_device_ptr(dcp_ctx* ctx, int field) {
+  if (!ctx || !ctx->have_mesh) return nullptr;
+  size_t n = 0;
+  try {
+    return field_ptr(*ctx, field, n);
+  } catch (...) {
+    return nullptr;
+  }
+}
+
+int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    PhaseTimer t(c, &c.timings.assemble_nse_ms);
+    NseOut out{};
+    if (flags & DCP_ASSEMBLE_MATRIX) {
+      c.A_val.zero(c.stream);
+      c.Bt_val.zero(c.stream);
+      c.B_val.zero(c.stream);
+      out.A = c.A_val.p;
+      out.Bt = c.Bt_val.p;
+      out.B = c.B_val.p;
+    }
+    if (flags & DCP_ASSEMBLE_RHS) {
+      c.nse_rhs.zero(c.stream);
+      out.rhs = c.nse_rhs.p;
+    }
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
+                        c.old_T.p, c.ph, out, c.stream);
+    t.stop();
+    if (flags & DCP_ASSEMBLE_MATRIX) c.nse_assembled = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    PhaseTimer t(c, &c.timings.build_precond_ms);
+    c.A_diag.zero(c.stream);
+    c.Mp_diag.zero(c.stream);
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_nse_precond_diag(c.cd(), c.color_begin(k), c.color_size(k), c.ph, c.A_diag.p,
+                              c.Mp_diag.p, c.stream);
+    reciprocal(c.n_u, c.A_diag.p, c.A_inv.p, c.stream);
+    reciprocal(c.n_p, c.Mp_diag.p, c.Mp_inv.p, c.stream);
+    t.stop();
+    c.precond_built = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_assemble_temperature_matrix(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    PhaseTimer t(c, &c.timings.assemble_T_matrix_ms);
+    c.Tmass.zero(c.stream);
+    c.Tstiff.zero(c.stream);
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_T_matrix(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.ph, c.Tmass.p,
+                      c.Tstiff.p, c.stream);
+    t.stop();
+    c.T_matrix_ok = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.T_matrix_ok, DCP_ERR_STATE, "assemble the temperature matrices first");
+    PhaseTimer t(c, &c.timings.assemble_T_rhs_ms);
+    // T_matrix = M + dt/interval K ; Jacobi rebuilt (:975-986)
+    lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
+    csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
+    c.T_rhs.zero(c.stream);
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_T_rhs(c.cd(), c.color_begin(k), c.color_size(k), c.old_T.p, c.nse_sol.p, c.ph,
+                   c.T_rhs.p, c.stream);
+    t.stop();
+    c.T_rhs_ok = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.nse_assembled && c.precond_built, DCP_ERR_STATE,
+            "assemble_nse_system and build_nse_preconditioner must run first");
+    PhaseTimer t(c, &c.timings.solve_nse_ms);
+    c.time_schur = true;
+    c.schur_ms_total = 0;
+    c.schur_count = 0;
+    const int rc = solve_nse(c, outer, inner);
+    c.time_schur = false;
+    c.timings.schur_apply_ms_avg = c.schur_count ? c.schur_ms_total / c.schur_count : 0.0;
+    c.timings.schur_applies = c.schur_count;
+    t.stop();
+    return rc;
+  });
+}
+
+int dcp_solve_temperature(dcp_ctx* ctx, int* iters, double* T_range) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.T_rhs_ok, DCP_ERR_STATE, "assemble_temperature_rhs must run first");
+    PhaseTimer t(c, &c.timings.solve_T_ms);
+    const int rc = solve_temperature(c, iters, T_range);
+    t.stop();
+    return rc;
+  });
+}
+
+int dcp_max_velocity(dcp_ctx* ctx, double* out) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(out != nullptr, DCP_ERR_INVALID, "NULL out");
+    Ctx& c = *ctx;
+    velocity_stats(c.cd(), c.nse_sol.p, c.dscal.p + 262, c.stream);
+    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
+                                 hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    *out = c.hpinned[0];
+    return DCP_OK;
+  });
+}
+
+int dcp_cfl_number(dcp_ctx* ctx, double* out) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(out != nullptr, DCP_ERR_INVALID, "NULL out");
+    Ctx& c = *ctx;
+    velocity_stats(c.cd(), c.nse_sol.p, c.dscal.p + 262, c.stream);
+    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
+                                 hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    *out = c.hpinned[1];
+    return DCP_OK;
+  });
+}
+
+int dcp_advance_state(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    copy(c.n_u + c.n_p, c.nse_sol.p, c.old_nse.p, c.stream);
+    copy(c.n_T, c.T_sol.p, c.old_T.p, c.stream);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_nse_vmult(dcp_ctx* ctx, const double* src, double* dst) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(ctx->nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
+    nse_vmult(*ctx, src, dst);
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_schur_vmult(dcp_ctx* ctx, const double* src, double* dst) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(ctx->nse_assembled && ctx->precond_built, DCP_ERR_STATE, "operator not ready");
+    schur_vmult(*ctx, src, dst);
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_block_preconditioner_vmult(dcp_ctx* ctx, const double* src, double* dst, int do_solve_A,
+                                   int* inner) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(ctx->nse_assembled && ctx->precond_built, DCP_ERR_STATE, "operator not ready");
+    const int rc = block_preconditioner_vmult(*ctx, src, dst, do_solve_A != 0, inner);
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return rc;
+  });
+}
+
+int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(nnz != nullptr, DCP_ERR_INVALID, "NULL nnz");
+    auto down_i = [&](const DBuf<int32_t>& b) {
+      std::vector<int32_t> h(b.n);
+      DCP_HIP_CHECK(hipMemcpy(h.data(), b.p, b.n * sizeof(int32_t), hipMemcpyDeviceToHost));
+      return h;
+    };
+    auto down_d = [&](const DBuf<double>& b) {
+      std::vector<double> h(b.n);
+      DCP_HIP_CHECK(hipMemcpy(h.data(), b.p, b.n * sizeof(double), hipMemcpyDeviceToHost));
+      return h;
+    };
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    const auto Ap = down_i(c.A_ptr), Ac = down_i(c.A_col), Btp = down_i(c.Bt_ptr),
+               Btc = down_i(c.Bt_col), Bp = down_i(c.B_ptr), Bc = down_i(c.B_col);
+    const int64_t total =
+        int64_t(Ap[c.n_vnodes]) * 9 + int64_t(Btp[c.n_vnodes]) * 3 + int64_t(Bp[c.n_p]) * 3;
+    *nnz = total;
+    if (!rowptr) return DCP_OK;
+    require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
+    const auto Av = down_d(c.A_val), Btv = down_d(c.Bt_val), Bv = down_d(c.B_val);
+    int64_t k = 0;
+    rowptr[0] = 0;
+    for (int n = 0; n < c.n_vnodes; ++n)
+      for (int r = 0; r < 3; ++r) {
+        for (int b = Ap[n]; b < Ap[n + 1]; ++b)
+          for (int cc = 0; cc < 3; ++cc) {
+            cols[k] = 3 * Ac[b] + cc;
+            vals[k++] = Av[9 * size_t(b) + 3 * r + cc];
+          }
+        for (int b = Btp[n]; b < Btp[n + 1]; ++b) {
+          cols[k] = c.n_u + Btc[b];
+          vals[k++] = Btv[3 * size_t(b) + r];
+        }
+        rowptr[3 * n + r + 1] = int32_t(k);
+      }
+    for (int v = 0; v < c.n_p; ++v) {
+      for (int b = Bp[v]; b < Bp[v + 1]; ++b)
+        for (int cc = 0; cc < 3; ++cc) {
+          cols[k] = 3 * Bc[b] + cc;
+          vals[k++] = Bv[3 * size_t(b) + cc];
+        }
+      rowptr[c.n_u + v + 1] = int32_t(k);
+    }
+    return DCP_OK;
+  });
+}
+
+int dcp_T_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(nnz != nullptr, DCP_ERR_INVALID, "NULL nnz");
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<int32_t> Tp(c.T_ptr.n);
+    DCP_HIP_CHECK(hipMemcpy(Tp.data(), c.T_ptr.p, Tp.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    *nnz = Tp[c.n_T];
+    if (!rowptr) return DCP_OK;
+    require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
+    std::copy(Tp.begin(), Tp.begin() + c.n_T + 1, rowptr);
+    DCP_HIP_CHECK(hipMemcpy(cols, c.T_col.p, size_t(Tp[c.n_T]) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(vals, c.Tmat.p, size_t(Tp[c.n_T]) * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_precond_diagonals(dcp_ctx* ctx, double* A_diag, double* Mp_diag) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(ctx->precond_built, DCP_ERR_STATE, "preconditioner not built");
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (A_diag)
+      DCP_HIP_CHECK(hipMemcpy(A_diag, ctx->A_diag.p, ctx->n_u * sizeof(double), hipMemcpyDeviceToHost));
+    if (Mp_diag)
+      DCP_HIP_CHECK(hipMemcpy(Mp_diag, ctx->Mp_diag.p, ctx->n_p * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(K && f && first >= 0 && n > 0 && first + n <= c.n_cells, DCP_ERR_INVALID,
+            "bad cell range");
+    DBuf<double> dK, df;
+    dK.alloc(size_t(n) * 89 * 89);
+    df.alloc(size_t(n) * 89);
+    launch_nse_system_elements(c.cd(), first, n, c.old_nse.p, c.old_T.p, c.ph, dK.p, df.p, c.stream);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    DCP_HIP_CHECK(hipMemcpy(K, dK.p, dK.n * sizeof(double), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(f, df.p, df.n * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out) {
+  if (!ctx || !out) return DCP_ERR_INVALID;
+  *out = ctx->timings;
+  return DCP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Host setup helpers
+
+struct dcp_host_mesh {
+  Mesh mesh;
+  Constraints nse, T;
+  TemperatureDofs tdofs;
+  std::vector<int32_t> cell_nse;
+  std::vector<double> cell_geom;
+};
+
+dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
+                                    int temperature_degree) {
+  try {
+    auto h = std::make_unique<dcp_host_mesh>();
+    h->mesh = cuboid ? build_cube(refine, length) : build_shell(refine, R0 / length, R1 / length);
+    h->nse = nse_constraints(h->mesh);
+    h->T = temperature_constraints(h->mesh, temperature_degree);
+    h->tdofs = temperature_dofs(h->mesh, temperature_degree);
+    h->cell_nse = nse_cell_dofs_dealii(h->mesh);
+    const Mesh& m = h->mesh;
+    h->cell_geom.resize(size_t(m.n_cells) * 81);
+    for (int c = 0; c < m.n_cells; ++c)
+      for (int l = 0; l < 27; ++l)
+        for (int d = 0; d < 3; ++d)
+          h->cell_geom[(size_t(c) * 27 + l) * 3 + d] = m.xyz[3 * size_t(m.cell_q2[27 * size_t(c) + l]) + d];
+    return h.release();
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void dcp_host_mesh_destroy(dcp_host_mesh* m) { delete m; }
+
+static dcp_constraints view_of(const Constraints& c) {
+  dcp_constraints v;
+  v.n_lines = c.n_lines();
+  v.line_dof = c.line_dof.data();
+  v.entry_ptr = c.entry_ptr.data();
+  v.entry_dof = c.entry_dof.data();
+  v.entry_w = c.entry_w.data();
+  v.inhomogeneity = c.inhomogeneity.data();
+  return v;
+}
+
+int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
+  if (!h || !out) return DCP_ERR_INVALID;
+  const Mesh& m = h->mesh;
+  out->n_cells = m.n_cells;
+  out->n_u = m.n_u();
+  out->n_p = m.n_p();
+  out->n_T = h->tdofs.n_dofs;
+  out->n_vnodes = m.n_vnodes;
+  out->cell_nse_dofs = h->cell_nse.data();
+  out->cell_T_dofs = h->tdofs.cell_dofs.data();
+  out->cell_geometry = h->cell_geom.data();
+  out->cell_diameter = m.cell_diameter.data();
+  out->node_xyz = m.xyz.data();
+  out->nse = view_of(h->nse);
+  out->T = view_of(h->T);
+  return DCP_OK;
+}
+
+int dcp_host_mesh_initial_temperature(const dcp_host_mesh* h, double* T) {
+  if (!h || !T) return DCP_ERR_INVALID;
+  for (int d = 0; d < h->tdofs.n_dofs; ++d)
+    T[d] = temperature_initial(h->mesh, &h->mesh.xyz[3 * size_t(h->tdofs.dof_vnode[d])]);
+  return DCP_OK;
+}
+
+int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len) {
+  try {
+    if (!path || !out) throw std::invalid_argument("NULL argument");
+    Parameters p;
+    p.parse(PrmFile::read(path));
+    const double L = p.reference_quantities.length, U = p.reference_quantities.velocity;
+    dcp_physics& ph = out->physics;
+    ph.time_step = p.time_step;
+    ph.one_over_reynolds = 1.0 / p.reynolds();
+    ph.one_over_peclet = 1.0 / p.peclet();
+    ph.expansion_coefficient = p.physical_constants.expansion_coefficient;
+    ph.temperature_ref = p.reference_quantities.temperature_ref;
+    ph.gravity_scale = L / (U * U);
+    ph.gravity_constant = p.physical_constants.gravity_constant;
+    ph.coriolis_scale = L / U;
+    ph.omega = p.physical_constants.omega;
+    ph.cuboid = p.cuboid_geometry ? 1 : 0;
+    ph.nse_solver_interval = int(p.NSE_solver_interval);
+    ph.temperature_degree = int(p.temperature_degree);
+    out->initial_global_refinement = int(p.initial_global_refinement);
+    out->space_dimension = int(p.space_dimension);
+    out->nse_velocity_degree = int(p.nse_velocity_degree);
+    out->use_schur_complement_solver = p.use_schur_complement_solver;
+    out->use_FEEC_solver = p.use_FEEC_solver;
+    out->adapt_time_step = p.adapt_time_step;
+    out->final_time = p.final_time;
+    out->R0 = p.physical_constants.R0;
+    out->R1 = p.physical_constants.R1;
+    out->length = L;
+    return DCP_OK;
+  } catch (const std::exception& e) {
+    if (err && err_len > 0) {
+      std::strncpy(err, e.what(), size_t(err_len) - 1);
+      err[err_len - 1] = 0;
+    }
+    return DCP_ERR_INVALID;
+  }
+}
+
+}  // extern "C"

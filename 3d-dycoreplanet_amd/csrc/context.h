@@ -1,0 +1,123 @@
+// Device-resident state of one dcp_ctx (one GPU / rank).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/dcp.h"
+#include "device.h"
+
+namespace dcp {
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  void alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+    n = count;
+  }
+  void upload(const std::vector<T>& h) {
+    alloc(h.size());
+    if (!h.empty()) DCP_HIP_CHECK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+  void zero(hipStream_t s) { DCP_HIP_CHECK(hipMemsetAsync(p, 0, n * sizeof(T), s)); }
+};
+
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  void init() {
+    DCP_HIP_CHECK(hipEventCreate(&a));
+    DCP_HIP_CHECK(hipEventCreate(&b));
+  }
+  void destroy() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    a = b = nullptr;
+  }
+};
+
+struct Ctx {
+  dcp_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  dcp_physics hph{};
+  PhysicsDev ph{};
+  bool have_physics = false, have_mesh = false;
+
+  int n_cells = 0, n_u = 0, n_p = 0, n_T = 0, n_vnodes = 0;
+  // mesh
+  DBuf<int32_t> cell_q2, cell_p, cell_T;
+  DBuf<double> xyz, diameter, T_bc;
+  DBuf<NodeConstraint> vcon;
+  DBuf<uint8_t> T_fixed;
+  std::vector<int> color_ptr;  // cells of colour k: color_cells[color_ptr[k] .. color_ptr[k+1])
+  DBuf<int32_t> color_cells;
+  // block-CSR patterns + values
+  DBuf<int32_t> A_ptr, A_col, Bt_ptr, Bt_col, B_ptr, B_col, T_ptr, T_col;
+  DBuf<double> A_val, Bt_val, B_val, Tmass, Tstiff, Tmat;
+  DBuf<int32_t> posA, posBt, posB, posT;
+  // state
+  DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;
+  DBuf<double> A_diag, Mp_diag, A_inv, Mp_inv, T_inv;
+  // scratch: reduction partials, device scalars
+  DBuf<double> partials, dscal;
+  double* hpinned = nullptr;   // pinned host mirror of small readbacks
+  bool nse_assembled = false, precond_built = false, T_matrix_ok = false, T_rhs_ok = false;
+  // Krylov workspaces (lazily sized)
+  std::vector<double*> fg_v, fg_z;   // FGMRES basis
+  DBuf<double> fg_aux;
+  std::vector<double*> sg_v;         // inner Schur GMRES basis (n_p)
+  DBuf<double> schur_tmp1, schur_tmp2, utmp;
+  std::vector<double*> ag_v;         // fallback A-GMRES basis (n_u)
+  DBuf<double> cg_g, cg_d, cg_h;
+  DBuf<double> coef;                 // multi_axpy coefficients
+  DBuf<const double*> ptrs;          // multi_axpy pointer table
+  dcp_timings timings{};
+  Timer ev_total, ev_schur;
+  double schur_ms_total = 0;
+  long schur_count = 0;
+  bool time_schur = false;
+
+  CellData cd() const {
+    CellData c;
+    c.n_cells = n_cells;
+    c.cell_q2 = cell_q2.p;
+    c.cell_p = cell_p.p;
+    c.cell_T = cell_T.p;
+    c.xyz = xyz.p;
+    c.vcon = vcon.p;
+    c.T_fixed = T_fixed.p;
+    c.T_bc = T_bc.p;
+    c.diameter = diameter.p;
+    return c;
+  }
+  ScatterMaps maps() const { return ScatterMaps{posA.p, posBt.p, posB.p, posT.p}; }
+  int n_colors() const { return int(color_ptr.size()) - 1; }
+  const int32_t* color_begin(int k) const { return color_cells.p + color_ptr[k]; }
+  int color_size(int k) const { return color_ptr[k + 1] - color_ptr[k]; }
+  ~Ctx();
+};
+
+// solver.cpp
+int solve_nse(Ctx& c, int* outer, int* inner);
+int solve_temperature(Ctx& c, int* iters, double* T_range);
+void nse_vmult(Ctx& c, const double* src, double* dst);
+void schur_vmult(Ctx& c, const double* src_p, double* dst_p);
+int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_solve_A,
+                               int* inner);
+void free_workspaces(Ctx& c);
+void ensure_workspaces(Ctx& c);
+
+}  // namespace dcp

@@ -1,0 +1,154 @@
+// Internal device interface: POD argument blocks and host-side launchers of
+// the HIP kernels (assembly.hip, linalg.hip). Host orchestration code
+// (api.cpp, solver.cpp) talks to the GPU only through these functions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dcp {
+
+#define DCP_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) throw dcp::DeviceError(#expr, _e, __FILE__, __LINE__);   \
+  } while (0)
+
+struct DeviceError {
+  const char* what_expr;
+  hipError_t code;
+  const char* file;
+  int line;
+  DeviceError(const char* w, hipError_t c, const char* f, int l)
+      : what_expr(w), code(c), file(f), line(l) {}
+};
+
+// Node-local constraint form of a velocity support point (the only shapes the
+// shell produces: homogeneous no-slip and no-normal-flux, both of which only
+// couple the 3 components of one node):
+//   type 0: unconstrained; 1: all 3 components fixed to 0;
+//   2: component k = sum_{d != k} w[d] u_d.
+struct NodeConstraint {
+  double w[3];
+  int32_t type;
+  int32_t k;
+};
+
+struct PhysicsDev {
+  double dt;            // time_step
+  double nu_sys;        // dt/Re: dt*(1/Re)*2*(eps:eps) = dt/Re*(delta grad.grad + d_c' s_a d_c s_b)
+  double nu_pre;        // dt/Re: preconditioner dt*(1/Re)*(grad:grad)
+  double beta, T_ref;
+  double grav_scale, g;
+  double coriolis_z;    // (L/U) * omega on the cuboid, else 0 (Q2)
+  double one_over_peclet;
+  double dt_T;          // dt / NSE_solver_interval (Q8)
+  int cuboid;
+};
+
+// Per-cell maps into the block-sparse global matrices (absolute entry index).
+struct ScatterMaps {
+  const int32_t* posA;   // [n_cells][27*27]  A block index of (a, b)
+  const int32_t* posBt;  // [n_cells][27*8]   Bt entry of (a, v)
+  const int32_t* posB;   // [n_cells][8*27]   B entry of (v, a)
+  const int32_t* posT;   // [n_cells][8*8]    T CSR entry of (i, j)
+};
+
+struct CellData {
+  int n_cells;
+  const int32_t* cell_q2;   // [n_cells][27] vnode ids (lexicographic)
+  const int32_t* cell_p;    // [n_cells][8]  pressure dofs (vertex order)
+  const int32_t* cell_T;    // [n_cells][8]  temperature dofs
+  const double* xyz;        // [n_vnodes][3]
+  const NodeConstraint* vcon;  // [n_vnodes]
+  const uint8_t* T_fixed;   // [n_T] 1 = Dirichlet
+  const double* T_bc;       // [n_T] inhomogeneity (valid where T_fixed)
+  const double* diameter;   // [n_cells]
+};
+
+struct NseOut {
+  double* A;     // [nnzb_A][9] or null
+  double* Bt;    // [nnz_Bt][3] or null
+  double* B;     // [nnz_B][3]  or null
+  double* rhs;   // velocity block of nse_rhs or null
+  double* elemK; // element mode: [n][89][89]
+  double* elemF; // element mode: [n][89]
+};
+
+// ---- assembly.hip ---------------------------------------------------------
+// Colour-wise NSE system assembly (cells of one colour share no node, so the
+// read-modify-write scatter needs no atomics and is deterministic).
+void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
+                       const double* u_old, const double* T_old, const PhysicsDev& ph,
+                       const NseOut& out, hipStream_t s);
+// Element mode: dense FESystem-ordered K/f of cells [first, first+n).
+void launch_nse_system_elements(const CellData& cd, int first, int n, const double* u_old,
+                                const double* T_old, const PhysicsDev& ph, double* K, double* f,
+                                hipStream_t s);
+void launch_nse_precond_diag(const CellData& cd, const int32_t* cells, int n, const PhysicsDev& ph,
+                             double* A_diag, double* Mp_diag, hipStream_t s);
+void launch_T_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
+                     const PhysicsDev& ph, double* Tmass, double* Tstiff, hipStream_t s);
+void launch_T_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
+                  const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
+// Builds posA/posBt/posB/posT by binary search in the sorted patterns.
+void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const int32_t* A_col,
+                               const int32_t* Bt_ptr, const int32_t* Bt_col, const int32_t* B_ptr,
+                               const int32_t* B_col, const int32_t* T_ptr, const int32_t* T_col,
+                               int32_t* posA, int32_t* posBt, int32_t* posB, int32_t* posT,
+                               hipStream_t s);
+
+// ---- linalg.hip -------------------------------------------------------------
+// y (=|+=) alpha * M x for block-CSR with R x C blocks (R,C in {1,3}).
+void spmv_bsr33(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s);
+void spmv_bsr31(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s);
+void spmv_bsr13(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s);
+void spmv_csr(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+              const double* x, double* y, bool add, hipStream_t s);
+
+// Scalars live in device memory ("device scalars") so Krylov kernels can
+// chain without host round trips. A coefficient argument is (ptr, mult):
+// value = mult * (ptr ? *ptr : 1).
+struct DScal {
+  const double* p;
+  double m;
+};
+// Partial-sum reduction buffer: kReduceBlocks doubles per slot.
+constexpr int kReduceBlocks = 512;
+// dot(a,b) -> *out (two launches, deterministic order)
+void dot(int n, const double* a, const double* b, double* partials, double* out, hipStream_t s);
+// v += c * x; then *out = v . w (w == v allowed) — deal.II add_and_dot
+void add_and_dot(int n, double* v, DScal c, const double* x, const double* w, double* partials,
+                 double* out, hipStream_t s);
+void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
+void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
+void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x
+void copy(int n, const double* x, double* y, hipStream_t s);
+void equ(int n, DScal c, const double* x, double* y, hipStream_t s);             // y = c x
+void axpby(int n, DScal a, const double* x, DScal b, double* y, hipStream_t s);  // y = a x + b y
+// *out = *num / *den (one thread)
+void scalar_div(const double* num, const double* den, double* out, hipStream_t s);
+void fill(int n, double v, double* y, hipStream_t s);
+void mul(int n, const double* a, const double* x, double* y, hipStream_t s);     // y = a .* x
+void reciprocal(int n, const double* a, double* y, hipStream_t s);                // y = 1/a
+// inv[r] = 1 / A(r,r) for a CSR matrix with sorted columns (Ifpack point Jacobi)
+void csr_diag_inverse(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                      double* inv, hipStream_t s);
+// y = sum_i coef[i] * X[i] (accumulated into y), X given as a device array of pointers
+void multi_axpy(int n, int k, const double* coef, const double* const* X, double* y,
+                hipStream_t s);
+// z = a + alpha * b (elementwise, e.g. T_matrix = M + dt K over one pattern)
+void lincomb(int n, const double* a, double alpha, const double* b, double* z, hipStream_t s);
+// constraints: velocity distribute (x_k = sum w x_d, Dirichlet -> 0)
+void distribute_velocity(int n_vnodes, const NodeConstraint* vcon, double* u, hipStream_t s);
+void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, double* T,
+                            hipStream_t s);
+// max |u_node| and max over cells of max(1e-10, max|u|)/diam -> out[0], out[1]
+void velocity_stats(const CellData& cd, const double* u, double* out2, hipStream_t s);
+// min/max of a vector -> out[0] = min, out[1] = max
+void minmax(int n, const double* x, double* out2, hipStream_t s);
+
+}  // namespace dcp

@@ -1,0 +1,400 @@
+// Sparse operator applies and Krylov BLAS-1 for CDNA4 (gfx950), FP64.
+//
+// Replaces the Trilinos/Epetra work under the reference's solvers
+// (boussinesq_model.tpp:1131-1245, 1417-1476; block_schur_preconditioner.hpp;
+// schur_complement.hpp): CSR SpMV of the nse_matrix blocks, Ifpack point
+// Jacobi, dot / add_and_dot / norms of deal.II's Krylov solvers.
+//
+// SpMV: block-CSR with RxC blocks; a group of G lanes (G | 64) owns one block
+// row, lanes stride over the row's blocks (contiguous RxC*8-byte loads),
+// shuffles reduce the R partial sums in a fixed order (deterministic).
+// Reductions: fixed-shape two-pass (kReduceBlocks partials, then one block),
+// so every dot product is bitwise reproducible run to run.
+#include <hip/hip_runtime.h>
+
+#include "../device.h"
+
+namespace dcp {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <int R, int C, int G>
+__global__ __launch_bounds__(kBlock) void k_spmv_bsr(int rows, const int32_t* __restrict__ ptr,
+                                                     const int32_t* __restrict__ col,
+                                                     const double* __restrict__ val,
+                                                     const double* __restrict__ x,
+                                                     double* __restrict__ y, int add) {
+  const int lane = threadIdx.x % G;
+  const long row = (long(blockIdx.x) * kBlock + threadIdx.x) / G;
+  if (row >= rows) return;  // whole group leaves together
+  double acc[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc[i] = 0.0;
+  const int e = ptr[row + 1];
+  for (int k = ptr[row] + lane; k < e; k += G) {
+    const size_t c = size_t(col[k]);
+    const double* v = val + size_t(k) * (R * C);
+    double xv[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) xv[j] = x[c * C + j];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < C; ++j) acc[i] += v[i * C + j] * xv[j];
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] += __shfl_xor(acc[i], off, G);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double* yp = y + size_t(row) * R + i;
+      *yp = add ? *yp + acc[i] : acc[i];
+    }
+  }
+}
+
+template <int R, int C, int G>
+void spmv(int rows, const int32_t* ptr, const int32_t* col, const double* val, const double* x,
+          double* y, bool add, hipStream_t s) {
+  if (rows <= 0) return;
+  const long threads = long(rows) * G;
+  const int grid = int((threads + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((k_spmv_bsr<R, C, G>), dim3(grid), dim3(kBlock), 0, s, rows, ptr, col, val, x,
+                     y, add ? 1 : 0);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+__device__ inline double block_sum(double v, double* sm) {
+  // wave reduce then LDS across the 4 waves; fixed order
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) sm[w] = v;
+  __syncthreads();
+  double r = 0;
+  if (threadIdx.x == 0) r = sm[0] + sm[1] + sm[2] + sm[3];
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dot_partial(int n, const double* __restrict__ a,
+                                                        const double* __restrict__ b,
+                                                        double* __restrict__ partials) {
+  __shared__ double sm[4];
+  double s = 0;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    s += a[i] * b[i];
+  const double r = block_sum(s, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = r;
+}
+
+// v += c x ; partial dot(v, w) (w may alias v)
+__global__ __launch_bounds__(kBlock) void k_add_and_dot(int n, double* v, DScal c,
+                                                        const double* __restrict__ x,
+                                                        const double* w, double* partials) {
+  __shared__ double sm[4];
+  const double cf = c.p ? c.m * (*c.p) : c.m;
+  double s = 0;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    const double nv = v[i] + cf * x[i];
+    v[i] = nv;
+    s += nv * (w == v ? nv : w[i]);
+  }
+  const double r = block_sum(s, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce_final(int nb, const double* __restrict__ partials,
+                                                         double* out) {
+  __shared__ double sm[4];
+  double s = 0;
+  for (int i = threadIdx.x; i < nb; i += kBlock) s += partials[i];
+  const double r = block_sum(s, sm);
+  if (threadIdx.x == 0) *out = r;
+}
+
+__global__ void k_axpy(int n, DScal c, const double* __restrict__ x, double* __restrict__ y) {
+  const double cf = c.p ? c.m * (*c.p) : c.m;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] += cf * x[i];
+}
+__global__ void k_scale(int n, DScal c, double* x) {
+  const double cf = c.p ? c.m * (*c.p) : c.m;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    x[i] *= cf;
+}
+__global__ void k_sadd(int n, double s, double a, const double* __restrict__ x, double* y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = s * y[i] + a * x[i];
+}
+__global__ void k_copy(int n, const double* __restrict__ x, double* __restrict__ y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = x[i];
+}
+__global__ void k_equ(int n, DScal c, const double* __restrict__ x, double* __restrict__ y) {
+  const double cf = c.p ? c.m * (*c.p) : c.m;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = cf * x[i];
+}
+__global__ void k_axpby(int n, DScal a, const double* __restrict__ x, DScal b, double* y) {
+  const double ca = a.p ? a.m * (*a.p) : a.m;
+  const double cb = b.p ? b.m * (*b.p) : b.m;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = cb * y[i] + ca * x[i];
+}
+__global__ void k_scalar_div(const double* num, const double* den, double* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *out = *num / *den;
+}
+__global__ void k_fill(int n, double v, double* y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = v;
+}
+__global__ void k_mul(int n, const double* __restrict__ a, const double* __restrict__ x,
+                      double* __restrict__ y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = x[i] * a[i];
+}
+__global__ void k_recip(int n, const double* __restrict__ a, double* __restrict__ y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] = 1.0 / a[i];
+}
+__global__ void k_csr_diag_inv(int rows, const int32_t* __restrict__ ptr,
+                               const int32_t* __restrict__ col, const double* __restrict__ val,
+                               double* __restrict__ inv) {
+  for (long r = long(blockIdx.x) * kBlock + threadIdx.x; r < rows; r += long(gridDim.x) * kBlock) {
+    int b = ptr[r], e = ptr[r + 1];
+    while (b < e) {
+      const int m = (b + e) >> 1;
+      if (col[m] < r) b = m + 1; else e = m;
+    }
+    inv[r] = 1.0 / val[b];
+  }
+}
+__global__ void k_lincomb(int n, const double* __restrict__ a, double alpha,
+                          const double* __restrict__ b, double* __restrict__ z) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    z[i] = a[i] + alpha * b[i];
+}
+__global__ void k_multi_axpy(int n, int k, const double* __restrict__ coef,
+                             const double* const* __restrict__ X, double* __restrict__ y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    double v = y[i];
+    for (int j = 0; j < k; ++j) v += coef[j] * X[j][i];
+    y[i] = v;
+  }
+}
+
+__global__ void k_distribute_velocity(int n, const NodeConstraint* __restrict__ vc, double* u) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    const NodeConstraint c = vc[i];
+    if (c.type == 1) {
+      u[3 * i] = u[3 * i + 1] = u[3 * i + 2] = 0.0;
+    } else if (c.type == 2) {
+      double v = 0;
+      for (int d = 0; d < 3; ++d)
+        if (d != c.k) v += c.w[d] * u[3 * i + d];
+      u[3 * i + c.k] = v;
+    }
+  }
+}
+
+__global__ void k_distribute_T(int n, const uint8_t* __restrict__ fixed, const double* __restrict__ bc,
+                               double* T) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    if (fixed[i]) T[i] = bc[i];
+}
+
+// non-negative doubles order like their bit patterns
+__device__ inline void atomic_max_nonneg(double* addr, double v) {
+  atomicMax(reinterpret_cast<unsigned long long*>(addr), __double_as_longlong(v));
+}
+
+__global__ __launch_bounds__(kBlock) void k_velocity_stats(CellData cd, const double* __restrict__ u,
+                                                           double* out2) {
+  __shared__ double sm[2][4];
+  const long c = long(blockIdx.x) * kBlock + threadIdx.x;
+  double mx = 0, cfl = 0;
+  if (c < cd.n_cells) {
+    double cm = 1e-10;  // get_cfl_number initialises the cell max with 1e-10
+    for (int n = 0; n < 27; ++n) {
+      const size_t b = 3 * size_t(cd.cell_q2[27 * c + n]);
+      const double v = sqrt(u[b] * u[b] + u[b + 1] * u[b + 1] + u[b + 2] * u[b + 2]);
+      mx = fmax(mx, v);
+      cm = fmax(cm, v);
+    }
+    cfl = cm / cd.diameter[c];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mx = fmax(mx, __shfl_xor(mx, off, 64));
+    cfl = fmax(cfl, __shfl_xor(cfl, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sm[0][threadIdx.x / 64] = mx;
+    sm[1][threadIdx.x / 64] = cfl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomic_max_nonneg(&out2[0], fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3])));
+    atomic_max_nonneg(&out2[1], fmax(fmax(sm[1][0], sm[1][1]), fmax(sm[1][2], sm[1][3])));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_minmax_partial(int n, const double* __restrict__ x,
+                                                           double* partials) {
+  __shared__ double sm[2][4];
+  double lo = 1.7976931348623157e308, hi = -1.7976931348623157e308;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    lo = fmin(lo, x[i]);
+    hi = fmax(hi, x[i]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off, 64));
+    hi = fmax(hi, __shfl_xor(hi, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sm[0][threadIdx.x / 64] = lo;
+    sm[1][threadIdx.x / 64] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = fmin(fmin(sm[0][0], sm[0][1]), fmin(sm[0][2], sm[0][3]));
+    partials[2 * blockIdx.x + 1] = fmax(fmax(sm[1][0], sm[1][1]), fmax(sm[1][2], sm[1][3]));
+  }
+}
+
+__global__ void k_minmax_final(int nb, const double* partials, double* out2) {
+  if (threadIdx.x != 0) return;
+  double lo = partials[0], hi = partials[1];
+  for (int i = 1; i < nb; ++i) {
+    lo = fmin(lo, partials[2 * i]);
+    hi = fmax(hi, partials[2 * i + 1]);
+  }
+  out2[0] = lo;
+  out2[1] = hi;
+}
+
+inline int grid_for(long n) {
+  long g = (n + kBlock - 1) / kBlock;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return int(g);
+}
+
+}  // namespace
+
+void spmv_bsr33(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s) {
+  spmv<3, 3, 32>(rows, ptr, col, val, x, y, add, s);
+}
+void spmv_bsr31(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s) {
+  spmv<3, 1, 8>(rows, ptr, col, val, x, y, add, s);
+}
+void spmv_bsr13(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                const double* x, double* y, bool add, hipStream_t s) {
+  spmv<1, 3, 32>(rows, ptr, col, val, x, y, add, s);
+}
+void spmv_csr(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+              const double* x, double* y, bool add, hipStream_t s) {
+  spmv<1, 1, 16>(rows, ptr, col, val, x, y, add, s);
+}
+
+void dot(int n, const double* a, const double* b, double* partials, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, a, b, partials);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, kReduceBlocks, partials, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void add_and_dot(int n, double* v, DScal c, const double* x, const double* w, double* partials,
+                 double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_and_dot, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, v, c, x, w,
+                     partials);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, kReduceBlocks, partials, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void axpy(int n, DScal c, const double* x, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, c, x, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void scale(int n, DScal c, double* x, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(kBlock), 0, s, n, c, x);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_sadd, dim3(grid_for(n)), dim3(kBlock), 0, s, n, s_, a, x, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void copy(int n, const double* x, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, x, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void equ(int n, DScal c, const double* x, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_equ, dim3(grid_for(n)), dim3(kBlock), 0, s, n, c, x, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void axpby(int n, DScal a, const double* x, DScal b, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x, b, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void scalar_div(const double* num, const double* den, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_scalar_div, dim3(1), dim3(64), 0, s, num, den, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void fill(int n, double v, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, n, v, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void mul(int n, const double* a, const double* x, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_mul, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, x, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void reciprocal(int n, const double* a, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_recip, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void csr_diag_inverse(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                      double* inv, hipStream_t s) {
+  hipLaunchKernelGGL(k_csr_diag_inv, dim3(grid_for(rows)), dim3(kBlock), 0, s, rows, ptr, col, val,
+                     inv);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void multi_axpy(int n, int k, const double* coef, const double* const* X, double* y,
+                hipStream_t s) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(k_multi_axpy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, coef, X, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void lincomb(int n, const double* a, double alpha, const double* b, double* z, hipStream_t s) {
+  hipLaunchKernelGGL(k_lincomb, dim3(grid_for(n)), dim3(kBlock), 0, s, n, a, alpha, b, z);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void distribute_velocity(int n_vnodes, const NodeConstraint* vcon, double* u, hipStream_t s) {
+  hipLaunchKernelGGL(k_distribute_velocity, dim3(grid_for(n_vnodes)), dim3(kBlock), 0, s, n_vnodes,
+                     vcon, u);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, double* T,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_distribute_T, dim3(grid_for(n_T)), dim3(kBlock), 0, s, n_T, fixed, bc, T);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void velocity_stats(const CellData& cd, const double* u, double* out2, hipStream_t s) {
+  DCP_HIP_CHECK(hipMemsetAsync(out2, 0, 2 * sizeof(double), s));
+  const int grid = (cd.n_cells + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_velocity_stats, dim3(grid), dim3(kBlock), 0, s, cd, u, out2);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void minmax(int n, const double* x, double* out2, hipStream_t s) {
+  // partial buffer: the caller's out2 must point at >= 2 + 2*kReduceBlocks doubles
+  double* partials = out2 + 2;
+  hipLaunchKernelGGL(k_minmax_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, x, partials);
+  hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, s, kReduceBlocks, partials, out2);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dcp

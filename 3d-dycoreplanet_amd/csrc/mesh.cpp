@@ -1,0 +1,434 @@
+// Host setup: refined mesh, DoF numbering, constraints. See mesh.h.
+#include "mesh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <map>
+#include <stdexcept>
+#include <tuple>
+
+#include "fe_tables.h"
+
+namespace dcp {
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+
+// Morton decode with x in the lowest bit: deal.II's child index c = cx + 2cy + 4cz
+// applied recursively, so tree order of the refined cells = increasing code.
+void demorton(uint32_t m, int refine, int& i, int& j, int& k) {
+  i = j = k = 0;
+  for (int b = 0; b < refine; ++b) {
+    i |= ((m >> (3 * b)) & 1u) << b;
+    j |= ((m >> (3 * b + 1)) & 1u) << b;
+    k |= ((m >> (3 * b + 2)) & 1u) << b;
+  }
+}
+
+double cell_diameter_of(const Mesh& m, int c) {
+  // CellAccessor::diameter for hexes: longest of the 4 space diagonals.
+  static const int diag[4][2] = {{0, 7}, {1, 6}, {2, 5}, {3, 4}};
+  double d = 0;
+  for (const auto& dg : diag) {
+    const double* a = &m.xyz[3 * m.cell_q2[27 * c + kQ1VertexToQ2Lex[dg[0]]]];
+    const double* b = &m.xyz[3 * m.cell_q2[27 * c + kQ1VertexToQ2Lex[dg[1]]]];
+    const double s = std::sqrt((a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) +
+                               (a[2] - b[2]) * (a[2] - b[2]));
+    d = std::max(d, s);
+  }
+  return d;
+}
+
+// Numbers nodes in deal.II first-encounter order: per cell (tree order),
+// vertices, lines, faces, interior (hierarchic order), and vertices separately
+// (the Q1 / pressure numbering). `key_of(cell, lex)` gives a global key.
+template <class KeyFn>
+void number_nodes(Mesh& m, size_t n_keys, KeyFn key_of, std::vector<int32_t>& key_node) {
+  key_node.assign(n_keys, -1);
+  std::vector<int32_t> key_vertex(n_keys, -1);
+  m.cell_q2.assign(size_t(m.n_cells) * 27, -1);
+  m.cell_q1.assign(size_t(m.n_cells) * 8, -1);
+  int nn = 0, nv = 0;
+  for (int c = 0; c < m.n_cells; ++c) {
+    for (int h = 0; h < 27; ++h) {
+      const int lex = kQ2HierToLex[h];
+      const size_t key = key_of(c, lex);
+      if (key_node[key] < 0) key_node[key] = nn++;
+      m.cell_q2[27 * size_t(c) + lex] = key_node[key];
+      if (h < 8) {
+        if (key_vertex[key] < 0) key_vertex[key] = nv++;
+        m.cell_q1[8 * size_t(c) + h] = key_vertex[key];
+      }
+    }
+  }
+  m.n_vnodes = nn;
+  m.n_vertices = nv;
+  m.vertex_vnode.assign(nv, -1);
+  m.vnode_vertex.assign(nn, -1);
+  for (int c = 0; c < m.n_cells; ++c)
+    for (int v = 0; v < 8; ++v) {
+      const int vid = m.cell_q1[8 * size_t(c) + v];
+      const int nid = m.cell_q2[27 * size_t(c) + kQ1VertexToQ2Lex[v]];
+      m.vertex_vnode[vid] = nid;
+      m.vnode_vertex[nid] = vid;
+    }
+}
+
+}  // namespace
+
+Mesh build_shell(int refine, double R0, double R1) {
+  if (refine < 0 || refine > 8) throw std::invalid_argument("shell refinement must be in [0,8]");
+  Mesh m;
+  m.cuboid = false;
+  m.refine = refine;
+  m.N = 1 << refine;
+  m.R0 = R0;
+  m.R1 = R1;
+  const int N = m.N, L2 = 2 * N + 1;  // Q2 lattice points per edge
+  m.n_cells = 6 * N * N * N;
+  // Panels of the cube (outward normal n, tangents e1, e2 with e1 x e2 = n), so
+  // that (xi, eta, zeta) = (e1, e2, radial) is right-handed in every cell.
+  static const int panel[6][3][3] = {
+      {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}},    // +x
+      {{-1, 0, 0}, {0, 0, 1}, {0, 1, 0}},   // -x
+      {{0, 1, 0}, {0, 0, 1}, {1, 0, 0}},    // +y
+      {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}},   // -y
+      {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}},    // +z
+      {{0, 0, -1}, {0, 1, 0}, {1, 0, 0}}};  // -z
+  // Global key: integer point P on the cube surface [-N,N]^3 plus radial index t.
+  const size_t n_keys = size_t(L2) * L2 * L2 * L2;
+  auto surf_point = [&](int c, int lex, int P[3], int& t) {
+    const int p = c / (N * N * N);
+    int i, j, k;
+    demorton(uint32_t(c % (N * N * N)), refine, i, j, k);
+    const int a = 2 * i + lex % 3, b = 2 * j + (lex / 3) % 3;
+    t = 2 * k + lex / 9;
+    for (int d = 0; d < 3; ++d)
+      P[d] = N * panel[p][0][d] + (a - N) * panel[p][1][d] + (b - N) * panel[p][2][d];
+  };
+  auto key_of = [&](int c, int lex) {
+    int P[3], t;
+    surf_point(c, lex, P, t);
+    return ((size_t(P[0] + N) * L2 + size_t(P[1] + N)) * L2 + size_t(P[2] + N)) * L2 + size_t(t);
+  };
+  std::vector<int32_t> key_node;
+  number_nodes(m, n_keys, key_of, key_node);
+  m.cell_coarse.resize(m.n_cells);
+  for (int c = 0; c < m.n_cells; ++c) m.cell_coarse[c] = c / (N * N * N);
+  m.xyz.assign(size_t(m.n_vnodes) * 3, 0.0);
+  m.vnode_bnd.assign(m.n_vnodes, 0);
+  std::vector<char> done(m.n_vnodes, 0);
+  for (int c = 0; c < m.n_cells; ++c)
+    for (int lex = 0; lex < 27; ++lex) {
+      const int n = m.cell_q2[27 * size_t(c) + lex];
+      if (done[n]) continue;
+      done[n] = 1;
+      int P[3], t;
+      surf_point(c, lex, P, t);
+      // Equiangular cube-sphere: components on the cube face stay +-1, the
+      // tangential ones map through tan(pi/4 * s); panel-independent.
+      double dir[3], nrm = 0;
+      for (int d = 0; d < 3; ++d) {
+        dir[d] = (std::abs(P[d]) == N) ? (P[d] > 0 ? 1.0 : -1.0)
+                                       : std::tan(0.25 * kPi * double(P[d]) / double(N));
+        nrm += dir[d] * dir[d];
+      }
+      nrm = std::sqrt(nrm);
+      const double r = (t == 0) ? R0 : (t == 2 * N) ? R1 : R0 + (R1 - R0) * double(t) / double(2 * N);
+      for (int d = 0; d < 3; ++d) m.xyz[3 * size_t(n) + d] = r * dir[d] / nrm;
+      if (t == 0) m.vnode_bnd[n] |= kBndInner;
+      if (t == 2 * N) m.vnode_bnd[n] |= kBndOuter;
+    }
+  m.cell_diameter.resize(m.n_cells);
+  for (int c = 0; c < m.n_cells; ++c) m.cell_diameter[c] = cell_diameter_of(m, c);
+  m.global_diameter = 2 * R1;
+  return m;
+}
+
+Mesh build_cube(int refine, double length) {
+  if (refine < 0 || refine > 9) throw std::invalid_argument("cube refinement must be in [0,9]");
+  Mesh m;
+  m.cuboid = true;
+  m.refine = refine;
+  m.N = 1 << refine;
+  const int N = m.N, L2 = 2 * N + 1;
+  m.n_cells = N * N * N;
+  auto lattice = [&](int c, int lex, int& a, int& b, int& d) {
+    int i, j, k;
+    demorton(uint32_t(c), refine, i, j, k);
+    a = 2 * i + lex % 3;
+    b = 2 * j + (lex / 3) % 3;
+    d = 2 * k + lex / 9;
+  };
+  auto key_of = [&](int c, int lex) {
+    int a, b, d;
+    lattice(c, lex, a, b, d);
+    return (size_t(d) * L2 + size_t(b)) * L2 + size_t(a);
+  };
+  std::vector<int32_t> key_node;
+  number_nodes(m, size_t(L2) * L2 * L2, key_of, key_node);
+  m.cell_coarse.assign(m.n_cells, 0);
+  m.xyz.assign(size_t(m.n_vnodes) * 3, 0.0);
+  m.vnode_bnd.assign(m.n_vnodes, 0);
+  const double h = 1.0 / (2.0 * N) / length;
+  for (int c = 0; c < m.n_cells; ++c)
+    for (int lex = 0; lex < 27; ++lex) {
+      const int n = m.cell_q2[27 * size_t(c) + lex];
+      int a, b, d;
+      lattice(c, lex, a, b, d);
+      m.xyz[3 * size_t(n) + 0] = a * h;
+      m.xyz[3 * size_t(n) + 1] = b * h;
+      m.xyz[3 * size_t(n) + 2] = d * h;
+      uint8_t bits = 0;
+      if (a == 0) bits |= kBndX0;
+      if (a == 2 * N) bits |= kBndX1;
+      if (b == 0) bits |= kBndY0;
+      if (b == 2 * N) bits |= kBndY1;
+      if (d == 0) bits |= kBndZ0;
+      if (d == 2 * N) bits |= kBndZ1;
+      m.vnode_bnd[n] = bits;
+    }
+  m.cell_diameter.resize(m.n_cells);
+  for (int c = 0; c < m.n_cells; ++c) m.cell_diameter[c] = cell_diameter_of(m, c);
+  // planet_geometry.tpp:35 center = (p0+p1)/2, rescaled with 1/L (boussinesq_model.tpp:54)
+  for (int d = 0; d < 3; ++d) m.center[d] = 0.5 / length;
+  m.global_diameter = std::sqrt(3.0) / length;
+  return m;
+}
+
+Mesh build_mesh(const Parameters& prm) {
+  if (prm.space_dimension != 3) throw std::invalid_argument("only space dimension 3 is built");
+  const double L = prm.reference_quantities.length;
+  if (prm.cuboid_geometry) return build_cube(int(prm.initial_global_refinement), L);
+  return build_shell(int(prm.initial_global_refinement), prm.physical_constants.R0 / L,
+                     prm.physical_constants.R1 / L);
+}
+
+// ---------------------------------------------------------------------------
+// Constraints
+
+namespace {
+
+struct Builder {
+  // dof -> (entries, inhomogeneity); std::map keeps entries sorted by dof.
+  std::vector<int> has;
+  std::vector<std::map<int, double>> entries;
+  std::vector<double> inhom;
+  explicit Builder(int n) : has(n, 0), entries(n), inhom(n, 0.0) {}
+  bool is_constrained(int d) const { return has[d] != 0; }
+  void add_line(int d) { has[d] = 1; }
+  void add_entry(int d, int t, double w) { entries[d][t] += w; }
+
+  // AffineConstraints::close(): resolve chains (targets that are themselves
+  // constrained are replaced by their expansion), sort entries.
+  Constraints close() {
+    const int n = int(has.size());
+    std::vector<int> state(n, 0);  // 0 = unresolved, 1 = in progress, 2 = resolved
+    std::function<void(int)> resolve = [&](int d) {
+      if (state[d] == 2) return;
+      if (state[d] == 1) throw std::runtime_error("cyclic constraints");
+      state[d] = 1;
+      std::map<int, double> out;
+      double g = inhom[d];
+      for (const auto& e : entries[d]) {
+        if (has[e.first]) {
+          resolve(e.first);
+          for (const auto& e2 : entries[e.first]) out[e2.first] += e.second * e2.second;
+          g += e.second * inhom[e.first];
+        } else {
+          out[e.first] += e.second;
+        }
+      }
+      entries[d].swap(out);
+      inhom[d] = g;
+      state[d] = 2;
+    };
+    Constraints c;
+    c.n_dofs = n;
+    c.line_of.assign(n, -1);
+    c.entry_ptr.push_back(0);
+    for (int d = 0; d < n; ++d) {
+      if (!has[d]) continue;
+      resolve(d);
+      c.line_of[d] = c.n_lines();
+      c.line_dof.push_back(d);
+      for (const auto& e : entries[d]) {
+        c.entry_dof.push_back(e.first);
+        c.entry_w.push_back(e.second);
+      }
+      c.entry_ptr.push_back(int(c.entry_dof.size()));
+      c.inhomogeneity.push_back(inhom[d]);
+    }
+    return c;
+  }
+};
+
+// VectorTools::compute_no_normal_flux_constraints, one normal per support
+// point (deal.II internal::add_constraint, dim = 3): the constrained component
+// is the dominant one with the 1e-10 / 2e-10 tie-breaking offsets, entries with
+// |ratio| <= eps are dropped; already constrained dofs are left alone.
+void add_no_normal_flux(Builder& b, const int dofs[3], const double n[3]) {
+  const double eps = 2.220446049250313e-16;
+  int k;
+  if (std::fabs(n[0]) >= std::fabs(n[1]) + 1e-10 && std::fabs(n[0]) >= std::fabs(n[2]) + 2e-10)
+    k = 0;
+  else if (std::fabs(n[1]) + 1e-10 >= std::fabs(n[0]) && std::fabs(n[1]) >= std::fabs(n[2]) + 1e-10)
+    k = 1;
+  else
+    k = 2;
+  if (b.is_constrained(dofs[k])) return;
+  b.add_line(dofs[k]);
+  for (int d = 0; d < 3; ++d) {
+    if (d == k) continue;
+    const double r = n[d] / n[k];
+    if (std::fabs(r) > eps) b.add_entry(dofs[k], dofs[d], -r);
+  }
+}
+
+// Periodic identification of the x = 1 face onto x = 0 and y = 1 onto y = 0
+// (DoFTools::make_periodicity_constraints, boussinesq_model.tpp:265-285). The
+// partner node is found from the lattice position. `dof_of(vnode)` < 0 skips.
+template <class DofFn>
+void add_periodic(const Mesh& m, Builder& b, DofFn dof_of, int n_comp) {
+  std::map<std::tuple<long, long, long>, int> at;
+  auto key = [&](int n) {
+    // xyz = lattice * h with h = 1/(2N L) and global_diameter = sqrt(3)/L
+    const double s = 2.0 * m.N * std::sqrt(3.0) / m.global_diameter;
+    return std::make_tuple(std::lround(m.xyz[3 * n] * s), std::lround(m.xyz[3 * n + 1] * s),
+                           std::lround(m.xyz[3 * n + 2] * s));
+  };
+  for (int n = 0; n < m.n_vnodes; ++n) at[key(n)] = n;
+  const long full = 2L * m.N;
+  for (int dir = 0; dir < 2; ++dir) {
+    const uint8_t hi = dir == 0 ? kBndX1 : kBndY1;
+    for (int n = 0; n < m.n_vnodes; ++n) {
+      if (!(m.vnode_bnd[n] & hi)) continue;
+      auto k = key(n);
+      if (dir == 0) std::get<0>(k) -= full; else std::get<1>(k) -= full;
+      const int partner = at.at(k);
+      for (int comp = 0; comp < n_comp; ++comp) {
+        const int ds = dof_of(n, comp), dm = dof_of(partner, comp);
+        if (ds < 0 || dm < 0 || b.is_constrained(ds)) continue;
+        b.add_line(ds);
+        b.add_entry(ds, dm, 1.0);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+Constraints nse_constraints(const Mesh& m) {
+  const int nu = m.n_u(), np = m.n_p();
+  Builder b(nu + np);
+  if (m.cuboid) {
+    add_periodic(m, b, [&](int n, int comp) {
+      if (comp < 3) return 3 * n + comp;
+      return m.vnode_vertex[n] >= 0 ? nu + m.vnode_vertex[n] : -1;
+    }, 4);
+    for (int n = 0; n < m.n_vnodes; ++n)
+      if (m.vnode_bnd[n] & kBndZ0)
+        for (int c = 0; c < 3; ++c)
+          if (!b.is_constrained(3 * n + c)) b.add_line(3 * n + c);
+    const double nz[3] = {0, 0, 1};
+    for (int n = 0; n < m.n_vnodes; ++n)
+      if ((m.vnode_bnd[n] & kBndZ1) && !(m.vnode_bnd[n] & kBndZ0)) {
+        const int dofs[3] = {3 * n, 3 * n + 1, 3 * n + 2};
+        add_no_normal_flux(b, dofs, nz);
+      }
+  } else {
+    for (int n = 0; n < m.n_vnodes; ++n)
+      if (m.vnode_bnd[n] & kBndInner)
+        for (int c = 0; c < 3; ++c) b.add_line(3 * n + c);
+    for (int n = 0; n < m.n_vnodes; ++n)
+      if (m.vnode_bnd[n] & kBndOuter) {
+        const double* x = &m.xyz[3 * size_t(n)];
+        const double r = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+        const double nn[3] = {x[0] / r, x[1] / r, x[2] / r};
+        const int dofs[3] = {3 * n, 3 * n + 1, 3 * n + 2};
+        add_no_normal_flux(b, dofs, nn);
+      }
+  }
+  return b.close();
+}
+
+double temperature_initial_shell(const double* p, double R0, double R1) {
+  // TemperatureInitialValues<3> (rotate = false): two Gaussians with
+  // covariance diag(20 / ((R1-R0)/2)), centres (R0+0.35h,0,0), (0,R0+0.65h,0).
+  const double cov = 20.0 / ((R1 - R0) / 2.0);
+  const double c1[3] = {R0 + (R1 - R0) * 0.35, 0, 0};
+  const double c2[3] = {0, R0 + (R1 - R0) * 0.65, 0};
+  const double sqrt_det = std::sqrt(cov * cov * cov);
+  const double norm = std::sqrt(std::pow(2 * kPi, 3));
+  double q1 = 0, q2 = 0;
+  for (int d = 0; d < 3; ++d) {
+    q1 += (p[d] - c1[d]) * cov * (p[d] - c1[d]);
+    q2 += (p[d] - c2[d]) * cov * (p[d] - c2[d]);
+  }
+  return sqrt_det * std::exp(-0.5 * q1) / norm + sqrt_det * std::exp(-0.5 * q2) / norm;
+}
+
+double temperature_initial_cuboid(const double* p, const double* center, double diameter) {
+  // TemperatureInitialValuesCuboid<3>: covariance diag(1/(0.1 d)^2)
+  const double cov = 1.0 / std::pow(diameter * 0.1, 2);
+  double q = 0;
+  for (int d = 0; d < 3; ++d) q += (p[d] - center[d]) * cov * (p[d] - center[d]);
+  return std::sqrt(cov * cov * cov) * std::exp(-0.5 * q) / (2 * std::sqrt(std::pow(2 * kPi, 2)));
+}
+
+double temperature_initial(const Mesh& m, const double* p) {
+  return m.cuboid ? temperature_initial_cuboid(p, m.center, m.global_diameter)
+                  : temperature_initial_shell(p, m.R0, m.R1);
+}
+
+TemperatureDofs temperature_dofs(const Mesh& m, int degree) {
+  TemperatureDofs t;
+  t.degree = degree;
+  if (degree == 1) {
+    t.n_dofs = m.n_vertices;
+    t.dofs_per_cell = 8;
+    t.cell_dofs = m.cell_q1;
+    t.dof_vnode = m.vertex_vnode;
+  } else if (degree == 2) {
+    t.n_dofs = m.n_vnodes;
+    t.dofs_per_cell = 27;
+    t.cell_dofs = m.cell_q2;
+    t.dof_vnode.resize(m.n_vnodes);
+    for (int n = 0; n < m.n_vnodes; ++n) t.dof_vnode[n] = n;
+  } else {
+    throw std::invalid_argument("temperature degree must be 1 or 2");
+  }
+  return t;
+}
+
+Constraints temperature_constraints(const Mesh& m, int degree) {
+  const TemperatureDofs td = temperature_dofs(m, degree);
+  std::vector<int> vnode_dof(m.n_vnodes, -1);
+  for (int d = 0; d < td.n_dofs; ++d) vnode_dof[td.dof_vnode[d]] = d;
+  Builder b(td.n_dofs);
+  const uint8_t dirichlet_bit = m.cuboid ? kBndZ0 : kBndInner;
+  if (m.cuboid) add_periodic(m, b, [&](int n, int) { return vnode_dof[n]; }, 1);
+  for (int d = 0; d < td.n_dofs; ++d) {
+    const int n = td.dof_vnode[d];
+    if (!(m.vnode_bnd[n] & dirichlet_bit) || b.is_constrained(d)) continue;
+    b.add_line(d);
+    b.inhom[d] = temperature_initial(m, &m.xyz[3 * size_t(n)]);
+  }
+  return b.close();
+}
+
+std::vector<int32_t> nse_cell_dofs_dealii(const Mesh& m) {
+  std::vector<int32_t> out(size_t(m.n_cells) * kNseDofs);
+  const int nu = m.n_u();
+  for (int c = 0; c < m.n_cells; ++c)
+    for (int i = 0; i < kNseDofs; ++i) {
+      const SysDof s = system_dof(i);
+      out[size_t(c) * kNseDofs + i] = s.comp < 3 ? 3 * m.cell_q2[27 * size_t(c) + s.lex] + s.comp
+                                                 : nu + m.cell_q1[8 * size_t(c) + s.lex];
+    }
+  return out;
+}
+
+}  // namespace dcp

@@ -1,0 +1,469 @@
+// Device-resident Krylov drivers: the deal.II solvers the reference calls,
+// restated over device vectors. The vector work (SpMV, Jacobi, Gram-Schmidt
+// add_and_dot chains, updates) runs as HIP kernels on the context stream with
+// scalars kept in device memory; the host only performs the O(restart^2)
+// scalar algebra (Givens rotations, Householder least squares, back
+// substitution) and the SolverControl checks, one readback per iteration.
+//
+//   solve_NSE_block_preconditioned   boussinesq_model.tpp:1131-1245
+//   BlockSchurPreconditioner::vmult  block_schur_preconditioner.hpp:42-70
+//   SchurComplement::vmult           schur_complement.hpp:143-150
+//   solve_temperature                boussinesq_model.tpp:1417-1476
+#include <cmath>
+#include <functional>
+#include <vector>
+
+#include "context.h"
+
+namespace dcp {
+namespace {
+
+enum State { kIterate, kSuccess, kFailure };
+
+// deal.II SolverControl::check (success tested before failure)
+struct Control {
+  unsigned max_steps;
+  double tol;
+  unsigned last_step = 0;
+  double last_value = 0;
+  State check(unsigned step, double value) {
+    last_step = step;
+    last_value = value;
+    if (value <= tol) return kSuccess;
+    if (step >= max_steps || std::isnan(value)) return kFailure;
+    return kIterate;
+  }
+};
+
+// Device scalar slots (c.dscal).
+constexpr int kSlotH = 0;        // 0..127: Gram-Schmidt coefficients
+constexpr int kSlotH2 = 128;     // 128..255: re-orthogonalisation pass
+constexpr int kSlotNN = 256;     // |vv|^2 after orthogonalisation
+constexpr int kSlotNStart = 257; // |vv|^2 before
+constexpr int kSlotA = 258;      // misc
+constexpr int kSlotB = 259;
+constexpr int kSlotC = 260;
+constexpr int kSlotD = 261;
+constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
+constexpr int kNumSlots = kSlotMinMax + 2 + 2 * kReduceBlocks;
+
+using Op = std::function<void(const double*, double*)>;
+
+double* slot(Ctx& c, int i) { return c.dscal.p + i; }
+
+// readback of n device scalars starting at slot i
+const double* fetch(Ctx& c, int i, int n) {
+  DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, slot(c, i), n * sizeof(double), hipMemcpyDeviceToHost,
+                               c.stream));
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  return c.hpinned;
+}
+
+double dot_host(Ctx& c, int n, const double* a, const double* b, int s) {
+  dot(n, a, b, c.partials.p, slot(c, s), c.stream);
+  return fetch(c, s, 1)[0];
+}
+
+void ensure_pool(std::vector<double*>& pool, int count, size_t n) {
+  while (int(pool.size()) < count) {
+    double* p = nullptr;
+    DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), (n ? n : 1) * sizeof(double)));
+    pool.push_back(p);
+  }
+}
+
+// x += sum_i y_i X_i
+void combine(Ctx& c, int n, const std::vector<double>& y, const std::vector<double*>& X,
+             double* x) {
+  const int k = int(y.size());
+  if (k == 0) return;
+  std::vector<const double*> ptrs(X.begin(), X.begin() + k);
+  DCP_HIP_CHECK(hipMemcpyAsync(c.coef.p, y.data(), k * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  DCP_HIP_CHECK(hipMemcpyAsync(c.ptrs.p, ptrs.data(), k * sizeof(double*), hipMemcpyHostToDevice,
+                               c.stream));
+  multi_axpy(n, k, c.coef.p, c.ptrs.p, x, c.stream);
+  // the host vectors above must outlive the async copies
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+void givens_rotation(std::vector<double>& h, std::vector<double>& b, std::vector<double>& ci,
+                     std::vector<double>& si, int col) {
+  for (int i = 0; i < col; i++) {
+    const double s = si[i], cc = ci[i], dummy = h[i];
+    h[i] = cc * dummy + s * h[i + 1];
+    h[i + 1] = -s * dummy + cc * h[i + 1];
+  }
+  const double r = 1. / std::sqrt(h[col] * h[col] + h[col + 1] * h[col + 1]);
+  si[col] = h[col + 1] * r;
+  ci[col] = h[col] * r;
+  h[col] = ci[col] * h[col] + si[col] * h[col + 1];
+  b[col + 1] = -si[col] * b[col];
+  b[col] *= ci[col];
+}
+
+// Modified Gram-Schmidt of deal.II SolverGMRES (add_and_dot chain; every 5th
+// step the loss-of-orthogonality test; once triggered a second pass for the
+// rest of the solve). Returns |vv| after orthogonalisation; h[0..dim) filled.
+double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int dim, double* vv,
+                             std::vector<double>& h, bool& reorth) {
+  const bool consider = !reorth && ((dim - 1) % 5 == 4);
+  if (consider) dot(n, vv, vv, c.partials.p, slot(c, kSlotNStart), c.stream);
+  dot(n, vv, V[0], c.partials.p, slot(c, kSlotH), c.stream);
+  for (int i = 1; i < dim; ++i)
+    add_and_dot(n, vv, DScal{slot(c, kSlotH + i - 1), -1.0}, V[i - 1], V[i], c.partials.p,
+                slot(c, kSlotH + i), c.stream);
+  add_and_dot(n, vv, DScal{slot(c, kSlotH + dim - 1), -1.0}, V[dim - 1], vv, c.partials.p,
+              slot(c, kSlotNN), c.stream);
+  const double* r = fetch(c, 0, kSlotNStart + 1);
+  for (int i = 0; i < dim; ++i) h[i] = r[kSlotH + i];
+  double norm_vv = std::sqrt(r[kSlotNN]);
+  if (consider) {
+    const double start = std::sqrt(r[kSlotNStart]);
+    if (norm_vv > 10. * start * std::sqrt(2.220446049250313e-16)) return norm_vv;
+    reorth = true;
+  }
+  if (reorth) {
+    dot(n, vv, V[0], c.partials.p, slot(c, kSlotH2), c.stream);
+    for (int i = 1; i < dim; ++i)
+      add_and_dot(n, vv, DScal{slot(c, kSlotH2 + i - 1), -1.0}, V[i - 1], V[i], c.partials.p,
+                  slot(c, kSlotH2 + i), c.stream);
+    add_and_dot(n, vv, DScal{slot(c, kSlotH2 + dim - 1), -1.0}, V[dim - 1], vv, c.partials.p,
+                slot(c, kSlotNN), c.stream);
+    const double* r2 = fetch(c, 0, kSlotNStart + 1);
+    for (int i = 0; i < dim; ++i) h[i] += r2[kSlotH2 + i];
+    norm_vv = std::sqrt(r2[kSlotNN]);
+  }
+  return norm_vv;
+}
+
+// deal.II SolverGMRES<VectorType> (left preconditioning, default residual,
+// n_tmp temporary vectors -> restart n_tmp-2). P == nullptr: identity.
+State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b, Control& ctl,
+            std::vector<double*>& tv, int n_tmp) {
+  ensure_pool(tv, n_tmp, size_t(n));
+  double* v = tv[0];
+  double* p = tv[n_tmp - 1];
+  std::vector<std::vector<double>> H(n_tmp, std::vector<double>(n_tmp - 1, 0.0));
+  std::vector<double> gamma(n_tmp, 0.0), ci(n_tmp - 1, 0.0), si(n_tmp - 1, 0.0), h(n_tmp - 1, 0.0);
+  unsigned accumulated = 0;
+  int dim = 0;
+  State st = kIterate;
+  bool reorth = false;
+  do {
+    std::fill(h.begin(), h.end(), 0.0);
+    A(x, p);
+    sadd(n, -1., 1., b, p, c.stream);  // p = b - A x
+    if (P) (*P)(p, v); else copy(n, p, v, c.stream);
+    double rho = std::sqrt(dot_host(c, n, v, v, kSlotA));
+    st = ctl.check(accumulated, rho);
+    if (st != kIterate) break;
+    gamma[0] = rho;
+    scale(n, DScal{nullptr, 1. / rho}, v, c.stream);
+    for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
+      ++accumulated;
+      double* vv = tv[inner + 1];
+      if (P) {
+        A(tv[inner], p);
+        (*P)(p, vv);
+      } else {
+        A(tv[inner], vv);  // identity preconditioner: vv = A v (bitwise the copy)
+      }
+      dim = inner + 1;
+      const double s = modified_gram_schmidt(c, n, tv, dim, vv, h, reorth);
+      h[inner + 1] = s;
+      if (s != 0) scale(n, DScal{nullptr, 1. / s}, vv, c.stream);
+      givens_rotation(h, gamma, ci, si, inner);
+      for (int i = 0; i < dim; ++i) H[i][inner] = h[i];
+      rho = std::fabs(gamma[dim]);
+      st = ctl.check(accumulated, rho);
+    }
+    // H1.backward(h, gamma)
+    std::vector<double> y(dim, 0.0);
+    for (int i = dim - 1; i >= 0; --i) {
+      double sum = gamma[i];
+      for (int j = i + 1; j < dim; ++j) sum -= y[j] * H[i][j];
+      y[i] = sum / H[i][i];
+    }
+    combine(c, n, y, tv, x);
+  } while (st == kIterate);
+  return st;
+}
+
+// deal.II Householder<double>::least_squares on the (m x n) matrix S.
+double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
+                                 std::vector<double>& dst, const std::vector<double>& src) {
+  std::vector<double> diagonal(m, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double sigma = 0;
+    for (int i = j; i < m; ++i) sigma += S[i][j] * S[i][j];
+    if (std::fabs(sigma) < 1.e-15) break;
+    const double s = (S[j][j] < 0) ? std::sqrt(sigma) : -std::sqrt(sigma);
+    const double beta = std::sqrt(1. / (sigma - s * S[j][j]));
+    diagonal[j] = beta * (S[j][j] - s);
+    S[j][j] = s;
+    for (int i = j + 1; i < m; ++i) S[i][j] *= beta;
+    for (int k = j + 1; k < n; ++k) {
+      double sum = diagonal[j] * S[j][k];
+      for (int i = j + 1; i < m; ++i) sum += S[i][j] * S[i][k];
+      S[j][k] -= sum * diagonal[j];
+      for (int i = j + 1; i < m; ++i) S[i][k] -= sum * S[i][j];
+    }
+  }
+  std::vector<double> aux = src;
+  for (int j = 0; j < n; ++j) {
+    double sum = diagonal[j] * aux[j];
+    for (int i = j + 1; i < m; ++i) sum += S[i][j] * aux[i];
+    aux[j] -= sum * diagonal[j];
+    for (int i = j + 1; i < m; ++i) aux[i] -= sum * S[i][j];
+  }
+  double sum = 0;
+  for (int i = n; i < m; ++i) sum += aux[i] * aux[i];
+  dst.assign(n, 0.0);
+  for (int i = n - 1; i >= 0; --i) {
+    double s = aux[i];
+    for (int j = i + 1; j < n; ++j) s -= dst[j] * S[i][j];
+    dst[i] = s / S[i][i];
+  }
+  return std::sqrt(sum);
+}
+
+struct NoConvergence {};
+
+int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inner) {
+  const int nu = c.n_u, np = c.n_p;
+  // inner GMRES on S = B D_A^-1 B^T, tol 1e-6 |src_p|, max 5000, identity
+  {
+    const double nrm = std::sqrt(dot_host(c, np, src + nu, src + nu, kSlotB));
+    Control ctl{5000, 1e-6 * nrm};
+    ensure_pool(c.sg_v, 30, size_t(np));
+    Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
+    const State st = gmres(c, np, S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
+    inner += int(ctl.last_step);
+    if (st != kSuccess) throw NoConvergence();
+    scale(np, DScal{nullptr, -1.0}, dst + nu, c.stream);
+  }
+  // utmp = src_u - B^T dst_p
+  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, dst + nu, c.utmp.p, false, c.stream);
+  sadd(nu, -1.0, 1.0, src, c.utmp.p, c.stream);
+  if (do_solve_A) {
+    // TrilinosWrappers::SolverGMRES (AztecOO) restated as deal.II GMRES with the
+    // A-Jacobi, tol 1e-2 |utmp| (block_schur_preconditioner.hpp:59-67)
+    const double nrm = std::sqrt(dot_host(c, nu, c.utmp.p, c.utmp.p, kSlotB));
+    Control ctl{5000, nrm * 1e-2};
+    Op A = [&](const double* x, double* y) {
+      spmv_bsr33(c.n_vnodes, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
+    };
+    Op P = [&](const double* x, double* y) { mul(nu, c.A_inv.p, x, y, c.stream); };
+    const State st = gmres(c, nu, A, &P, dst, c.utmp.p, ctl, c.ag_v, 30);
+    if (st != kSuccess) throw NoConvergence();
+  } else {
+    mul(nu, c.A_inv.p, c.utmp.p, dst, c.stream);  // Ifpack point Jacobi
+  }
+  return DCP_OK;
+}
+
+// deal.II SolverFGMRES (see oracle/oracle.cpp for the restated control flow).
+State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, double tol,
+             bool do_solve_A, int& acc_out, int& inner) {
+  const int n = c.n_u + c.n_p;
+  Control ctl{max_steps, tol};
+  ensure_pool(c.fg_v, basis, size_t(n));
+  ensure_pool(c.fg_z, basis, size_t(n));
+  std::vector<char> z_init(basis, 0);
+  double* aux = c.fg_aux.p;
+  unsigned accumulated = 0;
+  State st = kIterate;
+  std::vector<double> y;
+  std::vector<std::vector<double>> H;
+  do {
+    nse_vmult(c, x, aux);
+    sadd(n, -1., 1., b, aux, c.stream);
+    const double beta = std::sqrt(dot_host(c, n, aux, aux, kSlotA));
+    double res = beta;
+    st = ctl.check(accumulated, res);
+    if (st == kSuccess) break;
+    H.assign(basis + 1, std::vector<double>(basis, 0.0));
+    double a = beta;
+    y.clear();
+    for (int j = 0; j < basis; ++j) {
+      double* vj = c.fg_v[j];
+      double* zj = c.fg_z[j];
+      if (!z_init[j]) {
+        fill(n, 0.0, zj, c.stream);
+        z_init[j] = 1;
+      }
+      if (a != 0) equ(n, DScal{nullptr, 1. / a}, aux, vj, c.stream);
+      else fill(n, 0.0, vj, c.stream);
+      block_prec(c, vj, zj, do_solve_A, inner);
+      nse_vmult(c, zj, aux);
+      dot(n, aux, c.fg_v[0], c.partials.p, slot(c, kSlotH), c.stream);
+      for (int i = 1; i <= j; ++i)
+        add_and_dot(n, aux, DScal{slot(c, kSlotH + i - 1), -1.0}, c.fg_v[i - 1], c.fg_v[i],
+                    c.partials.p, slot(c, kSlotH + i), c.stream);
+      add_and_dot(n, aux, DScal{slot(c, kSlotH + j), -1.0}, vj, aux, c.partials.p,
+                  slot(c, kSlotNN), c.stream);
+      const double* r = fetch(c, 0, kSlotNN + 1);
+      for (int i = 0; i <= j; ++i) H[i][j] = r[kSlotH + i];
+      H[j + 1][j] = a = std::sqrt(r[kSlotNN]);
+      if (j > 0) {
+        std::vector<std::vector<double>> H1(j + 1, std::vector<double>(j, 0.0));
+        for (int rr = 0; rr <= j; ++rr)
+          for (int cc = 0; cc < j; ++cc) H1[rr][cc] = H[rr][cc];
+        std::vector<double> prhs(j + 1, 0.0);
+        prhs[0] = beta;
+        res = householder_least_squares(H1, j + 1, j, y, prhs);
+        st = ctl.check(++accumulated, res);
+        if (st != kIterate) break;
+      }
+    }
+    combine(c, n, y, c.fg_z, x);
+  } while (st == kIterate);
+  acc_out = int(ctl.last_step);
+  return st;
+}
+
+}  // namespace
+
+void nse_vmult(Ctx& c, const double* src, double* dst) {
+  // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
+  spmv_bsr33(c.n_vnodes, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
+  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src + c.n_u, dst, true, c.stream);
+  spmv_bsr13(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);
+}
+
+void schur_vmult(Ctx& c, const double* src, double* dst) {
+  if (c.time_schur) DCP_HIP_CHECK(hipEventRecord(c.ev_schur.a, c.stream));
+  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src, c.schur_tmp1.p, false, c.stream);
+  mul(c.n_u, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
+  spmv_bsr13(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, c.schur_tmp2.p, dst, false, c.stream);
+  if (c.time_schur) {
+    DCP_HIP_CHECK(hipEventRecord(c.ev_schur.b, c.stream));
+    DCP_HIP_CHECK(hipEventSynchronize(c.ev_schur.b));
+    float ms = 0;
+    DCP_HIP_CHECK(hipEventElapsedTime(&ms, c.ev_schur.a, c.ev_schur.b));
+    c.schur_ms_total += ms;
+    c.schur_count += 1;
+  }
+}
+
+void free_workspaces(Ctx& c) {
+  for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v}) {
+    for (double* p : *pool) (void)hipFree(p);
+    pool->clear();
+  }
+}
+
+void ensure_workspaces(Ctx& c) {
+  if (c.dscal.p == nullptr) {
+    c.dscal.alloc(kNumSlots);
+    c.partials.alloc(kReduceBlocks);
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hpinned), kNumSlots * sizeof(double)));
+    c.coef.alloc(128);
+    c.ptrs.alloc(128);
+  }
+}
+
+int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_solve_A,
+                               int* inner) {
+  int it = 0;
+  try {
+    block_prec(c, src, dst, do_solve_A, it);
+  } catch (const NoConvergence&) {
+    if (inner) *inner = it;
+    return DCP_NOT_CONVERGED;
+  }
+  if (inner) *inner = it;
+  return DCP_OK;
+}
+
+int solve_nse(Ctx& c, int* outer, int* inner_out) {
+  // solve_NSE_block_preconditioned (boussinesq_model.tpp:1131-1245)
+  const int nu = c.n_u, np = c.n_p, n = nu + np;
+  const double dt = c.ph.dt;
+  DBuf<double> x;
+  x.alloc(n);
+  copy(n, c.nse_sol.p, x.p, c.stream);
+  scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);      // :1151 (pressure dofs unconstrained)
+  const double tol = 1e-8 * std::sqrt(dot_host(c, n, c.nse_rhs.p, c.nse_rhs.p, kSlotA));  // :1165
+  scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);      // :1177 (Q1)
+  int inner = 0, acc1 = 0, acc2 = 0, status = DCP_OK;
+  try {
+    const State st = fgmres(c, x.p, c.nse_rhs.p, 30, 40, tol, false, acc1, inner);
+    if (st != kSuccess) throw NoConvergence();
+  } catch (const NoConvergence&) {
+    // :1203-1232 fallback (Q10): do_solve_A, FGMRES(50), max = nse_matrix.m()
+    try {
+      const State st = fgmres(c, x.p, c.nse_rhs.p, 50, unsigned(n), tol, true, acc2, inner);
+      if (st != kSuccess) status = DCP_NOT_CONVERGED;
+    } catch (const NoConvergence&) {
+      status = DCP_NOT_CONVERGED;
+    }
+  }
+  distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
+  scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);   // :1239 (x /= dt)
+  copy(n, x.p, c.nse_sol.p, c.stream);                       // :1241
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (outer) *outer = acc1 + acc2;
+  if (inner_out) *inner_out = inner;
+  return status;
+}
+
+int solve_temperature(Ctx& c, int* iters, double* T_range) {
+  // SolverCG + Ifpack Jacobi on T_matrix, tol 1e-12 |rhs|, max n_T (:1417-1476)
+  const int n = c.n_T;
+  const double rhs_norm = std::sqrt(dot_host(c, n, c.T_rhs.p, c.T_rhs.p, kSlotA));
+  Control ctl{unsigned(n), 1e-12 * rhs_norm};
+  if (c.cg_g.n < size_t(n)) {
+    c.cg_g.alloc(n);
+    c.cg_d.alloc(n);
+    c.cg_h.alloc(n);
+  }
+  double *x = c.T_sol.p, *g = c.cg_g.p, *d = c.cg_d.p, *h = c.cg_h.p;
+  auto Av = [&](const double* s, double* o) {
+    spmv_csr(n, c.T_ptr.p, c.T_col.p, c.Tmat.p, s, o, false, c.stream);
+  };
+  const bool all_zero = dot_host(c, n, x, x, kSlotA) == 0.0;
+  if (!all_zero) {
+    Av(x, g);
+    axpy(n, DScal{nullptr, -1.0}, c.T_rhs.p, g, c.stream);  // g.add(-1, b)
+  } else {
+    equ(n, DScal{nullptr, -1.0}, c.T_rhs.p, g, c.stream);
+  }
+  double res = std::sqrt(dot_host(c, n, g, g, kSlotA));
+  State conv = ctl.check(0, res);
+  int it = 0;
+  if (conv == kIterate) {
+    mul(n, c.T_inv.p, g, h, c.stream);
+    equ(n, DScal{nullptr, -1.0}, h, d, c.stream);
+    dot(n, g, h, c.partials.p, slot(c, kSlotC), c.stream);  // gh
+    while (conv == kIterate) {
+      it++;
+      Av(d, h);
+      dot(n, d, h, c.partials.p, slot(c, kSlotD), c.stream);    // d.h
+      scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);  // alpha = gh / dh
+      axpy(n, DScal{slot(c, kSlotA), 1.0}, d, x, c.stream);
+      add_and_dot(n, g, DScal{slot(c, kSlotA), 1.0}, h, g, c.partials.p, slot(c, kSlotB),
+                  c.stream);
+      res = std::sqrt(std::fabs(fetch(c, kSlotB, 1)[0]));
+      conv = ctl.check(it, res);
+      if (conv != kIterate) break;
+      mul(n, c.T_inv.p, g, h, c.stream);
+      copy(1, slot(c, kSlotC), slot(c, kSlotD), c.stream);       // beta = old gh
+      dot(n, g, h, c.partials.p, slot(c, kSlotC), c.stream);      // new gh
+      scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);  // beta
+      axpby(n, DScal{nullptr, -1.0}, h, DScal{slot(c, kSlotA), 1.0}, d, c.stream);  // d = beta d - h
+    }
+  }
+  distribute_temperature(n, c.T_fixed.p, c.T_bc.p, x, c.stream);
+  if (T_range) {
+    minmax(n, x, slot(c, kSlotMinMax), c.stream);
+    const double* r = fetch(c, kSlotMinMax, 2);
+    T_range[0] = r[0];
+    T_range[1] = r[1];
+  }
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (iters) *iters = int(ctl.last_step);
+  return conv == kSuccess ? DCP_OK : DCP_NOT_CONVERGED;
+}
+
+}  // namespace dcp

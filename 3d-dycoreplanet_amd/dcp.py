@@ -1,0 +1,426 @@
+"""ctypes binding of libdcp.so (include/dcp.h) — the host-side view of the
+MI355X Boussinesq hot path, mirroring the reference model's member calls
+(include/core/boussinesq_model.tpp):
+
+    assemble_nse_system      -> Context.assemble_nse_system()
+    build_nse_preconditioner -> Context.build_nse_preconditioner()
+    assemble_temperature_*   -> Context.assemble_temperature_matrix()/_rhs()
+    solve_NSE_block_...      -> Context.solve_nse()
+    solve_temperature        -> Context.solve_temperature()
+
+There is no CPU fallback: loading fails loudly when libdcp.so is missing and
+every compute call raises DcpError when no GPU is present.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdcp.so")
+
+DCP_OK, DCP_NOT_CONVERGED = 0, 1
+DCP_ERR_INVALID, DCP_ERR_UNSUPPORTED, DCP_ERR_DEVICE, DCP_ERR_STATE = -1, -2, -3, -4
+NSE_SOLUTION, OLD_NSE_SOLUTION, T_SOLUTION, OLD_T_SOLUTION, NSE_RHS, T_RHS = range(6)
+ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
+
+# Every symbol include/dcp.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "dcp_ctx_create", "dcp_ctx_destroy", "dcp_last_error", "dcp_device_count",
+    "dcp_set_physics", "dcp_set_time_step", "dcp_mesh_upload", "dcp_state_set",
+    "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
+    "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
+    "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
+    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult",
+    "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
+    "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
+    "dcp_get_timings", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
+    "dcp_host_mesh_view_get", "dcp_host_mesh_initial_temperature", "dcp_prm_load",
+]
+
+
+class DcpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"dcp error {code}: {msg}")
+        self.code = code
+
+
+class Physics(C.Structure):
+    _fields_ = [
+        ("time_step", C.c_double), ("one_over_reynolds", C.c_double),
+        ("one_over_peclet", C.c_double), ("expansion_coefficient", C.c_double),
+        ("temperature_ref", C.c_double), ("gravity_scale", C.c_double),
+        ("gravity_constant", C.c_double), ("coriolis_scale", C.c_double),
+        ("omega", C.c_double), ("cuboid", C.c_int), ("nse_solver_interval", C.c_int),
+        ("temperature_degree", C.c_int),
+    ]
+
+
+class Constraints(C.Structure):
+    _fields_ = [
+        ("n_lines", C.c_int), ("line_dof", C.POINTER(C.c_int)),
+        ("entry_ptr", C.POINTER(C.c_int)), ("entry_dof", C.POINTER(C.c_int)),
+        ("entry_w", C.POINTER(C.c_double)), ("inhomogeneity", C.POINTER(C.c_double)),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("rank", C.c_int), ("world_size", C.c_int),
+                ("nccl_id", C.c_void_p)]
+
+
+class Timings(C.Structure):
+    _fields_ = [
+        ("assemble_nse_ms", C.c_double), ("build_precond_ms", C.c_double),
+        ("assemble_T_matrix_ms", C.c_double), ("assemble_T_rhs_ms", C.c_double),
+        ("solve_nse_ms", C.c_double), ("solve_T_ms", C.c_double),
+        ("schur_apply_ms_avg", C.c_double), ("schur_applies", C.c_long),
+    ]
+
+
+class MeshView(C.Structure):
+    _fields_ = [
+        ("n_cells", C.c_int), ("n_u", C.c_int), ("n_p", C.c_int), ("n_T", C.c_int),
+        ("n_vnodes", C.c_int),
+        ("cell_nse_dofs", C.POINTER(C.c_int32)), ("cell_T_dofs", C.POINTER(C.c_int32)),
+        ("cell_geometry", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
+        ("node_xyz", C.POINTER(C.c_double)), ("nse", Constraints), ("T", Constraints),
+    ]
+
+
+class RunParams(C.Structure):
+    _fields_ = [
+        ("physics", Physics), ("initial_global_refinement", C.c_int),
+        ("space_dimension", C.c_int), ("nse_velocity_degree", C.c_int),
+        ("use_schur_complement_solver", C.c_int), ("use_FEEC_solver", C.c_int),
+        ("adapt_time_step", C.c_int), ("final_time", C.c_double), ("R0", C.c_double),
+        ("R1", C.c_double), ("length", C.c_double),
+    ]
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the hot path has no CPU fallback)")
+    lib = C.CDLL(path)
+    P, D, I = C.c_void_p, C.POINTER(C.c_double), C.c_int
+    lib.dcp_last_error.restype = C.c_char_p
+    lib.dcp_last_error.argtypes = [P]
+    lib.dcp_ctx_create.argtypes = [C.POINTER(Config), C.POINTER(P)]
+    lib.dcp_ctx_destroy.argtypes = [P]
+    lib.dcp_ctx_destroy.restype = None
+    lib.dcp_set_physics.argtypes = [P, C.POINTER(Physics)]
+    lib.dcp_set_time_step.argtypes = [P, C.c_double]
+    lib.dcp_mesh_upload.argtypes = [P, I, P, P, P, P, I, I, I, C.POINTER(Constraints),
+                                    C.POINTER(Constraints)]
+    lib.dcp_state_set.argtypes = [P, I, P, C.c_size_t]
+    lib.dcp_state_get.argtypes = [P, I, P, C.c_size_t]
+    lib.dcp_state_copy.argtypes = [P, I, I]
+    lib.dcp_state_device_ptr.argtypes = [P, I]
+    lib.dcp_state_device_ptr.restype = C.c_void_p
+    for f in ("dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
+              "dcp_assemble_temperature_rhs", "dcp_advance_state"):
+        getattr(lib, f).argtypes = [P]
+    lib.dcp_assemble_nse_system.argtypes = [P, I]
+    lib.dcp_solve_nse.argtypes = [P, C.POINTER(I), C.POINTER(I)]
+    lib.dcp_solve_temperature.argtypes = [P, C.POINTER(I), D]
+    lib.dcp_max_velocity.argtypes = [P, D]
+    lib.dcp_cfl_number.argtypes = [P, D]
+    lib.dcp_nse_vmult.argtypes = [P, P, P]
+    lib.dcp_schur_vmult.argtypes = [P, P, P]
+    lib.dcp_block_preconditioner_vmult.argtypes = [P, P, P, I, C.POINTER(I)]
+    lib.dcp_nse_matrix_export.argtypes = [P, C.POINTER(C.c_int64), P, P, P]
+    lib.dcp_T_matrix_export.argtypes = [P, C.POINTER(C.c_int64), P, P, P]
+    lib.dcp_precond_diagonals.argtypes = [P, P, P]
+    lib.dcp_cell_nse_system.argtypes = [P, I, I, P, P]
+    lib.dcp_get_timings.argtypes = [P, C.POINTER(Timings)]
+    lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I]
+    lib.dcp_host_mesh_create.restype = P
+    lib.dcp_host_mesh_destroy.argtypes = [P]
+    lib.dcp_host_mesh_destroy.restype = None
+    lib.dcp_host_mesh_view_get.argtypes = [P, C.POINTER(MeshView)]
+    lib.dcp_host_mesh_initial_temperature.argtypes = [P, P]
+    lib.dcp_prm_load.argtypes = [C.c_char_p, C.POINTER(RunParams), C.c_char_p, I]
+    return lib
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = load_library()
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _arr(p, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(p, shape=(n,)).astype(dtype, copy=True)
+
+
+class ConstraintSet:
+    """A closed AffineConstraints object (numpy arrays)."""
+
+    def __init__(self, line_dof, entry_ptr, entry_dof, entry_w, inhomogeneity):
+        self.line_dof = np.ascontiguousarray(line_dof, dtype=np.int32)
+        self.entry_ptr = np.ascontiguousarray(entry_ptr, dtype=np.int32)
+        self.entry_dof = np.ascontiguousarray(entry_dof, dtype=np.int32)
+        self.entry_w = np.ascontiguousarray(entry_w, dtype=np.float64)
+        self.inhomogeneity = np.ascontiguousarray(inhomogeneity, dtype=np.float64)
+
+    @classmethod
+    def from_view(cls, v: Constraints):
+        n = v.n_lines
+        ptr = _arr(v.entry_ptr, n + 1, np.int32)
+        ne = int(ptr[-1]) if n else 0
+        if n == 0:
+            ptr = np.zeros(1, np.int32)
+        return cls(_arr(v.line_dof, n, np.int32), ptr, _arr(v.entry_dof, ne, np.int32),
+                   _arr(v.entry_w, ne, np.float64), _arr(v.inhomogeneity, n, np.float64))
+
+    def as_struct(self) -> Constraints:
+        s = Constraints()
+        s.n_lines = len(self.line_dof)
+        s.line_dof = self.line_dof.ctypes.data_as(C.POINTER(C.c_int))
+        s.entry_ptr = self.entry_ptr.ctypes.data_as(C.POINTER(C.c_int))
+        s.entry_dof = self.entry_dof.ctypes.data_as(C.POINTER(C.c_int))
+        s.entry_w = self.entry_w.ctypes.data_as(C.POINTER(C.c_double))
+        s.inhomogeneity = self.inhomogeneity.ctypes.data_as(C.POINTER(C.c_double))
+        return s
+
+
+class HostMesh:
+    """Refined shell / cube with DoFs and constraints (setup_dofs restated)."""
+
+    def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1):
+        h = lib().dcp_host_mesh_create(int(cuboid), int(refine), float(R0), float(R1),
+                                       float(length), int(temperature_degree))
+        if not h:
+            raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
+        try:
+            v = MeshView()
+            lib().dcp_host_mesh_view_get(h, C.byref(v))
+            self.n_cells, self.n_u, self.n_p, self.n_T = v.n_cells, v.n_u, v.n_p, v.n_T
+            self.n_vnodes = v.n_vnodes
+            self.cell_nse_dofs = _arr(v.cell_nse_dofs, self.n_cells * 89, np.int32).reshape(-1, 89)
+            tdpc = 8 if temperature_degree == 1 else 27
+            self.cell_T_dofs = _arr(v.cell_T_dofs, self.n_cells * tdpc, np.int32).reshape(-1, tdpc)
+            self.cell_geometry = _arr(v.cell_geometry, self.n_cells * 81,
+                                      np.float64).reshape(-1, 27, 3)
+            self.cell_diameter = _arr(v.cell_diameter, self.n_cells, np.float64)
+            self.node_xyz = _arr(v.node_xyz, self.n_vnodes * 3, np.float64).reshape(-1, 3)
+            self.nse_constraints = ConstraintSet.from_view(v.nse)
+            self.T_constraints = ConstraintSet.from_view(v.T)
+            self.T0 = np.zeros(self.n_T)
+            lib().dcp_host_mesh_initial_temperature(h, _ptr(self.T0))
+        finally:
+            lib().dcp_host_mesh_destroy(h)
+        self.cuboid = bool(cuboid)
+        self.refine = refine
+        self.temperature_degree = temperature_degree
+
+
+def load_prm(path: str) -> RunParams:
+    rp = RunParams()
+    err = C.create_string_buffer(512)
+    rc = lib().dcp_prm_load(path.encode(), C.byref(rp), err, 512)
+    if rc != DCP_OK:
+        raise DcpError(rc, err.value.decode())
+    return rp
+
+
+class Context:
+    """One GPU context (dcp_ctx)."""
+
+    def __init__(self, device=0, rank=0, world_size=1, nccl_id=None):
+        cfg = Config(device, rank, world_size, None)
+        h = C.c_void_p()
+        rc = lib().dcp_ctx_create(C.byref(cfg), C.byref(h))
+        if rc != DCP_OK:
+            raise DcpError(rc, lib().dcp_last_error(None).decode())
+        self._h = h
+        self.mesh = None
+
+    def close(self):
+        if self._h:
+            lib().dcp_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, allow_not_converged=False):
+        if rc == DCP_OK or (allow_not_converged and rc == DCP_NOT_CONVERGED):
+            return rc
+        raise DcpError(rc, lib().dcp_last_error(self._h).decode())
+
+    # -- setup
+    def set_physics(self, ph: Physics):
+        self.physics = ph
+        self._check(lib().dcp_set_physics(self._h, C.byref(ph)))
+
+    def set_time_step(self, dt: float):
+        self._check(lib().dcp_set_time_step(self._h, float(dt)))
+
+    def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
+        nc = (nse_constraints or m.nse_constraints).as_struct()
+        tc = (T_constraints or m.T_constraints).as_struct()
+        self._keep = (m, nse_constraints, T_constraints)
+        self._check(lib().dcp_mesh_upload(
+            self._h, m.n_cells, _ptr(m.cell_nse_dofs), _ptr(m.cell_T_dofs),
+            _ptr(m.cell_geometry), _ptr(m.cell_diameter), m.n_u, m.n_p, m.n_T,
+            C.byref(nc), C.byref(tc)))
+        self.mesh = m
+
+    # -- state
+    def _size(self, field):
+        m = self.mesh
+        return m.n_u + m.n_p if field in (NSE_SOLUTION, OLD_NSE_SOLUTION, NSE_RHS) else m.n_T
+
+    def set_state(self, field, values):
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        self._check(lib().dcp_state_set(self._h, field, _ptr(a), a.size))
+
+    def get_state(self, field):
+        a = np.zeros(self._size(field))
+        self._check(lib().dcp_state_get(self._h, field, _ptr(a), a.size))
+        return a
+
+    def copy_state(self, dst, src):
+        self._check(lib().dcp_state_copy(self._h, dst, src))
+
+    def device_ptr(self, field):
+        return lib().dcp_state_device_ptr(self._h, field)
+
+    # -- hot path
+    def assemble_nse_system(self, matrix=True, rhs=True):
+        flags = (ASSEMBLE_MATRIX if matrix else 0) | (ASSEMBLE_RHS if rhs else 0)
+        self._check(lib().dcp_assemble_nse_system(self._h, flags))
+
+    def build_nse_preconditioner(self):
+        self._check(lib().dcp_build_nse_preconditioner(self._h))
+
+    def assemble_temperature_matrix(self):
+        self._check(lib().dcp_assemble_temperature_matrix(self._h))
+
+    def assemble_temperature_rhs(self):
+        self._check(lib().dcp_assemble_temperature_rhs(self._h))
+
+    def solve_nse(self):
+        o, i = C.c_int(0), C.c_int(0)
+        rc = self._check(lib().dcp_solve_nse(self._h, C.byref(o), C.byref(i)), True)
+        return rc, o.value, i.value
+
+    def solve_temperature(self):
+        it = C.c_int(0)
+        rng = np.zeros(2)
+        rc = self._check(lib().dcp_solve_temperature(
+            self._h, C.byref(it), rng.ctypes.data_as(C.POINTER(C.c_double))), True)
+        return rc, it.value, rng
+
+    def max_velocity(self):
+        v = C.c_double()
+        self._check(lib().dcp_max_velocity(self._h, C.byref(v)))
+        return v.value
+
+    def cfl_number(self):
+        v = C.c_double()
+        self._check(lib().dcp_cfl_number(self._h, C.byref(v)))
+        return v.value
+
+    def advance_state(self):
+        self._check(lib().dcp_advance_state(self._h))
+
+    # -- exports
+    def nse_matrix_csr(self):
+        nnz = C.c_int64()
+        self._check(lib().dcp_nse_matrix_export(self._h, C.byref(nnz), None, None, None))
+        n = self.mesh.n_u + self.mesh.n_p
+        rp = np.zeros(n + 1, np.int32)
+        cols = np.zeros(nnz.value, np.int32)
+        vals = np.zeros(nnz.value)
+        self._check(lib().dcp_nse_matrix_export(self._h, C.byref(nnz), _ptr(rp), _ptr(cols),
+                                                _ptr(vals)))
+        return rp, cols, vals
+
+    def T_matrix_csr(self):
+        nnz = C.c_int64()
+        self._check(lib().dcp_T_matrix_export(self._h, C.byref(nnz), None, None, None))
+        rp = np.zeros(self.mesh.n_T + 1, np.int32)
+        cols = np.zeros(nnz.value, np.int32)
+        vals = np.zeros(nnz.value)
+        self._check(lib().dcp_T_matrix_export(self._h, C.byref(nnz), _ptr(rp), _ptr(cols),
+                                              _ptr(vals)))
+        return rp, cols, vals
+
+    def precond_diagonals(self):
+        a = np.zeros(self.mesh.n_u)
+        p = np.zeros(self.mesh.n_p)
+        self._check(lib().dcp_precond_diagonals(self._h, _ptr(a), _ptr(p)))
+        return a, p
+
+    def cell_nse_system(self, first, n):
+        K = np.zeros((n, 89, 89))
+        f = np.zeros((n, 89))
+        self._check(lib().dcp_cell_nse_system(self._h, int(first), int(n), _ptr(K), _ptr(f)))
+        return K, f
+
+    def timings(self) -> dict:
+        t = Timings()
+        self._check(lib().dcp_get_timings(self._h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in Timings._fields_}
+
+    # -- operators on host arrays (copied through the device state buffers)
+    def _dev_roundtrip(self, fn, src, n_out):
+        import torch  # device memory plumbing only
+        d_src = torch.as_tensor(np.ascontiguousarray(src), device="cuda")
+        d_dst = torch.zeros(n_out, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        rc = fn(C.c_void_p(d_src.data_ptr()), C.c_void_p(d_dst.data_ptr()))
+        torch.cuda.synchronize()
+        return rc, d_dst.cpu().numpy()
+
+    def nse_vmult(self, src):
+        n = self.mesh.n_u + self.mesh.n_p
+        rc, out = self._dev_roundtrip(lambda s, d: lib().dcp_nse_vmult(self._h, s, d), src, n)
+        self._check(rc)
+        return out
+
+    def schur_vmult(self, src_p):
+        rc, out = self._dev_roundtrip(lambda s, d: lib().dcp_schur_vmult(self._h, s, d), src_p,
+                                      self.mesh.n_p)
+        self._check(rc)
+        return out
+
+    def block_preconditioner_vmult(self, src, do_solve_A=False):
+        n = self.mesh.n_u + self.mesh.n_p
+        it = C.c_int(0)
+        rc, out = self._dev_roundtrip(
+            lambda s, d: lib().dcp_block_preconditioner_vmult(self._h, s, d, int(do_solve_A),
+                                                              C.byref(it)), src, n)
+        self._check(rc, True)
+        return out, it.value
+
+
+def physics_from_params(rp: RunParams) -> Physics:
+    p = Physics()
+    C.pointer(p)[0] = rp.physics
+    return p
+
+
+def classic_physics(time_step=0.1) -> Physics:
+    """data/aqua_planet_shell_test_3d-classic.prm derived constants (L = U = 1,
+    nu = 1e-2, kappa = 1e-3, beta = 0.2, T_ref = 2, g = 1)."""
+    return Physics(time_step, 1.0 / 100.0, 1.0 / 1000.0, 0.2, 2.0, 1.0, 1.0, 1.0, 1.0, 0, 1, 1)

@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark of the Boussinesq per-time-step hot path on MI355X.
+
+Workload (BASELINE.json metric): 3D hypershell, classic Q2/Q1 Taylor-Hood,
+global refinement 5 (196,608 cells, 4,995,528 NSE dofs + 202,818 T dofs),
+data/aqua_planet_shell_test_3d-classic.prm physics, the reference initial state
+(u = 0, two-Gaussian temperature), synthetic mesh (equiangular cube-sphere).
+
+One "step" = one full reference time step (Standard::BoussinesqModel::run body,
+boussinesq_model.tpp:1843-1926): assemble_nse_system, build_nse_preconditioner,
+assemble_temperature_matrix/_rhs, solve_NSE_block_preconditioned (FGMRES with
+the block-Schur preconditioner and its inner GMRES), solve_temperature,
+get_cfl_number/get_maximal_velocity. Every step restarts from the initial
+state (the classic configuration runs exactly this one step, Q24).
+
+Output: one JSON line (rank 0). value = assembled NSE DoFs/s of the
+assemble_nse_system phase; GMRES iteration rates, per-phase times, the
+Schur-complement apply roofline and the CPU oracle baseline ride along.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-dycoreplanet_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--refine", type=int, default=5)
+    ap.add_argument("--prm", default=os.path.join(ROOT, "configs",
+                                                  "aqua_planet_shell_test_3d-classic.prm"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-refine", type=int, default=3)
+    return ap.parse_args()
+
+
+def schur_bytes(m, nnzb_bt, nnzb_b):
+    """Algorithmic HBM bytes of one Schur-complement apply B D_A^-1 B^T
+    (schur_complement.hpp:143-150) on the block-CSR layout:
+    B^T: 3x1 blocks (24 B values + 4 B column) + row pointers, gathered p (8 n_p),
+    tmp1 write (8 n_u); Jacobi: tmp1 + inv-diag read, tmp2 write (24 n_u);
+    B: 1x3 blocks (24 + 4 B) + row pointers, gathered tmp2 (8 n_u), dst (8 n_p)."""
+    n_v = m.n_u // 3
+    bt = 28 * nnzb_bt + 4 * (n_v + 1) + 8 * m.n_p + 8 * m.n_u
+    jac = 24 * m.n_u
+    b = 28 * nnzb_b + 4 * (m.n_p + 1) + 8 * m.n_u + 8 * m.n_p
+    return bt + jac + b
+
+
+def cpu_baseline(refine):
+    """Oracle (C++ restatement of assemble_nse_system, 1 core) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dcp
+    import oracle_py
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    orc = oracle_py.Model(ph, m)
+    u = np.zeros(m.n_u + m.n_p)
+    t0 = time.perf_counter()
+    orc.assemble_nse_system(u, m.T0)
+    dt = time.perf_counter() - t0
+    return {"value": (m.n_u + m.n_p) / dt, "unit": "assembled DoFs/s", "cores": 1, "kind": "port",
+            "sample": f"full assemble_nse_system (element matrices + AffineConstraints "
+                      f"distribute into CSR) of the refine={refine} shell: {m.n_cells} cells, "
+                      f"{m.n_u + m.n_p} NSE dofs, {dt:.2f} s on 1 core"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        import torch
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    import dcp
+
+    rp = dcp.load_prm(args.prm)
+    ph = dcp.physics_from_params(rp)
+    t_setup = time.perf_counter()
+    m = dcp.HostMesh(cuboid=False, refine=args.refine, R0=rp.R0, R1=rp.R1, length=rp.length,
+                     temperature_degree=ph.temperature_degree)
+    ctx = dcp.Context(device=local_rank)
+    ctx.set_physics(ph)
+    ctx.upload_mesh(m)
+    u0 = np.zeros(m.n_u + m.n_p)
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u0), (dcp.OLD_T_SOLUTION, m.T0)):
+        ctx.set_state(f, v)
+    t_setup = time.perf_counter() - t_setup
+
+    def step():
+        ctx.copy_state(dcp.NSE_SOLUTION, dcp.OLD_NSE_SOLUTION)
+        ctx.copy_state(dcp.T_SOLUTION, dcp.OLD_T_SOLUTION)
+        ctx.cfl_number()
+        ctx.max_velocity()
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        ctx.assemble_temperature_matrix()
+        ctx.assemble_temperature_rhs()
+        rc, outer, inner = ctx.solve_nse()
+        rcT, itT, _ = ctx.solve_temperature()
+        t = ctx.timings()
+        return rc, outer, inner, itT, t
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    barrier()
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    recs = [step() for _ in range(args.steps)]
+    hip.hipDeviceSynchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    n_nse = m.n_u + m.n_p
+    asm_ms = np.mean([r[4]["assemble_nse_ms"] for r in recs])
+    solve_ms = np.mean([r[4]["solve_nse_ms"] for r in recs])
+    outer = recs[-1][1]
+    inner = recs[-1][2]
+    schur_ms = np.mean([r[4]["schur_apply_ms_avg"] for r in recs])
+    nnzb_bt = int(ctx._nnzb_bt) if hasattr(ctx, "_nnzb_bt") else None
+    # nnz of the 3x1 / 1x3 blocks from the exported pattern size identities
+    rp_, cols, _ = (None, None, None)
+    n_v = m.n_u // 3
+    # B^T and B have identical block counts (node-vertex incidences)
+    nnz_total = None
+    try:
+        import ctypes as C
+        nnz = C.c_int64()
+        dcp.lib().dcp_nse_matrix_export(ctx._h, C.byref(nnz), None, None, None)
+        nnz_total = nnz.value
+    except Exception:
+        pass
+    # node-vertex incidences: every (vnode, vertex) pair sharing a cell
+    q2 = m.cell_nse_dofs[:, [0] + list(range(32, 89, 3))][:, :]
+    nodes = np.concatenate([m.cell_nse_dofs[:, 0:32:4], m.cell_nse_dofs[:, 32::3]], axis=1) // 3
+    pv = m.cell_nse_dofs[:, 3:32:4] - m.n_u
+    pairs = np.unique(nodes[:, :, None].astype(np.int64) * m.n_p + pv[:, None, :], axis=None)
+    nnzb = int(pairs.size)
+    sbytes = schur_bytes(m, nnzb, nnzb)
+    achieved = sbytes / (schur_ms * 1e-3) / 1e9 if schur_ms > 0 else 0.0
+    value = n_nse / (asm_ms * 1e-3) * world
+    out = {
+        "metric": "assembled DoFs/sec + GMRES iter/sec, 3D shell Q2/Q1 refine=5, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "assembled DoFs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic refined hypershell (equiangular cube-sphere), reference initial state",
+        "config": {"workload": f"classic shell Q2/Q1 refine={args.refine}, one full time step",
+                   "cells": m.n_cells, "nse_dofs": n_nse, "T_dofs": m.n_T,
+                   "parallelism": "single GPU" if world == 1 else f"{world} independent replicas"},
+        "gmres_outer_iter_per_s": outer / (solve_ms * 1e-3),
+        "gmres_inner_iter_per_s": inner / (solve_ms * 1e-3),
+        "fgmres_outer_iterations": outer,
+        "schur_gmres_inner_iterations": inner,
+        "T_cg_iterations": recs[-1][3],
+        "phase_ms": {k: float(np.mean([r[4][k] for r in recs])) for k in recs[0][4]
+                     if k.endswith("_ms") or k.endswith("_avg")},
+        "setup_s": t_setup,
+        "roofline": {"kernel": "Schur complement apply B D_A^-1 B^T (3 kernels)", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_refine)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

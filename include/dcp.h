@@ -1,0 +1,195 @@
+/*
+ * dcp.h — C ABI of the MI355X-native Boussinesq dynamical-core hot path
+ * (libdcp.so). Drop-in boundary for the per-time-step work of
+ * konsim83/3D-DyCorePlanet's Standard::BoussinesqModel<3>
+ * (include/core/boussinesq_model.tpp). Every entry point below names the
+ * reference member whose body it replaces.
+ *
+ * Conventions
+ *   - Plain C types only; no exceptions cross the boundary. Every call returns
+ *     DCP_OK (0), DCP_NOT_CONVERGED (1) or a negative error code; the message
+ *     of the last failure is available from dcp_last_error().
+ *   - Ownership: the caller owns every host buffer it passes; the library owns
+ *     all device buffers. Outputs are caller-allocated.
+ *   - Threading: one context per GPU / rank, calls on one context are not
+ *     re-entrant.
+ *   - DoF layout is the reference's after DoFRenumbering::component_wise(
+ *     {0,0,0,1}) (boussinesq_model.tpp:204): NSE vector = [velocity (n_u) |
+ *     pressure (n_p)], cell dof indices in FESystem(FE_Q(2)^3, FE_Q(1)) local
+ *     order (89 per cell), exactly what cell->get_dof_indices() returns.
+ *   - Geometry: per cell the 27 Q2 mapping support points in lexicographic
+ *     order (x fastest), already divided by the reference length.
+ *   - Arithmetic: IEEE FP64 throughout.
+ */
+#ifndef DCP_H
+#define DCP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  DCP_OK = 0,
+  DCP_NOT_CONVERGED = 1,      /* SolverControl::NoConvergence (boussinesq_model.tpp:1203) */
+  DCP_ERR_INVALID = -1,       /* bad argument / shape mismatch */
+  DCP_ERR_UNSUPPORTED = -2,   /* input the device path does not implement */
+  DCP_ERR_DEVICE = -3,        /* HIP / RCCL failure or no GPU */
+  DCP_ERR_STATE = -4          /* call out of order (e.g. solve before assemble) */
+};
+
+typedef struct dcp_ctx dcp_ctx;
+
+/* Derived, non-dimensional model constants (CoreModelData::Parameters after
+ * parse + rescaling, boussinesq_model.tpp:14-65, core_model_data.cc:7-22). */
+typedef struct {
+  double time_step;             /* parameters.time_step */
+  double one_over_reynolds;     /* 1 / Re */
+  double one_over_peclet;       /* 1 / Pe */
+  double expansion_coefficient; /* beta */
+  double temperature_ref;       /* reference_quantities.temperature_ref */
+  double gravity_scale;         /* L / U^2 */
+  double gravity_constant;      /* g */
+  double coriolis_scale;        /* L / U */
+  double omega;                 /* planetary angular velocity */
+  int cuboid;                   /* parameters.cuboid_geometry */
+  int nse_solver_interval;      /* parameters.NSE_solver_interval */
+  int temperature_degree;       /* 1 (device path); 2 reserved */
+} dcp_physics;
+
+/* A closed AffineConstraints object in CSR form (one line per constrained dof). */
+typedef struct {
+  int n_lines;
+  const int* line_dof;          /* [n_lines] */
+  const int* entry_ptr;         /* [n_lines + 1] */
+  const int* entry_dof;         /* [entry_ptr[n_lines]] */
+  const double* entry_w;
+  const double* inhomogeneity;  /* [n_lines] */
+} dcp_constraints;
+
+typedef struct {
+  int device;           /* HIP device ordinal (local rank) */
+  int rank;             /* rank in the node-local communicator */
+  int world_size;       /* number of ranks / GPUs */
+  const void* nccl_id;  /* ncclUniqueId (128 bytes) when world_size > 1, else NULL */
+} dcp_config;
+
+/* Context / errors ------------------------------------------------------- */
+int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out);
+void dcp_ctx_destroy(dcp_ctx* ctx);
+const char* dcp_last_error(const dcp_ctx* ctx);   /* ctx may be NULL */
+int dcp_device_count(void);
+
+/* Replaces the Parameters-derived scalars read inside the local_assemble_*
+ * workers (boussinesq_model.tpp:434-438, 564-568, 760-764, 907-911). */
+int dcp_set_physics(dcp_ctx* ctx, const dcp_physics* ph);
+/* parameters.time_step (changed by recompute_time_step, :1104-1125). */
+int dcp_set_time_step(dcp_ctx* ctx, double dt);
+
+/* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
+ * device sparsity patterns, cell colouring and scatter maps once. */
+int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs /*[n][89]*/,
+                    const int32_t* cell_T_dofs /*[n][8]*/, const double* cell_geometry /*[n][27][3]*/,
+                    const double* cell_diameter /*[n]*/, int n_u, int n_p, int n_T,
+                    const dcp_constraints* nse_constraints,
+                    const dcp_constraints* T_constraints);
+
+/* Device-resident state vectors ----------------------------------------- */
+enum {
+  DCP_NSE_SOLUTION = 0,      /* nse_solution (n_u + n_p) */
+  DCP_OLD_NSE_SOLUTION = 1,  /* old_nse_solution */
+  DCP_T_SOLUTION = 2,        /* temperature_solution (n_T) */
+  DCP_OLD_T_SOLUTION = 3,    /* old_temperature_solution */
+  DCP_NSE_RHS = 4,           /* nse_rhs */
+  DCP_T_RHS = 5              /* temperature_rhs */
+};
+int dcp_state_set(dcp_ctx* ctx, int field, const double* host, size_t n);
+int dcp_state_get(dcp_ctx* ctx, int field, double* host, size_t n);
+/* dst <- src (device copy), e.g. nse_solution <- old_nse_solution. */
+int dcp_state_copy(dcp_ctx* ctx, int dst_field, int src_field);
+/* Device pointer of a state field (for zero-copy interop). */
+double* dcp_state_device_ptr(dcp_ctx* ctx, int field);
+
+/* Hot path (one call per reference member) ------------------------------ */
+/* assemble_nse_system (:691-740): nse_matrix + nse_rhs from old_nse_solution
+ * and old_temperature_solution. flags: DCP_ASSEMBLE_MATRIX | DCP_ASSEMBLE_RHS. */
+enum { DCP_ASSEMBLE_MATRIX = 1, DCP_ASSEMBLE_RHS = 2 };
+int dcp_assemble_nse_system(dcp_ctx* ctx, int flags);
+/* assemble_nse_preconditioner + build_nse_preconditioner (:479-542): the
+ * point-Jacobi diagonals of P.block(0,0) and P.block(1,1). */
+int dcp_build_nse_preconditioner(dcp_ctx* ctx);
+/* assemble_temperature_matrix (:821-864). */
+int dcp_assemble_temperature_matrix(dcp_ctx* ctx);
+/* assemble_temperature_rhs (:966-1020); uses nse_solution (Q5). */
+int dcp_assemble_temperature_rhs(dcp_ctx* ctx);
+/* solve_NSE_block_preconditioned (:1131-1245) incl. the NoConvergence
+ * fallback; returns DCP_NOT_CONVERGED only if the fallback fails too. */
+int dcp_solve_nse(dcp_ctx* ctx, int* outer_iterations, int* inner_iterations);
+/* solve_temperature (:1417-1476). T_range may be NULL or double[2]. */
+int dcp_solve_temperature(dcp_ctx* ctx, int* iterations, double* T_range);
+/* get_maximal_velocity / get_cfl_number (:1023-1101) on nse_solution. */
+int dcp_max_velocity(dcp_ctx* ctx, double* out);
+int dcp_cfl_number(dcp_ctx* ctx, double* out);
+/* old <- current for both fields (:1921-1922). */
+int dcp_advance_state(dcp_ctx* ctx);
+
+/* Operators on device vectors (LinearAlgebra vmult seam) ----------------- */
+int dcp_nse_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst);          /* nse_matrix */
+int dcp_schur_vmult(dcp_ctx* ctx, const double* d_src_p, double* d_dst_p);    /* schur_complement.hpp:143-150 */
+/* BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70). */
+int dcp_block_preconditioner_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst,
+                                   int do_solve_A, int* inner_iterations);
+
+/* Parity / export ------------------------------------------------------- */
+/* nse_matrix as scalar CSR (rows n_u+n_p); call with NULL arrays to get nnz. */
+int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals);
+int dcp_T_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals);
+int dcp_precond_diagonals(dcp_ctx* ctx, double* A_diag, double* Mp_diag);
+/* Element matrices of local_assemble_nse_system for cells [first, first+n):
+ * K [n][89][89], f [n][89] in FESystem order (CopyData::NSESystem). */
+int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
+
+/* Timing of the last hot-path calls (device time, milliseconds). */
+typedef struct {
+  double assemble_nse_ms, build_precond_ms, assemble_T_matrix_ms, assemble_T_rhs_ms;
+  double solve_nse_ms, solve_T_ms;
+  double schur_apply_ms_avg; /* average device time of one Schur-complement apply */
+  long schur_applies;
+} dcp_timings;
+int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
+
+/* Host setup helpers (mesh generator, .prm) ----------------------------- */
+typedef struct dcp_host_mesh dcp_host_mesh;
+/* Builds the refined shell (cuboid = 0) or cube, DoFs and constraints the way
+ * setup_dofs() does (see mesh.h for the geometry convention). */
+dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
+                                    int temperature_degree);
+void dcp_host_mesh_destroy(dcp_host_mesh* m);
+typedef struct {
+  int n_cells, n_u, n_p, n_T, n_vnodes;
+  const int32_t* cell_nse_dofs;   /* [n_cells][89] */
+  const int32_t* cell_T_dofs;     /* [n_cells][8] */
+  const double* cell_geometry;    /* [n_cells][27][3] */
+  const double* cell_diameter;    /* [n_cells] */
+  const double* node_xyz;         /* [n_vnodes][3] */
+  dcp_constraints nse, T;
+} dcp_host_mesh_view;
+int dcp_host_mesh_view_get(const dcp_host_mesh* m, dcp_host_mesh_view* out);
+/* T dof values of the initial temperature at the support points. */
+int dcp_host_mesh_initial_temperature(const dcp_host_mesh* m, double* T);
+
+/* .prm -> dcp_physics (+ refinement etc.), CoreModelData::Parameters(file). */
+typedef struct {
+  dcp_physics physics;
+  int initial_global_refinement, space_dimension, nse_velocity_degree;
+  int use_schur_complement_solver, use_FEEC_solver, adapt_time_step;
+  double final_time, R0, R1, length;
+} dcp_run_params;
+int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

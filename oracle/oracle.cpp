@@ -1,0 +1,1160 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.h). CPU restatement of the
+// reference hot path. Reference paths are relative to konsim83/3D-DyCorePlanet.
+#include "oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Reference element (deal.II FE_Q / FESystem / QGauss conventions).
+
+// FE_Q(2) hierarchic -> lexicographic (vertices, lines 0..11, faces 0..5, interior).
+const int kHier2Lex[27] = {0, 2, 6, 8, 18, 20, 24, 26, 3, 5, 1, 7, 21, 23,
+                           19, 25, 9, 11, 15, 17, 12, 14, 10, 16, 4, 22, 13};
+const int kVertexLex[8] = {0, 2, 6, 8, 18, 20, 24, 26};
+
+double lag2(int a, double x) {
+  return a == 0 ? 2 * (x - 0.5) * (x - 1) : a == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+}
+double dlag2(int a, double x) { return a == 0 ? 4 * x - 3 : a == 1 ? -8 * x + 4 : 4 * x - 1; }
+double lag1(int a, double x) { return a == 0 ? 1 - x : x; }
+double dlag1(int a, double) { return a == 0 ? -1.0 : 1.0; }
+
+// QGauss(n) on [0,1], n = 1..4.
+void gauss1d(int n, double* x, double* w) {
+  if (n == 1) {
+    x[0] = 0.5; w[0] = 1.0;
+  } else if (n == 2) {
+    const double d = 0.5 / std::sqrt(3.0);
+    x[0] = 0.5 - d; x[1] = 0.5 + d; w[0] = w[1] = 0.5;
+  } else if (n == 3) {
+    const double d = 0.5 * std::sqrt(0.6);
+    x[0] = 0.5 - d; x[1] = 0.5; x[2] = 0.5 + d;
+    w[0] = w[2] = 5.0 / 18.0; w[1] = 8.0 / 18.0;
+  } else if (n == 4) {
+    const double a = std::sqrt(3.0 / 7.0 - 2.0 / 7.0 * std::sqrt(6.0 / 5.0));
+    const double b = std::sqrt(3.0 / 7.0 + 2.0 / 7.0 * std::sqrt(6.0 / 5.0));
+    const double wa = (18.0 + std::sqrt(30.0)) / 36.0, wb = (18.0 - std::sqrt(30.0)) / 36.0;
+    x[0] = 0.5 - 0.5 * b; x[1] = 0.5 - 0.5 * a; x[2] = 0.5 + 0.5 * a; x[3] = 0.5 + 0.5 * b;
+    w[0] = w[3] = 0.5 * wb; w[1] = w[2] = 0.5 * wa;
+  } else {
+    throw std::invalid_argument("QGauss n");
+  }
+}
+
+struct Vec3 {
+  double v[3] = {0, 0, 0};
+  double& operator[](int i) { return v[i]; }
+  double operator[](int i) const { return v[i]; }
+};
+double dot(const Vec3& a, const Vec3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// FEValues for one cell: Q2 isoparametric mapping from the 27 lexicographic
+// geometry nodes; Q2 and Q1 scalar shapes with physical gradients.
+struct CellValues {
+  int nq = 0;
+  std::vector<double> JxW;
+  std::vector<Vec3> xq;
+  std::vector<double> v2, v1;   // [q][27], [q][8]   (lexicographic / vertex order)
+  std::vector<Vec3> g2, g1;     // physical gradients
+
+  void reinit(const double* geom, int n1d) {
+    double qx[4], qw[4];
+    gauss1d(n1d, qx, qw);
+    nq = n1d * n1d * n1d;
+    JxW.assign(nq, 0);
+    xq.assign(nq, Vec3());
+    v2.assign(size_t(nq) * 27, 0);
+    v1.assign(size_t(nq) * 8, 0);
+    g2.assign(size_t(nq) * 27, Vec3());
+    g1.assign(size_t(nq) * 8, Vec3());
+    for (int q = 0; q < nq; ++q) {
+      const double p[3] = {qx[q % n1d], qx[(q / n1d) % n1d], qx[q / (n1d * n1d)]};
+      const double w = qw[q % n1d] * qw[(q / n1d) % n1d] * qw[q / (n1d * n1d)];
+      double rv2[27], rg2[27][3], rv1[8], rg1[8][3];
+      for (int n = 0; n < 27; ++n) {
+        const int a = n % 3, b = (n / 3) % 3, c = n / 9;
+        rv2[n] = lag2(a, p[0]) * lag2(b, p[1]) * lag2(c, p[2]);
+        rg2[n][0] = dlag2(a, p[0]) * lag2(b, p[1]) * lag2(c, p[2]);
+        rg2[n][1] = lag2(a, p[0]) * dlag2(b, p[1]) * lag2(c, p[2]);
+        rg2[n][2] = lag2(a, p[0]) * lag2(b, p[1]) * dlag2(c, p[2]);
+      }
+      for (int n = 0; n < 8; ++n) {
+        const int a = n & 1, b = (n >> 1) & 1, c = n >> 2;
+        rv1[n] = lag1(a, p[0]) * lag1(b, p[1]) * lag1(c, p[2]);
+        rg1[n][0] = dlag1(a, p[0]) * lag1(b, p[1]) * lag1(c, p[2]);
+        rg1[n][1] = lag1(a, p[0]) * dlag1(b, p[1]) * lag1(c, p[2]);
+        rg1[n][2] = lag1(a, p[0]) * lag1(b, p[1]) * dlag1(c, p[2]);
+      }
+      // Jacobian J[i][j] = d x_i / d xi_j
+      double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+      Vec3 x;
+      for (int n = 0; n < 27; ++n)
+        for (int i = 0; i < 3; ++i) {
+          x[i] += geom[3 * n + i] * rv2[n];
+          for (int j = 0; j < 3; ++j) J[i][j] += geom[3 * n + i] * rg2[n][j];
+        }
+      const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                         J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                         J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+      if (!(det > 0)) throw std::runtime_error("oracle: non-positive Jacobian");
+      double Ji[3][3];  // inverse
+      Ji[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / det;
+      Ji[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / det;
+      Ji[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / det;
+      Ji[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / det;
+      Ji[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / det;
+      Ji[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / det;
+      Ji[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / det;
+      Ji[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / det;
+      Ji[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / det;
+      JxW[q] = det * w;
+      xq[q] = x;
+      // physical gradient: grad_i = sum_j dN/dxi_j * Ji[j][i]
+      for (int n = 0; n < 27; ++n) {
+        v2[27 * q + n] = rv2[n];
+        for (int i = 0; i < 3; ++i)
+          g2[27 * q + n][i] = rg2[n][0] * Ji[0][i] + rg2[n][1] * Ji[1][i] + rg2[n][2] * Ji[2][i];
+      }
+      for (int n = 0; n < 8; ++n) {
+        v1[8 * q + n] = rv1[n];
+        for (int i = 0; i < 3; ++i)
+          g1[8 * q + n][i] = rg1[n][0] * Ji[0][i] + rg1[n][1] * Ji[1][i] + rg1[n][2] * Ji[2][i];
+      }
+    }
+  }
+};
+
+// FESystem(FE_Q(2)^3, FE_Q(1)) local dof i -> (component, scalar shape index).
+// Scalar index: lexicographic Q2 node for velocity, vertex for pressure.
+struct SysDof {
+  int comp, idx;
+};
+SysDof sysdof(int i) {
+  if (i < 32) return {i % 4, i % 4 == 3 ? i / 4 : kHier2Lex[i / 4]};
+  return {(i - 32) % 3, kHier2Lex[8 + (i - 32) / 3]};
+}
+
+// Temperature FE_Q(k) hierarchic local dof -> value/grad accessors.
+double T_value(const CellValues& cv, int deg, int q, int k) {
+  return deg == 1 ? cv.v1[8 * q + k] : cv.v2[27 * q + kHier2Lex[k]];
+}
+const Vec3& T_grad(const CellValues& cv, int deg, int q, int k) {
+  return deg == 1 ? cv.g1[8 * q + k] : cv.g2[27 * q + kHier2Lex[k]];
+}
+int T_dofs_per_cell(int deg) { return deg == 1 ? 8 : 27; }
+
+// Per-q views of the NSE system shape functions (FEValuesViews::Vector /
+// Scalar): value, gradient (row = component), symmetric gradient, divergence.
+struct NseShapes {
+  Vec3 phi_u[89];
+  double grad[89][3][3];
+  double eps[89][3][3];
+  double div[89];
+  double phi_p[89];
+  void at(const CellValues& cv, int q) {
+    for (int k = 0; k < 89; ++k) {
+      const SysDof s = sysdof(k);
+      phi_u[k] = Vec3();
+      std::memset(grad[k], 0, sizeof(grad[k]));
+      std::memset(eps[k], 0, sizeof(eps[k]));
+      div[k] = 0;
+      phi_p[k] = 0;
+      if (s.comp < 3) {
+        const double v = cv.v2[27 * q + s.idx];
+        const Vec3& g = cv.g2[27 * q + s.idx];
+        phi_u[k][s.comp] = v;
+        for (int d = 0; d < 3; ++d) grad[k][s.comp][d] = g[d];
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) eps[k][a][b] = 0.5 * (grad[k][a][b] + grad[k][b][a]);
+        div[k] = g[s.comp];
+      } else {
+        phi_p[k] = cv.v1[8 * q + s.idx];
+      }
+    }
+  }
+};
+
+double ddot(const double a[3][3], const double b[3][3]) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) s += a[i][j] * b[i][j];
+  return s;
+}
+
+// CoreModelData::gravity_vector (core_model_data.tpp:97-106, Q4)
+Vec3 gravity_vector(const Vec3& p, double g) {
+  const double r = std::sqrt(dot(p, p));
+  Vec3 out;
+  for (int d = 0; d < 3; ++d) out[d] = (r > 1) ? -g * p[d] / r : -g * p[d] / std::sqrt(r);
+  return out;
+}
+
+Vec3 cross(const Vec3& a, const Vec3& b) {
+  Vec3 c;
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+  return c;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Element level
+
+extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom27,
+                                    const double* u_local, const double* T_local, double* K,
+                                    double* f) {
+  // boussinesq_model.tpp:550-673; QGauss(nse_velocity_degree + 1) = 3 (:708)
+  CellValues cv;
+  cv.reinit(geom27, 3);
+  const int tdeg = ph->temperature_degree, ntd = T_dofs_per_cell(tdeg);
+  std::fill(K, K + 89 * 89, 0.0);
+  std::fill(f, f + 89, 0.0);
+  static thread_local NseShapes sh;
+  for (int q = 0; q < cv.nq; ++q) {
+    sh.at(cv, q);
+    // get_function_values / get_function_gradients (dof-order sums)
+    double old_temperature = 0;
+    for (int k = 0; k < ntd; ++k) old_temperature += T_local[k] * T_value(cv, tdeg, q, k);
+    Vec3 old_velocity;
+    double G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int k = 0; k < 89; ++k) {
+      const SysDof s = sysdof(k);
+      if (s.comp == 3) continue;
+      old_velocity[s.comp] += u_local[k] * sh.phi_u[k][s.comp];
+      for (int d = 0; d < 3; ++d) G[s.comp][d] += u_local[k] * sh.grad[k][s.comp][d];
+    }
+    // :594-597 density_scaling = 1 - beta (T - T_ref)   (core_model_data.cc:88-94)
+    const double density_scaling =
+        1 - ph->expansion_coefficient * (old_temperature - ph->temperature_ref);
+    // :599-600 transpose(grad u); advection (u . grad) u = u * transpose(grad u)
+    Vec3 advection;
+    for (int j = 0; j < 3; ++j)
+      for (int i = 0; i < 3; ++i) advection[j] += old_velocity[i] * G[j][i];
+    // :615-621 Coriolis only on the cuboid (Q2)
+    Vec3 coriolis;
+    if (ph->cuboid) coriolis[2] = ph->coriolis_scale * ph->omega;
+    const double JxW = cv.JxW[q];
+    const double dt = ph->time_step;
+    // :626-637
+    for (int i = 0; i < 89; ++i)
+      for (int j = 0; j < 89; ++j)
+        K[89 * i + j] += (dot(sh.phi_u[i], sh.phi_u[j]) +
+                          dt * (ph->one_over_reynolds * 2 * ddot(sh.eps[i], sh.eps[j])) -
+                          (sh.div[i] * sh.phi_p[j]) - (sh.phi_p[i] * sh.div[j])) *
+                         JxW;
+    // :640-650
+    Vec3 gravity;
+    if (ph->cuboid) {
+      gravity[2] = -ph->gravity_constant;  // vertical_gravity_vector (core_model_data.tpp:86-95)
+    } else {
+      gravity = gravity_vector(cv.xq[q], ph->gravity_constant);
+    }
+    for (int d = 0; d < 3; ++d) gravity[d] *= ph->gravity_scale;
+    const Vec3 cor_x_u = cross(coriolis, old_velocity);
+    // :655-669 (3D branch)
+    for (int i = 0; i < 89; ++i)
+      f[i] += (dot(sh.phi_u[i], old_velocity) + dt * density_scaling * dot(gravity, sh.phi_u[i]) -
+               dt * dot(sh.phi_u[i], advection) - dt * (2 * dot(sh.phi_u[i], cor_x_u))) *
+              JxW;
+  }
+}
+
+extern "C" void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom27,
+                                            double* P) {
+  // boussinesq_model.tpp:421-464
+  CellValues cv;
+  cv.reinit(geom27, 3);
+  std::fill(P, P + 89 * 89, 0.0);
+  static thread_local NseShapes sh;
+  for (int q = 0; q < cv.nq; ++q) {
+    sh.at(cv, q);
+    const double JxW = cv.JxW[q];
+    for (int i = 0; i < 89; ++i)
+      for (int j = 0; j < 89; ++j)
+        P[89 * i + j] += (dot(sh.phi_u[i], sh.phi_u[j]) +
+                          ph->time_step * ph->one_over_reynolds * ddot(sh.grad[i], sh.grad[j]) +
+                          sh.phi_p[i] * sh.phi_p[j]) *
+                         JxW;
+  }
+}
+
+extern "C" void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom27,
+                                            double* M, double* Kt) {
+  // boussinesq_model.tpp:748-800, QGauss(temperature_degree + 2) (:834)
+  const int tdeg = ph->temperature_degree, n = T_dofs_per_cell(tdeg);
+  CellValues cv;
+  cv.reinit(geom27, tdeg + 2);
+  std::fill(M, M + n * n, 0.0);
+  std::fill(Kt, Kt + n * n, 0.0);
+  for (int q = 0; q < cv.nq; ++q) {
+    const double JxW = cv.JxW[q];
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        M[n * i + j] += T_value(cv, tdeg, q, i) * T_value(cv, tdeg, q, j) * JxW;
+        Kt[n * i + j] +=
+            dot(T_grad(cv, tdeg, q, i), T_grad(cv, tdeg, q, j)) * ph->one_over_peclet * JxW;
+      }
+  }
+}
+
+extern "C" void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom27,
+                                         const double* T_local, const double* u_local,
+                                         const int* inhom_mask, double* rhs, double* mfbc) {
+  // boussinesq_model.tpp:873-952, QGauss(temperature_degree + 2) (:990)
+  const int tdeg = ph->temperature_degree, n = T_dofs_per_cell(tdeg);
+  CellValues cv;
+  cv.reinit(geom27, tdeg + 2);
+  std::fill(rhs, rhs + n, 0.0);
+  std::fill(mfbc, mfbc + n * n, 0.0);
+  const double dt_eff = ph->time_step / ph->nse_solver_interval;  // Q8
+  const double gamma = 0;                                          // Q6
+  for (int q = 0; q < cv.nq; ++q) {
+    double old_T = 0;
+    Vec3 old_grad_T, old_u;
+    for (int k = 0; k < n; ++k) {
+      old_T += T_local[k] * T_value(cv, tdeg, q, k);
+      const Vec3& g = T_grad(cv, tdeg, q, k);
+      for (int d = 0; d < 3; ++d) old_grad_T[d] += T_local[k] * g[d];
+    }
+    for (int k = 0; k < 89; ++k) {
+      const SysDof s = sysdof(k);
+      if (s.comp < 3) old_u[s.comp] += u_local[k] * cv.v2[27 * q + s.idx];
+    }
+    const double JxW = cv.JxW[q];
+    for (int i = 0; i < n; ++i) {
+      const double phi_i = T_value(cv, tdeg, q, i);
+      rhs[i] += (phi_i * old_T - dt_eff * phi_i * dot(old_u, old_grad_T) - dt_eff * gamma * phi_i) * JxW;
+      if (inhom_mask[i])
+        for (int j = 0; j < n; ++j)
+          mfbc[n * j + i] += (phi_i * T_value(cv, tdeg, q, j) +
+                              dt_eff * ph->one_over_peclet *
+                                  dot(T_grad(cv, tdeg, q, i), T_grad(cv, tdeg, q, j))) *
+                             JxW;
+    }
+  }
+}
+
+// ===========================================================================
+// Global objects
+
+namespace {
+
+struct Cons {
+  std::vector<int> line_of;
+  std::vector<std::vector<std::pair<int, double>>> entries;
+  std::vector<double> inhom;
+  void init(int n, const orc_constraints* c) {
+    line_of.assign(n, -1);
+    entries.clear();
+    inhom.clear();
+    if (!c) return;
+    for (int l = 0; l < c->n_lines; ++l) {
+      line_of[c->line_dof[l]] = l;
+      std::vector<std::pair<int, double>> e;
+      for (int k = c->entry_ptr[l]; k < c->entry_ptr[l + 1]; ++k)
+        e.push_back({c->entry_dof[k], c->entry_w[k]});
+      entries.push_back(e);
+      inhom.push_back(c->inhomogeneity[l]);
+    }
+  }
+  bool constrained(int d) const { return line_of[d] >= 0; }
+  // distribute(): x_i = sum w x_t + g for every constrained i
+  void distribute(double* x) const {
+    for (size_t d = 0; d < line_of.size(); ++d) {
+      const int l = line_of[d];
+      if (l < 0) continue;
+      double v = inhom[l];
+      for (const auto& e : entries[l]) v += e.second * x[e.first];
+      x[d] = v;
+    }
+  }
+};
+
+struct Csr {
+  int n = 0;
+  std::vector<int> rowptr, cols;
+  std::vector<double> vals;
+  // sorted pattern from row sets
+  void build(const std::vector<std::vector<int>>& rows) {
+    n = int(rows.size());
+    rowptr.assign(n + 1, 0);
+    for (int r = 0; r < n; ++r) rowptr[r + 1] = rowptr[r] + int(rows[r].size());
+    cols.resize(rowptr[n]);
+    for (int r = 0; r < n; ++r) std::copy(rows[r].begin(), rows[r].end(), cols.begin() + rowptr[r]);
+    vals.assign(cols.size(), 0.0);
+  }
+  double& at(int r, int c) {
+    auto b = cols.begin() + rowptr[r], e = cols.begin() + rowptr[r + 1];
+    auto it = std::lower_bound(b, e, c);
+    if (it == e || *it != c) throw std::runtime_error("oracle: entry not in sparsity pattern");
+    return vals[it - cols.begin()];
+  }
+  void zero() { std::fill(vals.begin(), vals.end(), 0.0); }
+};
+
+void add_sorted_unique(std::vector<int>& v) {
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
+// Expansion of a local dof under the constraints: unconstrained -> itself,
+// constrained -> its targets with weights (AffineConstraints condensation).
+void expand(const Cons& c, int dof, std::vector<std::pair<int, double>>& out) {
+  out.clear();
+  const int l = c.line_of[dof];
+  if (l < 0) {
+    out.push_back({dof, 1.0});
+  } else {
+    for (const auto& e : c.entries[l]) out.push_back(e);
+  }
+}
+
+// make_sparsity_pattern(dof_handler, coupling, sp, constraints, false)
+// coupling(ci, cj) decides local pairs; constrained rows keep only their diagonal.
+template <class Coupling>
+void make_pattern(Csr& A, int n, int n_cells, int dpc, const int* cell_dofs, const Cons& cons,
+                  Coupling coupling) {
+  std::vector<std::vector<int>> rows(n);
+  std::vector<std::pair<int, double>> ei, ej;
+  for (int c = 0; c < n_cells; ++c) {
+    const int* d = cell_dofs + size_t(c) * dpc;
+    for (int i = 0; i < dpc; ++i) {
+      expand(cons, d[i], ei);
+      for (int j = 0; j < dpc; ++j) {
+        if (!coupling(i, j)) continue;
+        expand(cons, d[j], ej);
+        for (const auto& a : ei)
+          for (const auto& b : ej) rows[a.first].push_back(b.first);
+      }
+    }
+  }
+  for (int r = 0; r < n; ++r) {
+    if (cons.constrained(r)) rows[r].push_back(r);
+    add_sorted_unique(rows[r]);
+  }
+  A.build(rows);
+}
+
+// AffineConstraints::distribute_local_to_global(local_matrix, [local_vector],
+// dofs, global_matrix, [global_vector]) with use_inhomogeneities_for_rhs =
+// false: condensed entries C^T K C, constrained diagonals += |K_ii| (or the
+// mean |K_jj| when K_ii == 0), rhs_t += w f_i, inhomogeneities lifted into
+// unconstrained rows: rhs_r -= K_rj g_j.
+void distribute_local_to_global(const Cons& cons, int dpc, const int* dofs, const double* K,
+                                const double* f, Csr* A, double* rhs) {
+  std::vector<std::pair<int, double>> ei, ej;
+  bool any_constrained = false;
+  for (int i = 0; i < dpc; ++i) any_constrained |= cons.constrained(dofs[i]);
+  for (int i = 0; i < dpc; ++i) {
+    expand(cons, dofs[i], ei);
+    if (A)
+      for (int j = 0; j < dpc; ++j) {
+        const double k = K[dpc * i + j];
+        if (k == 0.0) continue;
+        expand(cons, dofs[j], ej);
+        for (const auto& a : ei)
+          for (const auto& b : ej) A->at(a.first, b.first) += a.second * b.second * k;
+      }
+    if (rhs && f) {
+      for (const auto& a : ei) rhs[a.first] += a.second * f[i];
+      // inhomogeneity of constrained columns j into the rows of i
+      for (int j = 0; j < dpc; ++j) {
+        const int l = cons.line_of[dofs[j]];
+        if (l < 0 || cons.inhom[l] == 0.0) continue;
+        for (const auto& a : ei) rhs[a.first] -= a.second * K[dpc * i + j] * cons.inhom[l];
+      }
+    }
+  }
+  if (A && any_constrained) {
+    double avg = 0;
+    for (int i = 0; i < dpc; ++i) avg += std::fabs(K[dpc * i + i]);
+    avg /= dpc;
+    for (int i = 0; i < dpc; ++i)
+      if (cons.constrained(dofs[i])) {
+        const double kii = std::fabs(K[dpc * i + i]);
+        A->at(dofs[i], dofs[i]) += (kii != 0.0 ? kii : avg);
+      }
+  }
+}
+
+// distribute_local_to_global(local_vector, dofs, global_vector, local_matrix)
+// (the matrix_for_bc variant used by assemble_temperature_rhs).
+void distribute_rhs_with_bc(const Cons& cons, int dpc, const int* dofs, const double* f,
+                            const double* Mbc, double* rhs) {
+  for (int i = 0; i < dpc; ++i) {
+    const int l = cons.line_of[dofs[i]];
+    if (l < 0) {
+      rhs[dofs[i]] += f[i];
+      continue;
+    }
+    const double val = cons.inhom[l];
+    if (val != 0.0)
+      for (int j = 0; j < dpc; ++j) {
+        const int lj = cons.line_of[dofs[j]];
+        if (lj < 0) {
+          rhs[dofs[j]] -= val * Mbc[dpc * j + i];
+        } else {
+          const double me = Mbc[dpc * j + i];
+          if (me == 0.0) continue;
+          for (const auto& e : cons.entries[lj]) rhs[e.first] -= val * e.second * me;
+        }
+      }
+    for (const auto& e : cons.entries[l]) rhs[e.first] += f[i] * e.second;
+  }
+}
+
+double norm2(const std::vector<double>& v, size_t b, size_t e) {
+  double s = 0;
+  for (size_t i = b; i < e; ++i) s += v[i] * v[i];
+  return std::sqrt(s);
+}
+
+// SolverControl::check (success is tested before failure)
+enum State { kIterate, kSuccess, kFailure };
+struct Control {
+  unsigned max_steps;
+  double tol;
+  unsigned last_step = 0;
+  double last_value = 0;
+  State check(unsigned step, double value) {
+    last_step = step;
+    last_value = value;
+    if (value <= tol) return kSuccess;
+    if (step >= max_steps || std::isnan(value)) return kFailure;
+    return kIterate;
+  }
+};
+
+struct NoConvergence {};
+
+}  // namespace
+
+struct orc_model {
+  orc_physics ph;
+  int n_cells, n_u, n_p, n_T, tdeg, tdpc;
+  std::vector<int> cell_nse, cell_T;
+  std::vector<double> geom;
+  Cons cnse, cT;
+  Csr nse;  // full nse_matrix (blocks by index range)
+  std::vector<double> nse_rhs;
+  std::vector<double> A_diag, Mp_diag, A_inv, Mp_inv;
+  Csr Tmass, Tstiff, Tmat;
+  std::vector<double> T_rhs, T_inv;
+  // scratch of the Schur complement (schur_complement.hpp:113)
+  mutable std::vector<double> tmp1, tmp2;
+  int inner_iterations = 0;
+};
+
+extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
+                                 const int* cell_T_dofs, const double* cell_geom, int n_u, int n_p,
+                                 int n_T, const orc_constraints* nse_c, const orc_constraints* T_c) {
+  auto m = new orc_model();
+  m->ph = *ph;
+  m->n_cells = n_cells;
+  m->n_u = n_u;
+  m->n_p = n_p;
+  m->n_T = n_T;
+  m->tdeg = ph->temperature_degree;
+  m->tdpc = T_dofs_per_cell(m->tdeg);
+  m->cell_nse.assign(cell_nse_dofs, cell_nse_dofs + size_t(n_cells) * 89);
+  m->cell_T.assign(cell_T_dofs, cell_T_dofs + size_t(n_cells) * m->tdpc);
+  m->geom.assign(cell_geom, cell_geom + size_t(n_cells) * 81);
+  m->cnse.init(n_u + n_p, nse_c);
+  m->cT.init(n_T, T_c);
+  // setup_nse_matrices (boussinesq_model.tpp:79-112): couple everything but p-p
+  make_pattern(m->nse, n_u + n_p, n_cells, 89, m->cell_nse.data(), m->cnse,
+               [](int i, int j) { return !(sysdof(i).comp == 3 && sysdof(j).comp == 3); });
+  m->nse_rhs.assign(n_u + n_p, 0.0);
+  // setup_temperature_matrices (:153-180): full coupling
+  make_pattern(m->Tmass, n_T, n_cells, m->tdpc, m->cell_T.data(), m->cT,
+               [](int, int) { return true; });
+  m->Tstiff = m->Tmass;
+  m->Tmat = m->Tmass;
+  m->T_rhs.assign(n_T, 0.0);
+  m->tmp1.assign(n_u, 0.0);
+  m->tmp2.assign(n_u, 0.0);
+  return m;
+}
+
+extern "C" void orc_destroy(orc_model* m) { delete m; }
+extern "C" void orc_set_time_step(orc_model* m, double dt) { m->ph.time_step = dt; }
+
+namespace {
+void gather(const std::vector<int>& cd, size_t c, int dpc, const double* src, double* out) {
+  for (int i = 0; i < dpc; ++i) out[i] = src[cd[c * dpc + i]];
+}
+}  // namespace
+
+extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T) {
+  // assemble_nse_system (:691-740); the four unused block matrices of :700-704 (Q22) are not kept.
+  m->nse.zero();
+  std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
+  std::vector<double> K(89 * 89), f(89), ul(89), Tl(27);
+  for (int c = 0; c < m->n_cells; ++c) {
+    gather(m->cell_nse, c, 89, old_nse, ul.data());
+    gather(m->cell_T, c, m->tdpc, old_T, Tl.data());
+    orc_cell_nse_system(&m->ph, &m->geom[81 * size_t(c)], ul.data(), Tl.data(), K.data(), f.data());
+    // copy_local_to_global_nse_system (:677-687)
+    distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)], K.data(), f.data(),
+                               &m->nse, m->nse_rhs.data());
+  }
+}
+
+extern "C" void orc_build_nse_preconditioner(orc_model* m) {
+  // assemble_nse_preconditioner (:479-514) + build_nse_preconditioner (:518-542).
+  // Only the diagonals of block(0,0) / block(1,1) are consumed (Ifpack point
+  // Jacobi), so the condensed diagonal is accumulated directly.
+  m->A_diag.assign(m->n_u, 0.0);
+  m->Mp_diag.assign(m->n_p, 0.0);
+  std::vector<double> P(89 * 89);
+  std::vector<std::pair<int, double>> ei, ej;
+  for (int c = 0; c < m->n_cells; ++c) {
+    orc_cell_nse_preconditioner(&m->ph, &m->geom[81 * size_t(c)], P.data());
+    const int* d = &m->cell_nse[89 * size_t(c)];
+    bool any = false;
+    for (int i = 0; i < 89; ++i) any |= m->cnse.constrained(d[i]);
+    for (int i = 0; i < 89; ++i) {
+      expand(m->cnse, d[i], ei);
+      for (int j = 0; j < 89; ++j) {
+        const double k = P[89 * i + j];
+        if (k == 0.0) continue;
+        expand(m->cnse, d[j], ej);
+        for (const auto& a : ei)
+          for (const auto& b : ej)
+            if (a.first == b.first) {
+              if (a.first < m->n_u)
+                m->A_diag[a.first] += a.second * b.second * k;
+              else
+                m->Mp_diag[a.first - m->n_u] += a.second * b.second * k;
+            }
+      }
+    }
+    if (any) {
+      double avg = 0;
+      for (int i = 0; i < 89; ++i) avg += std::fabs(P[89 * i + i]);
+      avg /= 89;
+      for (int i = 0; i < 89; ++i)
+        if (m->cnse.constrained(d[i])) {
+          const double kii = std::fabs(P[89 * i + i]);
+          const double v = kii != 0.0 ? kii : avg;
+          if (d[i] < m->n_u) m->A_diag[d[i]] += v; else m->Mp_diag[d[i] - m->n_u] += v;
+        }
+    }
+  }
+  m->A_inv.resize(m->n_u);
+  m->Mp_inv.resize(m->n_p);
+  for (int i = 0; i < m->n_u; ++i) m->A_inv[i] = 1.0 / m->A_diag[i];
+  for (int i = 0; i < m->n_p; ++i) m->Mp_inv[i] = 1.0 / m->Mp_diag[i];
+}
+
+extern "C" void orc_assemble_temperature_matrix(orc_model* m) {
+  // :821-864
+  m->Tmass.zero();
+  m->Tstiff.zero();
+  const int n = m->tdpc;
+  std::vector<double> M(n * n), K(n * n);
+  for (int c = 0; c < m->n_cells; ++c) {
+    orc_cell_temperature_matrix(&m->ph, &m->geom[81 * size_t(c)], M.data(), K.data());
+    const int* d = &m->cell_T[size_t(n) * c];
+    distribute_local_to_global(m->cT, n, d, M.data(), nullptr, &m->Tmass, nullptr);
+    distribute_local_to_global(m->cT, n, d, K.data(), nullptr, &m->Tstiff, nullptr);
+  }
+}
+
+extern "C" void orc_assemble_temperature_rhs(orc_model* m, const double* old_T,
+                                             const double* nse_solution) {
+  // :966-1020: T_matrix = M + dt/interval K, Jacobi rebuilt (:975-986)
+  const double dt_eff = m->ph.time_step / m->ph.nse_solver_interval;
+  for (size_t k = 0; k < m->Tmat.vals.size(); ++k)
+    m->Tmat.vals[k] = m->Tmass.vals[k] + dt_eff * m->Tstiff.vals[k];
+  m->T_inv.assign(m->n_T, 0.0);
+  for (int r = 0; r < m->n_T; ++r) m->T_inv[r] = 1.0 / m->Tmat.at(r, r);
+  std::fill(m->T_rhs.begin(), m->T_rhs.end(), 0.0);
+  const int n = m->tdpc;
+  std::vector<double> Tl(n), ul(89), rhs(n), mfbc(n * n);
+  std::vector<int> mask(n);
+  for (int c = 0; c < m->n_cells; ++c) {
+    const int* d = &m->cell_T[size_t(n) * c];
+    gather(m->cell_T, c, n, old_T, Tl.data());
+    gather(m->cell_nse, c, 89, nse_solution, ul.data());
+    for (int i = 0; i < n; ++i) mask[i] = m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0;
+    orc_cell_temperature_rhs(&m->ph, &m->geom[81 * size_t(c)], Tl.data(), ul.data(), mask.data(),
+                             rhs.data(), mfbc.data());
+    distribute_rhs_with_bc(m->cT, n, d, rhs.data(), mfbc.data(), m->T_rhs.data());
+  }
+}
+
+extern "C" long orc_nse_matrix_nnz(const orc_model* m) { return long(m->nse.cols.size()); }
+extern "C" void orc_nse_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals) {
+  std::copy(m->nse.rowptr.begin(), m->nse.rowptr.end(), rowptr);
+  std::copy(m->nse.cols.begin(), m->nse.cols.end(), cols);
+  std::copy(m->nse.vals.begin(), m->nse.vals.end(), vals);
+}
+extern "C" void orc_nse_rhs(const orc_model* m, double* out) {
+  std::copy(m->nse_rhs.begin(), m->nse_rhs.end(), out);
+}
+extern "C" void orc_precond_diagonals(const orc_model* m, double* A, double* Mp) {
+  std::copy(m->A_diag.begin(), m->A_diag.end(), A);
+  std::copy(m->Mp_diag.begin(), m->Mp_diag.end(), Mp);
+}
+extern "C" long orc_T_matrix_nnz(const orc_model* m) { return long(m->Tmat.cols.size()); }
+extern "C" void orc_T_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals) {
+  std::copy(m->Tmat.rowptr.begin(), m->Tmat.rowptr.end(), rowptr);
+  std::copy(m->Tmat.cols.begin(), m->Tmat.cols.end(), cols);
+  std::copy(m->Tmat.vals.begin(), m->Tmat.vals.end(), vals);
+}
+extern "C" void orc_T_rhs(const orc_model* m, double* out) {
+  std::copy(m->T_rhs.begin(), m->T_rhs.end(), out);
+}
+
+// ===========================================================================
+// Operators
+
+namespace {
+
+// Block SpMV pieces of the NSE matrix (TrilinosWrappers::BlockSparseMatrix):
+// each block sums its row in column order; blocks are added afterwards.
+void block_vmult(const Csr& A, int row0, int row1, int col0, int col1, const double* src,
+                 double* dst, bool add) {
+  for (int r = row0; r < row1; ++r) {
+    double s = 0;
+    for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
+      const int c = A.cols[k];
+      if (c >= col0 && c < col1) s += A.vals[k] * src[c - col0];
+    }
+    if (add) dst[r - row0] += s; else dst[r - row0] = s;
+  }
+}
+
+void nse_vmult(const orc_model* m, const double* src, double* dst) {
+  // BlockSparseMatrix::vmult: block(0,0) then vmult_add block(0,1); block(1,0)
+  const int nu = m->n_u, np = m->n_p;
+  block_vmult(m->nse, 0, nu, 0, nu, src, dst, false);
+  block_vmult(m->nse, 0, nu, nu, nu + np, src + nu, dst, true);
+  block_vmult(m->nse, nu, nu + np, 0, nu, src, dst + nu, false);
+}
+
+void schur_vmult(const orc_model* m, const double* src, double* dst) {
+  // SchurComplement::vmult (schur_complement.hpp:143-150) with the A-Jacobi (Q9)
+  const int nu = m->n_u, np = m->n_p;
+  block_vmult(m->nse, 0, nu, nu, nu + np, src, m->tmp1.data(), false);   // block_01
+  for (int i = 0; i < nu; ++i) m->tmp2[i] = m->tmp1[i] * m->A_inv[i];    // Jacobi
+  block_vmult(m->nse, nu, nu + np, 0, nu, m->tmp2.data(), dst, false);   // block_10
+}
+
+double dotv(const double* a, const double* b, int n) {
+  double s = 0;
+  for (int i = 0; i < n; ++i) s += a[i] * b[i];
+  return s;
+}
+
+// Givens rotation of deal.II SolverGMRES::givens_rotation
+void givens_rotation(std::vector<double>& h, std::vector<double>& b, std::vector<double>& ci,
+                     std::vector<double>& si, int col) {
+  for (int i = 0; i < col; i++) {
+    const double s = si[i], c = ci[i], dummy = h[i];
+    h[i] = c * dummy + s * h[i + 1];
+    h[i + 1] = -s * dummy + c * h[i + 1];
+  }
+  const double r = 1. / std::sqrt(h[col] * h[col] + h[col + 1] * h[col + 1]);
+  si[col] = h[col + 1] * r;
+  ci[col] = h[col] * r;
+  h[col] = ci[col] * h[col] + si[col] * h[col + 1];
+  b[col + 1] = -si[col] * b[col];
+  b[col] *= ci[col];
+}
+
+// deal.II SolverGMRES (left preconditioning, use_default_residual, 30 tmp
+// vectors -> restart 28, modified Gram-Schmidt with add_and_dot and the
+// every-5th-step re-orthogonalisation test). Throws NoConvergence.
+template <class OpA, class OpP>
+void gmres(int n, OpA A, OpP P, double* x, const double* b, Control& ctl, int& iters_out,
+           int n_tmp = 30) {
+  std::vector<std::vector<double>> tv(n_tmp, std::vector<double>(n, 0.0));
+  std::vector<double>& v = tv[0];
+  std::vector<double>& p = tv[n_tmp - 1];
+  std::vector<std::vector<double>> H(n_tmp, std::vector<double>(n_tmp - 1, 0.0));
+  std::vector<double> gamma(n_tmp, 0.0), ci(n_tmp - 1, 0.0), si(n_tmp - 1, 0.0), h(n_tmp - 1, 0.0);
+  unsigned accumulated = 0;
+  int dim = 0;
+  State state = kIterate;
+  bool re_orthogonalize = false;
+  do {
+    std::fill(h.begin(), h.end(), 0.0);
+    A(x, p.data());
+    for (int i = 0; i < n; ++i) p[i] = -1. * p[i] + 1. * b[i];
+    P(p.data(), v.data());
+    double rho = std::sqrt(dotv(v.data(), v.data(), n));
+    state = ctl.check(accumulated, rho);
+    if (state != kIterate) break;
+    gamma[0] = rho;
+    for (int i = 0; i < n; ++i) v[i] *= 1. / rho;
+    for (int inner = 0; inner < n_tmp - 2 && state == kIterate; ++inner) {
+      ++accumulated;
+      std::vector<double>& vv = tv[inner + 1];
+      A(tv[inner].data(), p.data());
+      P(p.data(), vv.data());
+      dim = inner + 1;
+      // modified_gram_schmidt
+      double norm_vv_start = 0;
+      const bool consider_reorth = (!re_orthogonalize) && (inner % 5 == 4);
+      if (consider_reorth) norm_vv_start = std::sqrt(dotv(vv.data(), vv.data(), n));
+      h[0] = dotv(vv.data(), tv[0].data(), n);
+      for (int i = 1; i < dim; ++i) {
+        // add_and_dot(-h(i-1), v[i-1], v[i])
+        double s = 0;
+        const double a = -h[i - 1];
+        for (int k = 0; k < n; ++k) {
+          vv[k] += a * tv[i - 1][k];
+          s += vv[k] * tv[i][k];
+        }
+        h[i] = s;
+      }
+      double nn = 0;
+      {
+        const double a = -h[dim - 1];
+        for (int k = 0; k < n; ++k) {
+          vv[k] += a * tv[dim - 1][k];
+          nn += vv[k] * vv[k];
+        }
+      }
+      double norm_vv = std::sqrt(nn);
+      bool do_second = false;
+      if (consider_reorth) {
+        if (norm_vv > 10. * norm_vv_start * std::sqrt(2.220446049250313e-16)) {
+          // keep
+        } else {
+          re_orthogonalize = true;
+          do_second = true;
+        }
+      } else if (re_orthogonalize) {
+        do_second = true;
+      }
+      if (do_second) {
+        // second pass: classical correction, as in deal.II
+        double htmp = dotv(vv.data(), tv[0].data(), n);
+        h[0] += htmp;
+        for (int i = 1; i < dim; ++i) {
+          double s = 0;
+          const double a = -htmp;
+          for (int k = 0; k < n; ++k) {
+            vv[k] += a * tv[i - 1][k];
+            s += vv[k] * tv[i][k];
+          }
+          htmp = s;
+          h[i] += htmp;
+        }
+        nn = 0;
+        const double a = -htmp;
+        for (int k = 0; k < n; ++k) {
+          vv[k] += a * tv[dim - 1][k];
+          nn += vv[k] * vv[k];
+        }
+        norm_vv = std::sqrt(nn);
+      }
+      const double s = norm_vv;
+      h[inner + 1] = s;
+      if (s != 0)
+        for (int k = 0; k < n; ++k) vv[k] *= 1. / s;
+      givens_rotation(h, gamma, ci, si, inner);
+      for (int i = 0; i < dim; ++i) H[i][inner] = h[i];
+      rho = std::fabs(gamma[dim]);
+      state = ctl.check(accumulated, rho);
+    }
+    // H1.backward(h, gamma)
+    std::vector<double> y(dim, 0.0);
+    for (int i = dim - 1; i >= 0; --i) {
+      double s = gamma[i];
+      for (int j = i + 1; j < dim; ++j) s -= y[j] * H[i][j];
+      y[i] = s / H[i][i];
+    }
+    for (int i = 0; i < dim; ++i)
+      for (int k = 0; k < n; ++k) x[k] += y[i] * tv[i][k];
+  } while (state == kIterate);
+  iters_out = int(ctl.last_step);
+  if (state != kSuccess) throw NoConvergence();
+}
+
+// deal.II Householder<double> (initialize + least_squares).
+double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
+                                 std::vector<double>& dst, const std::vector<double>& src) {
+  std::vector<double> diagonal(m, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double sigma = 0;
+    for (int i = j; i < m; ++i) sigma += S[i][j] * S[i][j];
+    if (std::fabs(sigma) < 1.e-15) break;
+    const double s = (S[j][j] < 0) ? std::sqrt(sigma) : -std::sqrt(sigma);
+    const double beta = std::sqrt(1. / (sigma - s * S[j][j]));
+    diagonal[j] = beta * (S[j][j] - s);
+    S[j][j] = s;
+    for (int i = j + 1; i < m; ++i) S[i][j] *= beta;
+    for (int k = j + 1; k < n; ++k) {
+      double sum = diagonal[j] * S[j][k];
+      for (int i = j + 1; i < m; ++i) sum += S[i][j] * S[i][k];
+      S[j][k] -= sum * diagonal[j];
+      for (int i = j + 1; i < m; ++i) S[i][k] -= sum * S[i][j];
+    }
+  }
+  std::vector<double> aux = src;
+  for (int j = 0; j < n; ++j) {
+    double sum = diagonal[j] * aux[j];
+    for (int i = j + 1; i < m; ++i) sum += S[i][j] * aux[i];
+    aux[j] -= sum * diagonal[j];
+    for (int i = j + 1; i < m; ++i) aux[i] -= sum * S[i][j];
+  }
+  double sum = 0;
+  for (int i = n; i < m; ++i) sum += aux[i] * aux[i];
+  dst.assign(n, 0.0);
+  for (int i = n - 1; i >= 0; --i) {
+    double s = aux[i];
+    for (int j = i + 1; j < n; ++j) s -= dst[j] * S[i][j];
+    dst[i] = s / S[i][i];
+  }
+  return std::sqrt(sum);
+}
+
+// BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70)
+void block_prec_vmult(orc_model* m, const double* src, double* dst, bool do_solve_A, int& inner) {
+  const int nu = m->n_u, np = m->n_p;
+  std::vector<double> utmp(src, src + nu);
+  {
+    Control ctl{5000, 1e-6 * norm2(std::vector<double>(src + nu, src + nu + np), 0, np)};
+    int it = 0;
+    gmres(
+        np, [&](const double* x, double* y) { schur_vmult(m, x, y); },
+        [&](const double* x, double* y) { std::copy(x, x + np, y); }, dst + nu, src + nu, ctl, it);
+    inner += it;
+    for (int i = 0; i < np; ++i) dst[nu + i] *= -1.0;
+  }
+  {
+    block_vmult(m->nse, 0, nu, nu, nu + np, dst + nu, utmp.data(), false);
+    for (int i = 0; i < nu; ++i) utmp[i] *= -1.0;
+    for (int i = 0; i < nu; ++i) utmp[i] += src[i];
+  }
+  if (do_solve_A) {
+    // TrilinosWrappers::SolverGMRES (AztecOO) restated as deal.II GMRES with
+    // the A-Jacobi preconditioner, tol 1e-2 ||utmp|| (:59-67).
+    Control ctl{5000, norm2(utmp, 0, nu) * 1e-2};
+    int it = 0;
+    gmres(
+        nu, [&](const double* x, double* y) { block_vmult(m->nse, 0, nu, 0, nu, x, y, false); },
+        [&](const double* x, double* y) { for (int i = 0; i < nu; ++i) y[i] = x[i] * m->A_inv[i]; },
+        dst, utmp.data(), ctl, it);
+  } else {
+    for (int i = 0; i < nu; ++i) dst[i] = utmp[i] * m->A_inv[i];
+  }
+}
+
+// deal.II SolverFGMRES (restated; Householder least squares every step from
+// j = 1, solution update with the first y.size() z vectors; z vectors persist
+// across restarts within one solve and are zero on first use).
+State fgmres(orc_model* m, double* x, const double* b, int basis_size, unsigned max_steps,
+             double tol, bool do_solve_A, int& accumulated_out, int& inner) {
+  const int n = m->n_u + m->n_p;
+  Control ctl{max_steps, tol};
+  std::vector<std::vector<double>> v(basis_size), z(basis_size);
+  std::vector<double> aux(n);
+  unsigned accumulated = 0;
+  State state = kIterate;
+  std::vector<std::vector<double>> H;
+  std::vector<double> y;
+  double res = 0;
+  do {
+    nse_vmult(m, x, aux.data());
+    for (int i = 0; i < n; ++i) aux[i] = -1. * aux[i] + 1. * b[i];
+    const double beta = std::sqrt(dotv(aux.data(), aux.data(), n));
+    res = beta;
+    state = ctl.check(accumulated, res);
+    if (state == kSuccess) break;
+    H.assign(basis_size + 1, std::vector<double>(basis_size, 0.0));
+    double a = beta;
+    y.clear();
+    for (int j = 0; j < basis_size; ++j) {
+      if (v[j].empty()) v[j].assign(n, 0.0);
+      if (z[j].empty()) z[j].assign(n, 0.0);
+      if (a != 0)
+        for (int i = 0; i < n; ++i) v[j][i] = 1. / a * aux[i];
+      else
+        std::fill(v[j].begin(), v[j].end(), 0.0);
+      block_prec_vmult(m, v[j].data(), z[j].data(), do_solve_A, inner);
+      nse_vmult(m, z[j].data(), aux.data());
+      H[0][j] = dotv(aux.data(), v[0].data(), n);
+      for (int i = 1; i <= j; ++i) {
+        double s = 0;
+        const double c = -H[i - 1][j];
+        for (int k = 0; k < n; ++k) {
+          aux[k] += c * v[i - 1][k];
+          s += aux[k] * v[i][k];
+        }
+        H[i][j] = s;
+      }
+      {
+        double s = 0;
+        const double c = -H[j][j];
+        for (int k = 0; k < n; ++k) {
+          aux[k] += c * v[j][k];
+          s += aux[k] * aux[k];
+        }
+        H[j + 1][j] = a = std::sqrt(s);
+      }
+      if (j > 0) {
+        std::vector<std::vector<double>> H1(j + 1, std::vector<double>(j, 0.0));
+        for (int r = 0; r <= j; ++r)
+          for (int c = 0; c < j; ++c) H1[r][c] = H[r][c];
+        std::vector<double> prhs(j + 1, 0.0);
+        prhs[0] = beta;
+        res = householder_least_squares(H1, j + 1, j, y, prhs);
+        state = ctl.check(++accumulated, res);
+        if (state != kIterate) break;
+      }
+    }
+    for (size_t j = 0; j < y.size(); ++j)
+      for (int k = 0; k < n; ++k) x[k] += y[j] * z[j][k];
+  } while (state == kIterate);
+  accumulated_out = int(ctl.last_step);
+  return state;
+}
+
+}  // namespace
+
+extern "C" void orc_nse_vmult(const orc_model* m, const double* src, double* dst) {
+  nse_vmult(m, src, dst);
+}
+extern "C" void orc_schur_vmult(const orc_model* m, const double* src, double* dst) {
+  schur_vmult(m, src, dst);
+}
+extern "C" void orc_block_preconditioner_vmult(orc_model* m, const double* src, double* dst,
+                                               int do_solve_A, int* inner_iterations) {
+  int inner = 0;
+  try {
+    block_prec_vmult(m, src, dst, do_solve_A != 0, inner);
+  } catch (const NoConvergence&) {
+    inner = -1;
+  }
+  if (inner_iterations) *inner_iterations = inner;
+}
+
+extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inner_it,
+                             int max_outer) {
+  // solve_NSE_block_preconditioned (boussinesq_model.tpp:1131-1245)
+  const int nu = m->n_u, np = m->n_p, n = nu + np;
+  const double dt = m->ph.time_step;
+  std::vector<double> x(sol, sol + n);
+  for (int i = nu; i < n; ++i) x[i] *= dt;                         // :1151
+  for (int i = nu; i < n; ++i) if (m->cnse.constrained(i)) x[i] = 0;  // :1153-1161
+  const double tol = 1e-8 * norm2(m->nse_rhs, 0, n);               // :1165
+  for (int i = nu; i < n; ++i) x[i] *= dt;                         // :1177 (Q1)
+  int inner = 0, acc1 = 0, acc2 = 0;
+  int status = 0;
+  try {
+    State s = fgmres(m, x.data(), m->nse_rhs.data(), 30, unsigned(max_outer), tol, false, acc1, inner);
+    if (s != kSuccess) throw NoConvergence();
+  } catch (const NoConvergence&) {
+    // :1203-1232 fallback (Q10): do_solve_A, FGMRES(50), max_it = n
+    try {
+      State s = fgmres(m, x.data(), m->nse_rhs.data(), 50, unsigned(n), tol, true, acc2, inner);
+      if (s != kSuccess) status = 1;
+    } catch (const NoConvergence&) {
+      status = 1;
+    }
+  }
+  m->cnse.distribute(x.data());                                     // :1233
+  for (int i = nu; i < n; ++i) x[i] /= dt;                         // :1239
+  std::copy(x.begin(), x.end(), sol);
+  if (outer_it) *outer_it = acc1 + acc2;
+  if (inner_it) *inner_it = inner;
+  m->inner_iterations = inner;
+  return status;
+}
+
+extern "C" int orc_solve_temperature(orc_model* m, double* T, int* iterations) {
+  // solve_temperature (:1417-1476): SolverCG + Jacobi, tol 1e-12 ||rhs||, max n_T
+  const int n = m->n_T;
+  Control ctl{unsigned(n), 1e-12 * norm2(m->T_rhs, 0, n)};
+  std::vector<double> x(T, T + n), g(n), d(n), h(n);
+  const Csr& A = m->Tmat;
+  auto Av = [&](const std::vector<double>& s, std::vector<double>& o) {
+    for (int r = 0; r < n; ++r) {
+      double acc = 0;
+      for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) acc += A.vals[k] * s[A.cols[k]];
+      o[r] = acc;
+    }
+  };
+  bool all_zero = true;
+  for (double v : x) all_zero &= (v == 0.0);
+  if (!all_zero) {
+    Av(x, g);
+    for (int i = 0; i < n; ++i) g[i] += -1. * m->T_rhs[i];
+  } else {
+    for (int i = 0; i < n; ++i) g[i] = -1. * m->T_rhs[i];
+  }
+  double res = norm2(g, 0, n);
+  State conv = ctl.check(0, res);
+  int it = 0;
+  if (conv == kIterate) {
+    for (int i = 0; i < n; ++i) h[i] = g[i] * m->T_inv[i];
+    for (int i = 0; i < n; ++i) d[i] = -1. * h[i];
+    double gh = dotv(g.data(), h.data(), n);
+    while (conv == kIterate) {
+      it++;
+      Av(d, h);
+      double alpha = dotv(d.data(), h.data(), n);
+      alpha = gh / alpha;
+      for (int i = 0; i < n; ++i) x[i] += alpha * d[i];
+      double gg = 0;
+      for (int i = 0; i < n; ++i) {
+        g[i] += alpha * h[i];
+        gg += g[i] * g[i];
+      }
+      res = std::sqrt(std::fabs(gg));
+      conv = ctl.check(it, res);
+      if (conv != kIterate) break;
+      for (int i = 0; i < n; ++i) h[i] = g[i] * m->T_inv[i];
+      double beta = gh;
+      gh = dotv(g.data(), h.data(), n);
+      beta = gh / beta;
+      for (int i = 0; i < n; ++i) d[i] = beta * d[i] - h[i];
+    }
+  }
+  m->cT.distribute(x.data());
+  std::copy(x.begin(), x.end(), T);
+  if (iterations) *iterations = int(ctl.last_step);
+  return conv == kSuccess ? 0 : 1;
+}
+
+extern "C" double orc_max_velocity(const orc_model* m, const double* sol) {
+  // get_maximal_velocity (:1023-1061) on QIterated<QTrapez>(2) = the Q2 nodes
+  double mx = 0;
+  for (int c = 0; c < m->n_cells; ++c)
+    for (int n = 0; n < 27; ++n) {
+      const int b = m->cell_nse[89 * size_t(c) + (n < 8 ? 4 * n : 32 + 3 * (n - 8))];
+      const double u0 = sol[b], u1 = sol[b + 1], u2 = sol[b + 2];
+      mx = std::max(mx, std::sqrt(u0 * u0 + u1 * u1 + u2 * u2));
+    }
+  return mx;
+}
+
+extern "C" double orc_cfl(const orc_model* m, const double* sol, const double* diam) {
+  // get_cfl_number (:1064-1101)
+  double cfl = 0;
+  for (int c = 0; c < m->n_cells; ++c) {
+    double mx = 1e-10;
+    for (int n = 0; n < 27; ++n) {
+      const int b = m->cell_nse[89 * size_t(c) + (n < 8 ? 4 * n : 32 + 3 * (n - 8))];
+      const double u0 = sol[b], u1 = sol[b + 1], u2 = sol[b + 2];
+      mx = std::max(mx, std::sqrt(u0 * u0 + u1 * u1 + u2 * u2));
+    }
+    cfl = std::max(cfl, mx / diam[c]);
+  }
+  return cfl;
+}

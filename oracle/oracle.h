@@ -1,0 +1,119 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference hot path (konsim83/3D-DyCorePlanet,
+ * include/core/boussinesq_model.tpp, include/linear_algebra) used as
+ * the checker for the HIP implementation. Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it. The product library
+ * (3d-dycoreplanet_amd) never links or calls it.
+ *
+ * Parity status: UNPINNED against deal.II. The reference ships no golden
+ * vectors (its only test prints a string, test/test_dummy.cc:19-41) and its
+ * dependencies (deal.II >= 9.2, Trilinos, p4est) are absent from this image,
+ * so it cannot be built here. This file restates the cited reference code
+ * line by line, and the deal.II/Trilinos algorithms it calls (FEValues
+ * arithmetic, AffineConstraints::distribute_local_to_global, SolverGMRES,
+ * SolverFGMRES, SolverCG, SolverControl, Ifpack point Jacobi) from their
+ * published behaviour; see oracle.cpp for the per-function citations.
+ *
+ * Conventions:
+ *   - NSE local dofs in FESystem(FE_Q(2)^3, FE_Q(1)) order (89);
+ *   - cell geometry = the 27 Q2 mapping nodes in lexicographic order;
+ *   - temperature local dofs in FE_Q(k) hierarchic order (k = 1: vertex order);
+ *   - global NSE vector = [velocity (n_u) | pressure (n_p)].
+ */
+#ifndef DCP_ORACLE_H
+#define DCP_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  double time_step;          /* parameters.time_step */
+  double one_over_reynolds;  /* 1/Re, core_model_data.cc:7-13 */
+  double one_over_peclet;    /* 1/Pe, core_model_data.cc:16-22 */
+  double expansion_coefficient;
+  double temperature_ref;    /* reference_quantities.temperature_ref */
+  double gravity_scale;      /* L / U^2 (boussinesq_model.tpp:640-643) */
+  double gravity_constant;
+  double coriolis_scale;     /* L / U (boussinesq_model.tpp:617-621) */
+  double omega;
+  int cuboid;                /* parameters.cuboid_geometry */
+  int nse_solver_interval;   /* parameters.NSE_solver_interval */
+  int temperature_degree;    /* 1 or 2 */
+} orc_physics;
+
+typedef struct {
+  int n_lines;
+  const int* line_dof;
+  const int* entry_ptr;   /* n_lines + 1 */
+  const int* entry_dof;
+  const double* entry_w;
+  const double* inhomogeneity;
+} orc_constraints;
+
+/* ---- element level (one cell) ------------------------------------------ */
+/* local_assemble_nse_system (boussinesq_model.tpp:550-673). u_local: 89 NSE
+ * coefficients (pressure ignored); T_local: temperature coefficients. */
+void orc_cell_nse_system(const orc_physics* ph, const double* geom27,
+                         const double* u_local, const double* T_local,
+                         double* K /*89x89 row-major*/, double* f /*89*/);
+/* local_assemble_nse_preconditioner (:421-464) */
+void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom27, double* P);
+/* local_assemble_temperature_matrix (:748-800) */
+void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom27, double* M,
+                                 double* K);
+/* local_assemble_temperature_rhs (:873-952). inhom_mask[i] != 0 marks an
+ * inhomogeneously constrained local dof (fills matrix_for_bc column i). */
+void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom27,
+                              const double* T_local, const double* u_local,
+                              const int* inhom_mask, double* rhs, double* matrix_for_bc);
+
+/* ---- global model ------------------------------------------------------- */
+typedef struct orc_model orc_model;
+
+orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs /*89*/,
+                      const int* cell_T_dofs, const double* cell_geom /*27x3*/, int n_u,
+                      int n_p, int n_T, const orc_constraints* nse_c,
+                      const orc_constraints* T_c);
+void orc_destroy(orc_model* m);
+void orc_set_time_step(orc_model* m, double dt);
+
+/* assemble_nse_system (:691-740) into the internal CSR nse_matrix + nse_rhs */
+void orc_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T);
+/* assemble_nse_preconditioner + build_nse_preconditioner (:479-542) */
+void orc_build_nse_preconditioner(orc_model* m);
+/* assemble_temperature_matrix (:821-864) */
+void orc_assemble_temperature_matrix(orc_model* m);
+/* assemble_temperature_rhs (:966-1020): nse_solution = the current NSE state (Q5) */
+void orc_assemble_temperature_rhs(orc_model* m, const double* old_T, const double* nse_solution);
+
+/* Accessors for parity checks. */
+long orc_nse_matrix_nnz(const orc_model* m);
+void orc_nse_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals);
+void orc_nse_rhs(const orc_model* m, double* out);
+void orc_precond_diagonals(const orc_model* m, double* A_diag /*n_u*/, double* Mp_diag /*n_p*/);
+long orc_T_matrix_nnz(const orc_model* m);
+void orc_T_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals);
+void orc_T_rhs(const orc_model* m, double* out);
+
+/* Operators (for apply-level parity). */
+void orc_nse_vmult(const orc_model* m, const double* src, double* dst);
+void orc_schur_vmult(const orc_model* m, const double* src_p, double* dst_p);
+void orc_block_preconditioner_vmult(orc_model* m, const double* src, double* dst,
+                                    int do_solve_A, int* inner_iterations);
+
+/* Solvers. Return 0 on success, 1 on NoConvergence (after the reference fallback). */
+int orc_solve_nse(orc_model* m, double* nse_solution /*inout*/, int* outer_iterations,
+                  int* inner_iterations, int max_outer /* 40 in the reference */);
+int orc_solve_temperature(orc_model* m, double* T_solution /*inout*/, int* iterations);
+
+/* Step control (get_maximal_velocity / get_cfl_number, :1023-1101). */
+double orc_max_velocity(const orc_model* m, const double* nse_solution);
+double orc_cfl(const orc_model* m, const double* nse_solution, const double* cell_diameter);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

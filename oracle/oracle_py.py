@@ -1,0 +1,215 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY. ctypes binding of oracle/build/liboracle.so,
+the CPU restatement of the reference hot path (see oracle.h). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+Parity status vs deal.II: unpinned (see oracle.h)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+
+
+class OrcPhysics(C.Structure):
+    _fields_ = [
+        ("time_step", C.c_double), ("one_over_reynolds", C.c_double),
+        ("one_over_peclet", C.c_double), ("expansion_coefficient", C.c_double),
+        ("temperature_ref", C.c_double), ("gravity_scale", C.c_double),
+        ("gravity_constant", C.c_double), ("coriolis_scale", C.c_double),
+        ("omega", C.c_double), ("cuboid", C.c_int), ("nse_solver_interval", C.c_int),
+        ("temperature_degree", C.c_int),
+    ]
+
+
+class OrcConstraints(C.Structure):
+    _fields_ = [
+        ("n_lines", C.c_int), ("line_dof", C.c_void_p), ("entry_ptr", C.c_void_p),
+        ("entry_dof", C.c_void_p), ("entry_w", C.c_void_p), ("inhomogeneity", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = C.CDLL(LIB_PATH)
+        P, I, D = C.c_void_p, C.c_int, C.c_double
+        L.orc_cell_nse_system.argtypes = [P, P, P, P, P, P]
+        L.orc_cell_nse_preconditioner.argtypes = [P, P, P]
+        L.orc_cell_temperature_matrix.argtypes = [P, P, P, P]
+        L.orc_cell_temperature_rhs.argtypes = [P, P, P, P, P, P, P]
+        L.orc_create.argtypes = [P, I, P, P, P, I, I, I, P, P]
+        L.orc_create.restype = P
+        L.orc_destroy.argtypes = [P]
+        L.orc_set_time_step.argtypes = [P, D]
+        L.orc_assemble_nse_system.argtypes = [P, P, P]
+        L.orc_build_nse_preconditioner.argtypes = [P]
+        L.orc_assemble_temperature_matrix.argtypes = [P]
+        L.orc_assemble_temperature_rhs.argtypes = [P, P, P]
+        L.orc_nse_matrix_nnz.argtypes = [P]
+        L.orc_nse_matrix_nnz.restype = C.c_long
+        L.orc_nse_matrix_csr.argtypes = [P, P, P, P]
+        L.orc_nse_rhs.argtypes = [P, P]
+        L.orc_precond_diagonals.argtypes = [P, P, P]
+        L.orc_T_matrix_nnz.argtypes = [P]
+        L.orc_T_matrix_nnz.restype = C.c_long
+        L.orc_T_matrix_csr.argtypes = [P, P, P, P]
+        L.orc_T_rhs.argtypes = [P, P]
+        L.orc_nse_vmult.argtypes = [P, P, P]
+        L.orc_schur_vmult.argtypes = [P, P, P]
+        L.orc_block_preconditioner_vmult.argtypes = [P, P, P, I, P]
+        L.orc_solve_nse.argtypes = [P, P, P, P, I]
+        L.orc_solve_temperature.argtypes = [P, P, P]
+        L.orc_max_velocity.argtypes = [P, P]
+        L.orc_max_velocity.restype = D
+        L.orc_cfl.argtypes = [P, P, P]
+        L.orc_cfl.restype = D
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def physics(ph) -> OrcPhysics:
+    """Convert a dcp.Physics (same field layout) to OrcPhysics."""
+    o = OrcPhysics()
+    for name, _ in OrcPhysics._fields_:
+        setattr(o, name, getattr(ph, name))
+    return o
+
+
+def cell_nse_system(ph, geom27, u_local, T_local):
+    K = np.zeros((89, 89))
+    f = np.zeros(89)
+    o = physics(ph)
+    lib().orc_cell_nse_system(C.byref(o), _p(np.ascontiguousarray(geom27, np.float64)),
+                              _p(np.ascontiguousarray(u_local, np.float64)),
+                              _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
+    return K, f
+
+
+def cell_nse_preconditioner(ph, geom27):
+    P = np.zeros((89, 89))
+    o = physics(ph)
+    lib().orc_cell_nse_preconditioner(C.byref(o), _p(np.ascontiguousarray(geom27, np.float64)), _p(P))
+    return P
+
+
+class Model:
+    """Global oracle model over a dcp.HostMesh."""
+
+    def __init__(self, ph, mesh):
+        self.ph = physics(ph)
+        self.mesh = mesh
+        self._keep = []
+
+        def cons(cs):
+            s = OrcConstraints(len(cs.line_dof), _p(cs.line_dof).value, _p(cs.entry_ptr).value,
+                               _p(cs.entry_dof).value, _p(cs.entry_w).value,
+                               _p(cs.inhomogeneity).value)
+            self._keep.append(cs)
+            return s
+
+        self._nc, self._tc = cons(mesh.nse_constraints), cons(mesh.T_constraints)
+        self._cd = np.ascontiguousarray(mesh.cell_nse_dofs, np.int32)
+        self._td = np.ascontiguousarray(mesh.cell_T_dofs, np.int32)
+        self._g = np.ascontiguousarray(mesh.cell_geometry, np.float64)
+        self.h = lib().orc_create(C.byref(self.ph), mesh.n_cells, _p(self._cd), _p(self._td),
+                                  _p(self._g), mesh.n_u, mesh.n_p, mesh.n_T,
+                                  C.byref(self._nc), C.byref(self._tc))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def set_time_step(self, dt):
+        self.ph.time_step = dt
+        lib().orc_set_time_step(self.h, dt)
+
+    def assemble_nse_system(self, old_nse, old_T):
+        lib().orc_assemble_nse_system(self.h, _p(np.ascontiguousarray(old_nse, np.float64)),
+                                      _p(np.ascontiguousarray(old_T, np.float64)))
+
+    def build_nse_preconditioner(self):
+        lib().orc_build_nse_preconditioner(self.h)
+
+    def assemble_temperature_matrix(self):
+        lib().orc_assemble_temperature_matrix(self.h)
+
+    def assemble_temperature_rhs(self, old_T, nse_solution):
+        lib().orc_assemble_temperature_rhs(self.h, _p(np.ascontiguousarray(old_T, np.float64)),
+                                           _p(np.ascontiguousarray(nse_solution, np.float64)))
+
+    def nse_matrix_csr(self):
+        nnz = lib().orc_nse_matrix_nnz(self.h)
+        n = self.mesh.n_u + self.mesh.n_p
+        rp, cols, vals = np.zeros(n + 1, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
+        lib().orc_nse_matrix_csr(self.h, _p(rp), _p(cols), _p(vals))
+        return rp, cols, vals
+
+    def nse_rhs(self):
+        out = np.zeros(self.mesh.n_u + self.mesh.n_p)
+        lib().orc_nse_rhs(self.h, _p(out))
+        return out
+
+    def precond_diagonals(self):
+        a, p = np.zeros(self.mesh.n_u), np.zeros(self.mesh.n_p)
+        lib().orc_precond_diagonals(self.h, _p(a), _p(p))
+        return a, p
+
+    def T_matrix_csr(self):
+        nnz = lib().orc_T_matrix_nnz(self.h)
+        rp, cols, vals = np.zeros(self.mesh.n_T + 1, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
+        lib().orc_T_matrix_csr(self.h, _p(rp), _p(cols), _p(vals))
+        return rp, cols, vals
+
+    def T_rhs(self):
+        out = np.zeros(self.mesh.n_T)
+        lib().orc_T_rhs(self.h, _p(out))
+        return out
+
+    def nse_vmult(self, src):
+        dst = np.zeros(self.mesh.n_u + self.mesh.n_p)
+        lib().orc_nse_vmult(self.h, _p(np.ascontiguousarray(src, np.float64)), _p(dst))
+        return dst
+
+    def schur_vmult(self, src):
+        dst = np.zeros(self.mesh.n_p)
+        lib().orc_schur_vmult(self.h, _p(np.ascontiguousarray(src, np.float64)), _p(dst))
+        return dst
+
+    def block_preconditioner_vmult(self, src, do_solve_A=False):
+        dst = np.zeros(self.mesh.n_u + self.mesh.n_p)
+        it = C.c_int(0)
+        lib().orc_block_preconditioner_vmult(self.h, _p(np.ascontiguousarray(src, np.float64)),
+                                             _p(dst), int(do_solve_A), C.byref(it))
+        return dst, it.value
+
+    def solve_nse(self, nse_solution, max_outer=40):
+        x = np.array(nse_solution, dtype=np.float64, copy=True)
+        o, i = C.c_int(0), C.c_int(0)
+        rc = lib().orc_solve_nse(self.h, _p(x), C.byref(o), C.byref(i), int(max_outer))
+        return rc, x, o.value, i.value
+
+    def solve_temperature(self, T):
+        x = np.array(T, dtype=np.float64, copy=True)
+        it = C.c_int(0)
+        rc = lib().orc_solve_temperature(self.h, _p(x), C.byref(it))
+        return rc, x, it.value
+
+    def max_velocity(self, sol):
+        return lib().orc_max_velocity(self.h, _p(np.ascontiguousarray(sol, np.float64)))
+
+    def cfl(self, sol):
+        return lib().orc_cfl(self.h, _p(np.ascontiguousarray(sol, np.float64)),
+                             _p(np.ascontiguousarray(self.mesh.cell_diameter, np.float64)))

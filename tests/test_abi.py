@@ -1,0 +1,42 @@
+"""C-ABI boundary checks that run without a GPU: libdcp.so loads, exports every
+symbol include/dcp.h declares, and refuses to compute without a device (there
+is no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import dcp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "dcp.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dcp_[A-Za-z_0-9]+)\s*\(", text)))
+
+
+def test_header_matches_binding_list():
+    assert declared_symbols() == sorted(dcp.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(dcp.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_no_cpu_fallback():
+    if dcp.lib().dcp_device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(dcp.DcpError) as e:
+        dcp.Context()
+    assert e.value.code == dcp.DCP_ERR_DEVICE
+
+
+def test_host_mesh_helpers_without_gpu():
+    m = dcp.HostMesh(refine=1)
+    assert m.cell_geometry.shape == (48, 27, 3)
+    assert m.cell_nse_dofs.shape == (48, 89)
