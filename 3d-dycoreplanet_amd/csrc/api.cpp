@@ -143,6 +143,171 @@ void need_ready(Ctx& c) {
   require(c.have_mesh, DCP_ERR_STATE, "dcp_mesh_upload has not been called");
 }
 
+struct HostPrep {
+  int nv = 0;
+  std::vector<int32_t> q2, pd, td;
+  std::vector<double> xyz;
+  std::vector<NodeConstraint> vc;
+  std::vector<uint8_t> Tfix;
+  std::vector<double> Tbc;
+  std::vector<int> color_ptr;
+  std::vector<int32_t> ccells;
+  std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc;
+};
+
+// Host half of dcp_mesh_upload: validation, node map, node-local constraints,
+// colouring and block patterns (no device access, so it is testable on CPU).
+void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
+                  const int32_t* cell_T_dofs, const double* cell_geometry,
+                  const double* cell_diameter, int n_u, int n_p, int n_T,
+                  const dcp_constraints* nse_c, const dcp_constraints* T_c) {
+  require(cell_nse_dofs && cell_T_dofs && cell_geometry && cell_diameter, DCP_ERR_INVALID,
+          "NULL argument");
+  require(n_cells > 0 && n_u > 0 && n_u % 3 == 0 && n_p > 0 && n_T > 0, DCP_ERR_INVALID,
+          "invalid sizes");
+  const int nv = n_u / 3;
+  h.nv = nv;
+  auto& q2 = h.q2;
+  auto& pd = h.pd;
+  auto& td = h.td;
+  auto& xyz = h.xyz;
+  q2.assign(size_t(n_cells) * 27, 0);
+  pd.assign(size_t(n_cells) * 8, 0);
+  td.assign(size_t(n_cells) * 8, 0);
+  xyz.assign(size_t(nv) * 3, 0.0);
+  std::vector<char> seen(nv, 0);
+  for (int cell = 0; cell < n_cells; ++cell) {
+    const int32_t* d = cell_nse_dofs + size_t(cell) * kNseDofs;
+    for (int i = 0; i < kNseDofs; ++i) {
+      const SysDof s = system_dof(i);
+      if (s.comp < 3) {
+        require(d[i] >= 0 && d[i] < n_u && d[i] % 3 == s.comp, DCP_ERR_UNSUPPORTED,
+                "velocity dofs must be node-interleaved (3*node + component), as after "
+                "DoFRenumbering::component_wise({0,0,0,1})");
+        const int node = d[i] / 3;
+        if (s.comp == 0) {
+          q2[size_t(cell) * 27 + s.lex] = node;
+          if (!seen[node]) {
+            seen[node] = 1;
+            for (int k = 0; k < 3; ++k)
+              xyz[3 * size_t(node) + k] = cell_geometry[(size_t(cell) * 27 + s.lex) * 3 + k];
+          }
+        } else {
+          require(q2[size_t(cell) * 27 + s.lex] == node, DCP_ERR_UNSUPPORTED,
+                  "velocity components of one support point must share a node");
+        }
+      } else {
+        require(d[i] >= n_u && d[i] < n_u + n_p, DCP_ERR_INVALID, "pressure dof out of range");
+        pd[size_t(cell) * 8 + s.lex] = d[i] - n_u;
+      }
+    }
+    for (int v = 0; v < 8; ++v) {
+      const int t = cell_T_dofs[size_t(cell) * 8 + v];
+      require(t >= 0 && t < n_T, DCP_ERR_INVALID, "temperature dof out of range");
+      td[size_t(cell) * 8 + v] = t;
+    }
+  }
+  for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
+  // ---- constraints -> node-local form. A line without entries is a fixed
+  // component; three of them on one node form a no-slip node; a single one is
+  // a no-normal-flux line whose weights all vanished (normal along an axis).
+  auto& vc = h.vc;
+  vc.assign(nv, NodeConstraint{{0, 0, 0}, 0, -1});
+  std::vector<int> n_lines(nv, 0), fixed(nv, 0), fixed_comp(nv, -1);
+  if (nse_c) {
+    for (int l = 0; l < nse_c->n_lines; ++l) {
+      const int dof = nse_c->line_dof[l];
+      require(dof >= 0 && dof < n_u, DCP_ERR_UNSUPPORTED, "pressure constraints are not supported");
+      require(nse_c->inhomogeneity[l] == 0.0, DCP_ERR_UNSUPPORTED,
+              "inhomogeneous velocity constraints are not supported");
+      const int node = dof / 3, comp = dof % 3;
+      n_lines[node]++;
+      const int b = nse_c->entry_ptr[l], e = nse_c->entry_ptr[l + 1];
+      if (b == e) {
+        fixed[node]++;
+        fixed_comp[node] = comp;
+        continue;
+      }
+      vc[node].type = 2;
+      vc[node].k = comp;
+      for (int k = b; k < e; ++k) {
+        const int t = nse_c->entry_dof[k];
+        require(t / 3 == node && t % 3 != comp, DCP_ERR_UNSUPPORTED,
+                "constraint couples dofs of different support points (periodic / hanging "
+                "nodes are not supported by the device path)");
+        vc[node].w[t % 3] = nse_c->entry_w[k];
+      }
+    }
+    for (int k = 0; k < nv; ++k) {
+      if (n_lines[k] == 0) continue;
+      if (n_lines[k] == 3 && fixed[k] == 3) {
+        vc[k].type = 1;
+      } else if (n_lines[k] == 1 && fixed[k] == 1) {
+        vc[k] = NodeConstraint{{0, 0, 0}, 2, fixed_comp[k]};
+      } else if (n_lines[k] == 1) {
+        // no-normal-flux line with entries, set above
+      } else {
+        fail(DCP_ERR_UNSUPPORTED, "velocity constraints of node " + std::to_string(k) +
+                                      " are neither no-slip nor a single no-normal-flux line");
+      }
+    }
+  }
+  h.Tfix.assign(n_T, 0);
+  h.Tbc.assign(n_T, 0.0);
+  if (T_c)
+    for (int l = 0; l < T_c->n_lines; ++l) {
+      const int dof = T_c->line_dof[l];
+      require(dof >= 0 && dof < n_T, DCP_ERR_INVALID, "temperature constraint out of range");
+      require(T_c->entry_ptr[l] == T_c->entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
+              "temperature constraints must be Dirichlet lines");
+      h.Tfix[dof] = 1;
+      h.Tbc[dof] = T_c->inhomogeneity[l];
+    }
+  // ---- colouring (greedy over vertex-sharing cells; tree order)
+  std::vector<int32_t> vptr, vcells;
+  {
+    std::vector<int32_t> cnt(size_t(n_p) + 1, 0);
+    for (size_t i = 0; i < pd.size(); ++i) cnt[pd[i] + 1]++;
+    for (int v = 0; v < n_p; ++v) cnt[v + 1] += cnt[v];
+    vcells.resize(pd.size());
+    std::vector<int32_t> f(cnt.begin(), cnt.end() - 1);
+    for (int cell = 0; cell < n_cells; ++cell)
+      for (int v = 0; v < 8; ++v) vcells[f[pd[size_t(cell) * 8 + v]]++] = cell;
+    vptr.swap(cnt);
+  }
+  std::vector<int> color(n_cells, -1);
+  int n_colors = 0;
+  for (int cell = 0; cell < n_cells; ++cell) {
+    uint64_t used = 0;
+    for (int v = 0; v < 8; ++v) {
+      const int p = pd[size_t(cell) * 8 + v];
+      for (int k = vptr[p]; k < vptr[p + 1]; ++k) {
+        const int o = vcells[k];
+        if (color[o] >= 0) used |= (uint64_t(1) << color[o]);
+      }
+    }
+    int col = 0;
+    while (col < 64 && (used >> col) & 1) ++col;
+    require(col < 64, DCP_ERR_UNSUPPORTED, "cell colouring needs more than 64 colours");
+    color[cell] = col;
+    n_colors = std::max(n_colors, col + 1);
+  }
+  h.color_ptr.assign(n_colors + 1, 0);
+  for (int cell = 0; cell < n_cells; ++cell) h.color_ptr[color[cell] + 1]++;
+  for (int k = 0; k < n_colors; ++k) h.color_ptr[k + 1] += h.color_ptr[k];
+  h.ccells.assign(n_cells, 0);
+  auto& ccells = h.ccells;
+  {
+    std::vector<int> f(h.color_ptr.begin(), h.color_ptr.end() - 1);
+    for (int cell = 0; cell < n_cells; ++cell) ccells[f[color[cell]]++] = cell;
+  }
+  // ---- patterns
+  union_pattern(nv, n_cells, q2.data(), 27, q2.data(), 27, h.Ap, h.Ac);
+  union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, h.Btp, h.Btc);
+  union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, h.Bp, h.Bc);
+  union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, h.Tp, h.Tc);
+}
+
 }  // namespace
 
 extern "C" {
@@ -207,145 +372,40 @@ int dcp_set_time_step(dcp_ctx* ctx, double dt) {
   });
 }
 
+int dcp_mesh_check(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                   const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
+                   int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c,
+                   int* n_colors) {
+  return guarded(nullptr, [&] {
+    HostPrep h;
+    prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
+                 n_T, nse_c, T_c);
+    if (n_colors) *n_colors = int(h.color_ptr.size()) - 1;
+    return DCP_OK;
+  });
+}
+
 int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
                     const int32_t* cell_T_dofs, const double* cell_geometry,
                     const double* cell_diameter, int n_u, int n_p, int n_T,
                     const dcp_constraints* nse_c, const dcp_constraints* T_c) {
   return guarded(ctx, [&] {
-    require(ctx && cell_nse_dofs && cell_T_dofs && cell_geometry && cell_diameter, DCP_ERR_INVALID,
-            "NULL argument");
-    require(n_cells > 0 && n_u > 0 && n_u % 3 == 0 && n_p > 0 && n_T > 0, DCP_ERR_INVALID,
-            "invalid sizes");
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
     Ctx& c = *ctx;
+    HostPrep h;
+    prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
+                 n_T, nse_c, T_c);
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
-    const int nv = n_u / 3;
-    // ---- FESystem cell dofs -> node map (velocity dofs must be 3*node + comp)
-    std::vector<int32_t> q2(size_t(n_cells) * 27), pd(size_t(n_cells) * 8), td(size_t(n_cells) * 8);
-    std::vector<double> xyz(size_t(nv) * 3, 0.0);
-    std::vector<char> seen(nv, 0);
-    for (int cell = 0; cell < n_cells; ++cell) {
-      const int32_t* d = cell_nse_dofs + size_t(cell) * kNseDofs;
-      for (int i = 0; i < kNseDofs; ++i) {
-        const SysDof s = system_dof(i);
-        if (s.comp < 3) {
-          require(d[i] >= 0 && d[i] < n_u && d[i] % 3 == s.comp, DCP_ERR_UNSUPPORTED,
-                  "velocity dofs must be node-interleaved (3*node + component), as after "
-                  "DoFRenumbering::component_wise({0,0,0,1})");
-          const int node = d[i] / 3;
-          if (s.comp == 0) {
-            q2[size_t(cell) * 27 + s.lex] = node;
-            if (!seen[node]) {
-              seen[node] = 1;
-              for (int k = 0; k < 3; ++k)
-                xyz[3 * size_t(node) + k] = cell_geometry[(size_t(cell) * 27 + s.lex) * 3 + k];
-            }
-          } else {
-            require(q2[size_t(cell) * 27 + s.lex] == node, DCP_ERR_UNSUPPORTED,
-                    "velocity components of one support point must share a node");
-          }
-        } else {
-          require(d[i] >= n_u && d[i] < n_u + n_p, DCP_ERR_INVALID, "pressure dof out of range");
-          pd[size_t(cell) * 8 + s.lex] = d[i] - n_u;
-        }
-      }
-      for (int v = 0; v < 8; ++v) {
-        const int t = cell_T_dofs[size_t(cell) * 8 + v];
-        require(t >= 0 && t < n_T, DCP_ERR_INVALID, "temperature dof out of range");
-        td[size_t(cell) * 8 + v] = t;
-      }
-    }
-    for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
-    // ---- constraints -> node-local form
-    std::vector<NodeConstraint> vc(nv, NodeConstraint{{0, 0, 0}, 0, -1});
-    std::vector<int> fixed_count(nv, 0);
-    if (nse_c) {
-      for (int l = 0; l < nse_c->n_lines; ++l) {
-        const int dof = nse_c->line_dof[l];
-        require(dof >= 0 && dof < n_u, DCP_ERR_UNSUPPORTED, "pressure constraints are not supported");
-        require(nse_c->inhomogeneity[l] == 0.0, DCP_ERR_UNSUPPORTED,
-                "inhomogeneous velocity constraints are not supported");
-        const int node = dof / 3, comp = dof % 3;
-        const int b = nse_c->entry_ptr[l], e = nse_c->entry_ptr[l + 1];
-        if (b == e) {
-          fixed_count[node]++;
-          continue;
-        }
-        require(vc[node].type == 0, DCP_ERR_UNSUPPORTED, "two constraint lines on one node");
-        vc[node].type = 2;
-        vc[node].k = comp;
-        for (int k = b; k < e; ++k) {
-          const int t = nse_c->entry_dof[k];
-          require(t / 3 == node && t % 3 != comp, DCP_ERR_UNSUPPORTED,
-                  "constraint couples dofs of different support points (periodic / hanging "
-                  "nodes are not supported by the device path)");
-          vc[node].w[t % 3] = nse_c->entry_w[k];
-        }
-      }
-      for (int k = 0; k < nv; ++k) {
-        if (fixed_count[k] == 0) continue;
-        if (fixed_count[k] == 3 && vc[k].type == 0) {
-          vc[k].type = 1;
-        } else if (fixed_count[k] == 1 && vc[k].type == 0) {
-          fail(DCP_ERR_UNSUPPORTED, "single fixed velocity component (not a no-slip node)");
-        } else {
-          fail(DCP_ERR_UNSUPPORTED, "mixed velocity constraints on one node");
-        }
-      }
-    }
-    std::vector<uint8_t> Tfix(n_T, 0);
-    std::vector<double> Tbc(n_T, 0.0);
-    if (T_c)
-      for (int l = 0; l < T_c->n_lines; ++l) {
-        const int dof = T_c->line_dof[l];
-        require(dof >= 0 && dof < n_T, DCP_ERR_INVALID, "temperature constraint out of range");
-        require(T_c->entry_ptr[l] == T_c->entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
-                "temperature constraints must be Dirichlet lines");
-        Tfix[dof] = 1;
-        Tbc[dof] = T_c->inhomogeneity[l];
-      }
-    // ---- colouring (greedy over vertex-sharing cells; tree order)
-    std::vector<int32_t> vptr, vcells;
-    {
-      std::vector<int32_t> cnt(size_t(n_p) + 1, 0);
-      for (size_t i = 0; i < pd.size(); ++i) cnt[pd[i] + 1]++;
-      for (int v = 0; v < n_p; ++v) cnt[v + 1] += cnt[v];
-      vcells.resize(pd.size());
-      std::vector<int32_t> f(cnt.begin(), cnt.end() - 1);
-      for (int cell = 0; cell < n_cells; ++cell)
-        for (int v = 0; v < 8; ++v) vcells[f[pd[size_t(cell) * 8 + v]]++] = cell;
-      vptr.swap(cnt);
-    }
-    std::vector<int> color(n_cells, -1);
-    int n_colors = 0;
-    for (int cell = 0; cell < n_cells; ++cell) {
-      uint64_t used = 0;
-      for (int v = 0; v < 8; ++v) {
-        const int p = pd[size_t(cell) * 8 + v];
-        for (int k = vptr[p]; k < vptr[p + 1]; ++k) {
-          const int o = vcells[k];
-          if (color[o] >= 0) used |= (uint64_t(1) << color[o]);
-        }
-      }
-      int col = 0;
-      while (col < 64 && (used >> col) & 1) ++col;
-      require(col < 64, DCP_ERR_UNSUPPORTED, "cell colouring needs more than 64 colours");
-      color[cell] = col;
-      n_colors = std::max(n_colors, col + 1);
-    }
-    c.color_ptr.assign(n_colors + 1, 0);
-    for (int cell = 0; cell < n_cells; ++cell) c.color_ptr[color[cell] + 1]++;
-    for (int k = 0; k < n_colors; ++k) c.color_ptr[k + 1] += c.color_ptr[k];
-    std::vector<int32_t> ccells(n_cells);
-    {
-      std::vector<int> f(c.color_ptr.begin(), c.color_ptr.end() - 1);
-      for (int cell = 0; cell < n_cells; ++cell) ccells[f[color[cell]]++] = cell;
-    }
-    // ---- patterns
-    std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc;
-    union_pattern(nv, n_cells, q2.data(), 27, q2.data(), 27, Ap, Ac);
-    union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, Btp, Btc);
-    union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, Bp, Bc);
-    union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, Tp, Tc);
+    const int nv = h.nv;
+    c.color_ptr = h.color_ptr;
+    const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
+    const auto& xyz = h.xyz;
+    const auto& vc = h.vc;
+    const auto &Ap = h.Ap, &Ac = h.Ac, &Btp = h.Btp, &Btc = h.Btc, &Bp = h.Bp, &Bc = h.Bc,
+               &Tp = h.Tp, &Tc = h.Tc;
+    const auto& ccells = h.ccells;
+    const auto& Tfix = h.Tfix;
+    const auto& Tbc = h.Tbc;
     // ---- upload
     c.n_cells = n_cells;
     c.n_u = n_u;

@@ -29,7 +29,7 @@ ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "dcp_ctx_create", "dcp_ctx_destroy", "dcp_last_error", "dcp_device_count",
-    "dcp_set_physics", "dcp_set_time_step", "dcp_mesh_upload", "dcp_state_set",
+    "dcp_set_physics", "dcp_set_time_step", "dcp_mesh_upload", "dcp_mesh_check", "dcp_state_set",
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
     "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
@@ -116,6 +116,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_set_time_step.argtypes = [P, C.c_double]
     lib.dcp_mesh_upload.argtypes = [P, I, P, P, P, P, I, I, I, C.POINTER(Constraints),
                                     C.POINTER(Constraints)]
+    lib.dcp_mesh_check.argtypes = [I, P, P, P, P, I, I, I, C.POINTER(Constraints),
+                                   C.POINTER(Constraints), C.POINTER(I)]
     lib.dcp_state_set.argtypes = [P, I, P, C.c_size_t]
     lib.dcp_state_get.argtypes = [P, I, P, C.c_size_t]
     lib.dcp_state_copy.argtypes = [P, I, I]
@@ -226,6 +228,19 @@ class HostMesh:
             lib().dcp_host_mesh_destroy(h)
         self.cuboid = bool(cuboid)
         self.refine = refine
+
+    def check(self, nse_constraints=None, T_constraints=None):
+        """Host-only validation of the device upload; returns the number of
+        cell colours or raises DcpError (e.g. periodic constraints)."""
+        nc = (nse_constraints or self.nse_constraints).as_struct()
+        tc = (T_constraints or self.T_constraints).as_struct()
+        ncol = C.c_int(0)
+        rc = lib().dcp_mesh_check(self.n_cells, _ptr(self.cell_nse_dofs), _ptr(self.cell_T_dofs),
+                                  _ptr(self.cell_geometry), _ptr(self.cell_diameter), self.n_u,
+                                  self.n_p, self.n_T, C.byref(nc), C.byref(tc), C.byref(ncol))
+        if rc != DCP_OK:
+            raise DcpError(rc, lib().dcp_last_error(None).decode())
+        return ncol.value
         self.temperature_degree = temperature_degree
 
 

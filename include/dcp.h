@@ -96,6 +96,13 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs /*[n
                     const dcp_constraints* nse_constraints,
                     const dcp_constraints* T_constraints);
 
+/* Host-only dry run of dcp_mesh_upload's validation / conversion (node map,
+ * node-local constraints, colouring, patterns); no device needed. */
+int dcp_mesh_check(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                   const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
+                   int n_T, const dcp_constraints* nse_constraints,
+                   const dcp_constraints* T_constraints, int* n_colors);
+
 /* Device-resident state vectors ----------------------------------------- */
 enum {
   DCP_NSE_SOLUTION = 0,      /* nse_solution (n_u + n_p) */

@@ -40,3 +40,25 @@ def test_host_mesh_helpers_without_gpu():
     m = dcp.HostMesh(refine=1)
     assert m.cell_geometry.shape == (48, 27, 3)
     assert m.cell_nse_dofs.shape == (48, 89)
+
+
+@pytest.mark.parametrize("r", [0, 1, 2, 3])
+def test_upload_conversion_shell(r):
+    m = dcp.HostMesh(refine=r)
+    ncol = m.check()
+    assert (8 if r > 0 else 2) <= ncol <= 27
+
+
+def test_upload_rejects_periodic_cube():
+    m = dcp.HostMesh(cuboid=True, refine=1)
+    with pytest.raises(dcp.DcpError) as e:
+        m.check()
+    assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
+
+
+def test_upload_rejects_bad_dof_layout():
+    m = dcp.HostMesh(refine=1)
+    m.cell_nse_dofs = m.cell_nse_dofs.copy()
+    m.cell_nse_dofs[0, 0], m.cell_nse_dofs[0, 1] = m.cell_nse_dofs[0, 1], m.cell_nse_dofs[0, 0]
+    with pytest.raises(dcp.DcpError):
+        m.check()
