@@ -25,7 +25,7 @@ Ctx::~Ctx() {
   free_workspaces(*this);
   if (hpinned) (void)hipHostFree(hpinned);
   ev_total.destroy();
-  ev_schur.destroy();
+  for (auto& t : schur_ev) t.destroy();
   if (stream) (void)hipStreamDestroy(stream);
 }
 }  // namespace dcp
@@ -337,7 +337,8 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
     DCP_HIP_CHECK(hipSetDevice(c->cfg.device));
     DCP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->ev_total.init();
-    c->ev_schur.init();
+    c->schur_ev.resize(Ctx::kSchurEvents);
+    for (auto& t : c->schur_ev) t.init();
     ensure_workspaces(*c);
     *out = c.release();
     return DCP_OK;
@@ -601,12 +602,19 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
             "assemble_nse_system and build_nse_preconditioner must run first");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     c.time_schur = true;
-    c.schur_ms_total = 0;
-    c.schur_count = 0;
+    c.schur_ev_used = 0;
+    c.schur_calls = 0;
     const int rc = solve_nse(c, outer, inner);
     c.time_schur = false;
-    c.timings.schur_apply_ms_avg = c.schur_count ? c.schur_ms_total / c.schur_count : 0.0;
-    c.timings.schur_applies = c.schur_count;
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    double sum = 0;
+    for (int k = 0; k < c.schur_ev_used; ++k) {
+      float ms = 0;
+      DCP_HIP_CHECK(hipEventElapsedTime(&ms, c.schur_ev[k].a, c.schur_ev[k].b));
+      sum += ms;
+    }
+    c.timings.schur_apply_ms_avg = c.schur_ev_used ? sum / c.schur_ev_used : 0.0;
+    c.timings.schur_applies = c.schur_calls;
     t.stop();
     return rc;
   });
@@ -793,6 +801,17 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
   });
 }
 
+int dcp_pattern_info(dcp_ctx* ctx, int64_t* nA, int64_t* nBt, int64_t* nB, int64_t* nT) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    if (nA) *nA = int64_t(ctx->A_col.n);
+    if (nBt) *nBt = int64_t(ctx->Bt_col.n);
+    if (nB) *nB = int64_t(ctx->B_col.n);
+    if (nT) *nT = int64_t(ctx->T_col.n);
+    return DCP_OK;
+  });
+}
+
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out) {
   if (!ctx || !out) return DCP_ERR_INVALID;
   *out = ctx->timings;
@@ -811,11 +830,11 @@ struct dcp_host_mesh {
 };
 
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
-                                    int temperature_degree) {
+                                    int temperature_degree, int normal_mode) {
   try {
     auto h = std::make_unique<dcp_host_mesh>();
     h->mesh = cuboid ? build_cube(refine, length) : build_shell(refine, R0 / length, R1 / length);
-    h->nse = nse_constraints(h->mesh);
+    h->nse = nse_constraints(h->mesh, normal_mode == 1 ? NormalMode::Radial : NormalMode::Consistent);
     h->T = temperature_constraints(h->mesh, temperature_degree);
     h->tdofs = temperature_dofs(h->mesh, temperature_degree);
     h->cell_nse = nse_cell_dofs_dealii(h->mesh);

@@ -85,9 +85,12 @@ struct Ctx {
   DBuf<double> coef;                 // multi_axpy coefficients
   DBuf<const double*> ptrs;          // multi_axpy pointer table
   dcp_timings timings{};
-  Timer ev_total, ev_schur;
-  double schur_ms_total = 0;
-  long schur_count = 0;
+  Timer ev_total;
+  // sampled, deferred timing of Schur-complement applies (no host sync in the loop)
+  static constexpr int kSchurEvents = 256, kSchurSampleEvery = 8;
+  std::vector<Timer> schur_ev;
+  int schur_ev_used = 0;
+  long schur_calls = 0;
   bool time_schur = false;
 
   CellData cd() const {

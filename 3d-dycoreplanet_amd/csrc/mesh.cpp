@@ -318,9 +318,54 @@ void add_periodic(const Mesh& m, Builder& b, DofFn dof_of, int n_comp) {
   }
 }
 
+double lag2(int a, double x) {
+  return a == 0 ? 2 * (x - 0.5) * (x - 1) : a == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+}
+double dlag2(int a, double x) { return a == 0 ? 4 * x - 3 : a == 1 ? -8 * x + 4 : 4 * x - 1; }
+
 }  // namespace
 
-Constraints nse_constraints(const Mesh& m) {
+std::vector<double> consistent_normals(const Mesh& m, uint8_t boundary_bit) {
+  // n_i = sum_cells int grad(phi_i) dx with the Q2 mapping and QGauss(3), i.e.
+  // minus the row of B^T 1 of node i. Interior rows vanish to roundoff, so
+  // constraining u_i . n_i = 0 on the boundary makes C^T B^T 1 = 0 exactly
+  // (consistent normals, Engelman, Sani & Gresho 1982).
+  std::vector<double> nrm(size_t(m.n_vnodes) * 3, 0.0);
+  for (int c = 0; c < m.n_cells; ++c) {
+    bool touches = false;
+    for (int l = 0; l < 27; ++l) touches |= (m.vnode_bnd[m.cell_q2[27 * size_t(c) + l]] & boundary_bit) != 0;
+    if (!touches) continue;
+    for (int q = 0; q < 27; ++q) {
+      const double p[3] = {kGaussX[q % 3], kGaussX[(q / 3) % 3], kGaussX[q / 9]};
+      const double w = kGaussW[q % 3] * kGaussW[(q / 3) % 3] * kGaussW[q / 9];
+      double gref[27][3], J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+      for (int n = 0; n < 27; ++n) {
+        const int a = n % 3, b = (n / 3) % 3, cc = n / 9;
+        gref[n][0] = dlag2(a, p[0]) * lag2(b, p[1]) * lag2(cc, p[2]);
+        gref[n][1] = lag2(a, p[0]) * dlag2(b, p[1]) * lag2(cc, p[2]);
+        gref[n][2] = lag2(a, p[0]) * lag2(b, p[1]) * dlag2(cc, p[2]);
+        const double* X = &m.xyz[3 * size_t(m.cell_q2[27 * size_t(c) + n])];
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) J[i][j] += X[i] * gref[n][j];
+      }
+      // cofactor matrix: det(J) J^-T = cof(J); grad phi JxW = cof(J) gref w
+      double cof[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+          cof[i][j] = J[i1][j1] * J[i2][j2] - J[i1][j2] * J[i2][j1];
+        }
+      for (int n = 0; n < 27; ++n) {
+        double* out = &nrm[3 * size_t(m.cell_q2[27 * size_t(c) + n])];
+        for (int i = 0; i < 3; ++i)
+          out[i] += (cof[i][0] * gref[n][0] + cof[i][1] * gref[n][1] + cof[i][2] * gref[n][2]) * w;
+      }
+    }
+  }
+  return nrm;
+}
+
+Constraints nse_constraints(const Mesh& m, NormalMode mode) {
   const int nu = m.n_u(), np = m.n_p();
   Builder b(nu + np);
   if (m.cuboid) {
@@ -342,9 +387,11 @@ Constraints nse_constraints(const Mesh& m) {
     for (int n = 0; n < m.n_vnodes; ++n)
       if (m.vnode_bnd[n] & kBndInner)
         for (int c = 0; c < 3; ++c) b.add_line(3 * n + c);
+    const std::vector<double> cn =
+        mode == NormalMode::Consistent ? consistent_normals(m, kBndOuter) : std::vector<double>();
     for (int n = 0; n < m.n_vnodes; ++n)
       if (m.vnode_bnd[n] & kBndOuter) {
-        const double* x = &m.xyz[3 * size_t(n)];
+        const double* x = mode == NormalMode::Consistent ? &cn[3 * size_t(n)] : &m.xyz[3 * size_t(n)];
         const double r = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
         const double nn[3] = {x[0] / r, x[1] / r, x[2] / r};
         const int dofs[3] = {3 * n, 3 * n + 1, 3 * n + 2};

@@ -80,10 +80,21 @@ struct Constraints {
   }
 };
 
+// Normal used by the no-normal-flux constraint on the outer sphere.
+//   Consistent: n_i = sum_cells int grad(phi_i) dx (discretely consistent with
+//     the divergence block, so B^T 1 lies in the constrained space and the
+//     Schur complement's constant-pressure mode is exactly singular and never
+//     excited). Default; see DESIGN.md "no-normal-flux normals".
+//   Radial: the exact sphere normal at the support point (closest to deal.II's
+//     mapping normal); leaves S with a near-null eigenvalue ~ h^5.6 that the
+//     reference's identity-preconditioned Schur GMRES cannot resolve for r >= 3.
+enum class NormalMode { Consistent, Radial };
+std::vector<double> consistent_normals(const Mesh& m, uint8_t boundary_bit);
+
 // NSE constraints (boussinesq_model.tpp:259-333): shell -> no-slip on the
 // inner sphere, no-normal-flux on the outer sphere; cube -> periodic x/y,
 // no-slip z=0, no-normal-flux z=1. DoF space: [3*n_vnodes velocity | n_p pressure].
-Constraints nse_constraints(const Mesh& m);
+Constraints nse_constraints(const Mesh& m, NormalMode mode = NormalMode::Consistent);
 
 // Temperature constraints (:338-387): Dirichlet with the initial temperature on
 // the inner sphere (shell) or on z=0 (cube, + periodic x/y). degree 1 or 2.

@@ -36,7 +36,7 @@ EXPORTED = [
     "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult",
     "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
-    "dcp_get_timings", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
+    "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
     "dcp_host_mesh_view_get", "dcp_host_mesh_initial_temperature", "dcp_prm_load",
 ]
 
@@ -139,7 +139,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_precond_diagonals.argtypes = [P, P, P]
     lib.dcp_cell_nse_system.argtypes = [P, I, I, P, P]
     lib.dcp_get_timings.argtypes = [P, C.POINTER(Timings)]
-    lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I]
+    lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 4
+    lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_destroy.argtypes = [P]
     lib.dcp_host_mesh_destroy.restype = None
@@ -203,9 +204,13 @@ class ConstraintSet:
 class HostMesh:
     """Refined shell / cube with DoFs and constraints (setup_dofs restated)."""
 
-    def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1):
+    def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1,
+                 normals="consistent"):
+        if normals not in ("consistent", "radial"):
+            raise ValueError("normals must be 'consistent' or 'radial'")
         h = lib().dcp_host_mesh_create(int(cuboid), int(refine), float(R0), float(R1),
-                                       float(length), int(temperature_degree))
+                                       float(length), int(temperature_degree),
+                                       0 if normals == "consistent" else 1)
         if not h:
             raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
         try:
@@ -392,20 +397,24 @@ class Context:
         self._check(lib().dcp_cell_nse_system(self._h, int(first), int(n), _ptr(K), _ptr(f)))
         return K, f
 
+    def pattern_info(self) -> dict:
+        v = [C.c_int64() for _ in range(4)]
+        self._check(lib().dcp_pattern_info(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("nnzb_A", "nnzb_Bt", "nnzb_B", "nnz_T"), (x.value for x in v)))
+
     def timings(self) -> dict:
         t = Timings()
         self._check(lib().dcp_get_timings(self._h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in Timings._fields_}
 
-    # -- operators on host arrays (copied through the device state buffers)
+    # -- operators on host arrays (staged through scratch device buffers)
     def _dev_roundtrip(self, fn, src, n_out):
-        import torch  # device memory plumbing only
-        d_src = torch.as_tensor(np.ascontiguousarray(src), device="cuda")
-        d_dst = torch.zeros(n_out, dtype=torch.float64, device="cuda")
-        torch.cuda.synchronize()
-        rc = fn(C.c_void_p(d_src.data_ptr()), C.c_void_p(d_dst.data_ptr()))
-        torch.cuda.synchronize()
-        return rc, d_dst.cpu().numpy()
+        src = np.ascontiguousarray(src, dtype=np.float64)
+        with DeviceBuffer(src.size) as d_src, DeviceBuffer(n_out) as d_dst:
+            d_src.upload(src)
+            rc = fn(C.c_void_p(d_src.ptr), C.c_void_p(d_dst.ptr))
+            out = d_dst.download() if rc in (DCP_OK, DCP_NOT_CONVERGED) else None
+        return rc, out
 
     def nse_vmult(self, src):
         n = self.mesh.n_u + self.mesh.n_p
@@ -427,6 +436,56 @@ class Context:
                                                               C.byref(it)), src, n)
         self._check(rc, True)
         return out, it.value
+
+
+_hip = None
+
+
+def hip() -> C.CDLL:
+    """The HIP runtime libdcp.so links against (device-memory plumbing only)."""
+    global _hip
+    if _hip is None:
+        lib()
+        _hip = C.CDLL("libamdhip64.so")
+        _hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        _hip.hipFree.argtypes = [C.c_void_p]
+        _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _hip.hipDeviceSynchronize.argtypes = []
+    return _hip
+
+
+class DeviceBuffer:
+    """A raw FP64 device allocation (hipMalloc) for passing d_src/d_dst pointers."""
+
+    def __init__(self, n):
+        self.n = int(n)
+        p = C.c_void_p()
+        rc = hip().hipMalloc(C.byref(p), max(self.n, 1) * 8)
+        if rc != 0:
+            raise DcpError(DCP_ERR_DEVICE, f"hipMalloc failed ({rc})")
+        self.ptr = p.value
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        assert a.size == self.n
+        hip().hipMemcpy(C.c_void_p(self.ptr), a.ctypes.data_as(C.c_void_p), a.nbytes, 1)
+
+    def download(self):
+        out = np.zeros(self.n)
+        hip().hipDeviceSynchronize()
+        hip().hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes, 2)
+        return out
+
+    def close(self):
+        if self.ptr:
+            hip().hipFree(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def physics_from_params(rp: RunParams) -> Physics:

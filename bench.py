@@ -143,26 +143,8 @@ def main():
     outer = recs[-1][1]
     inner = recs[-1][2]
     schur_ms = np.mean([r[4]["schur_apply_ms_avg"] for r in recs])
-    nnzb_bt = int(ctx._nnzb_bt) if hasattr(ctx, "_nnzb_bt") else None
-    # nnz of the 3x1 / 1x3 blocks from the exported pattern size identities
-    rp_, cols, _ = (None, None, None)
-    n_v = m.n_u // 3
-    # B^T and B have identical block counts (node-vertex incidences)
-    nnz_total = None
-    try:
-        import ctypes as C
-        nnz = C.c_int64()
-        dcp.lib().dcp_nse_matrix_export(ctx._h, C.byref(nnz), None, None, None)
-        nnz_total = nnz.value
-    except Exception:
-        pass
-    # node-vertex incidences: every (vnode, vertex) pair sharing a cell
-    q2 = m.cell_nse_dofs[:, [0] + list(range(32, 89, 3))][:, :]
-    nodes = np.concatenate([m.cell_nse_dofs[:, 0:32:4], m.cell_nse_dofs[:, 32::3]], axis=1) // 3
-    pv = m.cell_nse_dofs[:, 3:32:4] - m.n_u
-    pairs = np.unique(nodes[:, :, None].astype(np.int64) * m.n_p + pv[:, None, :], axis=None)
-    nnzb = int(pairs.size)
-    sbytes = schur_bytes(m, nnzb, nnzb)
+    pinfo = ctx.pattern_info()
+    sbytes = schur_bytes(m, pinfo["nnzb_Bt"], pinfo["nnzb_B"])
     achieved = sbytes / (schur_ms * 1e-3) / 1e9 if schur_ms > 0 else 0.0
     value = n_nse / (asm_ms * 1e-3) * world
     out = {
@@ -189,6 +171,8 @@ def main():
         "phase_ms": {k: float(np.mean([r[4][k] for r in recs])) for k in recs[0][4]
                      if k.endswith("_ms") or k.endswith("_avg")},
         "setup_s": t_setup,
+        "converged": all(r[0] == 0 for r in recs),
+        "patterns": pinfo,
         "roofline": {"kernel": "Schur complement apply B D_A^-1 B^T (3 kernels)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -158,6 +158,10 @@ int dcp_precond_diagonals(dcp_ctx* ctx, double* A_diag, double* Mp_diag);
  * K [n][89][89], f [n][89] in FESystem order (CopyData::NSESystem). */
 int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 
+/* Sizes of the device block patterns: A (3x3 blocks), B^T (3x1), B (1x3), T (scalar). */
+int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* nnzb_B,
+                     int64_t* nnz_T);
+
 /* Timing of the last hot-path calls (device time, milliseconds). */
 typedef struct {
   double assemble_nse_ms, build_precond_ms, assemble_T_matrix_ms, assemble_T_rhs_ms;
@@ -170,9 +174,10 @@ int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
 /* Host setup helpers (mesh generator, .prm) ----------------------------- */
 typedef struct dcp_host_mesh dcp_host_mesh;
 /* Builds the refined shell (cuboid = 0) or cube, DoFs and constraints the way
- * setup_dofs() does (see mesh.h for the geometry convention). */
+ * setup_dofs() does (see mesh.h for the geometry convention). normal_mode of
+ * the no-normal-flux constraint: 0 = consistent (default), 1 = radial. */
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
-                                    int temperature_degree);
+                                    int temperature_degree, int normal_mode);
 void dcp_host_mesh_destroy(dcp_host_mesh* m);
 typedef struct {
   int n_cells, n_u, n_p, n_T, n_vnodes;

@@ -33,7 +33,7 @@ def test_dof_layout_component_wise():
 
 
 def test_shell_geometry_and_boundaries():
-    m = dcp.HostMesh(refine=2, R0=1.0, R1=3.0)
+    m = dcp.HostMesh(refine=2, R0=1.0, R1=3.0, normals="radial")
     r = np.linalg.norm(m.node_xyz, axis=1)
     assert np.isclose(r.min(), 1.0) and np.isclose(r.max(), 3.0)
     # inner sphere: no-slip on all 3 components; outer: one no-normal-flux line per node
