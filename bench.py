@@ -41,6 +41,8 @@ def parse():
                                                   "aqua_planet_shell_test_3d-classic.prm"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-refine", type=int, default=3)
+    ap.add_argument("--probe-schur", type=int, default=0,
+                    help="PMC probe: only N Schur-complement applies after one assembly")
     return ap.parse_args()
 
 
@@ -100,6 +102,20 @@ def main():
     for f, v in ((dcp.OLD_NSE_SOLUTION, u0), (dcp.OLD_T_SOLUTION, m.T0)):
         ctx.set_state(f, v)
     t_setup = time.perf_counter() - t_setup
+
+    if args.probe_schur:
+        # PMC probe: assemble once, then only Schur-complement applies (few dispatches)
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        x = np.random.default_rng(20261015).uniform(-1, 1, m.n_p)
+        x -= x.mean()
+        with dcp.DeviceBuffer(m.n_p) as d_src, dcp.DeviceBuffer(m.n_p) as d_dst:
+            d_src.upload(x)
+            for _ in range(args.probe_schur):
+                ctx._check(dcp.lib().dcp_schur_vmult(ctx._h, d_src.ptr, d_dst.ptr))
+        print(json.dumps({"probe": "schur", "applies": args.probe_schur, "refine": args.refine}))
+        ctx.close()
+        return
 
     def step():
         ctx.copy_state(dcp.NSE_SOLUTION, dcp.OLD_NSE_SOLUTION)
