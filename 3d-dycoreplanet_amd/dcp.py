@@ -451,6 +451,7 @@ def hip() -> C.CDLL:
         _hip.hipFree.argtypes = [C.c_void_p]
         _hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         _hip.hipDeviceSynchronize.argtypes = []
+        _hip.hipMemset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
     return _hip
 
 
@@ -464,6 +465,7 @@ class DeviceBuffer:
         if rc != 0:
             raise DcpError(DCP_ERR_DEVICE, f"hipMalloc failed ({rc})")
         self.ptr = p.value
+        hip().hipMemset(C.c_void_p(self.ptr), 0, max(self.n, 1) * 8)  # zero-initialised
 
     def upload(self, a):
         a = np.ascontiguousarray(a, dtype=np.float64)
