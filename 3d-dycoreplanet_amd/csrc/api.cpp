@@ -152,7 +152,8 @@ struct HostPrep {
   std::vector<double> Tbc;
   std::vector<int> color_ptr;
   std::vector<int32_t> ccells;
-  std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc;
+  std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc, Sp, Sc;
+  int S_max_row = 0;
 };
 
 // Host half of dcp_mesh_upload: validation, node map, node-local constraints,
@@ -306,6 +307,36 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, h.Btp, h.Btc);
   union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, h.Bp, h.Bc);
   union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, h.Tp, h.Tc);
+  // Pattern of the explicit Schur complement S = B D^-1 B^T: row p couples the
+  // vertices reachable through one velocity node (the 2-cell vertex patch).
+  h.Sp.assign(size_t(n_p) + 1, 0);
+  std::vector<std::vector<int32_t>> srow(n_p);
+#pragma omp parallel
+  {
+    std::vector<int32_t> mark(n_p, -1);
+#pragma omp for schedule(dynamic, 256)
+    for (int p = 0; p < n_p; ++p) {
+      std::vector<int32_t>& r = srow[p];
+      for (int k = h.Bp[p]; k < h.Bp[p + 1]; ++k) {
+        const int n = h.Bc[k];
+        for (int j = h.Btp[n]; j < h.Btp[n + 1]; ++j) {
+          const int q = h.Btc[j];
+          if (mark[q] != p) {
+            mark[q] = p;
+            r.push_back(q);
+          }
+        }
+      }
+      std::sort(r.begin(), r.end());
+    }
+  }
+  for (int p = 0; p < n_p; ++p) h.Sp[p + 1] = h.Sp[p] + int32_t(srow[p].size());
+  h.Sc.resize(size_t(h.Sp[n_p]));
+  h.S_max_row = 0;
+  for (int p = 0; p < n_p; ++p) {
+    std::copy(srow[p].begin(), srow[p].end(), h.Sc.begin() + h.Sp[p]);
+    h.S_max_row = std::max(h.S_max_row, int(srow[p].size()));
+  }
 }
 
 }  // namespace
@@ -361,6 +392,18 @@ int dcp_set_physics(dcp_ctx* ctx, const dcp_physics* ph) {
     set_physics_dev(*ctx);
     ctx->have_physics = true;
     return DCP_OK;
+  });
+}
+
+int dcp_set_option(dcp_ctx* ctx, int option, int value) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
+    if (option == DCP_OPT_SCHUR_EXPLICIT) {
+      ctx->schur_explicit = value != 0;
+      ctx->precond_built = false;  // S must be (re)formed
+      return DCP_OK;
+    }
+    fail(DCP_ERR_INVALID, "unknown option " + std::to_string(option));
   });
 }
 
@@ -430,6 +473,10 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.B_col.upload(Bc);
     c.T_ptr.upload(Tp);
     c.T_col.upload(Tc);
+    c.S_ptr.upload(h.Sp);
+    c.S_col.upload(h.Sc);
+    c.S_val.alloc(h.Sc.size());
+    c.S_max_row = h.S_max_row;
     c.A_val.alloc(Ac.size() * 9);
     c.Bt_val.alloc(Btc.size() * 3);
     c.B_val.alloc(Bc.size() * 3);
@@ -553,6 +600,14 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
                               c.Mp_diag.p, c.stream);
     reciprocal(c.n_u, c.A_diag.p, c.A_inv.p, c.stream);
     reciprocal(c.n_p, c.Mp_diag.p, c.Mp_inv.p, c.stream);
+    if (c.schur_explicit) {
+      require(c.nse_assembled, DCP_ERR_STATE,
+              "the explicit Schur complement needs the assembled B blocks: call "
+              "dcp_assemble_nse_system first");
+      form_schur_complement(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
+                            c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_val.p, c.S_max_row,
+                            c.stream);
+    }
     t.stop();
     c.precond_built = true;
     return DCP_OK;

@@ -68,6 +68,11 @@ struct Ctx {
   DBuf<int32_t> A_ptr, A_col, Bt_ptr, Bt_col, B_ptr, B_col, T_ptr, T_col;
   DBuf<double> A_val, Bt_val, B_val, Tmass, Tstiff, Tmat;
   DBuf<int32_t> posA, posBt, posB, posT;
+  // explicit Schur complement S = B D_A^-1 B^T (CSR over pressure dofs)
+  DBuf<int32_t> S_ptr, S_col;
+  DBuf<double> S_val;
+  int S_max_row = 0;
+  bool schur_explicit = true;
   // state
   DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;
   DBuf<double> A_diag, Mp_diag, A_inv, Mp_inv, T_inv;

@@ -98,6 +98,13 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
                                int32_t* posA, int32_t* posBt, int32_t* posB, int32_t* posT,
                                hipStream_t s);
 
+// S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
+// contributions summed in fixed node order: deterministic).
+void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
+                           const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
+                           const double* d, const int32_t* S_ptr, const int32_t* S_col,
+                           double* S_val, int max_row, hipStream_t s);
+
 // ---- linalg.hip -------------------------------------------------------------
 // y (=|+=) alpha * M x for block-CSR with R x C blocks (R,C in {1,3}).
 void spmv_bsr33(int rows, const int32_t* ptr, const int32_t* col, const double* val,
@@ -108,6 +115,9 @@ void spmv_bsr13(int rows, const int32_t* ptr, const int32_t* col, const double* 
                 const double* x, double* y, bool add, hipStream_t s);
 void spmv_csr(int rows, const int32_t* ptr, const int32_t* col, const double* val,
               const double* x, double* y, bool add, hipStream_t s);
+// CSR with long rows (~125 nnz, the Schur complement): 32 lanes per row
+void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                   const double* x, double* y, bool add, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):
@@ -123,6 +133,16 @@ void dot(int n, const double* a, const double* b, double* partials, double* out,
 // v += c * x; then *out = v . w (w == v allowed) — deal.II add_and_dot
 void add_and_dot(int n, double* v, DScal c, const double* x, const double* w, double* partials,
                  double* out, hipStream_t s);
+// Launch-lean Gram-Schmidt chain (one launch per step, no reduction launches):
+//   dot_partial writes nb block sums of a.b; chain_add_and_dot reduces the
+//   previous step's nb partials (stores the sum to *coef_store from block 0),
+//   does v += mult * sum * x and writes the nb partials of v.w.
+constexpr int kChainMaxBlocks = 1024;
+int chain_blocks(int n);
+void dot_partial(int n, const double* a, const double* b, double* partials, int nb, hipStream_t s);
+void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
+                       const double* w, double* partials, double* coef_store, int nb,
+                       hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

@@ -585,7 +585,63 @@ __global__ void k_scatter_maps(CellData cd, const int32_t* A_ptr, const int32_t*
   }
 }
 
+// S_pq = sum_n sum_c B[p][n][c] d[3n+c] B^T[n][q][c]; one 64-lane workgroup
+// per pressure row. The node loop is sequential and the lanes of one node
+// write distinct q, so every entry is summed in the same (node) order.
+__global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __restrict__ B_ptr,
+                                                   const int32_t* __restrict__ B_col,
+                                                   const double* __restrict__ B_val,
+                                                   const int32_t* __restrict__ Bt_ptr,
+                                                   const int32_t* __restrict__ Bt_col,
+                                                   const double* __restrict__ Bt_val,
+                                                   const double* __restrict__ d,
+                                                   const int32_t* __restrict__ S_ptr,
+                                                   const int32_t* __restrict__ S_col,
+                                                   double* __restrict__ S_val) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int p = blockIdx.x;
+  const int s0 = S_ptr[p], len = S_ptr[p + 1] - s0;
+  double* acc = reinterpret_cast<double*>(smem);
+  int* cols = reinterpret_cast<int*>(acc + len);
+  for (int j = threadIdx.x; j < len; j += 64) {
+    acc[j] = 0.0;
+    cols[j] = S_col[s0 + j];
+  }
+  __syncthreads();
+  for (int k = B_ptr[p]; k < B_ptr[p + 1]; ++k) {
+    const size_t n = size_t(B_col[k]);
+    const double w0 = B_val[3 * size_t(k)] * d[3 * n];
+    const double w1 = B_val[3 * size_t(k) + 1] * d[3 * n + 1];
+    const double w2 = B_val[3 * size_t(k) + 2] * d[3 * n + 2];
+    const int b = Bt_ptr[n], e = Bt_ptr[n + 1];
+    for (int j = b + int(threadIdx.x); j < e; j += 64) {
+      const int q = Bt_col[j];
+      const double v = w0 * Bt_val[3 * size_t(j)] + w1 * Bt_val[3 * size_t(j) + 1] +
+                       w2 * Bt_val[3 * size_t(j) + 2];
+      int lo = 0, hi = len;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (cols[m] < q) lo = m + 1; else hi = m;
+      }
+      acc[lo] += v;
+    }
+    __syncthreads();
+  }
+  for (int j = threadIdx.x; j < len; j += 64) S_val[s0 + j] = acc[j];
+}
+
 }  // namespace
+
+void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
+                           const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
+                           const double* d, const int32_t* S_ptr, const int32_t* S_col,
+                           double* S_val, int max_row, hipStream_t s) {
+  if (n_p <= 0) return;
+  const size_t lds = size_t(max_row) * (sizeof(double) + sizeof(int)) + 16;
+  hipLaunchKernelGGL(k_schur_form, dim3(n_p), dim3(64), lds, s, n_p, B_ptr, B_col, B_val, Bt_ptr,
+                     Bt_col, Bt_val, d, S_ptr, S_col, S_val);
+  DCP_HIP_CHECK(hipGetLastError());
+}
 
 void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                        const double* u_old, const double* T_old, const PhysicsDev& ph,

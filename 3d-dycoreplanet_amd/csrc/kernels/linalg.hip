@@ -106,6 +106,39 @@ __global__ __launch_bounds__(kBlock) void k_add_and_dot(int n, double* v, DScal 
   if (threadIdx.x == 0) partials[blockIdx.x] = r;
 }
 
+// Chained Gram-Schmidt step without a separate reduction launch: every block
+// first sums the previous step's nb partials in the same fixed order (so all
+// blocks agree bitwise), block 0 stores that coefficient, then
+// v += mult * coef * x and the partial dot(v, w) of this block is written.
+__global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(int n, double* v,
+                                                              const double* __restrict__ prev,
+                                                              int nb, double mult,
+                                                              const double* __restrict__ x,
+                                                              const double* w,
+                                                              double* __restrict__ partials,
+                                                              double* coef_store) {
+  __shared__ double sm[4];
+  __shared__ double coef_sh;
+  double s = 0;
+  for (int i = threadIdx.x; i < nb; i += kBlock) s += prev[i];
+  const double tot = block_sum(s, sm);
+  if (threadIdx.x == 0) {
+    coef_sh = tot;
+    if (blockIdx.x == 0) *coef_store = tot;
+  }
+  __syncthreads();
+  const double cf = mult * coef_sh;
+  double d = 0;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    const double nv = v[i] + cf * x[i];
+    v[i] = nv;
+    d += nv * (w == v ? nv : w[i]);
+  }
+  __syncthreads();
+  const double r = block_sum(d, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = r;
+}
+
 __global__ __launch_bounds__(kBlock) void k_reduce_final(int nb, const double* __restrict__ partials,
                                                          double* out) {
   __shared__ double sm[4];
@@ -303,9 +336,33 @@ void spmv_csr(int rows, const int32_t* ptr, const int32_t* col, const double* va
   spmv<1, 1, 16>(rows, ptr, col, val, x, y, add, s);
 }
 
+void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const double* val,
+                   const double* x, double* y, bool add, hipStream_t s) {
+  spmv<1, 1, 32>(rows, ptr, col, val, x, y, add, s);
+}
+
 void dot(int n, const double* a, const double* b, double* partials, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_dot_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, a, b, partials);
   hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, kReduceBlocks, partials, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+int chain_blocks(int n) {
+  int nb = (n + 4095) / 4096;
+  nb = ((nb + 63) / 64) * 64;
+  return nb < 64 ? 64 : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
+}
+
+void dot_partial(int n, const double* a, const double* b, double* partials, int nb, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, n, a, b, partials);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
+                       const double* w, double* partials, double* coef_store, int nb,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, n, v, prev, nb, mult, x, w,
+                     partials, coef_store);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -45,7 +45,10 @@ constexpr int kSlotB = 259;
 constexpr int kSlotC = 260;
 constexpr int kSlotD = 261;
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
-constexpr int kNumSlots = kSlotMinMax + 2 + 2 * kReduceBlocks;
+constexpr int kNumSlots = 4096;             // device slots; host mirror: partials at kHostPartials
+constexpr int kHostPartials = 2048;
+static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kHostPartials, "slot layout");
+static_assert(kHostPartials + kChainMaxBlocks <= kNumSlots, "slot layout");
 
 using Op = std::function<void(const double*, double*)>;
 
@@ -104,34 +107,60 @@ void givens_rotation(std::vector<double>& h, std::vector<double>& b, std::vector
 // Modified Gram-Schmidt of deal.II SolverGMRES (add_and_dot chain; every 5th
 // step the loss-of-orthogonality test; once triggered a second pass for the
 // rest of the solve). Returns |vv| after orthogonalisation; h[0..dim) filled.
+// Partial-sum buffers of the launch-lean chain (c.partials holds 4 of them).
+double* pbuf(Ctx& c, int i) { return c.partials.p + size_t(i) * kChainMaxBlocks; }
+
+// Host side of a chain: fetch `ncoef` coefficient slots starting at `s0` and
+// the nb final partials of buffer `b`; returns their fixed-order sum.
+double fetch_chain(Ctx& c, int s0, int ncoef, int b, int nb, std::vector<double>& coef) {
+  if (ncoef > 0)
+    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, slot(c, s0), ncoef * sizeof(double),
+                                 hipMemcpyDeviceToHost, c.stream));
+  DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + kHostPartials, pbuf(c, b),
+                               nb * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  coef.assign(c.hpinned, c.hpinned + ncoef);
+  double s = 0;
+  const double* p = c.hpinned + kHostPartials;
+  for (int i = 0; i < nb; ++i) s += p[i];
+  return s;
+}
+
+// Gram-Schmidt chain of deal.II's add_and_dot sequence:
+//   h_0 = w.V0; h_i = (w -= h_{i-1} V_{i-1}) . V_i; |w -= h_{last} V_last|^2
+// one launch per step; coefficients land in slots s0.. and on the host.
+double gs_chain(Ctx& c, int n, const std::vector<double*>& V, int dim, double* w, int s0,
+                std::vector<double>& h) {
+  const int nb = chain_blocks(n);
+  dot_partial(n, w, V[0], pbuf(c, 0), nb, c.stream);
+  for (int i = 1; i < dim; ++i)
+    chain_add_and_dot(n, w, pbuf(c, (i - 1) & 1), -1.0, V[i - 1], V[i], pbuf(c, i & 1),
+                      slot(c, s0 + i - 1), nb, c.stream);
+  chain_add_and_dot(n, w, pbuf(c, (dim - 1) & 1), -1.0, V[dim - 1], w, pbuf(c, dim & 1),
+                    slot(c, s0 + dim - 1), nb, c.stream);
+  return fetch_chain(c, s0, dim, dim & 1, nb, h);
+}
+
 double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int dim, double* vv,
                              std::vector<double>& h, bool& reorth) {
   const bool consider = !reorth && ((dim - 1) % 5 == 4);
-  if (consider) dot(n, vv, vv, c.partials.p, slot(c, kSlotNStart), c.stream);
-  dot(n, vv, V[0], c.partials.p, slot(c, kSlotH), c.stream);
-  for (int i = 1; i < dim; ++i)
-    add_and_dot(n, vv, DScal{slot(c, kSlotH + i - 1), -1.0}, V[i - 1], V[i], c.partials.p,
-                slot(c, kSlotH + i), c.stream);
-  add_and_dot(n, vv, DScal{slot(c, kSlotH + dim - 1), -1.0}, V[dim - 1], vv, c.partials.p,
-              slot(c, kSlotNN), c.stream);
-  const double* r = fetch(c, 0, kSlotNStart + 1);
-  for (int i = 0; i < dim; ++i) h[i] = r[kSlotH + i];
-  double norm_vv = std::sqrt(r[kSlotNN]);
+  double start2 = 0;
   if (consider) {
-    const double start = std::sqrt(r[kSlotNStart]);
-    if (norm_vv > 10. * start * std::sqrt(2.220446049250313e-16)) return norm_vv;
+    const int nb = chain_blocks(n);
+    dot_partial(n, vv, vv, pbuf(c, 2), nb, c.stream);
+    std::vector<double> none;
+    start2 = fetch_chain(c, 0, 0, 2, nb, none);
+  }
+  std::vector<double> hv;
+  double norm_vv = std::sqrt(gs_chain(c, n, V, dim, vv, kSlotH, hv));
+  for (int i = 0; i < dim; ++i) h[i] = hv[i];
+  if (consider) {
+    if (norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16)) return norm_vv;
     reorth = true;
   }
   if (reorth) {
-    dot(n, vv, V[0], c.partials.p, slot(c, kSlotH2), c.stream);
-    for (int i = 1; i < dim; ++i)
-      add_and_dot(n, vv, DScal{slot(c, kSlotH2 + i - 1), -1.0}, V[i - 1], V[i], c.partials.p,
-                  slot(c, kSlotH2 + i), c.stream);
-    add_and_dot(n, vv, DScal{slot(c, kSlotH2 + dim - 1), -1.0}, V[dim - 1], vv, c.partials.p,
-                slot(c, kSlotNN), c.stream);
-    const double* r2 = fetch(c, 0, kSlotNStart + 1);
-    for (int i = 0; i < dim; ++i) h[i] += r2[kSlotH2 + i];
-    norm_vv = std::sqrt(r2[kSlotNN]);
+    norm_vv = std::sqrt(gs_chain(c, n, V, dim, vv, kSlotH2, hv));
+    for (int i = 0; i < dim; ++i) h[i] += hv[i];
   }
   return norm_vv;
 }
@@ -296,15 +325,10 @@ State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, 
       else fill(n, 0.0, vj, c.stream);
       block_prec(c, vj, zj, do_solve_A, inner);
       nse_vmult(c, zj, aux);
-      dot(n, aux, c.fg_v[0], c.partials.p, slot(c, kSlotH), c.stream);
-      for (int i = 1; i <= j; ++i)
-        add_and_dot(n, aux, DScal{slot(c, kSlotH + i - 1), -1.0}, c.fg_v[i - 1], c.fg_v[i],
-                    c.partials.p, slot(c, kSlotH + i), c.stream);
-      add_and_dot(n, aux, DScal{slot(c, kSlotH + j), -1.0}, vj, aux, c.partials.p,
-                  slot(c, kSlotNN), c.stream);
-      const double* r = fetch(c, 0, kSlotNN + 1);
-      for (int i = 0; i <= j; ++i) H[i][j] = r[kSlotH + i];
-      H[j + 1][j] = a = std::sqrt(r[kSlotNN]);
+      std::vector<double> hv;
+      const double nn = gs_chain(c, n, c.fg_v, j + 1, aux, kSlotH, hv);
+      for (int i = 0; i <= j; ++i) H[i][j] = hv[i];
+      H[j + 1][j] = a = std::sqrt(nn);
       if (j > 0) {
         std::vector<std::vector<double>> H1(j + 1, std::vector<double>(j, 0.0));
         for (int rr = 0; rr <= j; ++rr)
@@ -332,6 +356,16 @@ void nse_vmult(Ctx& c, const double* src, double* dst) {
 }
 
 void schur_vmult(Ctx& c, const double* src, double* dst) {
+  if (c.schur_explicit) {
+    Timer* e = nullptr;
+    if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
+        c.schur_ev_used < Ctx::kSchurEvents)
+      e = &c.schur_ev[c.schur_ev_used++];
+    if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+    spmv_csr_long(c.n_p, c.S_ptr.p, c.S_col.p, c.S_val.p, src, dst, false, c.stream);
+    if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+    return;
+  }
   Timer* ev = nullptr;
   if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
       c.schur_ev_used < Ctx::kSchurEvents)
@@ -353,7 +387,7 @@ void free_workspaces(Ctx& c) {
 void ensure_workspaces(Ctx& c) {
   if (c.dscal.p == nullptr) {
     c.dscal.alloc(kNumSlots);
-    c.partials.alloc(kReduceBlocks);
+    c.partials.alloc(4 * size_t(kChainMaxBlocks));
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hpinned), kNumSlots * sizeof(double)));
     c.coef.alloc(128);
     c.ptrs.alloc(128);

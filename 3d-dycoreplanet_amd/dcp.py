@@ -25,11 +25,12 @@ DCP_OK, DCP_NOT_CONVERGED = 0, 1
 DCP_ERR_INVALID, DCP_ERR_UNSUPPORTED, DCP_ERR_DEVICE, DCP_ERR_STATE = -1, -2, -3, -4
 NSE_SOLUTION, OLD_NSE_SOLUTION, T_SOLUTION, OLD_T_SOLUTION, NSE_RHS, T_RHS = range(6)
 ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
+OPT_SCHUR_EXPLICIT = 1
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "dcp_ctx_create", "dcp_ctx_destroy", "dcp_last_error", "dcp_device_count",
-    "dcp_set_physics", "dcp_set_time_step", "dcp_mesh_upload", "dcp_mesh_check", "dcp_state_set",
+    "dcp_set_physics", "dcp_set_time_step", "dcp_set_option", "dcp_mesh_upload", "dcp_mesh_check", "dcp_state_set",
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
     "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
@@ -114,6 +115,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_ctx_destroy.restype = None
     lib.dcp_set_physics.argtypes = [P, C.POINTER(Physics)]
     lib.dcp_set_time_step.argtypes = [P, C.c_double]
+    lib.dcp_set_option.argtypes = [P, I, I]
     lib.dcp_mesh_upload.argtypes = [P, I, P, P, P, P, I, I, I, C.POINTER(Constraints),
                                     C.POINTER(Constraints)]
     lib.dcp_mesh_check.argtypes = [I, P, P, P, P, I, I, I, C.POINTER(Constraints),
@@ -293,6 +295,11 @@ class Context:
 
     def set_time_step(self, dt: float):
         self._check(lib().dcp_set_time_step(self._h, float(dt)))
+
+    def set_schur_explicit(self, on: bool):
+        """True: apply S = B D^-1 B^T as one formed CSR matrix (default);
+        False: B^T, Jacobi, B as SchurComplement::vmult does."""
+        self._check(lib().dcp_set_option(self._h, OPT_SCHUR_EXPLICIT, int(bool(on))))
 
     def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
         nc = (nse_constraints or m.nse_constraints).as_struct()

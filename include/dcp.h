@@ -88,6 +88,13 @@ int dcp_set_physics(dcp_ctx* ctx, const dcp_physics* ph);
 /* parameters.time_step (changed by recompute_time_step, :1104-1125). */
 int dcp_set_time_step(dcp_ctx* ctx, double dt);
 
+/* Execution options (no effect on the mathematics beyond rounding).
+ * DCP_OPT_SCHUR_EXPLICIT: 1 (default) = form S = B D_A^-1 B^T once per
+ *   build_nse_preconditioner and apply it as one CSR SpMV; 0 = apply it as
+ *   B^T, Jacobi, B like SchurComplement::vmult (schur_complement.hpp:143-150). */
+enum { DCP_OPT_SCHUR_EXPLICIT = 1 };
+int dcp_set_option(dcp_ctx* ctx, int option, int value);
+
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
  * device sparsity patterns, cell colouring and scatter maps once. */
 int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs /*[n][89]*/,

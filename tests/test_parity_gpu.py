@@ -120,8 +120,10 @@ def test_temperature_assembly(setup):
     assert rel_max(ctx.get_state(dcp.T_RHS), orc.T_rhs()) < 1e-12
 
 
-def test_operator_applies(setup):
+@pytest.mark.parametrize("explicit", [True, False], ids=["S-explicit", "S-composite"])
+def test_operator_applies(setup, explicit):
     m, ph, ctx, orc = setup
+    ctx.set_schur_explicit(explicit)
     rng = np.random.default_rng(SEED + 3)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
     ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
@@ -144,8 +146,10 @@ def test_operator_applies(setup):
     assert rel2(dg, do) < 1e-10
 
 
-def test_full_solve_and_temperature(setup):
+@pytest.mark.parametrize("explicit", [True, False], ids=["S-explicit", "S-composite"])
+def test_full_solve_and_temperature(setup, explicit):
     m, ph, ctx, orc = setup
+    ctx.set_schur_explicit(explicit)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
     for c in (ctx,):
         c.set_state(dcp.OLD_NSE_SOLUTION, u)
