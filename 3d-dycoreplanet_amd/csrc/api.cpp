@@ -856,13 +856,15 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
   });
 }
 
-int dcp_pattern_info(dcp_ctx* ctx, int64_t* nA, int64_t* nBt, int64_t* nB, int64_t* nT) {
+int dcp_pattern_info(dcp_ctx* ctx, int64_t* nA, int64_t* nBt, int64_t* nB, int64_t* nT,
+                     int64_t* nS) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
     if (nA) *nA = int64_t(ctx->A_col.n);
     if (nBt) *nBt = int64_t(ctx->Bt_col.n);
     if (nB) *nB = int64_t(ctx->B_col.n);
     if (nT) *nT = int64_t(ctx->T_col.n);
+    if (nS) *nS = int64_t(ctx->S_col.n);
     return DCP_OK;
   });
 }

@@ -348,9 +348,12 @@ void dot(int n, const double* a, const double* b, double* partials, double* out,
 }
 
 int chain_blocks(int n) {
-  int nb = (n + 4095) / 4096;
+  // >= 256 workgroups (one per CU) even for the 2e5-long pressure vectors: the
+  // chain steps are latency-bound, so width beats the cost of each block
+  // re-summing the previous step's nb partials.
+  int nb = (n + 1023) / 1024;
   nb = ((nb + 63) / 64) * 64;
-  return nb < 64 ? 64 : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
+  return nb < 256 ? 256 : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
 }
 
 void dot_partial(int n, const double* a, const double* b, double* partials, int nb, hipStream_t s) {

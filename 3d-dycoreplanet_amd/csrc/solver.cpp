@@ -112,14 +112,14 @@ double* pbuf(Ctx& c, int i) { return c.partials.p + size_t(i) * kChainMaxBlocks;
 
 // Host side of a chain: fetch `ncoef` coefficient slots starting at `s0` and
 // the nb final partials of buffer `b`; returns their fixed-order sum.
-double fetch_chain(Ctx& c, int s0, int ncoef, int b, int nb, std::vector<double>& coef) {
-  if (ncoef > 0)
-    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, slot(c, s0), ncoef * sizeof(double),
-                                 hipMemcpyDeviceToHost, c.stream));
-  DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + kHostPartials, pbuf(c, b),
-                               nb * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+// The last step of a chain writes its partials to slot kHostPartials, so one
+// contiguous copy [s0, kHostPartials + nb) brings coefficients and partials.
+double fetch_chain(Ctx& c, int s0, int ncoef, int nb, std::vector<double>& coef) {
+  DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + s0, slot(c, s0),
+                               (kHostPartials + nb - s0) * sizeof(double), hipMemcpyDeviceToHost,
+                               c.stream));
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
-  coef.assign(c.hpinned, c.hpinned + ncoef);
+  coef.assign(c.hpinned + s0, c.hpinned + s0 + ncoef);
   double s = 0;
   const double* p = c.hpinned + kHostPartials;
   for (int i = 0; i < nb; ++i) s += p[i];
@@ -136,9 +136,9 @@ double gs_chain(Ctx& c, int n, const std::vector<double*>& V, int dim, double* w
   for (int i = 1; i < dim; ++i)
     chain_add_and_dot(n, w, pbuf(c, (i - 1) & 1), -1.0, V[i - 1], V[i], pbuf(c, i & 1),
                       slot(c, s0 + i - 1), nb, c.stream);
-  chain_add_and_dot(n, w, pbuf(c, (dim - 1) & 1), -1.0, V[dim - 1], w, pbuf(c, dim & 1),
+  chain_add_and_dot(n, w, pbuf(c, (dim - 1) & 1), -1.0, V[dim - 1], w, slot(c, kHostPartials),
                     slot(c, s0 + dim - 1), nb, c.stream);
-  return fetch_chain(c, s0, dim, dim & 1, nb, h);
+  return fetch_chain(c, s0, dim, nb, h);
 }
 
 double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int dim, double* vv,
@@ -147,9 +147,9 @@ double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int d
   double start2 = 0;
   if (consider) {
     const int nb = chain_blocks(n);
-    dot_partial(n, vv, vv, pbuf(c, 2), nb, c.stream);
+    dot_partial(n, vv, vv, slot(c, kHostPartials), nb, c.stream);
     std::vector<double> none;
-    start2 = fetch_chain(c, 0, 0, 2, nb, none);
+    start2 = fetch_chain(c, kHostPartials, 0, nb, none);
   }
   std::vector<double> hv;
   double norm_vv = std::sqrt(gs_chain(c, n, V, dim, vv, kSlotH, hv));

@@ -141,7 +141,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_precond_diagonals.argtypes = [P, P, P]
     lib.dcp_cell_nse_system.argtypes = [P, I, I, P, P]
     lib.dcp_get_timings.argtypes = [P, C.POINTER(Timings)]
-    lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 4
+    lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 5
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_destroy.argtypes = [P]
@@ -405,9 +405,9 @@ class Context:
         return K, f
 
     def pattern_info(self) -> dict:
-        v = [C.c_int64() for _ in range(4)]
+        v = [C.c_int64() for _ in range(5)]
         self._check(lib().dcp_pattern_info(self._h, *[C.byref(x) for x in v]))
-        return dict(zip(("nnzb_A", "nnzb_Bt", "nnzb_B", "nnz_T"), (x.value for x in v)))
+        return dict(zip(("nnzb_A", "nnzb_Bt", "nnzb_B", "nnz_T", "nnz_S"), (x.value for x in v)))
 
     def timings(self) -> dict:
         t = Timings()

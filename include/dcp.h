@@ -167,7 +167,7 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 
 /* Sizes of the device block patterns: A (3x3 blocks), B^T (3x1), B (1x3), T (scalar). */
 int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* nnzb_B,
-                     int64_t* nnz_T);
+                     int64_t* nnz_T, int64_t* nnz_S);
 
 /* Timing of the last hot-path calls (device time, milliseconds). */
 typedef struct {
