@@ -490,6 +490,12 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     launch_build_scatter_maps(c.cd(), c.A_ptr.p, c.A_col.p, c.Bt_ptr.p, c.Bt_col.p, c.B_ptr.p,
                               c.B_col.p, c.T_ptr.p, c.T_col.p, c.posA.p, c.posBt.p, c.posB.p,
                               c.posT.p, c.stream);
+    c.first_touch_A = mark_first_touch(c.color_cells.p, c.color_ptr, 729, c.posA.p, n_cells,
+                                       Ac.size(), c.stream);
+    c.first_touch_Bt = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posBt.p, n_cells,
+                                        Btc.size(), c.stream);
+    c.first_touch_B = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posB.p, n_cells,
+                                       Bc.size(), c.stream);
     const size_t nn = size_t(n_u + n_p);
     c.nse_sol.alloc(nn);
     c.old_nse.alloc(nn);
@@ -568,9 +574,10 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
     NseOut out{};
     if (flags & DCP_ASSEMBLE_MATRIX) {
-      c.A_val.zero(c.stream);
-      c.Bt_val.zero(c.stream);
-      c.B_val.zero(c.stream);
+      // first-touch scatter positions store instead of adding: no zero fill
+      if (!c.first_touch_A) c.A_val.zero(c.stream);
+      if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
+      if (!c.first_touch_B) c.B_val.zero(c.stream);
       out.A = c.A_val.p;
       out.Bt = c.Bt_val.p;
       out.B = c.B_val.p;

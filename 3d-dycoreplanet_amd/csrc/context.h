@@ -68,6 +68,8 @@ struct Ctx {
   DBuf<int32_t> A_ptr, A_col, Bt_ptr, Bt_col, B_ptr, B_col, T_ptr, T_col;
   DBuf<double> A_val, Bt_val, B_val, Tmass, Tstiff, Tmat;
   DBuf<int32_t> posA, posBt, posB, posT;
+  // scatter positions carry first-touch marks (no zero fill before assembly)
+  bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
   // explicit Schur complement S = B D_A^-1 B^T (CSR over pressure dofs)
   DBuf<int32_t> S_ptr, S_col;
   DBuf<double> S_val;

@@ -2,6 +2,7 @@
 // the HIP kernels (assembly.hip, linalg.hip). Host orchestration code
 // (api.cpp, solver.cpp) talks to the GPU only through these functions.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -100,6 +101,13 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 
 // S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
 // contributions summed in fixed node order: deterministic).
+// Re-encode the scatter positions of the first cell (in colour launch order)
+// touching each block as ~pos; true if every one of the nnz blocks is touched
+// (then the assembly stores first and needs no zero fill), else the
+// positions are left plain.
+bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s);
+
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
                            const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,

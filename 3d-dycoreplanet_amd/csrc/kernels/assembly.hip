@@ -144,25 +144,175 @@ __device__ inline void condensation(const NodeConstraint& nc, double C[3][3]) {
 }
 
 // ---------------------------------------------------------------------------
+// Cell-independent reference tables at the QGauss(3) points, evaluated at
+// compile time with the same products the per-point helpers above use.
+struct RefTables {
+  double S2[27 * 27];      // [q][n] Q2 values
+  double G2[27 * 27 * 3];  // [q][n][e] Q2 reference gradients
+  double S1[27 * 8];       // [q][v] Q1 values
+};
+constexpr double ce_l2(int i, double x) {
+  return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+}
+constexpr double ce_dl2(int i, double x) {
+  return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1;
+}
+constexpr double ce_l1(int i, double x) { return i == 0 ? 1 - x : x; }
+constexpr RefTables make_ref_tables() {
+  RefTables t{};
+  for (int q = 0; q < 27; ++q) {
+    const double xa = kGaussX[q % 3], xb = kGaussX[(q / 3) % 3], xc = kGaussX[q / 9];
+    for (int n = 0; n < 27; ++n) {
+      const int na = n % 3, nb = (n / 3) % 3, nc = n / 9;
+      const double la = ce_l2(na, xa), lb = ce_l2(nb, xb), lc = ce_l2(nc, xc);
+      t.S2[27 * q + n] = la * lb * lc;
+      t.G2[3 * (27 * q + n) + 0] = ce_dl2(na, xa) * lb * lc;
+      t.G2[3 * (27 * q + n) + 1] = la * ce_dl2(nb, xb) * lc;
+      t.G2[3 * (27 * q + n) + 2] = la * lb * ce_dl2(nc, xc);
+    }
+    for (int v = 0; v < 8; ++v)
+      t.S1[8 * q + v] = ce_l1(v & 1, xa) * ce_l1((v >> 1) & 1, xb) * ce_l1(v >> 2, xc);
+  }
+  return t;
+}
+__constant__ RefTables cRef = make_ref_tables();
+
+// Node-group pairs (A <= B) of the 9 groups of 3 lexicographic nodes.
+constexpr int kGroupPairs = 45;
+__constant__ unsigned char cPairA[kGroupPairs] = {
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2,
+    2, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 7, 7, 8};
+__constant__ unsigned char cPairB[kGroupPairs] = {
+    0, 1, 2, 3, 4, 5, 6, 7, 8, 1, 2, 3, 4, 5, 6, 7, 8, 2, 3, 4, 5, 6, 7,
+    8, 3, 4, 5, 6, 7, 8, 4, 5, 6, 7, 8, 5, 6, 7, 8, 6, 7, 8, 7, 8, 8};
+
+// ---------------------------------------------------------------------------
 // NSE system: local_assemble_nse_system (:550-673) + distribute_local_to_global.
 // MODE 0 = scatter into block-CSR (colour launch), MODE 1 = dense element output.
+//
+// 256 threads (4 waves) per cell, ~31 KB LDS. The velocity-velocity block is
+// symmetric node-pair-wise (K_(b,.),(a,.) = K_(a,.),(b,.)^T), so only the 45
+// node-group pairs A <= B are summed: 135 1x3 tiles on waves 0-2, each written
+// as (a,b) and, off the diagonal groups, transposed as (b,a). Wave 3 sums the
+// 216 divergence blocks; 27 otherwise idle lanes of wave 2 the rhs nodes. The
+// average-diagonal value of the |K_ii| rule is computed up front from the 27
+// node-diagonal blocks.
+//
+// Writes are the bound (729 scattered 72-byte blocks per cell): every wave
+// stages its blocks in LDS (the gradient table is dead by then) and adds them
+// back with consecutive lanes on consecutive doubles, ~7 blocks per store
+// instruction instead of 64 scattered lanes. Scatter positions carry a
+// first-touch mark (~pos): the first cell in launch order that touches a block
+// stores instead of adding, so the matrices need no zero fill.
+constexpr int kNseThreads = 256;
+constexpr int kNseTiles = 3 * kGroupPairs;   // 135
+constexpr int kRhsLane0 = 160;               // wave 2 lanes 32..58: rhs nodes
+constexpr int kNoBlock = -2147483647 - 1;    // INT_MIN: lane offers no block
+
 struct NseSmem {
   double X[81], U[81], T[8];
   Geo geo;
-  double D[27 * 27 * 3];   // [q][n][d] physical gradients
+  double D[27 * 27 * 3];   // [q][n][d] reference, then physical gradients
   double S[27 * 27];       // [q][n] shape values
+  double W1[27 * 8];       // [q][v] JxW * Q1 value
   double F[27 * 3];        // JxW * rhs integrand (velocity part) per q
   double diag[27];         // sum_c |K_(a,c),(a,c)| per node (average-diagonal rule)
   int node[27];
   int pdof[8];
+  int spos[kNseThreads];   // write staging: destination block per lane
 };
 
+// Wave-cooperative block scatter: every lane offers NB doubles for block pos
+// (pos >= 0: add; ~pos: first touch, store; kNoBlock: nothing). The wave
+// writes them back with consecutive lanes on consecutive doubles.
+template <int NB>
+__device__ inline void wave_scatter(double* __restrict__ base, const double* v, int pos,
+                                    double* stage, int* spos, int lane) {
+#pragma unroll
+  for (int i = 0; i < NB; ++i) stage[NB * lane + i] = v[i];
+  spos[lane] = pos;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int e = 64 * j + lane;
+    const int blk = e / NB, comp = e - blk * NB;
+    const int p = spos[blk];
+    const double x = stage[e];
+    if (p >= 0)
+      base[NB * size_t(p) + comp] += x;
+    else if (p != kNoBlock)
+      base[NB * size_t(~p) + comp] = x;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Sum of the velocity-velocity 3x3 blocks (a, b0..b0+2) over the 27 points:
+// K_(a,c),(b,c') = delta_cc' (M + dt/Re L) + dt/Re Q_{c'c}   (2 eps:eps / 2)
+__device__ inline void nse_tile(const NseSmem& sh, const PhysicsDev& ph, int a, int b0,
+                                double blk[3][9]) {
+  double m[3] = {0, 0, 0}, Q[3][9];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Q[t][i] = 0;
+#pragma unroll 1
+  for (int q = 0; q < 27; ++q) {
+    const double w = sh.geo.JxW[q];
+    const double* Da = &sh.D[3 * (27 * q + a)];
+    const double da0 = w * Da[0], da1 = w * Da[1], da2 = w * Da[2];
+    const double sa = w * sh.S[27 * q + a];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const double* Db = &sh.D[3 * (27 * q + b0 + t)];
+      const double db0 = Db[0], db1 = Db[1], db2 = Db[2];
+      m[t] += sa * sh.S[27 * q + b0 + t];
+      Q[t][0] += da0 * db0; Q[t][1] += da0 * db1; Q[t][2] += da0 * db2;
+      Q[t][3] += da1 * db0; Q[t][4] += da1 * db1; Q[t][5] += da1 * db2;
+      Q[t][6] += da2 * db0; Q[t][7] += da2 * db1; Q[t][8] += da2 * db2;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const double L = Q[t][0] + Q[t][4] + Q[t][8];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int cp = 0; cp < 3; ++cp)
+        blk[t][3 * c + cp] = (c == cp ? m[t] + ph.nu_sys * L : 0.0) + ph.nu_sys * Q[t][3 * cp + c];
+  }
+}
+
+// B^T block of velocity node an and pressure vertex v: -sum_q JxW phi_p div phi_u
+__device__ inline void nse_div(const NseSmem& sh, int an, int v, double bt[3]) {
+  bt[0] = bt[1] = bt[2] = 0;
+#pragma unroll 1
+  for (int q = 0; q < 27; ++q) {
+    const double wp = sh.W1[8 * q + v];
+    const double* Da = &sh.D[3 * (27 * q + an)];
+    bt[0] -= Da[0] * wp; bt[1] -= Da[1] * wp; bt[2] -= Da[2] * wp;
+  }
+}
+
+__device__ inline void nse_rhs_node(const NseSmem& sh, int an, double fa[3]) {
+  fa[0] = fa[1] = fa[2] = 0;
+#pragma unroll 1
+  for (int q = 0; q < 27; ++q) {
+    const double s = sh.S[27 * q + an];
+    fa[0] += s * sh.F[3 * q]; fa[1] += s * sh.F[3 * q + 1]; fa[2] += s * sh.F[3 * q + 2];
+  }
+}
+
 template <int MODE>
-__global__ __launch_bounds__(256) void k_nse_system(CellData cd, ScatterMaps sm,
-                                                    const int32_t* __restrict__ cells, int first,
-                                                    const double* __restrict__ u_old,
-                                                    const double* __restrict__ T_old,
-                                                    PhysicsDev ph, NseOut out) {
+__global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, ScatterMaps sm,
+                                                            const int32_t* __restrict__ cells,
+                                                            int first,
+                                                            const double* __restrict__ u_old,
+                                                            const double* __restrict__ T_old,
+                                                            PhysicsDev ph, NseOut out) {
   __shared__ NseSmem sh;
   const int tid = threadIdx.x;
   const int cell = MODE == 0 ? cells[blockIdx.x] : first + blockIdx.x;
@@ -177,22 +327,79 @@ __global__ __launch_bounds__(256) void k_nse_system(CellData cd, ScatterMaps sm,
       sh.X[3 * tid + d] = cd.xyz[3 * size_t(n) + d];
       sh.U[3 * tid + d] = u_old[3 * size_t(n) + d];
     }
-  } else if (tid >= 32 && tid < 40) {
-    const int v = tid - 32;
+  } else if (tid >= 64 && tid < 72) {
+    const int v = tid - 64;
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
     sh.T[v] = T_old[cd.cell_T[8 * size_t(cell) + v]];
   }
-  for (int i = tid; i < 729; i += 256) sh.S[i] = q2_value(i / 27, i % 27);
-  __syncthreads();
-  if (tid < 27) cell_geometry(sh.X, sh.geo, tid);
-  __syncthreads();
-  for (int i = tid; i < 729; i += 256) q2_grad(sh.geo, i / 27, i % 27, &sh.D[3 * i]);
+  for (int i = tid; i < 729; i += kNseThreads) sh.S[i] = cRef.S2[i];
+  for (int i = tid; i < 3 * 729; i += kNseThreads) sh.D[i] = cRef.G2[i];
   __syncthreads();
 
-  // Right-hand-side integrand per quadrature point (:593-650, 655-669).
+  // Q2 isoparametric mapping: J[i][e] = sum_n X_n,i dN_n/dxi_e, thread (q, i)
+  if (tid < 81) {
+    const int q = tid / 3, i = tid % 3;
+    double J0 = 0, J1 = 0, J2 = 0, x = 0;
+#pragma unroll 1
+    for (int n = 0; n < 27; ++n) {
+      const double Xi = sh.X[3 * n + i];
+      const double* G = &sh.D[3 * (27 * q + n)];
+      x += Xi * sh.S[27 * q + n];
+      J0 += Xi * G[0];
+      J1 += Xi * G[1];
+      J2 += Xi * G[2];
+    }
+    sh.geo.Ji[9 * q + 3 * i + 0] = J0;
+    sh.geo.Ji[9 * q + 3 * i + 1] = J1;
+    sh.geo.Ji[9 * q + 3 * i + 2] = J2;
+    sh.geo.xq[3 * q + i] = x;
+  }
+  __syncthreads();
+  double Jinv[9], jxw = 0;
+  if (tid < 27) {
+    const int q = tid;
+    double J[3][3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) J[k / 3][k % 3] = sh.geo.Ji[9 * q + k];
+    const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+    const double c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+    const double c02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+    const double det = J[0][0] * c00 + J[0][1] * c01 + J[0][2] * c02;
+    const double id = 1.0 / det;
+    Jinv[0] = c00 * id;
+    Jinv[1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) * id;
+    Jinv[2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) * id;
+    Jinv[3] = c01 * id;
+    Jinv[4] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) * id;
+    Jinv[5] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) * id;
+    Jinv[6] = c02 * id;
+    Jinv[7] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) * id;
+    Jinv[8] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) * id;
+    jxw = det * cW[q % 3] * cW[(q / 3) % 3] * cW[q / 9];
+  }
+  __syncthreads();   // all J reads done before Ji overwrites them
+  if (tid < 27) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) sh.geo.Ji[9 * tid + k] = Jinv[k];
+    sh.geo.JxW[tid] = jxw;
+  }
+  __syncthreads();
+  // physical gradients in place: grad_d = sum_e dN/dxi_e Ji[e][d]
+  for (int i = tid; i < 729; i += kNseThreads) {
+    const double* Ji = &sh.geo.Ji[9 * (i / 27)];
+    double* g = &sh.D[3 * i];
+    const double r0 = g[0], r1 = g[1], r2 = g[2];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g[d] = r0 * Ji[d] + r1 * Ji[3 + d] + r2 * Ji[6 + d];
+  }
+  for (int i = tid; i < 216; i += kNseThreads) sh.W1[i] = sh.geo.JxW[i / 8] * cRef.S1[i];
+  __syncthreads();
+
   if (want_rhs && tid < 27) {
+    // Right-hand-side integrand per quadrature point (:593-650, 655-669).
     const int q = tid;
     double u[3] = {0, 0, 0}, G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll 1
     for (int n = 0; n < 27; ++n) {
       const double s = sh.S[27 * q + n];
       const double* Dn = &sh.D[3 * (27 * q + n)];
@@ -207,7 +414,7 @@ __global__ __launch_bounds__(256) void k_nse_system(CellData cd, ScatterMaps sm,
     }
     double T = 0;
 #pragma unroll
-    for (int v = 0; v < 8; ++v) T += sh.T[v] * q1_value(q, v);
+    for (int v = 0; v < 8; ++v) T += sh.T[v] * cRef.S1[8 * q + v];
     const double rho = 1 - ph.beta * (T - ph.T_ref);            // density_scaling
     double grav[3];
     if (ph.cuboid) {
@@ -229,164 +436,180 @@ __global__ __launch_bounds__(256) void k_nse_system(CellData cd, ScatterMaps sm,
       sh.F[3 * q + c] = (u[c] + ph.dt * rho * (ph.grav_scale * grav[c]) - ph.dt * adv -
                          ph.dt * (2 * cxu[c])) * w;
     }
-  }
-
-  // Velocity-velocity node blocks: 1x3 register tiles over (a, b0..b0+2).
-  double blk[3][9];
-  int a = 0, b0 = 0;
-  if (want_matrix && tid < 243) {
-    a = tid / 9;
-    b0 = 3 * (tid % 9);
-    double m[3] = {0, 0, 0}, Q[3][9];
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int i = 0; i < 9; ++i) Q[t][i] = 0;
+  } else if (MODE == 0 && want_matrix && tid >= 64 && tid < 91) {
+    // node-diagonal blocks for the |K_ii| / average-diagonal rule
+    const int a = tid - 64;
+    double msum = 0, g2[3] = {0, 0, 0};
+#pragma unroll 1
     for (int q = 0; q < 27; ++q) {
       const double w = sh.geo.JxW[q];
       const double* Da = &sh.D[3 * (27 * q + a)];
-      const double da0 = w * Da[0], da1 = w * Da[1], da2 = w * Da[2];
-      const double sa = w * sh.S[27 * q + a];
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const double* Db = &sh.D[3 * (27 * q + b0 + t)];
-        const double db0 = Db[0], db1 = Db[1], db2 = Db[2];
-        m[t] += sa * sh.S[27 * q + b0 + t];
-        Q[t][0] += da0 * db0; Q[t][1] += da0 * db1; Q[t][2] += da0 * db2;
-        Q[t][3] += da1 * db0; Q[t][4] += da1 * db1; Q[t][5] += da1 * db2;
-        Q[t][6] += da2 * db0; Q[t][7] += da2 * db1; Q[t][8] += da2 * db2;
-      }
+      const double sa = sh.S[27 * q + a];
+      msum += w * sa * sa;
+      g2[0] += w * Da[0] * Da[0];
+      g2[1] += w * Da[1] * Da[1];
+      g2[2] += w * Da[2] * Da[2];
     }
-    // K_(a,c),(b,c') = delta_cc' (M + dt/Re L) + dt/Re Q_{c'c}   (2 eps:eps / 2)
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const double L = Q[t][0] + Q[t][4] + Q[t][8];
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int cp = 0; cp < 3; ++cp)
-          blk[t][3 * c + cp] = (c == cp ? m[t] + ph.nu_sys * L : 0.0) + ph.nu_sys * Q[t][3 * cp + c];
-      if (b0 + t == a) sh.diag[a] = fabs(blk[t][0]) + fabs(blk[t][4]) + fabs(blk[t][8]);
-    }
+    const double L = g2[0] + g2[1] + g2[2];
+    sh.diag[a] = fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[0]) +
+                 fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[1]) +
+                 fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[2]);
   }
   __syncthreads();
 
+  constexpr int kAux = kNseThreads - kNseTiles;  // threads for B^T/B and rhs in MODE 1
   if (MODE == 1) {
     double* K = out.elemK + size_t(blockIdx.x) * 89 * 89;
     double* f = out.elemF + size_t(blockIdx.x) * 89;
-    if (tid < 243) {
+    if (tid < kNseTiles) {
+      const int A = cPairA[tid / 3], B = cPairB[tid / 3];
+      const int a = 3 * A + tid % 3, b0 = 3 * B;
+      double blk[3][9];
+      nse_tile(sh, ph, a, b0, blk);
 #pragma unroll
-      for (int t = 0; t < 3; ++t)
+      for (int tt = 0; tt < 3; ++tt)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
 #pragma unroll
-          for (int cp = 0; cp < 3; ++cp)
-            K[89 * fesys_velocity(a, c) + fesys_velocity(b0 + t, cp)] = blk[t][3 * c + cp];
-    }
-    if (tid < 216) {
-      const int an = tid / 8, v = tid % 8;
-      double bt[3] = {0, 0, 0};
-      for (int q = 0; q < 27; ++q) {
-        const double wp = sh.geo.JxW[q] * q1_value(q, v);
-        const double* Da = &sh.D[3 * (27 * q + an)];
-        bt[0] -= Da[0] * wp; bt[1] -= Da[1] * wp; bt[2] -= Da[2] * wp;
-      }
+          for (int cp = 0; cp < 3; ++cp) {
+            const int ia = fesys_velocity(a, c), ib = fesys_velocity(b0 + tt, cp);
+            K[89 * ia + ib] = blk[tt][3 * c + cp];
+            if (A != B) K[89 * ib + ia] = blk[tt][3 * c + cp];
+          }
+    } else {
+      for (int t = tid - kNseTiles; t < 216 + 27 + 8; t += kAux) {
+        if (t < 216) {
+          const int an = t / 8, v = t % 8;
+          double bt[3];
+          nse_div(sh, an, v, bt);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        K[89 * fesys_velocity(an, c) + 4 * v + 3] = bt[c];
-        K[89 * (4 * v + 3) + fesys_velocity(an, c)] = bt[c];
-      }
-    } else if (tid < 243) {
-      const int an = tid - 216;
-      double fa[3] = {0, 0, 0};
-      for (int q = 0; q < 27; ++q) {
-        const double s = sh.S[27 * q + an];
-        fa[0] += s * sh.F[3 * q]; fa[1] += s * sh.F[3 * q + 1]; fa[2] += s * sh.F[3 * q + 2];
-      }
+          for (int c = 0; c < 3; ++c) {
+            K[89 * fesys_velocity(an, c) + 4 * v + 3] = bt[c];
+            K[89 * (4 * v + 3) + fesys_velocity(an, c)] = bt[c];
+          }
+        } else if (t < 243) {
+          const int an = t - 216;
+          double fa[3];
+          nse_rhs_node(sh, an, fa);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) f[fesys_velocity(an, c)] = fa[c];
-    } else if (tid < 251) {
-      const int v = tid - 243;  // pressure rows of f and the empty p-p block
-      f[4 * v + 3] = 0.0;
-      for (int w = 0; w < 8; ++w) K[89 * (4 * v + 3) + 4 * w + 3] = 0.0;
+          for (int c = 0; c < 3; ++c) f[fesys_velocity(an, c)] = fa[c];
+        } else {
+          const int v = t - 243;  // pressure rows of f and the empty p-p block
+          f[4 * v + 3] = 0.0;
+          for (int w = 0; w < 8; ++w) K[89 * (4 * v + 3) + 4 * w + 3] = 0.0;
+        }
+      }
     }
     return;
   }
 
-  // ---- MODE 0: condensation + colour-exclusive read-modify-write -----------
-  double avg = 0;
-  if (want_matrix) {
-    for (int n = 0; n < 27; ++n) avg += sh.diag[n];
-    avg /= 89.0;  // pressure diagonals of the local matrix are 0
-  }
-  if (want_matrix && tid < 243) {
-    const NodeConstraint ca = cd.vcon[sh.node[a]];
-    double Ca[3][3];
-    condensation(ca, Ca);
+  // ---- MODE 0: condensation + colour-exclusive scatter ----------------------
+  const int wave = tid >> 6, lane = tid & 63;
+  double R[3][9];          // waves 0-2: condensed blocks (a, b0+tt); wave 3: B^T rows
+  int pos[4], posT[4];     // destinations of R and of its transposes (wave 3: B^T, B)
+  double fa[3] = {0, 0, 0};
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int b = b0 + t;
-      const NodeConstraint cb = cd.vcon[sh.node[b]];
-      double Cb[3][3];
-      condensation(cb, Cb);
-      double KC[3][3], R[9];
+  for (int k = 0; k < 4; ++k) pos[k] = kNoBlock;
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+  for (int k = 0; k < 4; ++k) posT[k] = kNoBlock;
+  const bool rhs_lane = want_rhs && tid >= kRhsLane0 && tid < kRhsLane0 + 27;
+  if (wave < 3) {
+    if (want_matrix && tid < kNseTiles) {
+      const int A = cPairA[tid / 3], B = cPairB[tid / 3];
+      const int a = 3 * A + tid % 3, b0 = 3 * B;
+      double blk[3][9];
+      nse_tile(sh, ph, a, b0, blk);
+      const NodeConstraint ca = cd.vcon[sh.node[a]];
+      double Ca[3][3];
+      condensation(ca, Ca);
+      const int32_t* posA = sm.posA + 729 * size_t(cell);
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          KC[i][j] = blk[t][3 * i] * Cb[0][j] + blk[t][3 * i + 1] * Cb[1][j] + blk[t][3 * i + 2] * Cb[2][j];
+      for (int tt = 0; tt < 3; ++tt) {
+        const int b = b0 + tt;
+        double Cb[3][3];
+        condensation(cd.vcon[sh.node[b]], Cb);
+        double KC[3][3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          R[3 * i + j] = Ca[0][i] * KC[0][j] + Ca[1][i] * KC[1][j] + Ca[2][i] * KC[2][j];
-      if (b == a && ca.type != 0) {
-        // constrained local dofs: global diagonal += |K_ii| (average if 0)
+          for (int j = 0; j < 3; ++j)
+            KC[i][j] = blk[tt][3 * i] * Cb[0][j] + blk[tt][3 * i + 1] * Cb[1][j] +
+                       blk[tt][3 * i + 2] * Cb[2][j];
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (ca.type == 1 || c == ca.k) {
-            const double kii = fabs(blk[t][4 * c]);
-            R[4 * c] += kii != 0.0 ? kii : avg;
-          }
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            R[tt][3 * i + j] = Ca[0][i] * KC[0][j] + Ca[1][i] * KC[1][j] + Ca[2][i] * KC[2][j];
+        if (b == a && ca.type != 0) {
+          // constrained local dofs: global diagonal += |K_ii| (average if 0)
+          double avg = 0;
+          for (int n = 0; n < 27; ++n) avg += sh.diag[n];
+          avg /= 89.0;  // pressure diagonals of the local matrix are 0
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            if (ca.type == 1 || c == ca.k) {
+              const double kii = fabs(blk[tt][4 * c]);
+              R[tt][4 * c] += kii != 0.0 ? kii : avg;
+            }
+        }
+        pos[tt] = posA[27 * a + b];
+        if (A != B) posT[tt] = posA[27 * b + a];
       }
-      double* dst = out.A + 9 * size_t(sm.posA[729 * size_t(cell) + 27 * a + b]);
+    } else if (rhs_lane) {
+      nse_rhs_node(sh, tid - kRhsLane0, fa);
+    }
+  } else if (want_matrix) {
+    // wave 3: B^T blocks (an, v), 4 rounds of 64
 #pragma unroll
-      for (int i = 0; i < 9; ++i) dst[i] += R[i];
+    for (int k = 0; k < 4; ++k) {
+      const int t = lane + 64 * k;
+      if (t < 216) {
+        const int an = t / 8, v = t % 8;
+        double bt[3];
+        nse_div(sh, an, v, bt);
+        double Ca[3][3];
+        condensation(cd.vcon[sh.node[an]], Ca);
+        double* r = &R[0][0] + 3 * k;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) r[j] = Ca[0][j] * bt[0] + Ca[1][j] * bt[1] + Ca[2][j] * bt[2];
+        pos[k] = sm.posBt[216 * size_t(cell) + 8 * an + v];
+        posT[k] = sm.posB[216 * size_t(cell) + 27 * v + an];
+      }
     }
   }
-  if (want_matrix && tid < 216) {
-    const int an = tid / 8, v = tid % 8;
-    double bt[3] = {0, 0, 0};
-    for (int q = 0; q < 27; ++q) {
-      const double wp = sh.geo.JxW[q] * q1_value(q, v);
-      const double* Da = &sh.D[3 * (27 * q + an)];
-      bt[0] -= Da[0] * wp; bt[1] -= Da[1] * wp; bt[2] -= Da[2] * wp;
-    }
-    double Ca[3][3];
-    condensation(cd.vcon[sh.node[an]], Ca);
-    double r[3];
+  __syncthreads();   // gradient table dead: reuse it as the write staging area
+  double* stage = sh.D + 576 * wave;
+  int* spos = sh.spos + 64 * wave;
+  if (wave < 3) {
+    if (want_matrix) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) r[j] = Ca[0][j] * bt[0] + Ca[1][j] * bt[1] + Ca[2][j] * bt[2];
-    double* dbt = out.Bt + 3 * size_t(sm.posBt[216 * size_t(cell) + 8 * an + v]);
-    double* db = out.B + 3 * size_t(sm.posB[216 * size_t(cell) + 27 * v + an]);
+      for (int tt = 0; tt < 3; ++tt) wave_scatter<9>(out.A, R[tt], pos[tt], stage, spos, lane);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      dbt[j] += r[j];
-      db[j] += r[j];
-    }
-  }
-  if (want_rhs && tid >= 216 && tid < 243) {
-    const int an = tid - 216;
-    double fa[3] = {0, 0, 0};
-    for (int q = 0; q < 27; ++q) {
-      const double s = sh.S[27 * q + an];
-      fa[0] += s * sh.F[3 * q]; fa[1] += s * sh.F[3 * q + 1]; fa[2] += s * sh.F[3 * q + 2];
-    }
-    double Ca[3][3];
-    condensation(cd.vcon[sh.node[an]], Ca);
-    double* dst = out.rhs + 3 * size_t(sh.node[an]);
+      for (int tt = 0; tt < 3; ++tt) {
+        double RT[9];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[tt][3 * j + i];
+        wave_scatter<9>(out.A, RT, posT[tt], stage, spos, lane);
+      }
+    }
+    if (rhs_lane) {
+      const int an = tid - kRhsLane0;
+      double Ca[3][3];
+      condensation(cd.vcon[sh.node[an]], Ca);
+      double* dst = out.rhs + 3 * size_t(sh.node[an]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+    }
+  } else if (want_matrix) {
+    // B^T row (an, v) and B row (v, an) hold the same 3 values
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double* r = &R[0][0] + 3 * k;
+      wave_scatter<3>(out.Bt, r, pos[k], stage, spos, lane);
+      wave_scatter<3>(out.B, r, posT[k], stage, spos, lane);
+    }
   }
 }
 
@@ -585,6 +808,36 @@ __global__ void k_scatter_maps(CellData cd, const int32_t* A_ptr, const int32_t*
   }
 }
 
+// First-touch marks for one colour: an entry whose block no earlier colour
+// touched is re-encoded as ~pos. Within a colour no two cells share a node, so
+// every block is touched at most once per launch.
+__global__ __launch_bounds__(256) void k_first_touch(const int32_t* __restrict__ cells, int per_cell,
+                                                     int32_t* __restrict__ pos,
+                                                     uint8_t* __restrict__ touched,
+                                                     unsigned long long* __restrict__ count) {
+  __shared__ unsigned int n_first;
+  if (threadIdx.x == 0) n_first = 0;
+  __syncthreads();
+  int32_t* pc = pos + size_t(per_cell) * cells[blockIdx.x];
+  unsigned int mine = 0;
+  for (int i = threadIdx.x; i < per_cell; i += blockDim.x) {
+    const int32_t p = pc[i];
+    if (p >= 0 && !touched[p]) {
+      touched[p] = 1;
+      pc[i] = ~p;
+      ++mine;
+    }
+  }
+  if (mine) atomicAdd(&n_first, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && n_first) atomicAdd(count, (unsigned long long)n_first);
+}
+
+__global__ void k_clear_first_touch(size_t n, int32_t* __restrict__ pos) {
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+    if (pos[i] < 0) pos[i] = ~pos[i];
+}
+
 // S_pq = sum_n sum_c B[p][n][c] d[3n+c] B^T[n][q][c]; one 64-lane workgroup
 // per pressure row. The node loop is sequential and the lanes of one node
 // write distinct q, so every entry is summed in the same (node) order.
@@ -647,8 +900,8 @@ void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t*
                        const double* u_old, const double* T_old, const PhysicsDev& ph,
                        const NseOut& out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_nse_system<0>, dim3(n), dim3(256), 0, s, cd, sm, cells, 0, u_old, T_old, ph,
-                     out);
+  hipLaunchKernelGGL((k_nse_system<0>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+                     u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -659,7 +912,7 @@ void launch_nse_system_elements(const CellData& cd, int first, int n, const doub
   NseOut out{};
   out.elemK = K;
   out.elemF = f;
-  hipLaunchKernelGGL(k_nse_system<1>, dim3(n), dim3(256), 0, s, cd, ScatterMaps{}, nullptr, first,
+  hipLaunchKernelGGL((k_nse_system<1>), dim3(n), dim3(kNseThreads), 0, s, cd, ScatterMaps{}, nullptr, first,
                      u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
@@ -694,6 +947,33 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
   hipLaunchKernelGGL(k_scatter_maps, dim3(cd.n_cells), dim3(256), 0, s, cd, A_ptr, A_col, Bt_ptr,
                      Bt_col, B_ptr, B_col, T_ptr, T_col, posA, posBt, posB, posT);
   DCP_HIP_CHECK(hipGetLastError());
+}
+
+bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s) {
+  uint8_t* touched = nullptr;
+  unsigned long long* count = nullptr;
+  DCP_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&touched), nnz, s));
+  DCP_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&count), sizeof(unsigned long long), s));
+  DCP_HIP_CHECK(hipMemsetAsync(touched, 0, nnz, s));
+  DCP_HIP_CHECK(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
+  for (size_t k = 0; k + 1 < color_ptr.size(); ++k) {
+    const int n = color_ptr[k + 1] - color_ptr[k];
+    if (n <= 0) continue;
+    hipLaunchKernelGGL(k_first_touch, dim3(n), dim3(256), 0, s, color_cells + color_ptr[k],
+                       per_cell, pos, touched, count);
+    DCP_HIP_CHECK(hipGetLastError());
+  }
+  unsigned long long h = 0;
+  DCP_HIP_CHECK(hipMemcpyAsync(&h, count, sizeof(h), hipMemcpyDeviceToHost, s));
+  DCP_HIP_CHECK(hipStreamSynchronize(s));
+  DCP_HIP_CHECK(hipFree(touched));
+  DCP_HIP_CHECK(hipFree(count));
+  if (h == nnz) return true;
+  // some block is never touched by a cell: keep plain positions (zero fill needed)
+  hipLaunchKernelGGL(k_clear_first_touch, dim3(1024), dim3(256), 0, s, size_t(per_cell) * n_cells, pos);
+  DCP_HIP_CHECK(hipGetLastError());
+  return false;
 }
 
 }  // namespace dcp

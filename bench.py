@@ -29,6 +29,21 @@ sys.path.insert(0, os.path.join(ROOT, "3d-dycoreplanet_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
+# roofline kernel, per (refine, schur mode): HBM bytes per launch
+PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_explicit_r5.json", "k_spmv_bsr<1, 1, 32>")}
+
+
+def pmc_traffic(refine, mode):
+    """HBM bytes per launch of the roofline kernel from the committed PMC
+    summary of the same workload, or None when none was collected."""
+    ent = PMC_SUMMARIES.get((refine, mode))
+    if ent is None or not os.path.exists(os.path.join(ROOT, ent[0])):
+        return None
+    with open(os.path.join(ROOT, ent[0])) as f:
+        tb = json.load(f)["traffic_bytes"]
+    hits = [v for k, v in tb.items() if ent[1] in k]
+    return hits[0] if hits else None
 
 
 def parse():
@@ -201,7 +216,8 @@ def main():
         "schur_mode": args.schur,
         "roofline": {"kernel": kernel, "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc_traffic(args.refine, args.schur),
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -92,6 +92,10 @@ def test_assembled_system(setup, state):
     assert abs(B - Bt.T).max() == 0.0
     A = Ag[:m.n_u, :m.n_u]
     assert abs(A - A.T).max() / abs(A).max() < 1e-13
+    # re-assembly over the first-touch scatter (store, then add) is idempotent
+    ctx.assemble_nse_system()
+    Ag2 = csr(*ctx.nse_matrix_csr(), n)
+    assert abs(Ag2 - Ag).max() == 0.0
 
 
 def test_preconditioner_diagonals(setup):
