@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Generates the regression fixtures in tests/golden/ from the CPU oracle.
+
+These vectors are oracle outputs (parity with deal.II is unpinned: the
+reference cannot be built in this image and ships no golden data, see
+DESIGN.md section 3). They freeze the restatement so that any change to the
+oracle or to the host mesh/DoF setup shows up as a diff, and give the GPU
+tests a fixed target that does not need the oracle at run time.
+
+Cases (classic shell physics, data/aqua_planet_shell_test_3d-classic.prm):
+  shell_r1.npz  refine 1 (48 cells): cell 0..3 element matrices/rhs for the
+                physical state (u=0, T0) and a seeded random state, the
+                assembled nse rhs, preconditioner diagonals, one full time
+                step's NSE solution / iteration counts, temperature solution.
+usage: python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (os.path.join(ROOT, "3d-dycoreplanet_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import dcp  # noqa: E402  (host mesh/prm helpers only: no device calls)
+import oracle_py  # noqa: E402
+
+SEED = 20261015
+
+
+def states(m):
+    rng = np.random.default_rng(SEED)
+    u_r = rng.uniform(-1, 1, m.n_u + m.n_p)
+    T_r = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+    return {"physical": (np.zeros(m.n_u + m.n_p), m.T0.copy()), "random": (u_r, T_r)}
+
+
+def make(refine=1):
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    out = {"n": np.array([m.n_cells, m.n_u, m.n_p, m.n_T], np.int64),
+           "cell_nse_dofs": m.cell_nse_dofs.astype(np.int32),
+           "cell_T_dofs": m.cell_T_dofs.astype(np.int32)}
+    for name, (u, T) in states(m).items():
+        K = np.zeros((4, 89, 89))
+        f = np.zeros((4, 89))
+        for c in range(4):
+            K[c], f[c] = oracle_py.cell_nse_system(ph, m.cell_geometry[c], u[m.cell_nse_dofs[c]],
+                                                   T[m.cell_T_dofs[c]])
+        out[f"{name}_K"], out[f"{name}_f"] = K, f
+        orc = oracle_py.Model(ph, m)
+        orc.assemble_nse_system(u, T)
+        out[f"{name}_rhs"] = orc.nse_rhs()
+        out[f"{name}_u"], out[f"{name}_T"] = u, T
+    # one full time step from the physical state (run(), boussinesq_model.tpp:1867-1905)
+    u, T = states(m)["physical"]
+    orc = oracle_py.Model(ph, m)
+    orc.assemble_nse_system(u, T)
+    orc.build_nse_preconditioner()
+    orc.assemble_temperature_matrix()
+    orc.assemble_temperature_rhs(T, u)
+    a_diag, p_diag = orc.precond_diagonals()
+    rc, x, outer, inner = orc.solve_nse(u)
+    rcT, Tn, itT = orc.solve_temperature(T)
+    out.update(A_diag=a_diag, Mp_diag=p_diag, T_rhs=orc.T_rhs(), nse_solution=x,
+               T_solution=Tn, iters=np.array([rc, outer, inner, rcT, itT], np.int64))
+    return out
+
+
+if __name__ == "__main__":
+    np.savez_compressed(os.path.join(HERE, "shell_r1.npz"), **make(1))
+    print("wrote", os.path.join(HERE, "shell_r1.npz"))

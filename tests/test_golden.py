@@ -1,0 +1,103 @@
+"""Regression fixtures (tests/golden/shell_r1.npz, made by
+tests/golden/make_golden.py from the oracle; parity with deal.II unpinned,
+DESIGN.md section 3).
+
+CPU: the host mesh/DoF setup and the oracle still reproduce the fixture.
+GPU: the HIP path matches the fixture through the C ABI, without the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+import dcp
+import oracle_py
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shell_r1.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLD) as d:
+        return {k: d[k] for k in d.files}
+
+
+@pytest.fixture(scope="module")
+def mesh():
+    return dcp.HostMesh(refine=1)
+
+
+def rel(a, b):
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+
+
+def test_dof_indexing_bit_exact(gold, mesh):
+    assert list(gold["n"]) == [mesh.n_cells, mesh.n_u, mesh.n_p, mesh.n_T]
+    assert np.array_equal(gold["cell_nse_dofs"], mesh.cell_nse_dofs)
+    assert np.array_equal(gold["cell_T_dofs"], mesh.cell_T_dofs)
+    assert np.array_equal(gold["physical_T"], mesh.T0)
+
+
+@pytest.mark.parametrize("state", ["physical", "random"])
+def test_oracle_reproduces_fixture(gold, mesh, state):
+    ph = dcp.classic_physics()
+    u, T = gold[f"{state}_u"], gold[f"{state}_T"]
+    for c in range(4):
+        K, f = oracle_py.cell_nse_system(ph, mesh.cell_geometry[c], u[mesh.cell_nse_dofs[c]],
+                                         T[mesh.cell_T_dofs[c]])
+        assert rel(K, gold[f"{state}_K"][c]) < 1e-14
+        assert rel(f, gold[f"{state}_f"][c]) < 1e-14
+    orc = oracle_py.Model(ph, mesh)
+    orc.assemble_nse_system(u, T)
+    assert rel(orc.nse_rhs(), gold[f"{state}_rhs"]) < 1e-14
+
+
+def test_oracle_time_step_reproduces_fixture(gold, mesh):
+    ph = dcp.classic_physics()
+    u, T = gold["physical_u"], gold["physical_T"]
+    orc = oracle_py.Model(ph, mesh)
+    orc.assemble_nse_system(u, T)
+    orc.build_nse_preconditioner()
+    orc.assemble_temperature_matrix()
+    orc.assemble_temperature_rhs(T, u)
+    rc, x, outer, inner = orc.solve_nse(u)
+    rcT, Tn, itT = orc.solve_temperature(T)
+    assert [rc, outer, inner, rcT, itT] == list(gold["iters"])
+    assert np.linalg.norm(x - gold["nse_solution"]) <= 1e-13 * np.linalg.norm(gold["nse_solution"])
+    assert rel(Tn, gold["T_solution"]) < 1e-13
+
+
+@pytest.mark.gpu
+def test_gpu_matches_fixture(gold, mesh):
+    ph = dcp.classic_physics()
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh(mesh)
+    for state in ("physical", "random"):
+        u, T = gold[f"{state}_u"], gold[f"{state}_T"]
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+        ctx.set_state(dcp.OLD_T_SOLUTION, T)
+        K, f = ctx.cell_nse_system(0, 4)
+        assert rel(K, gold[f"{state}_K"]) < 1e-12
+        assert rel(f, gold[f"{state}_f"]) < 1e-12
+        ctx.assemble_nse_system()
+        assert rel(ctx.get_state(dcp.NSE_RHS), gold[f"{state}_rhs"]) < 1e-12
+    u, T = gold["physical_u"], gold["physical_T"]
+    for fld, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                   (dcp.T_SOLUTION, T)):
+        ctx.set_state(fld, v)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    a_diag, p_diag = ctx.precond_diagonals()
+    assert rel(a_diag, gold["A_diag"]) < 1e-12 and rel(p_diag, gold["Mp_diag"]) < 1e-12
+    assert rel(ctx.get_state(dcp.T_RHS), gold["T_rhs"]) < 1e-12
+    rc, outer, inner = ctx.solve_nse()
+    g = gold["iters"]
+    assert rc == g[0] and outer == g[1] and abs(inner - g[2]) <= 0.05 * g[2]
+    x = ctx.get_state(dcp.NSE_SOLUTION)
+    assert np.linalg.norm(x - gold["nse_solution"]) <= 1e-10 * np.linalg.norm(gold["nse_solution"])
+    rcT, itT, _ = ctx.solve_temperature()
+    assert rcT == g[3] and itT == g[4]
+    assert rel(ctx.get_state(dcp.T_SOLUTION), gold["T_solution"]) < 1e-10
+    ctx.close()
