@@ -475,7 +475,33 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.T_col.upload(Tc);
     c.S_ptr.upload(h.Sp);
     c.S_col.upload(h.Sc);
-    c.S_val.alloc(h.Sc.size());
+    {
+      // SELL-64 layout of the S pattern: slice width = longest row of the slice
+      const int n_sl = (n_p + 63) / 64;
+      std::vector<int64_t> off(size_t(n_sl) + 1, 0);
+      for (int sl = 0; sl < n_sl; ++sl) {
+        int w = 0;
+        for (int p = 64 * sl; p < std::min(n_p, 64 * sl + 64); ++p)
+          w = std::max(w, h.Sp[p + 1] - h.Sp[p]);
+        off[sl + 1] = off[sl] + 64 * int64_t(w);
+      }
+      std::vector<int32_t> scol(size_t(off[n_sl]), 0);
+      for (int sl = 0; sl < n_sl; ++sl) {
+        const int64_t w = (off[sl + 1] - off[sl]) / 64;
+        for (int i = 0; i < 64; ++i) {
+          const int p = 64 * sl + i;
+          for (int64_t k = 0; k < w; ++k) {
+            const bool real = p < n_p && k < h.Sp[p + 1] - h.Sp[p];
+            scol[off[sl] + 64 * k + i] = real ? h.Sc[h.Sp[p] + k] : (p < n_p ? p : 0);
+          }
+        }
+      }
+      c.S_sell_off.upload(off);
+      c.S_sell_col.upload(scol);
+      c.S_val.alloc(scol.size());
+      c.S_val.zero(c.stream);  // padding entries stay 0
+      c.sell_part.alloc(2 * size_t(sell_fused_blocks(n_p)));
+    }
     c.S_max_row = h.S_max_row;
     c.A_val.alloc(Ac.size() * 9);
     c.Bt_val.alloc(Btc.size() * 3);
@@ -612,8 +638,8 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
               "the explicit Schur complement needs the assembled B blocks: call "
               "dcp_assemble_nse_system first");
       form_schur_complement(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
-                            c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_val.p, c.S_max_row,
-                            c.stream);
+                            c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_sell_off.p,
+                            c.S_val.p, c.S_max_row, c.stream);
     }
     t.stop();
     c.precond_built = true;

@@ -72,7 +72,11 @@ struct Ctx {
   bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
   // explicit Schur complement S = B D_A^-1 B^T (CSR over pressure dofs)
   DBuf<int32_t> S_ptr, S_col;
+  // its values live in the SELL-64 layout of that pattern (sell_spmv)
+  DBuf<int64_t> S_sell_off;
+  DBuf<int32_t> S_sell_col;
   DBuf<double> S_val;
+  DBuf<double> sell_part;            // 2 x sell_fused_blocks(n_p) partials
   int S_max_row = 0;
   bool schur_explicit = true;
   // state

@@ -99,8 +99,6 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
                                int32_t* posA, int32_t* posBt, int32_t* posB, int32_t* posT,
                                hipStream_t s);
 
-// S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
-// contributions summed in fixed node order: deterministic).
 // Re-encode the scatter positions of the first cell (in colour launch order)
 // touching each block as ~pos; true if every one of the nnz blocks is touched
 // (then the assembly stores first and needs no zero fill), else the
@@ -108,10 +106,13 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
                       int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s);
 
+// S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
+// contributions summed in fixed node order: deterministic). sell_off != null:
+// the values are stored in the SELL-64 layout of that pattern (see sell_spmv).
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
                            const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
-                           double* S_val, int max_row, hipStream_t s);
+                           const int64_t* sell_off, double* S_val, int max_row, hipStream_t s);
 
 // ---- linalg.hip -------------------------------------------------------------
 // y (=|+=) alpha * M x for block-CSR with R x C blocks (R,C in {1,3}).
@@ -126,6 +127,21 @@ void spmv_csr(int rows, const int32_t* ptr, const int32_t* col, const double* va
 // CSR with long rows (~125 nnz, the Schur complement): 32 lanes per row
 void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const double* val,
                    const double* x, double* y, bool add, hipStream_t s);
+
+// SELL-64 SpMV: slices of 64 consecutive rows (one wave, one row per lane);
+// inside a slice entries are stored column-major (row 64s+i, entry k at
+// off[s] + 64k + i; padding: col = own row, val = 0), so every load of a wave
+// is one contiguous 512-B (values) / 256-B (columns) segment.
+//   y = M (cf * x)
+void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* val,
+               const double* x, double cf, double* y, hipStream_t s);
+// Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
+// vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
+// part1 (sell_fused_blocks(rows) of each, fixed order).
+int sell_fused_blocks(int rows);
+void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
+                     const double* x, double cf, double* xs, double* y, const double* v0,
+                     double* part0, double* part1, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):
@@ -151,6 +167,13 @@ void dot_partial(int n, const double* a, const double* b, double* partials, int 
 void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s);
+// Same step with nb_prev previous partials (e.g. from sell_spmv_fused) and an
+// optional second partial array prev2 whose fixed-order sum block 0 stores to
+// *store2.
+void chain_add_and_dot_ex(int n, double* v, const double* prev, int nb_prev, double mult,
+                          const double* x, const double* w, double* partials,
+                          double* coef_store, int nb, const double* prev2, double* store2,
+                          hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

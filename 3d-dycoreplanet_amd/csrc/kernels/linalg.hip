@@ -107,36 +107,130 @@ __global__ __launch_bounds__(kBlock) void k_add_and_dot(int n, double* v, DScal 
 }
 
 // Chained Gram-Schmidt step without a separate reduction launch: every block
-// first sums the previous step's nb partials in the same fixed order (so all
-// blocks agree bitwise), block 0 stores that coefficient, then
+// first sums the previous step's nb_prev partials in the same fixed order (so
+// all blocks agree bitwise), block 0 stores that coefficient, then
 // v += mult * coef * x and the partial dot(v, w) of this block is written.
-__global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(int n, double* v,
-                                                              const double* __restrict__ prev,
-                                                              int nb, double mult,
-                                                              const double* __restrict__ x,
-                                                              const double* w,
-                                                              double* __restrict__ partials,
-                                                              double* coef_store) {
+// The block's first kChainPrefetch elements of v, x, w are loaded before the
+// partials, so the two dependent memory latencies overlap.
+constexpr int kChainPrefetch = 4;
+__global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
+    int n, double* v, const double* __restrict__ prev, int nb_prev, double mult,
+    const double* __restrict__ x, const double* w, double* __restrict__ partials,
+    double* coef_store, const double* __restrict__ prev2, double* store2) {
   __shared__ double sm[4];
   __shared__ double coef_sh;
+  const bool self = (w == v);
+  const long stride = long(gridDim.x) * kBlock;
+  const long i0 = long(blockIdx.x) * kBlock + threadIdx.x;
+  double rv[kChainPrefetch], rx[kChainPrefetch], rw[kChainPrefetch];
+#pragma unroll
+  for (int e = 0; e < kChainPrefetch; ++e) {
+    const long i = i0 + e * stride;
+    rv[e] = rx[e] = rw[e] = 0.0;
+    if (i < n) {
+      rv[e] = v[i];
+      rx[e] = x[i];
+      if (!self) rw[e] = w[i];
+    }
+  }
   double s = 0;
-  for (int i = threadIdx.x; i < nb; i += kBlock) s += prev[i];
+  for (int i = threadIdx.x; i < nb_prev; i += kBlock) s += prev[i];
   const double tot = block_sum(s, sm);
   if (threadIdx.x == 0) {
     coef_sh = tot;
     if (blockIdx.x == 0) *coef_store = tot;
   }
   __syncthreads();
+  if (prev2) {
+    double s2 = 0;
+    for (int i = threadIdx.x; i < nb_prev; i += kBlock) s2 += prev2[i];
+    const double t2 = block_sum(s2, sm);
+    if (threadIdx.x == 0 && blockIdx.x == 0) *store2 = t2;
+    __syncthreads();
+  }
   const double cf = mult * coef_sh;
   double d = 0;
-  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+#pragma unroll
+  for (int e = 0; e < kChainPrefetch; ++e) {
+    const long i = i0 + e * stride;
+    if (i < n) {
+      const double nv = rv[e] + cf * rx[e];
+      v[i] = nv;
+      d += nv * (self ? nv : rw[e]);
+    }
+  }
+  for (long i = i0 + kChainPrefetch * stride; i < n; i += stride) {
     const double nv = v[i] + cf * x[i];
     v[i] = nv;
-    d += nv * (w == v ? nv : w[i]);
+    d += nv * (self ? nv : w[i]);
   }
-  __syncthreads();
   const double r = block_sum(d, sm);
   if (threadIdx.x == 0) partials[blockIdx.x] = r;
+}
+
+// SELL-64 SpMV (see device.h). One 256-thread workgroup per slice: lane i of
+// every wave owns row 64s+i, wave j sums the j-th quarter of the slice's
+// entry columns (4 waves per slice keep enough loads in flight: one wave per
+// slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound), then
+// wave 0 adds the 4 quarters in order (fixed summation order).
+template <bool EPI>
+__global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* __restrict__ off,
+                                                      const int32_t* __restrict__ col,
+                                                      const double* __restrict__ val,
+                                                      const double* __restrict__ x, double cf,
+                                                      double* __restrict__ xs,
+                                                      double* __restrict__ y,
+                                                      const double* __restrict__ v0,
+                                                      double* __restrict__ part0,
+                                                      double* __restrict__ part1) {
+  __shared__ double quarter[3][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long sl = blockIdx.x;
+  const long row = sl * 64 + lane;
+  const int64_t b = off[sl];
+  const int w = int((off[sl + 1] - b) >> 6);
+  const int per = (w + 3) >> 2;
+  const int k0 = wave * per, k1 = min(w, k0 + per);
+  const int32_t* cp = col + b + 64 * int64_t(k0) + lane;
+  const double* vp = val + b + 64 * int64_t(k0) + lane;
+  double acc = 0.0;
+  int k = k0;
+  for (; k + 4 <= k1; k += 4, cp += 256, vp += 256) {
+    const int c0 = cp[0], c1 = cp[64], c2 = cp[128], c3 = cp[192];
+    const double a0 = vp[0], a1 = vp[64], a2 = vp[128], a3 = vp[192];
+    const double x0 = x[c0] * cf, x1 = x[c1] * cf, x2 = x[c2] * cf, x3 = x[c3] * cf;
+    acc += a0 * x0;
+    acc += a1 * x1;
+    acc += a2 * x2;
+    acc += a3 * x3;
+  }
+  for (; k < k1; ++k, cp += 64, vp += 64) acc += vp[0] * (x[cp[0]] * cf);
+  if (wave > 0) quarter[wave - 1][lane] = acc;
+  __syncthreads();
+  if (wave > 0) return;
+  acc += quarter[0][lane];
+  acc += quarter[1][lane];
+  acc += quarter[2][lane];
+  if (!EPI) {
+    if (row < rows) y[row] = acc;
+    return;
+  }
+  double d0 = 0, d1 = 0;
+  if (row < rows) {
+    y[row] = acc;
+    if (xs) xs[row] = x[row] * cf;
+    d0 = acc * v0[row];
+    d1 = acc * acc;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    d0 += __shfl_xor(d0, o, 64);
+    d1 += __shfl_xor(d1, o, 64);
+  }
+  if (lane == 0) {
+    part0[sl] = d0;
+    part1[sl] = d1;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce_final(int nb, const double* __restrict__ partials,
@@ -364,8 +458,34 @@ void dot_partial(int n, const double* a, const double* b, double* partials, int 
 void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s) {
-  hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, n, v, prev, nb, mult, x, w,
-                     partials, coef_store);
+  chain_add_and_dot_ex(n, v, prev, nb, mult, x, w, partials, coef_store, nb, nullptr, nullptr, s);
+}
+
+void chain_add_and_dot_ex(int n, double* v, const double* prev, int nb_prev, double mult,
+                          const double* x, const double* w, double* partials,
+                          double* coef_store, int nb, const double* prev2, double* store2,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, n, v, prev, nb_prev, mult,
+                     x, w, partials, coef_store, prev2, store2);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+int sell_fused_blocks(int rows) { return int((long(rows) + 63) / 64); }
+
+void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* val,
+               const double* x, double cf, double* y, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_fused_blocks(rows)), dim3(kBlock), 0, s, rows,
+                     off, col, val, x, cf, nullptr, y, nullptr, nullptr, nullptr);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
+                     const double* x, double cf, double* xs, double* y, const double* v0,
+                     double* part0, double* part1, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL((k_sell_spmv<true>), dim3(sell_fused_blocks(rows)), dim3(kBlock), 0, s, rows,
+                     off, col, val, x, cf, xs, y, v0, part0, part1);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -38,7 +38,6 @@ struct Control {
 // Device scalar slots (c.dscal).
 constexpr int kSlotH = 0;        // 0..127: Gram-Schmidt coefficients
 constexpr int kSlotH2 = 128;     // 128..255: re-orthogonalisation pass
-constexpr int kSlotNN = 256;     // |vv|^2 after orthogonalisation
 constexpr int kSlotNStart = 257; // |vv|^2 before
 constexpr int kSlotA = 258;      // misc
 constexpr int kSlotB = 259;
@@ -218,6 +217,102 @@ State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b,
   return st;
 }
 
+// The inner Schur GMRES of block_prec on the explicit S (identity
+// preconditioner): the same deal.II SolverGMRES as gmres() above, with the
+// vector work fused so one Arnoldi step is 1 + dim launches and one readback:
+//   * S v_k is the SELL SpMV of the unscaled previous vector w times 1/|w|
+//     (bitwise the product with the scaled vector), and the same launch
+//     stores v_k = w/|w| and the partials of (S v_k).v_0 and |S v_k|^2;
+//   * the modified Gram-Schmidt chain starts from those partials.
+Timer* schur_sample(Ctx& c);
+
+State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
+                  int n_tmp) {
+  const int n = c.n_p;
+  ensure_pool(tv, n_tmp + 2, size_t(n));
+  double* p = tv[n_tmp - 1];
+  double* wbuf[2] = {tv[n_tmp], tv[n_tmp + 1]};
+  const int nbs = sell_fused_blocks(n);
+  double* part0 = c.sell_part.p;
+  double* part1 = c.sell_part.p + nbs;
+  const int nb = chain_blocks(n);
+  std::vector<std::vector<double>> H(n_tmp, std::vector<double>(n_tmp - 1, 0.0));
+  std::vector<double> gamma(n_tmp, 0.0), ci(n_tmp - 1, 0.0), si(n_tmp - 1, 0.0), h(n_tmp - 1, 0.0);
+  std::vector<double> hv;
+  unsigned accumulated = 0;
+  int dim = 0;
+  State st = kIterate;
+  bool reorth = false;
+  auto S = [&](const double* src, double cf, double* xs, double* y, const double* v0) {
+    Timer* e = schur_sample(c);
+    if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+    sell_spmv_fused(n, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf, xs, y, v0, part0, part1,
+                    c.stream);
+    if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+  };
+  do {
+    std::fill(h.begin(), h.end(), 0.0);
+    schur_vmult(c, x, p);
+    sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
+    copy(n, p, tv[0], c.stream);        // identity preconditioner
+    double rho = std::sqrt(dot_host(c, n, tv[0], tv[0], kSlotA));
+    st = ctl.check(accumulated, rho);
+    if (st != kIterate) break;
+    gamma[0] = rho;
+    scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
+    const double* src = tv[0];
+    double cf = 1.0;
+    for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
+      ++accumulated;
+      double* w = wbuf[inner & 1];
+      // v_inner = src * cf is stored by the SpMV itself (inner > 0)
+      S(src, cf, inner > 0 ? tv[inner] : nullptr, w, tv[0]);
+      dim = inner + 1;
+      const bool consider = !reorth && ((dim - 1) % 5 == 4);
+      // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i
+      const double* prev = part0;
+      int nprev = nbs;
+      for (int i = 1; i <= dim; ++i) {
+        const bool last = i == dim;
+        double* out = last ? slot(c, kHostPartials) : pbuf(c, i & 1);
+        chain_add_and_dot_ex(n, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
+                             slot(c, kSlotH + i - 1), nb, i == 1 && consider ? part1 : nullptr,
+                             slot(c, kSlotNStart), c.stream);
+        prev = out;
+        nprev = nb;
+      }
+      double norm_vv = std::sqrt(fetch_chain(c, kSlotH, dim, nb, hv));
+      const double start2 = consider ? c.hpinned[kSlotNStart] : 0.0;
+      for (int i = 0; i < dim; ++i) h[i] = hv[i];
+      bool second = reorth;
+      if (consider && !(norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16))) {
+        reorth = true;
+        second = true;
+      }
+      if (second) {
+        norm_vv = std::sqrt(gs_chain(c, n, tv, dim, w, kSlotH2, hv));
+        for (int i = 0; i < dim; ++i) h[i] += hv[i];
+      }
+      const double sv = norm_vv;
+      h[inner + 1] = sv;
+      src = w;
+      cf = sv != 0 ? 1. / sv : 1.0;
+      givens_rotation(h, gamma, ci, si, inner);
+      for (int i = 0; i < dim; ++i) H[i][inner] = h[i];
+      rho = std::fabs(gamma[dim]);
+      st = ctl.check(accumulated, rho);
+    }
+    std::vector<double> y(dim, 0.0);
+    for (int i = dim - 1; i >= 0; --i) {
+      double sum = gamma[i];
+      for (int j = i + 1; j < dim; ++j) sum -= y[j] * H[i][j];
+      y[i] = sum / H[i][i];
+    }
+    combine(c, n, y, tv, x);
+  } while (st == kIterate);
+  return st;
+}
+
 // deal.II Householder<double>::least_squares on the (m x n) matrix S.
 double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
                                  std::vector<double>& dst, const std::vector<double>& src) {
@@ -264,9 +359,14 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
   {
     const double nrm = std::sqrt(dot_host(c, np, src + nu, src + nu, kSlotB));
     Control ctl{5000, 1e-6 * nrm};
-    ensure_pool(c.sg_v, 30, size_t(np));
-    Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
-    const State st = gmres(c, np, S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
+    ensure_pool(c.sg_v, 32, size_t(np));
+    State st;
+    if (c.schur_explicit) {
+      st = gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+    } else {
+      Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
+      st = gmres(c, np, S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
+    }
     inner += int(ctl.last_step);
     if (st != kSuccess) throw NoConvergence();
     scale(np, DScal{nullptr, -1.0}, dst + nu, c.stream);
@@ -355,21 +455,25 @@ void nse_vmult(Ctx& c, const double* src, double* dst) {
   spmv_bsr13(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);
 }
 
+namespace {
+// sampled, deferred timing of Schur-complement applies (no host sync)
+Timer* schur_sample(Ctx& c) {
+  if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
+      c.schur_ev_used < Ctx::kSchurEvents)
+    return &c.schur_ev[c.schur_ev_used++];
+  return nullptr;
+}
+}  // namespace
+
 void schur_vmult(Ctx& c, const double* src, double* dst) {
   if (c.schur_explicit) {
-    Timer* e = nullptr;
-    if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
-        c.schur_ev_used < Ctx::kSchurEvents)
-      e = &c.schur_ev[c.schur_ev_used++];
+    Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    spmv_csr_long(c.n_p, c.S_ptr.p, c.S_col.p, c.S_val.p, src, dst, false, c.stream);
+    sell_spmv(c.n_p, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, 1.0, dst, c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     return;
   }
-  Timer* ev = nullptr;
-  if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
-      c.schur_ev_used < Ctx::kSchurEvents)
-    ev = &c.schur_ev[c.schur_ev_used++];
+  Timer* ev = schur_sample(c);
   if (ev) DCP_HIP_CHECK(hipEventRecord(ev->a, c.stream));
   spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src, c.schur_tmp1.p, false, c.stream);
   mul(c.n_u, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
