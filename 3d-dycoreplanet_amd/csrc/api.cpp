@@ -14,11 +14,15 @@
 #include "context.h"
 #include "fe_tables.h"
 #include "mesh.h"
+#include "partition.h"
 #include "prm.h"
 
 using namespace dcp;
 
 struct dcp_ctx : Ctx {};
+struct dcp_group : dcp::LocalGroup {
+  explicit dcp_group(int n) : dcp::LocalGroup(n) {}
+};
 
 namespace dcp {
 Ctx::~Ctx() {
@@ -137,6 +141,16 @@ struct PhaseTimer {
     *out = ms;
   }
 };
+
+// get_maximal_velocity / get_cfl_number over the owned cells (+ MPI max)
+void velocity_stats_global(Ctx& c) {
+  halo_exchange(c, c.halo_nse, c.nse_sol.p);
+  velocity_stats(c.cd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
+  allreduce(c, c.dscal.p + 262, 2, true);
+  DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
+                               hipMemcpyDeviceToHost, c.stream));
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+}
 
 void need_ready(Ctx& c) {
   require(c.have_physics, DCP_ERR_STATE, "dcp_set_physics has not been called");
@@ -339,9 +353,142 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   }
 }
 
+// Device halo of one vector family from per-peer position lists.
+void make_halo(Ctx::Halo& h, const std::vector<int>& peers,
+               const std::vector<std::vector<int32_t>>& spos,
+               const std::vector<std::vector<int32_t>>& rpos) {
+  h.peers = peers;
+  h.sn.clear();
+  h.rn.clear();
+  h.soff.clear();
+  h.roff.clear();
+  std::vector<int32_t> sp, rp;
+  for (size_t i = 0; i < peers.size(); ++i) {
+    h.soff.push_back(sp.size());
+    h.roff.push_back(rp.size());
+    h.sn.push_back(spos[i].size());
+    h.rn.push_back(rpos[i].size());
+    sp.insert(sp.end(), spos[i].begin(), spos[i].end());
+    rp.insert(rp.end(), rpos[i].begin(), rpos[i].end());
+  }
+  h.ns = int(sp.size());
+  h.nr = int(rp.size());
+  h.spos.upload(sp);
+  h.rpos.upload(rp);
+  h.sbuf.alloc(sp.size());
+  h.rbuf.alloc(rp.size());
+}
+
+// positions of a HaloPlan's entities in a vector: entity e -> off + w*e + j
+void plan_positions(const HaloPlan& p, int off, std::vector<int>& peers,
+                    std::vector<std::vector<int32_t>>& s, std::vector<std::vector<int32_t>>& r) {
+  for (size_t i = 0; i < p.peers.size(); ++i) {
+    size_t k = 0;
+    while (k < peers.size() && peers[k] != p.peers[i]) ++k;
+    if (k == peers.size()) {
+      // keep peers ascending
+      k = std::lower_bound(peers.begin(), peers.end(), p.peers[i]) - peers.begin();
+      peers.insert(peers.begin() + k, p.peers[i]);
+      s.insert(s.begin() + k, std::vector<int32_t>());
+      r.insert(r.begin() + k, std::vector<int32_t>());
+    }
+    for (int j = p.send_ptr[i]; j < p.send_ptr[i + 1]; ++j)
+      for (int c = 0; c < p.width; ++c) s[k].push_back(off + p.width * p.send_idx[j] + c);
+    for (int j = p.recv_ptr[i]; j < p.recv_ptr[i + 1]; ++j)
+      for (int c = 0; c < p.width; ++c) r[k].push_back(off + p.width * p.recv_idx[j] + c);
+  }
+}
+
+void build_halos(Ctx& c, const LocalMesh& L) {
+  auto one = [&](Ctx::Halo& h, std::initializer_list<std::pair<const HaloPlan*, int>> parts) {
+    std::vector<int> peers;
+    std::vector<std::vector<int32_t>> s, r;
+    for (auto& pr : parts) plan_positions(*pr.first, pr.second, peers, s, r);
+    make_halo(h, peers, s, r);
+  };
+  one(c.halo_v, {{&L.hv, 0}});
+  one(c.halo_p, {{&L.hp, 0}});
+  one(c.halo_nse, {{&L.hv, 0}, {&L.hp, c.n_u}});
+  one(c.halo_T, {{&L.hT, 0}});
+}
+
+// global position of every local entry of a state field (identity on one GPU)
+std::vector<int64_t> global_positions(const Ctx& c, int field) {
+  std::vector<int64_t> g;
+  if (field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS) {
+    g.assign(c.T_g.begin(), c.T_g.end());
+  } else {
+    g.resize(size_t(c.n_u) + c.n_p);
+    for (int i = 0; i < c.n_u; ++i) g[i] = 3 * int64_t(c.vnode_g[i / 3]) + i % 3;
+    for (int i = 0; i < c.n_p; ++i) g[size_t(c.n_u) + i] = int64_t(c.n_u_g) + c.p_g[i];
+  }
+  return g;
+}
+
+// is local entry i of the field owned by this rank
+bool owned_entry(const Ctx& c, int field, size_t i) {
+  if (field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS)
+    return int(i) < c.nTo;
+  if (int(i) < c.n_u) return int(i) < 3 * c.nvo;
+  return int(i) - c.n_u < c.npo;
+}
+
 }  // namespace
 
 extern "C" {
+
+int dcp_nccl_unique_id(void* out128) {
+  return guarded(nullptr, [&] {
+    require(out128 != nullptr, DCP_ERR_INVALID, "NULL out");
+    rccl_unique_id(out128);
+    return DCP_OK;
+  });
+}
+
+dcp_group* dcp_group_create(int world_size) {
+  try {
+    return new dcp_group(world_size);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  } catch (const DeviceError& e) {
+    g_last_error = std::string("HIP error in ") + e.what_expr;
+    return nullptr;
+  }
+}
+
+void dcp_group_destroy(dcp_group* g) { delete g; }
+
+int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                       const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
+                       int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c, int rank,
+                       int world, int64_t* info, int32_t* peers, int32_t* send_ptr,
+                       int64_t* send_gid, int32_t* recv_ptr, int64_t* recv_gid) {
+  return guarded(nullptr, [&] {
+    require(info != nullptr, DCP_ERR_INVALID, "NULL info");
+    LocalMesh L;
+    try {
+      L = localize(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
+                   n_T, nse_c, T_c, rank, world);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+    HostPrep h;
+    prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
+                 L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc);
+    const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
+                           int64_t(L.hv.peers.size()), int64_t(L.hv.send_idx.size()),
+                           int64_t(L.hv.recv_idx.size()), int64_t(h.color_ptr.size()) - 1};
+    std::copy(v, v + 12, info);
+    if (peers) std::copy(L.hv.peers.begin(), L.hv.peers.end(), peers);
+    if (send_ptr) std::copy(L.hv.send_ptr.begin(), L.hv.send_ptr.end(), send_ptr);
+    if (recv_ptr) std::copy(L.hv.recv_ptr.begin(), L.hv.recv_ptr.end(), recv_ptr);
+    if (send_gid) std::copy(L.hv.send_gid.begin(), L.hv.send_gid.end(), send_gid);
+    if (recv_gid) std::copy(L.hv.recv_gid.begin(), L.hv.recv_gid.end(), recv_gid);
+    return DCP_OK;
+  });
+}
 
 int dcp_device_count(void) {
   int n = 0;
@@ -362,10 +509,19 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
     std::unique_ptr<dcp_ctx> c(new dcp_ctx());
     if (cfg) c->cfg = *cfg;
     if (c->cfg.world_size <= 0) c->cfg.world_size = 1;
-    require(c->cfg.world_size == 1, DCP_ERR_UNSUPPORTED,
-            "world_size > 1 needs the RCCL halo path (not built in this library version)");
     require(c->cfg.device >= 0 && c->cfg.device < ndev, DCP_ERR_INVALID, "device ordinal out of range");
+    require(c->cfg.rank >= 0 && c->cfg.rank < c->cfg.world_size, DCP_ERR_INVALID, "rank out of range");
     DCP_HIP_CHECK(hipSetDevice(c->cfg.device));
+    if (c->cfg.world_size > 1) {
+      if (c->cfg.group) {
+        require(c->cfg.group->size == c->cfg.world_size, DCP_ERR_INVALID, "group size != world_size");
+        c->comm = make_local_comm(c->cfg.group, c->cfg.rank);
+      } else {
+        require(c->cfg.nccl_id != nullptr, DCP_ERR_INVALID,
+                "world_size > 1 needs nccl_id (dcp_nccl_unique_id on rank 0) or a dcp_group");
+        c->comm = make_rccl_comm(c->cfg.nccl_id, c->cfg.rank, c->cfg.world_size);
+      }
+    }
     DCP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->ev_total.init();
     c->schur_ev.resize(Ctx::kSchurEvents);
@@ -437,8 +593,29 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
     Ctx& c = *ctx;
     HostPrep h;
-    prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
-                 n_T, nse_c, T_c);
+    const bool dist = c.comm != nullptr;
+    LocalMesh L;
+    const int n_u_g = n_u, n_p_g = n_p, n_T_g = n_T;
+    if (dist) {
+      // this rank's cells + two ghost layers in local numbering (partition.h)
+      try {
+        L = localize(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
+                     n_T, nse_c, T_c, c.cfg.rank, c.cfg.world_size);
+      } catch (const std::runtime_error& e) {
+        fail(DCP_ERR_INVALID, e.what());
+      }
+      const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+      n_cells = L.n_cells;
+      n_u = L.n_u();
+      n_p = L.n_p();
+      n_T = L.n_T();
+      cell_diameter = L.diameter.data();
+      prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
+                   cell_diameter, n_u, n_p, n_T, &lnc, &ltc);
+    } else {
+      prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u,
+                   n_p, n_T, nse_c, T_c);
+    }
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
@@ -456,6 +633,16 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.n_p = n_p;
     c.n_T = n_T;
     c.n_vnodes = nv;
+    c.n_u_g = n_u_g;
+    c.n_p_g = n_p_g;
+    c.n_T_g = n_T_g;
+    c.n_owned_cells = dist ? L.n_owned_cells : n_cells;
+    c.nvo = dist ? L.nvo : nv;
+    c.npo = dist ? L.npo : n_p;
+    c.nTo = dist ? L.nTo : n_T;
+    c.vnode_g = L.vnode_g;
+    c.p_g = L.p_g;
+    c.T_g = L.T_g;
     c.cell_q2.upload(q2);
     c.cell_p.upload(pd);
     c.cell_T.upload(td);
@@ -476,12 +663,14 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.S_ptr.upload(h.Sp);
     c.S_col.upload(h.Sc);
     {
-      // SELL-64 layout of the S pattern: slice width = longest row of the slice
-      const int n_sl = (n_p + 63) / 64;
+      // SELL-64 layout of the owned rows of the S pattern: slice width =
+      // longest row of the slice
+      const int rows = c.npo;
+      const int n_sl = (rows + 63) / 64;
       std::vector<int64_t> off(size_t(n_sl) + 1, 0);
       for (int sl = 0; sl < n_sl; ++sl) {
         int w = 0;
-        for (int p = 64 * sl; p < std::min(n_p, 64 * sl + 64); ++p)
+        for (int p = 64 * sl; p < std::min(rows, 64 * sl + 64); ++p)
           w = std::max(w, h.Sp[p + 1] - h.Sp[p]);
         off[sl + 1] = off[sl] + 64 * int64_t(w);
       }
@@ -491,8 +680,8 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         for (int i = 0; i < 64; ++i) {
           const int p = 64 * sl + i;
           for (int64_t k = 0; k < w; ++k) {
-            const bool real = p < n_p && k < h.Sp[p + 1] - h.Sp[p];
-            scol[off[sl] + 64 * k + i] = real ? h.Sc[h.Sp[p] + k] : (p < n_p ? p : 0);
+            const bool real = p < rows && k < h.Sp[p + 1] - h.Sp[p];
+            scol[off[sl] + 64 * k + i] = real ? h.Sc[h.Sp[p] + k] : (p < rows ? p : 0);
           }
         }
       }
@@ -500,7 +689,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.S_sell_col.upload(scol);
       c.S_val.alloc(scol.size());
       c.S_val.zero(c.stream);  // padding entries stay 0
-      c.sell_part.alloc(2 * size_t(sell_fused_blocks(n_p)));
+      c.sell_part_len = sell_fused_blocks(rows);
     }
     c.S_max_row = h.S_max_row;
     c.A_val.alloc(Ac.size() * 9);
@@ -540,6 +729,25 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.utmp.alloc(n_u);
     c.fg_aux.alloc(nn);
     free_workspaces(c);
+    // ---- multi-GPU: halo plans and the common widths of all-reduced partials
+    c.max_owned[0] = 3 * c.nvo + c.npo;
+    c.max_owned[1] = c.npo;
+    c.max_owned[2] = 3 * c.nvo;
+    c.max_owned[3] = c.nTo;
+    if (dist) {
+      build_halos(c, L);
+      double m[5] = {double(c.max_owned[0]), double(c.max_owned[1]), double(c.max_owned[2]),
+                     double(c.max_owned[3]), double(c.sell_part_len)};
+      double* d = c.dscal.p + 3500;
+      DCP_HIP_CHECK(hipMemcpyAsync(d, m, sizeof(m), hipMemcpyHostToDevice, c.stream));
+      c.comm->allreduce(d, 5, true, c.stream);
+      DCP_HIP_CHECK(hipMemcpyAsync(m, d, sizeof(m), hipMemcpyDeviceToHost, c.stream));
+      DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+      for (int k = 0; k < 4; ++k) c.max_owned[k] = int(m[k]);
+      c.sell_part_len = int(m[4]);
+    }
+    c.sell_part.alloc(2 * size_t(std::max(c.sell_part_len, 1)));
+    c.sell_part.zero(c.stream);  // entries past this rank's slices stay 0
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     c.have_mesh = true;
     c.nse_assembled = c.precond_built = c.T_matrix_ok = c.T_rhs_ok = false;
@@ -552,6 +760,17 @@ int dcp_state_set(dcp_ctx* ctx, int field, const double* host, size_t n) {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     size_t want = 0;
     double* p = field_ptr(*ctx, field, want);
+    if (ctx->comm) {
+      // global vector in, local (owned + ghost) entries uploaded
+      const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
+      require(n == size_t(T ? ctx->n_T_g : ctx->n_u_g + ctx->n_p_g), DCP_ERR_INVALID,
+              "state size mismatch (several GPUs: pass the global vector)");
+      const std::vector<int64_t> g = global_positions(*ctx, field);
+      std::vector<double> loc(want);
+      for (size_t i = 0; i < want; ++i) loc[i] = host[g[i]];
+      DCP_HIP_CHECK(hipMemcpy(p, loc.data(), want * sizeof(double), hipMemcpyHostToDevice));
+      return DCP_OK;
+    }
     require(n == want, DCP_ERR_INVALID, "state size mismatch");
     DCP_HIP_CHECK(hipMemcpyAsync(p, host, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -564,6 +783,19 @@ int dcp_state_get(dcp_ctx* ctx, int field, double* host, size_t n) {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     size_t want = 0;
     double* p = field_ptr(*ctx, field, want);
+    if (ctx->comm) {
+      // owned entries written into the global vector, the rest untouched
+      const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
+      require(n == size_t(T ? ctx->n_T_g : ctx->n_u_g + ctx->n_p_g), DCP_ERR_INVALID,
+              "state size mismatch (several GPUs: pass the global vector)");
+      DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      std::vector<double> loc(want);
+      DCP_HIP_CHECK(hipMemcpy(loc.data(), p, want * sizeof(double), hipMemcpyDeviceToHost));
+      const std::vector<int64_t> g = global_positions(*ctx, field);
+      for (size_t i = 0; i < want; ++i)
+        if (owned_entry(*ctx, field, i)) host[g[i]] = loc[i];
+      return DCP_OK;
+    }
     require(n == want, DCP_ERR_INVALID, "state size mismatch");
     DCP_HIP_CHECK(hipMemcpyAsync(host, p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -612,6 +844,9 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       c.nse_rhs.zero(c.stream);
       out.rhs = c.nse_rhs.p;
     }
+    // ghosted old solutions (the reference reads the ghosted vectors, :583-589)
+    halo_exchange(c, c.halo_nse, c.old_nse.p);
+    halo_exchange(c, c.halo_T, c.old_T.p);
     for (int k = 0; k < c.n_colors(); ++k)
       launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                         c.old_T.p, c.ph, out, c.stream);
@@ -637,7 +872,7 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
       require(c.nse_assembled, DCP_ERR_STATE,
               "the explicit Schur complement needs the assembled B blocks: call "
               "dcp_assemble_nse_system first");
-      form_schur_complement(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
+      form_schur_complement(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
                             c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_sell_off.p,
                             c.S_val.p, c.S_max_row, c.stream);
     }
@@ -673,6 +908,8 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
     csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
     c.T_rhs.zero(c.stream);
+    halo_exchange(c, c.halo_T, c.old_T.p);
+    halo_exchange(c, c.halo_nse, c.nse_sol.p);
     for (int k = 0; k < c.n_colors(); ++k)
       launch_T_rhs(c.cd(), c.color_begin(k), c.color_size(k), c.old_T.p, c.nse_sol.p, c.ph,
                    c.T_rhs.p, c.stream);
@@ -725,10 +962,7 @@ int dcp_max_velocity(dcp_ctx* ctx, double* out) {
     need_ready(*ctx);
     require(out != nullptr, DCP_ERR_INVALID, "NULL out");
     Ctx& c = *ctx;
-    velocity_stats(c.cd(), c.nse_sol.p, c.dscal.p + 262, c.stream);
-    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
-                                 hipMemcpyDeviceToHost, c.stream));
-    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    velocity_stats_global(c);
     *out = c.hpinned[0];
     return DCP_OK;
   });
@@ -739,10 +973,7 @@ int dcp_cfl_number(dcp_ctx* ctx, double* out) {
     need_ready(*ctx);
     require(out != nullptr, DCP_ERR_INVALID, "NULL out");
     Ctx& c = *ctx;
-    velocity_stats(c.cd(), c.nse_sol.p, c.dscal.p + 262, c.stream);
-    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
-                                 hipMemcpyDeviceToHost, c.stream));
-    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    velocity_stats_global(c);
     *out = c.hpinned[1];
     return DCP_OK;
   });

@@ -1,0 +1,151 @@
+// RCCL and in-process transports of comm.h.
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "device.h"
+
+namespace dcp {
+namespace {
+
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+
+struct RcclComm : Comm {
+  ncclComm_t comm = nullptr;
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void exchange(int npeers, const int* peers, double* const* sbuf, const size_t* sn,
+                double* const* rbuf, const size_t* rn, hipStream_t s) override {
+    if (npeers == 0) return;
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int i = 0; i < npeers; ++i) {
+      if (sn[i]) nccl_check(ncclSend(sbuf[i], sn[i], ncclDouble, peers[i], comm, s), "ncclSend");
+      if (rn[i]) nccl_check(ncclRecv(rbuf[i], rn[i], ncclDouble, peers[i], comm, s), "ncclRecv");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  void allreduce(double* buf, size_t n, bool max, hipStream_t s) override {
+    if (n == 0) return;
+    nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, max ? ncclMax : ncclSum, comm, s),
+               "ncclAllReduce");
+  }
+};
+
+struct LocalComm : Comm {
+  LocalGroup* g;
+  void exchange(int npeers, const int* peers, double* const* sbuf, const size_t* sn,
+                double* const* rbuf, const size_t* rn, hipStream_t s) override {
+    LocalGroup::Post& me = g->post[rank];
+    me.dest.assign(peers, peers + npeers);
+    me.ptr.assign(sbuf, sbuf + npeers);
+    me.n.assign(sn, sn + npeers);
+    DCP_HIP_CHECK(hipEventRecord(g->ready[rank], s));
+    g->barrier();
+    for (int i = 0; i < npeers; ++i) {
+      const LocalGroup::Post& o = g->post[peers[i]];
+      size_t k = 0;
+      while (k < o.dest.size() && o.dest[k] != rank) ++k;
+      if (k == o.dest.size() || o.n[k] != rn[i])
+        throw std::runtime_error("LocalComm: halo plans of ranks " + std::to_string(rank) +
+                                 " and " + std::to_string(peers[i]) + " disagree");
+      DCP_HIP_CHECK(hipStreamWaitEvent(s, g->ready[peers[i]], 0));
+      if (rn[i])
+        DCP_HIP_CHECK(hipMemcpyAsync(rbuf[i], o.ptr[k], rn[i] * sizeof(double),
+                                     hipMemcpyDeviceToDevice, s));
+    }
+    DCP_HIP_CHECK(hipEventRecord(g->done[rank], s));
+    g->barrier();
+    // a peer reuses its send buffer only after our copies out of it ran
+    for (int i = 0; i < npeers; ++i) DCP_HIP_CHECK(hipStreamWaitEvent(s, g->done[peers[i]], 0));
+  }
+  void allreduce(double* buf, size_t n, bool max, hipStream_t s) override {
+    LocalGroup::Post& me = g->post[rank];
+    me.buf = buf;
+    me.len = n;
+    if (g->tmp_len[rank] < n) {
+      if (g->tmp[rank]) DCP_HIP_CHECK(hipFree(g->tmp[rank]));
+      DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&g->tmp[rank]), n * sizeof(double)));
+      g->tmp_len[rank] = n;
+    }
+    DCP_HIP_CHECK(hipEventRecord(g->ready[rank], s));
+    g->barrier();
+    BufTable t{};
+    for (int r = 0; r < size; ++r) {
+      if (g->post[r].len != n) throw std::runtime_error("LocalComm: allreduce length mismatch");
+      DCP_HIP_CHECK(hipStreamWaitEvent(s, g->ready[r], 0));
+      t.p[r] = g->post[r].buf;
+    }
+    group_reduce(n, size, t, g->tmp[rank], max, s);
+    DCP_HIP_CHECK(hipEventRecord(g->done[rank], s));
+    g->barrier();
+    for (int r = 0; r < size; ++r) DCP_HIP_CHECK(hipStreamWaitEvent(s, g->done[r], 0));
+    DCP_HIP_CHECK(hipMemcpyAsync(buf, g->tmp[rank], n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    // nobody may overwrite its buffer before every rank has read it: the
+    // copies above are ordered after all ranks' reductions (done events)
+  }
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_rccl_comm(const void* nccl_id, int rank, int size) {
+  auto c = std::make_unique<RcclComm>();
+  c->rank = rank;
+  c->size = size;
+  ncclUniqueId id;
+  std::memcpy(&id, nccl_id, sizeof(id));
+  nccl_check(ncclCommInitRank(&c->comm, size, id, rank), "ncclCommInitRank");
+  return c;
+}
+
+void rccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  std::memcpy(out128, &id, sizeof(id));
+}
+
+LocalGroup::LocalGroup(int n) : size(n), post(n), ready(n), done(n), tmp(n, nullptr), tmp_len(n, 0) {
+  if (n < 1 || n > kMaxLocalRanks) throw std::runtime_error("LocalGroup: 1..16 ranks");
+  for (int r = 0; r < n; ++r) {
+    DCP_HIP_CHECK(hipEventCreateWithFlags(&ready[r], hipEventDisableTiming));
+    DCP_HIP_CHECK(hipEventCreateWithFlags(&done[r], hipEventDisableTiming));
+  }
+}
+
+LocalGroup::~LocalGroup() {
+  for (int r = 0; r < size; ++r) {
+    (void)hipEventDestroy(ready[r]);
+    (void)hipEventDestroy(done[r]);
+    if (tmp[r]) (void)hipFree(tmp[r]);
+  }
+}
+
+void LocalGroup::barrier() {
+  std::unique_lock<std::mutex> lk(m);
+  const long gen = generation;
+  if (++arrived == size) {
+    arrived = 0;
+    ++generation;
+    cv.notify_all();
+  } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; })) {
+    throw std::runtime_error("LocalGroup: a rank did not reach the collective within 120 s");
+  }
+}
+
+std::unique_ptr<Comm> make_local_comm(LocalGroup* g, int rank) {
+  auto c = std::make_unique<LocalComm>();
+  c->g = g;
+  c->rank = rank;
+  c->size = g->size;
+  return c;
+}
+
+}  // namespace dcp

@@ -4,7 +4,10 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "../../include/dcp.h"
+#include "comm.h"
 #include "device.h"
 
 namespace dcp {
@@ -56,7 +59,24 @@ struct Ctx {
   PhysicsDev ph{};
   bool have_physics = false, have_mesh = false;
 
+  // local sizes (owned + ghost on several GPUs; the whole mesh on one)
   int n_cells = 0, n_u = 0, n_p = 0, n_T = 0, n_vnodes = 0;
+  // owned parts (rows this rank computes) and global sizes
+  int n_owned_cells = 0, nvo = 0, npo = 0, nTo = 0;
+  int n_u_g = 0, n_p_g = 0, n_T_g = 0;
+  // multi-GPU: communicator (null on one GPU), halo plans, local->global maps
+  std::unique_ptr<Comm> comm;
+  struct Halo {
+    std::vector<int> peers;
+    std::vector<size_t> sn, rn, soff, roff;
+    int ns = 0, nr = 0;
+    DBuf<int32_t> spos, rpos;    // positions in the vector (send: owned, recv: ghost)
+    DBuf<double> sbuf, rbuf;
+  };
+  Halo halo_v, halo_p, halo_nse, halo_T;
+  std::vector<int32_t> vnode_g, p_g, T_g;
+  int max_owned[4] = {0, 0, 0, 0};   // max over ranks of |seg_nse|, |seg_p|, |seg_v|, |seg_T|
+  int sell_part_len = 0;             // common length of the SELL partial arrays
   // mesh
   DBuf<int32_t> cell_q2, cell_p, cell_T;
   DBuf<double> xyz, diameter, T_bc;
@@ -104,6 +124,11 @@ struct Ctx {
   long schur_calls = 0;
   bool time_schur = false;
 
+  Seg seg_nse() const { return Seg{3 * nvo, n_u, 3 * nvo + npo, 0}; }
+  Seg seg_p() const { return Seg::all(npo, 1); }
+  Seg seg_v() const { return Seg::all(3 * nvo, 2); }
+  Seg seg_T() const { return Seg::all(nTo, 3); }
+
   CellData cd() const {
     CellData c;
     c.n_cells = n_cells;
@@ -133,5 +158,9 @@ int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_s
                                int* inner);
 void free_workspaces(Ctx& c);
 void ensure_workspaces(Ctx& c);
+// multi-GPU plumbing (no-ops on one GPU)
+int chain_width(const Ctx& c, Seg g);
+void allreduce(Ctx& c, double* buf, size_t n, bool max = false);
+void halo_exchange(Ctx& c, Ctx::Halo& h, double* v);
 
 }  // namespace dcp

@@ -137,11 +137,12 @@ void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* v
                const double* x, double cf, double* y, hipStream_t s);
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
 // vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
-// part1 (sell_fused_blocks(rows) of each, fixed order).
+// part1 (one per slice, fixed order; zeros up to n_part, the length common to
+// all ranks whose partials are all-reduced).
 int sell_fused_blocks(int rows);
 void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
                      const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, hipStream_t s);
+                     double* part0, double* part1, int n_part, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):
@@ -150,27 +151,41 @@ struct DScal {
   const double* p;
   double m;
 };
+// Owned part of a local vector for reductions: entries [0, n1) and
+// [off2, off2 + n - n1). The multi-GPU NSE layout [u_own u_ghost | p_own
+// p_ghost] has two owned segments; every other vector (and every single-GPU
+// vector) is a prefix, Seg::all(n).
+struct Seg {
+  int n1, off2, n;
+  int kind;  // vector family (chain width selection on several GPUs), -1: any
+  static Seg all(int n, int kind = -1) { return Seg{n, 0, n, kind}; }
+};
 // Partial-sum reduction buffer: kReduceBlocks doubles per slot.
 constexpr int kReduceBlocks = 512;
 // dot(a,b) -> *out (two launches, deterministic order)
-void dot(int n, const double* a, const double* b, double* partials, double* out, hipStream_t s);
+void dot(Seg g, const double* a, const double* b, double* partials, double* out, hipStream_t s);
+// partials only (kReduceBlocks of them) / the final fixed-order sum
+void dot_partials(Seg g, const double* a, const double* b, double* partials, hipStream_t s);
+void reduce_final(int nb, const double* partials, double* out, hipStream_t s);
 // v += c * x; then *out = v . w (w == v allowed) — deal.II add_and_dot
-void add_and_dot(int n, double* v, DScal c, const double* x, const double* w, double* partials,
+void add_and_dot(Seg g, double* v, DScal c, const double* x, const double* w, double* partials,
                  double* out, hipStream_t s);
+void add_and_dot_partials(Seg g, double* v, DScal c, const double* x, const double* w,
+                          double* partials, hipStream_t s);
 // Launch-lean Gram-Schmidt chain (one launch per step, no reduction launches):
 //   dot_partial writes nb block sums of a.b; chain_add_and_dot reduces the
 //   previous step's nb partials (stores the sum to *coef_store from block 0),
 //   does v += mult * sum * x and writes the nb partials of v.w.
 constexpr int kChainMaxBlocks = 1024;
 int chain_blocks(int n);
-void dot_partial(int n, const double* a, const double* b, double* partials, int nb, hipStream_t s);
-void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
+void dot_partial(Seg g, const double* a, const double* b, double* partials, int nb, hipStream_t s);
+void chain_add_and_dot(Seg g, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s);
 // Same step with nb_prev previous partials (e.g. from sell_spmv_fused) and an
 // optional second partial array prev2 whose fixed-order sum block 0 stores to
 // *store2.
-void chain_add_and_dot_ex(int n, double* v, const double* prev, int nb_prev, double mult,
+void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, double mult,
                           const double* x, const double* w, double* partials,
                           double* coef_store, int nb, const double* prev2, double* store2,
                           hipStream_t s);
@@ -198,8 +213,12 @@ void distribute_velocity(int n_vnodes, const NodeConstraint* vcon, double* u, hi
 void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, double* T,
                             hipStream_t s);
 // max |u_node| and max over cells of max(1e-10, max|u|)/diam -> out[0], out[1]
-void velocity_stats(const CellData& cd, const double* u, double* out2, hipStream_t s);
+// (over the first n_cells cells of cd: the owned ones)
+void velocity_stats(const CellData& cd, int n_cells, const double* u, double* out2, hipStream_t s);
 // min/max of a vector -> out[0] = min, out[1] = max
 void minmax(int n, const double* x, double* out2, hipStream_t s);
+// halo staging: buf[k] = v[pos[k]] / v[pos[k]] = buf[k], k < n
+void gather(int n, const int32_t* pos, const double* v, double* buf, hipStream_t s);
+void scatter(int n, const int32_t* pos, const double* buf, double* v, hipStream_t s);
 
 }  // namespace dcp

@@ -12,6 +12,9 @@
 // so every dot product is bitwise reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
+#include "../comm.h"
 #include "../device.h"
 
 namespace dcp {
@@ -67,6 +70,9 @@ void spmv(int rows, const int32_t* ptr, const int32_t* col, const double* val, c
   DCP_HIP_CHECK(hipGetLastError());
 }
 
+// position of the i-th owned entry of a two-segment vector (device.h Seg)
+__device__ inline long seg_pos(const Seg& g, long i) { return i < g.n1 ? i : g.off2 + (i - g.n1); }
+
 __device__ inline double block_sum(double v, double* sm) {
   // wave reduce then LDS across the 4 waves; fixed order
 #pragma unroll
@@ -79,25 +85,28 @@ __device__ inline double block_sum(double v, double* sm) {
   return r;
 }
 
-__global__ __launch_bounds__(kBlock) void k_dot_partial(int n, const double* __restrict__ a,
+__global__ __launch_bounds__(kBlock) void k_dot_partial(Seg g, const double* __restrict__ a,
                                                         const double* __restrict__ b,
                                                         double* __restrict__ partials) {
   __shared__ double sm[4];
   double s = 0;
-  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
-    s += a[i] * b[i];
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < g.n; i += long(gridDim.x) * kBlock) {
+    const long j = seg_pos(g, i);
+    s += a[j] * b[j];
+  }
   const double r = block_sum(s, sm);
   if (threadIdx.x == 0) partials[blockIdx.x] = r;
 }
 
 // v += c x ; partial dot(v, w) (w may alias v)
-__global__ __launch_bounds__(kBlock) void k_add_and_dot(int n, double* v, DScal c,
+__global__ __launch_bounds__(kBlock) void k_add_and_dot(Seg g, double* v, DScal c,
                                                         const double* __restrict__ x,
                                                         const double* w, double* partials) {
   __shared__ double sm[4];
   const double cf = c.p ? c.m * (*c.p) : c.m;
   double s = 0;
-  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+  for (long k = long(blockIdx.x) * kBlock + threadIdx.x; k < g.n; k += long(gridDim.x) * kBlock) {
+    const long i = seg_pos(g, k);
     const double nv = v[i] + cf * x[i];
     v[i] = nv;
     s += nv * (w == v ? nv : w[i]);
@@ -114,7 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_add_and_dot(int n, double* v, DScal 
 // partials, so the two dependent memory latencies overlap.
 constexpr int kChainPrefetch = 4;
 __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
-    int n, double* v, const double* __restrict__ prev, int nb_prev, double mult,
+    Seg g, double* v, const double* __restrict__ prev, int nb_prev, double mult,
     const double* __restrict__ x, const double* w, double* __restrict__ partials,
     double* coef_store, const double* __restrict__ prev2, double* store2) {
   __shared__ double sm[4];
@@ -125,9 +134,10 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
   double rv[kChainPrefetch], rx[kChainPrefetch], rw[kChainPrefetch];
 #pragma unroll
   for (int e = 0; e < kChainPrefetch; ++e) {
-    const long i = i0 + e * stride;
+    const long k = i0 + e * stride;
+    const long i = seg_pos(g, k);
     rv[e] = rx[e] = rw[e] = 0.0;
-    if (i < n) {
+    if (k < g.n) {
       rv[e] = v[i];
       rx[e] = x[i];
       if (!self) rw[e] = w[i];
@@ -152,14 +162,16 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
   double d = 0;
 #pragma unroll
   for (int e = 0; e < kChainPrefetch; ++e) {
-    const long i = i0 + e * stride;
-    if (i < n) {
+    const long k = i0 + e * stride;
+    if (k < g.n) {
+      const long i = seg_pos(g, k);
       const double nv = rv[e] + cf * rx[e];
       v[i] = nv;
       d += nv * (self ? nv : rw[e]);
     }
   }
-  for (long i = i0 + kChainPrefetch * stride; i < n; i += stride) {
+  for (long k = i0 + kChainPrefetch * stride; k < g.n; k += stride) {
+    const long i = seg_pos(g, k);
     const double nv = v[i] + cf * x[i];
     v[i] = nv;
     d += nv * (self ? nv : w[i]);
@@ -187,6 +199,12 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long sl = blockIdx.x;
   const long row = sl * 64 + lane;
+  if (sl * 64 >= rows) {
+    // padding workgroup of the common partial length (several GPUs): the
+    // all-reduced partial arrays must hold zeros past this rank's slices
+    if (EPI && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
+    return;
+  }
   const int64_t b = off[sl];
   const int w = int((off[sl + 1] - b) >> 6);
   const int per = (w + 3) >> 2;
@@ -338,12 +356,13 @@ __device__ inline void atomic_max_nonneg(double* addr, double v) {
   atomicMax(reinterpret_cast<unsigned long long*>(addr), __double_as_longlong(v));
 }
 
-__global__ __launch_bounds__(kBlock) void k_velocity_stats(CellData cd, const double* __restrict__ u,
+__global__ __launch_bounds__(kBlock) void k_velocity_stats(CellData cd, int n_cells,
+                                                           const double* __restrict__ u,
                                                            double* out2) {
   __shared__ double sm[2][4];
   const long c = long(blockIdx.x) * kBlock + threadIdx.x;
   double mx = 0, cfl = 0;
-  if (c < cd.n_cells) {
+  if (c < n_cells) {
     double cm = 1e-10;  // get_cfl_number initialises the cell max with 1e-10
     for (int n = 0; n < 27; ++n) {
       const size_t b = 3 * size_t(cd.cell_q2[27 * c + n]);
@@ -404,6 +423,24 @@ __global__ void k_minmax_final(int nb, const double* partials, double* out2) {
   out2[1] = hi;
 }
 
+__global__ void k_group_reduce(size_t n, int nbufs, BufTable t, double* __restrict__ out, int mx) {
+  for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += size_t(gridDim.x) * kBlock) {
+    double v = t.p[0][i];
+    for (int r = 1; r < nbufs; ++r) v = mx ? fmax(v, t.p[r][i]) : v + t.p[r][i];
+    out[i] = v;
+  }
+}
+__global__ void k_gather(int n, const int32_t* __restrict__ pos, const double* __restrict__ v,
+                         double* __restrict__ buf) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    buf[i] = v[pos[i]];
+}
+__global__ void k_scatter(int n, const int32_t* __restrict__ pos, const double* __restrict__ buf,
+                          double* __restrict__ v) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    v[pos[i]] = buf[i];
+}
+
 inline int grid_for(long n) {
   long g = (n + kBlock - 1) / kBlock;
   if (g > 4096) g = 4096;
@@ -435,9 +472,16 @@ void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const doubl
   spmv<1, 1, 32>(rows, ptr, col, val, x, y, add, s);
 }
 
-void dot(int n, const double* a, const double* b, double* partials, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_dot_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, a, b, partials);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, kReduceBlocks, partials, out);
+void dot(Seg g, const double* a, const double* b, double* partials, double* out, hipStream_t s) {
+  dot_partials(g, a, b, partials, s);
+  reduce_final(kReduceBlocks, partials, out, s);
+}
+void dot_partials(Seg g, const double* a, const double* b, double* partials, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, g, a, b, partials);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void reduce_final(int nb, const double* partials, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, nb, partials, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -450,22 +494,22 @@ int chain_blocks(int n) {
   return nb < 256 ? 256 : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
 }
 
-void dot_partial(int n, const double* a, const double* b, double* partials, int nb, hipStream_t s) {
-  hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, n, a, b, partials);
+void dot_partial(Seg g, const double* a, const double* b, double* partials, int nb, hipStream_t s) {
+  hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, g, a, b, partials);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void chain_add_and_dot(int n, double* v, const double* prev, double mult, const double* x,
+void chain_add_and_dot(Seg g, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s) {
-  chain_add_and_dot_ex(n, v, prev, nb, mult, x, w, partials, coef_store, nb, nullptr, nullptr, s);
+  chain_add_and_dot_ex(g, v, prev, nb, mult, x, w, partials, coef_store, nb, nullptr, nullptr, s);
 }
 
-void chain_add_and_dot_ex(int n, double* v, const double* prev, int nb_prev, double mult,
+void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, double mult,
                           const double* x, const double* w, double* partials,
                           double* coef_store, int nb, const double* prev2, double* store2,
                           hipStream_t s) {
-  hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, n, v, prev, nb_prev, mult,
+  hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, g, v, prev, nb_prev, mult,
                      x, w, partials, coef_store, prev2, store2);
   DCP_HIP_CHECK(hipGetLastError());
 }
@@ -482,18 +526,23 @@ void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* v
 
 void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
                      const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, hipStream_t s) {
-  if (rows <= 0) return;
-  hipLaunchKernelGGL((k_sell_spmv<true>), dim3(sell_fused_blocks(rows)), dim3(kBlock), 0, s, rows,
+                     double* part0, double* part1, int n_part, hipStream_t s) {
+  const int nb = std::max(sell_fused_blocks(rows), n_part);
+  if (nb <= 0) return;
+  hipLaunchKernelGGL((k_sell_spmv<true>), dim3(nb), dim3(kBlock), 0, s, rows,
                      off, col, val, x, cf, xs, y, v0, part0, part1);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void add_and_dot(int n, double* v, DScal c, const double* x, const double* w, double* partials,
+void add_and_dot(Seg g, double* v, DScal c, const double* x, const double* w, double* partials,
                  double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_add_and_dot, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, v, c, x, w,
+  add_and_dot_partials(g, v, c, x, w, partials, s);
+  reduce_final(kReduceBlocks, partials, out, s);
+}
+void add_and_dot_partials(Seg g, double* v, DScal c, const double* x, const double* w,
+                          double* partials, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_and_dot, dim3(kReduceBlocks), dim3(kBlock), 0, s, g, v, c, x, w,
                      partials);
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, kReduceBlocks, partials, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -563,10 +612,11 @@ void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, dou
   hipLaunchKernelGGL(k_distribute_T, dim3(grid_for(n_T)), dim3(kBlock), 0, s, n_T, fixed, bc, T);
   DCP_HIP_CHECK(hipGetLastError());
 }
-void velocity_stats(const CellData& cd, const double* u, double* out2, hipStream_t s) {
+void velocity_stats(const CellData& cd, int n_cells, const double* u, double* out2, hipStream_t s) {
   DCP_HIP_CHECK(hipMemsetAsync(out2, 0, 2 * sizeof(double), s));
-  const int grid = (cd.n_cells + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_velocity_stats, dim3(grid), dim3(kBlock), 0, s, cd, u, out2);
+  const int grid = (n_cells + kBlock - 1) / kBlock;
+  if (grid == 0) return;
+  hipLaunchKernelGGL(k_velocity_stats, dim3(grid), dim3(kBlock), 0, s, cd, n_cells, u, out2);
   DCP_HIP_CHECK(hipGetLastError());
 }
 void minmax(int n, const double* x, double* out2, hipStream_t s) {
@@ -574,6 +624,23 @@ void minmax(int n, const double* x, double* out2, hipStream_t s) {
   double* partials = out2 + 2;
   hipLaunchKernelGGL(k_minmax_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, x, partials);
   hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, s, kReduceBlocks, partials, out2);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void group_reduce(size_t n, int nbufs, const BufTable& t, double* out, bool max, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_group_reduce, dim3(grid_for(long(n))), dim3(kBlock), 0, s, n, nbufs, t, out,
+                     max ? 1 : 0);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void gather(int n, const int32_t* pos, const double* v, double* buf, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kBlock), 0, s, n, pos, v, buf);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void scatter(int n, const int32_t* pos, const double* buf, double* v, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scatter, dim3(grid_for(n)), dim3(kBlock), 0, s, n, pos, buf, v);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,289 @@
+// Host partitioning for the multi-GPU path (see partition.h).
+#include "partition.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace dcp {
+
+dcp_constraints LocalMesh::nse_view() const {
+  return dcp_constraints{int(nse_line.size()), nse_line.data(), nse_ptr.data(), nse_edof.data(),
+                         nse_w.data(), nse_inh.data()};
+}
+dcp_constraints LocalMesh::T_view() const {
+  return dcp_constraints{int(T_line.size()), T_line.data(), T_ptr.data(), T_edof.data(),
+                         T_w.data(), T_inh.data()};
+}
+
+namespace {
+
+struct Global {
+  int n_cells, nv, n_p, n_T, world;
+  const int32_t* nse;   // [n][89] global dofs
+  const int32_t* Td;    // [n][8]
+  int n_u;
+  std::vector<int64_t> start;                 // cell range of each rank
+  std::vector<int32_t> vown, pown, Town;      // owner rank per entity
+  std::vector<int32_t> pc_ptr, pc_cells;      // pressure dof (vertex) -> cells
+
+  int rank_of(int c) const {
+    return int(std::upper_bound(start.begin(), start.end(), int64_t(c)) - start.begin()) - 1;
+  }
+};
+
+// Owned cells of rank s followed by its two ghost layers (ascending).
+std::vector<int32_t> local_cells(const Global& g, int s, std::vector<int>& stamp, int token) {
+  std::vector<int32_t> owned, ghosts, frontier, next;
+  for (int64_t c = g.start[s]; c < g.start[s + 1]; ++c) {
+    owned.push_back(int32_t(c));
+    stamp[c] = token;
+  }
+  frontier = owned;
+  for (int layer = 0; layer < 2; ++layer) {
+    next.clear();
+    for (int32_t c : frontier)
+      for (int k = 0; k < 89; ++k) {
+        const int d = g.nse[size_t(c) * 89 + k];
+        if (d < g.n_u) continue;
+        const int p = d - g.n_u;
+        for (int j = g.pc_ptr[p]; j < g.pc_ptr[p + 1]; ++j) {
+          const int o = g.pc_cells[j];
+          if (stamp[o] != token) {
+            stamp[o] = token;
+            next.push_back(o);
+          }
+        }
+      }
+    ghosts.insert(ghosts.end(), next.begin(), next.end());
+    frontier.swap(next);
+  }
+  std::sort(ghosts.begin(), ghosts.end());
+  owned.insert(owned.end(), ghosts.begin(), ghosts.end());
+  return owned;
+}
+
+// Entities of one field present in a cell list, split owned / ghost by rank.
+template <class F>
+void collect(const std::vector<int32_t>& cells, F&& for_each_entity, std::vector<int>& stamp,
+             int token, std::vector<int32_t>& out) {
+  out.clear();
+  for (int32_t c : cells)
+    for_each_entity(c, [&](int e) {
+      if (stamp[e] != token) {
+        stamp[e] = token;
+        out.push_back(e);
+      }
+    });
+  std::sort(out.begin(), out.end());
+}
+
+}  // namespace
+
+LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                   const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
+                   int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c, int rank,
+                   int world) {
+  if (!cell_nse_dofs || !cell_T_dofs || !cell_geometry || !cell_diameter)
+    throw std::runtime_error("localize: NULL argument");
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("localize: bad rank/world");
+  if (n_cells < world) throw std::runtime_error("localize: fewer cells than ranks");
+  if (n_u <= 0 || n_u % 3 || n_p <= 0 || n_T <= 0) throw std::runtime_error("localize: bad sizes");
+  Global g;
+  g.n_cells = n_cells;
+  g.n_u = n_u;
+  g.nv = n_u / 3;
+  g.n_p = n_p;
+  g.n_T = n_T;
+  g.world = world;
+  g.nse = cell_nse_dofs;
+  g.Td = cell_T_dofs;
+  g.start.resize(size_t(world) + 1);
+  for (int r = 0; r <= world; ++r) g.start[r] = int64_t(r) * n_cells / world;
+  g.vown.assign(g.nv, -1);
+  g.pown.assign(n_p, -1);
+  g.Town.assign(n_T, -1);
+  std::vector<int32_t> cnt(size_t(n_p) + 1, 0);
+  for (int c = 0; c < n_cells; ++c) {
+    const int rc = g.rank_of(c);
+    for (int k = 0; k < 89; ++k) {
+      const int d = cell_nse_dofs[size_t(c) * 89 + k];
+      if (d < 0 || d >= n_u + n_p) throw std::runtime_error("localize: NSE dof out of range");
+      if (d < n_u) {
+        if (g.vown[d / 3] < 0) g.vown[d / 3] = rc;
+      } else {
+        if (g.pown[d - n_u] < 0) g.pown[d - n_u] = rc;
+        cnt[d - n_u + 1]++;
+      }
+    }
+    for (int v = 0; v < 8; ++v) {
+      const int t = cell_T_dofs[size_t(c) * 8 + v];
+      if (t < 0 || t >= n_T) throw std::runtime_error("localize: T dof out of range");
+      if (g.Town[t] < 0) g.Town[t] = rc;
+    }
+  }
+  for (int p = 0; p < n_p; ++p) cnt[p + 1] += cnt[p];
+  g.pc_ptr = cnt;
+  g.pc_cells.resize(size_t(cnt[n_p]));
+  {
+    std::vector<int32_t> f(cnt.begin(), cnt.end() - 1);
+    for (int c = 0; c < n_cells; ++c)
+      for (int k = 0; k < 89; ++k) {
+        const int d = cell_nse_dofs[size_t(c) * 89 + k];
+        if (d >= n_u) g.pc_cells[f[d - n_u]++] = c;
+      }
+  }
+  std::vector<int> cstamp(n_cells, -1), vstamp(g.nv, -1), pstamp(n_p, -1), Tstamp(n_T, -1);
+  int token = 0;
+  auto vnodes_of = [&](int c, auto&& emit) {
+    for (int k = 0; k < 89; ++k) {
+      const int d = cell_nse_dofs[size_t(c) * 89 + k];
+      if (d < n_u && d % 3 == 0) emit(d / 3);
+    }
+  };
+  auto pdofs_of = [&](int c, auto&& emit) {
+    for (int k = 0; k < 89; ++k) {
+      const int d = cell_nse_dofs[size_t(c) * 89 + k];
+      if (d >= n_u) emit(d - n_u);
+    }
+  };
+  auto Tdofs_of = [&](int c, auto&& emit) {
+    for (int v = 0; v < 8; ++v) emit(cell_T_dofs[size_t(c) * 8 + v]);
+  };
+
+  LocalMesh L;
+  L.rank = rank;
+  L.world = world;
+  L.cells_g = local_cells(g, rank, cstamp, token++);
+  L.n_cells = int(L.cells_g.size());
+  L.n_owned_cells = int(g.start[rank + 1] - g.start[rank]);
+  // per-field entity lists: owned first, then ghosts (ascending global id)
+  auto order = [&](std::vector<int32_t>& ents, const std::vector<int32_t>& own, int& no, int& ng) {
+    std::stable_partition(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; });
+    no = int(std::count_if(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; }));
+    ng = int(ents.size()) - no;
+  };
+  collect(L.cells_g, vnodes_of, vstamp, token++, L.vnode_g);
+  collect(L.cells_g, pdofs_of, pstamp, token++, L.p_g);
+  collect(L.cells_g, Tdofs_of, Tstamp, token++, L.T_g);
+  order(L.vnode_g, g.vown, L.nvo, L.nvg);
+  order(L.p_g, g.pown, L.npo, L.npg);
+  order(L.T_g, g.Town, L.nTo, L.nTg);
+  std::vector<int32_t> vl(g.nv, -1), pl(n_p, -1), Tl(n_T, -1);
+  for (size_t i = 0; i < L.vnode_g.size(); ++i) vl[L.vnode_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.p_g.size(); ++i) pl[L.p_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.T_g.size(); ++i) Tl[L.T_g[i]] = int32_t(i);
+  const int nu_loc = L.n_u();
+  L.cell_nse_dofs.resize(size_t(L.n_cells) * 89);
+  L.cell_T_dofs.resize(size_t(L.n_cells) * 8);
+  L.geometry.resize(size_t(L.n_cells) * 81);
+  L.diameter.resize(L.n_cells);
+  for (int lc = 0; lc < L.n_cells; ++lc) {
+    const int c = L.cells_g[lc];
+    for (int k = 0; k < 89; ++k) {
+      const int d = cell_nse_dofs[size_t(c) * 89 + k];
+      L.cell_nse_dofs[size_t(lc) * 89 + k] =
+          d < n_u ? 3 * vl[d / 3] + d % 3 : nu_loc + pl[d - n_u];
+    }
+    for (int v = 0; v < 8; ++v) L.cell_T_dofs[size_t(lc) * 8 + v] = Tl[cell_T_dofs[size_t(c) * 8 + v]];
+    std::copy(cell_geometry + size_t(c) * 81, cell_geometry + size_t(c) * 81 + 81,
+              L.geometry.begin() + size_t(lc) * 81);
+    L.diameter[lc] = cell_diameter[c];
+  }
+  // constraints restricted to local dofs
+  L.nse_ptr.push_back(0);
+  if (nse_c)
+    for (int l = 0; l < nse_c->n_lines; ++l) {
+      const int d = nse_c->line_dof[l];
+      if (d >= n_u || vl[d / 3] < 0) {
+        if (d >= n_u && pl[d - n_u] >= 0) {  // keep pressure lines: upload rejects them
+          L.nse_line.push_back(nu_loc + pl[d - n_u]);
+          L.nse_inh.push_back(nse_c->inhomogeneity[l]);
+          L.nse_ptr.push_back(int(L.nse_edof.size()));
+        }
+        continue;
+      }
+      L.nse_line.push_back(3 * vl[d / 3] + d % 3);
+      L.nse_inh.push_back(nse_c->inhomogeneity[l]);
+      for (int k = nse_c->entry_ptr[l]; k < nse_c->entry_ptr[l + 1]; ++k) {
+        const int e = nse_c->entry_dof[k];
+        const int le = e < n_u && vl[e / 3] >= 0 ? 3 * vl[e / 3] + e % 3 : -1;
+        if (le < 0) throw std::runtime_error("localize: constraint entry outside the local mesh");
+        L.nse_edof.push_back(le);
+        L.nse_w.push_back(nse_c->entry_w[k]);
+      }
+      L.nse_ptr.push_back(int(L.nse_edof.size()));
+    }
+  L.T_ptr.push_back(0);
+  if (T_c)
+    for (int l = 0; l < T_c->n_lines; ++l) {
+      const int d = T_c->line_dof[l];
+      if (d < 0 || d >= n_T || Tl[d] < 0) continue;
+      L.T_line.push_back(Tl[d]);
+      L.T_inh.push_back(T_c->inhomogeneity[l]);
+      for (int k = T_c->entry_ptr[l]; k < T_c->entry_ptr[l + 1]; ++k) {
+        const int e = T_c->entry_dof[k];
+        if (e < 0 || e >= n_T || Tl[e] < 0)
+          throw std::runtime_error("localize: constraint entry outside the local mesh");
+        L.T_edof.push_back(Tl[e]);
+        L.T_w.push_back(T_c->entry_w[k]);
+      }
+      L.T_ptr.push_back(int(L.T_edof.size()));
+    }
+  // halo plans. Receive: my ghosts grouped by owner. Send: my owned entities
+  // present in another rank's local cells.
+  L.hv.width = 3;
+  struct Field {
+    HaloPlan* plan;
+    const std::vector<int32_t>* ents;
+    const std::vector<int32_t>* own;
+    const std::vector<int32_t>* lidx;
+    int no;
+    std::vector<int>* stamp;
+    int kind;
+  };
+  Field fields[3] = {{&L.hv, &L.vnode_g, &g.vown, &vl, L.nvo, &vstamp, 0},
+                     {&L.hp, &L.p_g, &g.pown, &pl, L.npo, &pstamp, 1},
+                     {&L.hT, &L.T_g, &g.Town, &Tl, L.nTo, &Tstamp, 2}};
+  std::vector<std::vector<std::vector<int32_t>>> sends(3, std::vector<std::vector<int32_t>>(world));
+  for (int s = 0; s < world; ++s) {
+    if (s == rank) continue;
+    const std::vector<int32_t> cs = local_cells(g, s, cstamp, token++);
+    for (auto& f : fields) {
+      std::vector<int32_t> ents;
+      if (f.kind == 0) collect(cs, vnodes_of, *f.stamp, token++, ents);
+      else if (f.kind == 1) collect(cs, pdofs_of, *f.stamp, token++, ents);
+      else collect(cs, Tdofs_of, *f.stamp, token++, ents);
+      auto& out = sends[f.kind][s];
+      for (int32_t e : ents)
+        if ((*f.own)[e] == rank) out.push_back(e);
+    }
+  }
+  for (auto& f : fields) {
+    std::vector<std::vector<int32_t>> recv(world);
+    for (size_t i = size_t(f.no); i < f.ents->size(); ++i) {
+      const int32_t e = (*f.ents)[i];
+      recv[(*f.own)[e]].push_back(e);
+    }
+    HaloPlan& h = *f.plan;
+    h.send_ptr.push_back(0);
+    h.recv_ptr.push_back(0);
+    for (int s = 0; s < world; ++s) {
+      if (s == rank || (sends[f.kind][s].empty() && recv[s].empty())) continue;
+      h.peers.push_back(s);
+      for (int32_t e : sends[f.kind][s]) {
+        h.send_idx.push_back((*f.lidx)[e]);
+        h.send_gid.push_back(e);
+      }
+      for (int32_t e : recv[s]) {
+        h.recv_idx.push_back((*f.lidx)[e]);
+        h.recv_gid.push_back(e);
+      }
+      h.send_ptr.push_back(int32_t(h.send_idx.size()));
+      h.recv_ptr.push_back(int32_t(h.recv_idx.size()));
+    }
+  }
+  return L;
+}
+
+}  // namespace dcp

@@ -9,8 +9,16 @@
 //   BlockSchurPreconditioner::vmult  block_schur_preconditioner.hpp:42-70
 //   SchurComplement::vmult           schur_complement.hpp:143-150
 //   solve_temperature                boussinesq_model.tpp:1417-1476
+//
+// Multi-GPU (c.comm != null): vectors are the rank-local layouts of
+// partition.h. Element-wise work runs over all local entries (ghost entries
+// carry junk that is never read before a halo refresh), reductions over the
+// owned entries (Seg) with the partial sums all-reduced before the final
+// fixed-order sum, so every rank takes the same decisions from bitwise equal
+// scalars. Every operator refreshes the ghost entries of its input first.
 #include <cmath>
 #include <functional>
+#include <stdexcept>
 #include <vector>
 
 #include "context.h"
@@ -61,8 +69,15 @@ const double* fetch(Ctx& c, int i, int n) {
   return c.hpinned;
 }
 
-double dot_host(Ctx& c, int n, const double* a, const double* b, int s) {
-  dot(n, a, b, c.partials.p, slot(c, s), c.stream);
+// global dot into a device slot: partials, all-reduce (multi-GPU), final sum
+void gdot(Ctx& c, Seg g, const double* a, const double* b, int s) {
+  dot_partials(g, a, b, c.partials.p, c.stream);
+  allreduce(c, c.partials.p, kReduceBlocks);
+  reduce_final(kReduceBlocks, c.partials.p, slot(c, s), c.stream);
+}
+
+double dot_host(Ctx& c, Seg g, const double* a, const double* b, int s) {
+  gdot(c, g, a, b, s);
   return fetch(c, s, 1)[0];
 }
 
@@ -103,9 +118,6 @@ void givens_rotation(std::vector<double>& h, std::vector<double>& b, std::vector
   b[col] *= ci[col];
 }
 
-// Modified Gram-Schmidt of deal.II SolverGMRES (add_and_dot chain; every 5th
-// step the loss-of-orthogonality test; once triggered a second pass for the
-// rest of the solve). Returns |vv| after orthogonalisation; h[0..dim) filled.
 // Partial-sum buffers of the launch-lean chain (c.partials holds 4 of them).
 double* pbuf(Ctx& c, int i) { return c.partials.p + size_t(i) * kChainMaxBlocks; }
 
@@ -127,38 +139,47 @@ double fetch_chain(Ctx& c, int s0, int ncoef, int nb, std::vector<double>& coef)
 
 // Gram-Schmidt chain of deal.II's add_and_dot sequence:
 //   h_0 = w.V0; h_i = (w -= h_{i-1} V_{i-1}) . V_i; |w -= h_{last} V_last|^2
-// one launch per step; coefficients land in slots s0.. and on the host.
-double gs_chain(Ctx& c, int n, const std::vector<double*>& V, int dim, double* w, int s0,
+// one launch per step (+ an all-reduce of its partials on several GPUs);
+// coefficients land in slots s0.. and on the host.
+double gs_chain(Ctx& c, Seg g, const std::vector<double*>& V, int dim, double* w, int s0,
                 std::vector<double>& h) {
-  const int nb = chain_blocks(n);
-  dot_partial(n, w, V[0], pbuf(c, 0), nb, c.stream);
-  for (int i = 1; i < dim; ++i)
-    chain_add_and_dot(n, w, pbuf(c, (i - 1) & 1), -1.0, V[i - 1], V[i], pbuf(c, i & 1),
+  const int nb = chain_width(c, g);
+  dot_partial(g, w, V[0], pbuf(c, 0), nb, c.stream);
+  allreduce(c, pbuf(c, 0), nb);
+  for (int i = 1; i < dim; ++i) {
+    chain_add_and_dot(g, w, pbuf(c, (i - 1) & 1), -1.0, V[i - 1], V[i], pbuf(c, i & 1),
                       slot(c, s0 + i - 1), nb, c.stream);
-  chain_add_and_dot(n, w, pbuf(c, (dim - 1) & 1), -1.0, V[dim - 1], w, slot(c, kHostPartials),
+    allreduce(c, pbuf(c, i & 1), nb);
+  }
+  chain_add_and_dot(g, w, pbuf(c, (dim - 1) & 1), -1.0, V[dim - 1], w, slot(c, kHostPartials),
                     slot(c, s0 + dim - 1), nb, c.stream);
+  allreduce(c, slot(c, kHostPartials), nb);
   return fetch_chain(c, s0, dim, nb, h);
 }
 
-double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int dim, double* vv,
+// Modified Gram-Schmidt of deal.II SolverGMRES (add_and_dot chain; every 5th
+// step the loss-of-orthogonality test; once triggered a second pass for the
+// rest of the solve). Returns |vv| after orthogonalisation; h[0..dim) filled.
+double modified_gram_schmidt(Ctx& c, Seg g, const std::vector<double*>& V, int dim, double* vv,
                              std::vector<double>& h, bool& reorth) {
   const bool consider = !reorth && ((dim - 1) % 5 == 4);
   double start2 = 0;
   if (consider) {
-    const int nb = chain_blocks(n);
-    dot_partial(n, vv, vv, slot(c, kHostPartials), nb, c.stream);
+    const int nb = chain_width(c, g);
+    dot_partial(g, vv, vv, slot(c, kHostPartials), nb, c.stream);
+    allreduce(c, slot(c, kHostPartials), nb);
     std::vector<double> none;
     start2 = fetch_chain(c, kHostPartials, 0, nb, none);
   }
   std::vector<double> hv;
-  double norm_vv = std::sqrt(gs_chain(c, n, V, dim, vv, kSlotH, hv));
+  double norm_vv = std::sqrt(gs_chain(c, g, V, dim, vv, kSlotH, hv));
   for (int i = 0; i < dim; ++i) h[i] = hv[i];
   if (consider) {
     if (norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16)) return norm_vv;
     reorth = true;
   }
   if (reorth) {
-    norm_vv = std::sqrt(gs_chain(c, n, V, dim, vv, kSlotH2, hv));
+    norm_vv = std::sqrt(gs_chain(c, g, V, dim, vv, kSlotH2, hv));
     for (int i = 0; i < dim; ++i) h[i] += hv[i];
   }
   return norm_vv;
@@ -166,8 +187,9 @@ double modified_gram_schmidt(Ctx& c, int n, const std::vector<double*>& V, int d
 
 // deal.II SolverGMRES<VectorType> (left preconditioning, default residual,
 // n_tmp temporary vectors -> restart n_tmp-2). P == nullptr: identity.
-State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b, Control& ctl,
-            std::vector<double*>& tv, int n_tmp) {
+// n: local vector length (element-wise work), g: owned entries (reductions).
+State gmres(Ctx& c, int n, Seg g, const Op& A, const Op* P, double* x, const double* b,
+            Control& ctl, std::vector<double*>& tv, int n_tmp) {
   ensure_pool(tv, n_tmp, size_t(n));
   double* v = tv[0];
   double* p = tv[n_tmp - 1];
@@ -182,7 +204,7 @@ State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b,
     A(x, p);
     sadd(n, -1., 1., b, p, c.stream);  // p = b - A x
     if (P) (*P)(p, v); else copy(n, p, v, c.stream);
-    double rho = std::sqrt(dot_host(c, n, v, v, kSlotA));
+    double rho = std::sqrt(dot_host(c, g, v, v, kSlotA));
     st = ctl.check(accumulated, rho);
     if (st != kIterate) break;
     gamma[0] = rho;
@@ -197,7 +219,7 @@ State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b,
         A(tv[inner], vv);  // identity preconditioner: vv = A v (bitwise the copy)
       }
       dim = inner + 1;
-      const double s = modified_gram_schmidt(c, n, tv, dim, vv, h, reorth);
+      const double s = modified_gram_schmidt(c, g, tv, dim, vv, h, reorth);
       h[inner + 1] = s;
       if (s != 0) scale(n, DScal{nullptr, 1. / s}, vv, c.stream);
       givens_rotation(h, gamma, ci, si, inner);
@@ -217,6 +239,8 @@ State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b,
   return st;
 }
 
+Timer* schur_sample(Ctx& c);
+
 // The inner Schur GMRES of block_prec on the explicit S (identity
 // preconditioner): the same deal.II SolverGMRES as gmres() above, with the
 // vector work fused so one Arnoldi step is 1 + dim launches and one readback:
@@ -224,18 +248,17 @@ State gmres(Ctx& c, int n, const Op& A, const Op* P, double* x, const double* b,
 //     (bitwise the product with the scaled vector), and the same launch
 //     stores v_k = w/|w| and the partials of (S v_k).v_0 and |S v_k|^2;
 //   * the modified Gram-Schmidt chain starts from those partials.
-Timer* schur_sample(Ctx& c);
-
 State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
                   int n_tmp) {
   const int n = c.n_p;
+  const Seg g = c.seg_p();
   ensure_pool(tv, n_tmp + 2, size_t(n));
   double* p = tv[n_tmp - 1];
   double* wbuf[2] = {tv[n_tmp], tv[n_tmp + 1]};
-  const int nbs = sell_fused_blocks(n);
+  const int nbs = c.sell_part_len;
   double* part0 = c.sell_part.p;
   double* part1 = c.sell_part.p + nbs;
-  const int nb = chain_blocks(n);
+  const int nb = chain_width(c, g);
   std::vector<std::vector<double>> H(n_tmp, std::vector<double>(n_tmp - 1, 0.0));
   std::vector<double> gamma(n_tmp, 0.0), ci(n_tmp - 1, 0.0), si(n_tmp - 1, 0.0), h(n_tmp - 1, 0.0);
   std::vector<double> hv;
@@ -243,24 +266,26 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
   int dim = 0;
   State st = kIterate;
   bool reorth = false;
-  auto S = [&](const double* src, double cf, double* xs, double* y, const double* v0) {
+  auto S = [&](double* src, double cf, double* xs, double* y, const double* v0) {
+    halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    sell_spmv_fused(n, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf, xs, y, v0, part0, part1,
-                    c.stream);
+    sell_spmv_fused(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf, xs, y, v0, part0,
+                    part1, nbs, c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+    allreduce(c, part0, 2 * size_t(nbs));
   };
   do {
     std::fill(h.begin(), h.end(), 0.0);
     schur_vmult(c, x, p);
     sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
     copy(n, p, tv[0], c.stream);        // identity preconditioner
-    double rho = std::sqrt(dot_host(c, n, tv[0], tv[0], kSlotA));
+    double rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
     st = ctl.check(accumulated, rho);
     if (st != kIterate) break;
     gamma[0] = rho;
     scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
-    const double* src = tv[0];
+    double* src = tv[0];
     double cf = 1.0;
     for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
       ++accumulated;
@@ -275,9 +300,10 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
       for (int i = 1; i <= dim; ++i) {
         const bool last = i == dim;
         double* out = last ? slot(c, kHostPartials) : pbuf(c, i & 1);
-        chain_add_and_dot_ex(n, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
+        chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
                              slot(c, kSlotH + i - 1), nb, i == 1 && consider ? part1 : nullptr,
                              slot(c, kSlotNStart), c.stream);
+        allreduce(c, out, nb);
         prev = out;
         nprev = nb;
       }
@@ -290,7 +316,7 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
         second = true;
       }
       if (second) {
-        norm_vv = std::sqrt(gs_chain(c, n, tv, dim, w, kSlotH2, hv));
+        norm_vv = std::sqrt(gs_chain(c, g, tv, dim, w, kSlotH2, hv));
         for (int i = 0; i < dim; ++i) h[i] += hv[i];
       }
       const double sv = norm_vv;
@@ -353,11 +379,17 @@ double householder_least_squares(std::vector<std::vector<double>> S, int m, int 
 
 struct NoConvergence {};
 
+// A (velocity-velocity block) on a velocity vector [u_own u_ghost]
+void a_vmult(Ctx& c, const double* src, double* dst) {
+  halo_exchange(c, c.halo_v, const_cast<double*>(src));
+  spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
+}
+
 int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inner) {
   const int nu = c.n_u, np = c.n_p;
   // inner GMRES on S = B D_A^-1 B^T, tol 1e-6 |src_p|, max 5000, identity
   {
-    const double nrm = std::sqrt(dot_host(c, np, src + nu, src + nu, kSlotB));
+    const double nrm = std::sqrt(dot_host(c, c.seg_p(), src + nu, src + nu, kSlotB));
     Control ctl{5000, 1e-6 * nrm};
     ensure_pool(c.sg_v, 32, size_t(np));
     State st;
@@ -365,25 +397,24 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
       st = gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else {
       Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
-      st = gmres(c, np, S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
+      st = gmres(c, np, c.seg_p(), S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
     }
     inner += int(ctl.last_step);
     if (st != kSuccess) throw NoConvergence();
     scale(np, DScal{nullptr, -1.0}, dst + nu, c.stream);
   }
   // utmp = src_u - B^T dst_p
-  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, dst + nu, c.utmp.p, false, c.stream);
+  halo_exchange(c, c.halo_p, dst + nu);
+  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, dst + nu, c.utmp.p, false, c.stream);
   sadd(nu, -1.0, 1.0, src, c.utmp.p, c.stream);
   if (do_solve_A) {
     // TrilinosWrappers::SolverGMRES (AztecOO) restated as deal.II GMRES with the
     // A-Jacobi, tol 1e-2 |utmp| (block_schur_preconditioner.hpp:59-67)
-    const double nrm = std::sqrt(dot_host(c, nu, c.utmp.p, c.utmp.p, kSlotB));
+    const double nrm = std::sqrt(dot_host(c, c.seg_v(), c.utmp.p, c.utmp.p, kSlotB));
     Control ctl{5000, nrm * 1e-2};
-    Op A = [&](const double* x, double* y) {
-      spmv_bsr33(c.n_vnodes, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
-    };
+    Op A = [&](const double* x, double* y) { a_vmult(c, x, y); };
     Op P = [&](const double* x, double* y) { mul(nu, c.A_inv.p, x, y, c.stream); };
-    const State st = gmres(c, nu, A, &P, dst, c.utmp.p, ctl, c.ag_v, 30);
+    const State st = gmres(c, nu, c.seg_v(), A, &P, dst, c.utmp.p, ctl, c.ag_v, 30);
     if (st != kSuccess) throw NoConvergence();
   } else {
     mul(nu, c.A_inv.p, c.utmp.p, dst, c.stream);  // Ifpack point Jacobi
@@ -395,6 +426,7 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
 State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, double tol,
              bool do_solve_A, int& acc_out, int& inner) {
   const int n = c.n_u + c.n_p;
+  const Seg g = c.seg_nse();
   Control ctl{max_steps, tol};
   ensure_pool(c.fg_v, basis, size_t(n));
   ensure_pool(c.fg_z, basis, size_t(n));
@@ -407,7 +439,7 @@ State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, 
   do {
     nse_vmult(c, x, aux);
     sadd(n, -1., 1., b, aux, c.stream);
-    const double beta = std::sqrt(dot_host(c, n, aux, aux, kSlotA));
+    const double beta = std::sqrt(dot_host(c, g, aux, aux, kSlotA));
     double res = beta;
     st = ctl.check(accumulated, res);
     if (st == kSuccess) break;
@@ -426,7 +458,7 @@ State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, 
       block_prec(c, vj, zj, do_solve_A, inner);
       nse_vmult(c, zj, aux);
       std::vector<double> hv;
-      const double nn = gs_chain(c, n, c.fg_v, j + 1, aux, kSlotH, hv);
+      const double nn = gs_chain(c, g, c.fg_v, j + 1, aux, kSlotH, hv);
       for (int i = 0; i <= j; ++i) H[i][j] = hv[i];
       H[j + 1][j] = a = std::sqrt(nn);
       if (j > 0) {
@@ -446,16 +478,6 @@ State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, 
   return st;
 }
 
-}  // namespace
-
-void nse_vmult(Ctx& c, const double* src, double* dst) {
-  // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
-  spmv_bsr33(c.n_vnodes, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
-  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src + c.n_u, dst, true, c.stream);
-  spmv_bsr13(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);
-}
-
-namespace {
 // sampled, deferred timing of Schur-complement applies (no host sync)
 Timer* schur_sample(Ctx& c) {
   if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
@@ -463,21 +485,58 @@ Timer* schur_sample(Ctx& c) {
     return &c.schur_ev[c.schur_ev_used++];
   return nullptr;
 }
+
 }  // namespace
+
+int chain_width(const Ctx& c, Seg g) {
+  // every rank launches the same number of chain workgroups (their partials
+  // are all-reduced element-wise): size it by the largest owned part
+  if (!c.comm) return chain_blocks(g.n);
+  if (g.kind < 0 || g.kind > 3) throw std::runtime_error("chain_width: untyped vector on several GPUs");
+  return chain_blocks(c.max_owned[g.kind]);
+}
+
+void allreduce(Ctx& c, double* buf, size_t n, bool max) {
+  if (c.comm) c.comm->allreduce(buf, n, max, c.stream);
+}
+
+void halo_exchange(Ctx& c, Ctx::Halo& h, double* v) {
+  if (!c.comm) return;
+  gather(h.ns, h.spos.p, v, h.sbuf.p, c.stream);
+  const int np = int(h.peers.size());
+  std::vector<double*> sb(np), rb(np);
+  for (int i = 0; i < np; ++i) {
+    sb[i] = h.sbuf.p + h.soff[i];
+    rb[i] = h.rbuf.p + h.roff[i];
+  }
+  c.comm->exchange(np, h.peers.data(), sb.data(), h.sn.data(), rb.data(), h.rn.data(), c.stream);
+  scatter(h.nr, h.rpos.p, h.rbuf.p, v, c.stream);
+}
+
+void nse_vmult(Ctx& c, const double* src, double* dst) {
+  // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
+  halo_exchange(c, c.halo_nse, const_cast<double*>(src));
+  spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
+  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src + c.n_u, dst, true, c.stream);
+  spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);
+}
 
 void schur_vmult(Ctx& c, const double* src, double* dst) {
   if (c.schur_explicit) {
+    halo_exchange(c, c.halo_p, const_cast<double*>(src));
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    sell_spmv(c.n_p, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, 1.0, dst, c.stream);
+    sell_spmv(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, 1.0, dst, c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     return;
   }
+  halo_exchange(c, c.halo_p, const_cast<double*>(src));
   Timer* ev = schur_sample(c);
   if (ev) DCP_HIP_CHECK(hipEventRecord(ev->a, c.stream));
-  spmv_bsr31(c.n_vnodes, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src, c.schur_tmp1.p, false, c.stream);
+  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src, c.schur_tmp1.p, false, c.stream);
   mul(c.n_u, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
-  spmv_bsr13(c.n_p, c.B_ptr.p, c.B_col.p, c.B_val.p, c.schur_tmp2.p, dst, false, c.stream);
+  halo_exchange(c, c.halo_v, c.schur_tmp2.p);
+  spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, c.schur_tmp2.p, dst, false, c.stream);
   if (ev) DCP_HIP_CHECK(hipEventRecord(ev->b, c.stream));
 }
 
@@ -519,7 +578,7 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   x.alloc(n);
   copy(n, c.nse_sol.p, x.p, c.stream);
   scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);      // :1151 (pressure dofs unconstrained)
-  const double tol = 1e-8 * std::sqrt(dot_host(c, n, c.nse_rhs.p, c.nse_rhs.p, kSlotA));  // :1165
+  const double tol = 1e-8 * std::sqrt(dot_host(c, c.seg_nse(), c.nse_rhs.p, c.nse_rhs.p, kSlotA));  // :1165
   scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);      // :1177 (Q1)
   int inner = 0, acc1 = 0, acc2 = 0, status = DCP_OK;
   try {
@@ -528,7 +587,8 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   } catch (const NoConvergence&) {
     // :1203-1232 fallback (Q10): do_solve_A, FGMRES(50), max = nse_matrix.m()
     try {
-      const State st = fgmres(c, x.p, c.nse_rhs.p, 50, unsigned(n), tol, true, acc2, inner);
+      const State st =
+          fgmres(c, x.p, c.nse_rhs.p, 50, unsigned(c.n_u_g + c.n_p_g), tol, true, acc2, inner);
       if (st != kSuccess) status = DCP_NOT_CONVERGED;
     } catch (const NoConvergence&) {
       status = DCP_NOT_CONVERGED;
@@ -537,6 +597,7 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
   scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);   // :1239 (x /= dt)
   copy(n, x.p, c.nse_sol.p, c.stream);                       // :1241
+  halo_exchange(c, c.halo_nse, c.nse_sol.p);                 // ghosted copy (:1241)
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
   if (outer) *outer = acc1 + acc2;
   if (inner_out) *inner_out = inner;
@@ -546,52 +607,61 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
 int solve_temperature(Ctx& c, int* iters, double* T_range) {
   // SolverCG + Ifpack Jacobi on T_matrix, tol 1e-12 |rhs|, max n_T (:1417-1476)
   const int n = c.n_T;
-  const double rhs_norm = std::sqrt(dot_host(c, n, c.T_rhs.p, c.T_rhs.p, kSlotA));
-  Control ctl{unsigned(n), 1e-12 * rhs_norm};
+  const Seg g = c.seg_T();
+  const double rhs_norm = std::sqrt(dot_host(c, g, c.T_rhs.p, c.T_rhs.p, kSlotA));
+  Control ctl{unsigned(c.n_T_g), 1e-12 * rhs_norm};
   if (c.cg_g.n < size_t(n)) {
     c.cg_g.alloc(n);
     c.cg_d.alloc(n);
     c.cg_h.alloc(n);
   }
-  double *x = c.T_sol.p, *g = c.cg_g.p, *d = c.cg_d.p, *h = c.cg_h.p;
-  auto Av = [&](const double* s, double* o) {
-    spmv_csr(n, c.T_ptr.p, c.T_col.p, c.Tmat.p, s, o, false, c.stream);
+  double *x = c.T_sol.p, *gv = c.cg_g.p, *d = c.cg_d.p, *h = c.cg_h.p;
+  auto Av = [&](double* s, double* o) {
+    halo_exchange(c, c.halo_T, s);
+    spmv_csr(c.nTo, c.T_ptr.p, c.T_col.p, c.Tmat.p, s, o, false, c.stream);
   };
-  const bool all_zero = dot_host(c, n, x, x, kSlotA) == 0.0;
+  auto gdot_slot = [&](const double* a, const double* b, int s) { gdot(c, g, a, b, s); };
+  const bool all_zero = dot_host(c, g, x, x, kSlotA) == 0.0;
   if (!all_zero) {
-    Av(x, g);
-    axpy(n, DScal{nullptr, -1.0}, c.T_rhs.p, g, c.stream);  // g.add(-1, b)
+    Av(x, gv);
+    axpy(n, DScal{nullptr, -1.0}, c.T_rhs.p, gv, c.stream);  // g.add(-1, b)
   } else {
-    equ(n, DScal{nullptr, -1.0}, c.T_rhs.p, g, c.stream);
+    equ(n, DScal{nullptr, -1.0}, c.T_rhs.p, gv, c.stream);
   }
-  double res = std::sqrt(dot_host(c, n, g, g, kSlotA));
+  double res = std::sqrt(dot_host(c, g, gv, gv, kSlotA));
   State conv = ctl.check(0, res);
   int it = 0;
   if (conv == kIterate) {
-    mul(n, c.T_inv.p, g, h, c.stream);
+    mul(n, c.T_inv.p, gv, h, c.stream);
     equ(n, DScal{nullptr, -1.0}, h, d, c.stream);
-    dot(n, g, h, c.partials.p, slot(c, kSlotC), c.stream);  // gh
+    gdot_slot(gv, h, kSlotC);  // gh
     while (conv == kIterate) {
       it++;
       Av(d, h);
-      dot(n, d, h, c.partials.p, slot(c, kSlotD), c.stream);    // d.h
+      gdot_slot(d, h, kSlotD);  // d.h
       scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);  // alpha = gh / dh
       axpy(n, DScal{slot(c, kSlotA), 1.0}, d, x, c.stream);
-      add_and_dot(n, g, DScal{slot(c, kSlotA), 1.0}, h, g, c.partials.p, slot(c, kSlotB),
-                  c.stream);
+      add_and_dot_partials(g, gv, DScal{slot(c, kSlotA), 1.0}, h, gv, c.partials.p, c.stream);
+      allreduce(c, c.partials.p, kReduceBlocks);
+      reduce_final(kReduceBlocks, c.partials.p, slot(c, kSlotB), c.stream);
       res = std::sqrt(std::fabs(fetch(c, kSlotB, 1)[0]));
       conv = ctl.check(it, res);
       if (conv != kIterate) break;
-      mul(n, c.T_inv.p, g, h, c.stream);
+      mul(n, c.T_inv.p, gv, h, c.stream);
       copy(1, slot(c, kSlotC), slot(c, kSlotD), c.stream);       // beta = old gh
-      dot(n, g, h, c.partials.p, slot(c, kSlotC), c.stream);      // new gh
+      gdot_slot(gv, h, kSlotC);                                  // new gh
       scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);  // beta
       axpby(n, DScal{nullptr, -1.0}, h, DScal{slot(c, kSlotA), 1.0}, d, c.stream);  // d = beta d - h
     }
   }
   distribute_temperature(n, c.T_fixed.p, c.T_bc.p, x, c.stream);
+  halo_exchange(c, c.halo_T, x);
   if (T_range) {
-    minmax(n, x, slot(c, kSlotMinMax), c.stream);
+    // min over ranks as max of -min
+    minmax(c.nTo, x, slot(c, kSlotMinMax), c.stream);
+    scale(1, DScal{nullptr, -1.0}, slot(c, kSlotMinMax), c.stream);
+    allreduce(c, slot(c, kSlotMinMax), 2, true);
+    scale(1, DScal{nullptr, -1.0}, slot(c, kSlotMinMax), c.stream);
     const double* r = fetch(c, kSlotMinMax, 2);
     T_range[0] = r[0];
     T_range[1] = r[1];

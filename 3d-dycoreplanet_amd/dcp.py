@@ -39,6 +39,7 @@ EXPORTED = [
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
     "dcp_host_mesh_view_get", "dcp_host_mesh_initial_temperature", "dcp_prm_load",
+    "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
 ]
 
 
@@ -69,7 +70,7 @@ class Constraints(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("rank", C.c_int), ("world_size", C.c_int),
-                ("nccl_id", C.c_void_p)]
+                ("nccl_id", C.c_void_p), ("group", C.c_void_p)]
 
 
 class Timings(C.Structure):
@@ -149,6 +150,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_host_mesh_view_get.argtypes = [P, C.POINTER(MeshView)]
     lib.dcp_host_mesh_initial_temperature.argtypes = [P, P]
     lib.dcp_prm_load.argtypes = [C.c_char_p, C.POINTER(RunParams), C.c_char_p, I]
+    lib.dcp_nccl_unique_id.argtypes = [P]
+    lib.dcp_group_create.argtypes = [I]
+    lib.dcp_group_create.restype = P
+    lib.dcp_group_destroy.argtypes = [P]
+    lib.dcp_group_destroy.restype = None
+    lib.dcp_partition_info.argtypes = [I, P, P, P, P, I, I, I, C.POINTER(Constraints),
+                                       C.POINTER(Constraints), I, I, P, P, P, P, P, P]
     return lib
 
 
@@ -260,11 +268,67 @@ def load_prm(path: str) -> RunParams:
     return rp
 
 
-class Context:
-    """One GPU context (dcp_ctx)."""
+def nccl_unique_id() -> bytes:
+    """ncclUniqueId (128 bytes) for dcp_config.nccl_id; call on rank 0 only."""
+    buf = C.create_string_buffer(128)
+    rc = lib().dcp_nccl_unique_id(buf)
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    return buf.raw
 
-    def __init__(self, device=0, rank=0, world_size=1, nccl_id=None):
-        cfg = Config(device, rank, world_size, None)
+
+class Group:
+    """In-process group of world_size contexts on one device (dcp_group):
+    drive each rank's Context from its own thread (tests of the multi-rank
+    path on one GPU)."""
+
+    def __init__(self, world_size):
+        self.world_size = world_size
+        self._h = lib().dcp_group_create(world_size)
+        if not self._h:
+            raise DcpError(DCP_ERR_DEVICE, lib().dcp_last_error(None).decode())
+
+    def close(self):
+        if self._h:
+            lib().dcp_group_destroy(self._h)
+            self._h = None
+
+
+def partition_info(m, rank, world):
+    """Host-only summary of rank's partition (dcp_partition_info): a dict of
+    sizes and the velocity-node halo lists (global ids) per peer."""
+    info = np.zeros(12, np.int64)
+    nc, tc = m.nse_constraints.as_struct(), m.T_constraints.as_struct()
+    args = (m.n_cells, _ptr(m.cell_nse_dofs), _ptr(m.cell_T_dofs), _ptr(m.cell_geometry),
+            _ptr(m.cell_diameter), m.n_u, m.n_p, m.n_T, C.byref(nc), C.byref(tc), rank, world)
+    rc = lib().dcp_partition_info(*args, _ptr(info), None, None, None, None, None)
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    npeer, ns, nr = int(info[8]), int(info[9]), int(info[10])
+    peers = np.zeros(npeer, np.int32)
+    sp, rp = np.zeros(npeer + 1, np.int32), np.zeros(npeer + 1, np.int32)
+    sg, rg = np.zeros(max(ns, 1), np.int64), np.zeros(max(nr, 1), np.int64)
+    rc = lib().dcp_partition_info(*args, _ptr(info), _ptr(peers), _ptr(sp), _ptr(sg), _ptr(rp),
+                                  _ptr(rg))
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    keys = ("n_cells", "n_owned_cells", "nvo", "nvg", "npo", "npg", "nTo", "nTg", "n_peers",
+            "n_send", "n_recv", "n_colors")
+    out = {k: int(v) for k, v in zip(keys, info)}
+    out["send"] = {int(p): sg[sp[i]:sp[i + 1]].copy() for i, p in enumerate(peers)}
+    out["recv"] = {int(p): rg[rp[i]:rp[i + 1]].copy() for i, p in enumerate(peers)}
+    return out
+
+
+class Context:
+    """One GPU context (dcp_ctx). world_size > 1: pass nccl_id (the bytes of
+    nccl_unique_id() from rank 0; one process per GPU) or group (Group)."""
+
+    def __init__(self, device=0, rank=0, world_size=1, nccl_id=None, group=None):
+        self._id = C.create_string_buffer(nccl_id, 128) if nccl_id is not None else None
+        cfg = Config(device, rank, world_size,
+                     C.cast(self._id, C.c_void_p) if self._id is not None else None,
+                     group._h if group is not None else None)
         h = C.c_void_p()
         rc = lib().dcp_ctx_create(C.byref(cfg), C.byref(h))
         if rc != DCP_OK:

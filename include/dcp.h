@@ -69,12 +69,41 @@ typedef struct {
   const double* inhomogeneity;  /* [n_lines] */
 } dcp_constraints;
 
+/* In-process group of world_size contexts on one device, each driven by its
+ * own host thread (tests of the multi-rank path on a single GPU). */
+typedef struct dcp_group dcp_group;
+
 typedef struct {
   int device;           /* HIP device ordinal (local rank) */
   int rank;             /* rank in the node-local communicator */
   int world_size;       /* number of ranks / GPUs */
   const void* nccl_id;  /* ncclUniqueId (128 bytes) when world_size > 1, else NULL */
+  dcp_group* group;     /* instead of nccl_id: in-process group (dcp_group_create) */
 } dcp_config;
+
+/* Multi-GPU ---------------------------------------------------------------
+ * Several GPUs split the cells p4est-style (planet_geometry.h:67): rank r owns
+ * cells [r n/P, (r+1) n/P) of the tree order, a DoF belongs to the rank of
+ * the lowest-index cell touching it, and every rank keeps two layers of ghost
+ * cells. Every rank passes the same GLOBAL mesh to dcp_mesh_upload and global
+ * vectors to dcp_state_set; dcp_state_get fills the rank's owned entries.
+ * Ghost DoFs are refreshed by RCCL send/recv (forward halo, the Trilinos
+ * Import of the reference) and Krylov partial sums are all-reduced. */
+int dcp_nccl_unique_id(void* out128);          /* rank 0; broadcast the 128 bytes */
+dcp_group* dcp_group_create(int world_size);   /* in-process group (tests) */
+void dcp_group_destroy(dcp_group* g);
+/* Host-only partition summary of rank/world (no device): cells, owned/ghost
+ * sizes per field, and the halo plan's global ids per peer for consistency
+ * checks. info[12] = {n_cells_local, n_owned_cells, nvo, nvg, npo, npg, nTo,
+ * nTg, n_peers_v, n_send_v, n_recv_v, n_colors}. Optional gid arrays
+ * (sizes n_send_v, n_recv_v) receive the velocity-node halo lists in peer
+ * order; peers (n_peers_v) the peer ranks, send_ptr/recv_ptr (n_peers_v+1). */
+int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                       const double* cell_geometry, const double* cell_diameter, int n_u,
+                       int n_p, int n_T, const dcp_constraints* nse_constraints,
+                       const dcp_constraints* T_constraints, int rank, int world, int64_t* info,
+                       int32_t* peers, int32_t* send_ptr, int64_t* send_gid, int32_t* recv_ptr,
+                       int64_t* recv_gid);
 
 /* Context / errors ------------------------------------------------------- */
 int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out);

@@ -1,0 +1,150 @@
+"""Multi-rank path (p4est-style cell partition, ghost layers,
+forward halo + all-reduced Krylov sums).
+
+CPU: two gloo processes each build their rank's partition on the host
+(dcp_partition_info) and check that every halo send list matches the peer's
+receive list, and that ownership covers every DoF exactly once.
+GPU: P ranks as an in-process group on one GPU (one host thread per rank,
+dcp_group) run one full time step; owned entries must match the 1-GPU run
+(assembly 1e-12, solver iterates 1e-10, same FGMRES iteration count)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dcp
+
+
+def _gloo_worker(rank, world, port, refine, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = dcp.HostMesh(refine=refine)
+        info = dcp.partition_info(m, rank, world)
+        mine = {"rank": rank, "nvo": info["nvo"], "npo": info["npo"], "nTo": info["nTo"],
+                "cells": info["n_owned_cells"],
+                "send": {k: v.tolist() for k, v in info["send"].items()},
+                "recv": {k: v.tolist() for k, v in info["recv"].items()}}
+        allinfo = [None] * world
+        dist.all_gather_object(allinfo, mine)
+        ok = True
+        for s, ids in mine["send"].items():
+            ok &= allinfo[s]["recv"].get(rank, []) == ids
+        for s, ids in mine["recv"].items():
+            ok &= allinfo[s]["send"].get(rank, []) == ids
+        tot = [sum(a[k] for a in allinfo) for k in ("nvo", "npo", "nTo", "cells")]
+        ok &= tot == [m.n_u // 3, m.n_p, m.n_T, m.n_cells]
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("refine", [2, 3])
+def test_partition_halo_consistency_gloo(refine):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29611 + refine
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, refine, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_partition_covers_and_matches(world):
+    m = dcp.HostMesh(refine=3)
+    infos = [dcp.partition_info(m, r, world) for r in range(world)]
+    assert sum(i["n_owned_cells"] for i in infos) == m.n_cells
+    assert sum(i["nvo"] for i in infos) == m.n_u // 3
+    assert sum(i["npo"] for i in infos) == m.n_p
+    for r, i in enumerate(infos):
+        for s, ids in i["send"].items():
+            assert np.array_equal(ids, infos[s]["recv"][r])
+
+
+def _time_step(ctx, m, u, T):
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    out = {"cfl0": ctx.cfl_number()}
+    ctx.assemble_nse_system()
+    out["rhs"] = ctx.get_state(dcp.NSE_RHS)
+    ctx.build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    out["T_rhs"] = ctx.get_state(dcp.T_RHS)
+    out["nse"] = ctx.solve_nse()
+    out["x"] = ctx.get_state(dcp.NSE_SOLUTION)
+    out["T"] = ctx.solve_temperature()
+    out["Tx"] = ctx.get_state(dcp.T_SOLUTION)
+    out["vmax"] = ctx.max_velocity()
+    out["cfl"] = ctx.cfl_number()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,refine", [(2, 2), (3, 2), (4, 3)])
+def test_group_time_step_matches_single_gpu(world, refine):
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(7)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    T = m.T0.copy()
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(ph)
+    ref_ctx.upload_mesh(m)
+    ref = _time_step(ref_ctx, m, u, T)
+    ref_ctx.close()
+
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(ph)
+            ctx.upload_mesh(m)
+            results[rank] = _time_step(ctx, m, u, T)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+    # merge owned entries (each rank fills only its owned entries of a zero vector)
+    def merged(key):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        return v
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    assert rel(merged("rhs"), ref["rhs"]) < 1e-12
+    assert rel(merged("T_rhs"), ref["T_rhs"]) < 1e-12
+    x = merged("x")
+    assert np.linalg.norm(x - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
+    assert rel(merged("Tx"), ref["Tx"]) < 1e-10
+    for r in results:
+        assert r["nse"][0] == ref["nse"][0] == 0
+        assert r["nse"][1] == ref["nse"][1]                      # FGMRES iterations
+        # the inner Schur GMRES stagnates near its 1e-6 target, so its count
+        # follows the summation order of the (partitioned) dot products
+        assert abs(r["nse"][2] - ref["nse"][2]) <= 0.15 * ref["nse"][2]
+        assert r["T"][1] == ref["T"][1]
+        assert np.isclose(r["cfl0"], ref["cfl0"], rtol=1e-13)
+        assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-10)
+        assert np.isclose(r["cfl"], ref["cfl"], rtol=1e-10)

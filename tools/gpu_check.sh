@@ -26,8 +26,9 @@ for s in $STEPS; do
       mkdir -p $OUT/pmc
       for ctr in FETCH_SIZE WRITE_SIZE; do
         rm -rf /tmp/pmc
-        timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d /tmp/pmc -o pmc \
-          -- python3 bench.py --refine $R --probe-schur 20 > $OUT/pmc/probe_$ctr.json 2> $OUT/pmc/probe_$ctr.err
+        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace --kernel-include-regex "${PMC_KERNELS:-k_sell_spmv|k_nse_system|k_chain}" \
+          --output-format csv -d /tmp/pmc -o pmc \
+          -- python3 bench.py --refine $R --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc/probe_$ctr.json 2> $OUT/pmc/probe_$ctr.err
         rc=$?; find /tmp/pmc -name "*counter_collection*.csv" -exec cp {} $OUT/pmc/${ctr}.csv \; ; ok $rc pmc_$ctr
       done ;;
   esac
