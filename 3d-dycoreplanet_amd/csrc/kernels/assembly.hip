@@ -18,6 +18,8 @@
 // deterministic (no atomics).
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "../device.h"
 #include "../fe_tables.h"
 
@@ -216,34 +218,52 @@ struct NseSmem {
   double S[27 * 27];       // [q][n] shape values
   double W1[27 * 8];       // [q][v] JxW * Q1 value
   double F[27 * 3];        // JxW * rhs integrand (velocity part) per q
+  double stage_pad[1024];  // write staging continues here (D..F are dead by then)
   double diag[27];         // sum_c |K_(a,c),(a,c)| per node (average-diagonal rule)
   int node[27];
   int pdof[8];
-  int spos[kNseThreads];   // write staging: destination block per lane
+  int spos[3 * 128 + 256];    // write staging: destination blocks per lane (2 / 4 per lane)
 };
+// staging: waves 0-2 take 2 x 576 doubles (A blocks + transposes), wave 3
+// 4 x 192 (B^T / B rows), all inside the dead D..stage_pad range
+static_assert(offsetof(NseSmem, diag) - offsetof(NseSmem, D) >= sizeof(double) * (3 * 1152 + 768),
+              "NSE write staging overlaps live LDS");
 
-// Wave-cooperative block scatter: every lane offers NB doubles for block pos
+// Wave-cooperative block scatter: every lane offers K blocks of NB doubles
 // (pos >= 0: add; ~pos: first touch, store; kNoBlock: nothing). The wave
-// writes them back with consecutive lanes on consecutive doubles.
-template <int NB>
-__device__ inline void wave_scatter(double* __restrict__ base, const double* v, int pos,
-                                    double* stage, int* spos, int lane) {
+// writes them back with consecutive lanes on consecutive doubles, and all
+// read-modify-write loads of the call are in flight before the first store
+// (the destinations of one call are distinct, so this only removes the
+// load-after-store serialisation the compiler must otherwise assume).
+template <int NB, int K>
+__device__ inline void wave_scatter(double* __restrict__ base, const double* const* v,
+                                    const int* pos, double* stage, int* spos, int lane) {
 #pragma unroll
-  for (int i = 0; i < NB; ++i) stage[NB * lane + i] = v[i];
-  spos[lane] = pos;
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) stage[64 * NB * k + NB * lane + i] = v[k][i];
+    spos[64 * k + lane] = pos[k];
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int J = NB * K;
+  double old[J];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
+  for (int j = 0; j < J; ++j) {
     const int e = 64 * j + lane;
-    const int blk = e / NB, comp = e - blk * NB;
-    const int p = spos[blk];
-    const double x = stage[e];
-    if (p >= 0)
-      base[NB * size_t(p) + comp] += x;
-    else if (p != kNoBlock)
-      base[NB * size_t(~p) + comp] = x;
+    const int k = e / (64 * NB), el = e - k * 64 * NB;
+    const int blk = el / NB, comp = el - blk * NB;
+    const int p = spos[64 * k + blk];
+    old[j] = p >= 0 ? base[NB * size_t(p) + comp] : 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int e = 64 * j + lane;
+    const int k = e / (64 * NB), el = e - k * 64 * NB;
+    const int blk = el / NB, comp = el - blk * NB;
+    const int p = spos[64 * k + blk];
+    if (p != kNoBlock) base[NB * size_t(p >= 0 ? p : ~p) + comp] = old[j] + stage[e];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -578,12 +598,11 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
     }
   }
   __syncthreads();   // gradient table dead: reuse it as the write staging area
-  double* stage = sh.D + 576 * wave;
-  int* spos = sh.spos + 64 * wave;
+  double* stage = sh.D + 1152 * wave;
+  int* spos = sh.spos + 128 * wave;
   if (wave < 3) {
     if (want_matrix) {
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt) wave_scatter<9>(out.A, R[tt], pos[tt], stage, spos, lane);
+      // block (a, b) and its transpose (b, a) in one call
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt) {
         double RT[9];
@@ -591,7 +610,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[tt][3 * j + i];
-        wave_scatter<9>(out.A, RT, posT[tt], stage, spos, lane);
+        const double* vv[2] = {R[tt], RT};
+        const int pp[2] = {pos[tt], posT[tt]};
+        wave_scatter<9, 2>(out.A, vv, pp, stage, spos, lane);
       }
     }
     if (rhs_lane) {
@@ -604,12 +625,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
     }
   } else if (want_matrix) {
     // B^T row (an, v) and B row (v, an) hold the same 3 values
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const double* r = &R[0][0] + 3 * k;
-      wave_scatter<3>(out.Bt, r, pos[k], stage, spos, lane);
-      wave_scatter<3>(out.B, r, posT[k], stage, spos, lane);
-    }
+    const double* vv[4] = {&R[0][0], &R[0][0] + 3, &R[0][0] + 6, &R[0][0] + 9};
+    wave_scatter<3, 4>(out.Bt, vv, pos, stage, spos, lane);
+    wave_scatter<3, 4>(out.B, vv, posT, stage, spos, lane);
   }
 }
 
