@@ -145,7 +145,10 @@ struct PhaseTimer {
 // get_maximal_velocity / get_cfl_number over the owned cells (+ MPI max)
 void velocity_stats_global(Ctx& c) {
   halo_exchange(c, c.halo_nse, c.nse_sol.p);
-  velocity_stats(c.cd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
+  if (c.feec)
+    feec_velocity_stats(c.fcd(), c.n_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
+  else
+    velocity_stats(c.cd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
   allreduce(c, c.dscal.p + 262, 2, true);
   DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned, c.dscal.p + 262, 2 * sizeof(double),
                                hipMemcpyDeviceToHost, c.stream));
@@ -559,6 +562,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->precond_built = false;  // S must be (re)formed
       return DCP_OK;
     }
+    if (option == DCP_OPT_FEEC_ZERO_MEAN) {
+      ctx->feec_zero_mean = value != 0;
+      return DCP_OK;
+    }
     fail(DCP_ERR_INVALID, "unknown option " + std::to_string(option));
   });
 }
@@ -617,6 +624,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
                    n_p, n_T, nse_c, T_c);
     }
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
+    c.feec = false;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -828,6 +836,7 @@ double* dcp_state_device_ptr(dcp_ctx* ctx, int field) {
 int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
+    require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
     NseOut out{};
@@ -859,6 +868,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
 int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
+    require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     PhaseTimer t(c, &c.timings.build_precond_ms);
     c.A_diag.zero(c.stream);
@@ -908,6 +918,15 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
     csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
     c.T_rhs.zero(c.stream);
+    if (c.feec) {
+      // velocity from the Raviart-Thomas field of nse_solution (FEEC.tpp:1000-1062)
+      for (int k = 0; k < c.n_colors(); ++k)
+        launch_feec_T_rhs(c.fcd(), c.color_begin(k), c.color_size(k), c.old_T.p, c.nse_sol.p, c.ph,
+                          c.T_fixed.p, c.T_bc.p, c.T_rhs.p, c.stream);
+      t.stop();
+      c.T_rhs_ok = true;
+      return DCP_OK;
+    }
     halo_exchange(c, c.halo_T, c.old_T.p);
     halo_exchange(c, c.halo_nse, c.nse_sol.p);
     for (int k = 0; k < c.n_colors(); ++k)
@@ -922,6 +941,7 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
 int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
+    require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     require(c.nse_assembled && c.precond_built, DCP_ERR_STATE,
             "assemble_nse_system and build_nse_preconditioner must run first");
@@ -1140,6 +1160,338 @@ int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out) {
 }
 
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FEEC variant (ExteriorCalculus::BoussinesqModel<3>, config 4)
+
+namespace {
+
+// rows -> sorted unique columns
+void build_csr(const std::vector<std::vector<int32_t>>& rows, std::vector<int32_t>& ptr,
+               std::vector<int32_t>& col) {
+  ptr.assign(rows.size() + 1, 0);
+  for (size_t r = 0; r < rows.size(); ++r) ptr[r + 1] = ptr[r] + int32_t(rows[r].size());
+  col.clear();
+  col.reserve(size_t(ptr.back()));
+  for (const auto& r : rows) col.insert(col.end(), r.begin(), r.end());
+}
+
+// make_sparsity_pattern(dof_handler, coupling, sp, constraints, false) for the
+// 19-dof FEEC cells: constrained rows/columns keep only the diagonal
+// (FEEC.tpp:82-130 system coupling, :146-185 preconditioner coupling).
+template <class Couple>
+void feec_pattern(int n, int n_cells, const std::vector<int32_t>& dofs,
+                  const std::vector<uint8_t>& fixed, Couple couple, std::vector<int32_t>& ptr,
+                  std::vector<int32_t>& col) {
+  std::vector<std::vector<int32_t>> rows(n);
+  for (int c = 0; c < n_cells; ++c) {
+    const int32_t* d = &dofs[19 * size_t(c)];
+    for (int i = 0; i < 19; ++i) {
+      if (fixed[d[i]]) continue;
+      for (int j = 0; j < 19; ++j)
+        if (!fixed[d[j]] && couple(i, j)) rows[d[i]].push_back(d[j]);
+    }
+  }
+  for (int r = 0; r < n; ++r) {
+    if (fixed[r]) rows[r].push_back(r);
+    std::sort(rows[r].begin(), rows[r].end());
+    rows[r].erase(std::unique(rows[r].begin(), rows[r].end()), rows[r].end());
+  }
+  build_csr(rows, ptr, col);
+}
+
+inline int feec_type(int i) { return i < 12 ? 0 : i < 18 ? 1 : 2; }
+
+}  // namespace
+
+extern "C" {
+
+int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr && m != nullptr, DCP_ERR_INVALID, "NULL argument");
+    Ctx& c = *ctx;
+    require(!c.comm, DCP_ERR_UNSUPPORTED, "the FEEC variant runs on one GPU (world_size 1)");
+    require(m->cell_w && m->sign_w && m->cell_u && m->sign_u && m->cell_vertices &&
+                m->cell_diameter && m->cell_T_dofs && m->w_fixed && m->u_fixed,
+            DCP_ERR_INVALID, "NULL array");
+    const int nc = m->n_cells, nw = m->n_w, nu = m->n_u, np = m->n_p, nT = m->n_T;
+    require(nc > 0 && nw > 0 && nu > 0 && np == nc && nT > 0, DCP_ERR_INVALID,
+            "invalid FEEC sizes (DGQ0: n_p == n_cells)");
+    const int n = nw + nu + np;
+    std::vector<int32_t> dofs(size_t(nc) * 19), td(size_t(nc) * 8);
+    std::vector<int8_t> sg(size_t(nc) * 19, 1);
+    for (int cell = 0; cell < nc; ++cell) {
+      for (int l = 0; l < 12; ++l) {
+        const int e = m->cell_w[12 * size_t(cell) + l];
+        const int s = m->sign_w[12 * size_t(cell) + l];
+        require(e >= 0 && e < nw && (s == 1 || s == -1), DCP_ERR_INVALID, "bad edge dof / sign");
+        dofs[19 * size_t(cell) + l] = e;
+        sg[19 * size_t(cell) + l] = int8_t(s);
+      }
+      for (int f = 0; f < 6; ++f) {
+        const int u = m->cell_u[6 * size_t(cell) + f];
+        const int s = m->sign_u[6 * size_t(cell) + f];
+        require(u >= 0 && u < nu && (s == 1 || s == -1), DCP_ERR_INVALID, "bad face dof / sign");
+        dofs[19 * size_t(cell) + 12 + f] = nw + u;
+        sg[19 * size_t(cell) + 12 + f] = int8_t(s);
+      }
+      dofs[19 * size_t(cell) + 18] = nw + nu + cell;
+      for (int v = 0; v < 8; ++v) {
+        const int t = m->cell_T_dofs[8 * size_t(cell) + v];
+        require(t >= 0 && t < nT, DCP_ERR_INVALID, "temperature dof out of range");
+        td[8 * size_t(cell) + v] = t;
+      }
+    }
+    std::vector<uint8_t> fixed(n, 0);
+    for (int e = 0; e < nw; ++e) fixed[e] = m->w_fixed[e] != 0;
+    for (int u = 0; u < nu; ++u) fixed[nw + u] = m->u_fixed[u] != 0;
+    // temperature constraints: Dirichlet lines
+    std::vector<uint8_t> Tfix(nT, 0);
+    std::vector<double> Tbc(nT, 0.0);
+    for (int l = 0; l < m->T.n_lines; ++l) {
+      const int d = m->T.line_dof[l];
+      require(d >= 0 && d < nT, DCP_ERR_INVALID, "temperature constraint out of range");
+      require(m->T.entry_ptr[l] == m->T.entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
+              "temperature constraints must be Dirichlet lines");
+      Tfix[d] = 1;
+      Tbc[d] = m->T.inhomogeneity[l];
+    }
+    // patterns: system (w:{w,u}, u:{w,u,p}, p:{u}), preconditioner (w:{w,u}, u:{w,u}, p:{w,p})
+    std::vector<int32_t> Sp, Sc, Pp, Pc;
+    feec_pattern(n, nc, dofs, fixed,
+                 [](int i, int j) {
+                   const int a = feec_type(i), b = feec_type(j);
+                   return a == 0 ? b < 2 : a == 1 ? true : b == 1;
+                 },
+                 Sp, Sc);
+    feec_pattern(n, nc, dofs, fixed,
+                 [](int i, int j) {
+                   const int a = feec_type(i), b = feec_type(j);
+                   return a < 2 ? b < 2 : b != 1;
+                 },
+                 Pp, Pc);
+    // temperature pattern
+    std::vector<std::vector<int32_t>> trows(nT);
+    for (int cell = 0; cell < nc; ++cell)
+      for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) trows[td[8 * size_t(cell) + i]].push_back(td[8 * size_t(cell) + j]);
+    for (auto& r : trows) {
+      std::sort(r.begin(), r.end());
+      r.erase(std::unique(r.begin(), r.end()), r.end());
+    }
+    std::vector<int32_t> Tp, Tc;
+    build_csr(trows, Tp, Tc);
+    std::vector<int32_t> posT(size_t(nc) * 64);
+    for (int cell = 0; cell < nc; ++cell)
+      for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) {
+          const int r = td[8 * size_t(cell) + i], col = td[8 * size_t(cell) + j];
+          const auto b = Tc.begin() + Tp[r], e = Tc.begin() + Tp[r + 1];
+          posT[64 * size_t(cell) + 8 * i + j] = int32_t(std::lower_bound(b, e, col) - Tc.begin());
+        }
+    // colouring over vertex-sharing cells (Q1 temperature dofs are the vertices)
+    std::vector<std::vector<int32_t>> vcells(nT);
+    for (int cell = 0; cell < nc; ++cell)
+      for (int v = 0; v < 8; ++v) vcells[td[8 * size_t(cell) + v]].push_back(cell);
+    std::vector<int> color(nc, -1);
+    int n_colors = 0;
+    for (int cell = 0; cell < nc; ++cell) {
+      uint64_t used = 0;
+      for (int v = 0; v < 8; ++v)
+        for (int o : vcells[td[8 * size_t(cell) + v]])
+          if (color[o] >= 0) used |= uint64_t(1) << color[o];
+      int col = 0;
+      while (col < 64 && ((used >> col) & 1)) ++col;
+      require(col < 64, DCP_ERR_UNSUPPORTED, "cell colouring needs more than 64 colours");
+      color[cell] = col;
+      n_colors = std::max(n_colors, col + 1);
+    }
+    c.color_ptr.assign(n_colors + 1, 0);
+    for (int cell = 0; cell < nc; ++cell) c.color_ptr[color[cell] + 1]++;
+    for (int k = 0; k < n_colors; ++k) c.color_ptr[k + 1] += c.color_ptr[k];
+    std::vector<int32_t> ccells(nc);
+    {
+      std::vector<int> f(c.color_ptr.begin(), c.color_ptr.end() - 1);
+      for (int cell = 0; cell < nc; ++cell) ccells[f[color[cell]]++] = cell;
+    }
+    // virtual Q2 geometry = trilinear interpolation of the vertices: the
+    // classic temperature-matrix kernel then integrates on MappingQ1
+    // (temperature_mapping(1), FEEC.tpp:20) exactly
+    std::vector<int32_t> q2(size_t(nc) * 27);
+    std::vector<double> xyz(size_t(nc) * 81);
+    for (int cell = 0; cell < nc; ++cell)
+      for (int k = 0; k < 27; ++k) {
+        const double t[3] = {0.5 * (k % 3), 0.5 * ((k / 3) % 3), 0.5 * (k / 9)};
+        q2[27 * size_t(cell) + k] = 27 * cell + k;
+        for (int d = 0; d < 3; ++d) {
+          double x = 0;
+          for (int v = 0; v < 8; ++v) {
+            const double w = ((v & 1) ? t[0] : 1 - t[0]) * (((v >> 1) & 1) ? t[1] : 1 - t[1]) *
+                             ((v >> 2) ? t[2] : 1 - t[2]);
+            x += w * m->cell_vertices[24 * size_t(cell) + 3 * v + d];
+          }
+          xyz[81 * size_t(cell) + 3 * k + d] = x;
+        }
+      }
+    DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
+    c.feec = true;
+    c.have_mesh = false;
+    c.n_cells = nc;
+    c.n_owned_cells = nc;
+    c.fe_nw = nw;
+    c.fe_nu = nu;
+    c.fe_np = np;
+    c.n_u = nw + nu;  // state API: NSE vector = [w u | p]
+    c.n_p = np;
+    c.n_T = nT;
+    c.n_u_g = c.n_u;
+    c.n_p_g = np;
+    c.n_T_g = nT;
+    c.nTo = nT;
+    c.n_vnodes = 0;
+    c.max_owned[3] = nT;
+    c.fe_dofs.upload(dofs);
+    c.fe_sign.upload(sg);
+    c.fe_X.upload(std::vector<double>(m->cell_vertices, m->cell_vertices + 24 * size_t(nc)));
+    c.diameter.upload(std::vector<double>(m->cell_diameter, m->cell_diameter + nc));
+    c.fe_fixed.upload(fixed);
+    c.cell_T.upload(td);
+    c.cell_q2.upload(q2);
+    c.xyz.upload(xyz);
+    c.T_fixed.upload(Tfix);
+    c.T_bc.upload(Tbc);
+    c.color_cells.upload(ccells);
+    c.fe_ptr.upload(Sp);
+    c.fe_col.upload(Sc);
+    c.fe_val.alloc(Sc.size());
+    c.fp_ptr.upload(Pp);
+    c.fp_col.upload(Pc);
+    c.fp_val.alloc(Pc.size());
+    c.fe_pos.alloc(size_t(nc) * 361);
+    c.fp_pos.alloc(size_t(nc) * 361);
+    feec_positions(c.fcd(), nc, c.fe_ptr.p, c.fe_col.p, c.fe_pos.p, c.stream);
+    feec_positions(c.fcd(), nc, c.fp_ptr.p, c.fp_col.p, c.fp_pos.p, c.stream);
+    c.T_ptr.upload(Tp);
+    c.T_col.upload(Tc);
+    c.Tmass.alloc(Tc.size());
+    c.Tstiff.alloc(Tc.size());
+    c.Tmat.alloc(Tc.size());
+    c.posT.upload(posT);
+    c.T_inv.alloc(nT);
+    c.fe_cellw.alloc(nc);
+    feec_cell_weights(c.fcd(), nc, c.fe_cellw.p, c.stream);
+    c.fe_dinv.alloc(nw + nu);
+    for (auto* b : {&c.fe_t1, &c.fe_t2, &c.fe_t3, &c.fe_t4}) b->alloc(n);
+    c.nse_sol.alloc(n);
+    c.old_nse.alloc(n);
+    c.nse_rhs.alloc(n);
+    c.T_sol.alloc(nT);
+    c.old_T.alloc(nT);
+    c.T_rhs.alloc(nT);
+    for (auto* b : {&c.nse_sol, &c.old_nse, &c.nse_rhs, &c.T_sol, &c.old_T, &c.T_rhs}) b->zero(c.stream);
+    free_workspaces(c);
+    {
+      std::vector<double> w(nc);
+      DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+      DCP_HIP_CHECK(hipMemcpy(w.data(), c.fe_cellw.p, nc * sizeof(double), hipMemcpyDeviceToHost));
+      c.fe_wsum = 0;
+      for (double x : w) c.fe_wsum += x;
+    }
+    c.have_mesh = true;
+    c.fe_assembled = c.fe_precond = c.T_matrix_ok = c.T_rhs_ok = false;
+    return DCP_OK;
+  });
+}
+
+int dcp_feec_assemble_nse_system(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
+    PhaseTimer t(c, &c.timings.assemble_nse_ms);
+    c.fe_val.zero(c.stream);
+    c.nse_rhs.zero(c.stream);
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_feec_system(c.fcd(), c.color_begin(k), c.color_size(k), c.fe_pos.p, c.old_nse.p,
+                         c.old_T.p, c.ph, c.fe_val.p, c.nse_rhs.p, c.stream);
+    t.stop();
+    c.fe_assembled = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_feec_build_nse_preconditioner(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
+    PhaseTimer t(c, &c.timings.build_precond_ms);
+    c.fp_val.zero(c.stream);
+    for (int k = 0; k < c.n_colors(); ++k)
+      launch_feec_precond(c.fcd(), c.color_begin(k), c.color_size(k), c.fp_pos.p, c.ph, c.fp_val.p,
+                          c.stream);
+    t.stop();
+    c.fe_precond = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_feec_solve_nse(dcp_ctx* ctx, int* iterations) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.feec && c.fe_assembled, DCP_ERR_STATE, "assemble the FEEC system first");
+    PhaseTimer t(c, &c.timings.solve_nse_ms);
+    const int rc = feec_solve_nse(c, iterations);
+    t.stop();
+    return rc;
+  });
+}
+
+int dcp_feec_cell_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
+    require(K && f && first >= 0 && n > 0 && first + n <= c.n_cells, DCP_ERR_INVALID,
+            "bad cell range");
+    DBuf<double> dK, df;
+    dK.alloc(size_t(n) * 361);
+    df.alloc(size_t(n) * 19);
+    launch_feec_elements(c.fcd(), first, n, c.old_nse.p, c.old_T.p, c.ph, dK.p, df.p, c.stream);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    DCP_HIP_CHECK(hipMemcpy(K, dK.p, dK.n * sizeof(double), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(f, df.p, df.n * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_feec_matrix_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,
+                           double* vals) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(c.feec && nnz, DCP_ERR_INVALID, "no FEEC mesh / NULL nnz");
+    const DBuf<int32_t>& P = which == 0 ? c.fe_ptr : c.fp_ptr;
+    const DBuf<int32_t>& C = which == 0 ? c.fe_col : c.fp_col;
+    const DBuf<double>& V = which == 0 ? c.fe_val : c.fp_val;
+    *nnz = int64_t(C.n);
+    if (!rowptr) return DCP_OK;
+    require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    DCP_HIP_CHECK(hipMemcpy(rowptr, P.p, P.n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(cols, C.p, C.n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(vals, V.p, V.n * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
 // Host setup helpers
 
 struct dcp_host_mesh {
@@ -1148,6 +1500,7 @@ struct dcp_host_mesh {
   TemperatureDofs tdofs;
   std::vector<int32_t> cell_nse;
   std::vector<double> cell_geom;
+  std::unique_ptr<FeecDofs> feec;  // built on first request
 };
 
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
@@ -1199,6 +1552,33 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
   out->cell_diameter = m.cell_diameter.data();
   out->node_xyz = m.xyz.data();
   out->nse = view_of(h->nse);
+  out->T = view_of(h->T);
+  return DCP_OK;
+}
+
+int dcp_host_feec_view_get(dcp_host_mesh* h, dcp_feec_mesh* out) {
+  if (!h || !out) return DCP_ERR_INVALID;
+  try {
+    if (!h->feec) h->feec = std::make_unique<FeecDofs>(feec_dofs(h->mesh));
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return DCP_ERR_INVALID;
+  }
+  const FeecDofs& f = *h->feec;
+  out->n_cells = h->mesh.n_cells;
+  out->n_w = f.n_w;
+  out->n_u = f.n_u;
+  out->n_p = f.n_p;
+  out->n_T = h->tdofs.n_dofs;
+  out->cell_w = f.cell_w.data();
+  out->sign_w = f.sign_w.data();
+  out->cell_u = f.cell_u.data();
+  out->sign_u = f.sign_u.data();
+  out->cell_vertices = f.cell_vertices.data();
+  out->cell_diameter = h->mesh.cell_diameter.data();
+  out->cell_T_dofs = h->tdofs.cell_dofs.data();
+  out->w_fixed = f.w_boundary.data();
+  out->u_fixed = f.u_boundary.data();
   out->T = view_of(h->T);
   return DCP_OK;
 }

@@ -9,6 +9,7 @@
 #include "../../include/dcp.h"
 #include "comm.h"
 #include "device.h"
+#include "feec.h"
 
 namespace dcp {
 
@@ -124,6 +125,24 @@ struct Ctx {
   long schur_calls = 0;
   bool time_schur = false;
 
+  // ---- FEEC variant (config 4): n_u = n_w + n_u(faces), n_p = cells
+  bool feec = false;
+  bool feec_zero_mean = true;          // parameters.correct_pressure_to_zero_mean
+  int fe_nw = 0, fe_nu = 0, fe_np = 0;
+  DBuf<int32_t> fe_dofs;
+  DBuf<int8_t> fe_sign;
+  DBuf<double> fe_X, fe_cellw;
+  DBuf<uint8_t> fe_fixed;
+  DBuf<int32_t> fe_ptr, fe_col, fe_pos, fp_ptr, fp_col, fp_pos;
+  DBuf<double> fe_val, fp_val, fe_dinv;   // system, preconditioner, Jacobi of the w/u diagonal blocks
+  double fe_wsum = 0;                      // sum of the mean-value weights
+  bool fe_assembled = false, fe_precond = false;
+  std::vector<double*> fe_v, fe_s, fe_n;  // Krylov bases: outer, shifted Schur, nested Schur
+  DBuf<double> fe_t1, fe_t2, fe_t3, fe_t4;
+  FeecCellData fcd() const {
+    return FeecCellData{n_cells, fe_dofs.p, fe_sign.p, fe_X.p, diameter.p, fe_fixed.p, cell_T.p};
+  }
+
   Seg seg_nse() const { return Seg{3 * nvo, n_u, 3 * nvo + npo, 0}; }
   Seg seg_p() const { return Seg::all(npo, 1); }
   Seg seg_v() const { return Seg::all(3 * nvo, 2); }
@@ -158,6 +177,8 @@ int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_s
                                int* inner);
 void free_workspaces(Ctx& c);
 void ensure_workspaces(Ctx& c);
+// FEEC solve (solve_NSE_block_preconditioned, boussineq_model_FEEC.tpp:1268-1477)
+int feec_solve_nse(Ctx& c, int* iterations);
 // multi-GPU plumbing (no-ops on one GPU)
 int chain_width(const Ctx& c, Seg g);
 void allreduce(Ctx& c, double* buf, size_t n, bool max = false);

@@ -217,6 +217,12 @@ void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, dou
 void velocity_stats(const CellData& cd, int n_cells, const double* u, double* out2, hipStream_t s);
 // min/max of a vector -> out[0] = min, out[1] = max
 void minmax(int n, const double* x, double* out2, hipStream_t s);
+// block of a CSR matrix: rows [r0, r1), columns [c0, c1) (other columns skipped):
+// y[r - r0] (+)= sum_k val[k] x[col[k] - c0]
+void spmv_block(int r0, int r1, int c0, int c1, const int32_t* ptr, const int32_t* col,
+                const double* val, const double* x, double* y, bool add, hipStream_t s);
+void shift(int n, DScal c, double* y, hipStream_t s);                         // y += c
+void zero_fixed(int n, const uint8_t* fixed, double* y, hipStream_t s);       // y[fixed] = 0
 // halo staging: buf[k] = v[pos[k]] / v[pos[k]] = buf[k], k < n
 void gather(int n, const int32_t* pos, const double* v, double* buf, hipStream_t s);
 void scatter(int n, const int32_t* pos, const double* buf, double* v, hipStream_t s);

@@ -423,6 +423,40 @@ __global__ void k_minmax_final(int nb, const double* partials, double* out2) {
   out2[1] = hi;
 }
 
+// rows [r0, r1) x columns [c0, c1) of a CSR matrix: y[r - r0] (+)= sum val x[col - c0]
+// (one 16-lane group per row, fixed-order shuffle reduction)
+__global__ __launch_bounds__(kBlock) void k_spmv_block(int r0, int r1, int c0, int c1,
+                                                       const int32_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ col,
+                                                       const double* __restrict__ val,
+                                                       const double* __restrict__ x,
+                                                       double* __restrict__ y, int add) {
+  constexpr int G = 16;
+  const int lane = threadIdx.x % G;
+  const long row = r0 + (long(blockIdx.x) * kBlock + threadIdx.x) / G;
+  if (row >= r1) return;
+  double acc = 0;
+  for (int k = ptr[row] + lane; k < ptr[row + 1]; k += G) {
+    const int c = col[k];
+    if (c >= c0 && c < c1) acc += val[k] * x[c - c0];
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, G);
+  if (lane == 0) {
+    double* yp = y + (row - r0);
+    *yp = add ? *yp + acc : acc;
+  }
+}
+__global__ void k_shift(int n, DScal c, double* y) {
+  const double cf = c.p ? c.m * (*c.p) : c.m;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    y[i] += cf;
+}
+__global__ void k_zero_fixed(int n, const uint8_t* __restrict__ fixed, double* y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
+    if (fixed[i]) y[i] = 0.0;
+}
+
 __global__ void k_group_reduce(size_t n, int nbufs, BufTable t, double* __restrict__ out, int mx) {
   for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += size_t(gridDim.x) * kBlock) {
     double v = t.p[0][i];
@@ -624,6 +658,23 @@ void minmax(int n, const double* x, double* out2, hipStream_t s) {
   double* partials = out2 + 2;
   hipLaunchKernelGGL(k_minmax_partial, dim3(kReduceBlocks), dim3(kBlock), 0, s, n, x, partials);
   hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, s, kReduceBlocks, partials, out2);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void spmv_block(int r0, int r1, int c0, int c1, const int32_t* ptr, const int32_t* col,
+                const double* val, const double* x, double* y, bool add, hipStream_t s) {
+  if (r1 <= r0) return;
+  const long threads = long(r1 - r0) * 16;
+  hipLaunchKernelGGL(k_spmv_block, dim3(int((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, r0,
+                     r1, c0, c1, ptr, col, val, x, y, add ? 1 : 0);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void shift(int n, DScal c, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_shift, dim3(grid_for(n)), dim3(kBlock), 0, s, n, c, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void zero_fixed(int n, const uint8_t* fixed, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_zero_fixed, dim3(grid_for(n)), dim3(kBlock), 0, s, n, fixed, y);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -115,6 +115,23 @@ struct TemperatureDofs {
 };
 TemperatureDofs temperature_dofs(const Mesh& m, int degree);
 
+// FEEC DoF topology (feec_mesh.cpp): lowest-order Nedelec (w, edges),
+// Raviart-Thomas (u, faces), DGQ0 (p, cells); local order = deal.II line /
+// face order. Signs orient each cell's local functions to the global DoFs.
+struct FeecDofs {
+  int n_w = 0, n_u = 0, n_p = 0;
+  std::vector<int32_t> cell_w;         // [n_cells][12] edge ids
+  std::vector<int8_t> sign_w;          // [n_cells][12]
+  std::vector<int32_t> cell_u;         // [n_cells][6] face ids
+  std::vector<int8_t> sign_u;          // [n_cells][6]
+  std::vector<uint8_t> w_boundary;     // [n_w] edge on the domain boundary
+  std::vector<uint8_t> u_boundary;     // [n_u] face on the domain boundary
+  std::vector<double> cell_vertices;   // [n_cells][8][3] (MappingQ1 geometry)
+};
+FeecDofs feec_dofs(const Mesh& m);
+extern const int kFeecLineVertex[12][2];
+extern const int kFeecFaceVertex[6][4];
+
 // FESystem-ordered (deal.II local order, 89 per cell) global NSE dof indices,
 // i.e. what cell->get_dof_indices() returns in the reference.
 std::vector<int32_t> nse_cell_dofs_dealii(const Mesh& m);

@@ -541,7 +541,7 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
 }
 
 void free_workspaces(Ctx& c) {
-  for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v}) {
+  for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v, &c.fe_v, &c.fe_s, &c.fe_n}) {
     for (double* p : *pool) (void)hipFree(p);
     pool->clear();
   }
@@ -602,6 +602,109 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   if (outer) *outer = acc1 + acc2;
   if (inner_out) *inner_out = inner;
   return status;
+}
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// FEEC solver chain (boussineq_model_FEEC.tpp:1268-1477) on the [w | u | p]
+// CSR nse_matrix; blocks are applied as row/column windows of it.
+struct FeecOps {
+  Ctx& c;
+  int nw, nu, np, ou, op, n;
+  const int32_t* ptr;
+  const int32_t* col;
+  const double* val;
+  // y = block(I, J) x
+  void block(int r0, int r1, int c0, int c1, const double* x, double* y, bool add) const {
+    spmv_block(r0, r1, c0, c1, ptr, col, val, x, y, add, c.stream);
+  }
+  // ShiftedSchurComplement::vmult (shifted_schur_complement.hpp:155-171):
+  // y = M_u x - B_10 D_w^-1 B_01 x
+  void shifted(const double* x, double* y) const {
+    block(ou, op, ou, op, x, y, false);              // block_11
+    block(0, nw, ou, op, x, c.fe_t3.p, false);       // tmp1 = block_01 x
+    mul(nw, c.fe_dinv.p, c.fe_t3.p, c.fe_t4.p, c.stream);  // tmp2 = Mw Jacobi tmp1
+    scale(nw, DScal{nullptr, -1.0}, c.fe_t4.p, c.stream);
+    block(ou, op, 0, nw, c.fe_t4.p, y, true);        // += block_10 tmp2
+  }
+  // SchurComplementLowerBlock::vmult, do_full_solve = false
+  // (schur_complement.hpp:256-276): y = B_21 D_u^-1 B_12 x
+  void lower(const double* x, double* y) const {
+    block(ou, op, op, n, x, c.fe_t3.p, false);
+    mul(nu, c.fe_dinv.p + nw, c.fe_t3.p, c.fe_t4.p, c.stream);
+    block(op, n, ou, op, c.fe_t4.p, y, false);
+  }
+};
+
+// BlockSchurPreconditionerFEEC::vmult (block_schur_preconditioner.hpp:115-147)
+void feec_precondition(Ctx& c, const FeecOps& o, const double* src, double* dst) {
+  const int nw = o.nw, nu = o.nu, np = o.np, ou = o.ou, op = o.op;
+  // dst_w = Mw^-1 src_w, Mw^-1 = the Jacobi preconditioner (Q16)
+  mul(nw, c.fe_dinv.p, src, dst, c.stream);
+  // utmp1 = src_u - B_10 dst_w ; dst_u = ApproxShiftedSchurComplementInverse(utmp1)
+  double* t1 = c.fe_t1.p;
+  o.block(ou, op, 0, nw, dst, t1, false);
+  sadd(nu, -1.0, 1.0, src + ou, t1, c.stream);
+  {
+    // GMRES (30 tmp vectors) <= 30 iterations, tol 1e-6 |src|, left
+    // preconditioner Mu Jacobi, failure swallowed; initial guess = dst_u
+    // (shifted_schur_complement.hpp:271-298)
+    const double nrm = std::sqrt(dot_host(c, Seg::all(nu), t1, t1, kSlotB));
+    Control ctl{30, 1e-6 * nrm};
+    Op A = [&](const double* x, double* y) { o.shifted(x, y); };
+    Op P = [&](const double* x, double* y) { mul(nu, c.fe_dinv.p + nw, x, y, c.stream); };
+    (void)gmres(c, nu, Seg::all(nu), A, &P, dst + ou, t1, ctl, c.fe_s, 30);
+  }
+  // ptmp = -2 src_p + B_21 dst_u (Q15) ; dst_p = ApproxNestedSchurComplementInverse(ptmp)
+  double* t2 = c.fe_t2.p;
+  equ(np, DScal{nullptr, -2.0}, src + op, t2, c.stream);
+  o.block(op, o.n, ou, op, dst + ou, t2, true);
+  {
+    // GMRES <= 100 iterations, tol 1e-6 |src|, identity, failure swallowed
+    // (nested_schur_complement.hpp:287-322)
+    const double nrm = std::sqrt(dot_host(c, Seg::all(np), t2, t2, kSlotB));
+    Control ctl{100, 1e-6 * nrm};
+    Op A = [&](const double* x, double* y) { o.lower(x, y); };
+    (void)gmres(c, np, Seg::all(np), A, nullptr, dst + op, t2, ctl, c.fe_n, 30);
+  }
+  if (c.feec_zero_mean) {
+    // dst -= compute_mean_value(DGQ0, QGauss(1), dst) (Q18: consistent cell map)
+    gdot(c, Seg::all(np), c.fe_cellw.p, dst + op, kSlotC);
+    fill(1, c.fe_wsum, slot(c, kSlotD), c.stream);
+    scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);
+    shift(np, DScal{slot(c, kSlotA), -1.0}, dst + op, c.stream);
+  }
+}
+
+}  // namespace
+
+int feec_solve_nse(Ctx& c, int* iterations) {
+  const int nw = c.fe_nw, nu = c.fe_nu, np = c.fe_np, n = nw + nu + np;
+  FeecOps o{c, nw, nu, np, nw, nw + nu, n, c.fe_ptr.p, c.fe_col.p, c.fe_val.p};
+  // Mw / Mu Jacobi: diagonals of nse_matrix.block(0,0) and block(1,1) (:1288-1303)
+  csr_diag_inverse(nw + nu, c.fe_ptr.p, c.fe_col.p, c.fe_val.p, c.fe_dinv.p, c.stream);
+  DBuf<double> x;
+  x.alloc(n);
+  copy(n, c.nse_sol.p, x.p, c.stream);
+  scale(np, DScal{nullptr, c.ph.dt}, x.p + o.op, c.stream);  // :1345 block(2) *= dt
+  const double tol = 1e-8 * std::sqrt(dot_host(c, Seg::all(n), c.nse_rhs.p, c.nse_rhs.p, kSlotA));
+  Control ctl{500, tol};
+  // SolverGMRES(AdditionalData(100)): fresh (zero) temporary vectors per solve;
+  // the preconditioner's output vector is the initial guess of its inner solves
+  ensure_pool(c.fe_v, 100, size_t(n));
+  for (int k = 0; k < 100; ++k) fill(n, 0.0, c.fe_v[k], c.stream);
+  Op A = [&](const double* xx, double* y) {
+    spmv_csr(n, c.fe_ptr.p, c.fe_col.p, c.fe_val.p, xx, y, false, c.stream);
+  };
+  Op P = [&](const double* s, double* d) { feec_precondition(c, o, s, d); };
+  const State st = gmres(c, n, Seg::all(n), A, &P, x.p, c.nse_rhs.p, ctl, c.fe_v, 100);
+  zero_fixed(n, c.fe_fixed.p, x.p, c.stream);                // constraints.distribute (:1440)
+  scale(np, DScal{nullptr, 1.0 / c.ph.dt}, x.p + o.op, c.stream);  // :1446 block(2) /= dt
+  copy(n, x.p, c.nse_sol.p, c.stream);
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (iterations) *iterations = int(ctl.last_step);
+  return st == kSuccess ? DCP_OK : DCP_NOT_CONVERGED;
 }
 
 int solve_temperature(Ctx& c, int* iters, double* T_range) {

@@ -26,6 +26,7 @@ DCP_ERR_INVALID, DCP_ERR_UNSUPPORTED, DCP_ERR_DEVICE, DCP_ERR_STATE = -1, -2, -3
 NSE_SOLUTION, OLD_NSE_SOLUTION, T_SOLUTION, OLD_T_SOLUTION, NSE_RHS, T_RHS = range(6)
 ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
 OPT_SCHUR_EXPLICIT = 1
+OPT_FEEC_ZERO_MEAN = 2
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -40,6 +41,9 @@ EXPORTED = [
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
     "dcp_host_mesh_view_get", "dcp_host_mesh_initial_temperature", "dcp_prm_load",
     "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
+    "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
+    "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
+    "dcp_host_feec_view_get",
 ]
 
 
@@ -89,6 +93,18 @@ class MeshView(C.Structure):
         ("cell_nse_dofs", C.POINTER(C.c_int32)), ("cell_T_dofs", C.POINTER(C.c_int32)),
         ("cell_geometry", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
         ("node_xyz", C.POINTER(C.c_double)), ("nse", Constraints), ("T", Constraints),
+    ]
+
+
+class FeecMeshView(C.Structure):
+    _fields_ = [
+        ("n_cells", C.c_int), ("n_w", C.c_int), ("n_u", C.c_int), ("n_p", C.c_int),
+        ("n_T", C.c_int),
+        ("cell_w", C.POINTER(C.c_int32)), ("sign_w", C.POINTER(C.c_int8)),
+        ("cell_u", C.POINTER(C.c_int32)), ("sign_u", C.POINTER(C.c_int8)),
+        ("cell_vertices", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
+        ("cell_T_dofs", C.POINTER(C.c_int32)), ("w_fixed", C.POINTER(C.c_uint8)),
+        ("u_fixed", C.POINTER(C.c_uint8)), ("T", Constraints),
     ]
 
 
@@ -150,6 +166,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_host_mesh_view_get.argtypes = [P, C.POINTER(MeshView)]
     lib.dcp_host_mesh_initial_temperature.argtypes = [P, P]
     lib.dcp_prm_load.argtypes = [C.c_char_p, C.POINTER(RunParams), C.c_char_p, I]
+    lib.dcp_host_feec_view_get.argtypes = [P, C.POINTER(FeecMeshView)]
+    lib.dcp_feec_mesh_upload.argtypes = [P, C.POINTER(FeecMeshView)]
+    for f in ("dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner"):
+        getattr(lib, f).argtypes = [P]
+    lib.dcp_feec_solve_nse.argtypes = [P, C.POINTER(I)]
+    lib.dcp_feec_cell_system.argtypes = [P, I, I, P, P]
+    lib.dcp_feec_matrix_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_nccl_unique_id.argtypes = [P]
     lib.dcp_group_create.argtypes = [I]
     lib.dcp_group_create.restype = P
@@ -215,7 +238,7 @@ class HostMesh:
     """Refined shell / cube with DoFs and constraints (setup_dofs restated)."""
 
     def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1,
-                 normals="consistent"):
+                 normals="consistent", feec=False):
         if normals not in ("consistent", "radial"):
             raise ValueError("normals must be 'consistent' or 'radial'")
         h = lib().dcp_host_mesh_create(int(cuboid), int(refine), float(R0), float(R1),
@@ -239,6 +262,7 @@ class HostMesh:
             self.T_constraints = ConstraintSet.from_view(v.T)
             self.T0 = np.zeros(self.n_T)
             lib().dcp_host_mesh_initial_temperature(h, _ptr(self.T0))
+            self.feec = FeecTopology(h, self) if feec else None
         finally:
             lib().dcp_host_mesh_destroy(h)
         self.cuboid = bool(cuboid)
@@ -257,6 +281,51 @@ class HostMesh:
             raise DcpError(rc, lib().dcp_last_error(None).decode())
         return ncol.value
         self.temperature_degree = temperature_degree
+
+
+class FeecTopology:
+    """FEEC DoFs of a host mesh (dcp_host_feec_view_get): Nedelec edges (w),
+    Raviart-Thomas faces (u), DGQ0 cells (p), with orientation signs."""
+
+    def __init__(self, h, mesh):
+        v = FeecMeshView()
+        rc = lib().dcp_host_feec_view_get(h, C.byref(v))
+        if rc != DCP_OK:
+            raise DcpError(rc, lib().dcp_last_error(None).decode())
+        nc = v.n_cells
+        self.n_cells, self.n_w, self.n_u, self.n_p, self.n_T = nc, v.n_w, v.n_u, v.n_p, v.n_T
+        self.cell_w = _arr(v.cell_w, nc * 12, np.int32).reshape(-1, 12)
+        self.sign_w = _arr(v.sign_w, nc * 12, np.int8).reshape(-1, 12)
+        self.cell_u = _arr(v.cell_u, nc * 6, np.int32).reshape(-1, 6)
+        self.sign_u = _arr(v.sign_u, nc * 6, np.int8).reshape(-1, 6)
+        self.cell_vertices = _arr(v.cell_vertices, nc * 24, np.float64).reshape(-1, 8, 3)
+        self.cell_diameter = _arr(v.cell_diameter, nc, np.float64)
+        self.cell_T_dofs = _arr(v.cell_T_dofs, nc * 8, np.int32).reshape(-1, 8)
+        self.w_fixed = _arr(v.w_fixed, self.n_w, np.uint8)
+        self.u_fixed = _arr(v.u_fixed, self.n_u, np.uint8)
+        self.T_constraints = mesh.T_constraints
+        self.n = self.n_w + self.n_u + self.n_p
+        # global [w | u | p] dofs of each cell's 19 local dofs and their signs
+        self.cell_dofs = np.concatenate(
+            [self.cell_w, self.n_w + self.cell_u,
+             (self.n_w + self.n_u + np.arange(nc, dtype=np.int32))[:, None]], axis=1)
+        self.signs = np.concatenate([self.sign_w, self.sign_u, np.ones((nc, 1), np.int8)], axis=1)
+        self.fixed = np.concatenate([self.w_fixed, self.u_fixed, np.zeros(self.n_p, np.uint8)])
+
+    def as_struct(self):
+        v = FeecMeshView()
+        v.n_cells, v.n_w, v.n_u, v.n_p, v.n_T = self.n_cells, self.n_w, self.n_u, self.n_p, self.n_T
+        for name, arr, ct in (("cell_w", self.cell_w, C.c_int32), ("sign_w", self.sign_w, C.c_int8),
+                              ("cell_u", self.cell_u, C.c_int32), ("sign_u", self.sign_u, C.c_int8),
+                              ("cell_vertices", self.cell_vertices, C.c_double),
+                              ("cell_diameter", self.cell_diameter, C.c_double),
+                              ("cell_T_dofs", self.cell_T_dofs, C.c_int32),
+                              ("w_fixed", self.w_fixed, C.c_uint8),
+                              ("u_fixed", self.u_fixed, C.c_uint8)):
+            setattr(v, name, arr.ctypes.data_as(C.POINTER(ct)))
+        self._tc = self.T_constraints.as_struct()
+        v.T = self._tc
+        return v
 
 
 def load_prm(path: str) -> RunParams:
@@ -366,6 +435,7 @@ class Context:
         self._check(lib().dcp_set_option(self._h, OPT_SCHUR_EXPLICIT, int(bool(on))))
 
     def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
+        self._feec_view = None
         nc = (nse_constraints or m.nse_constraints).as_struct()
         tc = (T_constraints or m.T_constraints).as_struct()
         self._keep = (m, nse_constraints, T_constraints)
@@ -375,10 +445,49 @@ class Context:
             C.byref(nc), C.byref(tc)))
         self.mesh = m
 
+    # -- FEEC variant (ExteriorCalculus::BoussinesqModel<3>)
+    def upload_feec_mesh(self, m: HostMesh):
+        if m.feec is None:
+            raise ValueError("HostMesh(feec=True) required")
+        self._feec_view = m.feec.as_struct()
+        self._keep = (m,)
+        self._check(lib().dcp_feec_mesh_upload(self._h, C.byref(self._feec_view)))
+        self.mesh = m
+
+    def set_feec_zero_mean(self, on: bool):
+        self._check(lib().dcp_set_option(self._h, OPT_FEEC_ZERO_MEAN, int(bool(on))))
+
+    def feec_assemble_nse_system(self):
+        self._check(lib().dcp_feec_assemble_nse_system(self._h))
+
+    def feec_build_nse_preconditioner(self):
+        self._check(lib().dcp_feec_build_nse_preconditioner(self._h))
+
+    def feec_solve_nse(self):
+        it = C.c_int(0)
+        rc = self._check(lib().dcp_feec_solve_nse(self._h, C.byref(it)), allow_not_converged=True)
+        return rc, it.value
+
+    def feec_cell_system(self, first, n):
+        K, f = np.zeros((n, 19, 19)), np.zeros((n, 19))
+        self._check(lib().dcp_feec_cell_system(self._h, first, n, _ptr(K), _ptr(f)))
+        return K, f
+
+    def feec_matrix_csr(self, which=0):
+        nnz = C.c_int64(0)
+        self._check(lib().dcp_feec_matrix_export(self._h, which, C.byref(nnz), None, None, None))
+        n = self.mesh.feec.n
+        rp, cols, vals = np.zeros(n + 1, np.int32), np.zeros(nnz.value, np.int32), np.zeros(nnz.value)
+        self._check(lib().dcp_feec_matrix_export(self._h, which, C.byref(nnz), _ptr(rp), _ptr(cols),
+                                                 _ptr(vals)))
+        return rp, cols, vals
+
     # -- state
     def _size(self, field):
         m = self.mesh
-        return m.n_u + m.n_p if field in (NSE_SOLUTION, OLD_NSE_SOLUTION, NSE_RHS) else m.n_T
+        if field in (NSE_SOLUTION, OLD_NSE_SOLUTION, NSE_RHS):
+            return m.feec.n if getattr(self, "_feec_view", None) is not None else m.n_u + m.n_p
+        return m.n_T
 
     def set_state(self, field, values):
         a = np.ascontiguousarray(values, dtype=np.float64)

@@ -207,6 +207,42 @@ typedef struct {
 } dcp_timings;
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
 
+/* FEEC variant --------------------------------------------------------------
+ * ExteriorCalculus::BoussinesqModel<3> (boussineq_model_FEEC.tpp, config 4):
+ * lowest-order Nedelec vorticity w (edges), Raviart-Thomas velocity u (faces),
+ * DGQ0 pressure p (cells), MappingQ1. NSE state vector = [w | u | p]
+ * (n_w + n_u + n_p); temperature as in the classic model (Q1). A context
+ * holds either a classic or an FEEC mesh; the temperature calls, CFL / max
+ * velocity and state calls dispatch on it. One GPU (world_size 1). */
+typedef struct {
+  int n_cells, n_w, n_u, n_p, n_T;
+  const int32_t* cell_w;          /* [n_cells][12] edge dofs, deal.II line order */
+  const int8_t* sign_w;           /* [n_cells][12] +-1 local edge direction vs global */
+  const int32_t* cell_u;          /* [n_cells][6] face dofs, deal.II face order */
+  const int8_t* sign_u;           /* [n_cells][6] +-1 local flux direction vs global */
+  const double* cell_vertices;    /* [n_cells][8][3] (lexicographic vertices) */
+  const double* cell_diameter;    /* [n_cells] */
+  const int32_t* cell_T_dofs;     /* [n_cells][8] */
+  const uint8_t* w_fixed;         /* [n_w] boundary edge: w = 0 (FEEC.tpp:311-350) */
+  const uint8_t* u_fixed;         /* [n_u] boundary face: u.n = 0 */
+  dcp_constraints T;              /* temperature constraints */
+} dcp_feec_mesh;
+int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m);
+/* assemble_nse_system (FEEC.tpp:669-873) */
+int dcp_feec_assemble_nse_system(dcp_ctx* ctx);
+/* assemble_nse_preconditioner / build_nse_preconditioner (FEEC.tpp:509-660) */
+int dcp_feec_build_nse_preconditioner(dcp_ctx* ctx);
+/* solve_NSE_block_preconditioned (FEEC.tpp:1268-1477): GMRES(100) <= 500 with
+ * BlockSchurPreconditionerFEEC; DCP_NOT_CONVERGED if it does not converge. */
+int dcp_feec_solve_nse(dcp_ctx* ctx, int* iterations);
+/* DCP_OPT_FEEC_ZERO_MEAN (default 1): parameters.correct_pressure_to_zero_mean */
+enum { DCP_OPT_FEEC_ZERO_MEAN = 2 };
+/* element matrices / rhs of cells [first, first+n): K [n][19][19], f [n][19] */
+int dcp_feec_cell_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
+/* which = 0: nse_matrix, 1: nse_preconditioner_matrix (CSR, n_w+n_u+n_p rows) */
+int dcp_feec_matrix_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,
+                           double* vals);
+
 /* Host setup helpers (mesh generator, .prm) ----------------------------- */
 typedef struct dcp_host_mesh dcp_host_mesh;
 /* Builds the refined shell (cuboid = 0) or cube, DoFs and constraints the way
@@ -225,6 +261,9 @@ typedef struct {
   dcp_constraints nse, T;
 } dcp_host_mesh_view;
 int dcp_host_mesh_view_get(const dcp_host_mesh* m, dcp_host_mesh_view* out);
+/* FEEC topology of the host mesh (edges, faces, signs, boundary flags); the
+ * arrays stay owned by the host mesh. */
+int dcp_host_feec_view_get(dcp_host_mesh* m, dcp_feec_mesh* out);
 /* T dof values of the initial temperature at the support points. */
 int dcp_host_mesh_initial_temperature(const dcp_host_mesh* m, double* T);
 

@@ -1158,3 +1158,564 @@ extern "C" double orc_cfl(const orc_model* m, const double* sol, const double* d
   }
   return cfl;
 }
+
+// ===========================================================================
+// FEEC variant: ExteriorCalculus::BoussinesqModel<3> (boussineq_model_FEEC.tpp)
+// FESystem(FE_Nedelec(0), FE_RaviartThomas(0), FE_DGQ(0)) with MappingQ1; local
+// dofs 0..11 edges (deal.II line order), 12..17 faces, 18 cell. Orientation
+// signs (one per local dof) stand for deal.II's line orientation (Nedelec) and
+// for the RT face-sign fix of utilities.cc:20-45.
+
+namespace {
+
+const int kLineVtx[12][2] = {{0, 2}, {1, 3}, {0, 1}, {2, 3}, {4, 6}, {5, 7},
+                             {4, 5}, {6, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
+
+// reference coordinate d of vertex v (lexicographic)
+int vbit(int v, int d) { return (v >> d) & 1; }
+
+// MappingQ1 (trilinear) at xi: J (dx_i/dxi_j) and x
+void map_q1(const double* X, const double* xi, double J[3][3], Vec3& x) {
+  for (int i = 0; i < 3; ++i) {
+    x[i] = 0;
+    for (int j = 0; j < 3; ++j) J[i][j] = 0;
+  }
+  for (int v = 0; v < 8; ++v) {
+    double s = 1, g[3] = {1, 1, 1};
+    for (int d = 0; d < 3; ++d) {
+      const double l = lag1(vbit(v, d), xi[d]), dl = dlag1(vbit(v, d), xi[d]);
+      s *= l;
+      for (int e = 0; e < 3; ++e) g[e] *= (e == d ? dl : l);
+    }
+    for (int i = 0; i < 3; ++i) {
+      x[i] += X[3 * v + i] * s;
+      for (int j = 0; j < 3; ++j) J[i][j] += X[3 * v + i] * g[j];
+    }
+  }
+}
+
+double det3(const double J[3][3]) {
+  return J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+         J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+         J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+}
+
+void inv3(const double J[3][3], double I[3][3]) {
+  const double d = det3(J);
+  I[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / d;
+  I[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / d;
+  I[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / d;
+  I[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / d;
+  I[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / d;
+  I[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / d;
+  I[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / d;
+  I[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / d;
+  I[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / d;
+}
+
+// FEValues of the FEEC system element at tensor points (n1d Gauss points, or
+// the given 1D point set with weights)
+struct FeecValues {
+  int nq = 0;
+  std::vector<double> JxW;
+  std::vector<Vec3> xq;
+  std::vector<Vec3> w, cw, u;   // [q][12], [q][12], [q][6]
+  std::vector<double> du;       // [q][6]
+  void reinit(const double* X, const signed char* sgn, int n1, const double* px,
+              const double* pw) {
+    nq = n1 * n1 * n1;
+    JxW.assign(nq, 0);
+    xq.assign(nq, Vec3());
+    w.assign(size_t(nq) * 12, Vec3());
+    cw.assign(size_t(nq) * 12, Vec3());
+    u.assign(size_t(nq) * 6, Vec3());
+    du.assign(size_t(nq) * 6, 0);
+    for (int q = 0; q < nq; ++q) {
+      const int ia = q % n1, ib = (q / n1) % n1, ic = q / (n1 * n1);
+      const double xi[3] = {px[ia], px[ib], px[ic]};
+      double J[3][3], Ji[3][3];
+      map_q1(X, xi, J, xq[q]);
+      const double det = det3(J);
+      inv3(J, Ji);
+      JxW[q] = det * (pw ? pw[ia] * pw[ib] * pw[ic] : 1.0);
+      // Nedelec: N = prod_{transverse c} l_{s_c}(xi_c) e_axis (unit tangential
+      // moment along the edge), covariant Piola
+      for (int l = 0; l < 12; ++l) {
+        const int a = kLineVtx[l][0], b = kLineVtx[l][1];
+        int axis = 0;
+        for (int d = 0; d < 3; ++d)
+          if (vbit(a, d) != vbit(b, d)) axis = d;
+        double g = 1, grad[3] = {1, 1, 1};
+        for (int d = 0; d < 3; ++d) {
+          if (d == axis) {
+            grad[d] = 0;
+            continue;
+          }
+          const double lv = lag1(vbit(a, d), xi[d]), dl = dlag1(vbit(a, d), xi[d]);
+          g *= lv;
+          for (int e = 0; e < 3; ++e)
+            if (e != axis) grad[e] *= (e == d ? dl : lv);
+        }
+        Vec3 N, curlN;
+        N[axis] = g;
+        // curl (g e_axis) = grad g x e_axis
+        Vec3 gg, ea;
+        for (int d = 0; d < 3; ++d) gg[d] = grad[d];
+        ea[axis] = 1;
+        curlN = cross(gg, ea);
+        const double s = sgn[l];
+        for (int i = 0; i < 3; ++i) {
+          double v = 0, c = 0;
+          for (int j = 0; j < 3; ++j) {
+            v += Ji[j][i] * N[j];
+            c += J[i][j] * curlN[j];
+          }
+          w[12 * q + l][i] = s * v;
+          cw[12 * q + l][i] = s * c / det;
+        }
+      }
+      // Raviart-Thomas: R = l_side(xi_axis) e_axis (unit flux), contravariant Piola
+      for (int f = 0; f < 6; ++f) {
+        const int axis = f / 2, side = f % 2;
+        const double r = lag1(side, xi[axis]);
+        const double s = sgn[12 + f];
+        for (int i = 0; i < 3; ++i) u[6 * q + f][i] = s * J[i][axis] * r / det;
+        du[6 * q + f] = s * dlag1(side, 0.0) / det;
+      }
+    }
+  }
+};
+
+// component views of local dof k (zero outside its own block)
+Vec3 phi_w(const FeecValues& fv, int q, int k) { return k < 12 ? fv.w[12 * q + k] : Vec3(); }
+Vec3 curl_w(const FeecValues& fv, int q, int k) { return k < 12 ? fv.cw[12 * q + k] : Vec3(); }
+Vec3 phi_u(const FeecValues& fv, int q, int k) {
+  return (k >= 12 && k < 18) ? fv.u[6 * q + k - 12] : Vec3();
+}
+double div_u(const FeecValues& fv, int q, int k) {
+  return (k >= 12 && k < 18) ? fv.du[6 * q + k - 12] : 0.0;
+}
+double phi_p(int k) { return k == 18 ? 1.0 : 0.0; }
+
+int feec_block(int k) { return k < 12 ? 0 : k < 18 ? 1 : 2; }
+
+}  // namespace
+
+extern "C" void orc_feec_cell_system(const orc_physics* ph, const double* X, const signed char* sgn,
+                                     const double* dofv, const double* T_local, double* K,
+                                     double* f) {
+  // local_assemble_nse_system (boussineq_model_FEEC.tpp:669-808), QGauss(deg+2)
+  double gx[4], gw[4];
+  gauss1d(3, gx, gw);
+  FeecValues fv;
+  fv.reinit(X, sgn, 3, gx, gw);
+  const double one_over_re = ph->one_over_reynolds, dt = ph->time_step;
+  std::fill(K, K + 361, 0.0);
+  std::fill(f, f + 19, 0.0);
+  for (int q = 0; q < fv.nq; ++q) {
+    // old T (Q1, MappingQ1): trilinear value at the point
+    const int ia = q % 3, ib = (q / 3) % 3, ic = q / 9;
+    const double xi[3] = {gx[ia], gx[ib], gx[ic]};
+    double T = 0;
+    for (int v = 0; v < 8; ++v)
+      T += T_local[v] * lag1(vbit(v, 0), xi[0]) * lag1(vbit(v, 1), xi[1]) * lag1(vbit(v, 2), xi[2]);
+    const double rho = 1 - ph->expansion_coefficient * (T - ph->temperature_ref);
+    Vec3 old_w, old_u;
+    for (int k = 0; k < 19; ++k) {
+      const Vec3 a = phi_w(fv, q, k), b = phi_u(fv, q, k);
+      for (int d = 0; d < 3; ++d) {
+        old_w[d] += dofv[k] * a[d];
+        old_u[d] += dofv[k] * b[d];
+      }
+    }
+    Vec3 coriolis;
+    if (ph->cuboid) coriolis[2] = ph->coriolis_scale * ph->omega;
+    for (int i = 0; i < 19; ++i)
+      for (int j = 0; j < 19; ++j)
+        K[19 * i + j] += (dot(phi_w(fv, q, i), phi_w(fv, q, j)) -
+                          dot(curl_w(fv, q, i), phi_u(fv, q, j)) +
+                          dot(phi_u(fv, q, i), phi_u(fv, q, j)) +
+                          dt * one_over_re * dot(phi_u(fv, q, i), curl_w(fv, q, j)) -
+                          div_u(fv, q, i) * phi_p(j) - phi_p(i) * div_u(fv, q, j)) *
+                         fv.JxW[q];
+    Vec3 grav;
+    if (ph->cuboid) {
+      grav[2] = -ph->gravity_constant;
+    } else {
+      grav = gravity_vector(fv.xq[q], ph->gravity_constant);
+    }
+    for (int d = 0; d < 3; ++d) grav[d] *= ph->gravity_scale;
+    const Vec3 wxu = cross(old_w, old_u), cxu = cross(coriolis, old_u);
+    for (int i = 0; i < 19; ++i)
+      f[i] += (dot(phi_u(fv, q, i), old_u) + dt * rho * dot(grav, phi_u(fv, q, i)) -
+               dt * (div_u(fv, q, i) * 0.5 * dot(old_u, old_u) + dot(phi_u(fv, q, i), wxu)) -
+               dt * 2 * dot(phi_u(fv, q, i), cxu)) *
+              fv.JxW[q];
+  }
+}
+
+extern "C" void orc_feec_cell_preconditioner(const orc_physics* ph, const double* X,
+                                             const signed char* sgn, double* P) {
+  // local_assemble_nse_preconditioner (FEEC.tpp:509-572), QGauss(deg+1); only
+  // phi_p phi_p carries JxW (Q14)
+  double gx[4], gw[4];
+  gauss1d(2, gx, gw);
+  FeecValues fv;
+  fv.reinit(X, sgn, 2, gx, gw);
+  const double c = ph->time_step * ph->one_over_reynolds;
+  std::fill(P, P + 361, 0.0);
+  auto ind = [](double v) { return std::fabs(v) > 1.0e-9 ? -2 * (std::signbit(v) - 0.5) : 0.0; };
+  for (int q = 0; q < fv.nq; ++q)
+    for (int i = 0; i < 19; ++i)
+      for (int j = 0; j < 19; ++j)
+        P[19 * i + j] += c * dot(curl_w(fv, q, i), curl_w(fv, q, j)) +
+                         ind(dot(phi_u(fv, q, i), phi_w(fv, q, j))) +
+                         ind(dot(phi_w(fv, q, i), phi_u(fv, q, j))) +
+                         phi_p(i) * phi_p(j) * fv.JxW[q];
+}
+
+struct orc_feec {
+  orc_physics ph;
+  int n_cells, n_w, n_u, n_p, n, n_T;
+  std::vector<int> dofs, cell_T;
+  std::vector<signed char> sgn;
+  std::vector<double> X, geom27, diam;
+  Cons cons, cT;
+  Csr nse, pre, Tmass, Tstiff, Tmat;
+  std::vector<double> rhs, T_rhs, T_inv;
+  bool zero_mean = true;
+};
+
+extern "C" orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const int* cell_dofs19,
+                                     const signed char* sign19, const double* X24,
+                                     const unsigned char* fixed, int n_w, int n_u, int n_p,
+                                     const int* cell_T, int n_T, const orc_constraints* T_c,
+                                     const double* diameter) {
+  auto m = new orc_feec();
+  m->ph = *ph;
+  m->n_cells = n_cells;
+  m->n_w = n_w;
+  m->n_u = n_u;
+  m->n_p = n_p;
+  m->n = n_w + n_u + n_p;
+  m->n_T = n_T;
+  m->dofs.assign(cell_dofs19, cell_dofs19 + 19 * size_t(n_cells));
+  m->sgn.assign(sign19, sign19 + 19 * size_t(n_cells));
+  m->X.assign(X24, X24 + 24 * size_t(n_cells));
+  m->cell_T.assign(cell_T, cell_T + 8 * size_t(n_cells));
+  m->diam.assign(diameter, diameter + n_cells);
+  // homogeneous boundary constraints (project_boundary_values_* of zero, FEEC.tpp:311-350)
+  std::vector<int> line, ptr(1, 0);
+  std::vector<double> inh;
+  for (int d = 0; d < m->n; ++d)
+    if (fixed[d]) {
+      line.push_back(d);
+      ptr.push_back(0);
+      inh.push_back(0.0);
+    }
+  const orc_constraints oc{int(line.size()), line.data(), ptr.data(), nullptr, nullptr, inh.data()};
+  m->cons.init(m->n, &oc);
+  m->cT.init(n_T, T_c);
+  // coupling tables of setup_nse_matrices (FEEC.tpp:82-130) / setup_nse_preconditioner (:146-185)
+  make_pattern(m->nse, m->n, n_cells, 19, m->dofs.data(), m->cons, [](int i, int j) {
+    const int a = feec_block(i), b = feec_block(j);
+    return a == 0 ? b < 2 : a == 1 ? true : b == 1;
+  });
+  make_pattern(m->pre, m->n, n_cells, 19, m->dofs.data(), m->cons, [](int i, int j) {
+    const int a = feec_block(i), b = feec_block(j);
+    return a < 2 ? b < 2 : b != 1;
+  });
+  make_pattern(m->Tmass, n_T, n_cells, 8, m->cell_T.data(), m->cT, [](int, int) { return true; });
+  m->Tstiff = m->Tmass;
+  m->Tmat = m->Tmass;
+  // Q1 temperature mapping as Q2-isoparametric nodes at the trilinear interpolants
+  m->geom27.resize(81 * size_t(n_cells));
+  for (int c = 0; c < n_cells; ++c)
+    for (int k = 0; k < 27; ++k) {
+      const double t[3] = {0.5 * (k % 3), 0.5 * ((k / 3) % 3), 0.5 * (k / 9)};
+      for (int d = 0; d < 3; ++d) {
+        double x = 0;
+        for (int v = 0; v < 8; ++v)
+          x += lag1(vbit(v, 0), t[0]) * lag1(vbit(v, 1), t[1]) * lag1(vbit(v, 2), t[2]) *
+               m->X[24 * size_t(c) + 3 * v + d];
+        m->geom27[81 * size_t(c) + 3 * k + d] = x;
+      }
+    }
+  m->rhs.assign(m->n, 0.0);
+  m->T_rhs.assign(n_T, 0.0);
+  return m;
+}
+
+extern "C" void orc_feec_destroy(orc_feec* m) { delete m; }
+extern "C" void orc_feec_set_zero_mean(orc_feec* m, int on) { m->zero_mean = on != 0; }
+
+extern "C" void orc_feec_assemble_nse_system(orc_feec* m, const double* old_nse, const double* old_T) {
+  m->nse.zero();
+  std::fill(m->rhs.begin(), m->rhs.end(), 0.0);
+  std::vector<double> K(361), f(19), dv(19), Tl(8);
+  for (int c = 0; c < m->n_cells; ++c) {
+    for (int i = 0; i < 19; ++i) dv[i] = old_nse[m->dofs[19 * size_t(c) + i]];
+    for (int v = 0; v < 8; ++v) Tl[v] = old_T[m->cell_T[8 * size_t(c) + v]];
+    orc_feec_cell_system(&m->ph, &m->X[24 * size_t(c)], &m->sgn[19 * size_t(c)], dv.data(),
+                         Tl.data(), K.data(), f.data());
+    distribute_local_to_global(m->cons, 19, &m->dofs[19 * size_t(c)], K.data(), f.data(), &m->nse,
+                               m->rhs.data());
+  }
+}
+
+extern "C" void orc_feec_assemble_preconditioner(orc_feec* m) {
+  m->pre.zero();
+  std::vector<double> P(361);
+  for (int c = 0; c < m->n_cells; ++c) {
+    orc_feec_cell_preconditioner(&m->ph, &m->X[24 * size_t(c)], &m->sgn[19 * size_t(c)], P.data());
+    distribute_local_to_global(m->cons, 19, &m->dofs[19 * size_t(c)], P.data(), nullptr, &m->pre,
+                               nullptr);
+  }
+}
+
+extern "C" long orc_feec_matrix_nnz(const orc_feec* m, int which) {
+  return long((which == 0 ? m->nse : m->pre).cols.size());
+}
+extern "C" void orc_feec_matrix_csr(const orc_feec* m, int which, int* rowptr, int* cols,
+                                    double* vals) {
+  const Csr& A = which == 0 ? m->nse : m->pre;
+  std::copy(A.rowptr.begin(), A.rowptr.end(), rowptr);
+  std::copy(A.cols.begin(), A.cols.end(), cols);
+  std::copy(A.vals.begin(), A.vals.end(), vals);
+}
+extern "C" void orc_feec_rhs(const orc_feec* m, double* out) {
+  std::copy(m->rhs.begin(), m->rhs.end(), out);
+}
+
+extern "C" void orc_feec_assemble_temperature(orc_feec* m, const double* old_T,
+                                              const double* nse_solution) {
+  // assemble_temperature_matrix (FEEC.tpp:882-960) + _rhs (:966-1100), MappingQ1,
+  // QGauss(T_degree + 2); u from the RT field of nse_solution (Q5)
+  m->Tmass.zero();
+  m->Tstiff.zero();
+  std::vector<double> M(64), K(64);
+  for (int c = 0; c < m->n_cells; ++c) {
+    orc_cell_temperature_matrix(&m->ph, &m->geom27[81 * size_t(c)], M.data(), K.data());
+    const int* d = &m->cell_T[8 * size_t(c)];
+    distribute_local_to_global(m->cT, 8, d, M.data(), nullptr, &m->Tmass, nullptr);
+    distribute_local_to_global(m->cT, 8, d, K.data(), nullptr, &m->Tstiff, nullptr);
+  }
+  const double dt_eff = m->ph.time_step / m->ph.nse_solver_interval;
+  for (size_t k = 0; k < m->Tmat.vals.size(); ++k)
+    m->Tmat.vals[k] = m->Tmass.vals[k] + dt_eff * m->Tstiff.vals[k];
+  m->T_inv.assign(m->n_T, 0.0);
+  for (int r = 0; r < m->n_T; ++r) m->T_inv[r] = 1.0 / m->Tmat.at(r, r);
+  std::fill(m->T_rhs.begin(), m->T_rhs.end(), 0.0);
+  double gx[4], gw[4];
+  gauss1d(3, gx, gw);
+  std::vector<double> rhs(8), mfbc(64);
+  CellValues cv;
+  FeecValues fv;
+  for (int c = 0; c < m->n_cells; ++c) {
+    const int* d = &m->cell_T[8 * size_t(c)];
+    cv.reinit(&m->geom27[81 * size_t(c)], 3);
+    fv.reinit(&m->X[24 * size_t(c)], &m->sgn[19 * size_t(c)], 3, gx, gw);
+    std::fill(rhs.begin(), rhs.end(), 0.0);
+    std::fill(mfbc.begin(), mfbc.end(), 0.0);
+    for (int q = 0; q < 27; ++q) {
+      double T = 0;
+      Vec3 gT, u;
+      for (int v = 0; v < 8; ++v) {
+        T += old_T[d[v]] * cv.v1[8 * q + v];
+        for (int k = 0; k < 3; ++k) gT[k] += old_T[d[v]] * cv.g1[8 * q + v][k];
+      }
+      for (int f = 0; f < 6; ++f)
+        for (int k = 0; k < 3; ++k)
+          u[k] += nse_solution[m->dofs[19 * size_t(c) + 12 + f]] * fv.u[6 * q + f][k];
+      for (int i = 0; i < 8; ++i) {
+        rhs[i] += (cv.v1[8 * q + i] * T - dt_eff * cv.v1[8 * q + i] * dot(u, gT)) * cv.JxW[q];
+        if (m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0)
+          for (int j = 0; j < 8; ++j)
+            mfbc[8 * j + i] += (cv.v1[8 * q + i] * cv.v1[8 * q + j] +
+                                dt_eff * m->ph.one_over_peclet *
+                                    dot(cv.g1[8 * q + i], cv.g1[8 * q + j])) *
+                               cv.JxW[q];
+      }
+    }
+    distribute_rhs_with_bc(m->cT, 8, d, rhs.data(), mfbc.data(), m->T_rhs.data());
+  }
+}
+
+extern "C" void orc_feec_T_rhs(const orc_feec* m, double* out) {
+  std::copy(m->T_rhs.begin(), m->T_rhs.end(), out);
+}
+
+namespace {
+void csr_block(const Csr& A, int r0, int r1, int c0, int c1, const double* x, double* y, bool add) {
+  for (int r = r0; r < r1; ++r) {
+    double acc = 0;
+    for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
+      if (A.cols[k] >= c0 && A.cols[k] < c1) acc += A.vals[k] * x[A.cols[k] - c0];
+    y[r - r0] = add ? y[r - r0] + acc : acc;
+  }
+}
+}  // namespace
+
+extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
+  // solve_NSE_block_preconditioned (FEEC.tpp:1268-1477), block preconditioner on
+  const int nw = m->n_w, nu = m->n_u, np = m->n_p, n = m->n, ou = nw, op = nw + nu;
+  const double dt = m->ph.time_step;
+  const Csr& A = m->nse;
+  // Mw / Mu: Ifpack Jacobi of nse_matrix.block(0,0) / block(1,1) (:1288-1303)
+  std::vector<double> dinv(nw + nu);
+  for (int r = 0; r < nw + nu; ++r) dinv[r] = 1.0 / const_cast<Csr&>(A).at(r, r);
+  std::vector<double> cellw(np);
+  double wsum = 0;
+  for (int c = 0; c < m->n_cells; ++c) {
+    const double xi[3] = {0.5, 0.5, 0.5};
+    double J[3][3];
+    Vec3 x;
+    map_q1(&m->X[24 * size_t(c)], xi, J, x);
+    cellw[c] = det3(J);  // QGauss(1) JxW of compute_mean_value
+    wsum += cellw[c];
+  }
+  std::vector<double> t1(nu), t2(np), s1(std::max(nw, nu)), s2(std::max(nw, nu));
+  // ShiftedSchurComplement::vmult (shifted_schur_complement.hpp:155-171)
+  auto shifted = [&](const double* x, double* y) {
+    csr_block(A, ou, op, ou, op, x, y, false);
+    csr_block(A, 0, nw, ou, op, x, s1.data(), false);
+    for (int i = 0; i < nw; ++i) s2[i] = s1[i] * dinv[i];
+    for (int i = 0; i < nw; ++i) s2[i] *= -1;
+    csr_block(A, ou, op, 0, nw, s2.data(), y, true);
+  };
+  auto mu_jacobi = [&](const double* x, double* y) {
+    for (int i = 0; i < nu; ++i) y[i] = x[i] * dinv[nw + i];
+  };
+  // SchurComplementLowerBlock::vmult, do_full_solve = false (schur_complement.hpp:256-276)
+  auto lower = [&](const double* x, double* y) {
+    csr_block(A, ou, op, op, n, x, s1.data(), false);
+    for (int i = 0; i < nu; ++i) s2[i] = s1[i] * dinv[nw + i];
+    csr_block(A, op, n, ou, op, s2.data(), y, false);
+  };
+  auto identity = [&](const double* x, double* y) { std::copy(x, x + np, y); };
+  // BlockSchurPreconditionerFEEC::vmult (block_schur_preconditioner.hpp:115-147)
+  auto precondition = [&](const double* src, double* dst) {
+    for (int i = 0; i < nw; ++i) dst[i] = src[i] * dinv[i];  // Mw Jacobi (Q16)
+    csr_block(A, ou, op, 0, nw, dst, t1.data(), false);
+    for (int i = 0; i < nu; ++i) t1[i] = -1.0 * t1[i] + src[ou + i];
+    {
+      // ApproxShiftedSchurComplementInverse (shifted_schur_complement.hpp:271-298)
+      Control ctl{30, 1e-6 * norm2(t1, 0, nu)};
+      int it = 0;
+      try {
+        gmres(nu, shifted, mu_jacobi, dst + ou, t1.data(), ctl, it);
+      } catch (const NoConvergence&) {
+      }
+    }
+    for (int i = 0; i < np; ++i) t2[i] = -1.0 * (src[op + i] + src[op + i]);  // Q15
+    csr_block(A, op, n, ou, op, dst + ou, t2.data(), true);
+    {
+      // ApproxNestedSchurComplementInverse (nested_schur_complement.hpp:287-322)
+      Control ctl{100, 1e-6 * norm2(t2, 0, np)};
+      int it = 0;
+      try {
+        gmres(np, lower, identity, dst + op, t2.data(), ctl, it);
+      } catch (const NoConvergence&) {
+      }
+    }
+    if (m->zero_mean) {
+      double s = 0;
+      for (int i = 0; i < np; ++i) s += cellw[i] * dst[op + i];
+      const double mean = s / wsum;
+      for (int i = 0; i < np; ++i) dst[op + i] += -mean;
+    }
+  };
+  auto Aop = [&](const double* x, double* y) { csr_block(A, 0, n, 0, n, x, y, false); };
+  std::vector<double> x(sol, sol + n);
+  for (int i = op; i < n; ++i) x[i] *= dt;  // :1345
+  Control ctl{500, 1e-8 * norm2(m->rhs, 0, n)};
+  int its = 0, rc = 0;
+  try {
+    gmres(n, Aop, precondition, x.data(), m->rhs.data(), ctl, its, 100);
+  } catch (const NoConvergence&) {
+    rc = 1;
+  }
+  m->cons.distribute(x.data());
+  for (int i = op; i < n; ++i) x[i] /= dt;
+  std::copy(x.begin(), x.end(), sol);
+  if (iterations) *iterations = int(ctl.last_step);
+  return rc;
+}
+
+extern "C" int orc_feec_solve_temperature(orc_feec* m, double* T, int* iterations) {
+  // solve_temperature: same CG + Jacobi as the classic model (:1417-1476)
+  const int n = m->n_T;
+  Control ctl{unsigned(n), 1e-12 * norm2(m->T_rhs, 0, n)};
+  std::vector<double> x(T, T + n), g(n), d(n), h(n);
+  const Csr& A = m->Tmat;
+  auto Av = [&](const std::vector<double>& s, std::vector<double>& o) {
+    for (int r = 0; r < n; ++r) {
+      double acc = 0;
+      for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) acc += A.vals[k] * s[A.cols[k]];
+      o[r] = acc;
+    }
+  };
+  bool all_zero = true;
+  for (double v : x) all_zero &= (v == 0.0);
+  if (!all_zero) {
+    Av(x, g);
+    for (int i = 0; i < n; ++i) g[i] += -1. * m->T_rhs[i];
+  } else {
+    for (int i = 0; i < n; ++i) g[i] = -1. * m->T_rhs[i];
+  }
+  double res = norm2(g, 0, n);
+  State conv = ctl.check(0, res);
+  int it = 0;
+  if (conv == kIterate) {
+    for (int i = 0; i < n; ++i) h[i] = g[i] * m->T_inv[i];
+    for (int i = 0; i < n; ++i) d[i] = -1. * h[i];
+    double gh = dotv(g.data(), h.data(), n);
+    while (conv == kIterate) {
+      it++;
+      Av(d, h);
+      double alpha = dotv(d.data(), h.data(), n);
+      alpha = gh / alpha;
+      for (int i = 0; i < n; ++i) x[i] += alpha * d[i];
+      double gg = 0;
+      for (int i = 0; i < n; ++i) {
+        g[i] += alpha * h[i];
+        gg += g[i] * g[i];
+      }
+      res = std::sqrt(std::fabs(gg));
+      conv = ctl.check(it, res);
+      if (conv != kIterate) break;
+      for (int i = 0; i < n; ++i) h[i] = g[i] * m->T_inv[i];
+      double beta = gh;
+      gh = dotv(g.data(), h.data(), n);
+      beta = gh / beta;
+      for (int i = 0; i < n; ++i) d[i] = beta * d[i] - h[i];
+    }
+  }
+  m->cT.distribute(x.data());
+  std::copy(x.begin(), x.end(), T);
+  if (iterations) *iterations = int(ctl.last_step);
+  return conv == kSuccess ? 0 : 1;
+}
+
+extern "C" void orc_feec_velocity_stats(const orc_feec* m, const double* sol, double* out2) {
+  // get_maximal_velocity / get_cfl_number (FEEC.tpp:1134-1230) on
+  // QIterated(QTrapez, 2): points {0, 1/2, 1}^3
+  const double px[3] = {0.0, 0.5, 1.0};
+  FeecValues fv;
+  double mx = 0, cfl = 0;
+  for (int c = 0; c < m->n_cells; ++c) {
+    fv.reinit(&m->X[24 * size_t(c)], &m->sgn[19 * size_t(c)], 3, px, nullptr);
+    double cm = 1e-10;
+    for (int q = 0; q < 27; ++q) {
+      Vec3 u;
+      for (int f = 0; f < 6; ++f)
+        for (int k = 0; k < 3; ++k) u[k] += sol[m->dofs[19 * size_t(c) + 12 + f]] * fv.u[6 * q + f][k];
+      const double nu = std::sqrt(dot(u, u));
+      mx = std::max(mx, nu);
+      cm = std::max(cm, nu);
+    }
+    cfl = std::max(cfl, cm / m->diam[c]);
+  }
+  out2[0] = mx;
+  out2[1] = cfl;
+}

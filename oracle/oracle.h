@@ -113,6 +113,31 @@ int orc_solve_temperature(orc_model* m, double* T_solution /*inout*/, int* itera
 double orc_max_velocity(const orc_model* m, const double* nse_solution);
 double orc_cfl(const orc_model* m, const double* nse_solution, const double* cell_diameter);
 
+/* ---- FEEC variant (ExteriorCalculus::BoussinesqModel<3>, config 4) ------ */
+/* local dofs: 12 Nedelec (edges) + 6 RT (faces) + 1 DGQ0; X: 8 vertices x 3 */
+void orc_feec_cell_system(const orc_physics* ph, const double* X, const signed char* sign19,
+                          const double* dofv19, const double* T_local, double* K, double* f);
+void orc_feec_cell_preconditioner(const orc_physics* ph, const double* X,
+                                  const signed char* sign19, double* P);
+typedef struct orc_feec orc_feec;
+orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const int* cell_dofs19,
+                          const signed char* sign19, const double* X24,
+                          const unsigned char* fixed, int n_w, int n_u, int n_p,
+                          const int* cell_T, int n_T, const orc_constraints* T_c,
+                          const double* diameter);
+void orc_feec_destroy(orc_feec* m);
+void orc_feec_set_zero_mean(orc_feec* m, int on);
+void orc_feec_assemble_nse_system(orc_feec* m, const double* old_nse, const double* old_T);
+void orc_feec_assemble_preconditioner(orc_feec* m);
+long orc_feec_matrix_nnz(const orc_feec* m, int which);
+void orc_feec_matrix_csr(const orc_feec* m, int which, int* rowptr, int* cols, double* vals);
+void orc_feec_rhs(const orc_feec* m, double* out);
+void orc_feec_assemble_temperature(orc_feec* m, const double* old_T, const double* nse_solution);
+void orc_feec_T_rhs(const orc_feec* m, double* out);
+int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations);
+int orc_feec_solve_temperature(orc_feec* m, double* T, int* iterations);
+void orc_feec_velocity_stats(const orc_feec* m, const double* sol, double* out2);
+
 #ifdef __cplusplus
 }
 #endif

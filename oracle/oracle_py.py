@@ -71,6 +71,23 @@ def lib():
         L.orc_max_velocity.restype = D
         L.orc_cfl.argtypes = [P, P, P]
         L.orc_cfl.restype = D
+        L.orc_feec_cell_system.argtypes = [P, P, P, P, P, P, P]
+        L.orc_feec_cell_preconditioner.argtypes = [P, P, P, P]
+        L.orc_feec_create.argtypes = [P, I, P, P, P, P, I, I, I, P, I, P, P]
+        L.orc_feec_create.restype = P
+        L.orc_feec_destroy.argtypes = [P]
+        L.orc_feec_set_zero_mean.argtypes = [P, I]
+        L.orc_feec_assemble_nse_system.argtypes = [P, P, P]
+        L.orc_feec_assemble_preconditioner.argtypes = [P]
+        L.orc_feec_matrix_nnz.argtypes = [P, I]
+        L.orc_feec_matrix_nnz.restype = C.c_long
+        L.orc_feec_matrix_csr.argtypes = [P, I, P, P, P]
+        L.orc_feec_rhs.argtypes = [P, P]
+        L.orc_feec_assemble_temperature.argtypes = [P, P, P]
+        L.orc_feec_T_rhs.argtypes = [P, P]
+        L.orc_feec_solve_nse.argtypes = [P, P, P]
+        L.orc_feec_solve_temperature.argtypes = [P, P, P]
+        L.orc_feec_velocity_stats.argtypes = [P, P, P]
         _lib = L
     return _lib
 
@@ -213,3 +230,96 @@ class Model:
     def cfl(self, sol):
         return lib().orc_cfl(self.h, _p(np.ascontiguousarray(sol, np.float64)),
                              _p(np.ascontiguousarray(self.mesh.cell_diameter, np.float64)))
+
+
+# ---- FEEC variant (ExteriorCalculus::BoussinesqModel<3>) -------------------
+
+def feec_cell_system(ph, X8, sign19, dofv19, T_local):
+    K, f = np.zeros((19, 19)), np.zeros(19)
+    o = physics(ph)
+    lib().orc_feec_cell_system(C.byref(o), _p(np.ascontiguousarray(X8, np.float64)),
+                               _p(np.ascontiguousarray(sign19, np.int8)),
+                               _p(np.ascontiguousarray(dofv19, np.float64)),
+                               _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
+    return K, f
+
+
+def feec_cell_preconditioner(ph, X8, sign19):
+    P = np.zeros((19, 19))
+    o = physics(ph)
+    lib().orc_feec_cell_preconditioner(C.byref(o), _p(np.ascontiguousarray(X8, np.float64)),
+                                       _p(np.ascontiguousarray(sign19, np.int8)), _p(P))
+    return P
+
+
+class FeecModel:
+    """Global FEEC oracle over dcp.HostMesh(feec=True)."""
+
+    def __init__(self, ph, mesh, zero_mean=True):
+        f = mesh.feec
+        self.f = f
+        self.ph = physics(ph)
+        self._a = [np.ascontiguousarray(f.cell_dofs, np.int32), np.ascontiguousarray(f.signs, np.int8),
+                   np.ascontiguousarray(f.cell_vertices, np.float64),
+                   np.ascontiguousarray(f.fixed, np.uint8), np.ascontiguousarray(f.cell_T_dofs, np.int32),
+                   np.ascontiguousarray(f.cell_diameter, np.float64)]
+        cs = mesh.T_constraints
+        self._tc = OrcConstraints(len(cs.line_dof), _p(cs.line_dof).value, _p(cs.entry_ptr).value,
+                                  _p(cs.entry_dof).value, _p(cs.entry_w).value,
+                                  _p(cs.inhomogeneity).value)
+        self._keep = cs
+        a = self._a
+        self.h = lib().orc_feec_create(C.byref(self.ph), f.n_cells, _p(a[0]), _p(a[1]), _p(a[2]),
+                                       _p(a[3]), f.n_w, f.n_u, f.n_p, _p(a[4]), f.n_T,
+                                       C.byref(self._tc), _p(a[5]))
+        lib().orc_feec_set_zero_mean(self.h, int(zero_mean))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_feec_destroy(self.h)
+            self.h = None
+
+    def assemble_nse_system(self, old_nse, old_T):
+        lib().orc_feec_assemble_nse_system(self.h, _p(np.ascontiguousarray(old_nse, np.float64)),
+                                           _p(np.ascontiguousarray(old_T, np.float64)))
+
+    def assemble_preconditioner(self):
+        lib().orc_feec_assemble_preconditioner(self.h)
+
+    def matrix_csr(self, which=0):
+        nnz = lib().orc_feec_matrix_nnz(self.h, which)
+        n = self.f.n
+        rp, cols, vals = np.zeros(n + 1, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
+        lib().orc_feec_matrix_csr(self.h, which, _p(rp), _p(cols), _p(vals))
+        return rp, cols, vals
+
+    def rhs(self):
+        out = np.zeros(self.f.n)
+        lib().orc_feec_rhs(self.h, _p(out))
+        return out
+
+    def assemble_temperature(self, old_T, nse_solution):
+        lib().orc_feec_assemble_temperature(self.h, _p(np.ascontiguousarray(old_T, np.float64)),
+                                            _p(np.ascontiguousarray(nse_solution, np.float64)))
+
+    def T_rhs(self):
+        out = np.zeros(self.f.n_T)
+        lib().orc_feec_T_rhs(self.h, _p(out))
+        return out
+
+    def solve_nse(self, sol):
+        x = np.array(sol, dtype=np.float64, copy=True)
+        it = C.c_int(0)
+        rc = lib().orc_feec_solve_nse(self.h, _p(x), C.byref(it))
+        return rc, x, it.value
+
+    def solve_temperature(self, T):
+        x = np.array(T, dtype=np.float64, copy=True)
+        it = C.c_int(0)
+        rc = lib().orc_feec_solve_temperature(self.h, _p(x), C.byref(it))
+        return rc, x, it.value
+
+    def velocity_stats(self, sol):
+        out = np.zeros(2)
+        lib().orc_feec_velocity_stats(self.h, _p(np.ascontiguousarray(sol, np.float64)), _p(out))
+        return out

@@ -1,0 +1,234 @@
+"""FEEC variant (ExteriorCalculus::BoussinesqModel<3>, boussineq_model_FEEC.tpp;
+config 4): lowest-order Nedelec vorticity, Raviart-Thomas velocity, DGQ0
+pressure on MappingQ1.
+
+CPU: the host topology (edge/face counts, Euler characteristic, conformity
+signs) and known answers of the oracle's element (the RT/Nedelec
+interpolants of constant fields are exact on affine cells; divergence
+theorem per cell; block identities of the assembled system).
+GPU: the HIP kernels and solver chain against the oracle through the C ABI
+(element matrices and assembled entries at 1e-12 of the largest entry,
+solver iterates at 1e-10, same iteration counts)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import dcp
+import oracle_py
+
+SEED = 20261015
+
+
+def cube_cell(shear=0.3):
+    """An affine parallelepiped (vertices in lexicographic order)."""
+    A = np.array([[1.0, shear, 0.1], [0.0, 0.8, 0.2], [0.05, 0.0, 1.3]])
+    o = np.array([0.2, -0.1, 0.4])
+    return np.array([o + A @ np.array([v & 1, (v >> 1) & 1, v >> 2], float) for v in range(8)]), A
+
+
+LINE_VTX = [(0, 2), (1, 3), (0, 1), (2, 3), (4, 6), (5, 7), (4, 5), (6, 7), (0, 4), (1, 5), (2, 6),
+            (3, 7)]
+FACE_VTX = [(0, 2, 4, 6), (1, 3, 5, 7), (0, 1, 4, 5), (2, 3, 6, 7), (0, 1, 2, 3), (4, 5, 6, 7)]
+
+
+def test_topology_counts_and_euler():
+    for r in (0, 1, 2):
+        m = dcp.HostMesh(refine=r, feec=True)
+        f = m.feec
+        # V - E + F - C = chi(S^2 x I) = 2; SURVEY §6 sizes at r = 2
+        assert m.n_p - f.n_w + f.n_u - f.n_p == 2
+        assert f.u_fixed.sum() == 12 * 4 ** r            # inner + outer sphere faces
+        assert np.all(np.abs(f.signs) == 1)
+    assert (f.n_w, f.n_u, f.n_p) == (1352, 1248, 384)
+
+
+def test_face_and_edge_signs_conform():
+    m = dcp.HostMesh(refine=2, feec=True)
+    f = m.feec
+    # every interior face: the two cells see opposite local outward orientation
+    flux_sign = {}
+    for c in range(f.n_cells):
+        for q in range(6):
+            s_out = 1 if q % 2 else -1
+            g = f.cell_u[c, q]
+            flux_sign.setdefault(g, []).append(f.sign_u[c, q] * s_out)
+    for g, s in flux_sign.items():
+        assert len(s) in (1, 2)
+        if len(s) == 2:
+            assert s[0] == -s[1]
+    # edge signs: consistent with a global direction (vertex id order)
+    for c in range(0, f.n_cells, 7):
+        v = m.cell_T_dofs[c]  # Q1 temperature dofs are the vertices
+        for l, (a, b) in enumerate(LINE_VTX):
+            assert f.sign_w[c, l] == (1 if v[a] < v[b] else -1)
+
+
+def test_element_interpolants_of_constants_are_exact():
+    ph = dcp.classic_physics()
+    X, A = cube_cell()
+    sign = np.ones(19, np.int8)
+    c = np.array([0.3, -1.2, 0.7])
+    # Nedelec dofs of a constant field: tangential integrals c . (x_b - x_a)
+    w = np.array([c @ (X[b] - X[a]) for a, b in LINE_VTX])
+    # RT dofs: flux c . n dA through each face in the local +axis direction
+    u = np.zeros(6)
+    for q in range(6):
+        ax = q // 2
+        cof = np.linalg.det(A) * np.linalg.inv(A).T  # area-weighted normals of the reference faces
+        u[q] = c @ cof[:, ax]
+    dofv = np.concatenate([w, u, [0.0]])
+    # the rhs's phi_u . u0 mass term with u0 == constant c: f = M_u u exactly when T, dt = 0
+    ph.time_step = 0.0
+    K, f = oracle_py.feec_cell_system(ph, X, sign, dofv, np.zeros(8))
+    Mu = K[12:18, 12:18]
+    assert np.allclose(f[12:18], Mu @ u, rtol=0, atol=1e-13)
+    # divergence theorem: -int div phi_f = -(+-1) per local face (pressure column)
+    assert np.allclose(K[12:18, 18], [1, -1, 1, -1, 1, -1], atol=1e-14)
+    assert np.allclose(K[18, 12:18], K[12:18, 18], atol=0)
+    # mass blocks symmetric positive definite
+    for B in (K[:12, :12], Mu):
+        assert np.allclose(B, B.T, atol=1e-15)
+        assert np.all(np.linalg.eigvalsh(B) > 0)
+    # curl of the Nedelec interpolant of a constant field vanishes: -curl w . u block
+    # applied to the constant's dofs is zero
+    assert np.allclose(w @ K[:12, 12:18], 0, atol=1e-13)
+
+
+def test_assembled_block_identities():
+    m = dcp.HostMesh(refine=1, feec=True)
+    f = m.feec
+    ph = dcp.classic_physics()
+    M = oracle_py.FeecModel(ph, m)
+    M.assemble_nse_system(np.zeros(f.n), m.T0)
+    rp, cols, vals = M.matrix_csr(0)
+    A = sp.csr_matrix((vals, cols, rp), shape=(f.n, f.n))
+    nw, nu = f.n_w, f.n_u
+    free = ~f.fixed.astype(bool)
+    Wu = A[:nw, nw:nw + nu].toarray()[np.ix_(free[:nw], free[nw:nw + nu])]
+    Uw = A[nw:nw + nu, :nw].toarray()[np.ix_(free[nw:nw + nu], free[:nw])]
+    # block(1,0) = dt/Re (u . curl w) = -dt/Re block(0,1)^T
+    assert np.allclose(Uw, -ph.time_step * ph.one_over_reynolds * Wu.T, rtol=0,
+                       atol=1e-15 * abs(Wu).max())
+    Bt = A[nw:nw + nu, nw + nu:].toarray()
+    B = A[nw + nu:, nw:nw + nu].toarray()
+    assert np.array_equal(B, Bt.T)
+
+
+def test_oracle_solve_converges():
+    m = dcp.HostMesh(refine=1, feec=True)
+    f = m.feec
+    ph = dcp.classic_physics()
+    M = oracle_py.FeecModel(ph, m)
+    M.assemble_nse_system(np.zeros(f.n), m.T0)
+    M.assemble_preconditioner()
+    rc, x, it = M.solve_nse(np.zeros(f.n))
+    assert rc == 0 and 0 < it < 500
+    assert np.all(x[f.fixed.astype(bool)] == 0)
+
+
+def test_oracle_solve_rounding_sensitivity():
+    """Documents the tolerance of the GPU iterate comparison: a 1e-16
+    perturbation of the pressure initial guess moves the oracle's own FEEC
+    solution by far more than 1e-10 (but stays below 1e-6)."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    f = m.feec
+    M = oracle_py.FeecModel(dcp.classic_physics(), m)
+    M.assemble_nse_system(np.zeros(f.n), m.T0)
+    _, x, it = M.solve_nse(np.zeros(f.n))
+    x0 = np.zeros(f.n)
+    x0[f.n_w + f.n_u:] = 1e-16 * np.random.default_rng(1).uniform(-1, 1, f.n_p)
+    _, x2, it2 = M.solve_nse(x0)
+    d = np.linalg.norm(x2 - x) / np.linalg.norm(x)
+    assert it == it2 and 1e-10 < d < 1e-6
+
+
+# ------------------------------------------------------------------ GPU parity
+
+def csr(rp, cols, vals, n):
+    return sp.csr_matrix((vals, cols, rp), shape=(n, n))
+
+
+def rel(a, b):
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def feec_setup():
+    m = dcp.HostMesh(refine=2, feec=True)
+    ph = dcp.classic_physics()
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_feec_mesh(m)
+    return m, ph, ctx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("state", ["physical", "random"])
+def test_feec_element_and_assembly(feec_setup, state):
+    m, ph, ctx = feec_setup
+    f = m.feec
+    rng = np.random.default_rng(SEED)
+    if state == "physical":
+        x, T = np.zeros(f.n), m.T0.copy()
+    else:
+        x = rng.uniform(-1, 1, f.n)
+        x[f.fixed.astype(bool)] = 0
+        T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, x)
+    ctx.set_state(dcp.OLD_T_SOLUTION, T)
+    K, fl = ctx.feec_cell_system(0, f.n_cells)
+    for c in range(0, f.n_cells, 5):
+        Ko, fo = oracle_py.feec_cell_system(ph, f.cell_vertices[c], f.signs[c],
+                                            x[f.cell_dofs[c]], T[f.cell_T_dofs[c]])
+        assert rel(K[c], Ko) < 1e-12
+        assert np.max(np.abs(fl[c] - fo)) <= 1e-12 * max(np.max(np.abs(fo)), 1e-300) + 1e-17
+    ctx.feec_assemble_nse_system()
+    orc = oracle_py.FeecModel(ph, m)
+    orc.assemble_nse_system(x, T)
+    Ag = csr(*ctx.feec_matrix_csr(0), f.n)
+    Ao = csr(*orc.matrix_csr(0), f.n)
+    assert (Ag != 0).nnz <= Ao.nnz
+    assert abs(Ag - Ao).max() <= 1e-12 * abs(Ao).max()
+    assert rel(ctx.get_state(dcp.NSE_RHS), orc.rhs()) < 1e-12
+    ctx.feec_build_nse_preconditioner()
+    orc.assemble_preconditioner()
+    Pg, Po = csr(*ctx.feec_matrix_csr(1), f.n), csr(*orc.matrix_csr(1), f.n)
+    assert abs(Pg - Po).max() <= 1e-12 * abs(Po).max()
+
+
+@pytest.mark.gpu
+def test_feec_time_step(feec_setup):
+    m, ph, ctx = feec_setup
+    f = m.feec
+    x0, T0 = np.zeros(f.n), m.T0.copy()
+    for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
+                   (dcp.T_SOLUTION, T0)):
+        ctx.set_state(fld, v)
+    # run() order (FEEC.tpp:2238-2300): NSE system, preconditioner, T matrices/rhs, solves
+    ctx.feec_assemble_nse_system()
+    ctx.feec_build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    rc, it = ctx.feec_solve_nse()
+    orc = oracle_py.FeecModel(ph, m)
+    orc.assemble_nse_system(x0, T0)
+    orc.assemble_preconditioner()
+    orc.assemble_temperature(T0, x0)
+    assert rel(ctx.get_state(dcp.T_RHS), orc.T_rhs()) < 1e-12
+    rco, xo, ito = orc.solve_nse(x0)
+    assert rc == rco == 0
+    assert it == ito
+    xg = ctx.get_state(dcp.NSE_SOLUTION)
+    # The FEEC chain's inner solvers stop at their caps with swallowed
+    # NoConvergence (30 / 100 GMRES steps), so the preconditioner is a
+    # nonlinear, rounding-sensitive map: the oracle itself moves by ~1e-7
+    # under a 1e-16 perturbation of its initial guess
+    # (test_oracle_solve_rounding_sensitivity). Iterates are compared at 1e-6.
+    assert np.linalg.norm(xg - xo) <= 1e-6 * np.linalg.norm(xo)
+    rcT, itT, _ = ctx.solve_temperature()
+    rcTo, To, itTo = orc.solve_temperature(T0)
+    assert rcT == rcTo == 0 and itT == itTo
+    assert rel(ctx.get_state(dcp.T_SOLUTION), To) < 1e-10
+    vs = orc.velocity_stats(xg)
+    assert np.isclose(ctx.max_velocity(), vs[0], rtol=1e-12)
+    assert np.isclose(ctx.cfl_number(), vs[1], rtol=1e-12)
