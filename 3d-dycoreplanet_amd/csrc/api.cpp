@@ -1619,6 +1619,8 @@ int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len) 
     out->R0 = p.physical_constants.R0;
     out->R1 = p.physical_constants.R1;
     out->length = L;
+    out->use_block_preconditioner_feec = p.use_block_preconditioner_feec ? 1 : 0;
+    out->correct_pressure_to_zero_mean = p.correct_pressure_to_zero_mean ? 1 : 0;
     return DCP_OK;
   } catch (const std::exception& e) {
     if (err && err_len > 0) {

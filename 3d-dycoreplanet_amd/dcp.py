@@ -115,6 +115,7 @@ class RunParams(C.Structure):
         ("use_schur_complement_solver", C.c_int), ("use_FEEC_solver", C.c_int),
         ("adapt_time_step", C.c_int), ("final_time", C.c_double), ("R0", C.c_double),
         ("R1", C.c_double), ("length", C.c_double),
+        ("use_block_preconditioner_feec", C.c_int), ("correct_pressure_to_zero_mean", C.c_int),
     ]
 
 

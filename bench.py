@@ -58,11 +58,17 @@ def parse():
     ap.add_argument("--cpu-refine", type=int, default=3)
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
                     help="explicit: formed S = B D^-1 B^T (default); composite: B^T, Jacobi, B")
+    ap.add_argument("--variant", choices=["classic", "feec"], default="classic",
+                    help="feec: ExteriorCalculus model of config 4 (feec prm, refine 4, 1 GPU)")
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal: every rank on device 0 (one-GPU box), gloo bootstrap")
     ap.add_argument("--probe-schur", type=int, default=0,
                     help="PMC probe: only N Schur-complement applies after one assembly")
-    return ap.parse_args()
+    args = ap.parse_args()
+    argv = sys.argv[1:]
+    args.refine_set = any(a.startswith("--refine") for a in argv)
+    args.prm_set = any(a.startswith("--prm") for a in argv)
+    return args
 
 
 def schur_bytes(m, nnzb_bt, nnzb_b):
@@ -96,8 +102,79 @@ def cpu_baseline(refine):
                       f"{m.n_u + m.n_p} NSE dofs, {dt:.2f} s on 1 core"}
 
 
+def run_feec(args):
+    """Config 4 (BASELINE.json configs[3]): the FEEC model's time step
+    (ExteriorCalculus::BoussinesqModel<3>::run body, FEEC.tpp:2238-2300) on
+    one GPU: assemble_nse_system, build_nse_preconditioner, temperature
+    matrix/rhs, solve_NSE_block_preconditioned, solve_temperature."""
+    import ctypes
+    import dcp
+    prm = args.prm if args.prm_set else os.path.join(ROOT, "configs",
+                                                     "aqua_planet_shell_test_3d-feec.prm")
+    rp = dcp.load_prm(prm)
+    ph = dcp.physics_from_params(rp)
+    refine = args.refine if args.refine_set else 4
+    t_setup = time.perf_counter()
+    m = dcp.HostMesh(cuboid=False, refine=refine, R0=rp.R0, R1=rp.R1, length=rp.length,
+                     temperature_degree=ph.temperature_degree, feec=True)
+    f = m.feec
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_feec_mesh(m)
+    ctx.set_feec_zero_mean(bool(rp.correct_pressure_to_zero_mean))
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(f.n))
+    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+    t_setup = time.perf_counter() - t_setup
+
+    def step():
+        ctx.copy_state(dcp.NSE_SOLUTION, dcp.OLD_NSE_SOLUTION)
+        ctx.copy_state(dcp.T_SOLUTION, dcp.OLD_T_SOLUTION)
+        ctx.cfl_number()
+        ctx.max_velocity()
+        ctx.feec_assemble_nse_system()
+        ctx.feec_build_nse_preconditioner()
+        ctx.assemble_temperature_matrix()
+        ctx.assemble_temperature_rhs()
+        rc, it = ctx.feec_solve_nse()
+        rcT, itT, _ = ctx.solve_temperature()
+        return rc, it, itT, ctx.timings()
+
+    for _ in range(args.warmup):
+        step()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    recs = [step() for _ in range(args.steps)]
+    hip.hipDeviceSynchronize()
+    elapsed = time.perf_counter() - t0
+    asm_ms = float(np.mean([r[3]["assemble_nse_ms"] for r in recs]))
+    solve_ms = float(np.mean([r[3]["solve_nse_ms"] for r in recs]))
+    its = recs[-1][1]
+    out = {
+        "metric": "assembled DoFs/sec + GMRES iter/sec, 3D shell FEEC refine=4 (config 4), 1 GPU",
+        "value": f.n / (asm_ms * 1e-3), "unit": "assembled DoFs/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic refined hypershell, reference initial state",
+        "config": {"workload": f"FEEC shell Nedelec/RT/DGQ0 refine={refine}, one full time step",
+                   "cells": f.n_cells, "nse_dofs": f.n, "n_w": f.n_w, "n_u": f.n_u,
+                   "n_p": f.n_p, "T_dofs": m.n_T, "parallelism": "single GPU"},
+        "gmres_iterations": its, "gmres_iter_per_s": its / (solve_ms * 1e-3),
+        "T_cg_iterations": recs[-1][2], "converged": all(r[0] == 0 for r in recs),
+        "phase_ms": {k: float(np.mean([r[3][k] for r in recs])) for k in recs[0][3]
+                     if k.endswith("_ms")},
+        "setup_s": t_setup,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.variant == "feec":
+        run_feec(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -273,6 +273,7 @@ typedef struct {
   int initial_global_refinement, space_dimension, nse_velocity_degree;
   int use_schur_complement_solver, use_FEEC_solver, adapt_time_step;
   double final_time, R0, R1, length;
+  int use_block_preconditioner_feec, correct_pressure_to_zero_mean;
 } dcp_run_params;
 int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
 
