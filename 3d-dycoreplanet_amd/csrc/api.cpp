@@ -680,16 +680,17 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         int w = 0;
         for (int p = 64 * sl; p < std::min(rows, 64 * sl + 64); ++p)
           w = std::max(w, h.Sp[p + 1] - h.Sp[p]);
+        w += w & 1;  // column pairs
         off[sl + 1] = off[sl] + 64 * int64_t(w);
       }
       std::vector<int32_t> scol(size_t(off[n_sl]), 0);
       for (int sl = 0; sl < n_sl; ++sl) {
-        const int64_t w = (off[sl + 1] - off[sl]) / 64;
+        const int w = int((off[sl + 1] - off[sl]) / 64);
         for (int i = 0; i < 64; ++i) {
           const int p = 64 * sl + i;
-          for (int64_t k = 0; k < w; ++k) {
+          for (int k = 0; k < w; ++k) {
             const bool real = p < rows && k < h.Sp[p + 1] - h.Sp[p];
-            scol[off[sl] + 64 * k + i] = real ? h.Sc[h.Sp[p] + k] : (p < rows ? p : 0);
+            scol[sell_pos(off.data(), p, k)] = real ? h.Sc[h.Sp[p] + k] : (p < rows ? p : 0);
           }
         }
       }

@@ -129,10 +129,15 @@ void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const doubl
                    const double* x, double* y, bool add, hipStream_t s);
 
 // SELL-64 SpMV: slices of 64 consecutive rows (one wave, one row per lane);
-// inside a slice entries are stored column-major (row 64s+i, entry k at
-// off[s] + 64k + i; padding: col = own row, val = 0), so every load of a wave
-// is one contiguous 512-B (values) / 256-B (columns) segment.
+// slice width even; inside a slice entries are stored in column pairs (row
+// 64s+i, entry k at off[s] + 128 (k/2) + 2i + k%2; padding: col = own row,
+// val = 0), so a lane reads two entries with one 16-B (values) / 8-B
+// (columns) load and every load of a wave is one contiguous 1-KB / 512-B
+// segment.
 //   y = M (cf * x)
+__host__ __device__ inline int64_t sell_pos(const int64_t* off, int p, int k) {
+  return off[p >> 6] + 128 * int64_t(k >> 1) + 2 * (p & 63) + (k & 1);
+}
 void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* val,
                const double* x, double cf, double* y, hipStream_t s);
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis

@@ -23,6 +23,7 @@
 #include "../device.h"
 #include "../fe_tables.h"
 
+
 namespace dcp {
 namespace {
 
@@ -192,25 +193,32 @@ __constant__ unsigned char cPairB[kGroupPairs] = {
 // NSE system: local_assemble_nse_system (:550-673) + distribute_local_to_global.
 // MODE 0 = scatter into block-CSR (colour launch), MODE 1 = dense element output.
 //
-// 256 threads (4 waves) per cell, ~31 KB LDS. The velocity-velocity block is
-// symmetric node-pair-wise (K_(b,.),(a,.) = K_(a,.),(b,.)^T), so only the 45
-// node-group pairs A <= B are summed: 135 1x3 tiles on waves 0-2, each written
-// as (a,b) and, off the diagonal groups, transposed as (b,a). Wave 3 sums the
-// 216 divergence blocks; 27 otherwise idle lanes of wave 2 the rhs nodes. The
-// average-diagonal value of the |K_ii| rule is computed up front from the 27
-// node-diagonal blocks.
+// 256 threads (4 waves) per cell, 38.4 KB LDS and 110 VGPRs: four workgroups
+// per CU. The velocity-velocity block is symmetric node-pair-wise
+// (K_(b,.),(a,.) = K_(a,.),(b,.)^T), so only the 45 node-group pairs A <= B are
+// summed: 135 1x3 tiles on waves 0-2. Wave 3 sums the 216 divergence blocks; 27
+// otherwise idle lanes of wave 2 the rhs nodes. The average-diagonal value of
+// the |K_ii| rule is computed up front from the 27 node-diagonal blocks.
 //
-// Writes are the bound (729 scattered 72-byte blocks per cell): every wave
-// stages its blocks in LDS (the gradient table is dead by then) and adds them
-// back with consecutive lanes on consecutive doubles, ~7 blocks per store
-// instruction instead of 64 scattered lanes. Scatter positions carry a
-// first-touch mark (~pos): the first cell in launch order that touches a block
-// stores instead of adding, so the matrices need no zero fill.
+// Writes are the bound (729 scattered 72-byte blocks per cell): the tile lanes
+// park their blocks in LDS (over the dead geometry/gradient tables; the
+// AffineConstraints condensation is applied there, only for blocks with a
+// constrained node), then all four waves write the whole element matrix back
+// with consecutive lanes on consecutive doubles of a block, 16
+// read-modify-write loads in flight per lane; the (b, a) transposes are read
+// from the staged (a, b) blocks (cSlot). Scatter positions (this cell's posA /
+// posBt / posB, loaded into LDS up front) carry a first-touch mark (~pos): the
+// first cell in launch order that touches a block stores instead of adding, so
+// the matrices need no zero fill.
 constexpr int kNseThreads = 256;
 constexpr int kNseTiles = 3 * kGroupPairs;   // 135
 constexpr int kRhsLane0 = 160;               // wave 2 lanes 32..58: rhs nodes
-constexpr int kNoBlock = -2147483647 - 1;    // INT_MIN: lane offers no block
 
+// Write staging (after the tile phase, over the dead X..F tables): the 405
+// condensed A blocks of the tiles (slot 3 tile + tt, 9 doubles) then the 216
+// condensed B^T rows (3 doubles).
+constexpr int kStageA = 405 * 9;
+constexpr int kStageDoubles = kStageA + 216 * 3;
 struct NseSmem {
   double X[81], U[81], T[8];
   Geo geo;
@@ -218,56 +226,84 @@ struct NseSmem {
   double S[27 * 27];       // [q][n] shape values
   double W1[27 * 8];       // [q][v] JxW * Q1 value
   double F[27 * 3];        // JxW * rhs integrand (velocity part) per q
-  double stage_pad[1024];  // write staging continues here (D..F are dead by then)
+  double stage_pad[559];   // write staging: X..stage_pad (dead by then)
   double diag[27];         // sum_c |K_(a,c),(a,c)| per node (average-diagonal rule)
   int node[27];
   int pdof[8];
-  int spos[3 * 128 + 256];    // write staging: destination blocks per lane (2 / 4 per lane)
+  int pos[729 + 216 + 216];  // this cell's posA, posBt, posB
 };
-// staging: waves 0-2 take 2 x 576 doubles (A blocks + transposes), wave 3
-// 4 x 192 (B^T / B rows), all inside the dead D..stage_pad range
-static_assert(offsetof(NseSmem, diag) - offsetof(NseSmem, D) >= sizeof(double) * (3 * 1152 + 768),
+static_assert(offsetof(NseSmem, diag) - offsetof(NseSmem, X) >= sizeof(double) * kStageDoubles,
               "NSE write staging overlaps live LDS");
+static_assert(sizeof(NseSmem) <= 40960, "NSE LDS above 40 KB (four workgroups per CU)");
 
-// Wave-cooperative block scatter: every lane offers K blocks of NB doubles
-// (pos >= 0: add; ~pos: first touch, store; kNoBlock: nothing). The wave
-// writes them back with consecutive lanes on consecutive doubles, and all
-// read-modify-write loads of the call are in flight before the first store
-// (the destinations of one call are distinct, so this only removes the
-// load-after-store serialisation the compiler must otherwise assume).
-template <int NB, int K>
-__device__ inline void wave_scatter(double* __restrict__ base, const double* const* v,
-                                    const int* pos, double* stage, int* spos, int lane) {
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) stage[64 * NB * k + NB * lane + i] = v[k][i];
-    spos[64 * k + lane] = pos[k];
+// Element-matrix block (a, b) -> staging slot: A blocks of group pairs
+// grp(a) <= grp(b) are stored (tile lane a % 3, tt = b % 3), the others are
+// the transposes of (b, a). Bit 15: transposed.
+constexpr int ce_pair_index(int A, int B) {
+  int i = 0;
+  for (int x = 0; x < A; ++x) i += 9 - x;
+  return i + (B - A);
+}
+struct SlotTable {
+  unsigned short s[729];
+};
+constexpr SlotTable make_slot_table() {
+  SlotTable t{};
+  for (int a = 0; a < 27; ++a)
+    for (int b = 0; b < 27; ++b) {
+      const int A = a / 3, B = b / 3;
+      if (A <= B) {
+        const int tile = 3 * ce_pair_index(A, B) + a % 3;
+        t.s[27 * a + b] = static_cast<unsigned short>(3 * tile + b % 3);
+      } else {
+        const int tile = 3 * ce_pair_index(B, A) + b % 3;
+        t.s[27 * a + b] = static_cast<unsigned short>((3 * tile + a % 3) | 0x8000);
+      }
+    }
+  return t;
+}
+__constant__ SlotTable cSlot = make_slot_table();
+
+// All-wave scatter of the staged element matrix: element e of
+// [0, kScatterElems) is component e % 9 of the A block e / 9 (posA order),
+// then the B^T rows, then the B rows (3 doubles each), so consecutive lanes
+// write consecutive doubles of a block. pos >= 0: add, ~pos: first touch
+// (store). A lane keeps kScatterBatch read-modify-write loads in flight (the
+// destinations of one cell are distinct).
+constexpr int kScatterElems = 729 * 9 + 2 * 216 * 3;
+#ifndef DCP_SCATTER_BATCH
+#define DCP_SCATTER_BATCH 16
+#endif
+constexpr int kScatterBatch = DCP_SCATTER_BATCH;
+__device__ inline double* scatter_target(const NseSmem& sh, const NseOut& out, int e, bool& add,
+                                         double& v) {
+  const double* st = sh.X;  // staging base
+  int p;
+  double* dst;
+  if (e < 729 * 9) {
+    const int pr = e / 9, comp = e - 9 * pr;
+    const int sl = cSlot.s[pr];
+    const int k = sl & 0x7fff;
+    const int i = comp / 3, j = comp - 3 * i;
+    v = st[9 * k + ((sl & 0x8000) ? 3 * j + i : comp)];
+    p = sh.pos[pr];
+    add = p >= 0;
+    dst = out.A + 9 * size_t(add ? p : ~p) + comp;
+  } else if (e < 729 * 9 + 648) {
+    const int r = (e - 729 * 9) / 3, c = e - 729 * 9 - 3 * r;
+    v = st[kStageA + 3 * r + c];
+    p = sh.pos[729 + r];
+    add = p >= 0;
+    dst = out.Bt + 3 * size_t(add ? p : ~p) + c;
+  } else {
+    const int r = (e - 729 * 9 - 648) / 3, c = e - 729 * 9 - 648 - 3 * r;
+    const int pv = r / 27, an = r - 27 * pv;  // B row (pv, an) = B^T row (an, pv)
+    v = st[kStageA + 3 * (8 * an + pv) + c];
+    p = sh.pos[945 + r];
+    add = p >= 0;
+    dst = out.B + 3 * size_t(add ? p : ~p) + c;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  constexpr int J = NB * K;
-  double old[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int e = 64 * j + lane;
-    const int k = e / (64 * NB), el = e - k * 64 * NB;
-    const int blk = el / NB, comp = el - blk * NB;
-    const int p = spos[64 * k + blk];
-    old[j] = p >= 0 ? base[NB * size_t(p) + comp] : 0.0;
-  }
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int e = 64 * j + lane;
-    const int k = e / (64 * NB), el = e - k * 64 * NB;
-    const int blk = el / NB, comp = el - blk * NB;
-    const int p = spos[64 * k + blk];
-    if (p != kNoBlock) base[NB * size_t(p >= 0 ? p : ~p) + comp] = old[j] + stage[e];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return dst;
 }
 
 // Sum of the velocity-velocity 3x3 blocks (a, b0..b0+2) over the 27 points:
@@ -351,6 +387,13 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
     const int v = tid - 64;
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
     sh.T[v] = T_old[cd.cell_T[8 * size_t(cell) + v]];
+  }
+  if (MODE == 0 && want_matrix) {
+    for (int i = tid; i < 729; i += kNseThreads) sh.pos[i] = sm.posA[729 * size_t(cell) + i];
+    for (int i = tid; i < 216; i += kNseThreads) {
+      sh.pos[729 + i] = sm.posBt[216 * size_t(cell) + i];
+      sh.pos[945 + i] = sm.posB[216 * size_t(cell) + i];
+    }
   }
   for (int i = tid; i < 729; i += kNseThreads) sh.S[i] = cRef.S2[i];
   for (int i = tid; i < 3 * 729; i += kNseThreads) sh.D[i] = cRef.G2[i];
@@ -525,109 +568,113 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 
   // ---- MODE 0: condensation + colour-exclusive scatter ----------------------
   const int wave = tid >> 6, lane = tid & 63;
-  double R[3][9];          // waves 0-2: condensed blocks (a, b0+tt); wave 3: B^T rows
-  int pos[4], posT[4];     // destinations of R and of its transposes (wave 3: B^T, B)
+  double blk[3][9];   // tile lanes: element blocks (a, b0+tt); wave 3: B^T rows
   double fa[3] = {0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pos[k] = kNoBlock;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) posT[k] = kNoBlock;
+  const bool tile_lane = want_matrix && tid < kNseTiles;
   const bool rhs_lane = want_rhs && tid >= kRhsLane0 && tid < kRhsLane0 + 27;
-  if (wave < 3) {
-    if (want_matrix && tid < kNseTiles) {
-      const int A = cPairA[tid / 3], B = cPairB[tid / 3];
-      const int a = 3 * A + tid % 3, b0 = 3 * B;
-      double blk[3][9];
-      nse_tile(sh, ph, a, b0, blk);
-      const NodeConstraint ca = cd.vcon[sh.node[a]];
-      double Ca[3][3];
-      condensation(ca, Ca);
-      const int32_t* posA = sm.posA + 729 * size_t(cell);
+  if (tile_lane) {
+    const int A = cPairA[tid / 3], B = cPairB[tid / 3];
+    nse_tile(sh, ph, 3 * A + tid % 3, 3 * B, blk);
+  } else if (rhs_lane) {
+    nse_rhs_node(sh, tid - kRhsLane0, fa);
+  } else if (want_matrix && wave == 3) {
+    // B^T rows (an, v), 4 rounds of 64
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt) {
-        const int b = b0 + tt;
-        double Cb[3][3];
-        condensation(cd.vcon[sh.node[b]], Cb);
-        double KC[3][3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            KC[i][j] = blk[tt][3 * i] * Cb[0][j] + blk[tt][3 * i + 1] * Cb[1][j] +
-                       blk[tt][3 * i + 2] * Cb[2][j];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            R[tt][3 * i + j] = Ca[0][i] * KC[0][j] + Ca[1][i] * KC[1][j] + Ca[2][i] * KC[2][j];
-        if (b == a && ca.type != 0) {
-          // constrained local dofs: global diagonal += |K_ii| (average if 0)
-          double avg = 0;
-          for (int n = 0; n < 27; ++n) avg += sh.diag[n];
-          avg /= 89.0;  // pressure diagonals of the local matrix are 0
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            if (ca.type == 1 || c == ca.k) {
-              const double kii = fabs(blk[tt][4 * c]);
-              R[tt][4 * c] += kii != 0.0 ? kii : avg;
-            }
-        }
-        pos[tt] = posA[27 * a + b];
-        if (A != B) posT[tt] = posA[27 * b + a];
-      }
-    } else if (rhs_lane) {
-      nse_rhs_node(sh, tid - kRhsLane0, fa);
+    for (int k = 0; k < 4; ++k) {
+      const int t = lane + 64 * k;
+      if (t < 216) nse_div(sh, t / 8, t % 8, &blk[0][0] + 3 * k);
     }
-  } else if (want_matrix) {
-    // wave 3: B^T blocks (an, v), 4 rounds of 64
+  }
+  __syncthreads();   // geometry and gradient tables dead: reuse them as the write staging area
+  double* stage = sh.X;
+  if (tile_lane) {
+    const int A = cPairA[tid / 3], B = cPairB[tid / 3];
+    const int a = 3 * A + tid % 3, b0 = 3 * B;
+    double* slot = stage + 27 * tid;   // slots 3 tid + tt
+#pragma unroll
+    for (int i = 0; i < 27; ++i) slot[i] = blk[i / 9][i % 9];
+    // condensation C_a^T K C_b in place, only where a constraint is involved
+    const NodeConstraint ca = cd.vcon[sh.node[a]];
+#pragma unroll 1
+    for (int tt = 0; tt < 3; ++tt) {
+      const int b = b0 + tt;
+      const NodeConstraint cb = cd.vcon[sh.node[b]];
+      if (ca.type == 0 && cb.type == 0) continue;
+      double* K = slot + 9 * tt;
+      double Ca[3][3], Cb[3][3], KC[3][3];
+      condensation(ca, Ca);
+      condensation(cb, Cb);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          KC[i][j] = K[3 * i] * Cb[0][j] + K[3 * i + 1] * Cb[1][j] + K[3 * i + 2] * Cb[2][j];
+      double kii[3] = {K[0], K[4], K[8]};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          K[3 * i + j] = Ca[0][i] * KC[0][j] + Ca[1][i] * KC[1][j] + Ca[2][i] * KC[2][j];
+      if (b == a && ca.type != 0) {
+        // constrained local dofs: global diagonal += |K_ii| (average if 0)
+        double avg = 0;
+        for (int n = 0; n < 27; ++n) avg += sh.diag[n];
+        avg /= 89.0;  // pressure diagonals of the local matrix are 0
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (ca.type == 1 || c == ca.k) {
+            const double d = fabs(kii[c]);
+            K[4 * c] += d != 0.0 ? d : avg;
+          }
+      }
+    }
+  } else if (rhs_lane) {
+    const int an = tid - kRhsLane0;
+    double Ca[3][3];
+    condensation(cd.vcon[sh.node[an]], Ca);
+    double* dst = out.rhs + 3 * size_t(sh.node[an]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+  } else if (want_matrix && wave == 3) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int t = lane + 64 * k;
       if (t < 216) {
-        const int an = t / 8, v = t % 8;
-        double bt[3];
-        nse_div(sh, an, v, bt);
+        const double* bt = &blk[0][0] + 3 * k;
         double Ca[3][3];
-        condensation(cd.vcon[sh.node[an]], Ca);
-        double* r = &R[0][0] + 3 * k;
+        condensation(cd.vcon[sh.node[t / 8]], Ca);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) r[j] = Ca[0][j] * bt[0] + Ca[1][j] * bt[1] + Ca[2][j] * bt[2];
-        pos[k] = sm.posBt[216 * size_t(cell) + 8 * an + v];
-        posT[k] = sm.posB[216 * size_t(cell) + 27 * v + an];
+        for (int j = 0; j < 3; ++j)
+          stage[kStageA + 3 * t + j] = Ca[0][j] * bt[0] + Ca[1][j] * bt[1] + Ca[2][j] * bt[2];
       }
     }
   }
-  __syncthreads();   // gradient table dead: reuse it as the write staging area
-  double* stage = sh.D + 1152 * wave;
-  int* spos = sh.spos + 128 * wave;
-  if (wave < 3) {
-    if (want_matrix) {
-      // block (a, b) and its transpose (b, a) in one call
+  if (!want_matrix) return;
+  __syncthreads();
+  // all four waves: read-modify-write / first-touch store of the 7857 doubles
+  for (int e0 = tid; e0 < kScatterElems; e0 += kNseThreads * kScatterBatch) {
+    double old[kScatterBatch];
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt) {
-        double RT[9];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[tt][3 * j + i];
-        const double* vv[2] = {R[tt], RT};
-        const int pp[2] = {pos[tt], posT[tt]};
-        wave_scatter<9, 2>(out.A, vv, pp, stage, spos, lane);
+    for (int j = 0; j < kScatterBatch; ++j) {
+      const int e = e0 + j * kNseThreads;
+      old[j] = 0.0;
+      if (e < kScatterElems) {
+        bool add;
+        double v;
+        const double* dst = scatter_target(sh, out, e, add, v);
+        if (add) old[j] = *dst;
       }
     }
-    if (rhs_lane) {
-      const int an = tid - kRhsLane0;
-      double Ca[3][3];
-      condensation(cd.vcon[sh.node[an]], Ca);
-      double* dst = out.rhs + 3 * size_t(sh.node[an]);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+    for (int j = 0; j < kScatterBatch; ++j) {
+      const int e = e0 + j * kNseThreads;
+      if (e < kScatterElems) {
+        bool add;
+        double v;
+        double* dst = scatter_target(sh, out, e, add, v);
+        *dst = old[j] + v;
+      }
     }
-  } else if (want_matrix) {
-    // B^T row (an, v) and B row (v, an) hold the same 3 values
-    const double* vv[4] = {&R[0][0], &R[0][0] + 3, &R[0][0] + 6, &R[0][0] + 9};
-    wave_scatter<3, 4>(out.Bt, vv, pos, stage, spos, lane);
-    wave_scatter<3, 4>(out.B, vv, posT, stage, spos, lane);
   }
 }
 
@@ -900,9 +947,7 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
     __syncthreads();
   }
   if (sell_off) {
-    // SELL-64 storage: entry j of row p at off[p / 64] + 64 j + p % 64
-    const int64_t base = sell_off[p >> 6] + (p & 63);
-    for (int j = threadIdx.x; j < len; j += 64) S_val[base + 64 * int64_t(j)] = acc[j];
+    for (int j = threadIdx.x; j < len; j += 64) S_val[sell_pos(sell_off, p, j)] = acc[j];
   } else {
     for (int j = threadIdx.x; j < len; j += 64) S_val[s0 + j] = acc[j];
   }

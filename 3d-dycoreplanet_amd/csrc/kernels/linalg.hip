@@ -206,23 +206,28 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
     return;
   }
   const int64_t b = off[sl];
-  const int w = int((off[sl + 1] - b) >> 6);
-  const int per = (w + 3) >> 2;
-  const int k0 = wave * per, k1 = min(w, k0 + per);
-  const int32_t* cp = col + b + 64 * int64_t(k0) + lane;
-  const double* vp = val + b + 64 * int64_t(k0) + lane;
+  const int np = int((off[sl + 1] - b) >> 7);  // column pairs of the slice
+  const int per = (np + 3) >> 2;
+  const int k0 = wave * per, k1 = min(np, k0 + per);
+  const int2* cp = reinterpret_cast<const int2*>(col + b) + 64 * int64_t(k0) + lane;
+  const double2* vp = reinterpret_cast<const double2*>(val + b) + 64 * int64_t(k0) + lane;
   double acc = 0.0;
   int k = k0;
-  for (; k + 4 <= k1; k += 4, cp += 256, vp += 256) {
-    const int c0 = cp[0], c1 = cp[64], c2 = cp[128], c3 = cp[192];
-    const double a0 = vp[0], a1 = vp[64], a2 = vp[128], a3 = vp[192];
-    const double x0 = x[c0] * cf, x1 = x[c1] * cf, x2 = x[c2] * cf, x3 = x[c3] * cf;
-    acc += a0 * x0;
-    acc += a1 * x1;
-    acc += a2 * x2;
-    acc += a3 * x3;
+  for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
+    const int2 c0 = cp[0], c1 = cp[64];
+    const double2 a0 = vp[0], a1 = vp[64];
+    const double x0 = x[c0.x] * cf, x1 = x[c0.y] * cf, x2 = x[c1.x] * cf, x3 = x[c1.y] * cf;
+    acc += a0.x * x0;
+    acc += a0.y * x1;
+    acc += a1.x * x2;
+    acc += a1.y * x3;
   }
-  for (; k < k1; ++k, cp += 64, vp += 64) acc += vp[0] * (x[cp[0]] * cf);
+  if (k < k1) {
+    const int2 c0 = cp[0];
+    const double2 a0 = vp[0];
+    acc += a0.x * (x[c0.x] * cf);
+    acc += a0.y * (x[c0.y] * cf);
+  }
   if (wave > 0) quarter[wave - 1][lane] = acc;
   __syncthreads();
   if (wave > 0) return;

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Builds timing variants of the assembly kernels into build/var/libdcp_<name>.so:
+#   VARIANTS="base: b12:-DDCP_SCATTER_BATCH=12" bash tools/variant_probe.sh
+# (name:extra hipcc flags for kernels/assembly.hip). Time them on the GPU box
+# with python3 tools/variant_probe.py.
+set -e
+cd "$(dirname "$0")/../3d-dycoreplanet_amd"
+make -s libdcp.so
+mkdir -p build/var
+OTHERS=$(ls build/*.o | grep -v assembly.o)
+for spec in ${VARIANTS:-base:}; do
+  name=${spec%%:*}; flags=${spec#*:}
+  /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics ${flags//,/ } \
+    -c csrc/kernels/assembly.hip -o build/var/assembly_$name.o
+  /opt/rocm/bin/hipcc -shared -fopenmp --offload-arch=gfx950 -o build/var/libdcp_$name.so $OTHERS \
+    build/var/assembly_$name.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+done
