@@ -30,6 +30,8 @@ Ctx::~Ctx() {
   if (hpinned) (void)hipHostFree(hpinned);
   ev_total.destroy();
   for (auto& t : schur_ev) t.destroy();
+  for (auto& v : mf_ev)
+    for (auto& t : v) t.destroy();
   if (stream) (void)hipStreamDestroy(stream);
 }
 }  // namespace dcp
@@ -529,6 +531,10 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
     c->ev_total.init();
     c->schur_ev.resize(Ctx::kSchurEvents);
     for (auto& t : c->schur_ev) t.init();
+    for (auto& v : c->mf_ev) {
+      v.resize(Ctx::kMfEvents);
+      for (auto& t : v) t.init();
+    }
     ensure_workspaces(*c);
     *out = c.release();
     return DCP_OK;
@@ -560,6 +566,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     if (option == DCP_OPT_SCHUR_EXPLICIT) {
       ctx->schur_explicit = value != 0;
       ctx->precond_built = false;  // S must be (re)formed
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_MATRIX_FREE) {
+      ctx->matrix_free = value != 0;
       return DCP_OK;
     }
     if (option == DCP_OPT_FEEC_ZERO_MEAN) {
@@ -720,6 +730,45 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
                                         Btc.size(), c.stream);
     c.first_touch_B = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posB.p, n_cells,
                                        Bc.size(), c.stream);
+    {
+      // matrix-free operator: first-touch bits in colour order, constrained
+      // velocity dofs with the position of their assembled diagonal entry,
+      // per-point geometry
+      std::vector<uint64_t> first(n_cells, 0);
+      std::vector<uint8_t> vt(nv, 0), pt(n_p, 0);
+      for (size_t e = 0; e < ccells.size(); ++e) {
+        const int cell = ccells[e];
+        uint64_t bits = 0;
+        for (int t = 0; t < 27; ++t) {
+          const int n = q2[27 * size_t(cell) + t];
+          if (!vt[n]) { vt[n] = 1; bits |= uint64_t(1) << t; }
+        }
+        for (int v = 0; v < 8; ++v) {
+          const int p = pd[8 * size_t(cell) + v];
+          if (!pt[p]) { pt[p] = 1; bits |= uint64_t(1) << (32 + v); }
+        }
+        first[cell] = bits;
+      }
+      std::vector<int32_t> cdof;
+      std::vector<int64_t> cpos;
+      for (int n = 0; n < nv; ++n) {
+        if (vc[n].type == 0) continue;
+        const auto* b = std::lower_bound(Ac.data() + Ap[n], Ac.data() + Ap[n + 1], n);
+        require(b != Ac.data() + Ap[n + 1] && *b == n, DCP_ERR_INVALID, "A pattern lacks a diagonal block");
+        const int64_t blk = b - Ac.data();
+        for (int comp = 0; comp < 3; ++comp)
+          if (vc[n].type == 1 || comp == vc[n].k) {
+            cdof.push_back(3 * n + comp);
+            cpos.push_back(9 * blk + 4 * comp);
+          }
+      }
+      c.mf_first.upload(first);
+      c.mf_cdof.upload(cdof);
+      c.mf_cpos.upload(cpos);
+      c.mf_ncon = int(cdof.size());
+      c.mf_geo.alloc(size_t(n_cells) * 270);
+      mf_geometry(c.cd(), c.mf_geo.p, c.stream);
+    }
     const size_t nn = size_t(n_u + n_p);
     c.nse_sol.alloc(nn);
     c.old_nse.alloc(nn);
@@ -950,6 +999,8 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     c.time_schur = true;
     c.schur_ev_used = 0;
     c.schur_calls = 0;
+    c.mf_ev_used[0] = c.mf_ev_used[1] = 0;
+    c.mf_calls[0] = c.mf_calls[1] = 0;
     const int rc = solve_nse(c, outer, inner);
     c.time_schur = false;
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -961,6 +1012,20 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     }
     c.timings.schur_apply_ms_avg = c.schur_ev_used ? sum / c.schur_ev_used : 0.0;
     c.timings.schur_applies = c.schur_calls;
+    double mf_ms[2] = {0, 0};
+    for (int v = 0; v < 2; ++v) {
+      double sm = 0;
+      for (int k = 0; k < c.mf_ev_used[v]; ++k) {
+        float ms = 0;
+        DCP_HIP_CHECK(hipEventElapsedTime(&ms, c.mf_ev[v][k].a, c.mf_ev[v][k].b));
+        sm += ms;
+      }
+      mf_ms[v] = c.mf_ev_used[v] ? sm / c.mf_ev_used[v] : 0.0;
+    }
+    c.timings.stokes_apply_ms_avg = mf_ms[0];
+    c.timings.velocity_apply_ms_avg = mf_ms[1];
+    c.timings.stokes_applies = c.mf_calls[0];
+    c.timings.velocity_applies = c.mf_calls[1];
     t.stop();
     return rc;
   });

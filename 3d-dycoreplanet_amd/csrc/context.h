@@ -100,6 +100,17 @@ struct Ctx {
   DBuf<double> sell_part;            // 2 x sell_fused_blocks(n_p) partials
   int S_max_row = 0;
   bool schur_explicit = true;
+  // matrix-free operator (kernels/matfree.hip): geometry, first-touch bits,
+  // constrained velocity dofs with their assembled diagonal entries
+  bool matrix_free = true;
+  DBuf<double> mf_geo;
+  DBuf<uint64_t> mf_first;
+  DBuf<int32_t> mf_cdof;
+  DBuf<int64_t> mf_cpos;
+  int mf_ncon = 0;
+  MfData mfd() const {
+    return MfData{n_u, cell_q2.p, cell_p.p, vcon.p, mf_geo.p, mf_first.p};
+  }
   // state
   DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;
   DBuf<double> A_diag, Mp_diag, A_inv, Mp_inv, T_inv;
@@ -124,6 +135,11 @@ struct Ctx {
   int schur_ev_used = 0;
   long schur_calls = 0;
   bool time_schur = false;
+  // the same for the matrix-free applies: [0] Stokes, [1] velocity block
+  static constexpr int kMfEvents = 128;
+  std::vector<Timer> mf_ev[2];
+  int mf_ev_used[2] = {0, 0};
+  long mf_calls[2] = {0, 0};
 
   // ---- FEEC variant (config 4): n_u = n_w + n_u(faces), n_p = cells
   bool feec = false;

@@ -1,0 +1,379 @@
+// Matrix-free Stokes operator of the classic Q2^3/Q1 system for CDNA4 (gfx950), FP64.
+//
+// Applies the operator that assemble_nse_system + distribute_local_to_global
+// build (boussinesq_model.tpp:550-687; its matrix part :626-637) without the
+// matrix:
+//   [A B^T; B 0] x = sum_cells C^T K_cell C x  (+ the constrained diagonal)
+// with, per quadrature point (w = JxW, nu = dt/Re, u / grad u / p of C x):
+//   velocity test a, component c:  w [ phi_a u_c + sum_d d_d phi_a F_cd ],
+//       F_cd = nu (d_d u_c + d_c u_d) - p delta_cd        (2 nu eps:eps, -p div)
+//   pressure test v:              -w psi_v div u.
+// C is the per-node AffineConstraints condensation of the assembly kernel
+// (no-normal-flux / no-slip velocity constraints; pressure unconstrained). The
+// rows and columns of constrained velocity dofs of C^T K C vanish; their
+// entries are the |K_ii| diagonal the assembly adds, applied by a small fix-up
+// pass from the assembled diagonal (k_mf_constrained).
+//
+// Layout: 27 lanes per cell (lexicographic node / quadrature index, x
+// fastest), two cells per wave, eight per 256-thread workgroup. Values and
+// reference gradients at the 27 Gauss points come from sum factorisation over
+// the 3x3 1D tables (3 passes forward, 3 back, 27 FMAs per component and pass
+// set), exchanged through a 12-field LDS slab per cell with wave-level
+// synchronisation only. J^-1 and JxW per point are precomputed once per mesh
+// (k_mf_geometry; the mesh does not move) and streamed: 2160 B per cell, the
+// dominant HBM traffic (SURVEY §8d's matrix-free byte count). The cell loop
+// runs over the colour classes of the assembly, so no two workgroups of a
+// launch touch the same dof: plain read-modify-write, deterministic, and the
+// first cell touching a dof (colour order) stores instead of adding, so dst
+// needs no zero fill.
+#include <hip/hip_runtime.h>
+
+#include "../device.h"
+#include "../fe_tables.h"
+
+namespace dcp {
+namespace {
+
+constexpr double l2c(int i, double x) {
+  return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+}
+constexpr double dl2c(int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; }
+constexpr double l1c(int i, double x) { return i == 0 ? 1 - x : x; }
+
+// 1D Q2 basis n at Gauss point q: value / derivative
+__constant__ double mL[3][3] = {{l2c(0, kGaussX[0]), l2c(0, kGaussX[1]), l2c(0, kGaussX[2])},
+                                {l2c(1, kGaussX[0]), l2c(1, kGaussX[1]), l2c(1, kGaussX[2])},
+                                {l2c(2, kGaussX[0]), l2c(2, kGaussX[1]), l2c(2, kGaussX[2])}};
+__constant__ double mD[3][3] = {{dl2c(0, kGaussX[0]), dl2c(0, kGaussX[1]), dl2c(0, kGaussX[2])},
+                                {dl2c(1, kGaussX[0]), dl2c(1, kGaussX[1]), dl2c(1, kGaussX[2])},
+                                {dl2c(2, kGaussX[0]), dl2c(2, kGaussX[1]), dl2c(2, kGaussX[2])}};
+struct PsiTable {
+  double v[27][8];  // Q1 vertex function v at Gauss point q
+};
+constexpr PsiTable make_psi() {
+  PsiTable t{};
+  for (int q = 0; q < 27; ++q)
+    for (int v = 0; v < 8; ++v)
+      t.v[q][v] = l1c(v & 1, kGaussX[q % 3]) * l1c((v >> 1) & 1, kGaussX[(q / 3) % 3]) *
+                  l1c(v >> 2, kGaussX[q / 9]);
+  return t;
+}
+__constant__ PsiTable mPsi = make_psi();
+__constant__ double mW[3] = {kGaussW[0], kGaussW[1], kGaussW[2]};
+
+constexpr int kMfCells = 8;     // cells per 256-thread workgroup
+constexpr int kMfFields = 13;   // LDS fields of 27 doubles per cell
+
+// wave-level LDS hand-off (a cell never spans waves)
+__device__ inline void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// full = C reduced (no-normal-flux: component k eliminated; no-slip: 0)
+__device__ inline void expand(const NodeConstraint& nc, const double r[3], double f[3]) {
+  if (nc.type == 0) {
+    f[0] = r[0]; f[1] = r[1]; f[2] = r[2];
+  } else if (nc.type == 1) {
+    f[0] = f[1] = f[2] = 0.0;
+  } else {
+    double s = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      f[d] = r[d];
+      if (d != nc.k) s += nc.w[d] * r[d];
+    }
+    f[nc.k] = s;
+  }
+}
+// reduced = C^T full
+__device__ inline void condense(const NodeConstraint& nc, double f[3]) {
+  if (nc.type == 1) {
+    f[0] = f[1] = f[2] = 0.0;
+  } else if (nc.type == 2) {
+    const double fk = f[nc.k];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) f[d] = d == nc.k ? 0.0 : f[d] + nc.w[d] * fk;
+  }
+}
+
+// J^-1 (dxi_e/dx_d as [e][d]) and JxW of the Q2 isoparametric map at every
+// Gauss point, stored [cell][k][q] (k < 9: J^-1, k = 9: JxW). Same formulas as
+// the assembly kernel (kernels/assembly.hip, k_nse_system).
+__global__ __launch_bounds__(256) void k_mf_geometry(CellData cd, double* __restrict__ geo) {
+  __shared__ double X[kMfCells][81];
+  const int slot = threadIdx.x >> 5, t = threadIdx.x & 31;
+  const int cell = blockIdx.x * kMfCells + slot;
+  const bool active = t < 27 && cell < cd.n_cells;
+  if (active) {
+    const int n = cd.cell_q2[27 * size_t(cell) + t];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) X[slot][3 * t + d] = cd.xyz[3 * size_t(n) + d];
+  }
+  __syncthreads();
+  if (!active) return;
+  const int q0 = t % 3, q1 = (t / 3) % 3, q2 = t / 9;
+  double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+  for (int n = 0; n < 27; ++n) {
+    const int a = n % 3, b = (n / 3) % 3, c = n / 9;
+    const double la = mL[a][q0], lb = mL[b][q1], lc = mL[c][q2];
+    const double g0 = mD[a][q0] * lb * lc, g1 = la * mD[b][q1] * lc, g2 = la * lb * mD[c][q2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double Xi = X[slot][3 * n + i];
+      J[i][0] += Xi * g0;
+      J[i][1] += Xi * g1;
+      J[i][2] += Xi * g2;
+    }
+  }
+  const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+  const double c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+  const double c02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+  const double det = J[0][0] * c00 + J[0][1] * c01 + J[0][2] * c02;
+  const double id = 1.0 / det;
+  double Ji[9];
+  Ji[0] = c00 * id;
+  Ji[1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) * id;
+  Ji[2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) * id;
+  Ji[3] = c01 * id;
+  Ji[4] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) * id;
+  Ji[5] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) * id;
+  Ji[6] = c02 * id;
+  Ji[7] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) * id;
+  Ji[8] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) * id;
+  double* g = geo + 270 * size_t(cell);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) g[27 * k + t] = Ji[k];
+  g[243 + t] = det * mW[q0] * mW[q1] * mW[q2];
+}
+
+// One colour class of the matrix-free apply. STOKES: [A B^T; B 0] on the
+// [u | p] vector (p at offset n_u); else the velocity block A alone.
+template <bool STOKES>
+__global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __restrict__ cells,
+                                                   int n, double nu,
+                                                   const double* __restrict__ src,
+                                                   double* __restrict__ dst) {
+  __shared__ double slab[kMfCells][kMfFields][27];
+  const int slot = threadIdx.x >> 5, t = threadIdx.x & 31;
+  const int ci = blockIdx.x * kMfCells + slot;
+  const bool active = t < 27 && ci < n;
+  double(*B)[27] = slab[slot];
+  const int i = t % 3, j = (t / 3) % 3, k = t / 9;
+  int cell = 0, node = 0;
+  NodeConstraint nc{};
+  uint64_t first = 0;
+  if (active) {
+    cell = cells[ci];
+    first = md.first[cell];
+    node = md.cell_q2[27 * size_t(cell) + t];
+    nc = md.vcon[node];
+    const double r[3] = {src[3 * size_t(node)], src[3 * size_t(node) + 1],
+                         src[3 * size_t(node) + 2]};
+    double f[3];
+    expand(nc, r, f);
+    B[0][t] = f[0];
+    B[1][t] = f[1];
+    B[2][t] = f[2];
+    if (STOKES && t < 8) B[3][t] = src[md.n_u + md.cell_p[8 * size_t(cell) + t]];
+  }
+  wsync();
+  // ---- values and reference gradients at the Gauss points
+  double o[9];
+  double pq = 0.0;
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // pass x: (n0 -> q0 = i)
+      const double* x = &B[c][3 * j + 9 * k];
+      o[c] = mL[0][i] * x[0] + mL[1][i] * x[1] + mL[2][i] * x[2];
+      o[3 + c] = mD[0][i] * x[0] + mD[1][i] * x[1] + mD[2][i] * x[2];
+    }
+    if (STOKES) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) pq += mPsi.v[t][v] * B[3][v];
+    }
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) B[f][t] = o[f];
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // pass y: (n1 -> q1 = j)
+      const double* v = &B[c][i + 9 * k];
+      const double* dx = &B[3 + c][i + 9 * k];
+      o[c] = mL[0][j] * v[0] + mL[1][j] * v[3] + mL[2][j] * v[6];
+      o[3 + c] = mL[0][j] * dx[0] + mL[1][j] * dx[3] + mL[2][j] * dx[6];
+      o[6 + c] = mD[0][j] * v[0] + mD[1][j] * v[3] + mD[2][j] * v[6];
+    }
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int f = 0; f < 9; ++f) B[f][t] = o[f];
+  }
+  wsync();
+  double Vh[3], Fh[3][3], sq = 0.0;
+  if (active) {
+    double u[3], Gh[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // pass z: (n2 -> q2 = k)
+      const double* v = &B[c][i + 3 * j];
+      const double* dx = &B[3 + c][i + 3 * j];
+      const double* dy = &B[6 + c][i + 3 * j];
+      u[c] = mL[0][k] * v[0] + mL[1][k] * v[9] + mL[2][k] * v[18];
+      Gh[c][0] = mL[0][k] * dx[0] + mL[1][k] * dx[9] + mL[2][k] * dx[18];
+      Gh[c][1] = mL[0][k] * dy[0] + mL[1][k] * dy[9] + mL[2][k] * dy[18];
+      Gh[c][2] = mD[0][k] * v[0] + mD[1][k] * v[9] + mD[2][k] * v[18];
+    }
+    // quadrature point q = t: physical gradient, flux, back to reference
+    const double* g = md.geo + 270 * size_t(cell) + t;
+    double Ji[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) Ji[e] = g[27 * e];
+    const double w = g[243];
+    double G[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+        G[c][d] = Gh[c][0] * Ji[d] + Gh[c][1] * Ji[3 + d] + Gh[c][2] * Ji[6 + d];
+    double F[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) F[c][d] = nu * (G[c][d] + G[d][c]);
+    if (STOKES) {
+      F[0][0] -= pq;
+      F[1][1] -= pq;
+      F[2][2] -= pq;
+      sq = -w * (G[0][0] + G[1][1] + G[2][2]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      Vh[c] = w * u[c];
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        Fh[c][e] = w * (Ji[3 * e] * F[c][0] + Ji[3 * e + 1] * F[c][1] + Ji[3 * e + 2] * F[c][2]);
+    }
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      B[c][t] = Vh[c];
+      B[3 + c][t] = Fh[c][0];
+      B[6 + c][t] = Fh[c][1];
+      B[9 + c][t] = Fh[c][2];
+    }
+    if (STOKES) B[12][t] = sq;
+  }
+  wsync();
+  // ---- test functions: transposed passes
+  double yp = 0.0;
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // back z: (q2 -> n2 = k)
+      const double* v = &B[c][i + 3 * j];
+      const double* fx = &B[3 + c][i + 3 * j];
+      const double* fy = &B[6 + c][i + 3 * j];
+      const double* fz = &B[9 + c][i + 3 * j];
+      o[c] = mL[k][0] * v[0] + mL[k][1] * v[9] + mL[k][2] * v[18] + mD[k][0] * fz[0] +
+             mD[k][1] * fz[9] + mD[k][2] * fz[18];
+      o[3 + c] = mL[k][0] * fx[0] + mL[k][1] * fx[9] + mL[k][2] * fx[18];
+      o[6 + c] = mL[k][0] * fy[0] + mL[k][1] * fy[9] + mL[k][2] * fy[18];
+    }
+    if (STOKES && t < 8) {
+      for (int q = 0; q < 27; ++q) yp += mPsi.v[q][t] * B[12][q];
+    }
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int f = 0; f < 9; ++f) B[f][t] = o[f];
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // back y: (q1 -> n1 = j)
+      const double* v = &B[c][i + 9 * k];
+      const double* fx = &B[3 + c][i + 9 * k];
+      const double* fy = &B[6 + c][i + 9 * k];
+      o[c] = mL[j][0] * v[0] + mL[j][1] * v[3] + mL[j][2] * v[6] + mD[j][0] * fy[0] +
+             mD[j][1] * fy[3] + mD[j][2] * fy[6];
+      o[3 + c] = mL[j][0] * fx[0] + mL[j][1] * fx[3] + mL[j][2] * fx[6];
+    }
+  }
+  wsync();
+  if (active) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) B[f][t] = o[f];
+  }
+  wsync();
+  if (!active) return;
+  double y[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {  // back x: (q0 -> n0 = i)
+    const double* v = &B[c][3 * j + 9 * k];
+    const double* fx = &B[3 + c][3 * j + 9 * k];
+    y[c] = mL[i][0] * v[0] + mL[i][1] * v[1] + mL[i][2] * v[2] + mD[i][0] * fx[0] +
+           mD[i][1] * fx[1] + mD[i][2] * fx[2];
+  }
+  condense(nc, y);
+  double* d = dst + 3 * size_t(node);
+  if ((first >> t) & 1) {
+    d[0] = y[0];
+    d[1] = y[1];
+    d[2] = y[2];
+  } else {
+    d[0] += y[0];
+    d[1] += y[1];
+    d[2] += y[2];
+  }
+  if (STOKES && t < 8) {
+    double* dp = dst + md.n_u + md.cell_p[8 * size_t(cell) + t];
+    *dp = ((first >> (32 + t)) & 1) ? yp : *dp + yp;
+  }
+}
+
+// constrained velocity dofs: dst = (assembled diagonal) * src
+__global__ void k_mf_constrained(int n, const int32_t* __restrict__ dof,
+                                 const int64_t* __restrict__ diag_pos,
+                                 const double* __restrict__ A_val, const double* __restrict__ src,
+                                 double* __restrict__ dst) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) dst[dof[e]] = A_val[diag_pos[e]] * src[dof[e]];
+}
+
+}  // namespace
+
+void mf_geometry(const CellData& cd, double* geo, hipStream_t s) {
+  if (cd.n_cells <= 0) return;
+  hipLaunchKernelGGL(k_mf_geometry, dim3((cd.n_cells + kMfCells - 1) / kMfCells), dim3(256), 0, s,
+                     cd, geo);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_apply_colour(const MfData& md, const int32_t* cells, int n, double nu, bool stokes,
+                     const double* src, double* dst, hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 grid((n + kMfCells - 1) / kMfCells);
+  if (stokes)
+    hipLaunchKernelGGL(k_mf_stokes<true>, grid, dim3(256), 0, s, md, cells, n, nu, src, dst);
+  else
+    hipLaunchKernelGGL(k_mf_stokes<false>, grid, dim3(256), 0, s, md, cells, n, nu, src, dst);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* A_val,
+                    const double* src, double* dst, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mf_constrained, dim3((n + 255) / 256), dim3(256), 0, s, n, dof, diag_pos,
+                     A_val, src, dst);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dcp

@@ -379,9 +379,29 @@ double householder_least_squares(std::vector<std::vector<double>> S, int m, int 
 
 struct NoConvergence {};
 
+// Matrix-free C^T K C over all (local) cells in colour order, then the
+// assembled diagonal on constrained velocity dofs (kernels/matfree.hip).
+void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
+  const MfData md = c.mfd();
+  const int v = stokes ? 0 : 1;
+  Timer* e = nullptr;
+  if (c.time_schur && c.mf_ev_used[v] < Ctx::kMfEvents) e = &c.mf_ev[v][c.mf_ev_used[v]++];
+  if (c.time_schur) c.mf_calls[v]++;
+  if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+  for (int k = 0; k < c.n_colors(); ++k)
+    mf_apply_colour(md, c.color_begin(k), c.color_size(k), c.ph.nu_sys, stokes, src, dst,
+                    c.stream);
+  mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.A_val.p, src, dst, c.stream);
+  if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+}
+
 // A (velocity-velocity block) on a velocity vector [u_own u_ghost]
 void a_vmult(Ctx& c, const double* src, double* dst) {
   halo_exchange(c, c.halo_v, const_cast<double*>(src));
+  if (c.matrix_free) {
+    mf_apply(c, src, dst, false);
+    return;
+  }
   spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
 }
 
@@ -516,6 +536,10 @@ void halo_exchange(Ctx& c, Ctx::Halo& h, double* v) {
 void nse_vmult(Ctx& c, const double* src, double* dst) {
   // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
   halo_exchange(c, c.halo_nse, const_cast<double*>(src));
+  if (c.matrix_free) {
+    mf_apply(c, src, dst, true);
+    return;
+  }
   spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
   spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src + c.n_u, dst, true, c.stream);
   spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);

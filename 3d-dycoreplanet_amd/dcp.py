@@ -27,6 +27,7 @@ NSE_SOLUTION, OLD_NSE_SOLUTION, T_SOLUTION, OLD_T_SOLUTION, NSE_RHS, T_RHS = ran
 ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
 OPT_SCHUR_EXPLICIT = 1
 OPT_FEEC_ZERO_MEAN = 2
+OPT_MATRIX_FREE = 3
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -83,6 +84,8 @@ class Timings(C.Structure):
         ("assemble_T_matrix_ms", C.c_double), ("assemble_T_rhs_ms", C.c_double),
         ("solve_nse_ms", C.c_double), ("solve_T_ms", C.c_double),
         ("schur_apply_ms_avg", C.c_double), ("schur_applies", C.c_long),
+        ("stokes_apply_ms_avg", C.c_double), ("velocity_apply_ms_avg", C.c_double),
+        ("stokes_applies", C.c_long), ("velocity_applies", C.c_long),
     ]
 
 
@@ -434,6 +437,11 @@ class Context:
         """True: apply S = B D^-1 B^T as one formed CSR matrix (default);
         False: B^T, Jacobi, B as SchurComplement::vmult does."""
         self._check(lib().dcp_set_option(self._h, OPT_SCHUR_EXPLICIT, int(bool(on))))
+
+    def set_matrix_free(self, on: bool):
+        """True (default): solver products with nse_matrix / its A block are
+        evaluated matrix-free; False: block-CSR SpMV of the assembled matrix."""
+        self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(bool(on))))
 
     def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
         self._feec_view = None

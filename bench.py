@@ -316,6 +316,28 @@ def main():
                      "traffic": pmc_traffic(args.refine, args.schur),
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
+    # matrix-free operator apply (north-star target, SURVEY §8d byte count):
+    # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point;
+    # one apply = one launch per cell colour + the constrained-dof fix-up
+    st_ms = np.mean([r[4]["stokes_apply_ms_avg"] for r in recs])
+    ve_ms = np.mean([r[4]["velocity_apply_ms_avg"] for r in recs])
+    if st_ms > 0 or ve_ms > 0:
+        nc = m.n_cells
+        st_bytes = 16 * n_nse + 4 * 89 * nc + 80 * 27 * nc
+        ve_bytes = 16 * m.n_u + 4 * 27 * nc + 80 * 27 * nc
+        if world > 1:
+            st_bytes, ve_bytes = st_bytes / world, ve_bytes / world
+        mf = {"kernel": "matrix-free [A B^T; B 0] x (k_mf_stokes<true>, one launch per colour)",
+              "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "bytes_per_apply": st_bytes, "avg_apply_ms": st_ms,
+              "applies_per_step": recs[-1][4]["stokes_applies"],
+              "achieved": st_bytes / (st_ms * 1e-3) / 1e9 if st_ms > 0 else None,
+              "velocity_block": {"bytes_per_apply": ve_bytes, "avg_apply_ms": ve_ms,
+                                 "applies_per_step": recs[-1][4]["velocity_applies"],
+                                 "achieved": ve_bytes / (ve_ms * 1e-3) / 1e9 if ve_ms > 0
+                                 else None}}
+        mf["frac"] = mf["achieved"] / HBM_PEAK_GBS if mf["achieved"] else None
+        out["roofline_matrix_free"] = mf
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_refine)
     if rank == 0:

@@ -122,6 +122,12 @@ int dcp_set_time_step(dcp_ctx* ctx, double dt);
  *   build_nse_preconditioner and apply it as one CSR SpMV; 0 = apply it as
  *   B^T, Jacobi, B like SchurComplement::vmult (schur_complement.hpp:143-150). */
 enum { DCP_OPT_SCHUR_EXPLICIT = 1 };
+/* DCP_OPT_MATRIX_FREE: 1 (default) = every [A B^T; B 0] and A product of the
+ *   solve (nse_matrix.vmult in SolverFGMRES, the A-GMRES of the do_solve_A
+ *   fallback) is evaluated matrix-free from the mesh (kernels/matfree.hip) with
+ *   the assembled diagonal for constrained dofs; 0 = block-CSR SpMV of the
+ *   assembled matrix. Same operator, different rounding. */
+enum { DCP_OPT_MATRIX_FREE = 3 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
@@ -204,6 +210,10 @@ typedef struct {
   double solve_nse_ms, solve_T_ms;
   double schur_apply_ms_avg; /* average device time of one Schur-complement apply */
   long schur_applies;
+  /* matrix-free applies of the last solve (DCP_OPT_MATRIX_FREE): [A B^T; B 0]
+   * (nse_matrix.vmult) and A alone (do_solve_A fallback); sampled device time */
+  double stokes_apply_ms_avg, velocity_apply_ms_avg;
+  long stokes_applies, velocity_applies;
 } dcp_timings;
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
 

@@ -124,10 +124,12 @@ def test_temperature_assembly(setup):
     assert rel_max(ctx.get_state(dcp.T_RHS), orc.T_rhs()) < 1e-12
 
 
-@pytest.mark.parametrize("explicit", [True, False], ids=["S-explicit", "S-composite"])
-def test_operator_applies(setup, explicit):
+@pytest.mark.parametrize("explicit,mfree", [(True, True), (False, True), (True, False)],
+                         ids=["S-explicit", "S-composite", "assembled-A"])
+def test_operator_applies(setup, explicit, mfree):
     m, ph, ctx, orc = setup
     ctx.set_schur_explicit(explicit)
+    ctx.set_matrix_free(mfree)
     rng = np.random.default_rng(SEED + 3)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
     ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
@@ -148,6 +150,7 @@ def test_operator_applies(setup, explicit):
     do, ito = orc.block_preconditioner_vmult(x)
     assert abs(itg - ito) <= max(2, 0.05 * ito)
     assert rel2(dg, do) < 1e-10
+    ctx.set_matrix_free(True)
 
 
 @pytest.mark.parametrize("explicit", [True, False], ids=["S-explicit", "S-composite"])
@@ -213,4 +216,26 @@ def test_large_mesh_properties():
     r1 = ctx.get_state(dcp.NSE_RHS)
     ctx.assemble_nse_system()
     assert np.array_equal(r1, ctx.get_state(dcp.NSE_RHS))
+    ctx.close()
+
+
+@pytest.mark.parametrize("kind", ["shell-r3", "shell-radial-r2", "shell-r1"])
+def test_matrix_free_matches_assembled(kind):
+    """kernels/matfree.hip against the block-CSR product of the assembled
+    nse_matrix (same operator, summation order differs), on random inputs
+    including the constrained entries."""
+    m = dcp.HostMesh(refine=int(kind[-1]), normals="radial" if "radial" in kind else "consistent")
+    ph = dcp.classic_physics()
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh(m)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
+    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+    ctx.assemble_nse_system()
+    x = np.random.default_rng(SEED + 11).uniform(-1, 1, m.n_u + m.n_p)
+    ctx.set_matrix_free(False)
+    ya = ctx.nse_vmult(x)
+    ctx.set_matrix_free(True)
+    ym = ctx.nse_vmult(x)
+    assert rel_max(ym, ya) < 1e-13
     ctx.close()
