@@ -735,20 +735,25 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       // velocity dofs with the position of their assembled diagonal entry,
       // per-point geometry
       std::vector<uint64_t> first(n_cells, 0);
+      std::vector<int32_t> oq2(size_t(n_cells) * 27), op(size_t(n_cells) * 8);
       std::vector<uint8_t> vt(nv, 0), pt(n_p, 0);
       for (size_t e = 0; e < ccells.size(); ++e) {
         const int cell = ccells[e];
         uint64_t bits = 0;
         for (int t = 0; t < 27; ++t) {
           const int n = q2[27 * size_t(cell) + t];
+          oq2[27 * e + t] = n;
           if (!vt[n]) { vt[n] = 1; bits |= uint64_t(1) << t; }
         }
         for (int v = 0; v < 8; ++v) {
           const int p = pd[8 * size_t(cell) + v];
+          op[8 * e + v] = p;
           if (!pt[p]) { pt[p] = 1; bits |= uint64_t(1) << (32 + v); }
         }
-        first[cell] = bits;
+        first[e] = bits;
       }
+      c.mf_q2.upload(oq2);
+      c.mf_p.upload(op);
       std::vector<int32_t> cdof;
       std::vector<int64_t> cpos;
       for (int n = 0; n < nv; ++n) {
@@ -767,7 +772,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_cpos.upload(cpos);
       c.mf_ncon = int(cdof.size());
       c.mf_geo.alloc(size_t(n_cells) * 270);
-      mf_geometry(c.cd(), c.mf_geo.p, c.stream);
+      mf_geometry(c.cd(), c.color_cells.p, c.mf_geo.p, c.stream);
     }
     const size_t nn = size_t(n_u + n_p);
     c.nse_sol.alloc(nn);

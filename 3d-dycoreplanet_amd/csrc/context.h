@@ -103,13 +103,14 @@ struct Ctx {
   // matrix-free operator (kernels/matfree.hip): geometry, first-touch bits,
   // constrained velocity dofs with their assembled diagonal entries
   bool matrix_free = true;
-  DBuf<double> mf_geo;
+  DBuf<double> mf_geo;                  // colour order (see MfData)
+  DBuf<int32_t> mf_q2, mf_p;
   DBuf<uint64_t> mf_first;
   DBuf<int32_t> mf_cdof;
   DBuf<int64_t> mf_cpos;
   int mf_ncon = 0;
   MfData mfd() const {
-    return MfData{n_u, cell_q2.p, cell_p.p, vcon.p, mf_geo.p, mf_first.p};
+    return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};
   }
   // state
   DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;

@@ -78,18 +78,20 @@ struct NseOut {
 
 // ---- matfree.hip ----------------------------------------------------------
 // Matrix-free [A B^T; B 0] (or A alone) of the classic Q2^3/Q1 system.
+// Per-cell arrays in colour order (position e = e-th cell of the colour-sorted
+// cell list).
 struct MfData {
   int n_u;                     // offset of the pressure block in [u | p]
   const int32_t* cell_q2;      // [n_cells][27]
   const int32_t* cell_p;       // [n_cells][8]
   const NodeConstraint* vcon;  // [n_vnodes]
   const double* geo;           // [n_cells][10][27]: J^-1 (9), JxW
-  const uint64_t* first;       // [n_cells] first-touch bits (colour order): node t -> bit t,
+  const uint64_t* first;       // [n_cells] first-touch bits: node t -> bit t,
                                // pressure vertex v -> bit 32 + v
 };
-void mf_geometry(const CellData& cd, double* geo, hipStream_t s);
-// one colour class: dst (+)= C^T K C src on the class's cells
-void mf_apply_colour(const MfData& md, const int32_t* cells, int n, double nu, bool stokes,
+void mf_geometry(const CellData& cd, const int32_t* order, double* geo, hipStream_t s);
+// one colour class = positions [base, base + n): dst (+)= C^T K C src
+void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);
 // constrained velocity dofs: dst[dof] = A_val[diag_pos] * src[dof]
 void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* A_val,

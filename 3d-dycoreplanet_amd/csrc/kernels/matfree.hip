@@ -15,7 +15,10 @@
 // pass from the assembled diagonal (k_mf_constrained).
 //
 // Layout: 27 lanes per cell (lexicographic node / quadrature index, x
-// fastest), two cells per wave, eight per 256-thread workgroup. Values and
+// fastest), two cells per wave, four per 128-thread workgroup; the per-cell
+// arrays (node map, pressure dofs, first-touch bits, geometry) are stored in
+// colour order, so a colour class is a contiguous range streamed without an
+// indirection. Values and
 // reference gradients at the 27 Gauss points come from sum factorisation over
 // the 3x3 1D tables (3 passes forward, 3 back, 27 FMAs per component and pass
 // set), exchanged through a 12-field LDS slab per cell with wave-level
@@ -27,6 +30,8 @@
 // first cell touching a dof (colour order) stores instead of adding, so dst
 // needs no zero fill.
 #include <hip/hip_runtime.h>
+
+#include <utility>
 
 #include "../device.h"
 #include "../fe_tables.h"
@@ -40,28 +45,54 @@ constexpr double l2c(int i, double x) {
 constexpr double dl2c(int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; }
 constexpr double l1c(int i, double x) { return i == 0 ? 1 - x : x; }
 
-// 1D Q2 basis n at Gauss point q: value / derivative
+// 1D Q2 basis n at Gauss point q: value / derivative (geometry precompute)
 __constant__ double mL[3][3] = {{l2c(0, kGaussX[0]), l2c(0, kGaussX[1]), l2c(0, kGaussX[2])},
                                 {l2c(1, kGaussX[0]), l2c(1, kGaussX[1]), l2c(1, kGaussX[2])},
                                 {l2c(2, kGaussX[0]), l2c(2, kGaussX[1]), l2c(2, kGaussX[2])}};
 __constant__ double mD[3][3] = {{dl2c(0, kGaussX[0]), dl2c(0, kGaussX[1]), dl2c(0, kGaussX[2])},
                                 {dl2c(1, kGaussX[0]), dl2c(1, kGaussX[1]), dl2c(1, kGaussX[2])},
                                 {dl2c(2, kGaussX[0]), dl2c(2, kGaussX[1]), dl2c(2, kGaussX[2])}};
-struct PsiTable {
-  double v[27][8];  // Q1 vertex function v at Gauss point q
-};
-constexpr PsiTable make_psi() {
-  PsiTable t{};
-  for (int q = 0; q < 27; ++q)
-    for (int v = 0; v < 8; ++v)
-      t.v[q][v] = l1c(v & 1, kGaussX[q % 3]) * l1c((v >> 1) & 1, kGaussX[(q / 3) % 3]) *
-                  l1c(v >> 2, kGaussX[q / 9]);
-  return t;
-}
-__constant__ PsiTable mPsi = make_psi();
 __constant__ double mW[3] = {kGaussW[0], kGaussW[1], kGaussW[2]};
 
-constexpr int kMfCells = 8;     // cells per 256-thread workgroup
+// The apply kernel picks its 1D coefficients by lane index with selects
+// between compile-time constants (no lane-divergent constant-memory loads).
+__device__ inline double sel3(int x, double a, double b, double c) {
+  return x == 0 ? a : (x == 1 ? b : c);
+}
+// L[n][q] / D[n][q] with n compile-time, q per lane
+template <int N>
+__device__ inline double Lq(int q) {
+  return sel3(q, l2c(N, kGaussX[0]), l2c(N, kGaussX[1]), l2c(N, kGaussX[2]));
+}
+template <int N>
+__device__ inline double Dq(int q) {
+  return sel3(q, dl2c(N, kGaussX[0]), dl2c(N, kGaussX[1]), dl2c(N, kGaussX[2]));
+}
+// L[n][q] / D[n][q] with q compile-time, n per lane
+template <int Q>
+__device__ inline double Ln(int n) {
+  return sel3(n, l2c(0, kGaussX[Q]), l2c(1, kGaussX[Q]), l2c(2, kGaussX[Q]));
+}
+template <int Q>
+__device__ inline double Dn(int n) {
+  return sel3(n, dl2c(0, kGaussX[Q]), dl2c(1, kGaussX[Q]), dl2c(2, kGaussX[Q]));
+}
+// Q1 vertex function v (per lane) at Gauss point Q (compile-time)
+template <int Q>
+__device__ inline double psi_v(int v) {
+  constexpr double x0 = kGaussX[Q % 3], x1 = kGaussX[(Q / 3) % 3], x2 = kGaussX[Q / 9];
+  return ((v & 1) ? l1c(1, x0) : l1c(0, x0)) * (((v >> 1) & 1) ? l1c(1, x1) : l1c(0, x1)) *
+         ((v >> 2) ? l1c(1, x2) : l1c(0, x2));
+}
+template <int... Q>
+__device__ inline double psi_dot(int v, const double* s, std::integer_sequence<int, Q...>) {
+  double r = 0.0;
+  ((r += psi_v<Q>(v) * s[Q]), ...);
+  return r;
+}
+
+constexpr int kMfCells = 4;    // cells per 128-thread workgroup (two per wave)
+constexpr int kGeoCells = 8;            // k_mf_geometry: cells per 256-thread workgroup
 constexpr int kMfFields = 13;   // LDS fields of 27 doubles per cell
 
 // wave-level LDS hand-off (a cell never spans waves)
@@ -101,11 +132,14 @@ __device__ inline void condense(const NodeConstraint& nc, double f[3]) {
 // J^-1 (dxi_e/dx_d as [e][d]) and JxW of the Q2 isoparametric map at every
 // Gauss point, stored [cell][k][q] (k < 9: J^-1, k = 9: JxW). Same formulas as
 // the assembly kernel (kernels/assembly.hip, k_nse_system).
-__global__ __launch_bounds__(256) void k_mf_geometry(CellData cd, double* __restrict__ geo) {
-  __shared__ double X[kMfCells][81];
+// Position e of the output belongs to cell order[e] (colour order).
+__global__ __launch_bounds__(256) void k_mf_geometry(CellData cd, const int32_t* __restrict__ order,
+                                                     double* __restrict__ geo) {
+  __shared__ double X[kGeoCells][81];
   const int slot = threadIdx.x >> 5, t = threadIdx.x & 31;
-  const int cell = blockIdx.x * kMfCells + slot;
-  const bool active = t < 27 && cell < cd.n_cells;
+  const int pos = blockIdx.x * kGeoCells + slot;
+  const bool active = t < 27 && pos < cd.n_cells;
+  const int cell = active ? order[pos] : 0;
   if (active) {
     const int n = cd.cell_q2[27 * size_t(cell) + t];
 #pragma unroll
@@ -142,17 +176,17 @@ __global__ __launch_bounds__(256) void k_mf_geometry(CellData cd, double* __rest
   Ji[6] = c02 * id;
   Ji[7] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) * id;
   Ji[8] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) * id;
-  double* g = geo + 270 * size_t(cell);
+  double* g = geo + 270 * size_t(pos);
 #pragma unroll
   for (int k = 0; k < 9; ++k) g[27 * k + t] = Ji[k];
   g[243 + t] = det * mW[q0] * mW[q1] * mW[q2];
 }
 
-// One colour class of the matrix-free apply. STOKES: [A B^T; B 0] on the
-// [u | p] vector (p at offset n_u); else the velocity block A alone.
+// One colour class of the matrix-free apply: positions [base, base + n) of the
+// colour-ordered cell arrays. STOKES: [A B^T; B 0] on the [u | p] vector (p at
+// offset n_u); else the velocity block A alone.
 template <bool STOKES>
-__global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __restrict__ cells,
-                                                   int n, double nu,
+__global__ __launch_bounds__(32 * kMfCells) void k_mf_stokes(MfData md, int base, int n, double nu,
                                                    const double* __restrict__ src,
                                                    double* __restrict__ dst) {
   __shared__ double slab[kMfCells][kMfFields][27];
@@ -161,13 +195,20 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
   const bool active = t < 27 && ci < n;
   double(*B)[27] = slab[slot];
   const int i = t % 3, j = (t / 3) % 3, k = t / 9;
-  int cell = 0, node = 0;
+  const size_t e = size_t(base) + (active ? ci : 0);
+  int node = 0, pdof = 0;
   NodeConstraint nc{};
   uint64_t first = 0;
+  double Ji[9], w = 0.0;
   if (active) {
-    cell = cells[ci];
-    first = md.first[cell];
-    node = md.cell_q2[27 * size_t(cell) + t];
+    // independent streamed loads first: node map, geometry, first-touch bits
+    node = md.cell_q2[27 * e + t];
+    const double* g = md.geo + 270 * e + t;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Ji[q] = g[27 * q];
+    w = g[243];
+    first = md.first[e];
+    if (STOKES && t < 8) pdof = md.cell_p[8 * e + t];
     nc = md.vcon[node];
     const double r[3] = {src[3 * size_t(node)], src[3 * size_t(node) + 1],
                          src[3 * size_t(node) + 2]};
@@ -176,22 +217,30 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
     B[0][t] = f[0];
     B[1][t] = f[1];
     B[2][t] = f[2];
-    if (STOKES && t < 8) B[3][t] = src[md.n_u + md.cell_p[8 * size_t(cell) + t]];
+    if (STOKES && t < 8) B[3][t] = src[md.n_u + pdof];
   }
   wsync();
   // ---- values and reference gradients at the Gauss points
   double o[9];
   double pq = 0.0;
   if (active) {
+    const double l0 = Lq<0>(i), l1 = Lq<1>(i), l2 = Lq<2>(i);
+    const double d0 = Dq<0>(i), d1 = Dq<1>(i), d2 = Dq<2>(i);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {  // pass x: (n0 -> q0 = i)
       const double* x = &B[c][3 * j + 9 * k];
-      o[c] = mL[0][i] * x[0] + mL[1][i] * x[1] + mL[2][i] * x[2];
-      o[3 + c] = mD[0][i] * x[0] + mD[1][i] * x[1] + mD[2][i] * x[2];
+      o[c] = l0 * x[0] + l1 * x[1] + l2 * x[2];
+      o[3 + c] = d0 * x[0] + d1 * x[1] + d2 * x[2];
     }
     if (STOKES) {
-#pragma unroll
-      for (int v = 0; v < 8; ++v) pq += mPsi.v[t][v] * B[3][v];
+      // p at q = t from the 8 vertex values
+      const double a0 = 1.0 - sel3(i, kGaussX[0], kGaussX[1], kGaussX[2]);
+      const double b0 = 1.0 - sel3(j, kGaussX[0], kGaussX[1], kGaussX[2]);
+      const double c0 = 1.0 - sel3(k, kGaussX[0], kGaussX[1], kGaussX[2]);
+      const double a1 = 1.0 - a0, b1 = 1.0 - b0, c1 = 1.0 - c0;
+      const double* p = B[3];
+      pq = c0 * (b0 * (a0 * p[0] + a1 * p[1]) + b1 * (a0 * p[2] + a1 * p[3])) +
+           c1 * (b0 * (a0 * p[4] + a1 * p[5]) + b1 * (a0 * p[6] + a1 * p[7]));
     }
   }
   wsync();
@@ -201,13 +250,15 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
   }
   wsync();
   if (active) {
+    const double l0 = Lq<0>(j), l1 = Lq<1>(j), l2 = Lq<2>(j);
+    const double d0 = Dq<0>(j), d1 = Dq<1>(j), d2 = Dq<2>(j);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {  // pass y: (n1 -> q1 = j)
       const double* v = &B[c][i + 9 * k];
       const double* dx = &B[3 + c][i + 9 * k];
-      o[c] = mL[0][j] * v[0] + mL[1][j] * v[3] + mL[2][j] * v[6];
-      o[3 + c] = mL[0][j] * dx[0] + mL[1][j] * dx[3] + mL[2][j] * dx[6];
-      o[6 + c] = mD[0][j] * v[0] + mD[1][j] * v[3] + mD[2][j] * v[6];
+      o[c] = l0 * v[0] + l1 * v[3] + l2 * v[6];
+      o[3 + c] = l0 * dx[0] + l1 * dx[3] + l2 * dx[6];
+      o[6 + c] = d0 * v[0] + d1 * v[3] + d2 * v[6];
     }
   }
   wsync();
@@ -216,25 +267,22 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
     for (int f = 0; f < 9; ++f) B[f][t] = o[f];
   }
   wsync();
-  double Vh[3], Fh[3][3], sq = 0.0;
+  double sq = 0.0;
   if (active) {
+    const double l0 = Lq<0>(k), l1 = Lq<1>(k), l2 = Lq<2>(k);
+    const double d0 = Dq<0>(k), d1 = Dq<1>(k), d2 = Dq<2>(k);
     double u[3], Gh[3][3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {  // pass z: (n2 -> q2 = k)
       const double* v = &B[c][i + 3 * j];
       const double* dx = &B[3 + c][i + 3 * j];
       const double* dy = &B[6 + c][i + 3 * j];
-      u[c] = mL[0][k] * v[0] + mL[1][k] * v[9] + mL[2][k] * v[18];
-      Gh[c][0] = mL[0][k] * dx[0] + mL[1][k] * dx[9] + mL[2][k] * dx[18];
-      Gh[c][1] = mL[0][k] * dy[0] + mL[1][k] * dy[9] + mL[2][k] * dy[18];
-      Gh[c][2] = mD[0][k] * v[0] + mD[1][k] * v[9] + mD[2][k] * v[18];
+      u[c] = l0 * v[0] + l1 * v[9] + l2 * v[18];
+      Gh[c][0] = l0 * dx[0] + l1 * dx[9] + l2 * dx[18];
+      Gh[c][1] = l0 * dy[0] + l1 * dy[9] + l2 * dy[18];
+      Gh[c][2] = d0 * v[0] + d1 * v[9] + d2 * v[18];
     }
     // quadrature point q = t: physical gradient, flux, back to reference
-    const double* g = md.geo + 270 * size_t(cell) + t;
-    double Ji[9];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) Ji[e] = g[27 * e];
-    const double w = g[243];
     double G[3][3];
 #pragma unroll
     for (int c = 0; c < 3; ++c)
@@ -252,27 +300,22 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
       F[2][2] -= pq;
       sq = -w * (G[0][0] + G[1][1] + G[2][2]);
     }
+    // every lane has read its pass-z inputs before any lane overwrites them
+    wsync();
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      Vh[c] = w * u[c];
+      B[c][t] = w * u[c];
 #pragma unroll
-      for (int e = 0; e < 3; ++e)
-        Fh[c][e] = w * (Ji[3 * e] * F[c][0] + Ji[3 * e + 1] * F[c][1] + Ji[3 * e + 2] * F[c][2]);
-    }
-  }
-  wsync();
-  if (active) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      B[c][t] = Vh[c];
-      B[3 + c][t] = Fh[c][0];
-      B[6 + c][t] = Fh[c][1];
-      B[9 + c][t] = Fh[c][2];
+      for (int e2 = 0; e2 < 3; ++e2)
+        B[3 + 3 * e2 + c][t] =
+            w * (Ji[3 * e2] * F[c][0] + Ji[3 * e2 + 1] * F[c][1] + Ji[3 * e2 + 2] * F[c][2]);
     }
     if (STOKES) B[12][t] = sq;
+  } else {
+    wsync();
   }
   wsync();
-  // ---- test functions: transposed passes
+  // ---- test functions: transposed passes (fields: V 0-2, Fx 3-5, Fy 6-8, Fz 9-11)
   double yp = 0.0;
   if (active) {
 #pragma unroll
@@ -281,14 +324,12 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
       const double* fx = &B[3 + c][i + 3 * j];
       const double* fy = &B[6 + c][i + 3 * j];
       const double* fz = &B[9 + c][i + 3 * j];
-      o[c] = mL[k][0] * v[0] + mL[k][1] * v[9] + mL[k][2] * v[18] + mD[k][0] * fz[0] +
-             mD[k][1] * fz[9] + mD[k][2] * fz[18];
-      o[3 + c] = mL[k][0] * fx[0] + mL[k][1] * fx[9] + mL[k][2] * fx[18];
-      o[6 + c] = mL[k][0] * fy[0] + mL[k][1] * fy[9] + mL[k][2] * fy[18];
+      o[c] = Ln<0>(k) * v[0] + Ln<1>(k) * v[9] + Ln<2>(k) * v[18] + Dn<0>(k) * fz[0] +
+             Dn<1>(k) * fz[9] + Dn<2>(k) * fz[18];
+      o[3 + c] = Ln<0>(k) * fx[0] + Ln<1>(k) * fx[9] + Ln<2>(k) * fx[18];
+      o[6 + c] = Ln<0>(k) * fy[0] + Ln<1>(k) * fy[9] + Ln<2>(k) * fy[18];
     }
-    if (STOKES && t < 8) {
-      for (int q = 0; q < 27; ++q) yp += mPsi.v[q][t] * B[12][q];
-    }
+    if (STOKES && t < 8) yp = psi_dot(t, B[12], std::make_integer_sequence<int, 27>{});
   }
   wsync();
   if (active) {
@@ -302,9 +343,9 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
       const double* v = &B[c][i + 9 * k];
       const double* fx = &B[3 + c][i + 9 * k];
       const double* fy = &B[6 + c][i + 9 * k];
-      o[c] = mL[j][0] * v[0] + mL[j][1] * v[3] + mL[j][2] * v[6] + mD[j][0] * fy[0] +
-             mD[j][1] * fy[3] + mD[j][2] * fy[6];
-      o[3 + c] = mL[j][0] * fx[0] + mL[j][1] * fx[3] + mL[j][2] * fx[6];
+      o[c] = Ln<0>(j) * v[0] + Ln<1>(j) * v[3] + Ln<2>(j) * v[6] + Dn<0>(j) * fy[0] +
+             Dn<1>(j) * fy[3] + Dn<2>(j) * fy[6];
+      o[3 + c] = Ln<0>(j) * fx[0] + Ln<1>(j) * fx[3] + Ln<2>(j) * fx[6];
     }
   }
   wsync();
@@ -319,8 +360,8 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
   for (int c = 0; c < 3; ++c) {  // back x: (q0 -> n0 = i)
     const double* v = &B[c][3 * j + 9 * k];
     const double* fx = &B[3 + c][3 * j + 9 * k];
-    y[c] = mL[i][0] * v[0] + mL[i][1] * v[1] + mL[i][2] * v[2] + mD[i][0] * fx[0] +
-           mD[i][1] * fx[1] + mD[i][2] * fx[2];
+    y[c] = Ln<0>(i) * v[0] + Ln<1>(i) * v[1] + Ln<2>(i) * v[2] + Dn<0>(i) * fx[0] +
+           Dn<1>(i) * fx[1] + Dn<2>(i) * fx[2];
   }
   condense(nc, y);
   double* d = dst + 3 * size_t(node);
@@ -334,7 +375,7 @@ __global__ __launch_bounds__(256) void k_mf_stokes(MfData md, const int32_t* __r
     d[2] += y[2];
   }
   if (STOKES && t < 8) {
-    double* dp = dst + md.n_u + md.cell_p[8 * size_t(cell) + t];
+    double* dp = dst + md.n_u + pdof;
     *dp = ((first >> (32 + t)) & 1) ? yp : *dp + yp;
   }
 }
@@ -350,21 +391,23 @@ __global__ void k_mf_constrained(int n, const int32_t* __restrict__ dof,
 
 }  // namespace
 
-void mf_geometry(const CellData& cd, double* geo, hipStream_t s) {
+void mf_geometry(const CellData& cd, const int32_t* order, double* geo, hipStream_t s) {
   if (cd.n_cells <= 0) return;
-  hipLaunchKernelGGL(k_mf_geometry, dim3((cd.n_cells + kMfCells - 1) / kMfCells), dim3(256), 0, s,
-                     cd, geo);
+  hipLaunchKernelGGL(k_mf_geometry, dim3((cd.n_cells + kGeoCells - 1) / kGeoCells), dim3(256), 0, s,
+                     cd, order, geo);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void mf_apply_colour(const MfData& md, const int32_t* cells, int n, double nu, bool stokes,
+void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s) {
   if (n <= 0) return;
   const dim3 grid((n + kMfCells - 1) / kMfCells);
   if (stokes)
-    hipLaunchKernelGGL(k_mf_stokes<true>, grid, dim3(256), 0, s, md, cells, n, nu, src, dst);
+    hipLaunchKernelGGL(k_mf_stokes<true>, grid, dim3(32 * kMfCells), 0, s, md, base, n, nu, src,
+                       dst);
   else
-    hipLaunchKernelGGL(k_mf_stokes<false>, grid, dim3(256), 0, s, md, cells, n, nu, src, dst);
+    hipLaunchKernelGGL(k_mf_stokes<false>, grid, dim3(32 * kMfCells), 0, s, md, base, n, nu, src,
+                       dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

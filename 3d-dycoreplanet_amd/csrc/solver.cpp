@@ -389,7 +389,7 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
   if (c.time_schur) c.mf_calls[v]++;
   if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
   for (int k = 0; k < c.n_colors(); ++k)
-    mf_apply_colour(md, c.color_begin(k), c.color_size(k), c.ph.nu_sys, stokes, src, dst,
+    mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.ph.nu_sys, stokes, src, dst,
                     c.stream);
   mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.A_val.p, src, dst, c.stream);
   if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
