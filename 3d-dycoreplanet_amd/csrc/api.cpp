@@ -28,6 +28,8 @@ namespace dcp {
 Ctx::~Ctx() {
   free_workspaces(*this);
   if (hpinned) (void)hipHostFree(hpinned);
+  for (auto& ev : spec_ev)
+    if (ev) (void)hipEventDestroy(ev);
   ev_total.destroy();
   for (auto& t : schur_ev) t.destroy();
   for (auto& v : mf_ev)

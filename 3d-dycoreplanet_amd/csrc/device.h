@@ -164,11 +164,14 @@ void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* v
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
 // vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
 // part1 (one per slice, fixed order; zeros up to n_part, the length common to
-// all ranks whose partials are all-reduced).
+// all ranks whose partials are all-reduced). nrm_part != null: cf is ignored
+// and computed on the device as 1/|w| from the nb_nrm partials of |w|^2
+// (block_sum order; |w| -> *nrm_store), so the launch needs no host scalar.
 int sell_fused_blocks(int rows);
 void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
                      const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, int n_part, hipStream_t s);
+                     double* part0, double* part1, int n_part, const double* nrm_part,
+                     int nb_nrm, double* nrm_store, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):

@@ -194,8 +194,12 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
                                                       double* __restrict__ y,
                                                       const double* __restrict__ v0,
                                                       double* __restrict__ part0,
-                                                      double* __restrict__ part1) {
+                                                      double* __restrict__ part1,
+                                                      const double* __restrict__ nrm_part,
+                                                      int nb_nrm, double* nrm_store) {
   __shared__ double quarter[3][64];
+  __shared__ double sm[4];
+  __shared__ double cf_sh;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long sl = blockIdx.x;
   const long row = sl * 64 + lane;
@@ -204,6 +208,20 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
     // all-reduced partial arrays must hold zeros past this rank's slices
     if (EPI && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
     return;
+  }
+  if (EPI && nrm_part) {
+    // cf = 1/|w| from the nb_nrm partials of |w|^2 (block_sum order: the host
+    // mirrors it bit for bit, solver.cpp block_sum_host)
+    double s = 0;
+    for (int i = threadIdx.x; i < nb_nrm; i += kBlock) s += nrm_part[i];
+    const double tot = block_sum(s, sm);
+    if (threadIdx.x == 0) {
+      const double nv = sqrt(tot);
+      cf_sh = nv != 0 ? 1.0 / nv : 1.0;
+      if (blockIdx.x == 0) *nrm_store = nv;
+    }
+    __syncthreads();
+    cf = cf_sh;
   }
   const int64_t b = off[sl];
   const int np = int((off[sl + 1] - b) >> 7);  // column pairs of the slice
@@ -559,17 +577,19 @@ void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* v
                const double* x, double cf, double* y, hipStream_t s) {
   if (rows <= 0) return;
   hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_fused_blocks(rows)), dim3(kBlock), 0, s, rows,
-                     off, col, val, x, cf, nullptr, y, nullptr, nullptr, nullptr);
+                     off, col, val, x, cf, nullptr, y, nullptr, nullptr, nullptr, nullptr, 0,
+                     nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
 void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
                      const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, int n_part, hipStream_t s) {
+                     double* part0, double* part1, int n_part, const double* nrm_part,
+                     int nb_nrm, double* nrm_store, hipStream_t s) {
   const int nb = std::max(sell_fused_blocks(rows), n_part);
   if (nb <= 0) return;
   hipLaunchKernelGGL((k_sell_spmv<true>), dim3(nb), dim3(kBlock), 0, s, rows,
-                     off, col, val, x, cf, xs, y, v0, part0, part1);
+                     off, col, val, x, cf, xs, y, v0, part0, part1, nrm_part, nb_nrm, nrm_store);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -46,16 +46,21 @@ struct Control {
 // Device scalar slots (c.dscal).
 constexpr int kSlotH = 0;        // 0..127: Gram-Schmidt coefficients
 constexpr int kSlotH2 = 128;     // 128..255: re-orthogonalisation pass
-constexpr int kSlotNStart = 257; // |vv|^2 before
 constexpr int kSlotA = 258;      // misc
 constexpr int kSlotB = 259;
 constexpr int kSlotC = 260;
 constexpr int kSlotD = 261;
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
-constexpr int kNumSlots = 4096;             // device slots; host mirror: partials at kHostPartials
 constexpr int kHostPartials = 2048;
+// gmres_schur's pipelined Arnoldi steps: one block per step parity,
+// [0, 128) coefficients, kSpNStart, kSpNorm, partials from kSpPart
+constexpr int kSpecBase = 4096, kSpecStride = 1280;
+constexpr int kSpNStart = 128, kSpNorm = 129, kSpPart = 192;
+constexpr int kNumSlots = 8192;             // device slots, mirrored in c.hpinned
 static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kHostPartials, "slot layout");
-static_assert(kHostPartials + kChainMaxBlocks <= kNumSlots, "slot layout");
+static_assert(kHostPartials + kChainMaxBlocks <= kSpecBase - 512, "slot layout");
+static_assert(kSpPart + kChainMaxBlocks <= kSpecStride, "slot layout");
+static_assert(kSpecBase + 2 * kSpecStride <= kNumSlots, "slot layout");
 
 using Op = std::function<void(const double*, double*)>;
 
@@ -121,6 +126,28 @@ void givens_rotation(std::vector<double>& h, std::vector<double>& b, std::vector
 // Partial-sum buffers of the launch-lean chain (c.partials holds 4 of them).
 double* pbuf(Ctx& c, int i) { return c.partials.p + size_t(i) * kChainMaxBlocks; }
 
+// The device's block_sum (kernels/linalg.hip: per-thread strided sums over
+// 256 threads, xor-butterfly per 64-lane wave, the four wave sums in order)
+// restated on the host, bit for bit: host and device derive the same |w|.
+double block_sum_host(const double* p, int nb) {
+  double sm[4];
+  for (int w = 0; w < 4; ++w) {
+    double v[64];
+    for (int l = 0; l < 64; ++l) {
+      double t = 0;
+      for (int i = 64 * w + l; i < nb; i += 256) t += p[i];
+      v[l] = t;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      double nv[64];
+      for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+      for (int l = 0; l < 64; ++l) v[l] = nv[l];
+    }
+    sm[w] = v[0];
+  }
+  return sm[0] + sm[1] + sm[2] + sm[3];
+}
+
 // Host side of a chain: fetch `ncoef` coefficient slots starting at `s0` and
 // the nb final partials of buffer `b`; returns their fixed-order sum.
 // The last step of a chain writes its partials to slot kHostPartials, so one
@@ -131,10 +158,7 @@ double fetch_chain(Ctx& c, int s0, int ncoef, int nb, std::vector<double>& coef)
                                c.stream));
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
   coef.assign(c.hpinned + s0, c.hpinned + s0 + ncoef);
-  double s = 0;
-  const double* p = c.hpinned + kHostPartials;
-  for (int i = 0; i < nb; ++i) s += p[i];
-  return s;
+  return block_sum_host(c.hpinned + kHostPartials, nb);
 }
 
 // Gram-Schmidt chain of deal.II's add_and_dot sequence:
@@ -248,6 +272,14 @@ Timer* schur_sample(Ctx& c);
 //     (bitwise the product with the scaled vector), and the same launch
 //     stores v_k = w/|w| and the partials of (S v_k).v_0 and |S v_k|^2;
 //   * the modified Gram-Schmidt chain starts from those partials.
+// Pipelining: step k+1 is enqueued before the host has read step k back (the
+// SpMV derives 1/|w_k| from the chain's partials itself), so the GPU never
+// waits for the host's Givens/convergence work. Step k+1 is launched ahead
+// only when step k cannot change what it computes: not a loss-of-
+// orthogonality test step (every 5th), no re-orthogonalisation, not the last
+// step of a cycle, and residual not predicted to converge at k. A launched-
+// ahead step that turns out unneeded (converged at k) writes only scratch: the
+// next basis vector, the other w buffer and the other parity's slots.
 State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
                   int n_tmp) {
   const int n = c.n_p;
@@ -266,14 +298,40 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
   int dim = 0;
   State st = kIterate;
   bool reorth = false;
-  auto S = [&](double* src, double cf, double* xs, double* y, const double* v0) {
+  auto base = [](int it) { return kSpecBase + (it & 1) * kSpecStride; };
+  // Arnoldi step `it`: v_it = src * cf (stored by the SpMV for it > 0), S v_it,
+  // the chain, the readback of the step's block. ahead: cf from the device.
+  auto launch = [&](int it, double cf, bool ahead) {
+    const int B0 = base(it);
+    double* w = wbuf[it & 1];
+    double* src = it == 0 ? tv[0] : wbuf[(it - 1) & 1];
     halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    sell_spmv_fused(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf, xs, y, v0, part0,
-                    part1, nbs, c.stream);
+    sell_spmv_fused(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf,
+                    it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
+                    ahead ? slot(c, base(it - 1) + kSpPart) : nullptr, nb,
+                    slot(c, B0 + kSpNorm), c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     allreduce(c, part0, 2 * size_t(nbs));
+    const int d = it + 1;
+    const bool consider = !reorth && (it % 5 == 4);
+    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i
+    const double* prev = part0;
+    int nprev = nbs;
+    for (int i = 1; i <= d; ++i) {
+      const bool last = i == d;
+      double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
+      chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
+                           slot(c, B0 + i - 1), nb, i == 1 && consider ? part1 : nullptr,
+                           slot(c, B0 + kSpNStart), c.stream);
+      allreduce(c, out, nb);
+      prev = out;
+      nprev = nb;
+    }
+    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B0, slot(c, B0), (kSpPart + nb) * sizeof(double),
+                                 hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
   };
   do {
     std::fill(h.begin(), h.end(), 0.0);
@@ -285,30 +343,27 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
     if (st != kIterate) break;
     gamma[0] = rho;
     scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
-    double* src = tv[0];
-    double cf = 1.0;
+    double rho_prev = rho;
+    double prev_norm = 0;   // |w| of the previous step (host value)
+    bool prev_ahead = false;
+    launch(0, 1.0, false);
     for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
       ++accumulated;
-      double* w = wbuf[inner & 1];
-      // v_inner = src * cf is stored by the SpMV itself (inner > 0)
-      S(src, cf, inner > 0 ? tv[inner] : nullptr, w, tv[0]);
       dim = inner + 1;
-      const bool consider = !reorth && ((dim - 1) % 5 == 4);
-      // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i
-      const double* prev = part0;
-      int nprev = nbs;
-      for (int i = 1; i <= dim; ++i) {
-        const bool last = i == dim;
-        double* out = last ? slot(c, kHostPartials) : pbuf(c, i & 1);
-        chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
-                             slot(c, kSlotH + i - 1), nb, i == 1 && consider ? part1 : nullptr,
-                             slot(c, kSlotNStart), c.stream);
-        allreduce(c, out, nb);
-        prev = out;
-        nprev = nb;
-      }
-      double norm_vv = std::sqrt(fetch_chain(c, kSlotH, dim, nb, hv));
-      const double start2 = consider ? c.hpinned[kSlotNStart] : 0.0;
+      const int B0 = base(inner);
+      const bool consider = !reorth && (inner % 5 == 4);
+      // launch step inner+1 now unless step inner may change it
+      const double rho_pred = rho * (rho / rho_prev);
+      const bool ahead = !reorth && !consider && inner + 1 < n_tmp - 2 &&
+                         accumulated < ctl.max_steps && rho_pred > 2.0 * ctl.tol;
+      if (ahead) launch(inner + 1, 0.0, true);
+      DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[inner & 1]));
+      const double* hp = c.hpinned + B0;
+      if (prev_ahead && hp[kSpNorm] != prev_norm)
+        throw std::runtime_error("gmres_schur: device and host |w| differ");
+      hv.assign(hp, hp + dim);
+      double norm_vv = std::sqrt(block_sum_host(hp + kSpPart, nb));
+      const double start2 = consider ? hp[kSpNStart] : 0.0;
       for (int i = 0; i < dim; ++i) h[i] = hv[i];
       bool second = reorth;
       if (consider && !(norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16))) {
@@ -316,17 +371,19 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
         second = true;
       }
       if (second) {
-        norm_vv = std::sqrt(gs_chain(c, g, tv, dim, w, kSlotH2, hv));
+        norm_vv = std::sqrt(gs_chain(c, g, tv, dim, wbuf[inner & 1], kSlotH2, hv));
         for (int i = 0; i < dim; ++i) h[i] += hv[i];
       }
-      const double sv = norm_vv;
-      h[inner + 1] = sv;
-      src = w;
-      cf = sv != 0 ? 1. / sv : 1.0;
+      h[inner + 1] = norm_vv;
       givens_rotation(h, gamma, ci, si, inner);
       for (int i = 0; i < dim; ++i) H[i][inner] = h[i];
+      rho_prev = rho;
       rho = std::fabs(gamma[dim]);
       st = ctl.check(accumulated, rho);
+      prev_norm = norm_vv;
+      prev_ahead = ahead;
+      if (st == kIterate && !ahead && inner + 1 < n_tmp - 2)
+        launch(inner + 1, norm_vv != 0 ? 1. / norm_vv : 1.0, false);
     }
     std::vector<double> y(dim, 0.0);
     for (int i = dim - 1; i >= 0; --i) {
@@ -576,6 +633,7 @@ void ensure_workspaces(Ctx& c) {
     c.dscal.alloc(kNumSlots);
     c.partials.alloc(4 * size_t(kChainMaxBlocks));
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hpinned), kNumSlots * sizeof(double)));
+    for (auto& ev : c.spec_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c.coef.alloc(128);
     c.ptrs.alloc(128);
   }
