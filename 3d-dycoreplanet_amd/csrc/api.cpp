@@ -28,6 +28,7 @@ namespace dcp {
 Ctx::~Ctx() {
   free_workspaces(*this);
   if (hpinned) (void)hipHostFree(hpinned);
+  if (hmapped) (void)hipHostFree(hmapped);
   for (auto& ev : spec_ev)
     if (ev) (void)hipEventDestroy(ev);
   ev_total.destroy();

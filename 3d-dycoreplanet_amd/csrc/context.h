@@ -119,6 +119,7 @@ struct Ctx {
   DBuf<double> partials, dscal;
   double* hpinned = nullptr;   // pinned host mirror of small readbacks
   hipEvent_t spec_ev[2] = {nullptr, nullptr};  // readbacks of pipelined Arnoldi steps
+  double* hmapped = nullptr;   // coherent mapped host memory written by kernels (one GPU)
   bool nse_assembled = false, precond_built = false, T_matrix_ok = false, T_rhs_ok = false;
   // Krylov workspaces (lazily sized)
   std::vector<double*> fg_v, fg_z;   // FGMRES basis

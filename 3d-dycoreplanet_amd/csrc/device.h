@@ -211,13 +211,14 @@ void dot_partial(Seg g, const double* a, const double* b, double* partials, int 
 void chain_add_and_dot(Seg g, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s);
-// Same step with nb_prev previous partials (e.g. from sell_spmv_fused) and an
+// Same step with nb_prev previous partials (e.g. from sell_spmv_fused), an
 // optional second partial array prev2 whose fixed-order sum block 0 stores to
-// *store2.
+// *store2, and optionally a second copy of the partials (partials_host: mapped
+// host memory, so the host reads them without a copy launch).
 void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, double mult,
                           const double* x, const double* w, double* partials,
                           double* coef_store, int nb, const double* prev2, double* store2,
-                          hipStream_t s);
+                          double* partials_host, hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

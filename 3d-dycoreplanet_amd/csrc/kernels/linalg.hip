@@ -125,7 +125,8 @@ constexpr int kChainPrefetch = 4;
 __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
     Seg g, double* v, const double* __restrict__ prev, int nb_prev, double mult,
     const double* __restrict__ x, const double* w, double* __restrict__ partials,
-    double* coef_store, const double* __restrict__ prev2, double* store2) {
+    double* coef_store, const double* __restrict__ prev2, double* store2,
+    double* partials_host) {
   __shared__ double sm[4];
   __shared__ double coef_sh;
   const bool self = (w == v);
@@ -177,7 +178,10 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
     d += nv * (self ? nv : w[i]);
   }
   const double r = block_sum(d, sm);
-  if (threadIdx.x == 0) partials[blockIdx.x] = r;
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x] = r;
+    if (partials_host) partials_host[blockIdx.x] = r;
+  }
 }
 
 // SELL-64 SpMV (see device.h). One 256-thread workgroup per slice: lane i of
@@ -559,15 +563,16 @@ void dot_partial(Seg g, const double* a, const double* b, double* partials, int 
 void chain_add_and_dot(Seg g, double* v, const double* prev, double mult, const double* x,
                        const double* w, double* partials, double* coef_store, int nb,
                        hipStream_t s) {
-  chain_add_and_dot_ex(g, v, prev, nb, mult, x, w, partials, coef_store, nb, nullptr, nullptr, s);
+  chain_add_and_dot_ex(g, v, prev, nb, mult, x, w, partials, coef_store, nb, nullptr, nullptr,
+                       nullptr, s);
 }
 
 void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, double mult,
                           const double* x, const double* w, double* partials,
                           double* coef_store, int nb, const double* prev2, double* store2,
-                          hipStream_t s) {
+                          double* partials_host, hipStream_t s) {
   hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, g, v, prev, nb_prev, mult,
-                     x, w, partials, coef_store, prev2, store2);
+                     x, w, partials, coef_store, prev2, store2, partials_host);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

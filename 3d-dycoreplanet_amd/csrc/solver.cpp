@@ -299,6 +299,7 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
   State st = kIterate;
   bool reorth = false;
   auto base = [](int it) { return kSpecBase + (it & 1) * kSpecStride; };
+  double* const hmir0 = c.comm ? nullptr : c.hmapped;
   // Arnoldi step `it`: v_it = src * cf (stored by the SpMV for it > 0), S v_it,
   // the chain, the readback of the step's block. ahead: cf from the device.
   auto launch = [&](int it, double cf, bool ahead) {
@@ -311,26 +312,33 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
     sell_spmv_fused(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf,
                     it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
                     ahead ? slot(c, base(it - 1) + kSpPart) : nullptr, nb,
-                    slot(c, B0 + kSpNorm), c.stream);
+                    hmir0 ? hmir0 + B0 + kSpNorm : slot(c, B0 + kSpNorm), c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     allreduce(c, part0, 2 * size_t(nbs));
     const int d = it + 1;
     const bool consider = !reorth && (it % 5 == 4);
-    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i
+    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i.
+    // One GPU: coefficients and final partials go straight to the mapped host
+    // mirror (no copy launch); several: the final partials are all-reduced on
+    // the device first, then copied.
+    double* hmir = hmir0;
     const double* prev = part0;
     int nprev = nbs;
     for (int i = 1; i <= d; ++i) {
       const bool last = i == d;
       double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
       chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
-                           slot(c, B0 + i - 1), nb, i == 1 && consider ? part1 : nullptr,
-                           slot(c, B0 + kSpNStart), c.stream);
+                           hmir ? hmir + B0 + i - 1 : slot(c, B0 + i - 1), nb,
+                           i == 1 && consider ? part1 : nullptr,
+                           hmir ? hmir + B0 + kSpNStart : slot(c, B0 + kSpNStart),
+                           hmir && last ? hmir + B0 + kSpPart : nullptr, c.stream);
       allreduce(c, out, nb);
       prev = out;
       nprev = nb;
     }
-    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B0, slot(c, B0), (kSpPart + nb) * sizeof(double),
-                                 hipMemcpyDeviceToHost, c.stream));
+    if (!hmir)
+      DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B0, slot(c, B0), (kSpPart + nb) * sizeof(double),
+                                   hipMemcpyDeviceToHost, c.stream));
     DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
   };
   do {
@@ -358,7 +366,7 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
                          accumulated < ctl.max_steps && rho_pred > 2.0 * ctl.tol;
       if (ahead) launch(inner + 1, 0.0, true);
       DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[inner & 1]));
-      const double* hp = c.hpinned + B0;
+      const double* hp = (hmir0 ? hmir0 : c.hpinned) + B0;
       if (prev_ahead && hp[kSpNorm] != prev_norm)
         throw std::runtime_error("gmres_schur: device and host |w| differ");
       hv.assign(hp, hp + dim);
@@ -634,6 +642,9 @@ void ensure_workspaces(Ctx& c) {
     c.partials.alloc(4 * size_t(kChainMaxBlocks));
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hpinned), kNumSlots * sizeof(double)));
     for (auto& ev : c.spec_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // coherent mapped host memory the kernels write directly (uncached on the GPU)
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hmapped), kNumSlots * sizeof(double),
+                                hipHostMallocMapped | hipHostMallocCoherent));
     c.coef.alloc(128);
     c.ptrs.alloc(128);
   }

@@ -11,8 +11,9 @@ SRC=${SRC:-assembly}
 OTHERS=$(ls build/*.o | grep -v "/$SRC.o")
 for spec in ${VARIANTS:-base:}; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics ${flags//,/ } \
-    -c csrc/kernels/$SRC.hip -o build/var/${SRC}_$name.o
+  if [ -f csrc/$SRC.cpp ]; then srcf=csrc/$SRC.cpp; extra=-fopenmp; else srcf=csrc/kernels/$SRC.hip; extra=-munsafe-fp-atomics; fi
+  /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 $extra ${flags//,/ } \
+    -c $srcf -o build/var/${SRC}_$name.o
   /opt/rocm/bin/hipcc -shared -fopenmp --offload-arch=gfx950 -o build/var/libdcp_$name.so $OTHERS \
     build/var/${SRC}_$name.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 done
