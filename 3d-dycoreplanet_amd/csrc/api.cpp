@@ -443,6 +443,141 @@ bool owned_entry(const Ctx& c, int field, size_t i) {
 
 }  // namespace
 
+namespace {
+
+// Reverse Cuthill-McKee order of a symmetric pattern (rows [0, n), columns
+// < n kept): BFS from a minimum-degree vertex of every component, neighbours
+// by ascending degree, reversed. Returns perm[new] = old.
+std::vector<int32_t> rcm_order(int n, const std::vector<int32_t>& ptr,
+                               const std::vector<int32_t>& col) {
+  std::vector<int32_t> deg(n), order;
+  order.reserve(n);
+  for (int i = 0; i < n; ++i) {
+    int d = 0;
+    for (int k = ptr[i]; k < ptr[i + 1]; ++k) d += col[k] < n;
+    deg[i] = d;
+  }
+  std::vector<int32_t> byd(n);
+  for (int i = 0; i < n; ++i) byd[i] = i;
+  std::stable_sort(byd.begin(), byd.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+  std::vector<uint8_t> seen(n, 0);
+  std::vector<int32_t> nb;
+  for (int start : byd) {
+    if (seen[start]) continue;
+    seen[start] = 1;
+    size_t head = order.size();
+    order.push_back(start);
+    while (head < order.size()) {
+      const int v = order[head++];
+      nb.clear();
+      for (int k = ptr[v]; k < ptr[v + 1]; ++k) {
+        const int u = col[k];
+        if (u < n && !seen[u]) {
+          seen[u] = 1;
+          nb.push_back(u);
+        }
+      }
+      std::stable_sort(nb.begin(), nb.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+      order.insert(order.end(), nb.begin(), nb.end());
+    }
+  }
+  std::reverse(order.begin(), order.end());
+  return order;
+}
+
+// SELL-64 storage of the owned rows of the S pattern (sell_spmv): slice width
+// = longest row of the slice, rounded to column pairs. One GPU: rows and
+// columns in reverse Cuthill-McKee order, so every slice's columns span less
+// than 2^16 and are stored as 16-bit offsets from a per-slice base (10 instead
+// of 12 bytes per entry); the inner Schur GMRES then runs in that order.
+// pmap: CSR entry -> SELL position (k_schur_form writes through it).
+void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_t>& Sc,
+                bool permute) {
+  const int rows = c.npo;
+  const int n_sl = (rows + 63) / 64;
+  std::vector<int32_t> perm, iperm;
+  if (permute && rows > 0) {
+    perm = rcm_order(rows, Sp, Sc);
+    iperm.assign(rows, 0);
+    for (int r = 0; r < rows; ++r) iperm[perm[r]] = r;
+  }
+  auto orow = [&](int r) { return perm.empty() ? r : perm[r]; };
+  auto ncol = [&](int q) { return iperm.empty() || q >= rows ? q : iperm[q]; };
+  std::vector<int64_t> off(size_t(n_sl) + 1, 0);
+  std::vector<int32_t> base(n_sl, 0);
+  bool c16 = !perm.empty();
+  for (int sl = 0; sl < n_sl; ++sl) {
+    int w = 0, lo = INT32_MAX, hi = 0;
+    for (int r = 64 * sl; r < std::min(rows, 64 * sl + 64); ++r) {
+      const int p = orow(r);
+      w = std::max(w, Sp[p + 1] - Sp[p]);
+      for (int k = Sp[p]; k < Sp[p + 1]; ++k) {
+        lo = std::min(lo, ncol(Sc[k]));
+        hi = std::max(hi, ncol(Sc[k]));
+      }
+      lo = std::min(lo, r);  // padding points at the own row
+      hi = std::max(hi, r);
+    }
+    base[sl] = lo == INT32_MAX ? 0 : lo;
+    if (hi - base[sl] >= 65536) c16 = false;
+    w += w & 1;  // column pairs
+    off[sl + 1] = off[sl] + 64 * int64_t(w);
+  }
+  const size_t len = size_t(off[n_sl]);
+  std::vector<int32_t> scol(len, 0), pmap(Sp[rows], 0);
+  std::vector<std::pair<int32_t, int32_t>> ent;
+  for (int sl = 0; sl < n_sl; ++sl) {
+    const int w = int((off[sl + 1] - off[sl]) / 64);
+    for (int i = 0; i < 64; ++i) {
+      const int r = 64 * sl + i;
+      ent.clear();
+      if (r < rows) {
+        const int p = orow(r);
+        for (int k = Sp[p]; k < Sp[p + 1]; ++k) ent.emplace_back(ncol(Sc[k]), k);
+        std::sort(ent.begin(), ent.end());
+      }
+      for (int k = 0; k < w; ++k) {
+        const int64_t pos = sell_pos(off.data(), r, k);
+        if (k < int(ent.size())) {
+          scol[pos] = ent[k].first;
+          pmap[ent[k].second] = int32_t(pos);
+        } else {
+          scol[pos] = r < rows ? r : base[sl];
+        }
+      }
+    }
+  }
+  require(len < size_t(INT32_MAX), DCP_ERR_UNSUPPORTED, "SELL storage of S above 2^31 entries");
+  c.S_sell_off.upload(off);
+  if (c16) {
+    std::vector<uint16_t> s16(len);
+    for (int sl = 0; sl < n_sl; ++sl)
+      for (int64_t e = off[sl]; e < off[sl + 1]; ++e) s16[e] = uint16_t(scol[e] - base[sl]);
+    c.S_sell_c16.upload(s16);
+    c.S_sell_base.upload(base);
+    c.S_sell_col.release();
+  } else {
+    c.S_sell_col.upload(scol);
+    c.S_sell_c16.release();
+    c.S_sell_base.release();
+  }
+  c.S_pmap.upload(pmap);
+  if (!perm.empty() && c16) {
+    c.S_perm.upload(perm);
+  } else {
+    // permutation only pays with the 16-bit columns: keep the identity order
+    c.S_perm.release();
+    if (!perm.empty()) return build_sell(c, Sp, Sc, false);
+  }
+  c.S_val.alloc(len);
+  c.S_val.zero(c.stream);  // padding entries stay 0
+  c.sell_part_len = sell_fused_blocks(rows);
+  c.sperm_x.alloc(std::max(rows, 1));
+  c.sperm_b.alloc(std::max(rows, 1));
+}
+
+}  // namespace
+
 extern "C" {
 
 int dcp_nccl_unique_id(void* out128) {
@@ -683,36 +818,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.T_col.upload(Tc);
     c.S_ptr.upload(h.Sp);
     c.S_col.upload(h.Sc);
-    {
-      // SELL-64 layout of the owned rows of the S pattern: slice width =
-      // longest row of the slice
-      const int rows = c.npo;
-      const int n_sl = (rows + 63) / 64;
-      std::vector<int64_t> off(size_t(n_sl) + 1, 0);
-      for (int sl = 0; sl < n_sl; ++sl) {
-        int w = 0;
-        for (int p = 64 * sl; p < std::min(rows, 64 * sl + 64); ++p)
-          w = std::max(w, h.Sp[p + 1] - h.Sp[p]);
-        w += w & 1;  // column pairs
-        off[sl + 1] = off[sl] + 64 * int64_t(w);
-      }
-      std::vector<int32_t> scol(size_t(off[n_sl]), 0);
-      for (int sl = 0; sl < n_sl; ++sl) {
-        const int w = int((off[sl + 1] - off[sl]) / 64);
-        for (int i = 0; i < 64; ++i) {
-          const int p = 64 * sl + i;
-          for (int k = 0; k < w; ++k) {
-            const bool real = p < rows && k < h.Sp[p + 1] - h.Sp[p];
-            scol[sell_pos(off.data(), p, k)] = real ? h.Sc[h.Sp[p] + k] : (p < rows ? p : 0);
-          }
-        }
-      }
-      c.S_sell_off.upload(off);
-      c.S_sell_col.upload(scol);
-      c.S_val.alloc(scol.size());
-      c.S_val.zero(c.stream);  // padding entries stay 0
-      c.sell_part_len = sell_fused_blocks(rows);
-    }
+    build_sell(c, h.Sp, h.Sc, !dist);
     c.S_max_row = h.S_max_row;
     c.A_val.alloc(Ac.size() * 9);
     c.Bt_val.alloc(Btc.size() * 3);
@@ -941,7 +1047,7 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
               "the explicit Schur complement needs the assembled B blocks: call "
               "dcp_assemble_nse_system first");
       form_schur_complement(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
-                            c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_sell_off.p,
+                            c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_pmap.p,
                             c.S_val.p, c.S_max_row, c.stream);
     }
     t.stop();
@@ -1223,6 +1329,17 @@ int dcp_pattern_info(dcp_ctx* ctx, int64_t* nA, int64_t* nBt, int64_t* nB, int64
     if (nB) *nB = int64_t(ctx->B_col.n);
     if (nT) *nT = int64_t(ctx->T_col.n);
     if (nS) *nS = int64_t(ctx->S_col.n);
+    return DCP_OK;
+  });
+}
+
+int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    const Ctx& c = *ctx;
+    if (col_bytes) *col_bytes = c.S_sell_c16.p ? 2 : 4;
+    if (stored) *stored = int64_t(c.S_val.n);
+    if (permuted) *permuted = c.S_perm.p != nullptr;
     return DCP_OK;
   });
 }

@@ -95,7 +95,15 @@ struct Ctx {
   DBuf<int32_t> S_ptr, S_col;
   // its values live in the SELL-64 layout of that pattern (sell_spmv)
   DBuf<int64_t> S_sell_off;
-  DBuf<int32_t> S_sell_col;
+  DBuf<int32_t> S_sell_col;          // 32-bit columns, or
+  DBuf<uint16_t> S_sell_c16;         // 16-bit offsets from S_sell_base[slice]
+  DBuf<int32_t> S_sell_base;
+  DBuf<int32_t> S_pmap;              // CSR entry of S -> SELL position
+  DBuf<int32_t> S_perm;              // SELL row r = pressure dof S_perm[r] (null: identity)
+  DBuf<double> sperm_x, sperm_b;     // permuted-order work vectors
+  SellView sell() const {
+    return SellView{npo, S_sell_off.p, S_sell_col.p, S_sell_c16.p, S_sell_base.p, S_val.p};
+  }
   DBuf<double> S_val;
   DBuf<double> sell_part;            // 2 x sell_fused_blocks(n_p) partials
   int S_max_row = 0;

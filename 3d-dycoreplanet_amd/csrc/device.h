@@ -128,12 +128,12 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
                       int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s);
 
 // S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
-// contributions summed in fixed node order: deterministic). sell_off != null:
-// the values are stored in the SELL-64 layout of that pattern (see sell_spmv).
+// contributions summed in fixed node order: deterministic). pmap != null:
+// entry j of the CSR pattern is stored at S_val[pmap[j]] (the SELL layout).
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
                            const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
-                           const int64_t* sell_off, double* S_val, int max_row, hipStream_t s);
+                           const int32_t* pmap, double* S_val, int max_row, hipStream_t s);
 
 // ---- linalg.hip -------------------------------------------------------------
 // y (=|+=) alpha * M x for block-CSR with R x C blocks (R,C in {1,3}).
@@ -152,15 +152,22 @@ void spmv_csr_long(int rows, const int32_t* ptr, const int32_t* col, const doubl
 // SELL-64 SpMV: slices of 64 consecutive rows (one wave, one row per lane);
 // slice width even; inside a slice entries are stored in column pairs (row
 // 64s+i, entry k at off[s] + 128 (k/2) + 2i + k%2; padding: col = own row,
-// val = 0), so a lane reads two entries with one 16-B (values) / 8-B
-// (columns) load and every load of a wave is one contiguous 1-KB / 512-B
-// segment.
+// val = 0), so a lane reads two entries with one 16-B (values) / 8-B or 4-B
+// (columns) load and every load of a wave is one contiguous segment. Columns
+// are 32-bit (col) or 16-bit offsets from a per-slice base (col16 + base).
 //   y = M (cf * x)
 __host__ __device__ inline int64_t sell_pos(const int64_t* off, int p, int k) {
   return off[p >> 6] + 128 * int64_t(k >> 1) + 2 * (p & 63) + (k & 1);
 }
-void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* val,
-               const double* x, double cf, double* y, hipStream_t s);
+struct SellView {
+  int rows;
+  const int64_t* off;
+  const int32_t* col;      // or null
+  const uint16_t* col16;   // with base, or null
+  const int32_t* base;
+  const double* val;
+};
+void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s);
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
 // vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
 // part1 (one per slice, fixed order; zeros up to n_part, the length common to
@@ -168,10 +175,9 @@ void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* v
 // and computed on the device as 1/|w| from the nb_nrm partials of |w|^2
 // (block_sum order; |w| -> *nrm_store), so the launch needs no host scalar.
 int sell_fused_blocks(int rows);
-void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
-                     const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, int n_part, const double* nrm_part,
-                     int nb_nrm, double* nrm_store, hipStream_t s);
+void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, double* y,
+                     const double* v0, double* part0, double* part1, int n_part,
+                     const double* nrm_part, int nb_nrm, double* nrm_store, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):

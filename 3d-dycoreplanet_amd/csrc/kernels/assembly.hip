@@ -915,7 +915,7 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
                                                    const double* __restrict__ d,
                                                    const int32_t* __restrict__ S_ptr,
                                                    const int32_t* __restrict__ S_col,
-                                                   const int64_t* __restrict__ sell_off,
+                                                   const int32_t* __restrict__ pmap,
                                                    double* __restrict__ S_val) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int p = blockIdx.x;
@@ -946,8 +946,8 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
     }
     __syncthreads();
   }
-  if (sell_off) {
-    for (int j = threadIdx.x; j < len; j += 64) S_val[sell_pos(sell_off, p, j)] = acc[j];
+  if (pmap) {
+    for (int j = threadIdx.x; j < len; j += 64) S_val[pmap[s0 + j]] = acc[j];
   } else {
     for (int j = threadIdx.x; j < len; j += 64) S_val[s0 + j] = acc[j];
   }
@@ -958,11 +958,11 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
                            const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
-                           const int64_t* sell_off, double* S_val, int max_row, hipStream_t s) {
+                           const int32_t* pmap, double* S_val, int max_row, hipStream_t s) {
   if (n_p <= 0) return;
   const size_t lds = size_t(max_row) * (sizeof(double) + sizeof(int)) + 16;
   hipLaunchKernelGGL(k_schur_form, dim3(n_p), dim3(64), lds, s, n_p, B_ptr, B_col, B_val, Bt_ptr,
-                     Bt_col, Bt_val, d, S_ptr, S_col, sell_off, S_val);
+                     Bt_col, Bt_val, d, S_ptr, S_col, pmap, S_val);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

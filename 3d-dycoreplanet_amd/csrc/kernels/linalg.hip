@@ -189,12 +189,9 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
 // entry columns (4 waves per slice keep enough loads in flight: one wave per
 // slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound), then
 // wave 0 adds the 4 quarters in order (fixed summation order).
-template <bool EPI>
-__global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* __restrict__ off,
-                                                      const int32_t* __restrict__ col,
-                                                      const double* __restrict__ val,
-                                                      const double* __restrict__ x, double cf,
-                                                      double* __restrict__ xs,
+template <bool EPI, bool C16>
+__global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* __restrict__ x,
+                                                      double cf, double* __restrict__ xs,
                                                       double* __restrict__ y,
                                                       const double* __restrict__ v0,
                                                       double* __restrict__ part0,
@@ -204,6 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
   __shared__ double quarter[3][64];
   __shared__ double sm[4];
   __shared__ double cf_sh;
+  const int rows = m.rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long sl = blockIdx.x;
   const long row = sl * 64 + lane;
@@ -227,28 +225,49 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int rows, const int64_t* _
     __syncthreads();
     cf = cf_sh;
   }
-  const int64_t b = off[sl];
-  const int np = int((off[sl + 1] - b) >> 7);  // column pairs of the slice
+  const int64_t b = m.off[sl];
+  const int np = int((m.off[sl + 1] - b) >> 7);  // column pairs of the slice
   const int per = (np + 3) >> 2;
   const int k0 = wave * per, k1 = min(np, k0 + per);
-  const int2* cp = reinterpret_cast<const int2*>(col + b) + 64 * int64_t(k0) + lane;
-  const double2* vp = reinterpret_cast<const double2*>(val + b) + 64 * int64_t(k0) + lane;
+  const double2* vp = reinterpret_cast<const double2*>(m.val + b) + 64 * int64_t(k0) + lane;
   double acc = 0.0;
   int k = k0;
-  for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
-    const int2 c0 = cp[0], c1 = cp[64];
-    const double2 a0 = vp[0], a1 = vp[64];
-    const double x0 = x[c0.x] * cf, x1 = x[c0.y] * cf, x2 = x[c1.x] * cf, x3 = x[c1.y] * cf;
-    acc += a0.x * x0;
-    acc += a0.y * x1;
-    acc += a1.x * x2;
-    acc += a1.y * x3;
-  }
-  if (k < k1) {
-    const int2 c0 = cp[0];
-    const double2 a0 = vp[0];
-    acc += a0.x * (x[c0.x] * cf);
-    acc += a0.y * (x[c0.y] * cf);
+  if (C16) {
+    const int cb = m.base[sl];
+    const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * int64_t(k0) + lane;
+    for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
+      const ushort2 c0 = cp[0], c1 = cp[64];
+      const double2 a0 = vp[0], a1 = vp[64];
+      const double x0 = x[cb + c0.x] * cf, x1 = x[cb + c0.y] * cf;
+      const double x2 = x[cb + c1.x] * cf, x3 = x[cb + c1.y] * cf;
+      acc += a0.x * x0;
+      acc += a0.y * x1;
+      acc += a1.x * x2;
+      acc += a1.y * x3;
+    }
+    if (k < k1) {
+      const ushort2 c0 = cp[0];
+      const double2 a0 = vp[0];
+      acc += a0.x * (x[cb + c0.x] * cf);
+      acc += a0.y * (x[cb + c0.y] * cf);
+    }
+  } else {
+    const int2* cp = reinterpret_cast<const int2*>(m.col + b) + 64 * int64_t(k0) + lane;
+    for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
+      const int2 c0 = cp[0], c1 = cp[64];
+      const double2 a0 = vp[0], a1 = vp[64];
+      const double x0 = x[c0.x] * cf, x1 = x[c0.y] * cf, x2 = x[c1.x] * cf, x3 = x[c1.y] * cf;
+      acc += a0.x * x0;
+      acc += a0.y * x1;
+      acc += a1.x * x2;
+      acc += a1.y * x3;
+    }
+    if (k < k1) {
+      const int2 c0 = cp[0];
+      const double2 a0 = vp[0];
+      acc += a0.x * (x[c0.x] * cf);
+      acc += a0.y * (x[c0.y] * cf);
+    }
   }
   if (wave > 0) quarter[wave - 1][lane] = acc;
   __syncthreads();
@@ -578,23 +597,29 @@ void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, dou
 
 int sell_fused_blocks(int rows) { return int((long(rows) + 63) / 64); }
 
-void sell_spmv(int rows, const int64_t* off, const int32_t* col, const double* val,
-               const double* x, double cf, double* y, hipStream_t s) {
-  if (rows <= 0) return;
-  hipLaunchKernelGGL((k_sell_spmv<false>), dim3(sell_fused_blocks(rows)), dim3(kBlock), 0, s, rows,
-                     off, col, val, x, cf, nullptr, y, nullptr, nullptr, nullptr, nullptr, 0,
-                     nullptr);
+void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s) {
+  if (m.rows <= 0) return;
+  const dim3 grid(sell_fused_blocks(m.rows));
+  if (m.col16)
+    hipLaunchKernelGGL((k_sell_spmv<false, true>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr);
+  else
+    hipLaunchKernelGGL((k_sell_spmv<false, false>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void sell_spmv_fused(int rows, const int64_t* off, const int32_t* col, const double* val,
-                     const double* x, double cf, double* xs, double* y, const double* v0,
-                     double* part0, double* part1, int n_part, const double* nrm_part,
-                     int nb_nrm, double* nrm_store, hipStream_t s) {
-  const int nb = std::max(sell_fused_blocks(rows), n_part);
+void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, double* y,
+                     const double* v0, double* part0, double* part1, int n_part,
+                     const double* nrm_part, int nb_nrm, double* nrm_store, hipStream_t s) {
+  const int nb = std::max(sell_fused_blocks(m.rows), n_part);
   if (nb <= 0) return;
-  hipLaunchKernelGGL((k_sell_spmv<true>), dim3(nb), dim3(kBlock), 0, s, rows,
-                     off, col, val, x, cf, xs, y, v0, part0, part1, nrm_part, nb_nrm, nrm_store);
+  if (m.col16)
+    hipLaunchKernelGGL((k_sell_spmv<true, true>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store);
+  else
+    hipLaunchKernelGGL((k_sell_spmv<true, false>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

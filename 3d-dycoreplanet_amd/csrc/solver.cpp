@@ -280,8 +280,24 @@ Timer* schur_sample(Ctx& c);
 // step of a cycle, and residual not predicted to converge at k. A launched-
 // ahead step that turns out unneeded (converged at k) writes only scratch: the
 // next basis vector, the other w buffer and the other parity's slots.
+State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
+                          std::vector<double*>& tv, int n_tmp);
+
+// On one GPU S is stored in reverse Cuthill-McKee order (api.cpp build_sell):
+// the solve runs in that order, entered and left by one gather / scatter.
 State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
                   int n_tmp) {
+  if (!c.S_perm.p) return gmres_schur_ordered(c, x, b, ctl, tv, n_tmp);
+  const int n = c.n_p;
+  gather(n, c.S_perm.p, x, c.sperm_x.p, c.stream);
+  gather(n, c.S_perm.p, b, c.sperm_b.p, c.stream);
+  const State st = gmres_schur_ordered(c, c.sperm_x.p, c.sperm_b.p, ctl, tv, n_tmp);
+  scatter(n, c.S_perm.p, c.sperm_x.p, x, c.stream);
+  return st;
+}
+
+State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
+                          std::vector<double*>& tv, int n_tmp) {
   const int n = c.n_p;
   const Seg g = c.seg_p();
   ensure_pool(tv, n_tmp + 2, size_t(n));
@@ -309,8 +325,7 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
     halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    sell_spmv_fused(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, cf,
-                    it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
+    sell_spmv_fused(c.sell(), src, cf, it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
                     ahead ? slot(c, base(it - 1) + kSpPart) : nullptr, nb,
                     hmir0 ? hmir0 + B0 + kSpNorm : slot(c, B0 + kSpNorm), c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
@@ -343,7 +358,10 @@ State gmres_schur(Ctx& c, double* x, const double* b, Control& ctl, std::vector<
   };
   do {
     std::fill(h.begin(), h.end(), 0.0);
-    schur_vmult(c, x, p);
+    if (c.S_perm.p)
+      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
+    else
+      schur_vmult(c, x, p);
     sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
     copy(n, p, tv[0], c.stream);        // identity preconditioner
     double rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
@@ -615,7 +633,13 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
     halo_exchange(c, c.halo_p, const_cast<double*>(src));
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    sell_spmv(c.npo, c.S_sell_off.p, c.S_sell_col.p, c.S_val.p, src, 1.0, dst, c.stream);
+    if (c.S_perm.p) {
+      gather(c.n_p, c.S_perm.p, src, c.sperm_x.p, c.stream);
+      sell_spmv(c.sell(), c.sperm_x.p, 1.0, c.sperm_b.p, c.stream);
+      scatter(c.n_p, c.S_perm.p, c.sperm_b.p, dst, c.stream);
+    } else {
+      sell_spmv(c.sell(), src, 1.0, dst, c.stream);
+    }
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     return;
   }

@@ -44,7 +44,7 @@ EXPORTED = [
     "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
-    "dcp_host_feec_view_get",
+    "dcp_host_feec_view_get", "dcp_schur_layout",
 ]
 
 
@@ -163,6 +163,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_cell_nse_system.argtypes = [P, I, I, P, P]
     lib.dcp_get_timings.argtypes = [P, C.POINTER(Timings)]
     lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 5
+    lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_int)]
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_destroy.argtypes = [P]
@@ -590,6 +592,11 @@ class Context:
         v = [C.c_int64() for _ in range(5)]
         self._check(lib().dcp_pattern_info(self._h, *[C.byref(x) for x in v]))
         return dict(zip(("nnzb_A", "nnzb_Bt", "nnzb_B", "nnz_T", "nnz_S"), (x.value for x in v)))
+
+    def schur_layout(self) -> dict:
+        cb, st, pm = C.c_int(), C.c_int64(), C.c_int()
+        self._check(lib().dcp_schur_layout(self._h, C.byref(cb), C.byref(st), C.byref(pm)))
+        return {"col_bytes": cb.value, "stored": st.value, "permuted": bool(pm.value)}
 
     def timings(self) -> dict:
         t = Timings()

@@ -31,7 +31,7 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
-PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_sell_r5.json", "k_sell_spmv<true>")}
+PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_sell16_r5.json", "k_sell_spmv<true, true>")}
 
 
 def pmc_traffic(refine, mode):
@@ -268,11 +268,17 @@ def main():
     schur_ms = np.mean([r[4]["schur_apply_ms_avg"] for r in recs])
     pinfo = ctx.pattern_info()
     if args.schur == "explicit":
-        # fused SELL SpMV with the formed S: values + columns (12 B per nonzero),
-        # slice offsets, gathered x, y write, scaled-basis write xs, v0 read
+        # fused SELL SpMV with the formed S: values + column indices per
+        # nonzero (8 + 2 B with the 16-bit RCM layout, 8 + 4 B otherwise),
+        # slice offsets (+ column bases), gathered x, y write, scaled-basis
+        # write xs, v0 read
+        lay = ctx.schur_layout()
         n_sl = (m.n_p + 63) // 64
-        sbytes = 12 * pinfo["nnz_S"] + 8 * (n_sl + 1) + 32 * m.n_p
-        kernel = "explicit Schur complement SpMV S x, SELL-64 fused (k_sell_spmv<true>)"
+        cb = lay["col_bytes"]
+        sbytes = (8 + cb) * pinfo["nnz_S"] + 8 * (n_sl + 1) + (4 * n_sl if cb == 2 else 0) \
+            + 32 * m.n_p
+        kernel = ("explicit Schur complement SpMV S x, SELL-64 fused (k_sell_spmv<true>"
+                  + (", 16-bit columns, RCM order)" if cb == 2 else ")"))
     else:
         sbytes = schur_bytes(m, pinfo["nnzb_Bt"], pinfo["nnzb_B"])
         kernel = "Schur complement apply B D_A^-1 B^T (3 kernels)"

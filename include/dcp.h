@@ -204,6 +204,11 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* nnzb_B,
                      int64_t* nnz_T, int64_t* nnz_S);
 
+/* Storage of the explicit Schur complement (SELL-64): bytes per column index
+ * (2: 16-bit offsets from a slice base, 4: int32), stored entries incl.
+ * padding, whether rows/columns are in reverse Cuthill-McKee order. */
+int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted);
+
 /* Timing of the last hot-path calls (device time, milliseconds). */
 typedef struct {
   double assemble_nse_ms, build_precond_ms, assemble_T_matrix_ms, assemble_T_rhs_ms;

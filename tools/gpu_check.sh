@@ -30,7 +30,11 @@ for s in $STEPS; do
           --output-format csv -d /tmp/pmc -o pmc \
           -- python3 bench.py --refine $R --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc/probe_$ctr.json 2> $OUT/pmc/probe_$ctr.err
         rc=$?; find /tmp/pmc -name "*counter_collection*.csv" -exec cp {} $OUT/pmc/${ctr}.csv \; ; ok $rc pmc_$ctr
-      done ;;
+      done
+      # summarise on the box: the per-dispatch CSVs exceed gpurun's copy-back cap
+      python3 tools/pmc_summary.py $OUT/pmc "rocprofv3 --pmc <CTR> --kernel-trace --kernel-include-regex '${PMC_KERNELS:-k_sell_spmv|k_nse_system|k_chain}' -- python3 bench.py --refine $R --steps 1 --warmup 0 --no-cpu-baseline" $OUT/pmc/summary.json
+      ok $? pmc_summary
+      rm -f $OUT/pmc/*.csv ;;
   esac
 done
 echo done >> $OUT/steps.log
