@@ -151,7 +151,7 @@ struct PhaseTimer {
 void velocity_stats_global(Ctx& c) {
   halo_exchange(c, c.halo_nse, c.nse_sol.p);
   if (c.feec)
-    feec_velocity_stats(c.fcd(), c.n_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
+    feec_velocity_stats(c.fcd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
   else
     velocity_stats(c.cd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
   allreduce(c, c.dscal.p + 262, 2, true);
@@ -425,6 +425,14 @@ std::vector<int64_t> global_positions(const Ctx& c, int field) {
   std::vector<int64_t> g;
   if (field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS) {
     g.assign(c.T_g.begin(), c.T_g.end());
+  } else if (c.feec) {
+    // [w | u | p]: edges, faces, cells
+    const int nw = c.fe_nw, nu = c.fe_nu;
+    g.resize(size_t(c.n_u) + c.n_p);
+    for (int i = 0; i < nw; ++i) g[i] = c.fe_w_g[i];
+    for (int i = 0; i < nu; ++i) g[size_t(nw) + i] = int64_t(c.fe_nw_g) + c.fe_u_g[i];
+    for (int i = 0; i < c.n_p; ++i)
+      g[size_t(nw + nu) + i] = int64_t(c.fe_nw_g) + c.fe_nu_g + c.p_g[i];
   } else {
     g.resize(size_t(c.n_u) + c.n_p);
     for (int i = 0; i < c.n_u; ++i) g[i] = 3 * int64_t(c.vnode_g[i / 3]) + i % 3;
@@ -437,6 +445,12 @@ std::vector<int64_t> global_positions(const Ctx& c, int field) {
 bool owned_entry(const Ctx& c, int field, size_t i) {
   if (field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS)
     return int(i) < c.nTo;
+  if (c.feec) {
+    const int k = int(i);
+    if (k < c.fe_nw) return k < c.fe_nwo;
+    if (k < c.fe_nw + c.fe_nu) return k - c.fe_nw < c.fe_nuo;
+    return k - c.fe_nw - c.fe_nu < c.fe_npo;
+  }
   if (int(i) < c.n_u) return int(i) < 3 * c.nvo;
   return int(i) - c.n_u < c.npo;
 }
@@ -1082,6 +1096,8 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
     csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
     c.T_rhs.zero(c.stream);
+    halo_exchange(c, c.halo_T, c.old_T.p);
+    halo_exchange(c, c.halo_nse, c.nse_sol.p);
     if (c.feec) {
       // velocity from the Raviart-Thomas field of nse_solution (FEEC.tpp:1000-1062)
       for (int k = 0; k < c.n_colors(); ++k)
@@ -1091,8 +1107,6 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
       c.T_rhs_ok = true;
       return DCP_OK;
     }
-    halo_exchange(c, c.halo_T, c.old_T.p);
-    halo_exchange(c, c.halo_nse, c.nse_sol.p);
     for (int k = 0; k < c.n_colors(); ++k)
       launch_T_rhs(c.cd(), c.color_begin(k), c.color_size(k), c.old_T.p, c.nse_sol.p, c.ph,
                    c.T_rhs.p, c.stream);
@@ -1398,17 +1412,31 @@ inline int feec_type(int i) { return i < 12 ? 0 : i < 18 ? 1 : 2; }
 
 extern "C" {
 
-int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m) {
+int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
   return guarded(ctx, [&] {
-    require(ctx != nullptr && m != nullptr, DCP_ERR_INVALID, "NULL argument");
+    require(ctx != nullptr && gm != nullptr, DCP_ERR_INVALID, "NULL argument");
     Ctx& c = *ctx;
-    require(!c.comm, DCP_ERR_UNSUPPORTED, "the FEEC variant runs on one GPU (world_size 1)");
-    require(m->cell_w && m->sign_w && m->cell_u && m->sign_u && m->cell_vertices &&
-                m->cell_diameter && m->cell_T_dofs && m->w_fixed && m->u_fixed,
+    require(gm->cell_w && gm->sign_w && gm->cell_u && gm->sign_u && gm->cell_vertices &&
+                gm->cell_diameter && gm->cell_T_dofs && gm->w_fixed && gm->u_fixed,
             DCP_ERR_INVALID, "NULL array");
+    require(gm->n_cells > 0 && gm->n_p == gm->n_cells, DCP_ERR_INVALID,
+            "invalid FEEC sizes (DGQ0: n_p == n_cells)");
+    // several GPUs: this rank's cells + two ghost layers (partition.h)
+    const bool dist = c.comm != nullptr;
+    FeecLocal L;
+    dcp_feec_mesh lv{};
+    if (dist) {
+      try {
+        L = localize_feec(*gm, c.cfg.rank, c.cfg.world_size);
+      } catch (const std::runtime_error& e) {
+        fail(DCP_ERR_INVALID, e.what());
+      }
+      lv = L.view();
+    }
+    const dcp_feec_mesh* m = dist ? &lv : gm;
     const int nc = m->n_cells, nw = m->n_w, nu = m->n_u, np = m->n_p, nT = m->n_T;
     require(nc > 0 && nw > 0 && nu > 0 && np == nc && nT > 0, DCP_ERR_INVALID,
-            "invalid FEEC sizes (DGQ0: n_p == n_cells)");
+            "invalid FEEC sizes");
     const int n = nw + nu + np;
     std::vector<int32_t> dofs(size_t(nc) * 19), td(size_t(nc) * 8);
     std::vector<int8_t> sg(size_t(nc) * 19, 1);
@@ -1529,19 +1557,32 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m) {
     c.feec = true;
     c.have_mesh = false;
     c.n_cells = nc;
-    c.n_owned_cells = nc;
+    c.n_owned_cells = dist ? L.n_owned_cells : nc;
     c.fe_nw = nw;
     c.fe_nu = nu;
     c.fe_np = np;
+    c.fe_nwo = dist ? L.nwo : nw;
+    c.fe_nuo = dist ? L.nuo : nu;
+    c.fe_npo = c.n_owned_cells;
+    c.fe_nw_g = gm->n_w;
+    c.fe_nu_g = gm->n_u;
     c.n_u = nw + nu;  // state API: NSE vector = [w u | p]
     c.n_p = np;
     c.n_T = nT;
-    c.n_u_g = c.n_u;
-    c.n_p_g = np;
-    c.n_T_g = nT;
-    c.nTo = nT;
+    c.n_u_g = gm->n_w + gm->n_u;
+    c.n_p_g = gm->n_p;
+    c.n_T_g = gm->n_T;
+    c.nTo = dist ? L.nTo : nT;
     c.n_vnodes = 0;
-    c.max_owned[3] = nT;
+    c.fe_w_g = L.w_g;
+    c.fe_u_g = L.u_g;
+    c.p_g = L.cells_g;
+    c.T_g = L.T_g;
+    c.max_owned[3] = c.nTo;
+    c.max_owned[4] = c.fe_nwo + c.fe_nuo + c.fe_npo;
+    c.max_owned[5] = c.fe_nwo;
+    c.max_owned[6] = c.fe_nuo;
+    c.max_owned[7] = c.fe_npo;
     c.fe_dofs.upload(dofs);
     c.fe_sign.upload(sg);
     c.fe_X.upload(std::vector<double>(m->cell_vertices, m->cell_vertices + 24 * size_t(nc)));
@@ -1583,11 +1624,37 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m) {
     for (auto* b : {&c.nse_sol, &c.old_nse, &c.nse_rhs, &c.T_sol, &c.old_T, &c.T_rhs}) b->zero(c.stream);
     free_workspaces(c);
     {
+      // sum of the mean-value weights over the owned cells (all ranks)
       std::vector<double> w(nc);
       DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
       DCP_HIP_CHECK(hipMemcpy(w.data(), c.fe_cellw.p, nc * sizeof(double), hipMemcpyDeviceToHost));
-      c.fe_wsum = 0;
-      for (double x : w) c.fe_wsum += x;
+      double ws = 0;
+      for (int k = 0; k < c.fe_npo; ++k) ws += w[k];
+      c.fe_wsum = ws;
+    }
+    if (dist) {
+      auto one = [&](Ctx::Halo& h, std::initializer_list<std::pair<const HaloPlan*, int>> parts) {
+        std::vector<int> peers;
+        std::vector<std::vector<int32_t>> sp, rp;
+        for (auto& pr : parts) plan_positions(*pr.first, pr.second, peers, sp, rp);
+        make_halo(h, peers, sp, rp);
+      };
+      one(c.halo_fw, {{&L.hw, 0}});
+      one(c.halo_fu, {{&L.hu, 0}});
+      one(c.halo_fp, {{&L.hp, 0}});
+      one(c.halo_nse, {{&L.hw, 0}, {&L.hu, nw}, {&L.hp, nw + nu}});
+      one(c.halo_T, {{&L.hT, 0}});
+      double mx[5] = {double(c.max_owned[3]), double(c.max_owned[4]), double(c.max_owned[5]),
+                      double(c.max_owned[6]), double(c.max_owned[7])};
+      double* d = c.dscal.p + 3500;
+      DCP_HIP_CHECK(hipMemcpyAsync(d, mx, sizeof(mx), hipMemcpyHostToDevice, c.stream));
+      c.comm->allreduce(d, 5, true, c.stream);
+      DCP_HIP_CHECK(hipMemcpyAsync(mx, d, sizeof(mx), hipMemcpyDeviceToHost, c.stream));
+      DCP_HIP_CHECK(hipMemcpyAsync(d, &c.fe_wsum, sizeof(double), hipMemcpyHostToDevice, c.stream));
+      c.comm->allreduce(d, 1, false, c.stream);
+      DCP_HIP_CHECK(hipMemcpyAsync(&c.fe_wsum, d, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+      DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+      for (int k = 0; k < 5; ++k) c.max_owned[3 + k] = int(mx[k]);
     }
     c.have_mesh = true;
     c.fe_assembled = c.fe_precond = c.T_matrix_ok = c.T_rhs_ok = false;
@@ -1601,6 +1668,8 @@ int dcp_feec_assemble_nse_system(dcp_ctx* ctx) {
     Ctx& c = *ctx;
     require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
+    halo_exchange(c, c.halo_nse, c.old_nse.p);
+    halo_exchange(c, c.halo_T, c.old_T.p);
     c.fe_val.zero(c.stream);
     c.nse_rhs.zero(c.stream);
     for (int k = 0; k < c.n_colors(); ++k)

@@ -76,7 +76,8 @@ struct Ctx {
   };
   Halo halo_v, halo_p, halo_nse, halo_T;
   std::vector<int32_t> vnode_g, p_g, T_g;
-  int max_owned[4] = {0, 0, 0, 0};   // max over ranks of |seg_nse|, |seg_p|, |seg_v|, |seg_T|
+  // max over ranks of |seg_nse|, |seg_p|, |seg_v|, |seg_T|, FEEC |[w u p]|, |w|, |u|, |p|
+  int max_owned[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int sell_part_len = 0;             // common length of the SELL partial arrays
   // mesh
   DBuf<int32_t> cell_q2, cell_p, cell_T;
@@ -155,7 +156,18 @@ struct Ctx {
   // ---- FEEC variant (config 4): n_u = n_w + n_u(faces), n_p = cells
   bool feec = false;
   bool feec_zero_mean = true;          // parameters.correct_pressure_to_zero_mean
-  int fe_nw = 0, fe_nu = 0, fe_np = 0;
+  int fe_nw = 0, fe_nu = 0, fe_np = 0;             // local (owned + ghost)
+  int fe_nwo = 0, fe_nuo = 0, fe_npo = 0;          // owned
+  int fe_nw_g = 0, fe_nu_g = 0;                    // global
+  std::vector<int32_t> fe_w_g, fe_u_g;             // local -> global (several GPUs)
+  Halo halo_fw, halo_fu, halo_fp;                  // per-field halos of [w | u | p] blocks
+  // owned segments: the [w | u | p] vector and its blocks
+  Seg seg_fe() const {
+    return Seg{fe_nwo, fe_nw, fe_nwo + fe_nuo, fe_nw + fe_nu, fe_nwo + fe_nuo + fe_npo, 4};
+  }
+  Seg seg_fw() const { return Seg::all(fe_nwo, 5); }
+  Seg seg_fu() const { return Seg::all(fe_nuo, 6); }
+  Seg seg_fp() const { return Seg::all(fe_npo, 7); }
   DBuf<int32_t> fe_dofs;
   DBuf<int8_t> fe_sign;
   DBuf<double> fe_X, fe_cellw;
@@ -170,7 +182,7 @@ struct Ctx {
     return FeecCellData{n_cells, fe_dofs.p, fe_sign.p, fe_X.p, diameter.p, fe_fixed.p, cell_T.p};
   }
 
-  Seg seg_nse() const { return Seg{3 * nvo, n_u, 3 * nvo + npo, 0}; }
+  Seg seg_nse() const { return Seg::two(3 * nvo, n_u, 3 * nvo + npo, 0); }
   Seg seg_p() const { return Seg::all(npo, 1); }
   Seg seg_v() const { return Seg::all(3 * nvo, 2); }
   Seg seg_T() const { return Seg::all(nTo, 3); }

@@ -186,14 +186,16 @@ struct DScal {
   const double* p;
   double m;
 };
-// Owned part of a local vector for reductions: entries [0, n1) and
-// [off2, off2 + n - n1). The multi-GPU NSE layout [u_own u_ghost | p_own
-// p_ghost] has two owned segments; every other vector (and every single-GPU
-// vector) is a prefix, Seg::all(n).
+// Owned part of a local vector for reductions: entries [0, n1),
+// [off2, off2 + n12 - n1) and [off3, off3 + n - n12). The multi-GPU NSE
+// layout [u_own u_ghost | p_own p_ghost] has two owned segments, the FEEC one
+// [w_own w_ghost | u_own u_ghost | p_own p_ghost] three; every other vector
+// (and every single-GPU vector) is a prefix, Seg::all(n).
 struct Seg {
-  int n1, off2, n;
+  int n1, off2, n12, off3, n;
   int kind;  // vector family (chain width selection on several GPUs), -1: any
-  static Seg all(int n, int kind = -1) { return Seg{n, 0, n, kind}; }
+  static Seg all(int n, int kind = -1) { return Seg{n, 0, n, 0, n, kind}; }
+  static Seg two(int n1, int off2, int n, int kind) { return Seg{n1, off2, n, 0, n, kind}; }
 };
 // Partial-sum reduction buffer: kReduceBlocks doubles per slot.
 constexpr int kReduceBlocks = 512;

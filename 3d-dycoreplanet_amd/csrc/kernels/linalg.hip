@@ -71,7 +71,9 @@ void spmv(int rows, const int32_t* ptr, const int32_t* col, const double* val, c
 }
 
 // position of the i-th owned entry of a two-segment vector (device.h Seg)
-__device__ inline long seg_pos(const Seg& g, long i) { return i < g.n1 ? i : g.off2 + (i - g.n1); }
+__device__ inline long seg_pos(const Seg& g, long i) {
+  return i < g.n1 ? i : (i < g.n12 ? g.off2 + (i - g.n1) : g.off3 + (i - g.n12));
+}
 
 __device__ inline double block_sum(double v, double* sm) {
   // wave reduce then LDS across the 4 waves; fixed order

@@ -286,4 +286,225 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
   return L;
 }
 
+dcp_feec_mesh FeecLocal::view() const {
+  dcp_feec_mesh v{};
+  v.n_cells = n_cells;
+  v.n_w = n_w();
+  v.n_u = n_u();
+  v.n_p = n_cells;
+  v.n_T = n_T();
+  v.cell_w = cell_w.data();
+  v.sign_w = sign_w.data();
+  v.cell_u = cell_u.data();
+  v.sign_u = sign_u.data();
+  v.cell_vertices = vertices.data();
+  v.cell_diameter = diameter.data();
+  v.cell_T_dofs = cell_T.data();
+  v.w_fixed = w_fixed.data();
+  v.u_fixed = u_fixed.data();
+  v.T = dcp_constraints{int(T_line.size()), T_line.data(), T_ptr.data(), T_edof.data(),
+                        T_w.data(), T_inh.data()};
+  return v;
+}
+
+FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
+  const int nc = m.n_cells;
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("localize: bad rank/world");
+  if (nc < world) throw std::runtime_error("localize: fewer cells than ranks");
+  std::vector<int64_t> start(size_t(world) + 1);
+  for (int r = 0; r <= world; ++r) start[r] = int64_t(r) * nc / world;
+  auto rank_of = [&](int c) {
+    return int(std::upper_bound(start.begin(), start.end(), int64_t(c)) - start.begin()) - 1;
+  };
+  // owners: rank of the lowest-index cell touching the entity
+  std::vector<int32_t> wown(m.n_w, -1), uown(m.n_u, -1), Town(m.n_T, -1);
+  for (int c = 0; c < nc; ++c) {
+    const int rc = rank_of(c);
+    for (int l = 0; l < 12; ++l) {
+      const int e = m.cell_w[12 * size_t(c) + l];
+      if (e < 0 || e >= m.n_w) throw std::runtime_error("localize: edge dof out of range");
+      if (wown[e] < 0) wown[e] = rc;
+    }
+    for (int f = 0; f < 6; ++f) {
+      const int u = m.cell_u[6 * size_t(c) + f];
+      if (u < 0 || u >= m.n_u) throw std::runtime_error("localize: face dof out of range");
+      if (uown[u] < 0) uown[u] = rc;
+    }
+    for (int v = 0; v < 8; ++v) {
+      const int t = m.cell_T_dofs[8 * size_t(c) + v];
+      if (t < 0 || t >= m.n_T) throw std::runtime_error("localize: T dof out of range");
+      if (Town[t] < 0) Town[t] = rc;
+    }
+  }
+  // vertex (T dof) -> cells, for the vertex-neighbour ghost layers
+  std::vector<int32_t> vptr(size_t(m.n_T) + 1, 0), vcells;
+  for (int c = 0; c < nc; ++c)
+    for (int v = 0; v < 8; ++v) vptr[m.cell_T_dofs[8 * size_t(c) + v] + 1]++;
+  for (int t = 0; t < m.n_T; ++t) vptr[t + 1] += vptr[t];
+  vcells.resize(size_t(vptr[m.n_T]));
+  {
+    std::vector<int32_t> f(vptr.begin(), vptr.end() - 1);
+    for (int c = 0; c < nc; ++c)
+      for (int v = 0; v < 8; ++v) vcells[f[m.cell_T_dofs[8 * size_t(c) + v]]++] = c;
+  }
+  std::vector<int> cstamp(nc, -1), wstamp(m.n_w, -1), ustamp(m.n_u, -1), Tstamp(m.n_T, -1);
+  int token = 0;
+  auto cells_of = [&](int s) {
+    const int tok = token++;
+    std::vector<int32_t> owned, ghosts, frontier, next;
+    for (int64_t c = start[s]; c < start[s + 1]; ++c) {
+      owned.push_back(int32_t(c));
+      cstamp[c] = tok;
+    }
+    frontier = owned;
+    for (int layer = 0; layer < 2; ++layer) {
+      next.clear();
+      for (int32_t c : frontier)
+        for (int v = 0; v < 8; ++v) {
+          const int t = m.cell_T_dofs[8 * size_t(c) + v];
+          for (int j = vptr[t]; j < vptr[t + 1]; ++j)
+            if (cstamp[vcells[j]] != tok) {
+              cstamp[vcells[j]] = tok;
+              next.push_back(vcells[j]);
+            }
+        }
+      ghosts.insert(ghosts.end(), next.begin(), next.end());
+      frontier.swap(next);
+    }
+    std::sort(ghosts.begin(), ghosts.end());
+    owned.insert(owned.end(), ghosts.begin(), ghosts.end());
+    return owned;
+  };
+  auto w_of = [&](int c, auto&& emit) {
+    for (int l = 0; l < 12; ++l) emit(m.cell_w[12 * size_t(c) + l]);
+  };
+  auto u_of = [&](int c, auto&& emit) {
+    for (int f = 0; f < 6; ++f) emit(m.cell_u[6 * size_t(c) + f]);
+  };
+  auto T_of = [&](int c, auto&& emit) {
+    for (int v = 0; v < 8; ++v) emit(m.cell_T_dofs[8 * size_t(c) + v]);
+  };
+  FeecLocal L;
+  L.rank = rank;
+  L.world = world;
+  L.cells_g = cells_of(rank);
+  L.n_cells = int(L.cells_g.size());
+  L.n_owned_cells = int(start[rank + 1] - start[rank]);
+  auto order = [&](std::vector<int32_t>& ents, const std::vector<int32_t>& own, int& no, int& ng) {
+    std::stable_partition(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; });
+    no = int(std::count_if(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; }));
+    ng = int(ents.size()) - no;
+  };
+  collect(L.cells_g, w_of, wstamp, token++, L.w_g);
+  collect(L.cells_g, u_of, ustamp, token++, L.u_g);
+  collect(L.cells_g, T_of, Tstamp, token++, L.T_g);
+  order(L.w_g, wown, L.nwo, L.nwg);
+  order(L.u_g, uown, L.nuo, L.nug);
+  order(L.T_g, Town, L.nTo, L.nTg);
+  std::vector<int32_t> wl(m.n_w, -1), ul(m.n_u, -1), Tl(m.n_T, -1), cl(nc, -1);
+  for (size_t i = 0; i < L.w_g.size(); ++i) wl[L.w_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.u_g.size(); ++i) ul[L.u_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.T_g.size(); ++i) Tl[L.T_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.cells_g.size(); ++i) cl[L.cells_g[i]] = int32_t(i);
+  const int lc_n = L.n_cells;
+  L.cell_w.resize(size_t(lc_n) * 12);
+  L.sign_w.resize(size_t(lc_n) * 12);
+  L.cell_u.resize(size_t(lc_n) * 6);
+  L.sign_u.resize(size_t(lc_n) * 6);
+  L.cell_T.resize(size_t(lc_n) * 8);
+  L.vertices.resize(size_t(lc_n) * 24);
+  L.diameter.resize(lc_n);
+  for (int lc = 0; lc < lc_n; ++lc) {
+    const size_t c = size_t(L.cells_g[lc]);
+    for (int l = 0; l < 12; ++l) {
+      L.cell_w[12 * size_t(lc) + l] = wl[m.cell_w[12 * c + l]];
+      L.sign_w[12 * size_t(lc) + l] = m.sign_w[12 * c + l];
+    }
+    for (int f = 0; f < 6; ++f) {
+      L.cell_u[6 * size_t(lc) + f] = ul[m.cell_u[6 * c + f]];
+      L.sign_u[6 * size_t(lc) + f] = m.sign_u[6 * c + f];
+    }
+    for (int v = 0; v < 8; ++v) L.cell_T[8 * size_t(lc) + v] = Tl[m.cell_T_dofs[8 * c + v]];
+    std::copy(m.cell_vertices + 24 * c, m.cell_vertices + 24 * c + 24,
+              L.vertices.begin() + 24 * size_t(lc));
+    L.diameter[lc] = m.cell_diameter[c];
+  }
+  L.w_fixed.resize(L.w_g.size());
+  L.u_fixed.resize(L.u_g.size());
+  for (size_t i = 0; i < L.w_g.size(); ++i) L.w_fixed[i] = m.w_fixed[L.w_g[i]];
+  for (size_t i = 0; i < L.u_g.size(); ++i) L.u_fixed[i] = m.u_fixed[L.u_g[i]];
+  L.T_ptr.push_back(0);
+  for (int l = 0; l < m.T.n_lines; ++l) {
+    const int d = m.T.line_dof[l];
+    if (d < 0 || d >= m.n_T || Tl[d] < 0) continue;
+    L.T_line.push_back(Tl[d]);
+    L.T_inh.push_back(m.T.inhomogeneity[l]);
+    for (int k = m.T.entry_ptr[l]; k < m.T.entry_ptr[l + 1]; ++k) {
+      const int e = m.T.entry_dof[k];
+      if (e < 0 || e >= m.n_T || Tl[e] < 0)
+        throw std::runtime_error("localize: constraint entry outside the local mesh");
+      L.T_edof.push_back(Tl[e]);
+      L.T_w.push_back(m.T.entry_w[k]);
+    }
+    L.T_ptr.push_back(int(L.T_edof.size()));
+  }
+  // halo plans: my ghosts grouped by owner; my owned entities in other
+  // ranks' local cells
+  std::vector<int32_t> cown(nc);
+  for (int c = 0; c < nc; ++c) cown[c] = rank_of(c);
+  std::vector<int32_t> pg_sorted;  // p: entities are cells
+  struct Field {
+    HaloPlan* plan;
+    const std::vector<int32_t>* ents;
+    const std::vector<int32_t>* own;
+    const std::vector<int32_t>* lidx;
+    int no;
+  };
+  const int npo = L.n_owned_cells;
+  Field fields[4] = {{&L.hw, &L.w_g, &wown, &wl, L.nwo},
+                     {&L.hu, &L.u_g, &uown, &ul, L.nuo},
+                     {&L.hp, &L.cells_g, &cown, &cl, npo},
+                     {&L.hT, &L.T_g, &Town, &Tl, L.nTo}};
+  std::vector<std::vector<std::vector<int32_t>>> sends(4, std::vector<std::vector<int32_t>>(world));
+  for (int s = 0; s < world; ++s) {
+    if (s == rank) continue;
+    const std::vector<int32_t> cs = cells_of(s);
+    for (int f = 0; f < 4; ++f) {
+      std::vector<int32_t> ents;
+      if (f == 0) collect(cs, w_of, wstamp, token++, ents);
+      else if (f == 1) collect(cs, u_of, ustamp, token++, ents);
+      else if (f == 2) { ents = cs; std::sort(ents.begin(), ents.end()); }
+      else collect(cs, T_of, Tstamp, token++, ents);
+      for (int32_t e : ents)
+        if ((*fields[f].own)[e] == rank) sends[f][s].push_back(e);
+    }
+  }
+  for (int f = 0; f < 4; ++f) {
+    const Field& F = fields[f];
+    std::vector<std::vector<int32_t>> recv(world);
+    for (size_t i = size_t(F.no); i < F.ents->size(); ++i) {
+      const int32_t e = (*F.ents)[i];
+      recv[(*F.own)[e]].push_back(e);
+    }
+    HaloPlan& h = *F.plan;
+    h.send_ptr.push_back(0);
+    h.recv_ptr.push_back(0);
+    for (int s = 0; s < world; ++s) {
+      if (s == rank || (sends[f][s].empty() && recv[s].empty())) continue;
+      h.peers.push_back(s);
+      for (int32_t e : sends[f][s]) {
+        h.send_idx.push_back((*F.lidx)[e]);
+        h.send_gid.push_back(e);
+      }
+      for (int32_t e : recv[s]) {
+        h.recv_idx.push_back((*F.lidx)[e]);
+        h.recv_gid.push_back(e);
+      }
+      h.send_ptr.push_back(int32_t(h.send_idx.size()));
+      h.recv_ptr.push_back(int32_t(h.recv_idx.size()));
+    }
+  }
+  return L;
+}
+
 }  // namespace dcp

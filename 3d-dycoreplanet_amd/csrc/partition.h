@@ -61,6 +61,28 @@ struct LocalMesh {
   dcp_constraints T_view() const;
 };
 
+// FEEC variant (config 4): the same split and two ghost layers; fields w
+// (edges), u (faces), p (cells: DGQ0), T (Q1 vertices), each numbered owned
+// first then ghosts. The local NSE vector is [w_l | u_l | p_l].
+struct FeecLocal {
+  int rank = 0, world = 1;
+  int n_cells = 0, n_owned_cells = 0;
+  int nwo = 0, nwg = 0, nuo = 0, nug = 0, nTo = 0, nTg = 0;
+  std::vector<int32_t> cells_g, w_g, u_g, T_g;  // local -> global (p_g = cells_g)
+  std::vector<int32_t> cell_w, cell_u, cell_T;  // local ids
+  std::vector<int8_t> sign_w, sign_u;
+  std::vector<double> vertices, diameter;
+  std::vector<uint8_t> w_fixed, u_fixed;
+  std::vector<int> T_line, T_ptr, T_edof;
+  std::vector<double> T_w, T_inh;
+  HaloPlan hw, hu, hp, hT;
+  int n_w() const { return nwo + nwg; }
+  int n_u() const { return nuo + nug; }
+  int n_T() const { return nTo + nTg; }
+  dcp_feec_mesh view() const;  // points into this object
+};
+FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world);
+
 // Builds rank `rank`'s local mesh of a `world`-way split of the global mesh
 // (arguments as dcp_mesh_upload). Throws std::runtime_error on bad input.
 LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,

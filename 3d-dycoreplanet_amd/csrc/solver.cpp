@@ -595,7 +595,7 @@ int chain_width(const Ctx& c, Seg g) {
   // every rank launches the same number of chain workgroups (their partials
   // are all-reduced element-wise): size it by the largest owned part
   if (!c.comm) return chain_blocks(g.n);
-  if (g.kind < 0 || g.kind > 3) throw std::runtime_error("chain_width: untyped vector on several GPUs");
+  if (g.kind < 0 || g.kind > 7) throw std::runtime_error("chain_width: untyped vector on several GPUs");
   return chain_blocks(c.max_owned[g.kind]);
 }
 
@@ -732,15 +732,21 @@ struct FeecOps {
   const int32_t* ptr;
   const int32_t* col;
   const double* val;
-  // y = block(I, J) x
-  void block(int r0, int r1, int c0, int c1, const double* x, double* y, bool add) const {
+  // y = block(I, J) x; x is the column block's sub-vector, whose ghost
+  // entries are refreshed first (several GPUs) unless `fresh`
+  void block(int r0, int r1, int c0, int c1, const double* x, double* y, bool add,
+             bool fresh = false) const {
+    if (!fresh) {
+      Ctx::Halo& h = c0 == 0 ? c.halo_fw : c0 == ou ? c.halo_fu : c.halo_fp;
+      halo_exchange(c, h, const_cast<double*>(x));
+    }
     spmv_block(r0, r1, c0, c1, ptr, col, val, x, y, add, c.stream);
   }
   // ShiftedSchurComplement::vmult (shifted_schur_complement.hpp:155-171):
   // y = M_u x - B_10 D_w^-1 B_01 x
   void shifted(const double* x, double* y) const {
     block(ou, op, ou, op, x, y, false);              // block_11
-    block(0, nw, ou, op, x, c.fe_t3.p, false);       // tmp1 = block_01 x
+    block(0, nw, ou, op, x, c.fe_t3.p, false, true); // tmp1 = block_01 x
     mul(nw, c.fe_dinv.p, c.fe_t3.p, c.fe_t4.p, c.stream);  // tmp2 = Mw Jacobi tmp1
     scale(nw, DScal{nullptr, -1.0}, c.fe_t4.p, c.stream);
     block(ou, op, 0, nw, c.fe_t4.p, y, true);        // += block_10 tmp2
@@ -767,11 +773,11 @@ void feec_precondition(Ctx& c, const FeecOps& o, const double* src, double* dst)
     // GMRES (30 tmp vectors) <= 30 iterations, tol 1e-6 |src|, left
     // preconditioner Mu Jacobi, failure swallowed; initial guess = dst_u
     // (shifted_schur_complement.hpp:271-298)
-    const double nrm = std::sqrt(dot_host(c, Seg::all(nu), t1, t1, kSlotB));
+    const double nrm = std::sqrt(dot_host(c, c.seg_fu(), t1, t1, kSlotB));
     Control ctl{30, 1e-6 * nrm};
     Op A = [&](const double* x, double* y) { o.shifted(x, y); };
     Op P = [&](const double* x, double* y) { mul(nu, c.fe_dinv.p + nw, x, y, c.stream); };
-    (void)gmres(c, nu, Seg::all(nu), A, &P, dst + ou, t1, ctl, c.fe_s, 30);
+    (void)gmres(c, nu, c.seg_fu(), A, &P, dst + ou, t1, ctl, c.fe_s, 30);
   }
   // ptmp = -2 src_p + B_21 dst_u (Q15) ; dst_p = ApproxNestedSchurComplementInverse(ptmp)
   double* t2 = c.fe_t2.p;
@@ -780,14 +786,14 @@ void feec_precondition(Ctx& c, const FeecOps& o, const double* src, double* dst)
   {
     // GMRES <= 100 iterations, tol 1e-6 |src|, identity, failure swallowed
     // (nested_schur_complement.hpp:287-322)
-    const double nrm = std::sqrt(dot_host(c, Seg::all(np), t2, t2, kSlotB));
+    const double nrm = std::sqrt(dot_host(c, c.seg_fp(), t2, t2, kSlotB));
     Control ctl{100, 1e-6 * nrm};
     Op A = [&](const double* x, double* y) { o.lower(x, y); };
-    (void)gmres(c, np, Seg::all(np), A, nullptr, dst + op, t2, ctl, c.fe_n, 30);
+    (void)gmres(c, np, c.seg_fp(), A, nullptr, dst + op, t2, ctl, c.fe_n, 30);
   }
   if (c.feec_zero_mean) {
     // dst -= compute_mean_value(DGQ0, QGauss(1), dst) (Q18: consistent cell map)
-    gdot(c, Seg::all(np), c.fe_cellw.p, dst + op, kSlotC);
+    gdot(c, c.seg_fp(), c.fe_cellw.p, dst + op, kSlotC);
     fill(1, c.fe_wsum, slot(c, kSlotD), c.stream);
     scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);
     shift(np, DScal{slot(c, kSlotA), -1.0}, dst + op, c.stream);
@@ -805,17 +811,18 @@ int feec_solve_nse(Ctx& c, int* iterations) {
   x.alloc(n);
   copy(n, c.nse_sol.p, x.p, c.stream);
   scale(np, DScal{nullptr, c.ph.dt}, x.p + o.op, c.stream);  // :1345 block(2) *= dt
-  const double tol = 1e-8 * std::sqrt(dot_host(c, Seg::all(n), c.nse_rhs.p, c.nse_rhs.p, kSlotA));
+  const double tol = 1e-8 * std::sqrt(dot_host(c, c.seg_fe(), c.nse_rhs.p, c.nse_rhs.p, kSlotA));
   Control ctl{500, tol};
   // SolverGMRES(AdditionalData(100)): fresh (zero) temporary vectors per solve;
   // the preconditioner's output vector is the initial guess of its inner solves
   ensure_pool(c.fe_v, 100, size_t(n));
   for (int k = 0; k < 100; ++k) fill(n, 0.0, c.fe_v[k], c.stream);
   Op A = [&](const double* xx, double* y) {
+    halo_exchange(c, c.halo_nse, const_cast<double*>(xx));
     spmv_csr(n, c.fe_ptr.p, c.fe_col.p, c.fe_val.p, xx, y, false, c.stream);
   };
   Op P = [&](const double* s, double* d) { feec_precondition(c, o, s, d); };
-  const State st = gmres(c, n, Seg::all(n), A, &P, x.p, c.nse_rhs.p, ctl, c.fe_v, 100);
+  const State st = gmres(c, n, c.seg_fe(), A, &P, x.p, c.nse_rhs.p, ctl, c.fe_v, 100);
   zero_fixed(n, c.fe_fixed.p, x.p, c.stream);                // constraints.distribute (:1440)
   scale(np, DScal{nullptr, 1.0 / c.ph.dt}, x.p + o.op, c.stream);  // :1446 block(2) /= dt
   copy(n, x.p, c.nse_sol.p, c.stream);

@@ -102,12 +102,44 @@ def cpu_baseline(refine):
                       f"{m.n_u + m.n_p} NSE dofs, {dt:.2f} s on 1 core"}
 
 
+def init_dist(args):
+    """One process per GPU (torchrun env); the library's own RCCL communicator
+    is created from rank 0's unique id broadcast through torch.distributed."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if args.shared_device:
+        local_rank = 0
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        import torch
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo" if args.shared_device else "nccl")
+    tdev = "cpu" if args.shared_device else "cuda"
+    import dcp
+    nccl_id = None
+    if world > 1:
+        import torch
+        idt = torch.zeros(128, dtype=torch.uint8, device=tdev)
+        if rank == 0:
+            idt.copy_(torch.frombuffer(bytearray(dcp.nccl_unique_id()), dtype=torch.uint8))
+        dist.broadcast(idt, 0)
+        nccl_id = bytes(idt.cpu().numpy().tobytes())
+
+    def make_ctx():
+        return dcp.Context(device=local_rank, rank=rank, world_size=world, nccl_id=nccl_id)
+    return world, rank, dist, tdev, make_ctx
+
+
 def run_feec(args):
     """Config 4 (BASELINE.json configs[3]): the FEEC model's time step
-    (ExteriorCalculus::BoussinesqModel<3>::run body, FEEC.tpp:2238-2300) on
-    one GPU: assemble_nse_system, build_nse_preconditioner, temperature
-    matrix/rhs, solve_NSE_block_preconditioned, solve_temperature."""
+    (ExteriorCalculus::BoussinesqModel<3>::run body, FEEC.tpp:2238-2300):
+    assemble_nse_system, build_nse_preconditioner, temperature matrix/rhs,
+    solve_NSE_block_preconditioned, solve_temperature; on N GPUs the p4est-style
+    cell split with a ghost-DoF halo (configs[3] asks for 2)."""
     import ctypes
+    world, rank, dist, tdev, make_ctx = init_dist(args)
     import dcp
     prm = args.prm if args.prm_set else os.path.join(ROOT, "configs",
                                                      "aqua_planet_shell_test_3d-feec.prm")
@@ -118,7 +150,7 @@ def run_feec(args):
     m = dcp.HostMesh(cuboid=False, refine=refine, R0=rp.R0, R1=rp.R1, length=rp.length,
                      temperature_degree=ph.temperature_degree, feec=True)
     f = m.feec
-    ctx = dcp.Context()
+    ctx = make_ctx()
     ctx.set_physics(ph)
     ctx.upload_feec_mesh(m)
     ctx.set_feec_zero_mean(bool(rp.correct_pressure_to_zero_mean))
@@ -142,32 +174,48 @@ def run_feec(args):
     for _ in range(args.warmup):
         step()
     hip = ctypes.CDLL("libamdhip64.so")
+    if dist is not None:
+        dist.barrier()
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
     recs = [step() for _ in range(args.steps)]
     hip.hipDeviceSynchronize()
+    if dist is not None:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
     asm_ms = float(np.mean([r[3]["assemble_nse_ms"] for r in recs]))
     solve_ms = float(np.mean([r[3]["solve_nse_ms"] for r in recs]))
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed, asm_ms, solve_ms], dtype=torch.float64, device=tdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, asm_ms, solve_ms = (float(v) for v in tt.tolist())
     its = recs[-1][1]
     out = {
-        "metric": "assembled DoFs/sec + GMRES iter/sec, 3D shell FEEC refine=4 (config 4), 1 GPU",
-        "value": f.n / (asm_ms * 1e-3), "unit": "assembled DoFs/s", "n_gpus": 1,
+        "metric": f"assembled DoFs/sec + GMRES iter/sec, 3D shell FEEC refine={refine} "
+                  f"(config 4), {world} GPU",
+        "value": f.n / (asm_ms * 1e-3), "unit": "assembled DoFs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic refined hypershell, reference initial state",
         "config": {"workload": f"FEEC shell Nedelec/RT/DGQ0 refine={refine}, one full time step",
                    "cells": f.n_cells, "nse_dofs": f.n, "n_w": f.n_w, "n_u": f.n_u,
-                   "n_p": f.n_p, "T_dofs": m.n_T, "parallelism": "single GPU"},
+                   "n_p": f.n_p, "T_dofs": m.n_T,
+                   "parallelism": "single GPU" if world == 1 else
+                   f"{world} GPUs: p4est-style cell partition, RCCL ghost halo + all-reduce"},
         "gmres_iterations": its, "gmres_iter_per_s": its / (solve_ms * 1e-3),
         "T_cg_iterations": recs[-1][2], "converged": all(r[0] == 0 for r in recs),
         "phase_ms": {k: float(np.mean([r[3][k] for r in recs])) for k in recs[0][3]
                      if k.endswith("_ms")},
         "setup_s": t_setup,
     }
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def main():
@@ -175,18 +223,7 @@ def main():
     if args.variant == "feec":
         run_feec(args)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if args.shared_device:
-        local_rank = 0
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
-        import torch
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("gloo" if args.shared_device else "nccl")
-    tdev = "cpu" if args.shared_device else "cuda"
+    world, rank, dist, tdev, make_ctx = init_dist(args)
     import dcp
 
     rp = dcp.load_prm(args.prm)
@@ -194,15 +231,7 @@ def main():
     t_setup = time.perf_counter()
     m = dcp.HostMesh(cuboid=False, refine=args.refine, R0=rp.R0, R1=rp.R1, length=rp.length,
                      temperature_degree=ph.temperature_degree)
-    nccl_id = None
-    if world > 1:
-        # one RCCL communicator for the halo / all-reduce path of libdcp (rank 0's id)
-        idt = torch.zeros(128, dtype=torch.uint8, device=tdev)
-        if rank == 0:
-            idt.copy_(torch.frombuffer(bytearray(dcp.nccl_unique_id()), dtype=torch.uint8))
-        dist.broadcast(idt, 0)
-        nccl_id = bytes(idt.cpu().numpy().tobytes())
-    ctx = dcp.Context(device=local_rank, rank=rank, world_size=world, nccl_id=nccl_id)
+    ctx = make_ctx()
     ctx.set_physics(ph)
     ctx.set_schur_explicit(args.schur == "explicit")
     ctx.upload_mesh(m)
@@ -260,6 +289,7 @@ def main():
     solve_ms = np.mean([r[4]["solve_nse_ms"] for r in recs])
     if dist is not None:
         # slowest rank bounds the job (wall time, assembly, solve)
+        import torch
         tt = torch.tensor([elapsed, asm_ms, solve_ms], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, asm_ms, solve_ms = (float(v) for v in tt.tolist())

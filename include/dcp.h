@@ -228,7 +228,9 @@ int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
  * DGQ0 pressure p (cells), MappingQ1. NSE state vector = [w | u | p]
  * (n_w + n_u + n_p); temperature as in the classic model (Q1). A context
  * holds either a classic or an FEEC mesh; the temperature calls, CFL / max
- * velocity and state calls dispatch on it. One GPU (world_size 1). */
+ * velocity and state calls dispatch on it. Several GPUs: every rank passes
+ * the global mesh and keeps its cells + two ghost layers (as for
+ * dcp_mesh_upload); state calls take global vectors. */
 typedef struct {
   int n_cells, n_w, n_u, n_p, n_T;
   const int32_t* cell_w;          /* [n_cells][12] edge dofs, deal.II line order */

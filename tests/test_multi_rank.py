@@ -148,3 +148,86 @@ def test_group_time_step_matches_single_gpu(world, refine):
         assert np.isclose(r["cfl0"], ref["cfl0"], rtol=1e-13)
         assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-10)
         assert np.isclose(r["cfl"], ref["cfl"], rtol=1e-10)
+
+
+def _feec_time_step(ctx, m, x0, T0):
+    for f, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
+                 (dcp.T_SOLUTION, T0)):
+        ctx.set_state(f, v)
+    out = {}
+    ctx.feec_assemble_nse_system()
+    out["rhs"] = ctx.get_state(dcp.NSE_RHS)
+    ctx.feec_build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    out["T_rhs"] = ctx.get_state(dcp.T_RHS)
+    out["nse"] = ctx.feec_solve_nse()
+    out["x"] = ctx.get_state(dcp.NSE_SOLUTION)
+    out["T"] = ctx.solve_temperature()
+    out["Tx"] = ctx.get_state(dcp.T_SOLUTION)
+    out["vmax"] = ctx.max_velocity()
+    out["cfl"] = ctx.cfl_number()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_feec_time_step_matches_single_gpu(world):
+    """Config 4 (FEEC, SURVEY §8e: 2 GPUs with a ghost-DoF halo) as an
+    in-process group: same outer GMRES count as one GPU; iterates at 1e-6
+    (the FEEC chain's rounding sensitivity, tests/test_feec.py)."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    f = m.feec
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(f.n)
+    x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
+    x0[f.fixed.astype(bool)] = 0
+    T0 = m.T0.copy()
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(ph)
+    ref_ctx.upload_feec_mesh(m)
+    ref = _feec_time_step(ref_ctx, m, x0, T0)
+    ref_ctx.close()
+
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(ph)
+            ctx.upload_feec_mesh(m)
+            results[rank] = _feec_time_step(ctx, m, x0, T0)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+
+    def merged(key):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        return v
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    assert rel(merged("rhs"), ref["rhs"]) < 1e-12
+    assert rel(merged("T_rhs"), ref["T_rhs"]) < 1e-12
+    x = merged("x")
+    assert np.linalg.norm(x - ref["x"]) <= 1e-6 * np.linalg.norm(ref["x"])
+    assert rel(merged("Tx"), ref["Tx"]) < 1e-6
+    for r in results:
+        assert r["nse"][0] == ref["nse"][0] == 0
+        assert r["nse"][1] == ref["nse"][1]                      # outer GMRES iterations
+        # CG to 1e-12 |b|: the last iteration can fall either side of the
+        # threshold with the partitioned summation order
+        assert abs(r["T"][1] - ref["T"][1]) <= 1
+        assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-6)
+        assert np.isclose(r["cfl"], ref["cfl"], rtol=1e-6)
