@@ -647,6 +647,32 @@ int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t*
   });
 }
 
+int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int field,
+                            int64_t* info, int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                            int32_t* recv_ptr, int64_t* recv_gid) {
+  return guarded(nullptr, [&] {
+    require(m != nullptr && info != nullptr, DCP_ERR_INVALID, "NULL argument");
+    require(field >= 0 && field < 4, DCP_ERR_INVALID, "field must be 0..3");
+    FeecLocal L;
+    try {
+      L = localize_feec(*m, rank, world);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    const HaloPlan& h = field == 0 ? L.hw : field == 1 ? L.hu : field == 2 ? L.hp : L.hT;
+    const int64_t v[11] = {L.n_cells, L.n_owned_cells, L.nwo, L.nwg, L.nuo, L.nug, L.nTo, L.nTg,
+                           int64_t(h.peers.size()), int64_t(h.send_idx.size()),
+                           int64_t(h.recv_idx.size())};
+    std::copy(v, v + 11, info);
+    if (peers) std::copy(h.peers.begin(), h.peers.end(), peers);
+    if (send_ptr) std::copy(h.send_ptr.begin(), h.send_ptr.end(), send_ptr);
+    if (recv_ptr) std::copy(h.recv_ptr.begin(), h.recv_ptr.end(), recv_ptr);
+    if (send_gid) std::copy(h.send_gid.begin(), h.send_gid.end(), send_gid);
+    if (recv_gid) std::copy(h.recv_gid.begin(), h.recv_gid.end(), recv_gid);
+    return DCP_OK;
+  });
+}
+
 int dcp_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -245,6 +245,13 @@ typedef struct {
   dcp_constraints T;              /* temperature constraints */
 } dcp_feec_mesh;
 int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m);
+/* Host-only summary of rank's FEEC partition (no GPU): info[11] = {n_cells
+ * local, n_owned_cells, nwo, nwg, nuo, nug, nTo, nTg, n_peers, n_send,
+ * n_recv} for the halo of `field` (0 edges w, 1 faces u, 2 cells p, 3 T
+ * vertices); optional arrays as in dcp_partition_info. */
+int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int field,
+                            int64_t* info, int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                            int32_t* recv_ptr, int64_t* recv_gid);
 /* assemble_nse_system (FEEC.tpp:669-873) */
 int dcp_feec_assemble_nse_system(dcp_ctx* ctx);
 /* assemble_nse_preconditioner / build_nse_preconditioner (FEEC.tpp:509-660) */

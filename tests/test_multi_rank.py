@@ -58,6 +58,51 @@ def test_partition_halo_consistency_gloo(refine):
     assert res == {0: True, 1: True}
 
 
+def _gloo_feec_worker(rank, world, port, refine, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = dcp.HostMesh(refine=refine, feec=True)
+        ok = True
+        mine = {}
+        for fld in ("w", "u", "p", "T"):
+            info = dcp.feec_partition_info(m, rank, world, fld)
+            mine[fld] = {"send": {k: v.tolist() for k, v in info["send"].items()},
+                         "recv": {k: v.tolist() for k, v in info["recv"].items()}}
+            mine["sizes"] = [info["nwo"], info["nuo"], info["n_owned_cells"], info["nTo"]]
+        allinfo = [None] * world
+        dist.all_gather_object(allinfo, mine)
+        for fld in ("w", "u", "p", "T"):
+            for s, ids in mine[fld]["send"].items():
+                ok &= allinfo[s][fld]["recv"].get(rank, []) == ids
+            for s, ids in mine[fld]["recv"].items():
+                ok &= allinfo[s][fld]["send"].get(rank, []) == ids
+        tot = [sum(a["sizes"][k] for a in allinfo) for k in range(4)]
+        f = m.feec
+        ok &= tot == [f.n_w, f.n_u, f.n_cells, m.n_T]
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_feec_partition_halo_consistency_gloo():
+    """FEEC (config 4) partition across two gloo processes: every halo send
+    list of edges, faces, cells and vertices matches the peer's receive list;
+    ownership covers every dof once."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_feec_worker, args=(r, world, 29631, 2, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
 @pytest.mark.parametrize("world", [3, 8])
 def test_partition_covers_and_matches(world):
     m = dcp.HostMesh(refine=3)
