@@ -8,6 +8,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dcp.h"
@@ -505,6 +506,107 @@ std::vector<int32_t> rcm_order(int n, const std::vector<int32_t>& ptr,
 // than 2^16 and are stored as 16-bit offsets from a per-slice base (10 instead
 // of 12 bytes per entry); the inner Schur GMRES then runs in that order.
 // pmap: CSR entry -> SELL position (k_schur_form writes through it).
+// Radially separable Q2 geometry (the hypershell of SphericalManifold: node
+// (a,b,c) of every cell sits at r_c * phi_ab, local c radial). Then
+//   X = R(zeta) Phi(xi, eta),  J = [R Phi_xi | R Phi_eta | R' Phi],
+//   J^-1 rows = m0 / R, m1 / R, m2 / R',  det J = R^2 R' D2,
+// with m0 = Phi_eta x Phi / D2, m1 = Phi x Phi_xi / D2, m2 = Phi_xi x Phi_eta / D2,
+// D2 = (Phi_xi x Phi_eta) . Phi at the 9 tangential Gauss points: one table per
+// column of cells, three radii per cell. Returns false (general on-the-fly
+// geometry) unless every cell fits within 1e-13 relative.
+bool separable_geometry(int n_cells, const std::vector<int32_t>& q2, const std::vector<double>& xyz,
+                        std::vector<int32_t>& col, std::vector<double>& colgeo,
+                        std::vector<double>& rad) {
+  auto l2 = [](int i, double x) {
+    return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+  };
+  auto dl2 = [](int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; };
+  constexpr double tol = 1e-13;
+  col.assign(n_cells, -1);
+  rad.assign(3 * size_t(n_cells), 0.0);
+  colgeo.clear();
+  std::vector<std::vector<double>> col_phi;  // [col][27] phi_ab of the column
+  struct Key {
+    int64_t k[3];
+    bool operator==(const Key& o) const { return k[0] == o.k[0] && k[1] == o.k[1] && k[2] == o.k[2]; }
+  };
+  struct KeyHash {
+    size_t operator()(const Key& a) const {
+      return size_t(a.k[0] * 73856093) ^ size_t(a.k[1] * 19349663) ^ size_t(a.k[2] * 83492791);
+    }
+  };
+  std::unordered_map<Key, int, KeyHash> cols;
+  for (int cell = 0; cell < n_cells; ++cell) {
+    double phi[9][3], r[3];
+    for (int c = 0; c < 3; ++c) {
+      double rc = 0;
+      for (int ab = 0; ab < 9; ++ab) {
+        const double* X = &xyz[3 * size_t(q2[27 * size_t(cell) + ab + 9 * c])];
+        const double rr = std::sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+        if (ab == 0) rc = rr;
+        if (!(std::fabs(rr - rc) <= tol * rc)) return false;
+        for (int d = 0; d < 3; ++d) {
+          if (c == 0) phi[ab][d] = X[d] / rr;
+          else if (!(std::fabs(X[d] / rr - phi[ab][d]) <= tol)) return false;
+        }
+      }
+      r[c] = rc;
+    }
+    if (!(r[0] < r[1] && r[1] < r[2])) return false;
+    for (int c = 0; c < 3; ++c) rad[3 * size_t(cell) + c] = r[c];
+    Key key{{std::llround(phi[4][0] * 1e9), std::llround(phi[4][1] * 1e9), std::llround(phi[4][2] * 1e9)}};
+    auto it = cols.find(key);
+    if (it == cols.end()) {
+      const int id = int(col_phi.size());
+      cols.emplace(key, id);
+      col_phi.emplace_back(&phi[0][0], &phi[0][0] + 27);
+      col[cell] = id;
+    } else {
+      const auto& ph = col_phi[it->second];
+      for (int i = 0; i < 27; ++i)
+        if (!(std::fabs(ph[i] - (&phi[0][0])[i]) <= tol)) return false;
+      col[cell] = it->second;
+    }
+  }
+  colgeo.assign(col_phi.size() * 90, 0.0);
+  for (size_t k = 0; k < col_phi.size(); ++k) {
+    const double* ph = col_phi[k].data();
+    for (int q1 = 0; q1 < 3; ++q1)
+      for (int q0 = 0; q0 < 3; ++q0) {
+        double F[3] = {0, 0, 0}, Fx[3] = {0, 0, 0}, Fy[3] = {0, 0, 0};
+        for (int b = 0; b < 3; ++b)
+          for (int a = 0; a < 3; ++a) {
+            const double la = l2(a, kGaussX[q0]), lb = l2(b, kGaussX[q1]);
+            const double da = dl2(a, kGaussX[q0]), db = dl2(b, kGaussX[q1]);
+            for (int d = 0; d < 3; ++d) {
+              const double v = ph[3 * (a + 3 * b) + d];
+              F[d] += la * lb * v;
+              Fx[d] += da * lb * v;
+              Fy[d] += la * db * v;
+            }
+          }
+        auto cross = [](const double* u, const double* v, double* w) {
+          w[0] = u[1] * v[2] - u[2] * v[1];
+          w[1] = u[2] * v[0] - u[0] * v[2];
+          w[2] = u[0] * v[1] - u[1] * v[0];
+        };
+        double m0[3], m1[3], m2[3];
+        cross(Fy, F, m0);
+        cross(F, Fx, m1);
+        cross(Fx, Fy, m2);
+        const double D2 = m2[0] * F[0] + m2[1] * F[1] + m2[2] * F[2];
+        double* g = &colgeo[90 * k + 10 * (q0 + 3 * q1)];
+        for (int d = 0; d < 3; ++d) {
+          g[d] = m0[d] / D2;
+          g[3 + d] = m1[d] / D2;
+          g[6 + d] = m2[d] / D2;
+        }
+        g[9] = D2;
+      }
+  }
+  return true;
+}
+
 void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_t>& Sc,
                 bool permute) {
   const int rows = c.npo;
@@ -747,7 +849,8 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       return DCP_OK;
     }
     if (option == DCP_OPT_MATRIX_FREE) {
-      ctx->matrix_free = value != 0;
+      require(value >= 0 && value <= 2, DCP_ERR_INVALID, "DCP_OPT_MATRIX_FREE must be 0, 1 or 2");
+      ctx->matrix_free = value;
       return DCP_OK;
     }
     if (option == DCP_OPT_FEEC_ZERO_MEAN) {
@@ -922,6 +1025,60 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_ncon = int(cdof.size());
       c.mf_geo.alloc(size_t(n_cells) * 270);
       mf_geometry(c.cd(), c.color_cells.p, c.mf_geo.p, c.stream);
+      // cell-order path: constrained-node masks, per-dof incidence lists into
+      // the cell records (ascending cell order = the gather's summation order)
+      std::vector<uint32_t> cmask(n_cells, 0);
+      std::vector<int32_t> vptr(nv + 1, 0), pptr(n_p + 1, 0);
+      for (int cell = 0; cell < n_cells; ++cell) {
+        for (int t = 0; t < 27; ++t) {
+          const int n = q2[27 * size_t(cell) + t];
+          vptr[n + 1]++;
+          if (vc[n].type != 0) cmask[cell] |= 1u << t;
+        }
+        for (int v = 0; v < 8; ++v) pptr[pd[8 * size_t(cell) + v] + 1]++;
+      }
+      for (int n = 0; n < nv; ++n) vptr[n + 1] += vptr[n];
+      for (int i = 0; i < n_p; ++i) pptr[i + 1] += pptr[i];
+      require(int64_t(n_cells) * 89 < (int64_t(1) << 31), DCP_ERR_UNSUPPORTED,
+              "mesh too large for 32-bit incidence slots");
+      const int32_t pbase = 3 * vptr[nv];
+      std::vector<int32_t> vslot(27 * size_t(n_cells)), pslot(8 * size_t(n_cells));
+      {
+        std::vector<int32_t> vf(vptr.begin(), vptr.end() - 1), pf(pptr.begin(), pptr.end() - 1);
+        for (int cell = 0; cell < n_cells; ++cell) {
+          for (int t = 0; t < 27; ++t)
+            vslot[27 * size_t(cell) + t] = 3 * vf[q2[27 * size_t(cell) + t]]++;
+          for (int v = 0; v < 8; ++v)
+            pslot[8 * size_t(cell) + v] = pbase + pf[pd[8 * size_t(cell) + v]]++;
+        }
+      }
+      std::vector<int32_t> cidx(nv, -1);
+      std::vector<int64_t> cblk;
+      for (int n = 0; n < nv; ++n) {
+        if (vc[n].type == 0) continue;
+        const auto* b = std::lower_bound(Ac.data() + Ap[n], Ac.data() + Ap[n + 1], n);
+        cidx[n] = int32_t(cblk.size());
+        cblk.push_back(b - Ac.data());
+      }
+      c.mf_cmask.upload(cmask);
+      c.mf_vptr.upload(vptr);
+      c.mf_vslot.upload(vslot);
+      c.mf_pbase = pbase;
+      c.mf_pptr.upload(pptr);
+      c.mf_pslot.upload(pslot);
+      c.mf_cidx.upload(cidx);
+      c.mf_cblk.upload(cblk);
+      c.mf_buf.alloc(size_t(pbase) + size_t(pptr[n_p]));
+      {
+        std::vector<int32_t> col;
+        std::vector<double> colgeo, rad;
+        c.mf_separable = separable_geometry(n_cells, q2, xyz, col, colgeo, rad);
+        if (c.mf_separable) {
+          c.mf_col.upload(col);
+          c.mf_colgeo.upload(colgeo);
+          c.mf_rad.upload(rad);
+        }
+      }
     }
     const size_t nn = size_t(n_u + n_p);
     c.nse_sol.alloc(nn);
@@ -1235,6 +1392,17 @@ int dcp_nse_vmult(dcp_ctx* ctx, const double* src, double* dst) {
     need_ready(*ctx);
     require(ctx->nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
     nse_vmult(*ctx, src, dst);
+    DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_velocity_vmult(dcp_ctx* ctx, const double* src, double* dst) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(ctx->nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
+    require(!ctx->feec, DCP_ERR_UNSUPPORTED, "classic Q2/Q1 system only");
+    velocity_vmult(*ctx, src, dst);
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     return DCP_OK;
   });

@@ -111,13 +111,33 @@ struct Ctx {
   bool schur_explicit = true;
   // matrix-free operator (kernels/matfree.hip): geometry, first-touch bits,
   // constrained velocity dofs with their assembled diagonal entries
-  bool matrix_free = true;
+  // 0: assembled block-CSR; 1 (default): cell-order pencil kernel + node
+  // gather (MfCells / MfGather); 2: colour-class launches (MfData)
+  int matrix_free = 1;
   DBuf<double> mf_geo;                  // colour order (see MfData)
   DBuf<int32_t> mf_q2, mf_p;
   DBuf<uint64_t> mf_first;
   DBuf<int32_t> mf_cdof;
   DBuf<int64_t> mf_cpos;
   int mf_ncon = 0;
+  DBuf<double> mf_buf;                  // dof-sorted incidence slots (89 per cell)
+  DBuf<uint32_t> mf_cmask;
+  DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx;
+  int32_t mf_pbase = 0;
+  DBuf<int64_t> mf_cblk;
+  DBuf<int32_t> mf_col;
+  DBuf<double> mf_colgeo, mf_rad;
+  bool mf_separable = false;
+  MfCells mfc() const {
+    return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
+                   xyz.p,      vcon.p,      mf_cmask.p, mf_vslot.p,
+                   mf_pslot.p, mf_separable ? mf_col.p : nullptr,
+                   mf_colgeo.p, mf_rad.p};
+  }
+  MfGather mfg() const {
+    return MfGather{n_vnodes, n_p,       n_u,       mf_vptr.p, mf_pptr.p, mf_pbase,
+                    mf_cidx.p, mf_cblk.p, vcon.p,    A_val.p};
+  }
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};
   }
@@ -211,6 +231,7 @@ struct Ctx {
 int solve_nse(Ctx& c, int* outer, int* inner);
 int solve_temperature(Ctx& c, int* iters, double* T_range);
 void nse_vmult(Ctx& c, const double* src, double* dst);
+void velocity_vmult(Ctx& c, const double* src, double* dst);
 void schur_vmult(Ctx& c, const double* src_p, double* dst_p);
 int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_solve_A,
                                int* inner);

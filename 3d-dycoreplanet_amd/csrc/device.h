@@ -90,6 +90,53 @@ struct MfData {
                                // pressure vertex v -> bit 32 + v
 };
 void mf_geometry(const CellData& cd, const int32_t* order, double* geo, hipStream_t s);
+
+// Cell-order matrix-free apply (two launches, no colouring):
+//   k_mf_pencil: every cell (tree order) evaluates K_cell C x with its geometry
+//     recomputed from the Q2 node coordinates and stores its 27 velocity
+//     triples and 8 pressure values to their slots in the dof-sorted
+//     incidence list (slot of (cell, t) = rank of the cell among the cells of
+//     node t, ascending cell order);
+//   k_mf_gather: every dof sums its contiguous run of slots in that order
+//     (deterministic), applies C^T and the constrained diagonal.
+// Workgroup b runs on XCD b % 8 (round-robin dispatch). This bijection gives
+// each XCD one contiguous range of logical blocks, so neighbouring cells (which
+// share nodes) meet in the same L2.
+__device__ inline int xcd_block(int b, int G) {
+  const int q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
+  return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+struct MfCells {
+  int n_cells;
+  int n_u;                     // offset of the pressure block in [u | p]
+  const int32_t* cell_q2;      // [n_cells][27] (tree order)
+  const int32_t* cell_p;       // [n_cells][8]
+  const double* xyz;           // [n_vnodes][3]
+  const NodeConstraint* vcon;  // [n_vnodes]
+  const uint32_t* cmask;       // [n_cells] bit t: local node t is constrained
+  const int32_t* vslot;        // [n_cells][27] buf offset (doubles) of the (cell, t) triple
+  const int32_t* pslot;        // [n_cells][8]  buf offset of the (cell, v) pressure value
+  // Radially separable geometry (null if the mesh is not): X(a,b,c) = r_c phi_ab
+  // in every cell, so J^-1 / JxW at a Gauss point follow from a per-column 2D
+  // table and the cell's three node-layer radii (see mf_separable_geometry).
+  const int32_t* col;          // [n_cells] column of the cell
+  const double* colgeo;        // [n_cols][9 points q0 + 3 q1][m0 m1 m2 D2] (10)
+  const double* rad;           // [n_cells][3] radii of the node layers c = 0, 1, 2
+};
+struct MfGather {
+  int n_vnodes, n_p, n_u;
+  const int32_t* vptr;         // [n_vnodes + 1] slot ranges: triples buf[3 k .. 3 k + 2]
+  const int32_t* pptr;         // [n_p + 1] slot ranges: buf[pbase + k]
+  int32_t pbase;               // 3 * vptr[n_vnodes]
+  const int32_t* cidx;         // [n_vnodes] index into cblk or -1
+  const int64_t* cblk;         // diagonal block of A for each constrained node
+  const NodeConstraint* vcon;
+  const double* A_val;
+};
+void mf_cells(const MfCells& mc, double nu, bool stokes, const double* src, double* buf,
+              hipStream_t s);
+void mf_gather(const MfGather& mg, bool stokes, const double* buf, const double* src,
+               double* dst, hipStream_t s);
 // one colour class = positions [base, base + n): dst (+)= C^T K C src
 void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);

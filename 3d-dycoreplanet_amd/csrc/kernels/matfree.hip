@@ -380,6 +380,552 @@ __global__ __launch_bounds__(32 * kMfCells) void k_mf_stokes(MfData md, int base
   }
 }
 
+// ---- cell-order pencil kernel -----------------------------------------------
+//
+// Nine lanes per cell, seven cells per wave (lane 63 works a dummy slot). Each
+// lane owns a "pencil" of three nodes / points along one axis, so every 1D
+// contraction of the sum factorisation runs in registers with compile-time
+// coefficients; the LDS only transposes between the x-, y- and z-pencil
+// layouts (x-pencil p = b + 3c, y-pencil p = a + 3c, z-pencil p = a + 3b over
+// lexicographic (a, b, c)). The geometry (J^-1, JxW at the 27 Gauss points)
+// is recomputed from the Q2 node coordinates the same way (MappingQ2 = the
+// assembly kernel's map), so the only per-cell HBM streams are the node map
+// and the 89 results; node coordinates and src are gathered and shared by the
+// neighbouring cells through the caches (cells in tree order).
+constexpr int kPenCells = 7;
+#ifndef DCP_MF_WAVES
+#define DCP_MF_WAVES 1
+#endif
+constexpr int kPenWaves = DCP_MF_WAVES;  // waves per workgroup
+#ifndef DCP_MF_SLOTS
+#define DCP_MF_SLOTS 7
+#endif
+// LDS cell slots per wave: 7 (lane 63, the dummy cell, stores nothing) or 8
+constexpr int kPenSlots = DCP_MF_SLOTS;
+// LDS: 9 fields of 27 doubles per cell slot, field-major ([field][slot][27]):
+// fewer bank conflicts for the three pencil patterns than cell-major slots;
+// then per slot the 8 vertex pressures and the 18 pressure-test partials.
+#ifndef DCP_MF_FIELD_MAJOR
+#define DCP_MF_FIELD_MAJOR 1
+#endif
+constexpr int kFS = DCP_MF_FIELD_MAJOR ? kPenSlots * 27 : 27;   // field stride (doubles)
+constexpr int kPenFields = 9 * kPenSlots * 27;           // per wave
+constexpr int kPenAux = 8 + 18 + 1;                      // per slot
+#ifndef DCP_MF_BATCHES
+#define DCP_MF_BATCHES 1
+#endif
+constexpr int kMfBatches = DCP_MF_BATCHES;  // cell batches per workgroup (pipelined)
+__host__ __device__ constexpr int kMfBatchTotal(int n_cells) {
+  return (n_cells + kPenCells * kPenWaves - 1) / (kPenCells * kPenWaves);
+}
+
+struct Tab3 {
+  double v[3][3];
+};
+constexpr Tab3 make_tab(bool deriv) {
+  Tab3 t{};
+  for (int n = 0; n < 3; ++n)
+    for (int q = 0; q < 3; ++q) t.v[n][q] = deriv ? dl2c(n, kGaussX[q]) : l2c(n, kGaussX[q]);
+  return t;
+}
+constexpr Tab3 kTL = make_tab(false);  // [node][point] value
+constexpr Tab3 kTD = make_tab(true);   // [node][point] derivative
+
+// out[q] = sum_n T[n][q] in[n]
+__device__ inline void fwd(const Tab3& T, const double in[3], double out[3]) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out[q] = T.v[0][q] * in[0] + T.v[1][q] * in[1] + T.v[2][q] * in[2];
+}
+// out[n] = sum_q T[n][q] in[q]
+__device__ inline void bwd(const Tab3& T, const double in[3], double out[3]) {
+#pragma unroll
+  for (int n = 0; n < 3; ++n) out[n] = T.v[n][0] * in[0] + T.v[n][1] * in[1] + T.v[n][2] * in[2];
+}
+
+#ifndef DCP_MF_WAVES_PER_EU
+#define DCP_MF_WAVES_PER_EU 2
+#endif
+template <bool STOKES, bool SEP>
+__global__ __launch_bounds__(64 * kPenWaves, DCP_MF_WAVES_PER_EU)
+void k_mf_pencil(MfCells mc, double nu,
+                                                             const double* __restrict__ src,
+                                                             double* __restrict__ buf) {
+  __shared__ double lds[kPenWaves][kPenFields];
+  __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // lane 63 shadows lane 54 (slot 6, pencil 0) with 7 LDS slots: it computes
+  // and stores the same LDS values and skips the global store; with 8 slots it
+  // works a dummy slot of its own
+  const bool dummy = lane == 63;
+#ifndef DCP_MF_SHADOW
+#define DCP_MF_SHADOW (kPenSlots == 7)
+#endif
+  const int cs = DCP_MF_SHADOW && dummy ? 6 : lane / 9;
+  const int p = DCP_MF_SHADOW && dummy ? 0 : lane - 9 * cs;
+  const int pa = p % 3, pb = p / 3;
+#ifndef DCP_MF_XCD
+#define DCP_MF_XCD 1
+#endif
+  const int blk = DCP_MF_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x);
+  double* S = lds[wave] + (DCP_MF_FIELD_MAJOR ? 27 * cs : 243 * cs);
+  double* P = aux[wave][cs];
+  double* SP = P + 8;
+  // LDS reads through a volatile view: keeps them single ds_read_b64 (256 B/clk)
+  // instead of merged ds_read2_b64 pairs (128 B/clk on gfx950)
+#ifndef DCP_MF_VOLATILE_READS
+#define DCP_MF_VOLATILE_READS 1
+#endif
+#if DCP_MF_VOLATILE_READS
+  typedef __attribute__((address_space(3))) const volatile double lds_vdouble;
+  lds_vdouble* SR = (lds_vdouble*)S;
+#else
+  const double* SR = S;
+#endif
+  const int yb = pa + 9 * pb;  // y-pencil (a = pa, c = pb): idx = yb + 3b
+  const double wab = sel3(pa, kGaussW[0], kGaussW[1], kGaussW[2]) *
+                     sel3(pb, kGaussW[0], kGaussW[1], kGaussW[2]);
+
+  // Software pipeline over the workgroup's kMfBatches batches of cells: the
+  // node ids of batch j + 2 and the node data of batch j + 1 are in flight
+  // while batch j computes.
+  auto cell_of = [&](int j) { return ((blk * kMfBatches + j) * kPenWaves + wave) * kPenCells + cs; };
+  struct Ids {
+    int nd[3], slot[3];
+    int pdof, pslot;
+    uint32_t mask;
+  };
+  struct Nodes {
+    double U[3][3], X[3][3];
+    double pv;
+  };
+  auto load_ids = [&](int j, Ids& I) {
+    const int cell = cell_of(j);
+    const size_t e = (cs < kPenCells && cell < mc.n_cells) ? size_t(cell) : 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      I.nd[a] = mc.cell_q2[27 * e + 3 * p + a];
+      I.slot[a] = mc.vslot[27 * e + 3 * p + a];
+    }
+    I.mask = mc.cmask[e];
+    I.pdof = (STOKES && p < 8) ? mc.cell_p[8 * e + p] : 0;
+    I.pslot = (STOKES && p < 8) ? mc.pslot[8 * e + p] : 0;
+  };
+  auto load_nodes = [&](const Ids& I, Nodes& N) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        if (!SEP) N.X[a][d] = mc.xyz[3 * size_t(I.nd[a]) + d];
+        N.U[a][d] = src[3 * size_t(I.nd[a]) + d];
+      }
+    N.pv = (STOKES && p < 8) ? src[mc.n_u + I.pdof] : 0.0;
+  };
+#ifndef DCP_MF_PREFETCH_NODES
+#define DCP_MF_PREFETCH_NODES 1
+#endif
+  Ids Ic, In;
+  Nodes Nc;
+  load_ids(0, Ic);
+  if (DCP_MF_PREFETCH_NODES) load_nodes(Ic, Nc);
+  if (kMfBatches > 1) load_ids(1, In);
+  for (int j = 0; j < kMfBatches; ++j) {
+  if (blk * kMfBatches + j >= kMfBatchTotal(mc.n_cells)) break;  // uniform per workgroup
+  Nodes Nn;
+  Ids Inn;
+  if (!DCP_MF_PREFETCH_NODES) load_nodes(Ic, Nc);
+  if (DCP_MF_PREFETCH_NODES && j + 1 < kMfBatches) load_nodes(In, Nn);
+  if (j + 2 < kMfBatches) load_ids(j + 2, Inn);
+  const int cell = cell_of(j);
+  const bool live = !dummy && cell < mc.n_cells;
+  // loads index the cell (the shadow lane must see exactly its twin's data)
+  const size_t e = (cs < kPenCells && cell < mc.n_cells) ? size_t(cell) : 0;
+  const int* nd = Ic.nd;
+  const uint32_t mask = Ic.mask;
+  double(&X)[3][3] = Nc.X;
+  double(&U)[3][3] = Nc.U;
+  const int colc = SEP ? mc.col[e] : 0;
+  if (STOKES && p < 8) P[p] = Nc.pv;
+  if (mask) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      if ((mask >> (3 * p + a)) & 1) {
+        const NodeConstraint nc = mc.vcon[nd[a]];
+        double f[3];
+        expand(nc, U[a], f);
+        U[a][0] = f[0];
+        U[a][1] = f[1];
+        U[a][2] = f[2];
+      }
+  }
+
+  // ---- geometry: J^-1 and JxW at the z-pencil's three points
+  double Ji[3][9], w[3];
+  if (!SEP) {
+    // general MappingQ2: J = dX/dxi by the same sum factorisation
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {  // x: value and d/dxi0 along the x-pencil
+    const double in[3] = {X[0][d], X[1][d], X[2][d]};
+    double v[3], g[3];
+    fwd(kTL, in, v);
+    fwd(kTD, in, g);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      S[d * kFS + 3 * p + q] = v[q];
+      S[(3 + d) * kFS + 3 * p + q] = g[q];
+    }
+  }
+  wsync();
+  {
+    double A[3][3], B[3][3], C[3][3];  // [d][q1]
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {  // y
+      double v[3], g[3];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        v[b] = SR[d * kFS + yb + 3 * b];
+        g[b] = SR[(3 + d) * kFS + yb + 3 * b];
+      }
+      fwd(kTL, v, A[d]);
+      fwd(kTD, v, B[d]);
+      fwd(kTL, g, C[d]);
+    }
+    wsync();
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        S[d * kFS + yb + 3 * q] = A[d][q];
+        S[(3 + d) * kFS + yb + 3 * q] = B[d][q];
+        S[(6 + d) * kFS + yb + 3 * q] = C[d][q];
+      }
+  }
+  wsync();
+  {
+    double J[3][3][3];  // [q2][d][e]
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {  // z
+      double A[3], B[3], C[3], t[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        A[k] = SR[d * kFS + p + 9 * k];
+        B[k] = SR[(3 + d) * kFS + p + 9 * k];
+        C[k] = SR[(6 + d) * kFS + p + 9 * k];
+      }
+      fwd(kTL, C, t);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) J[q][d][0] = t[q];
+      fwd(kTL, B, t);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) J[q][d][1] = t[q];
+      fwd(kTD, A, t);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) J[q][d][2] = t[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double(*M)[3] = J[q];
+      const double c00 = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+      const double c01 = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+      const double c02 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+      const double det = M[0][0] * c00 + M[0][1] * c01 + M[0][2] * c02;
+      const double id = 1.0 / det;
+      Ji[q][0] = c00 * id;
+      Ji[q][1] = (M[0][2] * M[2][1] - M[0][1] * M[2][2]) * id;
+      Ji[q][2] = (M[0][1] * M[1][2] - M[0][2] * M[1][1]) * id;
+      Ji[q][3] = c01 * id;
+      Ji[q][4] = (M[0][0] * M[2][2] - M[0][2] * M[2][0]) * id;
+      Ji[q][5] = (M[0][2] * M[1][0] - M[0][0] * M[1][2]) * id;
+      Ji[q][6] = c02 * id;
+      Ji[q][7] = (M[0][1] * M[2][0] - M[0][0] * M[2][1]) * id;
+      Ji[q][8] = (M[0][0] * M[1][1] - M[0][1] * M[1][0]) * id;
+      w[q] = det * (wab * kGaussW[q]);
+    }
+  }
+  wsync();
+
+  }
+  // ---- velocity: values and reference gradients
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {  // x
+    const double in[3] = {U[0][c], U[1][c], U[2][c]};
+    double v[3], g[3];
+    fwd(kTL, in, v);
+    fwd(kTD, in, g);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      S[c * kFS + 3 * p + q] = v[q];
+      S[(3 + c) * kFS + 3 * p + q] = g[q];
+    }
+  }
+  wsync();
+  {
+    double A[3][3], B[3][3], C[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {  // y: A = value, B = d/dxi1, C = d/dxi0
+      double v[3], g[3];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        v[b] = SR[c * kFS + yb + 3 * b];
+        g[b] = SR[(3 + c) * kFS + yb + 3 * b];
+      }
+      fwd(kTL, v, A[c]);
+      fwd(kTD, v, B[c]);
+      fwd(kTL, g, C[c]);
+    }
+    wsync();
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        S[c * kFS + yb + 3 * q] = A[c][q];
+        S[(3 + c) * kFS + yb + 3 * q] = B[c][q];
+        S[(6 + c) * kFS + yb + 3 * q] = C[c][q];
+      }
+  }
+  wsync();
+
+  // separable geometry: the z-pencil's 2D table entry and the cell's radii
+  // (small, L2-resident tables)
+  double m[10], rr[3];
+  if (SEP) {
+    const double* cg = mc.colgeo + 90 * size_t(colc) + 10 * p;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) m[i] = cg[i];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rr[c] = mc.rad[3 * e + c];
+  }
+  // ---- z-pencil: per point flux, accumulated straight into the back z pass
+  double Plo = 0.0, Phi = 0.0;
+  if (STOKES) {
+    const double xa = sel3(pa, kGaussX[0], kGaussX[1], kGaussX[2]);
+    const double xb = sel3(pb, kGaussX[0], kGaussX[1], kGaussX[2]);
+    Plo = (1.0 - xb) * ((1.0 - xa) * P[0] + xa * P[1]) + xb * ((1.0 - xa) * P[2] + xa * P[3]);
+    Phi = (1.0 - xb) * ((1.0 - xa) * P[4] + xa * P[5]) + xb * ((1.0 - xa) * P[6] + xa * P[7]);
+  }
+  double V[3][3], FX[3][3], FY[3][3];  // [c][node along z]
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) V[c][k] = FX[c][k] = FY[c][k] = 0.0;
+  double slo = 0.0, shi = 0.0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    double u[3], Gh[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double A[3], B[3], C[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        A[k] = SR[c * kFS + p + 9 * k];
+        B[k] = SR[(3 + c) * kFS + p + 9 * k];
+        C[k] = SR[(6 + c) * kFS + p + 9 * k];
+      }
+      u[c] = kTL.v[0][q] * A[0] + kTL.v[1][q] * A[1] + kTL.v[2][q] * A[2];
+      Gh[c][0] = kTL.v[0][q] * C[0] + kTL.v[1][q] * C[1] + kTL.v[2][q] * C[2];
+      Gh[c][1] = kTL.v[0][q] * B[0] + kTL.v[1][q] * B[1] + kTL.v[2][q] * B[2];
+      Gh[c][2] = kTD.v[0][q] * A[0] + kTD.v[1][q] * A[1] + kTD.v[2][q] * A[2];
+    }
+    double ji[9], wq;
+    if (SEP) {  // rows m0 / R, m1 / R, m2 / R'; JxW = R^2 R' D2 w
+      const double R = kTL.v[0][q] * rr[0] + kTL.v[1][q] * rr[1] + kTL.v[2][q] * rr[2];
+      const double Rp = kTD.v[0][q] * rr[0] + kTD.v[1][q] * rr[1] + kTD.v[2][q] * rr[2];
+      const double iR = 1.0 / R, iRp = 1.0 / Rp;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        ji[d] = m[d] * iR;
+        ji[3 + d] = m[3 + d] * iR;
+        ji[6 + d] = m[6 + d] * iRp;
+      }
+      wq = R * R * Rp * m[9] * (wab * kGaussW[q]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ji[i] = Ji[q][i];
+      wq = w[q];
+    }
+    double G[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+        G[c][d] = Gh[c][0] * ji[d] + Gh[c][1] * ji[3 + d] + Gh[c][2] * ji[6 + d];
+    double F[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) F[c][d] = nu * (G[c][d] + G[d][c]);
+    if (STOKES) {
+      const double pq = (1.0 - kGaussX[q]) * Plo + kGaussX[q] * Phi;
+      F[0][0] -= pq;
+      F[1][1] -= pq;
+      F[2][2] -= pq;
+      const double sq = -wq * (G[0][0] + G[1][1] + G[2][2]);
+      slo += (1.0 - kGaussX[q]) * sq;
+      shi += kGaussX[q] * sq;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double r0 = wq * (ji[0] * F[c][0] + ji[1] * F[c][1] + ji[2] * F[c][2]);
+      const double r1 = wq * (ji[3] * F[c][0] + ji[4] * F[c][1] + ji[5] * F[c][2]);
+      const double r2 = wq * (ji[6] * F[c][0] + ji[7] * F[c][1] + ji[8] * F[c][2]);
+      const double wu = wq * u[c];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        V[c][k] += kTL.v[k][q] * wu + kTD.v[k][q] * r2;
+        FX[c][k] += kTL.v[k][q] * r0;
+        FY[c][k] += kTL.v[k][q] * r1;
+      }
+    }
+  }
+  wsync();
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      S[c * kFS + p + 9 * k] = V[c][k];
+      S[(3 + c) * kFS + p + 9 * k] = FX[c][k];
+      S[(6 + c) * kFS + p + 9 * k] = FY[c][k];
+    }
+  if (STOKES) {
+    SP[p] = slo;
+    SP[9 + p] = shi;
+  }
+  wsync();
+
+  // ---- back y (y-pencil), the pressure test functions
+  double yp = 0.0;
+  {
+    double V1[3][3], FX1[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double v[3], fx[3], fy[3], t[3];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        v[b] = SR[c * kFS + yb + 3 * b];
+        fx[b] = SR[(3 + c) * kFS + yb + 3 * b];
+        fy[b] = SR[(6 + c) * kFS + yb + 3 * b];
+      }
+      bwd(kTL, v, V1[c]);
+      bwd(kTD, fy, t);
+#pragma unroll
+      for (int n = 0; n < 3; ++n) V1[c][n] += t[n];
+      bwd(kTL, fx, FX1[c]);
+    }
+    if (STOKES && p < 8) {
+      const int v0 = p & 1, v1 = (p >> 1) & 1, v2 = p >> 2;
+      const double* s = SP + 9 * v2;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const double pb1 = v1 ? kGaussX[b] : 1.0 - kGaussX[b];
+        double r = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) r += (v0 ? kGaussX[a] : 1.0 - kGaussX[a]) * s[a + 3 * b];
+        yp += pb1 * r;
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) {
+        S[c * kFS + yb + 3 * n] = V1[c][n];
+        S[(3 + c) * kFS + yb + 3 * n] = FX1[c][n];
+      }
+  }
+  wsync();
+
+  // ---- back x (x-pencil) and the cell record
+  double y[3][3];  // [node a][c]
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double v[3], fx[3], t0[3], t1[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      v[q] = SR[c * kFS + 3 * p + q];
+      fx[q] = SR[(3 + c) * kFS + 3 * p + q];
+    }
+    bwd(kTL, v, t0);
+    bwd(kTD, fx, t1);
+#pragma unroll
+    for (int n = 0; n < 3; ++n) y[n][c] = t0[n] + t1[n];
+  }
+  if (live) {
+#pragma unroll
+    for (int n = 0; n < 3; ++n) {
+      double* out = buf + Ic.slot[n];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) out[c] = y[n][c];
+    }
+    if (STOKES && p < 8) buf[Ic.pslot] = yp;
+  }
+  wsync();  // the next batch overwrites the slab this one just read
+  Ic = In;
+  In = Inn;
+  if (DCP_MF_PREFETCH_NODES) Nc = Nn;
+  }
+}
+
+#ifndef DCP_MF_GATHER_BATCH
+#define DCP_MF_GATHER_BATCH 8
+#endif
+constexpr int kGatherBatch = DCP_MF_GATHER_BATCH;
+
+// Every dof sums the records of its cells in cell order, then C^T and the
+// constrained diagonal: dst = C^T (sum_cells K C src) + D_c src.
+template <bool STOKES>
+__global__ __launch_bounds__(256) void k_mf_gather(MfGather g, const double* __restrict__ buf,
+                                                   const double* __restrict__ src,
+                                                   double* __restrict__ dst) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < g.n_vnodes) {
+    double s[3] = {0.0, 0.0, 0.0};
+    const int k0 = g.vptr[i], k1 = g.vptr[i + 1];
+    // the node's contiguous run of triples, up to kGatherBatch loads in flight
+    for (int k = k0; k < k1; k += kGatherBatch) {
+      double r[kGatherBatch][3];
+#pragma unroll
+      for (int u = 0; u < kGatherBatch; ++u)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) r[u][c] = k + u < k1 ? buf[3 * size_t(k + u) + c] : 0.0;
+#pragma unroll
+      for (int u = 0; u < kGatherBatch; ++u)
+        if (k + u < k1) {
+          s[0] += r[u][0];
+          s[1] += r[u][1];
+          s[2] += r[u][2];
+        }
+    }
+    const int ci = g.cidx[i];
+    if (ci >= 0) {
+      const NodeConstraint nc = g.vcon[i];
+      condense(nc, s);
+      const double* dg = g.A_val + 9 * g.cblk[ci];
+#pragma unroll
+      for (int comp = 0; comp < 3; ++comp)
+        if (nc.type == 1 || comp == nc.k) s[comp] = dg[4 * comp] * src[3 * size_t(i) + comp];
+    }
+    double* d = dst + 3 * size_t(i);
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+  } else if (STOKES) {
+    const int j = i - g.n_vnodes;
+    if (j < g.n_p) {
+      double s = 0.0;
+      const int k0 = g.pptr[j], k1 = g.pptr[j + 1];
+      const double* pb = buf + g.pbase;
+      for (int k = k0; k < k1; k += kGatherBatch) {
+        double r[kGatherBatch];
+#pragma unroll
+        for (int u = 0; u < kGatherBatch; ++u) r[u] = k + u < k1 ? pb[k + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kGatherBatch; ++u)
+          if (k + u < k1) s += r[u];
+      }
+      dst[g.n_u + j] = s;
+    }
+  }
+}
+
 // constrained velocity dofs: dst = (assembled diagonal) * src
 __global__ void k_mf_constrained(int n, const int32_t* __restrict__ dof,
                                  const int64_t* __restrict__ diag_pos,
@@ -408,6 +954,31 @@ void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
   else
     hipLaunchKernelGGL(k_mf_stokes<false>, grid, dim3(32 * kMfCells), 0, s, md, base, n, nu, src,
                        dst);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_cells(const MfCells& mc, double nu, bool stokes, const double* src, double* buf,
+              hipStream_t s) {
+  if (mc.n_cells <= 0) return;
+  const dim3 grid((kMfBatchTotal(mc.n_cells) + kMfBatches - 1) / kMfBatches);
+#ifndef DCP_MF_SEP
+#define DCP_MF_SEP 1
+#endif
+  const bool sep = DCP_MF_SEP && mc.col != nullptr;
+  auto k = stokes ? (sep ? k_mf_pencil<true, true> : k_mf_pencil<true, false>)
+                  : (sep ? k_mf_pencil<false, true> : k_mf_pencil<false, false>);
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, nu, src, buf);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_gather(const MfGather& mg, bool stokes, const double* buf, const double* src,
+               double* dst, hipStream_t s) {
+  const int n = mg.n_vnodes + (stokes ? mg.n_p : 0);
+  if (n <= 0) return;
+  if (stokes)
+    hipLaunchKernelGGL(k_mf_gather<true>, dim3((n + 255) / 256), dim3(256), 0, s, mg, buf, src, dst);
+  else
+    hipLaunchKernelGGL(k_mf_gather<false>, dim3((n + 255) / 256), dim3(256), 0, s, mg, buf, src, dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -471,10 +471,15 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
   if (c.time_schur && c.mf_ev_used[v] < Ctx::kMfEvents) e = &c.mf_ev[v][c.mf_ev_used[v]++];
   if (c.time_schur) c.mf_calls[v]++;
   if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-  for (int k = 0; k < c.n_colors(); ++k)
-    mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.ph.nu_sys, stokes, src, dst,
-                    c.stream);
-  mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.A_val.p, src, dst, c.stream);
+  if (c.matrix_free == 1) {
+    mf_cells(c.mfc(), c.ph.nu_sys, stokes, src, c.mf_buf.p, c.stream);
+    mf_gather(c.mfg(), stokes, c.mf_buf.p, src, dst, c.stream);
+  } else {
+    for (int k = 0; k < c.n_colors(); ++k)
+      mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.ph.nu_sys, stokes, src, dst,
+                      c.stream);
+    mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.A_val.p, src, dst, c.stream);
+  }
   if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
 }
 
@@ -615,6 +620,8 @@ void halo_exchange(Ctx& c, Ctx::Halo& h, double* v) {
   c.comm->exchange(np, h.peers.data(), sb.data(), h.sn.data(), rb.data(), h.rn.data(), c.stream);
   scatter(h.nr, h.rpos.p, h.rbuf.p, v, c.stream);
 }
+
+void velocity_vmult(Ctx& c, const double* src, double* dst) { a_vmult(c, src, dst); }
 
 void nse_vmult(Ctx& c, const double* src, double* dst) {
   // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)

@@ -36,7 +36,7 @@ EXPORTED = [
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
     "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
-    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult",
+    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult",
     "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
@@ -155,6 +155,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_max_velocity.argtypes = [P, D]
     lib.dcp_cfl_number.argtypes = [P, D]
     lib.dcp_nse_vmult.argtypes = [P, P, P]
+    lib.dcp_velocity_vmult.argtypes = [P, P, P]
     lib.dcp_schur_vmult.argtypes = [P, P, P]
     lib.dcp_block_preconditioner_vmult.argtypes = [P, P, P, I, C.POINTER(I)]
     lib.dcp_nse_matrix_export.argtypes = [P, C.POINTER(C.c_int64), P, P, P]
@@ -467,10 +468,12 @@ class Context:
         False: B^T, Jacobi, B as SchurComplement::vmult does."""
         self._check(lib().dcp_set_option(self._h, OPT_SCHUR_EXPLICIT, int(bool(on))))
 
-    def set_matrix_free(self, on: bool):
-        """True (default): solver products with nse_matrix / its A block are
-        evaluated matrix-free; False: block-CSR SpMV of the assembled matrix."""
-        self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(bool(on))))
+    def set_matrix_free(self, mode):
+        """True / 1 (default): solver products with nse_matrix / its A block are
+        evaluated matrix-free (cell-order kernel + dof gather); 2: matrix-free
+        in colour-class launches; False / 0: block-CSR SpMV of the assembled
+        matrix."""
+        self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(mode)))
 
     def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
         self._feec_view = None
@@ -642,6 +645,13 @@ class Context:
     def nse_vmult(self, src):
         n = self.mesh.n_u + self.mesh.n_p
         rc, out = self._dev_roundtrip(lambda s, d: lib().dcp_nse_vmult(self._h, s, d), src, n)
+        self._check(rc)
+        return out
+
+    def velocity_vmult(self, src_u):
+        """nse_matrix.block(0,0) * src_u (the do_solve_A GMRES operator)."""
+        rc, out = self._dev_roundtrip(lambda s, d: lib().dcp_velocity_vmult(self._h, s, d), src_u,
+                                      self.mesh.n_u)
         self._check(rc)
         return out
 

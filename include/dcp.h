@@ -186,6 +186,9 @@ int dcp_advance_state(dcp_ctx* ctx);
 
 /* Operators on device vectors (LinearAlgebra vmult seam) ----------------- */
 int dcp_nse_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst);          /* nse_matrix */
+/* nse_matrix.block(0,0) on a velocity vector: the A products of the do_solve_A
+ * GMRES (block_schur_preconditioner.hpp:59-67). */
+int dcp_velocity_vmult(dcp_ctx* ctx, const double* d_src_u, double* d_dst_u);
 int dcp_schur_vmult(dcp_ctx* ctx, const double* d_src_p, double* d_dst_p);    /* schur_complement.hpp:143-150 */
 /* BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70). */
 int dcp_block_preconditioner_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst,

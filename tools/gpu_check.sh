@@ -14,7 +14,7 @@ R=${R:-5}
 for s in $STEPS; do
   case $s in
     pytest)
-      timeout -k 10 600 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1; ok $? pytest ;;
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; ok $? pytest ;;
     bench)
       timeout -k 10 600 python bench.py --refine $R --steps ${K:-2} --warmup ${W:-1} > $OUT/bench.json 2> $OUT/bench.err; ok $? bench ;;
     profile)

@@ -16,7 +16,8 @@ import dcp  # noqa: E402
 R = int(os.environ.get("R", "5"))
 m = dcp.HostMesh(refine=R)
 hip = C.CDLL("libamdhip64.so")
-libs = sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/var/libdcp_*.so")))
+libs = sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__),
+                                   "build/var/libdcp_%s.so" % os.environ.get("VAR", "*"))))
 for path in libs or [dcp.LIB_PATH]:
     dcp._lib = dcp.load_library(path)
     ctx = dcp.Context(device=0)
@@ -28,7 +29,7 @@ for path in libs or [dcp.LIB_PATH]:
     n = m.n_u + m.n_p
     x = np.random.default_rng(1).uniform(-1, 1, n)
     res = {}
-    for mf in (True, False):
+    for mf in (1, 2, 0):
         ctx.set_matrix_free(mf)
         with dcp.DeviceBuffer(n) as ds, dcp.DeviceBuffer(n) as dd:
             ds.upload(x)
@@ -44,8 +45,10 @@ for path in libs or [dcp.LIB_PATH]:
                 hip.hipDeviceSynchronize()
                 ts.append((time.perf_counter() - t0) / 20 * 1e3)
             y = dd.download()
-        res["mf" if mf else "assembled"] = (float(np.median(ts)), y)
-    d = np.max(np.abs(res["mf"][1] - res["assembled"][1])) / np.max(np.abs(res["assembled"][1]))
-    print(json.dumps({"variant": os.path.basename(path), "mf_ms": res["mf"][0],
-                      "assembled_ms": res["assembled"][0], "rel_diff": float(d)}), flush=True)
+        res[{1: "mf", 2: "mf_colour", 0: "assembled"}[mf]] = (float(np.median(ts)), y)
+    ya = res["assembled"][1]
+    d = {k: float(np.max(np.abs(v[1] - ya)) / np.max(np.abs(ya))) for k, v in res.items()}
+    print(json.dumps({"variant": os.path.basename(path), "R": R,
+                      **{k + "_ms": v[0] for k, v in res.items()},
+                      "rel_diff": d}), flush=True)
     ctx.close()

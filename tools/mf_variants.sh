@@ -1,0 +1,21 @@
+# rocprofv3 kernel stats of the matrix-free apply, one run per variant library
+# (build/var/libdcp_<name>.so from tools/variant_probe.sh SRC=matfree).
+set -u
+OUT=$GRAFT_REPO_ROOT/gpurun_out/mfvar
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+for v in ${VARS}; do
+  rm -rf /tmp/pv
+  VAR=$v R=${R:-5} timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pv -o run \
+    -- python3 $GRAFT_REPO_ROOT/tools/mf_probe.py > $OUT/$v.log 2>&1 || exit $?
+  find /tmp/pv -name "*kernel_stats.csv" -exec cp {} $OUT/$v.csv \;
+done
+python3 - <<'PY'
+import csv, glob, os
+out = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/mfvar"
+for f in sorted(glob.glob(out + "/*.csv")):
+    rows = {r["Name"]: r for r in csv.DictReader(open(f))}
+    sel = {k.split("(")[0].split("::")[-1][:24]: float(r["AverageNs"]) / 1e3 for k, r in rows.items()
+           if "k_mf_pencil<true>" in k or "k_mf_gather<true>" in k or "k_mf_pencil<false>" in k or "k_mf_gather<false>" in k}
+    print(os.path.basename(f)[:-4], {k: round(v, 1) for k, v in sel.items()})
+PY
