@@ -1074,9 +1074,38 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         std::vector<double> colgeo, rad;
         c.mf_separable = separable_geometry(n_cells, q2, xyz, col, colgeo, rad);
         if (c.mf_separable) {
+          // radial layers (cells with the same three node radii): per Gauss
+          // point 1/R, 1/R' and R^2 R' of R(zeta) = sum_c L_c(zeta) r_c
+          std::vector<int32_t> layer(n_cells);
+          std::vector<double> laygeo;
+          std::unordered_map<int64_t, int> ids;
+          auto l2 = [](int i, double x) {
+            return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
+          };
+          auto dl2 = [](int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; };
+          for (int cell = 0; cell < n_cells; ++cell) {
+            const double* r = &rad[3 * size_t(cell)];
+            const int64_t key = std::llround(r[0] * 1e12) * 1000003 + std::llround(r[2] * 1e12);
+            auto it = ids.find(key);
+            if (it == ids.end()) {
+              it = ids.emplace(key, int(laygeo.size() / 9)).first;
+              for (int q = 0; q < 3; ++q) {
+                double R = 0, Rp = 0;
+                for (int k = 0; k < 3; ++k) {
+                  R += l2(k, kGaussX[q]) * r[k];
+                  Rp += dl2(k, kGaussX[q]) * r[k];
+                }
+                laygeo.push_back(1.0 / R);
+                laygeo.push_back(1.0 / Rp);
+                laygeo.push_back(R * R * Rp);
+              }
+            }
+            layer[cell] = it->second;
+          }
           c.mf_col.upload(col);
           c.mf_colgeo.upload(colgeo);
-          c.mf_rad.upload(rad);
+          c.mf_layer.upload(layer);
+          c.mf_laygeo.upload(laygeo);
         }
       }
     }

@@ -125,14 +125,14 @@ struct Ctx {
   DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx;
   int32_t mf_pbase = 0;
   DBuf<int64_t> mf_cblk;
-  DBuf<int32_t> mf_col;
-  DBuf<double> mf_colgeo, mf_rad;
+  DBuf<int32_t> mf_col, mf_layer;
+  DBuf<double> mf_colgeo, mf_laygeo;
   bool mf_separable = false;
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
                    xyz.p,      vcon.p,      mf_cmask.p, mf_vslot.p,
                    mf_pslot.p, mf_separable ? mf_col.p : nullptr,
-                   mf_colgeo.p, mf_rad.p};
+                   mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
   MfGather mfg() const {
     return MfGather{n_vnodes, n_p,       n_u,       mf_vptr.p, mf_pptr.p, mf_pbase,

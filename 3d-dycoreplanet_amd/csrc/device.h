@@ -121,7 +121,8 @@ struct MfCells {
   // table and the cell's three node-layer radii (see mf_separable_geometry).
   const int32_t* col;          // [n_cells] column of the cell
   const double* colgeo;        // [n_cols][9 points q0 + 3 q1][m0 m1 m2 D2] (10)
-  const double* rad;           // [n_cells][3] radii of the node layers c = 0, 1, 2
+  const int32_t* layer;        // [n_cells] radial layer of the cell
+  const double* laygeo;        // [n_layers][3 points][1/R, 1/R', R^2 R']
 };
 struct MfGather {
   int n_vnodes, n_p, n_u;

@@ -544,6 +544,7 @@ void k_mf_pencil(MfCells mc, double nu,
   double(&X)[3][3] = Nc.X;
   double(&U)[3][3] = Nc.U;
   const int colc = SEP ? mc.col[e] : 0;
+  const int layc = SEP ? mc.layer[e] : 0;
   if (STOKES && p < 8) P[p] = Nc.pv;
   if (mask) {
 #pragma unroll
@@ -686,13 +687,14 @@ void k_mf_pencil(MfCells mc, double nu,
 
   // separable geometry: the z-pencil's 2D table entry and the cell's radii
   // (small, L2-resident tables)
-  double m[10], rr[3];
+  double m[10], lg[9];
   if (SEP) {
     const double* cg = mc.colgeo + 90 * size_t(colc) + 10 * p;
 #pragma unroll
     for (int i = 0; i < 10; ++i) m[i] = cg[i];
+    const double* lp = mc.laygeo + 9 * size_t(layc);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) rr[c] = mc.rad[3 * e + c];
+    for (int i = 0; i < 9; ++i) lg[i] = lp[i];
   }
   // ---- z-pencil: per point flux, accumulated straight into the back z pass
   double Plo = 0.0, Phi = 0.0;
@@ -727,16 +729,14 @@ void k_mf_pencil(MfCells mc, double nu,
     }
     double ji[9], wq;
     if (SEP) {  // rows m0 / R, m1 / R, m2 / R'; JxW = R^2 R' D2 w
-      const double R = kTL.v[0][q] * rr[0] + kTL.v[1][q] * rr[1] + kTL.v[2][q] * rr[2];
-      const double Rp = kTD.v[0][q] * rr[0] + kTD.v[1][q] * rr[1] + kTD.v[2][q] * rr[2];
-      const double iR = 1.0 / R, iRp = 1.0 / Rp;
+      const double iR = lg[3 * q], iRp = lg[3 * q + 1];
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
         ji[d] = m[d] * iR;
         ji[3 + d] = m[3 + d] * iR;
         ji[6 + d] = m[6 + d] * iRp;
       }
-      wq = R * R * Rp * m[9] * (wab * kGaussW[q]);
+      wq = lg[3 * q + 2] * m[9] * (wab * kGaussW[q]);
     } else {
 #pragma unroll
       for (int i = 0; i < 9; ++i) ji[i] = Ji[q][i];
@@ -864,35 +864,50 @@ void k_mf_pencil(MfCells mc, double nu,
   }
 }
 
-#ifndef DCP_MF_GATHER_BATCH
-#define DCP_MF_GATHER_BATCH 8
+// Every dof sums its contiguous run of slots in slot (= ascending cell) order,
+// then C^T and the constrained diagonal. One wave per 64 consecutive dofs: the
+// runs of those dofs form one contiguous span, which the wave loads
+// cooperatively (coalesced) into LDS; each lane then adds its own run.
+constexpr int kGatherWaves = 4;
+#ifndef DCP_MF_GSPAN
+#define DCP_MF_GSPAN 768
 #endif
-constexpr int kGatherBatch = DCP_MF_GATHER_BATCH;
-
-// Every dof sums the records of its cells in cell order, then C^T and the
-// constrained diagonal: dst = C^T (sum_cells K C src) + D_c src.
+constexpr int kGvSpan = DCP_MF_GSPAN;  // doubles per wave window (longer spans: direct reads)
 template <bool STOKES>
-__global__ __launch_bounds__(256) void k_mf_gather(MfGather g, const double* __restrict__ buf,
-                                                   const double* __restrict__ src,
-                                                   double* __restrict__ dst) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < g.n_vnodes) {
+__global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g,
+                                                                  const double* __restrict__ buf,
+                                                                  const double* __restrict__ src,
+                                                                  double* __restrict__ dst) {
+  __shared__ double win[kGatherWaves][kGvSpan];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = blockIdx.x * kGatherWaves + wave;
+  const int nvw = (g.n_vnodes + 63) >> 6;
+  double* W = win[wave];
+  if (w < nvw) {
+    const int n0 = 64 * w, n1 = min(n0 + 64, g.n_vnodes);
+    const int s0 = g.vptr[n0];
+    const int len = 3 * (g.vptr[n1] - s0);
+    const double* b = buf + 3 * size_t(s0);
+    const bool fits = len <= kGvSpan;
+    if (fits)
+      for (int i = lane; i < len; i += 64) W[i] = b[i];
+    wsync();
+    const int i = n0 + lane;
+    if (i >= n1) return;
+    const int k0 = g.vptr[i] - s0, k1 = g.vptr[i + 1] - s0;
     double s[3] = {0.0, 0.0, 0.0};
-    const int k0 = g.vptr[i], k1 = g.vptr[i + 1];
-    // the node's contiguous run of triples, up to kGatherBatch loads in flight
-    for (int k = k0; k < k1; k += kGatherBatch) {
-      double r[kGatherBatch][3];
-#pragma unroll
-      for (int u = 0; u < kGatherBatch; ++u)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) r[u][c] = k + u < k1 ? buf[3 * size_t(k + u) + c] : 0.0;
-#pragma unroll
-      for (int u = 0; u < kGatherBatch; ++u)
-        if (k + u < k1) {
-          s[0] += r[u][0];
-          s[1] += r[u][1];
-          s[2] += r[u][2];
-        }
+    if (fits) {
+      for (int k = k0; k < k1; ++k) {
+        s[0] += W[3 * k];
+        s[1] += W[3 * k + 1];
+        s[2] += W[3 * k + 2];
+      }
+    } else {
+      for (int k = k0; k < k1; ++k) {
+        s[0] += b[3 * k];
+        s[1] += b[3 * k + 1];
+        s[2] += b[3 * k + 2];
+      }
     }
     const int ci = g.cidx[i];
     if (ci >= 0) {
@@ -908,21 +923,25 @@ __global__ __launch_bounds__(256) void k_mf_gather(MfGather g, const double* __r
     d[1] = s[1];
     d[2] = s[2];
   } else if (STOKES) {
-    const int j = i - g.n_vnodes;
-    if (j < g.n_p) {
-      double s = 0.0;
-      const int k0 = g.pptr[j], k1 = g.pptr[j + 1];
-      const double* pb = buf + g.pbase;
-      for (int k = k0; k < k1; k += kGatherBatch) {
-        double r[kGatherBatch];
-#pragma unroll
-        for (int u = 0; u < kGatherBatch; ++u) r[u] = k + u < k1 ? pb[k + u] : 0.0;
-#pragma unroll
-        for (int u = 0; u < kGatherBatch; ++u)
-          if (k + u < k1) s += r[u];
-      }
-      dst[g.n_u + j] = s;
-    }
+    const int j0 = 64 * (w - nvw);
+    if (j0 >= g.n_p) return;
+    const int j1 = min(j0 + 64, g.n_p);
+    const int s0 = g.pptr[j0];
+    const int len = g.pptr[j1] - s0;
+    const double* b = buf + g.pbase + s0;
+    const bool fits = len <= kGvSpan;
+    if (fits)
+      for (int i = lane; i < len; i += 64) W[i] = b[i];
+    wsync();
+    const int j = j0 + lane;
+    if (j >= j1) return;
+    const int k0 = g.pptr[j] - s0, k1 = g.pptr[j + 1] - s0;
+    double s = 0.0;
+    if (fits)
+      for (int k = k0; k < k1; ++k) s += W[k];
+    else
+      for (int k = k0; k < k1; ++k) s += b[k];
+    dst[g.n_u + j] = s;
   }
 }
 
@@ -973,12 +992,13 @@ void mf_cells(const MfCells& mc, double nu, bool stokes, const double* src, doub
 
 void mf_gather(const MfGather& mg, bool stokes, const double* buf, const double* src,
                double* dst, hipStream_t s) {
-  const int n = mg.n_vnodes + (stokes ? mg.n_p : 0);
-  if (n <= 0) return;
+  const int waves = (mg.n_vnodes + 63) / 64 + (stokes ? (mg.n_p + 63) / 64 : 0);
+  if (waves <= 0) return;
+  const dim3 grid((waves + kGatherWaves - 1) / kGatherWaves), block(64 * kGatherWaves);
   if (stokes)
-    hipLaunchKernelGGL(k_mf_gather<true>, dim3((n + 255) / 256), dim3(256), 0, s, mg, buf, src, dst);
+    hipLaunchKernelGGL(k_mf_gather<true>, grid, block, 0, s, mg, buf, src, dst);
   else
-    hipLaunchKernelGGL(k_mf_gather<false>, dim3((n + 255) / 256), dim3(256), 0, s, mg, buf, src, dst);
+    hipLaunchKernelGGL(k_mf_gather<false>, grid, block, 0, s, mg, buf, src, dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
