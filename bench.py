@@ -32,6 +32,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
 PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_sell16_r5.json", "k_sell_spmv<true, true>")}
+# the same for the matrix-free Stokes apply (pencil kernel + dof gather)
+PMC_MF = {5: ("profiles/r01_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
+
+
+def pmc_mf_traffic(refine):
+    """HBM bytes of one matrix-free Stokes apply (both launches) from the
+    committed PMC summary, or None."""
+    ent = PMC_MF.get(refine)
+    if ent is None or not os.path.exists(os.path.join(ROOT, ent[0])):
+        return None
+    with open(os.path.join(ROOT, ent[0])) as f:
+        tb = json.load(f)["traffic_bytes"]
+    parts = [sum(v for k, v in tb.items() if key in k) for key in ent[1]]
+    return sum(parts) if all(parts) else None
 
 
 def pmc_traffic(refine, mode):
@@ -353,8 +367,10 @@ def main():
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
-    # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point;
-    # one apply = one launch per cell colour + the constrained-dof fix-up
+    # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point
+    # (SURVEY's unit of work; the kernel recomputes the geometry instead of
+    # streaming it, so "traffic" - the PMC bytes actually moved - is lower);
+    # one apply = the cell-order pencil kernel + the dof gather
     st_ms = np.mean([r[4]["stokes_apply_ms_avg"] for r in recs])
     ve_ms = np.mean([r[4]["velocity_apply_ms_avg"] for r in recs])
     if st_ms > 0 or ve_ms > 0:
@@ -363,8 +379,10 @@ def main():
         ve_bytes = 16 * m.n_u + 4 * 27 * nc + 80 * 27 * nc
         if world > 1:
             st_bytes, ve_bytes = st_bytes / world, ve_bytes / world
-        mf = {"kernel": "matrix-free [A B^T; B 0] x (k_mf_stokes<true>, one launch per colour)",
+        mf = {"kernel": "matrix-free [A B^T; B 0] x (k_mf_pencil<true> cell-order sum "
+                        "factorisation + k_mf_gather dof gather)",
               "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "traffic": pmc_mf_traffic(args.refine) if world == 1 else None,
               "bytes_per_apply": st_bytes, "avg_apply_ms": st_ms,
               "applies_per_step": recs[-1][4]["stokes_applies"],
               "achieved": st_bytes / (st_ms * 1e-3) / 1e9 if st_ms > 0 else None,
