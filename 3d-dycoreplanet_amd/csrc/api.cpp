@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -36,6 +37,10 @@ Ctx::~Ctx() {
   for (auto& t : schur_ev) t.destroy();
   for (auto& v : mf_ev)
     for (auto& t : v) t.destroy();
+  for (auto& ev : mf_chunk_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (mf_join_ev) (void)hipEventDestroy(mf_join_ev);
+  if (mf_stream) (void)hipStreamDestroy(mf_stream);
   if (stream) (void)hipStreamDestroy(stream);
 }
 }  // namespace dcp
@@ -1039,18 +1044,65 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       }
       for (int n = 0; n < nv; ++n) vptr[n + 1] += vptr[n];
       for (int i = 0; i < n_p; ++i) pptr[i + 1] += pptr[i];
+      // chunks of the cell range; a dof is gathered after the chunk of its last cell
+      if (const char* e = std::getenv("DCP_MF_CHUNKS"))
+        c.mf_chunks = std::max(1, std::min(Ctx::kMfChunksMax, std::atoi(e)));
+      const int K = c.mf_chunks;
+      c.mf_cell_cut.assign(K + 1, 0);
+      for (int k = 0; k <= K; ++k) c.mf_cell_cut[k] = int(int64_t(n_cells) * k / K);
+      std::vector<int> vlast(nv, 0), plast(n_p, 0);
+      for (int k = 0; k < K; ++k)
+        for (int cell = c.mf_cell_cut[k]; cell < c.mf_cell_cut[k + 1]; ++cell) {
+          for (int t = 0; t < 27; ++t) vlast[q2[27 * size_t(cell) + t]] = k;
+          for (int v = 0; v < 8; ++v) plast[pd[8 * size_t(cell) + v]] = k;
+        }
+      // gather order: by last chunk, then id (stable counting sort)
+      auto order_of = [&](const std::vector<int>& last, std::vector<int32_t>& order,
+                          std::vector<int>& cut) {
+        cut.assign(K + 1, 0);
+        for (int l : last) cut[l + 1]++;
+        for (int k = 0; k < K; ++k) cut[k + 1] += cut[k];
+        order.assign(last.size(), 0);
+        std::vector<int> f(cut.begin(), cut.end() - 1);
+        for (size_t i = 0; i < last.size(); ++i) order[f[last[i]]++] = int32_t(i);
+      };
+      std::vector<int32_t> vorder, porder;
+      order_of(vlast, vorder, c.mf_vcut);
+      order_of(plast, porder, c.mf_pcut);
+      // slot ranges per gather position
+      std::vector<int32_t> vptr_o(nv + 1, 0), pptr_o(n_p + 1, 0), vpos(nv), ppos(n_p);
+      for (int i = 0; i < nv; ++i) {
+        vpos[vorder[i]] = i;
+        vptr_o[i + 1] = vptr_o[i] + (vptr[vorder[i] + 1] - vptr[vorder[i]]);
+      }
+      for (int i = 0; i < n_p; ++i) {
+        ppos[porder[i]] = i;
+        pptr_o[i + 1] = pptr_o[i] + (pptr[porder[i] + 1] - pptr[porder[i]]);
+      }
+      vptr.swap(vptr_o);
+      pptr.swap(pptr_o);
       require(int64_t(n_cells) * 89 < (int64_t(1) << 31), DCP_ERR_UNSUPPORTED,
               "mesh too large for 32-bit incidence slots");
       const int32_t pbase = 3 * vptr[nv];
       std::vector<int32_t> vslot(27 * size_t(n_cells)), pslot(8 * size_t(n_cells));
       {
-        std::vector<int32_t> vf(vptr.begin(), vptr.end() - 1), pf(pptr.begin(), pptr.end() - 1);
+        std::vector<int32_t> vf(nv), pf(n_p);
+        for (int n = 0; n < nv; ++n) vf[n] = vptr[vpos[n]];
+        for (int i = 0; i < n_p; ++i) pf[i] = pptr[ppos[i]];
         for (int cell = 0; cell < n_cells; ++cell) {
           for (int t = 0; t < 27; ++t)
             vslot[27 * size_t(cell) + t] = 3 * vf[q2[27 * size_t(cell) + t]]++;
           for (int v = 0; v < 8; ++v)
             pslot[8 * size_t(cell) + v] = pbase + pf[pd[8 * size_t(cell) + v]]++;
         }
+      }
+      c.mf_vorder.upload(vorder);
+      c.mf_porder.upload(porder);
+      if (!c.mf_stream) {
+        DCP_HIP_CHECK(hipStreamCreateWithFlags(&c.mf_stream, hipStreamNonBlocking));
+        for (auto& ev : c.mf_chunk_ev)
+          DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        DCP_HIP_CHECK(hipEventCreateWithFlags(&c.mf_join_ev, hipEventDisableTiming));
       }
       std::vector<int32_t> cidx(nv, -1);
       std::vector<int64_t> cblk;

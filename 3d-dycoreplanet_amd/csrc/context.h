@@ -122,8 +122,18 @@ struct Ctx {
   int mf_ncon = 0;
   DBuf<double> mf_buf;                  // dof-sorted incidence slots (89 per cell)
   DBuf<uint32_t> mf_cmask;
-  DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx;
+  DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx, mf_vorder, mf_porder;
   int32_t mf_pbase = 0;
+  // chunked apply (DCP_MF_CHUNKS > 1 at upload): the gather of chunk k's
+  // finished dofs runs on mf_stream while the pencil kernel works chunk k + 1.
+  // Measured slower at r=5 (the pencil launch fills every CU's LDS, so the
+  // gather cannot co-reside; each extra launch + event pair costs ~5 us):
+  // default 1 = both launches on the context stream.
+  static constexpr int kMfChunksMax = 16;
+  int mf_chunks = 1;
+  std::vector<int> mf_cell_cut, mf_vcut, mf_pcut;  // [mf_chunks + 1] each
+  hipStream_t mf_stream = nullptr;
+  hipEvent_t mf_chunk_ev[kMfChunksMax] = {}, mf_join_ev = nullptr;
   DBuf<int64_t> mf_cblk;
   DBuf<int32_t> mf_col, mf_layer;
   DBuf<double> mf_colgeo, mf_laygeo;
@@ -135,8 +145,8 @@ struct Ctx {
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
   MfGather mfg() const {
-    return MfGather{n_vnodes, n_p,       n_u,       mf_vptr.p, mf_pptr.p, mf_pbase,
-                    mf_cidx.p, mf_cblk.p, vcon.p,    A_val.p};
+    return MfGather{n_vnodes,    n_p,       n_u,       mf_vorder.p, mf_porder.p, mf_vptr.p,
+                    mf_pptr.p,   mf_pbase,  mf_cidx.p, mf_cblk.p,   vcon.p,      A_val.p};
   }
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};

@@ -126,18 +126,23 @@ struct MfCells {
 };
 struct MfGather {
   int n_vnodes, n_p, n_u;
-  const int32_t* vptr;         // [n_vnodes + 1] slot ranges: triples buf[3 k .. 3 k + 2]
-  const int32_t* pptr;         // [n_p + 1] slot ranges: buf[pbase + k]
+  // dofs in gather order (by the chunk of their last cell, then id): position
+  // i is velocity node vorder[i] / pressure dof porder[i]
+  const int32_t* vorder;
+  const int32_t* porder;
+  const int32_t* vptr;         // [n_vnodes + 1] slot ranges per position: triples buf[3 k .. 3 k + 2]
+  const int32_t* pptr;         // [n_p + 1] slot ranges per position: buf[pbase + k]
   int32_t pbase;               // 3 * vptr[n_vnodes]
   const int32_t* cidx;         // [n_vnodes] index into cblk or -1
   const int64_t* cblk;         // diagonal block of A for each constrained node
   const NodeConstraint* vcon;
   const double* A_val;
 };
-void mf_cells(const MfCells& mc, double nu, bool stokes, const double* src, double* buf,
-              hipStream_t s);
-void mf_gather(const MfGather& mg, bool stokes, const double* buf, const double* src,
-               double* dst, hipStream_t s);
+// cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
+void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
+              double* buf, hipStream_t s);
+void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, const double* buf,
+               const double* src, double* dst, hipStream_t s);
 // one colour class = positions [base, base + n): dst (+)= C^T K C src
 void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);

@@ -371,7 +371,12 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
                                                             PhysicsDev ph, NseOut out) {
   __shared__ NseSmem sh;
   const int tid = threadIdx.x;
-  const int cell = MODE == 0 ? cells[blockIdx.x] : first + blockIdx.x;
+#ifndef DCP_ASM_XCD
+#define DCP_ASM_XCD 0
+#endif
+  // DCP_ASM_XCD: each XCD takes one contiguous (tree-ordered) run of the colour class
+  const int cell = MODE == 0 ? cells[DCP_ASM_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x)]
+                             : first + blockIdx.x;
   const bool want_matrix = MODE == 1 || out.A != nullptr;
   const bool want_rhs = MODE == 1 || out.rhs != nullptr;
 

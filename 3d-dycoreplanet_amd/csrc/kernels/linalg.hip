@@ -191,6 +191,12 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
 // entry columns (4 waves per slice keep enough loads in flight: one wave per
 // slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound), then
 // wave 0 adds the 4 quarters in order (fixed summation order).
+// DCP_SELL_UNROLL4: four column pairs per iteration (measured within 1 % of
+// two at r=5: the value stream already runs at ~5.8 TB/s)
+#ifndef DCP_SELL_UNROLL4
+#define DCP_SELL_UNROLL4 0
+#endif
+#define SELL_LD(p) (*(p))
 template <bool EPI, bool C16>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* __restrict__ x,
                                                       double cf, double* __restrict__ xs,
@@ -237,9 +243,29 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   if (C16) {
     const int cb = m.base[sl];
     const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * int64_t(k0) + lane;
+#if DCP_SELL_UNROLL4
+    for (; k + 4 <= k1; k += 4, cp += 256, vp += 256) {
+      // four column pairs: all value / column loads issued before the gathers
+      const ushort2 c0 = cp[0], c1 = cp[64], c2 = cp[128], c3 = cp[192];
+      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 64), a2 = SELL_LD(vp + 128),
+                    a3 = SELL_LD(vp + 192);
+      const double x0 = x[cb + c0.x] * cf, x1 = x[cb + c0.y] * cf;
+      const double x2 = x[cb + c1.x] * cf, x3 = x[cb + c1.y] * cf;
+      const double x4 = x[cb + c2.x] * cf, x5 = x[cb + c2.y] * cf;
+      const double x6 = x[cb + c3.x] * cf, x7 = x[cb + c3.y] * cf;
+      acc += a0.x * x0;
+      acc += a0.y * x1;
+      acc += a1.x * x2;
+      acc += a1.y * x3;
+      acc += a2.x * x4;
+      acc += a2.y * x5;
+      acc += a3.x * x6;
+      acc += a3.y * x7;
+    }
+#endif
     for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
       const ushort2 c0 = cp[0], c1 = cp[64];
-      const double2 a0 = vp[0], a1 = vp[64];
+      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 64);
       const double x0 = x[cb + c0.x] * cf, x1 = x[cb + c0.y] * cf;
       const double x2 = x[cb + c1.x] * cf, x3 = x[cb + c1.y] * cf;
       acc += a0.x * x0;

@@ -447,7 +447,7 @@ __device__ inline void bwd(const Tab3& T, const double in[3], double out[3]) {
 #endif
 template <bool STOKES, bool SEP>
 __global__ __launch_bounds__(64 * kPenWaves, DCP_MF_WAVES_PER_EU)
-void k_mf_pencil(MfCells mc, double nu,
+void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
                                                              const double* __restrict__ src,
                                                              double* __restrict__ buf) {
   __shared__ double lds[kPenWaves][kPenFields];
@@ -488,7 +488,9 @@ void k_mf_pencil(MfCells mc, double nu,
   // Software pipeline over the workgroup's kMfBatches batches of cells: the
   // node ids of batch j + 2 and the node data of batch j + 1 are in flight
   // while batch j computes.
-  auto cell_of = [&](int j) { return ((blk * kMfBatches + j) * kPenWaves + wave) * kPenCells + cs; };
+  auto cell_of = [&](int j) {
+    return c0 + ((blk * kMfBatches + j) * kPenWaves + wave) * kPenCells + cs;
+  };
   struct Ids {
     int nd[3], slot[3];
     int pdof, pslot;
@@ -500,7 +502,7 @@ void k_mf_pencil(MfCells mc, double nu,
   };
   auto load_ids = [&](int j, Ids& I) {
     const int cell = cell_of(j);
-    const size_t e = (cs < kPenCells && cell < mc.n_cells) ? size_t(cell) : 0;
+    const size_t e = (cs < kPenCells && cell < c1) ? size_t(cell) : 0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       I.nd[a] = mc.cell_q2[27 * e + 3 * p + a];
@@ -529,16 +531,16 @@ void k_mf_pencil(MfCells mc, double nu,
   if (DCP_MF_PREFETCH_NODES) load_nodes(Ic, Nc);
   if (kMfBatches > 1) load_ids(1, In);
   for (int j = 0; j < kMfBatches; ++j) {
-  if (blk * kMfBatches + j >= kMfBatchTotal(mc.n_cells)) break;  // uniform per workgroup
+  if (blk * kMfBatches + j >= kMfBatchTotal(c1 - c0)) break;  // uniform per workgroup
   Nodes Nn;
   Ids Inn;
   if (!DCP_MF_PREFETCH_NODES) load_nodes(Ic, Nc);
   if (DCP_MF_PREFETCH_NODES && j + 1 < kMfBatches) load_nodes(In, Nn);
   if (j + 2 < kMfBatches) load_ids(j + 2, Inn);
   const int cell = cell_of(j);
-  const bool live = !dummy && cell < mc.n_cells;
+  const bool live = !dummy && cell < c1;
   // loads index the cell (the shadow lane must see exactly its twin's data)
-  const size_t e = (cs < kPenCells && cell < mc.n_cells) ? size_t(cell) : 0;
+  const size_t e = (cs < kPenCells && cell < c1) ? size_t(cell) : 0;
   const int* nd = Ic.nd;
   const uint32_t mask = Ic.mask;
   double(&X)[3][3] = Nc.X;
@@ -874,17 +876,18 @@ constexpr int kGatherWaves = 4;
 #endif
 constexpr int kGvSpan = DCP_MF_GSPAN;  // doubles per wave window (longer spans: direct reads)
 template <bool STOKES>
-__global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g,
+__global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int v0, int v1,
+                                                                  int p0, int p1,
                                                                   const double* __restrict__ buf,
                                                                   const double* __restrict__ src,
                                                                   double* __restrict__ dst) {
   __shared__ double win[kGatherWaves][kGvSpan];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int w = blockIdx.x * kGatherWaves + wave;
-  const int nvw = (g.n_vnodes + 63) >> 6;
+  const int nvw = (v1 - v0 + 63) >> 6;
   double* W = win[wave];
   if (w < nvw) {
-    const int n0 = 64 * w, n1 = min(n0 + 64, g.n_vnodes);
+    const int n0 = v0 + 64 * w, n1 = min(n0 + 64, v1);  // gather positions
     const int s0 = g.vptr[n0];
     const int len = 3 * (g.vptr[n1] - s0);
     const double* b = buf + 3 * size_t(s0);
@@ -892,9 +895,10 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g,
     if (fits)
       for (int i = lane; i < len; i += 64) W[i] = b[i];
     wsync();
-    const int i = n0 + lane;
-    if (i >= n1) return;
-    const int k0 = g.vptr[i] - s0, k1 = g.vptr[i + 1] - s0;
+    const int pos = n0 + lane;
+    if (pos >= n1) return;
+    const int i = g.vorder[pos];
+    const int k0 = g.vptr[pos] - s0, k1 = g.vptr[pos + 1] - s0;
     double s[3] = {0.0, 0.0, 0.0};
     if (fits) {
       for (int k = k0; k < k1; ++k) {
@@ -923,9 +927,9 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g,
     d[1] = s[1];
     d[2] = s[2];
   } else if (STOKES) {
-    const int j0 = 64 * (w - nvw);
-    if (j0 >= g.n_p) return;
-    const int j1 = min(j0 + 64, g.n_p);
+    const int j0 = p0 + 64 * (w - nvw);
+    if (j0 >= p1) return;
+    const int j1 = min(j0 + 64, p1);
     const int s0 = g.pptr[j0];
     const int len = g.pptr[j1] - s0;
     const double* b = buf + g.pbase + s0;
@@ -933,9 +937,10 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g,
     if (fits)
       for (int i = lane; i < len; i += 64) W[i] = b[i];
     wsync();
-    const int j = j0 + lane;
-    if (j >= j1) return;
-    const int k0 = g.pptr[j] - s0, k1 = g.pptr[j + 1] - s0;
+    const int pos = j0 + lane;
+    if (pos >= j1) return;
+    const int j = g.porder[pos];
+    const int k0 = g.pptr[pos] - s0, k1 = g.pptr[pos + 1] - s0;
     double s = 0.0;
     if (fits)
       for (int k = k0; k < k1; ++k) s += W[k];
@@ -976,29 +981,29 @@ void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void mf_cells(const MfCells& mc, double nu, bool stokes, const double* src, double* buf,
-              hipStream_t s) {
-  if (mc.n_cells <= 0) return;
-  const dim3 grid((kMfBatchTotal(mc.n_cells) + kMfBatches - 1) / kMfBatches);
+void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
+              double* buf, hipStream_t s) {
+  if (c1 <= c0) return;
+  const dim3 grid((kMfBatchTotal(c1 - c0) + kMfBatches - 1) / kMfBatches);
 #ifndef DCP_MF_SEP
 #define DCP_MF_SEP 1
 #endif
   const bool sep = DCP_MF_SEP && mc.col != nullptr;
   auto k = stokes ? (sep ? k_mf_pencil<true, true> : k_mf_pencil<true, false>)
                   : (sep ? k_mf_pencil<false, true> : k_mf_pencil<false, false>);
-  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, nu, src, buf);
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, nu, src, buf);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void mf_gather(const MfGather& mg, bool stokes, const double* buf, const double* src,
-               double* dst, hipStream_t s) {
-  const int waves = (mg.n_vnodes + 63) / 64 + (stokes ? (mg.n_p + 63) / 64 : 0);
+void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, const double* buf,
+               const double* src, double* dst, hipStream_t s) {
+  const int waves = (v1 - v0 + 63) / 64 + (stokes ? (p1 - p0 + 63) / 64 : 0);
   if (waves <= 0) return;
   const dim3 grid((waves + kGatherWaves - 1) / kGatherWaves), block(64 * kGatherWaves);
   if (stokes)
-    hipLaunchKernelGGL(k_mf_gather<true>, grid, block, 0, s, mg, buf, src, dst);
+    hipLaunchKernelGGL(k_mf_gather<true>, grid, block, 0, s, mg, v0, v1, p0, p1, buf, src, dst);
   else
-    hipLaunchKernelGGL(k_mf_gather<false>, grid, block, 0, s, mg, buf, src, dst);
+    hipLaunchKernelGGL(k_mf_gather<false>, grid, block, 0, s, mg, v0, v1, p0, p1, buf, src, dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -17,6 +17,7 @@
 // fixed-order sum, so every rank takes the same decisions from bitwise equal
 // scalars. Every operator refreshes the ghost entries of its input first.
 #include <cmath>
+#include <cstdlib>
 #include <functional>
 #include <stdexcept>
 #include <vector>
@@ -472,8 +473,26 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
   if (c.time_schur) c.mf_calls[v]++;
   if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
   if (c.matrix_free == 1) {
-    mf_cells(c.mfc(), c.ph.nu_sys, stokes, src, c.mf_buf.p, c.stream);
-    mf_gather(c.mfg(), stokes, c.mf_buf.p, src, dst, c.stream);
+    // chunk k's pencil launch, then (on mf_stream) the gather of the dofs whose
+    // last cell is in chunk k, overlapping chunk k + 1's pencil launch
+    const MfCells mc = c.mfc();
+    const MfGather mg = c.mfg();
+    const bool one_stream = c.mf_chunks == 1;
+    hipStream_t gs = one_stream ? c.stream : c.mf_stream;
+    for (int k = 0; k < c.mf_chunks; ++k) {
+      mf_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.ph.nu_sys, stokes, src, c.mf_buf.p,
+               c.stream);
+      if (!one_stream) {
+        DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[k], c.stream));
+        DCP_HIP_CHECK(hipStreamWaitEvent(gs, c.mf_chunk_ev[k], 0));
+      }
+      mf_gather(mg, c.mf_vcut[k], c.mf_vcut[k + 1], c.mf_pcut[k], c.mf_pcut[k + 1], stokes,
+                c.mf_buf.p, src, dst, gs);
+    }
+    if (!one_stream) {
+      DCP_HIP_CHECK(hipEventRecord(c.mf_join_ev, gs));
+      DCP_HIP_CHECK(hipStreamWaitEvent(c.stream, c.mf_join_ev, 0));
+    }
   } else {
     for (int k = 0; k < c.n_colors(); ++k)
       mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.ph.nu_sys, stokes, src, dst,

@@ -16,7 +16,8 @@ import dcp  # noqa: E402
 R = int(os.environ.get("R", "5"))
 m = dcp.HostMesh(refine=R)
 hip = C.CDLL("libamdhip64.so")
-libs = sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/var/libdcp_*.so")))
+libs = sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__),
+                                   "build/var/libdcp_%s.so" % os.environ.get("VAR", "*"))))
 for path in libs or [dcp.LIB_PATH]:
     dcp._lib = dcp.load_library(path)
     ctx = dcp.Context(device=0)

@@ -1,5 +1,5 @@
-# rocprofv3 kernel stats of the matrix-free apply, one run per variant library
-# (build/var/libdcp_<name>.so from tools/variant_probe.sh SRC=matfree).
+# rocprofv3 kernel stats of a probe script (PROBE, default tools/mf_probe.py), one
+# run per variant library (build/var/libdcp_<name>.so from tools/variant_probe.sh).
 set -u
 OUT=$GRAFT_REPO_ROOT/gpurun_out/mfvar
 mkdir -p $OUT
@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp
 for v in ${VARS}; do
   rm -rf /tmp/pv
   VAR=$v R=${R:-5} timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pv -o run \
-    -- python3 $GRAFT_REPO_ROOT/tools/mf_probe.py > $OUT/$v.log 2>&1 || exit $?
+    -- python3 $GRAFT_REPO_ROOT/${PROBE:-tools/mf_probe.py} > $OUT/$v.log 2>&1 || exit $?
   find /tmp/pv -name "*kernel_stats.csv" -exec cp {} $OUT/$v.csv \;
 done
 python3 - <<'PY'
