@@ -519,9 +519,14 @@ std::vector<int32_t> rcm_order(int n, const std::vector<int32_t>& ptr,
 // D2 = (Phi_xi x Phi_eta) . Phi at the 9 tangential Gauss points: one table per
 // column of cells, three radii per cell. Returns false (general on-the-fly
 // geometry) unless every cell fits within 1e-13 relative.
-bool separable_geometry(int n_cells, const std::vector<int32_t>& q2, const std::vector<double>& xyz,
-                        std::vector<int32_t>& col, std::vector<double>& colgeo,
-                        std::vector<double>& rad) {
+// node(cell, t): the coordinates of lexicographic support point t of a cell.
+// Also groups the cells into radial layers (same three node radii) with, per
+// layer and Gauss point, 1/R, 1/R' and R^2 R' of R(zeta) = sum_c L_c(zeta) r_c.
+template <class NodeFn>
+bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
+                        std::vector<double>& colgeo, std::vector<int32_t>& layer,
+                        std::vector<double>& laygeo) {
+  std::vector<double> rad;
   auto l2 = [](int i, double x) {
     return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
   };
@@ -546,7 +551,7 @@ bool separable_geometry(int n_cells, const std::vector<int32_t>& q2, const std::
     for (int c = 0; c < 3; ++c) {
       double rc = 0;
       for (int ab = 0; ab < 9; ++ab) {
-        const double* X = &xyz[3 * size_t(q2[27 * size_t(cell) + ab + 9 * c])];
+        const double* X = node(cell, ab + 9 * c);
         const double rr = std::sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
         if (ab == 0) rc = rr;
         if (!(std::fabs(rr - rc) <= tol * rc)) return false;
@@ -608,6 +613,29 @@ bool separable_geometry(int n_cells, const std::vector<int32_t>& q2, const std::
         }
         g[9] = D2;
       }
+  }
+  // radial layers
+  layer.assign(n_cells, 0);
+  laygeo.clear();
+  std::unordered_map<int64_t, int> ids;
+  for (int cell = 0; cell < n_cells; ++cell) {
+    const double* r = &rad[3 * size_t(cell)];
+    const int64_t key = std::llround(r[0] * 1e12) * 1000003 + std::llround(r[2] * 1e12);
+    auto it = ids.find(key);
+    if (it == ids.end()) {
+      it = ids.emplace(key, int(laygeo.size() / 9)).first;
+      for (int q = 0; q < 3; ++q) {
+        double R = 0, Rp = 0;
+        for (int k = 0; k < 3; ++k) {
+          R += l2(k, kGaussX[q]) * r[k];
+          Rp += dl2(k, kGaussX[q]) * r[k];
+        }
+        laygeo.push_back(1.0 / R);
+        laygeo.push_back(1.0 / Rp);
+        laygeo.push_back(R * R * Rp);
+      }
+    }
+    layer[cell] = it->second;
   }
   return true;
 }
@@ -888,6 +916,22 @@ int dcp_mesh_check(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
   });
 }
 
+int dcp_mesh_geometry_info(int n_cells, const double* cell_geometry, int* separable,
+                           int* n_columns, int* n_layers) {
+  return guarded(nullptr, [&] {
+    require(n_cells > 0 && cell_geometry != nullptr, DCP_ERR_INVALID, "empty mesh");
+    std::vector<int32_t> col, layer;
+    std::vector<double> colgeo, laygeo;
+    const bool sep = separable_geometry(
+        n_cells, [&](int cell, int t) { return cell_geometry + 81 * size_t(cell) + 3 * t; }, col,
+        colgeo, layer, laygeo);
+    if (separable) *separable = sep ? 1 : 0;
+    if (n_columns) *n_columns = sep ? int(colgeo.size() / 90) : 0;
+    if (n_layers) *n_layers = sep ? int(laygeo.size() / 9) : 0;
+    return DCP_OK;
+  });
+}
+
 int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
                     const int32_t* cell_T_dofs, const double* cell_geometry,
                     const double* cell_diameter, int n_u, int n_p, int n_T,
@@ -1028,8 +1072,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_cdof.upload(cdof);
       c.mf_cpos.upload(cpos);
       c.mf_ncon = int(cdof.size());
-      c.mf_geo.alloc(size_t(n_cells) * 270);
-      mf_geometry(c.cd(), c.color_cells.p, c.mf_geo.p, c.stream);
+      c.mf_geo.release();  // colour-launch mode only: computed on its first use
       // cell-order path: constrained-node masks, per-dof incidence lists into
       // the cell records (ascending cell order = the gather's summation order)
       std::vector<uint32_t> cmask(n_cells, 0);
@@ -1122,38 +1165,12 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_cblk.upload(cblk);
       c.mf_buf.alloc(size_t(pbase) + size_t(pptr[n_p]));
       {
-        std::vector<int32_t> col;
-        std::vector<double> colgeo, rad;
-        c.mf_separable = separable_geometry(n_cells, q2, xyz, col, colgeo, rad);
+        std::vector<int32_t> col, layer;
+        std::vector<double> colgeo, laygeo;
+        c.mf_separable = separable_geometry(
+            n_cells, [&](int cell, int t) { return &xyz[3 * size_t(q2[27 * size_t(cell) + t])]; },
+            col, colgeo, layer, laygeo);
         if (c.mf_separable) {
-          // radial layers (cells with the same three node radii): per Gauss
-          // point 1/R, 1/R' and R^2 R' of R(zeta) = sum_c L_c(zeta) r_c
-          std::vector<int32_t> layer(n_cells);
-          std::vector<double> laygeo;
-          std::unordered_map<int64_t, int> ids;
-          auto l2 = [](int i, double x) {
-            return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
-          };
-          auto dl2 = [](int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; };
-          for (int cell = 0; cell < n_cells; ++cell) {
-            const double* r = &rad[3 * size_t(cell)];
-            const int64_t key = std::llround(r[0] * 1e12) * 1000003 + std::llround(r[2] * 1e12);
-            auto it = ids.find(key);
-            if (it == ids.end()) {
-              it = ids.emplace(key, int(laygeo.size() / 9)).first;
-              for (int q = 0; q < 3; ++q) {
-                double R = 0, Rp = 0;
-                for (int k = 0; k < 3; ++k) {
-                  R += l2(k, kGaussX[q]) * r[k];
-                  Rp += dl2(k, kGaussX[q]) * r[k];
-                }
-                laygeo.push_back(1.0 / R);
-                laygeo.push_back(1.0 / Rp);
-                laygeo.push_back(R * R * Rp);
-              }
-            }
-            layer[cell] = it->second;
-          }
           c.mf_col.upload(col);
           c.mf_colgeo.upload(colgeo);
           c.mf_layer.upload(layer);

@@ -466,6 +466,11 @@ struct NoConvergence {};
 // Matrix-free C^T K C over all (local) cells in colour order, then the
 // assembled diagonal on constrained velocity dofs (kernels/matfree.hip).
 void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
+  if (c.matrix_free == 2 && !c.mf_geo.p) {
+    // colour-launch mode: the streamed J^-1 / JxW table (2160 B per cell)
+    c.mf_geo.alloc(size_t(c.n_cells) * 270);
+    mf_geometry(c.cd(), c.color_cells.p, c.mf_geo.p, c.stream);
+  }
   const MfData md = c.mfd();
   const int v = stokes ? 0 : 1;
   Timer* e = nullptr;

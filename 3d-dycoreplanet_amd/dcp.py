@@ -36,7 +36,7 @@ EXPORTED = [
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
     "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
-    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult",
+    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult", "dcp_mesh_geometry_info",
     "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
@@ -156,6 +156,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_cfl_number.argtypes = [P, D]
     lib.dcp_nse_vmult.argtypes = [P, P, P]
     lib.dcp_velocity_vmult.argtypes = [P, P, P]
+    lib.dcp_mesh_geometry_info.argtypes = [C.c_int, P, P, P, P]
     lib.dcp_schur_vmult.argtypes = [P, P, P]
     lib.dcp_block_preconditioner_vmult.argtypes = [P, P, P, I, C.POINTER(I)]
     lib.dcp_nse_matrix_export.argtypes = [P, C.POINTER(C.c_int64), P, P, P]
@@ -288,6 +289,16 @@ class HostMesh:
         if rc != DCP_OK:
             raise DcpError(rc, lib().dcp_last_error(None).decode())
         return ncol.value
+
+    def geometry_info(self):
+        """Host-only: (separable, n_columns, n_layers) of the radially separable
+        Q2 geometry the matrix-free operator uses (dcp_mesh_geometry_info)."""
+        sep, nc, nl = C.c_int(0), C.c_int(0), C.c_int(0)
+        rc = lib().dcp_mesh_geometry_info(self.n_cells, _ptr(self.cell_geometry), C.byref(sep),
+                                          C.byref(nc), C.byref(nl))
+        if rc != DCP_OK:
+            raise DcpError(rc, lib().dcp_last_error(None).decode())
+        return bool(sep.value), nc.value, nl.value
         self.temperature_degree = temperature_degree
 
 

@@ -145,6 +145,13 @@ int dcp_mesh_check(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
                    int n_T, const dcp_constraints* nse_constraints,
                    const dcp_constraints* T_constraints, int* n_colors);
 
+/* Host-only: is the Q2 geometry radially separable (every support point of a
+ * cell at r_c * phi_ab, local c radial; the SphericalManifold hypershell)?
+ * Then the matrix-free operator takes J^-1 / JxW from n_columns 2D tables and
+ * n_layers radial tables instead of recomputing the mapping per cell. */
+int dcp_mesh_geometry_info(int n_cells, const double* cell_geometry, int* separable,
+                           int* n_columns, int* n_layers);
+
 /* Device-resident state vectors ----------------------------------------- */
 enum {
   DCP_NSE_SOLUTION = 0,      /* nse_solution (n_u + n_p) */

@@ -5,6 +5,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 import dcp
@@ -62,3 +63,17 @@ def test_upload_rejects_bad_dof_layout():
     m.cell_nse_dofs[0, 0], m.cell_nse_dofs[0, 1] = m.cell_nse_dofs[0, 1], m.cell_nse_dofs[0, 0]
     with pytest.raises(dcp.DcpError):
         m.check()
+
+
+@pytest.mark.parametrize("r", [1, 2, 3])
+def test_separable_geometry_detection(r):
+    """The shell's Q2 support points are r_c * phi_ab: one 2D table per column
+    of cells (6 N^2) and one radial table per layer (N)."""
+    m = dcp.HostMesh(refine=r)
+    N = 2 ** r
+    assert m.geometry_info() == (True, 6 * N * N, N)
+    # a smooth displacement breaks the separability: general MappingQ2 path
+    m.cell_geometry = m.cell_geometry.copy()
+    X = m.cell_geometry.reshape(-1, 3)
+    X += 0.02 * np.sin(3.0 * X[:, [1, 2, 0]]) * np.cos(2.0 * X[:, [2, 0, 1]])
+    assert m.geometry_info() == (False, 0, 0)
