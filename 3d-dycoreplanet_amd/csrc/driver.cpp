@@ -1,0 +1,99 @@
+// Time-step driver: the do-while loop of BoussinesqModel<dim>::run
+// (Standard: include/core/boussinesq_model.tpp:1841-1926; ExteriorCalculus:
+// include/core/boussineq_model_FEEC.tpp:2236-2310) restated over the C ABI, so a
+// host program gets the reference's step sequence, step control and stopping
+// rule without re-implementing them. Mesh upload and the initial state
+// (setup_dofs, VectorTools::project of T0, :1793-1834) stay with the caller;
+// output_results is the callback.
+#include <algorithm>
+#include <cmath>
+#include <string>
+
+#include "../../include/dcp.h"
+
+namespace {
+
+// recompute_time_step (boussinesq_model.tpp:1104-1125; FEEC.tpp:1241-1261):
+// step-32's CFL rule in 3D, scaling 1/4
+double recomputed_time_step(const dcp_run_params* rp, double cfl) {
+  const double dim = 3.0;
+  const double scaling = 0.25;
+  const int deg = std::max(rp->physics.temperature_degree, rp->nse_velocity_degree);
+  return (scaling / (2.1 * dim * std::sqrt(dim))) / (double(deg) * cfl);
+}
+
+}  // namespace
+
+extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
+                       dcp_step_callback cb, void* user, dcp_run_report* rep) {
+  if (!ctx || !rp) return DCP_ERR_INVALID;
+  if (rp->use_schur_complement_solver)
+    return DCP_ERR_UNSUPPORTED;  // solve_NSE_Schur_complement (ILU): 2D / cube configs only
+  const bool feec = rp->use_FEEC_solver != 0;
+  const int interval = std::max(1, rp->physics.nse_solver_interval);
+  dcp_run_report r{};
+  r.time_step = rp->physics.time_step;
+  int rc = dcp_set_time_step(ctx, r.time_step);
+  if (rc < 0) return rc;
+  double time_index = 0.0;
+  int n = 0;
+  do {
+    // step control (:1843-1856): a new dt every NSE interval when adaptive,
+    // otherwise CFL and max velocity are informative only
+    if ((rc = dcp_cfl_number(ctx, &r.cfl)) < 0) return rc;
+    if (n > 0 && n % interval == 0 && rp->adapt_time_step) {
+      r.time_step = recomputed_time_step(rp, r.cfl);
+      if ((rc = dcp_set_time_step(ctx, r.time_step)) < 0) return rc;
+    }
+    if ((rc = dcp_max_velocity(ctx, &r.max_velocity)) < 0) return rc;
+    r.time_index = time_index;
+    r.timestep_number = n;
+    // NSE system (re)assembly on step 0 and every NSE interval (:1865-1881)
+    if (n == 0 || n % interval == 0) {
+      if (feec) {
+        if ((rc = dcp_feec_assemble_nse_system(ctx)) < 0) return rc;
+        if (rp->use_block_preconditioner_feec &&
+            (rc = dcp_feec_build_nse_preconditioner(ctx)) < 0)
+          return rc;
+      } else {
+        if ((rc = dcp_assemble_nse_system(ctx, DCP_ASSEMBLE_MATRIX | DCP_ASSEMBLE_RHS)) < 0)
+          return rc;
+        if ((rc = dcp_build_nse_preconditioner(ctx)) < 0) return rc;
+      }
+    }
+    if ((rc = dcp_assemble_temperature_matrix(ctx)) < 0) return rc;
+    if ((rc = dcp_assemble_temperature_rhs(ctx)) < 0) return rc;
+    // the NSE solve runs every step (:1895-1902)
+    if (feec) {
+      int it = 0;
+      rc = dcp_feec_solve_nse(ctx, &it);
+      r.fgmres_outer = it;
+      r.schur_inner = 0;
+    } else {
+      rc = dcp_solve_nse(ctx, &r.fgmres_outer, &r.schur_inner);
+    }
+    if (rc < 0) return rc;
+    if (rc == DCP_NOT_CONVERGED) {  // the reference throws out of run()
+      if (rep) *rep = r;
+      return rc;
+    }
+    r.total_outer += r.fgmres_outer;
+    r.total_inner += r.schur_inner;
+    double range[2] = {0.0, 0.0};
+    if ((rc = dcp_solve_temperature(ctx, &r.T_cg, range)) < 0) return rc;
+    r.T_min = range[0];
+    r.T_max = range[1];
+    r.total_T_cg += r.T_cg;
+    r.steps = n + 1;
+    if (cb && cb(user, &r) != 0) {  // output_results (:1907); non-zero stops the run
+      if ((rc = dcp_advance_state(ctx)) < 0) return rc;
+      break;
+    }
+    time_index += r.time_step / interval;  // :1918
+    ++n;
+    if ((rc = dcp_advance_state(ctx)) < 0) return rc;  // old_* = * (:1921-1922)
+    r.time_index = time_index;
+  } while (time_index <= rp->final_time && (max_steps <= 0 || n < max_steps));
+  if (rep) *rep = r;
+  return DCP_OK;
+}

@@ -1,0 +1,124 @@
+// dcp_aquaplanet -p <file.prm> [--refine R] [--max-steps N] [--device D]
+//
+// The reference executable (source/main.cxx: parse -p, construct the model
+// from the parameter file, run()) over libdcp.so: CoreModelData::Parameters
+// from the same .prm (dcp_prm_load), the refined shell / cube with its DoFs
+// and constraints (setup_dofs, dcp_host_mesh_create), the initial temperature,
+// then the time loop (dcp_run) with the reference's per-step log lines.
+// Single GPU; the multi-GPU path is driven through the same ABI by one process
+// per GPU (bench.py).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dcp.h"
+
+namespace {
+
+int fail(const char* what, dcp_ctx* ctx) {
+  std::fprintf(stderr, "Error: %s: %s\n", what, dcp_last_error(ctx));
+  return 1;
+}
+
+int print_step(void*, const dcp_run_report* r) {
+  std::printf("----------------------------------------\n");
+  std::printf("Time step %d:  t=%g -> t=%g  (dt=%g)\n", r->timestep_number, r->time_index,
+              r->time_index + r->time_step, r->time_step);
+  std::printf("   Max velocity (dimensionsless): %g\n", r->max_velocity);
+  std::printf("   Max of local CFL numbers: %g\n", r->cfl);
+  if (r->schur_inner > 0)
+    std::printf("   Solved (outer / inner Schur GMRES): %d / %d\n", r->fgmres_outer, r->schur_inner);
+  else
+    std::printf("   Solved (GMRES): %d\n", r->fgmres_outer);
+  std::printf("   Temperature: %d CG iterations, range %g %g\n", r->T_cg, r->T_min, r->T_max);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string prm;
+  int refine = -1, max_steps = 0, device = 0;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    if (a == "-p" && i + 1 < argc) {
+      prm = argv[++i];
+    } else if (a == "--refine" && i + 1 < argc) {
+      refine = std::atoi(argv[++i]);
+    } else if (a == "--max-steps" && i + 1 < argc) {
+      max_steps = std::atoi(argv[++i]);
+    } else if (a == "--device" && i + 1 < argc) {
+      device = std::atoi(argv[++i]);
+    } else {
+      std::fprintf(stderr, "Unknown command line option: %s\n", a.c_str());
+      return 1;
+    }
+  }
+  if (prm.empty()) {
+    std::fprintf(stderr, "Error: flag '-p' must be followed by the name of a parameter file.\n");
+    return 1;
+  }
+  dcp_run_params rp{};
+  char err[512] = {0};
+  if (dcp_prm_load(prm.c_str(), &rp, err, sizeof(err)) != DCP_OK) {
+    std::fprintf(stderr, "Error: %s\n", err);
+    return 1;
+  }
+  if (refine >= 0) rp.initial_global_refinement = refine;
+  if (rp.space_dimension != 3) {
+    std::fprintf(stderr, "Error: only the 3D models run on the device path\n");
+    return 1;
+  }
+  const bool feec = rp.use_FEEC_solver != 0;
+  dcp_host_mesh* m = dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0,
+                                          rp.R1, rp.length, rp.physics.temperature_degree, 0);
+  if (!m) return fail("mesh", nullptr);
+  dcp_host_mesh_view v{};
+  dcp_host_mesh_view_get(m, &v);
+  dcp_config cfg{device, 0, 1, nullptr, nullptr};
+  dcp_ctx* ctx = nullptr;
+  if (dcp_ctx_create(&cfg, &ctx) != DCP_OK) return fail("context", nullptr);
+  int rc = dcp_set_physics(ctx, &rp.physics);
+  size_t n_nse = size_t(v.n_u) + size_t(v.n_p);
+  dcp_feec_mesh fm{};
+  if (rc == DCP_OK) {
+    if (feec) {
+      rc = dcp_host_feec_view_get(m, &fm);
+      if (rc == DCP_OK) rc = dcp_feec_mesh_upload(ctx, &fm);
+      n_nse = size_t(fm.n_w) + size_t(fm.n_u) + size_t(fm.n_p);
+      if (rc == DCP_OK)
+        rc = dcp_set_option(ctx, DCP_OPT_FEEC_ZERO_MEAN, rp.correct_pressure_to_zero_mean);
+    } else {
+      rc = dcp_mesh_upload(ctx, v.n_cells, v.cell_nse_dofs, v.cell_T_dofs, v.cell_geometry,
+                           v.cell_diameter, v.n_u, v.n_p, v.n_T, &v.nse, &v.T);
+    }
+  }
+  if (rc != DCP_OK) return fail("upload", ctx);
+  std::printf("Number of active cells: %d\nNumber of degrees of freedom: %zu (NSE) + %d (T)\n",
+              v.n_cells, n_nse, v.n_T);
+  // initial values (run(), :1801-1834): u = 0, T = the projected initial field
+  std::vector<double> u(n_nse, 0.0), T(size_t(v.n_T), 0.0);
+  dcp_host_mesh_initial_temperature(m, T.data());
+  for (int f : {DCP_NSE_SOLUTION, DCP_OLD_NSE_SOLUTION})
+    if ((rc = dcp_state_set(ctx, f, u.data(), u.size())) != DCP_OK) return fail("state", ctx);
+  for (int f : {DCP_T_SOLUTION, DCP_OLD_T_SOLUTION})
+    if ((rc = dcp_state_set(ctx, f, T.data(), T.size())) != DCP_OK) return fail("state", ctx);
+  dcp_run_report rep{};
+  rc = dcp_run(ctx, &rp, max_steps, print_step, nullptr, &rep);
+  if (rc < 0) return fail("run", ctx);
+  dcp_timings t{};
+  dcp_get_timings(ctx, &t);
+  std::printf("----------------------------------------\n");
+  std::printf("%d steps to t=%g: %ld outer / %ld inner NSE iterations, %ld T CG iterations%s\n",
+              rep.steps, rep.time_index, rep.total_outer, rep.total_inner, rep.total_T_cg,
+              rc == DCP_NOT_CONVERGED ? " (NSE solve did not converge)" : "");
+  std::printf("last step (device ms): assemble NSE %.3f | NSE precond %.3f | T matrix %.3f | "
+              "T rhs %.3f | NSE solve %.1f | T solve %.3f\n",
+              t.assemble_nse_ms, t.build_precond_ms, t.assemble_T_matrix_ms, t.assemble_T_rhs_ms,
+              t.solve_nse_ms, t.solve_T_ms);
+  dcp_ctx_destroy(ctx);
+  dcp_host_mesh_destroy(m);
+  return rc == DCP_OK ? 0 : 2;
+}

@@ -36,7 +36,7 @@ EXPORTED = [
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
     "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
-    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult", "dcp_mesh_geometry_info",
+    "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult", "dcp_mesh_geometry_info", "dcp_run",
     "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
@@ -122,6 +122,20 @@ class RunParams(C.Structure):
     ]
 
 
+class RunReport(C.Structure):
+    """dcp_run_report: one time step of dcp_run (and the run totals)."""
+    _fields_ = [
+        ("timestep_number", C.c_int), ("steps", C.c_int), ("time_index", C.c_double),
+        ("time_step", C.c_double), ("cfl", C.c_double), ("max_velocity", C.c_double),
+        ("fgmres_outer", C.c_int), ("schur_inner", C.c_int), ("T_cg", C.c_int),
+        ("total_outer", C.c_long), ("total_inner", C.c_long), ("total_T_cg", C.c_long),
+        ("T_min", C.c_double), ("T_max", C.c_double),
+    ]
+
+
+STEP_CALLBACK = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(RunReport))
+
+
 def load_library(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError(
@@ -157,6 +171,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_nse_vmult.argtypes = [P, P, P]
     lib.dcp_velocity_vmult.argtypes = [P, P, P]
     lib.dcp_mesh_geometry_info.argtypes = [C.c_int, P, P, P, P]
+    lib.dcp_run.argtypes = [P, C.POINTER(RunParams), C.c_int, STEP_CALLBACK, P, C.POINTER(RunReport)]
     lib.dcp_schur_vmult.argtypes = [P, P, P]
     lib.dcp_block_preconditioner_vmult.argtypes = [P, P, P, I, C.POINTER(I)]
     lib.dcp_nse_matrix_export.argtypes = [P, C.POINTER(C.c_int64), P, P, P]
@@ -658,6 +673,25 @@ class Context:
         rc, out = self._dev_roundtrip(lambda s, d: lib().dcp_nse_vmult(self._h, s, d), src, n)
         self._check(rc)
         return out
+
+    def run(self, rp, max_steps=0, on_step=None):
+        """dcp_run: the reference's time loop from the uploaded mesh and state.
+        on_step(report) is output_results' hook (return True to stop).
+        Returns (rc, final report, list of per-step reports)."""
+        steps = []
+
+        def cb(_user, rep):
+            r = RunReport()
+            C.pointer(r)[0] = rep[0]
+            steps.append(r)
+            return 1 if (on_step is not None and on_step(r)) else 0
+
+        fn = STEP_CALLBACK(cb)
+        out = RunReport()
+        rc = lib().dcp_run(self._h, C.byref(rp), int(max_steps), fn, None, C.byref(out))
+        if rc < 0:
+            self._check(rc)
+        return rc, out, steps
 
     def velocity_vmult(self, src_u):
         """nse_matrix.block(0,0) * src_u (the do_solve_A GMRES operator)."""

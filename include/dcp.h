@@ -311,6 +311,29 @@ typedef struct {
 } dcp_run_params;
 int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
 
+/* Time-step driver: the do-while loop of BoussinesqModel<dim>::run
+ * (boussinesq_model.tpp:1841-1926, FEEC: boussineq_model_FEEC.tpp:2236-2310)
+ * over the calls above, after the caller has uploaded the mesh and the initial
+ * state: per step the CFL / max-velocity step control (recompute_time_step
+ * every NSE interval when adapt_time_step, :1104-1125), NSE (re)assembly and
+ * preconditioner on step 0 and every NSE interval, temperature matrix and
+ * rhs, the NSE and temperature solves, the callback (output_results; a
+ * non-zero return stops), time_index += dt / interval, old_* = *; until
+ * time_index > final_time or max_steps (> 0) steps. Returns DCP_NOT_CONVERGED
+ * where the reference's solve throws. Not supported: the ILU Schur-complement
+ * solver (use_schur_complement_solver, 2D / cube configs). */
+typedef struct {
+  int timestep_number, steps;       /* current step; steps completed */
+  double time_index, time_step;     /* t at the step's start; dt */
+  double cfl, max_velocity;         /* get_cfl_number / get_maximal_velocity */
+  int fgmres_outer, schur_inner, T_cg;           /* this step */
+  long total_outer, total_inner, total_T_cg;     /* whole run */
+  double T_min, T_max;              /* solve_temperature range */
+} dcp_run_report;
+typedef int (*dcp_step_callback)(void* user, const dcp_run_report* step);
+int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps, dcp_step_callback cb,
+            void* user, dcp_run_report* report);
+
 #ifdef __cplusplus
 }
 #endif

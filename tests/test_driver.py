@@ -1,0 +1,82 @@
+"""dcp_run (csrc/driver.cpp): the reference's time loop (boussinesq_model.tpp:
+1841-1926) over the C ABI, against the same calls made one by one from Python,
+and the dcp_aquaplanet executable (source/main.cxx -p <prm>)."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import dcp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRM = os.path.join(ROOT, "configs", "aqua_planet_shell_test_3d-classic.prm")
+
+
+def fresh(rp, m):
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.physics_from_params(rp))
+    ctx.upload_mesh(m)
+    u = np.zeros(m.n_u + m.n_p)
+    for f, v in ((dcp.NSE_SOLUTION, u), (dcp.OLD_NSE_SOLUTION, u), (dcp.T_SOLUTION, m.T0),
+                 (dcp.OLD_T_SOLUTION, m.T0)):
+        ctx.set_state(f, v)
+    return ctx
+
+
+@pytest.mark.gpu
+def test_run_matches_step_by_step_calls():
+    rp = dcp.load_prm(PRM)
+    rp.initial_global_refinement = 1
+    rp.adapt_time_step = 1           # recompute_time_step from step 1 on
+    rp.final_time = 100.0
+    m = dcp.HostMesh(refine=1, R0=rp.R0, R1=rp.R1, length=rp.length)
+    nsteps = 3
+    ctx = fresh(rp, m)
+    rc, rep, steps = ctx.run(rp, max_steps=nsteps)
+    assert rc == dcp.DCP_OK and rep.steps == nsteps and len(steps) == nsteps
+    u_run, T_run = ctx.get_state(dcp.NSE_SOLUTION), ctx.get_state(dcp.T_SOLUTION)
+    ctx.close()
+
+    ctx = fresh(rp, m)
+    dt = rp.physics.time_step
+    t = 0.0
+    for n in range(nsteps):
+        cfl = ctx.cfl_number()
+        if n > 0 and rp.adapt_time_step:
+            deg = max(rp.physics.temperature_degree, rp.nse_velocity_degree)
+            dt = (0.25 / (2.1 * 3 * math.sqrt(3))) / (deg * cfl)
+            ctx.set_time_step(dt)
+        ctx.max_velocity()
+        assert steps[n].time_step == dt and steps[n].time_index == t
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        ctx.assemble_temperature_matrix()
+        ctx.assemble_temperature_rhs()
+        rcn, outer, inner = ctx.solve_nse()
+        assert (rcn, outer, inner) == (0, steps[n].fgmres_outer, steps[n].schur_inner)
+        ctx.solve_temperature()
+        ctx.advance_state()
+        t += dt / rp.physics.nse_solver_interval
+    assert steps[1].time_step != steps[0].time_step  # the adaptive step took effect
+    assert np.array_equal(ctx.get_state(dcp.NSE_SOLUTION), u_run)
+    assert np.array_equal(ctx.get_state(dcp.T_SOLUTION), T_run)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_executable_runs_the_classic_prm():
+    exe = os.path.join(ROOT, "3d-dycoreplanet_amd", "dcp_aquaplanet")
+    out = subprocess.run([exe, "-p", PRM, "--refine", "2"], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    # the classic prm runs exactly one step (time_index += dt > final_time, Q24)
+    assert out.stdout.count("Time step ") == 1
+    assert "1 steps to t=" in out.stdout
+
+
+def test_executable_requires_a_parameter_file():
+    exe = os.path.join(ROOT, "3d-dycoreplanet_amd", "dcp_aquaplanet")
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1 and "-p" in out.stderr
