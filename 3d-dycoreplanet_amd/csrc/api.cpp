@@ -849,6 +849,9 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
       for (auto& t : v) t.init();
     }
     ensure_workspaces(*c);
+    if (const char* e = std::getenv("DCP_SCHUR_AHEAD")) c->schur_ahead = std::atoi(e) != 0;
+    if (const char* e = std::getenv("DCP_TEST_FORCE_REORTH_AT"))
+      c->test_force_reorth_at = std::atoi(e);
     *out = c.release();
     return DCP_OK;
   });
@@ -884,6 +887,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     if (option == DCP_OPT_MATRIX_FREE) {
       require(value >= 0 && value <= 2, DCP_ERR_INVALID, "DCP_OPT_MATRIX_FREE must be 0, 1 or 2");
       ctx->matrix_free = value;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_FUSED_CHAIN) {
+      ctx->fused_chain = value != 0;
       return DCP_OK;
     }
     if (option == DCP_OPT_FEEC_ZERO_MEAN) {

@@ -159,6 +159,17 @@ struct Ctx {
   double* hpinned = nullptr;   // pinned host mirror of small readbacks
   hipEvent_t spec_ev[2] = {nullptr, nullptr};  // readbacks of pipelined Arnoldi steps
   double* hmapped = nullptr;   // coherent mapped host memory written by kernels (one GPU)
+  // one-launch Gram-Schmidt chains (k_mgs_chain): hand-off granules, launch
+  // counter (the granule tags), CU count (residency bound), DCP_OPT_FUSED_CHAIN
+  DBuf<double> chain_gran;
+  unsigned long long chain_seq = 0;
+  int n_cus = 0;
+  bool fused_chain = true;
+  // test hooks, read at context creation: DCP_SCHUR_AHEAD=0 turns the inner
+  // Schur GMRES's launch-ahead off; DCP_TEST_FORCE_REORTH_AT=k makes the
+  // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger
+  bool schur_ahead = true;
+  int test_force_reorth_at = -1;
   bool nse_assembled = false, precond_built = false, T_matrix_ok = false, T_rhs_ok = false;
   // Krylov workspaces (lazily sized)
   std::vector<double*> fg_v, fg_z;   // FGMRES basis

@@ -280,6 +280,24 @@ void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, dou
                           const double* x, const double* w, double* partials,
                           double* coef_store, int nb, const double* prev2, double* store2,
                           double* partials_host, hipStream_t s);
+// The whole chain in one launch (kernels/linalg.hip k_mgs_chain; one GPU):
+// h_0 = w.V[0] (the sum of prev's nb_prev partials, or computed in-kernel when
+// prev is null), h_i = (w -= h_{i-1} V[i-1]).V[i], w -= h_{d-1} V[d-1], nb
+// partials of |w|^2 -> partials (+ partials_host); h_0..h_{d-1} -> coef.
+// Bitwise the per-step chain above. Needs every one of the nb workgroups
+// resident: mgs_chain_fits() says whether (n, nb, d) qualify on n_cus CUs.
+// gran: kMgsGranules doubles of hand-off scratch; seq: a per-context launch
+// counter (never reused); *err becomes 1 if a workgroup timed out waiting.
+constexpr int kMgsMaxVecs = 64;
+constexpr size_t kMgsGranules = size_t(2) * kMgsMaxVecs * kChainMaxBlocks;
+struct ChainVecs {
+  const double* v[kMgsMaxVecs];
+};
+bool mgs_chain_fits(long n, int nb, int d, int n_cus);
+void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, int nb_prev,
+               const double* prev2, double* store2, double* coef, double* partials,
+               double* partials_host, int nb, double* gran, unsigned long long seq, double* err,
+               hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

@@ -186,6 +186,183 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Whole modified-Gram-Schmidt chain in one launch (one GPU). The grid is the
+// chain's nb workgroups, all resident (nb <= the CU count, checked by the
+// launcher), and every workgroup keeps its <= kMgsElems entries of w in
+// registers for the whole chain. A step's nb block sums are handed to every
+// workgroup as 16-byte granules {sum, tag} written by one `sc1` store and
+// polled with `sc1` loads (agent-coherent, no fences: the tag travels with
+// the value in one untorn 16-byte access); the tag = launch sequence * 64 +
+// step is never reused, so the granule array needs no clearing. Every
+// workgroup then forms the coefficient from the nb sums in exactly the order
+// k_chain_add_and_dot uses, so the chain is bitwise the per-step one.
+// Spins are bounded (an unbounded wait would hang the device): a workgroup
+// that gives up writes 1 to *err and the host throws.
+constexpr int kMgsElems = 4;
+constexpr long kMgsMaxSpins = 1L << 21;
+typedef unsigned int mgs_u4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void granule_store(double* p, double v, unsigned long long tag) {
+  const unsigned long long b = __double_as_longlong(v);
+  mgs_u4 q;
+  q.x = unsigned(b);
+  q.y = unsigned(b >> 32);
+  q.z = unsigned(tag);
+  q.w = unsigned(tag >> 32);
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(q) : "memory");
+}
+
+__device__ inline bool tag_is(const mgs_u4& q, unsigned long long tag) {
+  return q.z == unsigned(tag) && q.w == unsigned(tag >> 32);
+}
+__device__ inline double granule_value(const mgs_u4& q) {
+  return __longlong_as_double((long long)(((unsigned long long)q.y << 32) | q.x));
+}
+
+// Wave 0 only: waits for the nb <= 256 granules of one step (lane l polls
+// granules l, l+64, l+128, l+192, four `sc1` loads in flight) and returns, in
+// every lane, their sum in exactly block_sum's order (thread t holds granule
+// t; xor butterfly per 64-thread wave; the four wave sums left to right).
+__device__ inline double granule_coef(const double* gran, int nb, unsigned long long tag,
+                                      double* err) {
+  const int l = threadIdx.x & 63;
+  const double* p = gran + 2 * size_t(l);
+  mgs_u4 q0, q1, q2, q3;
+  long spins = 0;
+  for (;;) {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off sc1\n\t"
+        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
+        : "v"(p)
+        : "memory");
+    const bool ok = (l >= nb || tag_is(q0, tag)) && (l + 64 >= nb || tag_is(q1, tag)) &&
+                    (l + 128 >= nb || tag_is(q2, tag)) && (l + 192 >= nb || tag_is(q3, tag));
+    if (__all(ok)) break;
+    if (++spins >= kMgsMaxSpins) {
+      if (l == 0) *err = 1.0;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  double v[4] = {l < nb ? granule_value(q0) : 0.0, l + 64 < nb ? granule_value(q1) : 0.0,
+                 l + 128 < nb ? granule_value(q2) : 0.0, l + 192 < nb ? granule_value(q3) : 0.0};
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[w] += __shfl_xor(v[w], off, 64);
+  return v[0] + v[1] + v[2] + v[3];
+}
+
+// h_0 = w.V[0] (from prev: nb_prev partials, e.g. the fused SpMV's; or, with
+// prev == null, computed here), then for i = 1..d-1:
+//   w -= h_{i-1} V[i-1];  h_i = w.V[i]
+// and finally w -= h_{d-1} V[d-1]; partials of |w|^2. Coefficients -> coef
+// (block 0), optional fixed-order sum of prev2 -> *store2 (block 0), the final
+// partials -> partials (+ partials_host), w written back once at the end.
+__global__ __launch_bounds__(kBlock) void k_mgs_chain(
+    Seg g, double* w, ChainVecs V, int d, const double* __restrict__ prev, int nb_prev,
+    const double* __restrict__ prev2, double* store2, double* coef, double* partials,
+    double* partials_host, double* gran, unsigned long long seq, double* err) {
+  __shared__ double sm[4];
+  __shared__ double coef_sh;
+  const int nb = gridDim.x;
+  const long stride = long(nb) * kBlock;
+  const long i0 = long(blockIdx.x) * kBlock + threadIdx.x;
+  // rx: the vector subtracted at step i (V[i-1]), ry: the one dotted (V[i]),
+  // rz: V[i+1], loaded before step i's hand-off wait so it lands meanwhile
+  double rw[kMgsElems], rx[kMgsElems], ry[kMgsElems], rz[kMgsElems];
+  long pos[kMgsElems];
+#pragma unroll
+  for (int e = 0; e < kMgsElems; ++e) {
+    const long k = i0 + e * stride;
+    pos[e] = k < g.n ? seg_pos(g, k) : -1;
+    rw[e] = pos[e] >= 0 ? w[pos[e]] : 0.0;
+    rx[e] = pos[e] >= 0 ? V.v[0][pos[e]] : 0.0;
+    ry[e] = pos[e] >= 0 && d > 1 ? V.v[1][pos[e]] : 0.0;
+  }
+  if (prev) {
+    double s = 0;
+    for (int i = threadIdx.x; i < nb_prev; i += kBlock) s += prev[i];
+    const double tot = block_sum(s, sm);
+    if (threadIdx.x == 0) {
+      coef_sh = tot;
+      if (blockIdx.x == 0) coef[0] = tot;
+    }
+  } else {
+    // h_0 = w.V0 here: the same per-thread order as k_dot_partial's grid stride
+    double p0 = 0;
+#pragma unroll
+    for (int e = 0; e < kMgsElems; ++e)
+      if (pos[e] >= 0) p0 += rw[e] * rx[e];
+    const double r0 = block_sum(p0, sm);
+    if (threadIdx.x == 0) granule_store(gran + 2 * size_t(blockIdx.x), r0, seq * 64);
+    if (threadIdx.x < 64) {
+      const double tot = granule_coef(gran, nb, seq * 64, err);
+      if (threadIdx.x == 0) {
+        coef_sh = tot;
+        if (blockIdx.x == 0) coef[0] = tot;
+      }
+    }
+  }
+  __syncthreads();
+  if (prev2) {
+    double s2 = 0;
+    for (int i = threadIdx.x; i < nb_prev; i += kBlock) s2 += prev2[i];
+    const double t2 = block_sum(s2, sm);
+    if (threadIdx.x == 0 && blockIdx.x == 0) *store2 = t2;
+    __syncthreads();
+  }
+  for (int i = 1; i <= d; ++i) {
+    const bool last = i == d;
+    const double cf = -1.0 * coef_sh;
+    double dd = 0;
+#pragma unroll
+    for (int e = 0; e < kMgsElems; ++e) {
+      if (pos[e] >= 0) {
+        const double nv = rw[e] + cf * rx[e];
+        rw[e] = nv;
+        dd += nv * (last ? nv : ry[e]);
+      }
+    }
+    const double r = block_sum(dd, sm);
+    if (last) {
+      if (threadIdx.x == 0) {
+        partials[blockIdx.x] = r;
+        if (partials_host) partials_host[blockIdx.x] = r;
+      }
+      break;
+    }
+    const unsigned long long tag = seq * 64 + unsigned(i);
+    double* gi = gran + 2 * size_t(i) * kChainMaxBlocks;
+    if (threadIdx.x == 0) granule_store(gi + 2 * size_t(blockIdx.x), r, tag);
+    if (i + 1 < d) {
+#pragma unroll
+      for (int e = 0; e < kMgsElems; ++e) rz[e] = pos[e] >= 0 ? V.v[i + 1][pos[e]] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < kMgsElems; ++e) {
+      rx[e] = ry[e];
+      ry[e] = rz[e];
+    }
+    if (threadIdx.x < 64) {
+      const double tot = granule_coef(gi, nb, tag, err);
+      if (threadIdx.x == 0) {
+        coef_sh = tot;
+        if (blockIdx.x == 0) coef[i] = tot;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < kMgsElems; ++e)
+    if (pos[e] >= 0) w[pos[e]] = rw[e];
+}
+
 // SELL-64 SpMV (see device.h). One 256-thread workgroup per slice: lane i of
 // every wave owns row 64s+i, wave j sums the j-th quarter of the slice's
 // entry columns (4 waves per slice keep enough loads in flight: one wave per
@@ -620,6 +797,20 @@ void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, dou
                           double* partials_host, hipStream_t s) {
   hipLaunchKernelGGL(k_chain_add_and_dot, dim3(nb), dim3(kBlock), 0, s, g, v, prev, nb_prev, mult,
                      x, w, partials, coef_store, prev2, store2, partials_host);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+bool mgs_chain_fits(long n, int nb, int d, int n_cus) {
+  return d >= 1 && d < kMgsMaxVecs && nb >= 1 && nb <= n_cus && nb <= kBlock &&
+         n <= long(kMgsElems) * nb * kBlock;
+}
+
+void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, int nb_prev,
+               const double* prev2, double* store2, double* coef, double* partials,
+               double* partials_host, int nb, double* gran, unsigned long long seq, double* err,
+               hipStream_t s) {
+  hipLaunchKernelGGL(k_mgs_chain, dim3(nb), dim3(kBlock), 0, s, g, w, V, d, prev, nb_prev, prev2,
+                     store2, coef, partials, partials_host, gran, seq, err);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

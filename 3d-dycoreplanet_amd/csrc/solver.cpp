@@ -149,6 +149,26 @@ double block_sum_host(const double* p, int nb) {
   return sm[0] + sm[1] + sm[2] + sm[3];
 }
 
+// One-launch chains (k_mgs_chain): one GPU, every workgroup resident, w in
+// registers. The timeout flag lives in mapped host memory and is sticky.
+constexpr int kChainErr = 8000;
+static_assert(kSpecBase + 2 * kSpecStride <= kChainErr && kChainErr < kNumSlots, "slot layout");
+bool fused_chain_ok(const Ctx& c, Seg g, int nb, int dim) {
+  return !c.comm && c.fused_chain && c.hmapped && mgs_chain_fits(g.n, nb, dim, c.n_cus);
+}
+double* chain_err(Ctx& c) { return c.hmapped + kChainErr; }
+void check_chain_err(Ctx& c) {
+  if (c.hmapped[kChainErr] != 0.0) {
+    c.hmapped[kChainErr] = 0.0;
+    throw std::runtime_error("Gram-Schmidt chain: a workgroup timed out waiting for a hand-off");
+  }
+}
+ChainVecs chain_vecs(const std::vector<double*>& V, int dim) {
+  ChainVecs cv{};
+  for (int i = 0; i < dim; ++i) cv.v[i] = V[i];
+  return cv;
+}
+
 // Host side of a chain: fetch `ncoef` coefficient slots starting at `s0` and
 // the nb final partials of buffer `b`; returns their fixed-order sum.
 // The last step of a chain writes its partials to slot kHostPartials, so one
@@ -169,6 +189,14 @@ double fetch_chain(Ctx& c, int s0, int ncoef, int nb, std::vector<double>& coef)
 double gs_chain(Ctx& c, Seg g, const std::vector<double*>& V, int dim, double* w, int s0,
                 std::vector<double>& h) {
   const int nb = chain_width(c, g);
+  if (fused_chain_ok(c, g, nb, dim)) {
+    mgs_chain(g, w, chain_vecs(V, dim), dim, nullptr, 0, nullptr, nullptr, slot(c, s0),
+              slot(c, kHostPartials), nullptr, nb, c.chain_gran.p, ++c.chain_seq, chain_err(c),
+              c.stream);
+    const double r = fetch_chain(c, s0, dim, nb, h);
+    check_chain_err(c);
+    return r;
+  }
   dot_partial(g, w, V[0], pbuf(c, 0), nb, c.stream);
   allreduce(c, pbuf(c, 0), nb);
   for (int i = 1; i < dim; ++i) {
@@ -276,11 +304,12 @@ Timer* schur_sample(Ctx& c);
 // Pipelining: step k+1 is enqueued before the host has read step k back (the
 // SpMV derives 1/|w_k| from the chain's partials itself), so the GPU never
 // waits for the host's Givens/convergence work. Step k+1 is launched ahead
-// only when step k cannot change what it computes: not a loss-of-
-// orthogonality test step (every 5th), no re-orthogonalisation, not the last
-// step of a cycle, and residual not predicted to converge at k. A launched-
-// ahead step that turns out unneeded (converged at k) writes only scratch: the
-// next basis vector, the other w buffer and the other parity's slots.
+// unless re-orthogonalisation is on, k ends the cycle, or the residual is
+// predicted to converge at k. A launched-ahead step that turns out unneeded
+// (converged at k) writes only scratch: the next basis vector, the other w
+// buffer and the other parity's slots; one launched ahead of a loss-of-
+// orthogonality test (every 5th step) that triggers is relaunched on the
+// re-orthogonalised w and overwrites all of it.
 State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                           std::vector<double*>& tv, int n_tmp);
 
@@ -340,6 +369,13 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     double* hmir = hmir0;
     const double* prev = part0;
     int nprev = nbs;
+    if (fused_chain_ok(c, g, nb, d)) {  // the whole chain in one launch
+      mgs_chain(g, w, chain_vecs(tv, d), d, part0, nbs, consider ? part1 : nullptr,
+                hmir + B0 + kSpNStart, hmir + B0, slot(c, B0 + kSpPart), hmir + B0 + kSpPart, nb,
+                c.chain_gran.p, ++c.chain_seq, chain_err(c), c.stream);
+      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
+      return;
+    }
     for (int i = 1; i <= d; ++i) {
       const bool last = i == d;
       double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
@@ -381,10 +417,12 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
       const bool consider = !reorth && (inner % 5 == 4);
       // launch step inner+1 now unless step inner may change it
       const double rho_pred = rho * (rho / rho_prev);
-      const bool ahead = !reorth && !consider && inner + 1 < n_tmp - 2 &&
-                         accumulated < ctl.max_steps && rho_pred > 2.0 * ctl.tol;
+      const bool ahead = c.schur_ahead && !reorth && inner + 1 < n_tmp - 2 &&
+                         accumulated < ctl.max_steps &&
+                         rho_pred > 2.0 * ctl.tol;
       if (ahead) launch(inner + 1, 0.0, true);
       DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[inner & 1]));
+      check_chain_err(c);
       const double* hp = (hmir0 ? hmir0 : c.hpinned) + B0;
       if (prev_ahead && hp[kSpNorm] != prev_norm)
         throw std::runtime_error("gmres_schur: device and host |w| differ");
@@ -393,7 +431,8 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
       const double start2 = consider ? hp[kSpNStart] : 0.0;
       for (int i = 0; i < dim; ++i) h[i] = hv[i];
       bool second = reorth;
-      if (consider && !(norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16))) {
+      if (consider && (!(norm_vv > 10. * std::sqrt(start2) * std::sqrt(2.220446049250313e-16)) ||
+                       inner == c.test_force_reorth_at)) {
         reorth = true;
         second = true;
       }
@@ -408,8 +447,12 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
       rho = std::fabs(gamma[dim]);
       st = ctl.check(accumulated, rho);
       prev_norm = norm_vv;
-      prev_ahead = ahead;
-      if (st == kIterate && !ahead && inner + 1 < n_tmp - 2)
+      // a step launched ahead of a loss-of-orthogonality test that triggered
+      // used the first-pass w: relaunch it (stream order puts it after the
+      // ahead step and the second pass; it rewrites everything that step wrote)
+      const bool redo = ahead && second;
+      prev_ahead = ahead && !redo;
+      if (st == kIterate && (!ahead || redo) && inner + 1 < n_tmp - 2)
         launch(inner + 1, norm_vv != 0 ? 1. / norm_vv : 1.0, false);
     }
     std::vector<double> y(dim, 0.0);
@@ -700,8 +743,12 @@ void ensure_workspaces(Ctx& c) {
     // coherent mapped host memory the kernels write directly (uncached on the GPU)
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hmapped), kNumSlots * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
+    std::fill(c.hmapped, c.hmapped + kNumSlots, 0.0);
     c.coef.alloc(128);
     c.ptrs.alloc(128);
+    c.chain_gran.alloc(kMgsGranules);
+    DCP_HIP_CHECK(hipMemset(c.chain_gran.p, 0, kMgsGranules * sizeof(double)));  // tag 0: never waited for
+    DCP_HIP_CHECK(hipDeviceGetAttribute(&c.n_cus, hipDeviceAttributeMultiprocessorCount, c.cfg.device));
   }
 }
 

@@ -28,6 +28,7 @@ ASSEMBLE_MATRIX, ASSEMBLE_RHS = 1, 2
 OPT_SCHUR_EXPLICIT = 1
 OPT_FEEC_ZERO_MEAN = 2
 OPT_MATRIX_FREE = 3
+OPT_FUSED_CHAIN = 4
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -520,6 +521,11 @@ class Context:
         self._keep = (m,)
         self._check(lib().dcp_feec_mesh_upload(self._h, C.byref(self._feec_view)))
         self.mesh = m
+
+    def set_fused_chain(self, on: bool):
+        """DCP_OPT_FUSED_CHAIN: one launch per Gram-Schmidt chain (default) or
+        one per step; bitwise the same results."""
+        self._check(lib().dcp_set_option(self._h, OPT_FUSED_CHAIN, int(bool(on))))
 
     def set_feec_zero_mean(self, on: bool):
         self._check(lib().dcp_set_option(self._h, OPT_FEEC_ZERO_MEAN, int(bool(on))))

@@ -128,6 +128,11 @@ enum { DCP_OPT_SCHUR_EXPLICIT = 1 };
  *   the assembled diagonal for constrained dofs; 0 = block-CSR SpMV of the
  *   assembled matrix. Same operator, different rounding. */
 enum { DCP_OPT_MATRIX_FREE = 3 };
+/* DCP_OPT_FUSED_CHAIN: 1 (default) = on one GPU every modified Gram-Schmidt
+ *   chain of the Krylov solvers (SolverGMRES's add_and_dot sequence) runs as
+ *   one launch whose workgroups hand each step's reduction to each other on the
+ *   device; 0 = one launch per step. Bitwise the same results. */
+enum { DCP_OPT_FUSED_CHAIN = 4 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the

@@ -252,3 +252,75 @@ def test_matrix_free_matches_assembled(kind):
         ctx.set_matrix_free(mode)
         assert rel_max(ctx.velocity_vmult(x[:m.n_u]), va) < 1e-13, mode
     ctx.close()
+
+
+def _fused_vs_per_step(ctx, run):
+    out = []
+    for fused in (True, False):
+        ctx.set_fused_chain(fused)
+        out.append(run())
+    ctx.set_fused_chain(True)
+    return out
+
+
+@pytest.mark.parametrize("refine", [2, 5])
+def test_fused_chain_is_bitwise_the_per_step_chain(refine):
+    """DCP_OPT_FUSED_CHAIN: the one-launch modified Gram-Schmidt chain
+    (k_mgs_chain, in-kernel hand-off of each step's reduction) against the
+    launch-per-step chain. Same block partition and summation order, so the
+    Krylov iterates must agree bit for bit. r=2: whole solve (inner Schur GMRES,
+    FGMRES, re-orthogonalisation); r=5 (n_p = 2e5, several entries per thread):
+    the block preconditioner with its inner Schur GMRES and the A-GMRES."""
+    m = dcp.HostMesh(refine=refine)
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.classic_physics())
+    ctx.upload_mesh(m)
+    u = np.zeros(m.n_u + m.n_p)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    rng = np.random.default_rng(SEED + refine)
+    x = rng.uniform(-1, 1, m.n_u + m.n_p)
+    for do_solve_A in (False, True):
+        (ya, ia), (yb, ib) = _fused_vs_per_step(
+            ctx, lambda: ctx.block_preconditioner_vmult(x, do_solve_A=do_solve_A))
+        assert ia == ib and ia > 0
+        assert np.array_equal(ya, yb)
+    if refine <= 2:
+        def solve():
+            ctx.set_state(dcp.NSE_SOLUTION, u)
+            rc, outer, inner = ctx.solve_nse()
+            return rc, outer, inner, ctx.get_state(dcp.NSE_SOLUTION)
+        a, b = _fused_vs_per_step(ctx, solve)
+        assert a[:3] == b[:3] and a[0] == 0
+        assert np.array_equal(a[3], b[3])
+    ctx.close()
+
+
+@pytest.mark.parametrize("force_reorth", [None, 4, 9])
+def test_schur_launch_ahead_is_bitwise_the_serial_loop(monkeypatch, force_reorth):
+    """The inner Schur GMRES enqueues Arnoldi step k+1 before reading step k
+    back, also ahead of the every-5th-step loss-of-orthogonality test; when
+    that test triggers (forced here at inner step 4 or 9 through a test hook),
+    the launched-ahead step is redone on the re-orthogonalised vector. Either
+    way the iterates must be bitwise those of the serial loop."""
+    m = dcp.HostMesh(refine=2)
+    if force_reorth is not None:
+        monkeypatch.setenv("DCP_TEST_FORCE_REORTH_AT", str(force_reorth))
+    res = []
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("DCP_SCHUR_AHEAD", ahead)
+        ctx = dcp.Context()
+        ctx.set_physics(dcp.classic_physics())
+        ctx.upload_mesh(m)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
+        ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        x = np.random.default_rng(SEED).uniform(-1, 1, m.n_u + m.n_p)
+        res.append(ctx.block_preconditioner_vmult(x))
+        ctx.close()
+    (ya, ia), (yb, ib) = res
+    assert ia == ib and ia > 10
+    assert np.array_equal(ya, yb)
