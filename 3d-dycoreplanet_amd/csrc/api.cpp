@@ -850,6 +850,8 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
     }
     ensure_workspaces(*c);
     if (const char* e = std::getenv("DCP_SCHUR_AHEAD")) c->schur_ahead = std::atoi(e) != 0;
+    if (const char* e = std::getenv("DCP_SCHUR_READY_FLAG"))
+      c->schur_ready_flag = std::atoi(e) != 0;
     if (const char* e = std::getenv("DCP_TEST_FORCE_REORTH_AT"))
       c->test_force_reorth_at = std::atoi(e);
     *out = c.release();

@@ -163,12 +163,14 @@ struct Ctx {
   // counter (the granule tags), CU count (residency bound), DCP_OPT_FUSED_CHAIN
   DBuf<double> chain_gran;
   unsigned long long chain_seq = 0;
+  unsigned long long spec_seq = 0;   // inner Schur GMRES step numbers (ready flags)
   int n_cus = 0;
   bool fused_chain = true;
   // test hooks, read at context creation: DCP_SCHUR_AHEAD=0 turns the inner
   // Schur GMRES's launch-ahead off; DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger
   bool schur_ahead = true;
+  bool schur_ready_flag = true;   // DCP_SCHUR_READY_FLAG=0: events instead
   int test_force_reorth_at = -1;
   bool nse_assembled = false, precond_built = false, T_matrix_ok = false, T_rhs_ok = false;
   // Krylov workspaces (lazily sized)

@@ -382,7 +382,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
                                                       double* __restrict__ part0,
                                                       double* __restrict__ part1,
                                                       const double* __restrict__ nrm_part,
-                                                      int nb_nrm, double* nrm_store) {
+                                                      int nb_nrm, double* nrm_store,
+                                                      StepReady ready) {
   __shared__ double quarter[3][64];
   __shared__ double sm[4];
   __shared__ double cf_sh;
@@ -405,7 +406,17 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
     if (threadIdx.x == 0) {
       const double nv = sqrt(tot);
       cf_sh = nv != 0 ? 1.0 / nv : 1.0;
-      if (blockIdx.x == 0) *nrm_store = nv;
+      if (blockIdx.x == 0) {
+        *nrm_store = nv;
+        if (ready.host) {
+          for (int j = 0; j < ready.n; ++j) ready.host[j] = ready.dev[j];
+          ready.host[kSpNStart] = ready.dev[kSpNStart];
+          ready.host[kSpNorm] = ready.dev[kSpNorm];
+          ready.host[kSpReadyNorm] = nv;
+          __threadfence_system();
+          ready.host[kSpReady] = __longlong_as_double((long long)ready.seq);
+        }
+      }
     }
     __syncthreads();
     cf = cf_sh;
@@ -821,24 +832,25 @@ void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStre
   const dim3 grid(sell_fused_blocks(m.rows));
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<false, true>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{});
   else
     hipLaunchKernelGGL((k_sell_spmv<false, false>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{});
   DCP_HIP_CHECK(hipGetLastError());
 }
 
 void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, double* y,
                      const double* v0, double* part0, double* part1, int n_part,
-                     const double* nrm_part, int nb_nrm, double* nrm_store, hipStream_t s) {
+                     const double* nrm_part, int nb_nrm, double* nrm_store, StepReady ready,
+                     hipStream_t s) {
   const int nb = std::max(sell_fused_blocks(m.rows), n_part);
   if (nb <= 0) return;
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<true, true>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store);
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready);
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store);
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -16,6 +16,7 @@
 // owned entries (Seg) with the partial sums all-reduced before the final
 // fixed-order sum, so every rank takes the same decisions from bitwise equal
 // scalars. Every operator refreshes the ghost entries of its input first.
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <functional>
@@ -54,9 +55,8 @@ constexpr int kSlotD = 261;
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
 constexpr int kHostPartials = 2048;
 // gmres_schur's pipelined Arnoldi steps: one block per step parity,
-// [0, 128) coefficients, kSpNStart, kSpNorm, partials from kSpPart
+// [0, 128) coefficients, kSpNStart, kSpNorm, ..., partials from kSpPart (device.h)
 constexpr int kSpecBase = 4096, kSpecStride = 1280;
-constexpr int kSpNStart = 128, kSpNorm = 129, kSpPart = 192;
 constexpr int kNumSlots = 8192;             // device slots, mirrored in c.hpinned
 static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kHostPartials, "slot layout");
 static_assert(kHostPartials + kChainMaxBlocks <= kSpecBase - 512, "slot layout");
@@ -346,8 +346,11 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   bool reorth = false;
   auto base = [](int it) { return kSpecBase + (it & 1) * kSpecStride; };
   double* const hmir0 = c.comm ? nullptr : c.hmapped;
+  unsigned long long step_seq[2] = {0, 0};
   // Arnoldi step `it`: v_it = src * cf (stored by the SpMV for it > 0), S v_it,
-  // the chain, the readback of the step's block. ahead: cf from the device.
+  // the chain, the readback of the step's block. ahead: cf from the device;
+  // on one GPU the SpMV of a launched-ahead step also raises step it-1's
+  // ready flag (no event between the launches: each costs ~3 us of device time).
   auto launch = [&](int it, double cf, bool ahead) {
     const int B0 = base(it);
     double* w = wbuf[it & 1];
@@ -355,43 +358,78 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+    step_seq[it & 1] = ++c.spec_seq;
+    StepReady rdy{};
+    if (hmir0 && ahead && c.schur_ready_flag)
+      rdy = StepReady{hmir0 + base(it - 1), slot(c, base(it - 1)), it, step_seq[(it - 1) & 1]};
     sell_spmv_fused(c.sell(), src, cf, it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
                     ahead ? slot(c, base(it - 1) + kSpPart) : nullptr, nb,
-                    hmir0 ? hmir0 + B0 + kSpNorm : slot(c, B0 + kSpNorm), c.stream);
+                    slot(c, B0 + kSpNorm), rdy, c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     allreduce(c, part0, 2 * size_t(nbs));
     const int d = it + 1;
     const bool consider = !reorth && (it % 5 == 4);
-    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i.
-    // One GPU: coefficients and final partials go straight to the mapped host
-    // mirror (no copy launch); several: the final partials are all-reduced on
-    // the device first, then copied.
-    double* hmir = hmir0;
-    const double* prev = part0;
-    int nprev = nbs;
+    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i;
+    // coefficients, start norm and final partials into the step's device block
     if (fused_chain_ok(c, g, nb, d)) {  // the whole chain in one launch
       mgs_chain(g, w, chain_vecs(tv, d), d, part0, nbs, consider ? part1 : nullptr,
-                hmir + B0 + kSpNStart, hmir + B0, slot(c, B0 + kSpPart), hmir + B0 + kSpPart, nb,
+                slot(c, B0 + kSpNStart), slot(c, B0), slot(c, B0 + kSpPart), nullptr, nb,
                 c.chain_gran.p, ++c.chain_seq, chain_err(c), c.stream);
-      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
-      return;
+    } else {
+      const double* prev = part0;
+      int nprev = nbs;
+      for (int i = 1; i <= d; ++i) {
+        const bool last = i == d;
+        double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
+        chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
+                             slot(c, B0 + i - 1), nb, i == 1 && consider ? part1 : nullptr,
+                             slot(c, B0 + kSpNStart), nullptr, c.stream);
+        allreduce(c, out, nb);
+        prev = out;
+        nprev = nb;
+      }
     }
-    for (int i = 1; i <= d; ++i) {
-      const bool last = i == d;
-      double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
-      chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
-                           hmir ? hmir + B0 + i - 1 : slot(c, B0 + i - 1), nb,
-                           i == 1 && consider ? part1 : nullptr,
-                           hmir ? hmir + B0 + kSpNStart : slot(c, B0 + kSpNStart),
-                           hmir && last ? hmir + B0 + kSpPart : nullptr, c.stream);
-      allreduce(c, out, nb);
-      prev = out;
-      nprev = nb;
-    }
-    if (!hmir)
+    if (!hmir0 || !c.schur_ready_flag) {  // the step's block down behind an event
       DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B0, slot(c, B0), (kSpPart + nb) * sizeof(double),
                                    hipMemcpyDeviceToHost, c.stream));
-    DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
+      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
+    }
+  };
+  // step `it` complete on the host; returns its block and |w|. One GPU: spin
+  // on the ready flag a launched-ahead next step's SpMV raises, or copy the
+  // block down behind an event now (nothing follows the step yet); several
+  // GPUs: the copy and event launch() queued.
+  auto wait_step = [&](int it, bool ahead_launched, double& norm) -> const double* {
+    if (hmir0 && ahead_launched && c.schur_ready_flag) {
+      const double* hp = hmir0 + base(it);
+      const volatile unsigned long long* f =
+          reinterpret_cast<const volatile unsigned long long*>(hp + kSpReady);
+      for (long spins = 1; *f != step_seq[it & 1]; ++spins) {
+        if ((spins & 0xFFFFF) == 0) {
+          const hipError_t q = hipStreamQuery(c.stream);
+          if (q != hipErrorNotReady && *f != step_seq[it & 1]) {
+            DCP_HIP_CHECK(q);
+            throw std::runtime_error("gmres_schur: stream idle without the step's ready flag");
+          }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+      norm = hp[kSpReadyNorm];
+      return hp;
+    }
+    const int B = base(it);
+    if (hmir0 && c.schur_ready_flag) {
+      DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B, slot(c, B), (kSpPart + nb) * sizeof(double),
+                                   hipMemcpyDeviceToHost, c.stream));
+      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
+    }
+    DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[it & 1]));
+    const double* hp = c.hpinned + B;
+    norm = std::sqrt(block_sum_host(hp + kSpPart, nb));
+    return hp;
   };
   do {
     std::fill(h.begin(), h.end(), 0.0);
@@ -413,7 +451,6 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
       ++accumulated;
       dim = inner + 1;
-      const int B0 = base(inner);
       const bool consider = !reorth && (inner % 5 == 4);
       // launch step inner+1 now unless step inner may change it
       const double rho_pred = rho * (rho / rho_prev);
@@ -421,13 +458,12 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                          accumulated < ctl.max_steps &&
                          rho_pred > 2.0 * ctl.tol;
       if (ahead) launch(inner + 1, 0.0, true);
-      DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[inner & 1]));
+      double norm_vv = 0;
+      const double* hp = wait_step(inner, ahead, norm_vv);
       check_chain_err(c);
-      const double* hp = (hmir0 ? hmir0 : c.hpinned) + B0;
-      if (prev_ahead && hp[kSpNorm] != prev_norm)
+      if (prev_ahead && hp[kSpNorm] != prev_norm)  // the launched-ahead SpMV's 1/|w|
         throw std::runtime_error("gmres_schur: device and host |w| differ");
       hv.assign(hp, hp + dim);
-      double norm_vv = std::sqrt(block_sum_host(hp + kSpPart, nb));
       const double start2 = consider ? hp[kSpNStart] : 0.0;
       for (int i = 0; i < dim; ++i) h[i] = hv[i];
       bool second = reorth;
