@@ -330,6 +330,12 @@ void reciprocal(int n, const double* a, double* y, hipStream_t s);              
 void csr_diag_inverse(int rows, const int32_t* ptr, const int32_t* col, const double* val,
                       double* inv, hipStream_t s);
 // y = sum_i coef[i] * X[i] (accumulated into y), X given as a device array of pointers
+// the same with up to kMgsMaxVecs coefficients and vectors passed by value
+struct CombineArgs {
+  double c[kMgsMaxVecs];
+  const double* x[kMgsMaxVecs];
+};
+void multi_axpy_args(int n, int k, const CombineArgs& a, double* y, hipStream_t s);
 void multi_axpy(int n, int k, const double* coef, const double* const* X, double* y,
                 hipStream_t s);
 // z = a + alpha * b (elementwise, e.g. T_matrix = M + dt K over one pattern)

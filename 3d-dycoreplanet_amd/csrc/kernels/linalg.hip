@@ -376,9 +376,9 @@ __global__ __launch_bounds__(kBlock) void k_mgs_chain(
 #define SELL_LD(p) (*(p))
 template <bool EPI, bool C16>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* __restrict__ x,
-                                                      double cf, double* __restrict__ xs,
+                                                      double cf, double* xs,
                                                       double* __restrict__ y,
-                                                      const double* __restrict__ v0,
+                                                      const double* v0,
                                                       double* __restrict__ part0,
                                                       double* __restrict__ part1,
                                                       const double* __restrict__ nrm_part,
@@ -498,8 +498,9 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   double d0 = 0, d1 = 0;
   if (row < rows) {
     y[row] = acc;
-    if (xs) xs[row] = x[row] * cf;
-    d0 = acc * v0[row];
+    const double xv = x[row] * cf;
+    if (xs) xs[row] = xv;
+    d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
     d1 = acc * acc;
   }
 #pragma unroll
@@ -589,6 +590,14 @@ __global__ void k_multi_axpy(int n, int k, const double* __restrict__ coef,
   for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
     double v = y[i];
     for (int j = 0; j < k; ++j) v += coef[j] * X[j][i];
+    y[i] = v;
+  }
+}
+
+__global__ void k_multi_axpy_args(int n, int k, CombineArgs a, double* __restrict__ y) {
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    double v = y[i];
+    for (int j = 0; j < k; ++j) v += a.c[j] * a.x[j][i];
     y[i] = v;
   }
 }
@@ -916,6 +925,10 @@ void multi_axpy(int n, int k, const double* coef, const double* const* X, double
                 hipStream_t s) {
   if (k <= 0) return;
   hipLaunchKernelGGL(k_multi_axpy, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, coef, X, y);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void multi_axpy_args(int n, int k, const CombineArgs& a, double* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_multi_axpy_args, dim3(grid_for(n)), dim3(kBlock), 0, s, n, k, a, y);
   DCP_HIP_CHECK(hipGetLastError());
 }
 void lincomb(int n, const double* a, double alpha, const double* b, double* z, hipStream_t s) {

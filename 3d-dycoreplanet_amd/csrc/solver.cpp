@@ -100,6 +100,15 @@ void combine(Ctx& c, int n, const std::vector<double>& y, const std::vector<doub
              double* x) {
   const int k = int(y.size());
   if (k == 0) return;
+  if (k <= kMgsMaxVecs) {  // coefficients and vectors as kernel arguments: no copies, no sync
+    CombineArgs a{};
+    for (int j = 0; j < k; ++j) {
+      a.c[j] = y[j];
+      a.x[j] = X[j];
+    }
+    multi_axpy_args(n, k, a, x, c.stream);
+    return;
+  }
   std::vector<const double*> ptrs(X.begin(), X.begin() + k);
   DCP_HIP_CHECK(hipMemcpyAsync(c.coef.p, y.data(), k * sizeof(double), hipMemcpyHostToDevice, c.stream));
   DCP_HIP_CHECK(hipMemcpyAsync(c.ptrs.p, ptrs.data(), k * sizeof(double*), hipMemcpyHostToDevice,
@@ -152,6 +161,11 @@ double block_sum_host(const double* p, int nb) {
 // One-launch chains (k_mgs_chain): one GPU, every workgroup resident, w in
 // registers. The timeout flag lives in mapped host memory and is sticky.
 constexpr int kChainErr = 8000;
+// the inner Schur GMRES restart's residual: |p| hand-over block (mapped host),
+// its nb partials (device slots)
+constexpr int kResBlock = 6784, kResPart = 7040;
+static_assert(kSpecBase + 2 * kSpecStride <= kResBlock && kResBlock + kSpPart <= kChainErr &&
+                  kResPart + kChainMaxBlocks <= kNumSlots, "slot layout");
 static_assert(kSpecBase + 2 * kSpecStride <= kChainErr && kChainErr < kNumSlots, "slot layout");
 bool fused_chain_ok(const Ctx& c, Seg g, int nb, int dim) {
   return !c.comm && c.fused_chain && c.hmapped && mgs_chain_fits(g.n, nb, dim, c.n_cus);
@@ -163,6 +177,24 @@ void check_chain_err(Ctx& c) {
     throw std::runtime_error("Gram-Schmidt chain: a workgroup timed out waiting for a hand-off");
   }
 }
+// Host spin on a sequence flag a kernel writes to mapped host memory; throws
+// if the stream went idle (or failed) without raising it.
+void spin_until(Ctx& c, const volatile unsigned long long* f, unsigned long long seq) {
+  for (long spins = 1; *f != seq; ++spins) {
+    if ((spins & 0xFFFFF) == 0) {
+      const hipError_t q = hipStreamQuery(c.stream);
+      if (q != hipErrorNotReady && *f != seq) {
+        DCP_HIP_CHECK(q);
+        throw std::runtime_error("gmres_schur: stream idle without the ready flag");
+      }
+    }
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+}
+
 ChainVecs chain_vecs(const std::vector<double*>& V, int dim) {
   ChainVecs cv{};
   for (int i = 0; i < dim; ++i) cv.v[i] = V[i];
@@ -351,10 +383,13 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   // the chain, the readback of the step's block. ahead: cf from the device;
   // on one GPU the SpMV of a launched-ahead step also raises step it-1's
   // ready flag (no event between the launches: each costs ~3 us of device time).
-  auto launch = [&](int it, double cf, bool ahead) {
+  // res_seq != 0 (step 0 only): launched ahead of the restart's convergence
+  // check, from the unscaled residual p: v_0 = p/|p| with |p| from the
+  // kResPart partials, and |p| handed to the host in the residual block.
+  auto launch = [&](int it, double cf, bool ahead, unsigned long long res_seq = 0) {
     const int B0 = base(it);
     double* w = wbuf[it & 1];
-    double* src = it == 0 ? tv[0] : wbuf[(it - 1) & 1];
+    double* src = it == 0 ? (res_seq ? p : tv[0]) : wbuf[(it - 1) & 1];
     halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
@@ -362,9 +397,11 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     StepReady rdy{};
     if (hmir0 && ahead && c.schur_ready_flag)
       rdy = StepReady{hmir0 + base(it - 1), slot(c, base(it - 1)), it, step_seq[(it - 1) & 1]};
-    sell_spmv_fused(c.sell(), src, cf, it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
-                    ahead ? slot(c, base(it - 1) + kSpPart) : nullptr, nb,
-                    slot(c, B0 + kSpNorm), rdy, c.stream);
+    if (res_seq) rdy = StepReady{hmir0 + kResBlock, slot(c, B0), 0, res_seq};
+    const double* nrm_part = res_seq ? slot(c, kResPart)
+                                     : (ahead ? slot(c, base(it - 1) + kSpPart) : nullptr);
+    sell_spmv_fused(c.sell(), src, cf, it > 0 || res_seq ? tv[it] : nullptr, w, tv[0], part0,
+                    part1, nbs, nrm_part, nb, slot(c, B0 + kSpNorm), rdy, c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     allreduce(c, part0, 2 * size_t(nbs));
     const int d = it + 1;
@@ -402,21 +439,8 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   auto wait_step = [&](int it, bool ahead_launched, double& norm) -> const double* {
     if (hmir0 && ahead_launched && c.schur_ready_flag) {
       const double* hp = hmir0 + base(it);
-      const volatile unsigned long long* f =
-          reinterpret_cast<const volatile unsigned long long*>(hp + kSpReady);
-      for (long spins = 1; *f != step_seq[it & 1]; ++spins) {
-        if ((spins & 0xFFFFF) == 0) {
-          const hipError_t q = hipStreamQuery(c.stream);
-          if (q != hipErrorNotReady && *f != step_seq[it & 1]) {
-            DCP_HIP_CHECK(q);
-            throw std::runtime_error("gmres_schur: stream idle without the step's ready flag");
-          }
-        }
-#if defined(__x86_64__)
-        __builtin_ia32_pause();
-#endif
-      }
-      std::atomic_thread_fence(std::memory_order_acquire);
+      spin_until(c, reinterpret_cast<const volatile unsigned long long*>(hp + kSpReady),
+                 step_seq[it & 1]);
       norm = hp[kSpReadyNorm];
       return hp;
     }
@@ -438,16 +462,35 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     else
       schur_vmult(c, x, p);
     sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
-    copy(n, p, tv[0], c.stream);        // identity preconditioner
-    double rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
-    st = ctl.check(accumulated, rho);
-    if (st != kIterate) break;
+    double rho;
+    if (hmir0 && c.schur_ready_flag && c.schur_ahead) {
+      // |p| from nb block partials (the host sums them in the device's order);
+      // step 0 runs while the host checks convergence (wasted scratch if so)
+      dot_partial(g, p, p, slot(c, kResPart), nb, c.stream);
+      const unsigned long long rs = ++c.spec_seq;
+      launch(0, 1.0, false, rs);
+      const volatile unsigned long long* f =
+          reinterpret_cast<const volatile unsigned long long*>(hmir0 + kResBlock + kSpReady);
+      spin_until(c, f, rs);
+      rho = hmir0[kResBlock + kSpReadyNorm];
+      st = ctl.check(accumulated, rho);
+      if (st != kIterate) {
+        DCP_HIP_CHECK(hipStreamSynchronize(c.stream));  // let the unneeded step finish
+        check_chain_err(c);
+        break;
+      }
+    } else {
+      copy(n, p, tv[0], c.stream);  // identity preconditioner
+      rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
+      st = ctl.check(accumulated, rho);
+      if (st != kIterate) break;
+      scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
+      launch(0, 1.0, false);
+    }
     gamma[0] = rho;
-    scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
     double rho_prev = rho;
     double prev_norm = 0;   // |w| of the previous step (host value)
     bool prev_ahead = false;
-    launch(0, 1.0, false);
     for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
       ++accumulated;
       dim = inner + 1;

@@ -750,6 +750,10 @@ class DeviceBuffer:
             raise DcpError(DCP_ERR_DEVICE, f"hipMalloc failed ({rc})")
         self.ptr = p.value
         hip().hipMemset(C.c_void_p(self.ptr), 0, max(self.n, 1) * 8)  # zero-initialised
+        # the memset runs on the null stream, which the context's non-blocking
+        # stream does not wait for: finish it before the buffer is handed over
+        # (dst doubles as the inner solvers' initial guess, as in the reference)
+        hip().hipDeviceSynchronize()
 
     def upload(self, a):
         a = np.ascontiguousarray(a, dtype=np.float64)

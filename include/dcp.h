@@ -202,7 +202,10 @@ int dcp_nse_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst);          /*
  * GMRES (block_schur_preconditioner.hpp:59-67). */
 int dcp_velocity_vmult(dcp_ctx* ctx, const double* d_src_u, double* d_dst_u);
 int dcp_schur_vmult(dcp_ctx* ctx, const double* d_src_p, double* d_dst_p);    /* schur_complement.hpp:143-150 */
-/* BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70). */
+/* BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70).
+ * As there, d_dst's pressure block is the inner Schur GMRES's initial guess
+ * (and its velocity block the A-GMRES's when do_solve_A): pass it zeroed, or
+ * holding what the caller's Krylov space left there. */
 int dcp_block_preconditioner_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst,
                                    int do_solve_A, int* inner_iterations);
 

@@ -29,7 +29,13 @@ for name, env, fused in (("all on", {}, True), ("per-step chain", {}, False),
     ctx.assemble_nse_system()
     ctx.build_nse_preconditioner()
     out = []
+    xin = np.random.default_rng(7).uniform(-1, 1, m.n_u + m.n_p)
     for r in range(REPS):
+        if os.environ.get("MODE") == "prec":
+            x, inner = ctx.block_preconditioner_vmult(xin, do_solve_A=False)
+            out.append((inner, hashlib.sha1(x.tobytes()).hexdigest()[:10],
+                        float(np.abs(x[m.n_u:]).max())))
+            continue
         ctx.set_state(dcp.NSE_SOLUTION, u)
         rc, outer, inner = ctx.solve_nse()
         x = ctx.get_state(dcp.NSE_SOLUTION)
