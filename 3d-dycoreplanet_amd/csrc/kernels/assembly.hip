@@ -657,23 +657,32 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   if (!want_matrix) return;
   __syncthreads();
   // all four waves: read-modify-write / first-touch store of the 7857 doubles
-  for (int e0 = tid; e0 < kScatterElems; e0 += kNseThreads * kScatterBatch) {
+  // (timing probes only: DCP_ASM_STOREONLY drops the reads, DCP_ASM_NOWRITE
+  // all but the first block's writes; both give wrong matrices)
+#ifndef DCP_ASM_STOREONLY
+#define DCP_ASM_STOREONLY 0
+#endif
+#ifndef DCP_ASM_NOWRITE
+#define DCP_ASM_NOWRITE 0
+#endif
+  constexpr int kElems = DCP_ASM_NOWRITE ? 9 : kScatterElems;
+  for (int e0 = tid; e0 < kElems; e0 += kNseThreads * kScatterBatch) {
     double old[kScatterBatch];
 #pragma unroll
     for (int j = 0; j < kScatterBatch; ++j) {
       const int e = e0 + j * kNseThreads;
       old[j] = 0.0;
-      if (e < kScatterElems) {
+      if (e < kElems) {
         bool add;
         double v;
         const double* dst = scatter_target(sh, out, e, add, v);
-        if (add) old[j] = *dst;
+        if (add && !DCP_ASM_STOREONLY) old[j] = *dst;
       }
     }
 #pragma unroll
     for (int j = 0; j < kScatterBatch; ++j) {
       const int e = e0 + j * kNseThreads;
-      if (e < kScatterElems) {
+      if (e < kElems) {
         bool add;
         double v;
         double* dst = scatter_target(sh, out, e, add, v);
