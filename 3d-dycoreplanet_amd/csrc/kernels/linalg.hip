@@ -199,7 +199,13 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
 // k_chain_add_and_dot uses, so the chain is bitwise the per-step one.
 // Spins are bounded (an unbounded wait would hang the device): a workgroup
 // that gives up writes 1 to *err and the host throws.
-constexpr int kMgsElems = 4;
+#ifndef DCP_MGS_ELEMS
+#define DCP_MGS_ELEMS 8
+#endif
+#ifndef DCP_MGS_SLEEP
+#define DCP_MGS_SLEEP 1
+#endif
+constexpr int kMgsElems = DCP_MGS_ELEMS;
 constexpr long kMgsMaxSpins = 1L << 21;
 typedef unsigned int mgs_u4 __attribute__((ext_vector_type(4)));
 
@@ -247,7 +253,7 @@ __device__ inline double granule_coef(const double* gran, int nb, unsigned long 
       if (l == 0) *err = 1.0;
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (DCP_MGS_SLEEP) __builtin_amdgcn_s_sleep(DCP_MGS_SLEEP);
   }
   double v[4] = {l < nb ? granule_value(q0) : 0.0, l + 64 < nb ? granule_value(q1) : 0.0,
                  l + 128 < nb ? granule_value(q2) : 0.0, l + 192 < nb ? granule_value(q3) : 0.0};
@@ -794,9 +800,16 @@ int chain_blocks(int n) {
   // >= 256 workgroups (one per CU) even for the 2e5-long pressure vectors: the
   // chain steps are latency-bound, so width beats the cost of each block
   // re-summing the previous step's nb partials.
-  int nb = (n + 1023) / 1024;
+#ifndef DCP_CHAIN_MIN_BLOCKS
+#define DCP_CHAIN_MIN_BLOCKS 256
+#endif
+#ifndef DCP_CHAIN_PER_BLOCK
+#define DCP_CHAIN_PER_BLOCK 2048
+#endif
+  int nb = (n + DCP_CHAIN_PER_BLOCK - 1) / DCP_CHAIN_PER_BLOCK;
   nb = ((nb + 63) / 64) * 64;
-  return nb < 256 ? 256 : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
+  return nb < DCP_CHAIN_MIN_BLOCKS ? DCP_CHAIN_MIN_BLOCKS
+                                   : (nb > kChainMaxBlocks ? kChainMaxBlocks : nb);
 }
 
 void dot_partial(Seg g, const double* a, const double* b, double* partials, int nb, hipStream_t s) {
