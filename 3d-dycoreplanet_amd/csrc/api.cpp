@@ -174,7 +174,7 @@ void need_ready(Ctx& c) {
 struct HostPrep {
   int nv = 0;
   std::vector<int32_t> q2, pd, td;
-  std::vector<double> xyz;
+  std::vector<double> geo;  // [n_cells][64][3] MappingQ(3) support points
   std::vector<NodeConstraint> vc;
   std::vector<uint8_t> Tfix;
   std::vector<double> Tbc;
@@ -199,11 +199,11 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   auto& q2 = h.q2;
   auto& pd = h.pd;
   auto& td = h.td;
-  auto& xyz = h.xyz;
   q2.assign(size_t(n_cells) * 27, 0);
   pd.assign(size_t(n_cells) * 8, 0);
   td.assign(size_t(n_cells) * 8, 0);
-  xyz.assign(size_t(nv) * 3, 0.0);
+  h.geo.assign(cell_geometry, cell_geometry + size_t(n_cells) * 3 * kMapPts);
+  for (double x : h.geo) require(std::isfinite(x), DCP_ERR_INVALID, "non-finite cell geometry");
   std::vector<char> seen(nv, 0);
   for (int cell = 0; cell < n_cells; ++cell) {
     const int32_t* d = cell_nse_dofs + size_t(cell) * kNseDofs;
@@ -216,11 +216,7 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
         const int node = d[i] / 3;
         if (s.comp == 0) {
           q2[size_t(cell) * 27 + s.lex] = node;
-          if (!seen[node]) {
-            seen[node] = 1;
-            for (int k = 0; k < 3; ++k)
-              xyz[3 * size_t(node) + k] = cell_geometry[(size_t(cell) * 27 + s.lex) * 3 + k];
-          }
+          seen[node] = 1;
         } else {
           require(q2[size_t(cell) * 27 + s.lex] == node, DCP_ERR_UNSUPPORTED,
                   "velocity components of one support point must share a node");
@@ -511,72 +507,84 @@ std::vector<int32_t> rcm_order(int n, const std::vector<int32_t>& ptr,
 // than 2^16 and are stored as 16-bit offsets from a per-slice base (10 instead
 // of 12 bytes per entry); the inner Schur GMRES then runs in that order.
 // pmap: CSR entry -> SELL position (k_schur_form writes through it).
-// Radially separable Q2 geometry (the hypershell of SphericalManifold: node
-// (a,b,c) of every cell sits at r_c * phi_ab, local c radial). Then
+// Radially separable MappingQ(3) geometry (the hyper_shell under
+// SphericalManifold: support point (a,b,c) of every cell at rho_c Phi_ab, c
+// the radial index; the cubic cells have |Phi_ab| = 1, the trilinear (9.2
+// MappingQ1) cells the bilinear blend of the corner directions). Then
 //   X = R(zeta) Phi(xi, eta),  J = [R Phi_xi | R Phi_eta | R' Phi],
 //   J^-1 rows = m0 / R, m1 / R, m2 / R',  det J = R^2 R' D2,
 // with m0 = Phi_eta x Phi / D2, m1 = Phi x Phi_xi / D2, m2 = Phi_xi x Phi_eta / D2,
 // D2 = (Phi_xi x Phi_eta) . Phi at the 9 tangential Gauss points: one table per
-// column of cells, three radii per cell. Returns false (general on-the-fly
-// geometry) unless every cell fits within 1e-13 relative.
+// column of cells (and mapping kind), four radii per cell. Returns false
+// (general streamed geometry) unless every cell fits within 1e-13 relative.
 // node(cell, t): the coordinates of lexicographic support point t of a cell.
-// Also groups the cells into radial layers (same three node radii) with, per
-// layer and Gauss point, 1/R, 1/R' and R^2 R' of R(zeta) = sum_c L_c(zeta) r_c.
+// Also groups the cells into radial layers (same support radii) with, per
+// layer and Gauss point, 1/R, 1/R' and R^2 R' of R(zeta) = sum_c L_c(zeta) rho_c.
 template <class NodeFn>
 bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
                         std::vector<double>& colgeo, std::vector<int32_t>& layer,
                         std::vector<double>& laygeo) {
   std::vector<double> rad;
-  auto l2 = [](int i, double x) {
-    return i == 0 ? 2 * (x - 0.5) * (x - 1) : i == 1 ? -4 * x * (x - 1) : 2 * x * (x - 0.5);
-  };
-  auto dl2 = [](int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8 * x + 4 : 4 * x - 1; };
   constexpr double tol = 1e-13;
+  constexpr int kP = kMapPts1, kP2 = kMapPts1 * kMapPts1;
   col.assign(n_cells, -1);
-  rad.assign(3 * size_t(n_cells), 0.0);
+  rad.assign(kP * size_t(n_cells), 0.0);
   colgeo.clear();
-  std::vector<std::vector<double>> col_phi;  // [col][27] phi_ab of the column
+  std::vector<std::vector<double>> col_phi;  // [col][16 * 3] Phi_ab of the column
   struct Key {
-    int64_t k[3];
-    bool operator==(const Key& o) const { return k[0] == o.k[0] && k[1] == o.k[1] && k[2] == o.k[2]; }
+    int64_t k[6];
+    bool operator==(const Key& o) const {
+      for (int i = 0; i < 6; ++i)
+        if (k[i] != o.k[i]) return false;
+      return true;
+    }
   };
   struct KeyHash {
     size_t operator()(const Key& a) const {
-      return size_t(a.k[0] * 73856093) ^ size_t(a.k[1] * 19349663) ^ size_t(a.k[2] * 83492791);
+      size_t h = 0;
+      for (int i = 0; i < 6; ++i) h = h * 1000003u ^ size_t(a.k[i]);
+      return h;
     }
   };
-  std::unordered_map<Key, int, KeyHash> cols;
+  std::unordered_map<Key, std::vector<int>, KeyHash> cols;
   for (int cell = 0; cell < n_cells; ++cell) {
-    double phi[9][3], r[3];
-    for (int c = 0; c < 3; ++c) {
-      double rc = 0;
-      for (int ab = 0; ab < 9; ++ab) {
-        const double* X = node(cell, ab + 9 * c);
-        const double rr = std::sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
-        if (ab == 0) rc = rr;
-        if (!(std::fabs(rr - rc) <= tol * rc)) return false;
+    double phi[kP2][3], r[kP];
+    for (int c = 0; c < kP; ++c) {
+      const double* X0 = node(cell, kP2 * c);
+      const double rc = std::sqrt(X0[0] * X0[0] + X0[1] * X0[1] + X0[2] * X0[2]);
+      if (!(rc > 0)) return false;
+      for (int ab = 0; ab < kP2; ++ab) {
+        const double* X = node(cell, ab + kP2 * c);
         for (int d = 0; d < 3; ++d) {
-          if (c == 0) phi[ab][d] = X[d] / rr;
-          else if (!(std::fabs(X[d] / rr - phi[ab][d]) <= tol)) return false;
+          if (c == 0) phi[ab][d] = X[d] / rc;
+          else if (!(std::fabs(X[d] / rc - phi[ab][d]) <= tol)) return false;
         }
       }
       r[c] = rc;
     }
-    if (!(r[0] < r[1] && r[1] < r[2])) return false;
-    for (int c = 0; c < 3; ++c) rad[3 * size_t(cell) + c] = r[c];
-    Key key{{std::llround(phi[4][0] * 1e9), std::llround(phi[4][1] * 1e9), std::llround(phi[4][2] * 1e9)}};
-    auto it = cols.find(key);
-    if (it == cols.end()) {
-      const int id = int(col_phi.size());
-      cols.emplace(key, id);
-      col_phi.emplace_back(&phi[0][0], &phi[0][0] + 27);
-      col[cell] = id;
-    } else {
-      const auto& ph = col_phi[it->second];
-      for (int i = 0; i < 27; ++i)
-        if (!(std::fabs(ph[i] - (&phi[0][0])[i]) <= tol)) return false;
-      col[cell] = it->second;
+    for (int c = 1; c < kP; ++c)
+      if (!(r[c - 1] < r[c])) return false;
+    for (int c = 0; c < kP; ++c) rad[kP * size_t(cell) + c] = r[c];
+    Key key{{std::llround(phi[0][0] * 1e9), std::llround(phi[0][1] * 1e9),
+             std::llround(phi[0][2] * 1e9), std::llround(phi[5][0] * 1e9),
+             std::llround(phi[5][1] * 1e9), std::llround(phi[5][2] * 1e9)}};
+    auto& cand = cols[key];
+    int id = -1;
+    for (int k : cand) {
+      const auto& ph = col_phi[k];
+      bool same = true;
+      for (int i = 0; i < 3 * kP2 && same; ++i) same = std::fabs(ph[i] - (&phi[0][0])[i]) <= tol;
+      if (same) {
+        id = k;
+        break;
+      }
     }
+    if (id < 0) {
+      id = int(col_phi.size());
+      cand.push_back(id);
+      col_phi.emplace_back(&phi[0][0], &phi[0][0] + 3 * kP2);
+    }
+    col[cell] = id;
   }
   colgeo.assign(col_phi.size() * 90, 0.0);
   for (size_t k = 0; k < col_phi.size(); ++k) {
@@ -584,12 +592,12 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
     for (int q1 = 0; q1 < 3; ++q1)
       for (int q0 = 0; q0 < 3; ++q0) {
         double F[3] = {0, 0, 0}, Fx[3] = {0, 0, 0}, Fy[3] = {0, 0, 0};
-        for (int b = 0; b < 3; ++b)
-          for (int a = 0; a < 3; ++a) {
-            const double la = l2(a, kGaussX[q0]), lb = l2(b, kGaussX[q1]);
-            const double da = dl2(a, kGaussX[q0]), db = dl2(b, kGaussX[q1]);
+        for (int b = 0; b < kP; ++b)
+          for (int a = 0; a < kP; ++a) {
+            const double la = map_lag(a, kGaussX[q0]), lb = map_lag(b, kGaussX[q1]);
+            const double da = map_dlag(a, kGaussX[q0]), db = map_dlag(b, kGaussX[q1]);
             for (int d = 0; d < 3; ++d) {
-              const double v = ph[3 * (a + 3 * b) + d];
+              const double v = ph[3 * (a + kP * b) + d];
               F[d] += la * lb * v;
               Fx[d] += da * lb * v;
               Fy[d] += la * db * v;
@@ -619,16 +627,16 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
   laygeo.clear();
   std::unordered_map<int64_t, int> ids;
   for (int cell = 0; cell < n_cells; ++cell) {
-    const double* r = &rad[3 * size_t(cell)];
-    const int64_t key = std::llround(r[0] * 1e12) * 1000003 + std::llround(r[2] * 1e12);
+    const double* r = &rad[kP * size_t(cell)];
+    const int64_t key = std::llround(r[0] * 1e12) * 1000003 + std::llround(r[kP - 1] * 1e12);
     auto it = ids.find(key);
     if (it == ids.end()) {
       it = ids.emplace(key, int(laygeo.size() / 9)).first;
       for (int q = 0; q < 3; ++q) {
         double R = 0, Rp = 0;
-        for (int k = 0; k < 3; ++k) {
-          R += l2(k, kGaussX[q]) * r[k];
-          Rp += dl2(k, kGaussX[q]) * r[k];
+        for (int k = 0; k < kP; ++k) {
+          R += map_lag(k, kGaussX[q]) * r[k];
+          Rp += map_dlag(k, kGaussX[q]) * r[k];
         }
         laygeo.push_back(1.0 / R);
         laygeo.push_back(1.0 / Rp);
@@ -932,8 +940,8 @@ int dcp_mesh_geometry_info(int n_cells, const double* cell_geometry, int* separa
     std::vector<int32_t> col, layer;
     std::vector<double> colgeo, laygeo;
     const bool sep = separable_geometry(
-        n_cells, [&](int cell, int t) { return cell_geometry + 81 * size_t(cell) + 3 * t; }, col,
-        colgeo, layer, laygeo);
+        n_cells, [&](int cell, int t) { return cell_geometry + 3 * kMapPts * size_t(cell) + 3 * t; },
+        col, colgeo, layer, laygeo);
     if (separable) *separable = sep ? 1 : 0;
     if (n_columns) *n_columns = sep ? int(colgeo.size() / 90) : 0;
     if (n_layers) *n_layers = sep ? int(laygeo.size() / 9) : 0;
@@ -977,7 +985,6 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
-    const auto& xyz = h.xyz;
     const auto& vc = h.vc;
     const auto &Ap = h.Ap, &Ac = h.Ac, &Btp = h.Btp, &Btc = h.Btc, &Bp = h.Bp, &Bc = h.Bc,
                &Tp = h.Tp, &Tc = h.Tc;
@@ -1003,7 +1010,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.cell_q2.upload(q2);
     c.cell_p.upload(pd);
     c.cell_T.upload(td);
-    c.xyz.upload(xyz);
+    c.cell_geo.upload(h.geo);
     c.diameter.upload(std::vector<double>(cell_diameter, cell_diameter + n_cells));
     c.vcon.upload(vc);
     c.T_fixed.upload(Tfix);
@@ -1177,13 +1184,17 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         std::vector<int32_t> col, layer;
         std::vector<double> colgeo, laygeo;
         c.mf_separable = separable_geometry(
-            n_cells, [&](int cell, int t) { return &xyz[3 * size_t(q2[27 * size_t(cell) + t])]; },
+            n_cells, [&](int cell, int t) { return &h.geo[3 * kMapPts * size_t(cell) + 3 * t]; },
             col, colgeo, layer, laygeo);
         if (c.mf_separable) {
           c.mf_col.upload(col);
           c.mf_colgeo.upload(colgeo);
           c.mf_layer.upload(layer);
           c.mf_laygeo.upload(laygeo);
+        } else {
+          // general mesh: J^-1 / JxW per Gauss point, tree order (2160 B per cell)
+          c.mf_geo_tree.alloc(size_t(n_cells) * 270);
+          mf_geometry(c.cd(), nullptr, c.mf_geo_tree.p, c.stream);
         }
       }
     }
@@ -1835,15 +1846,15 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
       std::vector<int> f(c.color_ptr.begin(), c.color_ptr.end() - 1);
       for (int cell = 0; cell < nc; ++cell) ccells[f[color[cell]]++] = cell;
     }
-    // virtual Q2 geometry = trilinear interpolation of the vertices: the
-    // classic temperature-matrix kernel then integrates on MappingQ1
+    // cell geometry = the trilinear map of the vertices at the 64 support
+    // points: the classic temperature kernels then integrate on MappingQ1
     // (temperature_mapping(1), FEEC.tpp:20) exactly
     std::vector<int32_t> q2(size_t(nc) * 27);
-    std::vector<double> xyz(size_t(nc) * 81);
-    for (int cell = 0; cell < nc; ++cell)
-      for (int k = 0; k < 27; ++k) {
-        const double t[3] = {0.5 * (k % 3), 0.5 * ((k / 3) % 3), 0.5 * (k / 9)};
-        q2[27 * size_t(cell) + k] = 27 * cell + k;
+    std::vector<double> geo(size_t(nc) * 3 * kMapPts);
+    for (int cell = 0; cell < nc; ++cell) {
+      for (int k = 0; k < 27; ++k) q2[27 * size_t(cell) + k] = 27 * cell + k;
+      for (int k = 0; k < kMapPts; ++k) {
+        const double t[3] = {kGL3[k % 4], kGL3[(k / 4) % 4], kGL3[k / 16]};
         for (int d = 0; d < 3; ++d) {
           double x = 0;
           for (int v = 0; v < 8; ++v) {
@@ -1851,9 +1862,10 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
                              ((v >> 2) ? t[2] : 1 - t[2]);
             x += w * m->cell_vertices[24 * size_t(cell) + 3 * v + d];
           }
-          xyz[81 * size_t(cell) + 3 * k + d] = x;
+          geo[3 * kMapPts * size_t(cell) + 3 * k + d] = x;
         }
       }
+    }
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
     c.feec = true;
     c.have_mesh = false;
@@ -1891,7 +1903,7 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     c.fe_fixed.upload(fixed);
     c.cell_T.upload(td);
     c.cell_q2.upload(q2);
-    c.xyz.upload(xyz);
+    c.cell_geo.upload(geo);
     c.T_fixed.upload(Tfix);
     c.T_bc.upload(Tbc);
     c.color_cells.upload(ccells);
@@ -2060,25 +2072,22 @@ struct dcp_host_mesh {
   Constraints nse, T;
   TemperatureDofs tdofs;
   std::vector<int32_t> cell_nse;
-  std::vector<double> cell_geom;
   std::unique_ptr<FeecDofs> feec;  // built on first request
 };
 
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
-                                    int temperature_degree, int normal_mode) {
+                                    int temperature_degree, int normal_mode,
+                                    int mapping_q_on_all_cells) {
   try {
     auto h = std::make_unique<dcp_host_mesh>();
-    h->mesh = cuboid ? build_cube(refine, length) : build_shell(refine, R0 / length, R1 / length);
-    h->nse = nse_constraints(h->mesh, normal_mode == 1 ? NormalMode::Radial : NormalMode::Consistent);
+    h->mesh = cuboid ? build_cube(refine, length)
+                     : build_shell(refine, R0 / length, R1 / length, mapping_q_on_all_cells != 0);
+    h->nse = nse_constraints(h->mesh, normal_mode == 1   ? NormalMode::Radial
+                                      : normal_mode == 2 ? NormalMode::Consistent
+                                                         : NormalMode::Mapping);
     h->T = temperature_constraints(h->mesh, temperature_degree);
     h->tdofs = temperature_dofs(h->mesh, temperature_degree);
     h->cell_nse = nse_cell_dofs_dealii(h->mesh);
-    const Mesh& m = h->mesh;
-    h->cell_geom.resize(size_t(m.n_cells) * 81);
-    for (int c = 0; c < m.n_cells; ++c)
-      for (int l = 0; l < 27; ++l)
-        for (int d = 0; d < 3; ++d)
-          h->cell_geom[(size_t(c) * 27 + l) * 3 + d] = m.xyz[3 * size_t(m.cell_q2[27 * size_t(c) + l]) + d];
     return h.release();
   } catch (const std::exception& e) {
     g_last_error = e.what();
@@ -2109,7 +2118,7 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
   out->n_vnodes = m.n_vnodes;
   out->cell_nse_dofs = h->cell_nse.data();
   out->cell_T_dofs = h->tdofs.cell_dofs.data();
-  out->cell_geometry = h->cell_geom.data();
+  out->cell_geometry = m.cell_map.data();
   out->cell_diameter = m.cell_diameter.data();
   out->node_xyz = m.xyz.data();
   out->nse = view_of(h->nse);

@@ -81,7 +81,7 @@ struct Ctx {
   int sell_part_len = 0;             // common length of the SELL partial arrays
   // mesh
   DBuf<int32_t> cell_q2, cell_p, cell_T;
-  DBuf<double> xyz, diameter, T_bc;
+  DBuf<double> cell_geo, diameter, T_bc;
   DBuf<NodeConstraint> vcon;
   DBuf<uint8_t> T_fixed;
   std::vector<int> color_ptr;  // cells of colour k: color_cells[color_ptr[k] .. color_ptr[k+1])
@@ -115,6 +115,7 @@ struct Ctx {
   // gather (MfCells / MfGather); 2: colour-class launches (MfData)
   int matrix_free = 1;
   DBuf<double> mf_geo;                  // colour order (see MfData)
+  DBuf<double> mf_geo_tree;             // tree order, non-separable meshes (MfCells::geo)
   DBuf<int32_t> mf_q2, mf_p;
   DBuf<uint64_t> mf_first;
   DBuf<int32_t> mf_cdof;
@@ -140,7 +141,7 @@ struct Ctx {
   bool mf_separable = false;
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
-                   xyz.p,      vcon.p,      mf_cmask.p, mf_vslot.p,
+                   mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p,
                    mf_pslot.p, mf_separable ? mf_col.p : nullptr,
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
@@ -236,7 +237,7 @@ struct Ctx {
     c.cell_q2 = cell_q2.p;
     c.cell_p = cell_p.p;
     c.cell_T = cell_T.p;
-    c.xyz = xyz.p;
+    c.geo = cell_geo.p;
     c.vcon = vcon.p;
     c.T_fixed = T_fixed.p;
     c.T_bc = T_bc.p;

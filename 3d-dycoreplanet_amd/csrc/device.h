@@ -60,7 +60,7 @@ struct CellData {
   const int32_t* cell_q2;   // [n_cells][27] vnode ids (lexicographic)
   const int32_t* cell_p;    // [n_cells][8]  pressure dofs (vertex order)
   const int32_t* cell_T;    // [n_cells][8]  temperature dofs
-  const double* xyz;        // [n_vnodes][3]
+  const double* geo;        // [n_cells][64][3] MappingQ(3) support points (fe_tables.h)
   const NodeConstraint* vcon;  // [n_vnodes]
   const uint8_t* T_fixed;   // [n_T] 1 = Dirichlet
   const double* T_bc;       // [n_T] inhomogeneity (valid where T_fixed)
@@ -93,7 +93,8 @@ void mf_geometry(const CellData& cd, const int32_t* order, double* geo, hipStrea
 
 // Cell-order matrix-free apply (two launches, no colouring):
 //   k_mf_pencil: every cell (tree order) evaluates K_cell C x with its geometry
-//     recomputed from the Q2 node coordinates and stores its 27 velocity
+//     from the radially separable tables (or the streamed per-point J^-1 /
+//     JxW of a general mesh) and stores its 27 velocity
 //     triples and 8 pressure values to their slots in the dof-sorted
 //     incidence list (slot of (cell, t) = rank of the cell among the cells of
 //     node t, ascending cell order);
@@ -111,7 +112,7 @@ struct MfCells {
   int n_u;                     // offset of the pressure block in [u | p]
   const int32_t* cell_q2;      // [n_cells][27] (tree order)
   const int32_t* cell_p;       // [n_cells][8]
-  const double* xyz;           // [n_vnodes][3]
+  const double* geo;           // [n_cells][10][27] J^-1 / JxW (non-separable meshes only)
   const NodeConstraint* vcon;  // [n_vnodes]
   const uint32_t* cmask;       // [n_cells] bit t: local node t is constrained
   const int32_t* vslot;        // [n_cells][27] buf offset (doubles) of the (cell, t) triple

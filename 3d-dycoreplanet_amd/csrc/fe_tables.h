@@ -69,4 +69,33 @@ constexpr double kGaussX[3] = {0.11270166537925831148, 0.5, 0.887298334620741688
 constexpr double kGaussW[3] = {0.27777777777777777778, 0.44444444444444444444,
                                0.27777777777777777778};
 
+// Cell geometry = MappingQ(3) (boussinesq_model.tpp:20, `const MappingQ<dim>
+// mapping` at boussinesq_model.h:211): MappingQGeneric's tensor-product
+// Lagrange basis on the 4 Gauss-Lobatto points of [0,1], i.e. 64 support
+// points per cell in lexicographic order (i + 4j + 16k). A cell the reference
+// maps with MappingQ1 (deal.II 9.2: cells without boundary lines) is passed as
+// the trilinear interpolant at those 64 points, which the cubic basis
+// reproduces exactly.
+constexpr int kMapPts1 = 4;
+constexpr int kMapPts = 64;
+constexpr double kGL3[4] = {0.0, 0.27639320225002103036, 0.72360679774997896964, 1.0};
+
+constexpr double map_lag(int i, double x) {
+  double v = 1.0;
+  for (int j = 0; j < 4; ++j)
+    if (j != i) v *= (x - kGL3[j]) / (kGL3[i] - kGL3[j]);
+  return v;
+}
+constexpr double map_dlag(int i, double x) {
+  double s = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    if (k == i) continue;
+    double v = 1.0 / (kGL3[i] - kGL3[k]);
+    for (int j = 0; j < 4; ++j)
+      if (j != i && j != k) v *= (x - kGL3[j]) / (kGL3[i] - kGL3[j]);
+    s += v;
+  }
+  return s;
+}
+
 }  // namespace dcp

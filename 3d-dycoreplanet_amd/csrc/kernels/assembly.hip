@@ -7,9 +7,9 @@
 //   local_assemble_temperature_matrix + copy                       :748-817
 //   local_assemble_temperature_rhs + copy (matrix_for_bc lift)     :873-964
 //
-// One 256-thread workgroup owns one cell. The Q2 isoparametric geometry is
-// recomputed from the 27 node coordinates (gathered through the cell's node
-// map, 648 B of unique-per-cell traffic instead of 2160 B of stored J^-1/JxW),
+// One 256-thread workgroup owns one cell. The MappingQ(3) geometry of the
+// reference (boussinesq_model.tpp:20) is recomputed from the cell's 64
+// support points (1536 B per cell instead of 2160 B of stored J^-1/JxW),
 // shape tables and per-quadrature physical gradients are staged in LDS, and the
 // 27x27 node-pair Gram sums run as 1x3 register tiles (243 threads). The
 // condensed (AffineConstraints) 3x3 node blocks are added into the block-CSR
@@ -41,6 +41,42 @@ __constant__ double cdL2[3][3] = {{4 * kGaussX[0] - 3, 4 * kGaussX[1] - 3, 4 * k
 __constant__ double cL1[2][3] = {{1 - kGaussX[0], 1 - kGaussX[1], 1 - kGaussX[2]},
                                  {kGaussX[0], kGaussX[1], kGaussX[2]}};
 __constant__ double cW[3] = {kGaussW[0], kGaussW[1], kGaussW[2]};
+// MappingQ(3) 1D basis (Gauss-Lobatto support points) at the 3 Gauss points: [basis][point]
+__constant__ double cL3[4][3] = {
+    {map_lag(0, kGaussX[0]), map_lag(0, kGaussX[1]), map_lag(0, kGaussX[2])},
+    {map_lag(1, kGaussX[0]), map_lag(1, kGaussX[1]), map_lag(1, kGaussX[2])},
+    {map_lag(2, kGaussX[0]), map_lag(2, kGaussX[1]), map_lag(2, kGaussX[2])},
+    {map_lag(3, kGaussX[0]), map_lag(3, kGaussX[1]), map_lag(3, kGaussX[2])}};
+__constant__ double cdL3[4][3] = {
+    {map_dlag(0, kGaussX[0]), map_dlag(0, kGaussX[1]), map_dlag(0, kGaussX[2])},
+    {map_dlag(1, kGaussX[0]), map_dlag(1, kGaussX[1]), map_dlag(1, kGaussX[2])},
+    {map_dlag(2, kGaussX[0]), map_dlag(2, kGaussX[1]), map_dlag(2, kGaussX[2])},
+    {map_dlag(3, kGaussX[0]), map_dlag(3, kGaussX[1]), map_dlag(3, kGaussX[2])}};
+
+// Row i of the MappingQ(3) Jacobian and x_i at Gauss point q from the 64
+// support points X (lexicographic): J[i][e] = sum_n X_n,i dN_n/dxi_e.
+__device__ inline void map_row(const double* X, int q, int i, double& x, double& J0, double& J1,
+                               double& J2) {
+  const int qa = q % 3, qb = (q / 3) % 3, qc = q / 9;
+  x = J0 = J1 = J2 = 0;
+#pragma unroll 1
+  for (int c = 0; c < 4; ++c) {
+    const double lc = cL3[c][qc], dc = cdL3[c][qc];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const double lb = cL3[b][qb], db = cdL3[b][qb];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const double Xi = X[3 * (a + 4 * b + 16 * c) + i];
+        const double la = cL3[a][qa];
+        x += Xi * la * lb * lc;
+        J0 += Xi * cdL3[a][qa] * lb * lc;
+        J1 += Xi * la * db * lc;
+        J2 += Xi * la * lb * dc;
+      }
+    }
+  }
+}
 
 // Lexicographic Q2 node -> hierarchic FE_Q(2) index (inverse of kQ2HierToLex).
 __constant__ int cLexToHier[27] = {0, 10, 1, 8, 24, 9, 2, 11, 3, 16, 22, 17, 20, 26,
@@ -58,26 +94,13 @@ struct Geo {
   double xq[27 * 3];
 };
 
-// 27 threads: Q2 isoparametric mapping at the QGauss(3) points.
+// 27 threads: the MappingQ(3) map at the QGauss(3) points (X: 64 support points).
 __device__ inline void cell_geometry(const double* X, Geo& g, int q) {
-  const int qa = q % 3, qb = (q / 3) % 3, qc = q / 9;
-  double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-  double x[3] = {0, 0, 0};
-#pragma unroll 1
-  for (int n = 0; n < 27; ++n) {
-    const int na = n % 3, nb = (n / 3) % 3, nc = n / 9;
-    const double la = cL2[na][qa], lb = cL2[nb][qb], lc = cL2[nc][qc];
-    const double gx = cdL2[na][qa] * lb * lc, gy = la * cdL2[nb][qb] * lc,
-                 gz = la * lb * cdL2[nc][qc], s = la * lb * lc;
+  double J[3][3];
+  double x[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const double Xi = X[3 * n + i];
-      x[i] += Xi * s;
-      J[i][0] += Xi * gx;
-      J[i][1] += Xi * gy;
-      J[i][2] += Xi * gz;
-    }
-  }
+  for (int i = 0; i < 3; ++i) map_row(X, q, i, x[i], J[i][0], J[i][1], J[i][2]);
+  const int qa = q % 3, qb = (q / 3) % 3, qc = q / 9;
   const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1];
   const double c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2];
   const double c02 = J[1][0] * J[2][1] - J[1][1] * J[2][0];
@@ -220,13 +243,13 @@ constexpr int kRhsLane0 = 160;               // wave 2 lanes 32..58: rhs nodes
 constexpr int kStageA = 405 * 9;
 constexpr int kStageDoubles = kStageA + 216 * 3;
 struct NseSmem {
-  double X[81], U[81], T[8];
+  double X[3 * kMapPts], U[81], T[8];
   Geo geo;
   double D[27 * 27 * 3];   // [q][n][d] reference, then physical gradients
   double S[27 * 27];       // [q][n] shape values
   double W1[27 * 8];       // [q][v] JxW * Q1 value
   double F[27 * 3];        // JxW * rhs integrand (velocity part) per q
-  double stage_pad[559];   // write staging: X..stage_pad (dead by then)
+  double stage_pad[448];   // write staging: X..stage_pad (dead by then)
   double diag[27];         // sum_c |K_(a,c),(a,c)| per node (average-diagonal rule)
   int node[27];
   int pdof[8];
@@ -380,14 +403,12 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   const bool want_matrix = MODE == 1 || out.A != nullptr;
   const bool want_rhs = MODE == 1 || out.rhs != nullptr;
 
+  if (tid < 3 * kMapPts) sh.X[tid] = cd.geo[3 * kMapPts * size_t(cell) + tid];
   if (tid < 27) {
     const int n = cd.cell_q2[27 * size_t(cell) + tid];
     sh.node[tid] = n;
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      sh.X[3 * tid + d] = cd.xyz[3 * size_t(n) + d];
-      sh.U[3 * tid + d] = u_old[3 * size_t(n) + d];
-    }
+    for (int d = 0; d < 3; ++d) sh.U[3 * tid + d] = u_old[3 * size_t(n) + d];
   } else if (tid >= 64 && tid < 72) {
     const int v = tid - 64;
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
@@ -404,19 +425,11 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   for (int i = tid; i < 3 * 729; i += kNseThreads) sh.D[i] = cRef.G2[i];
   __syncthreads();
 
-  // Q2 isoparametric mapping: J[i][e] = sum_n X_n,i dN_n/dxi_e, thread (q, i)
+  // MappingQ(3): J[i][e] = sum_n X_n,i dN_n/dxi_e over the 64 support points, thread (q, i)
   if (tid < 81) {
     const int q = tid / 3, i = tid % 3;
-    double J0 = 0, J1 = 0, J2 = 0, x = 0;
-#pragma unroll 1
-    for (int n = 0; n < 27; ++n) {
-      const double Xi = sh.X[3 * n + i];
-      const double* G = &sh.D[3 * (27 * q + n)];
-      x += Xi * sh.S[27 * q + n];
-      J0 += Xi * G[0];
-      J1 += Xi * G[1];
-      J2 += Xi * G[2];
-    }
+    double J0, J1, J2, x;
+    map_row(sh.X, q, i, x, J0, J1, J2);
     sh.geo.Ji[9 * q + 3 * i + 0] = J0;
     sh.geo.Ji[9 * q + 3 * i + 1] = J1;
     sh.geo.Ji[9 * q + 3 * i + 2] = J2;
@@ -700,15 +713,11 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int32_t* __restrict__ cells,
                                                          PhysicsDev ph, double* A_diag,
                                                          double* Mp_diag) {
-  __shared__ double X[81];
+  __shared__ double X[3 * kMapPts];
   __shared__ Geo geo;
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
-  if (tid < 27) {
-    const int n = cd.cell_q2[27 * size_t(cell) + tid];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) X[3 * tid + d] = cd.xyz[3 * size_t(n) + d];
-  }
+  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   __syncthreads();
   if (tid < 27) cell_geometry(X, geo, tid);
   __syncthreads();
@@ -745,19 +754,14 @@ __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int3
 __global__ __launch_bounds__(64) void k_T_matrix(CellData cd, ScatterMaps sm,
                                                  const int32_t* __restrict__ cells, PhysicsDev ph,
                                                  double* Tmass, double* Tstiff) {
-  __shared__ double X[81];
+  __shared__ double X[3 * kMapPts];
   __shared__ Geo geo;
   __shared__ double G1[27 * 8 * 3];
   __shared__ int dof[8];
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
-  if (tid < 27) {
-    const int n = cd.cell_q2[27 * size_t(cell) + tid];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) X[3 * tid + d] = cd.xyz[3 * size_t(n) + d];
-  } else if (tid >= 32 && tid < 40) {
-    dof[tid - 32] = cd.cell_T[8 * size_t(cell) + tid - 32];
-  }
+  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
+  if (tid >= 32 && tid < 40) dof[tid - 32] = cd.cell_T[8 * size_t(cell) + tid - 32];
   __syncthreads();
   if (tid < 27) cell_geometry(X, geo, tid);
   __syncthreads();
@@ -788,7 +792,7 @@ __global__ __launch_bounds__(64) void k_T_rhs(CellData cd, const int32_t* __rest
                                               const double* __restrict__ T_old,
                                               const double* __restrict__ u_cur, PhysicsDev ph,
                                               double* rhs) {
-  __shared__ double X[81], U[81];
+  __shared__ double X[3 * kMapPts], U[81];
   __shared__ Geo geo;
   __shared__ double G1[27 * 8 * 3];
   __shared__ double Tq[27], Fq[27];
@@ -796,13 +800,11 @@ __global__ __launch_bounds__(64) void k_T_rhs(CellData cd, const int32_t* __rest
   __shared__ int dof[8];
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
+  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   if (tid < 27) {
     const int n = cd.cell_q2[27 * size_t(cell) + tid];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      X[3 * tid + d] = cd.xyz[3 * size_t(n) + d];
-      U[3 * tid + d] = u_cur[3 * size_t(n) + d];
-    }
+    for (int d = 0; d < 3; ++d) U[3 * tid + d] = u_cur[3 * size_t(n) + d];
   } else if (tid >= 32 && tid < 40) {
     const int d = cd.cell_T[8 * size_t(cell) + tid - 32];
     dof[tid - 32] = d;

@@ -46,12 +46,6 @@ constexpr double dl2c(int i, double x) { return i == 0 ? 4 * x - 3 : i == 1 ? -8
 constexpr double l1c(int i, double x) { return i == 0 ? 1 - x : x; }
 
 // 1D Q2 basis n at Gauss point q: value / derivative (geometry precompute)
-__constant__ double mL[3][3] = {{l2c(0, kGaussX[0]), l2c(0, kGaussX[1]), l2c(0, kGaussX[2])},
-                                {l2c(1, kGaussX[0]), l2c(1, kGaussX[1]), l2c(1, kGaussX[2])},
-                                {l2c(2, kGaussX[0]), l2c(2, kGaussX[1]), l2c(2, kGaussX[2])}};
-__constant__ double mD[3][3] = {{dl2c(0, kGaussX[0]), dl2c(0, kGaussX[1]), dl2c(0, kGaussX[2])},
-                                {dl2c(1, kGaussX[0]), dl2c(1, kGaussX[1]), dl2c(1, kGaussX[2])},
-                                {dl2c(2, kGaussX[0]), dl2c(2, kGaussX[1]), dl2c(2, kGaussX[2])}};
 __constant__ double mW[3] = {kGaussW[0], kGaussW[1], kGaussW[2]};
 
 // The apply kernel picks its 1D coefficients by lane index with selects
@@ -129,30 +123,39 @@ __device__ inline void condense(const NodeConstraint& nc, double f[3]) {
   }
 }
 
-// J^-1 (dxi_e/dx_d as [e][d]) and JxW of the Q2 isoparametric map at every
+// J^-1 (dxi_e/dx_d as [e][d]) and JxW of the cell's MappingQ(3) at every
 // Gauss point, stored [cell][k][q] (k < 9: J^-1, k = 9: JxW). Same formulas as
-// the assembly kernel (kernels/assembly.hip, k_nse_system).
-// Position e of the output belongs to cell order[e] (colour order).
+// the assembly kernel (kernels/assembly.hip, cell_geometry).
+// Position e of the output belongs to cell order[e] (colour order; null =
+// identity). 8 cells per 256-thread block, thread t < 27 of a 32-lane slot
+// owns Gauss point t; the cell's 64 support points are staged in LDS.
+__constant__ double mL3[4][3] = {
+    {map_lag(0, kGaussX[0]), map_lag(0, kGaussX[1]), map_lag(0, kGaussX[2])},
+    {map_lag(1, kGaussX[0]), map_lag(1, kGaussX[1]), map_lag(1, kGaussX[2])},
+    {map_lag(2, kGaussX[0]), map_lag(2, kGaussX[1]), map_lag(2, kGaussX[2])},
+    {map_lag(3, kGaussX[0]), map_lag(3, kGaussX[1]), map_lag(3, kGaussX[2])}};
+__constant__ double mD3[4][3] = {
+    {map_dlag(0, kGaussX[0]), map_dlag(0, kGaussX[1]), map_dlag(0, kGaussX[2])},
+    {map_dlag(1, kGaussX[0]), map_dlag(1, kGaussX[1]), map_dlag(1, kGaussX[2])},
+    {map_dlag(2, kGaussX[0]), map_dlag(2, kGaussX[1]), map_dlag(2, kGaussX[2])},
+    {map_dlag(3, kGaussX[0]), map_dlag(3, kGaussX[1]), map_dlag(3, kGaussX[2])}};
 __global__ __launch_bounds__(256) void k_mf_geometry(CellData cd, const int32_t* __restrict__ order,
                                                      double* __restrict__ geo) {
-  __shared__ double X[kGeoCells][81];
+  __shared__ double X[kGeoCells][3 * kMapPts];
   const int slot = threadIdx.x >> 5, t = threadIdx.x & 31;
   const int pos = blockIdx.x * kGeoCells + slot;
-  const bool active = t < 27 && pos < cd.n_cells;
-  const int cell = active ? order[pos] : 0;
-  if (active) {
-    const int n = cd.cell_q2[27 * size_t(cell) + t];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) X[slot][3 * t + d] = cd.xyz[3 * size_t(n) + d];
-  }
+  const bool live = pos < cd.n_cells;
+  const int cell = live ? (order ? order[pos] : pos) : 0;
+  if (live)
+    for (int i = t; i < 3 * kMapPts; i += 32) X[slot][i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   __syncthreads();
-  if (!active) return;
+  if (!live || t >= 27) return;
   const int q0 = t % 3, q1 = (t / 3) % 3, q2 = t / 9;
   double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-  for (int n = 0; n < 27; ++n) {
-    const int a = n % 3, b = (n / 3) % 3, c = n / 9;
-    const double la = mL[a][q0], lb = mL[b][q1], lc = mL[c][q2];
-    const double g0 = mD[a][q0] * lb * lc, g1 = la * mD[b][q1] * lc, g2 = la * lb * mD[c][q2];
+  for (int n = 0; n < kMapPts; ++n) {
+    const int a = n % 4, b = (n / 4) % 4, c = n / 16;
+    const double la = mL3[a][q0], lb = mL3[b][q1], lc = mL3[c][q2];
+    const double g0 = mD3[a][q0] * lb * lc, g1 = la * mD3[b][q1] * lc, g2 = la * lb * mD3[c][q2];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const double Xi = X[slot][3 * n + i];
@@ -497,7 +500,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     uint32_t mask;
   };
   struct Nodes {
-    double U[3][3], X[3][3];
+    double U[3][3];
     double pv;
   };
   auto load_ids = [&](int j, Ids& I) {
@@ -517,7 +520,6 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     for (int a = 0; a < 3; ++a)
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        if (!SEP) N.X[a][d] = mc.xyz[3 * size_t(I.nd[a]) + d];
         N.U[a][d] = src[3 * size_t(I.nd[a]) + d];
       }
     N.pv = (STOKES && p < 8) ? src[mc.n_u + I.pdof] : 0.0;
@@ -543,7 +545,6 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
   const size_t e = (cs < kPenCells && cell < c1) ? size_t(cell) : 0;
   const int* nd = Ic.nd;
   const uint32_t mask = Ic.mask;
-  double(&X)[3][3] = Nc.X;
   double(&U)[3][3] = Nc.U;
   const int colc = SEP ? mc.col[e] : 0;
   const int layc = SEP ? mc.layer[e] : 0;
@@ -564,88 +565,15 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
   // ---- geometry: J^-1 and JxW at the z-pencil's three points
   double Ji[3][9], w[3];
   if (!SEP) {
-    // general MappingQ2: J = dX/dxi by the same sum factorisation
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {  // x: value and d/dxi0 along the x-pencil
-    const double in[3] = {X[0][d], X[1][d], X[2][d]};
-    double v[3], g[3];
-    fwd(kTL, in, v);
-    fwd(kTD, in, g);
+    // general MappingQ(3) geometry: J^-1 / JxW of the z-pencil's three points
+    // streamed from the per-cell table k_mf_geometry builds at upload
+    const double* g = mc.geo + 270 * e;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      S[d * kFS + 3 * p + q] = v[q];
-      S[(3 + d) * kFS + 3 * p + q] = g[q];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Ji[q][i] = g[27 * i + p + 9 * q];
+      w[q] = g[243 + p + 9 * q];
     }
-  }
-  wsync();
-  {
-    double A[3][3], B[3][3], C[3][3];  // [d][q1]
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {  // y
-      double v[3], g[3];
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        v[b] = SR[d * kFS + yb + 3 * b];
-        g[b] = SR[(3 + d) * kFS + yb + 3 * b];
-      }
-      fwd(kTL, v, A[d]);
-      fwd(kTD, v, B[d]);
-      fwd(kTL, g, C[d]);
-    }
-    wsync();
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        S[d * kFS + yb + 3 * q] = A[d][q];
-        S[(3 + d) * kFS + yb + 3 * q] = B[d][q];
-        S[(6 + d) * kFS + yb + 3 * q] = C[d][q];
-      }
-  }
-  wsync();
-  {
-    double J[3][3][3];  // [q2][d][e]
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {  // z
-      double A[3], B[3], C[3], t[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        A[k] = SR[d * kFS + p + 9 * k];
-        B[k] = SR[(3 + d) * kFS + p + 9 * k];
-        C[k] = SR[(6 + d) * kFS + p + 9 * k];
-      }
-      fwd(kTL, C, t);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) J[q][d][0] = t[q];
-      fwd(kTL, B, t);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) J[q][d][1] = t[q];
-      fwd(kTD, A, t);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) J[q][d][2] = t[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const double(*M)[3] = J[q];
-      const double c00 = M[1][1] * M[2][2] - M[1][2] * M[2][1];
-      const double c01 = M[1][2] * M[2][0] - M[1][0] * M[2][2];
-      const double c02 = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-      const double det = M[0][0] * c00 + M[0][1] * c01 + M[0][2] * c02;
-      const double id = 1.0 / det;
-      Ji[q][0] = c00 * id;
-      Ji[q][1] = (M[0][2] * M[2][1] - M[0][1] * M[2][2]) * id;
-      Ji[q][2] = (M[0][1] * M[1][2] - M[0][2] * M[1][1]) * id;
-      Ji[q][3] = c01 * id;
-      Ji[q][4] = (M[0][0] * M[2][2] - M[0][2] * M[2][0]) * id;
-      Ji[q][5] = (M[0][2] * M[1][0] - M[0][0] * M[1][2]) * id;
-      Ji[q][6] = c02 * id;
-      Ji[q][7] = (M[0][1] * M[2][0] - M[0][0] * M[2][1]) * id;
-      Ji[q][8] = (M[0][0] * M[1][1] - M[0][1] * M[1][0]) * id;
-      w[q] = det * (wab * kGaussW[q]);
-    }
-  }
-  wsync();
-
   }
   // ---- velocity: values and reference gradients
 #pragma unroll

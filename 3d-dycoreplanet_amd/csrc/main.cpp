@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
   }
   const bool feec = rp.use_FEEC_solver != 0;
   dcp_host_mesh* m = dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0,
-                                          rp.R1, rp.length, rp.physics.temperature_degree, 0);
+                                          rp.R1, rp.length, rp.physics.temperature_degree, 0, 0);
   if (!m) return fail("mesh", nullptr);
   dcp_host_mesh_view v{};
   dcp_host_mesh_view_get(m, &v);

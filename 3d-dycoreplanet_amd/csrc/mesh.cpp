@@ -6,7 +6,9 @@
 #include <functional>
 #include <map>
 #include <stdexcept>
+#include <array>
 #include <tuple>
+#include <unordered_map>
 
 #include "fe_tables.h"
 
@@ -78,7 +80,7 @@ void number_nodes(Mesh& m, size_t n_keys, KeyFn key_of, std::vector<int32_t>& ke
 
 }  // namespace
 
-Mesh build_shell(int refine, double R0, double R1) {
+Mesh build_shell(int refine, double R0, double R1, bool mapping_q_on_all_cells) {
   if (refine < 0 || refine > 8) throw std::invalid_argument("shell refinement must be in [0,8]");
   Mesh m;
   m.cuboid = false;
@@ -117,6 +119,108 @@ Mesh build_shell(int refine, double R0, double R1) {
   number_nodes(m, n_keys, key_of, key_node);
   m.cell_coarse.resize(m.n_cells);
   for (int c = 0; c < m.n_cells; ++c) m.cell_coarse[c] = c / (N * N * N);
+  // ---- vertex directions: hyper_shell's coarse corners (+-1,+-1,+-1)/sqrt(3),
+  // then per refinement level every line midpoint by get_intermediate_point
+  // (geodesic, w = 1/2) and every quad centre by get_new_point over its 4
+  // vertices (weight -1/4) and 4 line midpoints (+1/2) — TriaAccessor::
+  // center(true, true). Shell refinement is a radial extrusion: radial lines
+  // keep the direction (collinear case of get_intermediate_point), hex centres
+  // take their spherical faces' centre direction, so directions live on the
+  // unit sphere and are keyed by the surface lattice point P (Q2 lattice units).
+  std::unordered_map<int64_t, std::array<double, 3>> dir_of;
+  auto skey = [&](const int P[3]) {
+    return (int64_t(P[0] + N) * L2 + (P[1] + N)) * L2 + (P[2] + N);
+  };
+  const double o[3] = {0, 0, 0};
+  for (int p = 0; p < 6; ++p) {
+    // panel lattice (i, j) in [0, N]^2 of vertices -> surface point
+    auto P_of = [&](int i, int j, int P[3]) {
+      for (int d = 0; d < 3; ++d)
+        P[d] = N * panel[p][0][d] + (2 * i - N) * panel[p][1][d] + (2 * j - N) * panel[p][2][d];
+    };
+    auto get = [&](int i, int j) -> const std::array<double, 3>& {
+      int P[3];
+      P_of(i, j, P);
+      return dir_of.at(skey(P));
+    };
+    auto has = [&](int i, int j, int64_t& k) {
+      int P[3];
+      P_of(i, j, P);
+      k = skey(P);
+      return dir_of.count(k) != 0;
+    };
+    for (int j = 0; j <= N; j += N)
+      for (int i = 0; i <= N; i += N) {
+        int P[3];
+        P_of(i, j, P);
+        const int64_t k = skey(P);
+        if (dir_of.count(k)) continue;
+        std::array<double, 3> d;
+        for (int e = 0; e < 3; ++e) d[e] = (P[e] > 0 ? 1.0 : -1.0) / std::sqrt(3.0);
+        dir_of[k] = d;
+      }
+    auto midpoint = [&](int i0, int j0, int i1, int j1, int im, int jm) {
+      int64_t k;
+      if (has(im, jm, k)) return;
+      int Pa[3], Pb[3];
+      P_of(i0, j0, Pa);
+      P_of(i1, j1, Pb);
+      // canonical line orientation: lower surface key first
+      const bool sw = skey(Pb) < skey(Pa);
+      const auto& a = sw ? get(i1, j1) : get(i0, j0);
+      const auto& b = sw ? get(i0, j0) : get(i1, j1);
+      std::array<double, 3> out;
+      spherical_intermediate(o, a.data(), b.data(), 0.5, out.data());
+      dir_of[k] = out;
+    };
+    for (int s = N; s > 1; s /= 2) {
+      const int h = s / 2;
+      for (int j = 0; j <= N; j += s)
+        for (int i = 0; i < N; i += s) midpoint(i, j, i + s, j, i + h, j);
+      for (int i = 0; i <= N; i += s)
+        for (int j = 0; j < N; j += s) midpoint(i, j, i, j + s, i, j + h);
+      for (int j = 0; j < N; j += s)
+        for (int i = 0; i < N; i += s) {
+          int64_t k;
+          if (has(i + h, j + h, k)) continue;
+          const int pi[8][2] = {{i, j},     {i + s, j},     {i, j + s},     {i + s, j + s},
+                                {i, j + h}, {i + s, j + h}, {i + h, j}, {i + h, j + s}};
+          double src[24];
+          for (int t = 0; t < 8; ++t) {
+            const auto& d = get(pi[t][0], pi[t][1]);
+            for (int e = 0; e < 3; ++e) src[3 * t + e] = d[e];
+          }
+          const double w[8] = {-0.25, -0.25, -0.25, -0.25, 0.5, 0.5, 0.5, 0.5};
+          std::array<double, 3> out;
+          spherical_new_points(o, 8, src, 1, w, out.data());
+          dir_of[k] = out;
+        }
+    }
+  }
+  // radial levels: collinear get_intermediate_point = arithmetic midpoints
+  std::vector<double> rad(N + 1, 0.0);
+  rad[0] = R0;
+  rad[N] = R1;
+  for (int s = N; s > 1; s /= 2)
+    for (int k = 0; k < N; k += s) rad[k + s / 2] = 0.5 * rad[k + s] + 0.5 * rad[k];
+  // ---- MappingQ(3) support points of every cell from its 8 vertices
+  m.mapping_q_on_all_cells = mapping_q_on_all_cells;
+  m.cell_map.assign(size_t(m.n_cells) * 3 * kMapPts, 0.0);
+  for (int c = 0; c < m.n_cells; ++c) {
+    double V[24];
+    int kz = 0;
+    for (int v = 0; v < 8; ++v) {
+      int P[3], t;
+      surf_point(c, kQ1VertexToQ2Lex[v], P, t);
+      const auto& d = dir_of.at(skey(P));
+      for (int e = 0; e < 3; ++e) V[3 * v + e] = rad[t / 2] * d[e];
+      if (v == 0) kz = t / 2;
+    }
+    // CellAccessor::has_boundary_lines(): the innermost and outermost layers
+    const bool boundary = kz == 0 || kz == N - 1;
+    mapping_support_points(V, mapping_q_on_all_cells || boundary, &m.cell_map[size_t(c) * 3 * kMapPts]);
+  }
+  // ---- Q2 support points = the cell's map at (a, b, c) / 2 (first cell)
   m.xyz.assign(size_t(m.n_vnodes) * 3, 0.0);
   m.vnode_bnd.assign(m.n_vnodes, 0);
   std::vector<char> done(m.n_vnodes, 0);
@@ -127,17 +231,15 @@ Mesh build_shell(int refine, double R0, double R1) {
       done[n] = 1;
       int P[3], t;
       surf_point(c, lex, P, t);
-      // Equiangular cube-sphere: components on the cube face stay +-1, the
-      // tangential ones map through tan(pi/4 * s); panel-independent.
-      double dir[3], nrm = 0;
-      for (int d = 0; d < 3; ++d) {
-        dir[d] = (std::abs(P[d]) == N) ? (P[d] > 0 ? 1.0 : -1.0)
-                                       : std::tan(0.25 * kPi * double(P[d]) / double(N));
-        nrm += dir[d] * dir[d];
+      double* x = &m.xyz[3 * size_t(n)];
+      if (lex % 3 != 1 && (lex / 3) % 3 != 1 && lex / 9 != 1) {
+        const auto& d = dir_of.at(skey(P));  // a vertex: exact
+        for (int e = 0; e < 3; ++e) x[e] = rad[t / 2] * d[e];
+      } else {
+        const double xi[3] = {0.5 * (lex % 3), 0.5 * ((lex / 3) % 3), 0.5 * (lex / 9)};
+        double J[3][3];
+        mapping_eval(&m.cell_map[size_t(c) * 3 * kMapPts], xi, x, J);
       }
-      nrm = std::sqrt(nrm);
-      const double r = (t == 0) ? R0 : (t == 2 * N) ? R1 : R0 + (R1 - R0) * double(t) / double(2 * N);
-      for (int d = 0; d < 3; ++d) m.xyz[3 * size_t(n) + d] = r * dir[d] / nrm;
       if (t == 0) m.vnode_bnd[n] |= kBndInner;
       if (t == 2 * N) m.vnode_bnd[n] |= kBndOuter;
     }
@@ -192,6 +294,15 @@ Mesh build_cube(int refine, double length) {
     }
   m.cell_diameter.resize(m.n_cells);
   for (int c = 0; c < m.n_cells; ++c) m.cell_diameter[c] = cell_diameter_of(m, c);
+  // MappingQ(3) on a FlatManifold box = the trilinear map of its vertices
+  m.cell_map.assign(size_t(m.n_cells) * 3 * kMapPts, 0.0);
+  for (int c = 0; c < m.n_cells; ++c) {
+    double V[24];
+    for (int v = 0; v < 8; ++v)
+      for (int e = 0; e < 3; ++e)
+        V[3 * v + e] = m.xyz[3 * size_t(m.cell_q2[27 * size_t(c) + kQ1VertexToQ2Lex[v]]) + e];
+    mapping_support_points(V, false, &m.cell_map[size_t(c) * 3 * kMapPts]);
+  }
   // planet_geometry.tpp:35 center = (p0+p1)/2, rescaled with 1/L (boussinesq_model.tpp:54)
   for (int d = 0; d < 3; ++d) m.center[d] = 0.5 / length;
   m.global_diameter = std::sqrt(3.0) / length;
@@ -326,27 +437,26 @@ double dlag2(int a, double x) { return a == 0 ? 4 * x - 3 : a == 1 ? -8 * x + 4 
 }  // namespace
 
 std::vector<double> consistent_normals(const Mesh& m, uint8_t boundary_bit) {
-  // n_i = sum_cells int grad(phi_i) dx with the Q2 mapping and QGauss(3), i.e.
-  // minus the row of B^T 1 of node i. Interior rows vanish to roundoff, so
-  // constraining u_i . n_i = 0 on the boundary makes C^T B^T 1 = 0 exactly
-  // (consistent normals, Engelman, Sani & Gresho 1982).
+  // n_i = sum_cells int grad(phi_i) dx with the cell's MappingQ(3) and
+  // QGauss(3), i.e. minus the row of B^T 1 of node i. Interior rows vanish to
+  // roundoff, so constraining u_i . n_i = 0 on the boundary makes C^T B^T 1 = 0
+  // exactly (consistent normals, Engelman, Sani & Gresho 1982).
   std::vector<double> nrm(size_t(m.n_vnodes) * 3, 0.0);
   for (int c = 0; c < m.n_cells; ++c) {
     bool touches = false;
     for (int l = 0; l < 27; ++l) touches |= (m.vnode_bnd[m.cell_q2[27 * size_t(c) + l]] & boundary_bit) != 0;
     if (!touches) continue;
+    const double* X = &m.cell_map[size_t(c) * 3 * kMapPts];
     for (int q = 0; q < 27; ++q) {
       const double p[3] = {kGaussX[q % 3], kGaussX[(q / 3) % 3], kGaussX[q / 9]};
       const double w = kGaussW[q % 3] * kGaussW[(q / 3) % 3] * kGaussW[q / 9];
-      double gref[27][3], J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+      double x[3], J[3][3], gref[27][3];
+      mapping_eval(X, p, x, J);
       for (int n = 0; n < 27; ++n) {
         const int a = n % 3, b = (n / 3) % 3, cc = n / 9;
         gref[n][0] = dlag2(a, p[0]) * lag2(b, p[1]) * lag2(cc, p[2]);
         gref[n][1] = lag2(a, p[0]) * dlag2(b, p[1]) * lag2(cc, p[2]);
         gref[n][2] = lag2(a, p[0]) * lag2(b, p[1]) * dlag2(cc, p[2]);
-        const double* X = &m.xyz[3 * size_t(m.cell_q2[27 * size_t(c) + n])];
-        for (int i = 0; i < 3; ++i)
-          for (int j = 0; j < 3; ++j) J[i][j] += X[i] * gref[n][j];
       }
       // cofactor matrix: det(J) J^-T = cof(J); grad phi JxW = cof(J) gref w
       double cof[3][3];
@@ -359,6 +469,42 @@ std::vector<double> consistent_normals(const Mesh& m, uint8_t boundary_bit) {
         double* out = &nrm[3 * size_t(m.cell_q2[27 * size_t(c) + n])];
         for (int i = 0; i < 3; ++i)
           out[i] += (cof[i][0] * gref[n][0] + cof[i][1] * gref[n][1] + cof[i][2] * gref[n][2]) * w;
+      }
+    }
+  }
+  return nrm;
+}
+
+std::vector<double> mapping_normals(const Mesh& m, uint8_t boundary_bit) {
+  // VectorTools::compute_no_normal_flux_constraints (deal.II, called with the
+  // reference's mapping at boussinesq_model.tpp:324-329): the unit outward
+  // normal of each boundary face through the cell's mapping at the face's
+  // support points; a support point shared by several faces gets the
+  // normalised sum (the faces of a smooth sphere are all "close").
+  std::vector<double> nrm(size_t(m.n_vnodes) * 3, 0.0);
+  for (int c = 0; c < m.n_cells; ++c) {
+    const double* X = &m.cell_map[size_t(c) * 3 * kMapPts];
+    for (int f = 0; f < 6; ++f) {
+      const int axis = f / 2, side = f % 2;
+      bool on = true;
+      for (int l = 0; l < 27 && on; ++l) {
+        const int ab[3] = {l % 3, (l / 3) % 3, l / 9};
+        if (ab[axis] == 2 * side) on = (m.vnode_bnd[m.cell_q2[27 * size_t(c) + l]] & boundary_bit) != 0;
+      }
+      if (!on) continue;
+      for (int l = 0; l < 27; ++l) {
+        const int ab[3] = {l % 3, (l / 3) % 3, l / 9};
+        if (ab[axis] != 2 * side) continue;
+        const double xi[3] = {0.5 * ab[0], 0.5 * ab[1], 0.5 * ab[2]};
+        double x[3], J[3][3];
+        mapping_eval(X, xi, x, J);
+        // outward normal = +-(column t1 x column t2), t1, t2 the other two axes
+        const int t1 = (axis + 1) % 3, t2 = (axis + 2) % 3;
+        double n[3] = {J[1][t1] * J[2][t2] - J[2][t1] * J[1][t2], J[2][t1] * J[0][t2] - J[0][t1] * J[2][t2],
+                       J[0][t1] * J[1][t2] - J[1][t1] * J[0][t2]};
+        const double s = (side ? 1.0 : -1.0) / std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        double* out = &nrm[3 * size_t(m.cell_q2[27 * size_t(c) + l])];
+        for (int d = 0; d < 3; ++d) out[d] += s * n[d];
       }
     }
   }
@@ -387,11 +533,12 @@ Constraints nse_constraints(const Mesh& m, NormalMode mode) {
     for (int n = 0; n < m.n_vnodes; ++n)
       if (m.vnode_bnd[n] & kBndInner)
         for (int c = 0; c < 3; ++c) b.add_line(3 * n + c);
-    const std::vector<double> cn =
-        mode == NormalMode::Consistent ? consistent_normals(m, kBndOuter) : std::vector<double>();
+    const std::vector<double> cn = mode == NormalMode::Consistent ? consistent_normals(m, kBndOuter)
+                                   : mode == NormalMode::Mapping  ? mapping_normals(m, kBndOuter)
+                                                                  : std::vector<double>();
     for (int n = 0; n < m.n_vnodes; ++n)
       if (m.vnode_bnd[n] & kBndOuter) {
-        const double* x = mode == NormalMode::Consistent ? &cn[3 * size_t(n)] : &m.xyz[3 * size_t(n)];
+        const double* x = mode == NormalMode::Radial ? &m.xyz[3 * size_t(n)] : &cn[3 * size_t(n)];
         const double r = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
         const double nn[3] = {x[0] / r, x[1] / r, x[2] / r};
         const int dofs[3] = {3 * n, 3 * n + 1, 3 * n + 2};

@@ -7,11 +7,16 @@
 //   refine_global (planet_geometry.tpp:109-120), GridTools::scale(1/L) (boussinesq_model.tpp:42-63)
 //   setup_dofs: distribute_dofs + component_wise({0,0,0,1}) (boussinesq_model.tpp:194-206),
 //               constraints (:259-387)
-// Geometry convention (documented deviation, parity vs deal.II unpinned): the
-// shell's coarse cells are the 6 panels of an equiangular cube-sphere with the
-// radius linear in the third reference coordinate; every refined cell carries
-// a Q2 isoparametric geometry whose 27 nodes are exactly the Q2 velocity
-// support points (nodes on the inner/outer boundary lie on the spheres).
+// Geometry: the shell's 6 coarse cells are hyper_shell's (corners
+// (+-1,+-1,+-1) R/sqrt(3)); refinement places new vertices by
+// SphericalManifold's rules (manifold.cpp): line midpoints by
+// get_intermediate_point, quad / hex centres by get_new_point over the
+// vertices and line / face midpoints with TriaAccessor::center(true, true)'s
+// weights. Every cell carries the 64 support points of MappingQ(3)
+// (boussinesq_model.tpp:20): spherical on cells with boundary lines, trilinear
+// (MappingQ1) elsewhere unless mapping_q_on_all_cells (deal.II >= 9.3
+// behaviour). Parity with deal.II itself is unpinned (not in this image);
+// topology (panel frames, numbering) follows mesh.cpp's own convention.
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -50,6 +55,10 @@ struct Mesh {
   std::vector<int32_t> vnode_vertex;    // vnode id -> vertex id or -1
   std::vector<uint8_t> vnode_bnd;       // BoundaryBits
   std::vector<double> cell_diameter;    // max vertex diagonal (CellAccessor::diameter)
+  // MappingQ(3) support points per cell, [n_cells][64][3] lexicographic
+  // (fe_tables.h kGL3); xyz above = their image of the Q2 support points.
+  std::vector<double> cell_map;
+  bool mapping_q_on_all_cells = false;
   std::vector<int32_t> cell_coarse;     // coarse cell (tree) of each cell
 
   int n_u() const { return 3 * n_vnodes; }
@@ -57,8 +66,10 @@ struct Mesh {
 };
 
 // Builds the refined hyper shell (6 coarse cells) with radii already divided
-// by the reference length.
-Mesh build_shell(int refine, double R0, double R1);
+// by the reference length. mapping_q_on_all_cells: false = deal.II 9.2's
+// MappingQ (cubic map on boundary cells only, the version CMakeLists.txt:26
+// pins), true = deal.II >= 9.3 (cubic map on every cell).
+Mesh build_shell(int refine, double R0, double R1, bool mapping_q_on_all_cells = false);
 // Builds the refined unit cube [0,1]^3 / L (hyper_rectangle, colorize).
 Mesh build_cube(int refine, double length);
 // Dispatch on Parameters (cuboid geometry flag, refinement, scaling by L).
@@ -81,20 +92,37 @@ struct Constraints {
 };
 
 // Normal used by the no-normal-flux constraint on the outer sphere.
-//   Consistent: n_i = sum_cells int grad(phi_i) dx (discretely consistent with
-//     the divergence block, so B^T 1 lies in the constrained space and the
-//     Schur complement's constant-pressure mode is exactly singular and never
-//     excited). Default; see DESIGN.md "no-normal-flux normals".
-//   Radial: the exact sphere normal at the support point (closest to deal.II's
-//     mapping normal); leaves S with a near-null eigenvalue ~ h^5.6 that the
-//     reference's identity-preconditioned Schur GMRES cannot resolve for r >= 3.
-enum class NormalMode { Consistent, Radial };
+//   Mapping (default): deal.II's compute_no_normal_flux_constraints rule, as
+//     the reference calls it with its mapping (boussinesq_model.tpp:324-329) —
+//     the unit normal of every adjacent mapped boundary face at the support
+//     point (MappingQ(3) of the cell), summed over the faces and normalised.
+//   Radial: the exact sphere normal at the support point.
+//   Consistent: n_i = sum_cells int grad(phi_i) dx, minus the boundary row of
+//     B^T 1 (Engelman, Sani & Gresho 1982). Under MappingQ(3) + QGauss(3) the
+//     interior rows of B^T 1 no longer vanish (the quadrature is not exact for
+//     a cubic map), so no choice of normals makes the constant pressure an
+//     exact null vector of S; see DESIGN.md "no-normal-flux normals".
+enum class NormalMode { Consistent, Radial, Mapping };
 std::vector<double> consistent_normals(const Mesh& m, uint8_t boundary_bit);
+std::vector<double> mapping_normals(const Mesh& m, uint8_t boundary_bit);
+
+// deal.II geometry rules (manifold.cpp), centre = `center`:
+// SphericalManifold::get_intermediate_point(p1, p2, w)
+void spherical_intermediate(const double* center, const double* p1, const double* p2, double w,
+                            double* out);
+// SphericalManifold::get_new_points(src[n_src], weights[n_rows][n_src]) -> out[n_rows]
+void spherical_new_points(const double* center, int n_src, const double* src, int n_rows,
+                          const double* weights, double* out);
+// MappingQGeneric(3)::compute_mapping_support_points from the 8 vertices
+// (lexicographic): spherical (SphericalManifold, centre 0) or flat (trilinear).
+void mapping_support_points(const double* vertices, bool spherical, double* X /*[64][3]*/);
+// x(xi) and J = dx/dxi of the cubic map with support points X.
+void mapping_eval(const double* X, const double* xi, double* x, double J[3][3]);
 
 // NSE constraints (boussinesq_model.tpp:259-333): shell -> no-slip on the
 // inner sphere, no-normal-flux on the outer sphere; cube -> periodic x/y,
 // no-slip z=0, no-normal-flux z=1. DoF space: [3*n_vnodes velocity | n_p pressure].
-Constraints nse_constraints(const Mesh& m, NormalMode mode = NormalMode::Consistent);
+Constraints nse_constraints(const Mesh& m, NormalMode mode = NormalMode::Mapping);
 
 // Temperature constraints (:338-387): Dirichlet with the initial temperature on
 // the inner sphere (shell) or on z=0 (cube, + periodic x/y). degree 1 or 2.

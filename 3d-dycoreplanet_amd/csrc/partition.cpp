@@ -1,6 +1,8 @@
 // Host partitioning for the multi-GPU path (see partition.h).
 #include "partition.h"
 
+#include "fe_tables.h"
+
 #include <algorithm>
 #include <stdexcept>
 #include <string>
@@ -176,7 +178,7 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
   const int nu_loc = L.n_u();
   L.cell_nse_dofs.resize(size_t(L.n_cells) * 89);
   L.cell_T_dofs.resize(size_t(L.n_cells) * 8);
-  L.geometry.resize(size_t(L.n_cells) * 81);
+  L.geometry.resize(size_t(L.n_cells) * 3 * kMapPts);
   L.diameter.resize(L.n_cells);
   for (int lc = 0; lc < L.n_cells; ++lc) {
     const int c = L.cells_g[lc];
@@ -186,8 +188,8 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
           d < n_u ? 3 * vl[d / 3] + d % 3 : nu_loc + pl[d - n_u];
     }
     for (int v = 0; v < 8; ++v) L.cell_T_dofs[size_t(lc) * 8 + v] = Tl[cell_T_dofs[size_t(c) * 8 + v]];
-    std::copy(cell_geometry + size_t(c) * 81, cell_geometry + size_t(c) * 81 + 81,
-              L.geometry.begin() + size_t(lc) * 81);
+    std::copy(cell_geometry + size_t(c) * 3 * kMapPts, cell_geometry + size_t(c) * 3 * kMapPts + 3 * kMapPts,
+              L.geometry.begin() + size_t(lc) * 3 * kMapPts);
     L.diameter[lc] = cell_diameter[c];
   }
   // constraints restricted to local dofs

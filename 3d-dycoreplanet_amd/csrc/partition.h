@@ -46,7 +46,7 @@ struct LocalMesh {
   std::vector<int32_t> cells_g;              // local cell -> global cell
   std::vector<int32_t> cell_nse_dofs;        // [n_cells][89], local numbering
   std::vector<int32_t> cell_T_dofs;          // [n_cells][8]
-  std::vector<double> geometry;              // [n_cells][27][3]
+  std::vector<double> geometry;              // [n_cells][64][3] (MappingQ(3) support points)
   std::vector<double> diameter;              // [n_cells]
   std::vector<int32_t> vnode_g, p_g, T_g;    // local -> global id per field
   // local constraints (CSR lines as dcp_constraints expects)

@@ -184,7 +184,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int)]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
-    lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I]
+    lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_destroy.argtypes = [P]
     lib.dcp_host_mesh_destroy.restype = None
@@ -262,13 +262,16 @@ class ConstraintSet:
 class HostMesh:
     """Refined shell / cube with DoFs and constraints (setup_dofs restated)."""
 
+    NORMAL_MODES = ("mapping", "radial", "consistent")  # dcp_host_mesh_create normal_mode
+
     def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1,
-                 normals="consistent", feec=False):
-        if normals not in ("consistent", "radial"):
-            raise ValueError("normals must be 'consistent' or 'radial'")
+                 normals="mapping", feec=False, mapping_q_on_all_cells=False):
+        if normals not in self.NORMAL_MODES:
+            raise ValueError("normals must be one of %s" % (self.NORMAL_MODES,))
         h = lib().dcp_host_mesh_create(int(cuboid), int(refine), float(R0), float(R1),
                                        float(length), int(temperature_degree),
-                                       0 if normals == "consistent" else 1)
+                                       self.NORMAL_MODES.index(normals),
+                                       int(bool(mapping_q_on_all_cells)))
         if not h:
             raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
         try:
@@ -279,8 +282,9 @@ class HostMesh:
             self.cell_nse_dofs = _arr(v.cell_nse_dofs, self.n_cells * 89, np.int32).reshape(-1, 89)
             tdpc = 8 if temperature_degree == 1 else 27
             self.cell_T_dofs = _arr(v.cell_T_dofs, self.n_cells * tdpc, np.int32).reshape(-1, tdpc)
-            self.cell_geometry = _arr(v.cell_geometry, self.n_cells * 81,
-                                      np.float64).reshape(-1, 27, 3)
+            # MappingQ(3) support points per cell (64, lexicographic, Gauss-Lobatto)
+            self.cell_geometry = _arr(v.cell_geometry, self.n_cells * 192,
+                                      np.float64).reshape(-1, 64, 3)
             self.cell_diameter = _arr(v.cell_diameter, self.n_cells, np.float64)
             self.node_xyz = _arr(v.node_xyz, self.n_vnodes * 3, np.float64).reshape(-1, 3)
             self.nse_constraints = ConstraintSet.from_view(v.nse)
@@ -292,6 +296,8 @@ class HostMesh:
             lib().dcp_host_mesh_destroy(h)
         self.cuboid = bool(cuboid)
         self.refine = refine
+        self.temperature_degree = temperature_degree
+        self.mapping_q_on_all_cells = bool(mapping_q_on_all_cells)
 
     def check(self, nse_constraints=None, T_constraints=None):
         """Host-only validation of the device upload; returns the number of
@@ -308,14 +314,13 @@ class HostMesh:
 
     def geometry_info(self):
         """Host-only: (separable, n_columns, n_layers) of the radially separable
-        Q2 geometry the matrix-free operator uses (dcp_mesh_geometry_info)."""
+        MappingQ(3) geometry the matrix-free operator uses (dcp_mesh_geometry_info)."""
         sep, nc, nl = C.c_int(0), C.c_int(0), C.c_int(0)
         rc = lib().dcp_mesh_geometry_info(self.n_cells, _ptr(self.cell_geometry), C.byref(sep),
                                           C.byref(nc), C.byref(nl))
         if rc != DCP_OK:
             raise DcpError(rc, lib().dcp_last_error(None).decode())
         return bool(sep.value), nc.value, nl.value
-        self.temperature_degree = temperature_degree
 
 
 class FeecTopology:

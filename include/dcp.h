@@ -17,8 +17,14 @@
  *     {0,0,0,1}) (boussinesq_model.tpp:204): NSE vector = [velocity (n_u) |
  *     pressure (n_p)], cell dof indices in FESystem(FE_Q(2)^3, FE_Q(1)) local
  *     order (89 per cell), exactly what cell->get_dof_indices() returns.
- *   - Geometry: per cell the 27 Q2 mapping support points in lexicographic
- *     order (x fastest), already divided by the reference length.
+ *   - Geometry: per cell the 64 support points of the reference's mapping,
+ *     MappingQ(3) (boussinesq_model.tpp:20; boussinesq_model.h:211), in
+ *     lexicographic order over the 4 Gauss-Lobatto points {0, (1-1/sqrt5)/2,
+ *     (1+1/sqrt5)/2, 1} per direction (x fastest), already divided by the
+ *     reference length: what MappingQGeneric<3>(3)::compute_mapping_support_points
+ *     returns for the cell. A cell deal.II maps with MappingQ1 (deal.II 9.2
+ *     MappingQ: cells without boundary lines) is passed as its trilinear
+ *     interpolant at those points, which the cubic basis reproduces exactly.
  *   - Arithmetic: IEEE FP64 throughout.
  */
 #ifndef DCP_H
@@ -138,7 +144,7 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value);
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
  * device sparsity patterns, cell colouring and scatter maps once. */
 int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs /*[n][89]*/,
-                    const int32_t* cell_T_dofs /*[n][8]*/, const double* cell_geometry /*[n][27][3]*/,
+                    const int32_t* cell_T_dofs /*[n][8]*/, const double* cell_geometry /*[n][64][3]*/,
                     const double* cell_diameter /*[n]*/, int n_u, int n_p, int n_T,
                     const dcp_constraints* nse_constraints,
                     const dcp_constraints* T_constraints);
@@ -150,8 +156,9 @@ int dcp_mesh_check(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
                    int n_T, const dcp_constraints* nse_constraints,
                    const dcp_constraints* T_constraints, int* n_colors);
 
-/* Host-only: is the Q2 geometry radially separable (every support point of a
- * cell at r_c * phi_ab, local c radial; the SphericalManifold hypershell)?
+/* Host-only: is the MappingQ(3) geometry radially separable (support point
+ * (a,b,c) of every cell at rho_c * Phi_ab, local c radial: the hyper_shell
+ * under SphericalManifold, both for cubic and trilinear cells)?
  * Then the matrix-free operator takes J^-1 / JxW from n_columns 2D tables and
  * n_layers radial tables instead of recomputing the mapping per cell. */
 int dcp_mesh_geometry_info(int n_cells, const double* cell_geometry, int* separable,
@@ -288,16 +295,23 @@ int dcp_feec_matrix_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowpt
 /* Host setup helpers (mesh generator, .prm) ----------------------------- */
 typedef struct dcp_host_mesh dcp_host_mesh;
 /* Builds the refined shell (cuboid = 0) or cube, DoFs and constraints the way
- * setup_dofs() does (see mesh.h for the geometry convention). normal_mode of
- * the no-normal-flux constraint: 0 = consistent (default), 1 = radial. */
+ * setup_dofs() does (see mesh.h for the geometry convention: hyper_shell +
+ * SphericalManifold refinement, MappingQ(3) support points per cell).
+ * normal_mode of the no-normal-flux constraint: 0 = deal.II's
+ * compute_no_normal_flux_constraints rule (normals of the mapped boundary
+ * faces at the support point, averaged; default), 1 = radial (exact sphere
+ * normal), 2 = consistent (minus the B^T 1 row, Engelman et al.). mapping_q_on_all_cells: 0 =
+ * deal.II 9.2 MappingQ (cubic map on boundary cells, MappingQ1 inside), 1 =
+ * deal.II >= 9.3 (cubic everywhere). */
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
-                                    int temperature_degree, int normal_mode);
+                                    int temperature_degree, int normal_mode,
+                                    int mapping_q_on_all_cells);
 void dcp_host_mesh_destroy(dcp_host_mesh* m);
 typedef struct {
   int n_cells, n_u, n_p, n_T, n_vnodes;
   const int32_t* cell_nse_dofs;   /* [n_cells][89] */
   const int32_t* cell_T_dofs;     /* [n_cells][8] */
-  const double* cell_geometry;    /* [n_cells][27][3] */
+  const double* cell_geometry;    /* [n_cells][64][3] MappingQ(3) support points */
   const double* cell_diameter;    /* [n_cells] */
   const double* node_xyz;         /* [n_vnodes][3] */
   dcp_constraints nse, T;

@@ -56,8 +56,31 @@ struct Vec3 {
 };
 double dot(const Vec3& a, const Vec3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
-// FEValues for one cell: Q2 isoparametric mapping from the 27 lexicographic
-// geometry nodes; Q2 and Q1 scalar shapes with physical gradients.
+// MappingQ(3) (boussinesq_model.tpp:20; deal.II MappingQGeneric(3)): tensor-
+// product Lagrange polynomials on the 4 Gauss-Lobatto points of [0,1]
+// (0, (1-1/sqrt5)/2, (1+1/sqrt5)/2, 1), 64 support points per cell in
+// lexicographic order. Restated here independently of the product's tables.
+const double kGL[4] = {0.0, 0.5 - 0.5 / std::sqrt(5.0), 0.5 + 0.5 / std::sqrt(5.0), 1.0};
+double lag3(int i, double x) {
+  double v = 1.0;
+  for (int j = 0; j < 4; ++j)
+    if (j != i) v *= (x - kGL[j]) / (kGL[i] - kGL[j]);
+  return v;
+}
+double dlag3(int i, double x) {
+  double s = 0.0;
+  for (int k = 0; k < 4; ++k) {
+    if (k == i) continue;
+    double v = 1.0 / (kGL[i] - kGL[k]);
+    for (int j = 0; j < 4; ++j)
+      if (j != i && j != k) v *= (x - kGL[j]) / (kGL[i] - kGL[j]);
+    s += v;
+  }
+  return s;
+}
+
+// FEValues for one cell: the cell's MappingQ(3) from its 64 support points;
+// Q2 and Q1 scalar shapes with physical gradients.
 struct CellValues {
   int nq = 0;
   std::vector<double> JxW;
@@ -93,14 +116,20 @@ struct CellValues {
         rg1[n][1] = lag1(a, p[0]) * dlag1(b, p[1]) * lag1(c, p[2]);
         rg1[n][2] = lag1(a, p[0]) * lag1(b, p[1]) * dlag1(c, p[2]);
       }
-      // Jacobian J[i][j] = d x_i / d xi_j
+      // Jacobian J[i][j] = d x_i / d xi_j of the cubic map
       double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
       Vec3 x;
-      for (int n = 0; n < 27; ++n)
+      for (int n = 0; n < 64; ++n) {
+        const int a = n % 4, b = (n / 4) % 4, c = n / 16;
+        const double s = lag3(a, p[0]) * lag3(b, p[1]) * lag3(c, p[2]);
+        const double g[3] = {dlag3(a, p[0]) * lag3(b, p[1]) * lag3(c, p[2]),
+                             lag3(a, p[0]) * dlag3(b, p[1]) * lag3(c, p[2]),
+                             lag3(a, p[0]) * lag3(b, p[1]) * dlag3(c, p[2])};
         for (int i = 0; i < 3; ++i) {
-          x[i] += geom[3 * n + i] * rv2[n];
-          for (int j = 0; j < 3; ++j) J[i][j] += geom[3 * n + i] * rg2[n][j];
+          x[i] += geom[3 * n + i] * s;
+          for (int j = 0; j < 3; ++j) J[i][j] += geom[3 * n + i] * g[j];
         }
+      }
       const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
                          J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
                          J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
@@ -210,12 +239,12 @@ Vec3 cross(const Vec3& a, const Vec3& b) {
 // ===========================================================================
 // Element level
 
-extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom27,
+extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom64,
                                     const double* u_local, const double* T_local, double* K,
                                     double* f) {
   // boussinesq_model.tpp:550-673; QGauss(nse_velocity_degree + 1) = 3 (:708)
   CellValues cv;
-  cv.reinit(geom27, 3);
+  cv.reinit(geom64, 3);
   const int tdeg = ph->temperature_degree, ntd = T_dofs_per_cell(tdeg);
   std::fill(K, K + 89 * 89, 0.0);
   std::fill(f, f + 89, 0.0);
@@ -269,11 +298,11 @@ extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom27,
   }
 }
 
-extern "C" void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom27,
+extern "C" void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom64,
                                             double* P) {
   // boussinesq_model.tpp:421-464
   CellValues cv;
-  cv.reinit(geom27, 3);
+  cv.reinit(geom64, 3);
   std::fill(P, P + 89 * 89, 0.0);
   static thread_local NseShapes sh;
   for (int q = 0; q < cv.nq; ++q) {
@@ -288,12 +317,12 @@ extern "C" void orc_cell_nse_preconditioner(const orc_physics* ph, const double*
   }
 }
 
-extern "C" void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom27,
+extern "C" void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom64,
                                             double* M, double* Kt) {
   // boussinesq_model.tpp:748-800, QGauss(temperature_degree + 2) (:834)
   const int tdeg = ph->temperature_degree, n = T_dofs_per_cell(tdeg);
   CellValues cv;
-  cv.reinit(geom27, tdeg + 2);
+  cv.reinit(geom64, tdeg + 2);
   std::fill(M, M + n * n, 0.0);
   std::fill(Kt, Kt + n * n, 0.0);
   for (int q = 0; q < cv.nq; ++q) {
@@ -307,13 +336,13 @@ extern "C" void orc_cell_temperature_matrix(const orc_physics* ph, const double*
   }
 }
 
-extern "C" void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom27,
+extern "C" void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom64,
                                          const double* T_local, const double* u_local,
                                          const int* inhom_mask, double* rhs, double* mfbc) {
   // boussinesq_model.tpp:873-952, QGauss(temperature_degree + 2) (:990)
   const int tdeg = ph->temperature_degree, n = T_dofs_per_cell(tdeg);
   CellValues cv;
-  cv.reinit(geom27, tdeg + 2);
+  cv.reinit(geom64, tdeg + 2);
   std::fill(rhs, rhs + n, 0.0);
   std::fill(mfbc, mfbc + n * n, 0.0);
   const double dt_eff = ph->time_step / ph->nse_solver_interval;  // Q8
@@ -568,7 +597,7 @@ extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* 
   m->tdpc = T_dofs_per_cell(m->tdeg);
   m->cell_nse.assign(cell_nse_dofs, cell_nse_dofs + size_t(n_cells) * 89);
   m->cell_T.assign(cell_T_dofs, cell_T_dofs + size_t(n_cells) * m->tdpc);
-  m->geom.assign(cell_geom, cell_geom + size_t(n_cells) * 81);
+  m->geom.assign(cell_geom, cell_geom + size_t(n_cells) * 192);
   m->cnse.init(n_u + n_p, nse_c);
   m->cT.init(n_T, T_c);
   // setup_nse_matrices (boussinesq_model.tpp:79-112): couple everything but p-p
@@ -603,7 +632,7 @@ extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, con
   for (int c = 0; c < m->n_cells; ++c) {
     gather(m->cell_nse, c, 89, old_nse, ul.data());
     gather(m->cell_T, c, m->tdpc, old_T, Tl.data());
-    orc_cell_nse_system(&m->ph, &m->geom[81 * size_t(c)], ul.data(), Tl.data(), K.data(), f.data());
+    orc_cell_nse_system(&m->ph, &m->geom[192 * size_t(c)], ul.data(), Tl.data(), K.data(), f.data());
     // copy_local_to_global_nse_system (:677-687)
     distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)], K.data(), f.data(),
                                &m->nse, m->nse_rhs.data());
@@ -619,7 +648,7 @@ extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   std::vector<double> P(89 * 89);
   std::vector<std::pair<int, double>> ei, ej;
   for (int c = 0; c < m->n_cells; ++c) {
-    orc_cell_nse_preconditioner(&m->ph, &m->geom[81 * size_t(c)], P.data());
+    orc_cell_nse_preconditioner(&m->ph, &m->geom[192 * size_t(c)], P.data());
     const int* d = &m->cell_nse[89 * size_t(c)];
     bool any = false;
     for (int i = 0; i < 89; ++i) any |= m->cnse.constrained(d[i]);
@@ -664,7 +693,7 @@ extern "C" void orc_assemble_temperature_matrix(orc_model* m) {
   const int n = m->tdpc;
   std::vector<double> M(n * n), K(n * n);
   for (int c = 0; c < m->n_cells; ++c) {
-    orc_cell_temperature_matrix(&m->ph, &m->geom[81 * size_t(c)], M.data(), K.data());
+    orc_cell_temperature_matrix(&m->ph, &m->geom[192 * size_t(c)], M.data(), K.data());
     const int* d = &m->cell_T[size_t(n) * c];
     distribute_local_to_global(m->cT, n, d, M.data(), nullptr, &m->Tmass, nullptr);
     distribute_local_to_global(m->cT, n, d, K.data(), nullptr, &m->Tstiff, nullptr);
@@ -688,7 +717,7 @@ extern "C" void orc_assemble_temperature_rhs(orc_model* m, const double* old_T,
     gather(m->cell_T, c, n, old_T, Tl.data());
     gather(m->cell_nse, c, 89, nse_solution, ul.data());
     for (int i = 0; i < n; ++i) mask[i] = m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0;
-    orc_cell_temperature_rhs(&m->ph, &m->geom[81 * size_t(c)], Tl.data(), ul.data(), mask.data(),
+    orc_cell_temperature_rhs(&m->ph, &m->geom[192 * size_t(c)], Tl.data(), ul.data(), mask.data(),
                              rhs.data(), mfbc.data());
     distribute_rhs_with_bc(m->cT, n, d, rhs.data(), mfbc.data(), m->T_rhs.data());
   }
@@ -1379,7 +1408,7 @@ struct orc_feec {
   int n_cells, n_w, n_u, n_p, n, n_T;
   std::vector<int> dofs, cell_T;
   std::vector<signed char> sgn;
-  std::vector<double> X, geom27, diam;
+  std::vector<double> X, geom64, diam;
   Cons cons, cT;
   Csr nse, pre, Tmass, Tstiff, Tmat;
   std::vector<double> rhs, T_rhs, T_inv;
@@ -1428,17 +1457,18 @@ extern "C" orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const i
   make_pattern(m->Tmass, n_T, n_cells, 8, m->cell_T.data(), m->cT, [](int, int) { return true; });
   m->Tstiff = m->Tmass;
   m->Tmat = m->Tmass;
-  // Q1 temperature mapping as Q2-isoparametric nodes at the trilinear interpolants
-  m->geom27.resize(81 * size_t(n_cells));
+  // Q1 temperature mapping (temperature_mapping(1), FEEC.tpp:20) as the cubic
+  // map's support points at the trilinear interpolants
+  m->geom64.resize(192 * size_t(n_cells));
   for (int c = 0; c < n_cells; ++c)
-    for (int k = 0; k < 27; ++k) {
-      const double t[3] = {0.5 * (k % 3), 0.5 * ((k / 3) % 3), 0.5 * (k / 9)};
+    for (int k = 0; k < 64; ++k) {
+      const double t[3] = {kGL[k % 4], kGL[(k / 4) % 4], kGL[k / 16]};
       for (int d = 0; d < 3; ++d) {
         double x = 0;
         for (int v = 0; v < 8; ++v)
           x += lag1(vbit(v, 0), t[0]) * lag1(vbit(v, 1), t[1]) * lag1(vbit(v, 2), t[2]) *
                m->X[24 * size_t(c) + 3 * v + d];
-        m->geom27[81 * size_t(c) + 3 * k + d] = x;
+        m->geom64[192 * size_t(c) + 3 * k + d] = x;
       }
     }
   m->rhs.assign(m->n, 0.0);
@@ -1495,7 +1525,7 @@ extern "C" void orc_feec_assemble_temperature(orc_feec* m, const double* old_T,
   m->Tstiff.zero();
   std::vector<double> M(64), K(64);
   for (int c = 0; c < m->n_cells; ++c) {
-    orc_cell_temperature_matrix(&m->ph, &m->geom27[81 * size_t(c)], M.data(), K.data());
+    orc_cell_temperature_matrix(&m->ph, &m->geom64[192 * size_t(c)], M.data(), K.data());
     const int* d = &m->cell_T[8 * size_t(c)];
     distribute_local_to_global(m->cT, 8, d, M.data(), nullptr, &m->Tmass, nullptr);
     distribute_local_to_global(m->cT, 8, d, K.data(), nullptr, &m->Tstiff, nullptr);
@@ -1513,7 +1543,7 @@ extern "C" void orc_feec_assemble_temperature(orc_feec* m, const double* old_T,
   FeecValues fv;
   for (int c = 0; c < m->n_cells; ++c) {
     const int* d = &m->cell_T[8 * size_t(c)];
-    cv.reinit(&m->geom27[81 * size_t(c)], 3);
+    cv.reinit(&m->geom64[192 * size_t(c)], 3);
     fv.reinit(&m->X[24 * size_t(c)], &m->sgn[19 * size_t(c)], 3, gx, gw);
     std::fill(rhs.begin(), rhs.end(), 0.0);
     std::fill(mfbc.begin(), mfbc.end(), 0.0);

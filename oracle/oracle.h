@@ -18,7 +18,8 @@
  *
  * Conventions:
  *   - NSE local dofs in FESystem(FE_Q(2)^3, FE_Q(1)) order (89);
- *   - cell geometry = the 27 Q2 mapping nodes in lexicographic order;
+ *   - cell geometry = the 64 MappingQ(3) support points (Gauss-Lobatto,
+ *     lexicographic) of the reference's mapping(3) (boussinesq_model.tpp:20);
  *   - temperature local dofs in FE_Q(k) hierarchic order (k = 1: vertex order);
  *   - global NSE vector = [velocity (n_u) | pressure (n_p)].
  */
@@ -56,17 +57,17 @@ typedef struct {
 /* ---- element level (one cell) ------------------------------------------ */
 /* local_assemble_nse_system (boussinesq_model.tpp:550-673). u_local: 89 NSE
  * coefficients (pressure ignored); T_local: temperature coefficients. */
-void orc_cell_nse_system(const orc_physics* ph, const double* geom27,
+void orc_cell_nse_system(const orc_physics* ph, const double* geom64,
                          const double* u_local, const double* T_local,
                          double* K /*89x89 row-major*/, double* f /*89*/);
 /* local_assemble_nse_preconditioner (:421-464) */
-void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom27, double* P);
+void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom64, double* P);
 /* local_assemble_temperature_matrix (:748-800) */
-void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom27, double* M,
+void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom64, double* M,
                                  double* K);
 /* local_assemble_temperature_rhs (:873-952). inhom_mask[i] != 0 marks an
  * inhomogeneously constrained local dof (fills matrix_for_bc column i). */
-void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom27,
+void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom64,
                               const double* T_local, const double* u_local,
                               const int* inhom_mask, double* rhs, double* matrix_for_bc);
 
@@ -74,7 +75,7 @@ void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom27,
 typedef struct orc_model orc_model;
 
 orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs /*89*/,
-                      const int* cell_T_dofs, const double* cell_geom /*27x3*/, int n_u,
+                      const int* cell_T_dofs, const double* cell_geom /*64x3*/, int n_u,
                       int n_p, int n_T, const orc_constraints* nse_c,
                       const orc_constraints* T_c);
 void orc_destroy(orc_model* m);

@@ -104,20 +104,20 @@ def physics(ph) -> OrcPhysics:
     return o
 
 
-def cell_nse_system(ph, geom27, u_local, T_local):
+def cell_nse_system(ph, geom64, u_local, T_local):
     K = np.zeros((89, 89))
     f = np.zeros(89)
     o = physics(ph)
-    lib().orc_cell_nse_system(C.byref(o), _p(np.ascontiguousarray(geom27, np.float64)),
+    lib().orc_cell_nse_system(C.byref(o), _p(np.ascontiguousarray(geom64, np.float64)),
                               _p(np.ascontiguousarray(u_local, np.float64)),
                               _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
     return K, f
 
 
-def cell_nse_preconditioner(ph, geom27):
+def cell_nse_preconditioner(ph, geom64):
     P = np.zeros((89, 89))
     o = physics(ph)
-    lib().orc_cell_nse_preconditioner(C.byref(o), _p(np.ascontiguousarray(geom27, np.float64)), _p(P))
+    lib().orc_cell_nse_preconditioner(C.byref(o), _p(np.ascontiguousarray(geom64, np.float64)), _p(P))
     return P
 
 

@@ -42,7 +42,8 @@ def make(refine=1):
     ph = dcp.classic_physics()
     out = {"n": np.array([m.n_cells, m.n_u, m.n_p, m.n_T], np.int64),
            "cell_nse_dofs": m.cell_nse_dofs.astype(np.int32),
-           "cell_T_dofs": m.cell_T_dofs.astype(np.int32)}
+           "cell_T_dofs": m.cell_T_dofs.astype(np.int32),
+           "cell_geometry": m.cell_geometry.copy()}
     for name, (u, T) in states(m).items():
         K = np.zeros((4, 89, 89))
         f = np.zeros((4, 89))

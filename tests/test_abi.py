@@ -39,7 +39,7 @@ def test_no_cpu_fallback():
 
 def test_host_mesh_helpers_without_gpu():
     m = dcp.HostMesh(refine=1)
-    assert m.cell_geometry.shape == (48, 27, 3)
+    assert m.cell_geometry.shape == (48, 64, 3)  # MappingQ(3) support points
     assert m.cell_nse_dofs.shape == (48, 89)
 
 
@@ -66,13 +66,17 @@ def test_upload_rejects_bad_dof_layout():
 
 
 @pytest.mark.parametrize("r", [1, 2, 3])
-def test_separable_geometry_detection(r):
-    """The shell's Q2 support points are r_c * phi_ab: one 2D table per column
-    of cells (6 N^2) and one radial table per layer (N)."""
-    m = dcp.HostMesh(refine=r)
+@pytest.mark.parametrize("all_cells", [False, True])
+def test_separable_geometry_detection(r, all_cells):
+    """The shell's MappingQ(3) support points are rho_c * Phi_ab: one 2D table
+    per column of cells (6 N^2; twice that with deal.II 9.2's trilinear
+    interior cells, whose Phi is the bilinear blend) and one radial table per
+    layer (N)."""
+    m = dcp.HostMesh(refine=r, mapping_q_on_all_cells=all_cells)
     N = 2 ** r
-    assert m.geometry_info() == (True, 6 * N * N, N)
-    # a smooth displacement breaks the separability: general MappingQ2 path
+    kinds = 1 if (all_cells or N <= 2) else 2
+    assert m.geometry_info() == (True, kinds * 6 * N * N, N)
+    # a smooth displacement breaks the separability: general streamed path
     m.cell_geometry = m.cell_geometry.copy()
     X = m.cell_geometry.reshape(-1, 3)
     X += 0.02 * np.sin(3.0 * X[:, [1, 2, 0]]) * np.cos(2.0 * X[:, [2, 0, 1]])

@@ -30,8 +30,11 @@ def rel(a, b):
     return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
 
 
-def test_dof_indexing_bit_exact(gold, mesh):
+def test_host_setup_regression(gold, mesh):
+    """The host mesh/DoF setup reproduces its own earlier output (a regression
+    freeze of mesh.cpp, NOT a parity check against deal.II's numbering)."""
     assert list(gold["n"]) == [mesh.n_cells, mesh.n_u, mesh.n_p, mesh.n_T]
+    assert rel(mesh.cell_geometry, gold["cell_geometry"]) < 1e-15
     assert np.array_equal(gold["cell_nse_dofs"], mesh.cell_nse_dofs)
     assert np.array_equal(gold["cell_T_dofs"], mesh.cell_T_dofs)
     assert np.array_equal(gold["physical_T"], mesh.T0)
@@ -94,7 +97,7 @@ def test_gpu_matches_fixture(gold, mesh):
     assert rel(ctx.get_state(dcp.T_RHS), gold["T_rhs"]) < 1e-12
     rc, outer, inner = ctx.solve_nse()
     g = gold["iters"]
-    assert rc == g[0] and outer == g[1] and abs(inner - g[2]) <= 0.05 * g[2]
+    assert rc == g[0] and outer == g[1] and abs(inner - g[2]) <= 0.10 * g[2]
     x = ctx.get_state(dcp.NSE_SOLUTION)
     assert np.linalg.norm(x - gold["nse_solution"]) <= 1e-10 * np.linalg.norm(gold["nse_solution"])
     rcT, itT, _ = ctx.solve_temperature()

@@ -28,7 +28,20 @@ def kron3(a, b, c):
     return np.kron(c, np.kron(b, a))
 
 
+GL = np.array([0.0, 0.5 - 0.5 / np.sqrt(5.0), 0.5 + 0.5 / np.sqrt(5.0), 1.0])
+
+
 def cube_geom(h):
+    """MappingQ(3) support points of the affine cube [0,h]^3 (64, lexicographic
+    over the Gauss-Lobatto points)."""
+    g = np.zeros((64, 3))
+    for n in range(64):
+        g[n] = [h * GL[n % 4], h * GL[(n // 4) % 4], h * GL[n // 16]]
+    return g
+
+
+def cube_nodes(h):
+    """The 27 Q2 support points of the same cube (lexicographic)."""
     g = np.zeros((27, 3))
     for n in range(27):
         g[n] = [h * (n % 3) / 2, h * ((n // 3) % 3) / 2, h * (n // 9) / 2]
@@ -121,13 +134,13 @@ def test_rhs_advection_and_coriolis_linear_field():
     ph = dcp.classic_physics(time_step=0.2)
     ph.cuboid = 1
     ph.omega = 1.5
-    g = cube_geom(h)
+    g = cube_nodes(h)
     u = np.zeros(89)
     for i in range(89):
         c, l = sysdof(i)
         if c == 0:
             u[i] = g[l, 1]
-    K, f = oracle_py.cell_nse_system(ph, g, u, np.full(8, ph.temperature_ref))
+    K, f = oracle_py.cell_nse_system(ph, cube_geom(h), u, np.full(8, ph.temperature_ref))
     _, idx = velocity_block(K)
     M3 = kron3(M1, M1, M1)
     yv = g[:, 1]
@@ -178,9 +191,9 @@ def test_solver_tolerances_honoured():
     assert np.allclose(Tn[tc.line_dof], tc.inhomogeneity)
 
 
-def _schur_parts(r, normals):
+def _schur_parts(r, normals, all_cells=True):
     import scipy.sparse as sp
-    m = dcp.HostMesh(refine=r, normals=normals)
+    m = dcp.HostMesh(refine=r, normals=normals, mapping_q_on_all_cells=all_cells)
     ph = dcp.classic_physics()
     o = oracle_py.Model(ph, m)
     o.assemble_nse_system(np.zeros(m.n_u + m.n_p), m.T0)
@@ -192,14 +205,19 @@ def _schur_parts(r, normals):
     return m, o, A[m.n_u:, :m.n_u], A[:m.n_u, m.n_u:], Ad
 
 
-def test_consistent_normals_make_constant_pressure_exactly_singular():
-    """DESIGN.md 'no-normal-flux normals': with consistent normals C^T B^T 1 = 0
-    to roundoff, so S = B D^-1 B^T has the constant as an exact null vector that
-    the FGMRES Krylov vectors never excite; with radial (support-point) normals
-    the constant is only a near-null vector whose eigenvalue shrinks ~50x per
-    refinement (2.4e-3, 8.8e-5, 1.7e-6 at r = 1, 2, 3)."""
+def test_constant_pressure_mode_is_near_null():
+    """DESIGN.md 'no-normal-flux normals': under MappingQ(3) and QGauss(3) the
+    divergence block no longer integrates grad(phi_i) exactly (the cofactor of
+    a cubic map times grad phi exceeds degree 5 per direction), so B^T 1 does
+    not vanish on interior rows and the constant pressure is a near-null, not a
+    null, vector of S whatever the boundary normals: O(1e-6) at r = 2 with the
+    cubic map on every cell, O(1e-2) on the interface layer with deal.II 9.2's
+    MappingQ (cubic boundary cells against trilinear interior cells)."""
     m, o, B, Bt, Ad = _schur_parts(2, "consistent")
-    assert np.abs(Bt @ np.ones(m.n_p)).max() < 1e-14
+    v = np.abs(Bt @ np.ones(m.n_p))
+    assert 1e-8 < v.max() < 1e-5
+    m, o, B, Bt, Ad = _schur_parts(2, "consistent", all_cells=False)
+    assert np.abs(Bt @ np.ones(m.n_p)).max() > 1e-3
     m, o, B, Bt, Ad = _schur_parts(2, "radial")
     S = (B @ (Bt.multiply(1 / Ad[:, None]))).toarray()
     w = np.linalg.eigvalsh(0.5 * (S + S.T))
@@ -208,7 +226,9 @@ def test_consistent_normals_make_constant_pressure_exactly_singular():
     assert np.isclose(one @ S @ one, w[0], rtol=0.1)
 
 
-def test_shell_solve_converges_with_consistent_normals():
+def test_shell_solve_converges_r2():
+    """r = 2 with the reference's geometry (MappingQ(3), deal.II 9.2) and
+    no-normal-flux normals: 27 FGMRES iterations, ~1900 inner."""
     m = dcp.HostMesh(refine=2)
     o = oracle_py.Model(dcp.classic_physics(), m)
     u = np.zeros(m.n_u + m.n_p)

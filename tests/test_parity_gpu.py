@@ -175,12 +175,13 @@ def test_full_solve_and_temperature(setup, explicit):
     orc.assemble_temperature_rhs(T, u)
     rco, x_o, outer_o, inner_o = orc.solve_nse(u)
     assert rc == rco == 0
-    # The inner Schur GMRES stops on a 1e-6 residual estimate while stagnating,
-    # so its iteration count is sensitive to summation order: the oracle with
-    # its dot products summed in reverse order needs 3115 instead of 3078 inner
-    # iterations at r=2 while the solutions agree to 2e-12 (parity).
+    # The inner Schur GMRES stops on a 1e-6 residual estimate while it
+    # stagnates on the near-null constant pressure mode of S (DESIGN.md,
+    # "no-normal-flux normals"), so its iteration count follows the summation
+    # order: ~1870 inner iterations at r=2, GPU and oracle within a few
+    # percent, while the outer count is equal and the iterates agree to 1e-10.
     assert outer == outer_o
-    assert abs(inner - inner_o) <= 0.05 * inner_o
+    assert abs(inner - inner_o) <= 0.10 * inner_o
     x_g = ctx.get_state(dcp.NSE_SOLUTION)
     assert rel2(x_g, x_o) < 1e-10
     rc, it, rng_T = ctx.solve_temperature()
@@ -224,11 +225,11 @@ def test_matrix_free_matches_assembled(kind):
     """kernels/matfree.hip against the block-CSR product of the assembled
     nse_matrix (same operator, summation order differs), on random inputs
     including the constrained entries."""
-    m = dcp.HostMesh(refine=int(kind[-1]), normals="radial" if "radial" in kind else "consistent")
+    m = dcp.HostMesh(refine=int(kind[-1]), normals="radial" if "radial" in kind else "mapping")
     if kind.startswith("warped"):
         # a smooth displacement of every support point (a function of the point,
         # so shared nodes stay shared): the geometry is no longer radially
-        # separable and the kernel takes its general MappingQ2 path
+        # separable and the kernel takes its general (streamed J^-1 / JxW) path
         X = m.cell_geometry.reshape(-1, 3)
         X += 0.02 * np.sin(3.0 * X[:, [1, 2, 0]]) * np.cos(2.0 * X[:, [2, 0, 1]])
     ph = dcp.classic_physics()
