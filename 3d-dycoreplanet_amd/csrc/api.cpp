@@ -907,6 +907,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->feec_zero_mean = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_FGMRES_MAX_OUTER) {
+      require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_FGMRES_MAX_OUTER must be >= 1");
+      ctx->fgmres_max_outer = value;
+      return DCP_OK;
+    }
     fail(DCP_ERR_INVALID, "unknown option " + std::to_string(option));
   });
 }
@@ -1455,6 +1460,7 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     c.timings.velocity_apply_ms_avg = mf_ms[1];
     c.timings.stokes_applies = c.mf_calls[0];
     c.timings.velocity_applies = c.mf_calls[1];
+    c.timings.a_solve_iterations = c.a_solve_its;
     t.stop();
     return rc;
   });

@@ -167,6 +167,8 @@ struct Ctx {
   unsigned long long spec_seq = 0;   // inner Schur GMRES step numbers (ready flags)
   int n_cus = 0;
   bool fused_chain = true;
+  int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
+  long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
   // test hooks, read at context creation: DCP_SCHUR_AHEAD=0 turns the inner
   // Schur GMRES's launch-ahead off; DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger

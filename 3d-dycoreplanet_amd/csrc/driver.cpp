@@ -63,14 +63,19 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
     }
     if ((rc = dcp_assemble_temperature_matrix(ctx)) < 0) return rc;
     if ((rc = dcp_assemble_temperature_rhs(ctx)) < 0) return rc;
-    // the NSE solve runs every step (:1895-1902)
-    if (feec) {
-      int it = 0;
-      rc = dcp_feec_solve_nse(ctx, &it);
-      r.fgmres_outer = it;
-      r.schur_inner = 0;
-    } else {
-      rc = dcp_solve_nse(ctx, &r.fgmres_outer, &r.schur_inner);
+    // solve_NSE_block_preconditioned is called every step (:1895-1902) but
+    // solves only on step 0 and every NSE interval (its own guard, :1135-1137;
+    // FEEC.tpp:1272-1274); otherwise nse_solution stays as it is
+    r.fgmres_outer = r.schur_inner = 0;
+    rc = DCP_OK;
+    if (n == 0 || n % interval == 0) {
+      if (feec) {
+        int it = 0;
+        rc = dcp_feec_solve_nse(ctx, &it);
+        r.fgmres_outer = it;
+      } else {
+        rc = dcp_solve_nse(ctx, &r.fgmres_outer, &r.schur_inner);
+      }
     }
     if (rc < 0) return rc;
     if (rc == DCP_NOT_CONVERGED) {  // the reference throws out of run()

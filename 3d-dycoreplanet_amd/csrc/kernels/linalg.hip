@@ -191,10 +191,10 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
 // chain's nb workgroups, all resident (nb <= the CU count, checked by the
 // launcher), and every workgroup keeps its <= kMgsElems entries of w in
 // registers for the whole chain. A step's nb block sums are handed to every
-// workgroup as 16-byte granules {sum, tag} written by one `sc1` store and
-// polled with `sc1` loads (agent-coherent, no fences: the tag travels with
-// the value in one untorn 16-byte access); the tag = launch sequence * 64 +
-// step is never reused, so the granule array needs no clearing. Every
+// workgroup as 16-byte granules {sum, tag ^ mix(sum)} written by one `sc1`
+// store and polled with `sc1` loads (agent-coherent, no fences; the value
+// checksum in the tag half rejects a torn read); the tag = launch sequence *
+// 64 + step is never reused, so the granule array needs no clearing. Every
 // workgroup then forms the coefficient from the nb sums in exactly the order
 // k_chain_add_and_dot uses, so the chain is bitwise the per-step one.
 // Spins are bounded (an unbounded wait would hang the device): a workgroup
@@ -209,18 +209,33 @@ constexpr int kMgsElems = DCP_MGS_ELEMS;
 constexpr long kMgsMaxSpins = 1L << 21;
 typedef unsigned int mgs_u4 __attribute__((ext_vector_type(4)));
 
+// The tag half of a granule carries tag ^ mix(value bits): the memory model
+// guarantees single-copy atomicity only up to 64 bits, so a reader could see
+// the two halves of a 16-byte access from different writes; such a torn read
+// (new tag with an old value, or the reverse) fails the check below and is
+// simply polled again (a false match needs a 64-bit hash collision).
+__device__ inline unsigned long long granule_mix(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
 __device__ inline void granule_store(double* p, double v, unsigned long long tag) {
   const unsigned long long b = __double_as_longlong(v);
+  const unsigned long long t = tag ^ granule_mix(b);
   mgs_u4 q;
   q.x = unsigned(b);
   q.y = unsigned(b >> 32);
-  q.z = unsigned(tag);
-  q.w = unsigned(tag >> 32);
+  q.z = unsigned(t);
+  q.w = unsigned(t >> 32);
   asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(q) : "memory");
 }
 
 __device__ inline bool tag_is(const mgs_u4& q, unsigned long long tag) {
-  return q.z == unsigned(tag) && q.w == unsigned(tag >> 32);
+  const unsigned long long t = tag ^ granule_mix(((unsigned long long)q.y << 32) | q.x);
+  return q.z == unsigned(t) && q.w == unsigned(t >> 32);
 }
 __device__ inline double granule_value(const mgs_u4& q) {
   return __longlong_as_double((long long)(((unsigned long long)q.y << 32) | q.x));

@@ -29,6 +29,7 @@ OPT_SCHUR_EXPLICIT = 1
 OPT_FEEC_ZERO_MEAN = 2
 OPT_MATRIX_FREE = 3
 OPT_FUSED_CHAIN = 4
+OPT_FGMRES_MAX_OUTER = 5
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -87,6 +88,7 @@ class Timings(C.Structure):
         ("schur_apply_ms_avg", C.c_double), ("schur_applies", C.c_long),
         ("stokes_apply_ms_avg", C.c_double), ("velocity_apply_ms_avg", C.c_double),
         ("stokes_applies", C.c_long), ("velocity_applies", C.c_long),
+        ("a_solve_iterations", C.c_long),
     ]
 
 
@@ -526,6 +528,11 @@ class Context:
         self._keep = (m,)
         self._check(lib().dcp_feec_mesh_upload(self._h, C.byref(self._feec_view)))
         self.mesh = m
+
+    def set_fgmres_max_outer(self, n: int):
+        """DCP_OPT_FGMRES_MAX_OUTER (test hook): cap of the first FGMRES(30)
+        (the reference's 40); lower caps force the do_solve_A fallback."""
+        self._check(lib().dcp_set_option(self._h, OPT_FGMRES_MAX_OUTER, int(n)))
 
     def set_fused_chain(self, on: bool):
         """DCP_OPT_FUSED_CHAIN: one launch per Gram-Schmidt chain (default) or

@@ -139,6 +139,11 @@ enum { DCP_OPT_MATRIX_FREE = 3 };
  *   one launch whose workgroups hand each step's reduction to each other on the
  *   device; 0 = one launch per step. Bitwise the same results. */
 enum { DCP_OPT_FUSED_CHAIN = 4 };
+/* DCP_OPT_FGMRES_MAX_OUTER (test hook, default 40): the iteration cap of the
+ *   first FGMRES(30) (SolverControl(40, ...), boussinesq_model.tpp:1166); a
+ *   lower cap sends small meshes through the do_solve_A / FGMRES(50) fallback
+ *   (:1203-1232) that the reference takes when the cap is hit. */
+enum { DCP_OPT_FGMRES_MAX_OUTER = 5 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
@@ -244,6 +249,9 @@ typedef struct {
    * (nse_matrix.vmult) and A alone (do_solve_A fallback); sampled device time */
   double stokes_apply_ms_avg, velocity_apply_ms_avg;
   long stokes_applies, velocity_applies;
+  /* AztecOO A-GMRES iterations of the do_solve_A fallback (not reported by
+   * the reference; block_schur_preconditioner.hpp:59-67) */
+  long a_solve_iterations;
 } dcp_timings;
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
 

@@ -582,6 +582,7 @@ struct orc_model {
   // scratch of the Schur complement (schur_complement.hpp:113)
   mutable std::vector<double> tmp1, tmp2;
   int inner_iterations = 0;
+  long a_solve_iterations = 0;  // AztecOO A-GMRES iterations of the last solve (do_solve_A)
 };
 
 extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
@@ -914,6 +915,87 @@ void gmres(int n, OpA A, OpP P, double* x, const double* b, Control& ctl, int& i
   if (state != kSuccess) throw NoConvergence();
 }
 
+// TrilinosWrappers::SolverGMRES (block_schur_preconditioner.hpp:59-67; LA =
+// TrilinosWrappers, base/config.h:20-28) -> AztecOO's AZ_gmres, restated from
+// the published AztecOO algorithm (Trilinos az_gmres.c) with the options
+// deal.II's SolverBase::do_solve sets: AZ_kspace = restart parameter (default
+// 30), AZ_conv = AZ_noscaled (absolute |r|_2), AZ_orthog = AZ_classic
+// (classical Gram-Schmidt with one re-orthogonalisation pass), the
+// preconditioner applied from the RIGHT (v_{i+1} = A M^-1 v_i, x += M^-1 V y).
+// The recursive residual ends an Arnoldi cycle; convergence is then confirmed
+// on the true residual b - A x (a cycle whose true residual misses the
+// tolerance continues, AztecOO's loss-of-precision path). deal.II finally
+// checks the true residual: SolverControl::check(NumIters, TrueResidual),
+// NoConvergence when it exceeds the tolerance.
+template <class OpA, class OpP>
+void aztec_gmres(int n, OpA A, OpP Minv, double* x, const double* b, double tol, int max_it,
+                 int kspace, int& iters_out) {
+  std::vector<std::vector<double>> v(kspace + 1, std::vector<double>(n, 0.0));
+  std::vector<double> r(n), z(n), w(n);
+  std::vector<std::vector<double>> H(kspace + 1, std::vector<double>(kspace, 0.0));
+  std::vector<double> rs(kspace + 1, 0.0), cs(kspace, 0.0), sn(kspace, 0.0), h(kspace + 1, 0.0);
+  auto residual = [&]() {
+    A(x, r.data());
+    for (int k = 0; k < n; ++k) r[k] = b[k] - r[k];
+    return std::sqrt(dotv(r.data(), r.data(), n));
+  };
+  double rnorm = residual();
+  bool converged = rnorm < tol;
+  int iter = 0;
+  while (!converged && iter < max_it) {
+    for (int k = 0; k < n; ++k) v[0][k] = r[k] / rnorm;
+    rs[0] = rnorm;
+    int i = 0;
+    bool cycle_converged = false;
+    while (i < kspace && !cycle_converged && iter < max_it) {
+      ++iter;
+      Minv(v[i].data(), z.data());
+      A(z.data(), w.data());
+      for (int pass = 0; pass < 2; ++pass) {  // classical Gram-Schmidt, twice
+        std::vector<double> c(i + 1);
+        for (int k = 0; k <= i; ++k) c[k] = dotv(v[k].data(), w.data(), n);
+        for (int k = 0; k <= i; ++k)
+          for (int q = 0; q < n; ++q) w[q] -= c[k] * v[k][q];
+        for (int k = 0; k <= i; ++k) h[k] = pass ? h[k] + c[k] : c[k];
+      }
+      const double hn = std::sqrt(dotv(w.data(), w.data(), n));
+      h[i + 1] = hn;
+      if (hn != 0)
+        for (int q = 0; q < n; ++q) v[i + 1][q] = w[q] / hn;
+      for (int k = 0; k < i; ++k) {  // previous plane rotations
+        const double t = h[k];
+        h[k] = cs[k] * t + sn[k] * h[k + 1];
+        h[k + 1] = cs[k] * h[k + 1] - sn[k] * t;
+      }
+      const double d = std::sqrt(h[i] * h[i] + h[i + 1] * h[i + 1]);
+      cs[i] = h[i] / d;
+      sn[i] = h[i + 1] / d;
+      rs[i + 1] = -sn[i] * rs[i];
+      rs[i] = cs[i] * rs[i];
+      h[i] = cs[i] * h[i] + sn[i] * h[i + 1];
+      for (int k = 0; k <= i; ++k) H[k][i] = h[k];
+      cycle_converged = std::fabs(rs[i + 1]) < tol;
+      ++i;
+    }
+    // y = H^-1 rs (upper triangular), x += M^-1 (V y)
+    std::vector<double> y(i, 0.0);
+    for (int k = i - 1; k >= 0; --k) {
+      double t = rs[k];
+      for (int j = k + 1; j < i; ++j) t -= H[k][j] * y[j];
+      y[k] = t / H[k][k];
+    }
+    std::fill(w.begin(), w.end(), 0.0);
+    for (int k = 0; k < i; ++k)
+      for (int q = 0; q < n; ++q) w[q] += y[k] * v[k][q];
+    Minv(w.data(), z.data());
+    for (int q = 0; q < n; ++q) x[q] += z[q];
+    rnorm = residual();
+    converged = cycle_converged && rnorm < tol;
+  }
+  iters_out = iter;
+  if (!(rnorm <= tol)) throw NoConvergence();
+}
+
 // deal.II Householder<double> (initialize + least_squares).
 double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
                                  std::vector<double>& dst, const std::vector<double>& src) {
@@ -971,14 +1053,15 @@ void block_prec_vmult(orc_model* m, const double* src, double* dst, bool do_solv
     for (int i = 0; i < nu; ++i) utmp[i] += src[i];
   }
   if (do_solve_A) {
-    // TrilinosWrappers::SolverGMRES (AztecOO) restated as deal.II GMRES with
-    // the A-Jacobi preconditioner, tol 1e-2 ||utmp|| (:59-67).
-    Control ctl{5000, norm2(utmp, 0, nu) * 1e-2};
+    // LA::SolverGMRES = AztecOO GMRES(30) with the A-Jacobi (Ifpack point
+    // Jacobi) from the right, absolute tol 1e-2 ||utmp||, <= 5000 (:59-67);
+    // initial guess: what dst's velocity block holds.
     int it = 0;
-    gmres(
+    aztec_gmres(
         nu, [&](const double* x, double* y) { block_vmult(m->nse, 0, nu, 0, nu, x, y, false); },
         [&](const double* x, double* y) { for (int i = 0; i < nu; ++i) y[i] = x[i] * m->A_inv[i]; },
-        dst, utmp.data(), ctl, it);
+        dst, utmp.data(), norm2(utmp, 0, nu) * 1e-2, 5000, 30, it);
+    m->a_solve_iterations += it;
   } else {
     for (int i = 0; i < nu; ++i) dst[i] = utmp[i] * m->A_inv[i];
   }
@@ -1085,6 +1168,7 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
   for (int i = nu; i < n; ++i) x[i] *= dt;                         // :1177 (Q1)
   int inner = 0, acc1 = 0, acc2 = 0;
   int status = 0;
+  m->a_solve_iterations = 0;
   try {
     State s = fgmres(m, x.data(), m->nse_rhs.data(), 30, unsigned(max_outer), tol, false, acc1, inner);
     if (s != kSuccess) throw NoConvergence();
@@ -1105,6 +1189,8 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
   m->inner_iterations = inner;
   return status;
 }
+
+extern "C" long orc_a_solve_iterations(const orc_model* m) { return m->a_solve_iterations; }
 
 extern "C" int orc_solve_temperature(orc_model* m, double* T, int* iterations) {
   // solve_temperature (:1417-1476): SolverCG + Jacobi, tol 1e-12 ||rhs||, max n_T

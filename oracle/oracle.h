@@ -109,6 +109,8 @@ void orc_block_preconditioner_vmult(orc_model* m, const double* src, double* dst
 int orc_solve_nse(orc_model* m, double* nse_solution /*inout*/, int* outer_iterations,
                   int* inner_iterations, int max_outer /* 40 in the reference */);
 int orc_solve_temperature(orc_model* m, double* T_solution /*inout*/, int* iterations);
+/* AztecOO A-GMRES iterations of the last orc_solve_nse (do_solve_A fallback). */
+long orc_a_solve_iterations(const orc_model* m);
 
 /* Step control (get_maximal_velocity / get_cfl_number, :1023-1101). */
 double orc_max_velocity(const orc_model* m, const double* nse_solution);

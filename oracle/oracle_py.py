@@ -67,6 +67,8 @@ def lib():
         L.orc_block_preconditioner_vmult.argtypes = [P, P, P, I, P]
         L.orc_solve_nse.argtypes = [P, P, P, P, I]
         L.orc_solve_temperature.argtypes = [P, P, P]
+        L.orc_a_solve_iterations.argtypes = [P]
+        L.orc_a_solve_iterations.restype = C.c_long
         L.orc_max_velocity.argtypes = [P, P]
         L.orc_max_velocity.restype = D
         L.orc_cfl.argtypes = [P, P, P]
@@ -217,6 +219,10 @@ class Model:
         o, i = C.c_int(0), C.c_int(0)
         rc = lib().orc_solve_nse(self.h, _p(x), C.byref(o), C.byref(i), int(max_outer))
         return rc, x, o.value, i.value
+
+    def a_solve_iterations(self):
+        """AztecOO A-GMRES iterations of the last solve_nse (do_solve_A fallback)."""
+        return int(lib().orc_a_solve_iterations(self.h))
 
     def solve_temperature(self, T):
         x = np.array(T, dtype=np.float64, copy=True)

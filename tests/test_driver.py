@@ -26,11 +26,16 @@ def fresh(rp, m):
 
 
 @pytest.mark.gpu
-def test_run_matches_step_by_step_calls():
+@pytest.mark.parametrize("interval", [1, 2])
+def test_run_matches_step_by_step_calls(interval):
+    """interval = NSE solver interval: the NSE system is reassembled AND solved
+    only on step 0 and every interval-th step (run(), :1865-1881, and
+    solve_NSE_block_preconditioned's own guard, :1135-1137)."""
     rp = dcp.load_prm(PRM)
     rp.initial_global_refinement = 1
     rp.adapt_time_step = 1           # recompute_time_step from step 1 on
     rp.final_time = 100.0
+    rp.physics.nse_solver_interval = interval
     m = dcp.HostMesh(refine=1, R0=rp.R0, R1=rp.R1, length=rp.length)
     nsteps = 3
     ctx = fresh(rp, m)
@@ -44,22 +49,28 @@ def test_run_matches_step_by_step_calls():
     t = 0.0
     for n in range(nsteps):
         cfl = ctx.cfl_number()
-        if n > 0 and rp.adapt_time_step:
+        nse_step = n % interval == 0
+        if n > 0 and nse_step and rp.adapt_time_step:
             deg = max(rp.physics.temperature_degree, rp.nse_velocity_degree)
             dt = (0.25 / (2.1 * 3 * math.sqrt(3))) / (deg * cfl)
             ctx.set_time_step(dt)
         ctx.max_velocity()
         assert steps[n].time_step == dt and steps[n].time_index == t
-        ctx.assemble_nse_system()
-        ctx.build_nse_preconditioner()
+        if nse_step:
+            ctx.assemble_nse_system()
+            ctx.build_nse_preconditioner()
         ctx.assemble_temperature_matrix()
         ctx.assemble_temperature_rhs()
-        rcn, outer, inner = ctx.solve_nse()
+        if nse_step:
+            rcn, outer, inner = ctx.solve_nse()
+            assert outer > 0
+        else:
+            rcn, outer, inner = 0, 0, 0
         assert (rcn, outer, inner) == (0, steps[n].fgmres_outer, steps[n].schur_inner)
         ctx.solve_temperature()
         ctx.advance_state()
         t += dt / rp.physics.nse_solver_interval
-    assert steps[1].time_step != steps[0].time_step  # the adaptive step took effect
+    assert steps[interval].time_step != steps[0].time_step  # the adaptive step took effect
     assert np.array_equal(ctx.get_state(dcp.NSE_SOLUTION), u_run)
     assert np.array_equal(ctx.get_state(dcp.T_SOLUTION), T_run)
     ctx.close()

@@ -194,6 +194,39 @@ def test_full_solve_and_temperature(setup, explicit):
     assert np.isclose(ctx.cfl_number(), orc.cfl(x_g), rtol=1e-12)
 
 
+@pytest.mark.parametrize("max_outer", [10, 3])
+def test_fallback_solve_do_solve_A(setup, max_outer):
+    """Q10 (boussinesq_model.tpp:1166-1232): the first FGMRES(30) is capped
+    (test hook, identical in oracle and GPU) so the reference's fallback runs:
+    BlockSchurPreconditioner with do_solve_A = true, whose velocity block is
+    solved by TrilinosWrappers::SolverGMRES = AztecOO GMRES(30), right Jacobi,
+    tol 1e-2 |utmp| (block_schur_preconditioner.hpp:59-67), inside FGMRES(50).
+    Same outer count, iterate at 1e-10."""
+    m, ph, ctx, orc = setup
+    ctx.set_schur_explicit(True)
+    u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    ctx.set_fgmres_max_outer(max_outer)
+    try:
+        rc, outer, inner = ctx.solve_nse()
+        a_its = ctx.timings()["a_solve_iterations"]
+    finally:
+        ctx.set_fgmres_max_outer(40)
+    orc.assemble_nse_system(u, T)
+    orc.build_nse_preconditioner()
+    rco, x_o, outer_o, inner_o = orc.solve_nse(u, max_outer=max_outer)
+    a_o = orc.a_solve_iterations()
+    assert rc == rco == 0
+    assert outer == outer_o and outer > max_outer  # the fallback ran
+    assert a_o > 0 and abs(a_its - a_o) <= max(2, 0.02 * a_o)
+    assert abs(inner - inner_o) <= 0.10 * inner_o
+    assert rel2(ctx.get_state(dcp.NSE_SOLUTION), x_o) < 1e-10
+
+
 def test_large_mesh_properties():
     """r = 4 (24,576 cells, 634,600 NSE dofs): size-independent identities."""
     m = dcp.HostMesh(refine=4)
