@@ -4,7 +4,8 @@
 Workload (BASELINE.json metric): 3D hypershell, classic Q2/Q1 Taylor-Hood,
 global refinement 5 (196,608 cells, 4,995,528 NSE dofs + 202,818 T dofs),
 data/aqua_planet_shell_test_3d-classic.prm physics, the reference initial state
-(u = 0, two-Gaussian temperature), synthetic mesh (equiangular cube-sphere).
+(u = 0, two-Gaussian temperature), synthetic mesh (hyper_shell refined with
+SphericalManifold's rules, MappingQ(3) cell maps as deal.II 9.2's MappingQ).
 
 One "step" = one full reference time step (Standard::BoussinesqModel::run body,
 boussinesq_model.tpp:1843-1926): assemble_nse_system, build_nse_preconditioner,
@@ -98,22 +99,63 @@ def schur_bytes(m, nnzb_bt, nnzb_b):
     return bt + jac + b
 
 
-def cpu_baseline(refine):
-    """Oracle (C++ restatement of assemble_nse_system, 1 core) on a bounded sample."""
+def cpu_info():
+    """Host CPU model and the cores this process may use (GPU box: read at run time)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return model, os.cpu_count(), max(1, min(usable, omp) if omp > 0 else usable)
+
+
+def cpu_baseline(refine, inner_cap=200):
+    """The oracle (C++ restatement of the reference path) on a bounded sample,
+    timed on this host beside the GPU run:
+    * "Assemble NSE system" (boussinesq_model.tpp:695): the full
+      assemble_nse_system of the refine-`refine` shell on 1 core and on all
+      usable cores (WorkStream structure: threaded element work, serialized
+      copier in cell order);
+    * "Solve Stokes system" (:1139): inner Schur-complement GMRES iterations/s
+      of one BlockSchurPreconditioner::vmult (the loop that dominates the
+      solve), capped at `inner_cap` iterations."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import dcp
     import oracle_py
+    model, ncpu, threads = cpu_info()
     m = dcp.HostMesh(refine=refine)
     ph = dcp.classic_physics()
     orc = oracle_py.Model(ph, m)
     u = np.zeros(m.n_u + m.n_p)
+    n = m.n_u + m.n_p
     t0 = time.perf_counter()
     orc.assemble_nse_system(u, m.T0)
-    dt = time.perf_counter() - t0
-    return {"value": (m.n_u + m.n_p) / dt, "unit": "assembled DoFs/s", "cores": 1, "kind": "port",
+    t1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc.assemble_nse_system_threads(u, m.T0, threads)
+    tn = time.perf_counter() - t0
+    orc.build_nse_preconditioner()
+    orc.set_inner_max_steps(inner_cap)
+    src = np.random.default_rng(20261015).uniform(-1, 1, n)
+    t0 = time.perf_counter()
+    _, it = orc.block_preconditioner_vmult(src)
+    ts = time.perf_counter() - t0
+    its = inner_cap if it < 0 else it
+    return {"value": n / tn, "unit": "assembled DoFs/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "nproc": ncpu,
             "sample": f"full assemble_nse_system (element matrices + AffineConstraints "
                       f"distribute into CSR) of the refine={refine} shell: {m.n_cells} cells, "
-                      f"{m.n_u + m.n_p} NSE dofs, {dt:.2f} s on 1 core"}
+                      f"{n} NSE dofs, {tn:.2f} s on {threads} cores ({t1:.2f} s on 1)",
+            "one_core": {"value": n / t1, "unit": "assembled DoFs/s", "cores": 1},
+            "solve": {"value": its / ts, "unit": "inner Schur GMRES iter/s", "cores": 1,
+                      "sample": f"{its} inner iterations of one BlockSchurPreconditioner::vmult "
+                                f"(refine={refine}, n_p={m.n_p}), {ts:.2f} s"}}
 
 
 def init_dist(args):
@@ -211,7 +253,7 @@ def run_feec(args):
         "value": f.n / (asm_ms * 1e-3), "unit": "assembled DoFs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong",  # the global mesh is fixed whatever N
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic refined hypershell, reference initial state",
         "config": {"workload": f"FEEC shell Nedelec/RT/DGQ0 refine={refine}, one full time step",
@@ -356,10 +398,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong",  # the global refine-5 mesh is fixed whatever N
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic refined hypershell (equiangular cube-sphere), reference initial state",
+        "data": "synthetic refined hypershell (hyper_shell + SphericalManifold refinement, "
+                "MappingQ(3) as deal.II 9.2, deal.II no-normal-flux normals), reference "
+                "initial state",
         "config": {"workload": f"classic shell Q2/Q1 refine={args.refine}, one full time step",
                    "cells": m.n_cells, "nse_dofs": n_nse, "T_dofs": m.n_T,
                    "parallelism": "single GPU" if world == 1 else
@@ -373,6 +417,11 @@ def main():
                      if k.endswith("_ms") or k.endswith("_avg")},
         "setup_s": t_setup,
         "converged": all(r[0] == 0 for r in recs),
+        "nse_solve_status": "converged" if all(r[0] == 0 for r in recs) else
+        "NoConvergence: the reference's inner Schur GMRES (5000 iterations, tol 1e-6, "
+        "identity preconditioner) stagnates on the near-null constant pressure mode at the "
+        "first preconditioner application of both FGMRES attempts; the reference throws "
+        "here (DESIGN.md section 5b)",
         "patterns": pinfo,
         "schur_mode": args.schur,
         "pcie_inclusive": pcie,

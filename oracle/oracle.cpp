@@ -583,6 +583,7 @@ struct orc_model {
   mutable std::vector<double> tmp1, tmp2;
   int inner_iterations = 0;
   long a_solve_iterations = 0;  // AztecOO A-GMRES iterations of the last solve (do_solve_A)
+  int inner_max_steps = 5000;   // SolverControl(5000) of the inner Schur GMRES (timing hook)
 };
 
 extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
@@ -639,6 +640,36 @@ extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, con
                                &m->nse, m->nse_rhs.data());
   }
 }
+
+extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_nse,
+                                                const double* old_T, int threads) {
+  // The same assembly as orc_assemble_nse_system with deal.II WorkStream's
+  // structure (boussinesq_model.tpp:712-734): local_assemble_nse_system on
+  // `threads` threads (per-thread scratch), copy_local_to_global serialized in
+  // cell order, so the result is bitwise the single-threaded one. Used only by
+  // bench.py's cpu_baseline (all-cores leg).
+  m->nse.zero();
+  std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
+  const int chunk = 64 * (threads > 0 ? threads : 1);
+  std::vector<double> K(size_t(chunk) * 89 * 89), f(size_t(chunk) * 89);
+  for (int c0 = 0; c0 < m->n_cells; c0 += chunk) {
+    const int c1 = std::min(m->n_cells, c0 + chunk);
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 4)
+    for (int c = c0; c < c1; ++c) {
+      double ul[89], Tl[27];
+      gather(m->cell_nse, c, 89, old_nse, ul);
+      gather(m->cell_T, c, m->tdpc, old_T, Tl);
+      orc_cell_nse_system(&m->ph, &m->geom[192 * size_t(c)], ul, Tl,
+                          &K[size_t(c - c0) * 89 * 89], &f[size_t(c - c0) * 89]);
+    }
+    for (int c = c0; c < c1; ++c)
+      distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)],
+                                 &K[size_t(c - c0) * 89 * 89], &f[size_t(c - c0) * 89], &m->nse,
+                                 m->nse_rhs.data());
+  }
+}
+
+extern "C" void orc_set_inner_max_steps(orc_model* m, int n) { m->inner_max_steps = n; }
 
 extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   // assemble_nse_preconditioner (:479-514) + build_nse_preconditioner (:518-542).
@@ -1039,11 +1070,18 @@ void block_prec_vmult(orc_model* m, const double* src, double* dst, bool do_solv
   const int nu = m->n_u, np = m->n_p;
   std::vector<double> utmp(src, src + nu);
   {
-    Control ctl{5000, 1e-6 * norm2(std::vector<double>(src + nu, src + nu + np), 0, np)};
+    Control ctl{unsigned(m->inner_max_steps),
+                1e-6 * norm2(std::vector<double>(src + nu, src + nu + np), 0, np)};
     int it = 0;
-    gmres(
-        np, [&](const double* x, double* y) { schur_vmult(m, x, y); },
-        [&](const double* x, double* y) { std::copy(x, x + np, y); }, dst + nu, src + nu, ctl, it);
+    try {
+      gmres(
+          np, [&](const double* x, double* y) { schur_vmult(m, x, y); },
+          [&](const double* x, double* y) { std::copy(x, x + np, y); }, dst + nu, src + nu, ctl,
+          it);
+    } catch (const NoConvergence&) {
+      inner += it;  // count the failed solve's iterations too (as the device path does)
+      throw;
+    }
     inner += it;
     for (int i = 0; i < np; ++i) dst[nu + i] *= -1.0;
   }

@@ -83,6 +83,12 @@ void orc_set_time_step(orc_model* m, double dt);
 
 /* assemble_nse_system (:691-740) into the internal CSR nse_matrix + nse_rhs */
 void orc_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T);
+/* The same with WorkStream's structure: element work on `threads` threads,
+ * copier serialized in cell order (bitwise the serial result; CPU baseline). */
+void orc_assemble_nse_system_threads(orc_model* m, const double* old_nse, const double* old_T,
+                                     int threads);
+/* Timing hook: iteration cap of the inner Schur GMRES (the reference's 5000). */
+void orc_set_inner_max_steps(orc_model* m, int n);
 /* assemble_nse_preconditioner + build_nse_preconditioner (:479-542) */
 void orc_build_nse_preconditioner(orc_model* m);
 /* assemble_temperature_matrix (:821-864) */

@@ -67,6 +67,8 @@ def lib():
         L.orc_block_preconditioner_vmult.argtypes = [P, P, P, I, P]
         L.orc_solve_nse.argtypes = [P, P, P, P, I]
         L.orc_solve_temperature.argtypes = [P, P, P]
+        L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
+        L.orc_set_inner_max_steps.argtypes = [P, I]
         L.orc_a_solve_iterations.argtypes = [P]
         L.orc_a_solve_iterations.restype = C.c_long
         L.orc_max_velocity.argtypes = [P, P]
@@ -158,6 +160,16 @@ class Model:
     def assemble_nse_system(self, old_nse, old_T):
         lib().orc_assemble_nse_system(self.h, _p(np.ascontiguousarray(old_nse, np.float64)),
                                       _p(np.ascontiguousarray(old_T, np.float64)))
+
+    def assemble_nse_system_threads(self, old_nse, old_T, threads):
+        """WorkStream-style assembly on `threads` threads (bitwise the serial one)."""
+        lib().orc_assemble_nse_system_threads(
+            self.h, _p(np.ascontiguousarray(old_nse, np.float64)),
+            _p(np.ascontiguousarray(old_T, np.float64)), int(threads))
+
+    def set_inner_max_steps(self, n):
+        """Timing hook: cap of the inner Schur GMRES (the reference's 5000)."""
+        lib().orc_set_inner_max_steps(self.h, int(n))
 
     def build_nse_preconditioner(self):
         lib().orc_build_nse_preconditioner(self.h)

@@ -8,11 +8,15 @@ oracle or to the host mesh/DoF setup shows up as a diff, and give the GPU
 tests a fixed target that does not need the oracle at run time.
 
 Cases (classic shell physics, data/aqua_planet_shell_test_3d-classic.prm):
-  shell_r1.npz  refine 1 (48 cells): cell 0..3 element matrices/rhs for the
-                physical state (u=0, T0) and a seeded random state, the
-                assembled nse rhs, preconditioner diagonals, one full time
-                step's NSE solution / iteration counts, temperature solution.
-usage: python tests/golden/make_golden.py
+  shell_r1.npz       refine 1 (48 cells): cell 0..3 element matrices/rhs for the
+                     physical state (u=0, T0) and a seeded random state, the
+                     assembled nse rhs, preconditioner diagonals, one full time
+                     step's NSE solution / iteration counts, temperature solution.
+  shell_r3_step.npz  refine 3 (3,072 cells, 81,912 NSE dofs): one full time step
+                     from the physical state (about 15 min of oracle time: ~29,000
+                     inner Schur GMRES iterations): iteration counts, the NSE and
+                     temperature solutions, the assembled rhs.
+usage: python tests/golden/make_golden.py [r1|r3]
 """
 import os
 import sys
@@ -70,6 +74,28 @@ def make(refine=1):
     return out
 
 
+def make_step(refine):
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    u, T = states(m)["physical"]
+    orc = oracle_py.Model(ph, m)
+    orc.assemble_nse_system(u, T)
+    rhs = orc.nse_rhs()
+    orc.build_nse_preconditioner()
+    orc.assemble_temperature_matrix()
+    orc.assemble_temperature_rhs(T, u)
+    rc, x, outer, inner = orc.solve_nse(u)
+    rcT, Tn, itT = orc.solve_temperature(T)
+    return {"n": np.array([m.n_cells, m.n_u, m.n_p, m.n_T], np.int64), "nse_rhs": rhs,
+            "T_rhs": orc.T_rhs(), "nse_solution": x, "T_solution": Tn,
+            "iters": np.array([rc, outer, inner, rcT, itT], np.int64)}
+
+
 if __name__ == "__main__":
-    np.savez_compressed(os.path.join(HERE, "shell_r1.npz"), **make(1))
-    print("wrote", os.path.join(HERE, "shell_r1.npz"))
+    which = sys.argv[1] if len(sys.argv) > 1 else "r1"
+    if which == "r1":
+        np.savez_compressed(os.path.join(HERE, "shell_r1.npz"), **make(1))
+        print("wrote", os.path.join(HERE, "shell_r1.npz"))
+    elif which == "r3":
+        np.savez_compressed(os.path.join(HERE, "shell_r3_step.npz"), **make_step(3))
+        print("wrote", os.path.join(HERE, "shell_r3_step.npz"))

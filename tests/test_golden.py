@@ -104,3 +104,41 @@ def test_gpu_matches_fixture(gold, mesh):
     assert rcT == g[3] and itT == g[4]
     assert rel(ctx.get_state(dcp.T_SOLUTION), gold["T_solution"]) < 1e-10
     ctx.close()
+
+
+GOLD3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shell_r3_step.npz")
+
+
+@pytest.mark.gpu
+def test_gpu_time_step_r3_matches_oracle_fixture():
+    """One reference time step at refine 3 (3,072 cells, 81,912 NSE dofs) from
+    the physical state against the oracle's (tests/golden/make_golden.py r3,
+    ~15 min of oracle time): equal FGMRES count, inner count within 10 % (the
+    inner Schur GMRES stagnates near its tolerance), NSE iterate at 1e-10."""
+    with np.load(GOLD3) as d:
+        g = {k: d[k] for k in d.files}
+    m = dcp.HostMesh(refine=3)
+    assert list(g["n"]) == [m.n_cells, m.n_u, m.n_p, m.n_T]
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.classic_physics())
+    ctx.upload_mesh(m)
+    u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    assert rel(ctx.get_state(dcp.NSE_RHS), g["nse_rhs"]) < 1e-12
+    ctx.build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    assert rel(ctx.get_state(dcp.T_RHS), g["T_rhs"]) < 1e-12
+    rc, outer, inner = ctx.solve_nse()
+    it = g["iters"]
+    assert rc == it[0] == 0 and outer == it[1]
+    assert abs(inner - it[2]) <= 0.10 * it[2]
+    x = ctx.get_state(dcp.NSE_SOLUTION)
+    assert np.linalg.norm(x - g["nse_solution"]) <= 1e-10 * np.linalg.norm(g["nse_solution"])
+    rcT, itT, _ = ctx.solve_temperature()
+    assert rcT == it[3] and abs(itT - it[4]) <= 1
+    assert rel(ctx.get_state(dcp.T_SOLUTION), g["T_solution"]) < 1e-10
+    ctx.close()
