@@ -735,6 +735,29 @@ void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_
 
 }  // namespace
 
+namespace dcp {
+// nse_matrix.block(0,0) of the last assemble_nse_system (its dt, nse_ph) into
+// A_val: the full MODE 0 scatter, which rewrites B^T / B / con_diag with the
+// same values and leaves the rhs alone.
+void materialize_velocity_block(Ctx& c) {
+  if (c.A_current) return;
+  if (!c.first_touch_A) c.A_val.zero(c.stream);
+  if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
+  if (!c.first_touch_B) c.B_val.zero(c.stream);
+  c.con_diag.zero(c.stream);
+  NseOut out{};
+  out.A = c.A_val.p;
+  out.Bt = c.Bt_val.p;
+  out.B = c.B_val.p;
+  out.cdiag = c.con_diag.p;
+  out.cidx = c.mf_cidx.p;
+  for (int k = 0; k < c.n_colors(); ++k)
+    launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p, c.old_T.p,
+                      c.nse_ph, out, c.stream);
+  c.A_current = true;
+}
+}  // namespace dcp
+
 extern "C" {
 
 int dcp_nccl_unique_id(void* out128) {
@@ -907,6 +930,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->feec_zero_mean = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_ASSEMBLE_VELOCITY_BLOCK) {
+      ctx->assemble_A = value != 0;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_FGMRES_MAX_OUTER) {
       require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_FGMRES_MAX_OUTER must be >= 1");
       ctx->fgmres_max_outer = value;
@@ -1076,19 +1103,24 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       }
       c.mf_q2.upload(oq2);
       c.mf_p.upload(op);
-      std::vector<int32_t> cdof;
+      // constrained velocity nodes: index into con_diag (3 per node)
+      std::vector<int32_t> cdof, cidx(nv, -1);
       std::vector<int64_t> cpos;
+      int n_con = 0;
       for (int n = 0; n < nv; ++n) {
         if (vc[n].type == 0) continue;
         const auto* b = std::lower_bound(Ac.data() + Ap[n], Ac.data() + Ap[n + 1], n);
         require(b != Ac.data() + Ap[n + 1] && *b == n, DCP_ERR_INVALID, "A pattern lacks a diagonal block");
-        const int64_t blk = b - Ac.data();
+        cidx[n] = n_con;
         for (int comp = 0; comp < 3; ++comp)
           if (vc[n].type == 1 || comp == vc[n].k) {
             cdof.push_back(3 * n + comp);
-            cpos.push_back(9 * blk + 4 * comp);
+            cpos.push_back(3 * int64_t(n_con) + comp);
           }
+        ++n_con;
       }
+      c.mf_cidx.upload(cidx);
+      c.con_diag.alloc(3 * size_t(n_con));
       c.mf_first.upload(first);
       c.mf_cdof.upload(cdof);
       c.mf_cpos.upload(cpos);
@@ -1168,22 +1200,12 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
           DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         DCP_HIP_CHECK(hipEventCreateWithFlags(&c.mf_join_ev, hipEventDisableTiming));
       }
-      std::vector<int32_t> cidx(nv, -1);
-      std::vector<int64_t> cblk;
-      for (int n = 0; n < nv; ++n) {
-        if (vc[n].type == 0) continue;
-        const auto* b = std::lower_bound(Ac.data() + Ap[n], Ac.data() + Ap[n + 1], n);
-        cidx[n] = int32_t(cblk.size());
-        cblk.push_back(b - Ac.data());
-      }
       c.mf_cmask.upload(cmask);
       c.mf_vptr.upload(vptr);
       c.mf_vslot.upload(vslot);
       c.mf_pbase = pbase;
       c.mf_pptr.upload(pptr);
       c.mf_pslot.upload(pslot);
-      c.mf_cidx.upload(cidx);
-      c.mf_cblk.upload(cblk);
       c.mf_buf.alloc(size_t(pbase) + size_t(pptr[n_p]));
       {
         std::vector<int32_t> col, layer;
@@ -1323,15 +1345,21 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
+    const bool matrix = (flags & DCP_ASSEMBLE_MATRIX) != 0;
+    // the velocity block is materialised only when something reads it
+    const bool full = matrix && (c.assemble_A || c.matrix_free == 0);
     NseOut out{};
-    if (flags & DCP_ASSEMBLE_MATRIX) {
+    if (matrix) {
       // first-touch scatter positions store instead of adding: no zero fill
-      if (!c.first_touch_A) c.A_val.zero(c.stream);
+      if (full && !c.first_touch_A) c.A_val.zero(c.stream);
       if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
       if (!c.first_touch_B) c.B_val.zero(c.stream);
-      out.A = c.A_val.p;
+      c.con_diag.zero(c.stream);
+      out.A = full ? c.A_val.p : nullptr;
       out.Bt = c.Bt_val.p;
       out.B = c.B_val.p;
+      out.cdiag = c.con_diag.p;
+      out.cidx = c.mf_cidx.p;
     }
     if (flags & DCP_ASSEMBLE_RHS) {
       c.nse_rhs.zero(c.stream);
@@ -1340,11 +1368,20 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     // ghosted old solutions (the reference reads the ghosted vectors, :583-589)
     halo_exchange(c, c.halo_nse, c.old_nse.p);
     halo_exchange(c, c.halo_T, c.old_T.p);
-    for (int k = 0; k < c.n_colors(); ++k)
-      launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
-                        c.old_T.p, c.ph, out, c.stream);
+    for (int k = 0; k < c.n_colors(); ++k) {
+      if (full)
+        launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
+                          c.old_T.p, c.ph, out, c.stream);
+      else
+        launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
+                            c.old_T.p, c.ph, out, c.stream);
+    }
     t.stop();
-    if (flags & DCP_ASSEMBLE_MATRIX) c.nse_assembled = true;
+    if (matrix) {
+      c.nse_assembled = true;
+      c.A_current = full;
+      c.nse_ph = c.ph;
+    }
     return DCP_OK;
   });
 }
@@ -1576,6 +1613,9 @@ int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* 
     *nnz = total;
     if (!rowptr) return DCP_OK;
     require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
+    require(c.nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
+    materialize_velocity_block(c);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     const auto Av = down_d(c.A_val), Btv = down_d(c.Bt_val), Bv = down_d(c.B_val);
     int64_t k = 0;
     rowptr[0] = 0;

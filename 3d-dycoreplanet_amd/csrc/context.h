@@ -92,6 +92,15 @@ struct Ctx {
   DBuf<int32_t> posA, posBt, posB, posT;
   // scatter positions carry first-touch marks (no zero fill before assembly)
   bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
+  // nse_matrix in operator form: B^T, B and the diagonal of the constrained
+  // velocity rows (con_diag, [constrained node][3], indexed by mf_cidx) are
+  // assembled; the velocity-velocity block A is applied matrix-free and
+  // materialised into A_val only when read (export, DCP_OPT_MATRIX_FREE = 0)
+  // or when DCP_OPT_ASSEMBLE_VELOCITY_BLOCK asks for it on every assembly.
+  DBuf<double> con_diag;
+  bool assemble_A = false;   // DCP_OPT_ASSEMBLE_VELOCITY_BLOCK
+  bool A_current = false;    // A_val holds the block of the last assembly
+  PhysicsDev nse_ph{};       // physics (dt) of the last assemble_nse_system
   // explicit Schur complement S = B D_A^-1 B^T (CSR over pressure dofs)
   DBuf<int32_t> S_ptr, S_col;
   // its values live in the SELL-64 layout of that pattern (sell_spmv)
@@ -135,7 +144,6 @@ struct Ctx {
   std::vector<int> mf_cell_cut, mf_vcut, mf_pcut;  // [mf_chunks + 1] each
   hipStream_t mf_stream = nullptr;
   hipEvent_t mf_chunk_ev[kMfChunksMax] = {}, mf_join_ev = nullptr;
-  DBuf<int64_t> mf_cblk;
   DBuf<int32_t> mf_col, mf_layer;
   DBuf<double> mf_colgeo, mf_laygeo;
   bool mf_separable = false;
@@ -146,8 +154,8 @@ struct Ctx {
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
   MfGather mfg() const {
-    return MfGather{n_vnodes,    n_p,       n_u,       mf_vorder.p, mf_porder.p, mf_vptr.p,
-                    mf_pptr.p,   mf_pbase,  mf_cidx.p, mf_cblk.p,   vcon.p,      A_val.p};
+    return MfGather{n_vnodes, n_p,      n_u,       mf_vorder.p, mf_porder.p, mf_vptr.p,
+                    mf_pptr.p, mf_pbase, mf_cidx.p, vcon.p,      con_diag.p};
   }
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};
@@ -253,6 +261,8 @@ struct Ctx {
   ~Ctx();
 };
 
+// api.cpp: A_val <- nse_matrix.block(0,0) of the last assembly (if not current)
+void materialize_velocity_block(Ctx& c);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
 int solve_temperature(Ctx& c, int* iters, double* T_range);

@@ -74,6 +74,10 @@ struct NseOut {
   double* rhs;   // velocity block of nse_rhs or null
   double* elemK; // element mode: [n][89][89]
   double* elemF; // element mode: [n][89]
+  // assembled diagonal of the constrained velocity rows, [n_con_nodes][3]
+  // (component c of constrained node n at 3 cidx[n] + c), or null
+  double* cdiag;
+  const int32_t* cidx;  // [n_vnodes] constrained-node index or -1
 };
 
 // ---- matfree.hip ----------------------------------------------------------
@@ -134,10 +138,9 @@ struct MfGather {
   const int32_t* vptr;         // [n_vnodes + 1] slot ranges per position: triples buf[3 k .. 3 k + 2]
   const int32_t* pptr;         // [n_p + 1] slot ranges per position: buf[pbase + k]
   int32_t pbase;               // 3 * vptr[n_vnodes]
-  const int32_t* cidx;         // [n_vnodes] index into cblk or -1
-  const int64_t* cblk;         // diagonal block of A for each constrained node
+  const int32_t* cidx;         // [n_vnodes] constrained-node index or -1
   const NodeConstraint* vcon;
-  const double* A_val;
+  const double* cdiag;         // [n_con_nodes][3] assembled diagonal (NseOut::cdiag)
 };
 // cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
@@ -147,8 +150,8 @@ void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, 
 // one colour class = positions [base, base + n): dst (+)= C^T K C src
 void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);
-// constrained velocity dofs: dst[dof] = A_val[diag_pos] * src[dof]
-void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* A_val,
+// constrained velocity dofs: dst[dof] = cdiag[diag_pos] * src[dof]
+void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* cdiag,
                     const double* src, double* dst, hipStream_t s);
 
 // ---- assembly.hip ---------------------------------------------------------
@@ -157,6 +160,11 @@ void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const do
 void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                        const double* u_old, const double* T_old, const PhysicsDev& ph,
                        const NseOut& out, hipStream_t s);
+// Operator form (out.A ignored): B^T, B, rhs and out.cdiag; the velocity
+// block stays matrix-free.
+void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
+                         const double* u_old, const double* T_old, const PhysicsDev& ph,
+                         const NseOut& out, hipStream_t s);
 // Element mode: dense FESystem-ordered K/f of cells [first, first+n).
 void launch_nse_system_elements(const CellData& cd, int first, int n, const double* u_old,
                                 const double* T_old, const PhysicsDev& ph, double* K, double* f,

@@ -385,6 +385,11 @@ __device__ inline void nse_rhs_node(const NseSmem& sh, int an, double fa[3]) {
   }
 }
 
+// MODE 0: full distribute_local_to_global into block-CSR A, B^T, B (+ rhs);
+// MODE 1: dense element output; MODE 2: the operator form of nse_matrix that
+// the solve reads (B^T, B, rhs and the diagonal of the constrained velocity
+// rows), with the velocity-velocity block left to the matrix-free apply
+// (kernels/matfree.hip) and materialised only on request (MODE 0).
 template <int MODE>
 __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, ScatterMaps sm,
                                                             const int32_t* __restrict__ cells,
@@ -398,10 +403,12 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #define DCP_ASM_XCD 0
 #endif
   // DCP_ASM_XCD: each XCD takes one contiguous (tree-ordered) run of the colour class
-  const int cell = MODE == 0 ? cells[DCP_ASM_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x)]
+  const int cell = MODE != 1 ? cells[DCP_ASM_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x)]
                              : first + blockIdx.x;
-  const bool want_matrix = MODE == 1 || out.A != nullptr;
+  const bool want_matrix = MODE == 1 || (MODE == 0 && out.A != nullptr);
+  const bool want_B = want_matrix || (MODE == 2 && out.B != nullptr);
   const bool want_rhs = MODE == 1 || out.rhs != nullptr;
+  const bool want_cdiag = MODE != 1 && out.cdiag != nullptr;
 
   if (tid < 3 * kMapPts) sh.X[tid] = cd.geo[3 * kMapPts * size_t(cell) + tid];
   if (tid < 27) {
@@ -414,8 +421,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
     sh.T[v] = T_old[cd.cell_T[8 * size_t(cell) + v]];
   }
-  if (MODE == 0 && want_matrix) {
+  if (MODE == 0 && want_matrix)
     for (int i = tid; i < 729; i += kNseThreads) sh.pos[i] = sm.posA[729 * size_t(cell) + i];
+  if (MODE != 1 && want_B) {
     for (int i = tid; i < 216; i += kNseThreads) {
       sh.pos[729 + i] = sm.posBt[216 * size_t(cell) + i];
       sh.pos[945 + i] = sm.posB[216 * size_t(cell) + i];
@@ -517,7 +525,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
       sh.F[3 * q + c] = (u[c] + ph.dt * rho * (ph.grav_scale * grav[c]) - ph.dt * adv -
                          ph.dt * (2 * cxu[c])) * w;
     }
-  } else if (MODE == 0 && want_matrix && tid >= 64 && tid < 91) {
+  }
+  double kii_d[3] = {0, 0, 0};  // diag lanes: K_(a,c),(a,c) of node a
+  if (((MODE == 0 && want_matrix) || want_cdiag) && tid >= 64 && tid < 91) {
     // node-diagonal blocks for the |K_ii| / average-diagonal rule
     const int a = tid - 64;
     double msum = 0, g2[3] = {0, 0, 0};
@@ -532,11 +542,29 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
       g2[2] += w * Da[2] * Da[2];
     }
     const double L = g2[0] + g2[1] + g2[2];
-    sh.diag[a] = fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[0]) +
-                 fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[1]) +
-                 fabs(msum + ph.nu_sys * L + ph.nu_sys * g2[2]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) kii_d[c] = msum + ph.nu_sys * L + ph.nu_sys * g2[c];
+    sh.diag[a] = fabs(kii_d[0]) + fabs(kii_d[1]) + fabs(kii_d[2]);
   }
   __syncthreads();
+  if (want_cdiag && tid >= 64 && tid < 91) {
+    // diagonal of the constrained rows of nse_matrix: AffineConstraints puts
+    // |K_ii| of every cell (the average diagonal if 0) on a constrained dof
+    const int n = sh.node[tid - 64];
+    const int ci = out.cidx[n];
+    if (ci >= 0) {
+      const NodeConstraint nc = cd.vcon[n];
+      double avg = 0;
+      for (int m = 0; m < 27; ++m) avg += sh.diag[m];
+      avg /= 89.0;  // pressure diagonals of the local matrix are 0
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (nc.type == 1 || c == nc.k) {
+          const double d = fabs(kii_d[c]);
+          out.cdiag[3 * size_t(ci) + c] += d != 0.0 ? d : avg;
+        }
+    }
+  }
 
   constexpr int kAux = kNseThreads - kNseTiles;  // threads for B^T/B and rhs in MODE 1
   if (MODE == 1) {
@@ -579,6 +607,61 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
           f[4 * v + 3] = 0.0;
           for (int w = 0; w < 8; ++w) K[89 * (4 * v + 3) + 4 * w + 3] = 0.0;
         }
+      }
+    }
+    return;
+  }
+
+  if (MODE == 2) {
+    // B^T rows (an, v): one per thread, condensed C_a^T b; rhs nodes on 27 more
+    double bt[3] = {0, 0, 0};
+    if (want_B && tid < 216) {
+      nse_div(sh, tid / 8, tid % 8, bt);
+      double Ca[3][3];
+      condensation(cd.vcon[sh.node[tid / 8]], Ca);
+      const double b0 = bt[0], b1 = bt[1], b2 = bt[2];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) bt[j] = Ca[0][j] * b0 + Ca[1][j] * b1 + Ca[2][j] * b2;
+    } else if (want_rhs && tid >= 216 && tid < 216 + 27) {
+      const int an = tid - 216;
+      double fa[3];
+      nse_rhs_node(sh, an, fa);
+      double Ca[3][3];
+      condensation(cd.vcon[sh.node[an]], Ca);
+      double* dst = out.rhs + 3 * size_t(sh.node[an]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+    }
+    if (!want_B) return;
+    __syncthreads();  // gradient tables dead: stage the rows for the all-wave scatter
+    double* stage = sh.X;
+    if (tid < 216) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) stage[kStageA + 3 * tid + j] = bt[j];
+    }
+    __syncthreads();
+    // B^T then B rows: elements [729 * 9, kScatterElems) of the MODE 0 order
+    constexpr int kOpBatch = (2 * 648 + kNseThreads - 1) / kNseThreads;  // 6
+    double old[kOpBatch];
+#pragma unroll
+    for (int j = 0; j < kOpBatch; ++j) {
+      const int e = 729 * 9 + tid + j * kNseThreads;
+      old[j] = 0.0;
+      if (e < kScatterElems) {
+        bool add;
+        double v;
+        const double* dst = scatter_target(sh, out, e, add, v);
+        if (add) old[j] = *dst;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kOpBatch; ++j) {
+      const int e = 729 * 9 + tid + j * kNseThreads;
+      if (e < kScatterElems) {
+        bool add;
+        double v;
+        double* dst = scatter_target(sh, out, e, add, v);
+        *dst = old[j] + v;
       }
     }
     return;
@@ -987,6 +1070,15 @@ void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t*
                        const NseOut& out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL((k_nse_system<0>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+                     u_old, T_old, ph, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
+                         const double* u_old, const double* T_old, const PhysicsDev& ph,
+                         const NseOut& out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL((k_nse_system<2>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
                      u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }

@@ -845,10 +845,10 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     if (ci >= 0) {
       const NodeConstraint nc = g.vcon[i];
       condense(nc, s);
-      const double* dg = g.A_val + 9 * g.cblk[ci];
+      const double* dg = g.cdiag + 3 * size_t(ci);
 #pragma unroll
       for (int comp = 0; comp < 3; ++comp)
-        if (nc.type == 1 || comp == nc.k) s[comp] = dg[4 * comp] * src[3 * size_t(i) + comp];
+        if (nc.type == 1 || comp == nc.k) s[comp] = dg[comp] * src[3 * size_t(i) + comp];
     }
     double* d = dst + 3 * size_t(i);
     d[0] = s[0];
@@ -881,10 +881,10 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
 // constrained velocity dofs: dst = (assembled diagonal) * src
 __global__ void k_mf_constrained(int n, const int32_t* __restrict__ dof,
                                  const int64_t* __restrict__ diag_pos,
-                                 const double* __restrict__ A_val, const double* __restrict__ src,
+                                 const double* __restrict__ cdiag, const double* __restrict__ src,
                                  double* __restrict__ dst) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < n) dst[dof[e]] = A_val[diag_pos[e]] * src[dof[e]];
+  if (e < n) dst[dof[e]] = cdiag[diag_pos[e]] * src[dof[e]];
 }
 
 }  // namespace
@@ -935,11 +935,11 @@ void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, 
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* A_val,
+void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const double* cdiag,
                     const double* src, double* dst, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_mf_constrained, dim3((n + 255) / 256), dim3(256), 0, s, n, dof, diag_pos,
-                     A_val, src, dst);
+                     cdiag, src, dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -692,7 +692,7 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
     const bool one_stream = c.mf_chunks == 1;
     hipStream_t gs = one_stream ? c.stream : c.mf_stream;
     for (int k = 0; k < c.mf_chunks; ++k) {
-      mf_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.ph.nu_sys, stokes, src, c.mf_buf.p,
+      mf_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.nse_ph.nu_sys, stokes, src, c.mf_buf.p,
                c.stream);
       if (!one_stream) {
         DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[k], c.stream));
@@ -707,9 +707,9 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
     }
   } else {
     for (int k = 0; k < c.n_colors(); ++k)
-      mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.ph.nu_sys, stokes, src, dst,
+      mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.nse_ph.nu_sys, stokes, src, dst,
                       c.stream);
-    mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.A_val.p, src, dst, c.stream);
+    mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.con_diag.p, src, dst, c.stream);
   }
   if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
 }
@@ -721,6 +721,7 @@ void a_vmult(Ctx& c, const double* src, double* dst) {
     mf_apply(c, src, dst, false);
     return;
   }
+  materialize_velocity_block(c);
   spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
 }
 
@@ -862,6 +863,7 @@ void nse_vmult(Ctx& c, const double* src, double* dst) {
     mf_apply(c, src, dst, true);
     return;
   }
+  materialize_velocity_block(c);
   spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, src, dst, false, c.stream);
   spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src + c.n_u, dst, true, c.stream);
   spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, src, dst + c.n_u, false, c.stream);

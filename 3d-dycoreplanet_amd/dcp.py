@@ -30,6 +30,7 @@ OPT_FEEC_ZERO_MEAN = 2
 OPT_MATRIX_FREE = 3
 OPT_FUSED_CHAIN = 4
 OPT_FGMRES_MAX_OUTER = 5
+OPT_ASSEMBLE_VELOCITY_BLOCK = 6
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -508,6 +509,13 @@ class Context:
         in colour-class launches; False / 0: block-CSR SpMV of the assembled
         matrix."""
         self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(mode)))
+
+    def set_assemble_velocity_block(self, on: bool):
+        """DCP_OPT_ASSEMBLE_VELOCITY_BLOCK: False (default) = assemble_nse_system
+        produces nse_matrix in operator form (B^T, B, rhs, constrained-row
+        diagonal; A applied matrix-free, materialised on export); True = scatter
+        the velocity block too on every assembly."""
+        self._check(lib().dcp_set_option(self._h, OPT_ASSEMBLE_VELOCITY_BLOCK, int(bool(on))))
 
     def upload_mesh(self, m: HostMesh, nse_constraints=None, T_constraints=None):
         self._feec_view = None

@@ -139,6 +139,16 @@ enum { DCP_OPT_MATRIX_FREE = 3 };
  *   one launch whose workgroups hand each step's reduction to each other on the
  *   device; 0 = one launch per step. Bitwise the same results. */
 enum { DCP_OPT_FUSED_CHAIN = 4 };
+/* DCP_OPT_ASSEMBLE_VELOCITY_BLOCK: 0 (default with DCP_OPT_MATRIX_FREE) =
+ *   dcp_assemble_nse_system assembles nse_matrix in operator form: the B^T / B
+ *   blocks, the rhs and the diagonal entries of the constrained velocity rows,
+ *   which is everything the solve reads, while every product with the
+ *   velocity-velocity block A is matrix-free; A itself is materialised
+ *   (bitwise the same entries) only when something reads it
+ *   (dcp_nse_matrix_export, DCP_OPT_MATRIX_FREE = 0). 1 = scatter A on every
+ *   assembly too, as the reference's distribute_local_to_global does
+ *   (boussinesq_model.tpp:677-687). */
+enum { DCP_OPT_ASSEMBLE_VELOCITY_BLOCK = 6 };
 /* DCP_OPT_FGMRES_MAX_OUTER (test hook, default 40): the iteration cap of the
  *   first FGMRES(30) (SolverControl(40, ...), boussinesq_model.tpp:1166); a
  *   lower cap sends small meshes through the do_solve_A / FGMRES(50) fallback

@@ -98,6 +98,44 @@ def test_assembled_system(setup, state):
     assert abs(Ag2 - Ag).max() == 0.0
 
 
+def test_operator_form_assembly_is_the_full_assembly():
+    """DCP_OPT_ASSEMBLE_VELOCITY_BLOCK = 0 (default): assemble_nse_system
+    scatters B^T, B, the rhs and the constrained-row diagonal, and leaves the
+    velocity block to the matrix-free apply. Everything the solve reads must be
+    bitwise what the full distribute_local_to_global scatter produces, and the
+    block materialised on export must be the one of the assembly's time step."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(SEED + 21)
+    u, T = random_state(m, rng)
+    x = rng.uniform(-1, 1, m.n_u + m.n_p)
+    n = m.n_u + m.n_p
+    out = []
+    for full in (False, True):
+        ctx = dcp.Context()
+        ctx.set_physics(ph)
+        ctx.upload_mesh(m)
+        ctx.set_assemble_velocity_block(full)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+        ctx.set_state(dcp.OLD_T_SOLUTION, T)
+        ctx.assemble_nse_system()
+        y = ctx.nse_vmult(x)
+        yv = ctx.velocity_vmult(x[:m.n_u])
+        # a later time-step change must not leak into the assembled operator
+        ctx.set_time_step(2.0 * ph.time_step)
+        y2 = ctx.nse_vmult(x)
+        K = csr(*ctx.nse_matrix_csr(), n)
+        out.append((y, yv, y2, K, ctx.get_state(dcp.NSE_RHS)))
+        ctx.close()
+    (y0, yv0, y20, K0, r0), (y1, yv1, y21, K1, r1) = out
+    assert np.array_equal(r0, r1)
+    assert np.array_equal(y0, y1) and np.array_equal(yv0, yv1)
+    assert np.array_equal(y0, y20) and np.array_equal(y1, y21)
+    assert (K0 != K1).nnz == 0
+    # the materialised operator is the one the matrix-free apply evaluates
+    assert rel_max(K0 @ x, y0) < 1e-13
+
+
 def test_preconditioner_diagonals(setup):
     m, ph, ctx, orc = setup
     ctx.build_nse_preconditioner()
@@ -178,8 +216,9 @@ def test_full_solve_and_temperature(setup, explicit):
     # The inner Schur GMRES stops on a 1e-6 residual estimate while it
     # stagnates on the near-null constant pressure mode of S (DESIGN.md,
     # "no-normal-flux normals"), so its iteration count follows the summation
-    # order: ~1870 inner iterations at r=2, GPU and oracle within a few
-    # percent, while the outer count is equal and the iterates agree to 1e-10.
+    # order: 27 outer / ~1870 inner iterations at r=2 (oracle), GPU and oracle
+    # within a few percent, while the outer count is equal and the iterates
+    # agree to 1e-10.
     assert outer == outer_o
     assert abs(inner - inner_o) <= 0.10 * inner_o
     x_g = ctx.get_state(dcp.NSE_SOLUTION)
