@@ -31,6 +31,11 @@ Ctx::~Ctx() {
   free_workspaces(*this);
   if (hpinned) (void)hipHostFree(hpinned);
   if (hmapped) (void)hipHostFree(hmapped);
+  if (gm_init) (void)hipHostFree(gm_init);
+  if (gm_read) (void)hipHostFree(gm_read);
+  if (gm_flag) (void)hipHostFree(gm_flag);
+  for (auto& ev : gm_ev)
+    if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : spec_ev)
     if (ev) (void)hipEventDestroy(ev);
   ev_total.destroy();
@@ -928,6 +933,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     }
     if (option == DCP_OPT_FEEC_ZERO_MEAN) {
       ctx->feec_zero_mean = value != 0;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_GRAM_SCHMIDT) {
+      require(value == 0 || value == 1, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0 or 1");
+      ctx->gram_schmidt = value;
       return DCP_OK;
     }
     if (option == DCP_OPT_ASSEMBLE_VELOCITY_BLOCK) {

@@ -175,6 +175,20 @@ struct Ctx {
   unsigned long long spec_seq = 0;   // inner Schur GMRES step numbers (ready flags)
   int n_cus = 0;
   bool fused_chain = true;
+  // DCP_OPT_GRAM_SCHMIDT: 0 = modified (deal.II SolverGMRES, default), 1 = the
+  // inner Schur GMRES with classical Gram-Schmidt twice, each restart cycle
+  // device-resident (kernels/krylov.hip): state, polled status, partials,
+  // basis pointer table
+  int gram_schmidt = 0;
+  DBuf<GmresDev> gm_state;
+  GmresDev* gm_init = nullptr;       // pinned: cycle start state (host -> device)
+  GmresDev* gm_read = nullptr;       // pinned: cycle end state (device -> host)
+  int* gm_flag = nullptr;            // pinned [2]: status at the last two polls
+  hipEvent_t gm_ev[2] = {nullptr, nullptr};
+  DBuf<double> gm_part;
+  DBuf<unsigned> gm_cnt;             // last-block counter of the CGS2 launches
+  DBuf<const double*> gm_ptrs;
+  std::vector<const double*> gm_ptrs_host;
   int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
   long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
   // test hooks, read at context creation: DCP_SCHUR_AHEAD=0 turns the inner

@@ -257,6 +257,10 @@ void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, 
                      const double* v0, double* part0, double* part1, int n_part,
                      const double* nrm_part, int nb_nrm, double* nrm_store, StepReady ready,
                      hipStream_t s);
+// Step of the device-resident GMRES cycle: y = M (cf * x) with cf = *cf_dev
+// (cf_dev null: 1), xs = cf * x when xs != null; nothing if *status != 0.
+void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, double* xs,
+                    double* y, const int* status, hipStream_t s);
 
 // Scalars live in device memory ("device scalars") so Krylov kernels can
 // chain without host round trips. A coefficient argument is (ptr, mult):
@@ -324,6 +328,39 @@ void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, 
                const double* prev2, double* store2, double* coef, double* partials,
                double* partials_host, int nb, double* gran, unsigned long long seq, double* err,
                hipStream_t s);
+// ---- krylov.hip: device-resident GMRES cycle with classical Gram-Schmidt twice
+// State of one restart cycle of deal.II SolverGMRES kept in device memory: the
+// Hessenberg columns, Givens rotations, residual estimates and the
+// SolverControl decision (status 0: iterate, 1: success, 2: failure).
+constexpr int kGmMaxDim = 32;
+struct GmresDev {
+  double H[kGmMaxDim][kGmMaxDim];
+  double gamma[kGmMaxDim + 1], ci[kGmMaxDim], si[kGmMaxDim];
+  double coef[2 * kGmMaxDim];   // this step's first / second pass coefficients
+  double y[kGmMaxDim];          // back-substituted combination coefficients
+  double inv_norm, rho, tol;    // 1/|w| of the last step (1 if 0), |gamma_dim|, tolerance
+  double nrm2;                  // |w|^2 of the last step
+  int status, dim, accumulated, max_steps;
+};
+struct Comm;
+// Arnoldi step k = d - 1 after w = S v_k: w -= V (V^T w) twice, |w|, the
+// Givens update and the convergence check (every launch returns at entry once
+// st->status != 0). gran: cgs2_granules(g.n) doubles of hand-off granules;
+// cnt: a zeroed device counter; seq: the context's launch counter (granule
+// tags, never reused); err: set to 1 if a reduction timed out; comm: all-reduce
+// the sums (several GPUs) or null.
+size_t cgs2_granules(long n);
+// One GPU: the same step (w -= V V^T w twice, |w|, Givens) in one launch of
+// nb resident workgroups (cgs2_chain_fits: nb <= n_cus, enough entries per
+// thread) handing their sums over as granules in gran (kMgsGranules doubles).
+bool cgs2_chain_fits(long n, int nb, int n_cus);
+void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, double* gran,
+                     int nb, unsigned long long seq, double* err, hipStream_t s);
+void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,
+                     GmresDev* st, unsigned long long& seq, double* err, Comm* comm,
+                     hipStream_t s);
+// st->y = H^-1 gamma over st->dim
+void gmres_backsub(GmresDev* st, hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

@@ -16,6 +16,7 @@
 
 #include "../comm.h"
 #include "../device.h"
+#include "granule.h"
 
 namespace dcp {
 namespace {
@@ -202,83 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_chain_add_and_dot(
 #ifndef DCP_MGS_ELEMS
 #define DCP_MGS_ELEMS 8
 #endif
-#ifndef DCP_MGS_SLEEP
-#define DCP_MGS_SLEEP 1
-#endif
 constexpr int kMgsElems = DCP_MGS_ELEMS;
-constexpr long kMgsMaxSpins = 1L << 21;
-typedef unsigned int mgs_u4 __attribute__((ext_vector_type(4)));
-
-// The tag half of a granule carries tag ^ mix(value bits): the memory model
-// guarantees single-copy atomicity only up to 64 bits, so a reader could see
-// the two halves of a 16-byte access from different writes; such a torn read
-// (new tag with an old value, or the reverse) fails the check below and is
-// simply polled again (a false match needs a 64-bit hash collision).
-__device__ inline unsigned long long granule_mix(unsigned long long x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
-__device__ inline void granule_store(double* p, double v, unsigned long long tag) {
-  const unsigned long long b = __double_as_longlong(v);
-  const unsigned long long t = tag ^ granule_mix(b);
-  mgs_u4 q;
-  q.x = unsigned(b);
-  q.y = unsigned(b >> 32);
-  q.z = unsigned(t);
-  q.w = unsigned(t >> 32);
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(q) : "memory");
-}
-
-__device__ inline bool tag_is(const mgs_u4& q, unsigned long long tag) {
-  const unsigned long long t = tag ^ granule_mix(((unsigned long long)q.y << 32) | q.x);
-  return q.z == unsigned(t) && q.w == unsigned(t >> 32);
-}
-__device__ inline double granule_value(const mgs_u4& q) {
-  return __longlong_as_double((long long)(((unsigned long long)q.y << 32) | q.x));
-}
-
-// Wave 0 only: waits for the nb <= 256 granules of one step (lane l polls
-// granules l, l+64, l+128, l+192, four `sc1` loads in flight) and returns, in
-// every lane, their sum in exactly block_sum's order (thread t holds granule
-// t; xor butterfly per 64-thread wave; the four wave sums left to right).
-__device__ inline double granule_coef(const double* gran, int nb, unsigned long long tag,
-                                      double* err) {
-  const int l = threadIdx.x & 63;
-  const double* p = gran + 2 * size_t(l);
-  mgs_u4 q0, q1, q2, q3;
-  long spins = 0;
-  for (;;) {
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off sc1\n\t"
-        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
-        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
-        : "v"(p)
-        : "memory");
-    const bool ok = (l >= nb || tag_is(q0, tag)) && (l + 64 >= nb || tag_is(q1, tag)) &&
-                    (l + 128 >= nb || tag_is(q2, tag)) && (l + 192 >= nb || tag_is(q3, tag));
-    if (__all(ok)) break;
-    if (++spins >= kMgsMaxSpins) {
-      if (l == 0) *err = 1.0;
-      break;
-    }
-    if (DCP_MGS_SLEEP) __builtin_amdgcn_s_sleep(DCP_MGS_SLEEP);
-  }
-  double v[4] = {l < nb ? granule_value(q0) : 0.0, l + 64 < nb ? granule_value(q1) : 0.0,
-                 l + 128 < nb ? granule_value(q2) : 0.0, l + 192 < nb ? granule_value(q3) : 0.0};
-#pragma unroll
-  for (int w = 0; w < 4; ++w)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[w] += __shfl_xor(v[w], off, 64);
-  return v[0] + v[1] + v[2] + v[3];
-}
-
 // h_0 = w.V[0] (from prev: nb_prev partials, e.g. the fused SpMV's; or, with
 // prev == null, computed here), then for i = 1..d-1:
 //   w -= h_{i-1} V[i-1];  h_i = w.V[i]
@@ -404,10 +329,14 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
                                                       double* __restrict__ part1,
                                                       const double* __restrict__ nrm_part,
                                                       int nb_nrm, double* nrm_store,
-                                                      StepReady ready) {
+                                                      StepReady ready,
+                                                      const double* __restrict__ cf_dev,
+                                                      const int* __restrict__ status) {
   __shared__ double quarter[3][64];
   __shared__ double sm[4];
   __shared__ double cf_sh;
+  if (status && *status) return;  // device-resident GMRES cycle already stopped
+  if (cf_dev) cf = *cf_dev;
   const int rows = m.rows;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long sl = blockIdx.x;
@@ -415,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   if (sl * 64 >= rows) {
     // padding workgroup of the common partial length (several GPUs): the
     // all-reduced partial arrays must hold zeros past this rank's slices
-    if (EPI && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
+    if (EPI && part0 && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
     return;
   }
   if (EPI && nrm_part) {
@@ -521,9 +450,12 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
     y[row] = acc;
     const double xv = x[row] * cf;
     if (xs) xs[row] = xv;
-    d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
-    d1 = acc * acc;
+    if (part0) {
+      d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
+      d1 = acc * acc;
+    }
   }
+  if (!part0) return;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     d0 += __shfl_xor(d0, o, 64);
@@ -869,10 +801,12 @@ void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStre
   const dim3 grid(sell_fused_blocks(m.rows));
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<false, true>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{});
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, nullptr,
+                       nullptr);
   else
     hipLaunchKernelGGL((k_sell_spmv<false, false>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{});
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, nullptr,
+                       nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -884,10 +818,25 @@ void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, 
   if (nb <= 0) return;
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<true, true>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready);
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready, nullptr, nullptr);
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready);
+                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready, nullptr, nullptr);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, double* xs,
+                    double* y, const int* status, hipStream_t s) {
+  if (m.rows <= 0) return;
+  const dim3 grid(sell_fused_blocks(m.rows));
+  if (m.col16)
+    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, cf_dev,
+                       status);
+  else
+    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
+                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, cf_dev,
+                       status);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -16,9 +16,11 @@
 // owned entries (Seg) with the partial sums all-reduced before the final
 // fixed-order sum, so every rank takes the same decisions from bitwise equal
 // scalars. Every operator refreshes the ghost entries of its input first.
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <stdexcept>
 #include <vector>
@@ -630,6 +632,123 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   return st;
 }
 
+// The inner Schur GMRES on the explicit S with classical Gram-Schmidt twice
+// (DCP_OPT_GRAM_SCHMIDT = 1): deal.II SolverGMRES's cycle structure, Givens
+// rotations, residual estimate and SolverControl rule, with every restart
+// cycle enqueued at once and run on the device (kernels/krylov.hip). The host
+// polls the device status every kGmPoll steps so it stops enqueueing shortly
+// after convergence (the steps already queued return at entry).
+constexpr int kGmPoll = 4;
+State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
+                               std::vector<double*>& tv, int n_tmp) {
+  const int n = c.n_p;
+  const Seg g = c.seg_p();
+  const int restart = n_tmp - 2;
+  if (restart + 1 > kGmMaxDim) throw std::runtime_error("gmres_schur_cgs2: restart too long");
+  ensure_pool(tv, n_tmp + 2, size_t(n));
+  double* p = tv[n_tmp - 1];
+  double* wbuf[2] = {tv[n_tmp], tv[n_tmp + 1]};
+  if (!c.gm_init) {
+    c.gm_state.alloc(1);
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_init), sizeof(GmresDev)));
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_read), sizeof(GmresDev)));
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_flag), 2 * sizeof(int)));
+    for (auto& ev : c.gm_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  const size_t pn = cgs2_granules(g.n);
+  if (c.gm_part.n < pn) {
+    c.gm_part.alloc(pn);
+    c.gm_part.zero(c.stream);  // tag 0: never waited for
+  }
+  if (!c.gm_cnt.p) {
+    c.gm_cnt.alloc(1);
+    c.gm_cnt.zero(c.stream);
+  }
+  const std::vector<const double*> ptrs(tv.begin(), tv.begin() + restart);
+  if (ptrs != c.gm_ptrs_host) {
+    c.gm_ptrs.upload(ptrs);
+    c.gm_ptrs_host = ptrs;
+  }
+  GmresDev* dst = c.gm_state.p;
+  Comm* comm = c.comm.get();
+  const int nb1 = std::min(c.n_cus, 256);
+  const bool one_launch = !comm && c.fused_chain && c.hmapped && cgs2_chain_fits(g.n, nb1, c.n_cus);
+  State st = kIterate;
+  unsigned accumulated = 0;
+  for (;;) {
+    if (c.S_perm.p)
+      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
+    else
+      schur_vmult(c, x, p);
+    sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
+    const double rho = std::sqrt(dot_host(c, g, p, p, kSlotA));
+    st = ctl.check(accumulated, rho);
+    if (st != kIterate) break;
+    equ(n, DScal{nullptr, 1. / rho}, p, tv[0], c.stream);
+    std::memset(c.gm_init, 0, sizeof(GmresDev));
+    c.gm_init->gamma[0] = rho;
+    c.gm_init->tol = ctl.tol;
+    c.gm_init->inv_norm = 1.0;
+    c.gm_init->accumulated = int(accumulated);
+    c.gm_init->max_steps = int(ctl.max_steps);
+    DCP_HIP_CHECK(hipMemcpyAsync(dst, c.gm_init, sizeof(GmresDev), hipMemcpyHostToDevice, c.stream));
+    int polls = 0;
+    for (int k = 0; k < restart; ++k) {
+      double* src = k == 0 ? tv[0] : wbuf[(k - 1) & 1];
+      double* w = wbuf[k & 1];
+      halo_exchange(c, c.halo_p, src);
+      Timer* e = schur_sample(c);
+      if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+      sell_spmv_step(c.sell(), src, k == 0 ? nullptr : &dst->inv_norm, k == 0 ? nullptr : tv[k],
+                     w, &dst->status, c.stream);
+      if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+      if (one_launch)
+        cgs2_chain_step(g, w, chain_vecs(tv, k + 1), k + 1, dst, c.chain_gran.p, nb1,
+                        ++c.chain_seq, chain_err(c), c.stream);
+      else
+        cgs2_gmres_step(g, w, chain_vecs(tv, k + 1), k + 1, c.gm_part.p, c.gm_cnt.p, dst,
+                        c.chain_seq, comm ? c.dscal.p + kSlotD : chain_err(c), comm, c.stream);
+      if (k % kGmPoll == kGmPoll - 1 && k + 1 < restart) {
+        const int slot_now = polls & 1;
+        DCP_HIP_CHECK(hipMemcpyAsync(&c.gm_flag[slot_now], &dst->status, sizeof(int),
+                                     hipMemcpyDeviceToHost, c.stream));
+        DCP_HIP_CHECK(hipEventRecord(c.gm_ev[slot_now], c.stream));
+        if (polls > 0) {
+          // the previous poll's status: stop enqueueing once the cycle has stopped
+          DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[slot_now ^ 1]));
+          if (c.gm_flag[slot_now ^ 1] != 0) break;
+        }
+        ++polls;
+      }
+    }
+    DCP_HIP_CHECK(hipMemcpyAsync(c.gm_read, dst, sizeof(GmresDev), hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    if (!comm) check_chain_err(c);
+    const GmresDev& r = *c.gm_read;
+    accumulated = unsigned(r.accumulated);
+    ctl.last_step = accumulated;
+    ctl.last_value = r.rho;
+    if (r.dim > 0) {
+      gmres_backsub(dst, c.stream);
+      multi_axpy(n, r.dim, dst->y, c.gm_ptrs.p, x, c.stream);
+    }
+    st = r.status == 1 ? kSuccess : (r.status == 2 ? kFailure : kIterate);
+    if (st != kIterate) break;
+  }
+  return st;
+}
+
+State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
+                       int n_tmp) {
+  if (!c.S_perm.p) return gmres_schur_cgs2_ordered(c, x, b, ctl, tv, n_tmp);
+  const int n = c.n_p;
+  gather(n, c.S_perm.p, x, c.sperm_x.p, c.stream);
+  gather(n, c.S_perm.p, b, c.sperm_b.p, c.stream);
+  const State st = gmres_schur_cgs2_ordered(c, c.sperm_x.p, c.sperm_b.p, ctl, tv, n_tmp);
+  scatter(n, c.S_perm.p, c.sperm_x.p, x, c.stream);
+  return st;
+}
+
 // deal.II Householder<double>::least_squares on the (m x n) matrix S.
 double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
                                  std::vector<double>& dst, const std::vector<double>& src) {
@@ -733,7 +852,9 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
     Control ctl{5000, 1e-6 * nrm};
     ensure_pool(c.sg_v, 32, size_t(np));
     State st;
-    if (c.schur_explicit) {
+    if (c.schur_explicit && c.gram_schmidt == 1) {
+      st = gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+    } else if (c.schur_explicit) {
       st = gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else {
       Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };

@@ -31,6 +31,7 @@ OPT_MATRIX_FREE = 3
 OPT_FUSED_CHAIN = 4
 OPT_FGMRES_MAX_OUTER = 5
 OPT_ASSEMBLE_VELOCITY_BLOCK = 6
+OPT_GRAM_SCHMIDT = 7
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -509,6 +510,12 @@ class Context:
         in colour-class launches; False / 0: block-CSR SpMV of the assembled
         matrix."""
         self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(mode)))
+
+    def set_gram_schmidt(self, kind: str):
+        """DCP_OPT_GRAM_SCHMIDT of the inner Schur GMRES: "modified" (deal.II
+        SolverGMRES, default) or "classical2" (CGS2, device-resident cycles)."""
+        self._check(lib().dcp_set_option(self._h, OPT_GRAM_SCHMIDT,
+                                         {"modified": 0, "classical2": 1}[kind]))
 
     def set_assemble_velocity_block(self, on: bool):
         """DCP_OPT_ASSEMBLE_VELOCITY_BLOCK: False (default) = assemble_nse_system

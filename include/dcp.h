@@ -149,6 +149,14 @@ enum { DCP_OPT_FUSED_CHAIN = 4 };
  *   assembly too, as the reference's distribute_local_to_global does
  *   (boussinesq_model.tpp:677-687). */
 enum { DCP_OPT_ASSEMBLE_VELOCITY_BLOCK = 6 };
+/* DCP_OPT_GRAM_SCHMIDT: 0 (default) = the inner Schur-complement GMRES
+ *   orthogonalises like deal.II SolverGMRES (modified Gram-Schmidt, one
+ *   reduction per basis vector, re-orthogonalisation after a loss-of-
+ *   orthogonality test); 1 = classical Gram-Schmidt applied twice (CGS2: two
+ *   block reductions per Arnoldi step), with the Givens updates and the
+ *   SolverControl check on the device so a restart cycle runs without host
+ *   round trips. Same Krylov space and stopping rule; rounding differs. */
+enum { DCP_OPT_GRAM_SCHMIDT = 7 };
 /* DCP_OPT_FGMRES_MAX_OUTER (test hook, default 40): the iteration cap of the
  *   first FGMRES(30) (SolverControl(40, ...), boussinesq_model.tpp:1166); a
  *   lower cap sends small meshes through the do_solve_A / FGMRES(50) fallback

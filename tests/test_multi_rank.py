@@ -136,10 +136,14 @@ def _time_step(ctx, m, u, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,refine", [(2, 2), (3, 2), (4, 2)])
-def test_group_time_step_matches_single_gpu(world, refine):
+@pytest.mark.parametrize("world,refine,gs", [(2, 2, "modified"), (3, 2, "modified"),
+                                             (4, 2, "modified"), (2, 2, "classical2"),
+                                             (3, 2, "classical2")])
+def test_group_time_step_matches_single_gpu(world, refine, gs):
     """(At r = 3 this random state drives the reference's inner Schur GMRES
-    into its 5000-iteration cap on one GPU and on every partition alike.)"""
+    into its 5000-iteration cap on one GPU and on every partition alike.)
+    gs: DCP_OPT_GRAM_SCHMIDT of the inner Schur GMRES on every rank and on the
+    single-GPU reference run."""
     m = dcp.HostMesh(refine=refine)
     ph = dcp.classic_physics()
     rng = np.random.default_rng(7)
@@ -149,6 +153,7 @@ def test_group_time_step_matches_single_gpu(world, refine):
     ref_ctx = dcp.Context()
     ref_ctx.set_physics(ph)
     ref_ctx.upload_mesh(m)
+    ref_ctx.set_gram_schmidt(gs)
     ref = _time_step(ref_ctx, m, u, T)
     ref_ctx.close()
 
@@ -160,6 +165,7 @@ def test_group_time_step_matches_single_gpu(world, refine):
             ctx = dcp.Context(rank=rank, world_size=world, group=g)
             ctx.set_physics(ph)
             ctx.upload_mesh(m)
+            ctx.set_gram_schmidt(gs)
             results[rank] = _time_step(ctx, m, u, T)
             ctx.close()
         except Exception as e:  # noqa: BLE001

@@ -191,10 +191,16 @@ def test_operator_applies(setup, explicit, mfree):
     ctx.set_matrix_free(True)
 
 
-@pytest.mark.parametrize("explicit", [True, False], ids=["S-explicit", "S-composite"])
-def test_full_solve_and_temperature(setup, explicit):
+@pytest.mark.parametrize("explicit,gs", [(True, "modified"), (False, "modified"),
+                                         (True, "classical2")],
+                         ids=["S-explicit", "S-composite", "S-explicit-CGS2"])
+def test_full_solve_and_temperature(setup, explicit, gs):
+    """One reference time step against the oracle (deal.II's modified
+    Gram-Schmidt in the oracle in every case; DCP_OPT_GRAM_SCHMIDT=1 runs the
+    inner Schur GMRES with device-resident CGS2 cycles instead)."""
     m, ph, ctx, orc = setup
     ctx.set_schur_explicit(explicit)
+    ctx.set_gram_schmidt(gs)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
     for c in (ctx,):
         c.set_state(dcp.OLD_NSE_SOLUTION, u)
@@ -231,10 +237,11 @@ def test_full_solve_and_temperature(setup, explicit):
     # step control on the new velocity
     assert np.isclose(ctx.max_velocity(), orc.max_velocity(x_g), rtol=1e-12)
     assert np.isclose(ctx.cfl_number(), orc.cfl(x_g), rtol=1e-12)
+    ctx.set_gram_schmidt("modified")
 
 
-@pytest.mark.parametrize("max_outer", [10, 3])
-def test_fallback_solve_do_solve_A(setup, max_outer):
+@pytest.mark.parametrize("max_outer,gs", [(10, "modified"), (3, "modified"), (3, "classical2")])
+def test_fallback_solve_do_solve_A(setup, max_outer, gs):
     """Q10 (boussinesq_model.tpp:1166-1232): the first FGMRES(30) is capped
     (test hook, identical in oracle and GPU) so the reference's fallback runs:
     BlockSchurPreconditioner with do_solve_A = true, whose velocity block is
@@ -250,11 +257,13 @@ def test_fallback_solve_do_solve_A(setup, max_outer):
     ctx.assemble_nse_system()
     ctx.build_nse_preconditioner()
     ctx.set_fgmres_max_outer(max_outer)
+    ctx.set_gram_schmidt(gs)
     try:
         rc, outer, inner = ctx.solve_nse()
         a_its = ctx.timings()["a_solve_iterations"]
     finally:
         ctx.set_fgmres_max_outer(40)
+        ctx.set_gram_schmidt("modified")
     orc.assemble_nse_system(u, T)
     orc.build_nse_preconditioner()
     rco, x_o, outer_o, inner_o = orc.solve_nse(u, max_outer=max_outer)
@@ -397,3 +406,33 @@ def test_schur_launch_ahead_is_bitwise_the_serial_loop(monkeypatch, force_reorth
     (ya, ia), (yb, ib) = res
     assert ia == ib and ia > 10
     assert np.array_equal(ya, yb)
+
+
+def test_cgs2_cycle_is_deterministic_and_orthogonal():
+    """DCP_OPT_GRAM_SCHMIDT=1: every reduction of the device-resident cycle
+    has a fixed shape, so two applies are bitwise equal; the result solves the
+    Schur system to the SolverControl tolerance, as the modified Gram-Schmidt
+    path does (same Krylov space, rounding differs)."""
+    m = dcp.HostMesh(refine=2)
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.classic_physics())
+    ctx.upload_mesh(m)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
+    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    x = np.random.default_rng(SEED + 5).uniform(-1, 1, m.n_u + m.n_p)
+    x[m.n_u:] -= x[m.n_u:].mean()
+    out = {}
+    for gs in ("classical2", "classical2", "modified"):
+        ctx.set_gram_schmidt(gs)
+        out.setdefault(gs, []).append(ctx.block_preconditioner_vmult(x))
+    ctx.set_gram_schmidt("modified")
+    (ya, ia), (yb, ib) = out["classical2"]
+    assert ia == ib and ia > 10 and np.array_equal(ya, yb)
+    ym, im = out["modified"][0]
+    # dst_p = -S^-1 src_p to 1e-6 |src_p| in both; the pressure blocks agree to that
+    sp_ = x[m.n_u:]
+    assert np.linalg.norm(ya[m.n_u:] - ym[m.n_u:]) <= 1e-4 * np.linalg.norm(ym[m.n_u:])
+    assert abs(ia - im) <= 0.25 * im
+    ctx.close()

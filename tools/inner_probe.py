@@ -22,6 +22,8 @@ for path in libs or [dcp.LIB_PATH]:
     dcp._lib = dcp.load_library(path)
     ctx = dcp.Context(device=0)
     ctx.set_physics(dcp.classic_physics())
+    if os.environ.get("GS"):
+        ctx.set_gram_schmidt(os.environ["GS"])
     ctx.upload_mesh(m)
     ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
     ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
