@@ -202,6 +202,9 @@ constexpr RefTables make_ref_tables() {
   return t;
 }
 __constant__ RefTables cRef = make_ref_tables();
+__device__ inline double sel_gauss(int i) {
+  return i == 0 ? kGaussX[0] : (i == 1 ? kGaussX[1] : kGaussX[2]);
+}
 
 // Node-group pairs (A <= B) of the 9 groups of 3 lexicographic nodes.
 constexpr int kGroupPairs = 45;
@@ -429,12 +432,26 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
       sh.pos[945 + i] = sm.posB[216 * size_t(cell) + i];
     }
   }
-  for (int i = tid; i < 729; i += kNseThreads) sh.S[i] = cRef.S2[i];
-  for (int i = tid; i < 3 * 729; i += kNseThreads) sh.D[i] = cRef.G2[i];
+  // reference shape values / gradients at the Gauss points, formed from the 1D
+  // bases (a 23 KB table copy per cell would stream through L2 for every cell)
+  for (int i = tid; i < 729; i += kNseThreads) {
+    const int q = i / 27, n = i - 27 * q;
+    const double xa = sel_gauss(q % 3), xb = sel_gauss((q / 3) % 3), xc = sel_gauss(q / 9);
+    const int na = n % 3, nb = (n / 3) % 3, nc = n / 9;
+    const double la = ce_l2(na, xa), lb = ce_l2(nb, xb), lc = ce_l2(nc, xc);
+    sh.S[i] = la * lb * lc;
+    sh.D[3 * i + 0] = ce_dl2(na, xa) * lb * lc;
+    sh.D[3 * i + 1] = la * ce_dl2(nb, xb) * lc;
+    sh.D[3 * i + 2] = la * lb * ce_dl2(nc, xc);
+  }
   __syncthreads();
 
   // MappingQ(3): J[i][e] = sum_n X_n,i dN_n/dxi_e over the 64 support points, thread (q, i)
-  if (tid < 81) {
+  // (timing probe only: DCP_OP_NOGEO skips the map and the gradient transform)
+#ifndef DCP_OP_NOGEO
+#define DCP_OP_NOGEO 0
+#endif
+  if (tid < 81 && !DCP_OP_NOGEO) {
     const int q = tid / 3, i = tid % 3;
     double J0, J1, J2, x;
     map_row(sh.X, q, i, x, J0, J1, J2);
@@ -474,7 +491,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   }
   __syncthreads();
   // physical gradients in place: grad_d = sum_e dN/dxi_e Ji[e][d]
-  for (int i = tid; i < 729; i += kNseThreads) {
+  for (int i = tid; i < (DCP_OP_NOGEO ? 0 : 729); i += kNseThreads) {
     const double* Ji = &sh.geo.Ji[9 * (i / 27)];
     double* g = &sh.D[3 * i];
     const double r0 = g[0], r1 = g[1], r2 = g[2];
@@ -614,8 +631,16 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 
   if (MODE == 2) {
     // B^T rows (an, v): one per thread, condensed C_a^T b; rhs nodes on 27 more
+    // (timing probes only: DCP_OP_NOBT skips the rows, DCP_OP_NOSCATTER the
+    // matrix writes; both give wrong matrices)
+#ifndef DCP_OP_NOBT
+#define DCP_OP_NOBT 0
+#endif
+#ifndef DCP_OP_NOSCATTER
+#define DCP_OP_NOSCATTER 0
+#endif
     double bt[3] = {0, 0, 0};
-    if (want_B && tid < 216) {
+    if (want_B && tid < 216 && !DCP_OP_NOBT) {
       nse_div(sh, tid / 8, tid % 8, bt);
       double Ca[3][3];
       condensation(cd.vcon[sh.node[tid / 8]], Ca);
@@ -632,7 +657,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #pragma unroll
       for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
     }
-    if (!want_B) return;
+    if (!want_B || DCP_OP_NOSCATTER) return;
     __syncthreads();  // gradient tables dead: stage the rows for the all-wave scatter
     double* stage = sh.X;
     if (tid < 216) {
