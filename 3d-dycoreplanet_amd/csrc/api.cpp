@@ -187,6 +187,13 @@ struct HostPrep {
   std::vector<int32_t> ccells;
   std::vector<int32_t> Ap, Ac, Btp, Btc, Bp, Bc, Tp, Tc, Sp, Sc;
   int S_max_row = 0;
+  // periodic identification (DoFTools::make_periodicity_constraints): a dof
+  // whose closed constraint line is "= its partner" is replaced by the partner
+  // in the cell maps; the original maps (empty when nothing is identified)
+  // route the constrained-diagonal entries to the identified dof itself
+  std::vector<int32_t> q2o, pdo, tdo;
+  std::vector<int32_t> vmaster, pmaster, tmaster;  // -1 or the partner
+  int n_vslave = 0, n_pslave = 0, n_tslave = 0;
 };
 
 // Host half of dcp_mesh_upload: validation, node map, node-local constraints,
@@ -238,19 +245,95 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     }
   }
   for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
+  // ---- periodic identification. An identity line "dof = partner" (one
+  // entry, weight 1, homogeneous: a closed make_periodicity_constraints line)
+  // makes the dof an image of its partner. A velocity node is an image of node
+  // m when each component's line is the identity to m's component or equals
+  // m's own line (e.g. both fixed, where the partner's boundary condition was
+  // closed into the image's line).
+  auto identity_target = [](const dcp_constraints* c, int l) {
+    const int b = c->entry_ptr[l];
+    return (c->entry_ptr[l + 1] - b == 1 && c->entry_w[b] == 1.0 && c->inhomogeneity[l] == 0.0)
+               ? c->entry_dof[b]
+               : -1;
+  };
+  h.vmaster.assign(nv, -1);
+  h.pmaster.assign(n_p, -1);
+  h.tmaster.assign(n_T, -1);
+  std::vector<int> nse_line(size_t(n_u) + n_p, -1);
+  if (nse_c)
+    for (int l = 0; l < nse_c->n_lines; ++l) {
+      const int dof = nse_c->line_dof[l];
+      require(dof >= 0 && dof < n_u + n_p, DCP_ERR_INVALID, "constraint dof out of range");
+      nse_line[dof] = l;
+    }
+  auto same_line = [&](int a, int b) {
+    const int la = nse_line[a], lb = nse_line[b];
+    if (la < 0 || lb < 0) return la == lb;
+    const int na = nse_c->entry_ptr[la + 1] - nse_c->entry_ptr[la];
+    if (na != nse_c->entry_ptr[lb + 1] - nse_c->entry_ptr[lb]) return false;
+    if (nse_c->inhomogeneity[la] != nse_c->inhomogeneity[lb]) return false;
+    for (int k = 0; k < na; ++k) {
+      const int ea = nse_c->entry_ptr[la] + k, eb = nse_c->entry_ptr[lb] + k;
+      // entries on the partner's other components, translated to a's node
+      if (nse_c->entry_dof[ea] % 3 != nse_c->entry_dof[eb] % 3 ||
+          nse_c->entry_w[ea] != nse_c->entry_w[eb])
+        return false;
+    }
+    return true;
+  };
+  if (nse_c) {
+    for (int n = 0; n < nv; ++n) {
+      int m = -1;
+      for (int c = 0; c < 3 && m < 0; ++c) {
+        const int l = nse_line[3 * n + c];
+        const int t = l >= 0 ? identity_target(nse_c, l) : -1;
+        if (t >= 0 && t < n_u && t / 3 != n && t % 3 == c) m = t / 3;
+      }
+      if (m < 0) continue;
+      for (int c = 0; c < 3; ++c) {
+        const int l = nse_line[3 * n + c];
+        require(l >= 0, DCP_ERR_UNSUPPORTED, "partly periodic velocity node");
+        const bool ident = identity_target(nse_c, l) == 3 * m + c;
+        require(ident || same_line(3 * n + c, 3 * m + c),
+                DCP_ERR_UNSUPPORTED,
+                "velocity node " + std::to_string(n) + " is neither free, node-local nor an "
+                "image of one partner node");
+      }
+      h.vmaster[n] = m;
+      h.n_vslave++;
+    }
+    for (int p = 0; p < n_p; ++p) {
+      const int l = nse_line[n_u + p];
+      if (l < 0) continue;
+      const int t = identity_target(nse_c, l);
+      require(t >= n_u && t < n_u + n_p && t != n_u + p, DCP_ERR_UNSUPPORTED,
+              "pressure constraints other than periodic identities are not supported");
+      h.pmaster[p] = t - n_u;
+      h.n_pslave++;
+    }
+    for (int n = 0; n < nv; ++n)
+      require(h.vmaster[n] < 0 || h.vmaster[h.vmaster[n]] < 0, DCP_ERR_UNSUPPORTED,
+              "periodic chain not closed");
+    for (int p = 0; p < n_p; ++p)
+      require(h.pmaster[p] < 0 || h.pmaster[h.pmaster[p]] < 0, DCP_ERR_UNSUPPORTED,
+              "periodic chain not closed");
+  }
   // ---- constraints -> node-local form. A line without entries is a fixed
   // component; three of them on one node form a no-slip node; a single one is
   // a no-normal-flux line whose weights all vanished (normal along an axis).
+  // A periodic image is type 3 (every component constrained to its partner).
   auto& vc = h.vc;
   vc.assign(nv, NodeConstraint{{0, 0, 0}, 0, -1});
   std::vector<int> n_lines(nv, 0), fixed(nv, 0), fixed_comp(nv, -1);
   if (nse_c) {
     for (int l = 0; l < nse_c->n_lines; ++l) {
       const int dof = nse_c->line_dof[l];
-      require(dof >= 0 && dof < n_u, DCP_ERR_UNSUPPORTED, "pressure constraints are not supported");
+      if (dof >= n_u) continue;  // periodic pressure identities (above)
       require(nse_c->inhomogeneity[l] == 0.0, DCP_ERR_UNSUPPORTED,
               "inhomogeneous velocity constraints are not supported");
       const int node = dof / 3, comp = dof % 3;
+      if (h.vmaster[node] >= 0) continue;
       n_lines[node]++;
       const int b = nse_c->entry_ptr[l], e = nse_c->entry_ptr[l + 1];
       if (b == e) {
@@ -269,6 +352,10 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
       }
     }
     for (int k = 0; k < nv; ++k) {
+      if (h.vmaster[k] >= 0) {
+        vc[k] = NodeConstraint{{0, 0, 0}, 3, -1};
+        continue;
+      }
       if (n_lines[k] == 0) continue;
       if (n_lines[k] == 3 && fixed[k] == 3) {
         vc[k].type = 1;
@@ -288,11 +375,33 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     for (int l = 0; l < T_c->n_lines; ++l) {
       const int dof = T_c->line_dof[l];
       require(dof >= 0 && dof < n_T, DCP_ERR_INVALID, "temperature constraint out of range");
+      const int t = identity_target(T_c, l);
+      if (t >= 0 && t != dof) {  // periodic image
+        require(t < n_T, DCP_ERR_INVALID, "temperature constraint out of range");
+        h.tmaster[dof] = t;
+        h.n_tslave++;
+        continue;
+      }
       require(T_c->entry_ptr[l] == T_c->entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
-              "temperature constraints must be Dirichlet lines");
+              "temperature constraints must be Dirichlet lines or periodic identities");
       h.Tfix[dof] = 1;
       h.Tbc[dof] = T_c->inhomogeneity[l];
     }
+  for (int t = 0; t < n_T; ++t)
+    require(h.tmaster[t] < 0 || (h.tmaster[h.tmaster[t]] < 0 && !h.Tfix[h.tmaster[t]]),
+            DCP_ERR_UNSUPPORTED, "periodic temperature chain not closed");
+  // identified cell maps (the originals kept for the constrained diagonals)
+  if (h.n_vslave || h.n_pslave || h.n_tslave) {
+    h.q2o = q2;
+    h.pdo = pd;
+    h.tdo = td;
+    for (auto& n : q2)
+      if (h.vmaster[n] >= 0) n = h.vmaster[n];
+    for (auto& p : pd)
+      if (h.pmaster[p] >= 0) p = h.pmaster[p];
+    for (auto& t : td)
+      if (h.tmaster[t] >= 0) t = h.tmaster[t];
+  }
   // ---- colouring (greedy over vertex-sharing cells; tree order)
   std::vector<int32_t> vptr, vcells;
   {
@@ -331,11 +440,26 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     std::vector<int> f(h.color_ptr.begin(), h.color_ptr.end() - 1);
     for (int cell = 0; cell < n_cells; ++cell) ccells[f[color[cell]]++] = cell;
   }
-  // ---- patterns
+  // ---- patterns (an identified dof keeps only its diagonal, as a constrained
+  // row of make_sparsity_pattern)
   union_pattern(nv, n_cells, q2.data(), 27, q2.data(), 27, h.Ap, h.Ac);
   union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, h.Btp, h.Btc);
   union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, h.Bp, h.Bc);
   union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, h.Tp, h.Tc);
+  auto add_diagonals = [](std::vector<int32_t>& ptr, std::vector<int32_t>& col,
+                          const std::vector<int32_t>& master) {
+    std::vector<int32_t> np(ptr.size(), 0), nc;
+    nc.reserve(col.size() + master.size());
+    for (size_t r = 0; r + 1 < ptr.size(); ++r) {
+      if (master[r] >= 0) nc.push_back(int32_t(r));  // empty row: the diagonal only
+      else nc.insert(nc.end(), col.begin() + ptr[r], col.begin() + ptr[r + 1]);
+      np[r + 1] = int32_t(nc.size());
+    }
+    ptr.swap(np);
+    col.swap(nc);
+  };
+  if (h.n_vslave) add_diagonals(h.Ap, h.Ac, h.vmaster);
+  if (h.n_tslave) add_diagonals(h.Tp, h.Tc, h.tmaster);
   // Pattern of the explicit Schur complement S = B D^-1 B^T: row p couples the
   // vertices reachable through one velocity node (the 2-cell vertex patch).
   h.Sp.assign(size_t(n_p) + 1, 0);
@@ -756,9 +880,13 @@ void materialize_velocity_block(Ctx& c) {
   out.B = c.B_val.p;
   out.cdiag = c.con_diag.p;
   out.cidx = c.mf_cidx.p;
+  out.pcdiag = c.con_diag.p + 3 * size_t(c.n_con);
+  out.pcidx = c.periodic ? c.pcidx.p : nullptr;
   for (int k = 0; k < c.n_colors(); ++k)
     launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p, c.old_T.p,
                       c.nse_ph, out, c.stream);
+  image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
+                        c.A_val.p, c.stream);
   c.A_current = true;
 }
 }  // namespace dcp
@@ -1018,6 +1146,8 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       cell_diameter = L.diameter.data();
       prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
                    cell_diameter, n_u, n_p, n_T, &lnc, &ltc);
+      require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
+              "periodic constraints on several GPUs are not supported");
     } else {
       prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u,
                    n_p, n_T, nse_c, T_c);
@@ -1114,8 +1244,8 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_q2.upload(oq2);
       c.mf_p.upload(op);
       // constrained velocity nodes: index into con_diag (3 per node)
-      std::vector<int32_t> cdof, cidx(nv, -1);
-      std::vector<int64_t> cpos;
+      std::vector<int32_t> cdof, cidx(nv, -1), img_node;
+      std::vector<int64_t> cpos, img_blk;
       int n_con = 0;
       for (int n = 0; n < nv; ++n) {
         if (vc[n].type == 0) continue;
@@ -1123,14 +1253,76 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         require(b != Ac.data() + Ap[n + 1] && *b == n, DCP_ERR_INVALID, "A pattern lacks a diagonal block");
         cidx[n] = n_con;
         for (int comp = 0; comp < 3; ++comp)
-          if (vc[n].type == 1 || comp == vc[n].k) {
+          if (vc[n].type == 1 || vc[n].type == 3 || comp == vc[n].k) {
             cdof.push_back(3 * n + comp);
             cpos.push_back(3 * int64_t(n_con) + comp);
           }
+        if (vc[n].type == 3) {
+          img_node.push_back(n);
+          img_blk.push_back(b - Ac.data());
+        }
         ++n_con;
       }
+      // periodic pressure images after the velocity nodes in con_diag (and in
+      // the colour path's fix-up list, which the velocity-only apply cuts short)
+      c.mf_ncon_v = int(cdof.size());
+      std::vector<int32_t> pcidx(n_p, -1);
+      int n_pimg = 0;
+      for (int i = 0; i < n_p; ++i)
+        if (h.pmaster[i] >= 0) {
+          pcidx[i] = n_pimg;
+          cdof.push_back(n_u + i);
+          cpos.push_back(3 * int64_t(n_con) + n_pimg);
+          ++n_pimg;
+        }
       c.mf_cidx.upload(cidx);
-      c.con_diag.alloc(3 * size_t(n_con));
+      c.n_con = n_con;
+      c.con_diag.alloc(3 * size_t(n_con) + n_pimg);
+      c.periodic = h.n_vslave || h.n_pslave || h.n_tslave;
+      if (c.periodic) {
+        c.pcidx.upload(pcidx);
+        c.cell_q2o.upload(h.q2o);
+        c.cell_po.upload(h.pdo);
+        c.cell_To.upload(h.tdo);
+        std::vector<int32_t> iu, mu, ip, mp, iT, mT;
+        for (int n = 0; n < nv; ++n)
+          if (h.vmaster[n] >= 0)
+            for (int comp = 0; comp < 3; ++comp) {
+              iu.push_back(3 * n + comp);
+              mu.push_back(3 * h.vmaster[n] + comp);
+            }
+        for (int i = 0; i < n_p; ++i)
+          if (h.pmaster[i] >= 0) {
+            ip.push_back(n_u + i);
+            mp.push_back(n_u + h.pmaster[i]);
+          }
+        for (int t = 0; t < n_T; ++t)
+          if (h.tmaster[t] >= 0) {
+            iT.push_back(t);
+            mT.push_back(h.tmaster[t]);
+          }
+        c.img_u.upload(iu);
+        c.mst_u.upload(mu);
+        c.img_p.upload(ip);
+        c.mst_p.upload(mp);
+        c.img_T.upload(iT);
+        c.mst_T.upload(mT);
+        c.n_img_u = int(iu.size());
+        c.n_img_p = int(ip.size());
+        c.n_img_T = int(iT.size());
+        c.img_node.upload(img_node);
+        c.img_blk.upload(img_blk);
+        c.n_img_node = int(img_node.size());
+        std::vector<int32_t> pts(size_t(n_cells) * 8, -1);
+        for (int cell = 0; cell < n_cells; ++cell)
+          for (int v = 0; v < 8; ++v) {
+            const int o = h.tdo[8 * size_t(cell) + v];
+            if (o == td[8 * size_t(cell) + v]) continue;
+            const auto* b = std::lower_bound(Tc.data() + Tp[o], Tc.data() + Tp[o + 1], o);
+            pts[8 * size_t(cell) + v] = int32_t(b - Tc.data());
+          }
+        c.posTs.upload(pts);
+      }
       c.mf_first.upload(first);
       c.mf_cdof.upload(cdof);
       c.mf_cpos.upload(cpos);
@@ -1370,6 +1562,8 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       out.B = c.B_val.p;
       out.cdiag = c.con_diag.p;
       out.cidx = c.mf_cidx.p;
+      out.pcdiag = c.con_diag.p + 3 * size_t(c.n_con);
+      out.pcidx = c.periodic ? c.pcidx.p : nullptr;
     }
     if (flags & DCP_ASSEMBLE_RHS) {
       c.nse_rhs.zero(c.stream);
@@ -1386,6 +1580,9 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
         launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                             c.old_T.p, c.ph, out, c.stream);
     }
+    if (full)
+      image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
+                            c.A_val.p, c.stream);
     t.stop();
     if (matrix) {
       c.nse_assembled = true;
@@ -1432,7 +1629,7 @@ int dcp_assemble_temperature_matrix(dcp_ctx* ctx) {
     c.Tstiff.zero(c.stream);
     for (int k = 0; k < c.n_colors(); ++k)
       launch_T_matrix(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.ph, c.Tmass.p,
-                      c.Tstiff.p, c.stream);
+                      c.Tstiff.p, c.periodic ? c.posTs.p : nullptr, c.stream);
     t.stop();
     c.T_matrix_ok = true;
     return DCP_OK;
@@ -1618,8 +1815,8 @@ int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* 
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     const auto Ap = down_i(c.A_ptr), Ac = down_i(c.A_col), Btp = down_i(c.Bt_ptr),
                Btc = down_i(c.Bt_col), Bp = down_i(c.B_ptr), Bc = down_i(c.B_col);
-    const int64_t total =
-        int64_t(Ap[c.n_vnodes]) * 9 + int64_t(Btp[c.n_vnodes]) * 3 + int64_t(Bp[c.n_p]) * 3;
+    const int64_t total = int64_t(Ap[c.n_vnodes]) * 9 + int64_t(Btp[c.n_vnodes]) * 3 +
+                          int64_t(Bp[c.n_p]) * 3 + (c.periodic ? c.n_img_p : 0);
     *nnz = total;
     if (!rowptr) return DCP_OK;
     require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
@@ -1627,6 +1824,9 @@ int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* 
     materialize_velocity_block(c);
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     const auto Av = down_d(c.A_val), Btv = down_d(c.Bt_val), Bv = down_d(c.B_val);
+    const auto cdg = down_d(c.con_diag);
+    std::vector<int32_t> pci;
+    if (c.periodic) pci = down_i(c.pcidx);
     int64_t k = 0;
     rowptr[0] = 0;
     for (int n = 0; n < c.n_vnodes; ++n)
@@ -1648,6 +1848,10 @@ int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* 
           cols[k] = 3 * Bc[b] + cc;
           vals[k++] = Bv[3 * size_t(b) + cc];
         }
+      if (c.periodic && pci[v] >= 0) {  // a periodic pressure image: its diagonal only
+        cols[k] = c.n_u + v;
+        vals[k++] = cdg[3 * size_t(c.n_con) + pci[v]];
+      }
       rowptr[c.n_u + v + 1] = int32_t(k);
     }
     return DCP_OK;

@@ -97,7 +97,17 @@ struct Ctx {
   // assembled; the velocity-velocity block A is applied matrix-free and
   // materialised into A_val only when read (export, DCP_OPT_MATRIX_FREE = 0)
   // or when DCP_OPT_ASSEMBLE_VELOCITY_BLOCK asks for it on every assembly.
-  DBuf<double> con_diag;
+  DBuf<double> con_diag;            // [3 n_con | n_pimg]: velocity nodes, then pressure images
+  int n_con = 0;
+  // periodic identification (HostPrep): original cell maps, image lists
+  // (dof, partner) per field for distribute, pressure image index, the A
+  // pattern position of each velocity image's diagonal block, and the T
+  // pattern position of each image's own diagonal per cell vertex
+  DBuf<int32_t> cell_q2o, cell_po, cell_To, pcidx, posTs;
+  DBuf<int32_t> img_u, mst_u, img_p, mst_p, img_T, mst_T, img_node;
+  DBuf<int64_t> img_blk;
+  int n_img_u = 0, n_img_p = 0, n_img_T = 0, n_img_node = 0;
+  bool periodic = false;
   bool assemble_A = false;   // DCP_OPT_ASSEMBLE_VELOCITY_BLOCK
   bool A_current = false;    // A_val holds the block of the last assembly
   PhysicsDev nse_ph{};       // physics (dt) of the last assemble_nse_system
@@ -129,7 +139,7 @@ struct Ctx {
   DBuf<uint64_t> mf_first;
   DBuf<int32_t> mf_cdof;
   DBuf<int64_t> mf_cpos;
-  int mf_ncon = 0;
+  int mf_ncon = 0, mf_ncon_v = 0;  // fix-up entries: all / velocity dofs only
   DBuf<double> mf_buf;                  // dof-sorted incidence slots (89 per cell)
   DBuf<uint32_t> mf_cmask;
   DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx, mf_vorder, mf_porder;
@@ -154,8 +164,9 @@ struct Ctx {
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
   MfGather mfg() const {
-    return MfGather{n_vnodes, n_p,      n_u,       mf_vorder.p, mf_porder.p, mf_vptr.p,
-                    mf_pptr.p, mf_pbase, mf_cidx.p, vcon.p,      con_diag.p};
+    return MfGather{n_vnodes,  n_p,      n_u,       mf_vorder.p, mf_porder.p,
+                    mf_vptr.p, mf_pptr.p, mf_pbase, mf_cidx.p,   vcon.p,
+                    con_diag.p, periodic ? pcidx.p : nullptr, con_diag.p + 3 * size_t(n_con)};
   }
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};
@@ -266,6 +277,9 @@ struct Ctx {
     c.T_fixed = T_fixed.p;
     c.T_bc = T_bc.p;
     c.diameter = diameter.p;
+    c.cell_q2o = periodic ? cell_q2o.p : nullptr;
+    c.cell_po = periodic ? cell_po.p : nullptr;
+    c.cell_To = periodic ? cell_To.p : nullptr;
     return c;
   }
   ScatterMaps maps() const { return ScatterMaps{posA.p, posBt.p, posB.p, posT.p}; }

@@ -65,6 +65,11 @@ struct CellData {
   const uint8_t* T_fixed;   // [n_T] 1 = Dirichlet
   const double* T_bc;       // [n_T] inhomogeneity (valid where T_fixed)
   const double* diameter;   // [n_cells]
+  // periodic identification: the cell maps above hold the partner of an
+  // identified dof; these hold the original dofs (null when none identified)
+  const int32_t* cell_q2o;  // [n_cells][27]
+  const int32_t* cell_po;   // [n_cells][8]
+  const int32_t* cell_To;   // [n_cells][8]
 };
 
 struct NseOut {
@@ -78,6 +83,9 @@ struct NseOut {
   // (component c of constrained node n at 3 cidx[n] + c), or null
   double* cdiag;
   const int32_t* cidx;  // [n_vnodes] constrained-node index or -1
+  // the same for the identified (periodic) pressure dofs: [n_p] index or -1
+  double* pcdiag;
+  const int32_t* pcidx;
 };
 
 // ---- matfree.hip ----------------------------------------------------------
@@ -141,6 +149,8 @@ struct MfGather {
   const int32_t* cidx;         // [n_vnodes] constrained-node index or -1
   const NodeConstraint* vcon;
   const double* cdiag;         // [n_con_nodes][3] assembled diagonal (NseOut::cdiag)
+  const int32_t* pcidx;        // [n_p] identified pressure dof index or -1 (null: none)
+  const double* pcdiag;        // their assembled diagonal
 };
 // cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
@@ -171,8 +181,13 @@ void launch_nse_system_elements(const CellData& cd, int first, int n, const doub
                                 hipStream_t s);
 void launch_nse_precond_diag(const CellData& cd, const int32_t* cells, int n, const PhysicsDev& ph,
                              double* A_diag, double* Mp_diag, hipStream_t s);
+// posTs: [n_cells][8] position of (original, original) for identified T dofs, -1 else (or null)
 void launch_T_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
-                     const PhysicsDev& ph, double* Tmass, double* Tstiff, hipStream_t s);
+                     const PhysicsDev& ph, double* Tmass, double* Tstiff, const int32_t* posTs,
+                     hipStream_t s);
+// A(s,s) block of every identified velocity node s = diag(cdiag of s)
+void image_diagonal_blocks(int n, const int32_t* node, const int64_t* blk, const int32_t* cidx,
+                           const double* cdiag, double* A_val, hipStream_t s);
 void launch_T_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
                   const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
 // Builds posA/posBt/posB/posT by binary search in the sorted patterns.
@@ -390,6 +405,8 @@ void lincomb(int n, const double* a, double alpha, const double* b, double* z, h
 void distribute_velocity(int n_vnodes, const NodeConstraint* vcon, double* u, hipStream_t s);
 void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, double* T,
                             hipStream_t s);
+// periodic images: x[img[k]] = x[master[k]], k < n
+void copy_images(int n, const int32_t* img, const int32_t* master, double* x, hipStream_t s);
 // max |u_node| and max over cells of max(1e-10, max|u|)/diam -> out[0], out[1]
 // (over the first n_cells cells of cd: the owned ones)
 void velocity_stats(const CellData& cd, int n_cells, const double* u, double* out2, hipStream_t s);

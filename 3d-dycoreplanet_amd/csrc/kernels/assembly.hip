@@ -255,6 +255,7 @@ struct NseSmem {
   double stage_pad[448];   // write staging: X..stage_pad (dead by then)
   double diag[27];         // sum_c |K_(a,c),(a,c)| per node (average-diagonal rule)
   int node[27];
+  int orig[27];            // original node (!= node: a periodic image of node)
   int pdof[8];
   int pos[729 + 216 + 216];  // this cell's posA, posBt, posB
 };
@@ -417,12 +418,16 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   if (tid < 27) {
     const int n = cd.cell_q2[27 * size_t(cell) + tid];
     sh.node[tid] = n;
+    const int o = cd.cell_q2o ? cd.cell_q2o[27 * size_t(cell) + tid] : n;
+    sh.orig[tid] = o;
+    // the old solutions at the cell's own dofs (cell->get_dof_values; for a
+    // periodic image its own entry, not its partner's)
 #pragma unroll
-    for (int d = 0; d < 3; ++d) sh.U[3 * tid + d] = u_old[3 * size_t(n) + d];
+    for (int d = 0; d < 3; ++d) sh.U[3 * tid + d] = u_old[3 * size_t(o) + d];
   } else if (tid >= 64 && tid < 72) {
     const int v = tid - 64;
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
-    sh.T[v] = T_old[cd.cell_T[8 * size_t(cell) + v]];
+    sh.T[v] = T_old[(cd.cell_To ? cd.cell_To : cd.cell_T)[8 * size_t(cell) + v]];
   }
   if (MODE == 0 && want_matrix)
     for (int i = tid; i < 729; i += kNseThreads) sh.pos[i] = sm.posA[729 * size_t(cell) + i];
@@ -566,8 +571,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   __syncthreads();
   if (want_cdiag && tid >= 64 && tid < 91) {
     // diagonal of the constrained rows of nse_matrix: AffineConstraints puts
-    // |K_ii| of every cell (the average diagonal if 0) on a constrained dof
-    const int n = sh.node[tid - 64];
+    // |K_ii| of every cell (the average diagonal if 0) on a constrained local
+    // dof -- the original one for a periodic image (type 3, all components)
+    const int n = sh.orig[tid - 64];
     const int ci = out.cidx[n];
     if (ci >= 0) {
       const NodeConstraint nc = cd.vcon[n];
@@ -576,10 +582,19 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
       avg /= 89.0;  // pressure diagonals of the local matrix are 0
 #pragma unroll
       for (int c = 0; c < 3; ++c)
-        if (nc.type == 1 || c == nc.k) {
+        if (nc.type == 1 || nc.type == 3 || c == nc.k) {
           const double d = fabs(kii_d[c]);
           out.cdiag[3 * size_t(ci) + c] += d != 0.0 ? d : avg;
         }
+    }
+  } else if (want_cdiag && cd.cell_po && tid >= 96 && tid < 104) {
+    // identified pressure dofs: their local diagonal is 0, so the average
+    const int po = cd.cell_po[8 * size_t(cell) + tid - 96];
+    const int pci = out.pcidx[po];
+    if (pci >= 0) {
+      double avg = 0;
+      for (int m = 0; m < 27; ++m) avg += sh.diag[m];
+      out.pcdiag[pci] += avg / 89.0;
     }
   }
 
@@ -741,7 +756,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #pragma unroll
         for (int j = 0; j < 3; ++j)
           K[3 * i + j] = Ca[0][i] * KC[0][j] + Ca[1][i] * KC[1][j] + Ca[2][i] * KC[2][j];
-      if (b == a && ca.type != 0) {
+      if (b == a && ca.type != 0 && sh.orig[a] == sh.node[a]) {
         // constrained local dofs: global diagonal += |K_ii| (average if 0)
         double avg = 0;
         for (int n = 0; n < 27; ++n) avg += sh.diag[n];
@@ -839,12 +854,16 @@ __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int3
       p += (s * s + ph.nu_pre * (g[0] * g[0] + g[1] * g[1] + g[2] * g[2])) * geo.JxW[q];
     }
     const int n = cd.cell_q2[27 * size_t(cell) + a];
+    const int o = cd.cell_q2o ? cd.cell_q2o[27 * size_t(cell) + a] : n;
     const NodeConstraint nc = cd.vcon[n];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
+      const bool con = nc.type == 1 || (nc.type == 2 && d == nc.k);
       double f = 1.0;
       if (nc.type == 2 && d != nc.k) f = 1.0 + nc.w[d] * nc.w[d];
-      A_diag[3 * size_t(n) + d] += f * p;
+      // a periodic image: condensed onto its partner, |P_ii| onto itself
+      if (o == n || !con) A_diag[3 * size_t(n) + d] += f * p;
+      if (o != n) A_diag[3 * size_t(o) + d] += p;
     }
   } else if (tid >= 32 && tid < 40) {
     const int v = tid - 32;
@@ -853,7 +872,9 @@ __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int3
       const double s = q1_value(q, v);
       p += s * s * geo.JxW[q];
     }
-    Mp_diag[cd.cell_p[8 * size_t(cell) + v]] += p;
+    const int pi = cd.cell_p[8 * size_t(cell) + v];
+    Mp_diag[pi] += p;
+    if (cd.cell_po && cd.cell_po[8 * size_t(cell) + v] != pi) Mp_diag[cd.cell_po[8 * size_t(cell) + v]] += p;
   }
 }
 
@@ -861,7 +882,8 @@ __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int3
 // Temperature mass / stiffness (Q1, QGauss(3)) with Dirichlet condensation.
 __global__ __launch_bounds__(64) void k_T_matrix(CellData cd, ScatterMaps sm,
                                                  const int32_t* __restrict__ cells, PhysicsDev ph,
-                                                 double* Tmass, double* Tstiff) {
+                                                 double* Tmass, double* Tstiff,
+                                                 const int32_t* __restrict__ posTs) {
   __shared__ double X[3 * kMapPts];
   __shared__ Geo geo;
   __shared__ double G1[27 * 8 * 3];
@@ -893,6 +915,25 @@ __global__ __launch_bounds__(64) void k_T_matrix(CellData cd, ScatterMaps sm,
     Tmass[pos] += fabs(M);
     Tstiff[pos] += fabs(K);
   }
+  if (posTs && i == j) {
+    // a periodic image: its own (constrained) diagonal entry
+    const int ps = posTs[8 * size_t(cell) + i];
+    if (ps >= 0) {
+      Tmass[ps] += fabs(M);
+      Tstiff[ps] += fabs(K);
+    }
+  }
+}
+
+__global__ void k_image_diag(int n, const int32_t* __restrict__ node, const int64_t* __restrict__ blk,
+                             const int32_t* __restrict__ cidx, const double* __restrict__ cdiag,
+                             double* __restrict__ A) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double* d = cdiag + 3 * size_t(cidx[node[k]]);
+  double* b = A + 9 * size_t(blk[k]);
+#pragma unroll
+  for (int e = 0; e < 9; ++e) b[e] = (e % 4 == 0) ? d[e / 4] : 0.0;
 }
 
 // Temperature rhs with the matrix_for_bc lift of inhomogeneous Dirichlet dofs.
@@ -910,13 +951,13 @@ __global__ __launch_bounds__(64) void k_T_rhs(CellData cd, const int32_t* __rest
   const int cell = cells[blockIdx.x];
   for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   if (tid < 27) {
-    const int n = cd.cell_q2[27 * size_t(cell) + tid];
+    const int n = (cd.cell_q2o ? cd.cell_q2o : cd.cell_q2)[27 * size_t(cell) + tid];
 #pragma unroll
     for (int d = 0; d < 3; ++d) U[3 * tid + d] = u_cur[3 * size_t(n) + d];
   } else if (tid >= 32 && tid < 40) {
     const int d = cd.cell_T[8 * size_t(cell) + tid - 32];
     dof[tid - 32] = d;
-    Tn[tid - 32] = T_old[d];
+    Tn[tid - 32] = T_old[(cd.cell_To ? cd.cell_To : cd.cell_T)[8 * size_t(cell) + tid - 32]];
   }
   __syncthreads();
   if (tid < 27) cell_geometry(X, geo, tid);
@@ -1128,9 +1169,18 @@ void launch_nse_precond_diag(const CellData& cd, const int32_t* cells, int n, co
 }
 
 void launch_T_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
-                     const PhysicsDev& ph, double* Tmass, double* Tstiff, hipStream_t s) {
+                     const PhysicsDev& ph, double* Tmass, double* Tstiff, const int32_t* posTs,
+                     hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_T_matrix, dim3(n), dim3(64), 0, s, cd, sm, cells, ph, Tmass, Tstiff);
+  hipLaunchKernelGGL(k_T_matrix, dim3(n), dim3(64), 0, s, cd, sm, cells, ph, Tmass, Tstiff, posTs);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void image_diagonal_blocks(int n, const int32_t* node, const int64_t* blk, const int32_t* cidx,
+                           const double* cdiag, double* A_val, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_image_diag, dim3((n + 255) / 256), dim3(256), 0, s, n, node, blk, cidx,
+                     cdiag, A_val);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -569,6 +569,12 @@ __global__ void k_distribute_velocity(int n, const NodeConstraint* __restrict__ 
   }
 }
 
+__global__ void k_copy_images(int n, const int32_t* __restrict__ img,
+                              const int32_t* __restrict__ master, double* x) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) x[img[k]] = x[master[k]];
+}
+
 __global__ void k_distribute_T(int n, const uint8_t* __restrict__ fixed, const double* __restrict__ bc,
                                double* T) {
   for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock)
@@ -589,7 +595,8 @@ __global__ __launch_bounds__(kBlock) void k_velocity_stats(CellData cd, int n_ce
   if (c < n_cells) {
     double cm = 1e-10;  // get_cfl_number initialises the cell max with 1e-10
     for (int n = 0; n < 27; ++n) {
-      const size_t b = 3 * size_t(cd.cell_q2[27 * c + n]);
+      // the cell's own dof values (a periodic image's, not its partner's)
+      const size_t b = 3 * size_t((cd.cell_q2o ? cd.cell_q2o : cd.cell_q2)[27 * c + n]);
       const double v = sqrt(u[b] * u[b] + u[b + 1] * u[b + 1] + u[b + 2] * u[b + 2]);
       mx = fmax(mx, v);
       cm = fmax(cm, v);
@@ -915,6 +922,11 @@ void lincomb(int n, const double* a, double alpha, const double* b, double* z, h
 void distribute_velocity(int n_vnodes, const NodeConstraint* vcon, double* u, hipStream_t s) {
   hipLaunchKernelGGL(k_distribute_velocity, dim3(grid_for(n_vnodes)), dim3(kBlock), 0, s, n_vnodes,
                      vcon, u);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+void copy_images(int n, const int32_t* img, const int32_t* master, double* x, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy_images, dim3(grid_for(n)), dim3(kBlock), 0, s, n, img, master, x);
   DCP_HIP_CHECK(hipGetLastError());
 }
 void distribute_temperature(int n_T, const uint8_t* fixed, const double* bc, double* T,

@@ -114,7 +114,7 @@ __device__ inline void expand(const NodeConstraint& nc, const double r[3], doubl
 }
 // reduced = C^T full
 __device__ inline void condense(const NodeConstraint& nc, double f[3]) {
-  if (nc.type == 1) {
+  if (nc.type == 1 || nc.type == 3) {
     f[0] = f[1] = f[2] = 0.0;
   } else if (nc.type == 2) {
     const double fk = f[nc.k];
@@ -848,7 +848,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
       const double* dg = g.cdiag + 3 * size_t(ci);
 #pragma unroll
       for (int comp = 0; comp < 3; ++comp)
-        if (nc.type == 1 || comp == nc.k) s[comp] = dg[comp] * src[3 * size_t(i) + comp];
+        if (nc.type == 1 || nc.type == 3 || comp == nc.k) s[comp] = dg[comp] * src[3 * size_t(i) + comp];
     }
     double* d = dst + 3 * size_t(i);
     d[0] = s[0];
@@ -874,6 +874,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
       for (int k = k0; k < k1; ++k) s += W[k];
     else
       for (int k = k0; k < k1; ++k) s += b[k];
+    if (g.pcidx && g.pcidx[j] >= 0) s = g.pcdiag[g.pcidx[j]] * src[g.n_u + j];  // periodic image
     dst[g.n_u + j] = s;
   }
 }

@@ -828,7 +828,8 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
     for (int k = 0; k < c.n_colors(); ++k)
       mf_apply_colour(md, c.color_ptr[k], c.color_size(k), c.nse_ph.nu_sys, stokes, src, dst,
                       c.stream);
-    mf_constrained(c.mf_ncon, c.mf_cdof.p, c.mf_cpos.p, c.con_diag.p, src, dst, c.stream);
+    mf_constrained(stokes ? c.mf_ncon : c.mf_ncon_v, c.mf_cdof.p, c.mf_cpos.p, c.con_diag.p, src,
+                   dst, c.stream);
   }
   if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
 }
@@ -1082,6 +1083,10 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
     }
   }
   distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
+  if (c.periodic) {  // periodic images = their partners
+    copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
+    copy_images(c.n_img_p, c.img_p.p, c.mst_p.p, x.p, c.stream);
+  }
   scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);   // :1239 (x /= dt)
   copy(n, x.p, c.nse_sol.p, c.stream);                       // :1241
   halo_exchange(c, c.halo_nse, c.nse_sol.p);                 // ghosted copy (:1241)
@@ -1252,6 +1257,7 @@ int solve_temperature(Ctx& c, int* iters, double* T_range) {
     }
   }
   distribute_temperature(n, c.T_fixed.p, c.T_bc.p, x, c.stream);
+  if (c.periodic) copy_images(c.n_img_T, c.img_T.p, c.mst_T.p, x, c.stream);
   halo_exchange(c, c.halo_T, x);
   if (T_range) {
     // min over ranks as max of -min

@@ -799,10 +799,13 @@ void block_vmult(const Csr& A, int row0, int row1, int col0, int col1, const dou
 
 void nse_vmult(const orc_model* m, const double* src, double* dst) {
   // BlockSparseMatrix::vmult: block(0,0) then vmult_add block(0,1); block(1,0)
+  // then vmult_add block(1,1) (empty but for the constrained pressure dofs'
+  // diagonal, e.g. the cuboid's periodic images)
   const int nu = m->n_u, np = m->n_p;
   block_vmult(m->nse, 0, nu, 0, nu, src, dst, false);
   block_vmult(m->nse, 0, nu, nu, nu + np, src + nu, dst, true);
   block_vmult(m->nse, nu, nu + np, 0, nu, src, dst + nu, false);
+  block_vmult(m->nse, nu, nu + np, nu, nu + np, src + nu, dst + nu, true);
 }
 
 void schur_vmult(const orc_model* m, const double* src, double* dst) {

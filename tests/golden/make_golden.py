@@ -16,7 +16,12 @@ Cases (classic shell physics, data/aqua_planet_shell_test_3d-classic.prm):
                      from the physical state (about 15 min of oracle time: ~29,000
                      inner Schur GMRES iterations): iteration counts, the NSE and
                      temperature solutions, the assembled rhs.
-usage: python tests/golden/make_golden.py [r1|r3]
+  feec_r4_step.npz   BASELINE config 4: data/aqua_planet_shell_test_3d-feec.prm at
+                     refine 4 (24,576 cells; Nedelec/RT/DGQ0 + Q1 temperature),
+                     one full FEEC time step from u = 0 and the initial temperature:
+                     assembled rhs, GMRES(100) iterations and solution, temperature
+                     solution (FeecModel, boussineq_model_FEEC.tpp:2238-2300).
+usage: python tests/golden/make_golden.py [r1|r3|feec4]
 """
 import os
 import sys
@@ -91,11 +96,36 @@ def make_step(refine):
             "iters": np.array([rc, outer, inner, rcT, itT], np.int64)}
 
 
+def make_feec_step(refine=4):
+    rp = dcp.load_prm(os.path.join(ROOT, "configs", "aqua_planet_shell_test_3d-feec.prm"))
+    ph = dcp.physics_from_params(rp)
+    m = dcp.HostMesh(cuboid=False, refine=refine, R0=rp.R0, R1=rp.R1, length=rp.length,
+                     temperature_degree=ph.temperature_degree, feec=True)
+    f = m.feec
+    x0, T0 = np.zeros(f.n), m.T0.copy()
+    orc = oracle_py.FeecModel(ph, m, zero_mean=bool(rp.correct_pressure_to_zero_mean))
+    orc.assemble_nse_system(x0, T0)
+    rhs = orc.rhs()
+    orc.assemble_preconditioner()
+    orc.assemble_temperature(T0, x0)
+    T_rhs = orc.T_rhs()
+    rc, x, it = orc.solve_nse(x0)
+    rcT, Tn, itT = orc.solve_temperature(T0)
+    vs = orc.velocity_stats(x)
+    return {"n": np.array([f.n_cells, f.n_w, f.n_u, f.n_p, m.n_T], np.int64), "nse_rhs": rhs,
+            "T_rhs": T_rhs, "nse_solution": x, "T_solution": Tn,
+            "velocity_stats": np.asarray(vs, np.float64),
+            "iters": np.array([rc, it, rcT, itT], np.int64)}
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "r1"
     if which == "r1":
         np.savez_compressed(os.path.join(HERE, "shell_r1.npz"), **make(1))
         print("wrote", os.path.join(HERE, "shell_r1.npz"))
+    elif which == "feec4":
+        np.savez_compressed(os.path.join(HERE, "feec_r4_step.npz"), **make_feec_step(4))
+        print("wrote", os.path.join(HERE, "feec_r4_step.npz"))
     elif which == "r3":
         np.savez_compressed(os.path.join(HERE, "shell_r3_step.npz"), **make_step(3))
         print("wrote", os.path.join(HERE, "shell_r3_step.npz"))

@@ -50,11 +50,28 @@ def test_upload_conversion_shell(r):
     assert (8 if r > 0 else 2) <= ncol <= 27
 
 
-def test_upload_rejects_periodic_cube():
+@pytest.mark.parametrize("r", [1, 2, 3])
+def test_upload_accepts_periodic_cube(r):
+    """BASELINE C2: the periodic x/y identities of the cuboid
+    (make_periodicity_constraints, boussinesq_model.tpp:265-285) are folded into
+    the cell maps at upload (host-only dry run)."""
+    m = dcp.HostMesh(cuboid=True, refine=r)
+    assert 8 <= m.check() <= 64
+
+
+def test_upload_rejects_partly_periodic_node():
     m = dcp.HostMesh(cuboid=True, refine=1)
-    with pytest.raises(dcp.DcpError) as e:
-        m.check()
-    assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
+    nc = m.nse_constraints
+    # turn one periodic identity line into a coupling to two nodes
+    lens = np.diff(nc.entry_ptr)
+    l = int(np.flatnonzero((lens == 1) & (nc.line_dof < m.n_u))[0])
+    e = nc.entry_ptr[l]
+    w = nc.entry_w.copy()
+    w[e] = 0.5
+    bad = dcp.ConstraintSet(nc.line_dof, nc.entry_ptr, nc.entry_dof, w, nc.inhomogeneity)
+    with pytest.raises(dcp.DcpError) as err:
+        m.check(nse_constraints=bad)
+    assert err.value.code == dcp.DCP_ERR_UNSUPPORTED
 
 
 def test_upload_rejects_bad_dof_layout():

@@ -142,3 +142,114 @@ def test_gpu_time_step_r3_matches_oracle_fixture():
     assert rcT == it[3] and abs(itT - it[4]) <= 1
     assert rel(ctx.get_state(dcp.T_SOLUTION), g["T_solution"]) < 1e-10
     ctx.close()
+
+
+FEEC4 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "feec_r4_step.npz")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _feec4_setup():
+    rp = dcp.load_prm(os.path.join(ROOT, "configs", "aqua_planet_shell_test_3d-feec.prm"))
+    ph = dcp.physics_from_params(rp)
+    m = dcp.HostMesh(cuboid=False, refine=4, R0=rp.R0, R1=rp.R1, length=rp.length,
+                     temperature_degree=ph.temperature_degree, feec=True)
+    with np.load(FEEC4) as d:
+        g = {k: d[k] for k in d.files}
+    return rp, ph, m, g
+
+
+def _feec4_step(ctx, rp, ph, m):
+    f = m.feec
+    ctx.set_physics(ph)
+    ctx.upload_feec_mesh(m)
+    ctx.set_feec_zero_mean(bool(rp.correct_pressure_to_zero_mean))
+    x0, T0 = np.zeros(f.n), m.T0.copy()
+    for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
+                   (dcp.T_SOLUTION, T0)):
+        ctx.set_state(fld, v)
+    out = {}
+    ctx.feec_assemble_nse_system()
+    out["rhs"] = ctx.get_state(dcp.NSE_RHS)
+    ctx.feec_build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    out["T_rhs"] = ctx.get_state(dcp.T_RHS)
+    out["nse"] = ctx.feec_solve_nse()
+    out["x"] = ctx.get_state(dcp.NSE_SOLUTION)
+    out["T"] = ctx.solve_temperature()
+    out["Tx"] = ctx.get_state(dcp.T_SOLUTION)
+    out["vmax"] = ctx.max_velocity()
+    out["cfl"] = ctx.cfl_number()
+    return out
+
+
+def _check_feec4(g, outs):
+    """outs: one result per rank (owned entries filled, the rest zero)."""
+    def merged(key):
+        v = np.zeros_like(outs[0][key])
+        for r in outs:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        return v
+    rc, it, rcT, itT = (int(v) for v in g["iters"])
+    assert rel(merged("rhs"), g["nse_rhs"]) < 1e-12
+    assert rel(merged("T_rhs"), g["T_rhs"]) < 1e-12
+    for r in outs:
+        assert r["nse"] == (rc, it)
+        assert abs(r["T"][1] - itT) <= 1
+        # max velocity / CFL of the new solution (FEEC.tpp velocity stats)
+        assert np.isclose(r["vmax"], g["velocity_stats"][0], rtol=1e-6)
+        assert np.isclose(r["cfl"], g["velocity_stats"][1], rtol=1e-6)
+    # the FEEC chain swallows its inner NoConvergence (Q25), a rounding-sensitive
+    # map: iterates at 1e-6 (tests/test_feec.py::test_oracle_solve_rounding_sensitivity)
+    x = merged("x")
+    assert np.linalg.norm(x - g["nse_solution"]) <= 1e-6 * np.linalg.norm(g["nse_solution"])
+    # the temperature step reads the previous (zero) velocity (Q5): not affected
+    assert rel(merged("Tx"), g["T_solution"]) < 1e-10
+
+
+@pytest.mark.gpu
+def test_gpu_feec_config4_r4_matches_oracle_fixture():
+    """BASELINE config 4 (aqua_planet_shell_test_3d-feec.prm, refine 4) on one
+    GPU: one full FEEC time step against the oracle fixture."""
+    rp, ph, m, g = _feec4_setup()
+    ctx = dcp.Context()
+    out = _feec4_step(ctx, rp, ph, m)
+    ctx.close()
+    _check_feec4(g, [out])
+
+
+@pytest.mark.gpu
+def test_gpu_feec_config4_r4_two_ranks_matches_oracle_fixture():
+    """Config 4 as BASELINE asks: 2 ranks (in-process group on one GPU: the
+    partition, ghost layers, halo plans and all-reduced partials of the RCCL
+    path with host-barrier collectives) against the same fixture."""
+    import threading
+    rp, ph, m, g = _feec4_setup()
+    grp = dcp.Group(2)
+    outs, errors = [None, None], []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=2, group=grp)
+            outs[rank] = _feec4_step(ctx, rp, ph, m)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    grp.close()
+    assert not errors, errors
+    _check_feec4(g, outs)
+
+
+def test_feec4_fixture_shape():
+    """CPU: the fixture belongs to this host mesh (sizes) and its step converged."""
+    rp, ph, m, g = _feec4_setup()
+    f = m.feec
+    assert list(g["n"]) == [f.n_cells, f.n_w, f.n_u, f.n_p, m.n_T]
+    assert g["iters"][0] == 0 and g["iters"][1] > 0
