@@ -1,10 +1,13 @@
 // dcp_aquaplanet -p <file.prm> [--refine R] [--max-steps N] [--device D]
+//                [--output DIR [--output-stem NAME]]
 //
 // The reference executable (source/main.cxx: parse -p, construct the model
 // from the parameter file, run()) over libdcp.so: CoreModelData::Parameters
 // from the same .prm (dcp_prm_load), the refined shell / cube with its DoFs
 // and constraints (setup_dofs, dcp_host_mesh_create), the initial temperature,
 // then the time loop (dcp_run) with the reference's per-step log lines.
+// --output: output_results (boussinesq_model.tpp:1566-1680) before the loop
+// and after every step, DIR/NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu (classic).
 // Single GPU; the multi-GPU path is driven through the same ABI by one process
 // per GPU (bench.py).
 #include <cstdio>
@@ -22,7 +25,31 @@ int fail(const char* what, dcp_ctx* ctx) {
   return 1;
 }
 
-int print_step(void*, const dcp_run_report* r) {
+struct Output {
+  dcp_ctx* ctx = nullptr;
+  const dcp_host_mesh_view* view = nullptr;
+  std::string dir, stem;
+  int index = 0;
+  size_t n_nse = 0;
+};
+
+// output_results: the joint solution of this step as VTU + the pvtu record
+int write_output(Output& o) {
+  std::vector<double> u(o.n_nse), T(size_t(o.view->n_T));
+  int rc = dcp_state_get(o.ctx, DCP_NSE_SOLUTION, u.data(), u.size());
+  if (rc == DCP_OK) rc = dcp_state_get(o.ctx, DCP_T_SOLUTION, T.data(), T.size());
+  char idx[16];
+  std::snprintf(idx, sizeof(idx), "%05d", o.index++);
+  const std::string piece = o.stem + "-" + idx + ".0000.vtu";
+  if (rc == DCP_OK) rc = dcp_write_vtu(o.view, u.data(), T.data(), 0, (o.dir + "/" + piece).c_str());
+  const char* pieces[1] = {piece.c_str()};
+  if (rc == DCP_OK)
+    rc = dcp_write_pvtu_record((o.dir + "/" + o.stem + "-" + idx + ".pvtu").c_str(), 1, pieces);
+  if (rc != DCP_OK) std::fprintf(stderr, "Error: writing %s/%s\n", o.dir.c_str(), piece.c_str());
+  return rc;
+}
+
+int print_step(void* user, const dcp_run_report* r) {
   std::printf("----------------------------------------\n");
   std::printf("Time step %d:  t=%g -> t=%g  (dt=%g)\n", r->timestep_number, r->time_index,
               r->time_index + r->time_step, r->time_step);
@@ -33,13 +60,15 @@ int print_step(void*, const dcp_run_report* r) {
   else
     std::printf("   Solved (GMRES): %d\n", r->fgmres_outer);
   std::printf("   Temperature: %d CG iterations, range %g %g\n", r->T_cg, r->T_min, r->T_max);
+  Output* o = static_cast<Output*>(user);
+  if (o && write_output(*o) != DCP_OK) return 1;  // stop the run
   return 0;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string prm;
+  std::string prm, out_dir, out_stem = "boussinesq";
   int refine = -1, max_steps = 0, device = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -51,6 +80,10 @@ int main(int argc, char** argv) {
       max_steps = std::atoi(argv[++i]);
     } else if (a == "--device" && i + 1 < argc) {
       device = std::atoi(argv[++i]);
+    } else if (a == "--output" && i + 1 < argc) {
+      out_dir = argv[++i];
+    } else if (a == "--output-stem" && i + 1 < argc) {
+      out_stem = argv[++i];
     } else {
       std::fprintf(stderr, "Unknown command line option: %s\n", a.c_str());
       return 1;
@@ -105,8 +138,23 @@ int main(int argc, char** argv) {
     if ((rc = dcp_state_set(ctx, f, u.data(), u.size())) != DCP_OK) return fail("state", ctx);
   for (int f : {DCP_T_SOLUTION, DCP_OLD_T_SOLUTION})
     if ((rc = dcp_state_set(ctx, f, T.data(), T.size())) != DCP_OK) return fail("state", ctx);
+  Output out;
+  Output* outp = nullptr;
+  if (!out_dir.empty()) {
+    if (feec) {
+      std::fprintf(stderr, "Error: --output writes the classic model's fields only\n");
+      return 1;
+    }
+    out.ctx = ctx;
+    out.view = &v;
+    out.dir = out_dir;
+    out.stem = out_stem;
+    out.n_nse = n_nse;
+    outp = &out;
+    if (write_output(out) != DCP_OK) return fail("output", ctx);  // before the loop (:1840)
+  }
   dcp_run_report rep{};
-  rc = dcp_run(ctx, &rp, max_steps, print_step, nullptr, &rep);
+  rc = dcp_run(ctx, &rp, max_steps, print_step, outp, &rep);
   if (rc < 0) return fail("run", ctx);
   dcp_timings t{};
   dcp_get_timings(ctx, &t);

@@ -49,6 +49,7 @@ EXPORTED = [
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
     "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
+    "dcp_write_vtu", "dcp_write_pvtu_record",
 ]
 
 
@@ -209,6 +210,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_group_destroy.restype = None
     lib.dcp_partition_info.argtypes = [I, P, P, P, P, I, I, I, C.POINTER(Constraints),
                                        C.POINTER(Constraints), I, I, P, P, P, P, P, P]
+    lib.dcp_write_vtu.argtypes = [C.POINTER(MeshView), P, P, I, C.c_char_p]
+    lib.dcp_write_pvtu_record.argtypes = [C.c_char_p, I, C.POINTER(C.c_char_p)]
     return lib
 
 
@@ -302,6 +305,22 @@ class HostMesh:
         self.refine = refine
         self.temperature_degree = temperature_degree
         self.mapping_q_on_all_cells = bool(mapping_q_on_all_cells)
+
+    def write_vtu(self, path, nse_solution, T_solution, partition=0):
+        """output_results' DataOut::write_vtu of the joint [u p T] solution
+        (dcp_write_vtu; host-only, classic Q2/Q1 mesh)."""
+        v = MeshView()
+        v.n_cells, v.n_u, v.n_p, v.n_T = self.n_cells, self.n_u, self.n_p, self.n_T
+        v.cell_nse_dofs = self.cell_nse_dofs.ctypes.data_as(C.POINTER(C.c_int32))
+        v.cell_T_dofs = self.cell_T_dofs.ctypes.data_as(C.POINTER(C.c_int32))
+        v.cell_geometry = self.cell_geometry.ctypes.data_as(C.POINTER(C.c_double))
+        u = np.ascontiguousarray(nse_solution, dtype=np.float64)
+        T = np.ascontiguousarray(T_solution, dtype=np.float64)
+        if u.size != self.n_u + self.n_p or T.size != self.n_T:
+            raise ValueError("solution sizes do not match the mesh")
+        rc = lib().dcp_write_vtu(C.byref(v), _ptr(u), _ptr(T), int(partition), str(path).encode())
+        if rc != DCP_OK:
+            raise DcpError(rc, "dcp_write_vtu failed for " + str(path))
 
     def check(self, nse_constraints=None, T_constraints=None):
         """Host-only validation of the device upload; returns the number of

@@ -349,6 +349,17 @@ int dcp_host_feec_view_get(dcp_host_mesh* m, dcp_feec_mesh* out);
 /* T dof values of the initial temperature at the support points. */
 int dcp_host_mesh_initial_temperature(const dcp_host_mesh* m, double* T);
 
+/* output_results (boussinesq_model.tpp:1566-1680), classic model, host-only:
+ * DataOut::build_patches(nse_velocity_degree = 2) of the joint [u p T] solution
+ * -- per cell the 27 lattice points of {0, 1/2, 1}^3 under DataOut's default
+ * MappingQ1 and 8 sub-hexahedra -- with the Postprocessor's point data
+ * "velocity", "p", "T", "partition" (:1492-1554), written as a VTU file
+ * (XML, ASCII data arrays). nse: n_u + n_p global values, T: n_T. */
+int dcp_write_vtu(const dcp_host_mesh_view* mesh, const double* nse, const double* T,
+                  int partition, const char* vtu_path);
+/* write_pvtu_record: the .pvtu naming the n_pieces per-rank .vtu files. */
+int dcp_write_pvtu_record(const char* pvtu_path, int n_pieces, const char* const* piece_files);
+
 /* .prm -> dcp_physics (+ refinement etc.), CoreModelData::Parameters(file). */
 typedef struct {
   dcp_physics physics;

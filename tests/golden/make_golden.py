@@ -16,12 +16,18 @@ Cases (classic shell physics, data/aqua_planet_shell_test_3d-classic.prm):
                      from the physical state (about 15 min of oracle time: ~29,000
                      inner Schur GMRES iterations): iteration counts, the NSE and
                      temperature solutions, the assembled rhs.
+  shell_r4_step.npz  BASELINE config 3 (classic prm, refine 4: 24,576 cells, 634,600
+                     NSE dofs): one full time step. On the reference geometry the
+                     reference's inner Schur GMRES stagnates at its 5000-iteration
+                     cap in both FGMRES attempts (NoConvergence): the
+                     fixture holds the assembled rhs, the iteration counts of that
+                     failure and the temperature step.
   feec_r4_step.npz   BASELINE config 4: data/aqua_planet_shell_test_3d-feec.prm at
                      refine 4 (24,576 cells; Nedelec/RT/DGQ0 + Q1 temperature),
                      one full FEEC time step from u = 0 and the initial temperature:
                      assembled rhs, GMRES(100) iterations and solution, temperature
                      solution (FeecModel, boussineq_model_FEEC.tpp:2238-2300).
-usage: python tests/golden/make_golden.py [r1|r3|feec4]
+usage: python tests/golden/make_golden.py [r1|r3|r4|feec4]
 """
 import os
 import sys
@@ -126,6 +132,9 @@ if __name__ == "__main__":
     elif which == "feec4":
         np.savez_compressed(os.path.join(HERE, "feec_r4_step.npz"), **make_feec_step(4))
         print("wrote", os.path.join(HERE, "feec_r4_step.npz"))
+    elif which == "r4":
+        np.savez_compressed(os.path.join(HERE, "shell_r4_step.npz"), **make_step(4))
+        print("wrote", os.path.join(HERE, "shell_r4_step.npz"))
     elif which == "r3":
         np.savez_compressed(os.path.join(HERE, "shell_r3_step.npz"), **make_step(3))
         print("wrote", os.path.join(HERE, "shell_r3_step.npz"))

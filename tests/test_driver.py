@@ -91,3 +91,20 @@ def test_executable_requires_a_parameter_file():
     exe = os.path.join(ROOT, "3d-dycoreplanet_amd", "dcp_aquaplanet")
     out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert out.returncode == 1 and "-p" in out.stderr
+
+
+@pytest.mark.gpu
+def test_executable_writes_vtu_output(tmp_path):
+    """--output: output_results before the loop and after each step
+    (boussinesq_model.tpp:1840/1907), NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu."""
+    exe = os.path.join(ROOT, "3d-dycoreplanet_amd", "dcp_aquaplanet")
+    out = subprocess.run([exe, "-p", PRM, "--refine", "1", "--output", str(tmp_path),
+                          "--output-stem", "aqua"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    names = sorted(p.name for p in tmp_path.iterdir())
+    assert names == ["aqua-00000.0000.vtu", "aqua-00000.pvtu",
+                     "aqua-00001.0000.vtu", "aqua-00001.pvtu"]
+    text = (tmp_path / "aqua-00001.0000.vtu").read_text()
+    n_cells = dcp.HostMesh(refine=1).n_cells
+    assert 'NumberOfCells="%d"' % (8 * n_cells) in text  # 8 hexahedra per cell
+    assert 'Source="aqua-00001.0000.vtu"' in (tmp_path / "aqua-00001.pvtu").read_text()
