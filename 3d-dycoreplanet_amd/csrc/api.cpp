@@ -1063,6 +1063,12 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->feec_zero_mean = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_FEEC_FIXED_INNER) {
+      require(value >= 0 && value <= 100, DCP_ERR_INVALID,
+              "DCP_OPT_FEEC_FIXED_INNER must be in [0, 100]");
+      ctx->feec_fixed_inner = value;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_GRAM_SCHMIDT) {
       require(value == 0 || value == 1, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0 or 1");
       ctx->gram_schmidt = value;

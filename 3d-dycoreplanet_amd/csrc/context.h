@@ -235,6 +235,7 @@ struct Ctx {
   // ---- FEEC variant (config 4): n_u = n_w + n_u(faces), n_p = cells
   bool feec = false;
   bool feec_zero_mean = true;          // parameters.correct_pressure_to_zero_mean
+  int feec_fixed_inner = 0;            // DCP_OPT_FEEC_FIXED_INNER (test hook)
   int fe_nw = 0, fe_nu = 0, fe_np = 0;             // local (owned + ghost)
   int fe_nwo = 0, fe_nuo = 0, fe_npo = 0;          // owned
   int fe_nw_g = 0, fe_nu_g = 0;                    // global

@@ -484,7 +484,17 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #else
   const double* SR = S;
 #endif
-  const int yb = pa + 9 * pb;  // y-pencil (a = pa, c = pb): idx = yb + 3b
+  // Slot layout of node / point (a, b, c): 3a + b + 9c (DCP_MF_SWAP_AB, default)
+  // or lexicographic a + 3b + 9c. With 7 cells of 9 lanes per wave the swapped
+  // form makes the y-pencil accesses (15 of the 30 per batch) conflict-free and
+  // leaves x and z at 2-way, against 2-way y and z for the lexicographic one.
+#ifndef DCP_MF_SWAP_AB
+#define DCP_MF_SWAP_AB 1
+#endif
+  constexpr int xs = DCP_MF_SWAP_AB ? 3 : 1, ys = DCP_MF_SWAP_AB ? 1 : 3;
+  const int xo = DCP_MF_SWAP_AB ? pa + 9 * pb : 3 * p;       // x-pencil (b, c) = (pa, pb)
+  const int yo = DCP_MF_SWAP_AB ? 3 * pa + 9 * pb : pa + 9 * pb;  // y-pencil (a, c)
+  const int zo = DCP_MF_SWAP_AB ? 3 * pa + pb : p;            // z-pencil (a, b)
   const double wab = sel3(pa, kGaussW[0], kGaussW[1], kGaussW[2]) *
                      sel3(pb, kGaussW[0], kGaussW[1], kGaussW[2]);
 
@@ -584,8 +594,8 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     fwd(kTD, in, g);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      S[c * kFS + 3 * p + q] = v[q];
-      S[(3 + c) * kFS + 3 * p + q] = g[q];
+      S[c * kFS + xo + xs * q] = v[q];
+      S[(3 + c) * kFS + xo + xs * q] = g[q];
     }
   }
   wsync();
@@ -596,8 +606,8 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       double v[3], g[3];
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
-        v[b] = SR[c * kFS + yb + 3 * b];
-        g[b] = SR[(3 + c) * kFS + yb + 3 * b];
+        v[b] = SR[c * kFS + yo + ys * b];
+        g[b] = SR[(3 + c) * kFS + yo + ys * b];
       }
       fwd(kTL, v, A[c]);
       fwd(kTD, v, B[c]);
@@ -608,9 +618,9 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     for (int c = 0; c < 3; ++c)
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        S[c * kFS + yb + 3 * q] = A[c][q];
-        S[(3 + c) * kFS + yb + 3 * q] = B[c][q];
-        S[(6 + c) * kFS + yb + 3 * q] = C[c][q];
+        S[c * kFS + yo + ys * q] = A[c][q];
+        S[(3 + c) * kFS + yo + ys * q] = B[c][q];
+        S[(6 + c) * kFS + yo + ys * q] = C[c][q];
       }
   }
   wsync();
@@ -648,9 +658,9 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       double A[3], B[3], C[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        A[k] = SR[c * kFS + p + 9 * k];
-        B[k] = SR[(3 + c) * kFS + p + 9 * k];
-        C[k] = SR[(6 + c) * kFS + p + 9 * k];
+        A[k] = SR[c * kFS + zo + 9 * k];
+        B[k] = SR[(3 + c) * kFS + zo + 9 * k];
+        C[k] = SR[(6 + c) * kFS + zo + 9 * k];
       }
       u[c] = kTL.v[0][q] * A[0] + kTL.v[1][q] * A[1] + kTL.v[2][q] * A[2];
       Gh[c][0] = kTL.v[0][q] * C[0] + kTL.v[1][q] * C[1] + kTL.v[2][q] * C[2];
@@ -711,9 +721,9 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
   for (int c = 0; c < 3; ++c)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      S[c * kFS + p + 9 * k] = V[c][k];
-      S[(3 + c) * kFS + p + 9 * k] = FX[c][k];
-      S[(6 + c) * kFS + p + 9 * k] = FY[c][k];
+      S[c * kFS + zo + 9 * k] = V[c][k];
+      S[(3 + c) * kFS + zo + 9 * k] = FX[c][k];
+      S[(6 + c) * kFS + zo + 9 * k] = FY[c][k];
     }
   if (STOKES) {
     SP[p] = slo;
@@ -730,9 +740,9 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       double v[3], fx[3], fy[3], t[3];
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
-        v[b] = SR[c * kFS + yb + 3 * b];
-        fx[b] = SR[(3 + c) * kFS + yb + 3 * b];
-        fy[b] = SR[(6 + c) * kFS + yb + 3 * b];
+        v[b] = SR[c * kFS + yo + ys * b];
+        fx[b] = SR[(3 + c) * kFS + yo + ys * b];
+        fy[b] = SR[(6 + c) * kFS + yo + ys * b];
       }
       bwd(kTL, v, V1[c]);
       bwd(kTD, fy, t);
@@ -757,8 +767,8 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     for (int c = 0; c < 3; ++c)
 #pragma unroll
       for (int n = 0; n < 3; ++n) {
-        S[c * kFS + yb + 3 * n] = V1[c][n];
-        S[(3 + c) * kFS + yb + 3 * n] = FX1[c][n];
+        S[c * kFS + yo + ys * n] = V1[c][n];
+        S[(3 + c) * kFS + yo + ys * n] = FX1[c][n];
       }
   }
   wsync();
@@ -770,8 +780,8 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     double v[3], fx[3], t0[3], t1[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      v[q] = SR[c * kFS + 3 * p + q];
-      fx[q] = SR[(3 + c) * kFS + 3 * p + q];
+      v[q] = SR[c * kFS + xo + xs * q];
+      fx[q] = SR[(3 + c) * kFS + xo + xs * q];
     }
     bwd(kTL, v, t0);
     bwd(kTD, fx, t1);

@@ -1149,7 +1149,8 @@ void feec_precondition(Ctx& c, const FeecOps& o, const double* src, double* dst)
     // preconditioner Mu Jacobi, failure swallowed; initial guess = dst_u
     // (shifted_schur_complement.hpp:271-298)
     const double nrm = std::sqrt(dot_host(c, c.seg_fu(), t1, t1, kSlotB));
-    Control ctl{30, 1e-6 * nrm};
+    const int k = c.feec_fixed_inner;
+    Control ctl = k > 0 ? Control{unsigned(std::min(k, 30)), 0.0} : Control{30, 1e-6 * nrm};
     Op A = [&](const double* x, double* y) { o.shifted(x, y); };
     Op P = [&](const double* x, double* y) { mul(nu, c.fe_dinv.p + nw, x, y, c.stream); };
     (void)gmres(c, nu, c.seg_fu(), A, &P, dst + ou, t1, ctl, c.fe_s, 30);
@@ -1162,7 +1163,8 @@ void feec_precondition(Ctx& c, const FeecOps& o, const double* src, double* dst)
     // GMRES <= 100 iterations, tol 1e-6 |src|, identity, failure swallowed
     // (nested_schur_complement.hpp:287-322)
     const double nrm = std::sqrt(dot_host(c, c.seg_fp(), t2, t2, kSlotB));
-    Control ctl{100, 1e-6 * nrm};
+    const int k = c.feec_fixed_inner;
+    Control ctl = k > 0 ? Control{unsigned(k), 0.0} : Control{100, 1e-6 * nrm};
     Op A = [&](const double* x, double* y) { o.lower(x, y); };
     (void)gmres(c, np, c.seg_fp(), A, nullptr, dst + op, t2, ctl, c.fe_n, 30);
   }

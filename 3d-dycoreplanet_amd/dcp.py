@@ -32,6 +32,7 @@ OPT_FUSED_CHAIN = 4
 OPT_FGMRES_MAX_OUTER = 5
 OPT_ASSEMBLE_VELOCITY_BLOCK = 6
 OPT_GRAM_SCHMIDT = 7
+OPT_FEEC_FIXED_INNER = 8
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -575,6 +576,11 @@ class Context:
 
     def set_feec_zero_mean(self, on: bool):
         self._check(lib().dcp_set_option(self._h, OPT_FEEC_ZERO_MEAN, int(bool(on))))
+
+    def set_feec_fixed_inner(self, k: int):
+        """DCP_OPT_FEEC_FIXED_INNER (test hook): both inner GMRES of the FEEC
+        preconditioner run exactly k steps (0 = the reference's rule)."""
+        self._check(lib().dcp_set_option(self._h, OPT_FEEC_FIXED_INNER, int(k)))
 
     def feec_assemble_nse_system(self):
         self._check(lib().dcp_feec_assemble_nse_system(self._h))

@@ -312,6 +312,12 @@ int dcp_feec_build_nse_preconditioner(dcp_ctx* ctx);
 int dcp_feec_solve_nse(dcp_ctx* ctx, int* iterations);
 /* DCP_OPT_FEEC_ZERO_MEAN (default 1): parameters.correct_pressure_to_zero_mean */
 enum { DCP_OPT_FEEC_ZERO_MEAN = 2 };
+/* DCP_OPT_FEEC_FIXED_INNER (test hook, default 0 = the reference's rule): k > 0
+ *   runs both inner GMRES of BlockSchurPreconditionerFEEC for exactly k steps
+ *   (tolerance 0, the NoConvergence swallowed as the reference does), so the
+ *   preconditioner is a smooth map of its input with no early-stop decisions
+ *   for rounding to flip; the oracle has the same switch. */
+enum { DCP_OPT_FEEC_FIXED_INNER = 8 };
 /* element matrices / rhs of cells [first, first+n): K [n][19][19], f [n][19] */
 int dcp_feec_cell_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 /* which = 0: nse_matrix, 1: nse_preconditioner_matrix (CSR, n_w+n_u+n_p rows) */

@@ -1540,6 +1540,7 @@ struct orc_feec {
   Csr nse, pre, Tmass, Tstiff, Tmat;
   std::vector<double> rhs, T_rhs, T_inv;
   bool zero_mean = true;
+  int fixed_inner = 0;  // test hook: both inner GMRES run exactly this many steps
 };
 
 extern "C" orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const int* cell_dofs19,
@@ -1605,6 +1606,7 @@ extern "C" orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const i
 
 extern "C" void orc_feec_destroy(orc_feec* m) { delete m; }
 extern "C" void orc_feec_set_zero_mean(orc_feec* m, int on) { m->zero_mean = on != 0; }
+extern "C" void orc_feec_set_fixed_inner(orc_feec* m, int k) { m->fixed_inner = k; }
 
 extern "C" void orc_feec_assemble_nse_system(orc_feec* m, const double* old_nse, const double* old_T) {
   m->nse.zero();
@@ -1757,7 +1759,8 @@ extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
     for (int i = 0; i < nu; ++i) t1[i] = -1.0 * t1[i] + src[ou + i];
     {
       // ApproxShiftedSchurComplementInverse (shifted_schur_complement.hpp:271-298)
-      Control ctl{30, 1e-6 * norm2(t1, 0, nu)};
+      const int k = m->fixed_inner;
+      Control ctl = k > 0 ? Control{unsigned(std::min(k, 30)), 0.0} : Control{30, 1e-6 * norm2(t1, 0, nu)};
       int it = 0;
       try {
         gmres(nu, shifted, mu_jacobi, dst + ou, t1.data(), ctl, it);
@@ -1768,7 +1771,8 @@ extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
     csr_block(A, op, n, ou, op, dst + ou, t2.data(), true);
     {
       // ApproxNestedSchurComplementInverse (nested_schur_complement.hpp:287-322)
-      Control ctl{100, 1e-6 * norm2(t2, 0, np)};
+      const int k = m->fixed_inner;
+      Control ctl = k > 0 ? Control{unsigned(k), 0.0} : Control{100, 1e-6 * norm2(t2, 0, np)};
       int it = 0;
       try {
         gmres(np, lower, identity, dst + op, t2.data(), ctl, it);

@@ -136,6 +136,8 @@ orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const int* cell_do
                           const double* diameter);
 void orc_feec_destroy(orc_feec* m);
 void orc_feec_set_zero_mean(orc_feec* m, int on);
+/* test hook: both inner GMRES of the FEEC preconditioner run exactly k steps */
+void orc_feec_set_fixed_inner(orc_feec* m, int k);
 void orc_feec_assemble_nse_system(orc_feec* m, const double* old_nse, const double* old_T);
 void orc_feec_assemble_preconditioner(orc_feec* m);
 long orc_feec_matrix_nnz(const orc_feec* m, int which);

@@ -81,6 +81,7 @@ def lib():
         L.orc_feec_create.restype = P
         L.orc_feec_destroy.argtypes = [P]
         L.orc_feec_set_zero_mean.argtypes = [P, I]
+        L.orc_feec_set_fixed_inner.argtypes = [P, I]
         L.orc_feec_assemble_nse_system.argtypes = [P, P, P]
         L.orc_feec_assemble_preconditioner.argtypes = [P]
         L.orc_feec_matrix_nnz.argtypes = [P, I]
@@ -324,6 +325,10 @@ class FeecModel:
         out = np.zeros(self.f.n_T)
         lib().orc_feec_T_rhs(self.h, _p(out))
         return out
+
+    def set_fixed_inner(self, k):
+        """Test hook (DCP_OPT_FEEC_FIXED_INNER): both inner GMRES run exactly k steps."""
+        lib().orc_feec_set_fixed_inner(self.h, int(k))
 
     def solve_nse(self, sol):
         x = np.array(sol, dtype=np.float64, copy=True)

@@ -142,6 +142,25 @@ def test_oracle_solve_rounding_sensitivity():
     assert it == it2 and 1e-10 < d < 1e-6
 
 
+def test_oracle_fixed_inner_count_is_not_rounding_sensitive():
+    """With both inner GMRES held at 3 steps (DCP_OPT_FEEC_FIXED_INNER) the
+    chain's Krylov least-squares problems stay well conditioned: the same
+    1e-16 perturbation moves the solution by < 1e-12 (vs ~1e-7 with the
+    reference's 30 / 100-step caps), which is what lets the GPU parity test
+    below compare iterates at 1e-10."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    f = m.feec
+    M = oracle_py.FeecModel(dcp.classic_physics(), m)
+    M.set_fixed_inner(3)
+    M.assemble_nse_system(np.zeros(f.n), m.T0)
+    rc, x, it = M.solve_nse(np.zeros(f.n))
+    x0 = np.zeros(f.n)
+    x0[f.n_w + f.n_u:] = 1e-16 * np.random.default_rng(1).uniform(-1, 1, f.n_p)
+    rc2, x2, it2 = M.solve_nse(x0)
+    assert rc == rc2 == 0 and it == it2
+    assert np.linalg.norm(x2 - x) < 1e-12 * np.linalg.norm(x)
+
+
 # ------------------------------------------------------------------ GPU parity
 
 def csr(rp, cols, vals, n):
@@ -232,3 +251,32 @@ def test_feec_time_step(feec_setup):
     vs = orc.velocity_stats(xg)
     assert np.isclose(ctx.max_velocity(), vs[0], rtol=1e-12)
     assert np.isclose(ctx.cfl_number(), vs[1], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_feec_time_step_fixed_inner(feec_setup):
+    """The same step with both inner GMRES held at 3 steps in the GPU chain
+    and the oracle (DCP_OPT_FEEC_FIXED_INNER): a smooth preconditioner, so the
+    iterates agree at 1e-10 with equal outer counts."""
+    m, ph, ctx = feec_setup
+    f = m.feec
+    x0, T0 = np.zeros(f.n), m.T0.copy()
+    for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
+                   (dcp.T_SOLUTION, T0)):
+        ctx.set_state(fld, v)
+    ctx.feec_assemble_nse_system()
+    ctx.feec_build_nse_preconditioner()
+    ctx.set_feec_fixed_inner(3)
+    try:
+        rc, it = ctx.feec_solve_nse()
+    finally:
+        ctx.set_feec_fixed_inner(0)
+    orc = oracle_py.FeecModel(ph, m)
+    orc.set_fixed_inner(3)
+    orc.assemble_nse_system(x0, T0)
+    orc.assemble_preconditioner()
+    rco, xo, ito = orc.solve_nse(x0)
+    assert rc == rco == 0
+    assert it == ito
+    xg = ctx.get_state(dcp.NSE_SOLUTION)
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
