@@ -1334,26 +1334,49 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_cpos.upload(cpos);
       c.mf_ncon = int(cdof.size());
       c.mf_geo.release();  // colour-launch mode only: computed on its first use
-      // cell-order path: constrained-node masks, per-dof incidence lists into
-      // the cell records (ascending cell order = the gather's summation order)
-      std::vector<uint32_t> cmask(n_cells, 0);
-      std::vector<int32_t> vptr(nv + 1, 0), pptr(n_p + 1, 0);
-      for (int cell = 0; cell < n_cells; ++cell) {
-        for (int t = 0; t < 27; ++t) {
-          const int n = q2[27 * size_t(cell) + t];
-          vptr[n + 1]++;
-          if (vc[n].type != 0) cmask[cell] |= 1u << t;
-        }
-        for (int v = 0; v < 8; ++v) pptr[pd[8 * size_t(cell) + v] + 1]++;
-      }
-      for (int n = 0; n < nv; ++n) vptr[n + 1] += vptr[n];
-      for (int i = 0; i < n_p; ++i) pptr[i + 1] += pptr[i];
+      // cell-order path: constrained-node masks, per-dof lists of partial sums
+      // (velocity: one per cell group touching the node, pressure: one per
+      // cell; ascending cell order = the gather's summation order)
       // chunks of the cell range; a dof is gathered after the chunk of its last cell
       if (const char* e = std::getenv("DCP_MF_CHUNKS"))
         c.mf_chunks = std::max(1, std::min(Ctx::kMfChunksMax, std::atoi(e)));
       const int K = c.mf_chunks;
       c.mf_cell_cut.assign(K + 1, 0);
       for (int k = 0; k <= K; ++k) c.mf_cell_cut[k] = int(int64_t(n_cells) * k / K);
+      // cell groups: kMfGroupCells consecutive cells from each chunk's first cell
+      std::vector<int32_t> group_first(n_cells);  // first cell of the cell's group
+      for (int k = 0; k < K; ++k)
+        for (int cell = c.mf_cell_cut[k]; cell < c.mf_cell_cut[k + 1]; ++cell)
+          group_first[cell] = cell - (cell - c.mf_cell_cut[k]) % kMfGroupCells;
+      // per (cell, t): the owner is the node's first occurrence in its group (one
+      // partial sum per group, gathered in group order); later occurrences are
+      // chained to it in (cell, t) order by their group-local index 27 (cell - first) + t
+      std::vector<uint32_t> cmask(n_cells, 0);
+      std::vector<int32_t> vptr(nv + 1, 0), pptr(n_p + 1, 0);
+      std::vector<uint8_t> vnext(27 * size_t(n_cells), 0xff);
+      std::vector<char> vowner(27 * size_t(n_cells), 0);
+      {
+        std::vector<int> prev(nv, -1), prev_group(nv, -1);
+        for (int cell = 0; cell < n_cells; ++cell) {
+          const int g = group_first[cell];
+          for (int t = 0; t < 27; ++t) {
+            const size_t occ = 27 * size_t(cell) + t;
+            const int n = q2[occ];
+            if (vc[n].type != 0) cmask[cell] |= 1u << t;
+            if (prev_group[n] == g) {
+              vnext[size_t(prev[n])] = uint8_t(27 * (cell - g) + t);
+            } else {
+              vowner[occ] = 1;
+              vptr[n + 1]++;
+              prev_group[n] = g;
+            }
+            prev[n] = int(occ);
+          }
+          for (int v = 0; v < 8; ++v) pptr[pd[8 * size_t(cell) + v] + 1]++;
+        }
+      }
+      for (int n = 0; n < nv; ++n) vptr[n + 1] += vptr[n];
+      for (int i = 0; i < n_p; ++i) pptr[i + 1] += pptr[i];
       std::vector<int> vlast(nv, 0), plast(n_p, 0);
       for (int k = 0; k < K; ++k)
         for (int cell = c.mf_cell_cut[k]; cell < c.mf_cell_cut[k + 1]; ++cell) {
@@ -1394,8 +1417,10 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         for (int n = 0; n < nv; ++n) vf[n] = vptr[vpos[n]];
         for (int i = 0; i < n_p; ++i) pf[i] = pptr[ppos[i]];
         for (int cell = 0; cell < n_cells; ++cell) {
-          for (int t = 0; t < 27; ++t)
-            vslot[27 * size_t(cell) + t] = 3 * vf[q2[27 * size_t(cell) + t]]++;
+          for (int t = 0; t < 27; ++t) {
+            const size_t occ = 27 * size_t(cell) + t;
+            vslot[occ] = vowner[occ] ? 3 * vf[q2[occ]]++ : -1;
+          }
           for (int v = 0; v < 8; ++v)
             pslot[8 * size_t(cell) + v] = pbase + pf[pd[8 * size_t(cell) + v]]++;
         }
@@ -1411,6 +1436,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_cmask.upload(cmask);
       c.mf_vptr.upload(vptr);
       c.mf_vslot.upload(vslot);
+      c.mf_vnext.upload(vnext);
       c.mf_pbase = pbase;
       c.mf_pptr.upload(pptr);
       c.mf_pslot.upload(pslot);

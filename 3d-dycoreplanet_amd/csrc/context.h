@@ -140,9 +140,10 @@ struct Ctx {
   DBuf<int32_t> mf_cdof;
   DBuf<int64_t> mf_cpos;
   int mf_ncon = 0, mf_ncon_v = 0;  // fix-up entries: all / velocity dofs only
-  DBuf<double> mf_buf;                  // dof-sorted incidence slots (89 per cell)
+  DBuf<double> mf_buf;  // dof-sorted partial sums (velocity: one per node and cell group)
   DBuf<uint32_t> mf_cmask;
   DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx, mf_vorder, mf_porder;
+  DBuf<uint8_t> mf_vnext;
   int32_t mf_pbase = 0;
   // chunked apply (DCP_MF_CHUNKS > 1 at upload): the gather of chunk k's
   // finished dofs runs on mf_stream while the pencil kernel works chunk k + 1.
@@ -159,7 +160,7 @@ struct Ctx {
   bool mf_separable = false;
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
-                   mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p,
+                   mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p, mf_vnext.p,
                    mf_pslot.p, mf_separable ? mf_col.p : nullptr,
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }

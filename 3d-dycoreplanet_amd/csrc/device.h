@@ -127,7 +127,12 @@ struct MfCells {
   const double* geo;           // [n_cells][10][27] J^-1 / JxW (non-separable meshes only)
   const NodeConstraint* vcon;  // [n_vnodes]
   const uint32_t* cmask;       // [n_cells] bit t: local node t is constrained
-  const int32_t* vslot;        // [n_cells][27] buf offset (doubles) of the (cell, t) triple
+  // Velocity records are summed per cell group (kMfGroupCells consecutive
+  // cells from the launch's first cell, one wave) before they leave the
+  // kernel: the first occurrence of a node in its group owns the group's
+  // partial sum, the later ones are chained to it in (cell, t) order.
+  const int32_t* vslot;        // [n_cells][27] buf offset (doubles) of the owner's partial, or -1
+  const uint8_t* vnext;        // [n_cells][27] next occurrence in the group (27 * cell + t), or 0xff
   const int32_t* pslot;        // [n_cells][8]  buf offset of the (cell, v) pressure value
   // Radially separable geometry (null if the mesh is not): X(a,b,c) = r_c phi_ab
   // in every cell, so J^-1 / JxW at a Gauss point follow from a per-column 2D
@@ -152,6 +157,8 @@ struct MfGather {
   const int32_t* pcidx;        // [n_p] identified pressure dof index or -1 (null: none)
   const double* pcdiag;        // their assembled diagonal
 };
+// cells per wave of k_mf_pencil = the cell group of the velocity partial sums
+constexpr int kMfGroupCells = 7;
 // cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
               double* buf, hipStream_t s);

@@ -390,18 +390,25 @@ __global__ __launch_bounds__(32 * kMfCells) void k_mf_stokes(MfData md, int base
 // contraction of the sum factorisation runs in registers with compile-time
 // coefficients; the LDS only transposes between the x-, y- and z-pencil
 // layouts (x-pencil p = b + 3c, y-pencil p = a + 3c, z-pencil p = a + 3b over
-// lexicographic (a, b, c)). The geometry (J^-1, JxW at the 27 Gauss points)
-// is recomputed from the Q2 node coordinates the same way (MappingQ2 = the
-// assembly kernel's map), so the only per-cell HBM streams are the node map
-// and the 89 results; node coordinates and src are gathered and shared by the
-// neighbouring cells through the caches (cells in tree order).
-constexpr int kPenCells = 7;
+// lexicographic (a, b, c)). The MappingQ(3) geometry (J^-1, JxW at the 27
+// Gauss points) comes from the radially separable tables (a per-column 2D
+// table and per-layer radii, L2-resident) or, for other meshes, the streamed
+// per-cell table of k_mf_geometry. The seven cells of a wave are consecutive in
+// tree order and share nodes: their velocity results are summed per node in
+// LDS (one partial per node and wave, chained occurrences, host-built) before
+// the store, 35 % fewer records than one per (cell, node) at r=5; src is
+// gathered through the caches.
+#ifndef DCP_MF_CELLS
+#define DCP_MF_CELLS 7
+#endif
+constexpr int kPenCells = DCP_MF_CELLS;  // cells per wave
+static_assert(kPenCells == kMfGroupCells, "the host groups the velocity partial sums per wave");
 #ifndef DCP_MF_WAVES
 #define DCP_MF_WAVES 1
 #endif
 constexpr int kPenWaves = DCP_MF_WAVES;  // waves per workgroup
 #ifndef DCP_MF_SLOTS
-#define DCP_MF_SLOTS 7
+#define DCP_MF_SLOTS DCP_MF_CELLS
 #endif
 // LDS cell slots per wave: 7 (lane 63, the dummy cell, stores nothing) or 8
 constexpr int kPenSlots = DCP_MF_SLOTS;
@@ -455,16 +462,18 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
                                                              double* __restrict__ buf) {
   __shared__ double lds[kPenWaves][kPenFields];
   __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
+  __shared__ uint8_t nxt[kPenWaves][kPenSlots * 27];  // chain links of the group partial sums
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // lane 63 shadows lane 54 (slot 6, pencil 0) with 7 LDS slots: it computes
   // and stores the same LDS values and skips the global store; with 8 slots it
   // works a dummy slot of its own
-  const bool dummy = lane == 63;
+  // (with 6 cells per wave, lanes 54..62 shadow lanes 45..53 the same way)
+  const bool dummy = lane >= 9 * kPenCells;
 #ifndef DCP_MF_SHADOW
-#define DCP_MF_SHADOW (kPenSlots == 7)
+#define DCP_MF_SHADOW (kPenSlots == kPenCells)
 #endif
-  const int cs = DCP_MF_SHADOW && dummy ? 6 : lane / 9;
-  const int p = DCP_MF_SHADOW && dummy ? 0 : lane - 9 * cs;
+  const int cs = DCP_MF_SHADOW && dummy ? kPenCells - 1 : lane / 9;
+  const int p = DCP_MF_SHADOW && dummy ? (lane - 9 * (lane / 9)) % 9 : lane - 9 * cs;
   const int pa = p % 3, pb = p / 3;
 #ifndef DCP_MF_XCD
 #define DCP_MF_XCD 1
@@ -505,7 +514,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     return c0 + ((blk * kMfBatches + j) * kPenWaves + wave) * kPenCells + cs;
   };
   struct Ids {
-    int nd[3], slot[3];
+    int nd[3], slot[3], next[3];
     int pdof, pslot;
     uint32_t mask;
   };
@@ -520,6 +529,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
     for (int a = 0; a < 3; ++a) {
       I.nd[a] = mc.cell_q2[27 * e + 3 * p + a];
       I.slot[a] = mc.vslot[27 * e + 3 * p + a];
+      I.next[a] = mc.vnext[27 * e + 3 * p + a];
     }
     I.mask = mc.cmask[e];
     I.pdof = (STOKES && p < 8) ? mc.cell_p[8 * e + p] : 0;
@@ -682,6 +692,20 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       for (int i = 0; i < 9; ++i) ji[i] = Ji[q][i];
       wq = w[q];
     }
+#ifndef DCP_MF_NOZMATH
+#define DCP_MF_NOZMATH 0
+#endif
+    if (DCP_MF_NOZMATH) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          V[c][k] += u[c] * wq;
+          FX[c][k] += Gh[c][0];
+          FY[c][k] += Gh[c][1] + Gh[c][2] * ji[k];
+        }
+      continue;
+    }
     double G[3][3];
 #pragma unroll
     for (int c = 0; c < 3; ++c)
@@ -788,12 +812,43 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
     for (int n = 0; n < 3; ++n) y[n][c] = t0[n] + t1[n];
   }
-  if (live) {
+  // (timing probes only, wrong results: DCP_MF_NOSTORE skips the cell
+  // records, DCP_MF_NOZMATH the per-point flux of the z-pencil)
+#ifndef DCP_MF_NOSTORE
+#define DCP_MF_NOSTORE 0
+#endif
+  // group partial sums: every occurrence parks its triple (fields 0-2) and its
+  // chain link; the owner (first occurrence of the node in the group) adds the
+  // chained ones in (cell, t) order and stores one triple per node and group
+  wsync();  // every lane has read its back-x inputs
+#pragma unroll
+  for (int n = 0; n < 3; ++n) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) S[c * kFS + xo + xs * n] = y[n][c];
+    nxt[wave][27 * cs + 3 * p + n] = uint8_t(Ic.next[n]);
+  }
+  wsync();
+  if (live && !DCP_MF_NOSTORE) {
+    const double* Sw = lds[wave];
 #pragma unroll
     for (int n = 0; n < 3; ++n) {
+      if (Ic.slot[n] < 0) continue;
+      double s0 = y[n][0], s1 = y[n][1], s2 = y[n][2];
+      // links point forward inside the group (at most kPenCells - 1 hops)
+      int k = Ic.next[n];
+      for (int hop = 0; k != 0xff && hop < kPenCells; ++hop, k = nxt[wave][k]) {
+        const int ck = k / 27, tk = k - 27 * ck;
+        const int ak = tk % 3, bk = (tk / 3) % 3, zk = tk / 9;
+        const int idx = (DCP_MF_FIELD_MAJOR ? 27 : 243) * ck +
+                        (DCP_MF_SWAP_AB ? 3 * ak + bk + 9 * zk : tk);
+        s0 += Sw[idx];
+        s1 += Sw[kFS + idx];
+        s2 += Sw[2 * kFS + idx];
+      }
       double* out = buf + Ic.slot[n];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) out[c] = y[n][c];
+      out[0] = s0;
+      out[1] = s1;
+      out[2] = s2;
     }
     if (STOKES && p < 8) buf[Ic.pslot] = yp;
   }
