@@ -144,6 +144,61 @@ def test_gpu_time_step_r3_matches_oracle_fixture():
     ctx.close()
 
 
+GOLD4 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shell_r4_step.npz")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", ["modified", "classical2"])
+def test_gpu_config3_r4_matches_oracle_fixture(gs):
+    """BASELINE config 3 (classic prm at refine 4: 24,576 cells, 634,600 NSE
+    dofs) from the physical state against the oracle's full time step
+    (tests/golden/make_golden.py r4, 40 min of oracle time). On this geometry
+    the reference's inner Schur GMRES stagnates: both FGMRES attempts stop in
+    their first preconditioner application at the 5,000-step cap, so the
+    solve fails (NoConvergence) with 0 outer and 10,000 inner iterations and
+    the NSE solution keeps its initial value; the temperature step then runs on
+    that state. Checked: rhs at 1e-12, the failure and its counts exactly, the
+    untouched solution, the temperature at 1e-10."""
+    with np.load(GOLD4) as d:
+        g = {k: d[k] for k in d.files}
+    m = dcp.HostMesh(refine=4)
+    assert list(g["n"]) == [m.n_cells, m.n_u, m.n_p, m.n_T]
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.classic_physics())
+    ctx.upload_mesh(m)
+    ctx.set_gram_schmidt(gs)
+    u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    assert rel(ctx.get_state(dcp.NSE_RHS), g["nse_rhs"]) < 1e-12
+    ctx.build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    assert rel(ctx.get_state(dcp.T_RHS), g["T_rhs"]) < 1e-12
+    rc, outer, inner = ctx.solve_nse()
+    it = g["iters"]
+    assert it[0] == 1 and rc == dcp.DCP_NOT_CONVERGED
+    assert (outer, inner) == (it[1], it[2]) == (0, 10000)
+    assert np.array_equal(ctx.get_state(dcp.NSE_SOLUTION), g["nse_solution"])
+    rcT, itT, _ = ctx.solve_temperature()
+    assert rcT == it[3] and abs(itT - it[4]) <= 1
+    assert rel(ctx.get_state(dcp.T_SOLUTION), g["T_solution"]) < 1e-10
+    ctx.close()
+
+
+def test_config3_r4_fixture_matches_the_mesh():
+    """CPU: the committed config-3 fixture belongs to this mesh (dof counts)
+    and records the reference's failure mode at r=4 (rc 1, 0 / 10,000)."""
+    with np.load(GOLD4) as d:
+        n, it = d["n"], d["iters"]
+        assert d["nse_rhs"].shape == (n[1] + n[2],) and d["T_solution"].shape == (n[3],)
+    m = dcp.HostMesh(refine=4)
+    assert list(n) == [m.n_cells, m.n_u, m.n_p, m.n_T]
+    assert list(it[:3]) == [1, 0, 10000] and it[3] == 0 and it[4] > 0
+
+
 FEEC4 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "feec_r4_step.npz")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
