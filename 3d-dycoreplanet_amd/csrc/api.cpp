@@ -888,6 +888,15 @@ void materialize_velocity_block(Ctx& c) {
   image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
                         c.A_val.p, c.stream);
   c.A_current = true;
+  c.B_current = true;
+}
+
+// nse_matrix.block(1,0) of the last operator-form assembly: the transpose of
+// B^T, block by block (bitwise the B the full scatter produces)
+void materialize_B(Ctx& c) {
+  if (c.B_current) return;
+  transpose_blocks3(long(c.B_tperm.n), c.B_tperm.p, c.Bt_val.p, c.B_val.p, c.stream);
+  c.B_current = true;
 }
 }  // namespace dcp
 
@@ -1209,6 +1218,31 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.A_val.alloc(Ac.size() * 9);
     c.Bt_val.alloc(Btc.size() * 3);
     c.B_val.alloc(Bc.size() * 3);
+    {
+      // B entry (p, n) -> B^T entry (n, p), if every one exists locally
+      const int rows = int(Bp.size()) - 1;
+      std::vector<int32_t> tperm(Bc.size());
+      int missing = 0;
+#pragma omp parallel for schedule(static) reduction(+ : missing)
+      for (int p = 0; p < rows; ++p)
+        for (int k = Bp[p]; k < Bp[p + 1]; ++k) {
+          const int n = Bc[k];
+          // B^T holds the rows of the local (owned) velocity nodes only
+          const bool local = n >= 0 && n + 1 < int(Btp.size());
+          const int32_t* b = local ? Btc.data() + Btp[n] : nullptr;
+          const int32_t* e = local ? Btc.data() + Btp[n + 1] : nullptr;
+          const int32_t* f = local ? std::lower_bound(b, e, p) : nullptr;
+          if (!local || f == e || *f != p) {
+            ++missing;
+            tperm[k] = -1;
+          } else {
+            tperm[k] = int32_t(f - Btc.data());
+          }
+        }
+      c.B_transpose = missing == 0 && !Bc.empty();
+      if (c.B_transpose) c.B_tperm.upload(tperm);
+      else c.B_tperm.release();
+    }
     c.Tmass.alloc(Tc.size());
     c.Tstiff.alloc(Tc.size());
     c.Tmat.alloc(Tc.size());
@@ -1586,12 +1620,14 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     if (matrix) {
       // first-touch scatter positions store instead of adding: no zero fill
       if (full && !c.first_touch_A) c.A_val.zero(c.stream);
+      // operator form: B copied from B^T after the cell loop (c.B_transpose)
+      const bool scatter_B = full || !c.B_transpose;
       if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
-      if (!c.first_touch_B) c.B_val.zero(c.stream);
+      if (scatter_B && !c.first_touch_B) c.B_val.zero(c.stream);
       c.con_diag.zero(c.stream);
       out.A = full ? c.A_val.p : nullptr;
       out.Bt = c.Bt_val.p;
-      out.B = c.B_val.p;
+      out.B = scatter_B ? c.B_val.p : nullptr;
       out.cdiag = c.con_diag.p;
       out.cidx = c.mf_cidx.p;
       out.pcdiag = c.con_diag.p + 3 * size_t(c.n_con);
@@ -1617,6 +1653,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
                             c.A_val.p, c.stream);
     t.stop();
     if (matrix) {
+      c.B_current = out.B != nullptr;  // else B = (B^T)^T, materialised when read
       c.nse_assembled = true;
       c.A_current = full;
       c.nse_ph = c.ph;
@@ -1642,7 +1679,9 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
       require(c.nse_assembled, DCP_ERR_STATE,
               "the explicit Schur complement needs the assembled B blocks: call "
               "dcp_assemble_nse_system first");
-      form_schur_complement(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, c.Bt_ptr.p, c.Bt_col.p,
+      // B read through B^T's transpose map unless B is materialised
+      form_schur_complement(c.npo, c.B_ptr.p, c.B_col.p, c.B_current ? c.B_val.p : nullptr,
+                            c.B_current ? nullptr : c.B_tperm.p, c.Bt_ptr.p, c.Bt_col.p,
                             c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_pmap.p,
                             c.S_val.p, c.S_max_row, c.stream);
     }

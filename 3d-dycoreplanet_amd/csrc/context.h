@@ -109,6 +109,11 @@ struct Ctx {
   int n_img_u = 0, n_img_p = 0, n_img_T = 0, n_img_node = 0;
   bool periodic = false;
   bool assemble_A = false;   // DCP_OPT_ASSEMBLE_VELOCITY_BLOCK
+  // B entry k = B^T entry B_tperm[k] (every B entry has its B^T partner, one
+  // GPU): the operator form scatters B^T only and copies B from it
+  DBuf<int32_t> B_tperm;
+  bool B_transpose = false;
+  bool B_current = true;     // B_val holds the B block of the last assembly
   bool A_current = false;    // A_val holds the block of the last assembly
   PhysicsDev nse_ph{};       // physics (dt) of the last assemble_nse_system
   // explicit Schur complement S = B D_A^-1 B^T (CSR over pressure dofs)
@@ -293,6 +298,8 @@ struct Ctx {
 
 // api.cpp: A_val <- nse_matrix.block(0,0) of the last assembly (if not current)
 void materialize_velocity_block(Ctx& c);
+// B = (B^T)^T after an operator-form assembly that scattered B^T only
+void materialize_B(Ctx& c);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
 int solve_temperature(Ctx& c, int* iters, double* T_range);

@@ -182,6 +182,9 @@ void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t*
 void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                          const double* u_old, const double* T_old, const PhysicsDev& ph,
                          const NseOut& out, hipStream_t s);
+// dst block k (3 doubles) = src block tperm[k]: B from B^T (operator form)
+void transpose_blocks3(long n, const int32_t* tperm, const double* src, double* dst,
+                       hipStream_t s);
 // Element mode: dense FESystem-ordered K/f of cells [first, first+n).
 void launch_nse_system_elements(const CellData& cd, int first, int n, const double* u_old,
                                 const double* T_old, const PhysicsDev& ph, double* K, double* f,
@@ -214,8 +217,10 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
 // S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
 // contributions summed in fixed node order: deterministic). pmap != null:
 // entry j of the CSR pattern is stored at S_val[pmap[j]] (the SELL layout).
+// B_val == null: B[p][n] read as B^T block tperm[k] (B not materialised)
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
-                           const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
+                           const int32_t* tperm, const int32_t* Bt_ptr, const int32_t* Bt_col,
+                           const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
                            const int32_t* pmap, double* S_val, int max_row, hipStream_t s);
 

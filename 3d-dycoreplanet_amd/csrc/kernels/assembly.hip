@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   const int cell = MODE != 1 ? cells[DCP_ASM_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x)]
                              : first + blockIdx.x;
   const bool want_matrix = MODE == 1 || (MODE == 0 && out.A != nullptr);
-  const bool want_B = want_matrix || (MODE == 2 && out.B != nullptr);
+  const bool want_B = want_matrix || (MODE == 2 && out.Bt != nullptr);
   const bool want_rhs = MODE == 1 || out.rhs != nullptr;
   const bool want_cdiag = MODE != 1 && out.cdiag != nullptr;
 
@@ -431,10 +431,12 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   }
   if (MODE == 0 && want_matrix)
     for (int i = tid; i < 729; i += kNseThreads) sh.pos[i] = sm.posA[729 * size_t(cell) + i];
+  // MODE 2 with out.B == null: B^T only (B is its transpose, copied afterwards)
+  const bool scatter_B = MODE != 2 || out.B != nullptr;
   if (MODE != 1 && want_B) {
     for (int i = tid; i < 216; i += kNseThreads) {
       sh.pos[729 + i] = sm.posBt[216 * size_t(cell) + i];
-      sh.pos[945 + i] = sm.posB[216 * size_t(cell) + i];
+      if (scatter_B) sh.pos[945 + i] = sm.posB[216 * size_t(cell) + i];
     }
   }
   // reference shape values / gradients at the Gauss points, formed from the 1D
@@ -681,13 +683,15 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
     }
     __syncthreads();
     // B^T then B rows: elements [729 * 9, kScatterElems) of the MODE 0 order
+    // (B^T rows only: [729 * 9, 729 * 9 + 648))
     constexpr int kOpBatch = (2 * 648 + kNseThreads - 1) / kNseThreads;  // 6
+    const int e_end = scatter_B ? kScatterElems : 729 * 9 + 648;
     double old[kOpBatch];
 #pragma unroll
     for (int j = 0; j < kOpBatch; ++j) {
       const int e = 729 * 9 + tid + j * kNseThreads;
       old[j] = 0.0;
-      if (e < kScatterElems) {
+      if (e < e_end) {
         bool add;
         double v;
         const double* dst = scatter_target(sh, out, e, add, v);
@@ -697,7 +701,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #pragma unroll
     for (int j = 0; j < kOpBatch; ++j) {
       const int e = 729 * 9 + tid + j * kNseThreads;
-      if (e < kScatterElems) {
+      if (e < e_end) {
         bool add;
         double v;
         double* dst = scatter_target(sh, out, e, add, v);
@@ -1074,6 +1078,7 @@ __global__ void k_clear_first_touch(size_t n, int32_t* __restrict__ pos) {
 __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __restrict__ B_ptr,
                                                    const int32_t* __restrict__ B_col,
                                                    const double* __restrict__ B_val,
+                                                   const int32_t* __restrict__ tperm,
                                                    const int32_t* __restrict__ Bt_ptr,
                                                    const int32_t* __restrict__ Bt_col,
                                                    const double* __restrict__ Bt_val,
@@ -1094,9 +1099,11 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
   __syncthreads();
   for (int k = B_ptr[p]; k < B_ptr[p + 1]; ++k) {
     const size_t n = size_t(B_col[k]);
-    const double w0 = B_val[3 * size_t(k)] * d[3 * n];
-    const double w1 = B_val[3 * size_t(k) + 1] * d[3 * n + 1];
-    const double w2 = B_val[3 * size_t(k) + 2] * d[3 * n + 2];
+    // B[p][n] = B^T[n][p] (tperm: B not materialised)
+    const double* bk = tperm ? Bt_val + 3 * size_t(tperm[k]) : B_val + 3 * size_t(k);
+    const double w0 = bk[0] * d[3 * n];
+    const double w1 = bk[1] * d[3 * n + 1];
+    const double w2 = bk[2] * d[3 * n + 2];
     const int b = Bt_ptr[n], e = Bt_ptr[n + 1];
     for (int j = b + int(threadIdx.x); j < e; j += 64) {
       const int q = Bt_col[j];
@@ -1121,12 +1128,13 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
 }  // namespace
 
 void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, const double* B_val,
-                           const int32_t* Bt_ptr, const int32_t* Bt_col, const double* Bt_val,
+                           const int32_t* tperm, const int32_t* Bt_ptr, const int32_t* Bt_col,
+                           const double* Bt_val,
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
                            const int32_t* pmap, double* S_val, int max_row, hipStream_t s) {
   if (n_p <= 0) return;
   const size_t lds = size_t(max_row) * (sizeof(double) + sizeof(int)) + 16;
-  hipLaunchKernelGGL(k_schur_form, dim3(n_p), dim3(64), lds, s, n_p, B_ptr, B_col, B_val, Bt_ptr,
+  hipLaunchKernelGGL(k_schur_form, dim3(n_p), dim3(64), lds, s, n_p, B_ptr, B_col, B_val, tperm, Bt_ptr,
                      Bt_col, Bt_val, d, S_ptr, S_col, pmap, S_val);
   DCP_HIP_CHECK(hipGetLastError());
 }
@@ -1146,6 +1154,26 @@ void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_
   if (n <= 0) return;
   hipLaunchKernelGGL((k_nse_system<2>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
                      u_old, T_old, ph, out);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+// B = (B^T)^T: block k of B is block tperm[k] of B^T (bitwise: both are summed
+// over the same cells in the same colour order, and the local B and B^T
+// entries are the same products)
+__global__ void k_transpose_blocks3(long n, const int32_t* __restrict__ tperm,
+                                    const double* __restrict__ src, double* __restrict__ dst) {
+  const long i = blockIdx.x * long(blockDim.x) + threadIdx.x;  // one double of dst
+  if (i >= 3 * n) return;
+  const long k = i / 3;
+  dst[i] = src[3 * long(tperm[k]) + (i - 3 * k)];
+}
+
+void transpose_blocks3(long n, const int32_t* tperm, const double* src, double* dst,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  const long threads = 3 * n;
+  hipLaunchKernelGGL(k_transpose_blocks3, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, s,
+                     n, tperm, src, dst);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -1012,6 +1012,7 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
   spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, src, c.schur_tmp1.p, false, c.stream);
   mul(c.n_u, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
   halo_exchange(c, c.halo_v, c.schur_tmp2.p);
+  materialize_B(c);
   spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, c.schur_tmp2.p, dst, false, c.stream);
   if (ev) DCP_HIP_CHECK(hipEventRecord(ev->b, c.stream));
 }
