@@ -652,7 +652,8 @@ std::vector<int32_t> rcm_order(int n, const std::vector<int32_t>& ptr,
 template <class NodeFn>
 bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
                         std::vector<double>& colgeo, std::vector<int32_t>& layer,
-                        std::vector<double>& laygeo) {
+                        std::vector<double>& laygeo, std::vector<double>* colphi = nullptr,
+                        std::vector<double>* layR = nullptr) {
   std::vector<double> rad;
   constexpr double tol = 1e-13;
   constexpr int kP = kMapPts1, kP2 = kMapPts1 * kMapPts1;
@@ -716,6 +717,7 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
     col[cell] = id;
   }
   colgeo.assign(col_phi.size() * 90, 0.0);
+  if (colphi) colphi->assign(col_phi.size() * 27, 0.0);
   for (size_t k = 0; k < col_phi.size(); ++k) {
     const double* ph = col_phi[k].data();
     for (int q1 = 0; q1 < 3; ++q1)
@@ -749,11 +751,14 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
           g[6 + d] = m2[d] / D2;
         }
         g[9] = D2;
+        if (colphi)
+          for (int d = 0; d < 3; ++d) (*colphi)[27 * k + 3 * (q0 + 3 * q1) + d] = F[d];
       }
   }
   // radial layers
   layer.assign(n_cells, 0);
   laygeo.clear();
+  if (layR) layR->clear();
   std::unordered_map<int64_t, int> ids;
   for (int cell = 0; cell < n_cells; ++cell) {
     const double* r = &rad[kP * size_t(cell)];
@@ -770,6 +775,7 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
         laygeo.push_back(1.0 / R);
         laygeo.push_back(1.0 / Rp);
         laygeo.push_back(R * R * Rp);
+        if (layR) layR->push_back(R);
       }
     }
     layer[cell] = it->second;
@@ -1477,15 +1483,17 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       c.mf_buf.alloc(size_t(pbase) + size_t(pptr[n_p]));
       {
         std::vector<int32_t> col, layer;
-        std::vector<double> colgeo, laygeo;
+        std::vector<double> colgeo, laygeo, colphi, layR;
         c.mf_separable = separable_geometry(
             n_cells, [&](int cell, int t) { return &h.geo[3 * kMapPts * size_t(cell) + 3 * t]; },
-            col, colgeo, layer, laygeo);
+            col, colgeo, layer, laygeo, &colphi, &layR);
         if (c.mf_separable) {
           c.mf_col.upload(col);
           c.mf_colgeo.upload(colgeo);
           c.mf_layer.upload(layer);
           c.mf_laygeo.upload(laygeo);
+          c.mf_colphi.upload(colphi);
+          c.mf_layR.upload(layR);
         } else {
           // general mesh: J^-1 / JxW per Gauss point, tree order (2160 B per cell)
           c.mf_geo_tree.alloc(size_t(n_cells) * 270);

@@ -161,7 +161,7 @@ struct Ctx {
   hipStream_t mf_stream = nullptr;
   hipEvent_t mf_chunk_ev[kMfChunksMax] = {}, mf_join_ev = nullptr;
   DBuf<int32_t> mf_col, mf_layer;
-  DBuf<double> mf_colgeo, mf_laygeo;
+  DBuf<double> mf_colgeo, mf_laygeo, mf_colphi, mf_layR;
   bool mf_separable = false;
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
@@ -287,6 +287,13 @@ struct Ctx {
     c.cell_q2o = periodic ? cell_q2o.p : nullptr;
     c.cell_po = periodic ? cell_po.p : nullptr;
     c.cell_To = periodic ? cell_To.p : nullptr;
+    const bool sep = mf_separable && mf_colphi.p != nullptr;
+    c.sep_col = sep ? mf_col.p : nullptr;
+    c.sep_colgeo = sep ? mf_colgeo.p : nullptr;
+    c.sep_colphi = sep ? mf_colphi.p : nullptr;
+    c.sep_layer = sep ? mf_layer.p : nullptr;
+    c.sep_laygeo = sep ? mf_laygeo.p : nullptr;
+    c.sep_layR = sep ? mf_layR.p : nullptr;
     return c;
   }
   ScatterMaps maps() const { return ScatterMaps{posA.p, posBt.p, posB.p, posT.p}; }

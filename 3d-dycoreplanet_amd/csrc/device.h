@@ -70,6 +70,15 @@ struct CellData {
   const int32_t* cell_q2o;  // [n_cells][27]
   const int32_t* cell_po;   // [n_cells][8]
   const int32_t* cell_To;   // [n_cells][8]
+  // radially separable mesh (X(a,b,c) = r_c phi_ab, api.cpp separable_geometry;
+  // null otherwise): J^-1 / JxW / x at the Gauss points from per-column and
+  // per-layer tables instead of the MappingQ(3) sums over 64 support points
+  const int32_t* sep_col;      // [n_cells]
+  const double* sep_colgeo;    // [n_cols][9 points q0 + 3 q1][m0 m1 m2 (/D2), D2]
+  const double* sep_colphi;    // [n_cols][9][3] phi at the points
+  const int32_t* sep_layer;    // [n_cells]
+  const double* sep_laygeo;    // [n_layers][3 points q2][1/R, 1/R', R^2 R']
+  const double* sep_layR;      // [n_layers][3] R
 };
 
 struct NseOut {

@@ -94,6 +94,27 @@ struct Geo {
   double xq[27 * 3];
 };
 
+// Radially separable mesh (cd.sep_col != null): J^-1, JxW and x at Gauss point
+// q from the column / layer tables, the products the matrix-free kernel forms
+// (J^-1 rows m0 / R, m1 / R, m2 / R'; JxW = R^2 R' D2 w; x = R phi).
+__device__ inline void sep_geometry(const CellData& cd, int cell, Geo& g, int q) {
+  const int q0 = q % 3, q1 = (q / 3) % 3, q2 = q / 9;
+  const int col = cd.sep_col[cell], lay = cd.sep_layer[cell];
+  const double* m = cd.sep_colgeo + 90 * size_t(col) + 10 * (q0 + 3 * q1);
+  const double* lg = cd.sep_laygeo + 9 * size_t(lay) + 3 * q2;
+  const double* ph = cd.sep_colphi + 27 * size_t(col) + 3 * (q0 + 3 * q1);
+  const double iR = lg[0], iRp = lg[1], R = cd.sep_layR[3 * size_t(lay) + q2];
+  double* Ji = &g.Ji[9 * q];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    Ji[d] = m[d] * iR;
+    Ji[3 + d] = m[3 + d] * iR;
+    Ji[6 + d] = m[6 + d] * iRp;
+    g.xq[3 * q + d] = R * ph[d];
+  }
+  g.JxW[q] = lg[2] * m[9] * (cW[q0] * cW[q1] * cW[q2]);
+}
+
 // 27 threads: the MappingQ(3) map at the QGauss(3) points (X: 64 support points).
 __device__ inline void cell_geometry(const double* X, Geo& g, int q) {
   double J[3][3];
@@ -414,7 +435,8 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   const bool want_rhs = MODE == 1 || out.rhs != nullptr;
   const bool want_cdiag = MODE != 1 && out.cdiag != nullptr;
 
-  if (tid < 3 * kMapPts) sh.X[tid] = cd.geo[3 * kMapPts * size_t(cell) + tid];
+  const bool sep = cd.sep_col != nullptr;
+  if (!sep && tid < 3 * kMapPts) sh.X[tid] = cd.geo[3 * kMapPts * size_t(cell) + tid];
   if (tid < 27) {
     const int n = cd.cell_q2[27 * size_t(cell) + tid];
     sh.node[tid] = n;
@@ -458,7 +480,13 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #ifndef DCP_OP_NOGEO
 #define DCP_OP_NOGEO 0
 #endif
-  if (tid < 81 && !DCP_OP_NOGEO) {
+#ifndef DCP_OP_NOMAP
+#define DCP_OP_NOMAP 0  // timing probe: skips the map only (wrong results)
+#endif
+  if (sep) {
+    if (tid < 27) sep_geometry(cd, cell, sh.geo, tid);
+  } else {
+  if (tid < 81 && !DCP_OP_NOGEO && !DCP_OP_NOMAP) {
     const int q = tid / 3, i = tid % 3;
     double J0, J1, J2, x;
     map_row(sh.X, q, i, x, J0, J1, J2);
@@ -495,6 +523,7 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
 #pragma unroll
     for (int k = 0; k < 9; ++k) sh.geo.Ji[9 * tid + k] = Jinv[k];
     sh.geo.JxW[tid] = jxw;
+  }
   }
   __syncthreads();
   // physical gradients in place: grad_d = sum_e dN/dxi_e Ji[e][d]
@@ -844,9 +873,13 @@ __global__ __launch_bounds__(64) void k_nse_precond_diag(CellData cd, const int3
   __shared__ Geo geo;
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
-  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
+  if (!cd.sep_col)
+    for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   __syncthreads();
-  if (tid < 27) cell_geometry(X, geo, tid);
+  if (tid < 27) {
+    if (cd.sep_col) sep_geometry(cd, cell, geo, tid);
+    else cell_geometry(X, geo, tid);
+  }
   __syncthreads();
   if (tid < 27) {
     const int a = tid;
@@ -894,10 +927,14 @@ __global__ __launch_bounds__(64) void k_T_matrix(CellData cd, ScatterMaps sm,
   __shared__ int dof[8];
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
-  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
+  if (!cd.sep_col)
+    for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   if (tid >= 32 && tid < 40) dof[tid - 32] = cd.cell_T[8 * size_t(cell) + tid - 32];
   __syncthreads();
-  if (tid < 27) cell_geometry(X, geo, tid);
+  if (tid < 27) {
+    if (cd.sep_col) sep_geometry(cd, cell, geo, tid);
+    else cell_geometry(X, geo, tid);
+  }
   __syncthreads();
   for (int i = tid; i < 216; i += 64) q1_grad(geo, i / 8, i % 8, &G1[3 * i]);
   __syncthreads();
@@ -953,7 +990,8 @@ __global__ __launch_bounds__(64) void k_T_rhs(CellData cd, const int32_t* __rest
   __shared__ int dof[8];
   const int tid = threadIdx.x;
   const int cell = cells[blockIdx.x];
-  for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
+  if (!cd.sep_col)
+    for (int i = tid; i < 3 * kMapPts; i += 64) X[i] = cd.geo[3 * kMapPts * size_t(cell) + i];
   if (tid < 27) {
     const int n = (cd.cell_q2o ? cd.cell_q2o : cd.cell_q2)[27 * size_t(cell) + tid];
 #pragma unroll
@@ -964,7 +1002,10 @@ __global__ __launch_bounds__(64) void k_T_rhs(CellData cd, const int32_t* __rest
     Tn[tid - 32] = T_old[(cd.cell_To ? cd.cell_To : cd.cell_T)[8 * size_t(cell) + tid - 32]];
   }
   __syncthreads();
-  if (tid < 27) cell_geometry(X, geo, tid);
+  if (tid < 27) {
+    if (cd.sep_col) sep_geometry(cd, cell, geo, tid);
+    else cell_geometry(X, geo, tid);
+  }
   __syncthreads();
   for (int i = tid; i < 216; i += 64) q1_grad(geo, i / 8, i % 8, &G1[3 * i]);
   __syncthreads();
