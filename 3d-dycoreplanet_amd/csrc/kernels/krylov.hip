@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <stdexcept>
+#include <string>
 
 #include "../comm.h"
 #include "../device.h"
@@ -273,9 +275,9 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(Seg g, double* __restrict
 // two waves per SIMD). A reduction is two granule hops: every workgroup
 // publishes its d block sums (column j of the partial area), workgroup j sums
 // column j in block_sum order and publishes the result, and every workgroup
-// reads the d results. Three reductions per step (V^T w, V^T w after the
-// first update, |w|^2 -- the last one read by workgroup 0 alone, which then
-// does the Givens step). Overwriting a partial granule of the next reduction
+// reads the d results. Two reductions per step (V^T w, then V^T w and |w|^2
+// after the first update; the norm of the result is |w|^2 - |V^T w|^2), after
+// which workgroup 0 does the Givens step. Overwriting a partial granule of the next reduction
 // is safe: a workgroup only gets there after every reducer has published,
 // i.e. finished reading.
 constexpr int kChainThreads = 512;
@@ -393,18 +395,35 @@ __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, 
   }
   double* part = gran;
   double* res = gran + kCgsRes;
+  // The second pass also reduces |x|^2 of its input (entry K - 1 of the
+  // reduce-scatter, free since d < K; granule column d), so the norm of the
+  // result follows without a third reduction: |x - V h|^2 = |x|^2 - |h|^2
+  // for orthonormal V (h = V^T x).
   for (int pass = 0; pass < 2; ++pass) {
     const unsigned long long tag = seq * 64 + 4 * unsigned(pass);
-    const double r = chain_block_sums<K>(v, x, d, sm);
-    if (DCP_CGS_NOWAIT) {
-      if (int(threadIdx.x) < d) hs[threadIdx.x] = r * 1e-3;
+    double r;
+    if (pass == 1) {
+      double v2[kChainEntries][K];
+#pragma unroll
+      for (int e = 0; e < kChainEntries; ++e)
+#pragma unroll
+        for (int j = 0; j < K; ++j) v2[e][j] = j == K - 1 ? x[e] : v[e][j];
+      r = chain_block_sums<K>(v2, x, K, sm);
     } else {
-    if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(threadIdx.x) * nb + b), r, tag);
-    if (b < d && threadIdx.x < 64) {
+      r = chain_block_sums<K>(v, x, d, sm);
+    }
+    const int ncol = d + pass;  // pass 1: column d = |x|^2
+    const bool pub = int(threadIdx.x) < d || (pass == 1 && int(threadIdx.x) == K - 1);
+    const int col = int(threadIdx.x) < d ? int(threadIdx.x) : d;
+    if (DCP_CGS_NOWAIT) {
+      if (int(threadIdx.x) < ncol) hs[threadIdx.x] = r * 1e-3;
+    } else {
+    if (pub) granule_store(part + 2 * (size_t(col) * nb + b), r, tag);
+    if (b < ncol && threadIdx.x < 64) {
       const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err);
       if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + 1);
     }
-    if (int(threadIdx.x) < d) {
+    if (int(threadIdx.x) < ncol) {
       const double* p = res + 2 * threadIdx.x;
       mgs_u4 q = granule_load(p);
       for (long spins = 0; !tag_is(q, tag + 1); ++spins) {
@@ -416,7 +435,7 @@ __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, 
         q = granule_load(p);
       }
       hs[threadIdx.x] = granule_value(q);
-      if (b == 0) st->coef[pass * kGmMaxDim + threadIdx.x] = granule_value(q);
+      if (b == 0 && int(threadIdx.x) < d) st->coef[pass * kGmMaxDim + threadIdx.x] = granule_value(q);
     }
     }
     __syncthreads();
@@ -430,18 +449,12 @@ __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, 
 #pragma unroll
   for (int e = 0; e < kChainEntries; ++e)
     if (live[e]) w[pos[e]] = x[e];
-  {
-    const double t1[kChainEntries][1] = {{x[0]}, {x[1]}};
-    const double rn = chain_block_sums<1>(t1, x, 1, sm);
-    if (threadIdx.x == 0) granule_store(part + 2 * size_t(b), rn, seq * 64 + 8);
-  }
   if (b != 0) return;
-  if (threadIdx.x < 64) {
-    const double tot = granule_coef(part, nb, seq * 64 + 8, err);
-    if (threadIdx.x == 0) {
-      nrm_sh = tot;
-      st->nrm2 = tot;
-    }
+  if (threadIdx.x == 0) {
+    double n2 = hs[d];
+    for (int j = 0; j < d; ++j) n2 -= hs[j] * hs[j];
+    nrm_sh = fmax(n2, 0.0);
+    st->nrm2 = nrm_sh;
   }
   __syncthreads();
   gmres_step(st, nrm_sh, kstep);
@@ -509,8 +522,9 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
   ChainVecs Vp = V;  // unused slots point at V[0]: the kernel's loads are unconditional
   for (int j = d; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
   const dim3 grid(nb), block(kChainThreads);
+  // KL > d: the chain's second reduction keeps its |w|^2 entry at K - 1 >= d
 #define DCP_CGS_CASE(KL)                                                                       \
-  if (d <= KL) {                                                                               \
+  if (d < KL) {                                                                                \
     hipLaunchKernelGGL(k_cgs2_chain<KL>, grid, block, 0, s, g, w, Vp, d, st, d - 1, gran, seq, \
                        err);                                                                   \
     DCP_HIP_CHECK(hipGetLastError());                                                          \
@@ -519,6 +533,8 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
   DCP_CGS_CASE(4) DCP_CGS_CASE(8) DCP_CGS_CASE(12) DCP_CGS_CASE(16) DCP_CGS_CASE(20)
   DCP_CGS_CASE(24) DCP_CGS_CASE(28) DCP_CGS_CASE(32)
 #undef DCP_CGS_CASE
+  throw std::runtime_error("cgs2_chain_step: " + std::to_string(d) + " basis vectors (at most " +
+                           std::to_string(kGmMaxDim - 1) + ")");
 }
 
 size_t cgs2_granules(long n) {
