@@ -638,7 +638,7 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
 // cycle enqueued at once and run on the device (kernels/krylov.hip). The host
 // polls the device status every kGmPoll steps so it stops enqueueing shortly
 // after convergence (the steps already queued return at entry).
-constexpr int kGmPoll = 4;
+constexpr int kGmPoll = 8;
 State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                                std::vector<double*>& tv, int n_tmp) {
   const int n = c.n_p;
