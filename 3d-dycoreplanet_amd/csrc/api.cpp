@@ -31,9 +31,7 @@ Ctx::~Ctx() {
   free_workspaces(*this);
   if (hpinned) (void)hipHostFree(hpinned);
   if (hmapped) (void)hipHostFree(hmapped);
-  if (gm_init) (void)hipHostFree(gm_init);
-  if (gm_read) (void)hipHostFree(gm_read);
-  if (gm_flag) (void)hipHostFree(gm_flag);
+  if (gm_report) (void)hipHostFree(gm_report);
   for (auto& ev : gm_ev)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : spec_ev)

@@ -198,9 +198,7 @@ struct Ctx {
   // basis pointer table
   int gram_schmidt = 0;
   DBuf<GmresDev> gm_state;
-  GmresDev* gm_init = nullptr;       // pinned: cycle start state (host -> device)
-  GmresDev* gm_read = nullptr;       // pinned: cycle end state (device -> host)
-  int* gm_flag = nullptr;            // pinned [2]: status at the last two polls
+  GmresReport* gm_report = nullptr;  // pinned [2]: the reports of the last two cycles
   hipEvent_t gm_ev[2] = {nullptr, nullptr};
   DBuf<double> gm_part;
   DBuf<unsigned> gm_cnt;             // last-block counter of the CGS2 launches

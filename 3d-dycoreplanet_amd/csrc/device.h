@@ -376,7 +376,13 @@ struct GmresDev {
   double y[kGmMaxDim];          // back-substituted combination coefficients
   double inv_norm, rho, tol;    // 1/|w| of the last step (1 if 0), |gamma_dim|, tolerance
   double nrm2;                  // |w|^2 of the last step
+  double inv_rho;               // 1 / the residual norm at the start of the cycle
   int status, dim, accumulated, max_steps;
+};
+// What the host reads after a cycle (pinned, written by gmres_cycle_end)
+struct GmresReport {
+  double rho;
+  int status, accumulated;
 };
 struct Comm;
 // Arnoldi step k = d - 1 after w = S v_k: w -= V (V^T w) twice, |w|, the
@@ -394,6 +400,17 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
                      int nb, unsigned long long seq, double* err, hipStream_t s);
 void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,
                      GmresDev* st, unsigned long long& seq, double* err, Comm* comm,
+                     hipStream_t s);
+// Restart-cycle head on the device (SolverGMRES's start of a cycle):
+// rho = sqrt(*rho2) of the residual b - S x, SolverControl::check(accumulated,
+// rho), gamma_0 = rho, inv_rho = 1 / rho. first: a new solve (tol, max_steps,
+// counters reset). Once the solve has stopped (status != 0) it only zeroes
+// dim, so every launch of a cycle enqueued after the stop is a no-op.
+void gmres_cycle_init(GmresDev* st, const double* rho2, double tol, int max_steps, bool first,
+                      hipStream_t s);
+// Cycle tail: x += V y (y = the back-substituted coefficients, dim of them,
+// read on the device) and the report to the host.
+void gmres_cycle_end(GmresDev* st, int n, const double* const* V, double* x, GmresReport* report,
                      hipStream_t s);
 // st->y = H^-1 gamma over st->dim
 void gmres_backsub(GmresDev* st, hipStream_t s);

@@ -29,6 +29,7 @@
 // all-reduced between the launches and the Givens step is its own launch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -550,6 +551,69 @@ void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, 
     cgs_step_k<16>(g, w, V, d, gran, cnt, st, seq, err, comm, s);
   else
     cgs_step_k<kGmMaxDim>(g, w, V, d, gran, cnt, st, seq, err, comm, s);
+}
+
+__global__ void k_gmres_cycle_init(GmresDev* st, const double* __restrict__ rho2, double tol,
+                                   int max_steps, int first) {
+  if (threadIdx.x != 0) return;
+  if (first) {
+    st->status = 0;
+    st->accumulated = 0;
+    st->tol = tol;
+    st->max_steps = max_steps;
+  }
+  st->dim = 0;
+  if (st->status != 0) return;
+  const double rho = sqrt(*rho2);
+  const int acc = st->accumulated;
+  st->rho = rho;
+  // SolverControl::check(accumulated, rho) at the head of the cycle
+  const int status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+  st->status = status;
+  if (status != 0) return;
+  st->gamma[0] = rho;
+  st->inv_rho = 1.0 / rho;
+  st->inv_norm = 1.0;
+}
+
+// x += sum_{j < dim} y_j V_j, dim read on the device (0: nothing)
+__global__ void k_gmres_update(const GmresDev* __restrict__ st, int n, const double* const* V,
+                               double* __restrict__ x) {
+  const int dim = st->dim;
+  if (dim <= 0) return;
+  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+    double v = x[i];
+    for (int j = 0; j < dim; ++j) v += st->y[j] * V[j][i];
+    x[i] = v;
+  }
+}
+
+__global__ void k_gmres_report(const GmresDev* __restrict__ st, GmresReport* report) {
+  if (threadIdx.x != 0) return;
+  // plain vector stores into the pinned host record; the host reads it after
+  // an event recorded behind this launch
+  report->rho = st->rho;
+  report->status = st->status;
+  report->accumulated = st->accumulated;
+}
+
+void gmres_cycle_init(GmresDev* st, const double* rho2, double tol, int max_steps, bool first,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_gmres_cycle_init, dim3(1), dim3(64), 0, s, st, rho2, tol, max_steps,
+                     int(first));
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void gmres_cycle_end(GmresDev* st, int n, const double* const* V, double* x, GmresReport* report,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_gmres_backsub, dim3(1), dim3(kBlock), 0, s, st);
+  DCP_HIP_CHECK(hipGetLastError());
+  const long blocks = std::min<long>((long(n) + kBlock - 1) / kBlock, 2048);
+  hipLaunchKernelGGL(k_gmres_update, dim3(unsigned(std::max<long>(blocks, 1))), dim3(kBlock), 0, s,
+                     st, n, V, x);
+  DCP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_gmres_report, dim3(1), dim3(64), 0, s, st, report);
+  DCP_HIP_CHECK(hipGetLastError());
 }
 
 void gmres_backsub(GmresDev* st, hipStream_t s) {

@@ -634,11 +634,12 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
 
 // The inner Schur GMRES on the explicit S with classical Gram-Schmidt twice
 // (DCP_OPT_GRAM_SCHMIDT = 1): deal.II SolverGMRES's cycle structure, Givens
-// rotations, residual estimate and SolverControl rule, with every restart
-// cycle enqueued at once and run on the device (kernels/krylov.hip). The host
-// polls the device status every kGmPoll steps so it stops enqueueing shortly
-// after convergence (the steps already queued return at entry).
-constexpr int kGmPoll = 8;
+// rotations, residual estimate and SolverControl rule, run on the device
+// (kernels/krylov.hip) cycle after cycle: the head of a cycle (residual, its
+// norm, the SolverControl check, v_0) and its tail (back substitution, x +=
+// V y) are kernels too, so the host enqueues cycle i + 1 before it waits for
+// the report of cycle i and never leaves the stream idle. Once the solve has
+// stopped every launch of a cycle already queued returns at entry.
 State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                                std::vector<double*>& tv, int n_tmp) {
   const int n = c.n_p;
@@ -648,11 +649,9 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   ensure_pool(tv, n_tmp + 2, size_t(n));
   double* p = tv[n_tmp - 1];
   double* wbuf[2] = {tv[n_tmp], tv[n_tmp + 1]};
-  if (!c.gm_init) {
+  if (!c.gm_report) {
     c.gm_state.alloc(1);
-    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_init), sizeof(GmresDev)));
-    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_read), sizeof(GmresDev)));
-    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_flag), 2 * sizeof(int)));
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_report), 2 * sizeof(GmresReport)));
     for (auto& ev : c.gm_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   }
   const size_t pn = cgs2_granules(g.n);
@@ -673,26 +672,16 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   Comm* comm = c.comm.get();
   const int nb1 = std::min(c.n_cus, 256);
   const bool one_launch = !comm && c.fused_chain && c.hmapped && cgs2_chain_fits(g.n, nb1, c.n_cus);
-  State st = kIterate;
-  unsigned accumulated = 0;
-  for (;;) {
+  auto enqueue_cycle = [&](int cyc) {
+    // head: p = b - S x, rho = |p| (SolverControl check on the device), v_0 = p / rho
     if (c.S_perm.p)
       sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
     else
       schur_vmult(c, x, p);
-    sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
-    const double rho = std::sqrt(dot_host(c, g, p, p, kSlotA));
-    st = ctl.check(accumulated, rho);
-    if (st != kIterate) break;
-    equ(n, DScal{nullptr, 1. / rho}, p, tv[0], c.stream);
-    std::memset(c.gm_init, 0, sizeof(GmresDev));
-    c.gm_init->gamma[0] = rho;
-    c.gm_init->tol = ctl.tol;
-    c.gm_init->inv_norm = 1.0;
-    c.gm_init->accumulated = int(accumulated);
-    c.gm_init->max_steps = int(ctl.max_steps);
-    DCP_HIP_CHECK(hipMemcpyAsync(dst, c.gm_init, sizeof(GmresDev), hipMemcpyHostToDevice, c.stream));
-    int polls = 0;
+    sadd(n, -1., 1., b, p, c.stream);
+    gdot(c, g, p, p, kSlotA);
+    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
+    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
     for (int k = 0; k < restart; ++k) {
       double* src = k == 0 ? tv[0] : wbuf[(k - 1) & 1];
       double* w = wbuf[k & 1];
@@ -708,34 +697,28 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
       else
         cgs2_gmres_step(g, w, chain_vecs(tv, k + 1), k + 1, c.gm_part.p, c.gm_cnt.p, dst,
                         c.chain_seq, comm ? c.dscal.p + kSlotD : chain_err(c), comm, c.stream);
-      if (k % kGmPoll == kGmPoll - 1 && k + 1 < restart) {
-        const int slot_now = polls & 1;
-        DCP_HIP_CHECK(hipMemcpyAsync(&c.gm_flag[slot_now], &dst->status, sizeof(int),
-                                     hipMemcpyDeviceToHost, c.stream));
-        DCP_HIP_CHECK(hipEventRecord(c.gm_ev[slot_now], c.stream));
-        if (polls > 0) {
-          // the previous poll's status: stop enqueueing once the cycle has stopped
-          DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[slot_now ^ 1]));
-          if (c.gm_flag[slot_now ^ 1] != 0) break;
-        }
-        ++polls;
-      }
     }
-    DCP_HIP_CHECK(hipMemcpyAsync(c.gm_read, dst, sizeof(GmresDev), hipMemcpyDeviceToHost, c.stream));
-    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
-    if (!comm) check_chain_err(c);
-    const GmresDev& r = *c.gm_read;
-    accumulated = unsigned(r.accumulated);
-    ctl.last_step = accumulated;
-    ctl.last_value = r.rho;
-    if (r.dim > 0) {
-      gmres_backsub(dst, c.stream);
-      multi_axpy(n, r.dim, dst->y, c.gm_ptrs.p, x, c.stream);
-    }
-    st = r.status == 1 ? kSuccess : (r.status == 2 ? kFailure : kIterate);
-    if (st != kIterate) break;
+    // tail: H y = gamma, x += V y, the report for the host
+    gmres_cycle_end(dst, n, c.gm_ptrs.p, x, &c.gm_report[cyc & 1], c.stream);
+    DCP_HIP_CHECK(hipEventRecord(c.gm_ev[cyc & 1], c.stream));
+  };
+  int cyc = 0;
+  enqueue_cycle(cyc);
+  for (;;) {
+    // one cycle ahead: queue cycle cyc + 1, then wait for cycle cyc's report
+    enqueue_cycle(cyc + 1);
+    DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
+    if (c.gm_report[cyc & 1].status != 0) break;
+    ++cyc;
   }
-  return st;
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (!comm) check_chain_err(c);
+  // every cycle queued after the stop left the state alone: the report of
+  // cycle cyc is final
+  const GmresReport& r = c.gm_report[cyc & 1];
+  ctl.last_step = unsigned(r.accumulated);
+  ctl.last_value = r.rho;
+  return r.status == 1 ? kSuccess : kFailure;
 }
 
 State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
