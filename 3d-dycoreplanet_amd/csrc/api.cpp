@@ -1743,6 +1743,18 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
   });
 }
 
+int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
+    Ctx& c = *ctx;
+    require(c.nse_assembled, DCP_ERR_STATE, "assemble_nse_system must run first");
+    require(!c.comm, DCP_ERR_UNSUPPORTED, "the Schur-complement solver runs on one GPU");
+    PhaseTimer t(c, &c.timings.solve_nse_ms);
+    return solve_nse_schur(c, schur_iterations, a_solves);
+  });
+}
+
 int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
   return guarded(ctx, [&] {
     need_ready(*ctx);

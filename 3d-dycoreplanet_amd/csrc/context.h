@@ -113,6 +113,19 @@ struct Ctx {
   // GPU): the operator form scatters B^T only and copies B from it
   DBuf<int32_t> B_tperm;
   bool B_transpose = false;
+  // Schur-complement solver: ILU(0) structure of the velocity block (built on
+  // first use) and its factor
+  struct Ilu {
+    DBuf<int32_t> ptr, col, diag, pos, lf_ptr, lf_rows, lb_ptr, lb_rows, p_img;
+    std::vector<int> lf_host;
+    DBuf<double> lu;
+    int n = 0, n_lf = 0, n_lb = 0, n_p_img = 0;
+    IluView view() const {
+      return IluView{n,         long(col.n), ptr.p,     col.p,      diag.p,    pos.p,
+                     n_lf,      n_lb,        lf_ptr.p,  lf_rows.p,  lb_ptr.p,  lb_rows.p};
+    }
+  } ilu;
+  std::vector<double*> sc_v, sc_p;  // Schur-complement solver work vectors (velocity / pressure)
   bool B_current = true;     // B_val holds the B block of the last assembly
   bool A_current = false;    // A_val holds the block of the last assembly
   PhysicsDev nse_ph{};       // physics (dt) of the last assemble_nse_system
@@ -307,6 +320,8 @@ void materialize_velocity_block(Ctx& c);
 void materialize_B(Ctx& c);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
+// solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414)
+int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves);
 int solve_temperature(Ctx& c, int* iters, double* T_range);
 void nse_vmult(Ctx& c, const double* src, double* dst);
 void velocity_vmult(Ctx& c, const double* src, double* dst);

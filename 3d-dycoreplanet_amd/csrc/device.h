@@ -233,6 +233,23 @@ void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, 
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
                            const int32_t* pmap, double* S_val, int max_row, hipStream_t s);
 
+// ---- ilu.hip ------------------------------------------------------------------
+// ILU(0) of nse_matrix.block(0,0) on its scalar pattern (Schur-complement
+// solver). ptr/col/diag: scalar CSR of the block-CSR A (pos[k]: A_val index of
+// entry k); lf_*: row levels of the factorisation / forward solve, lb_*: of
+// the backward solve.
+struct IluView {
+  int n;
+  long nnz;
+  const int32_t *ptr, *col, *diag, *pos;
+  int n_lf, n_lb;
+  const int32_t *lf_ptr, *lf_rows, *lb_ptr, *lb_rows;
+};
+void ilu_factor(const IluView& f, const double* A_val, const int* lf_host_ptr, double* lu,
+                hipStream_t s);
+void ilu_apply(const IluView& f, const double* lu, const double* b, double* x, hipStream_t s);
+void zero_at(int n, const int32_t* idx, double* x, hipStream_t s);
+
 // ---- linalg.hip -------------------------------------------------------------
 // y (=|+=) alpha * M x for block-CSR with R x C blocks (R,C in {1,3}).
 void spmv_bsr33(int rows, const int32_t* ptr, const int32_t* col, const double* val,

@@ -27,9 +27,9 @@ double recomputed_time_step(const dcp_run_params* rp, double cfl) {
 extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
                        dcp_step_callback cb, void* user, dcp_run_report* rep) {
   if (!ctx || !rp) return DCP_ERR_INVALID;
-  if (rp->use_schur_complement_solver)
-    return DCP_ERR_UNSUPPORTED;  // solve_NSE_Schur_complement (ILU): 2D / cube configs only
   const bool feec = rp->use_FEEC_solver != 0;
+  // solve_NSE_Schur_complement instead of the block preconditioner (:1896-1902)
+  const bool schur = !feec && rp->use_schur_complement_solver != 0;
   const int interval = std::max(1, rp->physics.nse_solver_interval);
   dcp_run_report r{};
   r.time_step = rp->physics.time_step;
@@ -58,7 +58,8 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
       } else {
         if ((rc = dcp_assemble_nse_system(ctx, DCP_ASSEMBLE_MATRIX | DCP_ASSEMBLE_RHS)) < 0)
           return rc;
-        if ((rc = dcp_build_nse_preconditioner(ctx)) < 0) return rc;
+        // no preconditioner with the Schur-complement solver (:1871-1881)
+        if (!schur && (rc = dcp_build_nse_preconditioner(ctx)) < 0) return rc;
       }
     }
     if ((rc = dcp_assemble_temperature_matrix(ctx)) < 0) return rc;
@@ -73,6 +74,9 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
         int it = 0;
         rc = dcp_feec_solve_nse(ctx, &it);
         r.fgmres_outer = it;
+      } else if (schur) {
+        int a_solves = 0;  // schur_inner: the Schur GMRES steps
+        rc = dcp_solve_nse_schur(ctx, &r.schur_inner, &a_solves);
       } else {
         rc = dcp_solve_nse(ctx, &r.fgmres_outer, &r.schur_inner);
       }

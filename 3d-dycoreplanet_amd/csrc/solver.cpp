@@ -55,12 +55,14 @@ constexpr int kSlotB = 259;
 constexpr int kSlotC = 260;
 constexpr int kSlotD = 261;
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
+constexpr int kSlotCg = 1296;    // 4: pcg's gh, d.h, alpha / beta, |g|^2
 constexpr int kHostPartials = 2048;
 // gmres_schur's pipelined Arnoldi steps: one block per step parity,
 // [0, 128) coefficients, kSpNStart, kSpNorm, ..., partials from kSpPart (device.h)
 constexpr int kSpecBase = 4096, kSpecStride = 1280;
 constexpr int kNumSlots = 8192;             // device slots, mirrored in c.hpinned
-static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kHostPartials, "slot layout");
+static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kSlotCg, "slot layout");
+static_assert(kSlotCg + 4 <= kHostPartials, "slot layout");
 static_assert(kHostPartials + kChainMaxBlocks <= kSpecBase - 512, "slot layout");
 static_assert(kSpPart + kChainMaxBlocks <= kSpecStride, "slot layout");
 static_assert(kSpecBase + 2 * kSpecStride <= kNumSlots, "slot layout");
@@ -1001,7 +1003,7 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
 }
 
 void free_workspaces(Ctx& c) {
-  for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v, &c.fe_v, &c.fe_s, &c.fe_n}) {
+  for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v, &c.fe_v, &c.fe_s, &c.fe_n, &c.sc_v, &c.sc_p}) {
     for (double* p : *pool) (void)hipFree(p);
     pool->clear();
   }
@@ -1078,6 +1080,217 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   if (outer) *outer = acc1 + acc2;
   if (inner_out) *inner_out = inner;
   return status;
+}
+
+namespace {
+
+// deal.II SolverCG with a preconditioner (the temperature solve's CG with P in
+// place of the Jacobi): g = A x - b, h = P g, d = -h, ... Work vectors
+// w[0..2] of n entries; scalars in the kSlotCg slots (their own, as the CG may
+// run inside another solver's operator).
+State pcg(Ctx& c, int n, Seg g, const Op& A, const Op& P, double* x, const double* b,
+          Control& ctl, double* const w[3]) {
+  double *gv = w[0], *d = w[1], *h = w[2];
+  const int sGh = kSlotCg, sDh = kSlotCg + 1, sAl = kSlotCg + 2, sRes = kSlotCg + 3;
+  const bool all_zero = dot_host(c, g, x, x, sRes) == 0.0;
+  if (!all_zero) {
+    A(x, gv);
+    axpy(n, DScal{nullptr, -1.0}, b, gv, c.stream);
+  } else {
+    equ(n, DScal{nullptr, -1.0}, b, gv, c.stream);
+  }
+  double res = std::sqrt(dot_host(c, g, gv, gv, sRes));
+  State conv = ctl.check(0, res);
+  int it = 0;
+  if (conv == kIterate) {
+    P(gv, h);
+    equ(n, DScal{nullptr, -1.0}, h, d, c.stream);
+    gdot(c, g, gv, h, sGh);
+    while (conv == kIterate) {
+      it++;
+      A(d, h);
+      gdot(c, g, d, h, sDh);
+      scalar_div(slot(c, sGh), slot(c, sDh), slot(c, sAl), c.stream);  // alpha = gh / dh
+      axpy(n, DScal{slot(c, sAl), 1.0}, d, x, c.stream);
+      add_and_dot_partials(g, gv, DScal{slot(c, sAl), 1.0}, h, gv, c.partials.p, c.stream);
+      allreduce(c, c.partials.p, kReduceBlocks);
+      reduce_final(kReduceBlocks, c.partials.p, slot(c, sRes), c.stream);
+      res = std::sqrt(std::fabs(fetch(c, sRes, 1)[0]));
+      conv = ctl.check(it, res);
+      if (conv != kIterate) break;
+      P(gv, h);
+      copy(1, slot(c, sGh), slot(c, sDh), c.stream);  // beta = old gh
+      gdot(c, g, gv, h, sGh);                         // new gh
+      scalar_div(slot(c, sGh), slot(c, sDh), slot(c, sAl), c.stream);
+      axpby(n, DScal{nullptr, -1.0}, h, DScal{slot(c, sAl), 1.0}, d, c.stream);  // d = beta d - h
+    }
+  }
+  return conv;
+}
+
+// ILU(0) structure of the velocity block: scalar CSR over the block-CSR A and
+// the dependency levels (built once per mesh)
+void build_ilu(Ctx& c) {
+  Ctx::Ilu& f = c.ilu;
+  if (f.n == c.n_u && f.ptr.p) return;
+  const int nb = c.nvo;
+  std::vector<int32_t> bp(nb + 1), bc;
+  DCP_HIP_CHECK(hipMemcpy(bp.data(), c.A_ptr.p, (nb + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
+  bc.resize(size_t(bp[nb]));
+  DCP_HIP_CHECK(hipMemcpy(bc.data(), c.A_col.p, bc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  const int n = 3 * nb;
+  std::vector<int32_t> ptr(n + 1, 0), col, pos, diag(n, -1);
+  col.reserve(size_t(9) * bc.size());
+  pos.reserve(size_t(9) * bc.size());
+  for (int r = 0; r < nb; ++r)
+    for (int ci = 0; ci < 3; ++ci) {
+      const int i = 3 * r + ci;
+      for (int k = bp[r]; k < bp[r + 1]; ++k)
+        for (int cj = 0; cj < 3; ++cj) {
+          const int j = 3 * bc[k] + cj;
+          if (j == i) diag[i] = int(col.size());
+          col.push_back(j);
+          pos.push_back(9 * k + 3 * ci + cj);
+        }
+      ptr[i + 1] = int(col.size());
+    }
+  for (int i = 0; i < n; ++i)
+    if (diag[i] < 0) throw std::runtime_error("Schur-complement ILU: missing diagonal entry");
+  // levels: forward (reads rows j < i), backward (rows j > i)
+  auto levels = [&](bool fwd, std::vector<int32_t>& lp, std::vector<int32_t>& rows) {
+    std::vector<int> lev(n, 0);
+    int nl = 0;
+    for (int t = 0; t < n; ++t) {
+      const int i = fwd ? t : n - 1 - t;
+      int l = 0;
+      if (fwd) {
+        for (int p = ptr[i]; p < diag[i]; ++p) l = std::max(l, lev[col[p]] + 1);
+      } else {
+        for (int p = diag[i] + 1; p < ptr[i + 1]; ++p) l = std::max(l, lev[col[p]] + 1);
+      }
+      lev[i] = l;
+      nl = std::max(nl, l + 1);
+    }
+    lp.assign(nl + 1, 0);
+    for (int i = 0; i < n; ++i) lp[lev[i] + 1]++;
+    for (int l = 0; l < nl; ++l) lp[l + 1] += lp[l];
+    rows.assign(n, 0);
+    std::vector<int32_t> fill(lp.begin(), lp.end() - 1);
+    for (int i = 0; i < n; ++i) rows[fill[lev[i]]++] = i;
+    return nl;
+  };
+  std::vector<int32_t> lfp, lfr, lbp, lbr;
+  f.n_lf = levels(true, lfp, lfr);
+  f.n_lb = levels(false, lbp, lbr);
+  f.ptr.upload(ptr);
+  f.col.upload(col);
+  f.diag.upload(diag);
+  f.pos.upload(pos);
+  f.lf_ptr.upload(lfp);
+  f.lf_rows.upload(lfr);
+  f.lb_ptr.upload(lbp);
+  f.lb_rows.upload(lbr);
+  f.lf_host = lfp;
+  f.lu.alloc(col.size());
+  f.n = n;
+  // constrained pressure dofs (periodic images), zeroed before the solve (:1290-1292)
+  std::vector<int32_t> pimg;
+  if (c.periodic && c.n_img_p > 0) {
+    pimg.resize(size_t(c.n_img_p));
+    DCP_HIP_CHECK(hipMemcpy(pimg.data(), c.img_p.p, pimg.size() * sizeof(int32_t),
+                            hipMemcpyDeviceToHost));
+  }
+  f.p_img.upload(pimg);
+  f.n_p_img = int(pimg.size());
+}
+
+}  // namespace
+
+int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
+  // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414), one GPU
+  if (c.comm) throw std::runtime_error("the Schur-complement solver runs on one GPU");
+  const int nu = c.n_u, np = c.n_p, n = nu + np;
+  const double dt = c.ph.dt;
+  materialize_velocity_block(c);  // A (and B) as assembled
+  materialize_B(c);
+  build_ilu(c);
+  Ctx::Ilu& f = c.ilu;
+  const IluView iv = f.view();
+  // inner_schur_preconditioner->initialize(nse_matrix.block(0,0)) (:1266-1269)
+  ilu_factor(iv, c.A_val.p, f.lf_host.data(), f.lu.p, c.stream);
+  const Seg gu = Seg::all(nu), gp = Seg::all(np);
+  ensure_pool(c.sc_v, 8, size_t(nu));
+  double* const cg_u[3] = {c.sc_v[0], c.sc_v[1], c.sc_v[2]};
+  double *tmp = c.sc_v[3], *t1 = c.sc_v[4], *t2 = c.sc_v[5];
+  ensure_pool(c.sc_p, 4, size_t(np));
+  double* const cg_p[3] = {c.sc_p[0], c.sc_p[1], c.sc_p[2]};
+  double* srhs = c.sc_p[3];
+  Op Av = [&](const double* x, double* y) {
+    spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
+  };
+  Op Pilu = [&](const double* x, double* y) { ilu_apply(iv, f.lu.p, x, y, c.stream); };
+  int n_inv = 0;
+  // InverseMatrix<A, ILU>::vmult (inverse_matrix.hpp:93-120): CG, tol 1e-6 |src|,
+  // max(n, 1000) steps, dst = 0, NoConvergence swallowed
+  auto inverse = [&](const double* src, double* dst) {
+    const double nrm = std::sqrt(dot_host(c, gu, src, src, kSlotA));
+    Control ctl{unsigned(std::max(nu, 1000)), 1e-6 * nrm};
+    fill(nu, 0.0, dst, c.stream);
+    ++n_inv;
+    (void)pcg(c, nu, gu, Av, Pilu, dst, src, ctl, cg_u);
+  };
+  DBuf<double> x;
+  x.alloc(n);
+  copy(n, c.nse_sol.p, x.p, c.stream);
+  scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);                 // :1283
+  zero_at(f.n_p_img, f.p_img.p, x.p, c.stream);                      // :1290-1292
+  // schur_rhs = B A^-1 f - g (:1319-1321)
+  inverse(c.nse_rhs.p, tmp);
+  spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, tmp, srhs, false, c.stream);
+  sadd(np, 1.0, -1.0, c.nse_rhs.p + nu, srhs, c.stream);
+  // SchurComplement::vmult (schur_complement.hpp:143-150): B A^-1 B^T
+  Op S = [&](const double* s, double* d) {
+    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, s, t1, false, c.stream);
+    inverse(t1, t2);
+    spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, t2, d, false, c.stream);
+  };
+  // ApproximateSchurComplement::vmult (approximate_schur_complement.hpp:131-139)
+  Op Sa = [&](const double* s, double* d) {
+    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, s, t1, false, c.stream);
+    ilu_apply(iv, f.lu.p, t1, t2, c.stream);
+    spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, t2, d, false, c.stream);
+  };
+  Op Id = [&](const double* s, double* d) { copy(np, s, d, c.stream); };
+  // ApproximateInverseMatrix<S~, identity>(n_iter = invalid) (approximate_inverse.hpp)
+  Op Pre = [&](const double* s, double* d) {
+    const double nrm = std::sqrt(dot_host(c, gp, s, s, kSlotA));
+    Control ctl{~0u, 1e-6 * nrm};
+    fill(np, 0.0, d, c.stream);
+    (void)pcg(c, np, gp, Sa, Id, d, s, ctl, cg_p);
+  };
+  // SolverGMRES (30 tmp vectors), SolverControl(nse_matrix.m(), 1e-6 |schur_rhs|)
+  const double rn = std::sqrt(dot_host(c, gp, srhs, srhs, kSlotA));
+  Control ctl{unsigned(n), 1e-6 * rn};
+  const State st = gmres(c, np, gp, S, &Pre, x.p + nu, srhs, ctl, c.sg_v, 30);
+  auto distribute = [&] {
+    distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);
+    if (c.periodic) {
+      copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
+      copy_images(c.n_img_p, c.img_p.p, c.mst_p.p, x.p, c.stream);
+    }
+  };
+  distribute();                                                       // :1353
+  // u = A^-1 (f - B^T p) (:1366-1372)
+  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, x.p + nu, tmp, false, c.stream);
+  sadd(nu, -1.0, 1.0, c.nse_rhs.p, tmp, c.stream);
+  inverse(tmp, x.p);
+  distribute();                                                       // :1378
+  scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);           // :1384
+  copy(n, x.p, c.nse_sol.p, c.stream);
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (schur_iterations) *schur_iterations = int(ctl.last_step);
+  if (a_solves) *a_solves = n_inv;
+  return st == kSuccess ? DCP_OK : DCP_NOT_CONVERGED;
 }
 
 namespace {

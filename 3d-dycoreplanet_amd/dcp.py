@@ -40,7 +40,7 @@ EXPORTED = [
     "dcp_set_physics", "dcp_set_time_step", "dcp_set_option", "dcp_mesh_upload", "dcp_mesh_check", "dcp_state_set",
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
-    "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_temperature",
+    "dcp_assemble_temperature_rhs", "dcp_solve_nse", "dcp_solve_nse_schur", "dcp_solve_temperature",
     "dcp_max_velocity", "dcp_cfl_number", "dcp_advance_state", "dcp_nse_vmult", "dcp_velocity_vmult", "dcp_mesh_geometry_info", "dcp_run",
     "dcp_schur_vmult", "dcp_block_preconditioner_vmult", "dcp_nse_matrix_export",
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
@@ -172,6 +172,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         getattr(lib, f).argtypes = [P]
     lib.dcp_assemble_nse_system.argtypes = [P, I]
     lib.dcp_solve_nse.argtypes = [P, C.POINTER(I), C.POINTER(I)]
+    lib.dcp_solve_nse_schur.argtypes = [P, C.POINTER(I), C.POINTER(I)]
     lib.dcp_solve_temperature.argtypes = [P, C.POINTER(I), D]
     lib.dcp_max_velocity.argtypes = [P, D]
     lib.dcp_cfl_number.argtypes = [P, D]
@@ -646,6 +647,12 @@ class Context:
     def solve_nse(self):
         o, i = C.c_int(0), C.c_int(0)
         rc = self._check(lib().dcp_solve_nse(self._h, C.byref(o), C.byref(i)), True)
+        return rc, o.value, i.value
+
+    def solve_nse_schur(self):
+        """solve_NSE_Schur_complement: (rc, Schur GMRES steps, A^-1 solves)."""
+        o, i = C.c_int(0), C.c_int(0)
+        rc = self._check(lib().dcp_solve_nse_schur(self._h, C.byref(o), C.byref(i)), True)
         return rc, o.value, i.value
 
     def solve_temperature(self):

@@ -218,6 +218,13 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx);
 /* solve_NSE_block_preconditioned (:1131-1245) incl. the NoConvergence
  * fallback; returns DCP_NOT_CONVERGED only if the fallback fails too. */
 int dcp_solve_nse(dcp_ctx* ctx, int* outer_iterations, int* inner_iterations);
+/* solve_NSE_Schur_complement (:1248-1414), the use_schur_complement_solver
+ * path (no build_nse_preconditioner): GMRES on B A^-1 B^T with A^-1 = CG +
+ * ILU(0) of A (InverseMatrix, LA::PreconditionILU), preconditioned by CG on
+ * B ILU^-1 B^T (ApproximateInverseMatrix of ApproximateSchurComplement), then
+ * u = A^-1 (f - B^T p). One GPU. schur_iterations: the Schur GMRES steps;
+ * a_solves: the A^-1 applications. DCP_NOT_CONVERGED if the GMRES fails. */
+int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves);
 /* solve_temperature (:1417-1476). T_range may be NULL or double[2]. */
 int dcp_solve_temperature(dcp_ctx* ctx, int* iterations, double* T_range);
 /* get_maximal_velocity / get_cfl_number (:1023-1101) on nse_solution. */
@@ -385,8 +392,8 @@ int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
  * rhs, the NSE and temperature solves, the callback (output_results; a
  * non-zero return stops), time_index += dt / interval, old_* = *; until
  * time_index > final_time or max_steps (> 0) steps. Returns DCP_NOT_CONVERGED
- * where the reference's solve throws. Not supported: the ILU Schur-complement
- * solver (use_schur_complement_solver, 2D / cube configs). */
+ * where the reference's solve throws. use_schur_complement_solver selects
+ * dcp_solve_nse_schur (one GPU). */
 typedef struct {
   int timestep_number, steps;       /* current step; steps completed */
   double time_index, time_step;     /* t at the step's start; dt */

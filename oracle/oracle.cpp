@@ -1233,6 +1233,190 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
 
 extern "C" long orc_a_solve_iterations(const orc_model* m) { return m->a_solve_iterations; }
 
+namespace {
+// y = block (rows [r0, r1), cols [c0, c1)) of A times x (x indexed from c0)
+void csr_block(const Csr& A, int r0, int r1, int c0, int c1, const double* x, double* y, bool add) {
+  for (int r = r0; r < r1; ++r) {
+    double acc = 0;
+    for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
+      if (A.cols[k] >= c0 && A.cols[k] < c1) acc += A.vals[k] * x[A.cols[k] - c0];
+    y[r - r0] = add ? y[r - r0] + acc : acc;
+  }
+}
+
+// LA::PreconditionILU (linear_algebra/preconditioner.h:40) =
+// TrilinosWrappers::PreconditionILU with its default AdditionalData
+// (ilu_fill 0, ilu_atol 0, ilu_rtol 1, overlap 0): ILU(0) of
+// nse_matrix.block(0,0) on its own pattern. Restated as the row-wise IKJ
+// elimination (l_ik = a_ik / u_kk in column order k, then a_ij -= l_ik u_kj on
+// the pattern of row i); apply: unit-lower forward, upper backward (column
+// order sums, division by u_ii). Ifpack's CrsRiluk is not in this image, so
+// the operation order against Trilinos is unpinned.
+struct Ilu0 {
+  int n = 0;
+  std::vector<int> ptr, col, diag;
+  std::vector<double> val;
+  void factor(const Csr& A, int rows) {
+    n = rows;
+    ptr.assign(n + 1, 0);
+    col.clear();
+    val.clear();
+    for (int r = 0; r < n; ++r) {
+      for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
+        if (A.cols[k] < n) {
+          col.push_back(A.cols[k]);
+          val.push_back(A.vals[k]);
+        }
+      ptr[r + 1] = int(col.size());
+    }
+    diag.assign(n, -1);
+    for (int r = 0; r < n; ++r)
+      for (int k = ptr[r]; k < ptr[r + 1]; ++k)
+        if (col[k] == r) diag[r] = k;
+    for (int i = 0; i < n; ++i) {
+      for (int p = ptr[i]; p < ptr[i + 1] && col[p] < i; ++p) {
+        const int k = col[p];
+        val[p] /= val[diag[k]];
+        const double lik = val[p];
+        int r = p + 1;
+        for (int q = diag[k] + 1; q < ptr[k + 1]; ++q) {
+          while (r < ptr[i + 1] && col[r] < col[q]) ++r;
+          if (r == ptr[i + 1]) break;
+          if (col[r] == col[q]) val[r] -= lik * val[q];
+        }
+      }
+    }
+  }
+  void apply(const double* b, double* x) const {
+    for (int i = 0; i < n; ++i) {
+      double s = b[i];
+      for (int p = ptr[i]; p < diag[i]; ++p) s -= val[p] * x[col[p]];
+      x[i] = s;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = x[i];
+      for (int p = diag[i] + 1; p < ptr[i + 1]; ++p) s -= val[p] * x[col[p]];
+      x[i] = s / val[diag[i]];
+    }
+  }
+};
+
+// deal.II SolverCG with a preconditioner; throws NoConvergence
+template <class OpA, class OpP>
+void pcg(int n, OpA A, OpP P, double* x, const double* b, Control& ctl) {
+  std::vector<double> g(n), d(n), h(n);
+  bool all_zero = true;
+  for (int i = 0; i < n; ++i) all_zero &= (x[i] == 0.0);
+  if (!all_zero) {
+    A(x, g.data());
+    for (int i = 0; i < n; ++i) g[i] += -1. * b[i];
+  } else {
+    for (int i = 0; i < n; ++i) g[i] = -1. * b[i];
+  }
+  double res = std::sqrt(dotv(g.data(), g.data(), n));
+  State conv = ctl.check(0, res);
+  if (conv == kIterate) {
+    P(g.data(), h.data());
+    for (int i = 0; i < n; ++i) d[i] = -1. * h[i];
+    double gh = dotv(g.data(), h.data(), n);
+    int it = 0;
+    while (conv == kIterate) {
+      it++;
+      A(d.data(), h.data());
+      double alpha = dotv(d.data(), h.data(), n);
+      alpha = gh / alpha;
+      for (int i = 0; i < n; ++i) x[i] += alpha * d[i];
+      double gg = 0;
+      for (int i = 0; i < n; ++i) {
+        g[i] += alpha * h[i];
+        gg += g[i] * g[i];
+      }
+      res = std::sqrt(std::fabs(gg));
+      conv = ctl.check(it, res);
+      if (conv != kIterate) break;
+      P(g.data(), h.data());
+      double beta = gh;
+      gh = dotv(g.data(), h.data(), n);
+      beta = gh / beta;
+      for (int i = 0; i < n; ++i) d[i] = beta * d[i] - h[i];
+    }
+  }
+  if (conv != kSuccess) throw NoConvergence();
+}
+}  // namespace
+
+extern "C" int orc_solve_nse_schur(orc_model* m, double* sol, int* schur_iterations,
+                                   int* a_solves) {
+  // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414)
+  const int nu = m->n_u, np = m->n_p, n = nu + np;
+  const double dt = m->ph.time_step;
+  const Csr& M = m->nse;
+  Ilu0 ilu;
+  ilu.factor(M, nu);  // inner_schur_preconditioner->initialize(block(0,0))
+  auto A = [&](const double* x, double* y) { csr_block(M, 0, nu, 0, nu, x, y, false); };
+  auto P = [&](const double* x, double* y) { ilu.apply(x, y); };
+  int n_inv = 0;
+  // InverseMatrix<A, ILU>::vmult (inverse_matrix.hpp:93-120): CG, tol 1e-6 |src|,
+  // max(n, 1000) steps, dst = 0, NoConvergence swallowed
+  auto inverse = [&](const double* src, double* dst) {
+    Control ctl{unsigned(std::max(nu, 1000)), 1e-6 * std::sqrt(dotv(src, src, nu))};
+    std::fill(dst, dst + nu, 0.0);
+    ++n_inv;
+    try {
+      pcg(nu, A, P, dst, src, ctl);
+    } catch (const NoConvergence&) {
+    }
+  };
+  std::vector<double> x(sol, sol + n), tmp(nu), t1(nu), t2(nu), srhs(np);
+  for (int i = nu; i < n; ++i) x[i] *= dt;                                  // :1283
+  for (int i = nu; i < n; ++i) if (m->cnse.constrained(i)) x[i] = 0;       // :1290-1292
+  // schur_rhs = B A^-1 f - g (:1319-1321)
+  inverse(m->nse_rhs.data(), tmp.data());
+  csr_block(M, nu, n, 0, nu, tmp.data(), srhs.data(), false);
+  for (int i = 0; i < np; ++i) srhs[i] -= m->nse_rhs[nu + i];
+  // SchurComplement::vmult (schur_complement.hpp:143-150): B A^-1 B^T
+  auto S = [&](const double* s, double* d) {
+    csr_block(M, 0, nu, nu, n, s, t1.data(), false);
+    inverse(t1.data(), t2.data());
+    csr_block(M, nu, n, 0, nu, t2.data(), d, false);
+  };
+  // ApproximateSchurComplement::vmult (approximate_schur_complement.hpp:131-139): B ILU^-1 B^T
+  auto Sa = [&](const double* s, double* d) {
+    csr_block(M, 0, nu, nu, n, s, t1.data(), false);
+    ilu.apply(t1.data(), t2.data());
+    csr_block(M, nu, n, 0, nu, t2.data(), d, false);
+  };
+  auto identity = [&](const double* s, double* d) { std::copy(s, s + np, d); };
+  // ApproximateInverseMatrix<S~, identity>(n_iter = invalid): CG, tol 1e-6 |src|
+  auto precond = [&](const double* s, double* d) {
+    Control ctl{~0u, 1e-6 * std::sqrt(dotv(s, s, np))};
+    std::fill(d, d + np, 0.0);
+    try {
+      pcg(np, Sa, identity, d, s, ctl);
+    } catch (const NoConvergence&) {
+    }
+  };
+  // SolverGMRES (30 tmp vectors), SolverControl(nse_matrix.m(), 1e-6 |schur_rhs|)
+  Control ctl{unsigned(n), 1e-6 * std::sqrt(dotv(srhs.data(), srhs.data(), np))};
+  int its = 0, rc = 0;
+  try {
+    gmres(np, S, precond, x.data() + nu, srhs.data(), ctl, its);
+  } catch (const NoConvergence&) {
+    rc = 1;
+  }
+  m->cnse.distribute(x.data());                                             // :1353
+  // u = A^-1 (f - B^T p) (:1366-1372)
+  csr_block(M, 0, nu, nu, n, x.data() + nu, tmp.data(), false);
+  for (int i = 0; i < nu; ++i) tmp[i] = -1. * tmp[i] + m->nse_rhs[i];
+  inverse(tmp.data(), x.data());
+  m->cnse.distribute(x.data());                                             // :1378
+  for (int i = nu; i < n; ++i) x[i] /= dt;                                 // :1384
+  std::copy(x.begin(), x.end(), sol);
+  if (schur_iterations) *schur_iterations = int(ctl.last_step);
+  if (a_solves) *a_solves = n_inv;
+  return rc;
+}
+
 extern "C" int orc_solve_temperature(orc_model* m, double* T, int* iterations) {
   // solve_temperature (:1417-1476): SolverCG + Jacobi, tol 1e-12 ||rhs||, max n_T
   const int n = m->n_T;
@@ -1704,16 +1888,6 @@ extern "C" void orc_feec_T_rhs(const orc_feec* m, double* out) {
   std::copy(m->T_rhs.begin(), m->T_rhs.end(), out);
 }
 
-namespace {
-void csr_block(const Csr& A, int r0, int r1, int c0, int c1, const double* x, double* y, bool add) {
-  for (int r = r0; r < r1; ++r) {
-    double acc = 0;
-    for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
-      if (A.cols[k] >= c0 && A.cols[k] < c1) acc += A.vals[k] * x[A.cols[k] - c0];
-    y[r - r0] = add ? y[r - r0] + acc : acc;
-  }
-}
-}  // namespace
 
 extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
   // solve_NSE_block_preconditioned (FEEC.tpp:1268-1477), block preconditioner on

@@ -115,6 +115,11 @@ void orc_block_preconditioner_vmult(orc_model* m, const double* src, double* dst
 int orc_solve_nse(orc_model* m, double* nse_solution /*inout*/, int* outer_iterations,
                   int* inner_iterations, int max_outer /* 40 in the reference */);
 int orc_solve_temperature(orc_model* m, double* T_solution /*inout*/, int* iterations);
+/* solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414): GMRES on
+ * B A^-1 B^T (A^-1: CG + ILU(0)) preconditioned by CG on B ILU^-1 B^T, then
+ * u = A^-1 (f - B^T p). Returns 1 on NoConvergence of the Schur GMRES. */
+int orc_solve_nse_schur(orc_model* m, double* nse_solution /*inout*/, int* schur_iterations,
+                        int* a_solves);
 /* AztecOO A-GMRES iterations of the last orc_solve_nse (do_solve_A fallback). */
 long orc_a_solve_iterations(const orc_model* m);
 

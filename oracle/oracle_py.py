@@ -67,6 +67,7 @@ def lib():
         L.orc_block_preconditioner_vmult.argtypes = [P, P, P, I, P]
         L.orc_solve_nse.argtypes = [P, P, P, P, I]
         L.orc_solve_temperature.argtypes = [P, P, P]
+        L.orc_solve_nse_schur.argtypes = [P, P, P, P]
         L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
         L.orc_set_inner_max_steps.argtypes = [P, I]
         L.orc_a_solve_iterations.argtypes = [P]
@@ -242,6 +243,13 @@ class Model:
         it = C.c_int(0)
         rc = lib().orc_solve_temperature(self.h, _p(x), C.byref(it))
         return rc, x, it.value
+
+    def solve_nse_schur(self, sol):
+        """solve_NSE_Schur_complement: (rc, solution, Schur GMRES steps, A^-1 solves)."""
+        x = np.array(sol, dtype=np.float64, copy=True)
+        it, na = C.c_int(0), C.c_int(0)
+        rc = lib().orc_solve_nse_schur(self.h, _p(x), C.byref(it), C.byref(na))
+        return rc, x, it.value, na.value
 
     def max_velocity(self, sol):
         return lib().orc_max_velocity(self.h, _p(np.ascontiguousarray(sol, np.float64)))
