@@ -51,41 +51,33 @@ __global__ void k_ilu_factor(int nrows, const int32_t* __restrict__ rows,
 }
 
 // x = U^-1 L^-1 b: forward over the lower levels (unit diagonal), backward over
-// the upper ones. A level holds a handful of rows (the dependency chains of
-// ILU(0) on this pattern are long: ~2,000 levels for 10 k rows), so each row
-// gets a wave: lane-strided partial sums of the row, a fixed butterfly, lane 0
-// writes (deterministic; rounding differs from the oracle's column-order sums).
+// the upper ones, each row's sum in column order (the oracle's order: the
+// nested 1e-6 solves amplify any other rounding to ~1e-10 of the result; a
+// wave per row with a butterfly sum measured 1.2e-10 against the oracle).
+// The dependency chains of ILU(0) on this pattern are long (~2,000 levels for
+// 10 k rows), so the solve is latency-bound whatever the row mapping.
 constexpr int kIluThreads = 1024;
-constexpr int kIluWaves = kIluThreads / 64;
-__device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 __global__ __launch_bounds__(kIluThreads) void k_ilu_solve(
     int n_lf, const int32_t* __restrict__ lf_ptr, const int32_t* __restrict__ lf_rows, int n_lb,
     const int32_t* __restrict__ lb_ptr, const int32_t* __restrict__ lb_rows,
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ diag, const double* __restrict__ lu, const double* __restrict__ b,
     double* x) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int l = 0; l < n_lf; ++l) {
-    for (int t = lf_ptr[l] + wave; t < lf_ptr[l + 1]; t += kIluWaves) {
+    for (int t = lf_ptr[l] + threadIdx.x; t < lf_ptr[l + 1]; t += kIluThreads) {
       const int i = lf_rows[t];
-      double s = 0.0;
-      for (int p = ptr[i] + lane; p < diag[i]; p += 64) s += lu[p] * x[col[p]];
-      s = wave_sum(s);
-      if (lane == 0) x[i] = b[i] - s;
+      double s = b[i];
+      for (int p = ptr[i]; p < diag[i]; ++p) s -= lu[p] * x[col[p]];
+      x[i] = s;
     }
     __syncthreads();
   }
   for (int l = 0; l < n_lb; ++l) {
-    for (int t = lb_ptr[l] + wave; t < lb_ptr[l + 1]; t += kIluWaves) {
+    for (int t = lb_ptr[l] + threadIdx.x; t < lb_ptr[l + 1]; t += kIluThreads) {
       const int i = lb_rows[t];
-      double s = 0.0;
-      for (int p = diag[i] + 1 + lane; p < ptr[i + 1]; p += 64) s += lu[p] * x[col[p]];
-      s = wave_sum(s);
-      if (lane == 0) x[i] = (x[i] - s) / lu[diag[i]];
+      double s = x[i];
+      for (int p = diag[i] + 1; p < ptr[i + 1]; ++p) s -= lu[p] * x[col[p]];
+      x[i] = s / lu[diag[i]];
     }
     __syncthreads();
   }
