@@ -1465,6 +1465,13 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       }
       c.mf_vorder.upload(vorder);
       c.mf_porder.upload(porder);
+      {
+        // 64-position blocks of the gather order that hold a constrained node
+        std::vector<uint8_t> wcon((size_t(nv) + 63) / 64, 0);
+        for (int i = 0; i < nv; ++i)
+          if (cidx[size_t(vorder[i])] >= 0) wcon[size_t(i) >> 6] = 1;
+        c.mf_wcon.upload(wcon);
+      }
       if (!c.mf_stream) {
         DCP_HIP_CHECK(hipStreamCreateWithFlags(&c.mf_stream, hipStreamNonBlocking));
         for (auto& ev : c.mf_chunk_ev)

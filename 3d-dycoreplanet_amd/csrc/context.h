@@ -161,7 +161,7 @@ struct Ctx {
   DBuf<double> mf_buf;  // dof-sorted partial sums (velocity: one per node and cell group)
   DBuf<uint32_t> mf_cmask;
   DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx, mf_vorder, mf_porder;
-  DBuf<uint8_t> mf_vnext;
+  DBuf<uint8_t> mf_vnext, mf_wcon;
   int32_t mf_pbase = 0;
   // chunked apply (DCP_MF_CHUNKS > 1 at upload): the gather of chunk k's
   // finished dofs runs on mf_stream while the pencil kernel works chunk k + 1.
@@ -183,9 +183,12 @@ struct Ctx {
                    mf_colgeo.p, mf_layer.p, mf_laygeo.p};
   }
   MfGather mfg() const {
-    return MfGather{n_vnodes,  n_p,      n_u,       mf_vorder.p, mf_porder.p,
+    // one chunk: the gather order is the identity (no order arrays read)
+    return MfGather{n_vnodes,  n_p,      n_u,       mf_chunks > 1 ? mf_vorder.p : nullptr,
+                    mf_chunks > 1 ? mf_porder.p : nullptr,
                     mf_vptr.p, mf_pptr.p, mf_pbase, mf_cidx.p,   vcon.p,
-                    con_diag.p, periodic ? pcidx.p : nullptr, con_diag.p + 3 * size_t(n_con)};
+                    con_diag.p, periodic ? pcidx.p : nullptr, con_diag.p + 3 * size_t(n_con),
+                    mf_wcon.p};
   }
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};

@@ -165,6 +165,9 @@ struct MfGather {
   const double* cdiag;         // [n_con_nodes][3] assembled diagonal (NseOut::cdiag)
   const int32_t* pcidx;        // [n_p] identified pressure dof index or -1 (null: none)
   const double* pcdiag;        // their assembled diagonal
+  // [ceil(n_vnodes / 64)]: 1 if positions [64 b, 64 b + 64) hold a
+  // constrained node (null: always look cidx up)
+  const uint8_t* wcon;
 };
 // cells per wave of k_mf_pencil = the cell group of the velocity partial sums
 constexpr int kMfGroupCells = 7;

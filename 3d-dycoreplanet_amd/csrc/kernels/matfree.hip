@@ -863,9 +863,12 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 // then C^T and the constrained diagonal. One wave per 64 consecutive dofs: the
 // runs of those dofs form one contiguous span, which the wave loads
 // cooperatively (coalesced) into LDS; each lane then adds its own run.
-constexpr int kGatherWaves = 4;
+#ifndef DCP_MF_GWAVES
+#define DCP_MF_GWAVES 4
+#endif
+constexpr int kGatherWaves = DCP_MF_GWAVES;
 #ifndef DCP_MF_GSPAN
-#define DCP_MF_GSPAN 768
+#define DCP_MF_GSPAN 512  // 64 nodes x ~2.1 wave partials x 3 (r=5: 768 -> 512, 34.8 -> 32.0 us)
 #endif
 constexpr int kGvSpan = DCP_MF_GSPAN;  // doubles per wave window (longer spans: direct reads)
 template <bool STOKES>
@@ -890,7 +893,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     wsync();
     const int pos = n0 + lane;
     if (pos >= n1) return;
-    const int i = g.vorder[pos];
+    const int i = g.vorder ? g.vorder[pos] : pos;
     const int k0 = g.vptr[pos] - s0, k1 = g.vptr[pos + 1] - s0;
     double s[3] = {0.0, 0.0, 0.0};
     if (fits) {
@@ -906,7 +909,9 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
         s[2] += b[3 * k + 2];
       }
     }
-    const int ci = g.cidx[i];
+    // the cidx lookup only where the wave's positions hold a constrained node
+    const bool maybe = !g.wcon || g.wcon[n0 >> 6] || g.wcon[(n1 - 1) >> 6];
+    const int ci = maybe ? g.cidx[i] : -1;
     if (ci >= 0) {
       const NodeConstraint nc = g.vcon[i];
       condense(nc, s);
@@ -932,7 +937,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     wsync();
     const int pos = j0 + lane;
     if (pos >= j1) return;
-    const int j = g.porder[pos];
+    const int j = g.porder ? g.porder[pos] : pos;
     const int k0 = g.pptr[pos] - s0, k1 = g.pptr[pos + 1] - s0;
     double s = 0.0;
     if (fits)
