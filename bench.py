@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
 PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_sell16_r5.json", "k_sell_spmv<true, true>")}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
-PMC_MF = {5: ("profiles/r01_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
+PMC_MF = {5: ("profiles/r02_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
 
 
 def pmc_mf_traffic(refine):
