@@ -119,7 +119,7 @@ struct Ctx {
     DBuf<int32_t> ptr, col, diag, pos, lf_ptr, lf_rows, lb_ptr, lb_rows, p_img;
     std::vector<int> lf_host;
     DBuf<double> lu;
-    int n = 0, n_lf = 0, n_lb = 0, n_p_img = 0;
+    int n = 0, n_lf = 0, n_lb = 0, n_p_img = 0, max_row = 0;
     IluView view() const {
       return IluView{n,         long(col.n), ptr.p,     col.p,      diag.p,    pos.p,
                      n_lf,      n_lb,        lf_ptr.p,  lf_rows.p,  lb_ptr.p,  lb_rows.p};

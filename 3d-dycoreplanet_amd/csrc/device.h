@@ -248,8 +248,9 @@ struct IluView {
   int n_lf, n_lb;
   const int32_t *lf_ptr, *lf_rows, *lb_ptr, *lb_rows;
 };
+// max_row: the longest scalar row (a wave per row staged in LDS up to 512)
 void ilu_factor(const IluView& f, const double* A_val, const int* lf_host_ptr, double* lu,
-                hipStream_t s);
+                int max_row, hipStream_t s);
 void ilu_apply(const IluView& f, const double* lu, const double* b, double* x, hipStream_t s);
 void zero_at(int n, const int32_t* idx, double* x, hipStream_t s);
 

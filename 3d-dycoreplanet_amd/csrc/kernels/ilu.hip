@@ -50,34 +50,89 @@ __global__ void k_ilu_factor(int nrows, const int32_t* __restrict__ rows,
   }
 }
 
+// The same elimination with a wave per row (rows of up to kIluRowMax
+// entries): the row is staged in LDS; for each k of its lower part in column
+// order the lanes split row k's upper entries, each finding its column in the
+// row by binary search. Every entry receives its updates in k order with the
+// same arithmetic as the one-thread form (bitwise the same factor).
+constexpr int kIluRowMax = 512;
+__device__ inline void wsync64() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(64) void k_ilu_factor_wave(int nrows, const int32_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ ptr,
+                                                        const int32_t* __restrict__ col,
+                                                        const int32_t* __restrict__ diag,
+                                                        double* __restrict__ lu) {
+  __shared__ double rv[kIluRowMax];
+  __shared__ int rc[kIluRowMax];
+  const int t = blockIdx.x;
+  if (t >= nrows) return;
+  const int lane = threadIdx.x;
+  const int i = rows[t];
+  const int b = ptr[i], len = ptr[i + 1] - b;
+  for (int j = lane; j < len; j += 64) {
+    rv[j] = lu[b + j];
+    rc[j] = col[b + j];
+  }
+  wsync64();
+  for (int pj = 0; pj < len && rc[pj] < i; ++pj) {
+    const int k = rc[pj];
+    const double lik = rv[pj] / lu[diag[k]];
+    wsync64();  // every lane has read rv[pj]
+    if (lane == 0) rv[pj] = lik;
+    for (int q = diag[k] + 1 + lane; q < ptr[k + 1]; q += 64) {
+      const int cq = col[q];
+      int lo = pj + 1, hi = len;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (rc[m] < cq) lo = m + 1; else hi = m;
+      }
+      if (lo < len && rc[lo] == cq) rv[lo] -= lik * lu[q];
+    }
+    wsync64();
+  }
+  for (int j = lane; j < len; j += 64) lu[b + j] = rv[j];
+}
+
 // x = U^-1 L^-1 b: forward over the lower levels (unit diagonal), backward over
-// the upper ones, each row's sum in column order (the oracle's order: the
-// nested 1e-6 solves amplify any other rounding to ~1e-10 of the result; a
-// wave per row with a butterfly sum measured 1.2e-10 against the oracle).
-// The dependency chains of ILU(0) on this pattern are long (~2,000 levels for
-// 10 k rows), so the solve is latency-bound whatever the row mapping.
+// the upper ones. The dependency chains of ILU(0) on this pattern are long
+// (~2,000 levels for 10 k rows, a handful of rows each), so each row gets a
+// wave: 64 lane-strided partial sums combined by an xor butterfly, the order
+// the oracle's restatement uses too (oracle.cpp row_sum64).
 constexpr int kIluThreads = 1024;
+constexpr int kIluWaves = kIluThreads / 64;
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 __global__ __launch_bounds__(kIluThreads) void k_ilu_solve(
     int n_lf, const int32_t* __restrict__ lf_ptr, const int32_t* __restrict__ lf_rows, int n_lb,
     const int32_t* __restrict__ lb_ptr, const int32_t* __restrict__ lb_rows,
     const int32_t* __restrict__ ptr, const int32_t* __restrict__ col,
     const int32_t* __restrict__ diag, const double* __restrict__ lu, const double* __restrict__ b,
     double* x) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int l = 0; l < n_lf; ++l) {
-    for (int t = lf_ptr[l] + threadIdx.x; t < lf_ptr[l + 1]; t += kIluThreads) {
+    for (int t = lf_ptr[l] + wave; t < lf_ptr[l + 1]; t += kIluWaves) {
       const int i = lf_rows[t];
-      double s = b[i];
-      for (int p = ptr[i]; p < diag[i]; ++p) s -= lu[p] * x[col[p]];
-      x[i] = s;
+      double s = 0.0;
+      for (int p = ptr[i] + lane; p < diag[i]; p += 64) s += lu[p] * x[col[p]];
+      s = wave_sum(s);
+      if (lane == 0) x[i] = b[i] - s;
     }
     __syncthreads();
   }
   for (int l = 0; l < n_lb; ++l) {
-    for (int t = lb_ptr[l] + threadIdx.x; t < lb_ptr[l + 1]; t += kIluThreads) {
+    for (int t = lb_ptr[l] + wave; t < lb_ptr[l + 1]; t += kIluWaves) {
       const int i = lb_rows[t];
-      double s = x[i];
-      for (int p = diag[i] + 1; p < ptr[i + 1]; ++p) s -= lu[p] * x[col[p]];
-      x[i] = s / lu[diag[i]];
+      double s = 0.0;
+      for (int p = diag[i] + 1 + lane; p < ptr[i + 1]; p += 64) s += lu[p] * x[col[p]];
+      s = wave_sum(s);
+      if (lane == 0) x[i] = (x[i] - s) / lu[diag[i]];
     }
     __syncthreads();
   }
@@ -91,7 +146,7 @@ __global__ void k_zero_at(int n, const int32_t* __restrict__ idx, double* __rest
 }  // namespace
 
 void ilu_factor(const IluView& f, const double* A_val, const int* lf_host_ptr, double* lu,
-                hipStream_t s) {
+                int max_row, hipStream_t s) {
   if (f.nnz > 0) {
     const long g = std::min<long>((f.nnz + 255) / 256, 4096);
     hipLaunchKernelGGL(k_ilu_load, dim3(unsigned(g)), dim3(256), 0, s, f.nnz, f.pos, A_val, lu);
@@ -99,8 +154,12 @@ void ilu_factor(const IluView& f, const double* A_val, const int* lf_host_ptr, d
   }
   for (int l = 0; l < f.n_lf; ++l) {
     const int nr = lf_host_ptr[l + 1] - lf_host_ptr[l];
-    hipLaunchKernelGGL(k_ilu_factor, dim3((nr + 63) / 64), dim3(64), 0, s, nr,
-                       f.lf_rows + lf_host_ptr[l], f.ptr, f.col, f.diag, lu);
+    if (max_row <= kIluRowMax)
+      hipLaunchKernelGGL(k_ilu_factor_wave, dim3(nr), dim3(64), 0, s, nr,
+                         f.lf_rows + lf_host_ptr[l], f.ptr, f.col, f.diag, lu);
+    else
+      hipLaunchKernelGGL(k_ilu_factor, dim3((nr + 63) / 64), dim3(64), 0, s, nr,
+                         f.lf_rows + lf_host_ptr[l], f.ptr, f.col, f.diag, lu);
     DCP_HIP_CHECK(hipGetLastError());
   }
 }

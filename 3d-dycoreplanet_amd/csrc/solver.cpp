@@ -1191,6 +1191,8 @@ void build_ilu(Ctx& c) {
   f.lb_ptr.upload(lbp);
   f.lb_rows.upload(lbr);
   f.lf_host = lfp;
+  f.max_row = 0;
+  for (int i = 0; i < n; ++i) f.max_row = std::max(f.max_row, ptr[i + 1] - ptr[i]);
   f.lu.alloc(col.size());
   f.n = n;
   // constrained pressure dofs (periodic images), zeroed before the solve (:1290-1292)
@@ -1217,7 +1219,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   Ctx::Ilu& f = c.ilu;
   const IluView iv = f.view();
   // inner_schur_preconditioner->initialize(nse_matrix.block(0,0)) (:1266-1269)
-  ilu_factor(iv, c.A_val.p, f.lf_host.data(), f.lu.p, c.stream);
+  ilu_factor(iv, c.A_val.p, f.lf_host.data(), f.lu.p, f.max_row, c.stream);
   const Seg gu = Seg::all(nu), gp = Seg::all(np);
   ensure_pool(c.sc_v, 8, size_t(nu));
   double* const cg_u[3] = {c.sc_v[0], c.sc_v[1], c.sc_v[2]};

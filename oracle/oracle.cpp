@@ -1249,9 +1249,25 @@ void csr_block(const Csr& A, int r0, int r1, int c0, int c1, const double* x, do
 // (ilu_fill 0, ilu_atol 0, ilu_rtol 1, overlap 0): ILU(0) of
 // nse_matrix.block(0,0) on its own pattern. Restated as the row-wise IKJ
 // elimination (l_ik = a_ik / u_kk in column order k, then a_ij -= l_ik u_kj on
-// the pattern of row i); apply: unit-lower forward, upper backward (column
-// order sums, division by u_ii). Ifpack's CrsRiluk is not in this image, so
-// the operation order against Trilinos is unpinned.
+// the pattern of row i); apply: unit-lower forward, upper backward (division
+// by u_ii), a row summed as 64 lane-strided partial sums combined by an xor
+// butterfly (the device's wave-per-row order). Ifpack's CrsRiluk is not in
+// this image, so the operation order against Trilinos is unpinned.
+double row_sum64(const std::vector<double>& val, const std::vector<int>& col, int b, int e,
+                 const double* x) {
+  double v[64];
+  for (int l = 0; l < 64; ++l) {
+    v[l] = 0.0;
+    for (int p = b + l; p < e; p += 64) v[l] += val[p] * x[col[p]];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    double w[64];
+    for (int l = 0; l < 64; ++l) w[l] = v[l] + v[l ^ o];
+    for (int l = 0; l < 64; ++l) v[l] = w[l];
+  }
+  return v[0];
+}
+
 struct Ilu0 {
   int n = 0;
   std::vector<int> ptr, col, diag;
@@ -1288,16 +1304,9 @@ struct Ilu0 {
     }
   }
   void apply(const double* b, double* x) const {
-    for (int i = 0; i < n; ++i) {
-      double s = b[i];
-      for (int p = ptr[i]; p < diag[i]; ++p) s -= val[p] * x[col[p]];
-      x[i] = s;
-    }
-    for (int i = n - 1; i >= 0; --i) {
-      double s = x[i];
-      for (int p = diag[i] + 1; p < ptr[i + 1]; ++p) s -= val[p] * x[col[p]];
-      x[i] = s / val[diag[i]];
-    }
+    for (int i = 0; i < n; ++i) x[i] = b[i] - row_sum64(val, col, ptr[i], diag[i], x);
+    for (int i = n - 1; i >= 0; --i)
+      x[i] = (x[i] - row_sum64(val, col, diag[i] + 1, ptr[i + 1], x)) / val[diag[i]];
   }
 };
 

@@ -1,0 +1,37 @@
+"""BASELINE C2 on one GPU: the cube prm (classic model: use FEEC solver =
+false, nse velocity degree = 2, refine 3), one reference time step through
+dcp_run, which the prm sends through the ILU Schur-complement solver. Prints
+one JSON line with the phase timings and iteration counts."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "3d-dycoreplanet_amd"))
+import numpy as np  # noqa: E402
+import dcp  # noqa: E402
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+rp = dcp.load_prm(os.path.join(ROOT, "configs", "aqua_planet_cube_test_3d.prm"))
+rp.use_FEEC_solver = 0
+rp.nse_velocity_degree = 2
+refine = int(os.environ.get("REFINE", "3"))
+ph = dcp.physics_from_params(rp)
+m = dcp.HostMesh(cuboid=True, refine=refine, length=rp.length)
+ctx = dcp.Context()
+ctx.set_physics(ph)
+ctx.upload_mesh(m)
+z = np.zeros(m.n_u + m.n_p)
+for f, v in ((dcp.OLD_NSE_SOLUTION, z), (dcp.NSE_SOLUTION, z), (dcp.OLD_T_SOLUTION, m.T0),
+             (dcp.T_SOLUTION, m.T0)):
+    ctx.set_state(f, v)
+t0 = time.perf_counter()
+rc, rep, steps = ctx.run(rp, max_steps=1)
+wall = time.perf_counter() - t0
+print(json.dumps({"config": "BASELINE C2: aqua_planet_cube_test_3d.prm, classic Q2/Q1, refine %d"
+                  % refine, "n_cells": m.n_cells, "n_u": m.n_u, "n_p": m.n_p, "n_T": m.n_T,
+                  "rc": rc, "steps": rep.steps, "schur_gmres_iterations": rep.schur_inner,
+                  "T_cg_iterations": rep.T_cg, "step_wall_s": wall,
+                  "phase_ms": ctx.timings()}), flush=True)
+ctx.close()
