@@ -18,6 +18,7 @@
 #include "mesh.h"
 #include "partition.h"
 #include "prm.h"
+#include "renumber.h"
 
 using namespace dcp;
 
@@ -2428,6 +2429,7 @@ struct dcp_host_mesh {
   Constraints nse, T;
   TemperatureDofs tdofs;
   std::vector<int32_t> cell_nse;
+  std::vector<double> nse_xyz;     // support point of each velocity node once renumbered
   std::unique_ptr<FeecDofs> feec;  // built on first request
 };
 
@@ -2453,6 +2455,27 @@ dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1
 
 void dcp_host_mesh_destroy(dcp_host_mesh* m) { delete m; }
 
+int dcp_host_mesh_renumber_cuthill_mckee(dcp_host_mesh* h) {
+  if (!h) return DCP_ERR_INVALID;
+  try {
+    const Mesh& m = h->mesh;
+    const std::vector<int32_t> nw = cuthill_mckee_nodes(m.n_cells, h->cell_nse.data(), m.n_vnodes);
+    const std::vector<int32_t> map =
+        nse_dof_map(m.n_cells, h->cell_nse.data(), m.n_vnodes, m.n_p(), nw);
+    for (int32_t& d : h->cell_nse) d = map[d];
+    h->nse = renumber_constraints(h->nse, map);
+    const std::vector<double>& src = h->nse_xyz.empty() ? m.xyz : h->nse_xyz;
+    std::vector<double> xyz(src.size());
+    for (int n = 0; n < m.n_vnodes; ++n)
+      for (int k = 0; k < 3; ++k) xyz[3 * size_t(nw[n]) + k] = src[3 * size_t(n) + k];
+    h->nse_xyz.swap(xyz);
+    return DCP_OK;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return DCP_ERR_INVALID;
+  }
+}
+
 static dcp_constraints view_of(const Constraints& c) {
   dcp_constraints v;
   v.n_lines = c.n_lines();
@@ -2476,7 +2499,7 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
   out->cell_T_dofs = h->tdofs.cell_dofs.data();
   out->cell_geometry = m.cell_map.data();
   out->cell_diameter = m.cell_diameter.data();
-  out->node_xyz = m.xyz.data();
+  out->node_xyz = h->nse_xyz.empty() ? m.xyz.data() : h->nse_xyz.data();
   out->nse = view_of(h->nse);
   out->T = view_of(h->T);
   return DCP_OK;

@@ -4,7 +4,8 @@
 // The reference executable (source/main.cxx: parse -p, construct the model
 // from the parameter file, run()) over libdcp.so: CoreModelData::Parameters
 // from the same .prm (dcp_prm_load), the refined shell / cube with its DoFs
-// and constraints (setup_dofs, dcp_host_mesh_create), the initial temperature,
+// and constraints (setup_dofs, dcp_host_mesh_create; Cuthill-McKee for the
+// Schur-complement solver), the initial temperature,
 // then the time loop (dcp_run) with the reference's per-step log lines.
 // --output: output_results (boussinesq_model.tpp:1566-1680) before the loop
 // and after every step, DIR/NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu (classic).
@@ -108,6 +109,9 @@ int main(int argc, char** argv) {
   dcp_host_mesh* m = dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0,
                                           rp.R1, rp.length, rp.physics.temperature_degree, 0, 0);
   if (!m) return fail("mesh", nullptr);
+  // setup_dofs (:198-204): Cuthill_McKee before component_wise for the Schur solver
+  if (!feec && rp.use_schur_complement_solver && dcp_host_mesh_renumber_cuthill_mckee(m) != DCP_OK)
+    return fail("renumbering", nullptr);
   dcp_host_mesh_view v{};
   dcp_host_mesh_view_get(m, &v);
   dcp_config cfg{device, 0, 1, nullptr, nullptr};

@@ -346,6 +346,11 @@ dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1
                                     int temperature_degree, int normal_mode,
                                     int mapping_q_on_all_cells);
 void dcp_host_mesh_destroy(dcp_host_mesh* m);
+/* DoFRenumbering::Cuthill_McKee + component_wise of the NSE dofs, what
+ * setup_dofs() does when use_schur_complement_solver is set
+ * (boussinesq_model.tpp:198-204): cell dofs, NSE constraints and node_xyz of
+ * later views follow the new numbering (velocity 3 n + c stays node-major). */
+int dcp_host_mesh_renumber_cuthill_mckee(dcp_host_mesh* m);
 typedef struct {
   int n_cells, n_u, n_p, n_T, n_vnodes;
   const int32_t* cell_nse_dofs;   /* [n_cells][89] */

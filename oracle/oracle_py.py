@@ -354,3 +354,50 @@ class FeecModel:
         out = np.zeros(2)
         lib().orc_feec_velocity_stats(self.h, _p(np.ascontiguousarray(sol, np.float64)), _p(out))
         return out
+
+
+def cuthill_mckee_nse(cell_nse_dofs, n_vnodes, n_u, n_p):
+    """Checker for dcp_host_mesh_renumber_cuthill_mckee: deal.II's
+    SparsityTools::reorder_Cuthill_McKee (sparsity_tools.cc, called by
+    DoFRenumbering::Cuthill_McKee at boussinesq_model.tpp:200) restated in
+    numpy on support points, then component_wise (:204). Returns (node_new,
+    dof_map old -> new)."""
+    import scipy.sparse as sp
+    nc = cell_nse_dofs.shape[0]
+    vel = cell_nse_dofs[:, [4 * v for v in range(8)] + list(range(32, 89, 3))] // 3
+    vnode_p = np.full(n_p, -1, np.int64)
+    for v in range(8):
+        vnode_p[cell_nse_dofs[:, 4 * v + 3] - n_u] = cell_nse_dofs[:, 4 * v] // 3
+    ndof = np.full(n_vnodes, 3, np.int64)
+    ndof[vnode_p] = 4
+    rows = np.repeat(vel, 27, axis=1).ravel()
+    cols = np.tile(vel, (1, 27)).ravel()
+    A = sp.csr_matrix((np.ones(rows.size, np.int8), (rows, cols)), shape=(n_vnodes, n_vnodes))
+    A.sum_duplicates()
+    A.data[:] = 1
+    coord = np.asarray(A @ ndof).ravel()  # row length of every dof at the node
+    ptr, idx = A.indptr, A.indices
+    new = np.full(n_vnodes, -1, np.int64)
+
+    def start():  # find_unnumbered_starting_index: first of least coordination
+        free = np.flatnonzero(new < 0)
+        return int(free[np.argmin(coord[free])])
+
+    last = np.array([start()])
+    new[last] = 0
+    nxt = 1
+    while nxt < n_vnodes:
+        cand = np.unique(np.concatenate([idx[ptr[n]:ptr[n + 1]] for n in last]))
+        cand = cand[new[cand] < 0]
+        if cand.size == 0:
+            cand = np.array([start()])
+        order = cand[np.argsort(coord[cand], kind="stable")]
+        new[order] = np.arange(nxt, nxt + order.size)
+        nxt += order.size
+        last = order
+    newp = np.empty(n_p, np.int64)
+    newp[np.argsort(new[vnode_p], kind="stable")] = np.arange(n_p)
+    dmap = np.empty(n_u + n_p, np.int64)
+    dmap[:n_u] = 3 * new[np.arange(n_u) // 3] + np.arange(n_u) % 3
+    dmap[n_u:] = n_u + newp
+    return new, dmap

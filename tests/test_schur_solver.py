@@ -11,8 +11,10 @@ with equal Schur GMRES and A^-1 counts, on the shell (classic prm) and the cube 
 Coriolis, vertical gravity, periodic images), and dcp_run on the cube prm.
 
 The reference renumbers the NSE dofs with Cuthill_McKee before this solver
-(:196-200); ILU(0) depends on the order, so both sides here factor the
-numbering the mesh arrives with (parity with Trilinos' Ifpack unpinned)."""
+(:198-204); ILU(0) depends on the order, so both sides factor the numbering
+the mesh arrives with: the first-encounter one and the Cuthill-McKee one
+(cube-r2-cm, dcp_host_mesh_renumber_cuthill_mckee) that the reference's
+setup_dofs gives this solver (parity with Trilinos' Ifpack unpinned)."""
 import os
 
 import numpy as np
@@ -26,10 +28,11 @@ CUBE_PRM = os.path.join(ROOT, "configs", "aqua_planet_cube_test_3d.prm")
 
 
 def case(name):
-    if name == "cube-r2":
+    if name.startswith("cube-r2"):
         rp = dcp.load_prm(CUBE_PRM)
         ph = dcp.physics_from_params(rp)
-        return dcp.HostMesh(cuboid=True, refine=2, length=rp.length), ph
+        return dcp.HostMesh(cuboid=True, refine=2, length=rp.length,
+                            cuthill_mckee=name.endswith("-cm")), ph
     refine = int(name[-1])
     return dcp.HostMesh(refine=refine), dcp.classic_physics()
 
@@ -40,7 +43,7 @@ def oracle_solve(m, ph, u, T):
     return orc.solve_nse_schur(u)
 
 
-@pytest.mark.parametrize("name", ["shell-r1", "cube-r2"])
+@pytest.mark.parametrize("name", ["shell-r1", "cube-r2", "cube-r2-cm"])
 def test_oracle_schur_solver_converges(name):
     m, ph = case(name)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
@@ -52,7 +55,7 @@ def test_oracle_schur_solver_converges(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["shell-r1", "cube-r2"])
+@pytest.mark.parametrize("name", ["shell-r1", "cube-r2", "cube-r2-cm"])
 def test_gpu_schur_solver_matches_oracle(name):
     m, ph = case(name)
     rng = np.random.default_rng(7)
@@ -81,13 +84,14 @@ def test_gpu_schur_solver_matches_oracle(name):
 @pytest.mark.gpu
 def test_run_cube_prm_uses_the_schur_solver():
     """dcp_run with the cube prm (use schur complement solver = true): the
-    first step runs the Schur-complement solve, as run() does (:1896-1898)."""
+    first step runs the Schur-complement solve, as run() does (:1896-1898),
+    on the Cuthill-McKee numbering setup_dofs gives it."""
     rp = dcp.load_prm(CUBE_PRM)
     assert rp.use_schur_complement_solver == 1
     rp.use_FEEC_solver = 0  # the classic model (BASELINE C2 overrides)
     rp.nse_velocity_degree = 2
     ph = dcp.physics_from_params(rp)
-    m = dcp.HostMesh(cuboid=True, refine=2, length=rp.length)
+    m = dcp.HostMesh(cuboid=True, refine=2, length=rp.length, cuthill_mckee=True)
     ctx = dcp.Context()
     ctx.set_physics(ph)
     ctx.upload_mesh(m)

@@ -18,7 +18,10 @@ rp.use_FEEC_solver = 0
 rp.nse_velocity_degree = 2
 refine = int(os.environ.get("REFINE", "3"))
 ph = dcp.physics_from_params(rp)
-m = dcp.HostMesh(cuboid=True, refine=refine, length=rp.length)
+# setup_dofs renumbers with Cuthill_McKee for the Schur solver (:198-204); CM=0 keeps
+# the first-encounter numbering
+m = dcp.HostMesh(cuboid=True, refine=refine, length=rp.length,
+                 cuthill_mckee=os.environ.get("CM", "1") == "1")
 ctx = dcp.Context()
 ctx.set_physics(ph)
 ctx.upload_mesh(m)
@@ -29,8 +32,8 @@ for f, v in ((dcp.OLD_NSE_SOLUTION, z), (dcp.NSE_SOLUTION, z), (dcp.OLD_T_SOLUTI
 t0 = time.perf_counter()
 rc, rep, steps = ctx.run(rp, max_steps=1)
 wall = time.perf_counter() - t0
-print(json.dumps({"config": "BASELINE C2: aqua_planet_cube_test_3d.prm, classic Q2/Q1, refine %d"
-                  % refine, "n_cells": m.n_cells, "n_u": m.n_u, "n_p": m.n_p, "n_T": m.n_T,
+print(json.dumps({"config": "BASELINE C2: aqua_planet_cube_test_3d.prm, classic Q2/Q1, refine %d%s"
+                  % (refine, ", Cuthill-McKee" if os.environ.get("CM", "1") == "1" else ""), "n_cells": m.n_cells, "n_u": m.n_u, "n_p": m.n_p, "n_T": m.n_T,
                   "rc": rc, "steps": rep.steps, "schur_gmres_iterations": rep.schur_inner,
                   "T_cg_iterations": rep.T_cg, "step_wall_s": wall,
                   "phase_ms": ctx.timings()}), flush=True)
