@@ -889,7 +889,7 @@ void materialize_velocity_block(Ctx& c) {
   out.pcidx = c.periodic ? c.pcidx.p : nullptr;
   for (int k = 0; k < c.n_colors(); ++k)
     launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p, c.old_T.p,
-                      c.nse_ph, out, c.stream);
+                      c.nse_ph, out, c.stream, c.element_mfma);
   image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
                         c.A_val.p, c.stream);
   c.A_current = true;
@@ -1090,6 +1090,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     }
     if (option == DCP_OPT_ASSEMBLE_VELOCITY_BLOCK) {
       ctx->assemble_A = value != 0;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_ELEMENT_MFMA) {
+      require(value == 0 || value == 1, DCP_ERR_INVALID, "DCP_OPT_ELEMENT_MFMA must be 0 or 1");
+      ctx->element_mfma = value != 0;
       return DCP_OK;
     }
     if (option == DCP_OPT_FGMRES_MAX_OUTER) {
@@ -1657,7 +1662,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     for (int k = 0; k < c.n_colors(); ++k) {
       if (full)
         launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
-                          c.old_T.p, c.ph, out, c.stream);
+                          c.old_T.p, c.ph, out, c.stream, c.element_mfma);
       else
         launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                             c.old_T.p, c.ph, out, c.stream);
@@ -1995,7 +2000,8 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
     DBuf<double> dK, df;
     dK.alloc(size_t(n) * 89 * 89);
     df.alloc(size_t(n) * 89);
-    launch_nse_system_elements(c.cd(), first, n, c.old_nse.p, c.old_T.p, c.ph, dK.p, df.p, c.stream);
+    launch_nse_system_elements(c.cd(), first, n, c.old_nse.p, c.old_T.p, c.ph, dK.p, df.p, c.stream,
+                               c.element_mfma);
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     DCP_HIP_CHECK(hipMemcpy(K, dK.p, dK.n * sizeof(double), hipMemcpyDeviceToHost));
     DCP_HIP_CHECK(hipMemcpy(f, df.p, df.n * sizeof(double), hipMemcpyDeviceToHost));

@@ -109,6 +109,7 @@ struct Ctx {
   int n_img_u = 0, n_img_p = 0, n_img_T = 0, n_img_node = 0;
   bool periodic = false;
   bool assemble_A = false;   // DCP_OPT_ASSEMBLE_VELOCITY_BLOCK
+  bool element_mfma = false;  // DCP_OPT_ELEMENT_MFMA
   // B entry k = B^T entry B_tperm[k] (every B entry has its B^T partner, one
   // GPU): the operator form scatters B^T only and copies B from it
   DBuf<int32_t> B_tperm;

@@ -185,10 +185,11 @@ void mf_constrained(int n, const int32_t* dof, const int64_t* diag_pos, const do
 
 // ---- assembly.hip ---------------------------------------------------------
 // Colour-wise NSE system assembly (cells of one colour share no node, so the
-// read-modify-write scatter needs no atomics and is deterministic).
+// read-modify-write scatter needs no atomics and is deterministic). mfma: the
+// velocity-block Gram sums on v_mfma_f64_16x16x4_f64 (DCP_OPT_ELEMENT_MFMA).
 void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                        const double* u_old, const double* T_old, const PhysicsDev& ph,
-                       const NseOut& out, hipStream_t s);
+                       const NseOut& out, hipStream_t s, bool mfma = false);
 // Operator form (out.A ignored): B^T, B, rhs and out.cdiag; the velocity
 // block stays matrix-free.
 void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
@@ -200,7 +201,7 @@ void transpose_blocks3(long n, const int32_t* tperm, const double* src, double* 
 // Element mode: dense FESystem-ordered K/f of cells [first, first+n).
 void launch_nse_system_elements(const CellData& cd, int first, int n, const double* u_old,
                                 const double* T_old, const PhysicsDev& ph, double* K, double* f,
-                                hipStream_t s);
+                                hipStream_t s, bool mfma = false);
 void launch_nse_precond_diag(const CellData& cd, const int32_t* cells, int n, const PhysicsDev& ph,
                              double* A_diag, double* Mp_diag, hipStream_t s);
 // posTs: [n_cells][8] position of (original, original) for identified T dofs, -1 else (or null)

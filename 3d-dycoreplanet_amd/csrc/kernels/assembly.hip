@@ -410,12 +410,113 @@ __device__ inline void nse_rhs_node(const NseSmem& sh, int an, double fa[3]) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The velocity-velocity Gram sums on the matrix cores (DCP_OPT_ELEMENT_MFMA):
+// G = D^T W D over the 81 (node, direction) physical gradients -- D is [q][n][d]
+// in LDS, so column r = 3n + d of the 27 x 81 matrix is D[81 q + r] -- and the
+// mass M = S^T W S over the 27 shape values, both as v_mfma_f64_16x16x4_f64
+// tiles with K = 27 points padded to 28 (7 steps): the 21 upper tiles of the
+// 96 x 96 padded G and the 3 upper tiles of the 32 x 32 padded M, six per wave.
+// Lane l feeds A[l & 15][k = l >> 4] = w_q D[q][16 I + (l & 15)] and
+// B[k][l & 15] = D[q][16 J + (l & 15)]; result register i holds
+// G[16 I + (l >> 4) + 4 i][16 J + (l & 15)] (the f64 C/D map).
+// The element block then is K_(a,c),(b,c') = nu Q_c'c + delta_cc' (m + nu L),
+// Q_de = G[3a + d][3b + e], L = trace Q (nse_tile's formula, summed in MFMA order).
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+constexpr int kGramQTiles = 21;
+constexpr int kGramTilesPerWave = 6;  // 21 G + 3 M = 24 tiles over 4 waves
+__constant__ unsigned char cGramI[24] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5,
+                                         0, 0, 1};
+__constant__ unsigned char cGramJ[24] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5,
+                                         0, 1, 1};
+
+__device__ inline void gram_tiles(const NseSmem& sh, int wave, int lane,
+                                  f64x4_t acc[kGramTilesPerWave]) {
+  const int li = lane & 15, lk = lane >> 4;
+  {
+#pragma unroll
+    for (int t = 0; t < kGramTilesPerWave; ++t) {
+      const int tile = wave + 4 * t;
+      const bool mass = tile >= kGramQTiles;
+      const int ra = 16 * cGramI[tile] + li, cb = 16 * cGramJ[tile] + li;
+      const int nmax = mass ? 27 : 81;
+      const double* tab = mass ? sh.S : sh.D;
+      const int ld = mass ? 27 : 81;
+      f64x4_t c = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        const int q = 4 * s + lk;
+        double a = 0.0, b = 0.0;
+        if (q < 27) {
+          if (ra < nmax) a = sh.geo.JxW[q] * tab[ld * q + ra];
+          if (cb < nmax) b = tab[ld * q + cb];
+        }
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+      }
+      acc[t] = c;
+    }
+  }
+}
+
+// Staging slot of the element block (a, b), grp(a) <= grp(b) (stored untransposed).
+__device__ inline double* gram_slot(double* st, int a, int b) {
+  return st + 9 * (cSlot.s[27 * a + b] & 0x7fff);
+}
+
+// Phase 1: nu G into the staged blocks (entry [3 e + d] of block (a, b) for
+// G[3a + d][3b + e]); every (row, col) with grp(row / 3) <= grp(col / 3) is
+// written exactly once: directly from its upper tile, or, for a same-group
+// pair below a tile boundary, as the transpose of its mirror.
+__device__ inline void gram_stage_q(double* st, int wave, int lane,
+                                    const f64x4_t acc[kGramTilesPerWave], double nu) {
+#pragma unroll
+  for (int t = 0; t < kGramTilesPerWave; ++t) {
+    const int tile = wave + 4 * t;
+    if (tile >= kGramQTiles) continue;
+    const int I = cGramI[tile], J = cGramJ[tile];
+    const int col = 16 * J + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * I + (lane >> 4) + 4 * i;
+      if (row >= 81 || col >= 81) continue;
+      const double v = nu * acc[t][i];
+      if (row / 9 <= col / 9) gram_slot(st, row / 3, col / 3)[3 * (col % 3) + row % 3] = v;
+      if (I < J && row / 9 == col / 9) gram_slot(st, col / 3, row / 3)[3 * (row % 3) + col % 3] = v;
+    }
+  }
+}
+
+// Phase 2 (after phase 1 is visible): the diagonal m + nu L of every staged block.
+__device__ inline void gram_stage_m(double* st, int wave, int lane,
+                                    const f64x4_t acc[kGramTilesPerWave]) {
+  const int tile = wave + 4 * (kGramTilesPerWave - 1);
+  if (tile < kGramQTiles) return;
+  const int I = cGramI[tile], J = cGramJ[tile];
+  const int b = 16 * J + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a = 16 * I + (lane >> 4) + 4 * i;
+    if (a >= 27 || b >= 27) continue;
+    const double m = acc[kGramTilesPerWave - 1][i];
+    if (a / 3 <= b / 3) {
+      double* s = gram_slot(st, a, b);
+      const double d = m + (s[0] + s[4] + s[8]);
+      s[0] += d; s[4] += d; s[8] += d;
+    }
+    if (I < J && a / 3 == b / 3) {
+      double* s = gram_slot(st, b, a);
+      const double d = m + (s[0] + s[4] + s[8]);
+      s[0] += d; s[4] += d; s[8] += d;
+    }
+  }
+}
+
 // MODE 0: full distribute_local_to_global into block-CSR A, B^T, B (+ rhs);
 // MODE 1: dense element output; MODE 2: the operator form of nse_matrix that
 // the solve reads (B^T, B, rhs and the diagonal of the constrained velocity
 // rows), with the velocity-velocity block left to the matrix-free apply
 // (kernels/matfree.hip) and materialised only on request (MODE 0).
-template <int MODE>
+template <int MODE, bool GM>
 __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, ScatterMaps sm,
                                                             const int32_t* __restrict__ cells,
                                                             int first,
@@ -630,6 +731,51 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   }
 
   constexpr int kAux = kNseThreads - kNseTiles;  // threads for B^T/B and rhs in MODE 1
+  if (MODE == 1 && GM) {
+    double* K = out.elemK + size_t(blockIdx.x) * 89 * 89;
+    double* f = out.elemF + size_t(blockIdx.x) * 89;
+    const int wave = tid >> 6, lane = tid & 63;
+    f64x4_t acc[kGramTilesPerWave];
+    gram_tiles(sh, wave, lane, acc);
+    // B^T / B entries, rhs, the pressure rows (the tables are still live)
+    for (int t = tid; t < 216 + 27 + 8; t += kNseThreads) {
+      if (t < 216) {
+        const int an = t / 8, v = t % 8;
+        double bt[3];
+        nse_div(sh, an, v, bt);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          K[89 * fesys_velocity(an, c) + 4 * v + 3] = bt[c];
+          K[89 * (4 * v + 3) + fesys_velocity(an, c)] = bt[c];
+        }
+      } else if (t < 243) {
+        const int an = t - 216;
+        double fa[3];
+        nse_rhs_node(sh, an, fa);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) f[fesys_velocity(an, c)] = fa[c];
+      } else {
+        const int v = t - 243;
+        f[4 * v + 3] = 0.0;
+        for (int w = 0; w < 8; ++w) K[89 * (4 * v + 3) + 4 * w + 3] = 0.0;
+      }
+    }
+    __syncthreads();  // tables dead: stage the velocity blocks over them
+    double* stage = sh.X;
+    gram_stage_q(stage, wave, lane, acc, ph.nu_sys);
+    __syncthreads();
+    gram_stage_m(stage, wave, lane, acc);
+    __syncthreads();
+    for (int e = tid; e < 729 * 9; e += kNseThreads) {
+      const int pr = e / 9, comp = e - 9 * pr;
+      const int a = pr / 27, b = pr - 27 * a;
+      const int sl = cSlot.s[pr];
+      const int i = comp / 3, j = comp - 3 * i;
+      const double v = stage[9 * (sl & 0x7fff) + ((sl & 0x8000) ? 3 * j + i : comp)];
+      K[89 * fesys_velocity(a, i) + fesys_velocity(b, j)] = v;
+    }
+    return;
+  }
   if (MODE == 1) {
     double* K = out.elemK + size_t(blockIdx.x) * 89 * 89;
     double* f = out.elemF + size_t(blockIdx.x) * 89;
@@ -746,7 +892,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   double fa[3] = {0, 0, 0};
   const bool tile_lane = want_matrix && tid < kNseTiles;
   const bool rhs_lane = want_rhs && tid >= kRhsLane0 && tid < kRhsLane0 + 27;
-  if (tile_lane) {
+  f64x4_t acc[kGramTilesPerWave];
+  if (GM && want_matrix) gram_tiles(sh, wave, lane, acc);  // block-uniform branch
+  if (tile_lane && !GM) {
     const int A = cPairA[tid / 3], B = cPairB[tid / 3];
     nse_tile(sh, ph, 3 * A + tid % 3, 3 * B, blk);
   } else if (rhs_lane) {
@@ -761,12 +909,20 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   }
   __syncthreads();   // geometry and gradient tables dead: reuse them as the write staging area
   double* stage = sh.X;
+  if (GM && want_matrix) {
+    gram_stage_q(stage, wave, lane, acc, ph.nu_sys);
+    __syncthreads();
+    gram_stage_m(stage, wave, lane, acc);
+    __syncthreads();
+  }
   if (tile_lane) {
     const int A = cPairA[tid / 3], B = cPairB[tid / 3];
     const int a = 3 * A + tid % 3, b0 = 3 * B;
     double* slot = stage + 27 * tid;   // slots 3 tid + tt
+    if (!GM) {
 #pragma unroll
-    for (int i = 0; i < 27; ++i) slot[i] = blk[i / 9][i % 9];
+      for (int i = 0; i < 27; ++i) slot[i] = blk[i / 9][i % 9];
+    }
     // condensation C_a^T K C_b in place, only where a constraint is involved
     const NodeConstraint ca = cd.vcon[sh.node[a]];
 #pragma unroll 1
@@ -1182,10 +1338,14 @@ void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, 
 
 void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                        const double* u_old, const double* T_old, const PhysicsDev& ph,
-                       const NseOut& out, hipStream_t s) {
+                       const NseOut& out, hipStream_t s, bool mfma) {
   if (n <= 0) return;
-  hipLaunchKernelGGL((k_nse_system<0>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
-                     u_old, T_old, ph, out);
+  if (mfma)
+    hipLaunchKernelGGL((k_nse_system<0, true>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+                       u_old, T_old, ph, out);
+  else
+    hipLaunchKernelGGL((k_nse_system<0, false>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+                       u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -1193,7 +1353,7 @@ void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_
                          const double* u_old, const double* T_old, const PhysicsDev& ph,
                          const NseOut& out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL((k_nse_system<2>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+  hipLaunchKernelGGL((k_nse_system<2, false>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
                      u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
@@ -1220,13 +1380,17 @@ void transpose_blocks3(long n, const int32_t* tperm, const double* src, double* 
 
 void launch_nse_system_elements(const CellData& cd, int first, int n, const double* u_old,
                                 const double* T_old, const PhysicsDev& ph, double* K, double* f,
-                                hipStream_t s) {
+                                hipStream_t s, bool mfma) {
   if (n <= 0) return;
   NseOut out{};
   out.elemK = K;
   out.elemF = f;
-  hipLaunchKernelGGL((k_nse_system<1>), dim3(n), dim3(kNseThreads), 0, s, cd, ScatterMaps{}, nullptr, first,
-                     u_old, T_old, ph, out);
+  if (mfma)
+    hipLaunchKernelGGL((k_nse_system<1, true>), dim3(n), dim3(kNseThreads), 0, s, cd, ScatterMaps{},
+                       nullptr, first, u_old, T_old, ph, out);
+  else
+    hipLaunchKernelGGL((k_nse_system<1, false>), dim3(n), dim3(kNseThreads), 0, s, cd, ScatterMaps{},
+                       nullptr, first, u_old, T_old, ph, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

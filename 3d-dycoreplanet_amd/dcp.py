@@ -31,6 +31,7 @@ OPT_MATRIX_FREE = 3
 OPT_FUSED_CHAIN = 4
 OPT_FGMRES_MAX_OUTER = 5
 OPT_ASSEMBLE_VELOCITY_BLOCK = 6
+OPT_ELEMENT_MFMA = 9
 OPT_GRAM_SCHMIDT = 7
 OPT_FEEC_FIXED_INNER = 8
 
@@ -544,6 +545,12 @@ class Context:
         SolverGMRES, default) or "classical2" (CGS2, device-resident cycles)."""
         self._check(lib().dcp_set_option(self._h, OPT_GRAM_SCHMIDT,
                                          {"modified": 0, "classical2": 1}[kind]))
+
+    def set_element_mfma(self, on: bool):
+        """DCP_OPT_ELEMENT_MFMA: True = the velocity-block node-pair sums of the
+        NSE element matrix on the matrix cores (v_mfma_f64_16x16x4_f64 Gram
+        tiles) instead of FP64 VALU tiles; the same matrices up to rounding."""
+        self._check(lib().dcp_set_option(self._h, OPT_ELEMENT_MFMA, int(bool(on))))
 
     def set_assemble_velocity_block(self, on: bool):
         """DCP_OPT_ASSEMBLE_VELOCITY_BLOCK: False (default) = assemble_nse_system

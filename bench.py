@@ -388,8 +388,16 @@ def main():
     for _ in range(3):
         ctx.assemble_nse_system()
         full_ms.append(ctx.timings()["assemble_nse_ms"])
+    # and with its node-pair sums on the matrix cores (DCP_OPT_ELEMENT_MFMA)
+    ctx.set_element_mfma(True)
+    mfma_ms = []
+    for _ in range(3):
+        ctx.assemble_nse_system()
+        mfma_ms.append(ctx.timings()["assemble_nse_ms"])
+    ctx.set_element_mfma(False)
     ctx.set_assemble_velocity_block(False)
     full_ms = float(np.min(full_ms))
+    mfma_ms = float(np.min(mfma_ms))
     if dist is not None:
         import torch
         tt = torch.tensor([full_ms], dtype=torch.float64, device=tdev)
@@ -399,7 +407,11 @@ def main():
                    "what": "assemble_nse_system with the velocity block A scattered into "
                            "block-CSR as well (DCP_OPT_ASSEMBLE_VELOCITY_BLOCK=1); `value` "
                            "assembles nse_matrix in operator form (B^T, B, rhs, constrained "
-                           "diagonal), every A product being matrix-free"}
+                           "diagonal), every A product being matrix-free",
+                   "element_mfma": {"value": n_nse / (mfma_ms * 1e-3), "ms": mfma_ms,
+                                    "what": "the same with the node-pair Gram sums as "
+                                            "v_mfma_f64_16x16x4_f64 tiles "
+                                            "(DCP_OPT_ELEMENT_MFMA=1; DESIGN section 4e)"}}
     pinfo = ctx.pattern_info()
     if args.schur == "explicit":
         # fused SELL SpMV with the formed S: values + column indices per

@@ -162,6 +162,14 @@ enum { DCP_OPT_GRAM_SCHMIDT = 7 };
  *   lower cap sends small meshes through the do_solve_A / FGMRES(50) fallback
  *   (:1203-1232) that the reference takes when the cap is hit. */
 enum { DCP_OPT_FGMRES_MAX_OUTER = 5 };
+/* DCP_OPT_ELEMENT_MFMA: 0 (default) = the velocity-velocity node-pair sums of
+ *   the NSE element matrix (local_assemble_nse_system, boussinesq_model.tpp:
+ *   597-640: mass + eps:eps over the 27 QGauss points) run as FP64 VALU
+ *   register tiles; 1 = as v_mfma_f64_16x16x4_f64 Gram tiles (D^T W D,
+ *   S^T W S). Same element matrix up to rounding; used by the full scatter
+ *   (DCP_OPT_ASSEMBLE_VELOCITY_BLOCK, dcp_nse_matrix_export) and
+ *   dcp_cell_nse_system. DESIGN.md section 4e has the measurement. */
+enum { DCP_OPT_ELEMENT_MFMA = 9 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the

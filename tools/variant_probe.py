@@ -17,6 +17,8 @@ for path in sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/
     ctx = dcp.Context(device=0)
     ctx.set_physics(dcp.classic_physics())
     ctx.upload_mesh(m)
+    if os.environ.get("VB") == "1":  # time the full scatter with the velocity block
+        ctx.set_assemble_velocity_block(True)
     ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
     ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
     ms = []
