@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -353,13 +354,14 @@ template <int KL>
 constexpr int pow2_at_least() { return KL <= 1 ? 1 : 2 * pow2_at_least<(KL + 1) / 2>(); }
 // KL: basis vectors loaded (d <= KL); the reductions run over the next power
 // of two K with the entries past KL compile-time zero.
-template <int KL>
+template <int KL, bool WIDE>
 __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, ChainVecs V,
                                                               int d, GmresDev* st, int kstep,
                                                               double* gran,
                                                               unsigned long long seq,
                                                               double* err) {
   constexpr int K = pow2_at_least<KL>();
+  static_assert(kChainEntries == 2, "wide loads pair the two entries of a thread");
   __shared__ double sm[kChainWaves * K];
   __shared__ double hs[K];
   __shared__ double nrm_sh;
@@ -375,18 +377,39 @@ __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, 
   // the granule hand-offs; both give wrong results)
   // entries b * 1024 + e * 512 + t of the owned vector; branch-free loads
   // (V.v[j] for j >= d points at V.v[0]) all issued before the first use
+  // WIDE (one segment, n even, 16-byte aligned vectors): a thread owns the adjacent
+  // entries 2 t, 2 t + 1 of its block and reads each basis vector with one
+  // 16-byte load (8-byte loads leave the chain's load phase at ~2.9 TB/s)
   double x[kChainEntries], v[kChainEntries][K];
   unsigned pos[kChainEntries];
   bool live[kChainEntries];
+  const long kb = long(b) * (kChainThreads * kChainEntries);
+  if (WIDE) {
+    const long k0 = kb + 2 * long(threadIdx.x);
+    live[0] = live[1] = k0 < g.n;  // n even: a pair is all in or all out
+    pos[0] = live[0] ? unsigned(k0) : 0u;
+    pos[1] = pos[0] + 1;
+    const double2 xw = *reinterpret_cast<const double2*>(w + pos[0]);
+    x[0] = xw.x;
+    x[1] = xw.y;
 #pragma unroll
-  for (int e = 0; e < kChainEntries; ++e) {
-    const long k = long(b) * (kChainThreads * kChainEntries) + e * kChainThreads + threadIdx.x;
-    live[e] = k < g.n;
-    pos[e] = live[e] ? unsigned(seg_pos(g, k)) : 0u;
-    x[e] = w[pos[e]];
+    for (int j = 0; j < K; ++j) {
+      double2 t = {0.0, 0.0};
+      if (j < KL) t = *reinterpret_cast<const double2*>(V.v[j] + pos[0]);
+      v[0][j] = t.x;
+      v[1][j] = t.y;
+    }
+  } else {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-      v[e][j] = j >= KL ? 0.0 : (DCP_CGS_NOLOAD ? x[e] * (j + 1) : V.v[j][pos[e]]);
+    for (int e = 0; e < kChainEntries; ++e) {
+      const long k = kb + e * kChainThreads + threadIdx.x;
+      live[e] = k < g.n;
+      pos[e] = live[e] ? unsigned(seg_pos(g, k)) : 0u;
+      x[e] = w[pos[e]];
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        v[e][j] = j >= KL ? 0.0 : (DCP_CGS_NOLOAD ? x[e] * (j + 1) : V.v[j][pos[e]]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < kChainEntries; ++e) {
@@ -522,12 +545,18 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
                      int nb, unsigned long long seq, double* err, hipStream_t s) {
   ChainVecs Vp = V;  // unused slots point at V[0]: the kernel's loads are unconditional
   for (int j = d; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
+  bool wide = g.n1 == g.n && g.n % 2 == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
+  for (int j = 0; j < d; ++j) wide = wide && (reinterpret_cast<uintptr_t>(V.v[j]) & 15) == 0;
   const dim3 grid(nb), block(kChainThreads);
   // KL > d: the chain's second reduction keeps its |w|^2 entry at K - 1 >= d
 #define DCP_CGS_CASE(KL)                                                                       \
   if (d < KL) {                                                                                \
-    hipLaunchKernelGGL(k_cgs2_chain<KL>, grid, block, 0, s, g, w, Vp, d, st, d - 1, gran, seq, \
-                       err);                                                                   \
+    if (wide)                                                                                  \
+      hipLaunchKernelGGL((k_cgs2_chain<KL, true>), grid, block, 0, s, g, w, Vp, d, st, d - 1,  \
+                         gran, seq, err);                                                      \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_cgs2_chain<KL, false>), grid, block, 0, s, g, w, Vp, d, st, d - 1, \
+                         gran, seq, err);                                                      \
     DCP_HIP_CHECK(hipGetLastError());                                                          \
     return;                                                                                    \
   }
