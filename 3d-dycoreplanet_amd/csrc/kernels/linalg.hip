@@ -314,12 +314,27 @@ __global__ __launch_bounds__(kBlock) void k_mgs_chain(
 // entry columns (4 waves per slice keep enough loads in flight: one wave per
 // slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound), then
 // wave 0 adds the 4 quarters in order (fixed summation order).
-// DCP_SELL_UNROLL4: four column pairs per iteration (measured within 1 % of
-// two at r=5: the value stream already runs at ~5.8 TB/s)
+// DCP_SELL_UNROLL4 (default): four column pairs per iteration, all value /
+// column loads issued before the gathers; the same summation order as the
+// two-pair loop. r=5 inner probe (tools/inner_probe.py, rocprofv3): 39.65 ->
+// 38.50 us per S apply; DCP_SELL_NT (nontemporal values) 43.3 us.
 #ifndef DCP_SELL_UNROLL4
-#define DCP_SELL_UNROLL4 0
+#define DCP_SELL_UNROLL4 1
 #endif
-#define SELL_LD(p) (*(p))
+#ifndef DCP_SELL_NT
+#define DCP_SELL_NT 0
+#endif
+typedef double sell_d2v __attribute__((ext_vector_type(2)));
+// DCP_SELL_NT (timing variant): the value stream as nontemporal loads, so it
+// does not evict the gathered x from L2
+__device__ inline double2 sell_ld(const double2* p) {
+  if (DCP_SELL_NT) {
+    const sell_d2v t = __builtin_nontemporal_load(reinterpret_cast<const sell_d2v*>(p));
+    return double2{t.x, t.y};
+  }
+  return *p;
+}
+#define SELL_LD(p) sell_ld(p)
 template <bool EPI, bool C16>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* __restrict__ x,
                                                       double cf, double* xs,
