@@ -317,9 +317,13 @@ __global__ __launch_bounds__(kBlock) void k_mgs_chain(
 // DCP_SELL_UNROLL4 (default): four column pairs per iteration, all value /
 // column loads issued before the gathers; the same summation order as the
 // two-pair loop. r=5 inner probe (tools/inner_probe.py, rocprofv3): 39.65 ->
-// 38.50 us per S apply; DCP_SELL_NT (nontemporal values) 43.3 us.
+// 38.50 us per S apply; DCP_SELL_NT (nontemporal values) 43.3 us;
+// DCP_SELL_UNROLL8 (eight pairs first) 38.55 against 38.73 us, within noise.
 #ifndef DCP_SELL_UNROLL4
 #define DCP_SELL_UNROLL4 1
+#endif
+#ifndef DCP_SELL_UNROLL8
+#define DCP_SELL_UNROLL8 0
 #endif
 #ifndef DCP_SELL_NT
 #define DCP_SELL_NT 0
@@ -396,6 +400,28 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   if (C16) {
     const int cb = m.base[sl];
     const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * int64_t(k0) + lane;
+#if DCP_SELL_UNROLL8
+    for (; k + 8 <= k1; k += 8, cp += 512, vp += 512) {
+      // eight column pairs (timing variant)
+      ushort2 c[8];
+      double2 a[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) c[i] = cp[64 * i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = SELL_LD(vp + 64 * i);
+      double xv[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xv[2 * i] = x[cb + c[i].x] * cf;
+        xv[2 * i + 1] = x[cb + c[i].y] * cf;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc += a[i].x * xv[2 * i];
+        acc += a[i].y * xv[2 * i + 1];
+      }
+    }
+#endif
 #if DCP_SELL_UNROLL4
     for (; k + 4 <= k1; k += 4, cp += 256, vp += 256) {
       // four column pairs: all value / column loads issued before the gathers
