@@ -35,8 +35,6 @@ Ctx::~Ctx() {
   if (gm_report) (void)hipHostFree(gm_report);
   for (auto& ev : gm_ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (auto& ev : spec_ev)
-    if (ev) (void)hipEventDestroy(ev);
   ev_total.destroy();
   for (auto& t : schur_ev) t.destroy();
   for (auto& v : mf_ev)
@@ -986,6 +984,8 @@ int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int fie
   });
 }
 
+int dcp_abi_version(void) { return DCP_ABI_VERSION; }
+
 int dcp_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -1027,9 +1027,6 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
       for (auto& t : v) t.init();
     }
     ensure_workspaces(*c);
-    if (const char* e = std::getenv("DCP_SCHUR_AHEAD")) c->schur_ahead = std::atoi(e) != 0;
-    if (const char* e = std::getenv("DCP_SCHUR_READY_FLAG"))
-      c->schur_ready_flag = std::atoi(e) != 0;
     if (const char* e = std::getenv("DCP_TEST_FORCE_REORTH_AT"))
       c->test_force_reorth_at = std::atoi(e);
     *out = c.release();

@@ -121,6 +121,15 @@ struct Ctx {
     std::vector<int> lf_host;
     DBuf<double> lu;
     int n = 0, n_lf = 0, n_lb = 0, n_p_img = 0, max_row = 0;
+    // forget the structure and the factor (a new mesh may have the same n_u
+    // with another numbering or pattern)
+    void reset() {
+      for (auto* b : {&ptr, &col, &diag, &pos, &lf_ptr, &lf_rows, &lb_ptr, &lb_rows, &p_img})
+        b->release();
+      lu.release();
+      lf_host.clear();
+      n = n_lf = n_lb = n_p_img = max_row = 0;
+    }
     IluView view() const {
       return IluView{n,         long(col.n), ptr.p,     col.p,      diag.p,    pos.p,
                      n_lf,      n_lb,        lf_ptr.p,  lf_rows.p,  lb_ptr.p,  lb_rows.p};
@@ -200,13 +209,11 @@ struct Ctx {
   // scratch: reduction partials, device scalars
   DBuf<double> partials, dscal;
   double* hpinned = nullptr;   // pinned host mirror of small readbacks
-  hipEvent_t spec_ev[2] = {nullptr, nullptr};  // readbacks of pipelined Arnoldi steps
-  double* hmapped = nullptr;   // coherent mapped host memory written by kernels (one GPU)
+  double* hmapped = nullptr;   // coherent mapped host memory: the chain timeout flag (one GPU)
   // one-launch Gram-Schmidt chains (k_mgs_chain): hand-off granules, launch
   // counter (the granule tags), CU count (residency bound), DCP_OPT_FUSED_CHAIN
   DBuf<double> chain_gran;
   unsigned long long chain_seq = 0;
-  unsigned long long spec_seq = 0;   // inner Schur GMRES step numbers (ready flags)
   int n_cus = 0;
   bool fused_chain = true;
   // DCP_OPT_GRAM_SCHMIDT: 0 = modified (deal.II SolverGMRES, default), 1 = the
@@ -223,11 +230,8 @@ struct Ctx {
   std::vector<const double*> gm_ptrs_host;
   int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
   long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
-  // test hooks, read at context creation: DCP_SCHUR_AHEAD=0 turns the inner
-  // Schur GMRES's launch-ahead off; DCP_TEST_FORCE_REORTH_AT=k makes the
+  // test hook, read at context creation: DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger
-  bool schur_ahead = false;      // DCP_SCHUR_AHEAD=1: launch-ahead Arnoldi steps (not bitwise reproducible in long stagnating runs at r=5)
-  bool schur_ready_flag = true;   // DCP_SCHUR_READY_FLAG=0: events instead
   int test_force_reorth_at = -1;
   bool nse_assembled = false, precond_built = false, T_matrix_ok = false, T_rhs_ok = false;
   // Krylov workspaces (lazily sized)

@@ -291,30 +291,14 @@ void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStre
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
 // vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
 // part1 (one per slice, fixed order; zeros up to n_part, the length common to
-// all ranks whose partials are all-reduced). nrm_part != null: cf is ignored
-// and computed on the device as 1/|w| from the nb_nrm partials of |w|^2
-// (block_sum order; |w| -> *nrm_store), so the launch needs no host scalar;
-// ready.host != null: block 0 also hands the previous step over (StepReady).
-// Per-step block of the pipelined inner Schur GMRES (solver.cpp): [0, 128)
-// coefficients h_0.., then these slots, the chain's final partials from kSpPart.
-constexpr int kSpNStart = 128, kSpNorm = 129, kSpReady = 130, kSpReadyNorm = 131, kSpPart = 192;
-// The previous step's hand-over to the host, done by a launched-ahead SpMV's
-// block 0 (one GPU): copy n coefficients, kSpNStart and kSpNorm from the
-// device block `dev` to the mapped host block `host`, |w| -> host[kSpReadyNorm],
-// a system-scope fence, then the bits of seq -> host[kSpReady]. The host spins
-// on that flag instead of an event between the launches; it reads only values
-// this one thread wrote before its fence.
-struct StepReady {
-  double* host;
-  const double* dev;
-  int n;
-  unsigned long long seq;
-};
+// all ranks whose partials are all-reduced).
+// Per-step block of the inner Schur GMRES with modified Gram-Schmidt
+// (solver.cpp): [0, 128) coefficients h_0.., kSpNStart the start norm of the
+// loss-of-orthogonality test, the chain's final partials from kSpPart.
+constexpr int kSpNStart = 128, kSpPart = 192;
 int sell_fused_blocks(int rows);
 void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, double* y,
-                     const double* v0, double* part0, double* part1, int n_part,
-                     const double* nrm_part, int nb_nrm, double* nrm_store, StepReady ready,
-                     hipStream_t s);
+                     const double* v0, double* part0, double* part1, int n_part, hipStream_t s);
 // Step of the device-resident GMRES cycle: y = M (cf * x) with cf = *cf_dev
 // (cf_dev null: 1), xs = cf * x when xs != null; nothing if *status != 0.
 void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, double* xs,

@@ -346,14 +346,9 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
                                                       const double* v0,
                                                       double* __restrict__ part0,
                                                       double* __restrict__ part1,
-                                                      const double* __restrict__ nrm_part,
-                                                      int nb_nrm, double* nrm_store,
-                                                      StepReady ready,
                                                       const double* __restrict__ cf_dev,
                                                       const int* __restrict__ status) {
   __shared__ double quarter[3][64];
-  __shared__ double sm[4];
-  __shared__ double cf_sh;
   if (status && *status) return;  // device-resident GMRES cycle already stopped
   if (cf_dev) cf = *cf_dev;
   const int rows = m.rows;
@@ -365,30 +360,6 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
     // all-reduced partial arrays must hold zeros past this rank's slices
     if (EPI && part0 && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
     return;
-  }
-  if (EPI && nrm_part) {
-    // cf = 1/|w| from the nb_nrm partials of |w|^2 (block_sum order: the host
-    // mirrors it bit for bit, solver.cpp block_sum_host)
-    double s = 0;
-    for (int i = threadIdx.x; i < nb_nrm; i += kBlock) s += nrm_part[i];
-    const double tot = block_sum(s, sm);
-    if (threadIdx.x == 0) {
-      const double nv = sqrt(tot);
-      cf_sh = nv != 0 ? 1.0 / nv : 1.0;
-      if (blockIdx.x == 0) {
-        *nrm_store = nv;
-        if (ready.host) {
-          for (int j = 0; j < ready.n; ++j) ready.host[j] = ready.dev[j];
-          ready.host[kSpNStart] = ready.dev[kSpNStart];
-          ready.host[kSpNorm] = ready.dev[kSpNorm];
-          ready.host[kSpReadyNorm] = nv;
-          __threadfence_system();
-          ready.host[kSpReady] = __longlong_as_double((long long)ready.seq);
-        }
-      }
-    }
-    __syncthreads();
-    cf = cf_sh;
   }
   const int64_t b = m.off[sl];
   const int np = int((m.off[sl + 1] - b) >> 7);  // column pairs of the slice
@@ -849,27 +820,23 @@ void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStre
   const dim3 grid(sell_fused_blocks(m.rows));
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<false, true>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, nullptr,
-                       nullptr);
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL((k_sell_spmv<false, false>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, nullptr,
-                       nullptr);
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
 void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, double* y,
-                     const double* v0, double* part0, double* part1, int n_part,
-                     const double* nrm_part, int nb_nrm, double* nrm_store, StepReady ready,
-                     hipStream_t s) {
+                     const double* v0, double* part0, double* part1, int n_part, hipStream_t s) {
   const int nb = std::max(sell_fused_blocks(m.rows), n_part);
   if (nb <= 0) return;
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<true, true>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready, nullptr, nullptr);
+                       v0, part0, part1, nullptr, nullptr);
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nrm_part, nb_nrm, nrm_store, ready, nullptr, nullptr);
+                       v0, part0, part1, nullptr, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -879,12 +846,10 @@ void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, do
   const dim3 grid(sell_fused_blocks(m.rows));
   if (m.col16)
     hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, cf_dev,
-                       status);
+                       nullptr, nullptr, nullptr, cf_dev, status);
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
-                       nullptr, nullptr, nullptr, nullptr, 0, nullptr, StepReady{}, cf_dev,
-                       status);
+                       nullptr, nullptr, nullptr, cf_dev, status);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

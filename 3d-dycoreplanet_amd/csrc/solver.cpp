@@ -17,7 +17,6 @@
 // fixed-order sum, so every rank takes the same decisions from bitwise equal
 // scalars. Every operator refreshes the ghost entries of its input first.
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -54,18 +53,18 @@ constexpr int kSlotA = 258;      // misc
 constexpr int kSlotB = 259;
 constexpr int kSlotC = 260;
 constexpr int kSlotD = 261;
+constexpr int kSlotErr = 262;    // granule timeout flag of the CGS2 steps on several GPUs
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
 constexpr int kSlotCg = 1296;    // 4: pcg's gh, d.h, alpha / beta, |g|^2
 constexpr int kHostPartials = 2048;
-// gmres_schur's pipelined Arnoldi steps: one block per step parity,
-// [0, 128) coefficients, kSpNStart, kSpNorm, ..., partials from kSpPart (device.h)
-constexpr int kSpecBase = 4096, kSpecStride = 1280;
+// gmres_schur's Arnoldi step block: [0, 128) coefficients, kSpNStart, the
+// chain's final partials from kSpPart (device.h)
+constexpr int kStepBlock = 4096, kStepBlockLen = 1280;
 constexpr int kNumSlots = 8192;             // device slots, mirrored in c.hpinned
 static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kSlotCg, "slot layout");
 static_assert(kSlotCg + 4 <= kHostPartials, "slot layout");
-static_assert(kHostPartials + kChainMaxBlocks <= kSpecBase - 512, "slot layout");
-static_assert(kSpPart + kChainMaxBlocks <= kSpecStride, "slot layout");
-static_assert(kSpecBase + 2 * kSpecStride <= kNumSlots, "slot layout");
+static_assert(kHostPartials + kChainMaxBlocks <= kStepBlock, "slot layout");
+static_assert(kSpPart + kChainMaxBlocks <= kStepBlockLen, "slot layout");
 
 using Op = std::function<void(const double*, double*)>;
 
@@ -165,12 +164,7 @@ double block_sum_host(const double* p, int nb) {
 // One-launch chains (k_mgs_chain): one GPU, every workgroup resident, w in
 // registers. The timeout flag lives in mapped host memory and is sticky.
 constexpr int kChainErr = 8000;
-// the inner Schur GMRES restart's residual: |p| hand-over block (mapped host),
-// its nb partials (device slots)
-constexpr int kResBlock = 6784, kResPart = 7040;
-static_assert(kSpecBase + 2 * kSpecStride <= kResBlock && kResBlock + kSpPart <= kChainErr &&
-                  kResPart + kChainMaxBlocks <= kNumSlots, "slot layout");
-static_assert(kSpecBase + 2 * kSpecStride <= kChainErr && kChainErr < kNumSlots, "slot layout");
+static_assert(kStepBlock + kStepBlockLen <= kChainErr && kChainErr < kNumSlots, "slot layout");
 bool fused_chain_ok(const Ctx& c, Seg g, int nb, int dim) {
   return !c.comm && c.fused_chain && c.hmapped && mgs_chain_fits(g.n, nb, dim, c.n_cus);
 }
@@ -181,24 +175,6 @@ void check_chain_err(Ctx& c) {
     throw std::runtime_error("Gram-Schmidt chain: a workgroup timed out waiting for a hand-off");
   }
 }
-// Host spin on a sequence flag a kernel writes to mapped host memory; throws
-// if the stream went idle (or failed) without raising it.
-void spin_until(Ctx& c, const volatile unsigned long long* f, unsigned long long seq) {
-  for (long spins = 1; *f != seq; ++spins) {
-    if ((spins & 0xFFFFF) == 0) {
-      const hipError_t q = hipStreamQuery(c.stream);
-      if (q != hipErrorNotReady && *f != seq) {
-        DCP_HIP_CHECK(q);
-        throw std::runtime_error("gmres_schur: stream idle without the ready flag");
-      }
-    }
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
-  }
-  std::atomic_thread_fence(std::memory_order_acquire);
-}
-
 ChainVecs chain_vecs(const std::vector<double*>& V, int dim) {
   ChainVecs cv{};
   for (int i = 0; i < dim; ++i) cv.v[i] = V[i];
@@ -348,7 +324,8 @@ State aztec_gmres(Ctx& c, int n, Seg g, const Op& A, const Op& Minv, double* x, 
     return std::sqrt(dot_host(c, g, r, r, kSlotA));
   };
   double rnorm = residual();
-  bool converged = rnorm < tol;
+  // <= as SolverControl: a zero rhs (tol 0) with a zero residual is converged
+  bool converged = rnorm <= tol;
   int iter = 0;
   while (!converged && iter < max_it) {
     equ(n, DScal{nullptr, 1.0 / rnorm}, r, tv[0], c.stream);
@@ -379,13 +356,13 @@ State aztec_gmres(Ctx& c, int n, Seg g, const Op& A, const Op& Minv, double* x, 
         h[k + 1] = cs[k] * h[k + 1] - sn[k] * t;
       }
       const double d = std::sqrt(h[i] * h[i] + h[i + 1] * h[i + 1]);
-      cs[i] = h[i] / d;
-      sn[i] = h[i + 1] / d;
+      cs[i] = d != 0 ? h[i] / d : 1.0;  // d = 0: an exact breakdown, no rotation
+      sn[i] = d != 0 ? h[i + 1] / d : 0.0;
       rs[i + 1] = -sn[i] * rs[i];
       rs[i] = cs[i] * rs[i];
       h[i] = cs[i] * h[i] + sn[i] * h[i + 1];
       for (int k = 0; k <= i; ++k) H[k][i] = h[k];
-      cycle_converged = std::fabs(rs[i + 1]) < tol;
+      cycle_converged = std::fabs(rs[i + 1]) <= tol;
       ++i;
     }
     std::vector<double> y(i, 0.0);
@@ -399,7 +376,7 @@ State aztec_gmres(Ctx& c, int n, Seg g, const Op& A, const Op& Minv, double* x, 
     Minv(r, z);
     axpy(n, DScal{nullptr, 1.0}, z, x, c.stream);
     rnorm = residual();
-    converged = cycle_converged && rnorm < tol;
+    converged = cycle_converged && rnorm <= tol;
   }
   iters += iter;
   return rnorm <= tol ? kSuccess : kFailure;
@@ -409,20 +386,14 @@ Timer* schur_sample(Ctx& c);
 
 // The inner Schur GMRES of block_prec on the explicit S (identity
 // preconditioner): the same deal.II SolverGMRES as gmres() above, with the
-// vector work fused so one Arnoldi step is 1 + dim launches and one readback:
+// vector work fused so one Arnoldi step is two launches and one readback:
 //   * S v_k is the SELL SpMV of the unscaled previous vector w times 1/|w|
 //     (bitwise the product with the scaled vector), and the same launch
 //     stores v_k = w/|w| and the partials of (S v_k).v_0 and |S v_k|^2;
-//   * the modified Gram-Schmidt chain starts from those partials.
-// Pipelining: step k+1 is enqueued before the host has read step k back (the
-// SpMV derives 1/|w_k| from the chain's partials itself), so the GPU never
-// waits for the host's Givens/convergence work. Step k+1 is launched ahead
-// unless re-orthogonalisation is on, k ends the cycle, or the residual is
-// predicted to converge at k. A launched-ahead step that turns out unneeded
-// (converged at k) writes only scratch: the next basis vector, the other w
-// buffer and the other parity's slots; one launched ahead of a loss-of-
-// orthogonality test (every 5th step) that triggers is relaunched on the
-// re-orthogonalised w and overwrites all of it.
+//   * the modified Gram-Schmidt chain starts from those partials (one launch
+//     on one GPU, k_mgs_chain; one launch per basis vector on several).
+// The host reads the step's coefficients and |w| back, does the Givens step
+// and the SolverControl check, and launches the next step with 1/|w|.
 State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                           std::vector<double*>& tv, int n_tmp);
 
@@ -457,85 +428,48 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   int dim = 0;
   State st = kIterate;
   bool reorth = false;
-  bool left_in_flight = false;  // the last cycle ended with a launched-ahead step unneeded
-  auto base = [](int it) { return kSpecBase + (it & 1) * kSpecStride; };
-  double* const hmir0 = c.comm ? nullptr : c.hmapped;
-  unsigned long long step_seq[2] = {0, 0};
   // Arnoldi step `it`: v_it = src * cf (stored by the SpMV for it > 0), S v_it,
-  // the chain, the readback of the step's block. ahead: cf from the device;
-  // on one GPU the SpMV of a launched-ahead step also raises step it-1's
-  // ready flag (no event between the launches: each costs ~3 us of device time).
-  // res_seq != 0 (step 0 only): launched ahead of the restart's convergence
-  // check, from the unscaled residual p: v_0 = p/|p| with |p| from the
-  // kResPart partials, and |p| handed to the host in the residual block.
-  auto launch = [&](int it, double cf, bool ahead, unsigned long long res_seq = 0) {
-    const int B0 = base(it);
+  // the chain into the step block (coefficients, start norm, final partials of
+  // |w|^2), which comes back to the host; returns |w| (the device's
+  // block_sum order, summed on the host)
+  auto step = [&](int it, double cf, const double*& hp) {
     double* w = wbuf[it & 1];
-    double* src = it == 0 ? (res_seq ? p : tv[0]) : wbuf[(it - 1) & 1];
+    double* src = it == 0 ? tv[0] : wbuf[(it - 1) & 1];
     halo_exchange(c, c.halo_p, src);
     Timer* e = schur_sample(c);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-    step_seq[it & 1] = ++c.spec_seq;
-    StepReady rdy{};
-    if (hmir0 && ahead && c.schur_ready_flag)
-      rdy = StepReady{hmir0 + base(it - 1), slot(c, base(it - 1)), it, step_seq[(it - 1) & 1]};
-    if (res_seq) rdy = StepReady{hmir0 + kResBlock, slot(c, B0), 0, res_seq};
-    const double* nrm_part = res_seq ? slot(c, kResPart)
-                                     : (ahead ? slot(c, base(it - 1) + kSpPart) : nullptr);
-    sell_spmv_fused(c.sell(), src, cf, it > 0 || res_seq ? tv[it] : nullptr, w, tv[0], part0,
-                    part1, nbs, nrm_part, nb, slot(c, B0 + kSpNorm), rdy, c.stream);
+    sell_spmv_fused(c.sell(), src, cf, it > 0 ? tv[it] : nullptr, w, tv[0], part0, part1, nbs,
+                    c.stream);
     if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
     allreduce(c, part0, 2 * size_t(nbs));
     const int d = it + 1;
     const bool consider = !reorth && (it % 5 == 4);
-    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i;
-    // coefficients, start norm and final partials into the step's device block
+    // chain: h_0 from the SpMV partials, then h_i = (w -= h_{i-1} v_{i-1}).v_i
     if (fused_chain_ok(c, g, nb, d)) {  // the whole chain in one launch
       mgs_chain(g, w, chain_vecs(tv, d), d, part0, nbs, consider ? part1 : nullptr,
-                slot(c, B0 + kSpNStart), slot(c, B0), slot(c, B0 + kSpPart), nullptr, nb,
-                c.chain_gran.p, ++c.chain_seq, chain_err(c), c.stream);
+                slot(c, kStepBlock + kSpNStart), slot(c, kStepBlock),
+                slot(c, kStepBlock + kSpPart), nullptr, nb, c.chain_gran.p, ++c.chain_seq,
+                chain_err(c), c.stream);
     } else {
       const double* prev = part0;
       int nprev = nbs;
       for (int i = 1; i <= d; ++i) {
         const bool last = i == d;
-        double* out = last ? slot(c, B0 + kSpPart) : pbuf(c, i & 1);
+        double* out = last ? slot(c, kStepBlock + kSpPart) : pbuf(c, i & 1);
         chain_add_and_dot_ex(g, w, prev, nprev, -1.0, tv[i - 1], last ? w : tv[i], out,
-                             slot(c, B0 + i - 1), nb, i == 1 && consider ? part1 : nullptr,
-                             slot(c, B0 + kSpNStart), nullptr, c.stream);
+                             slot(c, kStepBlock + i - 1), nb, i == 1 && consider ? part1 : nullptr,
+                             slot(c, kStepBlock + kSpNStart), nullptr, c.stream);
         allreduce(c, out, nb);
         prev = out;
         nprev = nb;
       }
     }
-    if (!hmir0 || !c.schur_ready_flag) {  // the step's block down behind an event
-      DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B0, slot(c, B0), (kSpPart + nb) * sizeof(double),
-                                   hipMemcpyDeviceToHost, c.stream));
-      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
-    }
-  };
-  // step `it` complete on the host; returns its block and |w|. One GPU: spin
-  // on the ready flag a launched-ahead next step's SpMV raises, or copy the
-  // block down behind an event now (nothing follows the step yet); several
-  // GPUs: the copy and event launch() queued.
-  auto wait_step = [&](int it, bool ahead_launched, double& norm) -> const double* {
-    if (hmir0 && ahead_launched && c.schur_ready_flag) {
-      const double* hp = hmir0 + base(it);
-      spin_until(c, reinterpret_cast<const volatile unsigned long long*>(hp + kSpReady),
-                 step_seq[it & 1]);
-      norm = hp[kSpReadyNorm];
-      return hp;
-    }
-    const int B = base(it);
-    if (hmir0 && c.schur_ready_flag) {
-      DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + B, slot(c, B), (kSpPart + nb) * sizeof(double),
-                                   hipMemcpyDeviceToHost, c.stream));
-      DCP_HIP_CHECK(hipEventRecord(c.spec_ev[it & 1], c.stream));
-    }
-    DCP_HIP_CHECK(hipEventSynchronize(c.spec_ev[it & 1]));
-    const double* hp = c.hpinned + B;
-    norm = std::sqrt(block_sum_host(hp + kSpPart, nb));
-    return hp;
+    DCP_HIP_CHECK(hipMemcpyAsync(c.hpinned + kStepBlock, slot(c, kStepBlock),
+                                 (kSpPart + nb) * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    check_chain_err(c);
+    hp = c.hpinned + kStepBlock;
+    return std::sqrt(block_sum_host(hp + kSpPart, nb));
   };
   do {
     std::fill(h.begin(), h.end(), 0.0);
@@ -544,50 +478,19 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     else
       schur_vmult(c, x, p);
     sadd(n, -1., 1., b, p, c.stream);  // p = b - S x
-    double rho;
-    if (hmir0 && c.schur_ready_flag && c.schur_ahead) {
-      // |p| from nb block partials (the host sums them in the device's order);
-      // step 0 runs while the host checks convergence (wasted scratch if so)
-      dot_partial(g, p, p, slot(c, kResPart), nb, c.stream);
-      const unsigned long long rs = ++c.spec_seq;
-      launch(0, 1.0, false, rs);
-      const volatile unsigned long long* f =
-          reinterpret_cast<const volatile unsigned long long*>(hmir0 + kResBlock + kSpReady);
-      spin_until(c, f, rs);
-      rho = hmir0[kResBlock + kSpReadyNorm];
-      st = ctl.check(accumulated, rho);
-      if (st != kIterate) {
-        DCP_HIP_CHECK(hipStreamSynchronize(c.stream));  // let the unneeded step finish
-        check_chain_err(c);
-        break;
-      }
-    } else {
-      copy(n, p, tv[0], c.stream);  // identity preconditioner
-      rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
-      st = ctl.check(accumulated, rho);
-      if (st != kIterate) break;
-      scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
-      launch(0, 1.0, false);
-    }
+    copy(n, p, tv[0], c.stream);       // identity preconditioner
+    double rho = std::sqrt(dot_host(c, g, tv[0], tv[0], kSlotA));
+    st = ctl.check(accumulated, rho);
+    if (st != kIterate) break;
+    scale(n, DScal{nullptr, 1. / rho}, tv[0], c.stream);
     gamma[0] = rho;
-    double rho_prev = rho;
-    double prev_norm = 0;   // |w| of the previous step (host value)
-    bool prev_ahead = false;
+    double cf = 1.0;
     for (int inner = 0; inner < n_tmp - 2 && st == kIterate; ++inner) {
       ++accumulated;
       dim = inner + 1;
       const bool consider = !reorth && (inner % 5 == 4);
-      // launch step inner+1 now unless step inner may change it
-      const double rho_pred = rho * (rho / rho_prev);
-      const bool ahead = c.schur_ahead && !reorth && inner + 1 < n_tmp - 2 &&
-                         accumulated < ctl.max_steps &&
-                         rho_pred > 2.0 * ctl.tol;
-      if (ahead) launch(inner + 1, 0.0, true);
-      double norm_vv = 0;
-      const double* hp = wait_step(inner, ahead, norm_vv);
-      check_chain_err(c);
-      if (prev_ahead && hp[kSpNorm] != prev_norm)  // the launched-ahead SpMV's 1/|w|
-        throw std::runtime_error("gmres_schur: device and host |w| differ");
+      const double* hp = nullptr;
+      double norm_vv = step(inner, cf, hp);
       hv.assign(hp, hp + dim);
       const double start2 = consider ? hp[kSpNStart] : 0.0;
       for (int i = 0; i < dim; ++i) h[i] = hv[i];
@@ -604,19 +507,11 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
       h[inner + 1] = norm_vv;
       givens_rotation(h, gamma, ci, si, inner);
       for (int i = 0; i < dim; ++i) H[i][inner] = h[i];
-      rho_prev = rho;
       rho = std::fabs(gamma[dim]);
       st = ctl.check(accumulated, rho);
-      prev_norm = norm_vv;
-      // a step launched ahead of a loss-of-orthogonality test that triggered
-      // used the first-pass w: relaunch it (stream order puts it after the
-      // ahead step and the second pass; it rewrites everything that step wrote)
-      const bool redo = ahead && second;
-      prev_ahead = ahead && !redo;
-      left_in_flight = ahead && !redo && st != kIterate;
-      if (st == kIterate && (!ahead || redo) && inner + 1 < n_tmp - 2)
-        launch(inner + 1, norm_vv != 0 ? 1. / norm_vv : 1.0, false);
+      cf = norm_vv != 0 ? 1. / norm_vv : 1.0;
     }
+    // the last step's w was never scaled into the basis: nothing else to do
     std::vector<double> y(dim, 0.0);
     for (int i = dim - 1; i >= 0; --i) {
       double sum = gamma[i];
@@ -625,12 +520,6 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     }
     combine(c, n, y, tv, x);
   } while (st == kIterate);
-  if (left_in_flight) {
-    // an unneeded launched-ahead step may still be running: its chain's
-    // timeout flag belongs to this solve
-    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
-    check_chain_err(c);
-  }
   return st;
 }
 
@@ -698,12 +587,13 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                         ++c.chain_seq, chain_err(c), c.stream);
       else
         cgs2_gmres_step(g, w, chain_vecs(tv, k + 1), k + 1, c.gm_part.p, c.gm_cnt.p, dst,
-                        c.chain_seq, comm ? c.dscal.p + kSlotD : chain_err(c), comm, c.stream);
+                        c.chain_seq, comm ? slot(c, kSlotErr) : chain_err(c), comm, c.stream);
     }
     // tail: H y = gamma, x += V y, the report for the host
     gmres_cycle_end(dst, n, c.gm_ptrs.p, x, &c.gm_report[cyc & 1], c.stream);
     DCP_HIP_CHECK(hipEventRecord(c.gm_ev[cyc & 1], c.stream));
   };
+  if (comm) fill(1, 0.0, slot(c, kSlotErr), c.stream);
   int cyc = 0;
   enqueue_cycle(cyc);
   for (;;) {
@@ -714,7 +604,14 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     ++cyc;
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
-  if (!comm) check_chain_err(c);
+  if (!comm) {
+    check_chain_err(c);
+  } else {
+    // a timed-out hand-off on any rank fails the solve on every rank
+    allreduce(c, slot(c, kSlotErr), 1, true);
+    if (fetch(c, kSlotErr, 1)[0] != 0.0)
+      throw std::runtime_error("CGS2 step: a workgroup timed out waiting for a hand-off");
+  }
   // every cycle queued after the stop left the state alone: the report of
   // cycle cyc is final
   const GmresReport& r = c.gm_report[cyc & 1];
@@ -1003,6 +900,7 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
 }
 
 void free_workspaces(Ctx& c) {
+  c.ilu.reset();  // built on first use per mesh (build_ilu)
   for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v, &c.fe_v, &c.fe_s, &c.fe_n, &c.sc_v, &c.sc_p}) {
     for (double* p : *pool) (void)hipFree(p);
     pool->clear();
@@ -1014,7 +912,6 @@ void ensure_workspaces(Ctx& c) {
     c.dscal.alloc(kNumSlots);
     c.partials.alloc(4 * size_t(kChainMaxBlocks));
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hpinned), kNumSlots * sizeof(double)));
-    for (auto& ev : c.spec_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     // coherent mapped host memory the kernels write directly (uncached on the GPU)
     DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.hmapped), kNumSlots * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
@@ -1132,7 +1029,7 @@ State pcg(Ctx& c, int n, Seg g, const Op& A, const Op& P, double* x, const doubl
 // the dependency levels (built once per mesh)
 void build_ilu(Ctx& c) {
   Ctx::Ilu& f = c.ilu;
-  if (f.n == c.n_u && f.ptr.p) return;
+  if (f.ptr.p) return;  // reset by every mesh upload (free_workspaces)
   const int nb = c.nvo;
   std::vector<int32_t> bp(nb + 1), bc;
   DCP_HIP_CHECK(hipMemcpy(bp.data(), c.A_ptr.p, (nb + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));

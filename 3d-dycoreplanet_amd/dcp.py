@@ -34,10 +34,12 @@ OPT_ASSEMBLE_VELOCITY_BLOCK = 6
 OPT_ELEMENT_MFMA = 9
 OPT_GRAM_SCHMIDT = 7
 OPT_FEEC_FIXED_INNER = 8
+ABI_VERSION = 3            # include/dcp.h DCP_ABI_VERSION
+CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
 EXPORTED = [
-    "dcp_ctx_create", "dcp_ctx_destroy", "dcp_last_error", "dcp_device_count",
+    "dcp_abi_version", "dcp_ctx_create", "dcp_ctx_destroy", "dcp_last_error", "dcp_device_count",
     "dcp_set_physics", "dcp_set_time_step", "dcp_set_option", "dcp_mesh_upload", "dcp_mesh_check", "dcp_state_set",
     "dcp_state_get", "dcp_state_copy", "dcp_state_device_ptr", "dcp_assemble_nse_system",
     "dcp_build_nse_preconditioner", "dcp_assemble_temperature_matrix",
@@ -151,6 +153,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the hot path has no CPU fallback)")
     lib = C.CDLL(path)
+    if not hasattr(lib, "dcp_abi_version") or lib.dcp_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: ABI version {getattr(lib, 'dcp_abi_version', lambda: '?')()}"
+                          f" != {ABI_VERSION} (rebuild libdcp.so against include/dcp.h)")
     P, D, I = C.c_void_p, C.POINTER(C.c_double), C.c_int
     lib.dcp_last_error.restype = C.c_char_p
     lib.dcp_last_error.argtypes = [P]

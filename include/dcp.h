@@ -46,6 +46,16 @@ enum {
   DCP_ERR_STATE = -4          /* call out of order (e.g. solve before assemble) */
 };
 
+/* Version of this interface. It changes whenever a struct layout, an array
+ * shape or a signature below changes (round 2 widened cell_geometry from
+ * [n][27][3] to [n][64][3] and added a dcp_host_mesh_create parameter without
+ * one). A caller compiled against another header must refuse to run:
+ * dcp_abi_version() != DCP_ABI_VERSION. */
+#define DCP_ABI_VERSION 3
+int dcp_abi_version(void);
+/* Support points per cell in cell_geometry (MappingQ(3): 4^3). */
+#define DCP_CELL_SUPPORT_POINTS 64
+
 typedef struct dcp_ctx dcp_ctx;
 
 /* Derived, non-dimensional model constants (CoreModelData::Parameters after

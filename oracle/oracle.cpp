@@ -974,7 +974,8 @@ void aztec_gmres(int n, OpA A, OpP Minv, double* x, const double* b, double tol,
     return std::sqrt(dotv(r.data(), r.data(), n));
   };
   double rnorm = residual();
-  bool converged = rnorm < tol;
+  // <= as SolverControl: a zero rhs (tol 0) with a zero residual is converged
+  bool converged = rnorm <= tol;
   int iter = 0;
   while (!converged && iter < max_it) {
     for (int k = 0; k < n; ++k) v[0][k] = r[k] / rnorm;
@@ -1002,13 +1003,13 @@ void aztec_gmres(int n, OpA A, OpP Minv, double* x, const double* b, double tol,
         h[k + 1] = cs[k] * h[k + 1] - sn[k] * t;
       }
       const double d = std::sqrt(h[i] * h[i] + h[i + 1] * h[i + 1]);
-      cs[i] = h[i] / d;
-      sn[i] = h[i + 1] / d;
+      cs[i] = d != 0 ? h[i] / d : 1.0;  // d = 0: an exact breakdown, no rotation
+      sn[i] = d != 0 ? h[i + 1] / d : 0.0;
       rs[i + 1] = -sn[i] * rs[i];
       rs[i] = cs[i] * rs[i];
       h[i] = cs[i] * h[i] + sn[i] * h[i + 1];
       for (int k = 0; k <= i; ++k) H[k][i] = h[k];
-      cycle_converged = std::fabs(rs[i + 1]) < tol;
+      cycle_converged = std::fabs(rs[i + 1]) <= tol;
       ++i;
     }
     // y = H^-1 rs (upper triangular), x += M^-1 (V y)
@@ -1024,7 +1025,7 @@ void aztec_gmres(int n, OpA A, OpP Minv, double* x, const double* b, double tol,
     Minv(w.data(), z.data());
     for (int q = 0; q < n; ++q) x[q] += z[q];
     rnorm = residual();
-    converged = cycle_converged && rnorm < tol;
+    converged = cycle_converged && rnorm <= tol;
   }
   iters_out = iter;
   if (!(rnorm <= tol)) throw NoConvergence();

@@ -29,6 +29,17 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_abi_version_matches_header():
+    """DCP_ABI_VERSION in include/dcp.h, the library's dcp_abi_version() and the
+    binding's ABI_VERSION agree; the binding refuses a library built against
+    another header (layout changes such as [n][27][3] -> [n][64][3] geometry)."""
+    text = open(os.path.join(ROOT, "include", "dcp.h")).read()
+    v = int(re.search(r"#define DCP_ABI_VERSION (\d+)", text).group(1))
+    pts = int(re.search(r"#define DCP_CELL_SUPPORT_POINTS (\d+)", text).group(1))
+    assert v == dcp.ABI_VERSION == ctypes.CDLL(dcp.LIB_PATH).dcp_abi_version()
+    assert pts == dcp.CELL_SUPPORT_POINTS == dcp.HostMesh(refine=0).cell_geometry.shape[1]
+
+
 def test_no_cpu_fallback():
     if dcp.lib().dcp_device_count() > 0:
         pytest.skip("a GPU is present")

@@ -103,3 +103,31 @@ def test_run_cube_prm_uses_the_schur_solver():
     ctx.close()
     assert rc == 0 and rep.steps == 1
     assert rep.fgmres_outer == 0 and rep.schur_inner > 0
+
+
+@pytest.mark.gpu
+def test_schur_solver_after_reupload_with_another_numbering():
+    """The ILU(0) structure (pattern, levels, A_val positions) is built once per
+    mesh: uploading the Cuthill-McKee copy of the same mesh (same n_u, other
+    numbering) into the same context must rebuild it, so the second solve
+    matches the oracle on the new numbering exactly like a fresh context."""
+    rng = np.random.default_rng(11)
+    ctx = dcp.Context()
+    try:
+        for name in ("cube-r2", "cube-r2-cm"):
+            m, ph = case(name)
+            u = 0.1 * rng.uniform(-1, 1, m.n_u + m.n_p)
+            T = m.T0.copy()
+            ctx.set_physics(ph)
+            ctx.upload_mesh(m)
+            for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u),
+                         (dcp.OLD_T_SOLUTION, T), (dcp.T_SOLUTION, T)):
+                ctx.set_state(f, v)
+            ctx.assemble_nse_system()
+            rc, its, na = ctx.solve_nse_schur()
+            x = ctx.get_state(dcp.NSE_SOLUTION)
+            rco, xo, itso, nao = oracle_solve(m, ph, ctx.get_state(dcp.OLD_NSE_SOLUTION), T)
+            assert rc == rco == 0 and (its, na) == (itso, nao), name
+            assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo), name
+    finally:
+        ctx.close()
