@@ -409,6 +409,9 @@ struct Cons {
   }
 };
 
+// threads of the row-parallel operator applies (orc_set_threads; default 1)
+int g_threads = 1;
+
 struct Csr {
   int n = 0;
   std::vector<int> rowptr, cols;
@@ -429,6 +432,20 @@ struct Csr {
     return vals[it - cols.begin()];
   }
   void zero() { std::fill(vals.begin(), vals.end(), 0.0); }
+  // per row, the first entry with column >= c (the pattern never changes
+  // after build, so the table is built once per boundary)
+  mutable std::vector<int> split;
+  mutable int split_col = -1;
+  const int* split_at(int c) const {
+    if (split_col != c || int(split.size()) != n) {
+      split.resize(n);
+      for (int r = 0; r < n; ++r)
+        split[r] = int(std::lower_bound(cols.begin() + rowptr[r], cols.begin() + rowptr[r + 1], c) -
+                       cols.begin());
+      split_col = c;
+    }
+    return split.data();
+  }
 };
 
 void add_sorted_unique(std::vector<int>& v) {
@@ -785,14 +802,35 @@ namespace {
 
 // Block SpMV pieces of the NSE matrix (TrilinosWrappers::BlockSparseMatrix):
 // each block sums its row in column order; blocks are added afterwards.
+// A row's entries inside [col0, col1): the NSE blocks split every row at
+// column n_u (Csr::split, the first entry >= n_u, cached per boundary), so a
+// block visits only its own entries, as a separately stored Trilinos block
+// does. Rows are independent: g_threads > 1 splits them across threads with
+// bitwise the same sums (the CPU baseline's multi-core leg).
 void block_vmult(const Csr& A, int row0, int row1, int col0, int col1, const double* src,
                  double* dst, bool add) {
+  const int* sp = nullptr;
+  bool lo = false;
+  if (col0 > 0 && col1 >= A.n) {
+    sp = A.split_at(col0);
+    lo = false;  // [split, end)
+  } else if (col0 == 0 && col1 < A.n) {
+    sp = A.split_at(col1);
+    lo = true;   // [begin, split)
+  }
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
   for (int r = row0; r < row1; ++r) {
-    double s = 0;
-    for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k) {
-      const int c = A.cols[k];
-      if (c >= col0 && c < col1) s += A.vals[k] * src[c - col0];
+    int k0 = A.rowptr[r], k1 = A.rowptr[r + 1];
+    if (sp) {
+      if (lo) k1 = sp[r]; else k0 = sp[r];
+    } else {
+      const int* b = A.cols.data() + k0;
+      const int* e = A.cols.data() + k1;
+      k0 = int(std::lower_bound(b, e, col0) - A.cols.data());
+      k1 = int(std::lower_bound(b, e, col1) - A.cols.data());
     }
+    double s = 0;
+    for (int k = k0; k < k1; ++k) s += A.vals[k] * src[A.cols[k] - col0];
     if (add) dst[r - row0] += s; else dst[r - row0] = s;
   }
 }
@@ -1181,6 +1219,8 @@ State fgmres(orc_model* m, double* x, const double* b, int basis_size, unsigned 
 
 }  // namespace
 
+extern "C" void orc_set_threads(int n) { g_threads = n > 1 ? n : 1; }
+
 extern "C" void orc_nse_vmult(const orc_model* m, const double* src, double* dst) {
   nse_vmult(m, src, dst);
 }
@@ -1230,6 +1270,25 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
   if (inner_it) *inner_it = inner;
   m->inner_iterations = inner;
   return status;
+}
+
+// Timing hook (bench cpu_baseline): the first FGMRES(30) of
+// solve_NSE_block_preconditioned cut at k outer iterations (SolverControl(k)),
+// no fallback; the initial guess as the solve sets it up. Returns the
+// iterations done, inner Schur GMRES iterations to *inner_it.
+extern "C" int orc_fgmres_outer(orc_model* m, const double* sol, int k, int* inner_it) {
+  const int nu = m->n_u, np = m->n_p, n = nu + np;
+  const double dt = m->ph.time_step;
+  std::vector<double> x(sol, sol + n);
+  for (int i = nu; i < n; ++i) x[i] *= dt * dt;  // :1151, :1177 (Q1)
+  const double tol = 1e-8 * norm2(m->nse_rhs, 0, n);
+  int inner = 0, acc = 0;
+  try {
+    (void)fgmres(m, x.data(), m->nse_rhs.data(), 30, unsigned(k), tol, false, acc, inner);
+  } catch (const NoConvergence&) {
+  }
+  if (inner_it) *inner_it = inner;
+  return acc;
 }
 
 extern "C" long orc_a_solve_iterations(const orc_model* m) { return m->a_solve_iterations; }

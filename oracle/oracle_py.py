@@ -70,6 +70,8 @@ def lib():
         L.orc_solve_nse_schur.argtypes = [P, P, P, P]
         L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
         L.orc_set_inner_max_steps.argtypes = [P, I]
+        L.orc_set_threads.argtypes = [I]
+        L.orc_fgmres_outer.argtypes = [P, P, I, P]
         L.orc_a_solve_iterations.argtypes = [P]
         L.orc_a_solve_iterations.restype = C.c_long
         L.orc_max_velocity.argtypes = [P, P]
@@ -233,6 +235,14 @@ class Model:
         o, i = C.c_int(0), C.c_int(0)
         rc = lib().orc_solve_nse(self.h, _p(x), C.byref(o), C.byref(i), int(max_outer))
         return rc, x, o.value, i.value
+
+    def fgmres_outer(self, nse_solution, k):
+        """Timing hook: the first FGMRES(30) cut at k outer iterations, no
+        fallback -> (outer iterations done, inner Schur GMRES iterations)."""
+        i = C.c_int(0)
+        o = lib().orc_fgmres_outer(self.h, _p(np.ascontiguousarray(nse_solution, np.float64)),
+                                   int(k), C.byref(i))
+        return o, i.value
 
     def a_solve_iterations(self):
         """AztecOO A-GMRES iterations of the last solve_nse (do_solve_A fallback)."""

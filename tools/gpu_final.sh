@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round-end GPU call: the driver's smoke(), then the parity suite, the bench
-# line and its rocprofv3 kernel stats (tools/r02_gpu_round.sh).
+# line and its rocprofv3 kernel stats (tools/gpu_round.sh).
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -5 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log
-bash tools/r02_gpu_round.sh
+bash tools/gpu_round.sh

@@ -35,7 +35,7 @@ for path in libs or [dcp.LIB_PATH]:
     per = []
     with dcp.DeviceBuffer(n) as ds, dcp.DeviceBuffer(n) as dd:
         ds.upload(x)
-        for rep in range(5):
+        for rep in range(int(os.environ.get("REPS", "5"))):
             it = C.c_int(0)
             hip.hipDeviceSynchronize()
             t0 = time.perf_counter()
