@@ -1081,7 +1081,7 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       return DCP_OK;
     }
     if (option == DCP_OPT_GRAM_SCHMIDT) {
-      require(value == 0 || value == 1, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0 or 1");
+      require(value >= 0 && value <= 2, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0, 1 or 2");
       ctx->gram_schmidt = value;
       return DCP_OK;
     }

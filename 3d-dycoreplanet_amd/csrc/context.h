@@ -217,14 +217,15 @@ struct Ctx {
   int n_cus = 0;
   bool fused_chain = true;
   // DCP_OPT_GRAM_SCHMIDT: 0 = modified (deal.II SolverGMRES, default), 1 = the
-  // inner Schur GMRES with classical Gram-Schmidt twice, each restart cycle
-  // device-resident (kernels/krylov.hip): state, polled status, partials,
-  // basis pointer table
+  // inner Schur GMRES with classical Gram-Schmidt twice, 2 = DCGS2 (one
+  // reduction per step), each restart cycle device-resident
+  // (kernels/krylov.hip): state, polled status, partials, basis pointer table
   int gram_schmidt = 0;
   DBuf<GmresDev> gm_state;
   GmresReport* gm_report = nullptr;  // pinned [2]: the reports of the last two cycles
   hipEvent_t gm_ev[2] = {nullptr, nullptr};
   DBuf<double> gm_part;
+  DBuf<double> dcgs_gran;            // hand-off granules of the DCGS2 steps (their own tag scheme)
   DBuf<unsigned> gm_cnt;             // last-block counter of the CGS2 launches
   DBuf<const double*> gm_ptrs;
   std::vector<const double*> gm_ptrs_host;

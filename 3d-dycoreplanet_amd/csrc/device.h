@@ -376,7 +376,7 @@ void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, 
 // SolverControl decision (status 0: iterate, 1: success, 2: failure).
 constexpr int kGmMaxDim = 32;
 struct GmresDev {
-  double H[kGmMaxDim][kGmMaxDim];
+  double H[kGmMaxDim][kGmMaxDim];   // rotated columns (R of the Givens QR), back substitution
   double gamma[kGmMaxDim + 1], ci[kGmMaxDim], si[kGmMaxDim];
   double coef[2 * kGmMaxDim];   // this step's first / second pass coefficients
   double y[kGmMaxDim];          // back-substituted combination coefficients
@@ -384,6 +384,11 @@ struct GmresDev {
   double nrm2;                  // |w|^2 of the last step
   double inv_rho;               // 1 / the residual norm at the start of the cycle
   int status, dim, accumulated, max_steps;
+  // DCGS2 (one reduction per step, delayed re-orthogonalisation): the raw
+  // Hessenberg columns (provisional column k until step k + 1 corrects it)
+  // and the pending scale nu_k / beta_k of that correction
+  double Hr[kGmMaxDim + 1][kGmMaxDim];
+  double c_pend;
 };
 // What the host reads after a cycle (pinned, written by gmres_cycle_end)
 struct GmresReport {
@@ -407,6 +412,24 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
 void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,
                      GmresDev* st, unsigned long long& seq, double* err, Comm* comm,
                      hipStream_t s);
+// DCGS2 Arnoldi step k (delayed classical Gram-Schmidt with one global
+// reduction per step; Swirydowicz et al. 2020, Bielich et al. 2022) after
+// w = S t_k, where t_k = V[k] is the tentative (once orthogonalised) k-th
+// basis vector. One reduction gives V_{<k}^T [t w], t.t, t.w, w.w; then
+//   q_k = (t_k - V a) / beta, beta = sqrt(t.t - |a|^2)          -> V[k]
+//   t_{k+1} = (w - V z - g_k q_k) / nu, nu^2 = w.w - |g|^2      -> tnext
+// and the Hessenberg column k - 1 gets its correction (H[:k, k-1] += c a,
+// H[k, k-1] = c beta), its Givens rotation and the SolverControl check;
+// column k is left provisional. tail (tnext == null, w == null): only the
+// correction of column k - 1 (the cycle's last column). One launch of nb
+// resident workgroups on one GPU (dcgs2_fits, like cgs2_chain_fits), else
+// (several GPUs) partials + last-block reduction, all-reduce, update launch.
+bool dcgs2_fits(long n, int nb, int n_cus);
+// hand-off granules (doubles) dcgs2_step needs for vectors of n entries
+size_t dcgs2_granules(long n);
+void dcgs2_step(Seg g, const double* w, const ChainVecs& V, int k, double* tnext, GmresDev* st,
+                double* gran, unsigned* cnt, int nb, unsigned long long& seq, double* err,
+                Comm* comm, bool one_launch, hipStream_t s);
 // Restart-cycle head on the device (SolverGMRES's start of a cycle):
 // rho = sqrt(*rho2) of the residual b - S x, SolverControl::check(accumulated,
 // rho), gamma_0 = rho, inv_rho = 1 / rho. first: a new solve (tol, max_steps,

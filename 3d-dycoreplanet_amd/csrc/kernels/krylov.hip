@@ -582,6 +582,447 @@ void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, 
     cgs_step_k<kGmMaxDim>(g, w, V, d, gran, cnt, st, seq, err, comm, s);
 }
 
+// ---------------------------------------------------------------------------
+// DCGS2: delayed classical Gram-Schmidt, one reduction per Arnoldi step.
+// Step k holds the final basis q_0..q_{k-1} (V[0..k)), the tentative t_k
+// (V[k]: once orthogonalised at step k - 1 and scaled by the Pythagorean
+// norm estimate) and w = S t_k. Its one reduction is
+//   slots [0, k): a_i = q_i.t      slot KP - 1: alpha = t.t
+//   slots [KP, KP + k): z_i = q_i.w   2 KP - 2: zeta = t.w   2 KP - 1: omega = w.w
+// (KP a power of two >= KL + 2, K = 2 KP slots, unused slots idle). Then, with
+// beta = sqrt(alpha - |a|^2) (k > 0; q_0 = t_0 is exact: beta = 1),
+//   q_k = (t - V a) / beta                       (the delayed second pass)
+//   g = [z; (zeta - a.z) / beta] = Q_{k+1}^T w
+//   u = w - V z - g_k q_k,  nu^2 = omega - |g|^2, t_{k+1} = u / nu
+// and the Arnoldi relation S q_k = (w - S V a) / beta gives the provisional
+// column H[:k+1, k] = (g - H[:k+1, :k] a) / beta, corrected one step later by
+// the reorthogonalisation of t_{k+1}: H[:k+1, k] += (nu/beta) a',
+// H[k+1, k] = (nu/beta) beta'. The column's Givens rotation and SolverControl
+// check therefore run one step late (its residual estimate is exactly the
+// one deal.II checks after step k; only one extra S apply at the end of a
+// solve is wasted), and the cycle ends with a tail launch that only corrects
+// its last column.
+template <int KL>
+constexpr int dcgs_kp() { return pow2_at_least<KL + 2>(); }
+// result granules after the partial area (2 K nb <= 2 * 64 * 256 doubles)
+constexpr int kDcgsRes = 2 * 64 * 256;
+
+template <int KP>
+__device__ inline bool dcgs_used(int j, int k, bool tail) {
+  if (j < KP) return j < k || j == KP - 1;
+  return !tail && (j - KP < k || j >= 2 * KP - 2);
+}
+
+// Reduce-scatter over a wave of the K products prod(j) (j compile-time after
+// unrolling), as wave_reduce_scatter: lane l ends with the wave sum of slot
+// l >> (6 - log2 K).
+template <int K, class F>
+__device__ inline double wave_rs(F prod) {
+  const int l = threadIdx.x & 63;
+  double s[K / 2];
+  {
+    const bool up = (l & 32) != 0;
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) {
+      const double lo = prod(i), hi = prod(i + K / 2);
+      s[i] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, 64);
+    }
+  }
+  int o = 16;
+#pragma unroll
+  for (int c = K / 2; c > 1; c >>= 1, o >>= 1) {
+    const bool up = (l & o) != 0;
+#pragma unroll
+    for (int i = 0; i < c / 2; ++i) {
+      const double send = up ? s[i] : s[i + c / 2];
+      const double keep = up ? s[i + c / 2] : s[i];
+      s[i] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  double r = s[0];
+  for (; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+  return r;
+}
+
+// The scalars of the step from the reduced slots r[] (every workgroup computes
+// them identically): beta, g_k, 1/nu.
+struct DcgsScalars {
+  double beta, gk, inv_nu, nu;
+};
+template <int KP>
+__device__ inline DcgsScalars dcgs_scalars(const double* r, int k, bool tail) {
+  DcgsScalars c;
+  double aa = 0, az = 0, zz = 0;
+  for (int i = 0; i < k; ++i) {
+    aa += r[i] * r[i];
+    az += r[i] * r[KP + i];
+    zz += r[KP + i] * r[KP + i];
+  }
+  c.beta = k > 0 ? sqrt(fmax(r[KP - 1] - aa, 0.0)) : 1.0;
+  if (tail) {
+    c.gk = 0;
+    c.nu = 0;
+    c.inv_nu = 1;
+    return c;
+  }
+  c.gk = (r[2 * KP - 2] - az) / c.beta;
+  const double nu2 = r[2 * KP - 1] - zz - c.gk * c.gk;
+  c.nu = sqrt(fmax(nu2, 0.0));
+  c.inv_nu = c.nu != 0 ? 1.0 / c.nu : 1.0;
+  return c;
+}
+
+// Workgroup 0 after the reduction: correct column k - 1 of the raw Hessenberg,
+// its Givens rotation (solver_gmres.h givens_rotation) on the rotated copy,
+// the residual estimate and SolverControl::check; then the provisional column
+// k. r[] in LDS (the reduced slots), every thread of the workgroup calls.
+template <int KP>
+__device__ void dcgs_bookkeeping(GmresDev* st, const double* r, int k, bool tail,
+                                 const DcgsScalars& c) {
+  __shared__ double h[kGmMaxDim + 1], hp[kGmMaxDim + 1];
+  __shared__ int stop;
+  const int t = threadIdx.x;
+  if (k > 0) {
+    const int col = k - 1;
+    const double cp = st->c_pend;
+    if (t < k) h[t] = st->Hr[t][col] + cp * r[t];
+    if (t == k) h[t] = cp * c.beta;
+    __syncthreads();
+    if (t <= k) st->Hr[t][col] = h[t];
+    if (t == 0) {
+      for (int i = 0; i < col; i++) {
+        const double cs = st->ci[i], sn = st->si[i], dummy = h[i];
+        h[i] = cs * dummy + sn * h[i + 1];
+        h[i + 1] = -sn * dummy + cs * h[i + 1];
+      }
+      const double rr = 1. / sqrt(h[col] * h[col] + h[col + 1] * h[col + 1]);
+      const double sn = h[col + 1] * rr, cs = h[col] * rr;
+      st->si[col] = sn;
+      st->ci[col] = cs;
+      h[col] = cs * h[col] + sn * h[col + 1];
+      const double g0 = st->gamma[col];
+      const double gk1 = -sn * g0;
+      st->gamma[col + 1] = gk1;
+      st->gamma[col] = g0 * cs;
+      const int acc = st->accumulated + 1;
+      st->accumulated = acc;
+      st->dim = k;
+      const double rho = fabs(gk1);
+      st->rho = rho;
+      const int status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+      st->status = status;
+      stop = status;
+    }
+    __syncthreads();
+    if (t <= col) st->H[t][col] = h[t];
+  } else if (t == 0) {
+    stop = 0;
+  }
+  __syncthreads();
+  if (tail || stop) return;
+  // provisional column k: (g - H[:k+1, :k] a) / beta, rows i <= k (Hessenberg:
+  // H[i][j] = 0 for i > j + 1)
+  if (t <= k) {
+    double s = t < k ? r[KP + t] : c.gk;
+    for (int j = t > 0 ? t - 1 : 0; j < k; ++j) s -= st->Hr[t][j] * r[j];
+    hp[t] = s / c.beta;
+  }
+  __syncthreads();
+  if (t <= k) st->Hr[t][k] = hp[t];
+  if (t == 0) st->c_pend = c.nu / c.beta;
+}
+
+// One GPU: the whole DCGS2 step in one launch of nb resident 512-thread
+// workgroups, two vector entries per thread (16-byte loads when WIDE), the k
+// basis entries in registers from the loads to the update. The reduction is
+// two granule hops as in k_cgs2_chain (every workgroup publishes its slot
+// sums, workgroup j sums slot j, every workgroup reads the results).
+template <int KL, bool WIDE>
+__global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const double* w, ChainVecs V,
+                                                              int k, double* tnext, GmresDev* st,
+                                                              double* gran, unsigned long long seq,
+                                                              double* err) {
+  constexpr int KP = dcgs_kp<KL>();
+  constexpr int K = 2 * KP;
+  __shared__ double sm[kChainWaves * K];
+  __shared__ double hs[K];
+  if (st->status) return;
+  const bool tail = tnext == nullptr;
+  const int nb = gridDim.x, b = blockIdx.x;
+  double tv[kChainEntries], wv[kChainEntries], v[kChainEntries][KL];
+  unsigned pos[kChainEntries];
+  bool live[kChainEntries];
+  const double* t_in = V.v[k];
+  const long kb = long(b) * (kChainThreads * kChainEntries);
+  if (WIDE) {
+    const long k0 = kb + 2 * long(threadIdx.x);
+    live[0] = live[1] = k0 < g.n;
+    pos[0] = live[0] ? unsigned(k0) : 0u;
+    pos[1] = pos[0] + 1;
+    const double2 tw = *reinterpret_cast<const double2*>(t_in + pos[0]);
+    tv[0] = tw.x;
+    tv[1] = tw.y;
+    double2 ww = {0.0, 0.0};
+    if (!tail) ww = *reinterpret_cast<const double2*>(w + pos[0]);
+    wv[0] = ww.x;
+    wv[1] = ww.y;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      const double2 a = *reinterpret_cast<const double2*>(V.v[j] + pos[0]);
+      v[0][j] = a.x;
+      v[1][j] = a.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < kChainEntries; ++e) {
+      const long kk = kb + e * kChainThreads + threadIdx.x;
+      live[e] = kk < g.n;
+      pos[e] = live[e] ? unsigned(seg_pos(g, kk)) : 0u;
+      tv[e] = t_in[pos[e]];
+      wv[e] = tail ? 0.0 : w[pos[e]];
+#pragma unroll
+      for (int j = 0; j < KL; ++j) v[e][j] = V.v[j][pos[e]];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kChainEntries; ++e) {
+    tv[e] = live[e] ? tv[e] : 0.0;
+    wv[e] = live[e] ? wv[e] : 0.0;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) v[e][j] = live[e] && j < k ? v[e][j] : 0.0;
+  }
+  auto prod = [&](int j) -> double {
+    if (j < KL) return v[0][j] * tv[0] + v[1][j] * tv[1];
+    if (j == KP - 1) return tv[0] * tv[0] + tv[1] * tv[1];
+    if (j >= KP && j < KP + KL) return v[0][j - KP] * wv[0] + v[1][j - KP] * wv[1];
+    if (j == 2 * KP - 2) return tv[0] * wv[0] + tv[1] * wv[1];
+    if (j == 2 * KP - 1) return wv[0] * wv[0] + wv[1] * wv[1];
+    return 0.0;
+  };
+  {
+    const double r = wave_rs<K>(prod);
+    const int l = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+    constexpr int sh = 6 - log2i<K>();
+    if ((l & ((1 << sh) - 1)) == 0) sm[wv_ * K + (l >> sh)] = r;
+  }
+  __syncthreads();
+  double* part = gran;
+  double* res = gran + kDcgsRes;
+  const unsigned long long tag = seq * 128;
+  const int j = threadIdx.x;
+  const bool used = j < K && dcgs_used<KP>(j, k, tail);
+  if (used) {
+    double tot = 0.0;
+    for (int i = 0; i < kChainWaves; ++i) tot += sm[i * K + j];
+    granule_store(part + 2 * (size_t(j) * nb + b), tot, tag + j);
+  }
+  // reducer: workgroup b sums slot b over the nb workgroups
+  if (b < K && dcgs_used<KP>(b, k, tail) && threadIdx.x < 64) {
+    const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag + b, err);
+    if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + K + b);
+  }
+  if (used) {
+    const double* p = res + 2 * j;
+    mgs_u4 q = granule_load(p);
+    for (long spins = 0; !tag_is(q, tag + K + j); ++spins) {
+      if (spins >= kMgsMaxSpins) {
+        *err = 1.0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      q = granule_load(p);
+    }
+    hs[j] = granule_value(q);
+  } else if (j < K) {
+    hs[j] = 0.0;
+  }
+  __syncthreads();
+  const DcgsScalars c = dcgs_scalars<KP>(hs, k, tail);
+  if (!tail || k > 0) {
+    const double ib = 1.0 / c.beta;
+#pragma unroll
+    for (int e = 0; e < kChainEntries; ++e) {
+      double q = tv[e];
+      if (k > 0) {
+#pragma unroll
+        for (int i = 0; i < KL; ++i)
+          if (i < k) q -= hs[i] * v[e][i];
+        q *= ib;
+      }
+      if (!tail) {
+        double u = wv[e];
+#pragma unroll
+        for (int i = 0; i < KL; ++i)
+          if (i < k) u -= hs[KP + i] * v[e][i];
+        u -= c.gk * q;
+        if (live[e]) tnext[pos[e]] = u * c.inv_nu;
+      }
+      if (k > 0 && live[e]) const_cast<double*>(t_in)[pos[e]] = q;
+    }
+  }
+  if (b != 0) return;
+  dcgs_bookkeeping<KP>(st, hs, k, tail, c);
+}
+
+// Several GPUs (or vectors too long for one resident launch): block sums of
+// the used slots as granules, the last block to arrive sums them in block
+// order into st->coef[0, K) (all-reduced across ranks by the host before the
+// update launch).
+template <int KL>
+__global__ __launch_bounds__(kBlock) void k_dcgs_partials(Seg g, const double* __restrict__ w,
+                                                          ChainVecs V, int k, bool tail,
+                                                          double* gran, unsigned* cnt,
+                                                          GmresDev* st, unsigned long long seq,
+                                                          double* err) {
+  constexpr int KP = dcgs_kp<KL>();
+  constexpr int K = 2 * KP;
+  __shared__ double sm[4 * K];
+  __shared__ int is_last;
+  if (st->status) return;
+  double s[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) s[j] = 0.0;
+  const long k0 = long(blockIdx.x) * (kBlock * kCgsElems) + threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < kCgsElems; ++e) {
+    const long kk = k0 + e * kBlock;
+    if (kk >= g.n) continue;
+    const long i = seg_pos(g, kk);
+    const double t = V.v[k][i];
+    const double wv = tail ? 0.0 : w[i];
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      const double vj = j < k ? V.v[j][i] : 0.0;
+      s[j] += vj * t;
+      s[KP + j] += vj * wv;
+    }
+    s[KP - 1] += t * t;
+    s[2 * KP - 2] += t * wv;
+    s[2 * KP - 1] += wv * wv;
+  }
+  const double r = block_sums<K>(s, K, sm);
+  const int nb = gridDim.x;
+  const int j = threadIdx.x;
+  if (j < K && dcgs_used<KP>(j, k, tail))
+    granule_store(gran + 2 * (size_t(j) * nb + blockIdx.x), r, seq * 128 + j);
+  if (!last_block(cnt, &is_last)) return;
+  // the last block: slot j summed over the blocks (per-thread strided sums,
+  // then block_sums: a fixed order); unused slots stay 0
+  double s2[K];
+#pragma unroll
+  for (int jj = 0; jj < K; ++jj) {
+    s2[jj] = 0.0;
+    if (dcgs_used<KP>(jj, k, tail))
+      for (int bb = threadIdx.x; bb < nb; bb += kBlock) {
+        const double* p = gran + 2 * (size_t(jj) * nb + bb);
+        mgs_u4 q = granule_load(p);
+        for (long spins = 0; !tag_is(q, seq * 128 + jj); ++spins) {
+          if (spins >= kMgsMaxSpins) {
+            *err = 1.0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          q = granule_load(p);
+        }
+        s2[jj] += granule_value(q);
+      }
+  }
+  __syncthreads();
+  const double r2 = block_sums<K>(s2, K, sm);
+  if (j < K) st->coef[j] = r2;
+}
+
+// The update and bookkeeping of a DCGS2 step from the (all-reduced) slots in
+// st->coef.
+template <int KL>
+__global__ __launch_bounds__(kBlock) void k_dcgs_update(Seg g, const double* __restrict__ w,
+                                                        ChainVecs V, int k, double* tnext,
+                                                        GmresDev* st) {
+  constexpr int KP = dcgs_kp<KL>();
+  constexpr int K = 2 * KP;
+  __shared__ double hs[K];
+  if (st->status) return;
+  const bool tail = tnext == nullptr;
+  if (int(threadIdx.x) < K) hs[threadIdx.x] = st->coef[threadIdx.x];
+  __syncthreads();
+  const DcgsScalars c = dcgs_scalars<KP>(hs, k, tail);
+  const double ib = 1.0 / c.beta;
+  double* t_io = const_cast<double*>(V.v[k]);
+  for (long kk = long(blockIdx.x) * kBlock + threadIdx.x; kk < g.n;
+       kk += long(gridDim.x) * kBlock) {
+    const long i = seg_pos(g, kk);
+    double q = t_io[i];
+    if (k > 0) {
+      for (int j = 0; j < k; ++j) q -= hs[j] * V.v[j][i];
+      q *= ib;
+    }
+    if (!tail) {
+      double u = w[i];
+      for (int j = 0; j < k; ++j) u -= hs[KP + j] * V.v[j][i];
+      u -= c.gk * q;
+      tnext[i] = u * c.inv_nu;
+    }
+    if (k > 0) t_io[i] = q;
+  }
+  if (blockIdx.x != 0) return;
+  dcgs_bookkeeping<KP>(st, hs, k, tail, c);
+}
+
+bool dcgs2_fits(long n, int nb, int n_cus) { return cgs2_chain_fits(n, nb, n_cus); }
+
+size_t dcgs2_granules(long n) {
+  const size_t nbp = size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  return std::max<size_t>(kDcgsRes + 2 * 64 + 64, 2 * 64 * nbp + 64);
+}
+
+void dcgs2_step(Seg g, const double* w, const ChainVecs& V, int k, double* tnext, GmresDev* st,
+                double* gran, unsigned* cnt, int nb, unsigned long long& seq, double* err,
+                Comm* comm, bool one_launch, hipStream_t s) {
+  ChainVecs Vp = V;  // slots past k point at V[0]: the one-launch kernel loads them unconditionally
+  for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
+  const bool tail = tnext == nullptr;
+  if (one_launch) {
+    bool wide = g.n1 == g.n && g.n % 2 == 0 && (reinterpret_cast<uintptr_t>(tnext) & 15) == 0 &&
+                (reinterpret_cast<uintptr_t>(w) & 15) == 0;
+    for (int j = 0; j <= k; ++j) wide = wide && (reinterpret_cast<uintptr_t>(V.v[j]) & 15) == 0;
+    const dim3 grid(nb), block(kChainThreads);
+    ++seq;
+#define DCP_DCGS_CASE(KL)                                                                       \
+    if (k <= KL) {                                                                              \
+      if (wide)                                                                                 \
+        hipLaunchKernelGGL((k_dcgs2_step<KL, true>), grid, block, 0, s, g, w, Vp, k, tnext, st, \
+                           gran, seq, err);                                                     \
+      else                                                                                      \
+        hipLaunchKernelGGL((k_dcgs2_step<KL, false>), grid, block, 0, s, g, w, Vp, k, tnext,    \
+                           st, gran, seq, err);                                                 \
+      DCP_HIP_CHECK(hipGetLastError());                                                         \
+      return;                                                                                   \
+    }
+    DCP_DCGS_CASE(4) DCP_DCGS_CASE(8) DCP_DCGS_CASE(12) DCP_DCGS_CASE(16) DCP_DCGS_CASE(20)
+    DCP_DCGS_CASE(24) DCP_DCGS_CASE(28)
+#undef DCP_DCGS_CASE
+    throw std::runtime_error("dcgs2_step: basis of " + std::to_string(k) + " vectors");
+  }
+  const int nbp = int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  const int nbu = int(std::min<long>((long(g.n) + kBlock - 1) / kBlock, 2048));
+  if (nbp <= 0) return;
+  ++seq;
+#define DCP_DCGS_CASE2(KL)                                                                       \
+  if (k <= KL) {                                                                                 \
+    hipLaunchKernelGGL((k_dcgs_partials<KL>), dim3(nbp), dim3(kBlock), 0, s, g, w, Vp, k, tail,  \
+                       gran, cnt, st, seq, err);                                                 \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    if (comm) comm->allreduce(st->coef, size_t(2 * dcgs_kp<KL>()), false, s);                    \
+    hipLaunchKernelGGL((k_dcgs_update<KL>), dim3(std::max(nbu, 1)), dim3(kBlock), 0, s, g, w, Vp, \
+                       k, tnext, st);                                                            \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    return;                                                                                      \
+  }
+  DCP_DCGS_CASE2(8) DCP_DCGS_CASE2(16) DCP_DCGS_CASE2(28)
+#undef DCP_DCGS_CASE2
+  throw std::runtime_error("dcgs2_step: basis of " + std::to_string(k) + " vectors");
+}
+
 __global__ void k_gmres_cycle_init(GmresDev* st, const double* __restrict__ rho2, double tol,
                                    int max_steps, int first) {
   if (threadIdx.x != 0) return;

@@ -620,6 +620,105 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   return r.status == 1 ? kSuccess : kFailure;
 }
 
+// The inner Schur GMRES with DCGS2 (DCP_OPT_GRAM_SCHMIDT = 2): the same
+// device-resident cycles as gmres_schur_cgs2_ordered, one reduction per
+// Arnoldi step (kernels/krylov.hip k_dcgs2_step): the SpMV applies S to the
+// tentative basis vector t_k = V[k] as it is (no scaling), the step kernel
+// finishes q_k in place and writes t_{k+1} to V[k + 1]; the Givens rotation
+// and the SolverControl check of column k - 1 run in step k, and a tail launch
+// corrects the cycle's last column.
+State gmres_schur_dcgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
+                                std::vector<double*>& tv, int n_tmp) {
+  const int n = c.n_p;
+  const Seg g = c.seg_p();
+  const int restart = n_tmp - 2;
+  if (restart + 1 > kGmMaxDim || restart > 28)
+    throw std::runtime_error("gmres_schur_dcgs2: restart too long");
+  ensure_pool(tv, n_tmp + 1, size_t(n));
+  double* p = tv[n_tmp - 1];
+  double* w = tv[n_tmp];
+  if (!c.gm_report) {
+    c.gm_state.alloc(1);
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_report), 2 * sizeof(GmresReport)));
+    for (auto& ev : c.gm_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  const size_t pn = dcgs2_granules(g.n);
+  if (c.dcgs_gran.n < pn) {
+    c.dcgs_gran.alloc(pn);
+    c.dcgs_gran.zero(c.stream);  // tag 0: never waited for
+  }
+  if (!c.gm_cnt.p) {
+    c.gm_cnt.alloc(1);
+    c.gm_cnt.zero(c.stream);
+  }
+  const std::vector<const double*> ptrs(tv.begin(), tv.begin() + restart);
+  if (ptrs != c.gm_ptrs_host) {
+    c.gm_ptrs.upload(ptrs);
+    c.gm_ptrs_host = ptrs;
+  }
+  GmresDev* dst = c.gm_state.p;
+  Comm* comm = c.comm.get();
+  const int nb1 = std::min(c.n_cus, 256);
+  const bool one_launch = !comm && c.fused_chain && c.hmapped && dcgs2_fits(g.n, nb1, c.n_cus);
+  double* err = comm ? slot(c, kSlotErr) : chain_err(c);
+  auto enqueue_cycle = [&](int cyc) {
+    if (c.S_perm.p)
+      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
+    else
+      schur_vmult(c, x, p);
+    sadd(n, -1., 1., b, p, c.stream);
+    gdot(c, g, p, p, kSlotA);
+    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
+    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
+    for (int k = 0; k <= restart; ++k) {
+      const bool tail = k == restart;
+      if (!tail) {
+        halo_exchange(c, c.halo_p, tv[k]);
+        Timer* e = schur_sample(c);
+        if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+        sell_spmv_step(c.sell(), tv[k], nullptr, nullptr, w, &dst->status, c.stream);
+        if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+      }
+      dcgs2_step(g, tail ? nullptr : w, chain_vecs(tv, k + 1), k, tail ? nullptr : tv[k + 1], dst,
+                 c.dcgs_gran.p, c.gm_cnt.p, nb1, c.chain_seq, err, comm, one_launch, c.stream);
+    }
+    gmres_cycle_end(dst, n, c.gm_ptrs.p, x, &c.gm_report[cyc & 1], c.stream);
+    DCP_HIP_CHECK(hipEventRecord(c.gm_ev[cyc & 1], c.stream));
+  };
+  if (comm) fill(1, 0.0, slot(c, kSlotErr), c.stream);
+  int cyc = 0;
+  enqueue_cycle(cyc);
+  for (;;) {
+    enqueue_cycle(cyc + 1);
+    DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
+    if (c.gm_report[cyc & 1].status != 0) break;
+    ++cyc;
+  }
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (!comm) {
+    check_chain_err(c);
+  } else {
+    allreduce(c, slot(c, kSlotErr), 1, true);
+    if (fetch(c, kSlotErr, 1)[0] != 0.0)
+      throw std::runtime_error("DCGS2 step: a workgroup timed out waiting for a hand-off");
+  }
+  const GmresReport& r = c.gm_report[cyc & 1];
+  ctl.last_step = unsigned(r.accumulated);
+  ctl.last_value = r.rho;
+  return r.status == 1 ? kSuccess : kFailure;
+}
+
+State gmres_schur_dcgs2(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
+                        int n_tmp) {
+  if (!c.S_perm.p) return gmres_schur_dcgs2_ordered(c, x, b, ctl, tv, n_tmp);
+  const int n = c.n_p;
+  gather(n, c.S_perm.p, x, c.sperm_x.p, c.stream);
+  gather(n, c.S_perm.p, b, c.sperm_b.p, c.stream);
+  const State st = gmres_schur_dcgs2_ordered(c, c.sperm_x.p, c.sperm_b.p, ctl, tv, n_tmp);
+  scatter(n, c.S_perm.p, c.sperm_x.p, x, c.stream);
+  return st;
+}
+
 State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
                        int n_tmp) {
   if (!c.S_perm.p) return gmres_schur_cgs2_ordered(c, x, b, ctl, tv, n_tmp);
@@ -737,6 +836,8 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
     State st;
     if (c.schur_explicit && c.gram_schmidt == 1) {
       st = gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+    } else if (c.schur_explicit && c.gram_schmidt == 2) {
+      st = gmres_schur_dcgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit) {
       st = gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else {

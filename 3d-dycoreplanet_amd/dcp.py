@@ -547,9 +547,10 @@ class Context:
 
     def set_gram_schmidt(self, kind: str):
         """DCP_OPT_GRAM_SCHMIDT of the inner Schur GMRES: "modified" (deal.II
-        SolverGMRES, default) or "classical2" (CGS2, device-resident cycles)."""
+        SolverGMRES, default), "classical2" (CGS2, device-resident cycles) or
+        "dcgs2" (delayed CGS2: one reduction per Arnoldi step, device-resident)."""
         self._check(lib().dcp_set_option(self._h, OPT_GRAM_SCHMIDT,
-                                         {"modified": 0, "classical2": 1}[kind]))
+                                         {"modified": 0, "classical2": 1, "dcgs2": 2}[kind]))
 
     def set_element_mfma(self, on: bool):
         """DCP_OPT_ELEMENT_MFMA: True = the velocity-block node-pair sums of the

@@ -78,7 +78,8 @@ def parse():
                     help="skip the converging refine-3 step (GMRES outer iter/s)")
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
                     help="explicit: formed S = B D^-1 B^T (default); composite: B^T, Jacobi, B")
-    ap.add_argument("--gram-schmidt", choices=["modified", "classical2"], default="classical2",
+    ap.add_argument("--gram-schmidt", choices=["modified", "classical2", "dcgs2"],
+                    default="classical2",
                     help="inner Schur GMRES orthogonalisation: modified (deal.II) or "
                          "classical twice with device-resident cycles (DCP_OPT_GRAM_SCHMIDT)")
     ap.add_argument("--variant", choices=["classic", "feec"], default="classic",

@@ -163,9 +163,12 @@ enum { DCP_OPT_ASSEMBLE_VELOCITY_BLOCK = 6 };
  *   orthogonalises like deal.II SolverGMRES (modified Gram-Schmidt, one
  *   reduction per basis vector, re-orthogonalisation after a loss-of-
  *   orthogonality test); 1 = classical Gram-Schmidt applied twice (CGS2: two
- *   block reductions per Arnoldi step), with the Givens updates and the
- *   SolverControl check on the device so a restart cycle runs without host
- *   round trips. Same Krylov space and stopping rule; rounding differs. */
+ *   block reductions per Arnoldi step); 2 = DCGS2, classical Gram-Schmidt with
+ *   the second pass delayed into the next step (one block reduction per
+ *   Arnoldi step; each column's Givens rotation and check one step later).
+ *   1 and 2 run the Givens updates and the SolverControl check on the device
+ *   so a restart cycle runs without host round trips. Same Krylov space and
+ *   stopping rule; rounding differs. */
 enum { DCP_OPT_GRAM_SCHMIDT = 7 };
 /* DCP_OPT_FGMRES_MAX_OUTER (test hook, default 40): the iteration cap of the
  *   first FGMRES(30) (SolverControl(40, ...), boussinesq_model.tpp:1166); a

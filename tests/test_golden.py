@@ -110,7 +110,8 @@ GOLD3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shel
 
 
 @pytest.mark.gpu
-def test_gpu_time_step_r3_matches_oracle_fixture():
+@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2"])
+def test_gpu_time_step_r3_matches_oracle_fixture(gs):
     """One reference time step at refine 3 (3,072 cells, 81,912 NSE dofs) from
     the physical state against the oracle's (tests/golden/make_golden.py r3,
     ~15 min of oracle time): equal FGMRES count, inner count within 10 % (the
@@ -122,6 +123,7 @@ def test_gpu_time_step_r3_matches_oracle_fixture():
     ctx = dcp.Context()
     ctx.set_physics(dcp.classic_physics())
     ctx.upload_mesh(m)
+    ctx.set_gram_schmidt(gs)
     u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
     for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
                  (dcp.T_SOLUTION, T)):
@@ -148,7 +150,7 @@ GOLD4 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shel
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gs", ["modified", "classical2"])
+@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2"])
 def test_gpu_config3_r4_matches_oracle_fixture(gs):
     """BASELINE config 3 (classic prm at refine 4: 24,576 cells, 634,600 NSE
     dofs) from the physical state against the oracle's full time step
