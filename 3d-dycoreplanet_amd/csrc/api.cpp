@@ -871,8 +871,15 @@ namespace dcp {
 // nse_matrix.block(0,0) of the last assemble_nse_system (its dt, nse_ph) into
 // A_val: the full MODE 0 scatter, which rewrites B^T / B / con_diag with the
 // same values and leaves the rhs alone.
+void ensure_A_val(Ctx& c) {
+  // the velocity block's values (9 doubles per 3x3 block, 58 GB at r=6) exist
+  // only once something reads the block
+  if (!c.A_val.p) c.A_val.alloc(c.A_nnzb * 9);
+}
+
 void materialize_velocity_block(Ctx& c) {
   if (c.A_current) return;
+  ensure_A_val(c);
   if (!c.first_touch_A) c.A_val.zero(c.stream);
   if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
   if (!c.first_touch_B) c.B_val.zero(c.stream);
@@ -986,6 +993,89 @@ int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int fie
 
 int dcp_abi_version(void) { return DCP_ABI_VERSION; }
 
+// ---- TimerOutput / SolverControl log ---------------------------------------
+int dcp_timer_record(dcp_ctx* ctx, const char* section, double seconds) {
+  return guarded(ctx, [&] {
+    require(ctx && section, DCP_ERR_INVALID, "NULL argument");
+    ctx->section_add(section, seconds);
+    return DCP_OK;
+  });
+}
+
+int dcp_timer_section(dcp_ctx* ctx, const char* section, long* calls, double* seconds) {
+  return guarded(ctx, [&] {
+    require(ctx && section, DCP_ERR_INVALID, "NULL argument");
+    for (const auto& s : ctx->sections)
+      if (s.name == section) {
+        if (calls) *calls = s.calls;
+        if (seconds) *seconds = s.seconds;
+        return DCP_OK;
+      }
+    fail(DCP_ERR_INVALID, std::string("no timer section \"") + section + "\"");
+    return DCP_ERR_INVALID;
+  });
+}
+
+int dcp_timer_reset(dcp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL ctx");
+    ctx->sections.clear();
+    ctx->t_created = std::chrono::steady_clock::now();
+    return DCP_OK;
+  });
+}
+
+int dcp_timer_summary(dcp_ctx* ctx, char* buf, int len) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL ctx");
+    // TimerOutput::print_summary (wall times)
+    const double total =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - ctx->t_created).count();
+    std::string out, line(71, '-');
+    char row[256];
+    out += "\n+" + std::string(45, '-') + "+" + std::string(12, '-') + "+" + std::string(12, '-') +
+           "+\n";
+    std::snprintf(row, sizeof row, "| Total wallclock time elapsed since start    |%10.3gs |            |\n",
+                  total);
+    out += row;
+    out += "|                                             |            |            |\n";
+    out += "| Section                         | no. calls |  wall time | % of total |\n";
+    const std::string sep = "+" + std::string(33, '-') + "+" + std::string(11, '-') + "+" +
+                            std::string(12, '-') + "+" + std::string(12, '-') + "+\n";
+    out += sep;
+    std::vector<const Ctx::Section*> order;
+    for (const auto& s : ctx->sections) order.push_back(&s);
+    std::sort(order.begin(), order.end(),
+              [](const Ctx::Section* x, const Ctx::Section* y) { return x->name < y->name; });
+    for (const auto* s : order) {
+      std::snprintf(row, sizeof row, "| %-32s| %9ld |%10.3gs |%10.3g%% |\n", s->name.c_str(),
+                    s->calls, s->seconds, total > 0 ? 100.0 * s->seconds / total : 0.0);
+      out += row;
+    }
+    out += sep;
+    (void)line;
+    require(buf != nullptr && len > 0, DCP_ERR_INVALID, "NULL buffer");
+    std::snprintf(buf, size_t(len), "%s", out.c_str());
+    return int(out.size()) < len ? DCP_OK : DCP_ERR_INVALID;
+  });
+}
+
+int dcp_solver_history(dcp_ctx* ctx, int attempt, int* steps, double* values, int cap, int* n,
+                       int* result) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr && n != nullptr, DCP_ERR_INVALID, "NULL argument");
+    require(attempt == 0 || attempt == 1, DCP_ERR_INVALID, "attempt must be 0 or 1");
+    const Ctx::SolverLog& l = ctx->solver_log[attempt];
+    *n = int(l.checks.size());
+    if (result) *result = l.result;
+    for (int i = 0; i < std::min(cap, *n); ++i) {
+      if (steps) steps[i] = int(l.checks[size_t(i)].first);
+      if (values) values[i] = l.checks[size_t(i)].second;
+    }
+    return DCP_OK;
+  });
+}
+
 int dcp_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -1080,6 +1170,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->feec_fixed_inner = value;
       return DCP_OK;
     }
+    if (option == DCP_OPT_LOG_HISTORY) {
+      ctx->log_history = value != 0;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_GRAM_SCHMIDT) {
       require(value >= 0 && value <= 2, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0, 1 or 2");
       ctx->gram_schmidt = value;
@@ -1092,6 +1186,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     if (option == DCP_OPT_ELEMENT_MFMA) {
       require(value == 0 || value == 1, DCP_ERR_INVALID, "DCP_OPT_ELEMENT_MFMA must be 0 or 1");
       ctx->element_mfma = value != 0;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_INNER_MAX_STEPS) {
+      require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_INNER_MAX_STEPS must be >= 1");
+      ctx->inner_max_steps = value;
       return DCP_OK;
     }
     if (option == DCP_OPT_FGMRES_MAX_OUTER) {
@@ -1222,7 +1321,8 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.S_col.upload(h.Sc);
     build_sell(c, h.Sp, h.Sc, !dist);
     c.S_max_row = h.S_max_row;
-    c.A_val.alloc(Ac.size() * 9);
+    c.A_val.release();  // allocated on first use (ensure_A_val)
+    c.A_nnzb = Ac.size();
     c.Bt_val.alloc(Btc.size() * 3);
     c.B_val.alloc(Bc.size() * 3);
     {
@@ -1628,6 +1728,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     need_ready(*ctx);
     require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
+    SectionScope sec(c, "   Assemble NSE system");
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
     const bool matrix = (flags & DCP_ASSEMBLE_MATRIX) != 0;
     // the velocity block is materialised only when something reads it
@@ -1635,6 +1736,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     NseOut out{};
     if (matrix) {
       // first-touch scatter positions store instead of adding: no zero fill
+      if (full) ensure_A_val(c);
       if (full && !c.first_touch_A) c.A_val.zero(c.stream);
       // operator form: B copied from B^T after the cell loop (c.B_transpose)
       const bool scatter_B = full || !c.B_transpose;
@@ -1683,12 +1785,16 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
     need_ready(*ctx);
     require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
+    SectionScope sec(c, "   Build NSE preconditioner");
     PhaseTimer t(c, &c.timings.build_precond_ms);
-    c.A_diag.zero(c.stream);
-    c.Mp_diag.zero(c.stream);
-    for (int k = 0; k < c.n_colors(); ++k)
-      launch_nse_precond_diag(c.cd(), c.color_begin(k), c.color_size(k), c.ph, c.A_diag.p,
-                              c.Mp_diag.p, c.stream);
+    {
+      SectionScope sub(c, "   Assembly NSE preconditioner");
+      c.A_diag.zero(c.stream);
+      c.Mp_diag.zero(c.stream);
+      for (int k = 0; k < c.n_colors(); ++k)
+        launch_nse_precond_diag(c.cd(), c.color_begin(k), c.color_size(k), c.ph, c.A_diag.p,
+                                c.Mp_diag.p, c.stream);
+    }
     reciprocal(c.n_u, c.A_diag.p, c.A_inv.p, c.stream);
     reciprocal(c.n_p, c.Mp_diag.p, c.Mp_inv.p, c.stream);
     if (c.schur_explicit) {
@@ -1711,6 +1817,7 @@ int dcp_assemble_temperature_matrix(dcp_ctx* ctx) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
     Ctx& c = *ctx;
+    SectionScope sec(c, "   Assemble temperature matrices");
     PhaseTimer t(c, &c.timings.assemble_T_matrix_ms);
     c.Tmass.zero(c.stream);
     c.Tstiff.zero(c.stream);
@@ -1728,6 +1835,7 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(c.T_matrix_ok, DCP_ERR_STATE, "assemble the temperature matrices first");
+    SectionScope sec(c, "   Assemble temperature RHS");
     PhaseTimer t(c, &c.timings.assemble_T_rhs_ms);
     // T_matrix = M + dt/interval K ; Jacobi rebuilt (:975-986)
     lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
@@ -1760,6 +1868,7 @@ int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves) {
     Ctx& c = *ctx;
     require(c.nse_assembled, DCP_ERR_STATE, "assemble_nse_system must run first");
     require(!c.comm, DCP_ERR_UNSUPPORTED, "the Schur-complement solver runs on one GPU");
+    SectionScope sec(c, "   Solve NSE system");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     return solve_nse_schur(c, schur_iterations, a_solves);
   });
@@ -1772,6 +1881,7 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     Ctx& c = *ctx;
     require(c.nse_assembled && c.precond_built, DCP_ERR_STATE,
             "assemble_nse_system and build_nse_preconditioner must run first");
+    SectionScope sec(c, "   Solve Stokes system");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     c.time_schur = true;
     c.schur_ev_used = 0;
@@ -1814,6 +1924,7 @@ int dcp_solve_temperature(dcp_ctx* ctx, int* iters, double* T_range) {
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(c.T_rhs_ok, DCP_ERR_STATE, "assemble_temperature_rhs must run first");
+    SectionScope sec(c, "   Solve temperature system");
     PhaseTimer t(c, &c.timings.solve_T_ms);
     const int rc = solve_temperature(c, iters, T_range);
     t.stop();
@@ -2573,6 +2684,7 @@ int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len) 
     out->length = L;
     out->use_block_preconditioner_feec = p.use_block_preconditioner_feec ? 1 : 0;
     out->correct_pressure_to_zero_mean = p.correct_pressure_to_zero_mean ? 1 : 0;
+    out->solver_diagnostics_level = int(p.solver_diagnostics_print_level);
     return DCP_OK;
   } catch (const std::exception& e) {
     if (err && err_len > 0) {

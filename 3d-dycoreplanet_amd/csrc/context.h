@@ -1,5 +1,6 @@
 // Device-resident state of one dcp_ctx (one GPU / rank).
 #pragma once
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -53,6 +54,32 @@ struct Timer {
 };
 
 struct Ctx {
+  // SolverControl log of one solve (log_history / log_result): every
+  // check(step, value) and the result (0 iterating, 1 convergence, 2 failure)
+  struct SolverLog {
+    std::vector<std::pair<unsigned, double>> checks;
+    int result = 0;
+  };
+  SolverLog solver_log[2];           // the FGMRES attempts of the last dcp_solve_nse
+  bool log_history = false;          // DCP_OPT_LOG_HISTORY
+  // TimerOutput of the reference (computing_timer): wall time and calls per
+  // section, in first-use order, under the reference's section names
+  struct Section {
+    std::string name;
+    long calls = 0;
+    double seconds = 0;
+  };
+  std::vector<Section> sections;
+  std::chrono::steady_clock::time_point t_created = std::chrono::steady_clock::now();
+  void section_add(const char* name, double s) {
+    for (auto& x : sections)
+      if (x.name == name) {
+        ++x.calls;
+        x.seconds += s;
+        return;
+      }
+    sections.push_back(Section{name, 1, s});
+  }
   dcp_config cfg{};
   std::string err;
   hipStream_t stream = nullptr;
@@ -89,6 +116,7 @@ struct Ctx {
   // block-CSR patterns + values
   DBuf<int32_t> A_ptr, A_col, Bt_ptr, Bt_col, B_ptr, B_col, T_ptr, T_col;
   DBuf<double> A_val, Bt_val, B_val, Tmass, Tstiff, Tmat;
+  size_t A_nnzb = 0;                 // blocks of the A pattern (A_val allocated on first use)
   DBuf<int32_t> posA, posBt, posB, posT;
   // scatter positions carry first-touch marks (no zero fill before assembly)
   bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
@@ -230,6 +258,7 @@ struct Ctx {
   DBuf<const double*> gm_ptrs;
   std::vector<const double*> gm_ptrs_host;
   int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
+  int inner_max_steps = 5000;        // SolverControl(5000) of the inner Schur GMRES (probe hook)
   long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
   // test hook, read at context creation: DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger
@@ -323,6 +352,25 @@ struct Ctx {
   ~Ctx();
 };
 
+// TimerOutput::Scope: wall time of the enclosed work (the stream is
+// synchronised at the end of the scope) under a reference section name
+struct SectionScope {
+  Ctx& c;
+  const char* name;
+  std::chrono::steady_clock::time_point t0;
+  bool done = false;
+  SectionScope(Ctx& ctx, const char* n) : c(ctx), name(n), t0(std::chrono::steady_clock::now()) {}
+  void stop() {
+    if (done) return;
+    done = true;
+    (void)hipStreamSynchronize(c.stream);
+    c.section_add(name, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  }
+  ~SectionScope() { stop(); }
+};
+
+// api.cpp: A_val allocated for the A pattern (if not yet)
+void ensure_A_val(Ctx& c);
 // api.cpp: A_val <- nse_matrix.block(0,0) of the last assembly (if not current)
 void materialize_velocity_block(Ctx& c);
 // B = (B^T)^T after an operator-form assembly that scattered B^T only

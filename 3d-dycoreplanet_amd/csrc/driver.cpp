@@ -6,6 +6,7 @@
 // (setup_dofs, VectorTools::project of T0, :1793-1834) stay with the caller;
 // output_results is the callback.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <string>
 
@@ -27,6 +28,17 @@ double recomputed_time_step(const dcp_run_params* rp, double cfl) {
 extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
                        dcp_step_callback cb, void* user, dcp_run_report* rep) {
   if (!ctx || !rp) return DCP_ERR_INVALID;
+  // TimerOutput sections of run() and output_results (:1789, :1572)
+  using clock = std::chrono::steady_clock;
+  const auto t_run = clock::now();
+  struct RunSection {
+    dcp_ctx* c;
+    clock::time_point t0;
+    ~RunSection() {
+      dcp_timer_record(c, "BoussinesqModel - global run function",
+                       std::chrono::duration<double>(clock::now() - t0).count());
+    }
+  } run_section{ctx, t_run};
   const bool feec = rp->use_FEEC_solver != 0;
   // solve_NSE_Schur_complement instead of the block preconditioner (:1896-1902)
   const bool schur = !feec && rp->use_schur_complement_solver != 0;
@@ -94,7 +106,14 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
     r.T_max = range[1];
     r.total_T_cg += r.T_cg;
     r.steps = n + 1;
-    if (cb && cb(user, &r) != 0) {  // output_results (:1907); non-zero stops the run
+    int stop = 0;
+    if (cb) {  // output_results (:1907); non-zero stops the run
+      const auto t0 = clock::now();
+      stop = cb(user, &r);
+      dcp_timer_record(ctx, "Postprocessing and output",
+                       std::chrono::duration<double>(clock::now() - t0).count());
+    }
+    if (stop != 0) {
       if ((rc = dcp_advance_state(ctx)) < 0) return rc;
       break;
     }

@@ -50,6 +50,30 @@ int write_output(Output& o) {
   return rc;
 }
 
+struct Runner {
+  dcp_ctx* ctx = nullptr;
+  Output* out = nullptr;
+  int diagnostics = 1;  // deallog.depth_console(solver diagnostics level), main.cxx:89
+  int interval = 1;
+};
+
+// deallog at depth 2: SolverFGMRES's prefix and SolverControl's log_history /
+// log_result lines of the step's NSE solve (boussinesq_model.tpp:1166-1169)
+void print_solver_log(dcp_ctx* ctx) {
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    int n = 0, result = 0;
+    if (dcp_solver_history(ctx, attempt, nullptr, nullptr, 0, &n, &result) != DCP_OK || n == 0)
+      continue;
+    std::vector<int> steps(static_cast<size_t>(n));
+    std::vector<double> vals(static_cast<size_t>(n));
+    dcp_solver_history(ctx, attempt, steps.data(), vals.data(), n, &n, &result);
+    for (int i = 0; i < n; ++i) std::printf("DEAL:FGMRES::Check %d\t%g\n", steps[size_t(i)], vals[size_t(i)]);
+    if (result)
+      std::printf("DEAL:FGMRES::%s step %d value %g\n", result == 1 ? "Convergence" : "Failure",
+                  steps.back(), vals.back());
+  }
+}
+
 int print_step(void* user, const dcp_run_report* r) {
   std::printf("----------------------------------------\n");
   std::printf("Time step %d:  t=%g -> t=%g  (dt=%g)\n", r->timestep_number, r->time_index,
@@ -61,8 +85,15 @@ int print_step(void* user, const dcp_run_report* r) {
   else
     std::printf("   Solved (GMRES): %d\n", r->fgmres_outer);
   std::printf("   Temperature: %d CG iterations, range %g %g\n", r->T_cg, r->T_min, r->T_max);
-  Output* o = static_cast<Output*>(user);
-  if (o && write_output(*o) != DCP_OK) return 1;  // stop the run
+  Runner* run = static_cast<Runner*>(user);
+  if (run->diagnostics >= 2) print_solver_log(run->ctx);
+  if (run->out && write_output(*run->out) != DCP_OK) return 1;  // stop the run
+  // computing_timer.print_summary() after every NSE interval (:1912-1916)
+  if (r->timestep_number > 0 && r->timestep_number % run->interval == 0) {
+    std::vector<char> buf(1 << 16);
+    if (dcp_timer_summary(run->ctx, buf.data(), int(buf.size())) == DCP_OK)
+      std::printf("%s", buf.data());
+  }
   return 0;
 }
 
@@ -157,8 +188,14 @@ int main(int argc, char** argv) {
     outp = &out;
     if (write_output(out) != DCP_OK) return fail("output", ctx);  // before the loop (:1840)
   }
+  Runner runner;
+  runner.ctx = ctx;
+  runner.out = outp;
+  runner.diagnostics = rp.solver_diagnostics_level;
+  runner.interval = rp.physics.nse_solver_interval > 0 ? rp.physics.nse_solver_interval : 1;
+  if (runner.diagnostics >= 2) dcp_set_option(ctx, DCP_OPT_LOG_HISTORY, 1);
   dcp_run_report rep{};
-  rc = dcp_run(ctx, &rp, max_steps, print_step, outp, &rep);
+  rc = dcp_run(ctx, &rp, max_steps, print_step, &runner, &rep);
   if (rc < 0) return fail("run", ctx);
   dcp_timings t{};
   dcp_get_timings(ctx, &t);

@@ -37,12 +37,18 @@ struct Control {
   double tol;
   unsigned last_step = 0;
   double last_value = 0;
+  // SolverControl(..., log_history = true, log_result = true): every check
+  // and the final verdict (Ctx::SolverLog), or null
+  Ctx::SolverLog* log = nullptr;
   State check(unsigned step, double value) {
     last_step = step;
     last_value = value;
-    if (value <= tol) return kSuccess;
-    if (step >= max_steps || std::isnan(value)) return kFailure;
-    return kIterate;
+    if (log) log->checks.emplace_back(step, value);
+    State s = kIterate;
+    if (value <= tol) s = kSuccess;
+    else if (step >= max_steps || std::isnan(value)) s = kFailure;
+    if (log && s != kIterate) log->result = s == kSuccess ? 1 : 2;
+    return s;
   }
 };
 
@@ -53,7 +59,7 @@ constexpr int kSlotA = 258;      // misc
 constexpr int kSlotB = 259;
 constexpr int kSlotC = 260;
 constexpr int kSlotD = 261;
-constexpr int kSlotErr = 262;    // granule timeout flag of the CGS2 steps on several GPUs
+constexpr int kSlotErr = 1300;   // granule timeout flag of the CGS2 / DCGS2 steps on several GPUs
 constexpr int kSlotMinMax = 264; // 2 + 2*kReduceBlocks
 constexpr int kSlotCg = 1296;    // 4: pcg's gh, d.h, alpha / beta, |g|^2
 constexpr int kHostPartials = 2048;
@@ -62,7 +68,7 @@ constexpr int kHostPartials = 2048;
 constexpr int kStepBlock = 4096, kStepBlockLen = 1280;
 constexpr int kNumSlots = 8192;             // device slots, mirrored in c.hpinned
 static_assert(kSlotMinMax + 2 + 2 * kReduceBlocks <= kSlotCg, "slot layout");
-static_assert(kSlotCg + 4 <= kHostPartials, "slot layout");
+static_assert(kSlotCg + 4 <= kSlotErr && kSlotErr < kHostPartials, "slot layout");
 static_assert(kHostPartials + kChainMaxBlocks <= kStepBlock, "slot layout");
 static_assert(kSpPart + kChainMaxBlocks <= kStepBlockLen, "slot layout");
 
@@ -831,7 +837,7 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
   // inner GMRES on S = B D_A^-1 B^T, tol 1e-6 |src_p|, max 5000, identity
   {
     const double nrm = std::sqrt(dot_host(c, c.seg_p(), src + nu, src + nu, kSlotB));
-    Control ctl{5000, 1e-6 * nrm};
+    Control ctl{unsigned(c.inner_max_steps), 1e-6 * nrm};
     ensure_pool(c.sg_v, 32, size_t(np));
     State st;
     if (c.schur_explicit && c.gram_schmidt == 1) {
@@ -870,10 +876,11 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
 
 // deal.II SolverFGMRES (see oracle/oracle.cpp for the restated control flow).
 State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, double tol,
-             bool do_solve_A, int& acc_out, int& inner) {
+             bool do_solve_A, int& acc_out, int& inner, Ctx::SolverLog* log) {
   const int n = c.n_u + c.n_p;
   const Seg g = c.seg_nse();
   Control ctl{max_steps, tol};
+  ctl.log = log;
   ensure_pool(c.fg_v, basis, size_t(n));
   ensure_pool(c.fg_z, basis, size_t(n));
   std::vector<char> z_init(basis, 0);
@@ -1050,17 +1057,21 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
   scale(np, DScal{nullptr, dt}, x.p + nu, c.stream);      // :1177 (Q1)
   int inner = 0, acc1 = 0, acc2 = 0, status = DCP_OK;
   c.a_solve_its = 0;
+  for (auto& l : c.solver_log) l = Ctx::SolverLog{};
+  Ctx::SolverLog* log0 = c.log_history ? &c.solver_log[0] : nullptr;
+  Ctx::SolverLog* log1 = c.log_history ? &c.solver_log[1] : nullptr;
   try {
-    // SolverControl(40, ...) (:1166-1169); DCP_OPT_FGMRES_MAX_OUTER lowers the
-    // cap in tests so the fallback below runs on small meshes
-    const State st =
-        fgmres(c, x.p, c.nse_rhs.p, 30, unsigned(c.fgmres_max_outer), tol, false, acc1, inner);
+    // SolverControl(40, ..., log_history, log_result) (:1166-1169);
+    // DCP_OPT_FGMRES_MAX_OUTER lowers the cap in tests so the fallback below
+    // runs on small meshes
+    const State st = fgmres(c, x.p, c.nse_rhs.p, 30, unsigned(c.fgmres_max_outer), tol, false,
+                            acc1, inner, log0);
     if (st != kSuccess) throw NoConvergence();
   } catch (const NoConvergence&) {
     // :1203-1232 fallback (Q10): do_solve_A, FGMRES(50), max = nse_matrix.m()
     try {
-      const State st =
-          fgmres(c, x.p, c.nse_rhs.p, 50, unsigned(c.n_u_g + c.n_p_g), tol, true, acc2, inner);
+      const State st = fgmres(c, x.p, c.nse_rhs.p, 50, unsigned(c.n_u_g + c.n_p_g), tol, true,
+                              acc2, inner, log1);
       if (st != kSuccess) status = DCP_NOT_CONVERGED;
     } catch (const NoConvergence&) {
       status = DCP_NOT_CONVERGED;
@@ -1269,6 +1280,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
     (void)pcg(c, np, gp, Sa, Id, d, s, ctl, cg_p);
   };
   // SolverGMRES (30 tmp vectors), SolverControl(nse_matrix.m(), 1e-6 |schur_rhs|)
+  SectionScope sec_p(c, "      Solve NSE system - Schur complement solver (for pressure)");
   const double rn = std::sqrt(dot_host(c, gp, srhs, srhs, kSlotA));
   Control ctl{unsigned(n), 1e-6 * rn};
   const State st = gmres(c, np, gp, S, &Pre, x.p + nu, srhs, ctl, c.sg_v, 30);
@@ -1280,11 +1292,14 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
     }
   };
   distribute();                                                       // :1353
+  sec_p.stop();
+  SectionScope sec_u(c, "      Solve NSE system - outer CG solver (for u)");
   // u = A^-1 (f - B^T p) (:1366-1372)
   spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, x.p + nu, tmp, false, c.stream);
   sadd(nu, -1.0, 1.0, c.nse_rhs.p, tmp, c.stream);
   inverse(tmp, x.p);
   distribute();                                                       // :1378
+  sec_u.stop();
   scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);           // :1384
   copy(n, x.p, c.nse_sol.p, c.stream);
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));

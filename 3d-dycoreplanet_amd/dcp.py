@@ -34,6 +34,8 @@ OPT_ASSEMBLE_VELOCITY_BLOCK = 6
 OPT_ELEMENT_MFMA = 9
 OPT_GRAM_SCHMIDT = 7
 OPT_FEEC_FIXED_INNER = 8
+OPT_LOG_HISTORY = 10
+OPT_INNER_MAX_STEPS = 11
 ABI_VERSION = 3            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
@@ -54,7 +56,8 @@ EXPORTED = [
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
     "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
-    "dcp_write_vtu", "dcp_write_pvtu_record",
+    "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
+    "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
 ]
 
 
@@ -130,6 +133,7 @@ class RunParams(C.Structure):
         ("adapt_time_step", C.c_int), ("final_time", C.c_double), ("R0", C.c_double),
         ("R1", C.c_double), ("length", C.c_double),
         ("use_block_preconditioner_feec", C.c_int), ("correct_pressure_to_zero_mean", C.c_int),
+        ("solver_diagnostics_level", C.c_int),
     ]
 
 
@@ -222,6 +226,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.POINTER(Constraints), I, I, P, P, P, P, P, P]
     lib.dcp_write_vtu.argtypes = [C.POINTER(MeshView), P, P, I, C.c_char_p]
     lib.dcp_write_pvtu_record.argtypes = [C.c_char_p, I, C.POINTER(C.c_char_p)]
+    lib.dcp_solver_history.argtypes = [P, I, P, P, I, C.POINTER(I), C.POINTER(I)]
+    lib.dcp_timer_summary.argtypes = [P, C.c_char_p, I]
+    lib.dcp_timer_section.argtypes = [P, C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_double)]
+    lib.dcp_timer_record.argtypes = [P, C.c_char_p, C.c_double]
+    lib.dcp_timer_reset.argtypes = [P]
     return lib
 
 
@@ -544,6 +553,54 @@ class Context:
         in colour-class launches; False / 0: block-CSR SpMV of the assembled
         matrix."""
         self._check(lib().dcp_set_option(self._h, OPT_MATRIX_FREE, int(mode)))
+
+    def set_inner_max_steps(self, n: int):
+        """DCP_OPT_INNER_MAX_STEPS (probe hook): cap of the inner Schur GMRES
+        (the reference's SolverControl(5000, ...))."""
+        self._check(lib().dcp_set_option(self._h, OPT_INNER_MAX_STEPS, int(n)))
+
+    def set_log_history(self, on: bool):
+        """DCP_OPT_LOG_HISTORY: record the SolverControl checks of the NSE
+        solve's FGMRES attempts (log_history = true, :1166-1169)."""
+        self._check(lib().dcp_set_option(self._h, OPT_LOG_HISTORY, int(bool(on))))
+
+    def solver_history(self, attempt=0):
+        """(steps, residuals, result) of the last solve_nse's FGMRES attempt
+        (0: FGMRES(30), 1: the do_solve_A FGMRES(50) fallback); result 0 =
+        not run, 1 = convergence, 2 = failure."""
+        n, res = C.c_int(0), C.c_int(0)
+        self._check(lib().dcp_solver_history(self._h, int(attempt), None, None, 0, C.byref(n),
+                                             C.byref(res)))
+        steps, vals = np.zeros(n.value, np.int32), np.zeros(n.value)
+        self._check(lib().dcp_solver_history(self._h, int(attempt), _ptr(steps), _ptr(vals),
+                                             n.value, C.byref(n), C.byref(res)))
+        return steps, vals, res.value
+
+    def deallog(self, depth=2):
+        """The solver lines deallog prints at depth_console(depth) >= 2:
+        SolverFGMRES's prefix with SolverControl's log_history / log_result."""
+        lines = []
+        if depth < 2:
+            return lines
+        for attempt in (0, 1):
+            steps, vals, res = self.solver_history(attempt)
+            lines += [f"DEAL:FGMRES::Check {s}\t{v:g}" for s, v in zip(steps, vals)]
+            if res:
+                lines.append(f"DEAL:FGMRES::{'Convergence' if res == 1 else 'Failure'} step "
+                             f"{steps[-1]} value {vals[-1]:g}")
+        return lines
+
+    def timer_summary(self):
+        """TimerOutput::print_summary of the context's sections (reference names)."""
+        buf = C.create_string_buffer(1 << 16)
+        self._check(lib().dcp_timer_summary(self._h, buf, len(buf)))
+        return buf.value.decode()
+
+    def timer_section(self, name):
+        """(calls, wall seconds) of a TimerOutput section, e.g. '   Assemble NSE system'."""
+        calls, sec = C.c_long(0), C.c_double(0)
+        self._check(lib().dcp_timer_section(self._h, name.encode(), C.byref(calls), C.byref(sec)))
+        return calls.value, sec.value
 
     def set_gram_schmidt(self, kind: str):
         """DCP_OPT_GRAM_SCHMIDT of the inner Schur GMRES: "modified" (deal.II

@@ -108,6 +108,15 @@ def schur_bytes(m, nnzb_bt, nnzb_b):
     return bt + jac + b
 
 
+def device_mem_gb():
+    """Device memory in use (hipMemGetInfo: total - free), GB."""
+    import ctypes
+    import dcp
+    free, total = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    dcp.hip().hipMemGetInfo(ctypes.byref(free), ctypes.byref(total))
+    return (total.value - free.value) / 1e9
+
+
 def cpu_info():
     """Host CPU model and the cores this process may use (GPU box: read at run time)."""
     model = "unknown"
@@ -438,39 +447,47 @@ def main():
         pcie = {"value": n_nse / min(ts), "unit": "assembled DoFs/s",
                 "ms": min(ts) * 1e3,
                 "what": "host u_old/T_old upload + assemble_nse_system + rhs download, host clock"}
-    # one step with the other Gram-Schmidt variant of the inner Schur GMRES
-    # (deal.II's modified Gram-Schmidt is the reference's; CGS2 the default here)
-    other_gs = "modified" if args.gram_schmidt == "classical2" else "classical2"
-    ctx.set_gram_schmidt(other_gs)
-    r_o = step()
+    # one step with each other Gram-Schmidt variant of the inner Schur GMRES
+    # (deal.II's modified Gram-Schmidt is the reference's); at refine >= 6
+    # only the device-resident ones (the modified one reads every step back)
+    other = []
+    for other_gs in ("modified", "classical2", "dcgs2"):
+        if other_gs == args.gram_schmidt or (other_gs == "modified" and args.refine >= 6):
+            continue
+        ctx.set_gram_schmidt(other_gs)
+        r_o = step()
+        other.append({"gram_schmidt": other_gs, "fgmres_outer_iterations": r_o[1],
+                      "schur_gmres_inner_iterations": r_o[2],
+                      "solve_nse_ms": r_o[4]["solve_nse_ms"],
+                      "gmres_inner_iter_per_s": r_o[2] / (r_o[4]["solve_nse_ms"] * 1e-3),
+                      "converged": r_o[0] == 0})
     ctx.set_gram_schmidt(args.gram_schmidt)
-    other = {"gram_schmidt": other_gs, "fgmres_outer_iterations": r_o[1],
-             "schur_gmres_inner_iterations": r_o[2], "solve_nse_ms": r_o[4]["solve_nse_ms"],
-             "gmres_inner_iter_per_s": r_o[2] / (r_o[4]["solve_nse_ms"] * 1e-3),
-             "converged": r_o[0] == 0}
-    # the same assembly with the velocity block scattered as well (the
-    # reference's distribute_local_to_global output; DCP_OPT_ASSEMBLE_VELOCITY_BLOCK)
-    ctx.set_assemble_velocity_block(True)
-    full_ms = []
-    for _ in range(3):
-        ctx.assemble_nse_system()
-        full_ms.append(ctx.timings()["assemble_nse_ms"])
-    # and with its node-pair sums on the matrix cores (DCP_OPT_ELEMENT_MFMA)
-    ctx.set_element_mfma(True)
-    mfma_ms = []
-    for _ in range(3):
-        ctx.assemble_nse_system()
-        mfma_ms.append(ctx.timings()["assemble_nse_ms"])
-    ctx.set_element_mfma(False)
-    ctx.set_assemble_velocity_block(False)
-    full_ms = float(np.min(full_ms))
-    mfma_ms = float(np.min(mfma_ms))
+    full_ms = mfma_ms = float("nan")
+    if args.refine <= 5:
+        # the same assembly with the velocity block scattered as well (the
+        # reference's distribute_local_to_global output;
+        # DCP_OPT_ASSEMBLE_VELOCITY_BLOCK; 58 GB of block values at refine 6)
+        ctx.set_assemble_velocity_block(True)
+        full_ms = []
+        for _ in range(3):
+            ctx.assemble_nse_system()
+            full_ms.append(ctx.timings()["assemble_nse_ms"])
+        # and with its node-pair sums on the matrix cores (DCP_OPT_ELEMENT_MFMA)
+        ctx.set_element_mfma(True)
+        mfma_ms = []
+        for _ in range(3):
+            ctx.assemble_nse_system()
+            mfma_ms.append(ctx.timings()["assemble_nse_ms"])
+        ctx.set_element_mfma(False)
+        ctx.set_assemble_velocity_block(False)
+        full_ms = float(np.min(full_ms))
+        mfma_ms = float(np.min(mfma_ms))
     if dist is not None:
         import torch
         tt = torch.tensor([full_ms], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         full_ms = float(tt.item())
-    full_matrix = {"value": n_nse / (full_ms * 1e-3), "unit": "assembled DoFs/s", "ms": full_ms,
+    full_matrix = None if args.refine > 5 else {"value": n_nse / (full_ms * 1e-3), "unit": "assembled DoFs/s", "ms": full_ms,
                    "what": "assemble_nse_system with the velocity block A scattered into "
                            "block-CSR as well (DCP_OPT_ASSEMBLE_VELOCITY_BLOCK=1); `value` "
                            "assembles nse_matrix in operator form (B^T, B, rhs, constrained "
@@ -502,7 +519,9 @@ def main():
     # whole-job rate: the global system assembled by all ranks together
     value = n_nse / (asm_ms * 1e-3)
     out = {
-        "metric": "assembled DoFs/sec + GMRES iter/sec, 3D shell Q2/Q1 refine=5, 1/2/4/8 GPU",
+        "metric": "assembled DoFs/sec + GMRES iter/sec, 3D shell Q2/Q1 refine=5, 1/2/4/8 GPU"
+        if args.refine == 5 else
+        f"assembled DoFs/sec + GMRES iter/sec, 3D shell Q2/Q1 refine={args.refine}, {world} GPU",
         "value": value,
         "unit": "assembled DoFs/s",
         "n_gpus": world,
@@ -538,6 +557,7 @@ def main():
         "schur_mode": args.schur,
         "gram_schmidt": args.gram_schmidt,
         "other_gram_schmidt": other,
+        "device_mem_gb": device_mem_gb(),
         "pcie_inclusive": pcie,
         "assembly_with_velocity_block": full_matrix,
         "roofline": {"kernel": kernel, "bound": "hbm",

@@ -175,6 +175,11 @@ enum { DCP_OPT_GRAM_SCHMIDT = 7 };
  *   lower cap sends small meshes through the do_solve_A / FGMRES(50) fallback
  *   (:1203-1232) that the reference takes when the cap is hit. */
 enum { DCP_OPT_FGMRES_MAX_OUTER = 5 };
+/* DCP_OPT_INNER_MAX_STEPS (probe hook, default 5000): the iteration cap of the
+ *   inner Schur GMRES, SolverControl(5000, 1e-6 |src_p|) in
+ *   BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:46-51),
+ *   so a large mesh can be probed for a bounded number of steps. */
+enum { DCP_OPT_INNER_MAX_STEPS = 11 };
 /* DCP_OPT_ELEMENT_MFMA: 0 (default) = the velocity-velocity node-pair sums of
  *   the NSE element matrix (local_assemble_nse_system, boussinesq_model.tpp:
  *   597-640: mass + eps:eps over the 27 QGauss points) run as FP64 VALU
@@ -183,7 +188,34 @@ enum { DCP_OPT_FGMRES_MAX_OUTER = 5 };
  *   (DCP_OPT_ASSEMBLE_VELOCITY_BLOCK, dcp_nse_matrix_export) and
  *   dcp_cell_nse_system. DESIGN.md section 4e has the measurement. */
 enum { DCP_OPT_ELEMENT_MFMA = 9 };
+/* DCP_OPT_LOG_HISTORY: 1 = record every SolverControl::check of the two
+ *   FGMRES solves of dcp_solve_nse, as SolverControl(..., log_history = true,
+ *   log_result = true) logs them to deallog (boussinesq_model.tpp:1166-1169,
+ *   1215-1218); read back with dcp_solver_history. Default 0. */
+enum { DCP_OPT_LOG_HISTORY = 10 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
+
+/* The SolverControl log of the last dcp_solve_nse (DCP_OPT_LOG_HISTORY):
+ * attempt 0 = the FGMRES(30) of :1166-1199, 1 = the do_solve_A FGMRES(50)
+ * fallback of :1203-1232. steps/values (capacity cap, may be NULL) receive
+ * (step, residual) of every check in order, deallog's "Check <step>\t<value>"
+ * lines; *n their count; *result 0 = no verdict (not run), 1 = "Convergence
+ * step ...", 2 = "Failure step ..." (the last check). */
+int dcp_solver_history(dcp_ctx* ctx, int attempt, int* steps, double* values, int cap, int* n,
+                       int* result);
+
+/* TimerOutput of the reference (computing_timer with its section names, e.g.
+ * "   Assemble NSE system", "   Solve Stokes system", "   Solve NSE system"
+ * with its two nested sections; boussinesq_model.tpp:483-1572): wall time
+ * (stream synchronised at the section end) and call count per section,
+ * accumulated since context creation or dcp_timer_reset. dcp_timer_summary
+ * writes TimerOutput::print_summary's table into buf (DCP_ERR_INVALID if len
+ * is too small); dcp_timer_record adds host work of the caller under a
+ * section name (e.g. "Postprocessing and output"). */
+int dcp_timer_summary(dcp_ctx* ctx, char* buf, int len);
+int dcp_timer_section(dcp_ctx* ctx, const char* section, long* calls, double* seconds);
+int dcp_timer_record(dcp_ctx* ctx, const char* section, double seconds);
+int dcp_timer_reset(dcp_ctx* ctx);
 
 /* Mesh / DoF upload (the data setup_dofs() produces, :184-412). Builds the
  * device sparsity patterns, cell colouring and scatter maps once. */
@@ -406,6 +438,7 @@ typedef struct {
   int use_schur_complement_solver, use_FEEC_solver, adapt_time_step;
   double final_time, R0, R1, length;
   int use_block_preconditioner_feec, correct_pressure_to_zero_mean;
+  int solver_diagnostics_level;     /* deallog.depth_console level (main.cxx:89) */
 } dcp_run_params;
 int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
 

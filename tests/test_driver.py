@@ -108,3 +108,44 @@ def test_executable_writes_vtu_output(tmp_path):
     n_cells = dcp.HostMesh(refine=1).n_cells
     assert 'NumberOfCells="%d"' % (8 * n_cells) in text  # 8 hexahedra per cell
     assert 'Source="aqua-00001.0000.vtu"' in (tmp_path / "aqua-00001.pvtu").read_text()
+
+
+@pytest.mark.gpu
+def test_solver_history_and_timer_sections():
+    """§5 auxiliaries: SolverControl(..., log_history = true, log_result = true)
+    of the FGMRES solve (boussinesq_model.tpp:1166-1169) and the TimerOutput
+    sections under the reference's names (:483-1572)."""
+    rp = dcp.load_prm(PRM)
+    m = dcp.HostMesh(refine=2)
+    ctx = fresh(rp, m)
+    ctx.set_log_history(True)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    rc, outer, inner = ctx.solve_nse()
+    ctx.solve_temperature()
+    assert rc == 0
+    steps, vals, res = ctx.solver_history(0)
+    # one check per FGMRES restart head (step 0) and per iteration from j = 1
+    assert res == 1 and steps[0] == 0 and steps[-1] == outer and len(steps) == outer + 1
+    tol = 1e-8 * np.linalg.norm(ctx.get_state(dcp.NSE_RHS))
+    assert vals[-1] <= tol < vals[-2]
+    assert np.all(np.diff(vals) <= 1e-12 * vals[0])  # least-squares residuals never grow
+    assert ctx.solver_history(1)[2] == 0                 # the fallback did not run
+    lines = ctx.deallog(2)
+    assert lines[0].startswith("DEAL:FGMRES::Check 0\t") and lines[-1].startswith(
+        f"DEAL:FGMRES::Convergence step {outer} value ")
+    for name in ("   Assemble NSE system", "   Build NSE preconditioner",
+                 "   Assembly NSE preconditioner", "   Assemble temperature matrices",
+                 "   Assemble temperature RHS", "   Solve Stokes system",
+                 "   Solve temperature system"):
+        calls, sec = ctx.timer_section(name)
+        assert calls == 1 and sec > 0, name
+    assert ctx.timer_section("   Assembly NSE preconditioner")[1] <= \
+        ctx.timer_section("   Build NSE preconditioner")[1]
+    summary = ctx.timer_summary()
+    assert "Total wallclock time elapsed since start" in summary and "Solve Stokes system" in summary
+    with pytest.raises(dcp.DcpError):
+        ctx.timer_section("no such section")
+    ctx.close()
