@@ -604,6 +604,22 @@ void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, 
 // its last column.
 template <int KL>
 constexpr int dcgs_kp() { return pow2_at_least<KL + 2>(); }
+
+// Timing probe builds only (-DDCP_DCGS_TIMING=k, tools/dcgs_timing.py): the
+// step with basis size k records per-workgroup realtime stamps (100 MHz) at
+// its phase boundaries.
+#ifdef DCP_DCGS_TIMING
+__device__ unsigned long long g_dcgs_ts[256 * 8];
+#define DCGS_TS(slot)                                                                  \
+  do {                                                                                 \
+    if (k == DCP_DCGS_TIMING && threadIdx.x == 0) g_dcgs_ts[8 * blockIdx.x + (slot)] = \
+        wall_clock64();                                                                \
+  } while (0)
+#else
+#define DCGS_TS(slot) \
+  do {                \
+  } while (0)
+#endif
 // result granules after the partial area (2 K nb <= 2 * 64 * 256 doubles)
 constexpr int kDcgsRes = 2 * 64 * 256;
 
@@ -746,6 +762,7 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
   constexpr int K = 2 * KP;
   __shared__ double sm[kChainWaves * K];
   __shared__ double hs[K];
+  DCGS_TS(0);
   if (st->status) return;
   const bool tail = tnext == nullptr;
   const int nb = gridDim.x, b = blockIdx.x;
@@ -806,6 +823,7 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
     if ((l & ((1 << sh) - 1)) == 0) sm[wv_ * K + (l >> sh)] = r;
   }
   __syncthreads();
+  DCGS_TS(1);
   double* part = gran;
   double* res = gran + kDcgsRes;
   const unsigned long long tag = seq * 128;
@@ -817,10 +835,12 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
     granule_store(part + 2 * (size_t(j) * nb + b), tot, tag + j);
   }
   // reducer: workgroup b sums slot b over the nb workgroups
+  DCGS_TS(2);
   if (b < K && dcgs_used<KP>(b, k, tail) && threadIdx.x < 64) {
     const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag + b, err);
     if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + K + b);
   }
+  DCGS_TS(3);
   if (used) {
     const double* p = res + 2 * j;
     mgs_u4 q = granule_load(p);
@@ -837,6 +857,7 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
     hs[j] = 0.0;
   }
   __syncthreads();
+  DCGS_TS(4);
   const DcgsScalars c = dcgs_scalars<KP>(hs, k, tail);
   if (!tail || k > 0) {
     const double ib = 1.0 / c.beta;
@@ -860,8 +881,10 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
       if (k > 0 && live[e]) const_cast<double*>(t_in)[pos[e]] = q;
     }
   }
+  DCGS_TS(5);
   if (b != 0) return;
   dcgs_bookkeeping<KP>(st, hs, k, tail, c);
+  DCGS_TS(6);
 }
 
 // Several GPUs (or vectors too long for one resident launch): block sums of
@@ -969,6 +992,12 @@ __global__ __launch_bounds__(kBlock) void k_dcgs_update(Seg g, const double* __r
 }
 
 bool dcgs2_fits(long n, int nb, int n_cus) { return cgs2_chain_fits(n, nb, n_cus); }
+
+#ifdef DCP_DCGS_TIMING
+extern "C" int dcp_probe_dcgs_timestamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dcgs_ts), sizeof(g_dcgs_ts)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t dcgs2_granules(long n) {
   const size_t nbp = size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));

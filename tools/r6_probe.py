@@ -91,7 +91,9 @@ src[m.n_u:] = p - p.mean()
 t0 = time.perf_counter()
 dst, its = ctx.block_preconditioner_vmult(src)
 stage("inner_gmres_50", t0)
-r = ctx.schur_vmult(-dst[m.n_u:]) - src[m.n_u:]
+# at the cap the inner GMRES throws NoConvergence before dst_p = -y
+# (block_schur_preconditioner.hpp:48-51), so dst_p holds the iterate y
+r = ctx.schur_vmult(dst[m.n_u:]) - src[m.n_u:]
 checks["inner_steps"] = its
 checks["inner_residual_reduction"] = float(np.linalg.norm(r) / np.linalg.norm(src[m.n_u:]))
 out["checks"] = checks
