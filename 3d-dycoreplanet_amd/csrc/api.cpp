@@ -16,6 +16,7 @@
 #include "context.h"
 #include "fe_tables.h"
 #include "mesh.h"
+#include "mesh2d.h"
 #include "partition.h"
 #include "prm.h"
 #include "renumber.h"
@@ -50,11 +51,6 @@ Ctx::~Ctx() {
 namespace {
 
 thread_local std::string g_last_error;
-
-struct ApiError {
-  int code;
-  std::string msg;
-};
 
 template <class F>
 int guarded(dcp_ctx* ctx, F&& f) {
@@ -160,6 +156,8 @@ void velocity_stats_global(Ctx& c) {
   halo_exchange(c, c.halo_nse, c.nse_sol.p);
   if (c.feec)
     feec_velocity_stats(c.fcd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
+  else if (c.dim2)
+    velocity_stats_2d(c.m2(), c.nse_sol.p, c.dscal.p + 262, c.stream);
   else
     velocity_stats(c.cd(), c.n_owned_cells, c.nse_sol.p, c.dscal.p + 262, c.stream);
   allreduce(c, c.dscal.p + 262, 2, true);
@@ -1275,6 +1273,8 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     }
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
     c.feec = false;
+    c.dim2 = false;
+    c.vdim = 3;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -1730,6 +1730,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     Ctx& c = *ctx;
     SectionScope sec(c, "   Assemble NSE system");
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
+    if (c.dim2) {
+      assemble_nse_2d(c, flags);
+      t.stop();
+      return DCP_OK;
+    }
     const bool matrix = (flags & DCP_ASSEMBLE_MATRIX) != 0;
     // the velocity block is materialised only when something reads it
     const bool full = matrix && (c.assemble_A || c.matrix_free == 0);
@@ -1787,6 +1792,12 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
     Ctx& c = *ctx;
     SectionScope sec(c, "   Build NSE preconditioner");
     PhaseTimer t(c, &c.timings.build_precond_ms);
+    if (c.dim2) {
+      build_precond_2d(c);
+      t.stop();
+      c.precond_built = true;
+      return DCP_OK;
+    }
     {
       SectionScope sub(c, "   Assembly NSE preconditioner");
       c.A_diag.zero(c.stream);
@@ -1819,6 +1830,12 @@ int dcp_assemble_temperature_matrix(dcp_ctx* ctx) {
     Ctx& c = *ctx;
     SectionScope sec(c, "   Assemble temperature matrices");
     PhaseTimer t(c, &c.timings.assemble_T_matrix_ms);
+    if (c.dim2) {
+      assemble_T_matrix_2d(c);
+      t.stop();
+      c.T_matrix_ok = true;
+      return DCP_OK;
+    }
     c.Tmass.zero(c.stream);
     c.Tstiff.zero(c.stream);
     for (int k = 0; k < c.n_colors(); ++k)
@@ -1843,6 +1860,12 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     c.T_rhs.zero(c.stream);
     halo_exchange(c, c.halo_T, c.old_T.p);
     halo_exchange(c, c.halo_nse, c.nse_sol.p);
+    if (c.dim2) {
+      assemble_T_rhs_2d(c);
+      t.stop();
+      c.T_rhs_ok = true;
+      return DCP_OK;
+    }
     if (c.feec) {
       // velocity from the Raviart-Thomas field of nse_solution (FEEC.tpp:1000-1062)
       for (int k = 0; k < c.n_colors(); ++k)
@@ -2012,6 +2035,10 @@ int dcp_nse_matrix_export(dcp_ctx* ctx, int64_t* nnz, int32_t* rowptr, int32_t* 
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(nnz != nullptr, DCP_ERR_INVALID, "NULL nnz");
+    if (c.dim2) {
+      nse_matrix_export_2d(c, nnz, rowptr, cols, vals);
+      return DCP_OK;
+    }
     auto down_i = [&](const DBuf<int32_t>& b) {
       std::vector<int32_t> h(b.n);
       DCP_HIP_CHECK(hipMemcpy(h.data(), b.p, b.n * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -2105,6 +2132,10 @@ int dcp_cell_nse_system(dcp_ctx* ctx, int first, int n, double* K, double* f) {
     Ctx& c = *ctx;
     require(K && f && first >= 0 && n > 0 && first + n <= c.n_cells, DCP_ERR_INVALID,
             "bad cell range");
+    if (c.dim2) {
+      cell_nse_system_2d(c, first, n, K, f);
+      return DCP_OK;
+    }
     DBuf<double> dK, df;
     dK.alloc(size_t(n) * 89 * 89);
     df.alloc(size_t(n) * 89);
@@ -2339,6 +2370,8 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     }
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
     c.feec = true;
+    c.dim2 = false;
+    c.vdim = 3;
     c.have_mesh = false;
     c.n_cells = nc;
     c.n_owned_cells = dist ? L.n_owned_cells : nc;
@@ -2545,6 +2578,15 @@ struct dcp_host_mesh {
   std::vector<int32_t> cell_nse;
   std::vector<double> nse_xyz;     // support point of each velocity node once renumbered
   std::unique_ptr<FeecDofs> feec;  // built on first request
+  // the 2D shell (dcp_host_mesh2d_create); the members above stay empty
+  struct Two {
+    Mesh2D mesh;
+    int tdeg = 2, n_T = 0;
+    Constraints nse, T;
+    std::vector<int32_t> cell_nse, cell_T;
+    std::vector<double> node_xy;   // support point of each velocity node (current numbering)
+  };
+  std::unique_ptr<Two> two;
 };
 
 dcp_host_mesh* dcp_host_mesh_create(int cuboid, int refine, double R0, double R1, double length,
@@ -2571,6 +2613,22 @@ void dcp_host_mesh_destroy(dcp_host_mesh* m) { delete m; }
 
 int dcp_host_mesh_renumber_cuthill_mckee(dcp_host_mesh* h) {
   if (!h) return DCP_ERR_INVALID;
+  if (h->two) {
+    try {
+      dcp_host_mesh::Two& t = *h->two;
+      const std::vector<int32_t> map = cuthill_mckee_map_2d(t.mesh, t.cell_nse);
+      for (int32_t& d : t.cell_nse) d = map[d];
+      t.nse = renumber_constraints(t.nse, map);
+      std::vector<double> xy(t.node_xy.size());
+      for (int n = 0; n < t.mesh.n_vnodes; ++n)
+        for (int k = 0; k < 2; ++k) xy[2 * size_t(map[2 * n] / 2) + k] = t.node_xy[2 * size_t(n) + k];
+      t.node_xy.swap(xy);
+      return DCP_OK;
+    } catch (const std::exception& e) {
+      g_last_error = e.what();
+      return DCP_ERR_INVALID;
+    }
+  }
   try {
     const Mesh& m = h->mesh;
     const std::vector<int32_t> nw = cuthill_mckee_nodes(m.n_cells, h->cell_nse.data(), m.n_vnodes);
@@ -2603,6 +2661,10 @@ static dcp_constraints view_of(const Constraints& c) {
 
 int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
   if (!h || !out) return DCP_ERR_INVALID;
+  if (h->two) {
+    g_last_error = "a 2D host mesh: use dcp_host_mesh2d_view_get";
+    return DCP_ERR_INVALID;
+  }
   const Mesh& m = h->mesh;
   out->n_cells = m.n_cells;
   out->n_u = m.n_u();
@@ -2648,9 +2710,97 @@ int dcp_host_feec_view_get(dcp_host_mesh* h, dcp_feec_mesh* out) {
 
 int dcp_host_mesh_initial_temperature(const dcp_host_mesh* h, double* T) {
   if (!h || !T) return DCP_ERR_INVALID;
+  if (h->two) {
+    // TemperatureInitialValues<2> at the MappingQ1 support points
+    const Mesh2D& m = h->two->mesh;
+    for (int d = 0; d < h->two->n_T; ++d) {
+      const int n = h->two->tdeg == 2 ? d : m.vertex_vnode[d];
+      T[d] = temperature_initial_2d(&m.xy_q1[2 * size_t(n)], m.R0, m.R1);
+    }
+    return DCP_OK;
+  }
   for (int d = 0; d < h->tdofs.n_dofs; ++d)
     T[d] = temperature_initial(h->mesh, &h->mesh.xyz[3 * size_t(h->tdofs.dof_vnode[d])]);
   return DCP_OK;
+}
+
+dcp_host_mesh* dcp_host_mesh2d_create(int refine, double R0, double R1, double length,
+                                      int temperature_degree, int mapping_q_on_all_cells) {
+  try {
+    if (temperature_degree != 1 && temperature_degree != 2)
+      throw std::invalid_argument("2D temperature degree must be 1 or 2");
+    if (!(length > 0)) throw std::invalid_argument("reference length must be positive");
+    auto h = std::make_unique<dcp_host_mesh>();
+    h->two = std::make_unique<dcp_host_mesh::Two>();
+    dcp_host_mesh::Two& t = *h->two;
+    t.mesh = build_shell_2d(refine, R0 / length, R1 / length, mapping_q_on_all_cells != 0);
+    const Mesh2D& m = t.mesh;
+    t.tdeg = temperature_degree;
+    t.cell_nse = nse_cell_dofs_2d(m);
+    t.nse = nse_constraints_2d(m);
+    t.node_xy = m.xy;
+    if (temperature_degree == 2) {
+      t.cell_T = temperature_cell_dofs_2d(m);
+      t.T = temperature_constraints_2d(m);
+      t.n_T = m.n_vnodes;
+    } else {
+      // FE_Q(1): the vertices in first-encounter order, Dirichlet on the inner circle
+      t.cell_T = m.cell_q1;
+      t.n_T = m.n_vertices;
+      Constraints c;
+      c.n_dofs = t.n_T;
+      c.line_of.assign(t.n_T, -1);
+      c.entry_ptr.push_back(0);
+      for (int v = 0; v < t.n_T; ++v) {
+        const int n = m.vertex_vnode[v];
+        if (!(m.vnode_bnd[n] & kBndInner)) continue;
+        c.line_of[v] = c.n_lines();
+        c.line_dof.push_back(v);
+        c.inhomogeneity.push_back(temperature_initial_2d(&m.xy_q1[2 * size_t(n)], m.R0, m.R1));
+        c.entry_ptr.push_back(0);
+      }
+      t.T = std::move(c);
+    }
+    return h.release();
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+int dcp_host_mesh2d_view_get(const dcp_host_mesh* h, dcp_mesh2d* out, const double** node_xy,
+                             int* n_vnodes) {
+  if (!h || !out || !h->two) return DCP_ERR_INVALID;
+  const dcp_host_mesh::Two& t = *h->two;
+  out->n_cells = t.mesh.n_cells;
+  out->n_u = t.mesh.n_u();
+  out->n_p = t.mesh.n_p();
+  out->n_T = t.n_T;
+  out->temperature_degree = t.tdeg;
+  out->cell_nse_dofs = t.cell_nse.data();
+  out->cell_T_dofs = t.cell_T.data();
+  out->cell_geometry = t.mesh.cell_map.data();
+  out->cell_diameter = t.mesh.cell_diameter.data();
+  out->nse = view_of(t.nse);
+  out->T = view_of(t.T);
+  if (node_xy) *node_xy = t.node_xy.data();
+  if (n_vnodes) *n_vnodes = t.mesh.n_vnodes;
+  return DCP_OK;
+}
+
+int dcp_mesh2d_upload(dcp_ctx* ctx, const dcp_mesh2d* m) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
+    mesh2d_upload(*ctx, m);
+    return DCP_OK;
+  });
+}
+
+int dcp_mesh2d_check(const dcp_mesh2d* m, int* n_colors) {
+  return guarded(nullptr, [&] {
+    mesh2d_check(m, n_colors);
+    return DCP_OK;
+  });
 }
 
 int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len) {

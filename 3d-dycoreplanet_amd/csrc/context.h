@@ -14,6 +14,12 @@
 
 namespace dcp {
 
+// a failed C-ABI call: its return code and message (dcp_last_error)
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -317,9 +323,34 @@ struct Ctx {
     return FeecCellData{n_cells, fe_dofs.p, fe_sign.p, fe_X.p, diameter.p, fe_fixed.p, cell_T.p};
   }
 
-  Seg seg_nse() const { return Seg::two(3 * nvo, n_u, 3 * nvo + npo, 0); }
+  // ---- two-dimensional model (Standard::BoussinesqModel<2>, dcp_mesh2d_upload):
+  // nse_matrix [u | p] as one scalar CSR, blocks applied as row/column windows
+  bool dim2 = false;
+  int vdim = 3;                          // velocity components per support point
+  int m2_tdpc = 4;                       // temperature dofs per cell (FE_Q(1) / FE_Q(2))
+  DBuf<int32_t> m2_dofs, m2_tdofs, m2_pos, m2_posT;
+  DBuf<double> m2_X, m2_srcw;
+  DBuf<int8_t> m2_src;
+  DBuf<uint8_t> m2_fixed;
+  DBuf<int32_t> m2_ptr, m2_col;
+  DBuf<double> m2_val;
+  // NSE constraint lines (distribute) and the pressure dofs among them
+  int m2_nlines = 0;
+  DBuf<int32_t> m2_ldof, m2_lptr, m2_lent;
+  DBuf<double> m2_lw, m2_linh;
+  Mesh2DDev m2() const {
+    return Mesh2DDev{n_cells, n_u,      m2_tdpc,    m2_dofs.p, m2_tdofs.p, m2_X.p,    diameter.p,
+                     m2_src.p, m2_srcw.p, m2_fixed.p, m2_pos.p,  m2_posT.p,  T_fixed.p, T_bc.p};
+  }
+  // y = block (rows [r0, r1), columns [c0, c1)) of the 2D nse_matrix times x
+  // (x indexed from c0)
+  void m2_block(int r0, int r1, int c0, int c1, const double* x, double* y, bool add) const {
+    spmv_block(r0, r1, c0, c1, m2_ptr.p, m2_col.p, m2_val.p, x, y, add, stream);
+  }
+
+  Seg seg_nse() const { return Seg::two(vdim * nvo, n_u, vdim * nvo + npo, 0); }
   Seg seg_p() const { return Seg::all(npo, 1); }
-  Seg seg_v() const { return Seg::all(3 * nvo, 2); }
+  Seg seg_v() const { return Seg::all(vdim * nvo, 2); }
   Seg seg_T() const { return Seg::all(nTo, 3); }
 
   CellData cd() const {
@@ -375,6 +406,16 @@ void ensure_A_val(Ctx& c);
 void materialize_velocity_block(Ctx& c);
 // B = (B^T)^T after an operator-form assembly that scattered B^T only
 void materialize_B(Ctx& c);
+// model2d.cpp: the 2D model's upload and hot-path members
+void mesh2d_upload(Ctx& c, const dcp_mesh2d* m);
+void mesh2d_check(const dcp_mesh2d* m, int* n_colors);
+void assemble_nse_2d(Ctx& c, int flags);
+void build_precond_2d(Ctx& c);
+void assemble_T_matrix_2d(Ctx& c);
+void assemble_T_rhs_2d(Ctx& c);
+void distribute_nse_2d(Ctx& c, double* x);
+void nse_matrix_export_2d(Ctx& c, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals);
+void cell_nse_system_2d(Ctx& c, int first, int n, double* K, double* f);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
 // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414)

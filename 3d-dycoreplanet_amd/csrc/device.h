@@ -97,6 +97,41 @@ struct NseOut {
   const int32_t* pcidx;
 };
 
+// ---- assembly2d.hip -----------------------------------------------------------
+// Two-dimensional model (Standard::BoussinesqModel<2>): 22-dof cells over a
+// scalar CSR nse_matrix [u | p]; node-local constraint table per cell.
+struct Mesh2DDev {
+  int n_cells, n_u, tdpc;
+  const int32_t* dofs;      // [n_cells][22] FESystem local order
+  const int32_t* tdofs;     // [n_cells][tdpc] FE_Q local order
+  const double* X;          // [n_cells][16][2] MappingQ(3) support points
+  const double* diameter;   // [n_cells]
+  const int8_t* src;        // [n_cells][22] constrained local dof whose line targets this one, or -1
+  const double* srcw;       // [n_cells][22] its weight
+  const uint8_t* fixed;     // [n_cells][22] local dof constrained
+  const int32_t* pos;       // [n_cells][22][22] CSR entry of (dof_i, dof_j) or -1
+  const int32_t* posT;      // [n_cells][tdpc][tdpc]
+  const uint8_t* T_fixed;   // [n_T]
+  const double* T_bc;       // [n_T]
+};
+void launch2d_nse_system(const Mesh2DDev& m, const int32_t* cells, int n, const double* old_nse,
+                         const double* old_T, const PhysicsDev& ph, double* A, double* rhs,
+                         hipStream_t s);
+void launch2d_nse_elements(const Mesh2DDev& m, int first, int n, const double* old_nse,
+                           const double* old_T, const PhysicsDev& ph, double* K, double* f,
+                           hipStream_t s);
+void launch2d_precond_diag(const Mesh2DDev& m, const int32_t* cells, int n, const PhysicsDev& ph,
+                           double* Ad, double* Mpd, hipStream_t s);
+void launch2d_T_matrix(const Mesh2DDev& m, const int32_t* cells, int n, const PhysicsDev& ph,
+                       double* M, double* K, hipStream_t s);
+void launch2d_T_rhs(const Mesh2DDev& m, const int32_t* cells, int n, const double* T_old,
+                    const double* nse, const PhysicsDev& ph, double* rhs, hipStream_t s);
+void velocity_stats_2d(const Mesh2DDev& m, const double* nse, double* out2, hipStream_t s);
+void distribute_2d(int n_lines, const int32_t* line_dof, const int32_t* ptr, const int32_t* ent,
+                   const double* w, const double* inhom, double* x, hipStream_t s);
+void positions_2d(int n_cells, int dpc, const int32_t* dofs, const int32_t* ptr, const int32_t* col,
+                  int32_t* pos, hipStream_t s);
+
 // ---- matfree.hip ----------------------------------------------------------
 // Matrix-free [A B^T; B 0] (or A alone) of the classic Q2^3/Q1 system.
 // Per-cell arrays in colour order (position e = e-th cell of the colour-sorted

@@ -22,26 +22,34 @@
 #include <vector>
 
 #include "mesh.h"
+#include "mesh2d.h"
 #include "renumber.h"
 
 namespace dcp {
 namespace {
 
-// local index of the x component of the 27 velocity support points in the
-// FESystem order (4 per vertex: u, v, w, p; then 19 x 3 for lines/faces/interior)
-int vel_x(int t) { return t < 8 ? 4 * t : 32 + 3 * (t - 8); }
+// The FESystem(FE_Q(2)^dim, FE_Q(1)) cell layout: dofs per cell, support
+// points per cell (hierarchic), vertices, velocity components; local index of
+// the x velocity dof at support point t (dim + 1 dofs per vertex, dim per
+// other point) and of the pressure dof at vertex v.
+struct Layout {
+  int dpc, npc, nv, dim;
+  int vel_x(int t) const { return t < nv ? (dim + 1) * t : (dim + 1) * nv + dim * (t - nv); }
+  int p_local(int v) const { return (dim + 1) * v + dim; }
+};
+constexpr Layout kLayout3D{89, 27, 8, 3};
+constexpr Layout kLayout2D{kNseDofs2D, 9, 4, 2};
 
-}  // namespace
-
-std::vector<int32_t> cuthill_mckee_nodes(int n_cells, const int32_t* cell_nse, int n_vnodes) {
-  std::vector<int32_t> cn(size_t(n_cells) * 27);
+std::vector<int32_t> cm_nodes(const Layout& L, int n_cells, const int32_t* cell_nse, int n_vnodes) {
+  const int P = L.npc;
+  std::vector<int32_t> cn(size_t(n_cells) * P);
   std::vector<uint8_t> has_p(n_vnodes, 0);
   for (int c = 0; c < n_cells; ++c)
-    for (int t = 0; t < 27; ++t) {
-      const int n = cell_nse[size_t(c) * 89 + vel_x(t)] / 3;
+    for (int t = 0; t < P; ++t) {
+      const int n = cell_nse[size_t(c) * L.dpc + L.vel_x(t)] / L.dim;
       if (n < 0 || n >= n_vnodes) throw std::invalid_argument("cuthill_mckee: velocity dof out of range");
-      cn[size_t(c) * 27 + t] = n;
-      if (t < 8) has_p[n] = 1;
+      cn[size_t(c) * P + t] = n;
+      if (t < L.nv) has_p[n] = 1;
     }
   // node -> cells
   std::vector<int32_t> nptr(n_vnodes + 1, 0), ncell(cn.size());
@@ -50,13 +58,13 @@ std::vector<int32_t> cuthill_mckee_nodes(int n_cells, const int32_t* cell_nse, i
   {
     std::vector<int32_t> fill(nptr.begin(), nptr.end() - 1);
     for (int c = 0; c < n_cells; ++c)
-      for (int t = 0; t < 27; ++t) ncell[fill[cn[size_t(c) * 27 + t]]++] = c;
+      for (int t = 0; t < P; ++t) ncell[fill[cn[size_t(c) * P + t]]++] = c;
   }
   std::vector<int32_t> stamp(n_vnodes, -1);
   auto neighbours = [&](int n, std::vector<int32_t>& out) {
     for (int k = nptr[n]; k < nptr[n + 1]; ++k)
-      for (int t = 0; t < 27; ++t) {
-        const int m = cn[size_t(ncell[k]) * 27 + t];
+      for (int t = 0; t < P; ++t) {
+        const int m = cn[size_t(ncell[k]) * P + t];
         if (stamp[m] != n) {
           stamp[m] = n;
           out.push_back(m);
@@ -70,7 +78,7 @@ std::vector<int32_t> cuthill_mckee_nodes(int n_cells, const int32_t* cell_nse, i
     for (int n = 0; n < n_vnodes; ++n) {
       nb.clear();
       neighbours(n, nb);
-      for (int m : nb) coord[n] += 3 + has_p[m];
+      for (int m : nb) coord[n] += L.dim + has_p[m];
     }
   }
   std::fill(stamp.begin(), stamp.end(), -1);
@@ -103,19 +111,20 @@ std::vector<int32_t> cuthill_mckee_nodes(int n_cells, const int32_t* cell_nse, i
   return nw;
 }
 
-std::vector<int32_t> nse_dof_map(int n_cells, const int32_t* cell_nse, int n_vnodes, int n_p,
-                                 const std::vector<int32_t>& node_new) {
-  const int n_u = 3 * n_vnodes;
+std::vector<int32_t> dof_map(const Layout& L, int n_cells, const int32_t* cell_nse, int n_vnodes,
+                             int n_p, const std::vector<int32_t>& node_new) {
+  const int D = L.dim;
+  const int n_u = D * n_vnodes;
   std::vector<int32_t> map(size_t(n_u) + n_p, -1);
   for (int n = 0; n < n_vnodes; ++n)
-    for (int c = 0; c < 3; ++c) map[3 * size_t(n) + c] = 3 * node_new[n] + c;
+    for (int c = 0; c < D; ++c) map[D * size_t(n) + c] = D * node_new[n] + c;
   // pressure dofs in the order of their vertex node's new number
   std::vector<int32_t> pnode(n_p, -1);
   for (int c = 0; c < n_cells; ++c)
-    for (int v = 0; v < 8; ++v) {
-      const int p = cell_nse[size_t(c) * 89 + 4 * v + 3] - n_u;
+    for (int v = 0; v < L.nv; ++v) {
+      const int p = cell_nse[size_t(c) * L.dpc + L.p_local(v)] - n_u;
       if (p < 0 || p >= n_p) throw std::invalid_argument("cuthill_mckee: pressure dof out of range");
-      pnode[p] = cell_nse[size_t(c) * 89 + 4 * v] / 3;
+      pnode[p] = cell_nse[size_t(c) * L.dpc + L.vel_x(v)] / D;
     }
   std::vector<int32_t> order(n_p);
   std::iota(order.begin(), order.end(), 0);
@@ -125,6 +134,22 @@ std::vector<int32_t> nse_dof_map(int n_cells, const int32_t* cell_nse, int n_vno
                    [&](int a, int b) { return node_new[pnode[a]] < node_new[pnode[b]]; });
   for (int k = 0; k < n_p; ++k) map[size_t(n_u) + order[k]] = n_u + k;
   return map;
+}
+
+}  // namespace
+
+std::vector<int32_t> cuthill_mckee_nodes(int n_cells, const int32_t* cell_nse, int n_vnodes) {
+  return cm_nodes(kLayout3D, n_cells, cell_nse, n_vnodes);
+}
+
+std::vector<int32_t> nse_dof_map(int n_cells, const int32_t* cell_nse, int n_vnodes, int n_p,
+                                 const std::vector<int32_t>& node_new) {
+  return dof_map(kLayout3D, n_cells, cell_nse, n_vnodes, n_p, node_new);
+}
+
+std::vector<int32_t> cuthill_mckee_map_2d(const Mesh2D& m, const std::vector<int32_t>& cell_nse) {
+  const std::vector<int32_t> nw = cm_nodes(kLayout2D, m.n_cells, cell_nse.data(), m.n_vnodes);
+  return dof_map(kLayout2D, m.n_cells, cell_nse.data(), m.n_vnodes, m.n_p(), nw);
 }
 
 Constraints renumber_constraints(const Constraints& in, const std::vector<int32_t>& map) {

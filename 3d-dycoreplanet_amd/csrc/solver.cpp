@@ -823,6 +823,10 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
 
 // A (velocity-velocity block) on a velocity vector [u_own u_ghost]
 void a_vmult(Ctx& c, const double* src, double* dst) {
+  if (c.dim2) {
+    c.m2_block(0, c.n_u, 0, c.n_u, src, dst, false);
+    return;
+  }
   halo_exchange(c, c.halo_v, const_cast<double*>(src));
   if (c.matrix_free) {
     mf_apply(c, src, dst, false);
@@ -840,7 +844,11 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
     Control ctl{unsigned(c.inner_max_steps), 1e-6 * nrm};
     ensure_pool(c.sg_v, 32, size_t(np));
     State st;
-    if (c.schur_explicit && c.gram_schmidt == 1) {
+    if (c.dim2) {
+      // 2D: S = B D_A^-1 B^T as three products (schur_vmult), deal.II GMRES
+      Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
+      st = gmres(c, np, c.seg_p(), S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
+    } else if (c.schur_explicit && c.gram_schmidt == 1) {
       st = gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit && c.gram_schmidt == 2) {
       st = gmres_schur_dcgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
@@ -856,7 +864,10 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
   }
   // utmp = src_u - B^T dst_p
   halo_exchange(c, c.halo_p, dst + nu);
-  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, dst + nu, c.utmp.p, false, c.stream);
+  if (c.dim2)
+    c.m2_block(0, nu, nu, nu + np, dst + nu, c.utmp.p, false);
+  else
+    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, dst + nu, c.utmp.p, false, c.stream);
   sadd(nu, -1.0, 1.0, src, c.utmp.p, c.stream);
   if (do_solve_A) {
     // LA::SolverGMRES = AztecOO GMRES(30) with the A-Jacobi from the right,
@@ -970,6 +981,11 @@ void velocity_vmult(Ctx& c, const double* src, double* dst) { a_vmult(c, src, ds
 
 void nse_vmult(Ctx& c, const double* src, double* dst) {
   // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
+  if (c.dim2) {
+    const int n = c.n_u + c.n_p;
+    c.m2_block(0, n, 0, n, src, dst, false);
+    return;
+  }
   halo_exchange(c, c.halo_nse, const_cast<double*>(src));
   if (c.matrix_free) {
     mf_apply(c, src, dst, true);
@@ -982,6 +998,17 @@ void nse_vmult(Ctx& c, const double* src, double* dst) {
 }
 
 void schur_vmult(Ctx& c, const double* src, double* dst) {
+  if (c.dim2) {
+    // SchurComplement::vmult (schur_complement.hpp:143-150) with the Jacobi A^-1
+    const int nu = c.n_u, n = c.n_u + c.n_p;
+    Timer* ev = schur_sample(c);
+    if (ev) DCP_HIP_CHECK(hipEventRecord(ev->a, c.stream));
+    c.m2_block(0, nu, nu, n, src, c.schur_tmp1.p, false);
+    mul(nu, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
+    c.m2_block(nu, n, 0, nu, c.schur_tmp2.p, dst, false);
+    if (ev) DCP_HIP_CHECK(hipEventRecord(ev->b, c.stream));
+    return;
+  }
   if (c.schur_explicit) {
     halo_exchange(c, c.halo_p, const_cast<double*>(src));
     Timer* e = schur_sample(c);
@@ -1077,7 +1104,10 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
       status = DCP_NOT_CONVERGED;
     }
   }
-  distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
+  if (c.dim2)
+    distribute_nse_2d(c, x.p);                                 // :1233
+  else
+    distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
   if (c.periodic) {  // periodic images = their partners
     copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
     copy_images(c.n_img_p, c.img_p.p, c.mst_p.p, x.p, c.stream);
@@ -1142,27 +1172,45 @@ State pcg(Ctx& c, int n, Seg g, const Op& A, const Op& P, double* x, const doubl
 void build_ilu(Ctx& c) {
   Ctx::Ilu& f = c.ilu;
   if (f.ptr.p) return;  // reset by every mesh upload (free_workspaces)
-  const int nb = c.nvo;
-  std::vector<int32_t> bp(nb + 1), bc;
-  DCP_HIP_CHECK(hipMemcpy(bp.data(), c.A_ptr.p, (nb + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
-  bc.resize(size_t(bp[nb]));
-  DCP_HIP_CHECK(hipMemcpy(bc.data(), c.A_col.p, bc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-  const int n = 3 * nb;
+  const int n = c.dim2 ? c.n_u : 3 * c.nvo;
   std::vector<int32_t> ptr(n + 1, 0), col, pos, diag(n, -1);
-  col.reserve(size_t(9) * bc.size());
-  pos.reserve(size_t(9) * bc.size());
-  for (int r = 0; r < nb; ++r)
-    for (int ci = 0; ci < 3; ++ci) {
-      const int i = 3 * r + ci;
-      for (int k = bp[r]; k < bp[r + 1]; ++k)
-        for (int cj = 0; cj < 3; ++cj) {
-          const int j = 3 * bc[k] + cj;
-          if (j == i) diag[i] = int(col.size());
-          col.push_back(j);
-          pos.push_back(9 * k + 3 * ci + cj);
-        }
+  if (c.dim2) {
+    // the velocity window (rows and columns < n_u) of the scalar 2D nse_matrix;
+    // pos indexes its value array
+    std::vector<int32_t> mp(size_t(n) + 1), mc;
+    DCP_HIP_CHECK(hipMemcpy(mp.data(), c.m2_ptr.p, (n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    mc.resize(size_t(mp[n]));
+    DCP_HIP_CHECK(hipMemcpy(mc.data(), c.m2_col.p, mc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+      for (int k = mp[i]; k < mp[i + 1]; ++k) {
+        if (mc[k] >= n) continue;
+        if (mc[k] == i) diag[i] = int(col.size());
+        col.push_back(mc[k]);
+        pos.push_back(k);
+      }
       ptr[i + 1] = int(col.size());
     }
+  } else {
+    const int nb = c.nvo;
+    std::vector<int32_t> bp(nb + 1), bc;
+    DCP_HIP_CHECK(hipMemcpy(bp.data(), c.A_ptr.p, (nb + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    bc.resize(size_t(bp[nb]));
+    DCP_HIP_CHECK(hipMemcpy(bc.data(), c.A_col.p, bc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    col.reserve(size_t(9) * bc.size());
+    pos.reserve(size_t(9) * bc.size());
+    for (int r = 0; r < nb; ++r)
+      for (int ci = 0; ci < 3; ++ci) {
+        const int i = 3 * r + ci;
+        for (int k = bp[r]; k < bp[r + 1]; ++k)
+          for (int cj = 0; cj < 3; ++cj) {
+            const int j = 3 * bc[k] + cj;
+            if (j == i) diag[i] = int(col.size());
+            col.push_back(j);
+            pos.push_back(9 * k + 3 * ci + cj);
+          }
+        ptr[i + 1] = int(col.size());
+      }
+  }
   for (int i = 0; i < n; ++i)
     if (diag[i] < 0) throw std::runtime_error("Schur-complement ILU: missing diagonal entry");
   // levels: forward (reads rows j < i), backward (rows j > i)
@@ -1222,13 +1270,28 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   if (c.comm) throw std::runtime_error("the Schur-complement solver runs on one GPU");
   const int nu = c.n_u, np = c.n_p, n = nu + np;
   const double dt = c.ph.dt;
-  materialize_velocity_block(c);  // A (and B) as assembled
-  materialize_B(c);
+  if (!c.dim2) {
+    materialize_velocity_block(c);  // A (and B) as assembled
+    materialize_B(c);
+  }
   build_ilu(c);
   Ctx::Ilu& f = c.ilu;
   const IluView iv = f.view();
   // inner_schur_preconditioner->initialize(nse_matrix.block(0,0)) (:1266-1269)
-  ilu_factor(iv, c.A_val.p, f.lf_host.data(), f.lu.p, f.max_row, c.stream);
+  ilu_factor(iv, c.dim2 ? c.m2_val.p : c.A_val.p, f.lf_host.data(), f.lu.p, f.max_row, c.stream);
+  // the blocks of nse_matrix: A, B^T (velocity rows), B (pressure rows)
+  auto Ablk = [&](const double* x, double* y) {
+    if (c.dim2) c.m2_block(0, nu, 0, nu, x, y, false);
+    else spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
+  };
+  auto Btblk = [&](const double* p, double* y) {
+    if (c.dim2) c.m2_block(0, nu, nu, n, p, y, false);
+    else spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, p, y, false, c.stream);
+  };
+  auto Bblk = [&](const double* u, double* y) {
+    if (c.dim2) c.m2_block(nu, n, 0, nu, u, y, false);
+    else spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, u, y, false, c.stream);
+  };
   const Seg gu = Seg::all(nu), gp = Seg::all(np);
   ensure_pool(c.sc_v, 8, size_t(nu));
   double* const cg_u[3] = {c.sc_v[0], c.sc_v[1], c.sc_v[2]};
@@ -1236,9 +1299,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   ensure_pool(c.sc_p, 4, size_t(np));
   double* const cg_p[3] = {c.sc_p[0], c.sc_p[1], c.sc_p[2]};
   double* srhs = c.sc_p[3];
-  Op Av = [&](const double* x, double* y) {
-    spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
-  };
+  Op Av = [&](const double* x, double* y) { Ablk(x, y); };
   Op Pilu = [&](const double* x, double* y) { ilu_apply(iv, f.lu.p, x, y, c.stream); };
   int n_inv = 0;
   // InverseMatrix<A, ILU>::vmult (inverse_matrix.hpp:93-120): CG, tol 1e-6 |src|,
@@ -1257,19 +1318,19 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   zero_at(f.n_p_img, f.p_img.p, x.p, c.stream);                      // :1290-1292
   // schur_rhs = B A^-1 f - g (:1319-1321)
   inverse(c.nse_rhs.p, tmp);
-  spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, tmp, srhs, false, c.stream);
+  Bblk(tmp, srhs);
   sadd(np, 1.0, -1.0, c.nse_rhs.p + nu, srhs, c.stream);
   // SchurComplement::vmult (schur_complement.hpp:143-150): B A^-1 B^T
   Op S = [&](const double* s, double* d) {
-    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, s, t1, false, c.stream);
+    Btblk(s, t1);
     inverse(t1, t2);
-    spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, t2, d, false, c.stream);
+    Bblk(t2, d);
   };
   // ApproximateSchurComplement::vmult (approximate_schur_complement.hpp:131-139)
   Op Sa = [&](const double* s, double* d) {
-    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, s, t1, false, c.stream);
+    Btblk(s, t1);
     ilu_apply(iv, f.lu.p, t1, t2, c.stream);
-    spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, t2, d, false, c.stream);
+    Bblk(t2, d);
   };
   Op Id = [&](const double* s, double* d) { copy(np, s, d, c.stream); };
   // ApproximateInverseMatrix<S~, identity>(n_iter = invalid) (approximate_inverse.hpp)
@@ -1285,6 +1346,10 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   Control ctl{unsigned(n), 1e-6 * rn};
   const State st = gmres(c, np, gp, S, &Pre, x.p + nu, srhs, ctl, c.sg_v, 30);
   auto distribute = [&] {
+    if (c.dim2) {
+      distribute_nse_2d(c, x.p);
+      return;
+    }
     distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);
     if (c.periodic) {
       copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
@@ -1295,7 +1360,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   sec_p.stop();
   SectionScope sec_u(c, "      Solve NSE system - outer CG solver (for u)");
   // u = A^-1 (f - B^T p) (:1366-1372)
-  spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, x.p + nu, tmp, false, c.stream);
+  Btblk(x.p + nu, tmp);
   sadd(nu, -1.0, 1.0, c.nse_rhs.p, tmp, c.stream);
   inverse(tmp, x.p);
   distribute();                                                       // :1378

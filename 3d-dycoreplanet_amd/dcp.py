@@ -36,7 +36,7 @@ OPT_GRAM_SCHMIDT = 7
 OPT_FEEC_FIXED_INNER = 8
 OPT_LOG_HISTORY = 10
 OPT_INNER_MAX_STEPS = 11
-ABI_VERSION = 3            # include/dcp.h DCP_ABI_VERSION
+ABI_VERSION = 4            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
@@ -58,6 +58,7 @@ EXPORTED = [
     "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
+    "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
 ]
 
 
@@ -122,6 +123,17 @@ class FeecMeshView(C.Structure):
         ("cell_vertices", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
         ("cell_T_dofs", C.POINTER(C.c_int32)), ("w_fixed", C.POINTER(C.c_uint8)),
         ("u_fixed", C.POINTER(C.c_uint8)), ("T", Constraints),
+    ]
+
+
+class Mesh2DView(C.Structure):
+    """dcp_mesh2d: the 2D model's DoFs, geometry and constraints."""
+    _fields_ = [
+        ("n_cells", C.c_int), ("n_u", C.c_int), ("n_p", C.c_int), ("n_T", C.c_int),
+        ("temperature_degree", C.c_int),
+        ("cell_nse_dofs", C.POINTER(C.c_int32)), ("cell_T_dofs", C.POINTER(C.c_int32)),
+        ("cell_geometry", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
+        ("nse", Constraints), ("T", Constraints),
     ]
 
 
@@ -231,6 +243,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_timer_section.argtypes = [P, C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_double)]
     lib.dcp_timer_record.argtypes = [P, C.c_char_p, C.c_double]
     lib.dcp_timer_reset.argtypes = [P]
+    lib.dcp_mesh2d_upload.argtypes = [P, C.POINTER(Mesh2DView)]
+    lib.dcp_mesh2d_check.argtypes = [C.POINTER(Mesh2DView), C.POINTER(I)]
+    lib.dcp_host_mesh2d_create.argtypes = [I, C.c_double, C.c_double, C.c_double, I, I]
+    lib.dcp_host_mesh2d_create.restype = P
+    lib.dcp_host_mesh2d_view_get.argtypes = [P, C.POINTER(Mesh2DView), C.POINTER(D), C.POINTER(I)]
     return lib
 
 
@@ -368,6 +385,71 @@ class HostMesh:
         if rc != DCP_OK:
             raise DcpError(rc, lib().dcp_last_error(None).decode())
         return bool(sep.value), nc.value, nl.value
+
+
+class HostMesh2D:
+    """The 2D shell of Standard::BoussinesqModel<2> (dcp_host_mesh2d_create):
+    hyper_shell<2> with 12 cells, refine_global, FESystem(FE_Q(2)^2, FE_Q(1))
+    DoFs (22 per cell), FE_Q(temperature_degree) temperature, constraints."""
+
+    dim = 2
+
+    def __init__(self, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=2,
+                 mapping_q_on_all_cells=False, cuthill_mckee=False):
+        h = lib().dcp_host_mesh2d_create(int(refine), float(R0), float(R1), float(length),
+                                         int(temperature_degree), int(bool(mapping_q_on_all_cells)))
+        if not h:
+            raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
+        try:
+            if cuthill_mckee and lib().dcp_host_mesh_renumber_cuthill_mckee(h) != DCP_OK:
+                raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
+            v = Mesh2DView()
+            xy = C.POINTER(C.c_double)()
+            nv = C.c_int(0)
+            rc = lib().dcp_host_mesh2d_view_get(h, C.byref(v), C.byref(xy), C.byref(nv))
+            if rc != DCP_OK:
+                raise DcpError(rc, "dcp_host_mesh2d_view_get failed")
+            nc = v.n_cells
+            self.n_cells, self.n_u, self.n_p, self.n_T = nc, v.n_u, v.n_p, v.n_T
+            self.n_vnodes = nv.value
+            self.temperature_degree = v.temperature_degree
+            tdpc = (self.temperature_degree + 1) ** 2
+            self.cell_nse_dofs = _arr(v.cell_nse_dofs, nc * 22, np.int32).reshape(-1, 22)
+            self.cell_T_dofs = _arr(v.cell_T_dofs, nc * tdpc, np.int32).reshape(-1, tdpc)
+            # MappingQ(3) support points per cell (16, lexicographic, Gauss-Lobatto)
+            self.cell_geometry = _arr(v.cell_geometry, nc * 32, np.float64).reshape(-1, 16, 2)
+            self.cell_diameter = _arr(v.cell_diameter, nc, np.float64)
+            self.node_xy = _arr(xy, self.n_vnodes * 2, np.float64).reshape(-1, 2)
+            self.nse_constraints = ConstraintSet.from_view(v.nse)
+            self.T_constraints = ConstraintSet.from_view(v.T)
+            self.T0 = np.zeros(self.n_T)
+            lib().dcp_host_mesh_initial_temperature(h, _ptr(self.T0))
+        finally:
+            lib().dcp_host_mesh_destroy(h)
+        self.refine = refine
+        self.mapping_q_on_all_cells = bool(mapping_q_on_all_cells)
+
+    def as_struct(self, nse_constraints=None, T_constraints=None):
+        v = Mesh2DView()
+        v.n_cells, v.n_u, v.n_p, v.n_T = self.n_cells, self.n_u, self.n_p, self.n_T
+        v.temperature_degree = self.temperature_degree
+        v.cell_nse_dofs = self.cell_nse_dofs.ctypes.data_as(C.POINTER(C.c_int32))
+        v.cell_T_dofs = self.cell_T_dofs.ctypes.data_as(C.POINTER(C.c_int32))
+        v.cell_geometry = self.cell_geometry.ctypes.data_as(C.POINTER(C.c_double))
+        v.cell_diameter = self.cell_diameter.ctypes.data_as(C.POINTER(C.c_double))
+        self._nc = (nse_constraints or self.nse_constraints).as_struct()
+        self._tc = (T_constraints or self.T_constraints).as_struct()
+        v.nse, v.T = self._nc, self._tc
+        return v
+
+    def check(self, nse_constraints=None, T_constraints=None):
+        """Host-only validation of the 2D upload; returns the number of cell colours."""
+        v = self.as_struct(nse_constraints, T_constraints)
+        ncol = C.c_int(0)
+        rc = lib().dcp_mesh2d_check(C.byref(v), C.byref(ncol))
+        if rc != DCP_OK:
+            raise DcpError(rc, lib().dcp_last_error(None).decode())
+        return ncol.value
 
 
 class FeecTopology:
@@ -633,6 +715,14 @@ class Context:
             C.byref(nc), C.byref(tc)))
         self.mesh = m
 
+    def upload_mesh2d(self, m: HostMesh2D, nse_constraints=None, T_constraints=None):
+        """dcp_mesh2d_upload: the 2D model (Standard::BoussinesqModel<2>)."""
+        self._feec_view = None
+        v = m.as_struct(nse_constraints, T_constraints)
+        self._keep = (m, v)
+        self._check(lib().dcp_mesh2d_upload(self._h, C.byref(v)))
+        self.mesh = m
+
     # -- FEEC variant (ExteriorCalculus::BoussinesqModel<3>)
     def upload_feec_mesh(self, m: HostMesh):
         if m.feec is None:
@@ -781,8 +871,9 @@ class Context:
         return a, p
 
     def cell_nse_system(self, first, n):
-        K = np.zeros((n, 89, 89))
-        f = np.zeros((n, 89))
+        dpc = 22 if getattr(self.mesh, "dim", 3) == 2 else 89
+        K = np.zeros((n, dpc, dpc))
+        f = np.zeros((n, dpc))
         self._check(lib().dcp_cell_nse_system(self._h, int(first), int(n), _ptr(K), _ptr(f)))
         return K, f
 

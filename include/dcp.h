@@ -51,7 +51,7 @@ enum {
  * [n][27][3] to [n][64][3] and added a dcp_host_mesh_create parameter without
  * one). A caller compiled against another header must refuse to run:
  * dcp_abi_version() != DCP_ABI_VERSION. */
-#define DCP_ABI_VERSION 3
+#define DCP_ABI_VERSION 4
 int dcp_abi_version(void);
 /* Support points per cell in cell_geometry (MappingQ(3): 4^3). */
 #define DCP_CELL_SUPPORT_POINTS 64
@@ -72,7 +72,7 @@ typedef struct {
   double omega;                 /* planetary angular velocity */
   int cuboid;                   /* parameters.cuboid_geometry */
   int nse_solver_interval;      /* parameters.NSE_solver_interval */
-  int temperature_degree;       /* 1 (device path); 2 reserved */
+  int temperature_degree;       /* 3D: 1; 2D model: 1 or 2 (set by dcp_mesh2d) */
 } dcp_physics;
 
 /* A closed AffineConstraints object in CSR form (one line per constrained dof). */
@@ -384,6 +384,34 @@ int dcp_feec_cell_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 int dcp_feec_matrix_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,
                            double* vals);
 
+/* Two-dimensional model ---------------------------------------------------
+ * Standard::BoussinesqModel<2> (boussinesq_model.inst.cc:8; the 2D test
+ * configuration data/aqua_planet_test_2d.prm). FESystem(FE_Q(2)^2, FE_Q(1)):
+ * 22 dofs per cell in FESystem local order (per vertex u_x u_y p, per line
+ * u_x u_y, interior u_x u_y; deal.II vertex and line order); NSE vector =
+ * [u (n_u) | p (n_p)] after component_wise({0,0,1}); temperature
+ * FE_Q(temperature_degree), degree 1 or 2, in FE_Q local order (4 or 9 dofs
+ * per cell); geometry: the 16 MappingQ(3) support points per cell
+ * ([n][16][2], 4 x 4 Gauss-Lobatto, x fastest). The NSE constraint lines must
+ * be homogeneous with at most one entry on a dof of the same cells (the
+ * no-slip / no-normal-flux lines of the shell are), the temperature lines
+ * Dirichlet. One GPU. After the upload the hot-path calls above (assemble,
+ * preconditioner, dcp_solve_nse / dcp_solve_nse_schur, temperature, CFL,
+ * state, vmults, exports; dcp_cell_nse_system returns [n][22][22] / [n][22])
+ * act on the 2D model. */
+typedef struct {
+  int n_cells, n_u, n_p, n_T;
+  int temperature_degree;          /* 1 or 2 */
+  const int32_t* cell_nse_dofs;    /* [n_cells][22] */
+  const int32_t* cell_T_dofs;      /* [n_cells][(degree + 1)^2] */
+  const double* cell_geometry;     /* [n_cells][16][2] */
+  const double* cell_diameter;     /* [n_cells] */
+  dcp_constraints nse, T;
+} dcp_mesh2d;
+int dcp_mesh2d_upload(dcp_ctx* ctx, const dcp_mesh2d* m);
+/* Host-only dry run of dcp_mesh2d_upload's validation, patterns and colouring. */
+int dcp_mesh2d_check(const dcp_mesh2d* m, int* n_colors);
+
 /* Host setup helpers (mesh generator, .prm) ----------------------------- */
 typedef struct dcp_host_mesh dcp_host_mesh;
 /* Builds the refined shell (cuboid = 0) or cube, DoFs and constraints the way
@@ -419,6 +447,17 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* m, dcp_host_mesh_view* out);
 int dcp_host_feec_view_get(dcp_host_mesh* m, dcp_feec_mesh* out);
 /* T dof values of the initial temperature at the support points. */
 int dcp_host_mesh_initial_temperature(const dcp_host_mesh* m, double* T);
+/* The 2D shell: GridGenerator::hyper_shell<2>(0, R0, R1, 12 cells, colorize)
+ * under SphericalManifold, refine_global(refine) (planet_geometry.tpp:63-68),
+ * the DoFs of distribute_dofs + component_wise, the no-slip / no-normal-flux
+ * and temperature constraints of setup_dofs() (:255-387) with
+ * TemperatureInitialValues<2>. dcp_host_mesh_renumber_cuthill_mckee and
+ * dcp_host_mesh_initial_temperature accept it; dcp_host_mesh_view_get does
+ * not (use dcp_host_mesh2d_view_get: the arrays stay owned by the mesh). */
+dcp_host_mesh* dcp_host_mesh2d_create(int refine, double R0, double R1, double length,
+                                      int temperature_degree, int mapping_q_on_all_cells);
+int dcp_host_mesh2d_view_get(const dcp_host_mesh* m, dcp_mesh2d* out, const double** node_xy,
+                             int* n_vnodes);
 
 /* output_results (boussinesq_model.tpp:1566-1680), classic model, host-only:
  * DataOut::build_patches(nse_velocity_degree = 2) of the joint [u p T] solution

@@ -588,6 +588,7 @@ struct NoConvergence {};
 struct orc_model {
   orc_physics ph;
   int n_cells, n_u, n_p, n_T, tdeg, tdpc;
+  int dim = 3;  // 2: Standard::BoussinesqModel<2> (orc2d_create)
   std::vector<int> cell_nse, cell_T;
   std::vector<double> geom;
   Cons cnse, cT;
@@ -643,8 +644,14 @@ void gather(const std::vector<int>& cd, size_t c, int dpc, const double* src, do
 }
 }  // namespace
 
+void orc2d_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T);
+extern "C" void orc2d_cell_nse_preconditioner(const orc_physics* ph, const double* geom16, double* P);
+void orc2d_assemble_temperature_matrix(orc_model* m);
+void orc2d_assemble_temperature_rhs(orc_model* m, const double* old_T, const double* nse_solution);
+
 extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T) {
   // assemble_nse_system (:691-740); the four unused block matrices of :700-704 (Q22) are not kept.
+  if (m->dim == 2) return orc2d_assemble_nse_system(m, old_nse, old_T);
   m->nse.zero();
   std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
   std::vector<double> K(89 * 89), f(89), ul(89), Tl(27);
@@ -660,6 +667,7 @@ extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, con
 
 extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_nse,
                                                 const double* old_T, int threads) {
+  if (m->dim == 2) return orc2d_assemble_nse_system(m, old_nse, old_T);
   // The same assembly as orc_assemble_nse_system with deal.II WorkStream's
   // structure (boussinesq_model.tpp:712-734): local_assemble_nse_system on
   // `threads` threads (per-thread scratch), copy_local_to_global serialized in
@@ -694,17 +702,21 @@ extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   // Jacobi), so the condensed diagonal is accumulated directly.
   m->A_diag.assign(m->n_u, 0.0);
   m->Mp_diag.assign(m->n_p, 0.0);
-  std::vector<double> P(89 * 89);
+  const int npc = m->dim == 2 ? 22 : 89, ngeom = m->dim == 2 ? 32 : 192;
+  std::vector<double> P(npc * npc);
   std::vector<std::pair<int, double>> ei, ej;
   for (int c = 0; c < m->n_cells; ++c) {
-    orc_cell_nse_preconditioner(&m->ph, &m->geom[192 * size_t(c)], P.data());
-    const int* d = &m->cell_nse[89 * size_t(c)];
+    if (m->dim == 2)
+      orc2d_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P.data());
+    else
+      orc_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P.data());
+    const int* d = &m->cell_nse[npc * size_t(c)];
     bool any = false;
-    for (int i = 0; i < 89; ++i) any |= m->cnse.constrained(d[i]);
-    for (int i = 0; i < 89; ++i) {
+    for (int i = 0; i < npc; ++i) any |= m->cnse.constrained(d[i]);
+    for (int i = 0; i < npc; ++i) {
       expand(m->cnse, d[i], ei);
-      for (int j = 0; j < 89; ++j) {
-        const double k = P[89 * i + j];
+      for (int j = 0; j < npc; ++j) {
+        const double k = P[npc * i + j];
         if (k == 0.0) continue;
         expand(m->cnse, d[j], ej);
         for (const auto& a : ei)
@@ -719,11 +731,11 @@ extern "C" void orc_build_nse_preconditioner(orc_model* m) {
     }
     if (any) {
       double avg = 0;
-      for (int i = 0; i < 89; ++i) avg += std::fabs(P[89 * i + i]);
-      avg /= 89;
-      for (int i = 0; i < 89; ++i)
+      for (int i = 0; i < npc; ++i) avg += std::fabs(P[npc * i + i]);
+      avg /= npc;
+      for (int i = 0; i < npc; ++i)
         if (m->cnse.constrained(d[i])) {
-          const double kii = std::fabs(P[89 * i + i]);
+          const double kii = std::fabs(P[npc * i + i]);
           const double v = kii != 0.0 ? kii : avg;
           if (d[i] < m->n_u) m->A_diag[d[i]] += v; else m->Mp_diag[d[i] - m->n_u] += v;
         }
@@ -737,6 +749,7 @@ extern "C" void orc_build_nse_preconditioner(orc_model* m) {
 
 extern "C" void orc_assemble_temperature_matrix(orc_model* m) {
   // :821-864
+  if (m->dim == 2) return orc2d_assemble_temperature_matrix(m);
   m->Tmass.zero();
   m->Tstiff.zero();
   const int n = m->tdpc;
@@ -758,6 +771,7 @@ extern "C" void orc_assemble_temperature_rhs(orc_model* m, const double* old_T,
   m->T_inv.assign(m->n_T, 0.0);
   for (int r = 0; r < m->n_T; ++r) m->T_inv[r] = 1.0 / m->Tmat.at(r, r);
   std::fill(m->T_rhs.begin(), m->T_rhs.end(), 0.0);
+  if (m->dim == 2) return orc2d_assemble_temperature_rhs(m, old_T, nse_solution);
   const int n = m->tdpc;
   std::vector<double> Tl(n), ul(89), rhs(n), mfbc(n * n);
   std::vector<int> mask(n);
@@ -1242,6 +1256,7 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
                              int max_outer) {
   // solve_NSE_block_preconditioned (boussinesq_model.tpp:1131-1245)
   const int nu = m->n_u, np = m->n_p, n = nu + np;
+  if (int(m->A_inv.size()) != nu || int(m->Mp_inv.size()) != np) return -4;  // no preconditioner yet
   const double dt = m->ph.time_step;
   std::vector<double> x(sol, sol + n);
   for (int i = nu; i < n; ++i) x[i] *= dt;                         // :1151
@@ -1541,8 +1556,11 @@ extern "C" int orc_solve_temperature(orc_model* m, double* T, int* iterations) {
   return conv == kSuccess ? 0 : 1;
 }
 
+double orc2d_max_velocity(const orc_model* m, const double* sol, const double* diam);
+
 extern "C" double orc_max_velocity(const orc_model* m, const double* sol) {
   // get_maximal_velocity (:1023-1061) on QIterated<QTrapez>(2) = the Q2 nodes
+  if (m->dim == 2) return orc2d_max_velocity(m, sol, nullptr);
   double mx = 0;
   for (int c = 0; c < m->n_cells; ++c)
     for (int n = 0; n < 27; ++n) {
@@ -1555,6 +1573,7 @@ extern "C" double orc_max_velocity(const orc_model* m, const double* sol) {
 
 extern "C" double orc_cfl(const orc_model* m, const double* sol, const double* diam) {
   // get_cfl_number (:1064-1101)
+  if (m->dim == 2) return orc2d_max_velocity(m, sol, diam);
   double cfl = 0;
   for (int c = 0; c < m->n_cells; ++c) {
     double mx = 1e-10;
@@ -2122,4 +2141,333 @@ extern "C" void orc_feec_velocity_stats(const orc_feec* m, const double* sol, do
   }
   out2[0] = mx;
   out2[1] = cfl;
+}
+
+// ===========================================================================
+// Two-dimensional model: Standard::BoussinesqModel<2>
+// (boussinesq_model.inst.cc:8; data/aqua_planet_test_2d.prm, BASELINE C1).
+// FESystem(FE_Q(2)^2, FE_Q(1)): 22 local dofs (per vertex u_x u_y p, per line
+// u_x u_y, interior u_x u_y); temperature FE_Q(deg); MappingQ(3) from 16
+// support points; the 2D branches of local_assemble_nse_system (Q3: the
+// Coriolis term is -2 phi . cross_product_2d(u) without omega, :663-664).
+
+namespace {
+
+const int kHier2Lex2D[9] = {0, 2, 6, 8, 3, 5, 1, 7, 4};
+
+struct Vec2 {
+  double v[2] = {0, 0};
+  double& operator[](int i) { return v[i]; }
+  double operator[](int i) const { return v[i]; }
+};
+double dot2(const Vec2& a, const Vec2& b) { return a[0] * b[0] + a[1] * b[1]; }
+
+struct CellValues2D {
+  int nq = 0;
+  std::vector<double> JxW;
+  std::vector<Vec2> xq;
+  std::vector<double> v2, v1;  // [q][9], [q][4]
+  std::vector<Vec2> g2, g1;
+  void reinit(const double* geom16, int n1d) {
+    double qx[4], qw[4];
+    gauss1d(n1d, qx, qw);
+    nq = n1d * n1d;
+    JxW.assign(nq, 0);
+    xq.assign(nq, Vec2());
+    v2.assign(size_t(nq) * 9, 0);
+    v1.assign(size_t(nq) * 4, 0);
+    g2.assign(size_t(nq) * 9, Vec2());
+    g1.assign(size_t(nq) * 4, Vec2());
+    for (int q = 0; q < nq; ++q) {
+      const double p[2] = {qx[q % n1d], qx[q / n1d]};
+      const double w = qw[q % n1d] * qw[q / n1d];
+      double J[2][2] = {{0, 0}, {0, 0}};
+      Vec2 x;
+      for (int n = 0; n < 16; ++n) {
+        const int a = n % 4, b = n / 4;
+        const double s = lag3(a, p[0]) * lag3(b, p[1]);
+        const double g[2] = {dlag3(a, p[0]) * lag3(b, p[1]), lag3(a, p[0]) * dlag3(b, p[1])};
+        for (int i = 0; i < 2; ++i) {
+          x[i] += geom16[2 * n + i] * s;
+          for (int j = 0; j < 2; ++j) J[i][j] += geom16[2 * n + i] * g[j];
+        }
+      }
+      const double det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+      if (!(det > 0)) throw std::runtime_error("oracle 2D: non-positive Jacobian");
+      const double Ji[2][2] = {{J[1][1] / det, -J[0][1] / det}, {-J[1][0] / det, J[0][0] / det}};
+      JxW[q] = det * w;
+      xq[q] = x;
+      for (int n = 0; n < 9; ++n) {
+        const int a = n % 3, b = n / 3;
+        v2[9 * q + n] = lag2(a, p[0]) * lag2(b, p[1]);
+        const double r0 = dlag2(a, p[0]) * lag2(b, p[1]), r1 = lag2(a, p[0]) * dlag2(b, p[1]);
+        for (int i = 0; i < 2; ++i) g2[9 * q + n][i] = r0 * Ji[0][i] + r1 * Ji[1][i];
+      }
+      for (int n = 0; n < 4; ++n) {
+        const int a = n & 1, b = n >> 1;
+        v1[4 * q + n] = lag1(a, p[0]) * lag1(b, p[1]);
+        const double r0 = dlag1(a, p[0]) * lag1(b, p[1]), r1 = lag1(a, p[0]) * dlag1(b, p[1]);
+        for (int i = 0; i < 2; ++i) g1[4 * q + n][i] = r0 * Ji[0][i] + r1 * Ji[1][i];
+      }
+    }
+  }
+};
+
+// local dof -> (component 0, 1 velocity / 2 pressure, lexicographic point or vertex)
+SysDof sysdof2d(int i) {
+  if (i < 12) return {i % 3, i % 3 == 2 ? i / 3 : kHier2Lex2D[i / 3]};
+  if (i < 20) return {(i - 12) % 2, kHier2Lex2D[4 + (i - 12) / 2]};
+  return {i - 20, 4};
+}
+
+double T2_value(const CellValues2D& cv, int deg, int q, int k) {
+  return deg == 1 ? cv.v1[4 * q + k] : cv.v2[9 * q + kHier2Lex2D[k]];
+}
+const Vec2& T2_grad(const CellValues2D& cv, int deg, int q, int k) {
+  return deg == 1 ? cv.g1[4 * q + k] : cv.g2[9 * q + kHier2Lex2D[k]];
+}
+int T2_dofs_per_cell(int deg) { return deg == 1 ? 4 : 9; }
+
+}  // namespace
+
+extern "C" void orc2d_cell_nse_system(const orc_physics* ph, const double* geom16,
+                                      const double* u_local, const double* T_local, double* K,
+                                      double* f) {
+  // boussinesq_model.tpp:550-673 at dim = 2; QGauss(3)
+  CellValues2D cv;
+  cv.reinit(geom16, 3);
+  const int tdeg = ph->temperature_degree, ntd = T2_dofs_per_cell(tdeg);
+  std::fill(K, K + 22 * 22, 0.0);
+  std::fill(f, f + 22, 0.0);
+  Vec2 phi_u[22];
+  double grad[22][2][2], eps[22][2][2], div[22], phi_p[22];
+  for (int q = 0; q < cv.nq; ++q) {
+    for (int k = 0; k < 22; ++k) {
+      const SysDof s = sysdof2d(k);
+      phi_u[k] = Vec2();
+      std::memset(grad[k], 0, sizeof(grad[k]));
+      div[k] = phi_p[k] = 0;
+      if (s.comp < 2) {
+        const Vec2& g = cv.g2[9 * q + s.idx];
+        phi_u[k][s.comp] = cv.v2[9 * q + s.idx];
+        for (int d = 0; d < 2; ++d) grad[k][s.comp][d] = g[d];
+        div[k] = g[s.comp];
+      } else {
+        phi_p[k] = cv.v1[4 * q + s.idx];
+      }
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) eps[k][a][b] = 0.5 * (grad[k][a][b] + grad[k][b][a]);
+    }
+    double old_T = 0;
+    for (int k = 0; k < ntd; ++k) old_T += T_local[k] * T2_value(cv, tdeg, q, k);
+    Vec2 u;
+    double G[2][2] = {{0, 0}, {0, 0}};
+    for (int k = 0; k < 22; ++k) {
+      const SysDof s = sysdof2d(k);
+      if (s.comp == 2) continue;
+      u[s.comp] += u_local[k] * phi_u[k][s.comp];
+      for (int d = 0; d < 2; ++d) G[s.comp][d] += u_local[k] * grad[k][s.comp][d];
+    }
+    const double rho = 1 - ph->expansion_coefficient * (old_T - ph->temperature_ref);
+    Vec2 adv;  // (u . grad) u
+    for (int j = 0; j < 2; ++j)
+      for (int i = 0; i < 2; ++i) adv[j] += u[i] * G[j][i];
+    const double JxW = cv.JxW[q], dt = ph->time_step;
+    for (int i = 0; i < 22; ++i)
+      for (int j = 0; j < 22; ++j) {
+        double ee = 0;
+        for (int a = 0; a < 2; ++a)
+          for (int b = 0; b < 2; ++b) ee += eps[i][a][b] * eps[j][a][b];
+        K[22 * i + j] += (dot2(phi_u[i], phi_u[j]) + dt * (ph->one_over_reynolds * 2 * ee) -
+                          div[i] * phi_p[j] - phi_p[i] * div[j]) *
+                         JxW;
+      }
+    // gravity: vertical on the cuboid, gravity_vector (Q4) on the shell
+    Vec2 grav;
+    const Vec2& x = cv.xq[q];
+    if (ph->cuboid) {
+      grav[1] = -ph->gravity_constant;
+    } else {
+      const double r = std::sqrt(dot2(x, x));
+      for (int d = 0; d < 2; ++d)
+        grav[d] = (r > 1) ? -ph->gravity_constant * x[d] / r : -ph->gravity_constant * x[d] / std::sqrt(r);
+    }
+    for (int d = 0; d < 2; ++d) grav[d] *= ph->gravity_scale;
+    // cross_product_2d(u) = (u_y, -u_x); the 2D Coriolis term (Q3)
+    Vec2 cu;
+    cu[0] = u[1];
+    cu[1] = -u[0];
+    for (int i = 0; i < 22; ++i)
+      f[i] += (dot2(phi_u[i], u) + dt * rho * dot2(grav, phi_u[i]) - dt * dot2(phi_u[i], adv) -
+               dt * (-2 * dot2(phi_u[i], cu))) *
+              JxW;
+  }
+}
+
+extern "C" void orc2d_cell_nse_preconditioner(const orc_physics* ph, const double* geom16,
+                                              double* P) {
+  // boussinesq_model.tpp:421-464 at dim = 2
+  CellValues2D cv;
+  cv.reinit(geom16, 3);
+  std::fill(P, P + 22 * 22, 0.0);
+  for (int q = 0; q < cv.nq; ++q) {
+    Vec2 phi_u[22];
+    double grad[22][2][2] = {}, phi_p[22] = {};
+    for (int k = 0; k < 22; ++k) {
+      const SysDof s = sysdof2d(k);
+      if (s.comp < 2) {
+        phi_u[k][s.comp] = cv.v2[9 * q + s.idx];
+        for (int d = 0; d < 2; ++d) grad[k][s.comp][d] = cv.g2[9 * q + s.idx][d];
+      } else {
+        phi_p[k] = cv.v1[4 * q + s.idx];
+      }
+    }
+    for (int i = 0; i < 22; ++i)
+      for (int j = 0; j < 22; ++j) {
+        double gg = 0;
+        for (int a = 0; a < 2; ++a)
+          for (int b = 0; b < 2; ++b) gg += grad[i][a][b] * grad[j][a][b];
+        P[22 * i + j] += (dot2(phi_u[i], phi_u[j]) + ph->time_step * ph->one_over_reynolds * gg +
+                          phi_p[i] * phi_p[j]) *
+                         cv.JxW[q];
+      }
+  }
+}
+
+extern "C" void orc2d_cell_temperature_matrix(const orc_physics* ph, const double* geom16,
+                                              double* M, double* Kt) {
+  const int tdeg = ph->temperature_degree, n = T2_dofs_per_cell(tdeg);
+  CellValues2D cv;
+  cv.reinit(geom16, tdeg + 2);
+  std::fill(M, M + n * n, 0.0);
+  std::fill(Kt, Kt + n * n, 0.0);
+  for (int q = 0; q < cv.nq; ++q)
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        M[n * i + j] += T2_value(cv, tdeg, q, i) * T2_value(cv, tdeg, q, j) * cv.JxW[q];
+        Kt[n * i + j] += dot2(T2_grad(cv, tdeg, q, i), T2_grad(cv, tdeg, q, j)) *
+                         ph->one_over_peclet * cv.JxW[q];
+      }
+}
+
+extern "C" void orc2d_cell_temperature_rhs(const orc_physics* ph, const double* geom16,
+                                           const double* T_local, const double* u_local,
+                                           const int* inhom_mask, double* rhs, double* mfbc) {
+  const int tdeg = ph->temperature_degree, n = T2_dofs_per_cell(tdeg);
+  CellValues2D cv;
+  cv.reinit(geom16, tdeg + 2);
+  std::fill(rhs, rhs + n, 0.0);
+  std::fill(mfbc, mfbc + n * n, 0.0);
+  const double dt_eff = ph->time_step / ph->nse_solver_interval;
+  for (int q = 0; q < cv.nq; ++q) {
+    double T = 0;
+    Vec2 gT, u;
+    for (int k = 0; k < n; ++k) {
+      T += T_local[k] * T2_value(cv, tdeg, q, k);
+      const Vec2& g = T2_grad(cv, tdeg, q, k);
+      for (int d = 0; d < 2; ++d) gT[d] += T_local[k] * g[d];
+    }
+    for (int k = 0; k < 22; ++k) {
+      const SysDof s = sysdof2d(k);
+      if (s.comp < 2) u[s.comp] += u_local[k] * cv.v2[9 * q + s.idx];
+    }
+    const double JxW = cv.JxW[q];
+    for (int i = 0; i < n; ++i) {
+      const double phi_i = T2_value(cv, tdeg, q, i);
+      rhs[i] += (phi_i * T - dt_eff * phi_i * dot2(u, gT)) * JxW;
+      if (inhom_mask[i])
+        for (int j = 0; j < n; ++j)
+          mfbc[n * j + i] += (phi_i * T2_value(cv, tdeg, q, j) +
+                              dt_eff * ph->one_over_peclet *
+                                  dot2(T2_grad(cv, tdeg, q, i), T2_grad(cv, tdeg, q, j))) *
+                             JxW;
+    }
+  }
+}
+
+extern "C" orc_model* orc2d_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
+                                   const int* cell_T_dofs, const double* cell_geom, int n_u,
+                                   int n_p, int n_T, const orc_constraints* nse_c,
+                                   const orc_constraints* T_c) {
+  auto m = new orc_model();
+  m->dim = 2;
+  m->ph = *ph;
+  m->n_cells = n_cells;
+  m->n_u = n_u;
+  m->n_p = n_p;
+  m->n_T = n_T;
+  m->tdeg = ph->temperature_degree;
+  m->tdpc = T2_dofs_per_cell(m->tdeg);
+  m->cell_nse.assign(cell_nse_dofs, cell_nse_dofs + size_t(n_cells) * 22);
+  m->cell_T.assign(cell_T_dofs, cell_T_dofs + size_t(n_cells) * m->tdpc);
+  m->geom.assign(cell_geom, cell_geom + size_t(n_cells) * 32);
+  m->cnse.init(n_u + n_p, nse_c);
+  m->cT.init(n_T, T_c);
+  make_pattern(m->nse, n_u + n_p, n_cells, 22, m->cell_nse.data(), m->cnse,
+               [](int i, int j) { return !(sysdof2d(i).comp == 2 && sysdof2d(j).comp == 2); });
+  m->nse_rhs.assign(n_u + n_p, 0.0);
+  make_pattern(m->Tmass, n_T, n_cells, m->tdpc, m->cell_T.data(), m->cT, [](int, int) { return true; });
+  m->Tstiff = m->Tmass;
+  m->Tmat = m->Tmass;
+  m->T_rhs.assign(n_T, 0.0);
+  m->tmp1.assign(n_u, 0.0);
+  m->tmp2.assign(n_u, 0.0);
+  return m;
+}
+
+void orc2d_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T) {
+  m->nse.zero();
+  std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
+  std::vector<double> K(22 * 22), f(22), ul(22), Tl(9);
+  for (int c = 0; c < m->n_cells; ++c) {
+    gather(m->cell_nse, c, 22, old_nse, ul.data());
+    gather(m->cell_T, c, m->tdpc, old_T, Tl.data());
+    orc2d_cell_nse_system(&m->ph, &m->geom[32 * size_t(c)], ul.data(), Tl.data(), K.data(), f.data());
+    distribute_local_to_global(m->cnse, 22, &m->cell_nse[22 * size_t(c)], K.data(), f.data(),
+                               &m->nse, m->nse_rhs.data());
+  }
+}
+
+void orc2d_assemble_temperature_matrix(orc_model* m) {
+  m->Tmass.zero();
+  m->Tstiff.zero();
+  const int n = m->tdpc;
+  std::vector<double> M(n * n), K(n * n);
+  for (int c = 0; c < m->n_cells; ++c) {
+    orc2d_cell_temperature_matrix(&m->ph, &m->geom[32 * size_t(c)], M.data(), K.data());
+    const int* d = &m->cell_T[size_t(n) * c];
+    distribute_local_to_global(m->cT, n, d, M.data(), nullptr, &m->Tmass, nullptr);
+    distribute_local_to_global(m->cT, n, d, K.data(), nullptr, &m->Tstiff, nullptr);
+  }
+}
+
+void orc2d_assemble_temperature_rhs(orc_model* m, const double* old_T, const double* nse_solution) {
+  const int n = m->tdpc;
+  std::vector<double> Tl(n), ul(22), rhs(n), mfbc(n * n);
+  std::vector<int> mask(n);
+  for (int c = 0; c < m->n_cells; ++c) {
+    const int* d = &m->cell_T[size_t(n) * c];
+    gather(m->cell_T, c, n, old_T, Tl.data());
+    gather(m->cell_nse, c, 22, nse_solution, ul.data());
+    for (int i = 0; i < n; ++i)
+      mask[i] = m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0;
+    orc2d_cell_temperature_rhs(&m->ph, &m->geom[32 * size_t(c)], Tl.data(), ul.data(), mask.data(),
+                               rhs.data(), mfbc.data());
+    distribute_rhs_with_bc(m->cT, n, d, rhs.data(), mfbc.data(), m->T_rhs.data());
+  }
+}
+
+// get_maximal_velocity / get_cfl_number (:1023-1101) at dim = 2: the 9 Q2
+// support points (QIterated<QTrapez>(2)); diam == null: the maximal velocity
+double orc2d_max_velocity(const orc_model* m, const double* sol, const double* diam) {
+  double out = 0;
+  for (int c = 0; c < m->n_cells; ++c) {
+    double mx = diam ? 1e-10 : 0.0;
+    for (int t = 0; t < 9; ++t) {
+      const int* d = &m->cell_nse[22 * size_t(c) + (t < 4 ? 3 * t : 12 + 2 * (t - 4))];
+      mx = std::max(mx, std::sqrt(sol[d[0]] * sol[d[0]] + sol[d[1]] * sol[d[1]]));
+    }
+    out = std::max(out, diam ? mx / diam[c] : mx);
+  }
+  return out;
 }

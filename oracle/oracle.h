@@ -73,6 +73,20 @@ void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom64,
 
 /* ---- global model ------------------------------------------------------- */
 typedef struct orc_model orc_model;
+/* Standard::BoussinesqModel<2>: element level (22 NSE dofs, 16 support points
+ * per cell as [16][2]) and a 2D model whose other orc_* calls (schur solver,
+ * temperature solve, exports, cfl) work as for the 3D one. */
+void orc2d_cell_nse_system(const orc_physics* ph, const double* geom16, const double* u_local,
+                           const double* T_local, double* K, double* f);
+void orc2d_cell_nse_preconditioner(const orc_physics* ph, const double* geom16, double* P);
+void orc2d_cell_temperature_matrix(const orc_physics* ph, const double* geom16, double* M,
+                                   double* Kt);
+void orc2d_cell_temperature_rhs(const orc_physics* ph, const double* geom16,
+                                const double* T_local, const double* u_local,
+                                const int* inhom_mask, double* rhs, double* mfbc);
+orc_model* orc2d_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
+                        const int* cell_T_dofs, const double* cell_geom, int n_u, int n_p,
+                        int n_T, const orc_constraints* nse_c, const orc_constraints* T_c);
 
 orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs /*89*/,
                       const int* cell_T_dofs, const double* cell_geom /*64x3*/, int n_u,

@@ -96,6 +96,12 @@ def lib():
         L.orc_feec_solve_nse.argtypes = [P, P, P]
         L.orc_feec_solve_temperature.argtypes = [P, P, P]
         L.orc_feec_velocity_stats.argtypes = [P, P, P]
+        L.orc2d_cell_nse_system.argtypes = [P, P, P, P, P, P]
+        L.orc2d_cell_nse_preconditioner.argtypes = [P, P, P]
+        L.orc2d_cell_temperature_matrix.argtypes = [P, P, P, P]
+        L.orc2d_cell_temperature_rhs.argtypes = [P, P, P, P, P, P, P]
+        L.orc2d_create.argtypes = [P, I, P, P, P, I, I, I, P, P]
+        L.orc2d_create.restype = P
         _lib = L
     return _lib
 
@@ -129,11 +135,35 @@ def cell_nse_preconditioner(ph, geom64):
     return P
 
 
+def cell_nse_system_2d(ph, geom16, u_local, T_local):
+    """local_assemble_nse_system at dim = 2: K [22][22], f [22]."""
+    K = np.zeros((22, 22))
+    f = np.zeros(22)
+    o = physics(ph)
+    lib().orc2d_cell_nse_system(C.byref(o), _p(np.ascontiguousarray(geom16, np.float64)),
+                                _p(np.ascontiguousarray(u_local, np.float64)),
+                                _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
+    return K, f
+
+
+def cell_temperature_matrix_2d(ph, geom16):
+    n = (ph.temperature_degree + 1) ** 2
+    M, K = np.zeros((n, n)), np.zeros((n, n))
+    o = physics(ph)
+    lib().orc2d_cell_temperature_matrix(C.byref(o), _p(np.ascontiguousarray(geom16, np.float64)),
+                                        _p(M), _p(K))
+    return M, K
+
+
 class Model:
-    """Global oracle model over a dcp.HostMesh."""
+    """Global oracle model over a dcp.HostMesh (or a dcp.HostMesh2D: the 2D
+    model, orc2d_create)."""
 
     def __init__(self, ph, mesh):
         self.ph = physics(ph)
+        self.dim = getattr(mesh, "dim", 3)
+        if self.dim == 2:
+            self.ph.temperature_degree = mesh.temperature_degree
         self.mesh = mesh
         self._keep = []
 
@@ -148,9 +178,9 @@ class Model:
         self._cd = np.ascontiguousarray(mesh.cell_nse_dofs, np.int32)
         self._td = np.ascontiguousarray(mesh.cell_T_dofs, np.int32)
         self._g = np.ascontiguousarray(mesh.cell_geometry, np.float64)
-        self.h = lib().orc_create(C.byref(self.ph), mesh.n_cells, _p(self._cd), _p(self._td),
-                                  _p(self._g), mesh.n_u, mesh.n_p, mesh.n_T,
-                                  C.byref(self._nc), C.byref(self._tc))
+        create = lib().orc2d_create if self.dim == 2 else lib().orc_create
+        self.h = create(C.byref(self.ph), mesh.n_cells, _p(self._cd), _p(self._td), _p(self._g),
+                        mesh.n_u, mesh.n_p, mesh.n_T, C.byref(self._nc), C.byref(self._tc))
 
     def __del__(self):
         if getattr(self, "h", None):
