@@ -169,10 +169,16 @@ void velocity_stats_global(Ctx& c) {
 void need_ready(Ctx& c) {
   require(c.have_physics, DCP_ERR_STATE, "dcp_set_physics has not been called");
   require(c.have_mesh, DCP_ERR_STATE, "dcp_mesh_upload has not been called");
+  const int mesh_deg = c.dim2 ? (c.m2_tdpc == 9 ? 2 : 1) : (c.tdpc3 == 27 ? 2 : 1);
+  require(!c.feec || c.hph.temperature_degree == 1, DCP_ERR_UNSUPPORTED,
+          "the FEEC device temperature path implements FE_Q(1)");
+  require(c.feec || c.hph.temperature_degree == mesh_deg, DCP_ERR_INVALID,
+          "physics temperature degree differs from the uploaded mesh's");
 }
 
 struct HostPrep {
   int nv = 0;
+  int tdpc = 8;  // temperature dofs per cell: 8 (FE_Q(1)) or 27 (FE_Q(2), stored lexicographic)
   std::vector<int32_t> q2, pd, td;
   std::vector<double> geo;  // [n_cells][64][3] MappingQ(3) support points
   std::vector<NodeConstraint> vc;
@@ -203,12 +209,18 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
           "invalid sizes");
   const int nv = n_u / 3;
   h.nv = nv;
+  // FE_Q(2) temperature: one dof per velocity support point (n_T = n_u / 3),
+  // FE_Q(1): one per vertex (n_T = n_p)
+  const int tdpc = (n_T == nv && n_T != n_p) ? 27 : 8;
+  require(tdpc == 27 || n_T == n_p, DCP_ERR_INVALID,
+          "n_T must be the vertex count (FE_Q(1)) or the Q2 support-point count (FE_Q(2))");
+  h.tdpc = tdpc;
   auto& q2 = h.q2;
   auto& pd = h.pd;
   auto& td = h.td;
   q2.assign(size_t(n_cells) * 27, 0);
   pd.assign(size_t(n_cells) * 8, 0);
-  td.assign(size_t(n_cells) * 8, 0);
+  td.assign(size_t(n_cells) * tdpc, 0);
   h.geo.assign(cell_geometry, cell_geometry + size_t(n_cells) * 3 * kMapPts);
   for (double x : h.geo) require(std::isfinite(x), DCP_ERR_INVALID, "non-finite cell geometry");
   std::vector<char> seen(nv, 0);
@@ -233,10 +245,11 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
         pd[size_t(cell) * 8 + s.lex] = d[i] - n_u;
       }
     }
-    for (int v = 0; v < 8; ++v) {
-      const int t = cell_T_dofs[size_t(cell) * 8 + v];
+    for (int v = 0; v < tdpc; ++v) {
+      const int t = cell_T_dofs[size_t(cell) * tdpc + v];
       require(t >= 0 && t < n_T, DCP_ERR_INVALID, "temperature dof out of range");
-      td[size_t(cell) * 8 + v] = t;
+      // FE_Q(2): hierarchic local order -> lexicographic (the kernels' order)
+      td[size_t(cell) * tdpc + (tdpc == 27 ? kQ2HierToLex[v] : v)] = t;
     }
   }
   for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
@@ -385,6 +398,8 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   for (int t = 0; t < n_T; ++t)
     require(h.tmaster[t] < 0 || (h.tmaster[h.tmaster[t]] < 0 && !h.Tfix[h.tmaster[t]]),
             DCP_ERR_UNSUPPORTED, "periodic temperature chain not closed");
+  require(tdpc == 8 || h.n_tslave == 0, DCP_ERR_UNSUPPORTED,
+          "periodic FE_Q(2) temperature is not supported");
   // identified cell maps (the originals kept for the constrained diagonals)
   if (h.n_vslave || h.n_pslave || h.n_tslave) {
     h.q2o = q2;
@@ -440,7 +455,7 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   union_pattern(nv, n_cells, q2.data(), 27, q2.data(), 27, h.Ap, h.Ac);
   union_pattern(nv, n_cells, q2.data(), 27, pd.data(), 8, h.Btp, h.Btc);
   union_pattern(n_p, n_cells, pd.data(), 8, q2.data(), 27, h.Bp, h.Bc);
-  union_pattern(n_T, n_cells, td.data(), 8, td.data(), 8, h.Tp, h.Tc);
+  union_pattern(n_T, n_cells, td.data(), tdpc, td.data(), tdpc, h.Tp, h.Tc);
   auto add_diagonals = [](std::vector<int32_t>& ptr, std::vector<int32_t>& col,
                           const std::vector<int32_t>& master) {
     std::vector<int32_t> np(ptr.size(), 0), nc;
@@ -1131,8 +1146,8 @@ void dcp_ctx_destroy(dcp_ctx* ctx) {
 int dcp_set_physics(dcp_ctx* ctx, const dcp_physics* ph) {
   return guarded(ctx, [&] {
     require(ctx && ph, DCP_ERR_INVALID, "NULL argument");
-    require(ph->temperature_degree == 1, DCP_ERR_UNSUPPORTED,
-            "device temperature path implements FE_Q(1) (classic shell configuration)");
+    require(ph->temperature_degree == 1 || ph->temperature_degree == 2, DCP_ERR_UNSUPPORTED,
+            "temperature degree must be 1 or 2");
     require(ph->nse_solver_interval >= 1, DCP_ERR_INVALID, "NSE solver interval must be >= 1");
     ctx->hph = *ph;
     set_physics_dev(*ctx);
@@ -1275,6 +1290,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.feec = false;
     c.dim2 = false;
     c.vdim = 3;
+    c.tdpc3 = h.tdpc;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -1356,7 +1372,7 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     c.posA.alloc(size_t(n_cells) * 729);
     c.posBt.alloc(size_t(n_cells) * 216);
     c.posB.alloc(size_t(n_cells) * 216);
-    c.posT.alloc(size_t(n_cells) * 64);
+    c.posT.alloc(size_t(n_cells) * h.tdpc * h.tdpc);
     launch_build_scatter_maps(c.cd(), c.A_ptr.p, c.A_col.p, c.Bt_ptr.p, c.Bt_col.p, c.B_ptr.p,
                               c.B_col.p, c.T_ptr.p, c.T_col.p, c.posA.p, c.posBt.p, c.posB.p,
                               c.posT.p, c.stream);
@@ -2372,6 +2388,7 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     c.feec = true;
     c.dim2 = false;
     c.vdim = 3;
+    c.tdpc3 = 8;
     c.have_mesh = false;
     c.n_cells = nc;
     c.n_owned_cells = dist ? L.n_owned_cells : nc;

@@ -114,6 +114,7 @@ struct Ctx {
   int sell_part_len = 0;             // common length of the SELL partial arrays
   // mesh
   DBuf<int32_t> cell_q2, cell_p, cell_T;
+  int tdpc3 = 8;                      // temperature dofs per 3D cell: 8 (FE_Q(1)) or 27 (FE_Q(2))
   DBuf<double> cell_geo, diameter, T_bc;
   DBuf<NodeConstraint> vcon;
   DBuf<uint8_t> T_fixed;
@@ -359,6 +360,7 @@ struct Ctx {
     c.cell_q2 = cell_q2.p;
     c.cell_p = cell_p.p;
     c.cell_T = cell_T.p;
+    c.tdpc = tdpc3;
     c.geo = cell_geo.p;
     c.vcon = vcon.p;
     c.T_fixed = T_fixed.p;

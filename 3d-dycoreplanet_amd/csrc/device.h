@@ -52,14 +52,15 @@ struct ScatterMaps {
   const int32_t* posA;   // [n_cells][27*27]  A block index of (a, b)
   const int32_t* posBt;  // [n_cells][27*8]   Bt entry of (a, v)
   const int32_t* posB;   // [n_cells][8*27]   B entry of (v, a)
-  const int32_t* posT;   // [n_cells][8*8]    T CSR entry of (i, j)
+  const int32_t* posT;   // [n_cells][tdpc*tdpc] T CSR entry of (i, j)
 };
 
 struct CellData {
   int n_cells;
   const int32_t* cell_q2;   // [n_cells][27] vnode ids (lexicographic)
   const int32_t* cell_p;    // [n_cells][8]  pressure dofs (vertex order)
-  const int32_t* cell_T;    // [n_cells][8]  temperature dofs
+  const int32_t* cell_T;    // [n_cells][tdpc] temperature dofs (FE_Q(2): lexicographic)
+  int tdpc;                 // 8 (FE_Q(1)) or 27 (FE_Q(2)) temperature dofs per cell
   const double* geo;        // [n_cells][64][3] MappingQ(3) support points (fe_tables.h)
   const NodeConstraint* vcon;  // [n_vnodes]
   const uint8_t* T_fixed;   // [n_T] 1 = Dirichlet
@@ -246,6 +247,12 @@ void launch_T_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* c
 // A(s,s) block of every identified velocity node s = diag(cdiag of s)
 void image_diagonal_blocks(int n, const int32_t* node, const int64_t* blk, const int32_t* cidx,
                            const double* cdiag, double* A_val, hipStream_t s);
+// FE_Q(2) temperature (kernels/temperature_q2.hip); launch_T_matrix / launch_T_rhs
+// dispatch to these when cd.tdpc == 27
+void launch_T2_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
+                      const PhysicsDev& ph, double* Tmass, double* Tstiff, hipStream_t s);
+void launch_T2_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
+                   const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
 void launch_T_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
                   const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
 // Builds posA/posBt/posB/posT by binary search in the sorted patterns.

@@ -15,9 +15,9 @@
 namespace {
 
 // recompute_time_step (boussinesq_model.tpp:1104-1125; FEEC.tpp:1241-1261):
-// step-32's CFL rule in 3D, scaling 1/4
+// step-32's CFL rule, scaling 1/4, with the model's dimension
 double recomputed_time_step(const dcp_run_params* rp, double cfl) {
-  const double dim = 3.0;
+  const double dim = rp->space_dimension == 2 ? 2.0 : 3.0;
   const double scaling = 0.25;
   const int deg = std::max(rp->physics.temperature_degree, rp->nse_velocity_degree);
   return (scaling / (2.1 * dim * std::sqrt(dim))) / (double(deg) * cfl);

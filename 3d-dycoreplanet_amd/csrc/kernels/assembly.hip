@@ -267,7 +267,7 @@ constexpr int kRhsLane0 = 160;               // wave 2 lanes 32..58: rhs nodes
 constexpr int kStageA = 405 * 9;
 constexpr int kStageDoubles = kStageA + 216 * 3;
 struct NseSmem {
-  double X[3 * kMapPts], U[81], T[8];
+  double X[3 * kMapPts], U[81], T[27];  // T: 8 vertex (FE_Q(1)) or 27 lexicographic (FE_Q(2)) values
   Geo geo;
   double D[27 * 27 * 3];   // [q][n][d] reference, then physical gradients
   double S[27 * 27];       // [q][n] shape values
@@ -550,7 +550,9 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
   } else if (tid >= 64 && tid < 72) {
     const int v = tid - 64;
     sh.pdof[v] = cd.cell_p[8 * size_t(cell) + v];
-    sh.T[v] = T_old[(cd.cell_To ? cd.cell_To : cd.cell_T)[8 * size_t(cell) + v]];
+    if (cd.tdpc == 8) sh.T[v] = T_old[(cd.cell_To ? cd.cell_To : cd.cell_T)[8 * size_t(cell) + v]];
+  } else if (cd.tdpc == 27 && tid >= 96 && tid < 123) {
+    sh.T[tid - 96] = T_old[cd.cell_T[27 * size_t(cell) + tid - 96]];
   }
   if (MODE == 0 && want_matrix)
     for (int i = tid; i < 729; i += kNseThreads) sh.pos[i] = sm.posA[729 * size_t(cell) + i];
@@ -656,8 +658,13 @@ __global__ __launch_bounds__(kNseThreads) void k_nse_system(CellData cd, Scatter
       }
     }
     double T = 0;
+    if (cd.tdpc == 8) {
 #pragma unroll
-    for (int v = 0; v < 8; ++v) T += sh.T[v] * cRef.S1[8 * q + v];
+      for (int v = 0; v < 8; ++v) T += sh.T[v] * cRef.S1[8 * q + v];
+    } else {
+      // FE_Q(2) temperature: the Q2 basis of the velocity at the same points
+      for (int n = 0; n < 27; ++n) T += sh.T[n] * sh.S[27 * q + n];
+    }
     const double rho = 1 - ph.beta * (T - ph.T_ref);            // density_scaling
     double grav[3];
     if (ph.cuboid) {
@@ -1222,7 +1229,8 @@ __global__ void k_scatter_maps(CellData cd, const int32_t* A_ptr, const int32_t*
   const int cell = blockIdx.x;
   const int32_t* nodes = cd.cell_q2 + 27 * size_t(cell);
   const int32_t* pd = cd.cell_p + 8 * size_t(cell);
-  const int32_t* td = cd.cell_T + 8 * size_t(cell);
+  const int tp = cd.tdpc;
+  const int32_t* td = cd.cell_T + tp * size_t(cell);
   for (int i = threadIdx.x; i < 729; i += blockDim.x) {
     const int ra = nodes[i / 27], cb = nodes[i % 27];
     posA[729 * size_t(cell) + i] = find_sorted(A_col, A_ptr[ra], A_ptr[ra + 1], cb);
@@ -1233,9 +1241,9 @@ __global__ void k_scatter_maps(CellData cd, const int32_t* A_ptr, const int32_t*
     const int rv = pd[i / 27], cn = nodes[i % 27];
     posB[216 * size_t(cell) + i] = find_sorted(B_col, B_ptr[rv], B_ptr[rv + 1], cn);
   }
-  for (int i = threadIdx.x; i < 64; i += blockDim.x) {
-    const int r = td[i / 8], c = td[i % 8];
-    posT[64 * size_t(cell) + i] = find_sorted(T_col, T_ptr[r], T_ptr[r + 1], c);
+  for (int i = threadIdx.x; i < tp * tp; i += blockDim.x) {
+    const int r = td[i / tp], c = td[i % tp];
+    posT[size_t(tp) * tp * cell + i] = find_sorted(T_col, T_ptr[r], T_ptr[r + 1], c);
   }
 }
 
@@ -1405,6 +1413,7 @@ void launch_T_matrix(const CellData& cd, const ScatterMaps& sm, const int32_t* c
                      const PhysicsDev& ph, double* Tmass, double* Tstiff, const int32_t* posTs,
                      hipStream_t s) {
   if (n <= 0) return;
+  if (cd.tdpc == 27) return launch_T2_matrix(cd, sm, cells, n, ph, Tmass, Tstiff, s);
   hipLaunchKernelGGL(k_T_matrix, dim3(n), dim3(64), 0, s, cd, sm, cells, ph, Tmass, Tstiff, posTs);
   DCP_HIP_CHECK(hipGetLastError());
 }
@@ -1420,6 +1429,7 @@ void image_diagonal_blocks(int n, const int32_t* node, const int64_t* blk, const
 void launch_T_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
                   const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s) {
   if (n <= 0) return;
+  if (cd.tdpc == 27) return launch_T2_rhs(cd, cells, n, T_old, u_cur, ph, rhs, s);
   hipLaunchKernelGGL(k_T_rhs, dim3(n), dim3(64), 0, s, cd, cells, T_old, u_cur, ph, rhs);
   DCP_HIP_CHECK(hipGetLastError());
 }

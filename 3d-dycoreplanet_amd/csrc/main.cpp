@@ -132,19 +132,37 @@ int main(int argc, char** argv) {
     return 1;
   }
   if (refine >= 0) rp.initial_global_refinement = refine;
-  if (rp.space_dimension != 3) {
-    std::fprintf(stderr, "Error: only the 3D models run on the device path\n");
+  if (rp.space_dimension != 2 && rp.space_dimension != 3) {
+    std::fprintf(stderr, "Error: space dimension must be 2 or 3\n");
     return 1;
   }
+  const bool two_d = rp.space_dimension == 2;
   const bool feec = rp.use_FEEC_solver != 0;
-  dcp_host_mesh* m = dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0,
-                                          rp.R1, rp.length, rp.physics.temperature_degree, 0, 0);
+  if (two_d && (feec || rp.physics.cuboid)) {
+    std::fprintf(stderr, "Error: the 2D model runs the classic solver on the shell\n");
+    return 1;
+  }
+  // Standard::BoussinesqModel<2> / <3> (boussinesq_model.inst.cc)
+  dcp_host_mesh* m =
+      two_d ? dcp_host_mesh2d_create(rp.initial_global_refinement, rp.R0, rp.R1, rp.length,
+                                     rp.physics.temperature_degree, 0)
+            : dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0, rp.R1,
+                                   rp.length, rp.physics.temperature_degree, 0, 0);
   if (!m) return fail("mesh", nullptr);
   // setup_dofs (:198-204): Cuthill_McKee before component_wise for the Schur solver
   if (!feec && rp.use_schur_complement_solver && dcp_host_mesh_renumber_cuthill_mckee(m) != DCP_OK)
     return fail("renumbering", nullptr);
   dcp_host_mesh_view v{};
-  dcp_host_mesh_view_get(m, &v);
+  dcp_mesh2d v2{};
+  if (two_d) {
+    dcp_host_mesh2d_view_get(m, &v2, nullptr, nullptr);
+    v.n_cells = v2.n_cells;
+    v.n_u = v2.n_u;
+    v.n_p = v2.n_p;
+    v.n_T = v2.n_T;
+  } else {
+    dcp_host_mesh_view_get(m, &v);
+  }
   dcp_config cfg{device, 0, 1, nullptr, nullptr};
   dcp_ctx* ctx = nullptr;
   if (dcp_ctx_create(&cfg, &ctx) != DCP_OK) return fail("context", nullptr);
@@ -152,7 +170,9 @@ int main(int argc, char** argv) {
   size_t n_nse = size_t(v.n_u) + size_t(v.n_p);
   dcp_feec_mesh fm{};
   if (rc == DCP_OK) {
-    if (feec) {
+    if (two_d) {
+      rc = dcp_mesh2d_upload(ctx, &v2);
+    } else if (feec) {
       rc = dcp_host_feec_view_get(m, &fm);
       if (rc == DCP_OK) rc = dcp_feec_mesh_upload(ctx, &fm);
       n_nse = size_t(fm.n_w) + size_t(fm.n_u) + size_t(fm.n_p);
@@ -176,8 +196,8 @@ int main(int argc, char** argv) {
   Output out;
   Output* outp = nullptr;
   if (!out_dir.empty()) {
-    if (feec) {
-      std::fprintf(stderr, "Error: --output writes the classic model's fields only\n");
+    if (feec || two_d) {
+      std::fprintf(stderr, "Error: --output writes the classic 3D model's fields only\n");
       return 1;
     }
     out.ctx = ctx;

@@ -91,6 +91,8 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
   if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("localize: bad rank/world");
   if (n_cells < world) throw std::runtime_error("localize: fewer cells than ranks");
   if (n_u <= 0 || n_u % 3 || n_p <= 0 || n_T <= 0) throw std::runtime_error("localize: bad sizes");
+  // FE_Q(2) temperature: n_T = the Q2 support points (27 dofs per cell), else vertices (8)
+  const int tdpc = (n_T == n_u / 3 && n_T != n_p) ? 27 : 8;
   Global g;
   g.n_cells = n_cells;
   g.n_u = n_u;
@@ -118,8 +120,8 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
         cnt[d - n_u + 1]++;
       }
     }
-    for (int v = 0; v < 8; ++v) {
-      const int t = cell_T_dofs[size_t(c) * 8 + v];
+    for (int v = 0; v < tdpc; ++v) {
+      const int t = cell_T_dofs[size_t(c) * tdpc + v];
       if (t < 0 || t >= n_T) throw std::runtime_error("localize: T dof out of range");
       if (g.Town[t] < 0) g.Town[t] = rc;
     }
@@ -150,7 +152,7 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
     }
   };
   auto Tdofs_of = [&](int c, auto&& emit) {
-    for (int v = 0; v < 8; ++v) emit(cell_T_dofs[size_t(c) * 8 + v]);
+    for (int v = 0; v < tdpc; ++v) emit(cell_T_dofs[size_t(c) * tdpc + v]);
   };
 
   LocalMesh L;
@@ -177,7 +179,7 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
   for (size_t i = 0; i < L.T_g.size(); ++i) Tl[L.T_g[i]] = int32_t(i);
   const int nu_loc = L.n_u();
   L.cell_nse_dofs.resize(size_t(L.n_cells) * 89);
-  L.cell_T_dofs.resize(size_t(L.n_cells) * 8);
+  L.cell_T_dofs.resize(size_t(L.n_cells) * tdpc);
   L.geometry.resize(size_t(L.n_cells) * 3 * kMapPts);
   L.diameter.resize(L.n_cells);
   for (int lc = 0; lc < L.n_cells; ++lc) {
@@ -187,7 +189,8 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
       L.cell_nse_dofs[size_t(lc) * 89 + k] =
           d < n_u ? 3 * vl[d / 3] + d % 3 : nu_loc + pl[d - n_u];
     }
-    for (int v = 0; v < 8; ++v) L.cell_T_dofs[size_t(lc) * 8 + v] = Tl[cell_T_dofs[size_t(c) * 8 + v]];
+    for (int v = 0; v < tdpc; ++v)
+      L.cell_T_dofs[size_t(lc) * tdpc + v] = Tl[cell_T_dofs[size_t(c) * tdpc + v]];
     std::copy(cell_geometry + size_t(c) * 3 * kMapPts, cell_geometry + size_t(c) * 3 * kMapPts + 3 * kMapPts,
               L.geometry.begin() + size_t(lc) * 3 * kMapPts);
     L.diameter[lc] = cell_diameter[c];

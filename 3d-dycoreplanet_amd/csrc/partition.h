@@ -45,7 +45,7 @@ struct LocalMesh {
   int nvo = 0, nvg = 0, npo = 0, npg = 0, nTo = 0, nTg = 0;
   std::vector<int32_t> cells_g;              // local cell -> global cell
   std::vector<int32_t> cell_nse_dofs;        // [n_cells][89], local numbering
-  std::vector<int32_t> cell_T_dofs;          // [n_cells][8]
+  std::vector<int32_t> cell_T_dofs;          // [n_cells][8 or 27] (FE_Q(1) / FE_Q(2))
   std::vector<double> geometry;              // [n_cells][64][3] (MappingQ(3) support points)
   std::vector<double> diameter;              // [n_cells]
   std::vector<int32_t> vnode_g, p_g, T_g;    // local -> global id per field

@@ -44,7 +44,7 @@ def csr(rp, cols, vals, n):
 def make(refine=2, tdeg=2, cm=True):
     m = dcp.HostMesh2D(refine=refine, R0=R0, R1=R1, length=L, temperature_degree=tdeg,
                        cuthill_mckee=cm)
-    ph = physics_2d()
+    ph = physics_2d(temperature_degree=tdeg)
     ctx = dcp.Context()
     ctx.set_physics(ph)
     ctx.upload_mesh2d(m)
