@@ -978,6 +978,34 @@ int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t*
   });
 }
 
+int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, int64_t* info,
+                            int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                            int32_t* recv_ptr, int64_t* recv_gid) {
+  return guarded(nullptr, [&] {
+    require(m && comm && info, DCP_ERR_INVALID, "NULL argument");
+    LocalMesh L;
+    try {
+      L = localize_distributed(*m, *comm);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+    HostPrep h;
+    prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
+                 L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc);
+    const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
+                           int64_t(L.hv.peers.size()), int64_t(L.hv.send_idx.size()),
+                           int64_t(L.hv.recv_idx.size()), int64_t(h.color_ptr.size()) - 1};
+    std::copy(v, v + 12, info);
+    if (peers) std::copy(L.hv.peers.begin(), L.hv.peers.end(), peers);
+    if (send_ptr) std::copy(L.hv.send_ptr.begin(), L.hv.send_ptr.end(), send_ptr);
+    if (recv_ptr) std::copy(L.hv.recv_ptr.begin(), L.hv.recv_ptr.end(), recv_ptr);
+    if (send_gid) std::copy(L.hv.send_gid.begin(), L.hv.send_gid.end(), send_gid);
+    if (recv_gid) std::copy(L.hv.recv_gid.begin(), L.hv.recv_gid.end(), recv_gid);
+    return DCP_OK;
+  });
+}
+
 int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int field,
                             int64_t* info, int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
                             int32_t* recv_ptr, int64_t* recv_gid) {
@@ -1201,6 +1229,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->element_mfma = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_SCHUR_FIXED_INNER) {
+      require(value >= 0, DCP_ERR_INVALID, "DCP_OPT_SCHUR_FIXED_INNER must be >= 0");
+      ctx->schur_fixed_inner = value;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_INNER_MAX_STEPS) {
       require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_INNER_MAX_STEPS must be >= 1");
       ctx->inner_max_steps = value;
@@ -1253,39 +1286,14 @@ int dcp_mesh_geometry_info(int n_cells, const double* cell_geometry, int* separa
   });
 }
 
-int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
-                    const int32_t* cell_T_dofs, const double* cell_geometry,
-                    const double* cell_diameter, int n_u, int n_p, int n_T,
-                    const dcp_constraints* nse_c, const dcp_constraints* T_c) {
-  return guarded(ctx, [&] {
-    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
-    Ctx& c = *ctx;
-    HostPrep h;
-    const bool dist = c.comm != nullptr;
-    LocalMesh L;
-    const int n_u_g = n_u, n_p_g = n_p, n_T_g = n_T;
-    if (dist) {
-      // this rank's cells + two ghost layers in local numbering (partition.h)
-      try {
-        L = localize(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
-                     n_T, nse_c, T_c, c.cfg.rank, c.cfg.world_size);
-      } catch (const std::runtime_error& e) {
-        fail(DCP_ERR_INVALID, e.what());
-      }
-      const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
-      n_cells = L.n_cells;
-      n_u = L.n_u();
-      n_p = L.n_p();
-      n_T = L.n_T();
-      cell_diameter = L.diameter.data();
-      prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
-                   cell_diameter, n_u, n_p, n_T, &lnc, &ltc);
-      require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
-              "periodic constraints on several GPUs are not supported");
-    } else {
-      prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u,
-                   n_p, n_T, nse_c, T_c);
-    }
+}  // extern "C"
+
+// The device half of a mesh upload (one GPU, or this rank's LocalMesh `L`
+// when dist): buffers, patterns, scatter maps, the explicit Schur complement
+// layout, the matrix-free tables, halos.
+void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_cells,
+                     const double* cell_diameter, int n_u, int n_p, int n_T, int n_u_g, int n_p_g,
+                     int n_T_g) {
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
     c.feec = false;
     c.dim2 = false;
@@ -1665,6 +1673,126 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     c.have_mesh = true;
     c.nse_assembled = c.precond_built = c.T_matrix_ok = c.T_rhs_ok = false;
+}
+
+extern "C" {
+
+int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
+                    const int32_t* cell_T_dofs, const double* cell_geometry,
+                    const double* cell_diameter, int n_u, int n_p, int n_T,
+                    const dcp_constraints* nse_c, const dcp_constraints* T_c) {
+  return guarded(ctx, [&] {
+    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
+    Ctx& c = *ctx;
+    HostPrep h;
+    const bool dist = c.comm != nullptr;
+    LocalMesh L;
+    const int n_u_g = n_u, n_p_g = n_p, n_T_g = n_T;
+    if (dist) {
+      // this rank's cells + two ghost layers in local numbering (partition.h)
+      try {
+        L = localize(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
+                     n_T, nse_c, T_c, c.cfg.rank, c.cfg.world_size);
+      } catch (const std::runtime_error& e) {
+        fail(DCP_ERR_INVALID, e.what());
+      }
+      const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+      n_cells = L.n_cells;
+      n_u = L.n_u();
+      n_p = L.n_p();
+      n_T = L.n_T();
+      cell_diameter = L.diameter.data();
+      prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
+                   cell_diameter, n_u, n_p, n_T, &lnc, &ltc);
+      require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
+              "periodic constraints on several GPUs are not supported");
+    } else {
+      prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u,
+                   n_p, n_T, nse_c, T_c);
+    }
+    upload_prepared(c, h, L, dist, n_cells, cell_diameter, n_u, n_p, n_T, n_u_g, n_p_g, n_T_g);
+    return DCP_OK;
+  });
+}
+
+int dcp_mesh_upload_distributed(dcp_ctx* ctx, const dcp_dist_mesh* m, const dcp_host_comm* comm) {
+  return guarded(ctx, [&] {
+    require(ctx && m && comm, DCP_ERR_INVALID, "NULL argument");
+    Ctx& c = *ctx;
+    require(comm->world == c.cfg.world_size && comm->rank == c.cfg.rank, DCP_ERR_INVALID,
+            "host communicator rank/world differ from the context's");
+    LocalMesh L;
+    try {
+      L = localize_distributed(*m, *comm);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+    HostPrep h;
+    prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
+                 L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc);
+    require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
+            "periodic constraints on several GPUs are not supported");
+    // one GPU (world 1): the caller's whole mesh, no halos
+    upload_prepared(c, h, L, c.comm != nullptr, L.n_cells, L.diameter.data(), L.n_u(), L.n_p(),
+                    L.n_T(), int(m->n_u), int(m->n_p), int(m->n_T));
+    return DCP_OK;
+  });
+}
+
+// the owned segments [offset, offset + count) of a state field's local vector
+static std::vector<std::pair<size_t, size_t>> owned_segments(const Ctx& c, int field) {
+  if (field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS)
+    return {{0, size_t(c.nTo)}};
+  if (c.feec)
+    return {{0, size_t(c.fe_nwo)}, {size_t(c.fe_nw), size_t(c.fe_nuo)},
+            {size_t(c.fe_nw + c.fe_nu), size_t(c.fe_npo)}};
+  return {{0, size_t(c.vdim) * c.nvo}, {size_t(c.n_u), size_t(c.npo)}};
+}
+
+int dcp_state_set_owned(dcp_ctx* ctx, int field, const double* host, size_t n) {
+  return guarded(ctx, [&] {
+    require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
+    Ctx& c = *ctx;
+    size_t want = 0;
+    double* p = field_ptr(c, field, want);
+    const auto segs = owned_segments(c, field);
+    size_t total = 0;
+    for (auto& sgm : segs) total += sgm.second;
+    require(n == total, DCP_ERR_INVALID, "owned state size mismatch");
+    size_t o = 0;
+    for (auto& sgm : segs) {
+      if (sgm.second)
+        DCP_HIP_CHECK(hipMemcpyAsync(p + sgm.first, host + o, sgm.second * sizeof(double),
+                                     hipMemcpyHostToDevice, c.stream));
+      o += sgm.second;
+    }
+    // ghost entries from their owners (the Trilinos ghosted copy)
+    const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
+    if (c.comm) halo_exchange(c, T ? c.halo_T : c.halo_nse, p);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    return DCP_OK;
+  });
+}
+
+int dcp_state_get_owned(dcp_ctx* ctx, int field, double* host, size_t n) {
+  return guarded(ctx, [&] {
+    require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
+    Ctx& c = *ctx;
+    size_t want = 0;
+    double* p = field_ptr(c, field, want);
+    const auto segs = owned_segments(c, field);
+    size_t total = 0;
+    for (auto& sgm : segs) total += sgm.second;
+    require(n == total, DCP_ERR_INVALID, "owned state size mismatch");
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    size_t o = 0;
+    for (auto& sgm : segs) {
+      if (sgm.second)
+        DCP_HIP_CHECK(hipMemcpy(host + o, p + sgm.first, sgm.second * sizeof(double),
+                                hipMemcpyDeviceToHost));
+      o += sgm.second;
+    }
     return DCP_OK;
   });
 }

@@ -266,6 +266,7 @@ struct Ctx {
   std::vector<const double*> gm_ptrs_host;
   int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
   int inner_max_steps = 5000;        // SolverControl(5000) of the inner Schur GMRES (probe hook)
+  int schur_fixed_inner = 0;         // DCP_OPT_SCHUR_FIXED_INNER (parity hook of solve_nse_schur)
   long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
   // test hook, read at context creation: DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger

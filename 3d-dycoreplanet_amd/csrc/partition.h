@@ -90,4 +90,9 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
                    int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c, int rank,
                    int world);
 
+// Rank hc.rank's local mesh from what that rank holds in a distributed run
+// (dcp_mesh_upload_distributed; distributed.cpp): the caller's ownership, the
+// second ghost layer fetched from the ghost cells' owners through hc.
+LocalMesh localize_distributed(const dcp_dist_mesh& m, const dcp_host_comm& hc);
+
 }  // namespace dcp

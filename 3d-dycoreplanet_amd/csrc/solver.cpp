@@ -1304,9 +1304,10 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   int n_inv = 0;
   // InverseMatrix<A, ILU>::vmult (inverse_matrix.hpp:93-120): CG, tol 1e-6 |src|,
   // max(n, 1000) steps, dst = 0, NoConvergence swallowed
+  const int fk = c.schur_fixed_inner;  // > 0: both inner CGs run exactly fk steps (tol 0)
   auto inverse = [&](const double* src, double* dst) {
-    const double nrm = std::sqrt(dot_host(c, gu, src, src, kSlotA));
-    Control ctl{unsigned(std::max(nu, 1000)), 1e-6 * nrm};
+    const double nrm = fk > 0 ? 0.0 : std::sqrt(dot_host(c, gu, src, src, kSlotA));
+    Control ctl = fk > 0 ? Control{unsigned(fk), 0.0} : Control{unsigned(std::max(nu, 1000)), 1e-6 * nrm};
     fill(nu, 0.0, dst, c.stream);
     ++n_inv;
     (void)pcg(c, nu, gu, Av, Pilu, dst, src, ctl, cg_u);
@@ -1335,8 +1336,8 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   Op Id = [&](const double* s, double* d) { copy(np, s, d, c.stream); };
   // ApproximateInverseMatrix<S~, identity>(n_iter = invalid) (approximate_inverse.hpp)
   Op Pre = [&](const double* s, double* d) {
-    const double nrm = std::sqrt(dot_host(c, gp, s, s, kSlotA));
-    Control ctl{~0u, 1e-6 * nrm};
+    const double nrm = fk > 0 ? 0.0 : std::sqrt(dot_host(c, gp, s, s, kSlotA));
+    Control ctl = fk > 0 ? Control{unsigned(fk), 0.0} : Control{~0u, 1e-6 * nrm};
     fill(np, 0.0, d, c.stream);
     (void)pcg(c, np, gp, Sa, Id, d, s, ctl, cg_p);
   };

@@ -36,6 +36,7 @@ OPT_GRAM_SCHMIDT = 7
 OPT_FEEC_FIXED_INNER = 8
 OPT_LOG_HISTORY = 10
 OPT_INNER_MAX_STEPS = 11
+OPT_SCHUR_FIXED_INNER = 12
 ABI_VERSION = 4            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
@@ -59,6 +60,8 @@ EXPORTED = [
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
+    "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_state_set_owned",
+    "dcp_state_get_owned",
 ]
 
 
@@ -134,6 +137,38 @@ class Mesh2DView(C.Structure):
         ("cell_nse_dofs", C.POINTER(C.c_int32)), ("cell_T_dofs", C.POINTER(C.c_int32)),
         ("cell_geometry", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
         ("nse", Constraints), ("T", Constraints),
+    ]
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                           C.POINTER(C.c_size_t))
+
+
+class HostComm(C.Structure):
+    """dcp_host_comm: the caller's communicator for the distributed upload's
+    host-side exchanges (the reference binds MPI_Allgather / MPI_Alltoallv)."""
+    _fields_ = [("user", C.c_void_p), ("rank", C.c_int), ("world", C.c_int),
+                ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
+
+
+class Constraints64(C.Structure):
+    _fields_ = [("n_lines", C.c_int64), ("line_dof", C.POINTER(C.c_int64)),
+                ("entry_ptr", C.POINTER(C.c_int64)), ("entry_dof", C.POINTER(C.c_int64)),
+                ("entry_w", C.POINTER(C.c_double)), ("inhomogeneity", C.POINTER(C.c_double))]
+
+
+class DistMeshView(C.Structure):
+    """dcp_dist_mesh: one rank's owned + ghost cells in global numbering."""
+    _fields_ = [
+        ("n_cells", C.c_int), ("n_owned_cells", C.c_int),
+        ("cell_id", C.POINTER(C.c_int64)), ("cell_owner", C.POINTER(C.c_int32)),
+        ("cell_nse_dofs", C.POINTER(C.c_int64)), ("cell_T_dofs", C.POINTER(C.c_int64)),
+        ("cell_geometry", C.POINTER(C.c_double)), ("cell_diameter", C.POINTER(C.c_double)),
+        ("n_u", C.c_int64), ("n_p", C.c_int64), ("n_T", C.c_int64),
+        ("u_begin", C.c_int64), ("u_end", C.c_int64), ("p_begin", C.c_int64), ("p_end", C.c_int64),
+        ("T_begin", C.c_int64), ("T_end", C.c_int64),
+        ("nse", Constraints64), ("T", Constraints64),
     ]
 
 
@@ -248,6 +283,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_host_mesh2d_create.argtypes = [I, C.c_double, C.c_double, C.c_double, I, I]
     lib.dcp_host_mesh2d_create.restype = P
     lib.dcp_host_mesh2d_view_get.argtypes = [P, C.POINTER(Mesh2DView), C.POINTER(D), C.POINTER(I)]
+    lib.dcp_mesh_upload_distributed.argtypes = [P, C.POINTER(DistMeshView), C.POINTER(HostComm)]
+    lib.dcp_dist_partition_info.argtypes = [C.POINTER(DistMeshView), C.POINTER(HostComm), P, P, P,
+                                            P, P, P]
+    lib.dcp_state_set_owned.argtypes = [P, I, P, C.c_size_t]
+    lib.dcp_state_get_owned.argtypes = [P, I, P, C.c_size_t]
     return lib
 
 
@@ -497,6 +537,187 @@ class FeecTopology:
         return v
 
 
+def torch_host_comm(group=None):
+    """A dcp_host_comm over an initialised torch.distributed process group
+    (gloo on the host; any backend whose collectives take CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+    def allgather(_user, send, nbytes, recv):
+        try:
+            src = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,)) \
+                if nbytes else np.zeros(0, np.uint8)
+            t = torch.from_numpy(src.copy())
+            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(out, t, group=group)
+            if nbytes:
+                flat = torch.cat(out).numpy()   # kept alive across the copy
+                C.memmove(recv, flat.ctypes.data, nbytes * world)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the library as a failure
+            return 1
+
+    def alltoallv(_user, send, send_bytes, recv, recv_bytes):
+        try:
+            sb = [int(send_bytes[k]) for k in range(world)]
+            rb = [int(recv_bytes[k]) for k in range(world)]
+            src = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(sum(sb),)) \
+                if sum(sb) else np.zeros(0, np.uint8)
+            out = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(out, torch.from_numpy(src.copy()), output_split_sizes=rb,
+                                   input_split_sizes=sb, group=group)
+            if sum(rb):
+                flat = out.numpy()
+                C.memmove(recv, flat.ctypes.data, sum(rb))
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    hc = HostComm(None, rank, world, ALLGATHER_FN(allgather), ALLTOALLV_FN(alltoallv))
+    hc._keep = (hc.allgather, hc.alltoallv)
+    return hc
+
+
+class DistMesh:
+    """One rank's part of a distributed mesh (dcp_dist_mesh), built here from a
+    global HostMesh the way a p4est run would hold it: the rank's owned cells
+    (an equal split in tree order), its ghost cells (one vertex layer), DoFs
+    renumbered so every rank owns one contiguous range per block (what deal.II's
+    distribute_dofs + component_wise give), owner = rank of the lowest-index
+    cell touching the DoF. `perm_*` map the HostMesh numbering to this one."""
+
+    def __init__(self, m: HostMesh, rank: int, world: int):
+        nc, nv = m.n_cells, m.n_u // 3
+        start = [r * nc // world for r in range(world + 1)]
+        cell_rank = np.zeros(nc, np.int32)
+        for r in range(world):
+            cell_rank[start[r]:start[r + 1]] = r
+        vel = m.cell_nse_dofs[:, [4 * t for t in range(8)] + [32 + 3 * t for t in range(19)]] // 3
+        pre = m.cell_nse_dofs[:, [4 * t + 3 for t in range(8)]] - m.n_u
+        tdo = m.cell_T_dofs
+
+        def owners(ents, n):
+            own = np.full(n, world, np.int32)
+            for c in range(nc):   # lowest-index cell touching the entity
+                e = ents[c]
+                own[e] = np.minimum(own[e], cell_rank[c])
+            return own
+
+        vown, pown, Town = owners(vel, nv), owners(pre, m.n_p), owners(tdo, m.n_T)
+
+        def renumber(own):
+            order = np.lexsort((np.arange(len(own)), own))    # by (owner, old id)
+            new = np.empty(len(own), np.int64)
+            new[order] = np.arange(len(own))
+            bounds = np.searchsorted(own[order], np.arange(world + 1))
+            return new, bounds
+
+        self.perm_v, vb = renumber(vown)
+        self.perm_p, pb = renumber(pown)
+        self.perm_T, tb = renumber(Town)
+        n_u = m.n_u
+        perm_nse = np.empty(n_u + m.n_p, np.int64)
+        perm_nse[:n_u] = 3 * np.repeat(self.perm_v, 3) + np.tile(np.arange(3), nv)
+        perm_nse[n_u:] = n_u + self.perm_p
+        self.perm_nse = perm_nse
+        # owned cells + one vertex layer of ghosts
+        vcells = [[] for _ in range(m.n_p)]
+        for c in range(nc):
+            for p in pre[c]:
+                vcells[p].append(c)
+        owned = list(range(start[rank], start[rank + 1]))
+        ghost = sorted({o for c in owned for p in pre[c] for o in vcells[p]} - set(owned))
+        cells = np.array(owned + ghost, np.int64)
+        self.cells = cells
+        self.rank, self.world = rank, world
+        self.n_cells, self.n_owned_cells = len(cells), len(owned)
+        self.cell_id = cells.copy()
+        self.cell_owner = cell_rank[cells].astype(np.int32)
+        self.cell_nse_dofs = perm_nse[m.cell_nse_dofs[cells]].astype(np.int64)
+        self.cell_T_dofs = self.perm_T[m.cell_T_dofs[cells]].astype(np.int64)
+        self.cell_geometry = np.ascontiguousarray(m.cell_geometry[cells])
+        self.cell_diameter = np.ascontiguousarray(m.cell_diameter[cells])
+        self.n_u, self.n_p, self.n_T = m.n_u, m.n_p, m.n_T
+        self.u_begin, self.u_end = 3 * int(vb[rank]), 3 * int(vb[rank + 1])
+        self.p_begin, self.p_end = n_u + int(pb[rank]), n_u + int(pb[rank + 1])
+        self.T_begin, self.T_end = int(tb[rank]), int(tb[rank + 1])
+        # constraint lines of the locally relevant dofs, global (renumbered) ids
+        rel_nse = np.unique(self.cell_nse_dofs)
+        rel_T = np.unique(self.cell_T_dofs)
+        self.nse_lines = self._lines(m.nse_constraints, perm_nse, rel_nse)
+        self.T_lines = self._lines(m.T_constraints, self.perm_T, rel_T)
+
+    @staticmethod
+    def _lines(cs, perm, relevant):
+        keep = np.isin(perm[cs.line_dof], relevant)
+        line, ptr, edof, w, inh = [], [0], [], [], []
+        for l in np.nonzero(keep)[0]:
+            line.append(perm[cs.line_dof[l]])
+            inh.append(cs.inhomogeneity[l])
+            for k in range(cs.entry_ptr[l], cs.entry_ptr[l + 1]):
+                edof.append(perm[cs.entry_dof[k]])
+                w.append(cs.entry_w[k])
+            ptr.append(len(edof))
+        return (np.array(line, np.int64), np.array(ptr, np.int64), np.array(edof, np.int64),
+                np.array(w, np.float64), np.array(inh, np.float64))
+
+    def as_struct(self) -> DistMeshView:
+        v = DistMeshView()
+        v.n_cells, v.n_owned_cells = self.n_cells, self.n_owned_cells
+        for name, ct in (("cell_id", C.c_int64), ("cell_owner", C.c_int32),
+                         ("cell_nse_dofs", C.c_int64), ("cell_T_dofs", C.c_int64),
+                         ("cell_geometry", C.c_double), ("cell_diameter", C.c_double)):
+            setattr(v, name, getattr(self, name).ctypes.data_as(C.POINTER(ct)))
+        v.n_u, v.n_p, v.n_T = self.n_u, self.n_p, self.n_T
+        v.u_begin, v.u_end, v.p_begin, v.p_end = self.u_begin, self.u_end, self.p_begin, self.p_end
+        v.T_begin, v.T_end = self.T_begin, self.T_end
+        for field, lines in (("nse", self.nse_lines), ("T", self.T_lines)):
+            c = Constraints64()
+            c.n_lines = len(lines[0])
+            for name, arr, ct in zip(("line_dof", "entry_ptr", "entry_dof", "entry_w", "inhomogeneity"),
+                                     lines, (C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_double)):
+                setattr(c, name, arr.ctypes.data_as(C.POINTER(ct)))
+            setattr(v, field, c)
+        return v
+
+    def owned_nse(self, global_vec):
+        """This rank's owned entries of an NSE vector in the HostMesh numbering,
+        in the distributed numbering's ascending order."""
+        g = np.empty_like(global_vec)
+        g[self.perm_nse] = global_vec
+        return np.concatenate([g[self.u_begin:self.u_end], g[self.p_begin:self.p_end]])
+
+    def owned_T(self, global_vec):
+        g = np.empty_like(global_vec)
+        g[self.perm_T] = global_vec
+        return g[self.T_begin:self.T_end].copy()
+
+
+def dist_partition_info(dm: DistMesh, comm: HostComm):
+    """dcp_dist_partition_info on this rank (host only; every rank calls it)."""
+    view = dm.as_struct()
+    info = np.zeros(12, np.int64)
+    rc = lib().dcp_dist_partition_info(C.byref(view), C.byref(comm), _ptr(info), None, None, None,
+                                       None, None)
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    npeer, ns, nr = int(info[8]), int(info[9]), int(info[10])
+    peers = np.zeros(max(npeer, 1), np.int32)
+    sp, rp = np.zeros(npeer + 1, np.int32), np.zeros(npeer + 1, np.int32)
+    sg, rg = np.zeros(max(ns, 1), np.int64), np.zeros(max(nr, 1), np.int64)
+    rc = lib().dcp_dist_partition_info(C.byref(view), C.byref(comm), _ptr(info), _ptr(peers),
+                                       _ptr(sp), _ptr(sg), _ptr(rp), _ptr(rg))
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    keys = ("n_cells", "n_owned_cells", "nvo", "nvg", "npo", "npg", "nTo", "nTg", "n_peers",
+            "n_send", "n_recv", "n_colors")
+    out = {k: int(v) for k, v in zip(keys, info)}
+    out["send"] = {int(p): sg[sp[i]:sp[i + 1]].copy() for i, p in enumerate(peers[:npeer])}
+    out["recv"] = {int(p): rg[rp[i]:rp[i + 1]].copy() for i, p in enumerate(peers[:npeer])}
+    return out
+
+
 def load_prm(path: str) -> RunParams:
     rp = RunParams()
     err = C.create_string_buffer(512)
@@ -641,6 +862,11 @@ class Context:
         (the reference's SolverControl(5000, ...))."""
         self._check(lib().dcp_set_option(self._h, OPT_INNER_MAX_STEPS, int(n)))
 
+    def set_schur_fixed_inner(self, k: int):
+        """DCP_OPT_SCHUR_FIXED_INNER (parity hook): the Schur-complement solver's
+        inner CGs run exactly k steps (0 = the reference's 1e-6 rule)."""
+        self._check(lib().dcp_set_option(self._h, OPT_SCHUR_FIXED_INNER, int(k)))
+
     def set_log_history(self, on: bool):
         """DCP_OPT_LOG_HISTORY: record the SolverControl checks of the NSE
         solve's FGMRES attempts (log_history = true, :1166-1169)."""
@@ -714,6 +940,25 @@ class Context:
             _ptr(m.cell_geometry), _ptr(m.cell_diameter), m.n_u, m.n_p, m.n_T,
             C.byref(nc), C.byref(tc)))
         self.mesh = m
+
+    def upload_mesh_distributed(self, dm: DistMesh, comm: HostComm):
+        """dcp_mesh_upload_distributed: this rank's owned + ghost cells in global
+        numbering with the caller's ownership (every rank calls it)."""
+        self._feec_view = None
+        v = dm.as_struct()
+        self._keep = (dm, v, comm)
+        self._check(lib().dcp_mesh_upload_distributed(self._h, C.byref(v), C.byref(comm)))
+        self.mesh = dm
+
+    def set_state_owned(self, field, values):
+        """dcp_state_set_owned: this rank's owned entries (ascending global id)."""
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        self._check(lib().dcp_state_set_owned(self._h, field, _ptr(a), a.size))
+
+    def get_state_owned(self, field, n):
+        out = np.zeros(n)
+        self._check(lib().dcp_state_get_owned(self._h, field, _ptr(out), n))
+        return out
 
     def upload_mesh2d(self, m: HostMesh2D, nse_constraints=None, T_constraints=None):
         """dcp_mesh2d_upload: the 2D model (Standard::BoussinesqModel<2>)."""

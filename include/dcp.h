@@ -121,6 +121,67 @@ int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t*
                        int32_t* peers, int32_t* send_ptr, int64_t* send_gid, int32_t* recv_ptr,
                        int64_t* recv_gid);
 
+/* Distributed upload (the reference's MPI layout) -----------------------------
+ * What one deal.II rank holds after setup_dofs() on a
+ * parallel::distributed::Triangulation (planet_geometry.h:67,
+ * boussinesq_model.tpp:237-252): its locally owned cells and its ghost cells
+ * (one vertex-neighbour layer), DoF indices in the GLOBAL numbering
+ * (cell->get_dof_indices), its locally_owned_dofs() as one contiguous range per
+ * block (velocity, pressure, temperature; what component_wise gives), and the
+ * constraint lines of its locally relevant dofs. The library keeps this
+ * ownership (each rank computes the rows of the dofs the caller owns), fetches
+ * the second ghost layer the explicit Schur complement needs from the owners
+ * of the caller's ghost cells, and builds the halos; the host-side exchanges
+ * go through the caller's communicator (dcp_host_comm, e.g. MPI_Allgather /
+ * MPI_Alltoallv on MPI_COMM_WORLD), the solver's through RCCL (dcp_config). */
+typedef struct {
+  void* user;
+  int rank, world;
+  /* every rank's `bytes` bytes, in rank order, into recv (world * bytes) */
+  int (*allgather)(void* user, const void* send, size_t bytes, void* recv);
+  /* send_bytes[s] bytes of send (packed in rank order) to rank s; recv gets
+   * recv_bytes[s] bytes from rank s (packed in rank order) */
+  int (*alltoallv)(void* user, const void* send, const size_t* send_bytes, void* recv,
+                   const size_t* recv_bytes);
+} dcp_host_comm;
+
+typedef struct {
+  int64_t n_lines;
+  const int64_t* line_dof;      /* global dof of each line */
+  const int64_t* entry_ptr;     /* [n_lines + 1] */
+  const int64_t* entry_dof;     /* global dofs */
+  const double* entry_w;
+  const double* inhomogeneity;
+} dcp_constraints64;
+
+typedef struct {
+  int n_cells;                  /* locally owned + ghost cells */
+  int n_owned_cells;            /* the first n_owned_cells are the locally owned ones */
+  const int64_t* cell_id;       /* [n_cells] unique global cell id (e.g. the global active index) */
+  const int32_t* cell_owner;    /* [n_cells] subdomain id (rank) of each cell */
+  const int64_t* cell_nse_dofs; /* [n_cells][89] global NSE dofs, FESystem local order */
+  const int64_t* cell_T_dofs;   /* [n_cells][8 or 27] global temperature dofs */
+  const double* cell_geometry;  /* [n_cells][64][3] */
+  const double* cell_diameter;  /* [n_cells] */
+  int64_t n_u, n_p, n_T;        /* global sizes */
+  /* locally_owned_dofs(): [u_begin, u_end) velocity, [n_u + p_begin, n_u + p_end)
+   * pressure, [T_begin, T_end) temperature (global indices) */
+  int64_t u_begin, u_end, p_begin, p_end, T_begin, T_end;
+  dcp_constraints64 nse, T;     /* lines of the locally relevant dofs */
+} dcp_dist_mesh;
+int dcp_mesh_upload_distributed(dcp_ctx* ctx, const dcp_dist_mesh* m, const dcp_host_comm* comm);
+/* Host-only dry run of the distributed localisation (no device): info[12] as
+ * dcp_partition_info, and the velocity halo in global node ids. Every rank of
+ * `comm` must call it. */
+int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, int64_t* info,
+                            int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                            int32_t* recv_ptr, int64_t* recv_gid);
+/* The rank's locally owned entries of a state field, ascending global index
+ * (NSE: owned velocity, then owned pressure; the Trilinos vector's local part).
+ * Ghost entries are refreshed internally. Works after either upload. */
+int dcp_state_set_owned(dcp_ctx* ctx, int field, const double* host, size_t n);
+int dcp_state_get_owned(dcp_ctx* ctx, int field, double* host, size_t n);
+
 /* Context / errors ------------------------------------------------------- */
 int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out);
 void dcp_ctx_destroy(dcp_ctx* ctx);
@@ -180,6 +241,13 @@ enum { DCP_OPT_FGMRES_MAX_OUTER = 5 };
  *   BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:46-51),
  *   so a large mesh can be probed for a bounded number of steps. */
 enum { DCP_OPT_INNER_MAX_STEPS = 11 };
+/* DCP_OPT_SCHUR_FIXED_INNER (parity hook, default 0 = the reference's rule): k
+ *   > 0 runs both inner CGs of dcp_solve_nse_schur (InverseMatrix's A^-1,
+ *   inverse_matrix.hpp:93-120, and the ApproximateInverseMatrix
+ *   preconditioner) for exactly k steps with tolerance 0, so the solver is a
+ *   smooth map of its input with no early-stop decisions for rounding to flip;
+ *   the oracle has the same switch (orc_set_schur_fixed_inner). */
+enum { DCP_OPT_SCHUR_FIXED_INNER = 12 };
 /* DCP_OPT_ELEMENT_MFMA: 0 (default) = the velocity-velocity node-pair sums of
  *   the NSE element matrix (local_assemble_nse_system, boussinesq_model.tpp:
  *   597-640: mass + eps:eps over the 27 QGauss points) run as FP64 VALU

@@ -602,6 +602,7 @@ struct orc_model {
   int inner_iterations = 0;
   long a_solve_iterations = 0;  // AztecOO A-GMRES iterations of the last solve (do_solve_A)
   int inner_max_steps = 5000;   // SolverControl(5000) of the inner Schur GMRES (timing hook)
+  int schur_fixed_inner = 0;    // parity hook: the Schur solver's inner CGs run exactly k steps
 };
 
 extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
@@ -695,6 +696,7 @@ extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_
 }
 
 extern "C" void orc_set_inner_max_steps(orc_model* m, int n) { m->inner_max_steps = n; }
+extern "C" void orc_set_schur_fixed_inner(orc_model* m, int k) { m->schur_fixed_inner = k; }
 
 extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   // assemble_nse_preconditioner (:479-514) + build_nse_preconditioner (:518-542).
@@ -1442,8 +1444,10 @@ extern "C" int orc_solve_nse_schur(orc_model* m, double* sol, int* schur_iterati
   int n_inv = 0;
   // InverseMatrix<A, ILU>::vmult (inverse_matrix.hpp:93-120): CG, tol 1e-6 |src|,
   // max(n, 1000) steps, dst = 0, NoConvergence swallowed
+  const int fk = m->schur_fixed_inner;  // > 0: both inner CGs run exactly fk steps (tol 0)
   auto inverse = [&](const double* src, double* dst) {
-    Control ctl{unsigned(std::max(nu, 1000)), 1e-6 * std::sqrt(dotv(src, src, nu))};
+    Control ctl = fk > 0 ? Control{unsigned(fk), 0.0}
+                         : Control{unsigned(std::max(nu, 1000)), 1e-6 * std::sqrt(dotv(src, src, nu))};
     std::fill(dst, dst + nu, 0.0);
     ++n_inv;
     try {
@@ -1473,7 +1477,7 @@ extern "C" int orc_solve_nse_schur(orc_model* m, double* sol, int* schur_iterati
   auto identity = [&](const double* s, double* d) { std::copy(s, s + np, d); };
   // ApproximateInverseMatrix<S~, identity>(n_iter = invalid): CG, tol 1e-6 |src|
   auto precond = [&](const double* s, double* d) {
-    Control ctl{~0u, 1e-6 * std::sqrt(dotv(s, s, np))};
+    Control ctl = fk > 0 ? Control{unsigned(fk), 0.0} : Control{~0u, 1e-6 * std::sqrt(dotv(s, s, np))};
     std::fill(d, d + np, 0.0);
     try {
       pcg(np, Sa, identity, d, s, ctl);

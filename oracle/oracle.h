@@ -73,6 +73,9 @@ void orc_cell_temperature_rhs(const orc_physics* ph, const double* geom64,
 
 /* ---- global model ------------------------------------------------------- */
 typedef struct orc_model orc_model;
+/* parity hook: the Schur-complement solver's A^-1 and preconditioner CGs run
+ * exactly k steps (0 = the reference's 1e-6 relative rule) */
+void orc_set_schur_fixed_inner(orc_model* m, int k);
 /* Standard::BoussinesqModel<2>: element level (22 NSE dofs, 16 support points
  * per cell as [16][2]) and a 2D model whose other orc_* calls (schur solver,
  * temperature solve, exports, cfl) work as for the 3D one. */

@@ -70,6 +70,7 @@ def lib():
         L.orc_solve_nse_schur.argtypes = [P, P, P, P]
         L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
         L.orc_set_inner_max_steps.argtypes = [P, I]
+        L.orc_set_schur_fixed_inner.argtypes = [P, I]
         L.orc_set_threads.argtypes = [I]
         L.orc_fgmres_outer.argtypes = [P, P, I, P]
         L.orc_a_solve_iterations.argtypes = [P]
@@ -204,6 +205,10 @@ class Model:
     def set_inner_max_steps(self, n):
         """Timing hook: cap of the inner Schur GMRES (the reference's 5000)."""
         lib().orc_set_inner_max_steps(self.h, int(n))
+
+    def set_schur_fixed_inner(self, k):
+        """Parity hook: the Schur solver's inner CGs run exactly k steps (0 = off)."""
+        lib().orc_set_schur_fixed_inner(self.h, int(k))
 
     def build_nse_preconditioner(self):
         lib().orc_build_nse_preconditioner(self.h)

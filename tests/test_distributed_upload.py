@@ -1,0 +1,149 @@
+"""Distributed upload (dcp_mesh_upload_distributed): every rank passes only
+what a deal.II rank holds — its owned cells and one ghost layer, global DoF
+ids, its locally_owned_dofs() ranges and the constraint lines of its locally
+relevant dofs (boussinesq_model.tpp:237-252, planet_geometry.h:67) — and the
+library fetches the second ghost layer and builds the halos through the
+caller's communicator (dcp_host_comm; here torch.distributed gloo).
+
+CPU (gloo, 2 and 3 processes): with the ownership of the library's own
+global-mesh rule, the distributed localisation reproduces the global one
+exactly (cell/entity counts, colours, velocity halo lists in global ids), and
+ownership covers every DoF once.
+GPU (in the -m gpu run): one rank with world 1 uploads through the
+distributed entry point and matches the global upload bitwise."""
+import os
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dcp
+
+
+class Renumbered:
+    """The global HostMesh in a DistMesh's renumbered global ids."""
+
+    def __init__(self, m, dm):
+        self.n_cells, self.n_u, self.n_p, self.n_T = m.n_cells, m.n_u, m.n_p, m.n_T
+        self.cell_nse_dofs = dm.perm_nse[m.cell_nse_dofs].astype(np.int32)
+        self.cell_T_dofs = dm.perm_T[m.cell_T_dofs].astype(np.int32)
+        self.cell_geometry, self.cell_diameter = m.cell_geometry, m.cell_diameter
+
+        def ren(cs, perm):
+            return dcp.ConstraintSet(perm[cs.line_dof], cs.entry_ptr, perm[cs.entry_dof],
+                                     cs.entry_w, cs.inhomogeneity)
+
+        self.nse_constraints = ren(m.nse_constraints, dm.perm_nse)
+        self.T_constraints = ren(m.T_constraints, dm.perm_T)
+
+
+def _worker(rank, world, port, refine, tdeg, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = dcp.HostMesh(refine=refine, temperature_degree=tdeg)
+        dm = dcp.DistMesh(m, rank, world)
+        comm = dcp.torch_host_comm()
+        got = dcp.dist_partition_info(dm, comm)
+        want = dcp.partition_info(Renumbered(m, dm), rank, world)
+        same = all(got[k] == want[k] for k in want if k not in ("send", "recv"))
+        same &= got["send"].keys() == want["send"].keys() and got["recv"].keys() == want["recv"].keys()
+        for k in want["send"]:
+            same &= np.array_equal(got["send"][k], want["send"][k])
+            same &= np.array_equal(got["recv"][k], want["recv"][k])
+        # the caller's ownership is what the library keeps
+        same &= got["nvo"] == (dm.u_end - dm.u_begin) // 3 and got["npo"] == dm.p_end - dm.p_begin
+        same &= got["nTo"] == dm.T_end - dm.T_begin
+        owned = [None] * world
+        dist.all_gather_object(owned, (got["nvo"], got["npo"], got["nTo"]))
+        tot = [sum(o[i] for o in owned) for i in range(3)]
+        same &= tot == [m.n_u // 3, m.n_p, m.n_T]
+        q.put((rank, bool(same), got["n_cells"] > dm.n_cells))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), False))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,refine,tdeg", [(2, 2, 1), (3, 2, 2), (2, 3, 1)])
+def test_distributed_localisation_matches_global_gloo(world, refine, tdeg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + 10 * world + refine + tdeg
+    procs = [ctx.Process(target=_worker, args=(r, world, port, refine, tdeg, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, layer2 in sorted(res):
+        assert ok is True, (rank, ok)
+        assert layer2   # the second ghost layer came from the peers
+
+
+class LocalComm:
+    """A one-rank dcp_host_comm (no process group)."""
+
+    def __new__(cls):
+        import ctypes as C
+
+        def allgather(_u, send, n, recv):
+            C.memmove(recv, send, n)
+            return 0
+
+        def alltoallv(_u, send, sb, recv, rb):
+            C.memmove(recv, send, sb[0])
+            return 0
+
+        hc = dcp.HostComm(None, 0, 1, dcp.ALLGATHER_FN(allgather), dcp.ALLTOALLV_FN(alltoallv))
+        hc._keep = (hc.allgather, hc.alltoallv)
+        return hc
+
+
+def test_single_rank_distributed_partition_is_the_whole_mesh():
+    m = dcp.HostMesh(refine=2)
+    dm = dcp.DistMesh(m, 0, 1)
+    info = dcp.dist_partition_info(dm, LocalComm())
+    assert info["n_cells"] == m.n_cells and info["nvg"] == 0 and info["n_peers"] == 0
+    assert info["nvo"] == m.n_u // 3 and info["npo"] == m.n_p and info["nTo"] == m.n_T
+
+
+def test_distributed_input_errors():
+    m = dcp.HostMesh(refine=1)
+    dm = dcp.DistMesh(m, 0, 1)
+    dm.cell_owner = dm.cell_owner.copy()
+    dm.cell_owner[0] = 3              # an owned cell reported with another owner
+    with pytest.raises(dcp.DcpError):
+        dcp.dist_partition_info(dm, LocalComm())
+    dm = dcp.DistMesh(m, 0, 1)
+    dm.u_end -= 1                     # velocity range not aligned to support points
+    with pytest.raises(dcp.DcpError):
+        dcp.dist_partition_info(dm, LocalComm())
+
+
+@pytest.mark.gpu
+def test_distributed_upload_world1_is_the_global_upload():
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    dm = dcp.DistMesh(m, 0, 1)
+    rng = np.random.default_rng(7)
+    u = rng.uniform(-1, 1, m.n_u + m.n_p)
+    T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+    ref = dcp.Context()
+    ref.set_physics(ph)
+    ref.upload_mesh(Renumbered(m, dm))
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh_distributed(dm, LocalComm())
+    for c in (ref, ctx):
+        c.set_state_owned(dcp.OLD_NSE_SOLUTION, dm.owned_nse(u))
+        c.set_state_owned(dcp.OLD_T_SOLUTION, dm.owned_T(T))
+        c.assemble_nse_system()
+        c.build_nse_preconditioner()
+    n = m.n_u + m.n_p
+    assert np.array_equal(ref.get_state_owned(dcp.NSE_RHS, n), ctx.get_state_owned(dcp.NSE_RHS, n))
+    x = rng.uniform(-1, 1, n)
+    assert np.array_equal(ref.nse_vmult(x), ctx.nse_vmult(x))

@@ -37,8 +37,9 @@ def case(name):
     return dcp.HostMesh(refine=refine), dcp.classic_physics()
 
 
-def oracle_solve(m, ph, u, T):
+def oracle_solve(m, ph, u, T, fixed_inner=0):
     orc = oracle_py.Model(ph, m)
+    orc.set_schur_fixed_inner(fixed_inner)
     orc.assemble_nse_system(u, T)
     return orc.solve_nse_schur(u)
 
@@ -79,6 +80,32 @@ def test_gpu_schur_solver_matches_oracle(name):
     # contraction, the block SpMV's sum order) reaches ~1e-10 of the result
     # (1.5e-10 measured on the r=1 shell), hence 1e-9
     assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["shell-r1", "cube-r2-cm"])
+def test_gpu_schur_solver_fixed_inner_1e10(name):
+    """With DCP_OPT_SCHUR_FIXED_INNER both inner CGs run a fixed number of
+    steps in the oracle and on the device (no early-stop decision for rounding
+    to flip), and the Schur solve agrees to 1e-10 — the north-star bar."""
+    m, ph = case(name)
+    rng = np.random.default_rng(11)
+    u = 0.1 * rng.uniform(-1, 1, m.n_u + m.n_p)
+    T = m.T0 + 0.05 * rng.uniform(-1, 1, m.n_T)
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh(m)
+    ctx.set_schur_fixed_inner(40)
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    rc, its, na = ctx.solve_nse_schur()
+    x = ctx.get_state(dcp.NSE_SOLUTION)
+    rco, xo, itso, nao = oracle_solve(m, ph, ctx.get_state(dcp.OLD_NSE_SOLUTION), T, 40)
+    ctx.close()
+    assert rc == rco and (its, na) == (itso, nao)
+    assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
 
 
 @pytest.mark.gpu

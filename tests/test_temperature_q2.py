@@ -131,5 +131,7 @@ def test_q2_temperature_schur_steps_match_oracle():
         _, T_new, _ = orc.solve_temperature(T)
         u, T = u_new, T_new
         assert rc == rco == 0 and rcT == 0 and its == itso
-        assert rel2(ctx.get_state(dcp.NSE_SOLUTION), u) < 1e-8
-        assert rel2(ctx.get_state(dcp.T_SOLUTION), T) < 1e-8
+        # the reference's inner rule (1e-6 CGs): rounding reaches ~1e-8 (see
+        # test_parity_gpu_2d.py); the iteration counts must agree exactly
+        assert rel2(ctx.get_state(dcp.NSE_SOLUTION), u) < 1e-7
+        assert rel2(ctx.get_state(dcp.T_SOLUTION), T) < 1e-7
