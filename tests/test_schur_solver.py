@@ -83,8 +83,8 @@ def test_gpu_schur_solver_matches_oracle(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["shell-r1", "cube-r2-cm"])
-def test_gpu_schur_solver_fixed_inner_1e10(name):
+@pytest.mark.parametrize("name,k", [("shell-r1", 40), ("cube-r2-cm", 8)])
+def test_gpu_schur_solver_fixed_inner_1e10(name, k):
     """With DCP_OPT_SCHUR_FIXED_INNER both inner CGs run a fixed number of
     steps in the oracle and on the device (no early-stop decision for rounding
     to flip), and the Schur solve agrees to 1e-10 — the north-star bar."""
@@ -95,14 +95,16 @@ def test_gpu_schur_solver_fixed_inner_1e10(name):
     ctx = dcp.Context()
     ctx.set_physics(ph)
     ctx.upload_mesh(m)
-    ctx.set_schur_fixed_inner(40)
+    # k below the CG's exact convergence on the mesh: steps past it divide by
+    # round-off-level residuals, where no two implementations agree
+    ctx.set_schur_fixed_inner(k)
     for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
                  (dcp.T_SOLUTION, T)):
         ctx.set_state(f, v)
     ctx.assemble_nse_system()
     rc, its, na = ctx.solve_nse_schur()
     x = ctx.get_state(dcp.NSE_SOLUTION)
-    rco, xo, itso, nao = oracle_solve(m, ph, ctx.get_state(dcp.OLD_NSE_SOLUTION), T, 40)
+    rco, xo, itso, nao = oracle_solve(m, ph, ctx.get_state(dcp.OLD_NSE_SOLUTION), T, k)
     ctx.close()
     assert rc == rco and (its, na) == (itso, nao)
     assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
