@@ -1216,7 +1216,7 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       return DCP_OK;
     }
     if (option == DCP_OPT_GRAM_SCHMIDT) {
-      require(value >= 0 && value <= 2, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0, 1 or 2");
+      require(value >= 0 && value <= 3, DCP_ERR_INVALID, "DCP_OPT_GRAM_SCHMIDT must be 0..3");
       ctx->gram_schmidt = value;
       return DCP_OK;
     }
@@ -1957,6 +1957,7 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
               "the explicit Schur complement needs the assembled B blocks: call "
               "dcp_assemble_nse_system first");
       // B read through B^T's transpose map unless B is materialised
+      c.S_lambda = 0;  // the s-step shifts follow the new S
       form_schur_complement(c.npo, c.B_ptr.p, c.B_col.p, c.B_current ? c.B_val.p : nullptr,
                             c.B_current ? nullptr : c.B_tperm.p, c.Bt_ptr.p, c.Bt_col.p,
                             c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_pmap.p,

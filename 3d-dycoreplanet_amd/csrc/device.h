@@ -330,6 +330,12 @@ struct SellView {
   const double* val;
 };
 void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s);
+// y = (S x - theta x) * sscale (the s-step Newton basis); every launch returns
+// at entry once *status != 0
+void sell_spmv_shifted(const SellView& m, const double* x, double theta, double sscale, double* y,
+                       const int* status, hipStream_t s);
+// *out = max_i sum_j |S_ij| (Gershgorin bound of the spectrum of S)
+void sell_gershgorin(const SellView& m, double* out, hipStream_t s);
 // Krylov-fused form: additionally xs = cf * x on every row (the scaled basis
 // vector, xs != x), and per-workgroup partials of y.v0 -> part0 and y.y ->
 // part1 (one per slice, fixed order; zeros up to n_part, the length common to
@@ -445,6 +451,20 @@ struct Comm;
 // tags, never reused); err: set to 1 if a reduction timed out; comm: all-reduce
 // the sums (several GPUs) or null.
 size_t cgs2_granules(long n);
+// s-step Arnoldi block (kernels/krylov.hip k_sstep_block): the raw Newton
+// basis w[0..s) (w_i = (S - theta_i) w_{i-1} * (1/sigma), w_0 = q_k) is
+// orthogonalised against q_0..q_k twice and Cholesky-QR'd into q[0..s) =
+// q_{k+1..k+s}; workgroup 0 forms Hessenberg columns k..k+s-1 and runs their
+// Givens steps / checks. One GPU, nb resident workgroups as cgs2_chain_step.
+constexpr int kSStep = 4;
+struct SStepArgs {
+  const double* w[kSStep];
+  double* q[kSStep];
+  double theta[kSStep];
+  double sigma;
+};
+void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st, double* gran,
+                 int nb, unsigned long long seq, double* err, hipStream_t s);
 // One GPU: the same step (w -= V V^T w twice, |w|, Givens) in one launch of
 // nb resident workgroups (cgs2_chain_fits: nb <= n_cus, enough entries per
 // thread) handing their sums over as granules in gran (kMgsGranules doubles).

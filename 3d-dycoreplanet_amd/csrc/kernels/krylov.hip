@@ -567,6 +567,239 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
                            std::to_string(kGmMaxDim - 1) + ")");
 }
 
+// ---------------------------------------------------------------------------
+// s-step (communication-avoiding) Arnoldi block, s = kSStep: the host has
+// formed the raw Newton basis w_i = (S - theta_i) w_{i-1} / sigma, w_0 = q_k,
+// i = 1..s (sell_spmv_shifted, s back-to-back SpMVs); this launch
+//   1. C1 = Q^T W against the basis q_0..q_k, W -= Q C1          (reduction 1)
+//   2. C2 = Q^T W and G = W^T W, W -= Q C2, G' = G - C2^T C2      (reduction 2)
+//   3. R = chol(G'), q_{k+1..k+s} = W R^-1 (block Gram-Schmidt twice, then
+//      Cholesky QR; no further reduction)
+// and workgroup 0 turns the change of basis into the s new Hessenberg columns
+// k..k+s-1 (A [w_0..w_{s-1}] = [w_0..w_s] B, B = theta on the diagonal, sigma
+// below it; H_new = (Rhat B - H_old T_top) U^-1) and runs SolverGMRES's Givens
+// step and SolverControl check column by column, so the iteration count and
+// the stopping column are those of the one-vector-per-step Arnoldi process.
+// Two reductions per s steps instead of two per step; the same registers /
+// granule hand-off scheme as k_cgs2_chain (nb resident 512-thread workgroups,
+// two entries per thread).
+namespace {
+
+constexpr int kSsRes = 2 * 128 * 256;  // result granules after the partial area
+
+// column kk of SolverGMRES's Givens QR from the raw Hessenberg column h[0..kk+1]
+__device__ void gmres_column(GmresDev* st, double* h, int kk) {
+  // one thread
+  for (int i = 0; i < kk; i++) {
+    const double dummy = h[i];
+    h[i] = st->ci[i] * dummy + st->si[i] * h[i + 1];
+    h[i + 1] = -st->si[i] * dummy + st->ci[i] * h[i + 1];
+  }
+  const double r = 1. / sqrt(h[kk] * h[kk] + h[kk + 1] * h[kk + 1]);
+  const double sn = h[kk + 1] * r, cn = h[kk] * r;
+  st->si[kk] = sn;
+  st->ci[kk] = cn;
+  h[kk] = cn * h[kk] + sn * h[kk + 1];
+  const double g0 = st->gamma[kk];
+  const double gk1 = -sn * g0;
+  st->gamma[kk + 1] = gk1;
+  st->gamma[kk] = g0 * cn;
+  const int acc = st->accumulated + 1;
+  st->accumulated = acc;
+  st->dim = kk + 1;
+  const double rho = fabs(gk1);
+  st->rho = rho;
+  st->status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+  for (int t = 0; t <= kk; ++t) st->H[t][kk] = h[t];
+}
+
+template <int KL>
+__global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs V, SStepArgs a,
+                                                               int k, GmresDev* st, double* gran,
+                                                               unsigned long long seq, double* err) {
+  constexpr int K = pow2_at_least<KL>();
+  constexpr int S = kSStep;
+  static_assert(kChainEntries == 2, "two entries per thread");
+  __shared__ double sm[S][kChainWaves * K];
+  __shared__ double sm16[kChainWaves * 16];
+  __shared__ double c1[S * 32], c2[S * 32 + 16];
+  __shared__ double Rm[S][S];
+  __shared__ int bad;
+  if (st->status) return;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int d = k + 1;              // basis vectors q_0..q_k
+  const int ncol1 = S * d;          // C columns (i * d + j)
+  constexpr int nG = S * (S + 1) / 2;
+  // entries b * 1024 + e * 512 + t of the vectors (two per thread)
+  double v[kChainEntries][K], w[kChainEntries][S];
+  unsigned pos[kChainEntries];
+  bool live[kChainEntries];
+  const long kb = long(b) * (kChainThreads * kChainEntries);
+#pragma unroll
+  for (int e = 0; e < kChainEntries; ++e) {
+    const long kk = kb + e * kChainThreads + threadIdx.x;
+    live[e] = kk < g.n;
+    pos[e] = live[e] ? unsigned(seg_pos(g, kk)) : 0u;
+#pragma unroll
+    for (int i = 0; i < S; ++i) w[e][i] = live[e] ? a.w[i][pos[e]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[e][j] = (j < KL && j < d && live[e]) ? V.v[j][pos[e]] : 0.0;
+  }
+  double* part = gran;
+  double* res = gran + kSsRes;
+  for (int pass = 0; pass < 2; ++pass) {
+    const unsigned long long tag = seq * 256 + 2 * unsigned(pass);
+    const int ncol = pass == 0 ? ncol1 : ncol1 + nG;
+    // block sums of V^T w_i (and, pass 1, of w_a w_b)
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const double x[kChainEntries] = {w[0][i], w[1][i]};
+      const double r = chain_block_sums<K>(v, x, d, sm[i]);
+      if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
+    }
+    if (pass == 1) {
+      double pr[kChainEntries][16];
+#pragma unroll
+      for (int e = 0; e < kChainEntries; ++e) {
+        int p = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+          for (int l = i; l < S; ++l) pr[e][p++] = w[e][i] * w[e][l];
+#pragma unroll
+        for (; p < 16; ++p) pr[e][p] = 0.0;
+      }
+      const double one[kChainEntries] = {1.0, 1.0};
+      const double r = chain_block_sums<16>(pr, one, nG, sm16);
+      if (int(threadIdx.x) < nG) granule_store(part + 2 * (size_t(ncol1 + threadIdx.x) * nb + b), r, tag);
+    }
+    // workgroup c reduces column c and publishes the total
+    if (b < ncol && threadIdx.x < 64) {
+      const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err);
+      if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + 1);
+    }
+    for (int c = threadIdx.x; c < ncol; c += kChainThreads) {
+      const double* p = res + 2 * c;
+      mgs_u4 q = granule_load(p);
+      for (long spins = 0; !tag_is(q, tag + 1); ++spins) {
+        if (spins >= kMgsMaxSpins) {
+          *err = 1.0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        q = granule_load(p);
+      }
+      if (pass == 0) c1[c] = granule_value(q);
+      else c2[c] = granule_value(q);
+    }
+    __syncthreads();
+    const double* h = pass == 0 ? c1 : c2;
+#pragma unroll
+    for (int e = 0; e < kChainEntries; ++e)
+#pragma unroll
+      for (int i = 0; i < S; ++i)
+#pragma unroll
+        for (int j = 0; j < KL; ++j)
+          if (j < d) w[e][i] -= h[i * d + j] * v[e][j];
+    __syncthreads();
+  }
+  // G' = G - C2^T C2 and its Cholesky factor (every workgroup, the same
+  // arithmetic in the same order)
+  if (threadIdx.x == 0) {
+    double G[S][S];
+    int p = 0;
+    for (int i = 0; i < S; ++i)
+      for (int l = i; l < S; ++l) {
+        double gv = c2[ncol1 + p++];
+        for (int j = 0; j < d; ++j) gv -= c2[i * d + j] * c2[l * d + j];
+        G[i][l] = G[l][i] = gv;
+      }
+    int ok = 1;
+    for (int i = 0; i < S; ++i) {
+      double dd = G[i][i];
+      for (int l = 0; l < i; ++l) dd -= Rm[l][i] * Rm[l][i];
+      if (!(dd > 0)) {
+        ok = 0;
+        dd = 1.0;
+      }
+      Rm[i][i] = sqrt(dd);
+      for (int l = i + 1; l < S; ++l) {
+        double o = G[i][l];
+        for (int m = 0; m < i; ++m) o -= Rm[m][i] * Rm[m][l];
+        Rm[i][l] = o / Rm[i][i];
+      }
+      for (int l = 0; l < i; ++l) Rm[i][l] = 0.0;
+    }
+    bad = !ok;
+  }
+  __syncthreads();
+  // q_{k+1+i} = (w_i - sum_{l<i} q_{k+1+l} R[l][i]) / R[i][i]
+#pragma unroll
+  for (int e = 0; e < kChainEntries; ++e) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      double q = w[e][i];
+#pragma unroll
+      for (int l = 0; l < i; ++l) q -= w[e][l] * Rm[l][i];
+      w[e][i] = q / Rm[i][i];
+      if (live[e]) a.q[i][pos[e]] = w[e][i];
+    }
+  }
+  if (b != 0 || threadIdx.x != 0) return;
+  if (bad) {  // the block lost rank: a breakdown the one-vector process would not see
+    st->status = 2;
+    st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    return;
+  }
+  // ---- Hessenberg columns k..k+s-1 (raw, into Hr) and their Givens steps
+  const int rows = k + S + 1;
+  auto rhat = [&](int r, int c) -> double {  // Rhat (rows x (S+1)): [e_k | [C; R]]
+    if (c == 0) return r == k ? 1.0 : 0.0;
+    if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
+    return Rm[r - k - 1][c - 1];
+  };
+  double Hn[kGmMaxDim + 1][S];
+  for (int c = 0; c < S; ++c) {
+    for (int r = 0; r < rows; ++r) {
+      double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
+      if (r <= k && c > 0)
+        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= st->Hr[r][i] * rhat(i, c);
+      // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular)
+      for (int l = 0; l < c; ++l) x -= Hn[r][l] * rhat(k + l, c);
+      Hn[r][c] = x / rhat(k + c, c);
+    }
+  }
+  double h[kGmMaxDim + 1];
+  for (int c = 0; c < S; ++c) {
+    const int kk = k + c;
+    for (int r = 0; r <= kk + 1; ++r) {
+      st->Hr[r][kk] = Hn[r][c];
+      h[r] = Hn[r][c];
+    }
+    gmres_column(st, h, kk);
+    if (st->status) return;
+  }
+}
+
+}  // namespace
+
+void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st, double* gran,
+                 int nb, unsigned long long seq, double* err, hipStream_t s) {
+  ChainVecs Vp = V;
+  for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
+  const dim3 grid(nb), block(kChainThreads);
+#define DCP_SS_CASE(KL)                                                                        \
+  if (k + 1 <= KL) {                                                                           \
+    hipLaunchKernelGGL((k_sstep_block<KL>), grid, block, 0, s, g, Vp, a, k, st, gran, seq, err); \
+    DCP_HIP_CHECK(hipGetLastError());                                                          \
+    return;                                                                                    \
+  }
+  DCP_SS_CASE(4) DCP_SS_CASE(8) DCP_SS_CASE(12) DCP_SS_CASE(16) DCP_SS_CASE(20) DCP_SS_CASE(24)
+  DCP_SS_CASE(28)
+#undef DCP_SS_CASE
+  throw std::runtime_error("sstep_block: basis too long");
+}
+
 size_t cgs2_granules(long n) {
   return 2 * size_t(kGmMaxDim) * size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)) + 2;
 }

@@ -347,7 +347,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
                                                       double* __restrict__ part0,
                                                       double* __restrict__ part1,
                                                       const double* __restrict__ cf_dev,
-                                                      const int* __restrict__ status) {
+                                                      const int* __restrict__ status,
+                                                      double theta = 0.0, double sscale = 1.0) {
   __shared__ double quarter[3][64];
   if (status && *status) return;  // device-resident GMRES cycle already stopped
   if (cf_dev) cf = *cf_dev;
@@ -459,8 +460,10 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   }
   double d0 = 0, d1 = 0;
   if (row < rows) {
-    y[row] = acc;
     const double xv = x[row] * cf;
+    // s-step Newton basis: y = (S x - theta x) / sigma (sscale = 1 / sigma)
+    if (theta != 0.0 || sscale != 1.0) acc = (acc - theta * xv) * sscale;
+    y[row] = acc;
     if (xs) xs[row] = xv;
     if (part0) {
       d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
@@ -850,6 +853,45 @@ void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, do
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
                        nullptr, nullptr, nullptr, cf_dev, status);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void sell_spmv_shifted(const SellView& m, const double* x, double theta, double sscale, double* y,
+                       const int* status, hipStream_t s) {
+  if (m.rows <= 0) return;
+  const dim3 grid(sell_fused_blocks(m.rows));
+  if (m.col16)
+    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                       nullptr, nullptr, nullptr, nullptr, status, theta, sscale);
+  else
+    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                       nullptr, nullptr, nullptr, nullptr, status, theta, sscale);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+// Gershgorin bound of the stored S: max over rows of sum |s_ij| (padding
+// entries are zero), as a non-negative double through its bit pattern
+__global__ __launch_bounds__(64) void k_sell_rowabs(SellView m, double* out) {
+  const long sl = blockIdx.x;
+  const long row = sl * 64 + threadIdx.x;
+  const int64_t b = m.off[sl];
+  const int np = int((m.off[sl + 1] - b) >> 7);
+  const double2* vp = reinterpret_cast<const double2*>(m.val + b) + threadIdx.x;
+  double s = 0.0;
+  for (int k = 0; k < np; ++k, vp += 64) s += fabs(vp->x) + fabs(vp->y);
+  if (row >= m.rows) s = 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o, 64));
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(s));
+}
+}  // namespace
+
+void sell_gershgorin(const SellView& m, double* out, hipStream_t s) {
+  DCP_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double), s));
+  if (m.rows <= 0) return;
+  hipLaunchKernelGGL(k_sell_rowabs, dim3((m.rows + 63) / 64), dim3(64), 0, s, m, out);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -736,6 +736,113 @@ State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::ve
   return st;
 }
 
+// The inner Schur GMRES in s-step form (DCP_OPT_GRAM_SCHMIDT = 3; kernels/
+// krylov.hip k_sstep_block): the same device-resident restart cycles, each
+// cycle's 28 Arnoldi steps as 7 blocks of kSStep = 4. A block is 4 back-to-back
+// SpMVs forming the Newton basis w_i = (S - theta_i) w_{i-1} / sigma from the
+// last basis vector, then one launch orthogonalising the block (two
+// reductions) and running the 4 Givens steps / checks column by column. S is
+// symmetric positive semi-definite: the shifts are the Chebyshev points of
+// [0, lambda] with lambda the Gershgorin bound of the stored S, sigma =
+// lambda / 2, so the basis polynomials stay bounded on the spectrum. Falls back
+// to CGS2 when the block does not fit the resident grid or on several GPUs.
+bool sstep_fits(const Ctx& c, long n, int nb) {
+  constexpr int nG = kSStep * (kSStep + 1) / 2;
+  const int max_cols = kSStep * (kGmMaxDim - 1 - kSStep + 1) + nG;
+  return !c.comm && c.fused_chain && c.hmapped && nb >= max_cols && cgs2_chain_fits(n, nb, c.n_cus);
+}
+
+double schur_lambda(Ctx& c) {
+  if (c.S_lambda > 0) return c.S_lambda;
+  sell_gershgorin(c.sell(), slot(c, kSlotA), c.stream);
+  c.S_lambda = fetch(c, kSlotA, 1)[0];
+  if (!(c.S_lambda > 0)) c.S_lambda = 1.0;
+  return c.S_lambda;
+}
+
+State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl,
+                                std::vector<double*>& tv, int n_tmp) {
+  const int n = c.n_p;
+  const Seg g = c.seg_p();
+  const int restart = n_tmp - 2;
+  if (restart + 1 > kGmMaxDim || restart % kSStep)
+    throw std::runtime_error("gmres_schur_sstep: restart must be a multiple of the block size");
+  ensure_pool(tv, n_tmp + kSStep, size_t(n));
+  double* p = tv[n_tmp - 1];
+  double* wraw[kSStep];
+  for (int i = 0; i < kSStep; ++i) wraw[i] = tv[n_tmp + i];
+  if (!c.gm_report) {
+    c.gm_state.alloc(1);
+    DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.gm_report), 2 * sizeof(GmresReport)));
+    for (auto& ev : c.gm_ev) DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  const std::vector<const double*> ptrs(tv.begin(), tv.begin() + restart);
+  if (ptrs != c.gm_ptrs_host) {
+    c.gm_ptrs.upload(ptrs);
+    c.gm_ptrs_host = ptrs;
+  }
+  GmresDev* dst = c.gm_state.p;
+  const int nb1 = std::min(c.n_cus, 256);
+  // Chebyshev points of [0, lambda] (Leja-like order: outer, inner, ...)
+  const double lam = schur_lambda(c);
+  SStepArgs sa{};
+  const double pi = 3.14159265358979323846;
+  const int order[kSStep] = {0, 3, 1, 2};
+  for (int i = 0; i < kSStep; ++i)
+    sa.theta[i] = 0.5 * lam * (1.0 + std::cos((2.0 * order[i] + 1.0) * pi / (2.0 * kSStep)));
+  sa.sigma = 0.5 * lam;
+  for (int i = 0; i < kSStep; ++i) sa.w[i] = wraw[i];
+  auto enqueue_cycle = [&](int cyc) {
+    sell_spmv(c.sell(), x, 1.0, p, c.stream);
+    sadd(n, -1., 1., b, p, c.stream);
+    gdot(c, g, p, p, kSlotA);
+    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
+    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
+    for (int k = 0; k < restart; k += kSStep) {
+      const double* src = tv[k];
+      for (int i = 0; i < kSStep; ++i) {
+        Timer* e = schur_sample(c);
+        if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
+        sell_spmv_shifted(c.sell(), i == 0 ? src : wraw[i - 1], sa.theta[i], 1.0 / sa.sigma,
+                          wraw[i], &dst->status, c.stream);
+        if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
+      }
+      for (int i = 0; i < kSStep; ++i) sa.q[i] = tv[k + 1 + i];
+      sstep_block(g, chain_vecs(tv, k + 1), sa, k, dst, c.chain_gran.p, nb1, ++c.chain_seq,
+                  chain_err(c), c.stream);
+    }
+    gmres_cycle_end(dst, n, c.gm_ptrs.p, x, &c.gm_report[cyc & 1], c.stream);
+    DCP_HIP_CHECK(hipEventRecord(c.gm_ev[cyc & 1], c.stream));
+  };
+  int cyc = 0;
+  enqueue_cycle(cyc);
+  for (;;) {
+    enqueue_cycle(cyc + 1);
+    DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
+    if (c.gm_report[cyc & 1].status != 0) break;
+    ++cyc;
+  }
+  DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+  check_chain_err(c);
+  const GmresReport& r = c.gm_report[cyc & 1];
+  ctl.last_step = unsigned(r.accumulated);
+  ctl.last_value = r.rho;
+  return r.status == 1 ? kSuccess : kFailure;
+}
+
+State gmres_schur_sstep(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
+                        int n_tmp) {
+  if (!sstep_fits(c, c.seg_p().n, std::min(c.n_cus, 256)))
+    return gmres_schur_cgs2(c, x, b, ctl, tv, n_tmp);
+  if (!c.S_perm.p) return gmres_schur_sstep_ordered(c, x, b, ctl, tv, n_tmp);
+  const int n = c.n_p;
+  gather(n, c.S_perm.p, x, c.sperm_x.p, c.stream);
+  gather(n, c.S_perm.p, b, c.sperm_b.p, c.stream);
+  const State st = gmres_schur_sstep_ordered(c, c.sperm_x.p, c.sperm_b.p, ctl, tv, n_tmp);
+  scatter(n, c.S_perm.p, c.sperm_x.p, x, c.stream);
+  return st;
+}
+
 // deal.II Householder<double>::least_squares on the (m x n) matrix S.
 double householder_least_squares(std::vector<std::vector<double>> S, int m, int n,
                                  std::vector<double>& dst, const std::vector<double>& src) {
@@ -850,6 +957,8 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
       st = gmres(c, np, c.seg_p(), S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit && c.gram_schmidt == 1) {
       st = gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+    } else if (c.schur_explicit && c.gram_schmidt == 3) {
+      st = gmres_schur_sstep(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit && c.gram_schmidt == 2) {
       st = gmres_schur_dcgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit) {

@@ -915,7 +915,7 @@ class Context:
         SolverGMRES, default), "classical2" (CGS2, device-resident cycles) or
         "dcgs2" (delayed CGS2: one reduction per Arnoldi step, device-resident)."""
         self._check(lib().dcp_set_option(self._h, OPT_GRAM_SCHMIDT,
-                                         {"modified": 0, "classical2": 1, "dcgs2": 2}[kind]))
+                                         {"modified": 0, "classical2": 1, "dcgs2": 2, "sstep": 3}[kind]))
 
     def set_element_mfma(self, on: bool):
         """DCP_OPT_ELEMENT_MFMA: True = the velocity-block node-pair sums of the

@@ -192,8 +192,9 @@ def test_operator_applies(setup, explicit, mfree):
 
 
 @pytest.mark.parametrize("explicit,gs", [(True, "modified"), (False, "modified"),
-                                         (True, "classical2"), (True, "dcgs2")],
-                         ids=["S-explicit", "S-composite", "S-explicit-CGS2", "S-explicit-DCGS2"])
+                                         (True, "classical2"), (True, "dcgs2"), (True, "sstep")],
+                         ids=["S-explicit", "S-composite", "S-explicit-CGS2", "S-explicit-DCGS2",
+                              "S-explicit-sstep"])
 def test_full_solve_and_temperature(setup, explicit, gs):
     """One reference time step against the oracle (deal.II's modified
     Gram-Schmidt in the oracle in every case; DCP_OPT_GRAM_SCHMIDT=1 runs the
@@ -241,7 +242,7 @@ def test_full_solve_and_temperature(setup, explicit, gs):
 
 
 @pytest.mark.parametrize("max_outer,gs", [(10, "modified"), (3, "modified"), (3, "classical2"),
-                                          (3, "dcgs2")])
+                                          (3, "dcgs2"), (3, "sstep")])
 def test_fallback_solve_do_solve_A(setup, max_outer, gs):
     """Q10 (boussinesq_model.tpp:1166-1232): the first FGMRES(30) is capped
     (test hook, identical in oracle and GPU) so the reference's fallback runs:
@@ -414,7 +415,7 @@ def test_schur_forced_reorthogonalisation(monkeypatch, force_reorth):
     assert np.linalg.norm(ya[m.n_u:] - yu[m.n_u:]) <= 1e-4 * np.linalg.norm(yu[m.n_u:])
 
 
-@pytest.mark.parametrize("gs", ["classical2", "dcgs2"])
+@pytest.mark.parametrize("gs", ["classical2", "dcgs2", "sstep"])
 def test_cgs2_cycle_is_deterministic_and_orthogonal(gs):
     """DCP_OPT_GRAM_SCHMIDT=1 (CGS2) and 2 (DCGS2): every reduction of the
     device-resident cycle has a fixed shape, so two applies are bitwise equal;
@@ -444,8 +445,9 @@ def test_cgs2_cycle_is_deterministic_and_orthogonal(gs):
     ctx.close()
 
 
-@pytest.mark.parametrize("refine", [1, 2, 3])
-def test_dcgs2_inner_solve_residual(refine):
+@pytest.mark.parametrize("refine,gs", [(1, "dcgs2"), (2, "dcgs2"), (3, "dcgs2"), (1, "sstep"),
+                                      (2, "sstep"), (3, "sstep")])
+def test_dcgs2_inner_solve_residual(refine, gs):
     """DCGS2 (one reduction per Arnoldi step, delayed re-orthogonalisation):
     the inner Schur GMRES result meets the reference's SolverControl rule on
     the true residual, |S y + src_p| <= ~1e-6 |src_p| (the estimate GMRES
@@ -463,11 +465,11 @@ def test_dcgs2_inner_solve_residual(refine):
     x = np.random.default_rng(SEED + 9).uniform(-1, 1, m.n_u + m.n_p)
     x[m.n_u:] -= x[m.n_u:].mean()
     res = {}
-    for kind in ("dcgs2", "modified"):
+    for kind in (gs, "modified"):
         ctx.set_gram_schmidt(kind)
         res[kind] = ctx.block_preconditioner_vmult(x)
     ctx.set_gram_schmidt("modified")
-    yd, idd = res["dcgs2"]
+    yd, idd = res[gs]
     ym, im = res["modified"]
     src = x[m.n_u:]
     r = ctx.schur_vmult(-yd[m.n_u:]) - src
