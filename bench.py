@@ -78,7 +78,7 @@ def parse():
                     help="skip the converging refine-3 step (GMRES outer iter/s)")
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
                     help="explicit: formed S = B D^-1 B^T (default); composite: B^T, Jacobi, B")
-    ap.add_argument("--gram-schmidt", choices=["modified", "classical2", "dcgs2"],
+    ap.add_argument("--gram-schmidt", choices=["modified", "classical2", "dcgs2", "sstep"],
                     default="classical2",
                     help="inner Schur GMRES orthogonalisation: modified (deal.II) or "
                          "classical twice with device-resident cycles (DCP_OPT_GRAM_SCHMIDT)")
@@ -451,7 +451,7 @@ def main():
     # (deal.II's modified Gram-Schmidt is the reference's); at refine >= 6
     # only the device-resident ones (the modified one reads every step back)
     other = []
-    for other_gs in ("modified", "classical2", "dcgs2"):
+    for other_gs in ("modified", "classical2", "dcgs2", "sstep"):
         if other_gs == args.gram_schmidt or (other_gs == "modified" and args.refine >= 6):
             continue
         ctx.set_gram_schmidt(other_gs)
