@@ -613,6 +613,75 @@ __device__ void gmres_column(GmresDev* st, double* h, int kk) {
   for (int t = 0; t <= kk; ++t) st->H[t][kk] = h[t];
 }
 
+// G' = G - C2^T C2 (G: pass-2 Gram sums after C2's d * S coefficients at
+// c2[ncol1..]) and R = chol(G') upper triangular; false if G' is not
+// positive definite (the block lost rank)
+__device__ bool sstep_chol(const double* c2, int d, int ncol1, double (*Rm)[kSStep]) {
+  constexpr int S = kSStep;
+  double G[S][S];
+  int p = 0;
+  for (int i = 0; i < S; ++i)
+    for (int l = i; l < S; ++l) {
+      double gv = c2[ncol1 + p++];
+      for (int j = 0; j < d; ++j) gv -= c2[i * d + j] * c2[l * d + j];
+      G[i][l] = G[l][i] = gv;
+    }
+  bool ok = true;
+  for (int i = 0; i < S; ++i) {
+    double dd = G[i][i];
+    for (int l = 0; l < i; ++l) dd -= Rm[l][i] * Rm[l][i];
+    if (!(dd > 0)) {
+      ok = false;
+      dd = 1.0;
+    }
+    Rm[i][i] = sqrt(dd);
+    for (int l = i + 1; l < S; ++l) {
+      double o = G[i][l];
+      for (int m = 0; m < i; ++m) o -= Rm[m][i] * Rm[m][l];
+      Rm[i][l] = o / Rm[i][i];
+    }
+    for (int l = 0; l < i; ++l) Rm[i][l] = 0.0;
+  }
+  return ok;
+}
+
+// one thread: Hessenberg columns k..k+s-1 from the block's change of basis
+// (c1 + c2 the coefficients on q_0..q_k, Rm the Cholesky factor), into Hr,
+// and their Givens steps / checks
+__device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const double* c1,
+                                 const double* c2, const double (*Rm)[kSStep]) {
+  constexpr int S = kSStep;
+  const int d = k + 1;
+  const int rows = k + S + 1;
+  auto rhat = [&](int r, int c) -> double {  // Rhat (rows x (S+1)): [e_k | [C; R]]
+    if (c == 0) return r == k ? 1.0 : 0.0;
+    if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
+    return Rm[r - k - 1][c - 1];
+  };
+  double Hn[kGmMaxDim + 1][S];
+  for (int c = 0; c < S; ++c) {
+    for (int r = 0; r < rows; ++r) {
+      double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
+      if (r <= k && c > 0)
+        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= st->Hr[r][i] * rhat(i, c);
+      // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular)
+      for (int l = 0; l < c; ++l) x -= Hn[r][l] * rhat(k + l, c);
+      Hn[r][c] = x / rhat(k + c, c);
+    }
+  }
+  double h[kGmMaxDim + 1];
+  for (int c = 0; c < S; ++c) {
+    const int kk = k + c;
+    for (int r = 0; r <= kk + 1; ++r) {
+      st->Hr[r][kk] = Hn[r][c];
+      h[r] = Hn[r][c];
+    }
+    gmres_column(st, h, kk);
+    if (st->status) return;
+  }
+}
+
+
 template <int KL>
 __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs V, SStepArgs a,
                                                                int k, GmresDev* st, double* gran,
@@ -705,33 +774,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   }
   // G' = G - C2^T C2 and its Cholesky factor (every workgroup, the same
   // arithmetic in the same order)
-  if (threadIdx.x == 0) {
-    double G[S][S];
-    int p = 0;
-    for (int i = 0; i < S; ++i)
-      for (int l = i; l < S; ++l) {
-        double gv = c2[ncol1 + p++];
-        for (int j = 0; j < d; ++j) gv -= c2[i * d + j] * c2[l * d + j];
-        G[i][l] = G[l][i] = gv;
-      }
-    int ok = 1;
-    for (int i = 0; i < S; ++i) {
-      double dd = G[i][i];
-      for (int l = 0; l < i; ++l) dd -= Rm[l][i] * Rm[l][i];
-      if (!(dd > 0)) {
-        ok = 0;
-        dd = 1.0;
-      }
-      Rm[i][i] = sqrt(dd);
-      for (int l = i + 1; l < S; ++l) {
-        double o = G[i][l];
-        for (int m = 0; m < i; ++m) o -= Rm[m][i] * Rm[m][l];
-        Rm[i][l] = o / Rm[i][i];
-      }
-      for (int l = 0; l < i; ++l) Rm[i][l] = 0.0;
-    }
-    bad = !ok;
-  }
+  if (threadIdx.x == 0) bad = !sstep_chol(c2, d, ncol1, Rm);
   __syncthreads();
   // q_{k+1+i} = (w_i - sum_{l<i} q_{k+1+l} R[l][i]) / R[i][i]
 #pragma unroll
@@ -751,34 +794,144 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     st->rho = __longlong_as_double(0x7ff8000000000000LL);
     return;
   }
-  // ---- Hessenberg columns k..k+s-1 (raw, into Hr) and their Givens steps
-  const int rows = k + S + 1;
-  auto rhat = [&](int r, int c) -> double {  // Rhat (rows x (S+1)): [e_k | [C; R]]
-    if (c == 0) return r == k ? 1.0 : 0.0;
-    if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
-    return Rm[r - k - 1][c - 1];
-  };
-  double Hn[kGmMaxDim + 1][S];
-  for (int c = 0; c < S; ++c) {
-    for (int r = 0; r < rows; ++r) {
-      double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
-      if (r <= k && c > 0)
-        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= st->Hr[r][i] * rhat(i, c);
-      // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular)
-      for (int l = 0; l < c; ++l) x -= Hn[r][l] * rhat(k + l, c);
-      Hn[r][c] = x / rhat(k + c, c);
+  sstep_hessenberg(st, a, k, c1, c2, Rm);
+}
+
+// Several GPUs: the same block as three launches around two all-reduces of
+// the per-rank sums (one reduction per pass, over the owned entries of Seg g).
+// PASS 0: c1 = V^T w_i; PASS 1: w_i -= V c1 (written back), c2 = V^T w_i and
+// the Gram sums. Each block publishes its sums as granules, the last block
+// adds them per column in block order -> out.
+template <int KL, int PASS>
+__global__ __launch_bounds__(kBlock) void k_ss_dots(Seg g, ChainVecs V, SStepArgs a, int k,
+                                                    const double* __restrict__ cin, double* gran,
+                                                    unsigned* cnt, double* out,
+                                                    unsigned long long seq, double* err,
+                                                    const int* __restrict__ status) {
+  constexpr int K = pow2_at_least<KL>();
+  constexpr int S = kSStep;
+  constexpr int nG = S * (S + 1) / 2;
+  __shared__ double sm[4 * (K > 16 ? K : 16)];
+  __shared__ int is_last;
+  if (*status) return;
+  const int d = k + 1, ncol1 = S * d, ncol = PASS == 0 ? ncol1 : ncol1 + nG;
+  const long k0 = long(blockIdx.x) * (kBlock * kCgsElems) + threadIdx.x;
+  double v[kCgsElems][K], w[kCgsElems][S];
+  long pos[kCgsElems];
+  bool live[kCgsElems];
+#pragma unroll
+  for (int e = 0; e < kCgsElems; ++e) {
+    const long kk = k0 + e * kBlock;
+    live[e] = kk < g.n;
+    pos[e] = live[e] ? seg_pos(g, kk) : 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) w[e][i] = live[e] ? a.w[i][pos[e]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[e][j] = (j < KL && j < d && live[e]) ? V.v[j][pos[e]] : 0.0;
+  }
+  if (PASS == 1) {
+#pragma unroll
+    for (int e = 0; e < kCgsElems; ++e) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+#pragma unroll
+        for (int j = 0; j < KL; ++j)
+          if (j < d) w[e][i] -= cin[i * d + j] * v[e][j];
+        if (live[e]) const_cast<double*>(a.w[i])[pos[e]] = w[e][i];
+      }
     }
   }
-  double h[kGmMaxDim + 1];
-  for (int c = 0; c < S; ++c) {
-    const int kk = k + c;
-    for (int r = 0; r <= kk + 1; ++r) {
-      st->Hr[r][kk] = Hn[r][c];
-      h[r] = Hn[r][c];
-    }
-    gmres_column(st, h, kk);
-    if (st->status) return;
+  const int nb = gridDim.x;
+  const unsigned long long tag = seq * 256;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    double sj[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) sj[j] = v[0][j] * w[0][i] + v[1][j] * w[1][i];
+    const double r = block_sums<K>(sj, d, sm);
+    if (int(threadIdx.x) < d)
+      granule_store(gran + 2 * (size_t(i * d + threadIdx.x) * nb + blockIdx.x), r, tag + 1);
+    __syncthreads();
   }
+  if (PASS == 1) {
+    double sg[16];
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+      for (int l = i; l < S; ++l, ++p) sg[p] = w[0][i] * w[0][l] + w[1][i] * w[1][l];
+#pragma unroll
+    for (; p < 16; ++p) sg[p] = 0.0;
+    const double r = block_sums<16>(sg, nG, sm);
+    if (int(threadIdx.x) < nG)
+      granule_store(gran + 2 * (size_t(ncol1 + threadIdx.x) * nb + blockIdx.x), r, tag + 1);
+  }
+  if (!last_block(cnt, &is_last)) return;
+  // the last block: column c summed over the blocks in block order, one thread per column
+  for (int c = threadIdx.x; c < ncol; c += kBlock) {
+    double t = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      const double* q = gran + 2 * (size_t(c) * nb + b);
+      const unsigned long long* u = reinterpret_cast<const unsigned long long*>(q);
+      const unsigned long long vv = __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long tt = __hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t += tt == ((tag + 1) ^ granule_mix(vv)) ? __longlong_as_double((long long)vv)
+                                               : granule_poll(q, tag + 1, err);
+    }
+    out[c] = t;
+  }
+}
+
+// the last of the three launches: w_i -= V c2, the Cholesky factor of the
+// corrected Gram matrix, q = W R^-1 (owned entries), block 0 the Hessenberg
+// columns and Givens steps
+template <int KL>
+__global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepArgs a, int k,
+                                                     const double* __restrict__ c1g,
+                                                     const double* __restrict__ c2g, GmresDev* st) {
+  constexpr int S = kSStep;
+  __shared__ double c1[S * 32], c2[S * 32 + 16];
+  __shared__ double Rm[S][S];
+  __shared__ int bad;
+  if (st->status) return;
+  const int d = k + 1, ncol1 = S * d;
+  for (int c = threadIdx.x; c < ncol1 + S * (S + 1) / 2; c += kBlock) {
+    if (c < ncol1) c1[c] = c1g[c];
+    c2[c] = c2g[c];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) bad = !sstep_chol(c2, d, ncol1, Rm);
+  __syncthreads();
+  const long k0 = long(blockIdx.x) * (kBlock * kCgsElems) + threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < kCgsElems; ++e) {
+    const long kk = k0 + e * kBlock;
+    if (kk >= g.n) continue;
+    const long pos = seg_pos(g, kk);
+    double w[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      w[i] = a.w[i][pos];
+#pragma unroll
+      for (int j = 0; j < KL; ++j)
+        if (j < d) w[i] -= c2[i * d + j] * V.v[j][pos];
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      double q = w[i];
+#pragma unroll
+      for (int l = 0; l < i; ++l) q -= w[l] * Rm[l][i];
+      w[i] = q / Rm[i][i];
+      a.q[i][pos] = w[i];
+    }
+  }
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (bad) {
+    st->status = 2;
+    st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    return;
+  }
+  sstep_hessenberg(st, a, k, c1, c2, Rm);
 }
 
 }  // namespace
@@ -798,6 +951,42 @@ void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev*
   DCP_SS_CASE(28)
 #undef DCP_SS_CASE
   throw std::runtime_error("sstep_block: basis too long");
+}
+
+void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st,
+                       double* gran, unsigned* cnt, double* c1, double* c2,
+                       unsigned long long& seq, double* err, Comm* comm, hipStream_t s) {
+  ChainVecs Vp = V;
+  for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
+  const int nb = int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  const int ncol1 = kSStep * (k + 1), ncol2 = ncol1 + kSStep * (kSStep + 1) / 2;
+  const int* status = &st->status;
+  if (nb > 0) {
+#define DCP_SSM(KL)                                                                              \
+  if (k + 1 <= KL) {                                                                             \
+    hipLaunchKernelGGL((k_ss_dots<KL, 0>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, nullptr,   \
+                       gran, cnt, c1, ++seq, err, status);                                       \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    if (comm) comm->allreduce(c1, size_t(ncol1), false, s);                                      \
+    hipLaunchKernelGGL((k_ss_dots<KL, 1>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, gran, \
+                       cnt, c2, ++seq, err, status);                                             \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    if (comm) comm->allreduce(c2, size_t(ncol2), false, s);                                      \
+    hipLaunchKernelGGL((k_ss_final<KL>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, c2, st); \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    return;                                                                                      \
+  }
+    DCP_SSM(4) DCP_SSM(8) DCP_SSM(12) DCP_SSM(16) DCP_SSM(20) DCP_SSM(24) DCP_SSM(28)
+#undef DCP_SSM
+    throw std::runtime_error("sstep_block_multi: basis too long");
+  }
+  // no owned entries on this rank: still take part in the all-reduces
+  if (comm) {
+    DCP_HIP_CHECK(hipMemsetAsync(c1, 0, size_t(ncol1) * sizeof(double), s));
+    comm->allreduce(c1, size_t(ncol1), false, s);
+    DCP_HIP_CHECK(hipMemsetAsync(c2, 0, size_t(ncol2) * sizeof(double), s));
+    comm->allreduce(c2, size_t(ncol2), false, s);
+  }
 }
 
 size_t cgs2_granules(long n) {

@@ -745,7 +745,9 @@ State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::ve
 // symmetric positive semi-definite: the shifts are the Chebyshev points of
 // [0, lambda] with lambda the Gershgorin bound of the stored S, sigma =
 // lambda / 2, so the basis polynomials stay bounded on the spectrum. Falls back
-// to CGS2 when the block does not fit the resident grid or on several GPUs.
+// to the three-launch block (sstep_block_multi: per-rank sums all-reduced
+// between launches) on several GPUs or when the block does not fit the
+// resident grid.
 bool sstep_fits(const Ctx& c, long n, int nb) {
   constexpr int nG = kSStep * (kSStep + 1) / 2;
   const int max_cols = kSStep * (kGmMaxDim - 1 - kSStep + 1) + nG;
@@ -755,6 +757,7 @@ bool sstep_fits(const Ctx& c, long n, int nb) {
 double schur_lambda(Ctx& c) {
   if (c.S_lambda > 0) return c.S_lambda;
   sell_gershgorin(c.sell(), slot(c, kSlotA), c.stream);
+  allreduce(c, slot(c, kSlotA), 1, true);  // every rank the same shifts
   c.S_lambda = fetch(c, kSlotA, 1)[0];
   if (!(c.S_lambda > 0)) c.S_lambda = 1.0;
   return c.S_lambda;
@@ -783,6 +786,20 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   }
   GmresDev* dst = c.gm_state.p;
   const int nb1 = std::min(c.n_cus, 256);
+  Comm* comm = c.comm.get();
+  const bool fused = sstep_fits(c, g.n, nb1);
+  if (!fused) {
+    const size_t pn = 2 * size_t(128) * size_t((g.n + 511) / 512) + 2;
+    if (c.gm_part.n < pn) {
+      c.gm_part.alloc(pn);
+      c.gm_part.zero(c.stream);  // tag 0: never waited for
+    }
+    if (!c.gm_cnt.p) {
+      c.gm_cnt.alloc(1);
+      c.gm_cnt.zero(c.stream);
+    }
+    if (!c.ss_c.p) c.ss_c.alloc(2 * 160);
+  }
   // Chebyshev points of [0, lambda] (Leja-like order: outer, inner, ...)
   const double lam = schur_lambda(c);
   SStepArgs sa{};
@@ -793,7 +810,10 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   sa.sigma = 0.5 * lam;
   for (int i = 0; i < kSStep; ++i) sa.w[i] = wraw[i];
   auto enqueue_cycle = [&](int cyc) {
-    sell_spmv(c.sell(), x, 1.0, p, c.stream);
+    if (c.S_perm.p)
+      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
+    else
+      schur_vmult(c, x, p);
     sadd(n, -1., 1., b, p, c.stream);
     gdot(c, g, p, p, kSlotA);
     gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
@@ -801,19 +821,27 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
     for (int k = 0; k < restart; k += kSStep) {
       const double* src = tv[k];
       for (int i = 0; i < kSStep; ++i) {
+        const double* in = i == 0 ? src : wraw[i - 1];
+        halo_exchange(c, c.halo_p, const_cast<double*>(in));
         Timer* e = schur_sample(c);
         if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-        sell_spmv_shifted(c.sell(), i == 0 ? src : wraw[i - 1], sa.theta[i], 1.0 / sa.sigma,
-                          wraw[i], &dst->status, c.stream);
+        sell_spmv_shifted(c.sell(), in, sa.theta[i], 1.0 / sa.sigma, wraw[i], &dst->status,
+                          c.stream);
         if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
       }
       for (int i = 0; i < kSStep; ++i) sa.q[i] = tv[k + 1 + i];
-      sstep_block(g, chain_vecs(tv, k + 1), sa, k, dst, c.chain_gran.p, nb1, ++c.chain_seq,
-                  chain_err(c), c.stream);
+      if (fused)
+        sstep_block(g, chain_vecs(tv, k + 1), sa, k, dst, c.chain_gran.p, nb1, ++c.chain_seq,
+                    chain_err(c), c.stream);
+      else
+        sstep_block_multi(g, chain_vecs(tv, k + 1), sa, k, dst, c.gm_part.p, c.gm_cnt.p, c.ss_c.p,
+                          c.ss_c.p + 160, c.chain_seq, comm ? slot(c, kSlotErr) : chain_err(c),
+                          comm, c.stream);
     }
     gmres_cycle_end(dst, n, c.gm_ptrs.p, x, &c.gm_report[cyc & 1], c.stream);
     DCP_HIP_CHECK(hipEventRecord(c.gm_ev[cyc & 1], c.stream));
   };
+  if (comm) fill(1, 0.0, slot(c, kSlotErr), c.stream);
   int cyc = 0;
   enqueue_cycle(cyc);
   for (;;) {
@@ -823,7 +851,13 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
     ++cyc;
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
-  check_chain_err(c);
+  if (!comm) {
+    check_chain_err(c);
+  } else {
+    allreduce(c, slot(c, kSlotErr), 1, true);
+    if (fetch(c, kSlotErr, 1)[0] != 0.0)
+      throw std::runtime_error("s-step block: a workgroup timed out waiting for a hand-off");
+  }
   const GmresReport& r = c.gm_report[cyc & 1];
   ctl.last_step = unsigned(r.accumulated);
   ctl.last_value = r.rho;
@@ -832,8 +866,6 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
 
 State gmres_schur_sstep(Ctx& c, double* x, const double* b, Control& ctl, std::vector<double*>& tv,
                         int n_tmp) {
-  if (!sstep_fits(c, c.seg_p().n, std::min(c.n_cus, 256)))
-    return gmres_schur_cgs2(c, x, b, ctl, tv, n_tmp);
   if (!c.S_perm.p) return gmres_schur_sstep_ordered(c, x, b, ctl, tv, n_tmp);
   const int n = c.n_p;
   gather(n, c.S_perm.p, x, c.sperm_x.p, c.stream);

@@ -139,7 +139,7 @@ def _time_step(ctx, m, u, T):
 @pytest.mark.parametrize("world,refine,gs", [(2, 2, "modified"), (3, 2, "modified"),
                                              (4, 2, "modified"), (2, 2, "classical2"),
                                              (3, 2, "classical2"), (2, 2, "dcgs2"),
-                                             (3, 2, "dcgs2")])
+                                             (3, 2, "dcgs2"), (2, 2, "sstep"), (3, 2, "sstep")])
 def test_group_time_step_matches_single_gpu(world, refine, gs):
     """(At r = 3 this random state drives the reference's inner Schur GMRES
     into its 5000-iteration cap on one GPU and on every partition alike.)

@@ -476,3 +476,29 @@ def test_dcgs2_inner_solve_residual(refine, gs):
     assert np.linalg.norm(r) <= 1.05e-6 * np.linalg.norm(src)
     assert abs(idd - im) <= max(3, 0.10 * im)
     ctx.close()
+
+
+def test_sstep_three_launch_block_matches_fused():
+    """The s-step block in its three-launch form (several GPUs, or a basis that
+    does not fit the resident grid; here forced with DCP_OPT_FUSED_CHAIN = 0)
+    against the one-launch block: the same Krylov process and stopping column,
+    results equal to rounding."""
+    m = dcp.HostMesh(refine=2)
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.classic_physics())
+    ctx.upload_mesh(m)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
+    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    x = np.random.default_rng(SEED + 13).uniform(-1, 1, m.n_u + m.n_p)
+    x[m.n_u:] -= x[m.n_u:].mean()
+    ctx.set_gram_schmidt("sstep")
+    yf, itf = ctx.block_preconditioner_vmult(x)
+    ctx.set_fused_chain(False)
+    ym, itm = ctx.block_preconditioner_vmult(x)
+    ctx.set_fused_chain(True)
+    ctx.set_gram_schmidt("modified")
+    assert abs(itf - itm) <= max(2, 0.05 * itf)
+    assert np.linalg.norm(ym[m.n_u:] - yf[m.n_u:]) <= 1e-4 * np.linalg.norm(yf[m.n_u:])
+    ctx.close()
