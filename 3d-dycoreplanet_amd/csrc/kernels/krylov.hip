@@ -587,31 +587,6 @@ namespace {
 
 constexpr int kSsRes = 2 * 128 * 256;  // result granules after the partial area
 
-// column kk of SolverGMRES's Givens QR from the raw Hessenberg column h[0..kk+1]
-__device__ void gmres_column(GmresDev* st, double* h, int kk) {
-  // one thread
-  for (int i = 0; i < kk; i++) {
-    const double dummy = h[i];
-    h[i] = st->ci[i] * dummy + st->si[i] * h[i + 1];
-    h[i + 1] = -st->si[i] * dummy + st->ci[i] * h[i + 1];
-  }
-  const double r = 1. / sqrt(h[kk] * h[kk] + h[kk + 1] * h[kk + 1]);
-  const double sn = h[kk + 1] * r, cn = h[kk] * r;
-  st->si[kk] = sn;
-  st->ci[kk] = cn;
-  h[kk] = cn * h[kk] + sn * h[kk + 1];
-  const double g0 = st->gamma[kk];
-  const double gk1 = -sn * g0;
-  st->gamma[kk + 1] = gk1;
-  st->gamma[kk] = g0 * cn;
-  const int acc = st->accumulated + 1;
-  st->accumulated = acc;
-  st->dim = kk + 1;
-  const double rho = fabs(gk1);
-  st->rho = rho;
-  st->status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
-  for (int t = 0; t <= kk; ++t) st->H[t][kk] = h[t];
-}
 
 // G' = G - C2^T C2 (G: pass-2 Gram sums after C2's d * S coefficients at
 // c2[ncol1..]) and R = chol(G') upper triangular; false if G' is not
@@ -645,42 +620,100 @@ __device__ bool sstep_chol(const double* c2, int d, int ncol1, double (*Rm)[kSSt
   return ok;
 }
 
-// one thread: Hessenberg columns k..k+s-1 from the block's change of basis
-// (c1 + c2 the coefficients on q_0..q_k, Rm the Cholesky factor), into Hr,
-// and their Givens steps / checks
+// Hessenberg columns k..k+s-1 from the block's change of basis (c1 + c2 the
+// coefficients on q_0..q_k, Rm the Cholesky factor) into Hr, then their
+// Givens steps / checks. Called by every thread of one workgroup: the old
+// columns, rotations and gamma are staged in LDS, a thread per row forms the
+// new columns (rows are independent: H_new U = X row by row), and one thread
+// runs the sequential Givens updates on LDS data.
 __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const double* c1,
                                  const double* c2, const double (*Rm)[kSStep]) {
   constexpr int S = kSStep;
+  __shared__ double Hs[kGmMaxDim + 1][kGmMaxDim];
+  __shared__ double Hn[kGmMaxDim + 1][S];
+  __shared__ double cs[kGmMaxDim], sn[kGmMaxDim], gam[kGmMaxDim + 1];
+  __shared__ double Hrot[kGmMaxDim + 1][S];
+  __shared__ int last_col, acc0;
   const int d = k + 1;
   const int rows = k + S + 1;
+  const int t = threadIdx.x, nt = blockDim.x;
+  for (int e = t; e < d * k; e += nt) Hs[e / k][e % k] = st->Hr[e / k][e % k];
+  for (int i = t; i < k; i += nt) {
+    cs[i] = st->ci[i];
+    sn[i] = st->si[i];
+  }
+  if (t == 0) {
+    gam[k] = st->gamma[k];
+    acc0 = st->accumulated;
+  }
+  __syncthreads();
   auto rhat = [&](int r, int c) -> double {  // Rhat (rows x (S+1)): [e_k | [C; R]]
     if (c == 0) return r == k ? 1.0 : 0.0;
     if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
     return Rm[r - k - 1][c - 1];
   };
-  double Hn[kGmMaxDim + 1][S];
-  for (int c = 0; c < S; ++c) {
-    for (int r = 0; r < rows; ++r) {
+  if (t < rows) {
+    const int r = t;
+    double hrow[S];
+    for (int c = 0; c < S; ++c) {
       double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
       if (r <= k && c > 0)
-        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= st->Hr[r][i] * rhat(i, c);
+        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= Hs[r][i] * rhat(i, c);
       // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular)
-      for (int l = 0; l < c; ++l) x -= Hn[r][l] * rhat(k + l, c);
-      Hn[r][c] = x / rhat(k + c, c);
+      for (int l = 0; l < c; ++l) x -= hrow[l] * rhat(k + l, c);
+      hrow[c] = x / rhat(k + c, c);
+      Hn[r][c] = hrow[c];
     }
   }
-  double h[kGmMaxDim + 1];
-  for (int c = 0; c < S; ++c) {
-    const int kk = k + c;
-    for (int r = 0; r <= kk + 1; ++r) {
-      st->Hr[r][kk] = Hn[r][c];
-      h[r] = Hn[r][c];
+  __syncthreads();
+  if (t == 0) {
+    int acc = acc0;
+    last_col = S - 1;
+    for (int c = 0; c < S; ++c) {
+      const int kk = k + c;
+      // rotate the raw column in LDS (Hrot), carrying h[i+1] in a register
+      double hi = Hn[0][c];
+      for (int i = 0; i < kk; i++) {
+        const double hn = Hn[i + 1][c];
+        Hrot[i][c] = cs[i] * hi + sn[i] * hn;
+        hi = -sn[i] * hi + cs[i] * hn;
+      }
+      const double hk1 = Hn[kk + 1][c];
+      const double r = 1. / sqrt(hi * hi + hk1 * hk1);
+      const double s_ = hk1 * r, c_ = hi * r;
+      sn[kk] = s_;
+      cs[kk] = c_;
+      Hrot[kk][c] = c_ * hi + s_ * hk1;
+      const double g0 = gam[kk];
+      gam[kk + 1] = -s_ * g0;
+      gam[kk] = g0 * c_;
+      ++acc;
+      const double rho = fabs(gam[kk + 1]);
+      const int status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+      if (status || c == S - 1) {
+        st->accumulated = acc;
+        st->dim = kk + 1;
+        st->rho = rho;
+        st->status = status;
+        last_col = c;
+        break;
+      }
     }
-    gmres_column(st, h, kk);
-    if (st->status) return;
   }
+  __syncthreads();
+  const int nc = last_col + 1;
+  // write back: raw and rotated columns, rotations, gamma
+  for (int e = t; e < rows * nc; e += nt) {
+    const int r = e / nc, c = e % nc, kk = k + c;
+    if (r <= kk + 1) st->Hr[r][kk] = Hn[r][c];
+    if (r <= kk) st->H[r][kk] = Hrot[r][c];
+  }
+  for (int c = t; c < nc; c += nt) {
+    st->ci[k + c] = cs[k + c];
+    st->si[k + c] = sn[k + c];
+  }
+  for (int i = t; i <= nc; i += nt) st->gamma[k + i] = gam[k + i];
 }
-
 
 template <int KL>
 __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs V, SStepArgs a,
@@ -727,20 +760,17 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
       if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
     }
     if (pass == 1) {
-      double pr[kChainEntries][16];
+      // Gram sums w_i . w_l (l >= i): row i of W^T W as a 4-wide block sum,
+      // so only the 4 w entries are live next to the basis
 #pragma unroll
-      for (int e = 0; e < kChainEntries; ++e) {
-        int p = 0;
-#pragma unroll
-        for (int i = 0; i < S; ++i)
-#pragma unroll
-          for (int l = i; l < S; ++l) pr[e][p++] = w[e][i] * w[e][l];
-#pragma unroll
-        for (; p < 16; ++p) pr[e][p] = 0.0;
+      for (int i = 0; i < S; ++i) {
+        const double x[kChainEntries] = {w[0][i], w[1][i]};
+        const double r = chain_block_sums<S>(w, x, S, sm16 + (i & 1) * kChainWaves * S);
+        const int l = threadIdx.x;
+        if (l >= i && l < S)
+          granule_store(part + 2 * (size_t(ncol1 + i * S - i * (i - 1) / 2 + (l - i)) * nb + b), r,
+                        tag);
       }
-      const double one[kChainEntries] = {1.0, 1.0};
-      const double r = chain_block_sums<16>(pr, one, nG, sm16);
-      if (int(threadIdx.x) < nG) granule_store(part + 2 * (size_t(ncol1 + threadIdx.x) * nb + b), r, tag);
     }
     // workgroup c reduces column c and publishes the total
     if (b < ncol && threadIdx.x < 64) {
@@ -763,13 +793,22 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     }
     __syncthreads();
     const double* h = pass == 0 ? c1 : c2;
+    // basis vector by basis vector: the compiler barrier keeps the LDS loads of
+    // the 4 coefficients of vector j next to their use (hoisting all 4 KL of
+    // them spills the basis out of registers)
 #pragma unroll
-    for (int e = 0; e < kChainEntries; ++e)
+    for (int j = 0; j < KL; ++j) {
+      if (j < d) {
+        double hj[S];
 #pragma unroll
-      for (int i = 0; i < S; ++i)
+        for (int i = 0; i < S; ++i) hj[i] = h[i * d + j];
 #pragma unroll
-        for (int j = 0; j < KL; ++j)
-          if (j < d) w[e][i] -= h[i * d + j] * v[e][j];
+        for (int e = 0; e < kChainEntries; ++e)
+#pragma unroll
+          for (int i = 0; i < S; ++i) w[e][i] -= hj[i] * v[e][j];
+      }
+      asm volatile("" ::: "memory");
+    }
     __syncthreads();
   }
   // G' = G - C2^T C2 and its Cholesky factor (every workgroup, the same
@@ -788,10 +827,12 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
       if (live[e]) a.q[i][pos[e]] = w[e][i];
     }
   }
-  if (b != 0 || threadIdx.x != 0) return;
+  if (b != 0) return;
   if (bad) {  // the block lost rank: a breakdown the one-vector process would not see
-    st->status = 2;
-    st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    if (threadIdx.x == 0) {
+      st->status = 2;
+      st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    }
     return;
   }
   sstep_hessenberg(st, a, k, c1, c2, Rm);
@@ -925,10 +966,12 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
       a.q[i][pos] = w[i];
     }
   }
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (blockIdx.x != 0) return;
   if (bad) {
-    st->status = 2;
-    st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    if (threadIdx.x == 0) {
+      st->status = 2;
+      st->rho = __longlong_as_double(0x7ff8000000000000LL);
+    }
     return;
   }
   sstep_hessenberg(st, a, k, c1, c2, Rm);

@@ -35,7 +35,10 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
-PMC_SUMMARIES = {(5, "explicit"): ("profiles/r01_pmc_schur_sell16_r5.json", "k_sell_spmv<true, true>")}
+PMC_SUMMARIES = {(5, "explicit"): ("profiles/r03a_pmc_inner_r5.json", "k_sell_spmv<true, true>")}
+# rocprofv3 --kernel-trace --stats of the same bench (durations of the CGS2
+# chain launches, for the orthogonalisation roofline)
+CHAIN_STATS = {5: "profiles/r03a_bench_r5_kernel_stats.csv"}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
 PMC_MF = {5: ("profiles/r02_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
 
@@ -52,16 +55,51 @@ def pmc_mf_traffic(refine):
     return sum(parts) if all(parts) else None
 
 
-def pmc_traffic(refine, mode):
+def pmc_traffic(refine, mode, n_p):
     """HBM bytes per launch of the roofline kernel from the committed PMC
-    summary of the same workload, or None when none was collected."""
+    summary of the same workload, or None when none was collected. The
+    summary's traffic_bytes is 2 FETCH + WRITE (gfx950 FETCH_SIZE counts half
+    of wide coalesced streaming reads); the gathered x (8 n_p bytes, short
+    scattered reads counted in full) is taken back out of the doubling."""
     ent = PMC_SUMMARIES.get((refine, mode))
     if ent is None or not os.path.exists(os.path.join(ROOT, ent[0])):
         return None
     with open(os.path.join(ROOT, ent[0])) as f:
         tb = json.load(f)["traffic_bytes"]
     hits = [v for k, v in tb.items() if ent[1] in k]
-    return hits[0] if hits else None
+    return hits[0] - 8.0 * n_p if hits else None
+
+
+def chain_roofline(refine, n_p):
+    """The fused CGS2 chain (k_cgs2_chain<KL>, one launch per Arnoldi column)
+    from the committed kernel statistics: algorithmic bytes of column k are the
+    k+1 basis vectors read twice-free (one pass, registers) + w read + q
+    written = (k + 3) 8 n_p; template KL serves k = KL-4..KL-1, so a launch
+    averages (KL + 0.5) 8 n_p bytes. Bound: HBM, although at this size the
+    basis sits in the 256 MB MALL and the launch is hand-off latency bound."""
+    path = CHAIN_STATS.get(refine)
+    if path is None or not os.path.exists(os.path.join(ROOT, path)):
+        return None
+    import csv
+    rows = []
+    with open(os.path.join(ROOT, path)) as f:
+        for r in csv.DictReader(f):
+            name = r["Name"]
+            if "k_cgs2_chain<" not in name:
+                continue
+            kl = int(name.split("k_cgs2_chain<")[1].split(",")[0])
+            rows.append((kl, int(r["Calls"]), float(r["AverageNs"])))
+    if not rows:
+        return None
+    per = {kl: {"bytes": (kl + 0.5) * 8 * n_p, "avg_us": ns * 1e-3,
+                "achieved": (kl + 0.5) * 8 * n_p / (ns * 1e-9) / 1e9} for kl, _, ns in rows}
+    tot_b = sum(calls * (kl + 0.5) * 8 * n_p for kl, calls, _ in rows)
+    tot_t = sum(calls * ns * 1e-9 for _, calls, ns in rows)
+    ach = tot_b / tot_t / 1e9
+    return {"kernel": "fused CGS2 orthogonalisation chain k_cgs2_chain<KL> (one launch per "
+                      "inner Arnoldi column)", "bound": "hbm", "source": path,
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "per_template": per}
 
 
 def parse():
@@ -563,9 +601,12 @@ def main():
         "roofline": {"kernel": kernel, "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc_traffic(args.refine, args.schur),
+                     "traffic": pmc_traffic(args.refine, args.schur, m.n_p)
+                     if world == 1 else None,
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
+    if args.schur == "explicit" and world == 1 and args.gram_schmidt == "classical2":
+        out["roofline_chain"] = chain_roofline(args.refine, m.n_p)
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
     # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point
     # (SURVEY's unit of work; the kernel recomputes the geometry instead of
