@@ -2723,6 +2723,7 @@ struct dcp_host_mesh {
   TemperatureDofs tdofs;
   std::vector<int32_t> cell_nse;
   std::vector<double> nse_xyz;     // support point of each velocity node once renumbered
+  bool renumbered = false;         // the NSE dofs no longer follow the mesh's node ids
   std::unique_ptr<FeecDofs> feec;  // built on first request
   // the 2D shell (dcp_host_mesh2d_create); the members above stay empty
   struct Two {
@@ -2787,6 +2788,47 @@ int dcp_host_mesh_renumber_cuthill_mckee(dcp_host_mesh* h) {
     for (int n = 0; n < m.n_vnodes; ++n)
       for (int k = 0; k < 3; ++k) xyz[3 * size_t(nw[n]) + k] = src[3 * size_t(n) + k];
     h->nse_xyz.swap(xyz);
+    h->renumbered = true;
+    return DCP_OK;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return DCP_ERR_INVALID;
+  }
+}
+
+int dcp_host_mesh_renumber_dealii(dcp_host_mesh* h, int32_t* cell_order) {
+  if (!h) return DCP_ERR_INVALID;
+  try {
+    if (h->two)
+      throw std::invalid_argument("the 2D shell is already in deal.II's order (hyper_shell<2>)");
+    if (h->renumbered) throw std::invalid_argument("renumber to deal.II's order before Cuthill-McKee");
+    if (h->feec) throw std::invalid_argument("renumber before requesting the FEEC topology");
+    const Mesh& m = h->mesh;
+    std::vector<int32_t> cells;
+    const std::vector<int32_t> nw = dealii_shell_node_order(m, cell_order ? &cells : nullptr);
+    const std::vector<int32_t> map = nse_dof_map(m.n_cells, h->cell_nse.data(), m.n_vnodes, m.n_p(), nw);
+    for (int32_t& d : h->cell_nse) d = map[d];
+    h->nse = renumber_constraints(h->nse, map);
+    std::vector<double> xyz(m.xyz.size());
+    for (int n = 0; n < m.n_vnodes; ++n)
+      for (int k = 0; k < 3; ++k) xyz[3 * size_t(nw[n]) + k] = m.xyz[3 * size_t(n) + k];
+    h->nse_xyz.swap(xyz);
+    // temperature: distribute_dofs of FE_Q(1|2) alone, the same first-encounter
+    // order over the same cells, i.e. the order of the support points' new numbers
+    TemperatureDofs& td = h->tdofs;
+    std::vector<int32_t> byn(size_t(td.n_dofs));
+    for (int d = 0; d < td.n_dofs; ++d) byn[d] = d;
+    std::sort(byn.begin(), byn.end(),
+              [&](int32_t a, int32_t b) { return nw[td.dof_vnode[a]] < nw[td.dof_vnode[b]]; });
+    std::vector<int32_t> tmap(size_t(td.n_dofs)), vn(size_t(td.n_dofs));
+    for (int r = 0; r < td.n_dofs; ++r) {
+      tmap[byn[r]] = r;
+      vn[r] = td.dof_vnode[byn[r]];
+    }
+    for (int32_t& d : td.cell_dofs) d = tmap[d];
+    td.dof_vnode.swap(vn);
+    h->T = renumber_constraints(h->T, tmap);
+    if (cell_order) std::copy(cells.begin(), cells.end(), cell_order);
     return DCP_OK;
   } catch (const std::exception& e) {
     g_last_error = e.what();

@@ -1,5 +1,5 @@
 // dcp_aquaplanet -p <file.prm> [--refine R] [--max-steps N] [--device D]
-//                [--output DIR [--output-stem NAME]]
+//                [--output DIR [--output-stem NAME]] [--dof-order dealii|mesh]
 //
 // The reference executable (source/main.cxx: parse -p, construct the model
 // from the parameter file, run()) over libdcp.so: CoreModelData::Parameters
@@ -7,6 +7,8 @@
 // and constraints (setup_dofs, dcp_host_mesh_create; Cuthill-McKee for the
 // Schur-complement solver), the initial temperature,
 // then the time loop (dcp_run) with the reference's per-step log lines.
+// --dof-order: the 3D shell's dofs in deal.II's distribute_dofs order
+// (default; dcp_host_mesh_renumber_dealii) or the mesh's own tree order.
 // --output: output_results (boussinesq_model.tpp:1566-1680) before the loop
 // and after every step, DIR/NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu (classic).
 // Single GPU; the multi-GPU path is driven through the same ABI by one process
@@ -102,6 +104,7 @@ int print_step(void* user, const dcp_run_report* r) {
 int main(int argc, char** argv) {
   std::string prm, out_dir, out_stem = "boussinesq";
   int refine = -1, max_steps = 0, device = 0;
+  bool dealii_order = true;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "-p" && i + 1 < argc) {
@@ -116,6 +119,13 @@ int main(int argc, char** argv) {
       out_dir = argv[++i];
     } else if (a == "--output-stem" && i + 1 < argc) {
       out_stem = argv[++i];
+    } else if (a == "--dof-order" && i + 1 < argc) {
+      const std::string o = argv[++i];
+      if (o != "dealii" && o != "mesh") {
+        std::fprintf(stderr, "Error: --dof-order must be dealii or mesh\n");
+        return 1;
+      }
+      dealii_order = o == "dealii";
     } else {
       std::fprintf(stderr, "Unknown command line option: %s\n", a.c_str());
       return 1;
@@ -149,6 +159,10 @@ int main(int argc, char** argv) {
             : dcp_host_mesh_create(rp.physics.cuboid, rp.initial_global_refinement, rp.R0, rp.R1,
                                    rp.length, rp.physics.temperature_degree, 0, 0);
   if (!m) return fail("mesh", nullptr);
+  // setup_dofs (:197-206): distribute_dofs in deal.II's cell order (the 2D
+  // shell is built in it; the 3D shell is renumbered to it)
+  if (!two_d && !rp.physics.cuboid && dealii_order && dcp_host_mesh_renumber_dealii(m, nullptr) != DCP_OK)
+    return fail("deal.II dof order", nullptr);
   // setup_dofs (:198-204): Cuthill_McKee before component_wise for the Schur solver
   if (!feec && rp.use_schur_complement_solver && dcp_host_mesh_renumber_cuthill_mckee(m) != DCP_OK)
     return fail("renumbering", nullptr);

@@ -78,6 +78,40 @@ void number_nodes(Mesh& m, size_t n_keys, KeyFn key_of, std::vector<int32_t>& ke
     }
 }
 
+// Panels of the cube (outward normal n, tangents e1, e2 with e1 x e2 = n), so
+// that (xi, eta, zeta) = (e1, e2, radial) is right-handed in every cell.
+constexpr int kShellPanel[6][3][3] = {
+    {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}},    // +x
+    {{-1, 0, 0}, {0, 0, 1}, {0, 1, 0}},   // -x
+    {{0, 1, 0}, {0, 0, 1}, {1, 0, 0}},    // +y
+    {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}},   // -y
+    {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}},    // +z
+    {{0, 0, -1}, {0, 1, 0}, {1, 0, 0}}};  // -z
+
+size_t shell_key_of_point(int N, const int P[3], int t) {
+  const size_t L2 = size_t(2 * N + 1);
+  return ((size_t(P[0] + N) * L2 + size_t(P[1] + N)) * L2 + size_t(P[2] + N)) * L2 + size_t(t);
+}
+
+// Global key of Q2 lattice node `lex` of shell cell c: the integer point P on
+// the cube surface [-N,N]^3 (Q2 lattice units) the node's direction comes
+// from, plus its radial lattice index t (0 = inner sphere).
+void shell_surf_point(int N, int refine, int c, int lex, int P[3], int& t) {
+  const int p = c / (N * N * N);
+  int i, j, k;
+  demorton(uint32_t(c % (N * N * N)), refine, i, j, k);
+  const int a = 2 * i + lex % 3, b = 2 * j + (lex / 3) % 3;
+  t = 2 * k + lex / 9;
+  for (int d = 0; d < 3; ++d)
+    P[d] = N * kShellPanel[p][0][d] + (a - N) * kShellPanel[p][1][d] + (b - N) * kShellPanel[p][2][d];
+}
+
+size_t shell_node_key(int N, int refine, int c, int lex) {
+  int P[3], t;
+  shell_surf_point(N, refine, c, lex, P, t);
+  return shell_key_of_point(N, P, t);
+}
+
 }  // namespace
 
 Mesh build_shell(int refine, double R0, double R1, bool mapping_q_on_all_cells) {
@@ -90,31 +124,13 @@ Mesh build_shell(int refine, double R0, double R1, bool mapping_q_on_all_cells) 
   m.R1 = R1;
   const int N = m.N, L2 = 2 * N + 1;  // Q2 lattice points per edge
   m.n_cells = 6 * N * N * N;
-  // Panels of the cube (outward normal n, tangents e1, e2 with e1 x e2 = n), so
-  // that (xi, eta, zeta) = (e1, e2, radial) is right-handed in every cell.
-  static const int panel[6][3][3] = {
-      {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}},    // +x
-      {{-1, 0, 0}, {0, 0, 1}, {0, 1, 0}},   // -x
-      {{0, 1, 0}, {0, 0, 1}, {1, 0, 0}},    // +y
-      {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}},   // -y
-      {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}},    // +z
-      {{0, 0, -1}, {0, 1, 0}, {1, 0, 0}}};  // -z
+  const int (&panel)[6][3][3] = kShellPanel;
   // Global key: integer point P on the cube surface [-N,N]^3 plus radial index t.
   const size_t n_keys = size_t(L2) * L2 * L2 * L2;
   auto surf_point = [&](int c, int lex, int P[3], int& t) {
-    const int p = c / (N * N * N);
-    int i, j, k;
-    demorton(uint32_t(c % (N * N * N)), refine, i, j, k);
-    const int a = 2 * i + lex % 3, b = 2 * j + (lex / 3) % 3;
-    t = 2 * k + lex / 9;
-    for (int d = 0; d < 3; ++d)
-      P[d] = N * panel[p][0][d] + (a - N) * panel[p][1][d] + (b - N) * panel[p][2][d];
+    shell_surf_point(N, refine, c, lex, P, t);
   };
-  auto key_of = [&](int c, int lex) {
-    int P[3], t;
-    surf_point(c, lex, P, t);
-    return ((size_t(P[0] + N) * L2 + size_t(P[1] + N)) * L2 + size_t(P[2] + N)) * L2 + size_t(t);
-  };
+  auto key_of = [&](int c, int lex) { return shell_node_key(N, refine, c, lex); };
   std::vector<int32_t> key_node;
   number_nodes(m, n_keys, key_of, key_node);
   m.cell_coarse.resize(m.n_cells);
@@ -623,6 +639,76 @@ std::vector<int32_t> nse_cell_dofs_dealii(const Mesh& m) {
                                                  : nu + m.cell_q1[8 * size_t(c) + s.lex];
     }
   return out;
+}
+
+// deal.II's DoF order on the 6-cell hyper_shell (setup_dofs,
+// boussinesq_model.tpp:197-206): GridGenerator::hyper_shell(n_cells = 6) of
+// deal.II 9.2 (grid_generator.cc, not in this image; restated, unpinned) takes
+// the 8 corners of [-1,1]^3 (x fastest) scaled to the inner radius as vertices
+// 0-7 and to the outer radius as 8-15, and the cells
+//   bottom {8,9,10,11,0,1,2,3}, right {9,11,1,3,13,15,5,7}, top {12,13,4,5,14,15,6,7},
+//   left {8,0,10,2,12,4,14,6}, front {8,9,0,1,12,13,4,5}, back {10,2,11,3,14,6,15,7}.
+// refine_global puts the 8 children of a cell (child index x + 2y + 4z in the
+// parent's frame) consecutively on the next level in parent order, so the
+// active cells of level r are each coarse cell's Morton order. distribute_dofs
+// numbers a cell's unseen vertices, lines, faces, interior in that order
+// (FE_Q(2)'s hierarchic order); component_wise({0,0,0,1}) then keeps the
+// velocity dofs in that order (3 per node) and moves the pressure behind them.
+std::vector<int32_t> dealii_shell_node_order(const Mesh& m, std::vector<int32_t>* cell_order) {
+  if (m.cuboid) throw std::invalid_argument("deal.II order: the 6-cell shell only");
+  static const int kCells[6][8] = {{8, 9, 10, 11, 0, 1, 2, 3},   {9, 11, 1, 3, 13, 15, 5, 7},
+                                   {12, 13, 4, 5, 14, 15, 6, 7}, {8, 0, 10, 2, 12, 4, 14, 6},
+                                   {8, 9, 0, 1, 12, 13, 4, 5},   {10, 2, 11, 3, 14, 6, 15, 7}};
+  const int N = m.N, refine = m.refine, N3 = N * N * N;
+  std::unordered_map<size_t, int32_t> key_node, key_cell;
+  key_node.reserve(size_t(m.n_vnodes));
+  key_cell.reserve(size_t(m.n_cells));
+  for (int c = 0; c < m.n_cells; ++c) {
+    for (int lex = 0; lex < 27; ++lex)
+      key_node.emplace(shell_node_key(N, refine, c, lex), m.cell_q2[27 * size_t(c) + lex]);
+    key_cell.emplace(shell_node_key(N, refine, c, 13), c);
+  }
+  const int64_t den = int64_t(2 * N) * (2 * N) * (2 * N);
+  auto dealii_key = [&](int q, int X, int Y, int Z) {
+    int64_t num[4] = {0, 0, 0, 0};
+    for (int v = 0; v < 8; ++v) {
+      const int64_t w = int64_t((v & 1) ? X : 2 * N - X) * ((v & 2) ? Y : 2 * N - Y) *
+                        ((v & 4) ? Z : 2 * N - Z);
+      const int gv = kCells[q][v], corner = gv % 8;
+      num[0] += w * ((corner & 1) ? N : -N);
+      num[1] += w * ((corner & 2) ? N : -N);
+      num[2] += w * ((corner & 4) ? N : -N);
+      num[3] += w * (gv >= 8 ? 2 * N : 0);
+    }
+    int P[3];
+    for (int d = 0; d < 3; ++d) {
+      if (num[d] % den) throw std::logic_error("deal.II order: off-lattice point");
+      P[d] = int(num[d] / den);
+    }
+    if (num[3] % den) throw std::logic_error("deal.II order: off-lattice radius");
+    return shell_key_of_point(N, P, int(num[3] / den));
+  };
+  std::vector<int32_t> order(size_t(m.n_vnodes), -1);
+  if (cell_order) cell_order->assign(size_t(m.n_cells), -1);
+  int32_t next = 0;
+  for (int q = 0; q < 6; ++q)
+    for (int code = 0; code < N3; ++code) {
+      int i, j, k;
+      demorton(uint32_t(code), refine, i, j, k);
+      if (cell_order) {
+        const auto it = key_cell.find(dealii_key(q, 2 * i + 1, 2 * j + 1, 2 * k + 1));
+        if (it == key_cell.end()) throw std::logic_error("deal.II order: cell not found");
+        (*cell_order)[size_t(q) * N3 + code] = it->second;
+      }
+      for (int h = 0; h < 27; ++h) {
+        const int lex = kQ2HierToLex[h];
+        const auto it = key_node.find(dealii_key(q, 2 * i + lex % 3, 2 * j + (lex / 3) % 3, 2 * k + lex / 9));
+        if (it == key_node.end()) throw std::logic_error("deal.II order: node not found");
+        if (order[it->second] < 0) order[it->second] = next++;
+      }
+    }
+  if (next != m.n_vnodes) throw std::logic_error("deal.II order: nodes not covered");
+  return order;
 }
 
 }  // namespace dcp

@@ -164,4 +164,9 @@ extern const int kFeecFaceVertex[6][4];
 // i.e. what cell->get_dof_indices() returns in the reference.
 std::vector<int32_t> nse_cell_dofs_dealii(const Mesh& m);
 
+// New number of every velocity node in deal.II's distribute_dofs order on the
+// 6-cell hyper_shell (see mesh.cpp); cell_order (optional): the mesh cell of
+// each deal.II active cell, in deal.II's order.
+std::vector<int32_t> dealii_shell_node_order(const Mesh& m, std::vector<int32_t>* cell_order);
+
 }  // namespace dcp

@@ -52,6 +52,7 @@ EXPORTED = [
     "dcp_T_matrix_export", "dcp_precond_diagonals", "dcp_cell_nse_system",
     "dcp_get_timings", "dcp_pattern_info", "dcp_host_mesh_create", "dcp_host_mesh_destroy",
     "dcp_host_mesh_renumber_cuthill_mckee",
+    "dcp_host_mesh_renumber_dealii",
     "dcp_host_mesh_view_get", "dcp_host_mesh_initial_temperature", "dcp_prm_load",
     "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
@@ -252,6 +253,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_renumber_cuthill_mckee.argtypes = [P]
+    lib.dcp_host_mesh_renumber_dealii.argtypes = [P, P]
     lib.dcp_host_mesh_destroy.argtypes = [P]
     lib.dcp_host_mesh_destroy.restype = None
     lib.dcp_host_mesh_view_get.argtypes = [P, C.POINTER(MeshView)]
@@ -349,9 +351,13 @@ class HostMesh:
 
     def __init__(self, cuboid=False, refine=2, R0=1.0, R1=3.0, length=1.0, temperature_degree=1,
                  normals="mapping", feec=False, mapping_q_on_all_cells=False,
-                 cuthill_mckee=False):
+                 cuthill_mckee=False, dealii_order=False):
         """cuthill_mckee: renumber the NSE dofs as setup_dofs does for the
-        Schur-complement solver (dcp_host_mesh_renumber_cuthill_mckee)."""
+        Schur-complement solver (dcp_host_mesh_renumber_cuthill_mckee).
+        dealii_order: number the NSE and temperature dofs in deal.II's
+        distribute_dofs order on the 6-cell hyper_shell first
+        (dcp_host_mesh_renumber_dealii); `dealii_cells` then holds the mesh cell
+        of each deal.II active cell."""
         if normals not in self.NORMAL_MODES:
             raise ValueError("normals must be one of %s" % (self.NORMAL_MODES,))
         h = lib().dcp_host_mesh_create(int(cuboid), int(refine), float(R0), float(R1),
@@ -361,6 +367,12 @@ class HostMesh:
         if not h:
             raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
         try:
+            self.dealii_cells = None
+            if dealii_order:
+                cells = np.zeros(6 * 8 ** int(refine), dtype=np.int32)
+                if lib().dcp_host_mesh_renumber_dealii(h, _ptr(cells)) != DCP_OK:
+                    raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
+                self.dealii_cells = cells
             if cuthill_mckee and lib().dcp_host_mesh_renumber_cuthill_mckee(h) != DCP_OK:
                 raise DcpError(DCP_ERR_INVALID, lib().dcp_last_error(None).decode())
             v = MeshView()

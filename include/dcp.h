@@ -500,6 +500,16 @@ void dcp_host_mesh_destroy(dcp_host_mesh* m);
  * (boussinesq_model.tpp:198-204): cell dofs, NSE constraints and node_xyz of
  * later views follow the new numbering (velocity 3 n + c stays node-major). */
 int dcp_host_mesh_renumber_cuthill_mckee(dcp_host_mesh* m);
+/* deal.II's own DoF order on the 6-cell shell (setup_dofs,
+ * boussinesq_model.tpp:197-206: distribute_dofs over GridGenerator::
+ * hyper_shell's cells refined refine_global times, then component_wise
+ * {0,0,0,1}; the temperature dof handler's distribute_dofs likewise): NSE and
+ * temperature dofs, constraints and node_xyz of later views follow it; the
+ * cells themselves keep the mesh's order. cell_order (optional, [n_cells]):
+ * the mesh cell of each deal.II active cell, in deal.II's order. Call before
+ * dcp_host_mesh_renumber_cuthill_mckee (the Schur configs renumber from this
+ * order, as the reference does). 3D shell only. */
+int dcp_host_mesh_renumber_dealii(dcp_host_mesh* m, int32_t* cell_order);
 typedef struct {
   int n_cells, n_u, n_p, n_T, n_vnodes;
   const int32_t* cell_nse_dofs;   /* [n_cells][89] */
