@@ -103,9 +103,9 @@ def test_feec_partition_halo_consistency_gloo():
     assert res == {0: True, 1: True}
 
 
-@pytest.mark.parametrize("world", [3, 8])
-def test_partition_covers_and_matches(world):
-    m = dcp.HostMesh(refine=3)
+@pytest.mark.parametrize("refine,world", [(3, 3), (3, 8), (4, 8)])
+def test_partition_covers_and_matches(refine, world):
+    m = dcp.HostMesh(refine=refine)
     infos = [dcp.partition_info(m, r, world) for r in range(world)]
     assert sum(i["n_owned_cells"] for i in infos) == m.n_cells
     assert sum(i["nvo"] for i in infos) == m.n_u // 3
@@ -139,7 +139,8 @@ def _time_step(ctx, m, u, T):
 @pytest.mark.parametrize("world,refine,gs", [(2, 2, "modified"), (3, 2, "modified"),
                                              (4, 2, "modified"), (2, 2, "classical2"),
                                              (3, 2, "classical2"), (2, 2, "dcgs2"),
-                                             (3, 2, "dcgs2"), (2, 2, "sstep"), (3, 2, "sstep")])
+                                             (3, 2, "dcgs2"), (2, 2, "sstep"), (3, 2, "sstep"),
+                                             (8, 2, "classical2"), (8, 2, "sstep")])
 def test_group_time_step_matches_single_gpu(world, refine, gs):
     """(At r = 3 this random state drives the reference's inner Schur GMRES
     into its 5000-iteration cap on one GPU and on every partition alike.)
