@@ -258,6 +258,7 @@ struct Ctx {
   int gram_schmidt = 0;
   double S_lambda = 0;                // Gershgorin bound of S (s-step shifts), 0 = not yet formed
   DBuf<double> ss_c;                 // s-step block sums (several GPUs / large meshes)
+  DBuf<double> head_part;  // per-slice |p|^2 partials of the fused restart head
   DBuf<GmresDev> gm_state;
   GmresReport* gm_report = nullptr;  // pinned [2]: the reports of the last two cycles
   hipEvent_t gm_ev[2] = {nullptr, nullptr};

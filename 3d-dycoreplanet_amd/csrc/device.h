@@ -511,6 +511,19 @@ void gmres_cycle_end(GmresDev* st, int n, const double* const* V, double* x, Gmr
                      hipStream_t s);
 // st->y = H^-1 gamma over st->dim
 void gmres_backsub(GmresDev* st, hipStream_t s);
+// One GPU, S in SELL form: the restart head as two launches. y = b - S x with
+// per-slice partials of |y|^2 (sell_spmv_residual), then every workgroup sums
+// the partials in the same fixed order, workgroup 0 runs the cycle_init check
+// and all scale v0 = y / |y| (gmres_cycle_head).
+void sell_spmv_residual(const SellView& m, const double* x, const double* b, double* y,
+                        double* part, hipStream_t s);
+void gmres_cycle_head(GmresDev* st, const double* part, int n_part, double tol, int max_steps,
+                      bool first, int n, const double* p, double* v0, hipStream_t s);
+// The restart tail as one launch: every workgroup solves H y = gamma (the
+// same arithmetic as k_gmres_backsub), updates its share of x += V y;
+// workgroup 0 stores y and the host report.
+void gmres_cycle_finish(GmresDev* st, int n, const double* const* V, double* x,
+                        GmresReport* report, hipStream_t s);
 void axpy(int n, DScal c, const double* x, double* y, hipStream_t s);            // y += c x
 void scale(int n, DScal c, double* x, hipStream_t s);                             // x *= c
 void sadd(int n, double s_, double a, const double* x, double* y, hipStream_t s); // y = s y + a x

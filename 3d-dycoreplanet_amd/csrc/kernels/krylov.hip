@@ -623,9 +623,11 @@ __device__ bool sstep_chol(const double* c2, int d, int ncol1, double (*Rm)[kSSt
 // Hessenberg columns k..k+s-1 from the block's change of basis (c1 + c2 the
 // coefficients on q_0..q_k, Rm the Cholesky factor) into Hr, then their
 // Givens steps / checks. Called by every thread of one workgroup: the old
-// columns, rotations and gamma are staged in LDS, a thread per row forms the
-// new columns (rows are independent: H_new U = X row by row), and one thread
-// runs the sequential Givens updates on LDS data.
+// columns, rotations and gamma are staged in LDS; X (old columns weighted by
+// the change of basis) one thread per entry, the triangular solve
+// H_new U = X one thread per row, the k earlier rotations one thread per new
+// column, and one thread the block's own rotations and checks column by
+// column (a column after the converged one is never used).
 __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const double* c1,
                                  const double* c2, const double (*Rm)[kSStep]) {
   constexpr int S = kSStep;
@@ -652,28 +654,53 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
     return Rm[r - k - 1][c - 1];
   };
+  // X = Rhat-weighted old columns, one thread per (row, column) pair
+  __shared__ double Xs[kGmMaxDim + 1][S];
+  __shared__ double hk[S];
+  for (int e = t; e < rows * S; e += nt) {
+    const int r = e / S, c = e % S;
+    double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
+    if (r <= k && c > 0)
+      for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= Hs[r][i] * rhat(i, c);
+    Xs[r][c] = x;
+  }
+  __syncthreads();
+  // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular), row by row
   if (t < rows) {
     const int r = t;
     double hrow[S];
+#pragma unroll
     for (int c = 0; c < S; ++c) {
-      double x = a.theta[c] * rhat(r, c) + a.sigma * rhat(r, c + 1);
-      if (r <= k && c > 0)
-        for (int i = (r > 0 ? r - 1 : 0); i < k; ++i) x -= Hs[r][i] * rhat(i, c);
-      // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular)
+      double x = Xs[r][c];
       for (int l = 0; l < c; ++l) x -= hrow[l] * rhat(k + l, c);
       hrow[c] = x / rhat(k + c, c);
       Hn[r][c] = hrow[c];
     }
   }
   __syncthreads();
+  // the k rotations of the earlier columns, one thread per new column
+  if (t < S) {
+    const int c = t;
+    double hi = Hn[0][c];
+#pragma unroll 4
+    for (int i = 0; i < k; i++) {
+      const double hn = Hn[i + 1][c];
+      Hrot[i][c] = cs[i] * hi + sn[i] * hn;
+      hi = -sn[i] * hi + cs[i] * hn;
+    }
+    hk[c] = hi;
+  }
+  __syncthreads();
   if (t == 0) {
     int acc = acc0;
+    const double tol = st->tol;
+    const int max_steps = st->max_steps;
     last_col = S - 1;
     for (int c = 0; c < S; ++c) {
       const int kk = k + c;
-      // rotate the raw column in LDS (Hrot), carrying h[i+1] in a register
-      double hi = Hn[0][c];
-      for (int i = 0; i < kk; i++) {
+      // then the block's own rotations, carrying h[i+1] in a register
+      double hi = hk[c];
+      for (int i = k; i < kk; i++) {
         const double hn = Hn[i + 1][c];
         Hrot[i][c] = cs[i] * hi + sn[i] * hn;
         hi = -sn[i] * hi + cs[i] * hn;
@@ -689,7 +716,7 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
       gam[kk] = g0 * c_;
       ++acc;
       const double rho = fabs(gam[kk + 1]);
-      const int status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+      const int status = rho <= tol ? 1 : ((acc >= max_steps || isnan(rho)) ? 2 : 0);
       if (status || c == S - 1) {
         st->accumulated = acc;
         st->dim = kk + 1;
@@ -1541,25 +1568,95 @@ __global__ void k_gmres_cycle_init(GmresDev* st, const double* __restrict__ rho2
 }
 
 // x += sum_{j < dim} y_j V_j, dim read on the device (0: nothing)
-__global__ void k_gmres_update(const GmresDev* __restrict__ st, int n, const double* const* V,
-                               double* __restrict__ x) {
+
+__global__ __launch_bounds__(kBlock) void k_gmres_head(GmresDev* st, const double* __restrict__ part,
+                                                       int n_part, double tol, int max_steps,
+                                                       int first, int n,
+                                                       const double* __restrict__ p,
+                                                       double* __restrict__ v0) {
+  __shared__ double red[kBlock];
+  const int t = threadIdx.x;
+  double sum = 0.0;
+  for (int i = t; i < n_part; i += kBlock) sum += part[i];
+  red[t] = sum;
+  __syncthreads();
+#pragma unroll
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  const double rho = sqrt(red[0]);
+  // workgroup 0 may already have moved status 0 -> s; a reader that sees s
+  // skips v0, which the stopped cycle never uses
+  const int s0 = first ? 0 : st->status;
+  const int acc = first ? 0 : st->accumulated;
+  const int status = s0 != 0 ? s0 : (rho <= tol ? 1 : ((acc >= max_steps || isnan(rho)) ? 2 : 0));
+  if (blockIdx.x == 0 && t == 0) {
+    if (first) {
+      st->accumulated = 0;
+      st->tol = tol;
+      st->max_steps = max_steps;
+    }
+    st->dim = 0;
+    if (s0 == 0) {
+      st->rho = rho;
+      st->status = status;
+      if (status == 0) {
+        st->gamma[0] = rho;
+        st->inv_rho = 1.0 / rho;
+        st->inv_norm = 1.0;
+      }
+    }
+  }
+  if (status != 0) return;
+  const double cf = 1.0 * (1.0 / rho);
+  for (long i = long(blockIdx.x) * kBlock + t; i < n; i += long(gridDim.x) * kBlock) v0[i] = cf * p[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_gmres_finish(GmresDev* st, int n,
+                                                         const double* const* V,
+                                                         double* __restrict__ x,
+                                                         GmresReport* report) {
+  __shared__ double H[kGmMaxDim][kGmMaxDim + 1], gam[kGmMaxDim], y[kGmMaxDim];
   const int dim = st->dim;
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0 && t == 0) {
+    report->rho = st->rho;
+    report->status = st->status;
+    report->accumulated = st->accumulated;
+  }
   if (dim <= 0) return;
-  for (long i = long(blockIdx.x) * kBlock + threadIdx.x; i < n; i += long(gridDim.x) * kBlock) {
+  for (int e = t; e < dim * dim; e += kBlock) H[e / dim][e % dim] = st->H[e / dim][e % dim];
+  if (t < dim) gam[t] = st->gamma[t];
+  __syncthreads();
+  if (t == 0) {
+    // k_gmres_backsub's order, y in registers (the LDS round trips of the
+    // one-thread loop were its whole cost)
+    double yr[kGmMaxDim];
+#pragma unroll
+    for (int i = kGmMaxDim - 1; i >= 0; --i) {
+      if (i < dim) {
+        double sum = gam[i];
+#pragma unroll
+        for (int j = i + 1; j < kGmMaxDim; ++j)
+          if (j < dim) sum -= yr[j] * H[i][j];
+        yr[i] = sum / H[i][i];
+      } else {
+        yr[i] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kGmMaxDim; ++i) y[i] = yr[i];
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && t < dim) st->y[t] = y[t];
+  for (long i = long(blockIdx.x) * kBlock + t; i < n; i += long(gridDim.x) * kBlock) {
     double v = x[i];
-    for (int j = 0; j < dim; ++j) v += st->y[j] * V[j][i];
+    for (int j = 0; j < dim; ++j) v += y[j] * V[j][i];
     x[i] = v;
   }
 }
 
-__global__ void k_gmres_report(const GmresDev* __restrict__ st, GmresReport* report) {
-  if (threadIdx.x != 0) return;
-  // plain vector stores into the pinned host record; the host reads it after
-  // an event recorded behind this launch
-  report->rho = st->rho;
-  report->status = st->status;
-  report->accumulated = st->accumulated;
-}
 
 void gmres_cycle_init(GmresDev* st, const double* rho2, double tol, int max_steps, bool first,
                       hipStream_t s) {
@@ -1570,13 +1667,22 @@ void gmres_cycle_init(GmresDev* st, const double* rho2, double tol, int max_step
 
 void gmres_cycle_end(GmresDev* st, int n, const double* const* V, double* x, GmresReport* report,
                      hipStream_t s) {
-  hipLaunchKernelGGL(k_gmres_backsub, dim3(1), dim3(kBlock), 0, s, st);
+  gmres_cycle_finish(st, n, V, x, report, s);
+}
+
+void gmres_cycle_head(GmresDev* st, const double* part, int n_part, double tol, int max_steps,
+                      bool first, int n, const double* p, double* v0, hipStream_t s) {
+  const long blocks = std::min<long>((long(n) + kBlock - 1) / kBlock, 1024);
+  hipLaunchKernelGGL(k_gmres_head, dim3(unsigned(std::max<long>(blocks, 1))), dim3(kBlock), 0, s,
+                     st, part, n_part, tol, max_steps, int(first), n, p, v0);
   DCP_HIP_CHECK(hipGetLastError());
-  const long blocks = std::min<long>((long(n) + kBlock - 1) / kBlock, 2048);
-  hipLaunchKernelGGL(k_gmres_update, dim3(unsigned(std::max<long>(blocks, 1))), dim3(kBlock), 0, s,
-                     st, n, V, x);
-  DCP_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_gmres_report, dim3(1), dim3(64), 0, s, st, report);
+}
+
+void gmres_cycle_finish(GmresDev* st, int n, const double* const* V, double* x,
+                        GmresReport* report, hipStream_t s) {
+  const long blocks = std::min<long>((long(n) + kBlock - 1) / kBlock, 1024);
+  hipLaunchKernelGGL(k_gmres_finish, dim3(unsigned(std::max<long>(blocks, 1))), dim3(kBlock), 0, s,
+                     st, n, V, x, report);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

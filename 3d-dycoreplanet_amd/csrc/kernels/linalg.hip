@@ -348,7 +348,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
                                                       double* __restrict__ part1,
                                                       const double* __restrict__ cf_dev,
                                                       const int* __restrict__ status,
-                                                      double theta = 0.0, double sscale = 1.0) {
+                                                      double theta = 0.0, double sscale = 1.0,
+                                                      const double* __restrict__ bsub = nullptr) {
   __shared__ double quarter[3][64];
   if (status && *status) return;  // device-resident GMRES cycle already stopped
   if (cf_dev) cf = *cf_dev;
@@ -359,7 +360,10 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   if (sl * 64 >= rows) {
     // padding workgroup of the common partial length (several GPUs): the
     // all-reduced partial arrays must hold zeros past this rank's slices
-    if (EPI && part0 && threadIdx.x == 0) part0[sl] = part1[sl] = 0.0;
+    if (EPI && threadIdx.x == 0) {
+      if (part0) part0[sl] = 0.0;
+      if (part1) part1[sl] = 0.0;
+    }
     return;
   }
   const int64_t b = m.off[sl];
@@ -463,22 +467,22 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
     const double xv = x[row] * cf;
     // s-step Newton basis: y = (S x - theta x) / sigma (sscale = 1 / sigma)
     if (theta != 0.0 || sscale != 1.0) acc = (acc - theta * xv) * sscale;
+    // GMRES restart head: the residual y = b - S x
+    if (bsub) acc = bsub[row] - acc;
     y[row] = acc;
     if (xs) xs[row] = xv;
-    if (part0) {
-      d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
-      d1 = acc * acc;
-    }
+    if (part0) d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
+    if (part1) d1 = acc * acc;
   }
-  if (!part0) return;
+  if (!part0 && !part1) return;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     d0 += __shfl_xor(d0, o, 64);
     d1 += __shfl_xor(d1, o, 64);
   }
   if (lane == 0) {
-    part0[sl] = d0;
-    part1[sl] = d1;
+    if (part0) part0[sl] = d0;
+    if (part1) part1[sl] = d1;
   }
 }
 
@@ -866,6 +870,19 @@ void sell_spmv_shifted(const SellView& m, const double* x, double theta, double 
   else
     hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
                        nullptr, nullptr, nullptr, nullptr, status, theta, sscale);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void sell_spmv_residual(const SellView& m, const double* x, const double* b, double* y,
+                        double* part, hipStream_t s) {
+  if (m.rows <= 0) return;
+  const dim3 grid(sell_fused_blocks(m.rows));
+  if (m.col16)
+    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                       nullptr, nullptr, part, nullptr, nullptr, 0.0, 1.0, b);
+  else
+    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                       nullptr, nullptr, part, nullptr, nullptr, 0.0, 1.0, b);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -537,6 +537,32 @@ State gmres_schur_ordered(Ctx& c, double* x, const double* b, Control& ctl,
 // V y) are kernels too, so the host enqueues cycle i + 1 before it waits for
 // the report of cycle i and never leaves the stream idle. Once the solve has
 // stopped every launch of a cycle already queued returns at entry.
+// The head of a device-resident restart cycle: p = b - S x, rho = |p|, the
+// SolverControl check on the device, v_0 = p / rho. One GPU with S in SELL
+// form: two launches (the residual SpMV with per-slice |p|^2 partials, then
+// the check and the scaling); otherwise SpMV, sadd, the reduction, the check
+// and the scaling one by one.
+void schur_cycle_head(Ctx& c, const Seg& g, const double* x, const double* b, double* p,
+                      double* v0, GmresDev* dst, const Control& ctl, bool first) {
+  const int n = c.n_p;
+  if (!c.comm && c.S_perm.p) {
+    const int nsl = sell_fused_blocks(c.sell().rows);
+    if (c.head_part.n < size_t(nsl)) c.head_part.alloc(size_t(nsl));
+    sell_spmv_residual(c.sell(), x, b, p, c.head_part.p, c.stream);
+    gmres_cycle_head(dst, c.head_part.p, nsl, ctl.tol, int(ctl.max_steps), first, n, p, v0,
+                     c.stream);
+    return;
+  }
+  if (c.S_perm.p)
+    sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
+  else
+    schur_vmult(c, x, p);
+  sadd(n, -1., 1., b, p, c.stream);
+  gdot(c, g, p, p, kSlotA);
+  gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), first, c.stream);
+  equ(n, DScal{&dst->inv_rho, 1.0}, p, v0, c.stream);
+}
+
 State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
                                std::vector<double*>& tv, int n_tmp) {
   const int n = c.n_p;
@@ -571,14 +597,7 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
   const bool one_launch = !comm && c.fused_chain && c.hmapped && cgs2_chain_fits(g.n, nb1, c.n_cus);
   auto enqueue_cycle = [&](int cyc) {
     // head: p = b - S x, rho = |p| (SolverControl check on the device), v_0 = p / rho
-    if (c.S_perm.p)
-      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
-    else
-      schur_vmult(c, x, p);
-    sadd(n, -1., 1., b, p, c.stream);
-    gdot(c, g, p, p, kSlotA);
-    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
-    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
+    schur_cycle_head(c, g, x, b, p, tv[0], dst, ctl, cyc == 0);
     for (int k = 0; k < restart; ++k) {
       double* src = k == 0 ? tv[0] : wbuf[(k - 1) & 1];
       double* w = wbuf[k & 1];
@@ -668,14 +687,7 @@ State gmres_schur_dcgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl
   const bool one_launch = !comm && c.fused_chain && c.hmapped && dcgs2_fits(g.n, nb1, c.n_cus);
   double* err = comm ? slot(c, kSlotErr) : chain_err(c);
   auto enqueue_cycle = [&](int cyc) {
-    if (c.S_perm.p)
-      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
-    else
-      schur_vmult(c, x, p);
-    sadd(n, -1., 1., b, p, c.stream);
-    gdot(c, g, p, p, kSlotA);
-    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
-    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
+    schur_cycle_head(c, g, x, b, p, tv[0], dst, ctl, cyc == 0);
     for (int k = 0; k <= restart; ++k) {
       const bool tail = k == restart;
       if (!tail) {
@@ -810,14 +822,7 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   sa.sigma = 0.5 * lam;
   for (int i = 0; i < kSStep; ++i) sa.w[i] = wraw[i];
   auto enqueue_cycle = [&](int cyc) {
-    if (c.S_perm.p)
-      sell_spmv(c.sell(), x, 1.0, p, c.stream);  // S in the stored order
-    else
-      schur_vmult(c, x, p);
-    sadd(n, -1., 1., b, p, c.stream);
-    gdot(c, g, p, p, kSlotA);
-    gmres_cycle_init(dst, slot(c, kSlotA), ctl.tol, int(ctl.max_steps), cyc == 0, c.stream);
-    equ(n, DScal{&dst->inv_rho, 1.0}, p, tv[0], c.stream);
+    schur_cycle_head(c, g, x, b, p, tv[0], dst, ctl, cyc == 0);
     for (int k = 0; k < restart; k += kSStep) {
       const double* src = tv[k];
       for (int i = 0; i < kSStep; ++i) {

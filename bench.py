@@ -36,9 +36,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
 PMC_SUMMARIES = {(5, "explicit"): ("profiles/r03a_pmc_inner_r5.json", "k_sell_spmv<true, true>")}
-# rocprofv3 --kernel-trace --stats of the same bench (durations of the CGS2
-# chain launches, for the orthogonalisation roofline)
-CHAIN_STATS = {5: "profiles/r03a_bench_r5_kernel_stats.csv"}
+# rocprofv3 --kernel-trace --stats of the same workload (durations of the
+# orthogonalisation launches, for their roofline): the CGS2 chain (bench) and
+# the s-step block (inner probe)
+CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
+               (5, "sstep"): "profiles/r03m_inner_probe_sstep_kernel_stats.csv"}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
 PMC_MF = {5: ("profiles/r02_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
 
@@ -70,34 +72,42 @@ def pmc_traffic(refine, mode, n_p):
     return hits[0] - 8.0 * n_p if hits else None
 
 
-def chain_roofline(refine, n_p):
-    """The fused CGS2 chain (k_cgs2_chain<KL>, one launch per Arnoldi column)
-    from the committed kernel statistics: algorithmic bytes of column k are the
-    k+1 basis vectors read twice-free (one pass, registers) + w read + q
-    written = (k + 3) 8 n_p; template KL serves k = KL-4..KL-1, so a launch
-    averages (KL + 0.5) 8 n_p bytes. Bound: HBM, although at this size the
-    basis sits in the 256 MB MALL and the launch is hand-off latency bound."""
-    path = CHAIN_STATS.get(refine)
+def chain_roofline(refine, n_p, gs):
+    """The orthogonalisation launches of the inner Schur GMRES from the
+    committed kernel statistics (rocprofv3 --kernel-trace --stats).
+    classical2: k_cgs2_chain<KL>, one launch per Arnoldi column k: the k+1
+    basis vectors read once (registers for both passes) + w read + q written
+    = (k + 3) 8 n_p bytes; template KL serves k = KL-4..KL-1, on average
+    (KL + 0.5) 8 n_p. sstep: k_sstep_block<KL>, one launch per block of 4
+    columns starting at k = KL-4: the k+1 basis vectors + the 4 Newton vectors
+    read, the 4 new basis vectors written = (KL + 5) 8 n_p. Bound: HBM,
+    although at refine 5 the basis sits in the 256 MB MALL and the launches
+    are hand-off latency bound."""
+    path = CHAIN_STATS.get((refine, gs))
     if path is None or not os.path.exists(os.path.join(ROOT, path)):
         return None
     import csv
+    key, extra = ("k_cgs2_chain<", 0.5) if gs == "classical2" else ("k_sstep_block<", 5.0)
     rows = []
     with open(os.path.join(ROOT, path)) as f:
         for r in csv.DictReader(f):
             name = r["Name"]
-            if "k_cgs2_chain<" not in name:
+            if key not in name:
                 continue
-            kl = int(name.split("k_cgs2_chain<")[1].split(",")[0])
+            kl = int(name.split(key)[1].split(",")[0].split(">")[0])
             rows.append((kl, int(r["Calls"]), float(r["AverageNs"])))
     if not rows:
         return None
-    per = {kl: {"bytes": (kl + 0.5) * 8 * n_p, "avg_us": ns * 1e-3,
-                "achieved": (kl + 0.5) * 8 * n_p / (ns * 1e-9) / 1e9} for kl, _, ns in rows}
-    tot_b = sum(calls * (kl + 0.5) * 8 * n_p for kl, calls, _ in rows)
+    per = {kl: {"bytes": (kl + extra) * 8 * n_p, "avg_us": ns * 1e-3,
+                "achieved": (kl + extra) * 8 * n_p / (ns * 1e-9) / 1e9} for kl, _, ns in rows}
+    tot_b = sum(calls * (kl + extra) * 8 * n_p for kl, calls, _ in rows)
     tot_t = sum(calls * ns * 1e-9 for _, calls, ns in rows)
     ach = tot_b / tot_t / 1e9
-    return {"kernel": "fused CGS2 orthogonalisation chain k_cgs2_chain<KL> (one launch per "
-                      "inner Arnoldi column)", "bound": "hbm", "source": path,
+    what = ("fused CGS2 orthogonalisation chain k_cgs2_chain<KL> (one launch per inner "
+            "Arnoldi column)" if gs == "classical2" else
+            "s-step block k_sstep_block<KL> (one launch per 4 inner Arnoldi columns: BCGS2 + "
+            "Cholesky QR + Hessenberg/Givens)")
+    return {"kernel": what, "bound": "hbm", "source": path,
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "per_template": per}
 
@@ -117,9 +127,11 @@ def parse():
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
                     help="explicit: formed S = B D^-1 B^T (default); composite: B^T, Jacobi, B")
     ap.add_argument("--gram-schmidt", choices=["modified", "classical2", "dcgs2", "sstep"],
-                    default="classical2",
-                    help="inner Schur GMRES orthogonalisation: modified (deal.II) or "
-                         "classical twice with device-resident cycles (DCP_OPT_GRAM_SCHMIDT)")
+                    default="sstep",
+                    help="inner Schur GMRES orthogonalisation (DCP_OPT_GRAM_SCHMIDT): modified "
+                         "(deal.II's), classical2 / dcgs2 (classical twice, one launch per "
+                         "step), sstep (blocks of 4 Newton-basis steps, one orthogonalisation "
+                         "launch per block; DESIGN 9a); all device-resident cycles but modified")
     ap.add_argument("--variant", choices=["classic", "feec"], default="classic",
                     help="feec: ExteriorCalculus model of config 4 (feec prm, refine 4, 1 GPU)")
     ap.add_argument("--shared-device", action="store_true",
@@ -605,8 +617,8 @@ def main():
                      if world == 1 else None,
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
-    if args.schur == "explicit" and world == 1 and args.gram_schmidt == "classical2":
-        out["roofline_chain"] = chain_roofline(args.refine, m.n_p)
+    if args.schur == "explicit" and world == 1:
+        out["roofline_chain"] = chain_roofline(args.refine, m.n_p, args.gram_schmidt)
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
     # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point
     # (SURVEY's unit of work; the kernel recomputes the geometry instead of
