@@ -110,7 +110,7 @@ GOLD3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shel
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2"])
+@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2", "sstep"])
 def test_gpu_time_step_r3_matches_oracle_fixture(gs):
     """One reference time step at refine 3 (3,072 cells, 81,912 NSE dofs) from
     the physical state against the oracle's (tests/golden/make_golden.py r3,
@@ -136,6 +136,7 @@ def test_gpu_time_step_r3_matches_oracle_fixture(gs):
     assert rel(ctx.get_state(dcp.T_RHS), g["T_rhs"]) < 1e-12
     rc, outer, inner = ctx.solve_nse()
     it = g["iters"]
+    print(f"r3 step {gs}: outer {outer} (oracle {it[1]}), inner {inner} (oracle {it[2]})")
     assert rc == it[0] == 0 and outer == it[1]
     assert abs(inner - it[2]) <= 0.10 * it[2]
     x = ctx.get_state(dcp.NSE_SOLUTION)
