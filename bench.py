@@ -403,6 +403,11 @@ def run_feec(args):
         dist.destroy_process_group()
 
 
+def progress(msg):
+    """One line per bench stage on stderr (long refine-6 runs stay visibly alive)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.variant == "feec":
@@ -416,11 +421,13 @@ def main():
     t_setup = time.perf_counter()
     m = dcp.HostMesh(cuboid=False, refine=args.refine, R0=rp.R0, R1=rp.R1, length=rp.length,
                      temperature_degree=ph.temperature_degree)
+    progress(f"host mesh refine {args.refine}: {m.n_cells} cells")
     ctx = make_ctx()
     ctx.set_physics(ph)
     ctx.set_schur_explicit(args.schur == "explicit")
     ctx.set_gram_schmidt(args.gram_schmidt)
     ctx.upload_mesh(m)
+    progress("uploaded")
     u0 = np.zeros(m.n_u + m.n_p)
     for f, v in ((dcp.OLD_NSE_SOLUTION, u0), (dcp.OLD_T_SOLUTION, m.T0)):
         ctx.set_state(f, v)
@@ -452,6 +459,7 @@ def main():
         rc, outer, inner = ctx.solve_nse()
         rcT, itT, _ = ctx.solve_temperature()
         t = ctx.timings()
+        progress(f"step: solve {t['solve_nse_ms']:.1f} ms, {outer} outer / {inner} inner")
         return rc, outer, inner, itT, t
 
     for _ in range(args.warmup):

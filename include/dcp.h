@@ -226,8 +226,12 @@ enum { DCP_OPT_ASSEMBLE_VELOCITY_BLOCK = 6 };
  *   orthogonality test); 1 = classical Gram-Schmidt applied twice (CGS2: two
  *   block reductions per Arnoldi step); 2 = DCGS2, classical Gram-Schmidt with
  *   the second pass delayed into the next step (one block reduction per
- *   Arnoldi step; each column's Givens rotation and check one step later).
- *   1 and 2 run the Givens updates and the SolverControl check on the device
+ *   Arnoldi step; each column's Givens rotation and check one step later);
+ *   3 = s-step: blocks of 4 columns from a Chebyshev-shifted Newton basis (4
+ *   SpMVs), orthogonalised by one launch (block CGS twice + Cholesky QR, two
+ *   reductions per block), Hessenberg columns from the change of basis, then
+ *   the 4 Givens steps and checks column by column (restart must be a
+ *   multiple of 4). 1-3 run the Givens updates and the SolverControl check on the device
  *   so a restart cycle runs without host round trips. Same Krylov space and
  *   stopping rule; rounding differs. */
 enum { DCP_OPT_GRAM_SCHMIDT = 7 };
