@@ -2060,12 +2060,14 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     c.time_schur = false;
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     double sum = 0;
+    int napp = 0;
     for (int k = 0; k < c.schur_ev_used; ++k) {
       float ms = 0;
       DCP_HIP_CHECK(hipEventElapsedTime(&ms, c.schur_ev[k].a, c.schur_ev[k].b));
       sum += ms;
+      napp += c.schur_ev[k].count;
     }
-    c.timings.schur_apply_ms_avg = c.schur_ev_used ? sum / c.schur_ev_used : 0.0;
+    c.timings.schur_apply_ms_avg = napp ? sum / napp : 0.0;
     c.timings.schur_applies = c.schur_calls;
     double mf_ms[2] = {0, 0};
     for (int v = 0; v < 2; ++v) {

@@ -48,6 +48,7 @@ struct DBuf {
 
 struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
+  int count = 1;  // operator applies between a and b (averages divide by it)
   void init() {
     DCP_HIP_CHECK(hipEventCreate(&a));
     DCP_HIP_CHECK(hipEventCreate(&b));

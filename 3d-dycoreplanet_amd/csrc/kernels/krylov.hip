@@ -935,18 +935,30 @@ __global__ __launch_bounds__(kBlock) void k_ss_dots(Seg g, ChainVecs V, SStepArg
       granule_store(gran + 2 * (size_t(ncol1 + threadIdx.x) * nb + blockIdx.x), r, tag + 1);
   }
   if (!last_block(cnt, &is_last)) return;
-  // the last block: column c summed over the blocks in block order, one thread per column
-  for (int c = threadIdx.x; c < ncol; c += kBlock) {
-    double t = 0.0;
-    for (int b = 0; b < nb; ++b) {
-      const double* q = gran + 2 * (size_t(c) * nb + b);
-      const unsigned long long* u = reinterpret_cast<const unsigned long long*>(q);
-      const unsigned long long vv = __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long tt = __hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t += tt == ((tag + 1) ^ granule_mix(vv)) ? __longlong_as_double((long long)vv)
-                                               : granule_poll(q, tag + 1, err);
+  // the last block: 8 columns at a time, each thread sums a stride of the
+  // blocks, then block_sums (a fixed order; every granule load in flight at
+  // once instead of one thread walking all nb blocks of a column)
+  for (int c0 = 0; c0 < ncol; c0 += 8) {
+    const int nc = min(8, ncol - c0);
+    double t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      t[j] = 0.0;
+      if (j < nc)
+        for (int b = threadIdx.x; b < nb; b += kBlock) {
+          const double* q = gran + 2 * (size_t(c0 + j) * nb + b);
+          const unsigned long long* u = reinterpret_cast<const unsigned long long*>(q);
+          const unsigned long long vv =
+              __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long tt =
+              __hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t[j] += tt == ((tag + 1) ^ granule_mix(vv)) ? __longlong_as_double((long long)vv)
+                                                      : granule_poll(q, tag + 1, err);
+        }
     }
-    out[c] = t;
+    const double r = block_sums<8>(t, nc, sm);
+    if (int(threadIdx.x) < nc) out[c0 + threadIdx.x] = r;
+    __syncthreads();  // sm is reused by the next 8 columns
   }
 }
 

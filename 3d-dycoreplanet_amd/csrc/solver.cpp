@@ -825,15 +825,27 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
     schur_cycle_head(c, g, x, b, p, tv[0], dst, ctl, cyc == 0);
     for (int k = 0; k < restart; k += kSStep) {
       const double* src = tv[k];
+      // one GPU: one timing sample spans the block's 4 back-to-back SpMVs (the
+      // event pair's own cost spread over 4 launches); several GPUs: per SpMV
+      Timer* eb = nullptr;
+      if (!comm) {
+        eb = schur_sample(c);
+        c.schur_calls += kSStep - 1;
+        if (eb) {
+          eb->count = kSStep;
+          DCP_HIP_CHECK(hipEventRecord(eb->a, c.stream));
+        }
+      }
       for (int i = 0; i < kSStep; ++i) {
         const double* in = i == 0 ? src : wraw[i - 1];
         halo_exchange(c, c.halo_p, const_cast<double*>(in));
-        Timer* e = schur_sample(c);
+        Timer* e = comm ? schur_sample(c) : nullptr;
         if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
         sell_spmv_shifted(c.sell(), in, sa.theta[i], 1.0 / sa.sigma, wraw[i], &dst->status,
                           c.stream);
         if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
       }
+      if (eb) DCP_HIP_CHECK(hipEventRecord(eb->b, c.stream));
       for (int i = 0; i < kSStep; ++i) sa.q[i] = tv[k + 1 + i];
       if (fused)
         sstep_block(g, chain_vecs(tv, k + 1), sa, k, dst, c.chain_gran.p, nb1, ++c.chain_seq,
@@ -1091,8 +1103,11 @@ State fgmres(Ctx& c, double* x, const double* b, int basis, unsigned max_steps, 
 // sampled, deferred timing of Schur-complement applies (no host sync)
 Timer* schur_sample(Ctx& c) {
   if (c.time_schur && (c.schur_calls++ % Ctx::kSchurSampleEvery) == 0 &&
-      c.schur_ev_used < Ctx::kSchurEvents)
-    return &c.schur_ev[c.schur_ev_used++];
+      c.schur_ev_used < Ctx::kSchurEvents) {
+    Timer* e = &c.schur_ev[c.schur_ev_used++];
+    e->count = 1;
+    return e;
+  }
   return nullptr;
 }
 

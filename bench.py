@@ -447,13 +447,27 @@ def main():
         ctx.close()
         return
 
+    loud = args.refine >= 6   # minutes per step: a line per phase and a heartbeat
+    if loud:
+        import threading
+
+        def heartbeat():
+            while True:
+                time.sleep(60)
+                progress("running")
+        threading.Thread(target=heartbeat, daemon=True).start()
+
     def step():
         ctx.copy_state(dcp.NSE_SOLUTION, dcp.OLD_NSE_SOLUTION)
         ctx.copy_state(dcp.T_SOLUTION, dcp.OLD_T_SOLUTION)
         ctx.cfl_number()
         ctx.max_velocity()
         ctx.assemble_nse_system()
+        if loud:
+            progress("assembled")
         ctx.build_nse_preconditioner()
+        if loud:
+            progress("preconditioner built")
         ctx.assemble_temperature_matrix()
         ctx.assemble_temperature_rhs()
         rc, outer, inner = ctx.solve_nse()
