@@ -465,8 +465,8 @@ struct SStepArgs {
 };
 void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st, double* gran,
                  int nb, unsigned long long seq, double* err, hipStream_t s);
-// Several GPUs: the same block as three launches around two all-reduces of the
-// per-rank sums (c1: s (k+1) doubles, c2: s (k+1) + s (s+1) / 2; device
+// Several GPUs / large meshes: the same block as five launches (dots, column
+// sums, dots, column sums, final) around two all-reduces of the per-rank sums (c1: s (k+1) doubles, c2: s (k+1) + s (s+1) / 2; device
 // scratch), the reductions over the owned entries of g.
 void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st,
                        double* gran, unsigned* cnt, double* c1, double* c2,

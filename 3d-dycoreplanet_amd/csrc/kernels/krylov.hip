@@ -865,24 +865,22 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   sstep_hessenberg(st, a, k, c1, c2, Rm);
 }
 
-// Several GPUs: the same block as three launches around two all-reduces of
-// the per-rank sums (one reduction per pass, over the owned entries of Seg g).
-// PASS 0: c1 = V^T w_i; PASS 1: w_i -= V c1 (written back), c2 = V^T w_i and
-// the Gram sums. Each block publishes its sums as granules, the last block
-// adds them per column in block order -> out.
+// Several GPUs / large meshes: the same block as five launches around two
+// all-reduces of the per-rank sums (one reduction per pass, over the owned
+// entries of Seg g). PASS 0: c1 = V^T w_i; PASS 1: w_i -= V c1 (written back),
+// c2 = V^T w_i and the Gram sums. Each block publishes its sums as granules;
+// k_ss_colsum adds them per column in block order.
 template <int KL, int PASS>
 __global__ __launch_bounds__(kBlock) void k_ss_dots(Seg g, ChainVecs V, SStepArgs a, int k,
                                                     const double* __restrict__ cin, double* gran,
-                                                    unsigned* cnt, double* out,
-                                                    unsigned long long seq, double* err,
+                                                    unsigned long long seq,
                                                     const int* __restrict__ status) {
   constexpr int K = pow2_at_least<KL>();
   constexpr int S = kSStep;
   constexpr int nG = S * (S + 1) / 2;
   __shared__ double sm[4 * (K > 16 ? K : 16)];
-  __shared__ int is_last;
   if (*status) return;
-  const int d = k + 1, ncol1 = S * d, ncol = PASS == 0 ? ncol1 : ncol1 + nG;
+  const int d = k + 1, ncol1 = S * d;
   const long k0 = long(blockIdx.x) * (kBlock * kCgsElems) + threadIdx.x;
   double v[kCgsElems][K], w[kCgsElems][S];
   long pos[kCgsElems];
@@ -934,35 +932,33 @@ __global__ __launch_bounds__(kBlock) void k_ss_dots(Seg g, ChainVecs V, SStepArg
     if (int(threadIdx.x) < nG)
       granule_store(gran + 2 * (size_t(ncol1 + threadIdx.x) * nb + blockIdx.x), r, tag + 1);
   }
-  if (!last_block(cnt, &is_last)) return;
-  // the last block: 8 columns at a time, each thread sums a stride of the
-  // blocks, then block_sums (a fixed order; every granule load in flight at
-  // once instead of one thread walking all nb blocks of a column)
-  for (int c0 = 0; c0 < ncol; c0 += 8) {
-    const int nc = min(8, ncol - c0);
-    double t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      t[j] = 0.0;
-      if (j < nc)
-        for (int b = threadIdx.x; b < nb; b += kBlock) {
-          const double* q = gran + 2 * (size_t(c0 + j) * nb + b);
-          const unsigned long long* u = reinterpret_cast<const unsigned long long*>(q);
-          const unsigned long long vv =
-              __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const unsigned long long tt =
-              __hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          t[j] += tt == ((tag + 1) ^ granule_mix(vv)) ? __longlong_as_double((long long)vv)
-                                                      : granule_poll(q, tag + 1, err);
-        }
-    }
-    const double r = block_sums<8>(t, nc, sm);
-    if (int(threadIdx.x) < nc) out[c0 + threadIdx.x] = r;
-    __syncthreads();  // sm is reused by the next 8 columns
-  }
 }
 
-// the last of the three launches: w_i -= V c2, the Cholesky factor of the
+// out[c] = the column-c granules of k_ss_dots summed over its nb blocks in a
+// fixed order (thread-strided sums, then block_sums): one workgroup per column,
+// so the granule reads of all columns are in flight at once (a single
+// reducing workgroup reads ~6 MB at refine 6 and is load-latency bound).
+__global__ __launch_bounds__(kBlock) void k_ss_colsum(const double* __restrict__ gran, int nb,
+                                                      double* out, unsigned long long seq,
+                                                      double* err, const int* __restrict__ status) {
+  __shared__ double sm[4];
+  if (*status) return;
+  const int c = blockIdx.x;
+  const unsigned long long tag = seq * 256 + 1;
+  double t[1] = {0.0};
+  for (int b = threadIdx.x; b < nb; b += kBlock) {
+    const double* q = gran + 2 * (size_t(c) * nb + b);
+    const unsigned long long* u = reinterpret_cast<const unsigned long long*>(q);
+    const unsigned long long vv = __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long tt = __hip_atomic_load(u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t[0] += tt == (tag ^ granule_mix(vv)) ? __longlong_as_double((long long)vv)
+                                          : granule_poll(q, tag, err);
+  }
+  const double r = block_sums<1>(t, 1, sm);
+  if (threadIdx.x == 0) out[c] = r;
+}
+
+// the last of the five launches: w_i -= V c2, the Cholesky factor of the
 // corrected Gram matrix, q = W R^-1 (owned entries), block 0 the Hessenberg
 // columns and Givens steps
 template <int KL>
@@ -1047,11 +1043,17 @@ void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, Gmr
 #define DCP_SSM(KL)                                                                              \
   if (k + 1 <= KL) {                                                                             \
     hipLaunchKernelGGL((k_ss_dots<KL, 0>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, nullptr,   \
-                       gran, cnt, c1, ++seq, err, status);                                       \
+                       gran, ++seq, status);                                                     \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    hipLaunchKernelGGL(k_ss_colsum, dim3(ncol1), dim3(kBlock), 0, s, gran, nb, c1, seq, err,     \
+                       status);                                                                  \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     if (comm) comm->allreduce(c1, size_t(ncol1), false, s);                                      \
     hipLaunchKernelGGL((k_ss_dots<KL, 1>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, gran, \
-                       cnt, c2, ++seq, err, status);                                             \
+                       ++seq, status);                                                           \
+    DCP_HIP_CHECK(hipGetLastError());                                                            \
+    hipLaunchKernelGGL(k_ss_colsum, dim3(ncol2), dim3(kBlock), 0, s, gran, nb, c2, seq, err,     \
+                       status);                                                                  \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     if (comm) comm->allreduce(c2, size_t(ncol2), false, s);                                      \
     hipLaunchKernelGGL((k_ss_final<KL>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, c2, st); \

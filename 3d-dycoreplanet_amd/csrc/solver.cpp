@@ -757,7 +757,7 @@ State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::ve
 // symmetric positive semi-definite: the shifts are the Chebyshev points of
 // [0, lambda] with lambda the Gershgorin bound of the stored S, sigma =
 // lambda / 2, so the basis polynomials stay bounded on the spectrum. Falls back
-// to the three-launch block (sstep_block_multi: per-rank sums all-reduced
+// to the multi-launch block (sstep_block_multi: per-rank sums all-reduced
 // between launches) on several GPUs or when the block does not fit the
 // resident grid.
 bool sstep_fits(const Ctx& c, long n, int nb) {
