@@ -1139,7 +1139,7 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
     require(c->cfg.device >= 0 && c->cfg.device < ndev, DCP_ERR_INVALID, "device ordinal out of range");
     require(c->cfg.rank >= 0 && c->cfg.rank < c->cfg.world_size, DCP_ERR_INVALID, "rank out of range");
     DCP_HIP_CHECK(hipSetDevice(c->cfg.device));
-    if (c->cfg.world_size > 1) {
+    if (c->cfg.world_size > 1 || c->cfg.nccl_id) {
       if (c->cfg.group) {
         require(c->cfg.group->size == c->cfg.world_size, DCP_ERR_INVALID, "group size != world_size");
         c->comm = make_local_comm(c->cfg.group, c->cfg.rank);

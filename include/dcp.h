@@ -93,7 +93,10 @@ typedef struct {
   int device;           /* HIP device ordinal (local rank) */
   int rank;             /* rank in the node-local communicator */
   int world_size;       /* number of ranks / GPUs */
-  const void* nccl_id;  /* ncclUniqueId (128 bytes) when world_size > 1, else NULL */
+  const void* nccl_id;  /* ncclUniqueId (128 bytes) when world_size > 1, else NULL; with
+                           world_size == 1 a non-NULL id still builds a one-rank RCCL
+                           communicator, so the multi-GPU code path (partitioned
+                           layout, all-reduces, halos) runs on a single GPU */
   dcp_group* group;     /* instead of nccl_id: in-process group (dcp_group_create) */
 } dcp_config;
 

@@ -287,3 +287,34 @@ def test_group_feec_time_step_matches_single_gpu(world):
         assert abs(r["T"][1] - ref["T"][1]) <= 1
         assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-6)
         assert np.isclose(r["cfl"], ref["cfl"], rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", ["classical2", "sstep"])
+def test_one_rank_rccl_time_step_matches_single_gpu(gs):
+    """The multi-GPU code path on a one-rank RCCL communicator (dcp_config
+    nccl_id with world_size 1): the partitioned upload, RCCL all-reduces and
+    the (empty) halos, the multi-launch Krylov kernels, against the plain
+    single-GPU context. RCCL refuses two ranks on one GPU, so this is the
+    communicator's own code on this box; the 8-GPU run exercises the peers."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(11)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    out = []
+    for nccl in (False, True):
+        ctx = dcp.Context(nccl_id=dcp.nccl_unique_id() if nccl else None)
+        ctx.set_physics(ph)
+        ctx.upload_mesh(m)
+        ctx.set_gram_schmidt(gs)
+        out.append(_time_step(ctx, m, u, m.T0.copy()))
+        ctx.close()
+    ref, got = out
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    assert rel(got["rhs"], ref["rhs"]) < 1e-12
+    assert rel(got["T_rhs"], ref["T_rhs"]) < 1e-12
+    assert got["nse"][0] == ref["nse"][0] == 0 and got["nse"][1] == ref["nse"][1]
+    assert abs(got["nse"][2] - ref["nse"][2]) <= 0.15 * ref["nse"][2]
+    assert np.linalg.norm(got["x"] - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
+    assert rel(got["Tx"], ref["Tx"]) < 1e-10
