@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdlib>
 
 #include "../device.h"
 #include "../fe_tables.h"
@@ -1357,12 +1358,325 @@ void launch_nse_system(const CellData& cd, const ScatterMaps& sm, const int32_t*
   DCP_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// Operator form on the radially separable shell, one wave per cell
+// (k_nse_system<2> keeps one 256-thread workgroup per cell for every other
+// mesh). The 256-thread form spends most of its 3.4 ms at r=5 in
+// workgroup-barrier phases with 27-81 active lanes; here a 64-lane wave owns a
+// cell, lanes hold Gauss points (rhs integrand) or (node, 4 vertices) pairs
+// (B^T rows), reference shape values and gradients are formed in registers,
+// and the only synchronisation is the wave's own (no __syncthreads). Every
+// product and sum runs in k_nse_system's order (the q loops, the condensation,
+// the staged scatter), so the result is bitwise that of k_nse_system<2> / <0>
+// where they overlap.
+struct OpWaveSmem {
+  union {
+    struct {
+      double U[81], T[27];
+      Geo geo;
+      double F[81];
+      double diag[27];
+    } a;
+    double stage[648];  // condensed B^T rows (8 an + v), after the phases above
+  };
+  int node[27];
+  int pos[432];  // posBt, then posB (scatter_B)
+};
+constexpr int kOpWaves = 1;  // waves (cells) per workgroup
+
+__device__ inline double sel3v(int i, const double (&v)[3]) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
+}
+
+// wave-level LDS hand-off (a cell never spans waves)
+__device__ inline void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+
+__global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
+    CellData cd, ScatterMaps sm, const int32_t* __restrict__ cells, int n_cells,
+    const double* __restrict__ u_old, const double* __restrict__ T_old, PhysicsDev ph, NseOut out) {
+  __shared__ OpWaveSmem smem[kOpWaves];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int k = int(blockIdx.x) * kOpWaves + wave;
+  if (k >= n_cells) return;
+  OpWaveSmem& sh = smem[wave];
+  const int cell = cells[k];
+  const bool want_B = out.Bt != nullptr;
+  const bool scatter_B = out.B != nullptr;
+  const bool want_rhs = out.rhs != nullptr;
+  const bool want_cdiag = out.cdiag != nullptr;
+  // ---- state, scatter positions, geometry
+  if (lane < 27) {
+    const int nd = cd.cell_q2[27 * size_t(cell) + lane];
+    sh.node[lane] = nd;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) sh.a.U[3 * lane + d] = u_old[3 * size_t(nd) + d];
+    if (cd.tdpc == 27) sh.a.T[lane] = T_old[cd.cell_T[27 * size_t(cell) + lane]];
+    sep_geometry(cd, cell, sh.a.geo, lane);
+  } else if (lane >= 32 && lane < 40 && cd.tdpc == 8) {
+    sh.a.T[lane - 32] = T_old[cd.cell_T[8 * size_t(cell) + lane - 32]];
+  }
+  if (want_B)
+    for (int i = lane; i < 216; i += 64) {
+      sh.pos[i] = sm.posBt[216 * size_t(cell) + i];
+      if (scatter_B) sh.pos[216 + i] = sm.posB[216 * size_t(cell) + i];
+    }
+  wsync();
+  // ---- rhs integrand per Gauss point (lanes 0-26), k_nse_system's formulas
+  if (want_rhs && lane < 27) {
+    const int q = lane;
+    const double xa = sel_gauss(q % 3), xb = sel_gauss((q / 3) % 3), xc = sel_gauss(q / 9);
+    const double* Ji = &sh.a.geo.Ji[9 * q];
+    // the 1D factors at this lane's point; the node loop indexes them at
+    // compile time (same values and products as the table k_nse_system builds)
+    double LA[3], DA[3], LB[3], DB[3], LC[3], DC[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      LA[i] = ce_l2(i, xa);
+      DA[i] = ce_dl2(i, xa);
+      LB[i] = ce_l2(i, xb);
+      DB[i] = ce_dl2(i, xb);
+      LC[i] = ce_l2(i, xc);
+      DC[i] = ce_dl2(i, xc);
+    }
+    double u[3] = {0, 0, 0}, G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    // nodes n = na + 3 nb + 9 nc in order; na unrolled (register factors),
+    // the nb / nc factors picked once per row of three
+#pragma unroll 1
+    for (int nc = 0; nc < 3; ++nc) {
+      const double lc = sel3v(nc, LC), dc = sel3v(nc, DC);
+#pragma unroll 1
+      for (int nb = 0; nb < 3; ++nb) {
+        const double lb = sel3v(nb, LB), db = sel3v(nb, DB);
+#pragma unroll
+        for (int na = 0; na < 3; ++na) {
+          const int n = na + 3 * nb + 9 * nc;
+          const double s = LA[na] * lb * lc;
+          const double r0 = DA[na] * lb * lc;
+          const double r1 = LA[na] * db * lc;
+          const double r2 = LA[na] * lb * dc;
+          double Dn[3];
+#pragma unroll
+          for (int d = 0; d < 3; ++d) Dn[d] = r0 * Ji[d] + r1 * Ji[3 + d] + r2 * Ji[6 + d];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double un = sh.a.U[3 * n + c];
+            u[c] += un * s;
+            G[c][0] += un * Dn[0];
+            G[c][1] += un * Dn[1];
+            G[c][2] += un * Dn[2];
+          }
+        }
+      }
+    }
+    double T = 0;
+    if (cd.tdpc == 8) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) T += sh.a.T[v] * cRef.S1[8 * q + v];
+    } else {
+      for (int n = 0; n < 27; ++n)
+        T += sh.a.T[n] * (sel3v(n % 3, LA) * sel3v((n / 3) % 3, LB) * sel3v(n / 9, LC));
+    }
+    const double rho = 1 - ph.beta * (T - ph.T_ref);
+    double grav[3];
+    if (ph.cuboid) {
+      grav[0] = grav[1] = 0;
+      grav[2] = -ph.g;
+    } else {
+      const double* x = &sh.a.geo.xq[3 * q];
+      const double r = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+      const double den = r > 1 ? r : sqrt(r);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) grav[d] = -ph.g * x[d] / den;
+    }
+    const double cxu[3] = {-ph.coriolis_z * u[1], ph.coriolis_z * u[0], 0.0};
+    const double w = sh.a.geo.JxW[q];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double adv = u[0] * G[c][0] + u[1] * G[c][1] + u[2] * G[c][2];
+      sh.a.F[3 * q + c] = (u[c] + ph.dt * rho * (ph.grav_scale * grav[c]) - ph.dt * adv -
+                           ph.dt * (2 * cxu[c])) * w;
+    }
+  }
+  wsync();
+  // ---- B^T rows (an, v) for v in [4 h, 4 h + 4) on lanes an + 32 h; lanes
+  // 0-26 also the node-diagonal sums (|K_ii| rule), lanes 32-58 the rhs node
+  const int an = lane & 31, h = lane >> 5;
+  const bool row_lane = an < 27;
+  double bt[4][3];
+  double kii[3] = {0, 0, 0};
+  double fa[3] = {0, 0, 0};
+  const bool do_diag = want_cdiag && h == 0;
+  if (row_lane) {
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) bt[vv][0] = bt[vv][1] = bt[vv][2] = 0;
+    double msum = 0, g2[3] = {0, 0, 0};
+    // this lane's node: its 1D factors at the 3 Gauss points per direction; the
+    // point loop indexes them at compile time
+    const int na = an % 3, nb = (an / 3) % 3, nc = an / 9;
+    double La[3], Da1[3], Lb[3], Db1[3], Lc[3], Dc1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double x = sel_gauss(i);
+      La[i] = ce_l2(na, x);
+      Da1[i] = ce_dl2(na, x);
+      Lb[i] = ce_l2(nb, x);
+      Db1[i] = ce_dl2(nb, x);
+      Lc[i] = ce_l2(nc, x);
+      Dc1[i] = ce_dl2(nc, x);
+    }
+#pragma unroll 1
+    for (int q2 = 0; q2 < 3; ++q2) {
+      const double lc = sel3v(q2, Lc), dc = sel3v(q2, Dc1);
+#pragma unroll 1
+      for (int q1 = 0; q1 < 3; ++q1) {
+        const double lb = sel3v(q1, Lb), db = sel3v(q1, Db1);
+#pragma unroll
+        for (int q0 = 0; q0 < 3; ++q0) {
+          const int q = q0 + 3 * q1 + 9 * q2;
+          const double s = La[q0] * lb * lc;
+          const double r0 = Da1[q0] * lb * lc;
+          const double r1 = La[q0] * db * lc;
+          const double r2 = La[q0] * lb * dc;
+          const double* Ji = &sh.a.geo.Ji[9 * q];
+          double Da[3];
+#pragma unroll
+          for (int d = 0; d < 3; ++d) Da[d] = r0 * Ji[d] + r1 * Ji[3 + d] + r2 * Ji[6 + d];
+          const double w = sh.a.geo.JxW[q];
+          if (want_B) {
+#pragma unroll
+            for (int vv = 0; vv < 4; ++vv) {
+              const double wp = w * cRef.S1[8 * q + 4 * h + vv];
+              bt[vv][0] -= Da[0] * wp;
+              bt[vv][1] -= Da[1] * wp;
+              bt[vv][2] -= Da[2] * wp;
+            }
+          }
+          if (do_diag) {
+            msum += w * s * s;
+            g2[0] += w * Da[0] * Da[0];
+            g2[1] += w * Da[1] * Da[1];
+            g2[2] += w * Da[2] * Da[2];
+          }
+          if (want_rhs && h == 1) {
+            fa[0] += s * sh.a.F[3 * q];
+            fa[1] += s * sh.a.F[3 * q + 1];
+            fa[2] += s * sh.a.F[3 * q + 2];
+          }
+        }
+      }
+    }
+    if (do_diag) {
+      const double L = g2[0] + g2[1] + g2[2];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) kii[c] = msum + ph.nu_sys * L + ph.nu_sys * g2[c];
+      sh.a.diag[an] = fabs(kii[0]) + fabs(kii[1]) + fabs(kii[2]);
+    }
+    const int nd = sh.node[an];
+    double Ca[3][3];
+    condensation(cd.vcon[nd], Ca);
+    if (want_B) {
+#pragma unroll
+      for (int vv = 0; vv < 4; ++vv) {
+        const double b0 = bt[vv][0], b1 = bt[vv][1], b2 = bt[vv][2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) bt[vv][j] = Ca[0][j] * b0 + Ca[1][j] * b1 + Ca[2][j] * b2;
+      }
+    }
+    if (want_rhs && h == 1) {
+      double* dst = out.rhs + 3 * size_t(nd);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+    }
+  }
+  wsync();
+  if (do_diag && row_lane) {
+    const int nd = sh.node[an];
+    const int ci = out.cidx[nd];
+    if (ci >= 0) {
+      const NodeConstraint nc = cd.vcon[nd];
+      double avg = 0;
+      for (int m = 0; m < 27; ++m) avg += sh.a.diag[m];
+      avg /= 89.0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (nc.type == 1 || nc.type == 3 || c == nc.k) {
+          const double d = fabs(kii[c]);
+          out.cdiag[3 * size_t(ci) + c] += d != 0.0 ? d : avg;
+        }
+    }
+  }
+  if (!want_B) return;
+  wsync();  // every lane is past its reads of the phase tables: stage over them
+  if (row_lane) {
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sh.stage[3 * (8 * an + 4 * h + vv) + j] = bt[vv][j];
+  }
+  wsync();
+  // ---- the staged rows into B^T (and B): first touch stores, else add; 7
+  // read-modify-writes in flight per lane (more holds registers the waves need)
+  constexpr int kB = 7, kRounds = (2 * 648 + 64 * kB - 1) / (64 * kB);  // 3
+  const int e_end = scatter_B ? 2 * 648 : 648;
+#pragma unroll 1
+  for (int rd = 0; rd < kRounds; ++rd) {
+    double old[kB], val[kB];
+    double* dst[kB];
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const int e = lane + 64 * (kB * rd + j);
+      old[j] = 0.0;
+      val[j] = 0.0;
+      dst[j] = nullptr;
+      if (e < e_end) {
+        int p;
+        if (e < 648) {
+          const int r = e / 3, c = e - 3 * r;
+          val[j] = sh.stage[3 * r + c];
+          p = sh.pos[r];
+          dst[j] = out.Bt + 3 * size_t(p >= 0 ? p : ~p) + c;
+        } else {
+          const int r = (e - 648) / 3, c = e - 648 - 3 * r;
+          const int pv = r / 27, a = r - 27 * pv;  // B row (pv, a) = B^T row (a, pv)
+          val[j] = sh.stage[3 * (8 * a + pv) + c];
+          p = sh.pos[216 + r];
+          dst[j] = out.B + 3 * size_t(p >= 0 ? p : ~p) + c;
+        }
+        if (p >= 0) old[j] = *dst[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j)
+      if (dst[j]) *dst[j] = old[j] + val[j];
+  }
+}
+
+}  // namespace
+
 void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                          const double* u_old, const double* T_old, const PhysicsDev& ph,
                          const NseOut& out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL((k_nse_system<2, false>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
-                     u_old, T_old, ph, out);
+  // the wave-per-cell form on the separable shell (no periodic images there);
+  // DCP_ASM_CELL_BLOCK=1 keeps the workgroup-per-cell kernel (timing comparisons)
+  static const bool cell_block = [] {
+    const char* e = std::getenv("DCP_ASM_CELL_BLOCK");
+    return e && *e == '1';
+  }();
+  if (cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block) {
+    hipLaunchKernelGGL(k_nse_operator_wave, dim3((n + kOpWaves - 1) / kOpWaves), dim3(64 * kOpWaves),
+                       0, s, cd, sm, cells, n, u_old, T_old, ph, out);
+  } else {
+    hipLaunchKernelGGL((k_nse_system<2, false>), dim3(n), dim3(kNseThreads), 0, s, cd, sm, cells, 0,
+                       u_old, T_old, ph, out);
+  }
   DCP_HIP_CHECK(hipGetLastError());
 }
 

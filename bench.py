@@ -568,6 +568,22 @@ def main():
                                     "what": "the same with the node-pair Gram sums as "
                                             "v_mfma_f64_16x16x4_f64 tiles "
                                             "(DCP_OPT_ELEMENT_MFMA=1; DESIGN section 4e)"}}
+    if full_matrix is not None and world == 1:
+        # the element system's structural flops (0.884 MFLOP per
+        # cell, geometry excluded) against the FP64 peak (78.6 TFLOP/s, vector =
+        # matrix on gfx950) and its bytes (element matrix + rhs + indices out,
+        # state and geometry in: 67.4 KB per cell) against HBM; bound = the larger
+        # of the two times
+        fl, by = 0.884e6 * m.n_cells, 67372.0 * m.n_cells
+        t = full_ms * 1e-3
+        full_matrix["roofline"] = {
+            "bound": "mfma" if fl / 78.6e12 > by / 8e12 else "hbm",
+            "achieved_tflops": fl / t / 1e12, "peak_tflops": 78.6,
+            "frac_flops": fl / t / 78.6e12,
+            "achieved_gbs": by / t / 1e9, "peak_gbs": HBM_PEAK_GBS,
+            "frac_hbm": by / t / (HBM_PEAK_GBS * 1e9),
+            "what": "the full element system (SURVEY 8(d) flops / bytes per cell), timed "
+                    "as the velocity-block assembly leg"}
     pinfo = ctx.pattern_info()
     if args.schur == "explicit":
         # fused SELL SpMV with the formed S: values + column indices per
@@ -632,6 +648,10 @@ def main():
         "device_mem_gb": device_mem_gb(),
         "pcie_inclusive": pcie,
         "assembly_with_velocity_block": full_matrix,
+        # the temperature system's own assembled-DoFs rate
+        "T_assembly": {"value": m.n_T / (1e-3 * (np.mean([r[4]["assemble_T_matrix_ms"] for r in recs])
+                                                 + np.mean([r[4]["assemble_T_rhs_ms"] for r in recs]))),
+                       "unit": "assembled T DoFs/s (assemble_temperature_matrix + _rhs)"},
         "roofline": {"kernel": kernel, "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
