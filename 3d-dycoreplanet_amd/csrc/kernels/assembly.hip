@@ -1384,7 +1384,24 @@ struct OpWaveSmem {
   int node[27];
   int pos[432];  // posBt, then posB (scatter_B)
 };
-constexpr int kOpWaves = 1;  // waves (cells) per workgroup
+#ifndef DCP_OPW_WAVES
+#define DCP_OPW_WAVES 1
+#endif
+constexpr int kOpWaves = DCP_OPW_WAVES;  // waves (cells) per workgroup
+// timing probes only (wrong results): DCP_OPW_NOSCATTER skips the B^T / B
+// scatter, DCP_OPW_NORHS the rhs integrand, DCP_OPW_NOBT the B^T rows
+#ifndef DCP_OPW_NOSCATTER
+#define DCP_OPW_NOSCATTER 0
+#endif
+#ifndef DCP_OPW_NORHS
+#define DCP_OPW_NORHS 0
+#endif
+#ifndef DCP_OPW_NOBT
+#define DCP_OPW_NOBT 0
+#endif
+#ifndef DCP_OPW_BATCH
+#define DCP_OPW_BATCH 7
+#endif
 
 __device__ inline double sel3v(int i, const double (&v)[3]) {
   return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
@@ -1429,7 +1446,7 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
     }
   wsync();
   // ---- rhs integrand per Gauss point (lanes 0-26), k_nse_system's formulas
-  if (want_rhs && lane < 27) {
+  if (want_rhs && lane < 27 && !DCP_OPW_NORHS) {
     const int q = lane;
     const double xa = sel_gauss(q % 3), xb = sel_gauss((q / 3) % 3), xc = sel_gauss(q / 9);
     const double* Ji = &sh.a.geo.Ji[9 * q];
@@ -1612,7 +1629,7 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
         }
     }
   }
-  if (!want_B) return;
+  if (!want_B || DCP_OPW_NOSCATTER) return;
   wsync();  // every lane is past its reads of the phase tables: stage over them
   if (row_lane) {
 #pragma unroll
@@ -1621,9 +1638,10 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
       for (int j = 0; j < 3; ++j) sh.stage[3 * (8 * an + 4 * h + vv) + j] = bt[vv][j];
   }
   wsync();
-  // ---- the staged rows into B^T (and B): first touch stores, else add; 7
-  // read-modify-writes in flight per lane (more holds registers the waves need)
-  constexpr int kB = 7, kRounds = (2 * 648 + 64 * kB - 1) / (64 * kB);  // 3
+  // ---- the staged rows into B^T (and B): first touch stores, else add;
+  // DCP_OPW_BATCH (7) read-modify-writes in flight per lane (more holds
+  // registers the waves need)
+  constexpr int kB = DCP_OPW_BATCH, kRounds = (2 * 648 + 64 * kB - 1) / (64 * kB);
   const int e_end = scatter_B ? 2 * 648 : 648;
 #pragma unroll 1
   for (int rd = 0; rd < kRounds; ++rd) {
