@@ -1385,7 +1385,7 @@ struct OpWaveSmem {
   int pos[432];  // posBt, then posB (scatter_B)
 };
 #ifndef DCP_OPW_WAVES
-#define DCP_OPW_WAVES 1
+#define DCP_OPW_WAVES 4
 #endif
 constexpr int kOpWaves = DCP_OPW_WAVES;  // waves (cells) per workgroup
 // timing probes only (wrong results): DCP_OPW_NOSCATTER skips the B^T / B
@@ -1400,7 +1400,7 @@ constexpr int kOpWaves = DCP_OPW_WAVES;  // waves (cells) per workgroup
 #define DCP_OPW_NOBT 0
 #endif
 #ifndef DCP_OPW_BATCH
-#define DCP_OPW_BATCH 7
+#define DCP_OPW_BATCH 14
 #endif
 
 __device__ inline double sel3v(int i, const double (&v)[3]) {
@@ -1639,8 +1639,9 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
   }
   wsync();
   // ---- the staged rows into B^T (and B): first touch stores, else add;
-  // DCP_OPW_BATCH (7) read-modify-writes in flight per lane (more holds
-  // registers the waves need)
+  // DCP_OPW_BATCH (14) read-modify-writes in flight per lane: the B^T rows of
+  // one GPU in one round (r=5: 7 per lane 2.49 ms, 14 per lane and 4 waves
+  // per workgroup 2.21 ms; profiles/r03y_*)
   constexpr int kB = DCP_OPW_BATCH, kRounds = (2 * 648 + 64 * kB - 1) / (64 * kB);
   const int e_end = scatter_B ? 2 * 648 : 648;
 #pragma unroll 1
