@@ -686,6 +686,10 @@ def main():
                                  "achieved": ve_bytes / (ve_ms * 1e-3) / 1e9 if ve_ms > 0
                                  else None}}
         mf["frac"] = mf["achieved"] / HBM_PEAK_GBS if mf["achieved"] else None
+        # the bytes the apply actually moves (PMC; the geometry is recomputed,
+        # not read) over the same apply time
+        mf["frac_actual_traffic"] = (mf["traffic"] / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                     if mf["traffic"] and st_ms > 0 else None)
         out["roofline_matrix_free"] = mf
     if world == 1 and not args.no_converging_leg:
         out["converging_step"] = converging_leg(make_ctx, args)

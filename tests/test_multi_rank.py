@@ -318,3 +318,29 @@ def test_one_rank_rccl_time_step_matches_single_gpu(gs):
     assert abs(got["nse"][2] - ref["nse"][2]) <= 0.15 * ref["nse"][2]
     assert np.linalg.norm(got["x"] - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
     assert rel(got["Tx"], ref["Tx"]) < 1e-10
+
+
+@pytest.mark.gpu
+def test_one_rank_rccl_feec_time_step_matches_single_gpu():
+    """Config 4's FEEC path (localize_feec, three owned segments, halos per
+    field) on a one-rank RCCL communicator against the plain context."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    f = m.feec
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(f.n)
+    x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
+    x0[f.fixed.astype(bool)] = 0
+    out = []
+    for nccl in (False, True):
+        ctx = dcp.Context(nccl_id=dcp.nccl_unique_id() if nccl else None)
+        ctx.set_physics(ph)
+        ctx.upload_feec_mesh(m)
+        out.append(_feec_time_step(ctx, m, x0, m.T0.copy()))
+        ctx.close()
+    ref, got = out
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    assert rel(got["rhs"], ref["rhs"]) < 1e-12
+    assert got["nse"][0] == ref["nse"][0] == 0 and got["nse"][1] == ref["nse"][1]
+    assert np.linalg.norm(got["x"] - ref["x"]) <= 1e-6 * np.linalg.norm(ref["x"])
+    assert abs(got["T"][1] - ref["T"][1]) <= 1
