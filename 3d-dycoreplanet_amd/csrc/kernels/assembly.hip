@@ -1388,6 +1388,8 @@ struct OpWaveSmem {
 #define DCP_OPW_WAVES 4
 #endif
 constexpr int kOpWaves = DCP_OPW_WAVES;  // waves (cells) per workgroup
+// colour classes below this many cells take the workgroup-per-cell kernel
+constexpr int kOpSmallColour = 4096;
 // timing probes only (wrong results): DCP_OPW_NOSCATTER skips the B^T / B
 // scatter, DCP_OPW_NORHS the rhs integrand, DCP_OPW_NOBT the B^T rows
 #ifndef DCP_OPW_NOSCATTER
@@ -1689,7 +1691,15 @@ void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_
     const char* e = std::getenv("DCP_ASM_CELL_BLOCK");
     return e && *e == '1';
   }();
-  if (cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block) {
+  // small colour classes (the greedy colouring's tail: 6 of 14 classes hold
+  // 2.3 % of the cells at refine 5) are latency-bound: there the
+  // workgroup-per-cell kernel (4 waves on one cell) finishes sooner; both
+  // kernels give bitwise the same matrix (DCP_ASM_SMALL_COLOUR: the threshold)
+  static const int small_colour = [] {
+    const char* e = std::getenv("DCP_ASM_SMALL_COLOUR");
+    return e ? std::atoi(e) : kOpSmallColour;
+  }();
+  if (cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block && n >= small_colour) {
     hipLaunchKernelGGL(k_nse_operator_wave, dim3((n + kOpWaves - 1) / kOpWaves), dim3(64 * kOpWaves),
                        0, s, cd, sm, cells, n, u_old, T_old, ph, out);
   } else {

@@ -521,10 +521,12 @@ def main():
                 "what": "host u_old/T_old upload + assemble_nse_system + rhs download, host clock"}
     # one step with each other Gram-Schmidt variant of the inner Schur GMRES
     # (deal.II's modified Gram-Schmidt is the reference's); at refine >= 6
-    # only the device-resident ones (the modified one reads every step back)
+    # only the device-resident ones (the modified one reads every step back), and
+    # on several GPUs likewise (d + 1 all-reduces per column: seconds per step)
     other = []
     for other_gs in ("modified", "classical2", "dcgs2", "sstep"):
-        if other_gs == args.gram_schmidt or (other_gs == "modified" and args.refine >= 6):
+        if other_gs == args.gram_schmidt or (other_gs == "modified" and
+                                             (args.refine >= 6 or world > 1)):
             continue
         ctx.set_gram_schmidt(other_gs)
         r_o = step()

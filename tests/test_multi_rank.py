@@ -344,3 +344,99 @@ def test_one_rank_rccl_feec_time_step_matches_single_gpu():
     assert got["nse"][0] == ref["nse"][0] == 0 and got["nse"][1] == ref["nse"][1]
     assert np.linalg.norm(got["x"] - ref["x"]) <= 1e-6 * np.linalg.norm(ref["x"])
     assert abs(got["T"][1] - ref["T"][1]) <= 1
+
+
+def _bench_sequence(ctx, m, u, T):
+    """bench.py's calls on one rank at N > 1, in its order: a warm-up and a
+    timed step (s-step), one step per other device-resident Gram-Schmidt
+    variant, the velocity-block and matrix-core assembly legs, the pattern /
+    layout / timing queries the bench line reads."""
+    ctx.set_schur_explicit(True)
+    ctx.set_gram_schmidt("sstep")
+    ctx.upload_mesh(m)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+    ctx.set_state(dcp.OLD_T_SOLUTION, T)
+
+    def step():
+        ctx.copy_state(dcp.NSE_SOLUTION, dcp.OLD_NSE_SOLUTION)
+        ctx.copy_state(dcp.T_SOLUTION, dcp.OLD_T_SOLUTION)
+        ctx.cfl_number()
+        ctx.max_velocity()
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        ctx.assemble_temperature_matrix()
+        ctx.assemble_temperature_rhs()
+        r = ctx.solve_nse()
+        ctx.solve_temperature()
+        return r, ctx.timings()
+
+    out = {"steps": [step(), step()]}
+    out["rhs"] = ctx.get_state(dcp.NSE_RHS)
+    for gs in ("classical2", "dcgs2"):
+        ctx.set_gram_schmidt(gs)
+        out["steps"].append(step())
+    ctx.set_gram_schmidt("sstep")
+    ctx.set_assemble_velocity_block(True)
+    ctx.assemble_nse_system()
+    out["rhs_full"] = ctx.get_state(dcp.NSE_RHS)
+    ctx.set_element_mfma(True)
+    ctx.assemble_nse_system()
+    out["rhs_mfma"] = ctx.get_state(dcp.NSE_RHS)
+    ctx.set_element_mfma(False)
+    ctx.set_assemble_velocity_block(False)
+    out["pattern"] = ctx.pattern_info()
+    out["layout"] = ctx.schur_layout()
+    out["timings"] = ctx.timings()
+    return out
+
+
+@pytest.mark.gpu
+def test_group_bench_sequence_8_ranks():
+    """Every call bench.py makes on a rank at N = 8, on an 8-rank in-process
+    group: no rank throws, the ranks agree on every iteration count (the
+    control flow the collectives need), and the assembled rhs of each leg
+    matches the single-GPU one on the owned entries."""
+    world = 8
+    m = dcp.HostMesh(refine=2)
+    rng = np.random.default_rng(7)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    T = m.T0.copy()
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(dcp.classic_physics())
+    ref = _bench_sequence(ref_ctx, m, u, T)
+    ref_ctx.close()
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(dcp.classic_physics())
+            results[rank] = _bench_sequence(ctx, m, u, T)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    for key in ("rhs", "rhs_full", "rhs_mfma"):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        assert rel(v, ref[key]) < 1e-12, key
+    counts = [[s[0] for s in r["steps"]] for r in results]
+    assert all(c == counts[0] for c in counts)
+    for (rc, outer, inner), (rrc, router, rinner) in zip(counts[0], [s[0] for s in ref["steps"]]):
+        assert rc == rrc and outer == router
+        assert abs(inner - rinner) <= 0.15 * rinner
+    for r in results:
+        assert r["timings"]["assemble_nse_ms"] > 0
+        assert r["pattern"]["nnz_S"] > 0
