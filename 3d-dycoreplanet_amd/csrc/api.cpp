@@ -1,10 +1,13 @@
 // C ABI implementation (include/dcp.h): context management, the one-off
 // mesh/DoF upload (patterns, colouring, scatter maps) and the hot-path calls.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <stdexcept>
@@ -196,6 +199,166 @@ struct HostPrep {
   std::vector<int32_t> vmaster, pmaster, tmaster;  // -1 or the partner
   int n_vslave = 0, n_pslave = 0, n_tslave = 0;
 };
+
+// Eight colours on the hyper_shell (the greedy colouring of the tree order
+// needs 14 at refine 5, 6 of them small launches holding 2.3 % of the cells:
+// latency the colour launches pay six times). The shell is columns x radial
+// layers, the columns the cubed sphere's 6 patches of 2^r x 2^r quads; a
+// vertex-sharing colouring is (layer parity) x a lateral 4-colouring. On each
+// patch the lateral colour is a function of the quad's index parities
+// (p_b, p_c) along the patch's two tangential cube axes b, c (found by a
+// breadth-first walk from the patch's corner quad). The three ways of
+// splitting 4 colours into two pairs are tied to the three cube axes (split
+// pi_x: L & 1, pi_y: L >> 1, pi_z: the xor of both): the quads along a patch
+// edge parallel to axis b then use one pair of pi_b and the quads across it
+// the other pair, which holds on every edge and corner for one choice of the
+// 12 per-patch parity offsets (searched). Anything else (cube, partitions,
+// other manifolds) fails one of the checks and keeps the greedy colouring;
+// the result is checked against every vertex-sharing pair before use.
+bool shell_colouring(int n_cells, const double* geo, const std::vector<int32_t>& pd,
+                     const std::vector<int32_t>& vptr, const std::vector<int32_t>& vcells,
+                     std::vector<int>& color) {
+  constexpr int kP = 64;
+  const int corner[4] = {0, 3, 12, 15};  // lateral corners of the inner face
+  std::map<std::array<long long, 3>, int> vkey;
+  std::vector<std::array<int, 4>> cv(n_cells);
+  std::vector<double> rad(n_cells);
+  std::vector<std::array<double, 3>> cdir(n_cells);
+  for (int c = 0; c < n_cells; ++c) {
+    std::array<double, 3> cen{0, 0, 0};
+    for (int k = 0; k < 4; ++k) {
+      const double* X = geo + (size_t(c) * kP + corner[k]) * 3;
+      const double r = std::sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+      if (!(r > 0)) return false;
+      if (k == 0) rad[c] = r;
+      std::array<long long, 3> key;
+      for (int d = 0; d < 3; ++d) {
+        key[d] = std::llround(X[d] / r * 1e9);
+        cen[d] += X[d] / r;
+      }
+      cv[c][k] = vkey.emplace(key, int(vkey.size())).first->second;
+    }
+    cdir[c] = cen;
+    std::sort(cv[c].begin(), cv[c].end());
+  }
+  std::map<std::array<int, 4>, int> ckey;
+  std::vector<int> col(n_cells);
+  std::vector<std::array<int, 4>> ccv;
+  std::vector<std::array<double, 3>> cen;
+  for (int c = 0; c < n_cells; ++c) {
+    auto it = ckey.emplace(cv[c], int(ccv.size()));
+    if (it.second) {
+      ccv.push_back(cv[c]);
+      cen.push_back(cdir[c]);
+    }
+    col[c] = it.first->second;
+  }
+  const int ncol = int(ccv.size());
+  // layer parity: rank of the inner radius among the distinct ones
+  std::vector<double> ur(rad);
+  std::sort(ur.begin(), ur.end());
+  std::vector<double> lev;
+  for (double r : ur)
+    if (lev.empty() || r > lev.back() * (1 + 1e-10)) lev.push_back(r);
+  std::vector<int> lpar(n_cells);
+  for (int c = 0; c < n_cells; ++c) {
+    const auto it = std::lower_bound(lev.begin(), lev.end(), rad[c] * (1 - 1e-10));
+    if (it == lev.end()) return false;
+    lpar[c] = int(it - lev.begin()) & 1;
+  }
+  // patch (face) of a column and its tangential axes
+  std::vector<int> face(ncol);
+  for (int k = 0; k < ncol; ++k) {
+    int a = 0;
+    for (int d = 1; d < 3; ++d)
+      if (std::fabs(cen[k][d]) > std::fabs(cen[k][a])) a = d;
+    face[k] = 2 * a + (cen[k][a] > 0);
+  }
+  // columns sharing an edge (two corner vertices) / a vertex
+  std::map<std::pair<int, int>, std::vector<int>> ecols;
+  std::vector<std::vector<int>> vcols(vkey.size());
+  for (int k = 0; k < ncol; ++k)
+    for (int i = 0; i < 4; ++i) {
+      vcols[ccv[k][i]].push_back(k);
+      for (int j = i + 1; j < 4; ++j) ecols[{ccv[k][i], ccv[k][j]}].push_back(k);
+    }
+  std::vector<std::vector<int>> eadj(ncol);
+  for (const auto& e : ecols)
+    if (e.second.size() == 2) {
+      eadj[e.second[0]].push_back(e.second[1]);
+      eadj[e.second[1]].push_back(e.second[0]);
+    }
+  // index parities along the tangential cube axes, walking each patch from
+  // its corner quad (smallest gnomonic coordinates)
+  std::vector<std::array<int, 3>> par(ncol, {-1, -1, -1});
+  for (int f = 0; f < 6; ++f) {
+    const int a = f / 2, t0 = a == 0 ? 1 : 0, t1 = a == 2 ? 1 : 2;
+    int anchor = -1, count = 0;
+    double best = 0;
+    for (int k = 0; k < ncol; ++k) {
+      if (face[k] != f) continue;
+      ++count;
+      const double g = (cen[k][t0] + cen[k][t1]) / std::fabs(cen[k][a]);
+      if (anchor < 0 || g < best) {
+        anchor = k;
+        best = g;
+      }
+    }
+    if (anchor < 0) return false;
+    par[anchor][t0] = par[anchor][t1] = 0;
+    std::deque<int> q{anchor};
+    int seen = 1;
+    while (!q.empty()) {
+      const int x = q.front();
+      q.pop_front();
+      for (int y : eadj[x]) {
+        if (face[y] != f || par[y][t0] >= 0) continue;
+        const double d0 = cen[y][t0] / std::fabs(cen[y][a]) - cen[x][t0] / std::fabs(cen[x][a]);
+        const double d1 = cen[y][t1] / std::fabs(cen[y][a]) - cen[x][t1] / std::fabs(cen[x][a]);
+        par[y] = par[x];
+        par[y][std::fabs(d0) > std::fabs(d1) ? t0 : t1] ^= 1;
+        ++seen;
+        q.push_back(y);
+      }
+    }
+    if (seen != count) return false;
+  }
+  auto split = [](int axis, int L) { return axis == 0 ? (L & 1) : axis == 1 ? ((L >> 1) & 1) : ((L ^ (L >> 1)) & 1); };
+  std::vector<int> lab(ncol);
+  bool found = false;
+  for (int offs = 0; offs < 4096 && !found; ++offs) {
+    bool ok = true;
+    for (int k = 0; k < ncol && ok; ++k) {
+      const int f = face[k], a = f / 2, b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+      const int o0 = (offs >> (2 * f)) & 1, o1 = (offs >> (2 * f + 1)) & 1;
+      lab[k] = -1;
+      for (int L = 0; L < 4; ++L)
+        if (split(b, L) == (par[k][c] ^ o0) && split(c, L) == (par[k][b] ^ o1)) lab[k] = L;
+      ok = lab[k] >= 0;
+    }
+    if (!ok) return false;
+    for (int k = 0; k < ncol && ok; ++k)
+      for (int i = 0; i < 4 && ok; ++i)
+        for (int o : vcols[ccv[k][i]])
+          if (o != k && lab[o] == lab[k]) {
+            ok = false;
+            break;
+          }
+    found = ok;
+  }
+  if (!found) return false;
+  std::vector<int> out(n_cells);
+  for (int c = 0; c < n_cells; ++c) out[c] = lab[col[c]] + 4 * lpar[c];
+  // every pair of cells sharing a vertex differs
+  for (int c = 0; c < n_cells; ++c)
+    for (int v = 0; v < 8; ++v) {
+      const int p = pd[size_t(c) * 8 + v];
+      for (int k = vptr[p]; k < vptr[p + 1]; ++k)
+        if (vcells[k] != c && out[vcells[k]] == out[c]) return false;
+    }
+  color.swap(out);
+  return true;
+}
 
 // Host half of dcp_mesh_upload: validation, node map, node-local constraints,
 // colouring and block patterns (no device access, so it is testable on CPU).
@@ -441,6 +604,7 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     color[cell] = col;
     n_colors = std::max(n_colors, col + 1);
   }
+  if (n_colors > 8 && shell_colouring(n_cells, cell_geometry, pd, vptr, vcells, color)) n_colors = 8;
   h.color_ptr.assign(n_colors + 1, 0);
   for (int cell = 0; cell < n_cells; ++cell) h.color_ptr[color[cell] + 1]++;
   for (int k = 0; k < n_colors; ++k) h.color_ptr[k + 1] += h.color_ptr[k];

@@ -1389,7 +1389,7 @@ struct OpWaveSmem {
 #endif
 constexpr int kOpWaves = DCP_OPW_WAVES;  // waves (cells) per workgroup
 // colour classes below this many cells take the workgroup-per-cell kernel
-constexpr int kOpSmallColour = 4096;
+constexpr int kOpSmallColour = 1024;
 // timing probes only (wrong results): DCP_OPW_NOSCATTER skips the B^T / B
 // scatter, DCP_OPW_NORHS the rhs integrand, DCP_OPW_NOBT the B^T rows
 #ifndef DCP_OPW_NOSCATTER

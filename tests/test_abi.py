@@ -54,11 +54,14 @@ def test_host_mesh_helpers_without_gpu():
     assert m.cell_nse_dofs.shape == (48, 89)
 
 
-@pytest.mark.parametrize("r", [0, 1, 2, 3])
+@pytest.mark.parametrize("r", [0, 1, 2, 3, 4])
 def test_upload_conversion_shell(r):
     m = dcp.HostMesh(refine=r)
     ncol = m.check()
-    assert (8 if r > 0 else 2) <= ncol <= 27
+    # refine >= 1: the structured shell colouring (layer parity x a lateral
+    # 4-colouring of the cubed-sphere patches, checked on every vertex-sharing
+    # pair inside the library) replaces the greedy one's 14 classes
+    assert ncol == 8 if r > 0 else 2 <= ncol <= 8
 
 
 @pytest.mark.parametrize("r", [1, 2, 3])
