@@ -742,6 +742,21 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
   for (int i = t; i <= nc; i += nt) st->gamma[k + i] = gam[k + i];
 }
 
+// DCP_SS_NT (timing variant): the block's basis (1) and basis + W (2) loads
+// as nontemporal loads, so the up to 28 basis vectors the block streams do not
+// push the Schur complement (250 MB at refine 5) out of the 256 MiB Infinity
+// Cache between the block's four SpMVs
+#ifndef DCP_SS_NT
+#define DCP_SS_NT 2
+#endif
+__device__ inline double ss_ldv(const double* p) {
+  if (DCP_SS_NT >= 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ inline double ss_ldw(const double* p) {
+  if (DCP_SS_NT >= 2) return __builtin_nontemporal_load(p);
+  return *p;
+}
 template <int KL>
 __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs V, SStepArgs a,
                                                                int k, GmresDev* st, double* gran,
@@ -770,9 +785,10 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     live[e] = kk < g.n;
     pos[e] = live[e] ? unsigned(seg_pos(g, kk)) : 0u;
 #pragma unroll
-    for (int i = 0; i < S; ++i) w[e][i] = live[e] ? a.w[i][pos[e]] : 0.0;
+    for (int i = 0; i < S; ++i) w[e][i] = live[e] ? ss_ldw(a.w[i] + pos[e]) : 0.0;
 #pragma unroll
-    for (int j = 0; j < K; ++j) v[e][j] = (j < KL && j < d && live[e]) ? V.v[j][pos[e]] : 0.0;
+    for (int j = 0; j < K; ++j)
+      v[e][j] = (j < KL && j < d && live[e]) ? ss_ldv(V.v[j] + pos[e]) : 0.0;
   }
   double* part = gran;
   double* res = gran + kSsRes;

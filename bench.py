@@ -40,7 +40,7 @@ PMC_SUMMARIES = {(5, "explicit"): ("profiles/r03a_pmc_inner_r5.json", "k_sell_sp
 # orthogonalisation launches, for their roofline): the CGS2 chain (bench) and
 # the s-step block (inner probe)
 CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
-               (5, "sstep"): "profiles/r03o_inner_probe_sstep_kernel_stats.csv"}
+               (5, "sstep"): "profiles/r03ag_inner_probe_sstep_kernel_stats.csv"}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
 PMC_MF = {5: ("profiles/r02_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
 
