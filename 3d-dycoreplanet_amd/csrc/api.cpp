@@ -360,12 +360,38 @@ bool shell_colouring(int n_cells, const double* geo, const std::vector<int32_t>&
   return true;
 }
 
+// The whole mesh's 8-colour shell colouring restricted to a partition's cells
+// (localize: local cell -> global cell); empty when the mesh is no shell.
+std::vector<int> partition_colour_hint(int n_cells, const int32_t* cell_nse_dofs,
+                                       const double* cell_geometry, int n_u, int n_p,
+                                       const std::vector<int32_t>& cells_g) {
+  std::vector<int32_t> pd(size_t(n_cells) * 8);
+  for (int c = 0; c < n_cells; ++c)
+    for (int v = 0; v < 8; ++v) {
+      const int p = cell_nse_dofs[size_t(c) * 89 + 4 * v + 3] - n_u;
+      if (p < 0 || p >= n_p) return {};
+      pd[size_t(c) * 8 + v] = p;
+    }
+  std::vector<int32_t> vptr(size_t(n_p) + 1, 0), vcells(pd.size());
+  for (int32_t p : pd) vptr[p + 1]++;
+  for (int v = 0; v < n_p; ++v) vptr[v + 1] += vptr[v];
+  std::vector<int32_t> f(vptr.begin(), vptr.end() - 1);
+  for (int c = 0; c < n_cells; ++c)
+    for (int v = 0; v < 8; ++v) vcells[f[pd[size_t(c) * 8 + v]]++] = c;
+  std::vector<int> colour;
+  if (!shell_colouring(n_cells, cell_geometry, pd, vptr, vcells, colour)) return {};
+  std::vector<int> out(cells_g.size());
+  for (size_t i = 0; i < cells_g.size(); ++i) out[i] = colour[cells_g[i]];
+  return out;
+}
+
 // Host half of dcp_mesh_upload: validation, node map, node-local constraints,
 // colouring and block patterns (no device access, so it is testable on CPU).
 void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
                   const int32_t* cell_T_dofs, const double* cell_geometry,
                   const double* cell_diameter, int n_u, int n_p, int n_T,
-                  const dcp_constraints* nse_c, const dcp_constraints* T_c) {
+                  const dcp_constraints* nse_c, const dcp_constraints* T_c,
+                  const std::vector<int>* colour_hint = nullptr) {
   require(cell_nse_dofs && cell_T_dofs && cell_geometry && cell_diameter, DCP_ERR_INVALID,
           "NULL argument");
   require(n_cells > 0 && n_u > 0 && n_u % 3 == 0 && n_p > 0 && n_T > 0, DCP_ERR_INVALID,
@@ -603,6 +629,23 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     require(col < 64, DCP_ERR_UNSUPPORTED, "cell colouring needs more than 64 colours");
     color[cell] = col;
     n_colors = std::max(n_colors, col + 1);
+  }
+  if (colour_hint && int(colour_hint->size()) == n_cells) {
+    // a partition of the whole mesh keeps the whole mesh's colouring when it
+    // has fewer classes (checked again on the local cells)
+    const std::vector<int>& hc = *colour_hint;
+    const int nh = *std::max_element(hc.begin(), hc.end()) + 1;
+    bool ok = nh < n_colors && nh <= 64;
+    for (int c = 0; c < n_cells && ok; ++c)
+      for (int v = 0; v < 8 && ok; ++v) {
+        const int p = pd[size_t(c) * 8 + v];
+        for (int k = vptr[p]; k < vptr[p + 1]; ++k)
+          if (vcells[k] != c && hc[vcells[k]] == hc[c]) ok = false;
+      }
+    if (ok) {
+      color = hc;
+      n_colors = nh;
+    }
   }
   if (n_colors > 8 && shell_colouring(n_cells, cell_geometry, pd, vptr, vcells, color)) n_colors = 8;
   h.color_ptr.assign(n_colors + 1, 0);
@@ -1127,8 +1170,10 @@ int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t*
     }
     const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
     HostPrep h;
+    const std::vector<int> hint =
+        partition_colour_hint(n_cells, cell_nse_dofs, cell_geometry, n_u, n_p, L.cells_g);
     prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
-                 L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc);
+                 L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc, &hint);
     const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
                            int64_t(L.hv.peers.size()), int64_t(L.hv.send_idx.size()),
                            int64_t(L.hv.recv_idx.size()), int64_t(h.color_ptr.size()) - 1};
@@ -1861,13 +1906,15 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
         fail(DCP_ERR_INVALID, e.what());
       }
       const dcp_constraints lnc = L.nse_view(), ltc = L.T_view();
+      const std::vector<int> hint =
+          partition_colour_hint(n_cells, cell_nse_dofs, cell_geometry, n_u, n_p, L.cells_g);
       n_cells = L.n_cells;
       n_u = L.n_u();
       n_p = L.n_p();
       n_T = L.n_T();
       cell_diameter = L.diameter.data();
       prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
-                   cell_diameter, n_u, n_p, n_T, &lnc, &ltc);
+                   cell_diameter, n_u, n_p, n_T, &lnc, &ltc, &hint);
       require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
               "periodic constraints on several GPUs are not supported");
     } else {

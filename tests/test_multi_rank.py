@@ -113,6 +113,8 @@ def test_partition_covers_and_matches(refine, world):
     for r, i in enumerate(infos):
         for s, ids in i["send"].items():
             assert np.array_equal(ids, infos[s]["recv"][r])
+        # every partition keeps the whole shell's 8-colour layout
+        assert i["n_colors"] == 8
 
 
 def _time_step(ctx, m, u, T):
