@@ -128,6 +128,8 @@ void set_physics_dev(Ctx& c) {
 }
 
 double* field_ptr(Ctx& c, int field, size_t& n) {
+  if (field == DCP_OLD_NSE_SOLUTION) c.old_nse_ghosted = false;
+  if (field == DCP_OLD_T_SOLUTION) c.old_T_ghosted = false;
   switch (field) {
     case DCP_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.nse_sol.p;
     case DCP_OLD_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.old_nse.p;
@@ -137,6 +139,13 @@ double* field_ptr(Ctx& c, int field, size_t& n) {
     case DCP_T_RHS: n = size_t(c.n_T); return c.T_rhs.p;
     default: fail(DCP_ERR_INVALID, "unknown state field " + std::to_string(field));
   }
+}
+
+// the ghost entries of an old field were just made current (see Ctx)
+void mark_old_ghosted(Ctx& c, int field) {
+  if (c.old_external) return;
+  if (field == DCP_OLD_NSE_SOLUTION) c.old_nse_ghosted = true;
+  if (field == DCP_OLD_T_SOLUTION) c.old_T_ghosted = true;
 }
 
 struct PhaseTimer {
@@ -1504,6 +1513,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                      const double* cell_diameter, int n_u, int n_p, int n_T, int n_u_g, int n_p_g,
                      int n_T_g) {
     DCP_HIP_CHECK(hipSetDevice(c.cfg.device));
+    c.old_nse_ghosted = c.old_T_ghosted = false;
     c.feec = false;
     c.dim2 = false;
     c.vdim = 3;
@@ -1981,6 +1991,7 @@ int dcp_state_set_owned(dcp_ctx* ctx, int field, const double* host, size_t n) {
     // ghost entries from their owners (the Trilinos ghosted copy)
     const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
     if (c.comm) halo_exchange(c, T ? c.halo_T : c.halo_nse, p);
+    mark_old_ghosted(c, field);
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     return DCP_OK;
   });
@@ -2022,6 +2033,7 @@ int dcp_state_set(dcp_ctx* ctx, int field, const double* host, size_t n) {
       std::vector<double> loc(want);
       for (size_t i = 0; i < want; ++i) loc[i] = host[g[i]];
       DCP_HIP_CHECK(hipMemcpy(p, loc.data(), want * sizeof(double), hipMemcpyHostToDevice));
+      mark_old_ghosted(*ctx, field);
       return DCP_OK;
     }
     require(n == want, DCP_ERR_INVALID, "state size mismatch");
@@ -2064,12 +2076,20 @@ int dcp_state_copy(dcp_ctx* ctx, int dst_field, int src_field) {
     double* s = field_ptr(*ctx, src_field, ns);
     require(nd == ns, DCP_ERR_INVALID, "state size mismatch");
     copy(int(nd), s, d, ctx->stream);
+    if (dst_field == DCP_OLD_NSE_SOLUTION || dst_field == DCP_OLD_T_SOLUTION) {
+      // old = new as the reference's ghosted assignment: owned entries copied,
+      // ghosts imported from their owners (several GPUs)
+      Ctx& c = *ctx;
+      halo_exchange(c, dst_field == DCP_OLD_T_SOLUTION ? c.halo_T : c.halo_nse, d);
+      mark_old_ghosted(c, dst_field);
+    }
     return DCP_OK;
   });
 }
 
 double* dcp_state_device_ptr(dcp_ctx* ctx, int field) {
   if (!ctx || !ctx->have_mesh) return nullptr;
+  if (field == DCP_OLD_NSE_SOLUTION || field == DCP_OLD_T_SOLUTION) ctx->old_external = true;
   size_t n = 0;
   try {
     return field_ptr(*ctx, field, n);
@@ -2115,9 +2135,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       c.nse_rhs.zero(c.stream);
       out.rhs = c.nse_rhs.p;
     }
-    // ghosted old solutions (the reference reads the ghosted vectors, :583-589)
-    halo_exchange(c, c.halo_nse, c.old_nse.p);
-    halo_exchange(c, c.halo_T, c.old_T.p);
+    // ghosted old solutions (the reference reads the ghosted vectors, :583-589,
+    // which its time loop imported at old = new): exchanged here only if the
+    // old fields were written some other way since
+    if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
+    if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     for (int k = 0; k < c.n_colors(); ++k) {
       if (full)
         launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
@@ -2214,7 +2236,7 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
     csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
     c.T_rhs.zero(c.stream);
-    halo_exchange(c, c.halo_T, c.old_T.p);
+    if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     halo_exchange(c, c.halo_nse, c.nse_sol.p);
     if (c.dim2) {
       assemble_T_rhs_2d(c);
@@ -2341,6 +2363,10 @@ int dcp_advance_state(dcp_ctx* ctx) {
     Ctx& c = *ctx;
     copy(c.n_u + c.n_p, c.nse_sol.p, c.old_nse.p, c.stream);
     copy(c.n_T, c.T_sol.p, c.old_T.p, c.stream);
+    halo_exchange(c, c.halo_nse, c.old_nse.p);
+    halo_exchange(c, c.halo_T, c.old_T.p);
+    mark_old_ghosted(c, DCP_OLD_NSE_SOLUTION);
+    mark_old_ghosted(c, DCP_OLD_T_SOLUTION);
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     return DCP_OK;
   });

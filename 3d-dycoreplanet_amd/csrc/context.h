@@ -293,6 +293,13 @@ struct Ctx {
   int schur_ev_used = 0;
   long schur_calls = 0;
   bool time_schur = false;
+  // several GPUs: the ghost entries of old_nse / old_T are current (set where
+  // the library itself made them so: set_state, copy_state and advance_state
+  // into an old field, which exchange them as the reference's ghosted
+  // assignment old = new does; cleared by every other access to the field),
+  // so assemble_nse_system need not exchange them again
+  bool old_nse_ghosted = false, old_T_ghosted = false;
+  bool old_external = false;  // a caller holds a device pointer to an old field
   // the same for the matrix-free applies: [0] Stokes, [1] velocity block
   static constexpr int kMfEvents = 128;
   std::vector<Timer> mf_ev[2];

@@ -442,3 +442,73 @@ def test_group_bench_sequence_8_ranks():
     for r in results:
         assert r["timings"]["assemble_nse_ms"] > 0
         assert r["pattern"]["nnz_S"] > 0
+
+
+def _two_steps(ctx, m, u, T, via):
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    ctx.solve_nse()
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    ctx.solve_temperature()
+    if via == "advance":
+        ctx.advance_state()
+    else:
+        ctx.copy_state(dcp.OLD_NSE_SOLUTION, dcp.NSE_SOLUTION)
+        ctx.copy_state(dcp.OLD_T_SOLUTION, dcp.T_SOLUTION)
+    ctx.assemble_nse_system()
+    out = {"rhs": ctx.get_state(dcp.NSE_RHS)}
+    ctx.assemble_temperature_matrix()
+    ctx.assemble_temperature_rhs()
+    out["T_rhs"] = ctx.get_state(dcp.T_RHS)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,via", [(2, "advance"), (3, "copy")])
+def test_group_second_step_reads_current_ghosts(world, via):
+    """old = new (dcp_advance_state, or dcp_state_copy into the old fields)
+    imports the old fields' ghost entries, and assemble_nse_system then skips
+    its own exchange: the second step's assembled rhs on every rank's owned
+    entries matches one GPU (a stale ghost would show at O(1) near the
+    partition boundaries)."""
+    m = dcp.HostMesh(refine=2)
+    rng = np.random.default_rng(5)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    T = m.T0 + 0.01 * rng.uniform(-1, 1, m.n_T)
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(dcp.classic_physics())
+    ref_ctx.upload_mesh(m)
+    ref = _two_steps(ref_ctx, m, u, T, via)
+    ref_ctx.close()
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(dcp.classic_physics())
+            ctx.upload_mesh(m)
+            results[rank] = _two_steps(ctx, m, u, T, via)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    for key in ("rhs", "T_rhs"):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        assert rel(v, ref[key]) < 1e-9, key
