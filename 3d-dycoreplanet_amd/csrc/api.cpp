@@ -1606,9 +1606,9 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
     c.first_touch_A = mark_first_touch(c.color_cells.p, c.color_ptr, 729, c.posA.p, n_cells,
                                        Ac.size(), c.stream);
     c.first_touch_Bt = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posBt.p, n_cells,
-                                        Btc.size(), c.stream, c.Bt_val.p, 3);
+                                        Btc.size(), c.stream);
     c.first_touch_B = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posB.p, n_cells,
-                                       Bc.size(), c.stream, c.B_val.p, 3);
+                                       Bc.size(), c.stream);
     {
       // matrix-free operator: first-touch bits in colour order, constrained
       // velocity dofs with the position of their assembled diagonal entry,

@@ -267,8 +267,7 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (then the assembly stores first and needs no zero fill), else the
 // positions are left plain.
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
-                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
-                      double* val = nullptr, int blk = 0);
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s);
 
 // S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
 // contributions summed in fixed node order: deterministic). pmap != null:

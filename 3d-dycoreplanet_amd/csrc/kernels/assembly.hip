@@ -1788,20 +1788,8 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-namespace {
-// the blocks no cell touches (condensed-away couplings of constrained rows)
-__global__ void k_zero_untouched(size_t nnz, int blk, const uint8_t* __restrict__ touched,
-                                 double* __restrict__ val) {
-  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nnz;
-       i += size_t(gridDim.x) * blockDim.x)
-    if (!touched[i])
-      for (int k = 0; k < blk; ++k) val[size_t(blk) * i + k] = 0.0;
-}
-}  // namespace
-
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
-                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s, double* val,
-                      int blk) {
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s) {
   uint8_t* touched = nullptr;
   unsigned long long* count = nullptr;
   DCP_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&touched), nnz, s));
@@ -1818,17 +1806,9 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
   unsigned long long h = 0;
   DCP_HIP_CHECK(hipMemcpyAsync(&h, count, sizeof(h), hipMemcpyDeviceToHost, s));
   DCP_HIP_CHECK(hipStreamSynchronize(s));
-  const bool untouched_zeroed = h != nnz && val != nullptr;
-  if (untouched_zeroed) {
-    // zero the never-touched blocks once here; every other block is stored by
-    // its first cell, so the assembly needs no zero fill of the whole array
-    hipLaunchKernelGGL(k_zero_untouched, dim3(2048), dim3(256), 0, s, nnz, blk, touched, val);
-    DCP_HIP_CHECK(hipGetLastError());
-    DCP_HIP_CHECK(hipStreamSynchronize(s));
-  }
   DCP_HIP_CHECK(hipFree(touched));
   DCP_HIP_CHECK(hipFree(count));
-  if (h == nnz || untouched_zeroed) return true;
+  if (h == nnz) return true;
   // some block is never touched by a cell: keep plain positions (zero fill needed)
   hipLaunchKernelGGL(k_clear_first_touch, dim3(1024), dim3(256), 0, s, size_t(per_cell) * n_cells, pos);
   DCP_HIP_CHECK(hipGetLastError());
