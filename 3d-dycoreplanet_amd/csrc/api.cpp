@@ -1023,7 +1023,10 @@ void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_
   auto ncol = [&](int q) { return iperm.empty() || q >= rows ? q : iperm[q]; };
   std::vector<int64_t> off(size_t(n_sl) + 1, 0);
   std::vector<int32_t> base(n_sl, 0);
-  bool c16 = !perm.empty();
+  // 16-bit column offsets wherever every slice's columns span < 2^16: the
+  // RCM order on one GPU, and any rank's local S on several GPUs (local
+  // columns, owned + ghost, ~30 k at refine 5 on 8 ranks)
+  bool c16 = true;
   for (int sl = 0; sl < n_sl; ++sl) {
     int w = 0, lo = INT32_MAX, hi = 0;
     for (int r = 64 * sl; r < std::min(rows, 64 * sl + 64); ++r) {

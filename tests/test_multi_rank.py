@@ -442,6 +442,8 @@ def test_group_bench_sequence_8_ranks():
     for r in results:
         assert r["timings"]["assemble_nse_ms"] > 0
         assert r["pattern"]["nnz_S"] > 0
+        # a rank's local S (owned rows, owned + ghost columns) in 16-bit offsets
+        assert r["layout"]["col_bytes"] == 2 and not r["layout"]["permuted"]
 
 
 def _two_steps(ctx, m, u, T, via):
