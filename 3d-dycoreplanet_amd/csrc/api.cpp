@@ -1135,6 +1135,11 @@ void materialize_velocity_block(Ctx& c) {
 
 // nse_matrix.block(1,0) of the last operator-form assembly: the transpose of
 // B^T, block by block (bitwise the B the full scatter produces)
+void set_ctx_error(dcp_ctx* ctx, const char* msg) {
+  if (ctx) ctx->err = msg;
+  g_last_error = msg;
+}
+
 void materialize_B(Ctx& c) {
   if (c.B_current) return;
   transpose_blocks3(long(c.B_tperm.n), c.B_tperm.p, c.Bt_val.p, c.B_val.p, c.stream);
@@ -1460,6 +1465,15 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->inner_max_steps = value;
       return DCP_OK;
     }
+    if (option == DCP_OPT_BLOCK_FIXED_INNER) {
+      require(value >= 0, DCP_ERR_INVALID, "DCP_OPT_BLOCK_FIXED_INNER must be >= 0");
+      ctx->block_fixed_inner = value;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_HANDOFF_SPIN_LIMIT) {
+      set_handoff_spin_limit(value);
+      return DCP_OK;
+    }
     if (option == DCP_OPT_FGMRES_MAX_OUTER) {
       require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_FGMRES_MAX_OUTER must be >= 1");
       ctx->fgmres_max_outer = value;
@@ -1607,11 +1621,11 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                               c.B_col.p, c.T_ptr.p, c.T_col.p, c.posA.p, c.posBt.p, c.posB.p,
                               c.posT.p, c.stream);
     c.first_touch_A = mark_first_touch(c.color_cells.p, c.color_ptr, 729, c.posA.p, n_cells,
-                                       Ac.size(), c.stream);
+                                       Ac.size(), c.stream, &c.touched_A);
     c.first_touch_Bt = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posBt.p, n_cells,
-                                        Btc.size(), c.stream);
+                                        Btc.size(), c.stream, &c.touched_Bt);
     c.first_touch_B = mark_first_touch(c.color_cells.p, c.color_ptr, 216, c.posB.p, n_cells,
-                                       Bc.size(), c.stream);
+                                       Bc.size(), c.stream, &c.touched_B);
     {
       // matrix-free operator: first-touch bits in colour order, constrained
       // velocity dofs with the position of their assembled diagonal entry,
@@ -2548,6 +2562,108 @@ int dcp_pattern_info(dcp_ctx* ctx, int64_t* nA, int64_t* nBt, int64_t* nB, int64
   });
 }
 
+int dcp_halo_selftest(dcp_ctx* ctx, int n, double* vec, int n_list, const int32_t* send_pos,
+                      const int32_t* recv_pos, int n_peers) {
+  return guarded(ctx, [&] {
+    require(ctx && vec && send_pos && recv_pos, DCP_ERR_INVALID, "NULL argument");
+    Ctx& c = *ctx;
+    require(c.comm != nullptr, DCP_ERR_STATE, "no communicator (nccl_id or group)");
+    require(n > 0 && n_list >= 0 && n_peers >= 1 && n_peers <= n_list + 1, DCP_ERR_INVALID,
+            "bad sizes");
+    for (int i = 0; i < n_list; ++i)
+      require(send_pos[i] >= 0 && send_pos[i] < n && recv_pos[i] >= 0 && recv_pos[i] < n,
+              DCP_ERR_INVALID, "position out of range");
+    // the forward halo of the solver (gather, grouped send/recv, scatter) with
+    // every peer this rank itself: the list split into n_peers chunks
+    Ctx::Halo h;
+    h.ns = h.nr = n_list;
+    for (int k = 0; k < n_peers; ++k) {
+      const size_t b = size_t(n_list) * k / n_peers, e = size_t(n_list) * (k + 1) / n_peers;
+      h.peers.push_back(c.comm->rank);
+      h.soff.push_back(b);
+      h.roff.push_back(b);
+      h.sn.push_back(e - b);
+      h.rn.push_back(e - b);
+    }
+    h.spos.upload(std::vector<int32_t>(send_pos, send_pos + n_list));
+    h.rpos.upload(std::vector<int32_t>(recv_pos, recv_pos + n_list));
+    h.sbuf.alloc(std::max(n_list, 1));
+    h.rbuf.alloc(std::max(n_list, 1));
+    DBuf<double> v;
+    v.upload(std::vector<double>(vec, vec + n));
+    halo_exchange(c, h, v.p);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    DCP_HIP_CHECK(hipMemcpy(vec, v.p, size_t(n) * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_touch) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    const Ctx& c = *ctx;
+    require(!c.dim2 && !c.feec, DCP_ERR_UNSUPPORTED, "3D classic mesh only");
+    const int64_t t[3] = {int64_t(c.touched_A), int64_t(c.touched_Bt), int64_t(c.touched_B)};
+    const int64_t n[3] = {int64_t(c.A_col.n), int64_t(c.Bt_col.n), int64_t(c.B_col.n)};
+    const int f[3] = {c.first_touch_A, c.first_touch_Bt, c.first_touch_B};
+    for (int i = 0; i < 3; ++i) {
+      if (touched) touched[i] = t[i];
+      if (nnzb) nnzb[i] = n[i];
+      if (first_touch) first_touch[i] = f[i];
+    }
+    return DCP_OK;
+  });
+}
+
+int dcp_nse_coupling_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,
+                            double* vals) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(!c.dim2 && !c.feec, DCP_ERR_UNSUPPORTED, "3D classic mesh only");
+    require(nnz != nullptr && (which == 0 || which == 1), DCP_ERR_INVALID, "bad arguments");
+    const DBuf<int32_t>& P = which == 0 ? c.Bt_ptr : c.B_ptr;
+    const DBuf<int32_t>& C = which == 0 ? c.Bt_col : c.B_col;
+    const int rows = int(P.n) - 1;  // local rows (the owned nodes' on several GPUs)
+    *nnz = int64_t(C.n) * 3;
+    if (!rowptr) return DCP_OK;
+    require(cols && vals, DCP_ERR_INVALID, "NULL cols/vals");
+    require(c.nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
+    // the operator form's own blocks: B^T as scattered, B as the solve reads it
+    // (materialised from B^T unless scattered); the velocity block untouched
+    if (which == 1) materialize_B(c);
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<int32_t> p(P.n), cl(C.n);
+    std::vector<double> v(C.n * 3);
+    DCP_HIP_CHECK(hipMemcpy(p.data(), P.p, P.n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(cl.data(), C.p, C.n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipMemcpy(v.data(), which == 0 ? c.Bt_val.p : c.B_val.p, v.size() * sizeof(double),
+                            hipMemcpyDeviceToHost));
+    int64_t k = 0;
+    rowptr[0] = 0;
+    if (which == 0) {  // scalar rows 3 n + r, columns the pressure dofs
+      for (int n = 0; n < rows; ++n)
+        for (int r = 0; r < 3; ++r) {
+          for (int b = p[n]; b < p[n + 1]; ++b) {
+            cols[k] = cl[b];
+            vals[k++] = v[3 * size_t(b) + r];
+          }
+          rowptr[3 * n + r + 1] = int32_t(k);
+        }
+    } else {  // pressure rows, columns the velocity dofs 3 n + c
+      for (int q = 0; q < rows; ++q) {
+        for (int b = p[q]; b < p[q + 1]; ++b)
+          for (int cc = 0; cc < 3; ++cc) {
+            cols[k] = 3 * cl[b] + cc;
+            vals[k++] = v[3 * size_t(b) + cc];
+          }
+        rowptr[q + 1] = int32_t(k);
+      }
+    }
+    return DCP_OK;
+  });
+}
+
 int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
@@ -2561,6 +2677,7 @@ int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permute
 
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out) {
   if (!ctx || !out) return DCP_ERR_INVALID;
+  ctx->timings.handoff_timeouts = ctx->handoff_timeouts;
   *out = ctx->timings;
   return DCP_OK;
 }
@@ -2872,6 +2989,7 @@ int dcp_feec_assemble_nse_system(dcp_ctx* ctx) {
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
+    SectionScope sec(c, "   Assemble NSE system");  // FEEC.tpp:831
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
     halo_exchange(c, c.halo_nse, c.old_nse.p);
     halo_exchange(c, c.halo_T, c.old_T.p);
@@ -2891,11 +3009,15 @@ int dcp_feec_build_nse_preconditioner(dcp_ctx* ctx) {
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(c.feec, DCP_ERR_STATE, "no FEEC mesh uploaded");
+    SectionScope sec(c, "   Build NSE FEEC preconditioner");  // FEEC.tpp:630
     PhaseTimer t(c, &c.timings.build_precond_ms);
-    c.fp_val.zero(c.stream);
-    for (int k = 0; k < c.n_colors(); ++k)
-      launch_feec_precond(c.fcd(), c.color_begin(k), c.color_size(k), c.fp_pos.p, c.ph, c.fp_val.p,
-                          c.stream);
+    {
+      SectionScope sub(c, "   Assembly NSE preconditioner");  // FEEC.tpp:592
+      c.fp_val.zero(c.stream);
+      for (int k = 0; k < c.n_colors(); ++k)
+        launch_feec_precond(c.fcd(), c.color_begin(k), c.color_size(k), c.fp_pos.p, c.ph,
+                            c.fp_val.p, c.stream);
+    }
     t.stop();
     c.fe_precond = true;
     return DCP_OK;
@@ -2907,6 +3029,7 @@ int dcp_feec_solve_nse(dcp_ctx* ctx, int* iterations) {
     need_ready(*ctx);
     Ctx& c = *ctx;
     require(c.feec && c.fe_assembled, DCP_ERR_STATE, "assemble the FEEC system first");
+    SectionScope sec(c, "   Solve NSE system");  // FEEC.tpp:1277
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     const int rc = feec_solve_nse(c, iterations);
     t.stop();
@@ -3113,6 +3236,13 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
 
 int dcp_host_feec_view_get(dcp_host_mesh* h, dcp_feec_mesh* out) {
   if (!h || !out) return DCP_ERR_INVALID;
+  if (h->mesh.cuboid) {
+    // the cuboid's x/y periodicity (planet_geometry.tpp:44-56) would need
+    // periodic identification of the Nedelec / RT / DGQ0 dofs, which
+    // feec_dofs does not do: periodic faces would silently become boundary faces
+    g_last_error = "FEEC on the periodic cuboid is not supported (no periodic FEEC dofs)";
+    return DCP_ERR_UNSUPPORTED;
+  }
   try {
     if (!h->feec) h->feec = std::make_unique<FeecDofs>(feec_dofs(h->mesh));
   } catch (const std::exception& e) {
@@ -3265,6 +3395,7 @@ int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len) 
     out->use_block_preconditioner_feec = p.use_block_preconditioner_feec ? 1 : 0;
     out->correct_pressure_to_zero_mean = p.correct_pressure_to_zero_mean ? 1 : 0;
     out->solver_diagnostics_level = int(p.solver_diagnostics_print_level);
+    out->use_direct_solver = p.use_direct_solver ? 1 : 0;
     return DCP_OK;
   } catch (const std::exception& e) {
     if (err && err_len > 0) {

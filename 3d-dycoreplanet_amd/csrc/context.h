@@ -128,6 +128,8 @@ struct Ctx {
   DBuf<int32_t> posA, posBt, posB, posT;
   // scatter positions carry first-touch marks (no zero fill before assembly)
   bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
+  // blocks some cell's scatter position reaches (first-touch marking at upload)
+  unsigned long long touched_A = 0, touched_Bt = 0, touched_B = 0;
   // nse_matrix in operator form: B^T, B and the diagonal of the constrained
   // velocity rows (con_diag, [constrained node][3], indexed by mf_cidx) are
   // assembled; the velocity-velocity block A is applied matrix-free and
@@ -252,6 +254,8 @@ struct Ctx {
   unsigned long long chain_seq = 0;
   int n_cus = 0;
   bool fused_chain = true;
+  int handoff_timeouts = 0;  // one-launch hand-offs that timed out (fused_chain then off)
+  DBuf<double> inner_x0;     // the inner Schur solve's initial guess (rerun after a timeout)
   // DCP_OPT_GRAM_SCHMIDT: 0 = modified (deal.II SolverGMRES, default), 1 = the
   // inner Schur GMRES with classical Gram-Schmidt twice, 2 = DCGS2 (one
   // reduction per step), each restart cycle device-resident
@@ -271,6 +275,7 @@ struct Ctx {
   int fgmres_max_outer = 40;         // SolverControl(40) of the first FGMRES (test hook)
   int inner_max_steps = 5000;        // SolverControl(5000) of the inner Schur GMRES (probe hook)
   int schur_fixed_inner = 0;         // DCP_OPT_SCHUR_FIXED_INNER (parity hook of solve_nse_schur)
+  int block_fixed_inner = 0;         // DCP_OPT_BLOCK_FIXED_INNER (parity hook of block_prec)
   long a_solve_its = 0;              // AztecOO A-GMRES iterations of the last solve_nse
   // test hook, read at context creation: DCP_TEST_FORCE_REORTH_AT=k makes the
   // loss-of-orthogonality test at inner step k (a multiple of 5 minus 1) trigger

@@ -267,7 +267,8 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (then the assembly stores first and needs no zero fill), else the
 // positions are left plain.
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
-                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s);
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
+                      unsigned long long* touched_out = nullptr);
 
 // S = B diag(d) B^T into the precomputed CSR pattern (one wavefront per row,
 // contributions summed in fixed node order: deterministic). pmap != null:
@@ -475,6 +476,9 @@ void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, Gmr
 // nb resident workgroups (cgs2_chain_fits: nb <= n_cus, enough entries per
 // thread) handing their sums over as granules in gran (kMgsGranules doubles).
 bool cgs2_chain_fits(long n, int nb, int n_cus);
+// Test hook: the hand-off poll bound of the one-launch CGS2 / DCGS2 / s-step
+// kernels (<= 0: the default, kernels/granule.h kMgsMaxSpins).
+void set_handoff_spin_limit(long spins);
 void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, double* gran,
                      int nb, unsigned long long seq, double* err, hipStream_t s);
 void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,

@@ -12,6 +12,10 @@
 
 #include "../../include/dcp.h"
 
+namespace dcp {
+void set_ctx_error(dcp_ctx* ctx, const char* msg);  // api.cpp: dcp_last_error(ctx)
+}
+
 namespace {
 
 // recompute_time_step (boussinesq_model.tpp:1104-1125; FEEC.tpp:1241-1261):
@@ -40,8 +44,27 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
     }
   } run_section{ctx, t_run};
   const bool feec = rp->use_FEEC_solver != 0;
-  // solve_NSE_Schur_complement instead of the block preconditioner (:1896-1902)
-  const bool schur = !feec && rp->use_schur_complement_solver != 0;
+  // solve_NSE_Schur_complement instead of the block preconditioner (:1896-1902;
+  // FEEC.tpp:2292-2298)
+  const bool schur = rp->use_schur_complement_solver != 0;
+  auto unsupported = [&](const char* what) {
+    dcp::set_ctx_error(ctx, what);
+    return DCP_ERR_UNSUPPORTED;
+  };
+  if (rp->use_direct_solver)  // the reference throws at its first step (:1886-1893)
+    return unsupported("Solver not implemented: MUMPS does not work on "
+                       "TrilinosWrappers::MPI::BlockSparseMatrix classes.");
+  if (feec) {
+    if (rp->nse_velocity_degree != 1)
+      return unsupported("FEEC: only nse velocity degree = 1 (Nedelec(0) / RT(0) / DGQ(0))");
+    if (rp->physics.cuboid)
+      return unsupported("FEEC on the periodic cuboid is not supported");
+    if (!schur && !rp->use_block_preconditioner_feec)
+      return unsupported("FEEC: use block preconditioner feec = false (identity-preconditioned "
+                         "GMRES, FEEC.tpp:1420-1431) is not implemented");
+  } else if (rp->nse_velocity_degree != 2) {
+    return unsupported("classic model: only nse velocity degree = 2 (Q2/Q1)");
+  }
   const int interval = std::max(1, rp->physics.nse_solver_interval);
   dcp_run_report r{};
   r.time_step = rp->physics.time_step;
@@ -64,7 +87,8 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
     if (n == 0 || n % interval == 0) {
       if (feec) {
         if ((rc = dcp_feec_assemble_nse_system(ctx)) < 0) return rc;
-        if (rp->use_block_preconditioner_feec &&
+        // FEEC.tpp:2264-2276: only without the Schur-complement solver
+        if (!schur && rp->use_block_preconditioner_feec &&
             (rc = dcp_feec_build_nse_preconditioner(ctx)) < 0)
           return rc;
       } else {
@@ -82,7 +106,10 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
     r.fgmres_outer = r.schur_inner = 0;
     rc = DCP_OK;
     if (n == 0 || n % interval == 0) {
-      if (feec) {
+      if (feec && schur) {
+        // FEEC's solve_NSE_Schur_complement is commented out (FEEC.tpp:1480-
+        // 1500): nothing is solved, nse_solution keeps its value
+      } else if (feec) {
         int it = 0;
         rc = dcp_feec_solve_nse(ctx, &it);
         r.fgmres_outer = it;

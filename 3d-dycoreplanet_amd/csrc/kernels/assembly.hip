@@ -1789,7 +1789,8 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 }
 
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
-                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s) {
+                      int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
+                      unsigned long long* touched_out) {
   uint8_t* touched = nullptr;
   unsigned long long* count = nullptr;
   DCP_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&touched), nnz, s));
@@ -1808,6 +1809,7 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
   DCP_HIP_CHECK(hipStreamSynchronize(s));
   DCP_HIP_CHECK(hipFree(touched));
   DCP_HIP_CHECK(hipFree(count));
+  if (touched_out) *touched_out = h;
   if (h == nnz) return true;
   // some block is never touched by a cell: keep plain positions (zero fill needed)
   hipLaunchKernelGGL(k_clear_first_touch, dim3(1024), dim3(256), 0, s, size_t(per_cell) * n_cells, pos);

@@ -45,14 +45,26 @@ __device__ inline double granule_value(const mgs_u4& q) {
 #ifndef DCP_MGS_SLEEP
 #define DCP_MGS_SLEEP 1
 #endif
-constexpr long kMgsMaxSpins = 1L << 21;
+// A hand-off normally completes in microseconds; ~2^19 polls (tenths of a
+// second) mean a producer never ran (the grid was not all resident).
+constexpr long kMgsMaxSpins = 1L << 19;
+
+// Timed out waiting for a hand-off: the host flag (err, mapped memory) and,
+// with a device GMRES state, status 3 so every later launch of the solve
+// returns at entry and the host's cycle loop stops at the next report instead
+// of spinning through thousands of stuck launches.
+__device__ inline void handoff_timeout(double* err, int* status) {
+  *err = 1.0;
+  if (status) atomicMax(status, 3);
+}
 
 // Wave 0 only: waits for the nb <= 256 granules of one step (lane l polls
 // granules l, l+64, l+128, l+192, four `sc1` loads in flight) and returns, in
 // every lane, their sum in exactly block_sum's order (thread t holds granule
 // t; xor butterfly per 64-thread wave; the four wave sums left to right).
 __device__ inline double granule_coef(const double* gran, int nb, unsigned long long tag,
-                                      double* err) {
+                                      double* err, int* status = nullptr,
+                                      long max_spins = kMgsMaxSpins) {
   const int l = threadIdx.x & 63;
   const double* p = gran + 2 * size_t(l);
   mgs_u4 q0, q1, q2, q3;
@@ -70,8 +82,8 @@ __device__ inline double granule_coef(const double* gran, int nb, unsigned long 
     const bool ok = (l >= nb || tag_is(q0, tag)) && (l + 64 >= nb || tag_is(q1, tag)) &&
                     (l + 128 >= nb || tag_is(q2, tag)) && (l + 192 >= nb || tag_is(q3, tag));
     if (__all(ok)) break;
-    if (++spins >= kMgsMaxSpins) {
-      if (l == 0) *err = 1.0;
+    if (++spins >= max_spins) {
+      if (l == 0) handoff_timeout(err, status);
       break;
     }
     if (DCP_MGS_SLEEP) __builtin_amdgcn_s_sleep(DCP_MGS_SLEEP);

@@ -67,6 +67,10 @@ __device__ inline double block_sums(double (&s)[K], int d, double* sm) {
   return j < d ? sm[j] + sm[K + j] + sm[2 * K + j] + sm[3 * K + j] : 0.0;
 }
 
+// hand-off poll bound of the one-launch kernels below (kMgsMaxSpins; a test
+// hook lowers it to make the timeout path run, set_handoff_spin_limit)
+__constant__ long g_spin_limit = kMgsMaxSpins;
+
 constexpr int kCgsElems = 2;          // vector entries per thread
 constexpr long kCgsMaxSpins = 1L << 22;
 
@@ -165,7 +169,7 @@ __device__ void gmres_step(GmresDev* st, double nrm2, int k) {
     const double rho = fabs(gk1);
     st->rho = rho;
     st->inv_norm = nrm != 0 ? 1.0 / nrm : 1.0;
-    st->status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
+    atomicMax(&st->status, rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0));
   }
   __syncthreads();
   if (t <= k) st->H[t][k] = h[t];
@@ -444,15 +448,15 @@ __global__ __launch_bounds__(kChainThreads) void k_cgs2_chain(Seg g, double* w, 
     } else {
     if (pub) granule_store(part + 2 * (size_t(col) * nb + b), r, tag);
     if (b < ncol && threadIdx.x < 64) {
-      const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err);
+      const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err, &st->status, g_spin_limit);
       if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + 1);
     }
     if (int(threadIdx.x) < ncol) {
       const double* p = res + 2 * threadIdx.x;
       mgs_u4 q = granule_load(p);
       for (long spins = 0; !tag_is(q, tag + 1); ++spins) {
-        if (spins >= kMgsMaxSpins) {
-          *err = 1.0;
+        if (spins >= g_spin_limit) {
+          handoff_timeout(err, &st->status);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -513,8 +517,9 @@ template <int K>
 void cgs_step_k(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,
                 GmresDev* st, unsigned long long& seq, double* err, Comm* comm, hipStream_t s) {
   const int* status = &st->status;
-  const int nb = int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
-  if (nb <= 0) return;
+  // a rank with no owned pressure rows still runs one (empty) block per launch:
+  // it must join every all-reduce and run the Givens step like the others
+  const int nb = std::max(1, int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)));
   hipLaunchKernelGGL((k_cgs_dot<K>), dim3(nb), dim3(kBlock), 0, s, g, w, V, d, gran, cnt,
                      st->coef, ++seq, err, status);
   DCP_HIP_CHECK(hipGetLastError());
@@ -535,6 +540,11 @@ void cgs_step_k(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsig
 }
 
 }  // namespace
+
+void set_handoff_spin_limit(long spins) {
+  const long v = spins > 0 ? spins : kMgsMaxSpins;
+  DCP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &v, sizeof(v)));
+}
 
 bool cgs2_chain_fits(long n, int nb, int n_cus) {
   return nb >= kGmMaxDim && nb <= n_cus && nb <= 256 &&
@@ -721,7 +731,7 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
         st->accumulated = acc;
         st->dim = kk + 1;
         st->rho = rho;
-        st->status = status;
+        atomicMax(&st->status, status);
         last_col = c;
         break;
       }
@@ -817,15 +827,15 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     }
     // workgroup c reduces column c and publishes the total
     if (b < ncol && threadIdx.x < 64) {
-      const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err);
+      const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err, &st->status, g_spin_limit);
       if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + 1);
     }
     for (int c = threadIdx.x; c < ncol; c += kChainThreads) {
       const double* p = res + 2 * c;
       mgs_u4 q = granule_load(p);
       for (long spins = 0; !tag_is(q, tag + 1); ++spins) {
-        if (spins >= kMgsMaxSpins) {
-          *err = 1.0;
+        if (spins >= g_spin_limit) {
+          handoff_timeout(err, &st->status);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -873,7 +883,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   if (b != 0) return;
   if (bad) {  // the block lost rank: a breakdown the one-vector process would not see
     if (threadIdx.x == 0) {
-      st->status = 2;
+      atomicMax(&st->status, 2);
       st->rho = __longlong_as_double(0x7ff8000000000000LL);
     }
     return;
@@ -1020,7 +1030,7 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
   if (blockIdx.x != 0) return;
   if (bad) {
     if (threadIdx.x == 0) {
-      st->status = 2;
+      atomicMax(&st->status, 2);
       st->rho = __longlong_as_double(0x7ff8000000000000LL);
     }
     return;
@@ -1052,10 +1062,13 @@ void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, Gmr
                        unsigned long long& seq, double* err, Comm* comm, hipStream_t s) {
   ChainVecs Vp = V;
   for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
-  const int nb = int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  // a rank with no owned pressure rows still runs one (empty) block per launch:
+  // it joins both all-reduces and block 0 of k_ss_final runs the Hessenberg
+  // columns, Givens steps and status like every other rank
+  const int nb = std::max(1, int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)));
   const int ncol1 = kSStep * (k + 1), ncol2 = ncol1 + kSStep * (kSStep + 1) / 2;
   const int* status = &st->status;
-  if (nb > 0) {
+  {
 #define DCP_SSM(KL)                                                                              \
   if (k + 1 <= KL) {                                                                             \
     hipLaunchKernelGGL((k_ss_dots<KL, 0>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, nullptr,   \
@@ -1080,17 +1093,12 @@ void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, Gmr
 #undef DCP_SSM
     throw std::runtime_error("sstep_block_multi: basis too long");
   }
-  // no owned entries on this rank: still take part in the all-reduces
-  if (comm) {
-    DCP_HIP_CHECK(hipMemsetAsync(c1, 0, size_t(ncol1) * sizeof(double), s));
-    comm->allreduce(c1, size_t(ncol1), false, s);
-    DCP_HIP_CHECK(hipMemsetAsync(c2, 0, size_t(ncol2) * sizeof(double), s));
-    comm->allreduce(c2, size_t(ncol2), false, s);
-  }
 }
 
 size_t cgs2_granules(long n) {
-  return 2 * size_t(kGmMaxDim) * size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)) + 2;
+  return 2 * size_t(kGmMaxDim) *
+             std::max<size_t>(1, size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems))) +
+         2;
 }
 
 void cgs2_gmres_step(Seg g, double* w, const ChainVecs& V, int d, double* gran, unsigned* cnt,
@@ -1248,7 +1256,7 @@ __device__ void dcgs_bookkeeping(GmresDev* st, const double* r, int k, bool tail
       const double rho = fabs(gk1);
       st->rho = rho;
       const int status = rho <= st->tol ? 1 : ((acc >= st->max_steps || isnan(rho)) ? 2 : 0);
-      st->status = status;
+      atomicMax(&st->status, status);
       stop = status;
     }
     __syncthreads();
@@ -1359,7 +1367,7 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
   // reducer: workgroup b sums slot b over the nb workgroups
   DCGS_TS(2);
   if (b < K && dcgs_used<KP>(b, k, tail) && threadIdx.x < 64) {
-    const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag + b, err);
+    const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag + b, err, &st->status, g_spin_limit);
     if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + K + b);
   }
   DCGS_TS(3);
@@ -1367,8 +1375,8 @@ __global__ __launch_bounds__(kChainThreads) void k_dcgs2_step(Seg g, const doubl
     const double* p = res + 2 * j;
     mgs_u4 q = granule_load(p);
     for (long spins = 0; !tag_is(q, tag + K + j); ++spins) {
-      if (spins >= kMgsMaxSpins) {
-        *err = 1.0;
+      if (spins >= g_spin_limit) {
+        handoff_timeout(err, &st->status);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -1522,7 +1530,7 @@ extern "C" int dcp_probe_dcgs_timestamps(unsigned long long* out) {
 #endif
 
 size_t dcgs2_granules(long n) {
-  const size_t nbp = size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  const size_t nbp = std::max<size_t>(1, size_t((n + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)));
   return std::max<size_t>(kDcgsRes + 2 * 64 + 64, 2 * 64 * nbp + 64);
 }
 
@@ -1554,9 +1562,10 @@ void dcgs2_step(Seg g, const double* w, const ChainVecs& V, int k, double* tnext
 #undef DCP_DCGS_CASE
     throw std::runtime_error("dcgs2_step: basis of " + std::to_string(k) + " vectors");
   }
-  const int nbp = int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems));
+  // at least one (empty) block on a rank without owned rows: it joins the
+  // all-reduce and does the bookkeeping like the others
+  const int nbp = std::max(1, int((long(g.n) + kBlock * kCgsElems - 1) / (kBlock * kCgsElems)));
   const int nbu = int(std::min<long>((long(g.n) + kBlock - 1) / kBlock, 2048));
-  if (nbp <= 0) return;
   ++seq;
 #define DCP_DCGS_CASE2(KL)                                                                       \
   if (k <= KL) {                                                                                 \

@@ -10,7 +10,8 @@
 // --dof-order: the 3D shell's dofs in deal.II's distribute_dofs order
 // (default; dcp_host_mesh_renumber_dealii) or the mesh's own tree order.
 // --output: output_results (boussinesq_model.tpp:1566-1680) before the loop
-// and after every step, DIR/NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu (classic).
+// and after every step, DIR/NAME-XXXXX.0000.vtu + NAME-XXXXX.pvtu (classic;
+// FEEC: boussineq_model_FEEC.tpp:1917-2030, vorticity / velocity / p / T).
 // Single GPU; the multi-GPU path is driven through the same ABI by one process
 // per GPU (bench.py).
 #include <cstdio>
@@ -31,6 +32,7 @@ int fail(const char* what, dcp_ctx* ctx) {
 struct Output {
   dcp_ctx* ctx = nullptr;
   const dcp_host_mesh_view* view = nullptr;
+  const dcp_feec_mesh* feec = nullptr;  // FEEC model: its own output_results
   std::string dir, stem;
   int index = 0;
   size_t n_nse = 0;
@@ -44,10 +46,14 @@ int write_output(Output& o) {
   char idx[16];
   std::snprintf(idx, sizeof(idx), "%05d", o.index++);
   const std::string piece = o.stem + "-" + idx + ".0000.vtu";
-  if (rc == DCP_OK) rc = dcp_write_vtu(o.view, u.data(), T.data(), 0, (o.dir + "/" + piece).c_str());
+  const std::string vtu = o.dir + "/" + piece, pvtu = o.dir + "/" + o.stem + "-" + idx + ".pvtu";
+  if (rc == DCP_OK)
+    rc = o.feec ? dcp_write_feec_vtu(o.feec, u.data(), T.data(), 0, vtu.c_str())
+                : dcp_write_vtu(o.view, u.data(), T.data(), 0, vtu.c_str());
   const char* pieces[1] = {piece.c_str()};
   if (rc == DCP_OK)
-    rc = dcp_write_pvtu_record((o.dir + "/" + o.stem + "-" + idx + ".pvtu").c_str(), 1, pieces);
+    rc = o.feec ? dcp_write_feec_pvtu_record(pvtu.c_str(), 1, pieces)
+                : dcp_write_pvtu_record(pvtu.c_str(), 1, pieces);
   if (rc != DCP_OK) std::fprintf(stderr, "Error: writing %s/%s\n", o.dir.c_str(), piece.c_str());
   return rc;
 }
@@ -210,12 +216,13 @@ int main(int argc, char** argv) {
   Output out;
   Output* outp = nullptr;
   if (!out_dir.empty()) {
-    if (feec || two_d) {
-      std::fprintf(stderr, "Error: --output writes the classic 3D model's fields only\n");
+    if (two_d) {
+      std::fprintf(stderr, "Error: --output writes the 3D models' fields only\n");
       return 1;
     }
     out.ctx = ctx;
     out.view = &v;
+    out.feec = feec ? &fm : nullptr;
     out.dir = out_dir;
     out.stem = out_stem;
     out.n_nse = n_nse;

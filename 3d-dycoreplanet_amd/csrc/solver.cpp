@@ -18,6 +18,7 @@
 // scalars. Every operator refreshes the ghost entries of its input first.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -175,10 +176,17 @@ bool fused_chain_ok(const Ctx& c, Seg g, int nb, int dim) {
   return !c.comm && c.fused_chain && c.hmapped && mgs_chain_fits(g.n, nb, dim, c.n_cus);
 }
 double* chain_err(Ctx& c) { return c.hmapped + kChainErr; }
+// A one-launch kernel's workgroups hand partial sums to each other, which
+// needs the whole grid resident at once; a hand-off that never completes
+// (another queue holding CUs, fewer CUs than reported) times out and raises
+// this. The inner Schur solve then reruns on the multi-launch kernels.
+struct HandoffTimeout : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 void check_chain_err(Ctx& c) {
   if (c.hmapped[kChainErr] != 0.0) {
     c.hmapped[kChainErr] = 0.0;
-    throw std::runtime_error("Gram-Schmidt chain: a workgroup timed out waiting for a hand-off");
+    throw HandoffTimeout("Gram-Schmidt chain: a workgroup timed out waiting for a hand-off");
   }
 }
 ChainVecs chain_vecs(const std::vector<double*>& V, int dim) {
@@ -625,7 +633,7 @@ State gmres_schur_cgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl,
     // one cycle ahead: queue cycle cyc + 1, then wait for cycle cyc's report
     enqueue_cycle(cyc + 1);
     DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
-    if (c.gm_report[cyc & 1].status != 0) break;
+    if (c.gm_report[cyc & 1].status != 0 || (!comm && c.hmapped[kChainErr] != 0.0)) break;
     ++cyc;
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -709,7 +717,7 @@ State gmres_schur_dcgs2_ordered(Ctx& c, double* x, const double* b, Control& ctl
   for (;;) {
     enqueue_cycle(cyc + 1);
     DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
-    if (c.gm_report[cyc & 1].status != 0) break;
+    if (c.gm_report[cyc & 1].status != 0 || (!comm && c.hmapped[kChainErr] != 0.0)) break;
     ++cyc;
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -801,7 +809,7 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   Comm* comm = c.comm.get();
   const bool fused = sstep_fits(c, g.n, nb1);
   if (!fused) {
-    const size_t pn = 2 * size_t(128) * size_t((g.n + 511) / 512) + 2;
+    const size_t pn = 2 * size_t(128) * std::max<size_t>(1, size_t((g.n + 511) / 512)) + 2;
     if (c.gm_part.n < pn) {
       c.gm_part.alloc(pn);
       c.gm_part.zero(c.stream);  // tag 0: never waited for
@@ -864,7 +872,7 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   for (;;) {
     enqueue_cycle(cyc + 1);
     DCP_HIP_CHECK(hipEventSynchronize(c.gm_ev[cyc & 1]));
-    if (c.gm_report[cyc & 1].status != 0) break;
+    if (c.gm_report[cyc & 1].status != 0 || (!comm && c.hmapped[kChainErr] != 0.0)) break;
     ++cyc;
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -997,27 +1005,52 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
   // inner GMRES on S = B D_A^-1 B^T, tol 1e-6 |src_p|, max 5000, identity
   {
     const double nrm = std::sqrt(dot_host(c, c.seg_p(), src + nu, src + nu, kSlotB));
-    Control ctl{unsigned(c.inner_max_steps), 1e-6 * nrm};
+    // parity hook (DCP_OPT_BLOCK_FIXED_INNER = k): exactly k steps, no
+    // tolerance decision for rounding to flip, the k-step iterate used as is
+    const bool fixed = c.block_fixed_inner > 0;
+    const unsigned cap = fixed ? unsigned(c.block_fixed_inner) : unsigned(c.inner_max_steps);
+    const double tol = fixed ? 0.0 : 1e-6 * nrm;
+    Control ctl{cap, tol};
     ensure_pool(c.sg_v, 32, size_t(np));
     State st;
     if (c.dim2) {
       // 2D: S = B D_A^-1 B^T as three products (schur_vmult), deal.II GMRES
       Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
       st = gmres(c, np, c.seg_p(), S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
-    } else if (c.schur_explicit && c.gram_schmidt == 1) {
-      st = gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
-    } else if (c.schur_explicit && c.gram_schmidt == 3) {
-      st = gmres_schur_sstep(c, dst + nu, src + nu, ctl, c.sg_v, 30);
-    } else if (c.schur_explicit && c.gram_schmidt == 2) {
-      st = gmres_schur_dcgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
     } else if (c.schur_explicit) {
-      st = gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+      auto inner_solve = [&] {
+        if (c.gram_schmidt == 1) return gmres_schur_cgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+        if (c.gram_schmidt == 3) return gmres_schur_sstep(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+        if (c.gram_schmidt == 2) return gmres_schur_dcgs2(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+        return gmres_schur(c, dst + nu, src + nu, ctl, c.sg_v, 30);
+      };
+      if (c.comm || !c.fused_chain) {
+        st = inner_solve();
+      } else {
+        // one GPU: the one-launch kernels need their grid resident; if a
+        // hand-off times out, rerun from the same initial guess on the
+        // multi-launch kernels (same arithmetic) and keep them for the context
+        if (c.inner_x0.n < size_t(np)) c.inner_x0.alloc(size_t(np));
+        copy(np, dst + nu, c.inner_x0.p, c.stream);
+        try {
+          st = inner_solve();
+        } catch (const HandoffTimeout& e) {
+          std::fprintf(stderr, "dcp: %s; the inner Schur solves run on the multi-launch kernels\n",
+                       e.what());
+          c.fused_chain = false;
+          ++c.handoff_timeouts;
+          DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+          copy(np, c.inner_x0.p, dst + nu, c.stream);
+          ctl = Control{cap, tol};
+          st = inner_solve();
+        }
+      }
     } else {
       Op S = [&](const double* x, double* y) { schur_vmult(c, x, y); };
       st = gmres(c, np, c.seg_p(), S, nullptr, dst + nu, src + nu, ctl, c.sg_v, 30);
     }
     inner += int(ctl.last_step);
-    if (st != kSuccess) throw NoConvergence();
+    if (st != kSuccess && !fixed) throw NoConvergence();
     scale(np, DScal{nullptr, -1.0}, dst + nu, c.stream);
   }
   // utmp = src_u - B^T dst_p

@@ -37,7 +37,9 @@ OPT_FEEC_FIXED_INNER = 8
 OPT_LOG_HISTORY = 10
 OPT_INNER_MAX_STEPS = 11
 OPT_SCHUR_FIXED_INNER = 12
-ABI_VERSION = 4            # include/dcp.h DCP_ABI_VERSION
+OPT_HANDOFF_SPIN_LIMIT = 13
+OPT_BLOCK_FIXED_INNER = 14
+ABI_VERSION = 5            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
 # Every symbol include/dcp.h declares (checked by tests/test_abi.py).
@@ -62,7 +64,8 @@ EXPORTED = [
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
     "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_state_set_owned",
-    "dcp_state_get_owned",
+    "dcp_state_get_owned", "dcp_scatter_info", "dcp_nse_coupling_export",
+    "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
 
 
@@ -104,7 +107,7 @@ class Timings(C.Structure):
         ("schur_apply_ms_avg", C.c_double), ("schur_applies", C.c_long),
         ("stokes_apply_ms_avg", C.c_double), ("velocity_apply_ms_avg", C.c_double),
         ("stokes_applies", C.c_long), ("velocity_applies", C.c_long),
-        ("a_solve_iterations", C.c_long),
+        ("a_solve_iterations", C.c_long), ("handoff_timeouts", C.c_long),
     ]
 
 
@@ -181,7 +184,7 @@ class RunParams(C.Structure):
         ("adapt_time_step", C.c_int), ("final_time", C.c_double), ("R0", C.c_double),
         ("R1", C.c_double), ("length", C.c_double),
         ("use_block_preconditioner_feec", C.c_int), ("correct_pressure_to_zero_mean", C.c_int),
-        ("solver_diagnostics_level", C.c_int),
+        ("solver_diagnostics_level", C.c_int), ("use_direct_solver", C.c_int),
     ]
 
 
@@ -249,6 +252,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 5
     lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int)]
+    lib.dcp_scatter_info.argtypes = [P, P, P, P]
+    lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
+    lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I, I]
     lib.dcp_host_mesh_create.restype = P
@@ -275,6 +281,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.POINTER(Constraints), I, I, P, P, P, P, P, P]
     lib.dcp_write_vtu.argtypes = [C.POINTER(MeshView), P, P, I, C.c_char_p]
     lib.dcp_write_pvtu_record.argtypes = [C.c_char_p, I, C.POINTER(C.c_char_p)]
+    lib.dcp_write_feec_vtu.argtypes = [C.POINTER(FeecMeshView), P, P, I, C.c_char_p]
+    lib.dcp_write_feec_pvtu_record.argtypes = [C.c_char_p, I, C.POINTER(C.c_char_p)]
     lib.dcp_solver_history.argtypes = [P, I, P, P, I, C.POINTER(I), C.POINTER(I)]
     lib.dcp_timer_summary.argtypes = [P, C.c_char_p, I]
     lib.dcp_timer_section.argtypes = [P, C.c_char_p, C.POINTER(C.c_long), C.POINTER(C.c_double)]
@@ -532,6 +540,20 @@ class FeecTopology:
              (self.n_w + self.n_u + np.arange(nc, dtype=np.int32))[:, None]], axis=1)
         self.signs = np.concatenate([self.sign_w, self.sign_u, np.ones((nc, 1), np.int8)], axis=1)
         self.fixed = np.concatenate([self.w_fixed, self.u_fixed, np.zeros(self.n_p, np.uint8)])
+
+    def write_vtu(self, path, nse_solution, T_solution, partition=0):
+        """The FEEC model's output_results (dcp_write_feec_vtu; host-only):
+        one hexahedron per cell, vorticity / velocity / p / T / partition at
+        its vertices."""
+        x = np.ascontiguousarray(nse_solution, dtype=np.float64)
+        T = np.ascontiguousarray(T_solution, dtype=np.float64)
+        if x.size != self.n or T.size != self.n_T:
+            raise ValueError("solution sizes do not match the FEEC mesh")
+        v = self.as_struct()
+        rc = lib().dcp_write_feec_vtu(C.byref(v), _ptr(x), _ptr(T), int(partition),
+                                      str(path).encode())
+        if rc != DCP_OK:
+            raise DcpError(rc, "dcp_write_feec_vtu failed for " + str(path))
 
     def as_struct(self):
         v = FeecMeshView()
@@ -999,6 +1021,17 @@ class Context:
         one per step; bitwise the same results."""
         self._check(lib().dcp_set_option(self._h, OPT_FUSED_CHAIN, int(bool(on))))
 
+    def set_block_fixed_inner(self, k: int):
+        """DCP_OPT_BLOCK_FIXED_INNER (parity hook): the block preconditioner's
+        inner Schur GMRES runs exactly k steps, no tolerance test (0 = the
+        reference's rule)."""
+        self._check(lib().dcp_set_option(self._h, OPT_BLOCK_FIXED_INNER, int(k)))
+
+    def set_handoff_spin_limit(self, spins: int):
+        """DCP_OPT_HANDOFF_SPIN_LIMIT (test hook, process-wide): polls before a
+        one-launch Gram-Schmidt hand-off counts as timed out (<= 0: default)."""
+        self._check(lib().dcp_set_option(self._h, OPT_HANDOFF_SPIN_LIMIT, int(spins)))
+
     def set_feec_zero_mean(self, on: bool):
         self._check(lib().dcp_set_option(self._h, OPT_FEEC_ZERO_MEAN, int(bool(on))))
 
@@ -1138,6 +1171,40 @@ class Context:
         v = [C.c_int64() for _ in range(5)]
         self._check(lib().dcp_pattern_info(self._h, *[C.byref(x) for x in v]))
         return dict(zip(("nnzb_A", "nnzb_Bt", "nnzb_B", "nnz_T", "nnz_S"), (x.value for x in v)))
+
+    def halo_selftest(self, vec, send_pos, recv_pos, n_peers: int):
+        """The forward halo with self-peers: returns vec with
+        vec[recv_pos] = vec[send_pos], moved through the communicator."""
+        v = np.ascontiguousarray(vec, dtype=np.float64).copy()
+        sp_ = np.ascontiguousarray(send_pos, dtype=np.int32)
+        rp_ = np.ascontiguousarray(recv_pos, dtype=np.int32)
+        self._check(lib().dcp_halo_selftest(self._h, v.size, _ptr(v), sp_.size, _ptr(sp_),
+                                            _ptr(rp_), int(n_peers)))
+        return v
+
+    def scatter_info(self) -> dict:
+        """Per block pattern (A, B^T, B): blocks reached by some cell's scatter
+        position, the pattern size, and whether the assembly stores at first
+        touch (else it zero-fills and adds)."""
+        t = np.zeros(3, np.int64)
+        n = np.zeros(3, np.int64)
+        f = np.zeros(3, np.int32)
+        self._check(lib().dcp_scatter_info(self._h, _ptr(t), _ptr(n), _ptr(f)))
+        return {k: (int(t[i]), int(n[i]), bool(f[i])) for i, k in enumerate(("A", "Bt", "B"))}
+
+    def coupling_csr(self, which: str):
+        """The operator form's B^T ("Bt", 3 n_vnodes x n_p) or B ("B", n_p x n_u)
+        as scalar CSR, without materialising the velocity block."""
+        w = {"Bt": 0, "B": 1}[which]
+        nnz = C.c_int64()
+        self._check(lib().dcp_nse_coupling_export(self._h, w, C.byref(nnz), None, None, None))
+        rows = self.mesh.n_u if w == 0 else self.mesh.n_p
+        rp = np.zeros(rows + 1, np.int32)
+        cols = np.zeros(nnz.value, np.int32)
+        vals = np.zeros(nnz.value)
+        self._check(lib().dcp_nse_coupling_export(self._h, w, C.byref(nnz), _ptr(rp), _ptr(cols),
+                                                  _ptr(vals)))
+        return rp, cols, vals
 
     def schur_layout(self) -> dict:
         cb, st, pm = C.c_int(), C.c_int64(), C.c_int()

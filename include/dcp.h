@@ -51,7 +51,7 @@ enum {
  * [n][27][3] to [n][64][3] and added a dcp_host_mesh_create parameter without
  * one). A caller compiled against another header must refuse to run:
  * dcp_abi_version() != DCP_ABI_VERSION. */
-#define DCP_ABI_VERSION 4
+#define DCP_ABI_VERSION 5
 int dcp_abi_version(void);
 /* Support points per cell in cell_geometry (MappingQ(3): 4^3). */
 #define DCP_CELL_SUPPORT_POINTS 64
@@ -268,6 +268,17 @@ enum { DCP_OPT_ELEMENT_MFMA = 9 };
  *   log_result = true) logs them to deallog (boussinesq_model.tpp:1166-1169,
  *   1215-1218); read back with dcp_solver_history. Default 0. */
 enum { DCP_OPT_LOG_HISTORY = 10 };
+/* DCP_OPT_HANDOFF_SPIN_LIMIT (test hook, process-wide, <= 0 = the default
+ * 2^19): polls before a one-launch kernel's hand-off counts as timed out; a
+ * tiny value makes the timeout path (rerun on the multi-launch kernels) run. */
+enum { DCP_OPT_HANDOFF_SPIN_LIMIT = 13 };
+/* DCP_OPT_BLOCK_FIXED_INNER (parity hook, default 0 = the reference's rule):
+ * k > 0 runs the inner Schur GMRES of BlockSchurPreconditioner::vmult
+ * (block_schur_preconditioner.hpp:47-51) for exactly k steps with no
+ * tolerance test and uses the k-step iterate (no NoConvergence), so runs whose
+ * dot products are summed in different orders (1 vs P GPUs) take the same
+ * control decisions. */
+enum { DCP_OPT_BLOCK_FIXED_INNER = 14 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* The SolverControl log of the last dcp_solve_nse (DCP_OPT_LOG_HISTORY):
@@ -392,6 +403,26 @@ int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* n
  * padding, whether rows/columns are in reverse Cuthill-McKee order. */
 int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted);
 
+/* Communicator self-test (no mesh needed): the solver's forward halo (gather
+ * of vec[send_pos], grouped send/recv, scatter into vec[recv_pos]) with every
+ * peer this rank itself, the n_list entries split over n_peers self-peers. On
+ * a one-rank RCCL communicator this runs ncclSend/ncclRecv to its own rank. */
+int dcp_halo_selftest(dcp_ctx* ctx, int n, double* vec, int n_list, const int32_t* send_pos,
+                      const int32_t* recv_pos, int n_peers);
+
+/* Scatter bookkeeping of the assembly (copy_local_to_global_nse_system,
+ * boussinesq_model.tpp:677-687): per block pattern A, B^T, B ([3] each) the
+ * blocks some cell's scatter position reaches, the pattern size, and whether
+ * the assembly stores at first touch (1) or zero-fills and adds (0). */
+int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_touch);
+
+/* The operator form's coupling blocks of nse_matrix as scalar CSR, without
+ * materialising the velocity block: which = 0 -> B^T (3 n_vnodes rows, pressure
+ * columns), 1 -> B (n_p rows, velocity columns 3 n + c), the B the Schur
+ * complement reads. nnz first (rowptr NULL), then the arrays. */
+int dcp_nse_coupling_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,
+                            double* vals);
+
 /* Timing of the last hot-path calls (device time, milliseconds). */
 typedef struct {
   double assemble_nse_ms, build_precond_ms, assemble_T_matrix_ms, assemble_T_rhs_ms;
@@ -405,6 +436,10 @@ typedef struct {
   /* AztecOO A-GMRES iterations of the do_solve_A fallback (not reported by
    * the reference; block_schur_preconditioner.hpp:59-67) */
   long a_solve_iterations;
+  /* one-launch Gram-Schmidt hand-offs that timed out since the context was
+   * created (each reran its inner solve on the multi-launch kernels and turned
+   * DCP_OPT_FUSED_CHAIN off; 0 on a healthy GPU) */
+  long handoff_timeouts;
 } dcp_timings;
 int dcp_get_timings(dcp_ctx* ctx, dcp_timings* out);
 
@@ -554,6 +589,15 @@ int dcp_write_vtu(const dcp_host_mesh_view* mesh, const double* nse, const doubl
                   int partition, const char* vtu_path);
 /* write_pvtu_record: the .pvtu naming the n_pieces per-rank .vtu files. */
 int dcp_write_pvtu_record(const char* pvtu_path, int n_pieces, const char* const* piece_files);
+/* FEEC output_results (boussineq_model_FEEC.tpp:1917-2030): DataOut::
+ * build_patches(min(nse_velocity_degree, temperature_degree) = 1) of the joint
+ * [w u p T] solution -- one hexahedron per cell on its 8 vertices -- with the
+ * Postprocessor's point data "vorticity" (Nedelec(0), covariant Piola),
+ * "velocity" (RT(0), contravariant Piola), "p" (DGQ0), "T", "partition"
+ * (:1808-1912). nse: n_w + n_u + n_p global values [w | u | p], T: n_T. */
+int dcp_write_feec_vtu(const dcp_feec_mesh* mesh, const double* nse, const double* T,
+                       int partition, const char* vtu_path);
+int dcp_write_feec_pvtu_record(const char* pvtu_path, int n_pieces, const char* const* piece_files);
 
 /* .prm -> dcp_physics (+ refinement etc.), CoreModelData::Parameters(file). */
 typedef struct {
@@ -563,6 +607,7 @@ typedef struct {
   double final_time, R0, R1, length;
   int use_block_preconditioner_feec, correct_pressure_to_zero_mean;
   int solver_diagnostics_level;     /* deallog.depth_console level (main.cxx:89) */
+  int use_direct_solver;            /* MUMPS branch: the reference throws (:1886-1893) */
 } dcp_run_params;
 int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
 
@@ -576,7 +621,15 @@ int dcp_prm_load(const char* path, dcp_run_params* out, char* err, int err_len);
  * non-zero return stops), time_index += dt / interval, old_* = *; until
  * time_index > final_time or max_steps (> 0) steps. Returns DCP_NOT_CONVERGED
  * where the reference's solve throws. use_schur_complement_solver selects
- * dcp_solve_nse_schur (one GPU). */
+ * dcp_solve_nse_schur (one GPU); with use_FEEC_solver it selects the FEEC
+ * model's solve_NSE_Schur_complement, whose body is commented out
+ * (boussineq_model_FEEC.tpp:1480-1500): no preconditioner build and no NSE
+ * solve, nse_solution keeps its value (FEEC.tpp:2264-2298). Returns
+ * DCP_ERR_UNSUPPORTED where the reference throws (use_direct_solver,
+ * :1886-1893, FEEC.tpp:2282-2290) and for what the device path does not
+ * implement: nse_velocity_degree other than 2 (classic) / 1 (FEEC), FEEC
+ * without its block preconditioner (the identity-preconditioned GMRES branch,
+ * FEEC.tpp:1420-1431), FEEC on the periodic cuboid. */
 typedef struct {
   int timestep_number, steps;       /* current step; steps completed */
   double time_index, time_step;     /* t at the step's start; dt */

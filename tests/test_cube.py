@@ -121,3 +121,42 @@ def test_cube_matrix_free_operator(cube):
     # and the oracle's product with its own matrix
     orc.assemble_nse_system(u, T)
     assert rel_max(ctx.nse_vmult(x), orc.nse_vmult(x)) < 1e-12
+
+
+def test_cube_repeated_operator_form_assembly(cube):
+    """On the periodic cube the velocity pattern holds the periodic images'
+    diagonal-only rows, which no cell's scatter position reaches (A is
+    zero-filled and added, not stored at first touch). Three operator-form
+    assemblies with different states on the module's context, each against the
+    oracle: B^T / B as the solve reads them, the rhs and S = B D_A^-1 B^T at
+    1e-12; then the full export (velocity block materialised) at 1e-12."""
+    m, ph, ctx, orc, u0, T0 = cube
+    info = ctx.scatter_info()
+    print("scatter info (touched, nnzb, first touch):", info)
+    assert info["A"][0] < info["A"][1] and not info["A"][2]
+    assert info["Bt"][0] == info["Bt"][1]
+    rng = np.random.default_rng(SEED + 9)
+    n = m.n_u + m.n_p
+    for i in range(3):
+        u = rng.uniform(-1, 1, n)
+        T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+        ctx.set_state(dcp.OLD_T_SOLUTION, T)
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        orc.assemble_nse_system(u, T)
+        orc.build_nse_preconditioner()
+        Ao = csr(*orc.nse_matrix_csr(), n)
+        Bt_g = sp.csr_matrix(ctx.coupling_csr("Bt"), shape=(m.n_u, m.n_p))
+        B_g = sp.csr_matrix(ctx.coupling_csr("B"), shape=(m.n_p, m.n_u))
+        Bt_o, B_o = Ao[:m.n_u, m.n_u:], Ao[m.n_u:, :m.n_u]
+        assert abs(Bt_g - Bt_o).max() / abs(Bt_o).max() < 1e-12, i
+        assert abs(B_g - B_o).max() / abs(B_o).max() < 1e-12, i
+        assert rel_max(ctx.get_state(dcp.NSE_RHS), orc.nse_rhs()) < 1e-12, i
+        p = rng.uniform(-1, 1, m.n_p)
+        assert rel_max(ctx.schur_vmult(p), orc.schur_vmult(p)) < 1e-12, i
+    Ag = csr(*ctx.nse_matrix_csr(), n)
+    assert abs(Ag - Ao).max() / abs(Ao).max() < 1e-12
+    # leave the module state as the fixture made it
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, u0)
+    ctx.set_state(dcp.OLD_T_SOLUTION, T0)

@@ -149,3 +149,81 @@ def test_solver_history_and_timer_sections():
     with pytest.raises(dcp.DcpError):
         ctx.timer_section("no such section")
     ctx.close()
+
+
+FEEC_PRM = os.path.join(ROOT, "configs", "aqua_planet_shell_test_3d-feec.prm")
+
+
+def fresh_feec(rp, m):
+    ctx = dcp.Context()
+    ctx.set_physics(dcp.physics_from_params(rp))
+    ctx.upload_feec_mesh(m)
+    x0 = np.zeros(m.feec.n)
+    for f, v in ((dcp.NSE_SOLUTION, x0), (dcp.OLD_NSE_SOLUTION, x0), (dcp.T_SOLUTION, m.T0),
+                 (dcp.OLD_T_SOLUTION, m.T0)):
+        ctx.set_state(f, v)
+    return ctx
+
+
+@pytest.mark.gpu
+def test_run_feec_with_schur_complement_solver_is_the_reference_no_op():
+    """FEEC with use_schur_complement_solver (FEEC.tpp:2264-2298): run() skips
+    build_nse_preconditioner and calls solve_NSE_Schur_complement, whose body is
+    commented out (:1480-1500): nse_solution keeps its value, no FGMRES
+    iterations, no preconditioner section, the temperature still solves. The
+    same run with the block preconditioner builds it and solves."""
+    rp = dcp.load_prm(FEEC_PRM)
+    rp.initial_global_refinement = 1
+    m = dcp.HostMesh(refine=1, feec=True, R0=rp.R0, R1=rp.R1, length=rp.length)
+    rng = np.random.default_rng(2)
+    out = {}
+    for schur in (1, 0):
+        rp.use_schur_complement_solver = schur
+        ctx = fresh_feec(rp, m)
+        x0 = np.zeros(m.feec.n)
+        x0[:m.feec.n_w + m.feec.n_u] = 0.01 * rng.uniform(-1, 1, m.feec.n_w + m.feec.n_u)
+        x0[m.feec.fixed.astype(bool)] = 0
+        ctx.set_state(dcp.NSE_SOLUTION, x0)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, x0)
+        rc, rep, steps = ctx.run(rp, max_steps=1)
+        out[schur] = (rc, rep, ctx.get_state(dcp.NSE_SOLUTION), x0,
+                      ctx.timer_section("   Build NSE FEEC preconditioner")[0],
+                      ctx.timer_section("   Solve NSE system")[0])
+        ctx.close()
+    rc, rep, x, x0, n_prec, n_solve = out[1]
+    assert rc == dcp.DCP_OK and rep.steps == 1 and rep.fgmres_outer == 0
+    assert np.array_equal(x, x0) and n_prec == 0 and n_solve == 0 and rep.T_cg > 0
+    rc, rep, x, x0, n_prec, n_solve = out[0]
+    assert rc == dcp.DCP_OK and rep.fgmres_outer > 0 and n_prec == 1 and n_solve == 1
+    assert not np.array_equal(x, x0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["feec-degree-2", "classic-degree-1", "direct-solver",
+                                  "feec-identity-preconditioner"])
+def test_run_rejects_what_the_device_path_does_not_implement(case):
+    """dcp_run refuses up front (DCP_ERR_UNSUPPORTED, nothing stepped) instead
+    of silently running another discretisation: FEEC with nse velocity degree
+    != 1 (FE_Nedelec/RT/DGQ(degree - 1), FEEC.tpp:21-30), the classic model
+    with degree != 2, the MUMPS branch the reference itself throws on
+    (:1886-1893), and FEEC without its block preconditioner (the identity-
+    preconditioned GMRES branch, FEEC.tpp:1420-1431)."""
+    feec = case.startswith("feec")
+    rp = dcp.load_prm(FEEC_PRM if feec else PRM)
+    rp.initial_global_refinement = 1
+    if case == "feec-degree-2":
+        rp.nse_velocity_degree = 2
+    elif case == "classic-degree-1":
+        rp.nse_velocity_degree = 1
+    elif case == "direct-solver":
+        rp.use_direct_solver = 1
+    else:
+        rp.use_block_preconditioner_feec = 0
+        rp.use_schur_complement_solver = 0
+    m = dcp.HostMesh(refine=1, feec=feec, R0=rp.R0, R1=rp.R1, length=rp.length)
+    ctx = fresh_feec(rp, m) if feec else fresh(rp, m)
+    with pytest.raises(dcp.DcpError) as e:
+        ctx.run(rp, max_steps=1)
+    assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
+    assert ctx.timer_section("   Assemble NSE system")[0] == 0
+    ctx.close()

@@ -151,7 +151,7 @@ GOLD4 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shel
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2"])
+@pytest.mark.parametrize("gs", ["modified", "classical2", "dcgs2", "sstep"])
 def test_gpu_config3_r4_matches_oracle_fixture(gs):
     """BASELINE config 3 (classic prm at refine 4: 24,576 cells, 634,600 NSE
     dofs) from the physical state against the oracle's full time step

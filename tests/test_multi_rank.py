@@ -143,11 +143,11 @@ def _time_step(ctx, m, u, T):
                                              (3, 2, "classical2"), (2, 2, "dcgs2"),
                                              (3, 2, "dcgs2"), (2, 2, "sstep"), (3, 2, "sstep"),
                                              (8, 2, "classical2"), (8, 2, "sstep")])
-def test_group_time_step_matches_single_gpu(world, refine, gs):
+def test_group_time_step_matches_single_gpu(world, refine, gs, fixed_inner=0):
     """(At r = 3 this random state drives the reference's inner Schur GMRES
     into its 5000-iteration cap on one GPU and on every partition alike.)
     gs: DCP_OPT_GRAM_SCHMIDT of the inner Schur GMRES on every rank and on the
-    single-GPU reference run."""
+    single-GPU reference run; fixed_inner: DCP_OPT_BLOCK_FIXED_INNER."""
     m = dcp.HostMesh(refine=refine)
     ph = dcp.classic_physics()
     rng = np.random.default_rng(7)
@@ -158,6 +158,7 @@ def test_group_time_step_matches_single_gpu(world, refine, gs):
     ref_ctx.set_physics(ph)
     ref_ctx.upload_mesh(m)
     ref_ctx.set_gram_schmidt(gs)
+    ref_ctx.set_block_fixed_inner(fixed_inner)
     ref = _time_step(ref_ctx, m, u, T)
     ref_ctx.close()
 
@@ -170,6 +171,7 @@ def test_group_time_step_matches_single_gpu(world, refine, gs):
             ctx.set_physics(ph)
             ctx.upload_mesh(m)
             ctx.set_gram_schmidt(gs)
+            ctx.set_block_fixed_inner(fixed_inner)
             results[rank] = _time_step(ctx, m, u, T)
             ctx.close()
         except Exception as e:  # noqa: BLE001
@@ -200,6 +202,9 @@ def test_group_time_step_matches_single_gpu(world, refine, gs):
         assert r["nse"][1] == ref["nse"][1]                      # FGMRES iterations
         # the inner Schur GMRES stagnates near its 1e-6 target, so its count
         # follows the summation order of the (partitioned) dot products
+        # (with fixed_inner every inner solve runs exactly k steps)
+        if fixed_inner:
+            assert r["nse"][2] == ref["nse"][2]
         assert abs(r["nse"][2] - ref["nse"][2]) <= 0.15 * ref["nse"][2]
         # CG to 1e-12: partitioned dot products may shift the stop by one step
         assert abs(r["T"][1] - ref["T"][1]) <= 1
@@ -514,3 +519,70 @@ def test_group_second_step_reads_current_ghosts(world, via):
             nz = r[key] != 0
             v[nz] = r[key][nz]
         assert rel(v, ref[key]) < 1e-9, key
+
+
+def test_partition_with_a_rank_without_pressure_rows():
+    """The refine-1 shell (48 cells) on 13 ranks: rank 9 owns 3 cells and 15
+    velocity nodes but no pressure dof (each vertex belongs to the rank of its
+    lowest-index cell). The GPU test below runs that partition."""
+    m = dcp.HostMesh(refine=1)
+    infos = [dcp.partition_info(m, r, 13) for r in range(13)]
+    empty = [r for r, i in enumerate(infos) if i["npo"] == 0]
+    assert empty and all(infos[r]["n_owned_cells"] > 0 for r in empty)
+    assert sum(i["npo"] for i in infos) == m.n_p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", ["classical2", "sstep", "dcgs2", "modified"])
+def test_group_rank_without_pressure_rows(gs):
+    """A rank with no owned pressure rows (the partition above) must still
+    join every all-reduce of the inner Schur GMRES and advance its device
+    GMRES state like the others (the multi-launch CGS2 / s-step / DCGS2 steps
+    run one empty block there); otherwise its cycle loop never stops and the
+    collectives mismatch. One time step on 13 in-process ranks against one
+    GPU."""
+    test_group_time_step_matches_single_gpu(13, 1, gs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "group"])
+@pytest.mark.parametrize("n_peers", [1, 3])
+def test_halo_exchange_round_trip_self_peer(transport, n_peers):
+    """RcclComm::exchange (csrc/comm.cpp) with real traffic on one GPU: a
+    one-rank RCCL communicator whose halo plan lists the rank itself as its
+    peer(s), so the grouped ncclSend/ncclRecv move data to their own rank
+    through the solver's gather -> exchange -> scatter (the forward ghost import
+    of boussinesq_model.tpp:1145-1146). Every received entry must equal the
+    sent one bitwise, everything else untouched; the in-process transport
+    (LocalComm) the same."""
+    rng = np.random.default_rng(5)
+    n = 50_000
+    vec = rng.standard_normal(n)
+    vec[::7] = np.nan_to_num(np.array([np.inf]))  # extreme values travel unchanged
+    send = rng.choice(n // 2, 4_000, replace=False).astype(np.int32)
+    recv = (n // 2 + rng.choice(n // 2, 4_000, replace=False)).astype(np.int32)
+    if transport == "rccl":
+        ctx = dcp.Context(nccl_id=dcp.nccl_unique_id())
+        g = None
+    else:
+        g = dcp.Group(1)
+        ctx = dcp.Context(rank=0, world_size=1, group=g)
+    out = ctx.halo_selftest(vec, send, recv, n_peers)
+    ctx.close()
+    if g is not None:
+        g.close()
+    want = vec.copy()
+    want[recv] = vec[send]
+    assert np.array_equal(out.view(np.int64), want.view(np.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", ["sstep", "classical2"])
+def test_group_8_ranks_refine4_fixed_inner(gs):
+    """BASELINE config 3's mesh (refine 4, 634,600 NSE dofs) on 8 in-process
+    ranks against one GPU. At refine 4 the reference's inner Schur GMRES
+    stagnates at its 5,000-step cap (the config-3 fixture, tests/test_golden.py),
+    so the comparison runs the parity hook DCP_OPT_BLOCK_FIXED_INNER = 28: every inner
+    solve takes exactly 28 steps and the outer FGMRES converges on every
+    partition alike. rhs 1e-12, equal outer and inner counts, iterates 1e-10."""
+    test_group_time_step_matches_single_gpu(8, 4, gs, fixed_inner=28)

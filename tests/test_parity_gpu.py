@@ -531,3 +531,105 @@ def test_sstep_three_launch_block_matches_fused():
     assert abs(itf - itm) <= max(2, 0.05 * itf)
     assert np.linalg.norm(ym[m.n_u:] - yf[m.n_u:]) <= 1e-4 * np.linalg.norm(yf[m.n_u:])
     ctx.close()
+
+
+def _coupling(ctx, m):
+    Bt = sp.csr_matrix(ctx.coupling_csr("Bt"), shape=(m.n_u, m.n_p))
+    B = sp.csr_matrix(ctx.coupling_csr("B"), shape=(m.n_p, m.n_u))
+    return Bt, B
+
+
+@pytest.mark.parametrize("gs", ["sstep", "classical2"])
+def test_repeated_operator_form_assembly_matches_oracle(gs):
+    """Three operator-form assemblies on ONE context with three different old
+    states (copy_local_to_global_nse_system, boussinesq_model.tpp:677-687, and
+    the zeroing of assemble_nse_system, :700-706): after each, B^T and B as the
+    solve reads them, the rhs, the explicit Schur complement S = B D_A^-1 B^T
+    and the matrix-free nse_matrix apply against the oracle at 1e-12; after the
+    third, the time step's solve at 1e-10. Any block a scatter store overwrites
+    instead of adding to, or a block that keeps an earlier assembly's value,
+    shows at O(1) in the second or third round."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh(m)
+    ctx.set_gram_schmidt(gs)
+    orc = oracle_py.Model(ph, m)
+    info = ctx.scatter_info()
+    print("scatter info (touched, nnzb, first touch):", info)
+    # every block of the (union) B^T / B patterns is reached by some cell, so
+    # the assembly stores at first touch on every shell: the path under test
+    for k in ("A", "Bt", "B"):
+        touched, nnzb, first = info[k]
+        assert touched == nnzb and first, (k, info[k])
+    rng = np.random.default_rng(SEED + 40)
+    n = m.n_u + m.n_p
+    u2 = np.zeros(n)
+    u2[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    states = [(np.zeros(n), m.T0.copy()), random_state(m, rng), (u2, m.T0.copy())]
+    for i, (u, T) in enumerate(states):
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+        ctx.set_state(dcp.OLD_T_SOLUTION, T)
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        orc.assemble_nse_system(u, T)
+        orc.build_nse_preconditioner()
+        Ao = csr(*orc.nse_matrix_csr(), n)
+        Bt_o, B_o = Ao[:m.n_u, m.n_u:], Ao[m.n_u:, :m.n_u]
+        Bt_g, B_g = _coupling(ctx, m)
+        assert abs(Bt_g - Bt_o).max() / abs(Bt_o).max() < 1e-12, i
+        assert abs(B_g - B_o).max() / abs(B_o).max() < 1e-12, i
+        assert abs(B_g - Bt_g.T).max() == 0.0, i
+        assert rel_max(ctx.get_state(dcp.NSE_RHS), orc.nse_rhs()) < 1e-12, i
+        p = rng.uniform(-1, 1, m.n_p)
+        assert rel_max(ctx.schur_vmult(p), orc.schur_vmult(p)) < 1e-12, i
+        x = rng.uniform(-1, 1, n)
+        assert rel_max(ctx.nse_vmult(x), orc.nse_vmult(x)) < 1e-12, i
+    u, T = states[-1]
+    ctx.set_state(dcp.NSE_SOLUTION, u)
+    rc, outer, inner = ctx.solve_nse()
+    rco, x_o, outer_o, inner_o = orc.solve_nse(u)
+    assert rc == rco == 0
+    assert outer == outer_o
+    assert abs(inner - inner_o) <= 0.10 * inner_o
+    assert rel2(ctx.get_state(dcp.NSE_SOLUTION), x_o) < 1e-10
+    ctx.close()
+
+
+@pytest.mark.parametrize("gs", ["sstep", "classical2", "dcgs2"])
+def test_handoff_timeout_reruns_on_multi_launch_kernels(gs):
+    """The one-launch Gram-Schmidt kernels hand partial sums between their
+    resident workgroups. A hand-off that never completes must neither hang nor
+    return a wrong solve: the test hook shrinks the poll bound to one poll, so
+    hand-offs time out; the kernels abort the device GMRES state (status 3, every
+    queued launch returns at entry), the inner solve reruns from its initial
+    guess on the multi-launch kernels and the context keeps them. The time step
+    must still match the oracle (same bar as test_full_solve_and_temperature)."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_mesh(m)
+    ctx.set_gram_schmidt(gs)
+    orc = oracle_py.Model(ph, m)
+    u, T = np.zeros(m.n_u + m.n_p), m.T0.copy()
+    for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                 (dcp.T_SOLUTION, T)):
+        ctx.set_state(f, v)
+    ctx.assemble_nse_system()
+    ctx.build_nse_preconditioner()
+    ctx.set_handoff_spin_limit(1)
+    try:
+        rc, outer, inner = ctx.solve_nse()
+    finally:
+        ctx.set_handoff_spin_limit(0)
+    timeouts = ctx.timings()["handoff_timeouts"]
+    orc.assemble_nse_system(u, T)
+    orc.build_nse_preconditioner()
+    rco, x_o, outer_o, inner_o = orc.solve_nse(u)
+    assert timeouts == 1
+    assert rc == rco == 0 and outer == outer_o
+    assert abs(inner - inner_o) <= 0.10 * inner_o
+    assert rel2(ctx.get_state(dcp.NSE_SOLUTION), x_o) < 1e-10
+    ctx.close()
