@@ -127,9 +127,11 @@ void set_physics_dev(Ctx& c) {
   c.ph.cuboid = p.cuboid;
 }
 
-double* field_ptr(Ctx& c, int field, size_t& n) {
-  if (field == DCP_OLD_NSE_SOLUTION) c.old_nse_ghosted = false;
-  if (field == DCP_OLD_T_SOLUTION) c.old_T_ghosted = false;
+// write = true: the caller changes the field, so an old field's ghost entries
+// are no longer known to be current (reads leave the flags alone)
+double* field_ptr(Ctx& c, int field, size_t& n, bool write) {
+  if (write && field == DCP_OLD_NSE_SOLUTION) c.old_nse_ghosted = false;
+  if (write && field == DCP_OLD_T_SOLUTION) c.old_T_ghosted = false;
   switch (field) {
     case DCP_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.nse_sol.p;
     case DCP_OLD_NSE_SOLUTION: n = size_t(c.n_u + c.n_p); return c.old_nse.p;
@@ -1133,13 +1135,13 @@ void materialize_velocity_block(Ctx& c) {
   c.B_current = true;
 }
 
-// nse_matrix.block(1,0) of the last operator-form assembly: the transpose of
-// B^T, block by block (bitwise the B the full scatter produces)
 void set_ctx_error(dcp_ctx* ctx, const char* msg) {
   if (ctx) ctx->err = msg;
   g_last_error = msg;
 }
 
+// nse_matrix.block(1,0) of the last operator-form assembly: the transpose of
+// B^T, block by block (bitwise the B the full scatter produces)
 void materialize_B(Ctx& c) {
   if (c.B_current) return;
   transpose_blocks3(long(c.B_tperm.n), c.B_tperm.p, c.Bt_val.p, c.B_val.p, c.stream);
@@ -1867,6 +1869,84 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           c.mf_geo_tree.alloc(size_t(n_cells) * 270);
           mf_geometry(c.cd(), nullptr, c.mf_geo_tree.p, c.stream);
         }
+        // B^T by tasks of rows (k_bt_tasks) on the separable shell: per velocity
+        // node row its cells in colour order (cell << 5 | lexicographic position)
+        c.bt_rows = false;
+        const char* env = std::getenv("DCP_BT_ROWS");
+        if (c.mf_separable && !c.periodic && !(env && *env == '0') && n_cells < (1 << 26)) {
+          const int nrows = int(Btp.size()) - 1;
+          std::vector<int32_t> rp(size_t(nrows) + 1, 0);
+          for (const int cell : ccells)
+            for (int t = 0; t < 27; ++t) {
+              const int n = q2[27 * size_t(cell) + t];
+              if (n < nrows) rp[n + 1]++;
+            }
+          int most = 0;
+          for (int n = 0; n < nrows; ++n) {
+            most = std::max(most, rp[n + 1]);
+            rp[n + 1] += rp[n];
+          }
+          // B rows (several GPUs): per owned pressure row its cells, colour order
+          const int prows = int(Bp.size()) - 1;
+          std::vector<int32_t> pp(size_t(prows) + 1, 0);
+          for (const int cell : ccells)
+            for (int v = 0; v < 8; ++v) {
+              const int q = pd[8 * size_t(cell) + v];
+              if (q < prows) pp[q + 1]++;
+            }
+          for (int q = 0; q < prows; ++q) {
+            most = std::max(most, pp[q + 1]);
+            pp[q + 1] += pp[q];
+          }
+          if (most <= 8 && *std::max_element(layer.begin(), layer.end()) < 65536) {
+            // one wave: 8 cells x 8 vertices (27 nodes)
+            std::vector<int32_t> inc(static_cast<size_t>(rp[nrows]));
+            std::vector<int32_t> f(rp.begin(), rp.end() - 1);
+            for (const int cell : ccells)
+              for (int t = 0; t < 27; ++t) {
+                const int n = q2[27 * size_t(cell) + t];
+                if (n < nrows) inc[size_t(f[n]++)] = int32_t(cell) << 5 | t;
+              }
+            // tasks: runs of consecutive rows with <= 8 slots and <= 64 entries
+            std::vector<int32_t> hdr, rec;
+            int first = 0, ns = 0, ne = 0, rec0 = 0;
+            auto flush = [&](int next_row) {
+              if (next_row > first)
+                hdr.insert(hdr.end(), {Btp[first], first, ns | ne << 8, rec0});
+              first = next_row;
+              ns = ne = 0;
+              rec0 = int32_t(rec.size() / 4);
+            };
+            for (int n = 0; n < nrows; ++n) {
+              const int cnt = rp[n + 1] - rp[n], len = Btp[n + 1] - Btp[n];
+              require(cnt <= 8 && len <= 64, DCP_ERR_INVALID, "B^T task sizes");
+              if (ns + cnt > 8 || ne + len > 64) flush(n);
+              for (int k = rp[n]; k < rp[n + 1]; ++k) {
+                const int cell = inc[size_t(k)] >> 5, lex = inc[size_t(k)] & 31;
+                uint64_t dm = 0;
+                for (int v = 0; v < 8; ++v) {
+                  const int q = pd[8 * size_t(cell) + v];
+                  const int32_t* b = Btc.data() + Btp[n];
+                  const int32_t* e = Btc.data() + Btp[n + 1];
+                  const int32_t* it = std::lower_bound(b, e, q);
+                  require(it != e && *it == q, DCP_ERR_INVALID, "B^T pattern lacks a cell's entry");
+                  dm |= uint64_t(ne + (it - b)) << (6 * v);
+                }
+                rec.insert(rec.end(), {col[size_t(cell)], layer[size_t(cell)] << 16 | lex << 8 | (n - first),
+                                       int32_t(uint32_t(dm)), int32_t(uint32_t(dm >> 32))});
+                ++ns;
+              }
+              ne += len;
+            }
+            flush(nrows);
+            c.bt_task_hdr.upload(hdr);
+            c.bt_slot_rec.upload(rec);
+            c.bt_ntasks = int(hdr.size() / 4);
+            c.bt_ncols = int(c.mf_colgeo.n / 90);
+            c.bt_P.alloc(size_t(216) * c.bt_ncols);
+            c.bt_rows = true;
+          }
+        }
       }
     }
     const size_t nn = size_t(n_u + n_p);
@@ -1993,7 +2073,7 @@ int dcp_state_set_owned(dcp_ctx* ctx, int field, const double* host, size_t n) {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     Ctx& c = *ctx;
     size_t want = 0;
-    double* p = field_ptr(c, field, want);
+    double* p = field_ptr(c, field, want, true);
     const auto segs = owned_segments(c, field);
     size_t total = 0;
     for (auto& sgm : segs) total += sgm.second;
@@ -2019,7 +2099,7 @@ int dcp_state_get_owned(dcp_ctx* ctx, int field, double* host, size_t n) {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     Ctx& c = *ctx;
     size_t want = 0;
-    double* p = field_ptr(c, field, want);
+    double* p = field_ptr(c, field, want, false);
     const auto segs = owned_segments(c, field);
     size_t total = 0;
     for (auto& sgm : segs) total += sgm.second;
@@ -2040,7 +2120,7 @@ int dcp_state_set(dcp_ctx* ctx, int field, const double* host, size_t n) {
   return guarded(ctx, [&] {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     size_t want = 0;
-    double* p = field_ptr(*ctx, field, want);
+    double* p = field_ptr(*ctx, field, want, true);
     if (ctx->comm) {
       // global vector in, local (owned + ghost) entries uploaded
       const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
@@ -2064,7 +2144,7 @@ int dcp_state_get(dcp_ctx* ctx, int field, double* host, size_t n) {
   return guarded(ctx, [&] {
     require(ctx && host && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     size_t want = 0;
-    double* p = field_ptr(*ctx, field, want);
+    double* p = field_ptr(*ctx, field, want, false);
     if (ctx->comm) {
       // owned entries written into the global vector, the rest untouched
       const bool T = field == DCP_T_SOLUTION || field == DCP_OLD_T_SOLUTION || field == DCP_T_RHS;
@@ -2089,8 +2169,8 @@ int dcp_state_copy(dcp_ctx* ctx, int dst_field, int src_field) {
   return guarded(ctx, [&] {
     require(ctx && ctx->have_mesh, DCP_ERR_STATE, "mesh not uploaded");
     size_t nd = 0, ns = 0;
-    double* d = field_ptr(*ctx, dst_field, nd);
-    double* s = field_ptr(*ctx, src_field, ns);
+    double* d = field_ptr(*ctx, dst_field, nd, true);
+    double* s = field_ptr(*ctx, src_field, ns, false);
     require(nd == ns, DCP_ERR_INVALID, "state size mismatch");
     copy(int(nd), s, d, ctx->stream);
     if (dst_field == DCP_OLD_NSE_SOLUTION || dst_field == DCP_OLD_T_SOLUTION) {
@@ -2109,7 +2189,7 @@ double* dcp_state_device_ptr(dcp_ctx* ctx, int field) {
   if (field == DCP_OLD_NSE_SOLUTION || field == DCP_OLD_T_SOLUTION) ctx->old_external = true;
   size_t n = 0;
   try {
-    return field_ptr(*ctx, field, n);
+    return field_ptr(*ctx, field, n, true);
   } catch (...) {
     return nullptr;
   }
@@ -2131,18 +2211,22 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     // the velocity block is materialised only when something reads it
     const bool full = matrix && (c.assemble_A || c.matrix_free == 0);
     NseOut out{};
+    bool bt_rows = false;
     if (matrix) {
       // first-touch scatter positions store instead of adding: no zero fill
       if (full) ensure_A_val(c);
       if (full && !c.first_touch_A) c.A_val.zero(c.stream);
       // operator form: B copied from B^T after the cell loop (c.B_transpose)
       const bool scatter_B = full || !c.B_transpose;
-      if (!c.first_touch_Bt) c.Bt_val.zero(c.stream);
-      if (scatter_B && !c.first_touch_B) c.B_val.zero(c.stream);
+      // operator form on the separable shell: B^T by rows (k_bt_rows), the
+      // cell kernel only the rhs and the constrained diagonals
+      bt_rows = c.bt_rows && !full;
+      if (!bt_rows && !c.first_touch_Bt) c.Bt_val.zero(c.stream);
+      if (!bt_rows && scatter_B && !c.first_touch_B) c.B_val.zero(c.stream);
       c.con_diag.zero(c.stream);
       out.A = full ? c.A_val.p : nullptr;
-      out.Bt = c.Bt_val.p;
-      out.B = scatter_B ? c.B_val.p : nullptr;
+      out.Bt = bt_rows ? nullptr : c.Bt_val.p;
+      out.B = scatter_B && !bt_rows ? c.B_val.p : nullptr;
       out.cdiag = c.con_diag.p;
       out.cidx = c.mf_cidx.p;
       out.pcdiag = c.con_diag.p + 3 * size_t(c.n_con);
@@ -2165,12 +2249,17 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
         launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                             c.old_T.p, c.ph, out, c.stream);
     }
+    if (bt_rows)
+      launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, c.bt_ntasks, c.bt_task_hdr.p, c.bt_slot_rec.p,
+                     c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p, c.bt_p_inc.p, c.B_ptr.p,
+                     c.B_col.p, c.B_transpose ? nullptr : c.B_val.p, c.stream);
     if (full)
       image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
                             c.A_val.p, c.stream);
     t.stop();
     if (matrix) {
-      c.B_current = out.B != nullptr;  // else B = (B^T)^T, materialised when read
+      // else B = (B^T)^T, materialised when read
+      c.B_current = out.B != nullptr || (bt_rows && !c.B_transpose);
       c.nse_assembled = true;
       c.A_current = full;
       c.nse_ph = c.ph;

@@ -128,6 +128,14 @@ struct Ctx {
   DBuf<int32_t> posA, posBt, posB, posT;
   // scatter positions carry first-touch marks (no zero fill before assembly)
   bool first_touch_A = false, first_touch_Bt = false, first_touch_B = false;
+  // B^T by tasks of rows on the separable shell (assembly.hip k_bt_tasks):
+  // task headers and (row, cell) slot records [4 int32 each], built at upload
+  bool bt_rows = false;
+  DBuf<int32_t> bt_task_hdr, bt_slot_rec;
+  int bt_ntasks = 0;
+  DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
+  DBuf<double> bt_P;  // [n_cols][216] column factors, formed every assembly
+  int bt_ncols = 0;
   // blocks some cell's scatter position reaches (first-touch marking at upload)
   unsigned long long touched_A = 0, touched_Bt = 0, touched_B = 0;
   // nse_matrix in operator form: B^T, B and the diagonal of the constrained

@@ -198,21 +198,61 @@ LocalMesh localize_distributed(const dcp_dist_mesh& m, const dcp_host_comm& hc) 
   if (!hc.allgather || !hc.alltoallv) throw std::runtime_error("distributed upload: NULL communicator");
   const int W = hc.world, R = hc.rank;
   if (W < 1 || R < 0 || R >= W) throw std::runtime_error("distributed upload: bad rank/world");
-  if (!m.cell_id || !m.cell_owner || !m.cell_nse_dofs || !m.cell_T_dofs || !m.cell_geometry ||
-      !m.cell_diameter)
-    throw std::runtime_error("distributed upload: NULL array");
-  if (m.n_cells < 1 || m.n_owned_cells < 1 || m.n_owned_cells > m.n_cells)
-    throw std::runtime_error("distributed upload: bad cell counts");
-  if (m.n_u <= 0 || m.n_u % 3 || m.n_p <= 0 || m.n_T <= 0 || m.n_u + m.n_p >= (int64_t(1) << 31) ||
-      m.n_T >= (int64_t(1) << 31))
-    throw std::runtime_error("distributed upload: bad global sizes (32-bit global ids)");
-  if (m.u_begin % 3 || m.u_end % 3 || m.u_begin < 0 || m.u_end > m.n_u || m.p_begin < m.n_u ||
-      m.p_end > m.n_u + m.n_p || m.T_begin < 0 || m.T_end > m.n_T)
-    throw std::runtime_error("distributed upload: owned ranges outside the blocks "
-                             "(velocity range aligned to support points)");
   const HostComm comm{hc};
+  // ---- the caller's input, checked locally first; the verdict is all-gathered
+  // before any other exchange, so a bad input on one rank fails every rank
+  // instead of leaving the others blocked in a collective
+  std::string bad;
+  auto check = [&](bool ok, const char* msg) {
+    if (!ok && bad.empty()) bad = std::string("distributed upload: ") + msg;
+    return ok;
+  };
+  check(m.cell_id && m.cell_owner && m.cell_nse_dofs && m.cell_T_dofs && m.cell_geometry &&
+            m.cell_diameter,
+        "NULL array");
+  check(m.n_cells >= 1 && m.n_owned_cells >= 1 && m.n_owned_cells <= m.n_cells, "bad cell counts");
+  check(m.n_u > 0 && m.n_u % 3 == 0 && m.n_p > 0 && m.n_T > 0 &&
+            m.n_u + m.n_p < (int64_t(1) << 31) && m.n_T < (int64_t(1) << 31),
+        "bad global sizes (32-bit global ids)");
+  check(m.u_begin % 3 == 0 && m.u_end % 3 == 0 && m.u_begin >= 0 && m.u_end <= m.n_u &&
+            m.p_begin >= m.n_u && m.p_end <= m.n_u + m.n_p && m.T_begin >= 0 && m.T_end <= m.n_T,
+        "owned ranges outside the blocks (velocity range aligned to support points)");
   const int64_t n_u = m.n_u, n_p = m.n_p, n_T = m.n_T, nvg = n_u / 3;
   const int tdpc = (n_T == nvg && n_T != n_p) ? 27 : 8;
+  std::vector<CellRec> cells;
+  std::unordered_map<int64_t, int> by_id;
+  if (bad.empty()) {
+    cells.resize(m.n_cells);
+    for (int c = 0; c < m.n_cells && bad.empty(); ++c) {
+      CellRec& r = cells[c];
+      r.id = m.cell_id[c];
+      r.owner = m.cell_owner[c];
+      if (!check((c < m.n_owned_cells) == (r.owner == R),
+                 "the first n_owned_cells cells must be the owned ones") ||
+          !check(r.owner >= 0 && r.owner < W, "bad cell owner"))
+        break;
+      r.nse.assign(m.cell_nse_dofs + size_t(c) * kNseDofs, m.cell_nse_dofs + size_t(c + 1) * kNseDofs);
+      r.T.assign(m.cell_T_dofs + size_t(c) * tdpc, m.cell_T_dofs + size_t(c + 1) * tdpc);
+      r.geo.assign(m.cell_geometry + size_t(c) * 3 * kMapPts,
+                   m.cell_geometry + size_t(c + 1) * 3 * kMapPts);
+      r.diam = m.cell_diameter[c];
+      for (int64_t d : r.nse) check(d >= 0 && d < n_u + n_p, "NSE dof out of range");
+      for (int64_t d : r.T) check(d >= 0 && d < n_T, "T dof out of range");
+      check(by_id.emplace(r.id, c).second, "duplicate cell id");
+    }
+  }
+  LineMap nlines, tlines;
+  if (bad.empty()) {
+    try {
+      read_lines(m.nse, nlines);
+      read_lines(m.T, tlines);
+    } catch (const std::exception& e) {
+      bad = e.what();
+    }
+  }
+  for (int64_t f : comm.allgather({bad.empty() ? 0 : 1}))
+    if (f) throw std::runtime_error(bad.empty() ? "distributed upload: another rank's input is invalid"
+                                                : bad);
   // ---- ownership ranges of every rank: velocity nodes, pressure, temperature
   const std::vector<int64_t> all =
       comm.allgather({m.u_begin / 3, m.u_end / 3, m.p_begin - n_u, m.p_end - n_u, m.T_begin, m.T_end});
@@ -220,29 +260,6 @@ LocalMesh localize_distributed(const dcp_dist_mesh& m, const dcp_host_comm& hc) 
   rv.build(all, W, 0);
   rp.build(all, W, 1);
   rt.build(all, W, 2);
-  // ---- the caller's cells
-  LineMap nlines, tlines;
-  read_lines(m.nse, nlines);
-  read_lines(m.T, tlines);
-  std::vector<CellRec> cells(m.n_cells);
-  std::unordered_map<int64_t, int> by_id;
-  for (int c = 0; c < m.n_cells; ++c) {
-    CellRec& r = cells[c];
-    r.id = m.cell_id[c];
-    r.owner = m.cell_owner[c];
-    if ((c < m.n_owned_cells) != (r.owner == R))
-      throw std::runtime_error("distributed upload: the first n_owned_cells cells must be the owned ones");
-    if (r.owner < 0 || r.owner >= W) throw std::runtime_error("distributed upload: bad cell owner");
-    r.nse.assign(m.cell_nse_dofs + size_t(c) * kNseDofs, m.cell_nse_dofs + size_t(c + 1) * kNseDofs);
-    r.T.assign(m.cell_T_dofs + size_t(c) * tdpc, m.cell_T_dofs + size_t(c + 1) * tdpc);
-    r.geo.assign(m.cell_geometry + size_t(c) * 3 * kMapPts, m.cell_geometry + size_t(c + 1) * 3 * kMapPts);
-    r.diam = m.cell_diameter[c];
-    for (int64_t d : r.nse)
-      if (d < 0 || d >= n_u + n_p) throw std::runtime_error("distributed upload: NSE dof out of range");
-    for (int64_t d : r.T)
-      if (d < 0 || d >= n_T) throw std::runtime_error("distributed upload: T dof out of range");
-    if (!by_id.emplace(r.id, c).second) throw std::runtime_error("distributed upload: duplicate cell id");
-  }
   // ---- second ghost layer: ask the owner of each ghost cell for its neighbours
   std::vector<std::vector<int64_t>> req(W);
   for (int c = m.n_owned_cells; c < m.n_cells; ++c) req[cells[c].owner].push_back(cells[c].id);

@@ -1531,7 +1531,11 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
   double bt[4][3];
   double kii[3] = {0, 0, 0};
   double fa[3] = {0, 0, 0};
-  const bool do_diag = want_cdiag && h == 0;
+  // the constrained-row diagonal (|K_ii| or the cell average) only matters on
+  // cells with a constrained node (boundary layers): skip the sums elsewhere
+  const bool cell_con =
+      want_cdiag && __any(lane < 27 && out.cidx[sh.node[lane < 27 ? lane : 0]] >= 0);
+  const bool do_diag = cell_con && h == 0;
   if (row_lane) {
 #pragma unroll
     for (int vv = 0; vv < 4; ++vv) bt[vv][0] = bt[vv][1] = bt[vv][2] = 0;
@@ -1679,6 +1683,167 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
   }
 }
 
+// ---------------------------------------------------------------------------
+// B^T by rows on the radially separable shell (copy_local_to_global_nse_system
+// of the B^T block, boussinesq_model.tpp:626-637 / 677-687, restated as a
+// gather). The entry of velocity node n = (a, b, c) of cell K and vertex
+// p = (i, j, k) of K is -sum_q JxW psi_p d_d phi_n, and with the separable map
+// (J^-1 rows m0 / R, m1 / R, m2 / R', JxW = R^2 R' D2 w; sep_geometry) the
+// 27-point sum factors into a 9-point column sum and a 3-point layer sum:
+//   B^T = -(P01[a b i j][d] Q01[c][k] + P2[a b i j][d] Q2[c][k])
+//   P01 = sum_xy w w psi_i psi_j D2 (m0[d] l'_a l_b + m1[d] l_a l'_b)
+//   P2  = sum_xy w w psi_i psi_j D2 m2[d] l_a l_b
+//   Q01 = sum_z w R^2 R' / R l_c psi_k,   Q2 = sum_z w R^2 R' / R' l'_c psi_k.
+// k_bt_coltab forms P per column (216 values) from the column table every
+// assembly. k_bt_tasks then writes B^T by tasks: a task is a run of consecutive
+// velocity node rows with at most 8 (row, cell) slots and 64 row entries in
+// all, so the task's entries are one contiguous piece of the B^T values. Lane
+// (slot k, vertex v) evaluates that cell's contribution and knows (from the
+// slot record built at upload) which task entry it belongs to; lane j sums
+// entry j over its contributions in slot order (the row's cells in colour
+// order), condenses it with its row's constraint (C_a^T b: linear, so the same
+// as condensing each cell's part) and stores it -- every entry written once,
+// the task's piece coalesced, no read-modify-write, no zero fill, no colouring.
+constexpr int kBtRowWaves = 4;
+constexpr int kBtColEntries = 216;  // [P01 | P2][a][b][i][j][d]
+
+__global__ __launch_bounds__(kBtColEntries) void k_bt_coltab(const double* __restrict__ colgeo,
+                                                             double* __restrict__ P) {
+  const int col = blockIdx.x, t = threadIdx.x;
+  const int which = t / 108, r = t % 108;
+  const int a = r / 36, b = (r / 12) % 3, i = (r / 6) % 2, j = (r / 3) % 2, d = r % 3;
+  double s = 0.0;
+#pragma unroll
+  for (int q1 = 0; q1 < 3; ++q1)
+#pragma unroll
+    for (int q0 = 0; q0 < 3; ++q0) {
+      const double* m = colgeo + 90 * size_t(col) + 10 * (q0 + 3 * q1);
+      const double w = cW[q0] * cW[q1] * m[9] * cL1[i][q0] * cL1[j][q1];
+      if (which == 0)
+        s += w * (m[d] * cdL2[a][q0] * cL2[b][q1] + m[3 + d] * cL2[a][q0] * cdL2[b][q1]);
+      else
+        s += w * (m[6 + d] * cL2[a][q0] * cL2[b][q1]);
+    }
+  P[kBtColEntries * size_t(col) + t] = s;
+}
+
+// the (node lex, vertex v) contribution of a cell in column-table entry col
+// and layer lay, components d = 0..2
+__device__ inline void bt_entry(const CellData& cd, const double* __restrict__ P, int col, int lay,
+                                int lex, int v, double out[3]) {
+  const int a = lex % 3, b = (lex / 3) % 3, c = lex / 9;
+  const int i = v & 1, j = (v >> 1) & 1, k = v >> 2;
+  const double* lg = cd.sep_laygeo + 9 * size_t(lay);
+  double q01 = 0.0, q2 = 0.0;
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+    const double wz = cW[z] * lg[3 * z + 2] * cL1[k][z];
+    q01 += wz * lg[3 * z] * cL2[c][z];
+    q2 += wz * lg[3 * z + 1] * cdL2[c][z];
+  }
+  const double* pp = P + kBtColEntries * size_t(col) + 6 * (2 * (3 * a + b) + i) + 3 * j;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) out[d] = -(pp[d] * q01 + pp[108 + d] * q2);
+}
+__device__ inline void bt_cell_entry(const CellData& cd, const double* __restrict__ P, int cell,
+                                     int lex, int v, double out[3]) {
+  bt_entry(cd, P, cd.sep_col[cell], cd.sep_layer[cell], lex, v, out);
+}
+
+// task header: {first B^T entry, first row, slots | entries << 8, first slot
+// record}; slot record: {column-table entry, layer << 16 | lex << 8 | row in
+// task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
+__global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
+    CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
+    const double* __restrict__ P, double* __restrict__ Bt) {
+  __shared__ double vals[kBtRowWaves][64 * 3];
+  __shared__ int dst_e[kBtRowWaves][64];
+  __shared__ int rowl[kBtRowWaves][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int task = int(blockIdx.x) * kBtRowWaves + wave;
+  if (task >= n_tasks) return;
+  const int4 h = hdr[task];
+  const int ns = h.z & 255, ne = h.z >> 8;
+  const int k = lane >> 3, v = lane & 7;
+  int de = -1;
+  if (k < ns) {
+    const int4 r = rec[h.w + k];
+    const unsigned long long dm = (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
+    de = int((dm >> (6 * v)) & 63);
+    double e[3];
+    bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
+    vals[wave][3 * lane] = e[0];
+    vals[wave][3 * lane + 1] = e[1];
+    vals[wave][3 * lane + 2] = e[2];
+    rowl[wave][lane] = r.y & 255;
+  }
+  dst_e[wave][lane] = de;
+  wsync();
+  if (lane >= ne) return;
+  double acc[3] = {0.0, 0.0, 0.0};
+  int rl = 0;
+  for (int e = 0; e < 8 * ns; ++e)
+    if (dst_e[wave][e] == lane) {
+      acc[0] += vals[wave][3 * e];
+      acc[1] += vals[wave][3 * e + 1];
+      acc[2] += vals[wave][3 * e + 2];
+      rl = rowl[wave][e];
+    }
+  double Ca[3][3];
+  condensation(cd.vcon[h.y + rl], Ca);
+  double* dst = Bt + 3 * size_t(h.x + lane);
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+}
+
+// B by pressure rows (several GPUs, where B is not the transpose of the owned
+// B^T rows): one wave per owned pressure row p; pair e = (cell slot s, node
+// position t) of p's cells (colour order) evaluates bt_cell_entry for p's
+// vertex in that cell, then lane j sums entry j (node n) over the pairs with
+// node n in slot order -- the cells common to n and p in the same colour order
+// k_bt_tasks sums them, so B is bitwise the transpose of B^T -- and condenses
+// it with node n's constraint (the B^T row's C_n^T b).
+__global__ __launch_bounds__(64 * kBtRowWaves) void k_b_rows(
+    CellData cd, int n_rows, const int32_t* __restrict__ p_ptr, const int32_t* __restrict__ p_inc,
+    const int32_t* __restrict__ B_ptr, const int32_t* __restrict__ B_col,
+    const double* __restrict__ P, double* __restrict__ B) {
+  __shared__ double vals[kBtRowWaves][216 * 3];
+  __shared__ int node[kBtRowWaves][216];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = int(blockIdx.x) * kBtRowWaves + wave;
+  if (row >= n_rows) return;
+  const int b0 = p_ptr[row], nc = p_ptr[row + 1] - b0;  // <= 8 cells
+  for (int e = lane; e < 27 * nc; e += 64) {
+    const int s = e / 27, t = e - 27 * s;
+    const int inc = p_inc[b0 + s];
+    const int cell = inc >> 3, v = inc & 7;
+    double val[3];
+    bt_cell_entry(cd, P, cell, t, v, val);
+    vals[wave][3 * e] = val[0];
+    vals[wave][3 * e + 1] = val[1];
+    vals[wave][3 * e + 2] = val[2];
+    node[wave][e] = cd.cell_q2[27 * size_t(cell) + t];
+  }
+  wsync();
+  const int r0 = B_ptr[row], len = B_ptr[row + 1] - r0;
+  for (int j = lane; j < len; j += 64) {
+    const int n = B_col[r0 + j];
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int e = 0; e < 27 * nc; ++e)
+      if (node[wave][e] == n) {
+        acc[0] += vals[wave][3 * e];
+        acc[1] += vals[wave][3 * e + 1];
+        acc[2] += vals[wave][3 * e + 2];
+      }
+    double Ca[3][3];
+    condensation(cd.vcon[n], Ca);
+    double* dst = B + 3 * size_t(r0 + j);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj)
+      dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+  }
+}
+
 }  // namespace
 
 void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
@@ -1815,6 +1980,29 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
   hipLaunchKernelGGL(k_clear_first_touch, dim3(1024), dim3(256), 0, s, size_t(per_cell) * n_cells, pos);
   DCP_HIP_CHECK(hipGetLastError());
   return false;
+}
+
+void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, const int32_t* task_hdr,
+                    const int32_t* slot_rec, double* Bt, int n_prows, const int32_t* p_ptr,
+                    const int32_t* p_inc, const int32_t* B_ptr, const int32_t* B_col, double* B,
+                    hipStream_t s) {
+  if (n_cols > 0) {
+    hipLaunchKernelGGL(k_bt_coltab, dim3(n_cols), dim3(kBtColEntries), 0, s, cd.sep_colgeo, P);
+    DCP_HIP_CHECK(hipGetLastError());
+  }
+  if (n_tasks > 0) {
+    hipLaunchKernelGGL(k_bt_tasks, dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves),
+                       dim3(64 * kBtRowWaves), 0, s, cd, n_tasks,
+                       reinterpret_cast<const int4*>(task_hdr),
+                       reinterpret_cast<const int4*>(slot_rec), P, Bt);
+    DCP_HIP_CHECK(hipGetLastError());
+  }
+  if (B && n_prows > 0) {
+    hipLaunchKernelGGL(k_b_rows, dim3((n_prows + kBtRowWaves - 1) / kBtRowWaves),
+                       dim3(64 * kBtRowWaves), 0, s, cd, n_prows, p_ptr, p_inc, B_ptr, B_col, P,
+                       B);
+    DCP_HIP_CHECK(hipGetLastError());
+  }
 }
 
 }  // namespace dcp

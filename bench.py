@@ -642,7 +642,7 @@ def main():
         "NoConvergence: the reference's inner Schur GMRES (5000 iterations, tol 1e-6, "
         "identity preconditioner) stagnates on the near-null constant pressure mode at the "
         "first preconditioner application of both FGMRES attempts; the reference throws "
-        "here (DESIGN.md section 5b)",
+        "here (DESIGN.md section 5, the config-3 fixture)",
         "patterns": pinfo,
         "schur_mode": args.schur,
         "gram_schmidt": args.gram_schmidt,

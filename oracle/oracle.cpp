@@ -603,6 +603,7 @@ struct orc_model {
   long a_solve_iterations = 0;  // AztecOO A-GMRES iterations of the last solve (do_solve_A)
   int inner_max_steps = 5000;   // SolverControl(5000) of the inner Schur GMRES (timing hook)
   int schur_fixed_inner = 0;    // parity hook: the Schur solver's inner CGs run exactly k steps
+  int block_fixed_inner = 0;    // parity hook: the block preconditioner's inner GMRES runs exactly k steps
 };
 
 extern "C" orc_model* orc_create(const orc_physics* ph, int n_cells, const int* cell_nse_dofs,
@@ -697,6 +698,7 @@ extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_
 
 extern "C" void orc_set_inner_max_steps(orc_model* m, int n) { m->inner_max_steps = n; }
 extern "C" void orc_set_schur_fixed_inner(orc_model* m, int k) { m->schur_fixed_inner = k; }
+extern "C" void orc_set_block_fixed_inner(orc_model* m, int k) { m->block_fixed_inner = k; }
 
 extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   // assemble_nse_preconditioner (:479-514) + build_nse_preconditioner (:518-542).
@@ -1128,8 +1130,12 @@ void block_prec_vmult(orc_model* m, const double* src, double* dst, bool do_solv
   const int nu = m->n_u, np = m->n_p;
   std::vector<double> utmp(src, src + nu);
   {
-    Control ctl{unsigned(m->inner_max_steps),
-                1e-6 * norm2(std::vector<double>(src + nu, src + nu + np), 0, np)};
+    // parity hook (block_fixed_inner = k, the device's DCP_OPT_BLOCK_FIXED_INNER):
+    // exactly k steps, no tolerance test, the k-step iterate used as is
+    const int fk = m->block_fixed_inner;
+    Control ctl = fk > 0 ? Control{unsigned(fk), 0.0}
+                         : Control{unsigned(m->inner_max_steps),
+                                   1e-6 * norm2(std::vector<double>(src + nu, src + nu + np), 0, np)};
     int it = 0;
     try {
       gmres(
@@ -1138,7 +1144,8 @@ void block_prec_vmult(orc_model* m, const double* src, double* dst, bool do_solv
           it);
     } catch (const NoConvergence&) {
       inner += it;  // count the failed solve's iterations too (as the device path does)
-      throw;
+      if (fk <= 0) throw;
+      it = 0;
     }
     inner += it;
     for (int i = 0; i < np; ++i) dst[nu + i] *= -1.0;

@@ -71,6 +71,7 @@ def lib():
         L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
         L.orc_set_inner_max_steps.argtypes = [P, I]
         L.orc_set_schur_fixed_inner.argtypes = [P, I]
+        L.orc_set_block_fixed_inner.argtypes = [P, I]
         L.orc_set_threads.argtypes = [I]
         L.orc_fgmres_outer.argtypes = [P, P, I, P]
         L.orc_a_solve_iterations.argtypes = [P]
@@ -205,6 +206,11 @@ class Model:
     def set_inner_max_steps(self, n):
         """Timing hook: cap of the inner Schur GMRES (the reference's 5000)."""
         lib().orc_set_inner_max_steps(self.h, int(n))
+
+    def set_block_fixed_inner(self, k):
+        """Parity hook: the block preconditioner's inner Schur GMRES runs
+        exactly k steps with no tolerance test (0 = the reference's rule)."""
+        lib().orc_set_block_fixed_inner(self.h, int(k))
 
     def set_schur_fixed_inner(self, k):
         """Parity hook: the Schur solver's inner CGs run exactly k steps (0 = off)."""

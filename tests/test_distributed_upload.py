@@ -151,3 +151,40 @@ def test_distributed_upload_world1_is_the_global_upload():
     assert np.array_equal(ref.get_state_owned(dcp.NSE_RHS, n), ctx.get_state_owned(dcp.NSE_RHS, n))
     x = rng.uniform(-1, 1, n)
     assert np.array_equal(ref.nse_vmult(x), ctx.nse_vmult(x))
+
+
+def _bad_input_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = dcp.HostMesh(refine=1)
+        dm = dcp.DistMesh(m, rank, world)
+        if rank == 1:
+            dm.cell_nse_dofs[0, 0] = m.n_u + m.n_p + 5   # an NSE dof out of range on rank 1 only
+        comm = dcp.torch_host_comm()
+        try:
+            dcp.dist_partition_info(dm, comm)
+            q.put((rank, "no error"))
+        except dcp.DcpError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_upload_bad_input_on_one_rank_fails_every_rank_gloo():
+    """A bad input on ONE rank must fail the distributed upload on EVERY rank
+    (DCP_ERR_INVALID), not leave the other ranks blocked in the next
+    collective: the local checks run first and their verdict is all-gathered
+    before any other exchange (csrc/distributed.cpp)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bad_input_worker, args=(r, world, 29651, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert "NSE dof out of range" in res[1], res
+    assert "another rank's input is invalid" in res[0], res

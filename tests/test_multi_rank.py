@@ -545,32 +545,24 @@ def test_group_rank_without_pressure_rows(gs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["rccl", "group"])
 @pytest.mark.parametrize("n_peers", [1, 3])
-def test_halo_exchange_round_trip_self_peer(transport, n_peers):
+def test_halo_exchange_round_trip_self_peer(n_peers):
     """RcclComm::exchange (csrc/comm.cpp) with real traffic on one GPU: a
     one-rank RCCL communicator whose halo plan lists the rank itself as its
     peer(s), so the grouped ncclSend/ncclRecv move data to their own rank
     through the solver's gather -> exchange -> scatter (the forward ghost import
     of boussinesq_model.tpp:1145-1146). Every received entry must equal the
-    sent one bitwise, everything else untouched; the in-process transport
-    (LocalComm) the same."""
+    sent one bitwise, everything else untouched (n_peers = 3: the list split
+    over three self-peers in one ncclGroupStart/End)."""
     rng = np.random.default_rng(5)
     n = 50_000
     vec = rng.standard_normal(n)
     vec[::7] = np.nan_to_num(np.array([np.inf]))  # extreme values travel unchanged
     send = rng.choice(n // 2, 4_000, replace=False).astype(np.int32)
     recv = (n // 2 + rng.choice(n // 2, 4_000, replace=False)).astype(np.int32)
-    if transport == "rccl":
-        ctx = dcp.Context(nccl_id=dcp.nccl_unique_id())
-        g = None
-    else:
-        g = dcp.Group(1)
-        ctx = dcp.Context(rank=0, world_size=1, group=g)
+    ctx = dcp.Context(nccl_id=dcp.nccl_unique_id())
     out = ctx.halo_selftest(vec, send, recv, n_peers)
     ctx.close()
-    if g is not None:
-        g.close()
     want = vec.copy()
     want[recv] = vec[send]
     assert np.array_equal(out.view(np.int64), want.view(np.int64))
