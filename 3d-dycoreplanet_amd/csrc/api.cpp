@@ -1942,6 +1942,25 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.bt_task_hdr.upload(hdr);
             c.bt_slot_rec.upload(rec);
             c.bt_ntasks = int(hdr.size() / 4);
+            // several GPUs: the rhs / constrained diagonal are read on owned rows
+            // only, so the cell kernel runs over the cells with an owned
+            // velocity node (owned cells + the first ghost layer), per colour
+            c.rhs_color_ptr.clear();
+            c.rhs_color_cells.release();
+            if (dist || nrows < nv) {
+              std::vector<int32_t> sub;
+              c.rhs_color_ptr.assign(1, 0);
+              for (size_t k = 0; k + 1 < h.color_ptr.size(); ++k) {
+                for (int e = h.color_ptr[k]; e < h.color_ptr[k + 1]; ++e) {
+                  const int cell = ccells[size_t(e)];
+                  bool own = false;
+                  for (int t = 0; t < 27 && !own; ++t) own = q2[27 * size_t(cell) + t] < nrows;
+                  if (own) sub.push_back(cell);
+                }
+                c.rhs_color_ptr.push_back(int(sub.size()));
+              }
+              c.rhs_color_cells.upload(sub);
+            }
             c.bt_ncols = int(c.mf_colgeo.n / 90);
             c.bt_P.alloc(size_t(216) * c.bt_ncols);
             c.bt_rows = true;
@@ -2241,10 +2260,15 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     // old fields were written some other way since
     if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
+    const bool rhs_subset = bt_rows && !c.rhs_color_ptr.empty();
     for (int k = 0; k < c.n_colors(); ++k) {
       if (full)
         launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                           c.old_T.p, c.ph, out, c.stream, c.element_mfma);
+      else if (rhs_subset)
+        launch_nse_operator(c.cd(), c.maps(), c.rhs_color_cells.p + c.rhs_color_ptr[k],
+                            c.rhs_color_ptr[k + 1] - c.rhs_color_ptr[k], c.old_nse.p, c.old_T.p,
+                            c.ph, out, c.stream);
       else
         launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                             c.old_T.p, c.ph, out, c.stream);

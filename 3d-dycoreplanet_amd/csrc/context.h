@@ -133,6 +133,9 @@ struct Ctx {
   bool bt_rows = false;
   DBuf<int32_t> bt_task_hdr, bt_slot_rec;
   int bt_ntasks = 0;
+  // several GPUs: per colour the cells with an owned velocity node (the rhs)
+  std::vector<int> rhs_color_ptr;
+  DBuf<int32_t> rhs_color_cells;
   DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
   DBuf<double> bt_P;  // [n_cols][216] column factors, formed every assembly
   int bt_ncols = 0;

@@ -1684,6 +1684,207 @@ __global__ __launch_bounds__(64 * kOpWaves) void k_nse_operator_wave(
 }
 
 // ---------------------------------------------------------------------------
+// The operator form without B^T (B^T by row tasks, k_bt_tasks): what stays per
+// cell is the rhs (local_assemble_nse_system's f_i, boussinesq_model.tpp:
+// 655-669, condensed and added into nse_rhs) and the constrained-row diagonal.
+// Half a wave per cell, two cells per wave (the rhs phases use 27 lanes):
+// lanes 0-26 of the half hold Gauss points (state, geometry, integrand), then
+// nodes (test-function sums, on cells with a constrained node also the
+// |K_ii| sums of k_nse_operator_wave). Every sum in k_nse_operator_wave's
+// order: the rhs and the diagonal are bitwise that kernel's.
+struct RhsCellSmem {
+  double U[81], T[27];
+  Geo geo;
+  double F[81];
+  double diag[27];
+  int node[27];
+};
+constexpr int kRhsCellsPerGroup = 8;  // 4 waves x 2 cells
+
+__global__ __launch_bounds__(256) void k_nse_rhs_halfwave(
+    CellData cd, const int32_t* __restrict__ cells, int n_cells, const double* __restrict__ u_old,
+    const double* __restrict__ T_old, PhysicsDev ph, NseOut out) {
+  __shared__ RhsCellSmem smem[kRhsCellsPerGroup];
+  const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
+  const int k = int(blockIdx.x) * kRhsCellsPerGroup + half;
+  const bool live = k < n_cells;
+  RhsCellSmem& sh = smem[half];
+  const int cell = live ? cells[k] : 0;
+  const bool want_cdiag = out.cdiag != nullptr;
+  // ---- state and geometry (lanes 0-26: nodes / points)
+  bool con = false;
+  if (live && hl < 27) {
+    const int nd = cd.cell_q2[27 * size_t(cell) + hl];
+    sh.node[hl] = nd;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) sh.U[3 * hl + d] = u_old[3 * size_t(nd) + d];
+    if (cd.tdpc == 27) sh.T[hl] = T_old[cd.cell_T[27 * size_t(cell) + hl]];
+    sep_geometry(cd, cell, sh.geo, hl);
+    con = want_cdiag && out.cidx[nd] >= 0;
+  }
+  if (live && cd.tdpc == 8 && hl < 8) sh.T[hl] = T_old[cd.cell_T[8 * size_t(cell) + hl]];
+  // this half's cell has a constrained node
+  const unsigned long long bal = __ballot(con);
+  const bool cell_con = ((bal >> (32 * ((threadIdx.x >> 5) & 1))) & 0xffffffffull) != 0;
+  wsync();
+  // ---- rhs integrand per Gauss point (k_nse_operator_wave's formulas)
+  if (live && hl < 27) {
+    const int q = hl;
+    const double xa = sel_gauss(q % 3), xb = sel_gauss((q / 3) % 3), xc = sel_gauss(q / 9);
+    const double* Ji = &sh.geo.Ji[9 * q];
+    double LA[3], DA[3], LB[3], DB[3], LC[3], DC[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      LA[i] = ce_l2(i, xa);
+      DA[i] = ce_dl2(i, xa);
+      LB[i] = ce_l2(i, xb);
+      DB[i] = ce_dl2(i, xb);
+      LC[i] = ce_l2(i, xc);
+      DC[i] = ce_dl2(i, xc);
+    }
+    double u[3] = {0, 0, 0}, G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll 1
+    for (int nc = 0; nc < 3; ++nc) {
+      const double lc = sel3v(nc, LC), dc = sel3v(nc, DC);
+#pragma unroll 1
+      for (int nb = 0; nb < 3; ++nb) {
+        const double lb = sel3v(nb, LB), db = sel3v(nb, DB);
+#pragma unroll
+        for (int na = 0; na < 3; ++na) {
+          const int n = na + 3 * nb + 9 * nc;
+          const double s = LA[na] * lb * lc;
+          const double r0 = DA[na] * lb * lc;
+          const double r1 = LA[na] * db * lc;
+          const double r2 = LA[na] * lb * dc;
+          double Dn[3];
+#pragma unroll
+          for (int d = 0; d < 3; ++d) Dn[d] = r0 * Ji[d] + r1 * Ji[3 + d] + r2 * Ji[6 + d];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double un = sh.U[3 * n + c];
+            u[c] += un * s;
+            G[c][0] += un * Dn[0];
+            G[c][1] += un * Dn[1];
+            G[c][2] += un * Dn[2];
+          }
+        }
+      }
+    }
+    double T = 0;
+    if (cd.tdpc == 8) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) T += sh.T[v] * cRef.S1[8 * q + v];
+    } else {
+      for (int n = 0; n < 27; ++n)
+        T += sh.T[n] * (sel3v(n % 3, LA) * sel3v((n / 3) % 3, LB) * sel3v(n / 9, LC));
+    }
+    const double rho = 1 - ph.beta * (T - ph.T_ref);
+    double grav[3];
+    if (ph.cuboid) {
+      grav[0] = grav[1] = 0;
+      grav[2] = -ph.g;
+    } else {
+      const double* x = &sh.geo.xq[3 * q];
+      const double r = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+      const double den = r > 1 ? r : sqrt(r);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) grav[d] = -ph.g * x[d] / den;
+    }
+    const double cxu[3] = {-ph.coriolis_z * u[1], ph.coriolis_z * u[0], 0.0};
+    const double w = sh.geo.JxW[q];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double adv = u[0] * G[c][0] + u[1] * G[c][1] + u[2] * G[c][2];
+      sh.F[3 * q + c] = (u[c] + ph.dt * rho * (ph.grav_scale * grav[c]) - ph.dt * adv -
+                         ph.dt * (2 * cxu[c])) * w;
+    }
+  }
+  wsync();
+  // ---- per node: the rhs test-function sums (and on constrained cells the
+  // node-diagonal sums of the |K_ii| rule)
+  const int an = hl;
+  double kii[3] = {0, 0, 0};
+  if (live && an < 27) {
+    double fa[3] = {0, 0, 0};
+    double msum = 0, g2[3] = {0, 0, 0};
+    const int na = an % 3, nb = (an / 3) % 3, nc = an / 9;
+    double La[3], Da1[3], Lb[3], Db1[3], Lc[3], Dc1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double x = sel_gauss(i);
+      La[i] = ce_l2(na, x);
+      Da1[i] = ce_dl2(na, x);
+      Lb[i] = ce_l2(nb, x);
+      Db1[i] = ce_dl2(nb, x);
+      Lc[i] = ce_l2(nc, x);
+      Dc1[i] = ce_dl2(nc, x);
+    }
+#pragma unroll 1
+    for (int q2 = 0; q2 < 3; ++q2) {
+      const double lc = sel3v(q2, Lc), dc = sel3v(q2, Dc1);
+#pragma unroll 1
+      for (int q1 = 0; q1 < 3; ++q1) {
+        const double lb = sel3v(q1, Lb), db = sel3v(q1, Db1);
+#pragma unroll
+        for (int q0 = 0; q0 < 3; ++q0) {
+          const int q = q0 + 3 * q1 + 9 * q2;
+          const double s = La[q0] * lb * lc;
+          fa[0] += s * sh.F[3 * q];
+          fa[1] += s * sh.F[3 * q + 1];
+          fa[2] += s * sh.F[3 * q + 2];
+          if (cell_con) {
+            const double r0 = Da1[q0] * lb * lc;
+            const double r1 = La[q0] * db * lc;
+            const double r2 = La[q0] * lb * dc;
+            const double* Ji = &sh.geo.Ji[9 * q];
+            double Da[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) Da[d] = r0 * Ji[d] + r1 * Ji[3 + d] + r2 * Ji[6 + d];
+            const double w = sh.geo.JxW[q];
+            msum += w * s * s;
+            g2[0] += w * Da[0] * Da[0];
+            g2[1] += w * Da[1] * Da[1];
+            g2[2] += w * Da[2] * Da[2];
+          }
+        }
+      }
+    }
+    if (cell_con) {
+      const double L = g2[0] + g2[1] + g2[2];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) kii[c] = msum + ph.nu_sys * L + ph.nu_sys * g2[c];
+      sh.diag[an] = fabs(kii[0]) + fabs(kii[1]) + fabs(kii[2]);
+    }
+    const int nd = sh.node[an];
+    double Ca[3][3];
+    condensation(cd.vcon[nd], Ca);
+    if (out.rhs) {
+      double* dst = out.rhs + 3 * size_t(nd);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j] += Ca[0][j] * fa[0] + Ca[1][j] * fa[1] + Ca[2][j] * fa[2];
+    }
+  }
+  if (!cell_con) return;
+  wsync();
+  if (live && an < 27) {
+    const int nd = sh.node[an];
+    const int ci = out.cidx[nd];
+    if (ci >= 0) {
+      const NodeConstraint nc = cd.vcon[nd];
+      double avg = 0;
+      for (int m = 0; m < 27; ++m) avg += sh.diag[m];
+      avg /= 89.0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (nc.type == 1 || nc.type == 3 || c == nc.k) {
+          const double d = fabs(kii[c]);
+          out.cdiag[3 * size_t(ci) + c] += d != 0.0 ? d : avg;
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // B^T by rows on the radially separable shell (copy_local_to_global_nse_system
 // of the B^T block, boussinesq_model.tpp:626-637 / 677-687, restated as a
 // gather). The entry of velocity node n = (a, b, c) of cell K and vertex
@@ -1864,7 +2065,17 @@ void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_
     const char* e = std::getenv("DCP_ASM_SMALL_COLOUR");
     return e ? std::atoi(e) : kOpSmallColour;
   }();
-  if (cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block && n >= small_colour) {
+  // without B^T / B (written by row tasks): the rhs-only half-wave kernel
+  // (DCP_ASM_RHS_HALFWAVE=0 keeps the wave kernel, for comparisons)
+  static const bool halfwave = [] {
+    const char* e = std::getenv("DCP_ASM_RHS_HALFWAVE");
+    return !(e && *e == '0');
+  }();
+  const bool sep = cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block;
+  if (sep && halfwave && !out.Bt && !out.B && !out.A) {
+    hipLaunchKernelGGL(k_nse_rhs_halfwave, dim3((n + kRhsCellsPerGroup - 1) / kRhsCellsPerGroup),
+                       dim3(256), 0, s, cd, cells, n, u_old, T_old, ph, out);
+  } else if (sep && n >= small_colour) {
     hipLaunchKernelGGL(k_nse_operator_wave, dim3((n + kOpWaves - 1) / kOpWaves), dim3(64 * kOpWaves),
                        0, s, cd, sm, cells, n, u_old, T_old, ph, out);
   } else {

@@ -33,6 +33,19 @@ sys.path.insert(0, os.path.join(ROOT, "3d-dycoreplanet_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# measured on this GPU model (tools/stream_probe.hip, 1 GiB arrays, best of 10):
+# the read / copy / triad ceilings every frac is also reported against
+CEILING_FILE = "profiles/r04c_stream_probe.json"
+
+
+def measured_ceilings():
+    path = os.path.join(ROOT, CEILING_FILE)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {"read_GBps": 1e3 * d["read_TBps"], "copy_GBps": 1e3 * d["copy_TBps"],
+            "triad_GBps": 1e3 * d["triad_TBps"], "source": CEILING_FILE}
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
 PMC_SUMMARIES = {(5, "explicit"): ("profiles/r03a_pmc_inner_r5.json", "k_sell_spmv<true, true>")}
@@ -661,6 +674,25 @@ def main():
                      if world == 1 else None,
                      "bytes_per_apply": sbytes, "avg_apply_ms": schur_ms},
     }
+    ceil = measured_ceilings()
+    if ceil:
+        # the SpMV streams S (read-dominated): against the measured read ceiling
+        out["roofline"]["frac_measured_read_ceiling"] = achieved / ceil["read_GBps"]
+        out["measured_ceilings"] = ceil
+    # the metric's own kernel work (value): operator-form assemble_nse_system.
+    # Algorithmic bytes = its outputs written once (B^T values 24 B per block,
+    # the velocity rhs 8 B per dof) + the old state read once (u 8 B per velocity
+    # dof, T 8 B per dof); index data and geometry tables excluded
+    asm_bytes = 24.0 * pinfo["nnzb_Bt"] + 16.0 * m.n_u + 8.0 * m.n_T
+    if world > 1:
+        asm_bytes /= world
+    asm_ach = asm_bytes / (asm_ms * 1e-3) / 1e9
+    out["roofline_assembly"] = {
+        "kernel": "operator-form assemble_nse_system (B^T by row tasks k_bt_tasks + rhs / "
+                  "constrained diagonal k_nse_rhs_halfwave per colour)",
+        "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
+        "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None}
     if args.schur == "explicit" and world == 1:
         out["roofline_chain"] = chain_roofline(args.refine, m.n_p, args.gram_schmidt)
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
@@ -688,6 +720,8 @@ def main():
                                  "achieved": ve_bytes / (ve_ms * 1e-3) / 1e9 if ve_ms > 0
                                  else None}}
         mf["frac"] = mf["achieved"] / HBM_PEAK_GBS if mf["achieved"] else None
+        if ceil and mf["achieved"]:
+            mf["frac_measured_read_ceiling"] = mf["achieved"] / ceil["read_GBps"]
         # the bytes the apply actually moves (PMC; the geometry is recomputed,
         # not read) over the same apply time
         mf["frac_actual_traffic"] = (mf["traffic"] / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
