@@ -340,6 +340,7 @@ struct SellView {
   const uint16_t* col16;   // with base, or null
   const int32_t* base;
   const double* val;
+  const int32_t* rowmap = nullptr;  // row -> vector entry (null: the row itself)
 };
 void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s);
 // y = (S x - theta x) * sscale (the s-step Newton basis); every launch returns

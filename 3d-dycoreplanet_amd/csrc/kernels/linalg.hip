@@ -310,21 +310,18 @@ __global__ __launch_bounds__(kBlock) void k_mgs_chain(
 }
 
 // SELL-64 SpMV (see device.h). One 256-thread workgroup per slice: lane i of
-// every wave owns row 64s+i, wave j sums the j-th quarter of the slice's
-// entry columns (4 waves per slice keep enough loads in flight: one wave per
-// slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound), then
-// wave 0 adds the 4 quarters in order (fixed summation order).
-// DCP_SELL_UNROLL4 (default): four column pairs per iteration, all value /
-// column loads issued before the gathers; the same summation order as the
-// two-pair loop. r=5 inner probe (tools/inner_probe.py, rocprofv3): 39.65 ->
-// 38.50 us per S apply; DCP_SELL_NT (nontemporal values) 43.3 us;
-// DCP_SELL_UNROLL8 (eight pairs first) 38.55 against 38.73 us, within noise.
-#ifndef DCP_SELL_UNROLL4
-#define DCP_SELL_UNROLL4 1
-#endif
-#ifndef DCP_SELL_UNROLL8
-#define DCP_SELL_UNROLL8 0
-#endif
+// every wave owns row 64s+i; wave j sums the column pairs j, j+4, j+8, ... of
+// the slice (round robin; 4 waves per slice keep enough loads in flight: one
+// wave per slice leaves ~3 waves per SIMD on a 2e5-row matrix, latency-bound),
+// then wave 0 adds the 4 partial sums in order (fixed summation order). A
+// row's sum depends only on its entries and their order, not on the slice's
+// width (padding pairs add exact zeros), so a row gives the same bits in any
+// slice: the matrix powers of the multi-GPU s-step basis evaluate ghost rows
+// on a rank other than their owner (solver.cpp).
+// Four column pairs per iteration, all value / column loads issued before the
+// gathers; r=5 inner probe (tools/inner_probe.py, rocprofv3): 39.65 -> 38.50 us
+// per S apply against the two-pair loop; DCP_SELL_NT (nontemporal values)
+// 43.3 us.
 #ifndef DCP_SELL_NT
 #define DCP_SELL_NT 0
 #endif
@@ -368,42 +365,17 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   }
   const int64_t b = m.off[sl];
   const int np = int((m.off[sl + 1] - b) >> 7);  // column pairs of the slice
-  const int per = (np + 3) >> 2;
-  const int k0 = wave * per, k1 = min(np, k0 + per);
-  const double2* vp = reinterpret_cast<const double2*>(m.val + b) + 64 * int64_t(k0) + lane;
+  const double2* vp = reinterpret_cast<const double2*>(m.val + b) + 64 * wave + lane;
   double acc = 0.0;
-  int k = k0;
+  int k = wave;
   if (C16) {
     const int cb = m.base[sl];
-    const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * int64_t(k0) + lane;
-#if DCP_SELL_UNROLL8
-    for (; k + 8 <= k1; k += 8, cp += 512, vp += 512) {
-      // eight column pairs (timing variant)
-      ushort2 c[8];
-      double2 a[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) c[i] = cp[64 * i];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = SELL_LD(vp + 64 * i);
-      double xv[16];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        xv[2 * i] = x[cb + c[i].x] * cf;
-        xv[2 * i + 1] = x[cb + c[i].y] * cf;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc += a[i].x * xv[2 * i];
-        acc += a[i].y * xv[2 * i + 1];
-      }
-    }
-#endif
-#if DCP_SELL_UNROLL4
-    for (; k + 4 <= k1; k += 4, cp += 256, vp += 256) {
-      // four column pairs: all value / column loads issued before the gathers
-      const ushort2 c0 = cp[0], c1 = cp[64], c2 = cp[128], c3 = cp[192];
-      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 64), a2 = SELL_LD(vp + 128),
-                    a3 = SELL_LD(vp + 192);
+    const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * wave + lane;
+    for (; k + 12 < np; k += 16, cp += 1024, vp += 1024) {
+      // pairs k, k + 4, k + 8, k + 12: all loads before the gathers
+      const ushort2 c0 = cp[0], c1 = cp[256], c2 = cp[512], c3 = cp[768];
+      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 256), a2 = SELL_LD(vp + 512),
+                    a3 = SELL_LD(vp + 768);
       const double x0 = x[cb + c0.x] * cf, x1 = x[cb + c0.y] * cf;
       const double x2 = x[cb + c1.x] * cf, x3 = x[cb + c1.y] * cf;
       const double x4 = x[cb + c2.x] * cf, x5 = x[cb + c2.y] * cf;
@@ -417,37 +389,32 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
       acc += a3.x * x6;
       acc += a3.y * x7;
     }
-#endif
-    for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
-      const ushort2 c0 = cp[0], c1 = cp[64];
-      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 64);
-      const double x0 = x[cb + c0.x] * cf, x1 = x[cb + c0.y] * cf;
-      const double x2 = x[cb + c1.x] * cf, x3 = x[cb + c1.y] * cf;
-      acc += a0.x * x0;
-      acc += a0.y * x1;
-      acc += a1.x * x2;
-      acc += a1.y * x3;
-    }
-    if (k < k1) {
+    for (; k < np; k += 4, cp += 256, vp += 256) {
       const ushort2 c0 = cp[0];
-      const double2 a0 = vp[0];
+      const double2 a0 = SELL_LD(vp);
       acc += a0.x * (x[cb + c0.x] * cf);
       acc += a0.y * (x[cb + c0.y] * cf);
     }
   } else {
-    const int2* cp = reinterpret_cast<const int2*>(m.col + b) + 64 * int64_t(k0) + lane;
-    for (; k + 2 <= k1; k += 2, cp += 128, vp += 128) {
-      const int2 c0 = cp[0], c1 = cp[64];
-      const double2 a0 = vp[0], a1 = vp[64];
+    const int2* cp = reinterpret_cast<const int2*>(m.col + b) + 64 * wave + lane;
+    for (; k + 12 < np; k += 16, cp += 1024, vp += 1024) {
+      const int2 c0 = cp[0], c1 = cp[256], c2 = cp[512], c3 = cp[768];
+      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 256), a2 = SELL_LD(vp + 512),
+                    a3 = SELL_LD(vp + 768);
       const double x0 = x[c0.x] * cf, x1 = x[c0.y] * cf, x2 = x[c1.x] * cf, x3 = x[c1.y] * cf;
+      const double x4 = x[c2.x] * cf, x5 = x[c2.y] * cf, x6 = x[c3.x] * cf, x7 = x[c3.y] * cf;
       acc += a0.x * x0;
       acc += a0.y * x1;
       acc += a1.x * x2;
       acc += a1.y * x3;
+      acc += a2.x * x4;
+      acc += a2.y * x5;
+      acc += a3.x * x6;
+      acc += a3.y * x7;
     }
-    if (k < k1) {
+    for (; k < np; k += 4, cp += 256, vp += 256) {
       const int2 c0 = cp[0];
-      const double2 a0 = vp[0];
+      const double2 a0 = SELL_LD(vp);
       acc += a0.x * (x[c0.x] * cf);
       acc += a0.y * (x[c0.y] * cf);
     }
@@ -458,20 +425,23 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   acc += quarter[0][lane];
   acc += quarter[1][lane];
   acc += quarter[2][lane];
+  // the vector entry of the row (m.rowmap: rows kept apart from the vector
+  // order, the ghost rows of the matrix powers)
+  const long orow = (m.rowmap && row < rows) ? long(m.rowmap[row]) : row;
   if (!EPI) {
-    if (row < rows) y[row] = acc;
+    if (row < rows) y[orow] = acc;
     return;
   }
   double d0 = 0, d1 = 0;
   if (row < rows) {
-    const double xv = x[row] * cf;
+    const double xv = x[orow] * cf;
     // s-step Newton basis: y = (S x - theta x) / sigma (sscale = 1 / sigma)
     if (theta != 0.0 || sscale != 1.0) acc = (acc - theta * xv) * sscale;
     // GMRES restart head: the residual y = b - S x
-    if (bsub) acc = bsub[row] - acc;
-    y[row] = acc;
-    if (xs) xs[row] = xv;
-    if (part0) d0 = acc * (v0 == xs ? xv : v0[row]);  // v0 == xs: the first Arnoldi vector
+    if (bsub) acc = bsub[orow] - acc;
+    y[orow] = acc;
+    if (xs) xs[orow] = xv;
+    if (part0) d0 = acc * (v0 == xs ? xv : v0[orow]);  // v0 == xs: the first Arnoldi vector
     if (part1) d1 = acc * acc;
   }
   if (!part0 && !part1) return;
