@@ -720,7 +720,11 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   }
 }
 
-// Device halo of one vector family from per-peer position lists.
+}  // namespace
+
+namespace dcp {
+// Device halo of one vector family from per-peer position lists (also the
+// matrix powers' halos, matpow.cpp).
 void make_halo(Ctx::Halo& h, const std::vector<int>& peers,
                const std::vector<std::vector<int32_t>>& spos,
                const std::vector<std::vector<int32_t>>& rpos) {
@@ -745,6 +749,9 @@ void make_halo(Ctx::Halo& h, const std::vector<int>& peers,
   h.sbuf.alloc(sp.size());
   h.rbuf.alloc(rp.size());
 }
+}  // namespace dcp
+
+namespace {
 
 // positions of a HaloPlan's entities in a vector: entity e -> off + w*e + j
 void plan_positions(const HaloPlan& p, int off, std::vector<int>& peers,
@@ -1094,6 +1101,7 @@ void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_
   }
   c.S_val.alloc(len);
   c.S_val.zero(c.stream);  // padding entries stay 0
+  c.mp.reset();            // the matrix powers follow the pattern of S
   c.sell_part_len = sell_fused_blocks(rows);
   c.sperm_x.alloc(std::max(rows, 1));
   c.sperm_b.alloc(std::max(rows, 1));
@@ -1465,6 +1473,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
     if (option == DCP_OPT_INNER_MAX_STEPS) {
       require(value >= 1, DCP_ERR_INVALID, "DCP_OPT_INNER_MAX_STEPS must be >= 1");
       ctx->inner_max_steps = value;
+      return DCP_OK;
+    }
+    if (option == DCP_OPT_MATRIX_POWERS) {
+      ctx->matrix_powers = value != 0;
       return DCP_OK;
     }
     if (option == DCP_OPT_BLOCK_FIXED_INNER) {
@@ -2325,6 +2337,7 @@ int dcp_build_nse_preconditioner(dcp_ctx* ctx) {
                             c.B_current ? nullptr : c.B_tperm.p, c.Bt_ptr.p, c.Bt_col.p,
                             c.Bt_val.p, c.A_inv.p, c.S_ptr.p, c.S_col.p, c.S_pmap.p,
                             c.S_val.p, c.S_max_row, c.stream);
+      ++c.S_version;
     }
     t.stop();
     c.precond_built = true;
@@ -2724,6 +2737,19 @@ int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_t
       if (nnzb) nnzb[i] = n[i];
       if (first_touch) first_touch[i] = f[i];
     }
+    return DCP_OK;
+  });
+}
+
+int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(info != nullptr, DCP_ERR_INVALID, "NULL info");
+    const Ctx& c = *ctx;
+    const Ctx::MatPow& m = c.mp;
+    const int64_t v[8] = {m.built ? 1 : 0, m.n_ext, m.rows[1], m.rows[2], m.rows[3],
+                          m.halo.nr, m.vals.nr, c.halo_p.nr};
+    for (int i = 0; i < 8; ++i) info[i] = m.built || i == 7 ? v[i] : 0;
     return DCP_OK;
   });
 }

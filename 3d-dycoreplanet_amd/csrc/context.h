@@ -202,6 +202,27 @@ struct Ctx {
     return SellView{npo, S_sell_off.p, S_sell_col.p, S_sell_c16.p, S_sell_base.p, S_val.p};
   }
   DBuf<double> S_val;
+  long S_version = 0;                // formations of S_val (matrix powers: ghost values current?)
+  // several GPUs, s-step inner solve: matrix powers (matpow.cpp). Ghost rows
+  // of S (depth 1..3 from the owned rows, by depth) in SELL-64 with a row map
+  // into the extended pressure vector [local dofs | further dofs the ghost
+  // rows reach], their values from the owners, and the depth-4 halo
+  bool matrix_powers = true;         // DCP_OPT_MATRIX_POWERS
+  struct MatPow {
+    bool built = false;
+    int n_ext = 0;                   // extended pressure vector length
+    int rows[4] = {0, 0, 0, 0};      // ghost rows of depth <= 0, 1, 2, 3
+    DBuf<int64_t> off;
+    DBuf<int32_t> col, rowmap;
+    DBuf<double> val;
+    Halo halo;                       // depth-4 halo of a block's start vector
+    Halo vals;                       // owner SELL positions -> ghost SELL positions
+    long version = -1;               // the S_version of val
+    SellView view(int depth) const {
+      return SellView{rows[depth], off.p, col.p, nullptr, nullptr, val.p, rowmap.p};
+    }
+    void reset();
+  } mp;
   DBuf<double> sell_part;            // 2 x sell_fused_blocks(n_p) partials
   int S_max_row = 0;
   bool schur_explicit = true;
@@ -295,7 +316,8 @@ struct Ctx {
   // Krylov workspaces (lazily sized)
   std::vector<double*> fg_v, fg_z;   // FGMRES basis
   DBuf<double> fg_aux;
-  std::vector<double*> sg_v;         // inner Schur GMRES basis (n_p)
+  std::vector<double*> sg_v;         // inner Schur GMRES basis (n_p, or mp.n_ext)
+  size_t sg_len = 0;                 // length of the sg_v vectors
   DBuf<double> schur_tmp1, schur_tmp2, utmp;
   std::vector<double*> ag_v;         // fallback A-GMRES basis (n_u)
   DBuf<double> cg_g, cg_d, cg_h;
@@ -464,5 +486,9 @@ int feec_solve_nse(Ctx& c, int* iterations);
 int chain_width(const Ctx& c, Seg g);
 void allreduce(Ctx& c, double* buf, size_t n, bool max = false);
 void halo_exchange(Ctx& c, Ctx::Halo& h, double* v);
+// matpow.cpp: build the matrix powers (collective, once per mesh) and copy the
+// ghost rows' values from their owners when S was formed again (collective)
+void matpow_setup(Ctx& c);
+void matpow_prepare(Ctx& c);
 
 }  // namespace dcp

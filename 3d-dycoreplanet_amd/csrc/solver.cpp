@@ -790,7 +790,7 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   const int restart = n_tmp - 2;
   if (restart + 1 > kGmMaxDim || restart % kSStep)
     throw std::runtime_error("gmres_schur_sstep: restart must be a multiple of the block size");
-  ensure_pool(tv, n_tmp + kSStep, size_t(n));
+  ensure_pool(tv, n_tmp + kSStep, size_t(std::max(n, c.mp.n_ext)));
   double* p = tv[n_tmp - 1];
   double* wraw[kSStep];
   for (int i = 0; i < kSStep; ++i) wraw[i] = tv[n_tmp + i];
@@ -808,6 +808,8 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   const int nb1 = std::min(c.n_cus, 256);
   Comm* comm = c.comm.get();
   const bool fused = sstep_fits(c, g.n, nb1);
+  // matrix powers: prepared by the caller (block_prec), pool vectors n_ext long
+  const bool mp = comm && c.mp.built && c.mp.version == c.S_version;
   if (!fused) {
     const size_t pn = 2 * size_t(128) * std::max<size_t>(1, size_t((g.n + 511) / 512)) + 2;
     if (c.gm_part.n < pn) {
@@ -844,13 +846,20 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
           DCP_HIP_CHECK(hipEventRecord(eb->a, c.stream));
         }
       }
+      // matrix powers (several GPUs): the start vector once on every dof
+      // within distance 4, then basis vector i on the ghost rows of depth
+      // <= 3 - i as well (matpow.cpp); else one halo exchange per SpMV
+      if (mp) halo_exchange(c, c.mp.halo, const_cast<double*>(src));
       for (int i = 0; i < kSStep; ++i) {
         const double* in = i == 0 ? src : wraw[i - 1];
-        halo_exchange(c, c.halo_p, const_cast<double*>(in));
+        if (!mp) halo_exchange(c, c.halo_p, const_cast<double*>(in));
         Timer* e = comm ? schur_sample(c) : nullptr;
         if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
         sell_spmv_shifted(c.sell(), in, sa.theta[i], 1.0 / sa.sigma, wraw[i], &dst->status,
                           c.stream);
+        if (mp && i < kSStep - 1 && c.mp.rows[kSStep - 1 - i] > 0)
+          sell_spmv_shifted(c.mp.view(kSStep - 1 - i), in, sa.theta[i], 1.0 / sa.sigma, wraw[i],
+                            &dst->status, c.stream);
         if (e) DCP_HIP_CHECK(hipEventRecord(e->b, c.stream));
       }
       if (eb) DCP_HIP_CHECK(hipEventRecord(eb->b, c.stream));
@@ -1011,7 +1020,19 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
     const unsigned cap = fixed ? unsigned(c.block_fixed_inner) : unsigned(c.inner_max_steps);
     const double tol = fixed ? 0.0 : 1e-6 * nrm;
     Control ctl{cap, tol};
-    ensure_pool(c.sg_v, 32, size_t(np));
+    // several GPUs, s-step: the matrix powers' ghost rows current (collective)
+    // and the basis vectors long enough for the further dofs they reach
+    size_t pn = size_t(np);
+    if (c.comm && c.schur_explicit && !c.dim2 && c.gram_schmidt == 3 && c.matrix_powers) {
+      matpow_prepare(c);
+      pn = std::max(pn, size_t(c.mp.n_ext));
+    }
+    if (pn > c.sg_len) {
+      for (double* q : c.sg_v) (void)hipFree(q);
+      c.sg_v.clear();
+      c.sg_len = pn;
+    }
+    ensure_pool(c.sg_v, 32, c.sg_len);
     State st;
     if (c.dim2) {
       // 2D: S = B D_A^-1 B^T as three products (schur_vmult), deal.II GMRES
@@ -1234,6 +1255,8 @@ void free_workspaces(Ctx& c) {
     for (double* p : *pool) (void)hipFree(p);
     pool->clear();
   }
+  c.sg_len = 0;
+  c.mp.reset();  // the matrix powers follow the mesh
 }
 
 void ensure_workspaces(Ctx& c) {

@@ -39,6 +39,7 @@ OPT_INNER_MAX_STEPS = 11
 OPT_SCHUR_FIXED_INNER = 12
 OPT_HANDOFF_SPIN_LIMIT = 13
 OPT_BLOCK_FIXED_INNER = 14
+OPT_MATRIX_POWERS = 15
 ABI_VERSION = 5            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
@@ -64,7 +65,7 @@ EXPORTED = [
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
     "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_state_set_owned",
-    "dcp_state_get_owned", "dcp_scatter_info", "dcp_nse_coupling_export",
+    "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_nse_coupling_export",
     "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
 
@@ -253,6 +254,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int)]
     lib.dcp_scatter_info.argtypes = [P, P, P, P]
+    lib.dcp_matrix_powers_info.argtypes = [P, P]
     lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
@@ -1021,6 +1023,13 @@ class Context:
         one per step; bitwise the same results."""
         self._check(lib().dcp_set_option(self._h, OPT_FUSED_CHAIN, int(bool(on))))
 
+    def set_matrix_powers(self, on=True):
+        """DCP_OPT_MATRIX_POWERS (default on): on several GPUs the s-step inner
+        Schur GMRES exchanges each block's start vector once to S-graph depth 4
+        and computes the next basis vectors on its ghost rows (bitwise the same
+        iterates as one exchange per SpMV)."""
+        self._check(lib().dcp_set_option(self._h, OPT_MATRIX_POWERS, int(bool(on))))
+
     def set_block_fixed_inner(self, k: int):
         """DCP_OPT_BLOCK_FIXED_INNER (parity hook): the block preconditioner's
         inner Schur GMRES runs exactly k steps, no tolerance test (0 = the
@@ -1191,6 +1200,14 @@ class Context:
         f = np.zeros(3, np.int32)
         self._check(lib().dcp_scatter_info(self._h, _ptr(t), _ptr(n), _ptr(f)))
         return {k: (int(t[i]), int(n[i]), bool(f[i])) for i, k in enumerate(("A", "Bt", "B"))}
+
+    def matrix_powers_info(self) -> dict:
+        """The matrix powers of the last s-step inner solve on several GPUs
+        (dcp_matrix_powers_info)."""
+        v = np.zeros(8, np.int64)
+        self._check(lib().dcp_matrix_powers_info(self._h, _ptr(v)))
+        return {"built": bool(v[0]), "n_ext": int(v[1]), "rows": [int(x) for x in v[2:5]],
+                "halo_recv": int(v[5]), "value_recv": int(v[6]), "spmv_halo_recv": int(v[7])}
 
     def coupling_csr(self, which: str):
         """The operator form's B^T ("Bt", 3 n_vnodes x n_p) or B ("B", n_p x n_u)

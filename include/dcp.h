@@ -279,6 +279,14 @@ enum { DCP_OPT_HANDOFF_SPIN_LIMIT = 13 };
  * dot products are summed in different orders (1 vs P GPUs) take the same
  * control decisions. */
 enum { DCP_OPT_BLOCK_FIXED_INNER = 14 };
+/* DCP_OPT_MATRIX_POWERS: 1 (default) = on several GPUs the s-step inner Schur
+ * GMRES (DCP_OPT_GRAM_SCHMIDT = 3) receives each block's start vector once on
+ * every pressure dof within S-graph distance 4 of the owned rows and computes
+ * the next three basis vectors on the ghost rows itself (rows of S copied from
+ * their owners after each formation): one halo exchange per block of 4 SpMVs
+ * instead of 4. Bitwise the same iterates; 0 = one exchange per SpMV. No
+ * effect on one GPU or with another DCP_OPT_GRAM_SCHMIDT. */
+enum { DCP_OPT_MATRIX_POWERS = 15 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* The SolverControl log of the last dcp_solve_nse (DCP_OPT_LOG_HISTORY):
@@ -415,6 +423,14 @@ int dcp_halo_selftest(dcp_ctx* ctx, int n, double* vec, int n_list, const int32_
  * blocks some cell's scatter position reaches, the pattern size, and whether
  * the assembly stores at first touch (1) or zero-fills and adds (0). */
 int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_touch);
+
+/* The matrix powers of the last s-step inner solve (DCP_OPT_MATRIX_POWERS,
+ * several GPUs): info[0] = 1 if built, [1] the extended pressure vector length
+ * (local dofs + the further dofs the ghost rows reach), [2..4] ghost rows of
+ * depth <= 1, 2, 3, [5] entries received per block (the depth-4 halo), [6]
+ * ghost-row values received per formation of S, [7] the per-SpMV halo's
+ * receive count. Zeros on one GPU or before the first such solve. */
+int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]);
 
 /* The operator form's coupling blocks of nse_matrix as scalar CSR, without
  * materialising the velocity block: which = 0 -> B^T (3 n_vnodes rows, pressure

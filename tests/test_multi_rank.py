@@ -578,3 +578,73 @@ def test_group_8_ranks_refine4_fixed_inner(gs):
     solve takes exactly 28 steps and the outer FGMRES converges on every
     partition alike. rhs 1e-12, equal outer and inner counts, iterates 1e-10."""
     test_group_time_step_matches_single_gpu(8, 4, gs, fixed_inner=28)
+
+
+def _group_run(world, m, ph, u, T, setup, collect=None):
+    """One time step on `world` in-process ranks; setup(ctx) before it,
+    collect(ctx) after it (its result added under "extra")."""
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(ph)
+            ctx.upload_mesh(m)
+            setup(ctx)
+            results[rank] = _time_step(ctx, m, u, T)
+            if collect:
+                results[rank]["extra"] = collect(ctx)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+    return results
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,refine,fixed_inner", [(2, 2, 0), (3, 2, 0), (8, 3, 0),
+                                                      (13, 1, 0), (8, 4, 28)])
+def test_group_matrix_powers_bitwise(world, refine, fixed_inner):
+    """DCP_OPT_MATRIX_POWERS (csrc/matpow.cpp): the s-step inner Schur GMRES
+    with one depth-4 exchange per block of 4 SpMVs, the ghost rows computed
+    locally from S rows copied from their owners, against one exchange per SpMV.
+    The SELL kernel sums a row in an order fixed by the row alone, so every
+    iterate -- and every rank's solution, iteration counts and temperature --
+    must agree bitwise. (13, 1): a rank without pressure rows; (8, 4): BASELINE
+    config 3's mesh with the fixed-inner parity hook."""
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(11)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    T = m.T0.copy()
+
+    def setup(on):
+        def f(ctx):
+            ctx.set_gram_schmidt("sstep")
+            ctx.set_block_fixed_inner(fixed_inner)
+            ctx.set_matrix_powers(on)
+        return f
+
+    on = _group_run(world, m, ph, u, T, setup(True), lambda c: c.matrix_powers_info())
+    off = _group_run(world, m, ph, u, T, setup(False), lambda c: c.matrix_powers_info())
+    for r, (a, b) in enumerate(zip(on, off)):
+        info = a["extra"]
+        assert info["built"], r
+        assert not b["extra"]["built"]
+        # ghost rows by depth, nested; the extended vector holds the local dofs
+        assert 0 <= info["rows"][0] <= info["rows"][1] <= info["rows"][2]
+        assert info["n_ext"] >= m.n_p // world or info["rows"][2] == 0
+        assert a["nse"] == b["nse"], r
+        assert a["T"] == b["T"], r
+        for key in ("x", "Tx", "rhs"):
+            assert np.array_equal(a[key].view(np.int64), b[key].view(np.int64)), (r, key)
+    print("matrix powers", world, refine, [x["extra"] for x in on[:2]])

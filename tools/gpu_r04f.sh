@@ -13,6 +13,7 @@ timeout -k 10 600 python3 -u -m pytest -x -v -s --timeout 300 --timeout-method t
   tests/test_cube.py::test_cube_repeated_operator_form_assembly \
   tests/test_multi_rank.py::test_group_rank_without_pressure_rows \
   tests/test_multi_rank.py::test_group_8_ranks_refine4_fixed_inner \
+  tests/test_multi_rank.py::test_group_matrix_powers_bitwise \
   tests/test_driver.py tests/test_refine6.py > $OUT/new_tests.log 2>&1 || { echo "new tests failed"; tail -60 $OUT/new_tests.log; exit 1; }
 grep -E "PASSED|FAILED|scatter info|device memory|residual reduction" $OUT/new_tests.log | tail -40
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
