@@ -147,8 +147,10 @@ def test_cube_repeated_operator_form_assembly(cube):
         orc.assemble_nse_system(u, T)
         orc.build_nse_preconditioner()
         Ao = csr(*orc.nse_matrix_csr(), n)
-        Bt_g = sp.csr_matrix(ctx.coupling_csr("Bt"), shape=(m.n_u, m.n_p))
-        B_g = sp.csr_matrix(ctx.coupling_csr("B"), shape=(m.n_p, m.n_u))
+        rp, cols, vals = ctx.coupling_csr("Bt")
+        Bt_g = sp.csr_matrix((vals, cols, rp), shape=(m.n_u, m.n_p))
+        rp, cols, vals = ctx.coupling_csr("B")
+        B_g = sp.csr_matrix((vals, cols, rp), shape=(m.n_p, m.n_u))
         Bt_o, B_o = Ao[:m.n_u, m.n_u:], Ao[m.n_u:, :m.n_u]
         assert abs(Bt_g - Bt_o).max() / abs(Bt_o).max() < 1e-12, i
         assert abs(B_g - B_o).max() / abs(B_o).max() < 1e-12, i

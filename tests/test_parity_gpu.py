@@ -535,8 +535,10 @@ def test_sstep_three_launch_block_matches_fused():
 
 
 def _coupling(ctx, m):
-    Bt = sp.csr_matrix(ctx.coupling_csr("Bt"), shape=(m.n_u, m.n_p))
-    B = sp.csr_matrix(ctx.coupling_csr("B"), shape=(m.n_p, m.n_u))
+    rp, cols, vals = ctx.coupling_csr("Bt")
+    Bt = sp.csr_matrix((vals, cols, rp), shape=(m.n_u, m.n_p))
+    rp, cols, vals = ctx.coupling_csr("B")
+    B = sp.csr_matrix((vals, cols, rp), shape=(m.n_p, m.n_u))
     return Bt, B
 
 

@@ -6,7 +6,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 240 python3 -u tools/bt_rows_probe.py > $OUT/probe.json 2> $OUT/probe.err || { echo "probe failed"; tail -20 $OUT/probe.err; exit 1; }
 cat $OUT/probe.json
-timeout -k 10 600 python3 -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu \
+timeout -k 10 900 python3 -u -m pytest -v -s --timeout 300 --timeout-method thread -m gpu \
   tests/test_multi_rank.py::test_halo_exchange_round_trip_self_peer \
   "tests/test_parity_gpu.py::test_repeated_operator_form_assembly_matches_oracle" \
   "tests/test_parity_gpu.py::test_handoff_timeout_reruns_on_multi_launch_kernels" \
