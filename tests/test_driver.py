@@ -111,6 +111,15 @@ def test_executable_writes_vtu_output(tmp_path):
 
 
 @pytest.mark.gpu
+def _calls(ctx, name):
+    """Calls of a TimerOutput section; 0 for a section never entered (the
+    library knows only sections that ran)."""
+    try:
+        return ctx.timer_section(name)[0]
+    except dcp.DcpError:
+        return 0
+
+
 def test_solver_history_and_timer_sections():
     """§5 auxiliaries: SolverControl(..., log_history = true, log_result = true)
     of the FGMRES solve (boussinesq_model.tpp:1166-1169) and the TimerOutput
@@ -187,8 +196,8 @@ def test_run_feec_with_schur_complement_solver_is_the_reference_no_op():
         ctx.set_state(dcp.OLD_NSE_SOLUTION, x0)
         rc, rep, steps = ctx.run(rp, max_steps=1)
         out[schur] = (rc, rep, ctx.get_state(dcp.NSE_SOLUTION), x0,
-                      ctx.timer_section("   Build NSE FEEC preconditioner")[0],
-                      ctx.timer_section("   Solve NSE system")[0])
+                      _calls(ctx, "   Build NSE FEEC preconditioner"),
+                      _calls(ctx, "   Solve NSE system"))
         ctx.close()
     rc, rep, x, x0, n_prec, n_solve = out[1]
     assert rc == dcp.DCP_OK and rep.steps == 1 and rep.fgmres_outer == 0
@@ -225,5 +234,5 @@ def test_run_rejects_what_the_device_path_does_not_implement(case):
     with pytest.raises(dcp.DcpError) as e:
         ctx.run(rp, max_steps=1)
     assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
-    assert ctx.timer_section("   Assemble NSE system")[0] == 0
+    assert _calls(ctx, "   Assemble NSE system") == 0
     ctx.close()
