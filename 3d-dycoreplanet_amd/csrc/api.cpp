@@ -1020,6 +1020,7 @@ bool separable_geometry(int n_cells, NodeFn node, std::vector<int32_t>& col,
 
 void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_t>& Sc,
                 bool permute) {
+  c.S_nbr.release();
   const int rows = c.npo;
   const int n_sl = (rows + 63) / 64;
   std::vector<int32_t> perm, iperm;
@@ -1105,6 +1106,163 @@ void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_
   c.sell_part_len = sell_fused_blocks(rows);
   c.sperm_x.alloc(std::max(rows, 1));
   c.sperm_b.alloc(std::max(rows, 1));
+}
+
+// S with structured columns (one GPU, SellView::nbr). On a radially layered
+// shell the Q1 pressure dofs form a grid of levels (radial vertex layers) x
+// lateral vertices, and S = B D^-1 B^T couples (l, c) with (l', c') exactly
+// when |l' - l| <= 2 and c' is in c's lateral two-ring N(c) (cells are
+// products of a lateral quad and a radial interval, so the coupling through a
+// shared velocity node factors): the pattern of row (l, c) is {l-2..l+2} x N(c).
+// Rows are ordered level-major, laterals in reverse Cuthill-McKee order of the
+// two-ring graph; entry k = 5 j + d of row (l, c) is column (l + d - 2, N(c)_j).
+// The kernel then streams the values only (8 instead of 10 bytes per entry,
+// plus 5 / 159 zero entries at the boundary levels at refine 5) and forms the
+// column from the row's level and the L2-resident neighbour table. Returns
+// false (and changes nothing) unless every check holds; DCP_S_STRUCT=0 turns
+// it off.
+bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_t>& Sc,
+                           const std::vector<int32_t>& pd, const std::vector<double>& geo,
+                           int n_cells) {
+  const char* env = std::getenv("DCP_S_STRUCT");
+  if (env && *env == '0') return false;
+  const int n = c.npo;
+  if (n <= 0 || n != c.n_p || n_cells <= 0 || geo.size() < size_t(n_cells) * 3 * kMapPts ||
+      pd.size() != size_t(n_cells) * 8)
+    return false;
+  // radius of every pressure dof (its vertex: lexicographic support point
+  // 3a + 12b + 48c of the cubic map); vertices v and v + 4 one level apart
+  std::vector<double> rad(size_t(n), -1.0);
+  for (int cell = 0; cell < n_cells; ++cell)
+    for (int v = 0; v < 8; ++v) {
+      const int t = 3 * (v & 1) + 12 * ((v >> 1) & 1) + 48 * (v >> 2);
+      const double* X = &geo[3 * (size_t(kMapPts) * cell + t)];
+      const double r = std::sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+      const int p = pd[8 * size_t(cell) + v];
+      if (p < 0 || p >= n) return false;
+      if (rad[p] < 0) rad[p] = r;
+      else if (std::fabs(rad[p] - r) > 1e-12 * r) return false;
+    }
+  std::vector<double> ur(rad);
+  std::sort(ur.begin(), ur.end());
+  if (!(ur[0] > 0)) return false;
+  std::vector<double> lev;
+  for (double r : ur)
+    if (lev.empty() || r > lev.back() * (1 + 1e-10)) lev.push_back(r);
+  const int nl = int(lev.size());
+  std::vector<int32_t> level(static_cast<size_t>(n));
+  for (int p = 0; p < n; ++p)
+    level[p] = int32_t(std::lower_bound(lev.begin(), lev.end(), rad[p] * (1 - 1e-10)) - lev.begin());
+  // lateral vertices: dofs v and v + 4 of a cell lie on one radial line
+  std::vector<int32_t> par(static_cast<size_t>(n));
+  std::iota(par.begin(), par.end(), 0);
+  auto find = [&](int32_t a) {
+    while (par[a] != a) a = par[a] = par[par[a]];
+    return a;
+  };
+  for (int cell = 0; cell < n_cells; ++cell)
+    for (int v = 0; v < 4; ++v) {
+      const int32_t a = pd[8 * size_t(cell) + v], b = pd[8 * size_t(cell) + v + 4];
+      if (std::abs(level[b] - level[a]) != 1) return false;
+      const int32_t ra = find(a), rb = find(b);
+      if (ra != rb) par[std::max(ra, rb)] = std::min(ra, rb);
+    }
+  std::vector<int32_t> lat(size_t(n), -1), rootid(size_t(n), -1);
+  int nc = 0;
+  for (int p = 0; p < n; ++p) {
+    const int32_t r = find(p);
+    if (rootid[r] < 0) rootid[r] = nc++;
+    lat[p] = rootid[r];
+  }
+  if (int64_t(nc) * nl != n) return false;
+  std::vector<int32_t> dof_at(size_t(n), -1);  // [l * nc + lateral] -> dof
+  for (int p = 0; p < n; ++p) {
+    int32_t& d = dof_at[size_t(level[p]) * nc + lat[p]];
+    if (d >= 0) return false;
+    d = p;
+  }
+  // lateral two-ring sets from the pattern; every coupling within two levels
+  std::vector<std::vector<int32_t>> ring(nc);
+  for (int p = 0; p < n; ++p)
+    for (int k = Sp[p]; k < Sp[p + 1]; ++k) {
+      const int q = Sc[k];
+      if (std::abs(level[q] - level[p]) > 2) return false;
+      ring[lat[p]].push_back(lat[q]);
+    }
+  size_t ring_nnz = 0;
+  for (auto& r : ring) {
+    std::sort(r.begin(), r.end());
+    r.erase(std::unique(r.begin(), r.end()), r.end());
+    ring_nnz += r.size();
+  }
+  // lateral order: reverse Cuthill-McKee of the two-ring graph
+  std::vector<int32_t> rp(size_t(nc) + 1, 0), rc;
+  rc.reserve(ring_nnz);
+  for (int a = 0; a < nc; ++a) {
+    rc.insert(rc.end(), ring[a].begin(), ring[a].end());
+    rp[a + 1] = int32_t(rc.size());
+  }
+  const std::vector<int32_t> lperm = rcm_order(nc, rp, rc);  // new lateral -> old
+  std::vector<int32_t> lrank(static_cast<size_t>(nc));
+  for (int i = 0; i < nc; ++i) lrank[lperm[i]] = i;
+  // neighbour lists in the new lateral order, ascending
+  std::vector<std::vector<int32_t>> nbl(nc);
+  int jmax = 0;
+  for (int i = 0; i < nc; ++i) {
+    for (int32_t q : ring[lperm[i]]) nbl[i].push_back(lrank[q]);
+    std::sort(nbl[i].begin(), nbl[i].end());
+    jmax = std::max(jmax, int(nbl[i].size()));
+  }
+  // rows: r = l * nc + i
+  std::vector<int32_t> perm(static_cast<size_t>(n)), iperm(static_cast<size_t>(n));
+  for (int l = 0; l < nl; ++l)
+    for (int i = 0; i < nc; ++i) {
+      const int r = l * nc + i;
+      perm[r] = dof_at[size_t(l) * nc + lperm[i]];
+      iperm[perm[r]] = r;
+    }
+  const int n_sl = (n + 63) / 64;
+  std::vector<int64_t> off(size_t(n_sl) + 1, 0);
+  for (int sl = 0; sl < n_sl; ++sl) {
+    int w = 0;
+    for (int r = 64 * sl; r < std::min(n, 64 * sl + 64); ++r)
+      w = std::max(w, 5 * int(nbl[r % nc].size()));
+    w += w & 1;
+    off[sl + 1] = off[sl] + 64 * int64_t(w);
+  }
+  const size_t len = size_t(off[n_sl]);
+  if (len >= size_t(INT32_MAX)) return false;
+  std::vector<int32_t> pmap(size_t(Sp[n]), -1);
+  for (int p = 0; p < n; ++p) {
+    const int r = iperm[p], l = r / nc, i = r - l * nc;
+    const std::vector<int32_t>& nb = nbl[i];
+    for (int k = Sp[p]; k < Sp[p + 1]; ++k) {
+      const int rq = iperm[Sc[k]], lq = rq / nc, iq = rq - lq * nc;
+      const auto it = std::lower_bound(nb.begin(), nb.end(), iq);
+      if (it == nb.end() || *it != iq) return false;
+      pmap[k] = int32_t(sell_pos(off.data(), r, 5 * int(it - nb.begin()) + (lq - l + 2)));
+    }
+  }
+  std::vector<int32_t> tab(size_t(std::max(jmax, 1)) * nc);
+  for (int j = 0; j < jmax; ++j)
+    for (int i = 0; i < nc; ++i)
+      tab[size_t(j) * nc + i] = j < int(nbl[i].size()) ? nbl[i][j] : i;
+  c.S_sell_off.upload(off);
+  c.S_sell_col.release();
+  c.S_sell_c16.release();
+  c.S_sell_base.release();
+  c.S_nbr.upload(tab);
+  c.S_nc = nc;
+  c.S_nl = nl;
+  c.S_pmap.upload(pmap);
+  c.S_perm.upload(perm);
+  c.S_val.alloc(len);
+  c.S_val.zero(c.stream);  // entries outside the pattern stay 0
+  c.mp.reset();
+  c.sell_part_len = sell_fused_blocks(n);
+  c.sperm_x.alloc(size_t(n));
+  c.sperm_b.alloc(size_t(n));
+  return true;
 }
 
 }  // namespace
@@ -1593,7 +1751,8 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
     c.T_col.upload(Tc);
     c.S_ptr.upload(h.Sp);
     c.S_col.upload(h.Sc);
-    build_sell(c, h.Sp, h.Sc, !dist);
+    if (dist || !build_sell_structured(c, h.Sp, h.Sc, pd, h.geo, n_cells))
+      build_sell(c, h.Sp, h.Sc, !dist);
     c.S_max_row = h.S_max_row;
     c.A_val.release();  // allocated on first use (ensure_A_val)
     c.A_nnzb = Ac.size();
@@ -2807,7 +2966,7 @@ int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permute
   return guarded(ctx, [&] {
     need_ready(*ctx);
     const Ctx& c = *ctx;
-    if (col_bytes) *col_bytes = c.S_sell_c16.p ? 2 : 4;
+    if (col_bytes) *col_bytes = c.S_nbr.p ? 0 : c.S_sell_c16.p ? 2 : 4;
     if (stored) *stored = int64_t(c.S_val.n);
     if (permuted) *permuted = c.S_perm.p != nullptr;
     return DCP_OK;

@@ -198,8 +198,17 @@ struct Ctx {
   DBuf<int32_t> S_pmap;              // CSR entry of S -> SELL position
   DBuf<int32_t> S_perm;              // SELL row r = pressure dof S_perm[r] (null: identity)
   DBuf<double> sperm_x, sperm_b;     // permuted-order work vectors
+  // structured columns (SellView::nbr): lateral neighbour table [j][nc]
+  DBuf<int32_t> S_nbr;
+  int S_nc = 0, S_nl = 0;
   SellView sell() const {
-    return SellView{npo, S_sell_off.p, S_sell_col.p, S_sell_c16.p, S_sell_base.p, S_val.p};
+    SellView v{npo, S_sell_off.p, S_sell_col.p, S_sell_c16.p, S_sell_base.p, S_val.p};
+    if (S_nbr.p) {
+      v.nbr = S_nbr.p;
+      v.nc = S_nc;
+      v.nl = S_nl;
+    }
+    return v;
   }
   DBuf<double> S_val;
   long S_version = 0;                // formations of S_val (matrix powers: ghost values current?)

@@ -341,6 +341,12 @@ struct SellView {
   const int32_t* base;
   const double* val;
   const int32_t* rowmap = nullptr;  // row -> vector entry (null: the row itself)
+  // structured columns (one GPU, radially layered shell; col / col16 null):
+  // row r = level l * nc + lateral c (r = l nc + c), entry k = 5 j + d of a row
+  // is column (l + d - 2) nc + nbr[j nc + c] (levels outside [0, nl) and
+  // entries past the row's own neighbour count hold value 0)
+  const int32_t* nbr = nullptr;
+  int nc = 0, nl = 0;
 };
 void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s);
 // y = (S x - theta x) * sscale (the s-step Newton basis); every launch returns

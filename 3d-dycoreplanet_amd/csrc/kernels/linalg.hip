@@ -336,7 +336,20 @@ __device__ inline double2 sell_ld(const double2* p) {
   return *p;
 }
 #define SELL_LD(p) sell_ld(p)
-template <bool EPI, bool C16>
+// CM: column mode, 0 = 32-bit columns, 1 = 16-bit offsets, 2 = structured
+// (SellView::nbr: only values stream from HBM, the column of entry k = 5 j + d
+// comes from the level of the row and the L2-resident neighbour table)
+struct SlotPos {  // entry k = 5 j + d of a structured row
+  int j, d;
+  __device__ void step(int n) {  // k += n, 0 < n <= 10
+    d += n;
+    while (d >= 5) {
+      d -= 5;
+      ++j;
+    }
+  }
+};
+template <bool EPI, int CM>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* __restrict__ x,
                                                       double cf, double* xs,
                                                       double* __restrict__ y,
@@ -368,7 +381,51 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
   const double2* vp = reinterpret_cast<const double2*>(m.val + b) + 64 * wave + lane;
   double acc = 0.0;
   int k = wave;
-  if (C16) {
+  if (CM == 2) {
+    const int nc = m.nc, nl = m.nl;
+    const long rr = row < rows ? row : rows - 1;  // lanes past the end: any valid row
+    const int l = int(rr / nc), cc = int(rr - long(l) * nc);
+    const int32_t* nb = m.nbr + cc;
+    auto xat = [&](SlotPos p) {
+      int lv = l + p.d - 2;
+      lv = lv < 0 ? 0 : (lv >= nl ? nl - 1 : lv);  // value 0 there: any finite x
+      return x[lv * nc + nb[p.j * nc]] * cf;
+    };
+    SlotPos p0{0, 2 * k};
+    p0.step(0);
+    for (; k + 12 < np; k += 16, vp += 1024) {
+      // pairs k, k + 4, k + 8, k + 12: slots 2k .. 2k + 1 and 8, 16, 24 on
+      SlotPos q[8];
+      q[0] = p0;
+#pragma unroll
+      for (int i = 1; i < 8; ++i) {
+        q[i] = q[i - 1];
+        q[i].step((i & 1) ? 1 : 7);
+      }
+      const double2 a0 = SELL_LD(vp), a1 = SELL_LD(vp + 256), a2 = SELL_LD(vp + 512),
+                    a3 = SELL_LD(vp + 768);
+      const double x0 = xat(q[0]), x1 = xat(q[1]), x2 = xat(q[2]), x3 = xat(q[3]);
+      const double x4 = xat(q[4]), x5 = xat(q[5]), x6 = xat(q[6]), x7 = xat(q[7]);
+      acc += a0.x * x0;
+      acc += a0.y * x1;
+      acc += a1.x * x2;
+      acc += a1.y * x3;
+      acc += a2.x * x4;
+      acc += a2.y * x5;
+      acc += a3.x * x6;
+      acc += a3.y * x7;
+      p0 = q[7];
+      p0.step(7);
+    }
+    for (; k < np; k += 4, vp += 256) {
+      SlotPos p1 = p0;
+      p1.step(1);
+      const double2 a0 = SELL_LD(vp);
+      acc += a0.x * xat(p0);
+      acc += a0.y * xat(p1);
+      p0.step(8);
+    }
+  } else if (CM == 1) {
     const int cb = m.base[sl];
     const ushort2* cp = reinterpret_cast<const ushort2*>(m.col16 + b) + 64 * wave + lane;
     for (; k + 12 < np; k += 16, cp += 1024, vp += 1024) {
@@ -792,15 +849,20 @@ void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, 
 
 int sell_fused_blocks(int rows) { return int((long(rows) + 63) / 64); }
 
+namespace {
+// the instantiation for the view's column mode
+template <bool EPI>
+decltype(&k_sell_spmv<EPI, 0>) sell_kernel(const SellView& m) {
+  if (m.nbr) return k_sell_spmv<EPI, 2>;
+  return m.col16 ? k_sell_spmv<EPI, 1> : k_sell_spmv<EPI, 0>;
+}
+}  // namespace
+
 void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s) {
   if (m.rows <= 0) return;
   const dim3 grid(sell_fused_blocks(m.rows));
-  if (m.col16)
-    hipLaunchKernelGGL((k_sell_spmv<false, true>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL((k_sell_spmv<false, false>), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(sell_kernel<false>(m), grid, dim3(kBlock), 0, s, m, x, cf, nullptr, y, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, 0.0, 1.0, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -808,12 +870,8 @@ void sell_spmv_fused(const SellView& m, const double* x, double cf, double* xs, 
                      const double* v0, double* part0, double* part1, int n_part, hipStream_t s) {
   const int nb = std::max(sell_fused_blocks(m.rows), n_part);
   if (nb <= 0) return;
-  if (m.col16)
-    hipLaunchKernelGGL((k_sell_spmv<true, true>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL((k_sell_spmv<true, false>), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y,
-                       v0, part0, part1, nullptr, nullptr);
+  hipLaunchKernelGGL(sell_kernel<true>(m), dim3(nb), dim3(kBlock), 0, s, m, x, cf, xs, y, v0,
+                     part0, part1, nullptr, nullptr, 0.0, 1.0, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -821,12 +879,8 @@ void sell_spmv_step(const SellView& m, const double* x, const double* cf_dev, do
                     double* y, const int* status, hipStream_t s) {
   if (m.rows <= 0) return;
   const dim3 grid(sell_fused_blocks(m.rows));
-  if (m.col16)
-    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
-                       nullptr, nullptr, nullptr, cf_dev, status);
-  else
-    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y,
-                       nullptr, nullptr, nullptr, cf_dev, status);
+  hipLaunchKernelGGL(sell_kernel<true>(m), grid, dim3(kBlock), 0, s, m, x, 1.0, xs, y, nullptr,
+                     nullptr, nullptr, cf_dev, status, 0.0, 1.0, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -834,12 +888,8 @@ void sell_spmv_shifted(const SellView& m, const double* x, double theta, double 
                        const int* status, hipStream_t s) {
   if (m.rows <= 0) return;
   const dim3 grid(sell_fused_blocks(m.rows));
-  if (m.col16)
-    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, status, theta, sscale);
-  else
-    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
-                       nullptr, nullptr, nullptr, nullptr, status, theta, sscale);
+  hipLaunchKernelGGL(sell_kernel<true>(m), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                     nullptr, nullptr, nullptr, nullptr, status, theta, sscale, nullptr);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -847,12 +897,8 @@ void sell_spmv_residual(const SellView& m, const double* x, const double* b, dou
                         double* part, hipStream_t s) {
   if (m.rows <= 0) return;
   const dim3 grid(sell_fused_blocks(m.rows));
-  if (m.col16)
-    hipLaunchKernelGGL((k_sell_spmv<true, true>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
-                       nullptr, nullptr, part, nullptr, nullptr, 0.0, 1.0, b);
-  else
-    hipLaunchKernelGGL((k_sell_spmv<true, false>), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
-                       nullptr, nullptr, part, nullptr, nullptr, 0.0, 1.0, b);
+  hipLaunchKernelGGL(sell_kernel<true>(m), grid, dim3(kBlock), 0, s, m, x, 1.0, nullptr, y,
+                     nullptr, nullptr, part, nullptr, nullptr, 0.0, 1.0, b);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

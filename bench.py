@@ -602,16 +602,19 @@ def main():
     pinfo = ctx.pattern_info()
     if args.schur == "explicit":
         # fused SELL SpMV with the formed S: values + column indices per
-        # nonzero (8 + 2 B with the 16-bit RCM layout, 8 + 4 B otherwise),
-        # slice offsets (+ column bases), gathered x, y write, scaled-basis
-        # write xs, v0 read
+        # nonzero (8 + 0 B with structured columns -- level-major rows, column
+        # from the row's level and the L2-resident lateral neighbour table,
+        # DESIGN section 10 --, 8 + 2 B with the 16-bit RCM layout, 8 + 4 B
+        # otherwise), slice offsets (+ column bases), gathered x, y write,
+        # scaled-basis write xs, v0 read
         lay = ctx.schur_layout()
         n_sl = (m.n_p + 63) // 64
         cb = lay["col_bytes"]
         sbytes = (8 + cb) * pinfo["nnz_S"] + 8 * (n_sl + 1) + (4 * n_sl if cb == 2 else 0) \
             + 32 * m.n_p
         kernel = ("explicit Schur complement SpMV S x, SELL-64 fused (k_sell_spmv<true>"
-                  + (", 16-bit columns, RCM order)" if cb == 2 else ")"))
+                  + {0: ", structured columns, level-major order)",
+                     2: ", 16-bit columns, RCM order)"}.get(cb, ")"))
     else:
         sbytes = schur_bytes(m, pinfo["nnzb_Bt"], pinfo["nnzb_B"])
         kernel = "Schur complement apply B D_A^-1 B^T (3 kernels)"

@@ -407,8 +407,11 @@ int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* n
                      int64_t* nnz_T, int64_t* nnz_S);
 
 /* Storage of the explicit Schur complement (SELL-64): bytes per column index
- * (2: 16-bit offsets from a slice base, 4: int32), stored entries incl.
- * padding, whether rows/columns are in reverse Cuthill-McKee order. */
+ * (0: structured columns formed from the row's radial level and a lateral
+ * neighbour table, one GPU on the layered shell; 2: 16-bit offsets from a
+ * slice base; 4: int32), stored entries incl. padding, whether rows/columns
+ * are permuted (level-major with structured columns, else reverse
+ * Cuthill-McKee). */
 int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted);
 
 /* Communicator self-test (no mesh needed): the solver's forward halo (gather
