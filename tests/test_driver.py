@@ -110,7 +110,6 @@ def test_executable_writes_vtu_output(tmp_path):
     assert 'Source="aqua-00001.0000.vtu"' in (tmp_path / "aqua-00001.pvtu").read_text()
 
 
-@pytest.mark.gpu
 def _calls(ctx, name):
     """Calls of a TimerOutput section; 0 for a section never entered (the
     library knows only sections that ran)."""
@@ -120,6 +119,7 @@ def _calls(ctx, name):
         return 0
 
 
+@pytest.mark.gpu
 def test_solver_history_and_timer_sections():
     """§5 auxiliaries: SolverControl(..., log_history = true, log_result = true)
     of the FGMRES solve (boussinesq_model.tpp:1166-1169) and the TimerOutput
