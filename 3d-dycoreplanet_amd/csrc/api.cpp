@@ -1243,10 +1243,27 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
       pmap[k] = int32_t(sell_pos(off.data(), r, 5 * int(it - nb.begin()) + (lq - l + 2)));
     }
   }
-  std::vector<int32_t> tab(size_t(std::max(jmax, 1)) * nc);
-  for (int j = 0; j < jmax; ++j)
+  // jmax + 1 rows: an odd 5 J rounds the slice width up by one entry, whose
+  // j is J (value 0, the row's own lateral)
+  const int jrows = jmax + 1;
+  std::vector<int32_t> tab(size_t(jrows) * nc);
+  for (int j = 0; j < jrows; ++j)
     for (int i = 0; i < nc; ++i)
       tab[size_t(j) * nc + i] = j < int(nbl[i].size()) ? nbl[i][j] : i;
+  // every column the kernel forms (k_sell_spmv<.., 2>, lanes past the last
+  // row as the last row) must index the vector
+  for (int sl = 0; sl < n_sl; ++sl) {
+    const int w = int((off[sl + 1] - off[sl]) / 64);
+    if ((w - 1) / 5 >= jrows) return false;
+    for (int i = 0; i < 64; ++i) {
+      const int r = std::min(64 * sl + i, n - 1), l = r / nc, cc = r - l * nc;
+      for (int k = 0; k < w; ++k) {
+        const int lv = std::min(std::max(l + k % 5 - 2, 0), nl - 1);
+        const int64_t col = int64_t(lv) * nc + tab[size_t(k / 5) * nc + cc];
+        if (col < 0 || col >= n) return false;
+      }
+    }
+  }
   c.S_sell_off.upload(off);
   c.S_sell_col.release();
   c.S_sell_c16.release();
