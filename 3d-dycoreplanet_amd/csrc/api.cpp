@@ -1115,10 +1115,11 @@ void build_sell(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_
 // products of a lateral quad and a radial interval, so the coupling through a
 // shared velocity node factors): the pattern of row (l, c) is {l-2..l+2} x N(c).
 // Rows are ordered level-major, laterals in reverse Cuthill-McKee order of the
-// two-ring graph; entry k = 5 j + d of row (l, c) is column (l + d - 2, N(c)_j).
-// The kernel then streams the values only (8 instead of 10 bytes per entry,
-// plus 5 / 159 zero entries at the boundary levels at refine 5) and forms the
-// column from the row's level and the L2-resident neighbour table. Returns
+// two-ring graph; with nd the levels of [l - 2, l + 2] inside the mesh from
+// l + dlo on, entry k = nd j + d of row (l, c) is column (l + dlo + d, N(c)_j).
+// The kernel then streams the values only (8 instead of 10 bytes per entry)
+// and forms the column from the row's level and the L2-resident neighbour
+// table. Returns
 // false (and changes nothing) unless every check holds; DCP_S_STRUCT=0 turns
 // it off.
 bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::vector<int32_t>& Sc,
@@ -1221,12 +1222,17 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
       perm[r] = dof_at[size_t(l) * nc + lperm[i]];
       iperm[perm[r]] = r;
     }
+  // levels in reach of level l: l + dlo .. l + dlo + nd - 1 (as the kernel)
+  auto reach = [&](int l, int& dlo) {
+    dlo = l < 2 ? -l : -2;
+    return std::min(l + 2, nl - 1) - (l + dlo) + 1;
+  };
   const int n_sl = (n + 63) / 64;
   std::vector<int64_t> off(size_t(n_sl) + 1, 0);
   for (int sl = 0; sl < n_sl; ++sl) {
-    int w = 0;
+    int w = 0, dlo;
     for (int r = 64 * sl; r < std::min(n, 64 * sl + 64); ++r)
-      w = std::max(w, 5 * int(nbl[r % nc].size()));
+      w = std::max(w, reach(r / nc, dlo) * int(nbl[r % nc].size()));
     w += w & 1;
     off[sl + 1] = off[sl] + 64 * int64_t(w);
   }
@@ -1240,11 +1246,14 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
       const int rq = iperm[Sc[k]], lq = rq / nc, iq = rq - lq * nc;
       const auto it = std::lower_bound(nb.begin(), nb.end(), iq);
       if (it == nb.end() || *it != iq) return false;
-      pmap[k] = int32_t(sell_pos(off.data(), r, 5 * int(it - nb.begin()) + (lq - l + 2)));
+      int dlo;
+      const int nd = reach(l, dlo);
+      pmap[k] = int32_t(sell_pos(off.data(), r, nd * int(it - nb.begin()) + (lq - l - dlo)));
     }
   }
-  // jmax + 1 rows: an odd 5 J rounds the slice width up by one entry, whose
-  // j is J (value 0, the row's own lateral)
+  // jmax + 1 rows, the last one the lateral itself: the kernel reads padding
+  // entries (value 0; a narrower row of the slice, or the even round-up)
+  // through row min(j, jmax)
   const int jrows = jmax + 1;
   std::vector<int32_t> tab(size_t(jrows) * nc);
   for (int j = 0; j < jrows; ++j)
@@ -1254,13 +1263,14 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
   // row as the last row) must index the vector
   for (int sl = 0; sl < n_sl; ++sl) {
     const int w = int((off[sl + 1] - off[sl]) / 64);
-    if ((w - 1) / 5 >= jrows) return false;
     for (int i = 0; i < 64; ++i) {
       const int r = std::min(64 * sl + i, n - 1), l = r / nc, cc = r - l * nc;
+      int dlo;
+      const int nd = reach(l, dlo);
       for (int k = 0; k < w; ++k) {
-        const int lv = std::min(std::max(l + k % 5 - 2, 0), nl - 1);
-        const int64_t col = int64_t(lv) * nc + tab[size_t(k / 5) * nc + cc];
-        if (col < 0 || col >= n) return false;
+        const int lv = l + dlo + k % nd;
+        const int64_t col = int64_t(lv) * nc + tab[size_t(std::min(k / nd, jmax)) * nc + cc];
+        if (lv < 0 || lv >= nl || col < 0 || col >= n) return false;
       }
     }
   }
@@ -1271,6 +1281,7 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
   c.S_nbr.upload(tab);
   c.S_nc = nc;
   c.S_nl = nl;
+  c.S_nj = jrows;
   c.S_pmap.upload(pmap);
   c.S_perm.upload(perm);
   c.S_val.alloc(len);

@@ -200,13 +200,14 @@ struct Ctx {
   DBuf<double> sperm_x, sperm_b;     // permuted-order work vectors
   // structured columns (SellView::nbr): lateral neighbour table [j][nc]
   DBuf<int32_t> S_nbr;
-  int S_nc = 0, S_nl = 0;
+  int S_nc = 0, S_nl = 0, S_nj = 0;
   SellView sell() const {
     SellView v{npo, S_sell_off.p, S_sell_col.p, S_sell_c16.p, S_sell_base.p, S_val.p};
     if (S_nbr.p) {
       v.nbr = S_nbr.p;
       v.nc = S_nc;
       v.nl = S_nl;
+      v.nj = S_nj;
     }
     return v;
   }

@@ -342,11 +342,12 @@ struct SellView {
   const double* val;
   const int32_t* rowmap = nullptr;  // row -> vector entry (null: the row itself)
   // structured columns (one GPU, radially layered shell; col / col16 null):
-  // row r = level l * nc + lateral c (r = l nc + c), entry k = 5 j + d of a row
-  // is column (l + d - 2) nc + nbr[j nc + c] (levels outside [0, nl) and
-  // entries past the row's own neighbour count hold value 0)
+  // row r = level l * nc + lateral c, with nd = the levels of [l - 2, l + 2]
+  // inside [0, nl) from l + dlo on, entry k = nd j + d of the row is column
+  // (l + dlo + d) nc + nbr[min(j, nj - 1) nc + c] (entries past the row's own
+  // neighbour count hold value 0; table row nj - 1 is the lateral itself)
   const int32_t* nbr = nullptr;
-  int nc = 0, nl = 0;
+  int nc = 0, nl = 0, nj = 0;
 };
 void sell_spmv(const SellView& m, const double* x, double cf, double* y, hipStream_t s);
 // y = (S x - theta x) * sscale (the s-step Newton basis); every launch returns

@@ -337,14 +337,14 @@ __device__ inline double2 sell_ld(const double2* p) {
 }
 #define SELL_LD(p) sell_ld(p)
 // CM: column mode, 0 = 32-bit columns, 1 = 16-bit offsets, 2 = structured
-// (SellView::nbr: only values stream from HBM, the column of entry k = 5 j + d
+// (SellView::nbr: only values stream from HBM, the column of entry k = nd j + d
 // comes from the level of the row and the L2-resident neighbour table)
-struct SlotPos {  // entry k = 5 j + d of a structured row
-  int j, d;
-  __device__ void step(int n) {  // k += n, 0 < n <= 10
+struct SlotPos {  // entry k = nd j + d of a structured row (nd levels in reach)
+  int j, d, nd;
+  __device__ void step(int n) {  // k += n, 0 <= n <= 8
     d += n;
-    while (d >= 5) {
-      d -= 5;
+    while (d >= nd) {
+      d -= nd;
       ++j;
     }
   }
@@ -385,13 +385,15 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(SellView m, const double* 
     const int nc = m.nc, nl = m.nl;
     const long rr = row < rows ? row : rows - 1;  // lanes past the end: any valid row
     const int l = int(rr / nc), cc = int(rr - long(l) * nc);
+    // levels l + dlo .. l + dlo + nd - 1 within [l - 2, l + 2] and the mesh
+    const int dlo = l < 2 ? -l : -2;
+    const int nd = min(l + 2, nl - 1) - (l + dlo) + 1;
     const int32_t* nb = m.nbr + cc;
+    const int jlast = m.nj - 1;  // padding entries (value 0): the spare row, own lateral
     auto xat = [&](SlotPos p) {
-      int lv = l + p.d - 2;
-      lv = lv < 0 ? 0 : (lv >= nl ? nl - 1 : lv);  // value 0 there: any finite x
-      return x[lv * nc + nb[p.j * nc]] * cf;
+      return x[(l + dlo + p.d) * nc + nb[min(p.j, jlast) * nc]] * cf;
     };
-    SlotPos p0{0, 2 * k};
+    SlotPos p0{0, 2 * k, nd};
     p0.step(0);
     for (; k + 12 < np; k += 16, vp += 1024) {
       // pairs k, k + 4, k + 8, k + 12: slots 2k .. 2k + 1 and 8, 16, 24 on
