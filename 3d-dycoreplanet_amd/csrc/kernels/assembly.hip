@@ -1954,6 +1954,14 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
 // record}; slot record: {column-table entry, layer << 16 | lex << 8 | row in
 // task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
+// DCP_BT_TPW tasks per wave, one after the other, the next task's header and
+// slot record in flight while the current one is evaluated (the chain header
+// -> record -> tables is three dependent loads)
+#ifndef DCP_BT_TPW
+#define DCP_BT_TPW 1
+#endif
+constexpr int kBtTpw = DCP_BT_TPW;
+__host__ __device__ constexpr int bt_task_waves(int n_tasks) { return (n_tasks + kBtTpw - 1) / kBtTpw; }
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
     const double* __restrict__ P, double* __restrict__ Bt) {
@@ -1961,40 +1969,58 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
   __shared__ int dst_e[kBtRowWaves][64];
   __shared__ int rowl[kBtRowWaves][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int task = int(blockIdx.x) * kBtRowWaves + wave;
-  if (task >= n_tasks) return;
-  const int4 h = hdr[task];
-  const int ns = h.z & 255, ne = h.z >> 8;
+  const int t0 = (int(blockIdx.x) * kBtRowWaves + wave) * kBtTpw;
+  if (t0 >= n_tasks) return;
   const int k = lane >> 3, v = lane & 7;
-  int de = -1;
-  if (k < ns) {
-    const int4 r = rec[h.w + k];
-    const unsigned long long dm = (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
-    de = int((dm >> (6 * v)) & 63);
-    double e[3];
-    bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
-    vals[wave][3 * lane] = e[0];
-    vals[wave][3 * lane + 1] = e[1];
-    vals[wave][3 * lane + 2] = e[2];
-    rowl[wave][lane] = r.y & 255;
-  }
-  dst_e[wave][lane] = de;
-  wsync();
-  if (lane >= ne) return;
-  double acc[3] = {0.0, 0.0, 0.0};
-  int rl = 0;
-  for (int e = 0; e < 8 * ns; ++e)
-    if (dst_e[wave][e] == lane) {
-      acc[0] += vals[wave][3 * e];
-      acc[1] += vals[wave][3 * e + 1];
-      acc[2] += vals[wave][3 * e + 2];
-      rl = rowl[wave][e];
+  auto load_rec = [&](const int4& h) {
+    return k < (h.z & 255) ? rec[h.w + k] : make_int4(0, 0, 0, 0);
+  };
+  int4 h = hdr[t0];
+  int4 r = load_rec(h);
+  for (int i = 0; i < kBtTpw; ++i) {
+    const int task = t0 + i;
+    if (task >= n_tasks) break;  // uniform per wave
+    int4 hn = h, rn = r;
+    if (kBtTpw > 1 && i + 1 < kBtTpw && task + 1 < n_tasks) {
+      hn = hdr[task + 1];
+      rn = load_rec(hn);
     }
-  double Ca[3][3];
-  condensation(cd.vcon[h.y + rl], Ca);
-  double* dst = Bt + 3 * size_t(h.x + lane);
+    const int ns = h.z & 255, ne = h.z >> 8;
+    int de = -1;
+    if (k < ns) {
+      const unsigned long long dm =
+          (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
+      de = int((dm >> (6 * v)) & 63);
+      double e[3];
+      bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
+      vals[wave][3 * lane] = e[0];
+      vals[wave][3 * lane + 1] = e[1];
+      vals[wave][3 * lane + 2] = e[2];
+      rowl[wave][lane] = r.y & 255;
+    }
+    dst_e[wave][lane] = de;
+    wsync();
+    if (lane < ne) {
+      double acc[3] = {0.0, 0.0, 0.0};
+      int rl = 0;
+      for (int e = 0; e < 8 * ns; ++e)
+        if (dst_e[wave][e] == lane) {
+          acc[0] += vals[wave][3 * e];
+          acc[1] += vals[wave][3 * e + 1];
+          acc[2] += vals[wave][3 * e + 2];
+          rl = rowl[wave][e];
+        }
+      double Ca[3][3];
+      condensation(cd.vcon[h.y + rl], Ca);
+      double* dst = Bt + 3 * size_t(h.x + lane);
 #pragma unroll
-  for (int jj = 0; jj < 3; ++jj) dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+      for (int jj = 0; jj < 3; ++jj)
+        dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+    }
+    wsync();  // the next task overwrites this one's LDS
+    h = hn;
+    r = rn;
+  }
 }
 
 // B by pressure rows (several GPUs, where B is not the transpose of the owned
@@ -2202,7 +2228,7 @@ void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, cons
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (n_tasks > 0) {
-    hipLaunchKernelGGL(k_bt_tasks, dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves),
+    hipLaunchKernelGGL(k_bt_tasks, dim3((bt_task_waves(n_tasks) + kBtRowWaves - 1) / kBtRowWaves),
                        dim3(64 * kBtRowWaves), 0, s, cd, n_tasks,
                        reinterpret_cast<const int4*>(task_hdr),
                        reinterpret_cast<const int4*>(slot_rec), P, Bt);

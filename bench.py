@@ -48,14 +48,40 @@ def measured_ceilings():
             "triad_GBps": 1e3 * d["triad_TBps"], "source": CEILING_FILE}
 # rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE summaries (tools/pmc_summary.py) of the
 # roofline kernel, per (refine, schur mode): HBM bytes per launch
-PMC_SUMMARIES = {(5, "explicit"): ("profiles/r03a_pmc_inner_r5.json", "k_sell_spmv<true, true>")}
+PMC_SUMMARIES = {(5, "explicit"): ("profiles/r04j_pmc_inner_r5.json", "k_sell_spmv<true, 2>")}
 # rocprofv3 --kernel-trace --stats of the same workload (durations of the
 # orthogonalisation launches, for their roofline): the CGS2 chain (bench) and
 # the s-step block (inner probe)
 CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
-               (5, "sstep"): "profiles/r03ag_inner_probe_sstep_kernel_stats.csv"}
+               (5, "sstep"): "profiles/r04i_inner_r5_structured_kernel_stats.csv"}
+# the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
+# launches per assembly (the rhs kernel once per colour class)
+PMC_ASM = {5: ("profiles/r04j_pmc_asm_r5.json",
+               {"k_bt_tasks": 1, "k_bt_coltab": 1, "k_nse_rhs_halfwave": 8})}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
-PMC_MF = {5: ("profiles/r02_pmc_mfpencil_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
+PMC_MF = {5: ("profiles/r04j_pmc_mf_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
+
+
+def pmc_asm_traffic(refine):
+    """HBM bytes of one operator-form assembly from the committed PMC summary:
+    FETCH + WRITE as counted, and with the gfx950 2x FETCH correction (which
+    holds for wide coalesced streams; the rhs kernel's node gathers are short
+    reads counted in full, so the truth lies between the two)."""
+    ent = PMC_ASM.get(refine)
+    if ent is None or not os.path.exists(os.path.join(ROOT, ent[0])):
+        return None
+    with open(os.path.join(ROOT, ent[0])) as f:
+        ctr = json.load(f)["counters"]
+    fetch = write = 0.0
+    for key, launches in ent[1].items():
+        fk = [v["mean_kB"] for k, v in ctr["FETCH_SIZE"].items() if key in k]
+        wk = [v["mean_kB"] for k, v in ctr["WRITE_SIZE"].items() if key in k]
+        if not fk or not wk:
+            return None
+        fetch += launches * fk[0] * 1e3
+        write += launches * wk[0] * 1e3
+    return {"fetch_plus_write": fetch + write, "two_fetch_plus_write": 2 * fetch + write,
+            "write": write, "source": ent[0]}
 
 
 def pmc_mf_traffic(refine):
@@ -695,7 +721,8 @@ def main():
                   "constrained diagonal k_nse_rhs_halfwave per colour)",
         "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
-        "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None}
+        "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None,
+        "traffic": pmc_asm_traffic(args.refine) if world == 1 else None}
     if args.schur == "explicit" and world == 1:
         out["roofline_chain"] = chain_roofline(args.refine, m.n_p, args.gram_schmidt)
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):

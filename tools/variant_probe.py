@@ -12,6 +12,7 @@ import dcp  # noqa: E402
 
 R = int(os.environ.get("R", "5"))
 m = dcp.HostMesh(refine=R)
+ref = None
 for path in sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/var/libdcp_*.so"))):
     dcp._lib = dcp.load_library(path)
     ctx = dcp.Context(device=0)
@@ -25,6 +26,12 @@ for path in sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/
     for _ in range(6):
         ctx.assemble_nse_system()
         ms.append(ctx.timings()["assemble_nse_ms"])
+    # B^T and the rhs bitwise against the first variant
+    bt = ctx.coupling_csr("Bt")[2]
+    rhs = ctx.get_state(dcp.NSE_RHS)
+    if ref is None:
+        ref = (bt, rhs)
+    same = bool(np.array_equal(bt, ref[0]) and np.array_equal(rhs, ref[1]))
     ctx.close()
     print(json.dumps({"variant": os.path.basename(path), "ms_median": float(np.median(ms[1:])),
-                      "ms": ms}), flush=True)
+                      "ms": ms, "bitwise_first_variant": same}), flush=True)
