@@ -2071,7 +2071,9 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
         // B^T by tasks of rows (k_bt_tasks) on the separable shell: per velocity
         // node row its cells in colour order (cell << 5 | lexicographic position)
         c.bt_rows = false;
+        c.rhs_cell_order = false;
         const char* env = std::getenv("DCP_BT_ROWS");
+        const char* env_rhs = std::getenv("DCP_ASM_RHS_CELL_ORDER");
         if (c.mf_separable && !c.periodic && !(env && *env == '0') && n_cells < (1 << 26)) {
           const int nrows = int(Btp.size()) - 1;
           std::vector<int32_t> rp(size_t(nrows) + 1, 0);
@@ -2159,6 +2161,27 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                 c.rhs_color_ptr.push_back(int(sub.size()));
               }
               c.rhs_color_cells.upload(sub);
+            }
+            // the rhs in cell order (mf_rhs_cells + the velocity gather) with
+            // FE_Q(1) temperature; the cell kernel then only forms the
+            // constrained-row diagonals, on the cells with a constrained node
+            // (and an owned node, several GPUs)
+            c.con_color_ptr.clear();
+            c.con_color_cells.release();
+            c.rhs_cell_order = h.tdpc == 8 && !(env_rhs && *env_rhs == '0');
+            if (c.rhs_cell_order) {
+              std::vector<int32_t> sub;
+              c.con_color_ptr.assign(1, 0);
+              for (size_t k = 0; k + 1 < h.color_ptr.size(); ++k) {
+                for (int e = h.color_ptr[k]; e < h.color_ptr[k + 1]; ++e) {
+                  const int cell = ccells[size_t(e)];
+                  bool own = false;
+                  for (int t = 0; t < 27 && !own; ++t) own = q2[27 * size_t(cell) + t] < nrows;
+                  if (cmask[size_t(cell)] != 0 && own) sub.push_back(cell);
+                }
+                c.con_color_ptr.push_back(int(sub.size()));
+              }
+              c.con_color_cells.upload(sub);
             }
             c.bt_ncols = int(c.mf_colgeo.n / 90);
             c.bt_P.alloc(size_t(216) * c.bt_ncols);
@@ -2450,9 +2473,16 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       out.pcdiag = c.con_diag.p + 3 * size_t(c.n_con);
       out.pcidx = c.periodic ? c.pcidx.p : nullptr;
     }
+    // the rhs in cell order (operator form on the separable shell, FE_Q(1)
+    // temperature): the pencil kernel + the velocity gather write every
+    // velocity entry; the cell kernel forms only the constrained diagonals
+    const bool rhs_co = (flags & DCP_ASSEMBLE_RHS) && c.bt_rows && c.rhs_cell_order && !full;
     if (flags & DCP_ASSEMBLE_RHS) {
-      c.nse_rhs.zero(c.stream);
-      out.rhs = c.nse_rhs.p;
+      if (rhs_co)
+        fill(c.n_p, 0.0, c.nse_rhs.p + c.n_u, c.stream);  // B rows: no rhs
+      else
+        c.nse_rhs.zero(c.stream);
+      out.rhs = rhs_co ? nullptr : c.nse_rhs.p;
     }
     // ghosted old solutions (the reference reads the ghosted vectors, :583-589,
     // which its time loop imported at old = new): exchanged here only if the
@@ -2460,8 +2490,12 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     const bool rhs_subset = bt_rows && !c.rhs_color_ptr.empty();
-    for (int k = 0; k < c.n_colors(); ++k) {
-      if (full)
+    for (int k = 0; k < c.n_colors() && !(rhs_co && !out.cdiag); ++k) {
+      if (rhs_co)  // the constrained-row diagonals only
+        launch_nse_operator(c.cd(), c.maps(), c.con_color_cells.p + c.con_color_ptr[k],
+                            c.con_color_ptr[k + 1] - c.con_color_ptr[k], c.old_nse.p, c.old_T.p,
+                            c.ph, out, c.stream);
+      else if (full)
         launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                           c.old_T.p, c.ph, out, c.stream, c.element_mfma);
       else if (rhs_subset)
@@ -2471,6 +2505,16 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       else
         launch_nse_operator(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                             c.old_T.p, c.ph, out, c.stream);
+    }
+    if (rhs_co) {
+      const MfCells mc = c.mfc();
+      for (int k = 0; k < c.mf_chunks; ++k)
+        mf_rhs_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.old_nse.p, c.old_T.p, c.ph,
+                     c.mf_buf.p, c.stream);
+      MfGather g = c.mfg();
+      g.cdiag = nullptr;  // condensation only
+      g.pcidx = nullptr;
+      mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
     if (bt_rows)
       launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, c.bt_ntasks, c.bt_task_hdr.p, c.bt_slot_rec.p,

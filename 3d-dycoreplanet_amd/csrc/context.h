@@ -136,6 +136,11 @@ struct Ctx {
   // several GPUs: per colour the cells with an owned velocity node (the rhs)
   std::vector<int> rhs_color_ptr;
   DBuf<int32_t> rhs_color_cells;
+  // the rhs in cell order (mf_rhs_cells + gather, DCP_ASM_RHS_CELL_ORDER=0 off):
+  // per colour the cells with a constrained node, for the constrained diagonals
+  bool rhs_cell_order = false;
+  std::vector<int> con_color_ptr;
+  DBuf<int32_t> con_color_cells;
   DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
   DBuf<double> bt_P;  // [n_cols][216] column factors, formed every assembly
   int bt_ncols = 0;
@@ -270,7 +275,7 @@ struct Ctx {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
                    mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p, mf_vnext.p,
                    mf_pslot.p, mf_separable ? mf_col.p : nullptr,
-                   mf_colgeo.p, mf_layer.p, mf_laygeo.p};
+                   mf_colgeo.p, mf_layer.p, mf_laygeo.p, cell_T.p, mf_colphi.p, mf_layR.p};
   }
   MfGather mfg() const {
     // one chunk: the gather order is the identity (no order arrays read)

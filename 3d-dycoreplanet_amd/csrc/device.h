@@ -186,6 +186,12 @@ struct MfCells {
   const double* colgeo;        // [n_cols][9 points q0 + 3 q1][m0 m1 m2 D2] (10)
   const int32_t* layer;        // [n_cells] radial layer of the cell
   const double* laygeo;        // [n_layers][3 points][1/R, 1/R', R^2 R']
+  // the NSE rhs in cell order (mf_rhs): temperature dofs, the lateral
+  // directions Phi at the 9 column points and the layer radii R at the 3
+  // radial points (x = R Phi)
+  const int32_t* cell_T = nullptr;  // [n_cells][8]
+  const double* colphi = nullptr;   // [n_cols][9][3]
+  const double* layR = nullptr;     // [n_layers][3]
 };
 struct MfGather {
   int n_vnodes, n_p, n_u;
@@ -212,6 +218,13 @@ void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const d
               double* buf, hipStream_t s);
 void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, const double* buf,
                const double* src, double* dst, hipStream_t s);
+// The velocity rhs of local_assemble_nse_system (boussinesq_model.tpp:655-669)
+// in cell order (separable shell or cuboid, FE_Q(1) temperature): the pencil
+// kernel with the rhs flux per point into the velocity records of buf (cells
+// [c0, c1), one chunk of the cell-order layout), then mf_gather of the
+// velocity positions with mg.cdiag = null (condensation only) into rhs[0, n_u)
+void mf_rhs_cells(const MfCells& mc, int c0, int c1, const double* u_old, const double* T_old,
+                  const PhysicsDev& ph, double* buf, hipStream_t s);
 // one colour class = positions [base, base + n): dst (+)= C^T K C src
 void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);

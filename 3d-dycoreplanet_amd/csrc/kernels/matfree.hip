@@ -452,14 +452,64 @@ __device__ inline void bwd(const Tab3& T, const double in[3], double out[3]) {
   for (int n = 0; n < 3; ++n) out[n] = T.v[n][0] * in[0] + T.v[n][1] * in[1] + T.v[n][2] * in[2];
 }
 
+// -g R / den(R |Phi|) with den(r) = r for r > 1, else sqrt(r): the gravity
+// x -> -g x / den(|x|) of the reference's rhs at x = R Phi, as a factor of Phi
+// (outside the point loop: the square roots and the division would otherwise
+// be interleaved over the unrolled points, +130 VGPRs)
+__device__ __noinline__ double rhs_gravity(double g, double R, const double rphi[3]) {
+  const double x0 = R * rphi[0], x1 = R * rphi[1], x2 = R * rphi[2];
+  const double r = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
+  return -g * R / (r > 1 ? r : sqrt(r));
+}
+// the NSE rhs flux of one Gauss point (k_mf_pencil<.., RHS>): value u,
+// reference gradients Gh[c][e], J^-1 ji (rows e), JxW wq, temperature Tq,
+// position R Phi (separable shell; cuboid: constant gravity), added to the
+// z-pencil's test sums V[c][k] with the values of the point's 1D functions
+__device__ __forceinline__ void rhs_flux(const PhysicsDev& ph, const double u[3],
+                                         const double Gh[3][3], const double ji[9], double wq,
+                                         double Tq, double gs, const double rphi[3], int q,
+                                         double V[3][3]) {
+  double G[3][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) G[c][d] = Gh[c][0] * ji[d] + Gh[c][1] * ji[3 + d] + Gh[c][2] * ji[6 + d];
+  const double rho = 1 - ph.beta * (Tq - ph.T_ref);
+  double grav[3];
+  if (ph.cuboid) {
+    grav[0] = grav[1] = 0;
+    grav[2] = -ph.g;
+  } else {
+    // -g x / den(|x|) with x = R Phi: gs = -g R / den(R |Phi|) (rhs_gravity)
+    grav[0] = gs * rphi[0];
+    grav[1] = gs * rphi[1];
+    grav[2] = gs * rphi[2];
+  }
+  const double cxu[3] = {-ph.coriolis_z * u[1], ph.coriolis_z * u[0], 0.0};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double adv = u[0] * G[c][0] + u[1] * G[c][1] + u[2] * G[c][2];
+    const double F =
+        (u[c] + ph.dt * rho * (ph.grav_scale * grav[c]) - ph.dt * adv - ph.dt * (2 * cxu[c])) * wq;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) V[c][k] += kTL.v[k][q] * F;
+  }
+}
+
 #ifndef DCP_MF_WAVES_PER_EU
 #define DCP_MF_WAVES_PER_EU 2
 #endif
-template <bool STOKES, bool SEP>
+// RHS: the NSE rhs instead of an operator apply (mf_rhs): src = the old
+// velocity (a full vector: no constraint expansion), T_old its temperature
+// (FE_Q(1), interpolated like the pressure), and per Gauss point the flux
+// F = (u + dt rho g' - dt (u.grad) u - 2 dt Omega x u) JxW of
+// local_assemble_nse_system (boussinesq_model.tpp:655-669) against the test
+// function values only
+template <bool STOKES, bool SEP, bool RHS = false>
 __global__ __launch_bounds__(64 * kPenWaves, DCP_MF_WAVES_PER_EU)
-void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
-                                                             const double* __restrict__ src,
-                                                             double* __restrict__ buf) {
+void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict__ src,
+                 double* __restrict__ buf, const double* __restrict__ T_old, PhysicsDev ph) {
+  static_assert(!(RHS && STOKES), "the rhs pass has no pressure");
   __shared__ double lds[kPenWaves][kPenFields];
   __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
   __shared__ uint8_t nxt[kPenWaves][kPenSlots * 27];  // chain links of the group partial sums
@@ -532,7 +582,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       I.next[a] = mc.vnext[27 * e + 3 * p + a];
     }
     I.mask = mc.cmask[e];
-    I.pdof = (STOKES && p < 8) ? mc.cell_p[8 * e + p] : 0;
+    I.pdof = (STOKES && p < 8) ? mc.cell_p[8 * e + p] : (RHS && p < 8) ? mc.cell_T[8 * e + p] : 0;
     I.pslot = (STOKES && p < 8) ? mc.pslot[8 * e + p] : 0;
   };
   auto load_nodes = [&](const Ids& I, Nodes& N) {
@@ -542,7 +592,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
       for (int d = 0; d < 3; ++d) {
         N.U[a][d] = src[3 * size_t(I.nd[a]) + d];
       }
-    N.pv = (STOKES && p < 8) ? src[mc.n_u + I.pdof] : 0.0;
+    N.pv = (STOKES && p < 8) ? src[mc.n_u + I.pdof] : (RHS && p < 8) ? T_old[I.pdof] : 0.0;
   };
 #ifndef DCP_MF_PREFETCH_NODES
 #define DCP_MF_PREFETCH_NODES 1
@@ -568,8 +618,8 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
   double(&U)[3][3] = Nc.U;
   const int colc = SEP ? mc.col[e] : 0;
   const int layc = SEP ? mc.layer[e] : 0;
-  if (STOKES && p < 8) P[p] = Nc.pv;
-  if (mask) {
+  if ((STOKES || RHS) && p < 8) P[p] = Nc.pv;  // pressure / temperature at the vertices
+  if (mask && !RHS) {
 #pragma unroll
     for (int a = 0; a < 3; ++a)
       if ((mask >> (3 * p + a)) & 1) {
@@ -648,7 +698,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
   }
   // ---- z-pencil: per point flux, accumulated straight into the back z pass
   double Plo = 0.0, Phi = 0.0;
-  if (STOKES) {
+  if (STOKES || RHS) {
     const double xa = sel3(pa, kGaussX[0], kGaussX[1], kGaussX[2]);
     const double xb = sel3(pb, kGaussX[0], kGaussX[1], kGaussX[2]);
     Plo = (1.0 - xb) * ((1.0 - xa) * P[0] + xa * P[1]) + xb * ((1.0 - xa) * P[2] + xa * P[3]);
@@ -660,6 +710,14 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
     for (int k = 0; k < 3; ++k) V[c][k] = FX[c][k] = FY[c][k] = 0.0;
   double slo = 0.0, shi = 0.0;
+  // RHS: Phi of the lane's column point, the gravity factor per point
+  double rphi[3] = {0, 0, 0}, rR[3] = {0, 0, 0};
+  if (RHS && SEP && !ph.cuboid) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) rphi[d] = mc.colphi[27 * size_t(colc) + 3 * p + d];
+#pragma unroll 1
+    for (int q = 0; q < 3; ++q) rR[q] = rhs_gravity(ph.g, mc.layR[3 * size_t(layc) + q], rphi);
+  }
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     double u[3], Gh[3][3];
@@ -693,6 +751,10 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
       for (int i = 0; i < 9; ++i) ji[i] = Ji[q][i];
       wq = w[q];
+    }
+    if (RHS) {
+      rhs_flux(ph, u, Gh, ji, wq, (1.0 - kGaussX[q]) * Plo + kGaussX[q] * Phi, rR[q], rphi, q, V);
+      continue;
     }
 #ifndef DCP_MF_NOZMATH
 #define DCP_MF_NOZMATH 0
@@ -748,8 +810,10 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       S[c * kFS + zo + 9 * k] = V[c][k];
-      S[(3 + c) * kFS + zo + 9 * k] = FX[c][k];
-      S[(6 + c) * kFS + zo + 9 * k] = FY[c][k];
+      if (!RHS) {
+        S[(3 + c) * kFS + zo + 9 * k] = FX[c][k];
+        S[(6 + c) * kFS + zo + 9 * k] = FY[c][k];
+      }
     }
   if (STOKES) {
     SP[p] = slo;
@@ -767,14 +831,16 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
         v[b] = SR[c * kFS + yo + ys * b];
-        fx[b] = SR[(3 + c) * kFS + yo + ys * b];
-        fy[b] = SR[(6 + c) * kFS + yo + ys * b];
+        fx[b] = RHS ? 0.0 : SR[(3 + c) * kFS + yo + ys * b];
+        fy[b] = RHS ? 0.0 : SR[(6 + c) * kFS + yo + ys * b];
       }
       bwd(kTL, v, V1[c]);
-      bwd(kTD, fy, t);
+      if (!RHS) {
+        bwd(kTD, fy, t);
 #pragma unroll
-      for (int n = 0; n < 3; ++n) V1[c][n] += t[n];
-      bwd(kTL, fx, FX1[c]);
+        for (int n = 0; n < 3; ++n) V1[c][n] += t[n];
+        bwd(kTL, fx, FX1[c]);
+      }
     }
     if (STOKES && p < 8) {
       const int v0 = p & 1, v1 = (p >> 1) & 1, v2 = p >> 2;
@@ -794,7 +860,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
       for (int n = 0; n < 3; ++n) {
         S[c * kFS + yo + ys * n] = V1[c][n];
-        S[(3 + c) * kFS + yo + ys * n] = FX1[c][n];
+        if (!RHS) S[(3 + c) * kFS + yo + ys * n] = FX1[c][n];
       }
   }
   wsync();
@@ -807,12 +873,17 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu,
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       v[q] = SR[c * kFS + xo + xs * q];
-      fx[q] = SR[(3 + c) * kFS + xo + xs * q];
+      fx[q] = RHS ? 0.0 : SR[(3 + c) * kFS + xo + xs * q];
     }
     bwd(kTL, v, t0);
-    bwd(kTD, fx, t1);
+    if (RHS) {
 #pragma unroll
-    for (int n = 0; n < 3; ++n) y[n][c] = t0[n] + t1[n];
+      for (int n = 0; n < 3; ++n) y[n][c] = t0[n];
+    } else {
+      bwd(kTD, fx, t1);
+#pragma unroll
+      for (int n = 0; n < 3; ++n) y[n][c] = t0[n] + t1[n];
+    }
   }
   // (timing probes only, wrong results: DCP_MF_NOSTORE skips the cell
   // records, DCP_MF_NOZMATH the per-point flux of the z-pencil)
@@ -917,10 +988,13 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     if (ci >= 0) {
       const NodeConstraint nc = g.vcon[i];
       condense(nc, s);
-      const double* dg = g.cdiag + 3 * size_t(ci);
+      if (g.cdiag) {  // operator rows (null: the rhs, condensation only)
+        const double* dg = g.cdiag + 3 * size_t(ci);
 #pragma unroll
-      for (int comp = 0; comp < 3; ++comp)
-        if (nc.type == 1 || nc.type == 3 || comp == nc.k) s[comp] = dg[comp] * src[3 * size_t(i) + comp];
+        for (int comp = 0; comp < 3; ++comp)
+          if (nc.type == 1 || nc.type == 3 || comp == nc.k)
+            s[comp] = dg[comp] * src[3 * size_t(i) + comp];
+      }
     }
     double* d = dst + 3 * size_t(i);
     d[0] = s[0];
@@ -992,7 +1066,18 @@ void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const d
   const bool sep = DCP_MF_SEP && mc.col != nullptr;
   auto k = stokes ? (sep ? k_mf_pencil<true, true> : k_mf_pencil<true, false>)
                   : (sep ? k_mf_pencil<false, true> : k_mf_pencil<false, false>);
-  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, nu, src, buf);
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, nu, src, buf, nullptr,
+                     PhysicsDev{});
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_rhs_cells(const MfCells& mc, int c0, int c1, const double* u_old, const double* T_old,
+                  const PhysicsDev& ph, double* buf, hipStream_t s) {
+  if (c1 <= c0) return;
+  const dim3 grid((kMfBatchTotal(c1 - c0) + kMfBatches - 1) / kMfBatches);
+  const bool sep = DCP_MF_SEP && mc.col != nullptr;
+  auto k = sep ? k_mf_pencil<false, true, true> : k_mf_pencil<false, false, true>;
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, 0.0, u_old, buf, T_old, ph);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,6 +1,7 @@
-"""B^T by rows (k_bt_coltab + k_bt_rows) against the cell scatter
-(DCP_BT_ROWS=0) at refine R (default 5): assemble_nse_system time per
-variant, max relative difference of B^T, rhs bitwise."""
+"""B^T by rows (k_bt_coltab + k_bt_tasks) with the rhs in cell order (pencil +
+gather), the same with the per-colour rhs kernel (DCP_ASM_RHS_CELL_ORDER=0)
+and the cell scatter (DCP_BT_ROWS=0) at refine R (default 5):
+assemble_nse_system time per variant, max relative differences."""
 import json
 import os
 import sys
@@ -17,8 +18,10 @@ u = np.zeros(m.n_u + m.n_p)
 u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
 out = {"refine": R}
 res = {}
-for variant in ("1", "0"):
-    os.environ["DCP_BT_ROWS"] = variant
+for variant, env in (("1", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1"}),
+                     ("h", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "0"}),
+                     ("0", {"DCP_BT_ROWS": "0", "DCP_ASM_RHS_CELL_ORDER": "1"})):
+    os.environ.update(env)
     ctx = dcp.Context()
     ctx.set_physics(dcp.classic_physics())
     ctx.upload_mesh(m)
@@ -30,9 +33,12 @@ for variant in ("1", "0"):
         ms.append(ctx.timings()["assemble_nse_ms"])
     rp, ci, v = ctx.coupling_csr("Bt")
     res[variant] = (v, ctx.get_state(dcp.NSE_RHS))
-    out["ms_bt_rows" if variant == "1" else "ms_cell_scatter"] = [round(x, 4) for x in ms]
+    out[{"1": "ms_bt_rows", "h": "ms_bt_rows_halfwave_rhs", "0": "ms_cell_scatter"}[variant]] = \
+        [round(x, 4) for x in ms]
     ctx.close()
 (v1, r1), (v0, r0) = res["1"], res["0"]
 out["bt_rel_max"] = float(np.max(np.abs(v1 - v0)) / np.max(np.abs(v0)))
 out["rhs_bitwise"] = bool(np.array_equal(r1, r0))
+out["rhs_rel_max"] = float(np.max(np.abs(r1 - r0)) / np.max(np.abs(r0)))
+out["rhs_halfwave_bitwise_cell_scatter"] = bool(np.array_equal(res["h"][1], r0))
 print(json.dumps(out), flush=True)
