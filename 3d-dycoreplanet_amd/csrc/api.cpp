@@ -2111,9 +2111,13 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             // tasks: runs of consecutive rows with <= 8 slots and <= 64 entries
             std::vector<int32_t> hdr, rec;
             int first = 0, ns = 0, ne = 0, rec0 = 0;
+            // 8 slot records per task (unused ones zero): a lane loads its
+            // record at 8 task + slot without waiting for the header
             auto flush = [&](int next_row) {
-              if (next_row > first)
+              if (next_row > first) {
                 hdr.insert(hdr.end(), {Btp[first], first, ns | ne << 8, rec0});
+                rec.resize(size_t(rec0 + 8) * 4, 0);
+              }
               first = next_row;
               ns = ne = 0;
               rec0 = int32_t(rec.size() / 4);

@@ -1952,8 +1952,8 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 }
 
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
-// record}; slot record: {column-table entry, layer << 16 | lex << 8 | row in
-// task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
+// record (= 8 task)}; slot record: {column-table entry, layer << 16 | lex << 8
+// | row in task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
 // DCP_BT_TPW tasks per wave, one after the other, the next task's header and
 // slot record in flight while the current one is evaluated (the chain header
 // -> record -> tables is three dependent loads)
@@ -1972,18 +1972,17 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
   const int t0 = (int(blockIdx.x) * kBtRowWaves + wave) * kBtTpw;
   if (t0 >= n_tasks) return;
   const int k = lane >> 3, v = lane & 7;
-  auto load_rec = [&](const int4& h) {
-    return k < (h.z & 255) ? rec[h.w + k] : make_int4(0, 0, 0, 0);
-  };
+  // records at 8 task + slot (unused slots zero): header and record loads
+  // issue together
   int4 h = hdr[t0];
-  int4 r = load_rec(h);
+  int4 r = rec[8 * size_t(t0) + k];
   for (int i = 0; i < kBtTpw; ++i) {
     const int task = t0 + i;
     if (task >= n_tasks) break;  // uniform per wave
     int4 hn = h, rn = r;
     if (kBtTpw > 1 && i + 1 < kBtTpw && task + 1 < n_tasks) {
       hn = hdr[task + 1];
-      rn = load_rec(hn);
+      rn = rec[8 * size_t(task + 1) + k];
     }
     const int ns = h.z & 255, ne = h.z >> 8;
     int de = -1;
