@@ -1955,7 +1955,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
       // chained to it in (cell, t) order by their group-local index 27 (cell - first) + t
       std::vector<uint32_t> cmask(n_cells, 0);
       std::vector<int32_t> vptr(nv + 1, 0), pptr(n_p + 1, 0);
-      std::vector<uint8_t> vnext(27 * size_t(n_cells), 0xff);
+      std::vector<MfLink> vnext(27 * size_t(n_cells), kMfLinkEnd);
       std::vector<char> vowner(27 * size_t(n_cells), 0);
       {
         std::vector<int> prev(nv, -1), prev_group(nv, -1);
@@ -1966,7 +1966,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             const int n = q2[occ];
             if (vc[n].type != 0) cmask[cell] |= 1u << t;
             if (prev_group[n] == g) {
-              vnext[size_t(prev[n])] = uint8_t(27 * (cell - g) + t);
+              vnext[size_t(prev[n])] = MfLink(27 * (cell - g) + t);
             } else {
               vowner[occ] = 1;
               vptr[n + 1]++;

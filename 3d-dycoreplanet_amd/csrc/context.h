@@ -256,7 +256,8 @@ struct Ctx {
   DBuf<double> mf_buf;  // dof-sorted partial sums (velocity: one per node and cell group)
   DBuf<uint32_t> mf_cmask;
   DBuf<int32_t> mf_vptr, mf_pptr, mf_vslot, mf_pslot, mf_cidx, mf_vorder, mf_porder;
-  DBuf<uint8_t> mf_vnext, mf_wcon;
+  DBuf<MfLink> mf_vnext;
+  DBuf<uint8_t> mf_wcon;
   int32_t mf_pbase = 0;
   // chunked apply (DCP_MF_CHUNKS > 1 at upload): the gather of chunk k's
   // finished dofs runs on mf_stream while the pencil kernel works chunk k + 1.

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace dcp {
 
@@ -164,6 +165,12 @@ __device__ inline int xcd_block(int b, int G) {
   const int q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
   return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
+#ifndef DCP_MF_WAVES
+#define DCP_MF_WAVES 1
+#endif
+// chain links of the velocity partial sums inside a cell group (27 per cell)
+using MfLink = std::conditional_t<(27 * 7 * DCP_MF_WAVES < 255), uint8_t, uint16_t>;
+constexpr MfLink kMfLinkEnd = MfLink(~MfLink(0));
 struct MfCells {
   int n_cells;
   int n_u;                     // offset of the pressure block in [u | p]
@@ -177,7 +184,7 @@ struct MfCells {
   // kernel: the first occurrence of a node in its group owns the group's
   // partial sum, the later ones are chained to it in (cell, t) order.
   const int32_t* vslot;        // [n_cells][27] buf offset (doubles) of the owner's partial, or -1
-  const uint8_t* vnext;        // [n_cells][27] next occurrence in the group (27 * cell + t), or 0xff
+  const MfLink* vnext;         // [n_cells][27] next occurrence in the group (27 * cell + t), or kMfLinkEnd
   const int32_t* pslot;        // [n_cells][8]  buf offset of the (cell, v) pressure value
   // Radially separable geometry (null if the mesh is not): X(a,b,c) = r_c phi_ab
   // in every cell, so J^-1 / JxW at a Gauss point follow from a per-column 2D
@@ -211,8 +218,9 @@ struct MfGather {
   // constrained node (null: always look cidx up)
   const uint8_t* wcon;
 };
-// cells per wave of k_mf_pencil = the cell group of the velocity partial sums
-constexpr int kMfGroupCells = 7;
+// waves per workgroup of k_mf_pencil (7 cells each); the workgroup's cells
+// are the cell group of the velocity partial sums
+constexpr int kMfGroupCells = 7 * DCP_MF_WAVES;
 // cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
               double* buf, hipStream_t s);

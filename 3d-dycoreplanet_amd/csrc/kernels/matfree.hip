@@ -402,11 +402,9 @@ __global__ __launch_bounds__(32 * kMfCells) void k_mf_stokes(MfData md, int base
 #define DCP_MF_CELLS 7
 #endif
 constexpr int kPenCells = DCP_MF_CELLS;  // cells per wave
-static_assert(kPenCells == kMfGroupCells, "the host groups the velocity partial sums per wave");
-#ifndef DCP_MF_WAVES
-#define DCP_MF_WAVES 1
-#endif
-constexpr int kPenWaves = DCP_MF_WAVES;  // waves per workgroup
+constexpr int kPenWaves = DCP_MF_WAVES;  // waves per workgroup (device.h)
+static_assert(kPenCells * kPenWaves == kMfGroupCells,
+              "the host groups the velocity partial sums per workgroup");
 #ifndef DCP_MF_SLOTS
 #define DCP_MF_SLOTS DCP_MF_CELLS
 #endif
@@ -512,7 +510,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   static_assert(!(RHS && STOKES), "the rhs pass has no pressure");
   __shared__ double lds[kPenWaves][kPenFields];
   __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
-  __shared__ uint8_t nxt[kPenWaves][kPenSlots * 27];  // chain links of the group partial sums
+  __shared__ MfLink nxt[kPenWaves * kPenCells * 27];  // chain links of the group partial sums
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // lane 63 shadows lane 54 (slot 6, pencil 0) with 7 LDS slots: it computes
   // and stores the same LDS values and skips the global store; with 8 slots it
@@ -898,22 +896,27 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   for (int n = 0; n < 3; ++n) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) S[c * kFS + xo + xs * n] = y[n][c];
-    nxt[wave][27 * cs + 3 * p + n] = uint8_t(Ic.next[n]);
+    if (cs < kPenCells) nxt[27 * (kPenCells * wave + cs) + 3 * p + n] = MfLink(Ic.next[n]);
   }
-  wsync();
+  // the group spans the workgroup's waves: their records are read across waves
+  if (kPenWaves > 1)
+    __syncthreads();
+  else
+    wsync();
   if (live && !DCP_MF_NOSTORE) {
-    const double* Sw = lds[wave];
 #pragma unroll
     for (int n = 0; n < 3; ++n) {
       if (Ic.slot[n] < 0) continue;
       double s0 = y[n][0], s1 = y[n][1], s2 = y[n][2];
-      // links point forward inside the group (at most kPenCells - 1 hops)
+      // links point forward inside the group (at most kMfGroupCells - 1 hops)
       int k = Ic.next[n];
-      for (int hop = 0; k != 0xff && hop < kPenCells; ++hop, k = nxt[wave][k]) {
+      for (int hop = 0; k != kMfLinkEnd && hop < kMfGroupCells; ++hop, k = nxt[k]) {
         const int ck = k / 27, tk = k - 27 * ck;
+        const int wk = ck / kPenCells, sk = ck - kPenCells * wk;  // wave and cell slot
         const int ak = tk % 3, bk = (tk / 3) % 3, zk = tk / 9;
-        const int idx = (DCP_MF_FIELD_MAJOR ? 27 : 243) * ck +
+        const int idx = (DCP_MF_FIELD_MAJOR ? 27 : 243) * sk +
                         (DCP_MF_SWAP_AB ? 3 * ak + bk + 9 * zk : tk);
+        const double* Sw = lds[wk];
         s0 += Sw[idx];
         s1 += Sw[kFS + idx];
         s2 += Sw[2 * kFS + idx];
@@ -925,7 +928,11 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
     }
     if (STOKES && p < 8) buf[Ic.pslot] = yp;
   }
-  wsync();  // the next batch overwrites the slab this one just read
+  // the next batch overwrites the slabs this one just read
+  if (kPenWaves > 1)
+    __syncthreads();
+  else
+    wsync();
   Ic = In;
   In = Inn;
   if (DCP_MF_PREFETCH_NODES) Nc = Nn;

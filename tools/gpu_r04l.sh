@@ -15,6 +15,8 @@ timeout -k 10 900 python3 -u -m pytest -v --timeout 300 --timeout-method thread 
 tail -2 $OUT/tests.log
 timeout -k 10 300 python3 -u tools/variant_probe.py > $OUT/variants.json 2> $OUT/variants.err || { echo "variants failed"; tail -5 $OUT/variants.err; exit 1; }
 cat $OUT/variants.json
+timeout -k 10 300 python3 -u tools/mf_probe.py > $OUT/mf_variants.json 2> $OUT/mf_variants.err || { echo "mf probe failed"; tail -5 $OUT/mf_variants.err; exit 1; }
+cat $OUT/mf_variants.json
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_SALU"; do
   i=$((i+1)); rm -rf /tmp/pmc
