@@ -1954,77 +1954,74 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
 // record (= 8 task)}; slot record: {column-table entry, layer << 16 | lex << 8
 // | row in task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
-// One task per wave. The header and the lane's slot record load together;
-// the slot row's constraint loads with the column / layer tables (phase 1),
-// so the entry lanes (phase 2) find it in LDS next to the values. Phase 2
-// scans the task's destination bytes four per LDS read, in slot order (the
-// row's cells in colour order). Several tasks per wave with the next header /
-// record prefetched measured slower (profiles/r04l_bt_tpw_variants.json).
-__host__ __device__ constexpr int bt_task_waves(int n_tasks) { return n_tasks; }
-__global__ __launch_bounds__(64 * kBtRowWaves, 8) void k_bt_tasks(
+// DCP_BT_TPW tasks per wave, one after the other, the next task's header and
+// slot record in flight while the current one is evaluated (timing variant:
+// 2 and 4 measured 10 / 17 % slower than 1, profiles/r04l_bt_tpw_variants.json;
+// loading the row constraints in phase 1 into LDS with a packed destination
+// scan was 20 % slower, r04m)
+#ifndef DCP_BT_TPW
+#define DCP_BT_TPW 1
+#endif
+constexpr int kBtTpw = DCP_BT_TPW;
+__host__ __device__ constexpr int bt_task_waves(int n_tasks) { return (n_tasks + kBtTpw - 1) / kBtTpw; }
+__global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
     const double* __restrict__ P, double* __restrict__ Bt) {
   __shared__ double vals[kBtRowWaves][64 * 3];
-  __shared__ double cons[kBtRowWaves][64 * 4];  // the slot row's constraint: w[3], type | k << 32
-  __shared__ uint32_t dst4[kBtRowWaves][16];     // destination entry per (slot, vertex), bytes
+  __shared__ int dst_e[kBtRowWaves][64];
+  __shared__ int rowl[kBtRowWaves][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int task = int(blockIdx.x) * kBtRowWaves + wave;
-  if (task >= n_tasks) return;
+  const int t0 = (int(blockIdx.x) * kBtRowWaves + wave) * kBtTpw;
+  if (t0 >= n_tasks) return;
   const int k = lane >> 3, v = lane & 7;
-  // records at 8 task + slot (unused slots zero)
-  const int4 h = hdr[task];
-  const int4 r = rec[8 * size_t(task) + k];
-  const int ns = h.z & 255, ne = h.z >> 8;
-  uint32_t de = 0xff;
-  if (k < ns) {
-    const unsigned long long dm =
-        (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
-    de = uint32_t((dm >> (6 * v)) & 63);
-    const NodeConstraint nc = cd.vcon[h.y + (r.y & 255)];
-    double e[3];
-    bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
-    vals[wave][3 * lane] = e[0];
-    vals[wave][3 * lane + 1] = e[1];
-    vals[wave][3 * lane + 2] = e[2];
-    double* cw = &cons[wave][4 * lane];
-    cw[0] = nc.w[0];
-    cw[1] = nc.w[1];
-    cw[2] = nc.w[2];
-    cw[3] = __longlong_as_double((long long)(unsigned)nc.type | ((long long)nc.k << 32));
-  }
-  // the destination bytes of 4 lanes per word
-  const uint32_t b1 = __shfl_down(de, 1, 64), b2 = __shfl_down(de, 2, 64),
-                 b3 = __shfl_down(de, 3, 64);
-  if ((lane & 3) == 0) dst4[wave][lane >> 2] = de | b1 << 8 | b2 << 16 | b3 << 24;
-  wsync();
-  if (lane >= ne) return;
-  double acc[3] = {0.0, 0.0, 0.0};
-  int last = 0;
-  for (int q = 0; q < 2 * ns; ++q) {
-    const uint32_t wd = dst4[wave][q];
+  // records at 8 task + slot (unused slots zero): header and record loads
+  // issue together
+  int4 h = hdr[t0];
+  int4 r = rec[8 * size_t(t0) + k];
+  for (int i = 0; i < kBtTpw; ++i) {
+    const int task = t0 + i;
+    if (task >= n_tasks) break;  // uniform per wave
+    int4 hn = h, rn = r;
+    if (kBtTpw > 1 && i + 1 < kBtTpw && task + 1 < n_tasks) {
+      hn = hdr[task + 1];
+      rn = rec[8 * size_t(task + 1) + k];
+    }
+    const int ns = h.z & 255, ne = h.z >> 8;
+    int de = -1;
+    if (k < ns) {
+      const unsigned long long dm =
+          (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
+      de = int((dm >> (6 * v)) & 63);
+      double e[3];
+      bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
+      vals[wave][3 * lane] = e[0];
+      vals[wave][3 * lane + 1] = e[1];
+      vals[wave][3 * lane + 2] = e[2];
+      rowl[wave][lane] = r.y & 255;
+    }
+    dst_e[wave][lane] = de;
+    wsync();
+    if (lane < ne) {
+      double acc[3] = {0.0, 0.0, 0.0};
+      int rl = 0;
+      for (int e = 0; e < 8 * ns; ++e)
+        if (dst_e[wave][e] == lane) {
+          acc[0] += vals[wave][3 * e];
+          acc[1] += vals[wave][3 * e + 1];
+          acc[2] += vals[wave][3 * e + 2];
+          rl = rowl[wave][e];
+        }
+      double Ca[3][3];
+      condensation(cd.vcon[h.y + rl], Ca);
+      double* dst = Bt + 3 * size_t(h.x + lane);
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb)
-      if (((wd >> (8 * bb)) & 255) == uint32_t(lane)) {
-        const int e = 4 * q + bb;
-        acc[0] += vals[wave][3 * e];
-        acc[1] += vals[wave][3 * e + 1];
-        acc[2] += vals[wave][3 * e + 2];
-        last = e;
-      }
+      for (int jj = 0; jj < 3; ++jj)
+        dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+    }
+    wsync();  // the next task overwrites this one's LDS
+    h = hn;
+    r = rn;
   }
-  const double* cw = &cons[wave][4 * last];
-  NodeConstraint nc;
-  nc.w[0] = cw[0];
-  nc.w[1] = cw[1];
-  nc.w[2] = cw[2];
-  const long long tk = __double_as_longlong(cw[3]);
-  nc.type = int32_t(tk & 0xffffffff);
-  nc.k = int32_t(tk >> 32);
-  double Ca[3][3];
-  condensation(nc, Ca);
-  double* dst = Bt + 3 * size_t(h.x + lane);
-#pragma unroll
-  for (int jj = 0; jj < 3; ++jj) dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
 }
 
 // B by pressure rows (several GPUs, where B is not the transpose of the owned
