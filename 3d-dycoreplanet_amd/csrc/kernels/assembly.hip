@@ -1278,9 +1278,14 @@ __global__ void k_clear_first_touch(size_t n, int32_t* __restrict__ pos) {
     if (pos[i] < 0) pos[i] = ~pos[i];
 }
 
-// S_pq = sum_n sum_c B[p][n][c] d[3n+c] B^T[n][q][c]; one 64-lane workgroup
-// per pressure row. The node loop is sequential and the lanes of one node
-// write distinct q, so every entry is summed in the same (node) order.
+// S_pq = sum_n sum_c B[p][n][c] d[3n+c] B^T[n][q][c]; one wave per pressure
+// row. The row's nodes (n, the weights B[p][n][c] d[3n+c], the B^T row range)
+// are staged in LDS first, all lanes at once; then the node loop runs in node
+// order, kSchurU nodes per iteration with their B^T loads issued together,
+// each lane one entry q of a node's B^T row (distinct q per node: the adds
+// into the row's accumulators keep node order, and one wave needs no barrier
+// between nodes). Every entry is summed in the same (node) order as before.
+constexpr int kSchurU = 4;
 __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __restrict__ B_ptr,
                                                    const int32_t* __restrict__ B_col,
                                                    const double* __restrict__ B_val,
@@ -1292,42 +1297,67 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
                                                    const int32_t* __restrict__ S_ptr,
                                                    const int32_t* __restrict__ S_col,
                                                    const int32_t* __restrict__ pmap,
-                                                   double* __restrict__ S_val) {
+                                                   double* __restrict__ S_val, int max_row) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int p = blockIdx.x;
+  const int p = blockIdx.x, lane = threadIdx.x;
   const int s0 = S_ptr[p], len = S_ptr[p + 1] - s0;
+  const int k0 = B_ptr[p], nb = B_ptr[p + 1] - k0;
   double* acc = reinterpret_cast<double*>(smem);
-  int* cols = reinterpret_cast<int*>(acc + len);
-  for (int j = threadIdx.x; j < len; j += 64) {
+  double* wv = acc + max_row;                                   // [nb][3]
+  int* cols = reinterpret_cast<int*>(wv + 3 * size_t(max_row)); // [len]
+  int* rb = cols + max_row;                                     // [nb] B^T row begin
+  int* rn = rb + max_row;                                       // [nb] B^T row length
+  for (int j = lane; j < len; j += 64) {
     acc[j] = 0.0;
     cols[j] = S_col[s0 + j];
   }
-  __syncthreads();
-  for (int k = B_ptr[p]; k < B_ptr[p + 1]; ++k) {
+  for (int i = lane; i < nb; i += 64) {
+    const int k = k0 + i;
     const size_t n = size_t(B_col[k]);
     // B[p][n] = B^T[n][p] (tperm: B not materialised)
     const double* bk = tperm ? Bt_val + 3 * size_t(tperm[k]) : B_val + 3 * size_t(k);
-    const double w0 = bk[0] * d[3 * n];
-    const double w1 = bk[1] * d[3 * n + 1];
-    const double w2 = bk[2] * d[3 * n + 2];
-    const int b = Bt_ptr[n], e = Bt_ptr[n + 1];
-    for (int j = b + int(threadIdx.x); j < e; j += 64) {
-      const int q = Bt_col[j];
-      const double v = w0 * Bt_val[3 * size_t(j)] + w1 * Bt_val[3 * size_t(j) + 1] +
-                       w2 * Bt_val[3 * size_t(j) + 2];
-      int lo = 0, hi = len;
-      while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (cols[m] < q) lo = m + 1; else hi = m;
-      }
-      acc[lo] += v;
-    }
-    __syncthreads();
+    wv[3 * i] = bk[0] * d[3 * n];
+    wv[3 * i + 1] = bk[1] * d[3 * n + 1];
+    wv[3 * i + 2] = bk[2] * d[3 * n + 2];
+    const int b = Bt_ptr[n];
+    rb[i] = b;
+    rn[i] = Bt_ptr[n + 1] - b;
   }
+  __syncthreads();
+  auto find = [&](int q) {
+    int lo = 0, hi = len;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (cols[m] < q) lo = m + 1; else hi = m;
+    }
+    return lo;
+  };
+  for (int i0 = 0; i0 < nb; i0 += kSchurU) {
+    int q[kSchurU];
+    double bv[kSchurU][3];
+#pragma unroll
+    for (int u = 0; u < kSchurU; ++u) {
+      const int i = i0 + u;
+      const bool on = i < nb && lane < rn[i < nb ? i : 0];
+      const int j = on ? rb[i] + lane : 0;
+      q[u] = on ? Bt_col[j] : -1;
+      bv[u][0] = on ? Bt_val[3 * size_t(j)] : 0.0;
+      bv[u][1] = on ? Bt_val[3 * size_t(j) + 1] : 0.0;
+      bv[u][2] = on ? Bt_val[3 * size_t(j) + 2] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kSchurU; ++u) {
+      if (q[u] < 0) continue;
+      const int i = i0 + u;
+      const double v = wv[3 * i] * bv[u][0] + wv[3 * i + 1] * bv[u][1] + wv[3 * i + 2] * bv[u][2];
+      acc[find(q[u])] += v;
+    }
+  }
+  __syncthreads();
   if (pmap) {
-    for (int j = threadIdx.x; j < len; j += 64) S_val[pmap[s0 + j]] = acc[j];
+    for (int j = lane; j < len; j += 64) S_val[pmap[s0 + j]] = acc[j];
   } else {
-    for (int j = threadIdx.x; j < len; j += 64) S_val[s0 + j] = acc[j];
+    for (int j = lane; j < len; j += 64) S_val[s0 + j] = acc[j];
   }
 }
 
@@ -1339,9 +1369,10 @@ void form_schur_complement(int n_p, const int32_t* B_ptr, const int32_t* B_col, 
                            const double* d, const int32_t* S_ptr, const int32_t* S_col,
                            const int32_t* pmap, double* S_val, int max_row, hipStream_t s) {
   if (n_p <= 0) return;
-  const size_t lds = size_t(max_row) * (sizeof(double) + sizeof(int)) + 16;
+  // max_row bounds both the S row and the B row (nodes) lengths
+  const size_t lds = size_t(max_row) * (4 * sizeof(double) + 3 * sizeof(int)) + 16;
   hipLaunchKernelGGL(k_schur_form, dim3(n_p), dim3(64), lds, s, n_p, B_ptr, B_col, B_val, tperm, Bt_ptr,
-                     Bt_col, Bt_val, d, S_ptr, S_col, pmap, S_val);
+                     Bt_col, Bt_val, d, S_ptr, S_col, pmap, S_val, max_row);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
