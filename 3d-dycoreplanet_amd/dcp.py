@@ -615,6 +615,55 @@ def torch_host_comm(group=None):
     return hc
 
 
+class ThreadHostComms:
+    """dcp_host_comm for `world` ranks of ONE process, one thread per rank (the
+    in-process groups of the tests): the collectives meet on a barrier and
+    exchange bytes through shared slots. comm(rank) is that rank's HostComm."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+        self._comms = {}
+
+    def comm(self, rank):
+        if rank in self._comms:
+            return self._comms[rank]
+        world = self.world
+
+        def allgather(_user, send, nbytes, recv):
+            try:
+                self.slots[rank] = C.string_at(send, nbytes) if nbytes else b""
+                self.bar.wait()
+                if nbytes:
+                    C.memmove(recv, b"".join(self.slots), nbytes * world)
+                self.bar.wait()
+                return 0
+            except Exception:  # noqa: BLE001 - reported to the library as a failure
+                return 1
+
+        def alltoallv(_user, send, send_bytes, recv, recv_bytes):
+            try:
+                sb = [int(send_bytes[k]) for k in range(world)]
+                data = C.string_at(send, sum(sb)) if sum(sb) else b""
+                off = np.concatenate([[0], np.cumsum(sb)]).astype(int)
+                self.slots[rank] = [data[off[k]:off[k + 1]] for k in range(world)]
+                self.bar.wait()
+                out = b"".join(self.slots[k][rank] for k in range(world))
+                if out:
+                    C.memmove(recv, out, len(out))
+                self.bar.wait()
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        hc = HostComm(None, rank, world, ALLGATHER_FN(allgather), ALLTOALLV_FN(alltoallv))
+        hc._keep = (hc.allgather, hc.alltoallv)
+        self._comms[rank] = hc
+        return hc
+
+
 class DistMesh:
     """One rank's part of a distributed mesh (dcp_dist_mesh), built here from a
     global HostMesh the way a p4est run would hold it: the rank's owned cells

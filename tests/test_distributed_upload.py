@@ -188,3 +188,114 @@ def test_distributed_upload_bad_input_on_one_rank_fails_every_rank_gloo():
         p.join(timeout=60)
     assert "NSE dof out of range" in res[1], res
     assert "another rank's input is invalid" in res[0], res
+
+
+def _threads(world, fn):
+    import threading
+    out, errors = [None] * world, []
+
+    def run(r):
+        try:
+            out[r] = fn(r)
+        except Exception as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errors, errors
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_threaded_host_comm_localisation_matches_global(world):
+    """dcp.ThreadHostComms (the in-process dcp_host_comm of the GPU group test
+    below) gives the same distributed localisation as the global partition:
+    counts, layers and velocity halo lists in global ids."""
+    m = dcp.HostMesh(refine=2)
+    comms = dcp.ThreadHostComms(world)
+
+    def fn(r):
+        dm = dcp.DistMesh(m, r, world)
+        got = dcp.dist_partition_info(dm, comms.comm(r))
+        want = dcp.partition_info(Renumbered(m, dm), r, world)
+        return got, want
+
+    for got, want in _threads(world, fn):
+        for k in want:
+            if k in ("send", "recv", "n_colors"):
+                continue
+            assert got[k] == want[k], k
+        assert got["send"].keys() == want["send"].keys()
+        for k in want["send"]:
+            assert np.array_equal(got["send"][k], want["send"][k])
+            assert np.array_equal(got["recv"][k], want["recv"][k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_upload_group_time_step_matches_single_gpu(world):
+    """The distributed entry point on several ranks (in-process group, one
+    thread per rank, ThreadHostComms as the caller's communicator): one full
+    time step -- assembly, preconditioner, the s-step inner GMRES with the
+    matrix powers, temperature -- against one GPU with the global upload, on
+    every rank's owned entries. The inner solves run 28 fixed steps
+    (DCP_OPT_BLOCK_FIXED_INNER) so both take the same control decisions:
+    rhs 1e-12, iterates 1e-10, equal outer counts."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(17)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    T = m.T0.copy()
+
+    def step(ctx, setv):
+        ctx.set_gram_schmidt("sstep")
+        ctx.set_block_fixed_inner(28)
+        for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
+                     (dcp.T_SOLUTION, T)):
+            setv(f, v)
+        ctx.assemble_nse_system()
+        ctx.build_nse_preconditioner()
+        ctx.assemble_temperature_matrix()
+        ctx.assemble_temperature_rhs()
+        return ctx.solve_nse(), ctx.solve_temperature()
+
+    ref = dcp.Context()
+    ref.set_physics(ph)
+    ref.upload_mesh(m)
+    ref_counts = step(ref, ref.set_state)
+    ref_rhs, ref_x, ref_T = (ref.get_state(f) for f in (dcp.NSE_RHS, dcp.NSE_SOLUTION, dcp.T_SOLUTION))
+    ref.close()
+    g = dcp.Group(world)
+    comms = dcp.ThreadHostComms(world)
+
+    def fn(r):
+        dm = dcp.DistMesh(m, r, world)
+        ctx = dcp.Context(rank=r, world_size=world, group=g)
+        ctx.set_physics(ph)
+        ctx.upload_mesh_distributed(dm, comms.comm(r))
+
+        def setv(f, v):
+            ctx.set_state_owned(f, dm.owned_T(v) if f in (dcp.OLD_T_SOLUTION, dcp.T_SOLUTION)
+                                else dm.owned_nse(v))
+        counts = step(ctx, setv)
+        nn = (dm.u_end - dm.u_begin) + (dm.p_end - dm.p_begin)
+        nt = dm.T_end - dm.T_begin
+        res = (counts, ctx.get_state_owned(dcp.NSE_RHS, nn), ctx.get_state_owned(dcp.NSE_SOLUTION, nn),
+               ctx.get_state_owned(dcp.T_SOLUTION, nt), dm)
+        ctx.close()
+        return res
+
+    out = _threads(world, fn)
+    g.close()
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    for counts, rhs, x, Tx, dm in out:
+        assert counts[0][0] == ref_counts[0][0] == 0
+        assert counts[0][1] == ref_counts[0][1]           # FGMRES iterations
+        assert counts[0][2] == ref_counts[0][2]           # inner (fixed) steps
+        assert rel(rhs, dm.owned_nse(ref_rhs)) < 1e-12
+        assert rel(x, dm.owned_nse(ref_x)) < 1e-10
+        assert rel(Tx, dm.owned_T(ref_T)) < 1e-10
