@@ -1371,13 +1371,35 @@ dcp_group* dcp_group_create(int world_size) {
 
 void dcp_group_destroy(dcp_group* g) { delete g; }
 
-int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
-                       const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
-                       int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c, int rank,
-                       int world, int64_t* info, int32_t* peers, int32_t* send_ptr,
-                       int64_t* send_gid, int32_t* recv_ptr, int64_t* recv_gid) {
+namespace dcp {
+// counts (the halo of `field`: 0 velocity nodes, 1 pressure, 2 temperature)
+// and that halo's peer lists in global ids (dcp_partition_info[_field],
+// dcp_dist_partition_info[_field])
+void partition_info_out(const LocalMesh& L, int n_colors, int field, int64_t* info, int32_t* peers,
+                        int32_t* send_ptr, int64_t* send_gid, int32_t* recv_ptr,
+                        int64_t* recv_gid) {
+  const HaloPlan& hp = field == 0 ? L.hv : field == 1 ? L.hp : L.hT;
+  const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
+                         int64_t(hp.peers.size()), int64_t(hp.send_idx.size()),
+                         int64_t(hp.recv_idx.size()), int64_t(n_colors)};
+  std::copy(v, v + 12, info);
+  if (peers) std::copy(hp.peers.begin(), hp.peers.end(), peers);
+  if (send_ptr) std::copy(hp.send_ptr.begin(), hp.send_ptr.end(), send_ptr);
+  if (recv_ptr) std::copy(hp.recv_ptr.begin(), hp.recv_ptr.end(), recv_ptr);
+  if (send_gid) std::copy(hp.send_gid.begin(), hp.send_gid.end(), send_gid);
+  if (recv_gid) std::copy(hp.recv_gid.begin(), hp.recv_gid.end(), recv_gid);
+}
+}  // namespace dcp
+
+int dcp_partition_info_field(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                             const double* cell_geometry, const double* cell_diameter, int n_u,
+                             int n_p, int n_T, const dcp_constraints* nse_c,
+                             const dcp_constraints* T_c, int rank, int world, int field,
+                             int64_t* info, int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                             int32_t* recv_ptr, int64_t* recv_gid) {
   return guarded(nullptr, [&] {
     require(info != nullptr, DCP_ERR_INVALID, "NULL info");
+    require(field >= 0 && field <= 2, DCP_ERR_INVALID, "field must be 0..2");
     LocalMesh L;
     try {
       L = localize(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u, n_p,
@@ -1391,24 +1413,28 @@ int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t*
         partition_colour_hint(n_cells, cell_nse_dofs, cell_geometry, n_u, n_p, L.cells_g);
     prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
                  L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc, &hint);
-    const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
-                           int64_t(L.hv.peers.size()), int64_t(L.hv.send_idx.size()),
-                           int64_t(L.hv.recv_idx.size()), int64_t(h.color_ptr.size()) - 1};
-    std::copy(v, v + 12, info);
-    if (peers) std::copy(L.hv.peers.begin(), L.hv.peers.end(), peers);
-    if (send_ptr) std::copy(L.hv.send_ptr.begin(), L.hv.send_ptr.end(), send_ptr);
-    if (recv_ptr) std::copy(L.hv.recv_ptr.begin(), L.hv.recv_ptr.end(), recv_ptr);
-    if (send_gid) std::copy(L.hv.send_gid.begin(), L.hv.send_gid.end(), send_gid);
-    if (recv_gid) std::copy(L.hv.recv_gid.begin(), L.hv.recv_gid.end(), recv_gid);
+    partition_info_out(L, int(h.color_ptr.size()) - 1, field, info, peers, send_ptr, send_gid,
+                       recv_ptr, recv_gid);
     return DCP_OK;
   });
 }
 
-int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, int64_t* info,
-                            int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
-                            int32_t* recv_ptr, int64_t* recv_gid) {
+int dcp_partition_info(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                       const double* cell_geometry, const double* cell_diameter, int n_u, int n_p,
+                       int n_T, const dcp_constraints* nse_c, const dcp_constraints* T_c, int rank,
+                       int world, int64_t* info, int32_t* peers, int32_t* send_ptr,
+                       int64_t* send_gid, int32_t* recv_ptr, int64_t* recv_gid) {
+  return dcp_partition_info_field(n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter,
+                                  n_u, n_p, n_T, nse_c, T_c, rank, world, 0, info, peers, send_ptr,
+                                  send_gid, recv_ptr, recv_gid);
+}
+
+int dcp_dist_partition_info_field(const dcp_dist_mesh* m, const dcp_host_comm* comm, int field,
+                                  int64_t* info, int32_t* peers, int32_t* send_ptr,
+                                  int64_t* send_gid, int32_t* recv_ptr, int64_t* recv_gid) {
   return guarded(nullptr, [&] {
     require(m && comm && info, DCP_ERR_INVALID, "NULL argument");
+    require(field >= 0 && field <= 2, DCP_ERR_INVALID, "field must be 0..2");
     LocalMesh L;
     try {
       L = localize_distributed(*m, *comm);
@@ -1419,17 +1445,17 @@ int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, i
     HostPrep h;
     prepare_mesh(h, L.n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
                  L.diameter.data(), L.n_u(), L.n_p(), L.n_T(), &lnc, &ltc);
-    const int64_t v[12] = {L.n_cells, L.n_owned_cells, L.nvo, L.nvg, L.npo, L.npg, L.nTo, L.nTg,
-                           int64_t(L.hv.peers.size()), int64_t(L.hv.send_idx.size()),
-                           int64_t(L.hv.recv_idx.size()), int64_t(h.color_ptr.size()) - 1};
-    std::copy(v, v + 12, info);
-    if (peers) std::copy(L.hv.peers.begin(), L.hv.peers.end(), peers);
-    if (send_ptr) std::copy(L.hv.send_ptr.begin(), L.hv.send_ptr.end(), send_ptr);
-    if (recv_ptr) std::copy(L.hv.recv_ptr.begin(), L.hv.recv_ptr.end(), recv_ptr);
-    if (send_gid) std::copy(L.hv.send_gid.begin(), L.hv.send_gid.end(), send_gid);
-    if (recv_gid) std::copy(L.hv.recv_gid.begin(), L.hv.recv_gid.end(), recv_gid);
+    partition_info_out(L, int(h.color_ptr.size()) - 1, field, info, peers, send_ptr, send_gid,
+                       recv_ptr, recv_gid);
     return DCP_OK;
   });
+}
+
+int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, int64_t* info,
+                            int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                            int32_t* recv_ptr, int64_t* recv_gid) {
+  return dcp_dist_partition_info_field(m, comm, 0, info, peers, send_ptr, send_gid, recv_ptr,
+                                       recv_gid);
 }
 
 int dcp_feec_partition_info(const dcp_feec_mesh* m, int rank, int world, int field,

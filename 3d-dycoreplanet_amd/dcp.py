@@ -64,7 +64,8 @@ EXPORTED = [
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
-    "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_state_set_owned",
+    "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_dist_partition_info_field",
+    "dcp_partition_info_field", "dcp_state_set_owned",
     "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_nse_coupling_export",
     "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
@@ -298,6 +299,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_mesh_upload_distributed.argtypes = [P, C.POINTER(DistMeshView), C.POINTER(HostComm)]
     lib.dcp_dist_partition_info.argtypes = [C.POINTER(DistMeshView), C.POINTER(HostComm), P, P, P,
                                             P, P, P]
+    lib.dcp_dist_partition_info_field.argtypes = [C.POINTER(DistMeshView), C.POINTER(HostComm), I,
+                                                  P, P, P, P, P, P]
+    lib.dcp_partition_info_field.argtypes = [I, P, P, P, P, I, I, I, C.POINTER(Constraints),
+                                             C.POINTER(Constraints), I, I, I, P, P, P, P, P, P]
     lib.dcp_state_set_owned.argtypes = [P, I, P, C.c_size_t]
     lib.dcp_state_get_owned.argtypes = [P, I, P, C.c_size_t]
     return lib
@@ -779,19 +784,22 @@ class DistMesh:
         return g[self.T_begin:self.T_end].copy()
 
 
-def dist_partition_info(dm: DistMesh, comm: HostComm):
-    """dcp_dist_partition_info on this rank (host only; every rank calls it)."""
+def dist_partition_info(dm: DistMesh, comm: HostComm, field: str = "v"):
+    """dcp_dist_partition_info_field on this rank (host only; every rank calls
+    it): sizes and the halo lists (global ids) of `field` ("v" velocity
+    support points, "p" pressure, "T" temperature) per peer."""
+    fid = {"v": 0, "p": 1, "T": 2}[field]
     view = dm.as_struct()
     info = np.zeros(12, np.int64)
-    rc = lib().dcp_dist_partition_info(C.byref(view), C.byref(comm), _ptr(info), None, None, None,
-                                       None, None)
+    rc = lib().dcp_dist_partition_info_field(C.byref(view), C.byref(comm), fid, _ptr(info), None,
+                                             None, None, None, None)
     if rc != DCP_OK:
         raise DcpError(rc, lib().dcp_last_error(None).decode())
     npeer, ns, nr = int(info[8]), int(info[9]), int(info[10])
     peers = np.zeros(max(npeer, 1), np.int32)
     sp, rp = np.zeros(npeer + 1, np.int32), np.zeros(npeer + 1, np.int32)
     sg, rg = np.zeros(max(ns, 1), np.int64), np.zeros(max(nr, 1), np.int64)
-    rc = lib().dcp_dist_partition_info(C.byref(view), C.byref(comm), _ptr(info), _ptr(peers),
+    rc = lib().dcp_dist_partition_info_field(C.byref(view), C.byref(comm), fid, _ptr(info), _ptr(peers),
                                        _ptr(sp), _ptr(sg), _ptr(rp), _ptr(rg))
     if rc != DCP_OK:
         raise DcpError(rc, lib().dcp_last_error(None).decode())
@@ -838,22 +846,24 @@ class Group:
             self._h = None
 
 
-def partition_info(m, rank, world):
-    """Host-only summary of rank's partition (dcp_partition_info): a dict of
-    sizes and the velocity-node halo lists (global ids) per peer."""
+def partition_info(m, rank, world, field="v"):
+    """Host-only summary of rank's partition (dcp_partition_info_field): a dict
+    of sizes and the halo lists (global ids) of `field` ("v" velocity support
+    points, "p" pressure, "T" temperature) per peer."""
     info = np.zeros(12, np.int64)
     nc, tc = m.nse_constraints.as_struct(), m.T_constraints.as_struct()
     args = (m.n_cells, _ptr(m.cell_nse_dofs), _ptr(m.cell_T_dofs), _ptr(m.cell_geometry),
-            _ptr(m.cell_diameter), m.n_u, m.n_p, m.n_T, C.byref(nc), C.byref(tc), rank, world)
-    rc = lib().dcp_partition_info(*args, _ptr(info), None, None, None, None, None)
+            _ptr(m.cell_diameter), m.n_u, m.n_p, m.n_T, C.byref(nc), C.byref(tc), rank, world,
+            {"v": 0, "p": 1, "T": 2}[field])
+    rc = lib().dcp_partition_info_field(*args, _ptr(info), None, None, None, None, None)
     if rc != DCP_OK:
         raise DcpError(rc, lib().dcp_last_error(None).decode())
     npeer, ns, nr = int(info[8]), int(info[9]), int(info[10])
     peers = np.zeros(npeer, np.int32)
     sp, rp = np.zeros(npeer + 1, np.int32), np.zeros(npeer + 1, np.int32)
     sg, rg = np.zeros(max(ns, 1), np.int64), np.zeros(max(nr, 1), np.int64)
-    rc = lib().dcp_partition_info(*args, _ptr(info), _ptr(peers), _ptr(sp), _ptr(sg), _ptr(rp),
-                                  _ptr(rg))
+    rc = lib().dcp_partition_info_field(*args, _ptr(info), _ptr(peers), _ptr(sp), _ptr(sg),
+                                        _ptr(rp), _ptr(rg))
     if rc != DCP_OK:
         raise DcpError(rc, lib().dcp_last_error(None).decode())
     keys = ("n_cells", "n_owned_cells", "nvo", "nvg", "npo", "npg", "nTo", "nTg", "n_peers",

@@ -179,6 +179,18 @@ int dcp_mesh_upload_distributed(dcp_ctx* ctx, const dcp_dist_mesh* m, const dcp_
 int dcp_dist_partition_info(const dcp_dist_mesh* m, const dcp_host_comm* comm, int64_t* info,
                             int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
                             int32_t* recv_ptr, int64_t* recv_gid);
+/* dcp_partition_info / dcp_dist_partition_info with the halo of `field`: 0 =
+ * velocity support points, 1 = pressure dofs, 2 = temperature dofs (peer
+ * lists in global ids; the counts as in the velocity form). */
+int dcp_partition_info_field(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,
+                             const double* cell_geometry, const double* cell_diameter, int n_u,
+                             int n_p, int n_T, const dcp_constraints* nse_constraints,
+                             const dcp_constraints* T_constraints, int rank, int world, int field,
+                             int64_t* info, int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                             int32_t* recv_ptr, int64_t* recv_gid);
+int dcp_dist_partition_info_field(const dcp_dist_mesh* m, const dcp_host_comm* comm, int field,
+                                  int64_t* info, int32_t* peers, int32_t* send_ptr,
+                                  int64_t* send_gid, int32_t* recv_ptr, int64_t* recv_gid);
 /* The rank's locally owned entries of a state field, ascending global index
  * (NSE: owned velocity, then owned pressure; the Trilinos vector's local part).
  * Ghost entries are refreshed internally. Works after either upload. */

@@ -7,8 +7,8 @@ caller's communicator (dcp_host_comm; here torch.distributed gloo).
 
 CPU (gloo, 2 and 3 processes): with the ownership of the library's own
 global-mesh rule, the distributed localisation reproduces the global one
-exactly (cell/entity counts, colours, velocity halo lists in global ids), and
-ownership covers every DoF once.
+exactly (cell/entity counts, colours, the velocity, pressure and temperature
+halo lists in global ids), and ownership covers every DoF once.
 GPU (in the -m gpu run): one rank with world 1 uploads through the
 distributed entry point and matches the global upload bitwise."""
 import os
@@ -57,6 +57,14 @@ def _worker(rank, world, port, refine, tdeg, q):
         for k in want["send"]:
             same &= np.array_equal(got["send"][k], want["send"][k])
             same &= np.array_equal(got["recv"][k], want["recv"][k])
+        # the pressure and temperature halos (global ids) as well
+        for f in ("p", "T"):
+            gf = dcp.dist_partition_info(dm, comm, f)
+            wf = dcp.partition_info(Renumbered(m, dm), rank, world, f)
+            same &= gf["send"].keys() == wf["send"].keys() and gf["recv"].keys() == wf["recv"].keys()
+            for k in wf["send"]:
+                same &= np.array_equal(gf["send"][k], wf["send"][k])
+                same &= np.array_equal(gf["recv"][k], wf["recv"][k])
         # the caller's ownership is what the library keeps
         same &= got["nvo"] == (dm.u_end - dm.u_begin) // 3 and got["npo"] == dm.p_end - dm.p_begin
         same &= got["nTo"] == dm.T_end - dm.T_begin
@@ -219,19 +227,20 @@ def test_threaded_host_comm_localisation_matches_global(world):
 
     def fn(r):
         dm = dcp.DistMesh(m, r, world)
-        got = dcp.dist_partition_info(dm, comms.comm(r))
-        want = dcp.partition_info(Renumbered(m, dm), r, world)
-        return got, want
+        return [(dcp.dist_partition_info(dm, comms.comm(r), f),
+                 dcp.partition_info(Renumbered(m, dm), r, world, f)) for f in ("v", "p", "T")]
 
-    for got, want in _threads(world, fn):
-        for k in want:
-            if k in ("send", "recv", "n_colors"):
-                continue
-            assert got[k] == want[k], k
-        assert got["send"].keys() == want["send"].keys()
-        for k in want["send"]:
-            assert np.array_equal(got["send"][k], want["send"][k])
-            assert np.array_equal(got["recv"][k], want["recv"][k])
+    for per_field in _threads(world, fn):
+        for got, want in per_field:
+            for k in want:
+                if k in ("send", "recv", "n_colors"):
+                    continue
+                assert got[k] == want[k], k
+            assert got["send"].keys() == want["send"].keys()
+            assert got["recv"].keys() == want["recv"].keys()
+            for k in want["send"]:
+                assert np.array_equal(got["send"][k], want["send"][k])
+                assert np.array_equal(got["recv"][k], want["recv"][k])
 
 
 @pytest.mark.gpu
