@@ -2138,15 +2138,18 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                 const int n = q2[27 * size_t(cell) + t];
                 if (n < nrows) inc[size_t(f[n]++)] = int32_t(cell) << 5 | t;
               }
-            // tasks: runs of consecutive rows with <= 8 slots and <= 64 entries
+            // tasks: runs of consecutive rows with <= SL slots and <= 64
+            // entries (SL = 16, DCP_BT_SLOTS=8 for the one-record-per-lane form)
+            const char* env_sl = std::getenv("DCP_BT_SLOTS");
+            const int SL = env_sl && std::atoi(env_sl) == 8 ? 8 : 16;
             std::vector<int32_t> hdr, rec;
             int first = 0, ns = 0, ne = 0, rec0 = 0;
-            // 8 slot records per task (unused ones zero): a lane loads its
-            // record at 8 task + slot without waiting for the header
+            // SL slot records per task (unused ones zero): a lane loads its
+            // records at SL task + slot without waiting for the header
             auto flush = [&](int next_row) {
               if (next_row > first) {
                 hdr.insert(hdr.end(), {Btp[first], first, ns | ne << 8, rec0});
-                rec.resize(size_t(rec0 + 8) * 4, 0);
+                rec.resize(size_t(rec0 + SL) * 4, 0);
               }
               first = next_row;
               ns = ne = 0;
@@ -2155,7 +2158,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             for (int n = 0; n < nrows; ++n) {
               const int cnt = rp[n + 1] - rp[n], len = Btp[n + 1] - Btp[n];
               require(cnt <= 8 && len <= 64, DCP_ERR_INVALID, "B^T task sizes");
-              if (ns + cnt > 8 || ne + len > 64) flush(n);
+              if (ns + cnt > SL || ne + len > 64) flush(n);
               for (int k = rp[n]; k < rp[n + 1]; ++k) {
                 const int cell = inc[size_t(k)] >> 5, lex = inc[size_t(k)] & 31;
                 uint64_t dm = 0;
@@ -2177,6 +2180,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.bt_task_hdr.upload(hdr);
             c.bt_slot_rec.upload(rec);
             c.bt_ntasks = int(hdr.size() / 4);
+            c.bt_slots = SL;
             // several GPUs: the rhs / constrained diagonal are read on owned rows
             // only, so the cell kernel runs over the cells with an owned
             // velocity node (owned cells + the first ghost layer), per colour
@@ -2551,7 +2555,8 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
     if (bt_rows)
-      launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, c.bt_ntasks, c.bt_task_hdr.p, c.bt_slot_rec.p,
+      launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
+                     c.bt_slot_rec.p,
                      c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p, c.bt_p_inc.p, c.B_ptr.p,
                      c.B_col.p, c.B_transpose ? nullptr : c.B_val.p, c.stream);
     if (full)

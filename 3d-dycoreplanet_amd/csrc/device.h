@@ -294,10 +294,10 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (api.cpp build_bt_tasks). Writes every B^T entry once. B != null (several
 // GPUs): also B by pressure rows (k_b_rows; p_inc: cell << 3 | vertex), bitwise
 // the transpose of B^T.
-void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, const int32_t* task_hdr,
-                    const int32_t* slot_rec, double* Bt, int n_prows, const int32_t* p_ptr,
-                    const int32_t* p_inc, const int32_t* B_ptr, const int32_t* B_col, double* B,
-                    hipStream_t s);
+void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, int slots,
+                    const int32_t* task_hdr, const int32_t* slot_rec, double* Bt, int n_prows,
+                    const int32_t* p_ptr, const int32_t* p_inc, const int32_t* B_ptr,
+                    const int32_t* B_col, double* B, hipStream_t s);
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
                       int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
                       unsigned long long* touched_out = nullptr);

@@ -1983,76 +1983,68 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 }
 
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
-// record (= 8 task)}; slot record: {column-table entry, layer << 16 | lex << 8
-// | row in task, the 8 vertices' task entries as 6-bit fields (lo, hi words)}
-// DCP_BT_TPW tasks per wave, one after the other, the next task's header and
-// slot record in flight while the current one is evaluated (timing variant:
-// 2 and 4 measured 10 / 17 % slower than 1, profiles/r04l_bt_tpw_variants.json;
-// loading the row constraints in phase 1 into LDS with a packed destination
-// scan was 20 % slower, r04m)
-#ifndef DCP_BT_TPW
-#define DCP_BT_TPW 1
-#endif
-constexpr int kBtTpw = DCP_BT_TPW;
-__host__ __device__ constexpr int bt_task_waves(int n_tasks) { return (n_tasks + kBtTpw - 1) / kBtTpw; }
+// record (= SL task)}; slot record: {column-table entry, layer << 16 | lex <<
+// 8 | row in task, the 8 vertices' task entries as 6-bit fields (lo, hi
+// words)}. SL slots per task (8 or 16, DCP_BT_SLOTS at upload), at most 64
+// entries: lane (k, v) evaluates slot k (and k + 8) for vertex v, so a task of
+// 16 slots fills the 64 entry lanes (~32 entries per 8-slot task at r=5) and
+// one wave's chain of dependent loads (header / record -> tables -> row
+// constraint) serves twice the entries. Several tasks per wave one after the
+// other (the next header / record prefetched) measured 10 / 17 % slower for 2
+// / 4 (profiles/r04l_bt_tpw_variants.json); loading the row constraints in
+// phase 1 into LDS with a packed destination scan, 20 % slower (r04m).
+template <int SL>
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
     const double* __restrict__ P, double* __restrict__ Bt) {
-  __shared__ double vals[kBtRowWaves][64 * 3];
-  __shared__ int dst_e[kBtRowWaves][64];
-  __shared__ int rowl[kBtRowWaves][64];
+  constexpr int R = SL / 8;  // slot records per lane
+  __shared__ double vals[kBtRowWaves][R * 64 * 3];
+  __shared__ int dst_e[kBtRowWaves][R * 64];
+  __shared__ int rowl[kBtRowWaves][R * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int t0 = (int(blockIdx.x) * kBtRowWaves + wave) * kBtTpw;
-  if (t0 >= n_tasks) return;
+  const int task = int(blockIdx.x) * kBtRowWaves + wave;
+  if (task >= n_tasks) return;
   const int k = lane >> 3, v = lane & 7;
-  // records at 8 task + slot (unused slots zero): header and record loads
+  // records at SL task + slot (unused slots zero): header and record loads
   // issue together
-  int4 h = hdr[t0];
-  int4 r = rec[8 * size_t(t0) + k];
-  for (int i = 0; i < kBtTpw; ++i) {
-    const int task = t0 + i;
-    if (task >= n_tasks) break;  // uniform per wave
-    int4 hn = h, rn = r;
-    if (kBtTpw > 1 && i + 1 < kBtTpw && task + 1 < n_tasks) {
-      hn = hdr[task + 1];
-      rn = rec[8 * size_t(task + 1) + k];
-    }
-    const int ns = h.z & 255, ne = h.z >> 8;
-    int de = -1;
-    if (k < ns) {
-      const unsigned long long dm =
-          (unsigned long long)(unsigned)r.z | ((unsigned long long)(unsigned)r.w << 32);
-      de = int((dm >> (6 * v)) & 63);
-      double e[3];
-      bt_entry(cd, P, r.x, r.y >> 16, (r.y >> 8) & 255, v, e);
-      vals[wave][3 * lane] = e[0];
-      vals[wave][3 * lane + 1] = e[1];
-      vals[wave][3 * lane + 2] = e[2];
-      rowl[wave][lane] = r.y & 255;
-    }
-    dst_e[wave][lane] = de;
-    wsync();
-    if (lane < ne) {
-      double acc[3] = {0.0, 0.0, 0.0};
-      int rl = 0;
-      for (int e = 0; e < 8 * ns; ++e)
-        if (dst_e[wave][e] == lane) {
-          acc[0] += vals[wave][3 * e];
-          acc[1] += vals[wave][3 * e + 1];
-          acc[2] += vals[wave][3 * e + 2];
-          rl = rowl[wave][e];
-        }
-      double Ca[3][3];
-      condensation(cd.vcon[h.y + rl], Ca);
-      double* dst = Bt + 3 * size_t(h.x + lane);
+  const int4 h = hdr[task];
+  int4 r[R];
 #pragma unroll
-      for (int jj = 0; jj < 3; ++jj)
-        dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+  for (int i = 0; i < R; ++i) r[i] = rec[SL * size_t(task) + 8 * i + k];
+  const int ns = h.z & 255, ne = h.z >> 8;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int e = 64 * i + lane;  // = 8 slot + v
+    int de = -1;
+    if (8 * i + k < ns) {
+      const unsigned long long dm =
+          (unsigned long long)(unsigned)r[i].z | ((unsigned long long)(unsigned)r[i].w << 32);
+      de = int((dm >> (6 * v)) & 63);
+      double ev[3];
+      bt_entry(cd, P, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
+      vals[wave][3 * e] = ev[0];
+      vals[wave][3 * e + 1] = ev[1];
+      vals[wave][3 * e + 2] = ev[2];
+      rowl[wave][e] = r[i].y & 255;
     }
-    wsync();  // the next task overwrites this one's LDS
-    h = hn;
-    r = rn;
+    dst_e[wave][e] = de;
   }
+  wsync();
+  if (lane >= ne) return;
+  double acc[3] = {0.0, 0.0, 0.0};
+  int rl = 0;
+  for (int e = 0; e < 8 * ns; ++e)
+    if (dst_e[wave][e] == lane) {
+      acc[0] += vals[wave][3 * e];
+      acc[1] += vals[wave][3 * e + 1];
+      acc[2] += vals[wave][3 * e + 2];
+      rl = rowl[wave][e];
+    }
+  double Ca[3][3];
+  condensation(cd.vcon[h.y + rl], Ca);
+  double* dst = Bt + 3 * size_t(h.x + lane);
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
 }
 
 // B by pressure rows (several GPUs, where B is not the transpose of the owned
@@ -2251,18 +2243,18 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
   return false;
 }
 
-void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, const int32_t* task_hdr,
-                    const int32_t* slot_rec, double* Bt, int n_prows, const int32_t* p_ptr,
-                    const int32_t* p_inc, const int32_t* B_ptr, const int32_t* B_col, double* B,
-                    hipStream_t s) {
+void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, int slots,
+                    const int32_t* task_hdr, const int32_t* slot_rec, double* Bt, int n_prows,
+                    const int32_t* p_ptr, const int32_t* p_inc, const int32_t* B_ptr,
+                    const int32_t* B_col, double* B, hipStream_t s) {
   if (n_cols > 0) {
     hipLaunchKernelGGL(k_bt_coltab, dim3(n_cols), dim3(kBtColEntries), 0, s, cd.sep_colgeo, P);
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (n_tasks > 0) {
-    hipLaunchKernelGGL(k_bt_tasks, dim3((bt_task_waves(n_tasks) + kBtRowWaves - 1) / kBtRowWaves),
-                       dim3(64 * kBtRowWaves), 0, s, cd, n_tasks,
-                       reinterpret_cast<const int4*>(task_hdr),
+    hipLaunchKernelGGL(slots == 16 ? k_bt_tasks<16> : k_bt_tasks<8>,
+                       dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves), dim3(64 * kBtRowWaves), 0,
+                       s, cd, n_tasks, reinterpret_cast<const int4*>(task_hdr),
                        reinterpret_cast<const int4*>(slot_rec), P, Bt);
     DCP_HIP_CHECK(hipGetLastError());
   }
