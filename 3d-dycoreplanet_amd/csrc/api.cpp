@@ -714,14 +714,14 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
   for (int p = 0; p < n_p; ++p) h.Sp[p + 1] = h.Sp[p] + int32_t(srow[p].size());
   h.Sc.resize(size_t(h.Sp[n_p]));
   // S_max_row also bounds the B rows' node counts: k_schur_form stages a
-  // row's nodes in LDS (one wave per row, one lane per B^T row entry)
+  // row's nodes in LDS (one wave per row, one half-wave lane per B^T row entry)
   h.S_max_row = 0;
   for (int p = 0; p < n_p; ++p) {
     std::copy(srow[p].begin(), srow[p].end(), h.Sc.begin() + h.Sp[p]);
     h.S_max_row = std::max({h.S_max_row, int(srow[p].size()), h.Bp[p + 1] - h.Bp[p]});
   }
   for (size_t n = 0; n + 1 < h.Btp.size(); ++n)
-    require(h.Btp[n + 1] - h.Btp[n] <= 64, DCP_ERR_UNSUPPORTED, "B^T rows above 64 entries");
+    require(h.Btp[n + 1] - h.Btp[n] <= 32, DCP_ERR_UNSUPPORTED, "B^T rows above 32 entries");
 }
 
 }  // namespace

@@ -1281,10 +1281,11 @@ __global__ void k_clear_first_touch(size_t n, int32_t* __restrict__ pos) {
 // S_pq = sum_n sum_c B[p][n][c] d[3n+c] B^T[n][q][c]; one wave per pressure
 // row. The row's nodes (n, the weights B[p][n][c] d[3n+c], the B^T row range)
 // are staged in LDS first, all lanes at once; then the node loop runs in node
-// order, kSchurU nodes per iteration with their B^T loads issued together,
-// each lane one entry q of a node's B^T row (distinct q per node: the adds
-// into the row's accumulators keep node order, and one wave needs no barrier
-// between nodes). Every entry is summed in the same (node) order as before.
+// order, 2 kSchurU nodes per iteration (one per half-wave) with their B^T
+// loads and column searches issued together, each lane one entry q of a
+// node's B^T row (distinct q per node: the adds into the row's accumulators
+// keep node order, and one wave needs no barrier between nodes). Every entry
+// is summed in the same (node) order as before.
 constexpr int kSchurU = 4;
 __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __restrict__ B_ptr,
                                                    const int32_t* __restrict__ B_col,
@@ -1332,25 +1333,35 @@ __global__ __launch_bounds__(64) void k_schur_form(int n_p, const int32_t* __res
     }
     return lo;
   };
-  for (int i0 = 0; i0 < nb; i0 += kSchurU) {
-    int q[kSchurU];
-    double bv[kSchurU][3];
+  // half-waves: nodes i0 + 2u (lanes 0-31) and i0 + 2u + 1 (lanes 32-63), one
+  // lane per B^T row entry (<= 32); the two halves' adds run one after the
+  // other, so node order is kept
+  const int half = lane >> 5, hl = lane & 31;
+  for (int i0 = 0; i0 < nb; i0 += 2 * kSchurU) {
+    int q[kSchurU], pos[kSchurU];
+    double val[kSchurU];
 #pragma unroll
     for (int u = 0; u < kSchurU; ++u) {
-      const int i = i0 + u;
-      const bool on = i < nb && lane < rn[i < nb ? i : 0];
-      const int j = on ? rb[i] + lane : 0;
+      const int i = i0 + 2 * u + half;
+      const bool on = i < nb && hl < rn[i < nb ? i : 0];
+      const int j = on ? rb[i] + hl : 0;
       q[u] = on ? Bt_col[j] : -1;
-      bv[u][0] = on ? Bt_val[3 * size_t(j)] : 0.0;
-      bv[u][1] = on ? Bt_val[3 * size_t(j) + 1] : 0.0;
-      bv[u][2] = on ? Bt_val[3 * size_t(j) + 2] : 0.0;
+      const double b0 = on ? Bt_val[3 * size_t(j)] : 0.0;
+      const double b1 = on ? Bt_val[3 * size_t(j) + 1] : 0.0;
+      const double b2 = on ? Bt_val[3 * size_t(j) + 2] : 0.0;
+      val[u] = on ? wv[3 * i] * b0 + wv[3 * i + 1] * b1 + wv[3 * i + 2] * b2 : 0.0;
     }
 #pragma unroll
+    for (int u = 0; u < kSchurU; ++u) pos[u] = q[u] >= 0 ? find(q[u]) : 0;
+    // node 2u (half 0) before node 2u + 1 (half 1): two masked read-modify-
+    // writes kept apart (a merged one would lose an update where both halves
+    // hit the same column)
+#pragma unroll
     for (int u = 0; u < kSchurU; ++u) {
-      if (q[u] < 0) continue;
-      const int i = i0 + u;
-      const double v = wv[3 * i] * bv[u][0] + wv[3 * i + 1] * bv[u][1] + wv[3 * i + 2] * bv[u][2];
-      acc[find(q[u])] += v;
+      if (half == 0 && q[u] >= 0) acc[pos[u]] += val[u];
+      __builtin_amdgcn_wave_barrier();
+      if (half == 1 && q[u] >= 0) acc[pos[u]] += val[u];
+      __builtin_amdgcn_wave_barrier();
     }
   }
   __syncthreads();
