@@ -2010,8 +2010,11 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     const double* __restrict__ P, double* __restrict__ Bt) {
   constexpr int R = SL / 8;  // slot records per lane
   __shared__ double vals[kBtRowWaves][R * 64 * 3];
-  __shared__ int dst_e[kBtRowWaves][R * 64];
-  __shared__ int rowl[kBtRowWaves][R * 64];
+  // per (slot, task entry) the slot's vertex contributing to that entry, or
+  // 0xff: the entry lanes read their contributions slot by slot (no scan over
+  // every (slot, vertex) pair)
+  __shared__ uint8_t vof[kBtRowWaves][SL][64];
+  __shared__ int rowl[kBtRowWaves][SL];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int task = int(blockIdx.x) * kBtRowWaves + wave;
   if (task >= n_tasks) return;
@@ -2024,33 +2027,40 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
   for (int i = 0; i < R; ++i) r[i] = rec[SL * size_t(task) + 8 * i + k];
   const int ns = h.z & 255, ne = h.z >> 8;
 #pragma unroll
+  for (int i = 0; i < R; ++i)
+    reinterpret_cast<unsigned long long*>(&vof[wave][8 * i][0])[lane] = ~0ull;
+  wsync();
+#pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int e = 64 * i + lane;  // = 8 slot + v
-    int de = -1;
-    if (8 * i + k < ns) {
+    const int sl = 8 * i + k, e = 64 * i + lane;  // e = 8 slot + v
+    if (sl < ns) {
       const unsigned long long dm =
           (unsigned long long)(unsigned)r[i].z | ((unsigned long long)(unsigned)r[i].w << 32);
-      de = int((dm >> (6 * v)) & 63);
+      vof[wave][sl][int((dm >> (6 * v)) & 63)] = uint8_t(v);
       double ev[3];
       bt_entry(cd, P, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
       vals[wave][3 * e] = ev[0];
       vals[wave][3 * e + 1] = ev[1];
       vals[wave][3 * e + 2] = ev[2];
-      rowl[wave][e] = r[i].y & 255;
+      if (v == 0) rowl[wave][sl] = r[i].y & 255;
     }
-    dst_e[wave][e] = de;
   }
   wsync();
   if (lane >= ne) return;
+  // entry `lane`: its contributions in slot order (the row's cells in colour
+  // order), the same order as a scan over (slot, vertex)
   double acc[3] = {0.0, 0.0, 0.0};
   int rl = 0;
-  for (int e = 0; e < 8 * ns; ++e)
-    if (dst_e[wave][e] == lane) {
+  for (int sl = 0; sl < ns; ++sl) {
+    const int vv = vof[wave][sl][lane];
+    if (vv != 0xff) {
+      const int e = 8 * sl + vv;
       acc[0] += vals[wave][3 * e];
       acc[1] += vals[wave][3 * e + 1];
       acc[2] += vals[wave][3 * e + 2];
-      rl = rowl[wave][e];
+      rl = rowl[wave][sl];
     }
+  }
   double Ca[3][3];
   condensation(cd.vcon[h.y + rl], Ca);
   double* dst = Bt + 3 * size_t(h.x + lane);

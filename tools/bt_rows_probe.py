@@ -18,10 +18,10 @@ u = np.zeros(m.n_u + m.n_p)
 u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
 out = {"refine": R}
 res = {}
-for variant, env in (("1", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "16"}),
-                     ("8", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "8"}),
-                     ("h", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "0", "DCP_BT_SLOTS": "16"}),
-                     ("0", {"DCP_BT_ROWS": "0", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "16"})):
+for variant, env in (("1", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "8"}),
+                     ("16", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "16"}),
+                     ("h", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "0", "DCP_BT_SLOTS": "8"}),
+                     ("0", {"DCP_BT_ROWS": "0", "DCP_ASM_RHS_CELL_ORDER": "1", "DCP_BT_SLOTS": "8"})):
     os.environ.update(env)
     ctx = dcp.Context()
     ctx.set_physics(dcp.classic_physics())
@@ -34,7 +34,7 @@ for variant, env in (("1", {"DCP_BT_ROWS": "1", "DCP_ASM_RHS_CELL_ORDER": "1", "
         ms.append(ctx.timings()["assemble_nse_ms"])
     rp, ci, v = ctx.coupling_csr("Bt")
     res[variant] = (v, ctx.get_state(dcp.NSE_RHS))
-    out[{"1": "ms_bt_rows", "8": "ms_bt_rows_8_slots", "h": "ms_bt_rows_halfwave_rhs",
+    out[{"1": "ms_bt_rows", "16": "ms_bt_rows_16_slots", "h": "ms_bt_rows_halfwave_rhs",
          "0": "ms_cell_scatter"}[variant]] = \
         [round(x, 4) for x in ms]
     ctx.close()
@@ -43,5 +43,5 @@ out["bt_rel_max"] = float(np.max(np.abs(v1 - v0)) / np.max(np.abs(v0)))
 out["rhs_bitwise"] = bool(np.array_equal(r1, r0))
 out["rhs_rel_max"] = float(np.max(np.abs(r1 - r0)) / np.max(np.abs(r0)))
 out["rhs_halfwave_bitwise_cell_scatter"] = bool(np.array_equal(res["h"][1], r0))
-out["bt_16_bitwise_8_slots"] = bool(np.array_equal(res["1"][0], res["8"][0]))
+out["bt_16_bitwise_8_slots"] = bool(np.array_equal(res["1"][0], res["16"][0]))
 print(json.dumps(out), flush=True)
