@@ -2220,6 +2220,24 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                 c.con_color_ptr.push_back(int(sub.size()));
               }
               c.con_color_cells.upload(sub);
+              // one launch over the list: per (list cell, node) of a constrained
+              // node its slot, slots of a node in list (= colour) order
+              std::vector<int32_t> cptr(size_t(n_con) + 1, 0), cslot(27 * sub.size(), -1);
+              for (const int cell : sub)
+                for (int t = 0; t < 27; ++t) {
+                  const int ci = cidx[size_t(q2[27 * size_t(cell) + t])];
+                  if (ci >= 0) cptr[size_t(ci) + 1]++;
+                }
+              for (int i = 0; i < n_con; ++i) cptr[i + 1] += cptr[i];
+              std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+              for (size_t k = 0; k < sub.size(); ++k)
+                for (int t = 0; t < 27; ++t) {
+                  const int ci = cidx[size_t(q2[27 * size_t(sub[k]) + t])];
+                  if (ci >= 0) cslot[27 * k + t] = fill[size_t(ci)]++;
+                }
+              c.con_cptr.upload(cptr);
+              c.con_cslot.upload(cslot);
+              c.con_cbuf.alloc(3 * size_t(std::max(cptr[n_con], 1)));
             }
             c.bt_ncols = int(c.mf_colgeo.n / 90);
             c.bt_P.alloc(size_t(216) * c.bt_ncols);
@@ -2528,12 +2546,18 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     const bool rhs_subset = bt_rows && !c.rhs_color_ptr.empty();
-    for (int k = 0; k < c.n_colors() && !(rhs_co && !out.cdiag); ++k) {
-      if (rhs_co)  // the constrained-row diagonals only
-        launch_nse_operator(c.cd(), c.maps(), c.con_color_cells.p + c.con_color_ptr[k],
-                            c.con_color_ptr[k + 1] - c.con_color_ptr[k], c.old_nse.p, c.old_T.p,
-                            c.ph, out, c.stream);
-      else if (full)
+    if (rhs_co && out.cdiag) {
+      // the constrained-row diagonals only: the cells with a constrained node
+      // in one launch, per (cell, node) slots, summed per node in colour order
+      NseOut oc = out;
+      oc.cbuf = c.con_cbuf.p;
+      oc.cslot = c.con_cslot.p;
+      launch_nse_operator(c.cd(), c.maps(), c.con_color_cells.p, c.con_color_ptr.back(),
+                          c.old_nse.p, c.old_T.p, c.ph, oc, c.stream);
+      con_gather(c.n_con, c.con_cptr.p, c.con_cbuf.p, c.con_diag.p, c.stream);
+    }
+    for (int k = 0; k < c.n_colors() && !rhs_co; ++k) {
+      if (full)
         launch_nse_system(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.old_nse.p,
                           c.old_T.p, c.ph, out, c.stream, c.element_mfma);
       else if (rhs_subset)

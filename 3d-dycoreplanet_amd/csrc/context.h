@@ -142,6 +142,8 @@ struct Ctx {
   bool rhs_cell_order = false;
   std::vector<int> con_color_ptr;
   DBuf<int32_t> con_color_cells;
+  DBuf<int32_t> con_cptr, con_cslot;  // slots of the constrained diagonals (con_gather)
+  DBuf<double> con_cbuf;
   DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
   DBuf<double> bt_P;  // [n_cols][216] column factors, formed every assembly
   int bt_ncols = 0;

@@ -97,7 +97,15 @@ struct NseOut {
   // the same for the identified (periodic) pressure dofs: [n_p] index or -1
   double* pcdiag;
   const int32_t* pcidx;
+  // k_nse_rhs_halfwave over one list of cells (the cells with a constrained
+  // node, colour order): each (list cell k, node t) of a constrained node
+  // stores its |K_ii| triple at cbuf[3 cslot[27 k + t]] instead of adding into
+  // cdiag; con_gather then sums them per node in list order (null: add)
+  double* cbuf = nullptr;
+  const int32_t* cslot = nullptr;
 };
+// cdiag[3 i + c] = sum over slots [cptr[i], cptr[i + 1]) of cbuf[3 slot + c]
+void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdiag, hipStream_t s);
 
 // ---- assembly2d.hip -----------------------------------------------------------
 // Two-dimensional model (Standard::BoussinesqModel<2>): 22-dof cells over a

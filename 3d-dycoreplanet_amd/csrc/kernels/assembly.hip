@@ -1916,14 +1916,35 @@ __global__ __launch_bounds__(256) void k_nse_rhs_halfwave(
       double avg = 0;
       for (int m = 0; m < 27; ++m) avg += sh.diag[m];
       avg /= 89.0;
+      double* slot = out.cbuf ? out.cbuf + 3 * size_t(out.cslot[27 * size_t(k) + an]) : nullptr;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        if (nc.type == 1 || nc.type == 3 || c == nc.k) {
-          const double d = fabs(kii[c]);
+      for (int c = 0; c < 3; ++c) {
+        const bool on = nc.type == 1 || nc.type == 3 || c == nc.k;
+        const double d = fabs(kii[c]);
+        if (slot)
+          slot[c] = on ? (d != 0.0 ? d : avg) : 0.0;
+        else if (on)
           out.cdiag[3 * size_t(ci) + c] += d != 0.0 ? d : avg;
-        }
+      }
     }
   }
+}
+
+// the constrained-row diagonals from their per-cell slots, in slot (= the
+// cells' colour) order: the sums the per-colour additions formed
+__global__ void k_con_gather(int n_con, const int32_t* __restrict__ cptr,
+                             const double* __restrict__ cbuf, double* __restrict__ cdiag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_con) return;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int k = cptr[i]; k < cptr[i + 1]; ++k) {
+    s0 += cbuf[3 * size_t(k)];
+    s1 += cbuf[3 * size_t(k) + 1];
+    s2 += cbuf[3 * size_t(k) + 2];
+  }
+  cdiag[3 * size_t(i)] = s0;
+  cdiag[3 * size_t(i) + 1] = s1;
+  cdiag[3 * size_t(i) + 2] = s2;
 }
 
 // ---------------------------------------------------------------------------
@@ -2117,6 +2138,13 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_b_rows(
 }
 
 }  // namespace
+
+void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdiag, hipStream_t s) {
+  if (n_con <= 0) return;
+  hipLaunchKernelGGL(k_con_gather, dim3((n_con + 255) / 256), dim3(256), 0, s, n_con, cptr, cbuf,
+                     cdiag);
+  DCP_HIP_CHECK(hipGetLastError());
+}
 
 void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_t* cells, int n,
                          const double* u_old, const double* T_old, const PhysicsDev& ph,
