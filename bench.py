@@ -56,8 +56,9 @@ CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
                (5, "sstep"): "profiles/r04i_inner_r5_structured_kernel_stats.csv"}
 # the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
 # launches per assembly (the rhs kernel once per colour class)
-PMC_ASM = {5: ("profiles/r04j_pmc_asm_r5.json",
-               {"k_bt_tasks": 1, "k_bt_coltab": 1, "k_nse_rhs_halfwave": 8})}
+PMC_ASM = {5: ("profiles/r04r_pmc_asm_r5.json",
+               {"k_bt_tasks": 1, "k_bt_coltab": 1, "k_mf_pencil": 1, "k_mf_gather": 1,
+                "k_nse_rhs_halfwave": 1, "k_con_gather": 1})}
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
 PMC_MF = {5: ("profiles/r04j_pmc_mf_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
 
@@ -717,8 +718,9 @@ def main():
         asm_bytes /= world
     asm_ach = asm_bytes / (asm_ms * 1e-3) / 1e9
     out["roofline_assembly"] = {
-        "kernel": "operator-form assemble_nse_system (B^T by row tasks k_bt_tasks + rhs / "
-                  "constrained diagonal k_nse_rhs_halfwave per colour)",
+        "kernel": "operator-form assemble_nse_system (B^T by row tasks k_bt_tasks, the rhs "
+                  "by the pencil kernel + velocity gather, the constrained diagonals by "
+                  "k_nse_rhs_halfwave over the constrained cells + k_con_gather)",
         "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
         "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None,

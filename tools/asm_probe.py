@@ -1,6 +1,5 @@
-"""Times assemble_nse_system at refine R (default 5) and prints a checksum of
-the assembled matrix at refine 3 (to compare kernel variants bit for bit)."""
-import hashlib
+"""assemble_nse_system at refine R (default 5) with the default options, six
+times (a PMC / kernel-statistics target: one configuration only)."""
 import json
 import os
 import sys
@@ -10,28 +9,19 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import numpy as np  # noqa: E402
 import dcp  # noqa: E402
 
-
-def run(refine, reps, export=False):
-    m = dcp.HostMesh(refine=refine)
-    ctx = dcp.Context(device=0)
-    ctx.set_physics(dcp.classic_physics())
-    ctx.upload_mesh(m)
-    ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
-    ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
-    ms = []
-    for _ in range(reps):
-        ctx.assemble_nse_system()
-        ms.append(ctx.timings()["assemble_nse_ms"])
-    h = None
-    if export:
-        rp, ci, v = ctx.nse_matrix_csr()
-        h = hashlib.sha1(np.ascontiguousarray(v).tobytes()).hexdigest()[:16]
-        h += "/" + hashlib.sha1(ctx.get_state(dcp.NSE_RHS).tobytes()).hexdigest()[:8]
-    ctx.close()
-    return ms, h
-
-
-ms3, h3 = run(3, 2, export=True)
-ms, _ = run(int(os.environ.get("R", "5")), 4)
-print(json.dumps({"variant": os.environ.get("DCP_ASM_WRITE", "0"), "ms": ms, "hash_r3": h3}),
-      flush=True)
+R = int(os.environ.get("R", "5"))
+m = dcp.HostMesh(refine=R)
+rng = np.random.default_rng(1)
+u = np.zeros(m.n_u + m.n_p)
+u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+ctx = dcp.Context()
+ctx.set_physics(dcp.classic_physics())
+ctx.upload_mesh(m)
+ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+ms = []
+for _ in range(6):
+    ctx.assemble_nse_system()
+    ms.append(round(ctx.timings()["assemble_nse_ms"], 4))
+ctx.close()
+print(json.dumps({"refine": R, "assemble_nse_ms": ms}), flush=True)
