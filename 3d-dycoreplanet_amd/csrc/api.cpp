@@ -2093,6 +2093,21 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           c.mf_laygeo.upload(laygeo);
           c.mf_colphi.upload(colphi);
           c.mf_layR.upload(layR);
+          // the rhs gravity -g x / den(|x|), x = R Phi, den(r) = r (r > 1) or
+          // sqrt(r): per column point |Phi|, 1 / |Phi|, 1 / sqrt|Phi|, per
+          // layer point sqrt(R) (k_mf_pencil<.., RHS>: no square root or
+          // division on the device)
+          std::vector<double> pn(colphi.size()), rs(layR.size());
+          for (size_t i = 0; i < colphi.size() / 3; ++i) {
+            const double* f = &colphi[3 * i];
+            const double a = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+            pn[3 * i] = a;
+            pn[3 * i + 1] = 1.0 / a;
+            pn[3 * i + 2] = 1.0 / std::sqrt(a);
+          }
+          for (size_t i = 0; i < layR.size(); ++i) rs[i] = std::sqrt(layR[i]);
+          c.mf_colphin.upload(pn);
+          c.mf_layRs.upload(rs);
         } else {
           // general mesh: J^-1 / JxW per Gauss point, tree order (2160 B per cell)
           c.mf_geo_tree.alloc(size_t(n_cells) * 270);
@@ -2239,8 +2254,12 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
               c.con_cslot.upload(cslot);
               c.con_cbuf.alloc(3 * size_t(std::max(cptr[n_con], 1)));
             }
+            // the column factors P of the B^T entries are mesh geometry
+            // (the column tables, reference functions): formed once here
             c.bt_ncols = int(c.mf_colgeo.n / 90);
             c.bt_P.alloc(size_t(216) * c.bt_ncols);
+            launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, 0, c.bt_slots, nullptr, nullptr, nullptr,
+                           0, nullptr, nullptr, nullptr, nullptr, nullptr, c.stream);
             c.bt_rows = true;
           }
         }
@@ -2579,7 +2598,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
     if (bt_rows)
-      launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
+      launch_bt_rows(c.cd(), 0, c.bt_P.p, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
                      c.bt_slot_rec.p,
                      c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p, c.bt_p_inc.p, c.B_ptr.p,
                      c.B_col.p, c.B_transpose ? nullptr : c.B_val.p, c.stream);

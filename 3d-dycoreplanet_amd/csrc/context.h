@@ -273,13 +273,14 @@ struct Ctx {
   hipStream_t mf_stream = nullptr;
   hipEvent_t mf_chunk_ev[kMfChunksMax] = {}, mf_join_ev = nullptr;
   DBuf<int32_t> mf_col, mf_layer;
-  DBuf<double> mf_colgeo, mf_laygeo, mf_colphi, mf_layR;
+  DBuf<double> mf_colgeo, mf_laygeo, mf_colphi, mf_layR, mf_colphin, mf_layRs;
   bool mf_separable = false;
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
                    mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p, mf_vnext.p,
                    mf_pslot.p, mf_separable ? mf_col.p : nullptr,
-                   mf_colgeo.p, mf_layer.p, mf_laygeo.p, cell_T.p, mf_colphi.p, mf_layR.p};
+                   mf_colgeo.p, mf_layer.p, mf_laygeo.p, cell_T.p, mf_colphi.p, mf_layR.p,
+                   mf_colphin.p, mf_layRs.p};
   }
   MfGather mfg() const {
     // one chunk: the gather order is the identity (no order arrays read)

@@ -207,6 +207,8 @@ struct MfCells {
   const int32_t* cell_T = nullptr;  // [n_cells][8]
   const double* colphi = nullptr;   // [n_cols][9][3]
   const double* layR = nullptr;     // [n_layers][3]
+  const double* colphin = nullptr;  // [n_cols][9][|Phi|, 1/|Phi|, 1/sqrt|Phi|]
+  const double* layRs = nullptr;    // [n_layers][3] sqrt(R)
 };
 struct MfGather {
   int n_vnodes, n_p, n_u;
@@ -296,7 +298,8 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (then the assembly stores first and needs no zero fill), else the
 // positions are left plain.
 // B^T of the operator-form assembly on the radially separable shell
-// (assembly.hip k_bt_coltab + k_bt_tasks): P = [n_cols][216] scratch;
+// (assembly.hip k_bt_coltab + k_bt_tasks): P = [n_cols][216] column factors,
+// formed when n_cols > 0 (once, at upload: geometry only);
 // task_hdr [n_tasks][4] / slot_rec [slots][4]: runs of consecutive velocity
 // node rows (<= 8 (row, cell) slots, <= 64 entries) built at upload
 // (api.cpp build_bt_tasks). Writes every B^T entry once. B != null (several

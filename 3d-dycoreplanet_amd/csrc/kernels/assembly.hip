@@ -1755,22 +1755,26 @@ __global__ __launch_bounds__(256) void k_nse_rhs_halfwave(
   const bool want_cdiag = out.cdiag != nullptr;
   // ---- state and geometry (lanes 0-26: nodes / points)
   bool con = false;
+  // without the rhs (the constrained diagonals only) the state is not read
+  const bool want_rhs = out.rhs != nullptr;
   if (live && hl < 27) {
     const int nd = cd.cell_q2[27 * size_t(cell) + hl];
     sh.node[hl] = nd;
+    if (want_rhs) {
 #pragma unroll
-    for (int d = 0; d < 3; ++d) sh.U[3 * hl + d] = u_old[3 * size_t(nd) + d];
-    if (cd.tdpc == 27) sh.T[hl] = T_old[cd.cell_T[27 * size_t(cell) + hl]];
+      for (int d = 0; d < 3; ++d) sh.U[3 * hl + d] = u_old[3 * size_t(nd) + d];
+      if (cd.tdpc == 27) sh.T[hl] = T_old[cd.cell_T[27 * size_t(cell) + hl]];
+    }
     sep_geometry(cd, cell, sh.geo, hl);
     con = want_cdiag && out.cidx[nd] >= 0;
   }
-  if (live && cd.tdpc == 8 && hl < 8) sh.T[hl] = T_old[cd.cell_T[8 * size_t(cell) + hl]];
+  if (want_rhs && live && cd.tdpc == 8 && hl < 8) sh.T[hl] = T_old[cd.cell_T[8 * size_t(cell) + hl]];
   // this half's cell has a constrained node
   const unsigned long long bal = __ballot(con);
   const bool cell_con = ((bal >> (32 * ((threadIdx.x >> 5) & 1))) & 0xffffffffull) != 0;
   wsync();
   // ---- rhs integrand per Gauss point (k_nse_operator_wave's formulas)
-  if (live && hl < 27) {
+  if (want_rhs && live && hl < 27) {
     const int q = hl;
     const double xa = sel_gauss(q % 3), xb = sel_gauss((q / 3) % 3), xc = sel_gauss(q / 9);
     const double* Ji = &sh.geo.Ji[9 * q];
@@ -1871,9 +1875,11 @@ __global__ __launch_bounds__(256) void k_nse_rhs_halfwave(
         for (int q0 = 0; q0 < 3; ++q0) {
           const int q = q0 + 3 * q1 + 9 * q2;
           const double s = La[q0] * lb * lc;
-          fa[0] += s * sh.F[3 * q];
-          fa[1] += s * sh.F[3 * q + 1];
-          fa[2] += s * sh.F[3 * q + 2];
+          if (want_rhs) {
+            fa[0] += s * sh.F[3 * q];
+            fa[1] += s * sh.F[3 * q + 1];
+            fa[2] += s * sh.F[3 * q + 2];
+          }
           if (cell_con) {
             const double r0 = Da1[q0] * lb * lc;
             const double r1 = La[q0] * db * lc;
@@ -1958,8 +1964,8 @@ __global__ void k_con_gather(int n_con, const int32_t* __restrict__ cptr,
 //   P01 = sum_xy w w psi_i psi_j D2 (m0[d] l'_a l_b + m1[d] l_a l'_b)
 //   P2  = sum_xy w w psi_i psi_j D2 m2[d] l_a l_b
 //   Q01 = sum_z w R^2 R' / R l_c psi_k,   Q2 = sum_z w R^2 R' / R' l'_c psi_k.
-// k_bt_coltab forms P per column (216 values) from the column table every
-// assembly. k_bt_tasks then writes B^T by tasks: a task is a run of consecutive
+// k_bt_coltab forms P per column (216 values) from the column table once at
+// upload (mesh geometry). k_bt_tasks then writes B^T by tasks: a task is a run of consecutive
 // velocity node rows with at most 8 (row, cell) slots and 64 row entries in
 // all, so the task's entries are one contiguous piece of the B^T values. Lane
 // (slot k, vertex v) evaluates that cell's contribution and knows (from the

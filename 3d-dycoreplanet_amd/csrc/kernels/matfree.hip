@@ -450,15 +450,6 @@ __device__ inline void bwd(const Tab3& T, const double in[3], double out[3]) {
   for (int n = 0; n < 3; ++n) out[n] = T.v[n][0] * in[0] + T.v[n][1] * in[1] + T.v[n][2] * in[2];
 }
 
-// -g R / den(R |Phi|) with den(r) = r for r > 1, else sqrt(r): the gravity
-// x -> -g x / den(|x|) of the reference's rhs at x = R Phi, as a factor of Phi
-// (outside the point loop: the square roots and the division would otherwise
-// be interleaved over the unrolled points, +130 VGPRs)
-__device__ __noinline__ double rhs_gravity(double g, double R, const double rphi[3]) {
-  const double x0 = R * rphi[0], x1 = R * rphi[1], x2 = R * rphi[2];
-  const double r = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
-  return -g * R / (r > 1 ? r : sqrt(r));
-}
 // the NSE rhs flux of one Gauss point (k_mf_pencil<.., RHS>): value u,
 // reference gradients Gh[c][e], J^-1 ji (rows e), JxW wq, temperature Tq,
 // position R Phi (separable shell; cuboid: constant gravity), added to the
@@ -478,7 +469,7 @@ __device__ __forceinline__ void rhs_flux(const PhysicsDev& ph, const double u[3]
     grav[0] = grav[1] = 0;
     grav[2] = -ph.g;
   } else {
-    // -g x / den(|x|) with x = R Phi: gs = -g R / den(R |Phi|) (rhs_gravity)
+    // -g x / den(|x|) with x = R Phi: gs = -g R / den(R |Phi|) (MfCells::colphin)
     grav[0] = gs * rphi[0];
     grav[1] = gs * rphi[1];
     grav[2] = gs * rphi[2];
@@ -713,8 +704,14 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   if (RHS && SEP && !ph.cuboid) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) rphi[d] = mc.colphi[27 * size_t(colc) + 3 * p + d];
-#pragma unroll 1
-    for (int q = 0; q < 3; ++q) rR[q] = rhs_gravity(ph.g, mc.layR[3 * size_t(layc) + q], rphi);
+    // -g R / den(R |Phi|): -g / |Phi| where R |Phi| > 1, else -g sqrt(R) / sqrt|Phi|
+    const double* pn = mc.colphin + 27 * size_t(colc) + 3 * p;
+    const double am = pn[0], ai = pn[1], asi = pn[2];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double R = mc.layR[3 * size_t(layc) + q];
+      rR[q] = R * am > 1 ? -ph.g * ai : -ph.g * mc.layRs[3 * size_t(layc) + q] * asi;
+    }
   }
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
