@@ -1,4 +1,5 @@
-# round 4: B^T task kernel, per-slot vertex table (no scan over all (slot,
+# round 4: assembly variants (bitwise / time), kernel split, parity files;
+# (earlier: B^T task kernel, per-slot vertex table (no scan over all (slot,
 # vertex) pairs) against the scan (bitwise, assembly time); kernel split;
 # parity files
 set -o pipefail
