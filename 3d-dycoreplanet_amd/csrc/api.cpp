@@ -2257,9 +2257,12 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             // the column factors P of the B^T entries are mesh geometry
             // (the column tables, reference functions): formed once here
             c.bt_ncols = int(c.mf_colgeo.n / 90);
-            c.bt_P.alloc(size_t(216) * c.bt_ncols);
-            launch_bt_rows(c.cd(), c.bt_ncols, c.bt_P.p, 0, c.bt_slots, nullptr, nullptr, nullptr,
-                           0, nullptr, nullptr, nullptr, nullptr, nullptr, c.stream);
+            const int nlay = int(c.mf_laygeo.n / 9);
+            c.bt_P.alloc(size_t(216) * c.bt_ncols + size_t(12) * nlay);
+            c.bt_Q = c.bt_P.p + size_t(216) * c.bt_ncols;
+            launch_bt_rows(c.cd(), c.bt_ncols, nlay, c.bt_P.p, c.bt_Q, 0, c.bt_slots, nullptr,
+                           nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           c.stream);
             c.bt_rows = true;
           }
         }
@@ -2598,7 +2601,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
     if (bt_rows)
-      launch_bt_rows(c.cd(), 0, c.bt_P.p, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
+      launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
                      c.bt_slot_rec.p,
                      c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p, c.bt_p_inc.p, c.B_ptr.p,
                      c.B_col.p, c.B_transpose ? nullptr : c.B_val.p, c.stream);

@@ -145,7 +145,8 @@ struct Ctx {
   DBuf<int32_t> con_cptr, con_cslot;  // slots of the constrained diagonals (con_gather)
   DBuf<double> con_cbuf;
   DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
-  DBuf<double> bt_P;  // [n_cols][216] column factors, formed every assembly
+  DBuf<double> bt_P;  // [n_cols][216] column factors, then [n_layers][12] layer factors (upload)
+  double* bt_Q = nullptr;
   int bt_ncols = 0;
   // blocks some cell's scatter position reaches (first-touch marking at upload)
   unsigned long long touched_A = 0, touched_Bt = 0, touched_B = 0;

@@ -298,17 +298,18 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (then the assembly stores first and needs no zero fill), else the
 // positions are left plain.
 // B^T of the operator-form assembly on the radially separable shell
-// (assembly.hip k_bt_coltab + k_bt_tasks): P = [n_cols][216] column factors,
-// formed when n_cols > 0 (once, at upload: geometry only);
+// (assembly.hip k_bt_coltab + k_bt_tasks): P = [n_cols][216] column factors
+// and Q = [n_layers][12] layer factors, formed when n_cols / n_layers > 0
+// (once, at upload: geometry only);
 // task_hdr [n_tasks][4] / slot_rec [slots][4]: runs of consecutive velocity
 // node rows (<= 8 (row, cell) slots, <= 64 entries) built at upload
 // (api.cpp build_bt_tasks). Writes every B^T entry once. B != null (several
 // GPUs): also B by pressure rows (k_b_rows; p_inc: cell << 3 | vertex), bitwise
 // the transpose of B^T.
-void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, int slots,
-                    const int32_t* task_hdr, const int32_t* slot_rec, double* Bt, int n_prows,
-                    const int32_t* p_ptr, const int32_t* p_inc, const int32_t* B_ptr,
-                    const int32_t* B_col, double* B, hipStream_t s);
+void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, double* Q,
+                    int n_tasks, int slots, const int32_t* task_hdr, const int32_t* slot_rec,
+                    double* Bt, int n_prows, const int32_t* p_ptr, const int32_t* p_inc,
+                    const int32_t* B_ptr, const int32_t* B_col, double* B, hipStream_t s);
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
                       int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
                       unsigned long long* touched_out = nullptr);

@@ -1997,27 +1997,41 @@ __global__ __launch_bounds__(kBtColEntries) void k_bt_coltab(const double* __res
   P[kBtColEntries * size_t(col) + t] = s;
 }
 
-// the (node lex, vertex v) contribution of a cell in column-table entry col
-// and layer lay, components d = 0..2
-__device__ inline void bt_entry(const CellData& cd, const double* __restrict__ P, int col, int lay,
-                                int lex, int v, double out[3]) {
-  const int a = lex % 3, b = (lex / 3) % 3, c = lex / 9;
-  const int i = v & 1, j = (v >> 1) & 1, k = v >> 2;
-  const double* lg = cd.sep_laygeo + 9 * size_t(lay);
-  double q01 = 0.0, q2 = 0.0;
+// the layer factors Q01, Q2 of (node layer c, vertex layer k) for layer lay:
+// [lay][c][k][Q01 | Q2], formed once at upload (k_bt_laytab)
+constexpr int kBtLayEntries = 12;
+__device__ inline double bt_layer_factor(const double* __restrict__ lg, int c, int k, bool d2) {
+  double q = 0.0;
 #pragma unroll
   for (int z = 0; z < 3; ++z) {
     const double wz = cW[z] * lg[3 * z + 2] * cL1[k][z];
-    q01 += wz * lg[3 * z] * cL2[c][z];
-    q2 += wz * lg[3 * z + 1] * cdL2[c][z];
+    q += d2 ? wz * lg[3 * z + 1] * cdL2[c][z] : wz * lg[3 * z] * cL2[c][z];
   }
+  return q;
+}
+__global__ __launch_bounds__(kBtLayEntries) void k_bt_laytab(const double* __restrict__ laygeo,
+                                                             double* __restrict__ Q) {
+  const int lay = blockIdx.x, t = threadIdx.x;
+  Q[kBtLayEntries * size_t(lay) + t] =
+      bt_layer_factor(laygeo + 9 * size_t(lay), t / 4, (t / 2) % 2, t % 2 == 1);
+}
+
+// the (node lex, vertex v) contribution of a cell in column-table entry col
+// and layer lay, components d = 0..2
+__device__ inline void bt_entry(const double* __restrict__ P, const double* __restrict__ Q, int col,
+                                int lay, int lex, int v, double out[3]) {
+  const int a = lex % 3, b = (lex / 3) % 3, c = lex / 9;
+  const int i = v & 1, j = (v >> 1) & 1, k = v >> 2;
+  const double* qq = Q + kBtLayEntries * size_t(lay) + 4 * c + 2 * k;
+  const double q01 = qq[0], q2 = qq[1];
   const double* pp = P + kBtColEntries * size_t(col) + 6 * (2 * (3 * a + b) + i) + 3 * j;
 #pragma unroll
   for (int d = 0; d < 3; ++d) out[d] = -(pp[d] * q01 + pp[108 + d] * q2);
 }
-__device__ inline void bt_cell_entry(const CellData& cd, const double* __restrict__ P, int cell,
-                                     int lex, int v, double out[3]) {
-  bt_entry(cd, P, cd.sep_col[cell], cd.sep_layer[cell], lex, v, out);
+__device__ inline void bt_cell_entry(const CellData& cd, const double* __restrict__ P,
+                                     const double* __restrict__ Q, int cell, int lex, int v,
+                                     double out[3]) {
+  bt_entry(P, Q, cd.sep_col[cell], cd.sep_layer[cell], lex, v, out);
 }
 
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
@@ -2034,7 +2048,7 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 template <int SL>
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
-    const double* __restrict__ P, double* __restrict__ Bt) {
+    const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ Bt) {
   constexpr int R = SL / 8;  // slot records per lane
   __shared__ double vals[kBtRowWaves][R * 64 * 3];
   // per (slot, task entry) the slot's vertex contributing to that entry, or
@@ -2065,7 +2079,7 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
           (unsigned long long)(unsigned)r[i].z | ((unsigned long long)(unsigned)r[i].w << 32);
       vof[wave][sl][int((dm >> (6 * v)) & 63)] = uint8_t(v);
       double ev[3];
-      bt_entry(cd, P, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
+      bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
       vals[wave][3 * e] = ev[0];
       vals[wave][3 * e + 1] = ev[1];
       vals[wave][3 * e + 2] = ev[2];
@@ -2105,7 +2119,7 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_b_rows(
     CellData cd, int n_rows, const int32_t* __restrict__ p_ptr, const int32_t* __restrict__ p_inc,
     const int32_t* __restrict__ B_ptr, const int32_t* __restrict__ B_col,
-    const double* __restrict__ P, double* __restrict__ B) {
+    const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ B) {
   __shared__ double vals[kBtRowWaves][216 * 3];
   __shared__ int node[kBtRowWaves][216];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2117,7 +2131,7 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_b_rows(
     const int inc = p_inc[b0 + s];
     const int cell = inc >> 3, v = inc & 7;
     double val[3];
-    bt_cell_entry(cd, P, cell, t, v, val);
+    bt_cell_entry(cd, P, Q, cell, t, v, val);
     vals[wave][3 * e] = val[0];
     vals[wave][3 * e + 1] = val[1];
     vals[wave][3 * e + 2] = val[2];
@@ -2298,25 +2312,29 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
   return false;
 }
 
-void launch_bt_rows(const CellData& cd, int n_cols, double* P, int n_tasks, int slots,
-                    const int32_t* task_hdr, const int32_t* slot_rec, double* Bt, int n_prows,
-                    const int32_t* p_ptr, const int32_t* p_inc, const int32_t* B_ptr,
-                    const int32_t* B_col, double* B, hipStream_t s) {
+void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, double* Q,
+                    int n_tasks, int slots, const int32_t* task_hdr, const int32_t* slot_rec,
+                    double* Bt, int n_prows, const int32_t* p_ptr, const int32_t* p_inc,
+                    const int32_t* B_ptr, const int32_t* B_col, double* B, hipStream_t s) {
   if (n_cols > 0) {
     hipLaunchKernelGGL(k_bt_coltab, dim3(n_cols), dim3(kBtColEntries), 0, s, cd.sep_colgeo, P);
+    DCP_HIP_CHECK(hipGetLastError());
+  }
+  if (n_layers > 0) {
+    hipLaunchKernelGGL(k_bt_laytab, dim3(n_layers), dim3(kBtLayEntries), 0, s, cd.sep_laygeo, Q);
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (n_tasks > 0) {
     hipLaunchKernelGGL(slots == 16 ? k_bt_tasks<16> : k_bt_tasks<8>,
                        dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves), dim3(64 * kBtRowWaves), 0,
                        s, cd, n_tasks, reinterpret_cast<const int4*>(task_hdr),
-                       reinterpret_cast<const int4*>(slot_rec), P, Bt);
+                       reinterpret_cast<const int4*>(slot_rec), P, Q, Bt);
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (B && n_prows > 0) {
     hipLaunchKernelGGL(k_b_rows, dim3((n_prows + kBtRowWaves - 1) / kBtRowWaves),
                        dim3(64 * kBtRowWaves), 0, s, cd, n_prows, p_ptr, p_inc, B_ptr, B_col, P,
-                       B);
+                       Q, B);
     DCP_HIP_CHECK(hipGetLastError());
   }
 }
