@@ -2154,9 +2154,9 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                 if (n < nrows) inc[size_t(f[n]++)] = int32_t(cell) << 5 | t;
               }
             // tasks: runs of consecutive rows with <= SL slots and <= 64
-            // entries (SL = 8; DCP_BT_SLOTS=16: two records per lane, no faster)
+            // entries (SL = 16: two records per lane; DCP_BT_SLOTS=8: one)
             const char* env_sl = std::getenv("DCP_BT_SLOTS");
-            const int SL = env_sl && std::atoi(env_sl) == 16 ? 16 : 8;
+            const int SL = env_sl && std::atoi(env_sl) == 8 ? 8 : 16;
             std::vector<int32_t> hdr, rec;
             int first = 0, ns = 0, ne = 0, rec0 = 0;
             // SL slot records per task (unused ones zero): a lane loads its

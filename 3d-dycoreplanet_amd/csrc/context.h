@@ -133,7 +133,7 @@ struct Ctx {
   bool bt_rows = false;
   DBuf<int32_t> bt_task_hdr, bt_slot_rec;
   int bt_ntasks = 0;
-  int bt_slots = 8;   // slot records per task (8 or 16)
+  int bt_slots = 16;  // slot records per task (8 or 16)
   // several GPUs: per colour the cells with an owned velocity node (the rhs)
   std::vector<int> rhs_color_ptr;
   DBuf<int32_t> rhs_color_cells;
