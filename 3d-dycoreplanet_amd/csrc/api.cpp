@@ -2154,9 +2154,11 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                 if (n < nrows) inc[size_t(f[n]++)] = int32_t(cell) << 5 | t;
               }
             // tasks: runs of consecutive rows with <= SL slots and <= 64
-            // entries (SL = 16: two records per lane; DCP_BT_SLOTS=8: one)
+            // entries (SL = 16: two records per lane; DCP_BT_SLOTS=8: one; =32: four, 128 entries)
             const char* env_sl = std::getenv("DCP_BT_SLOTS");
-            const int SL = env_sl && std::atoi(env_sl) == 8 ? 8 : 16;
+            const int SL = env_sl && (std::atoi(env_sl) == 8 || std::atoi(env_sl) == 32)
+                               ? std::atoi(env_sl) : 16;
+            const int NE = SL == 32 ? 128 : 64, FB = SL == 32 ? 7 : 6;  // entries, field bits
             std::vector<int32_t> hdr, rec;
             int first = 0, ns = 0, ne = 0, rec0 = 0;
             // SL slot records per task (unused ones zero): a lane loads its
@@ -2173,7 +2175,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             for (int n = 0; n < nrows; ++n) {
               const int cnt = rp[n + 1] - rp[n], len = Btp[n + 1] - Btp[n];
               require(cnt <= 8 && len <= 64, DCP_ERR_INVALID, "B^T task sizes");
-              if (ns + cnt > SL || ne + len > 64) flush(n);
+              if (ns + cnt > SL || ne + len > NE) flush(n);
               for (int k = rp[n]; k < rp[n + 1]; ++k) {
                 const int cell = inc[size_t(k)] >> 5, lex = inc[size_t(k)] & 31;
                 uint64_t dm = 0;
@@ -2183,7 +2185,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                   const int32_t* e = Btc.data() + Btp[n + 1];
                   const int32_t* it = std::lower_bound(b, e, q);
                   require(it != e && *it == q, DCP_ERR_INVALID, "B^T pattern lacks a cell's entry");
-                  dm |= uint64_t(ne + (it - b)) << (6 * v);
+                  dm |= uint64_t(ne + (it - b)) << (FB * v);
                 }
                 rec.insert(rec.end(), {col[size_t(cell)], layer[size_t(cell)] << 16 | lex << 8 | (n - first),
                                        int32_t(uint32_t(dm)), int32_t(uint32_t(dm >> 32))});

@@ -2045,16 +2045,18 @@ __device__ inline void bt_cell_entry(const CellData& cd, const double* __restric
 // other (the next header / record prefetched) measured 10 / 17 % slower for 2
 // / 4 (profiles/r04l_bt_tpw_variants.json); loading the row constraints in
 // phase 1 into LDS with a packed destination scan, 20 % slower (r04m).
-template <int SL>
+template <int SL, int EL>
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
     const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ Bt) {
-  constexpr int R = SL / 8;  // slot records per lane
+  constexpr int R = SL / 8;             // slot records per lane
+  constexpr int NE = 64 * EL;           // task entries (EL per lane)
+  constexpr int FB = EL == 1 ? 6 : 7;   // bits per destination field of a record
   __shared__ double vals[kBtRowWaves][R * 64 * 3];
   // per (slot, task entry) the slot's vertex contributing to that entry, or
   // 0xff: the entry lanes read their contributions slot by slot (no scan over
   // every (slot, vertex) pair)
-  __shared__ uint8_t vof[kBtRowWaves][SL][64];
+  __shared__ uint8_t vof[kBtRowWaves][SL][NE];
   __shared__ int rowl[kBtRowWaves][SL];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int task = int(blockIdx.x) * kBtRowWaves + wave;
@@ -2067,9 +2069,9 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 #pragma unroll
   for (int i = 0; i < R; ++i) r[i] = rec[SL * size_t(task) + 8 * i + k];
   const int ns = h.z & 255, ne = h.z >> 8;
+  unsigned long long* vw = reinterpret_cast<unsigned long long*>(&vof[wave][0][0]);
 #pragma unroll
-  for (int i = 0; i < R; ++i)
-    reinterpret_cast<unsigned long long*>(&vof[wave][8 * i][0])[lane] = ~0ull;
+  for (int i = 0; i < SL * NE / 8 / 64; ++i) vw[64 * i + lane] = ~0ull;
   wsync();
 #pragma unroll
   for (int i = 0; i < R; ++i) {
@@ -2077,7 +2079,7 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     if (sl < ns) {
       const unsigned long long dm =
           (unsigned long long)(unsigned)r[i].z | ((unsigned long long)(unsigned)r[i].w << 32);
-      vof[wave][sl][int((dm >> (6 * v)) & 63)] = uint8_t(v);
+      vof[wave][sl][int((dm >> (FB * v)) & (NE - 1))] = uint8_t(v);
       double ev[3];
       bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
       vals[wave][3 * e] = ev[0];
@@ -2087,26 +2089,31 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     }
   }
   wsync();
-  if (lane >= ne) return;
-  // entry `lane`: its contributions in slot order (the row's cells in colour
-  // order), the same order as a scan over (slot, vertex)
-  double acc[3] = {0.0, 0.0, 0.0};
-  int rl = 0;
-  for (int sl = 0; sl < ns; ++sl) {
-    const int vv = vof[wave][sl][lane];
-    if (vv != 0xff) {
-      const int e = 8 * sl + vv;
-      acc[0] += vals[wave][3 * e];
-      acc[1] += vals[wave][3 * e + 1];
-      acc[2] += vals[wave][3 * e + 2];
-      rl = rowl[wave][sl];
-    }
-  }
-  double Ca[3][3];
-  condensation(cd.vcon[h.y + rl], Ca);
-  double* dst = Bt + 3 * size_t(h.x + lane);
 #pragma unroll
-  for (int jj = 0; jj < 3; ++jj) dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+  for (int q = 0; q < EL; ++q) {
+    const int j = lane + 64 * q;
+    if (j >= ne) break;
+    // entry j: its contributions in slot order (the row's cells in colour
+    // order), the same order as a scan over (slot, vertex)
+    double acc[3] = {0.0, 0.0, 0.0};
+    int rl = 0;
+    for (int sl = 0; sl < ns; ++sl) {
+      const int vv = vof[wave][sl][j];
+      if (vv != 0xff) {
+        const int e = 8 * sl + vv;
+        acc[0] += vals[wave][3 * e];
+        acc[1] += vals[wave][3 * e + 1];
+        acc[2] += vals[wave][3 * e + 2];
+        rl = rowl[wave][sl];
+      }
+    }
+    double Ca[3][3];
+    condensation(cd.vcon[h.y + rl], Ca);
+    double* dst = Bt + 3 * size_t(h.x + j);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj)
+      dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+  }
 }
 
 // B by pressure rows (several GPUs, where B is not the transpose of the owned
@@ -2325,7 +2332,7 @@ void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, dou
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (n_tasks > 0) {
-    hipLaunchKernelGGL(slots == 16 ? k_bt_tasks<16> : k_bt_tasks<8>,
+    hipLaunchKernelGGL((slots == 32 ? k_bt_tasks<32, 2> : slots == 16 ? k_bt_tasks<16, 1> : k_bt_tasks<8, 1>),
                        dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves), dim3(64 * kBtRowWaves), 0,
                        s, cd, n_tasks, reinterpret_cast<const int4*>(task_hdr),
                        reinterpret_cast<const int4*>(slot_rec), P, Q, Bt);

@@ -15,4 +15,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p
 f=$(find /tmp/prof -name "*kernel_stats.csv" | head -1)
 cp "$f" $OUT/bench_kernel_stats.csv
 TAG=${TAGR:-r04r}_pmc_asm REGEX="k_bt_tasks|k_bt_coltab|k_mf_pencil|k_mf_gather|k_nse_rhs_halfwave|k_con_gather" bash tools/pmc_pass.sh tools/asm_probe.py || { echo "pmc asm failed"; exit 1; }
+
+timeout -k 10 200 python3 -u tools/bt_slots_probe.py > $OUT/bt_slots.json 2> $OUT/bt_slots.err || { echo "bt slots probe failed"; tail -5 $OUT/bt_slots.err; exit 1; }
+cat $OUT/bt_slots.json
 echo ALLOK
