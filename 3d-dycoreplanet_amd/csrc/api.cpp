@@ -2570,6 +2570,23 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     const bool rhs_subset = bt_rows && !c.rhs_color_ptr.empty();
+    // B^T (geometry only) and the rhs (state) are independent: with
+    // DCP_ASM_OVERLAP the B^T tasks run on the second stream beside the rhs
+    // launches (1: B^T launched first, 2: after the rhs launches)
+    const char* env_ov = std::getenv("DCP_ASM_OVERLAP");
+    const int overlap = bt_rows && rhs_co && c.mf_stream && env_ov ? std::atoi(env_ov) : 0;
+    const hipStream_t bt_stream = overlap ? c.mf_stream : c.stream;
+    auto launch_bt = [&] {
+      launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
+                     c.bt_slot_rec.p, c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p,
+                     c.bt_p_inc.p, c.B_ptr.p, c.B_col.p, c.B_transpose ? nullptr : c.B_val.p,
+                     bt_stream);
+    };
+    if (overlap) {
+      DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[0], c.stream));
+      DCP_HIP_CHECK(hipStreamWaitEvent(c.mf_stream, c.mf_chunk_ev[0], 0));
+      if (overlap == 1) launch_bt();
+    }
     if (rhs_co && out.cdiag) {
       // the constrained-row diagonals only: the cells with a constrained node
       // in one launch, per (cell, node) slots, summed per node in colour order
@@ -2602,11 +2619,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       g.pcidx = nullptr;
       mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
-    if (bt_rows)
-      launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
-                     c.bt_slot_rec.p,
-                     c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p, c.bt_p_inc.p, c.B_ptr.p,
-                     c.B_col.p, c.B_transpose ? nullptr : c.B_val.p, c.stream);
+    if (bt_rows && overlap != 1) launch_bt();
+    if (overlap) {
+      DCP_HIP_CHECK(hipEventRecord(c.mf_join_ev, c.mf_stream));
+      DCP_HIP_CHECK(hipStreamWaitEvent(c.stream, c.mf_join_ev, 0));
+    }
     if (full)
       image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
                             c.A_val.p, c.stream);

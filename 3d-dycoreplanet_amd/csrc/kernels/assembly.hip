@@ -1974,7 +1974,13 @@ __global__ void k_con_gather(int n_con, const int32_t* __restrict__ cptr,
 // order), condenses it with its row's constraint (C_a^T b: linear, so the same
 // as condensing each cell's part) and stores it -- every entry written once,
 // the task's piece coalesced, no read-modify-write, no zero fill, no colouring.
-constexpr int kBtRowWaves = 4;
+#ifndef DCP_BT_WAVES
+#define DCP_BT_WAVES 4
+#endif
+constexpr int kBtRowWaves = DCP_BT_WAVES;
+#ifndef DCP_BT_STORE
+#define DCP_BT_STORE 0
+#endif
 constexpr int kBtColEntries = 216;  // [P01 | P2][a][b][i][j][d]
 
 __global__ __launch_bounds__(kBtColEntries) void k_bt_coltab(const double* __restrict__ colgeo,
@@ -2069,6 +2075,9 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 #pragma unroll
   for (int i = 0; i < R; ++i) r[i] = rec[SL * size_t(task) + 8 * i + k];
   const int ns = h.z & 255, ne = h.z >> 8;
+#if DCP_BT_STORE && DCP_BT_STORE != 3
+  double out[EL][3];
+#endif
   unsigned long long* vw = reinterpret_cast<unsigned long long*>(&vof[wave][0][0]);
 #pragma unroll
   for (int i = 0; i < SL * NE / 8 / 64; ++i) vw[64 * i + lane] = ~0ull;
@@ -2109,11 +2118,51 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     }
     double Ca[3][3];
     condensation(cd.vcon[h.y + rl], Ca);
+#if DCP_BT_STORE == 3
+    double* dst = Bt + 3 * size_t(h.x + j);
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj)
+      __builtin_nontemporal_store(Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2],
+                                  dst + jj);
+#elif DCP_BT_STORE
+    out[q][0] = Ca[0][0] * acc[0] + Ca[1][0] * acc[1] + Ca[2][0] * acc[2];
+    out[q][1] = Ca[0][1] * acc[0] + Ca[1][1] * acc[1] + Ca[2][1] * acc[2];
+    out[q][2] = Ca[0][2] * acc[0] + Ca[1][2] * acc[1] + Ca[2][2] * acc[2];
+#else
     double* dst = Bt + 3 * size_t(h.x + j);
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj)
       dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+#endif
   }
+#if DCP_BT_STORE && DCP_BT_STORE != 3
+  // the task's piece through LDS (over vals, every lane past its reads): each
+  // store instruction then covers 512 consecutive bytes instead of every
+  // third double of 1536
+  wsync();
+#pragma unroll
+  for (int q = 0; q < EL; ++q) {
+    const int j = lane + 64 * q;
+    if (j < ne) {
+      vals[wave][3 * j] = out[q][0];
+      vals[wave][3 * j + 1] = out[q][1];
+      vals[wave][3 * j + 2] = out[q][2];
+    }
+  }
+  wsync();
+  double* dst = Bt + 3 * size_t(h.x);
+#pragma unroll
+  for (int q = 0; q < 3 * EL; ++q) {
+    const int idx = 64 * q + lane;
+    if (idx < 3 * ne) {
+#if DCP_BT_STORE == 2
+      __builtin_nontemporal_store(vals[wave][idx], dst + idx);
+#else
+      dst[idx] = vals[wave][idx];
+#endif
+    }
+  }
+#endif
 }
 
 // B by pressure rows (several GPUs, where B is not the transpose of the owned
