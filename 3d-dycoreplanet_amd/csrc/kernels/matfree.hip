@@ -418,7 +418,16 @@ constexpr int kPenSlots = DCP_MF_SLOTS;
 #endif
 constexpr int kFS = DCP_MF_FIELD_MAJOR ? kPenSlots * 27 : 27;   // field stride (doubles)
 constexpr int kPenFields = 9 * kPenSlots * 27;           // per wave
-constexpr int kPenAux = 8 + 18 + 1;                      // per slot
+// DCP_MF_LDS_ALIAS: the vertex pressures, the pressure-test partials and the
+// chain links live in field slabs that are dead at the time (see the kernel),
+// so a wave needs only the 9 fields: 13.6 instead of 15.3 KB, 12 instead of
+// 10 waves per CU (the 166 VGPRs allow 3 per SIMD)
+#ifndef DCP_MF_LDS_ALIAS
+#define DCP_MF_LDS_ALIAS 1
+#endif
+#if !DCP_MF_LDS_ALIAS
+constexpr int kPenAux = 8 + 18 + 1;  // per slot
+#endif
 #ifndef DCP_MF_BATCHES
 #define DCP_MF_BATCHES 1
 #endif
@@ -500,8 +509,10 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
                  double* __restrict__ buf, const double* __restrict__ T_old, PhysicsDev ph) {
   static_assert(!(RHS && STOKES), "the rhs pass has no pressure");
   __shared__ double lds[kPenWaves][kPenFields];
+#if !DCP_MF_LDS_ALIAS
   __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
-  __shared__ MfLink nxt[kPenWaves * kPenCells * 27];  // chain links of the group partial sums
+  __shared__ MfLink nxt_own[kPenWaves * kPenCells * 27];  // chain links of the group partial sums
+#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // lane 63 shadows lane 54 (slot 6, pencil 0) with 7 LDS slots: it computes
   // and stores the same LDS values and skips the global store; with 8 slots it
@@ -519,8 +530,23 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
 #endif
   const int blk = DCP_MF_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x);
   double* S = lds[wave] + (DCP_MF_FIELD_MAJOR ? 27 * cs : 243 * cs);
+#if DCP_MF_LDS_ALIAS
+  // P (vertex values): field 8 of the slot, read before the forward y pass
+  // writes it; SP (pressure-test partials): field 6, written after the back y
+  // pass has read it; the chain links: bytes of fields 3.. of the wave, written
+  // after the back x pass has read them
+  double* P = S + 8 * kFS;
+  double* SP = S + 6 * kFS;
+  MfLink* nxt0 = reinterpret_cast<MfLink*>(&lds[0][3 * kFS]);
+  auto nxt = [&](int k) -> MfLink& {
+    const int wk = k / (27 * kPenCells);
+    return nxt0[wk * int(sizeof(double)) * kPenFields + (k - 27 * kPenCells * wk)];
+  };
+#else
   double* P = aux[wave][cs];
   double* SP = P + 8;
+  auto nxt = [&](int k) -> MfLink& { return nxt_own[k]; };
+#endif
   // LDS reads through a volatile view: keeps them single ds_read_b64 (256 B/clk)
   // instead of merged ds_read2_b64 pairs (128 B/clk on gfx950)
 #ifndef DCP_MF_VOLATILE_READS
@@ -648,6 +674,15 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
     }
   }
   wsync();
+  // the pressure (temperature) at the z-pencil's two end levels, read before
+  // the forward y pass reuses P's slab (DCP_MF_LDS_ALIAS)
+  double Plo = 0.0, Phi = 0.0;
+  if (STOKES || RHS) {
+    const double xa = sel3(pa, kGaussX[0], kGaussX[1], kGaussX[2]);
+    const double xb = sel3(pb, kGaussX[0], kGaussX[1], kGaussX[2]);
+    Plo = (1.0 - xb) * ((1.0 - xa) * P[0] + xa * P[1]) + xb * ((1.0 - xa) * P[2] + xa * P[3]);
+    Phi = (1.0 - xb) * ((1.0 - xa) * P[4] + xa * P[5]) + xb * ((1.0 - xa) * P[6] + xa * P[7]);
+  }
   {
     double A[3][3], B[3][3], C[3][3];
 #pragma unroll
@@ -686,13 +721,6 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
     for (int i = 0; i < 9; ++i) lg[i] = lp[i];
   }
   // ---- z-pencil: per point flux, accumulated straight into the back z pass
-  double Plo = 0.0, Phi = 0.0;
-  if (STOKES || RHS) {
-    const double xa = sel3(pa, kGaussX[0], kGaussX[1], kGaussX[2]);
-    const double xb = sel3(pb, kGaussX[0], kGaussX[1], kGaussX[2]);
-    Plo = (1.0 - xb) * ((1.0 - xa) * P[0] + xa * P[1]) + xb * ((1.0 - xa) * P[2] + xa * P[3]);
-    Phi = (1.0 - xb) * ((1.0 - xa) * P[4] + xa * P[5]) + xb * ((1.0 - xa) * P[6] + xa * P[7]);
-  }
   double V[3][3], FX[3][3], FY[3][3];  // [c][node along z]
 #pragma unroll
   for (int c = 0; c < 3; ++c)
@@ -810,7 +838,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
         S[(6 + c) * kFS + zo + 9 * k] = FY[c][k];
       }
     }
-  if (STOKES) {
+  if (STOKES && !DCP_MF_LDS_ALIAS) {
     SP[p] = slo;
     SP[9 + p] = shi;
   }
@@ -818,6 +846,20 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
 
   // ---- back y (y-pencil), the pressure test functions
   double yp = 0.0;
+  auto pressure_test = [&] {
+    if (STOKES && p < 8) {
+      const int v0 = p & 1, v1 = (p >> 1) & 1, v2 = p >> 2;
+      const double* s = SP + 9 * v2;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const double pb1 = v1 ? kGaussX[b] : 1.0 - kGaussX[b];
+        double r = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) r += (v0 ? kGaussX[a] : 1.0 - kGaussX[a]) * s[a + 3 * b];
+        yp += pb1 * r;
+      }
+    }
+  };
   {
     double V1[3][3], FX1[3][3];
 #pragma unroll
@@ -837,19 +879,12 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
         bwd(kTL, fx, FX1[c]);
       }
     }
-    if (STOKES && p < 8) {
-      const int v0 = p & 1, v1 = (p >> 1) & 1, v2 = p >> 2;
-      const double* s = SP + 9 * v2;
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const double pb1 = v1 ? kGaussX[b] : 1.0 - kGaussX[b];
-        double r = 0.0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) r += (v0 ? kGaussX[a] : 1.0 - kGaussX[a]) * s[a + 3 * b];
-        yp += pb1 * r;
-      }
-    }
+    if (!DCP_MF_LDS_ALIAS) pressure_test();
     wsync();
+    if (STOKES && DCP_MF_LDS_ALIAS) {  // field 6 is dead now (FY read above)
+      SP[p] = slo;
+      SP[9 + p] = shi;
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c)
 #pragma unroll
@@ -859,6 +894,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
       }
   }
   wsync();
+  if (DCP_MF_LDS_ALIAS) pressure_test();
 
   // ---- back x (x-pencil) and the cell record
   double y[3][3];  // [node a][c]
@@ -893,7 +929,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   for (int n = 0; n < 3; ++n) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) S[c * kFS + xo + xs * n] = y[n][c];
-    if (cs < kPenCells) nxt[27 * (kPenCells * wave + cs) + 3 * p + n] = MfLink(Ic.next[n]);
+    if (cs < kPenCells) nxt(27 * (kPenCells * wave + cs) + 3 * p + n) = MfLink(Ic.next[n]);
   }
   // the group spans the workgroup's waves: their records are read across waves
   if (kPenWaves > 1)
@@ -907,7 +943,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
       double s0 = y[n][0], s1 = y[n][1], s2 = y[n][2];
       // links point forward inside the group (at most kMfGroupCells - 1 hops)
       int k = Ic.next[n];
-      for (int hop = 0; k != kMfLinkEnd && hop < kMfGroupCells; ++hop, k = nxt[k]) {
+      for (int hop = 0; k != kMfLinkEnd && hop < kMfGroupCells; ++hop, k = nxt(k)) {
         const int ck = k / 27, tk = k - 27 * ck;
         const int wk = ck / kPenCells, sk = ck - kPenCells * wk;  // wave and cell slot
         const int ak = tk % 3, bk = (tk / 3) % 3, zk = tk / 9;

@@ -15,7 +15,7 @@ import csv, glob, os
 out = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/mfvar"
 for f in sorted(glob.glob(out + "/*.csv")):
     rows = {r["Name"]: r for r in csv.DictReader(open(f))}
-    sel = {k.split("(")[0].split("::")[-1][:24]: float(r["AverageNs"]) / 1e3 for k, r in rows.items()
-           if "k_mf_pencil<true>" in k or "k_mf_gather<true>" in k or "k_mf_pencil<false>" in k or "k_mf_gather<false>" in k}
+    sel = {k.split("(")[0].split("::")[-1][:36]: float(r["AverageNs"]) / 1e3 for k, r in rows.items()
+           if "k_mf_pencil<" in k or "k_mf_gather<" in k}
     print(os.path.basename(f)[:-4], {k: round(v, 1) for k, v in sel.items()})
 PY
