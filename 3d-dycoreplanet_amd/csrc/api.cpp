@@ -2570,12 +2570,15 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     const bool rhs_subset = bt_rows && !c.rhs_color_ptr.empty();
-    // B^T (geometry only) and the rhs (state) are independent: with
-    // DCP_ASM_OVERLAP the B^T tasks run on the second stream beside the rhs
-    // launches (1: B^T launched first, 2: after the rhs launches)
+    // B^T (geometry only), the constrained diagonals and the rhs (state) are
+    // independent: with DCP_ASM_OVERLAP the B^T tasks run on the second stream
+    // beside the rhs launches (1: B^T launched first, 2: after the rhs
+    // launches), or (3) the constrained-diagonal pass runs there while B^T
+    // (launched first) and the rhs run on the main stream
     const char* env_ov = std::getenv("DCP_ASM_OVERLAP");
     const int overlap = bt_rows && rhs_co && c.mf_stream && env_ov ? std::atoi(env_ov) : 0;
-    const hipStream_t bt_stream = overlap ? c.mf_stream : c.stream;
+    const hipStream_t bt_stream = overlap == 1 || overlap == 2 ? c.mf_stream : c.stream;
+    const hipStream_t con_stream = overlap == 3 ? c.mf_stream : c.stream;
     auto launch_bt = [&] {
       launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
                      c.bt_slot_rec.p, c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p,
@@ -2587,6 +2590,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       DCP_HIP_CHECK(hipStreamWaitEvent(c.mf_stream, c.mf_chunk_ev[0], 0));
       if (overlap == 1) launch_bt();
     }
+    if (overlap == 3 && !out.cdiag) launch_bt();  // nothing to overlap: B^T first anyway
     if (rhs_co && out.cdiag) {
       // the constrained-row diagonals only: the cells with a constrained node
       // in one launch, per (cell, node) slots, summed per node in colour order
@@ -2594,8 +2598,9 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       oc.cbuf = c.con_cbuf.p;
       oc.cslot = c.con_cslot.p;
       launch_nse_operator(c.cd(), c.maps(), c.con_color_cells.p, c.con_color_ptr.back(),
-                          c.old_nse.p, c.old_T.p, c.ph, oc, c.stream);
-      con_gather(c.n_con, c.con_cptr.p, c.con_cbuf.p, c.con_diag.p, c.stream);
+                          c.old_nse.p, c.old_T.p, c.ph, oc, con_stream);
+      con_gather(c.n_con, c.con_cptr.p, c.con_cbuf.p, c.con_diag.p, con_stream);
+      if (overlap == 3) launch_bt();
     }
     for (int k = 0; k < c.n_colors() && !rhs_co; ++k) {
       if (full)
@@ -2619,7 +2624,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       g.pcidx = nullptr;
       mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
     }
-    if (bt_rows && overlap != 1) launch_bt();
+    if (bt_rows && overlap != 1 && overlap != 3) launch_bt();
     if (overlap) {
       DCP_HIP_CHECK(hipEventRecord(c.mf_join_ev, c.mf_stream));
       DCP_HIP_CHECK(hipStreamWaitEvent(c.stream, c.mf_join_ev, 0));

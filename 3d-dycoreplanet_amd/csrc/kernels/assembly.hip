@@ -1978,8 +1978,12 @@ __global__ void k_con_gather(int n_con, const int32_t* __restrict__ cptr,
 #define DCP_BT_WAVES 4
 #endif
 constexpr int kBtRowWaves = DCP_BT_WAVES;
+// B^T entry stores: 0 plain, 1 / 2 through LDS in 512-byte runs (2:
+// nontemporal), 3 nontemporal from the entry lanes (default: B^T is 584 MB at
+// r=5, larger than the Infinity Cache, and is next read by the S formation;
+// 0.553 -> 0.525 ms per assembly, bitwise, profiles/r04y_bt_store_variants.json)
 #ifndef DCP_BT_STORE
-#define DCP_BT_STORE 0
+#define DCP_BT_STORE 3
 #endif
 constexpr int kBtColEntries = 216;  // [P01 | P2][a][b][i][j][d]
 

@@ -11,11 +11,11 @@ for v in ${VARS}; do
   find /tmp/pv -name "*kernel_stats.csv" -exec cp {} $OUT/$v.csv \;
 done
 python3 - <<'PY'
-import csv, glob, os
+import csv, glob, os, re
 out = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/mfvar"
 for f in sorted(glob.glob(out + "/*.csv")):
     rows = {r["Name"]: r for r in csv.DictReader(open(f))}
-    sel = {k.split("(")[0].split("::")[-1][:36]: float(r["AverageNs"]) / 1e3 for k, r in rows.items()
-           if "k_mf_pencil<" in k or "k_mf_gather<" in k}
+    sel = {re.search(r"k_mf_\w+<[^>]*>", k).group(0): float(r["AverageNs"]) / 1e3
+           for k, r in rows.items() if "k_mf_pencil<" in k or "k_mf_gather<" in k}
     print(os.path.basename(f)[:-4], {k: round(v, 1) for k, v in sel.items()})
 PY
