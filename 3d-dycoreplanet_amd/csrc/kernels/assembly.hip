@@ -1986,6 +1986,20 @@ constexpr int kBtRowWaves = DCP_BT_WAVES;
 #define DCP_BT_STORE 3
 #endif
 constexpr int kBtColEntries = 216;  // [P01 | P2][a][b][i][j][d]
+// DCP_BT_NTLOAD (timing variant): the task headers and slot records (read once
+// per assembly) as nontemporal loads, keeping the caches for the tables
+#ifndef DCP_BT_NTLOAD
+#define DCP_BT_NTLOAD 0
+#endif
+__device__ __forceinline__ int4 bt_ld4(const int4* p) {
+#if DCP_BT_NTLOAD
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i x = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+  return make_int4(x.x, x.y, x.z, x.w);
+#else
+  return *p;
+#endif
+}
 
 __global__ __launch_bounds__(kBtColEntries) void k_bt_coltab(const double* __restrict__ colgeo,
                                                              double* __restrict__ P) {
@@ -2074,10 +2088,10 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
   const int k = lane >> 3, v = lane & 7;
   // records at SL task + slot (unused slots zero): header and record loads
   // issue together
-  const int4 h = hdr[task];
+  const int4 h = bt_ld4(hdr + task);
   int4 r[R];
 #pragma unroll
-  for (int i = 0; i < R; ++i) r[i] = rec[SL * size_t(task) + 8 * i + k];
+  for (int i = 0; i < R; ++i) r[i] = bt_ld4(rec + SL * size_t(task) + 8 * i + k);
   const int ns = h.z & 255, ne = h.z >> 8;
 #if DCP_BT_STORE && DCP_BT_STORE != 3
   double out[EL][3];

@@ -587,18 +587,27 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
     double U[3][3];
     double pv;
   };
+  // DCP_MF_NTIDX (timing variant): the per-cell index streams (read once per
+  // apply) as nontemporal loads, keeping the caches for the gathered src
+#ifndef DCP_MF_NTIDX
+#define DCP_MF_NTIDX 0
+#endif
+  auto ldi = [](const auto* q) {
+    if (DCP_MF_NTIDX) return __builtin_nontemporal_load(q);
+    return *q;
+  };
   auto load_ids = [&](int j, Ids& I) {
     const int cell = cell_of(j);
     const size_t e = (cs < kPenCells && cell < c1) ? size_t(cell) : 0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      I.nd[a] = mc.cell_q2[27 * e + 3 * p + a];
-      I.slot[a] = mc.vslot[27 * e + 3 * p + a];
-      I.next[a] = mc.vnext[27 * e + 3 * p + a];
+      I.nd[a] = ldi(mc.cell_q2 + 27 * e + 3 * p + a);
+      I.slot[a] = ldi(mc.vslot + 27 * e + 3 * p + a);
+      I.next[a] = ldi(mc.vnext + 27 * e + 3 * p + a);
     }
-    I.mask = mc.cmask[e];
-    I.pdof = (STOKES && p < 8) ? mc.cell_p[8 * e + p] : (RHS && p < 8) ? mc.cell_T[8 * e + p] : 0;
-    I.pslot = (STOKES && p < 8) ? mc.pslot[8 * e + p] : 0;
+    I.mask = ldi(mc.cmask + e);
+    I.pdof = (STOKES && p < 8) ? ldi(mc.cell_p + 8 * e + p) : (RHS && p < 8) ? ldi(mc.cell_T + 8 * e + p) : 0;
+    I.pslot = (STOKES && p < 8) ? ldi(mc.pslot + 8 * e + p) : 0;
   };
   auto load_nodes = [&](const Ids& I, Nodes& N) {
 #pragma unroll
