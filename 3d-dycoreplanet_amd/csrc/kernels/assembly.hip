@@ -1986,10 +1986,10 @@ constexpr int kBtRowWaves = DCP_BT_WAVES;
 #define DCP_BT_STORE 3
 #endif
 constexpr int kBtColEntries = 216;  // [P01 | P2][a][b][i][j][d]
-// DCP_BT_NTLOAD (timing variant): the task headers and slot records (read once
+// DCP_BT_NTLOAD (default on): the task headers and slot records (read once
 // per assembly) as nontemporal loads, keeping the caches for the tables
 #ifndef DCP_BT_NTLOAD
-#define DCP_BT_NTLOAD 0
+#define DCP_BT_NTLOAD 1
 #endif
 __device__ __forceinline__ int4 bt_ld4(const int4* p) {
 #if DCP_BT_NTLOAD

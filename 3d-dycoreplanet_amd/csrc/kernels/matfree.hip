@@ -587,10 +587,10 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
     double U[3][3];
     double pv;
   };
-  // DCP_MF_NTIDX (timing variant): the per-cell index streams (read once per
+  // DCP_MF_NTIDX (default on): the per-cell index streams (read once per
   // apply) as nontemporal loads, keeping the caches for the gathered src
 #ifndef DCP_MF_NTIDX
-#define DCP_MF_NTIDX 0
+#define DCP_MF_NTIDX 1
 #endif
   auto ldi = [](const auto* q) {
     if (DCP_MF_NTIDX) return __builtin_nontemporal_load(q);
