@@ -2119,7 +2119,10 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
         c.rhs_cell_order = false;
         const char* env = std::getenv("DCP_BT_ROWS");
         const char* env_rhs = std::getenv("DCP_ASM_RHS_CELL_ORDER");
-        if (c.mf_separable && !c.periodic && !(env && *env == '0') && n_cells < (1 << 26)) {
+        // (B is then read as the transpose of B^T: every local B entry must have
+        // its B^T entry, c.B_transpose)
+        if (c.mf_separable && !c.periodic && c.B_transpose && !(env && *env == '0') &&
+            n_cells < (1 << 26)) {
           const int nrows = int(Btp.size()) - 1;
           std::vector<int32_t> rp(size_t(nrows) + 1, 0);
           for (const int cell : ccells)
@@ -2131,18 +2134,6 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           for (int n = 0; n < nrows; ++n) {
             most = std::max(most, rp[n + 1]);
             rp[n + 1] += rp[n];
-          }
-          // B rows (several GPUs): per owned pressure row its cells, colour order
-          const int prows = int(Bp.size()) - 1;
-          std::vector<int32_t> pp(size_t(prows) + 1, 0);
-          for (const int cell : ccells)
-            for (int v = 0; v < 8; ++v) {
-              const int q = pd[8 * size_t(cell) + v];
-              if (q < prows) pp[q + 1]++;
-            }
-          for (int q = 0; q < prows; ++q) {
-            most = std::max(most, pp[q + 1]);
-            pp[q + 1] += pp[q];
           }
           if (most <= 8 && *std::max_element(layer.begin(), layer.end()) < 65536) {
             // one wave: 8 cells x 8 vertices (27 nodes)
@@ -2179,13 +2170,21 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
               for (int k = rp[n]; k < rp[n + 1]; ++k) {
                 const int cell = inc[size_t(k)] >> 5, lex = inc[size_t(k)] & 31;
                 uint64_t dm = 0;
+                int dest[8];
                 for (int v = 0; v < 8; ++v) {
                   const int q = pd[8 * size_t(cell) + v];
                   const int32_t* b = Btc.data() + Btp[n];
                   const int32_t* e = Btc.data() + Btp[n + 1];
                   const int32_t* it = std::lower_bound(b, e, q);
                   require(it != e && *it == q, DCP_ERR_INVALID, "B^T pattern lacks a cell's entry");
-                  dm |= uint64_t(ne + (it - b)) << (FB * v);
+                  dest[v] = int(ne + (it - b));
+                  // k_bt_tasks keeps one vertex per (slot, entry): a cell whose
+                  // vertices share a pressure dof (identified vertices) would
+                  // lose a contribution, so refuse it here
+                  for (int w = 0; w < v; ++w)
+                    require(dest[w] != dest[v], DCP_ERR_INVALID,
+                            "B^T task: two vertices of a cell map to one entry");
+                  dm |= uint64_t(dest[v]) << (FB * v);
                 }
                 rec.insert(rec.end(), {col[size_t(cell)], layer[size_t(cell)] << 16 | lex << 8 | (n - first),
                                        int32_t(uint32_t(dm)), int32_t(uint32_t(dm >> 32))});
@@ -2263,8 +2262,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.bt_P.alloc(size_t(216) * c.bt_ncols + size_t(12) * nlay);
             c.bt_Q = c.bt_P.p + size_t(216) * c.bt_ncols;
             launch_bt_rows(c.cd(), c.bt_ncols, nlay, c.bt_P.p, c.bt_Q, 0, c.bt_slots, nullptr,
-                           nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           c.stream);
+                           nullptr, nullptr, c.stream);
             c.bt_rows = true;
           }
         }
@@ -2581,9 +2579,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     const hipStream_t con_stream = overlap == 3 ? c.mf_stream : c.stream;
     auto launch_bt = [&] {
       launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
-                     c.bt_slot_rec.p, c.Bt_val.p, int(c.bt_p_ptr.n) - 1, c.bt_p_ptr.p,
-                     c.bt_p_inc.p, c.B_ptr.p, c.B_col.p, c.B_transpose ? nullptr : c.B_val.p,
-                     bt_stream);
+                     c.bt_slot_rec.p, c.Bt_val.p, bt_stream);
     };
     if (overlap) {
       DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[0], c.stream));
@@ -2635,7 +2631,7 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     t.stop();
     if (matrix) {
       // else B = (B^T)^T, materialised when read
-      c.B_current = out.B != nullptr || (bt_rows && !c.B_transpose);
+      c.B_current = out.B != nullptr;
       c.nse_assembled = true;
       c.A_current = full;
       c.nse_ph = c.ph;
@@ -3092,6 +3088,12 @@ int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]) {
     for (int i = 0; i < 8; ++i) info[i] = m.built || i == 7 ? v[i] : 0;
     return DCP_OK;
   });
+}
+
+int dcp_device_memory(int64_t* live_bytes, int64_t* peak_bytes) {
+  if (live_bytes) *live_bytes = dev_mem().live;
+  if (peak_bytes) *peak_bytes = dev_mem().peak;
+  return DCP_OK;
 }
 
 int dcp_nse_coupling_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowptr, int32_t* cols,

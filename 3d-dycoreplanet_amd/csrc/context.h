@@ -3,6 +3,7 @@
 #include <chrono>
 #include <cstdint>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include <memory>
@@ -20,6 +21,30 @@ struct ApiError {
   std::string msg;
 };
 
+// Device bytes held by the buffers the calling host thread allocated (one
+// rank = one thread in an in-process group): dcp_device_memory.
+struct DevMemTrack {
+  int64_t live = 0, peak = 0;
+  std::unordered_map<const void*, int64_t> sizes;
+};
+inline DevMemTrack& dev_mem() {
+  static thread_local DevMemTrack t;
+  return t;
+}
+inline void dev_mem_alloc(const void* p, size_t bytes) {
+  DevMemTrack& t = dev_mem();
+  t.sizes[p] = int64_t(bytes);
+  t.live += int64_t(bytes);
+  if (t.live > t.peak) t.peak = t.live;
+}
+inline void dev_mem_free(const void* p) {
+  DevMemTrack& t = dev_mem();
+  auto it = t.sizes.find(p);
+  if (it == t.sizes.end()) return;  // allocated on another thread
+  t.live -= it->second;
+  t.sizes.erase(it);
+}
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -29,7 +54,10 @@ struct DBuf {
   DBuf& operator=(const DBuf&) = delete;
   ~DBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      dev_mem_free(p);
+      (void)hipFree(p);
+    }
     p = nullptr;
     n = 0;
   }
@@ -37,6 +65,7 @@ struct DBuf {
     release();
     if (count == 0) count = 1;
     DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+    dev_mem_alloc(p, count * sizeof(T));
     n = count;
   }
   void upload(const std::vector<T>& h) {
@@ -144,7 +173,6 @@ struct Ctx {
   DBuf<int32_t> con_color_cells;
   DBuf<int32_t> con_cptr, con_cslot;  // slots of the constrained diagonals (con_gather)
   DBuf<double> con_cbuf;
-  DBuf<int32_t> bt_p_ptr, bt_p_inc;  // per owned pressure row its cells (cell << 3 | vertex)
   DBuf<double> bt_P;  // [n_cols][216] column factors, then [n_layers][12] layer factors (upload)
   double* bt_Q = nullptr;
   int bt_ncols = 0;

@@ -303,13 +303,12 @@ void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const i
 // (once, at upload: geometry only);
 // task_hdr [n_tasks][4] / slot_rec [slots][4]: runs of consecutive velocity
 // node rows (<= 8 (row, cell) slots, <= 64 entries) built at upload
-// (api.cpp build_bt_tasks). Writes every B^T entry once. B != null (several
-// GPUs): also B by pressure rows (k_b_rows; p_inc: cell << 3 | vertex), bitwise
-// the transpose of B^T.
+// (api.cpp build_bt_tasks). Writes every B^T entry once; B is read as its
+// transpose (the row tasks are used only where every local B entry has its
+// B^T entry, Ctx::B_transpose).
 void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, double* Q,
                     int n_tasks, int slots, const int32_t* task_hdr, const int32_t* slot_rec,
-                    double* Bt, int n_prows, const int32_t* p_ptr, const int32_t* p_inc,
-                    const int32_t* B_ptr, const int32_t* B_col, double* B, hipStream_t s);
+                    double* Bt, hipStream_t s);
 bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_ptr, int per_cell,
                       int32_t* pos, size_t n_cells, size_t nnz, hipStream_t s,
                       unsigned long long* touched_out = nullptr);

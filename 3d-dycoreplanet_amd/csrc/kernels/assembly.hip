@@ -18,6 +18,8 @@
 // deterministic (no atomics).
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include <cstddef>
 #include <cstdlib>
 
@@ -2052,11 +2054,6 @@ __device__ inline void bt_entry(const double* __restrict__ P, const double* __re
 #pragma unroll
   for (int d = 0; d < 3; ++d) out[d] = -(pp[d] * q01 + pp[108 + d] * q2);
 }
-__device__ inline void bt_cell_entry(const CellData& cd, const double* __restrict__ P,
-                                     const double* __restrict__ Q, int cell, int lex, int v,
-                                     double out[3]) {
-  bt_entry(P, Q, cd.sep_col[cell], cd.sep_layer[cell], lex, v, out);
-}
 
 // task header: {first B^T entry, first row, slots | entries << 8, first slot
 // record (= SL task)}; slot record: {column-table entry, layer << 16 | lex <<
@@ -2183,54 +2180,6 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 #endif
 }
 
-// B by pressure rows (several GPUs, where B is not the transpose of the owned
-// B^T rows): one wave per owned pressure row p; pair e = (cell slot s, node
-// position t) of p's cells (colour order) evaluates bt_cell_entry for p's
-// vertex in that cell, then lane j sums entry j (node n) over the pairs with
-// node n in slot order -- the cells common to n and p in the same colour order
-// k_bt_tasks sums them, so B is bitwise the transpose of B^T -- and condenses
-// it with node n's constraint (the B^T row's C_n^T b).
-__global__ __launch_bounds__(64 * kBtRowWaves) void k_b_rows(
-    CellData cd, int n_rows, const int32_t* __restrict__ p_ptr, const int32_t* __restrict__ p_inc,
-    const int32_t* __restrict__ B_ptr, const int32_t* __restrict__ B_col,
-    const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ B) {
-  __shared__ double vals[kBtRowWaves][216 * 3];
-  __shared__ int node[kBtRowWaves][216];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = int(blockIdx.x) * kBtRowWaves + wave;
-  if (row >= n_rows) return;
-  const int b0 = p_ptr[row], nc = p_ptr[row + 1] - b0;  // <= 8 cells
-  for (int e = lane; e < 27 * nc; e += 64) {
-    const int s = e / 27, t = e - 27 * s;
-    const int inc = p_inc[b0 + s];
-    const int cell = inc >> 3, v = inc & 7;
-    double val[3];
-    bt_cell_entry(cd, P, Q, cell, t, v, val);
-    vals[wave][3 * e] = val[0];
-    vals[wave][3 * e + 1] = val[1];
-    vals[wave][3 * e + 2] = val[2];
-    node[wave][e] = cd.cell_q2[27 * size_t(cell) + t];
-  }
-  wsync();
-  const int r0 = B_ptr[row], len = B_ptr[row + 1] - r0;
-  for (int j = lane; j < len; j += 64) {
-    const int n = B_col[r0 + j];
-    double acc[3] = {0.0, 0.0, 0.0};
-    for (int e = 0; e < 27 * nc; ++e)
-      if (node[wave][e] == n) {
-        acc[0] += vals[wave][3 * e];
-        acc[1] += vals[wave][3 * e + 1];
-        acc[2] += vals[wave][3 * e + 2];
-      }
-    double Ca[3][3];
-    condensation(cd.vcon[n], Ca);
-    double* dst = B + 3 * size_t(r0 + j);
-#pragma unroll
-    for (int jj = 0; jj < 3; ++jj)
-      dst[jj] = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
-  }
-}
-
 }  // namespace
 
 void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdiag, hipStream_t s) {
@@ -2264,6 +2213,19 @@ void launch_nse_operator(const CellData& cd, const ScatterMaps& sm, const int32_
     const char* e = std::getenv("DCP_ASM_RHS_HALFWAVE");
     return !(e && *e == '0');
   }();
+  // The one-launch constrained-diagonal pass (out.cbuf: every (cell, node) into
+  // its own slot, summed per node in colour order by con_gather) runs over the
+  // cells of ALL colours at once; only the half-wave kernel writes slots, the
+  // others add straight into con_diag and would race across colours. So that
+  // pass always takes the half-wave kernel, whatever the timing switches say.
+  if (out.cbuf) {
+    if (!(cd.sep_col && !cd.cell_q2o && !cd.cell_po) || out.Bt || out.B || out.A)
+      throw std::runtime_error("constrained-diagonal slots need the separable-shell rhs kernel");
+    hipLaunchKernelGGL(k_nse_rhs_halfwave, dim3((n + kRhsCellsPerGroup - 1) / kRhsCellsPerGroup),
+                       dim3(256), 0, s, cd, cells, n, u_old, T_old, ph, out);
+    DCP_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const bool sep = cd.sep_col && !cd.cell_q2o && !cd.cell_po && !cell_block;
   if (sep && halfwave && !out.Bt && !out.B && !out.A) {
     hipLaunchKernelGGL(k_nse_rhs_halfwave, dim3((n + kRhsCellsPerGroup - 1) / kRhsCellsPerGroup),
@@ -2388,8 +2350,7 @@ bool mark_first_touch(const int32_t* color_cells, const std::vector<int>& color_
 
 void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, double* Q,
                     int n_tasks, int slots, const int32_t* task_hdr, const int32_t* slot_rec,
-                    double* Bt, int n_prows, const int32_t* p_ptr, const int32_t* p_inc,
-                    const int32_t* B_ptr, const int32_t* B_col, double* B, hipStream_t s) {
+                    double* Bt, hipStream_t s) {
   if (n_cols > 0) {
     hipLaunchKernelGGL(k_bt_coltab, dim3(n_cols), dim3(kBtColEntries), 0, s, cd.sep_colgeo, P);
     DCP_HIP_CHECK(hipGetLastError());
@@ -2403,12 +2364,6 @@ void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, dou
                        dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves), dim3(64 * kBtRowWaves), 0,
                        s, cd, n_tasks, reinterpret_cast<const int4*>(task_hdr),
                        reinterpret_cast<const int4*>(slot_rec), P, Q, Bt);
-    DCP_HIP_CHECK(hipGetLastError());
-  }
-  if (B && n_prows > 0) {
-    hipLaunchKernelGGL(k_b_rows, dim3((n_prows + kBtRowWaves - 1) / kBtRowWaves),
-                       dim3(64 * kBtRowWaves), 0, s, cd, n_prows, p_ptr, p_inc, B_ptr, B_col, P,
-                       Q, B);
     DCP_HIP_CHECK(hipGetLastError());
   }
 }

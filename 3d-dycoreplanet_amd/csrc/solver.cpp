@@ -101,6 +101,7 @@ void ensure_pool(std::vector<double*>& pool, int count, size_t n) {
   while (int(pool.size()) < count) {
     double* p = nullptr;
     DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), (n ? n : 1) * sizeof(double)));
+    dev_mem_alloc(p, (n ? n : 1) * sizeof(double));
     pool.push_back(p);
   }
 }
@@ -809,7 +810,9 @@ State gmres_schur_sstep_ordered(Ctx& c, double* x, const double* b, Control& ctl
   Comm* comm = c.comm.get();
   const bool fused = sstep_fits(c, g.n, nb1);
   // matrix powers: prepared by the caller (block_prec), pool vectors n_ext long
-  const bool mp = comm && c.mp.built && c.mp.version == c.S_version;
+  // (the same condition block_prec prepares them under, so switching the
+  // option off after a solve takes effect even while S is unchanged)
+  const bool mp = comm && c.matrix_powers && c.mp.built && c.mp.version == c.S_version;
   if (!fused) {
     const size_t pn = 2 * size_t(128) * std::max<size_t>(1, size_t((g.n + 511) / 512)) + 2;
     if (c.gm_part.n < pn) {
@@ -1028,7 +1031,10 @@ int block_prec(Ctx& c, const double* src, double* dst, bool do_solve_A, int& inn
       pn = std::max(pn, size_t(c.mp.n_ext));
     }
     if (pn > c.sg_len) {
-      for (double* q : c.sg_v) (void)hipFree(q);
+      for (double* q : c.sg_v) {
+        dev_mem_free(q);
+        (void)hipFree(q);
+      }
       c.sg_v.clear();
       c.sg_len = pn;
     }
@@ -1252,7 +1258,10 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
 void free_workspaces(Ctx& c) {
   c.ilu.reset();  // built on first use per mesh (build_ilu)
   for (auto* pool : {&c.fg_v, &c.fg_z, &c.sg_v, &c.ag_v, &c.fe_v, &c.fe_s, &c.fe_n, &c.sc_v, &c.sc_p}) {
-    for (double* p : *pool) (void)hipFree(p);
+    for (double* p : *pool) {
+      dev_mem_free(p);
+      (void)hipFree(p);
+    }
     pool->clear();
   }
   c.sg_len = 0;

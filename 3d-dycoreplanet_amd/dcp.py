@@ -66,7 +66,8 @@ EXPORTED = [
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
     "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_dist_partition_info_field",
     "dcp_partition_info_field", "dcp_state_set_owned",
-    "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_nse_coupling_export",
+    "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_device_memory",
+    "dcp_nse_coupling_export",
     "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
 
@@ -256,6 +257,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                      C.POINTER(C.c_int)]
     lib.dcp_scatter_info.argtypes = [P, P, P, P]
     lib.dcp_matrix_powers_info.argtypes = [P, P]
+    lib.dcp_device_memory.argtypes = [P, P]
     lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
@@ -1267,6 +1269,16 @@ class Context:
         self._check(lib().dcp_matrix_powers_info(self._h, _ptr(v)))
         return {"built": bool(v[0]), "n_ext": int(v[1]), "rows": [int(x) for x in v[2:5]],
                 "halo_recv": int(v[5]), "value_recv": int(v[6]), "spmv_halo_recv": int(v[7])}
+
+    @staticmethod
+    def device_memory() -> dict:
+        """dcp_device_memory: device bytes held by the buffers this host thread
+        allocated (one rank's context in an in-process group), live and peak."""
+        live, peak = C.c_int64(0), C.c_int64(0)
+        rc = lib().dcp_device_memory(C.byref(live), C.byref(peak))
+        if rc != DCP_OK:
+            raise DcpError(rc, "dcp_device_memory")
+        return {"live": live.value, "peak": peak.value}
 
     def coupling_csr(self, which: str):
         """The operator form's B^T ("Bt", 3 n_vnodes x n_p) or B ("B", n_p x n_u)

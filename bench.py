@@ -161,7 +161,6 @@ def parse():
     ap.add_argument("--prm", default=os.path.join(ROOT, "configs",
                                                   "aqua_planet_shell_test_3d-classic.prm"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-refine", type=int, default=3)
     ap.add_argument("--no-converging-leg", action="store_true",
                     help="skip the converging refine-3 step (GMRES outer iter/s)")
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
@@ -223,57 +222,113 @@ def cpu_info():
     return model, os.cpu_count(), max(1, min(usable, omp) if omp > 0 else usable)
 
 
-def cpu_baseline(refine, outer_k=1):
-    """The oracle (C++ restatement of the reference path) on a bounded sample,
-    timed on this host beside the GPU run, on the same
-    refine-`refine` step the converging leg times on the GPU:
+class _SubMesh:
+    """Cells [c0, c1) of a HostMesh with the whole mesh's dof numbering and
+    constraints (the oracle's input for a bounded sample of its assembly)."""
+
+    def __init__(self, m, c0, c1):
+        self.n_cells = c1 - c0
+        self.cell_nse_dofs = m.cell_nse_dofs[c0:c1]
+        self.cell_T_dofs = m.cell_T_dofs[c0:c1]
+        self.cell_geometry = m.cell_geometry[c0:c1]
+        self.cell_diameter = m.cell_diameter[c0:c1]
+        for k in ("n_u", "n_p", "n_T", "nse_constraints", "T_constraints", "T0"):
+            setattr(self, k, getattr(m, k))
+
+
+def cpu_baseline(ctx, m, refine, gpu_inner_per_s, gpu_full_asm_per_s, outer_refine=3,
+                 outer_k=1):
+    """The oracle (C++ restatement of the reference path) timed on bounded
+    samples of the bench's own workload (refine 5) on this host, beside the GPU
+    run:
     * "Assemble NSE system" (boussinesq_model.tpp:695): the full
-      assemble_nse_system on 1 core and on all usable cores (WorkStream
-      structure: threaded element work, serialized copier in cell order);
-    * "Solve Stokes system" (:1139): the first k = outer_k FGMRES outer
-      iterations of the step (each a block preconditioner application with
-      its inner Schur GMRES, an nse_matrix product and the Gram-Schmidt step)
-      on all usable cores (row-parallel operator applies) and on 1 core."""
+      assemble_nse_system -- element matrices with the velocity block and
+      AffineConstraints::distribute_local_to_global into CSR, WorkStream's
+      result (threaded element work, copier in cell order) -- over a contiguous
+      1/8 of the refine-5 cells in tree order (one 8-way partition's share) on
+      all usable cores, and over 1/64 on one core; scaled to the whole mesh;
+    * the inner Schur GMRES (block_schur_preconditioner.hpp:46-51): 28 steps
+      (one restart cycle) of deal.II's SolverGMRES on the refine-5
+      S = B D_A^-1 B^T, its blocks and the A-Jacobi exported from the GPU
+      context (the parity tests hold them to the oracle's at 1e-12), on all
+      usable cores (row-parallel CSR products) and on one core;
+    * the outer FGMRES (:1139): the first outer iteration of the converging
+      refine-3 step (the r=5 step never completes one; its inner solve fails).
+    same_config_ratio: GPU / CPU at refine 5 for the full assembly (GPU
+    assembly_with_velocity_block, the same output) and the inner Schur GMRES."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import dcp
     import oracle_py
     model, ncpu, threads = cpu_info()
-    m = dcp.HostMesh(refine=refine)
     ph = dcp.classic_physics()
-    orc = oracle_py.Model(ph, m)
-    u = np.zeros(m.n_u + m.n_p)
     n = m.n_u + m.n_p
+    u = np.zeros(n)
+    # 1. assembly samples
+    oracle_py.set_threads(threads)
+    c_all = m.n_cells // 8
+    orc = oracle_py.Model(ph, _SubMesh(m, 0, c_all))
     t0 = time.perf_counter()
     orc.assemble_nse_system(u, m.T0)
-    t1 = time.perf_counter() - t0
+    t_all = time.perf_counter() - t0
+    del orc
+    oracle_py.set_threads(1)
+    c_one = m.n_cells // 64
+    orc = oracle_py.Model(ph, _SubMesh(m, 0, c_one))
     t0 = time.perf_counter()
-    orc.assemble_nse_system_threads(u, m.T0, threads)
-    tn = time.perf_counter() - t0
-    orc.build_nse_preconditioner()
-    solve = {}
+    orc.assemble_nse_system(u, m.T0)
+    t_one = time.perf_counter() - t0
+    del orc
+    full_all = t_all * m.n_cells / c_all
+    full_one = t_one * m.n_cells / c_one
+    # 2. inner Schur GMRES sample on the refine-5 operator
+    Bt, B = ctx.coupling_csr("Bt"), ctx.coupling_csr("B")
+    a_diag, _ = ctx.precond_diagonals()
+    a_inv = 1.0 / a_diag
+    src = np.random.default_rng(20261015).uniform(-1, 1, m.n_p)
+    src -= src.mean()
+    k = 28
+    sol = {}
     for cores in (threads, 1):
-        oracle_py.lib().orc_set_threads(cores)
-        t0 = time.perf_counter()
-        k, its = orc.fgmres_outer(u, outer_k)
-        ts = time.perf_counter() - t0
-        solve[cores] = (k, its, ts)
-    oracle_py.lib().orc_set_threads(1)
-    k, its, ts = solve[threads]
-    k1, its1, ts1 = solve[1]
-    return {"value": n / tn, "unit": "assembled DoFs/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "nproc": ncpu,
-            "sample": f"full assemble_nse_system (element matrices + AffineConstraints "
-                      f"distribute into CSR) of the refine={refine} shell: {m.n_cells} cells, "
-                      f"{n} NSE dofs, {tn:.2f} s on {threads} cores ({t1:.2f} s on 1)",
-            "one_core": {"value": n / t1, "unit": "assembled DoFs/s", "cores": 1},
-            "solve": {"value": its / ts, "unit": "inner Schur GMRES iter/s", "cores": threads,
-                      "outer_iter_per_s": k / ts,
-                      "sample": f"the first k = {k} FGMRES outer iterations of the "
-                                f"refine={refine} step ({its} inner Schur GMRES iterations, "
-                                f"n_p={m.n_p}; the initial guess of the step, no fallback): "
-                                f"{ts:.2f} s on {threads} cores",
-                      "one_core": {"value": its1 / ts1, "outer_iter_per_s": k1 / ts1,
-                                   "cores": 1, "seconds": ts1}}}
+        oracle_py.set_threads(cores)
+        sol[cores] = oracle_py.schur_gmres_sample(Bt, B, a_inv, src, k)[0]
+    del Bt, B
+    # 3. outer FGMRES sample on the converging refine-3 step
+    m3 = dcp.HostMesh(refine=outer_refine)
+    oracle_py.set_threads(threads)
+    orc = oracle_py.Model(ph, m3)
+    orc.assemble_nse_system(np.zeros(m3.n_u + m3.n_p), m3.T0)
+    orc.build_nse_preconditioner()
+    t0 = time.perf_counter()
+    ko, its = orc.fgmres_outer(np.zeros(m3.n_u + m3.n_p), outer_k)
+    ts = time.perf_counter() - t0
+    oracle_py.set_threads(1)
+    del orc
+    out = {"value": n / full_all, "unit": "assembled DoFs/s", "cores": threads, "kind": "port",
+           "cpu_model": model, "nproc": ncpu,
+           "sample": f"full assemble_nse_system (element matrices incl. the velocity block + "
+                     f"AffineConstraints distribute into CSR) over cells [0, {c_all}) of the "
+                     f"refine-{refine} shell (1/8, tree order): {t_all:.2f} s on {threads} cores, "
+                     f"scaled x{m.n_cells / c_all:g} to the {m.n_cells} cells / {n} NSE dofs",
+           "one_core": {"value": n / full_one, "unit": "assembled DoFs/s", "cores": 1,
+                        "sample": f"cells [0, {c_one}) (1/64): {t_one:.2f} s, scaled"},
+           "solve": {"value": k / sol[threads], "unit": "inner Schur GMRES iter/s",
+                     "cores": threads,
+                     "sample": f"{k} steps of deal.II's SolverGMRES (MGS, restart 28) on the "
+                               f"refine-{refine} S = B D_A^-1 B^T (n_p = {m.n_p}; blocks from the GPU "
+                               f"context): {sol[threads]:.2f} s on {threads} cores",
+                     "one_core": {"value": k / sol[1], "cores": 1, "seconds": sol[1]}},
+           "outer": {"value": ko / ts, "unit": "FGMRES outer iter/s", "cores": threads,
+                     "inner_iter_per_s": its / ts,
+                     "sample": f"the first {ko} FGMRES outer iteration(s) of the converging "
+                               f"refine-{outer_refine} step ({its} inner Schur GMRES "
+                               f"iterations): {ts:.2f} s on {threads} cores"}}
+    out["same_config_ratio"] = {
+        "assembly_full": gpu_full_asm_per_s / out["value"] if gpu_full_asm_per_s else None,
+        "inner_gmres": gpu_inner_per_s / out["solve"]["value"],
+        "what": f"refine {refine}, GPU / CPU: the full assembly (GPU "
+                "assembly_with_velocity_block: the same CSR output) and the inner Schur GMRES "
+                "(the GPU's s-step cycles vs the CPU's deal.II GMRES sample)"}
+    return out
 
 
 def converging_leg(make_ctx, args, refine=3):
@@ -762,15 +817,14 @@ def main():
     if world == 1 and not args.no_converging_leg:
         out["converging_step"] = converging_leg(make_ctx, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_refine)
+        progress("cpu baseline")
+        out["cpu_baseline"] = cpu_baseline(
+            ctx, m, args.refine, out["gmres_inner_iter_per_s"],
+            full_matrix["value"] if full_matrix else None)
         cs = out.get("converging_step")
         if cs:
-            # same-config ratios (refine 3): GPU / CPU oracle
-            out["cpu_baseline"]["same_config_ratio"] = {
-                "assembly": cs["assembled_dofs_per_s"] / out["cpu_baseline"]["value"],
-                "inner_gmres": cs["gmres_inner_iter_per_s"] / out["cpu_baseline"]["solve"]["value"],
-                "outer_fgmres": cs["gmres_outer_iter_per_s"]
-                / out["cpu_baseline"]["solve"]["outer_iter_per_s"]}
+            out["cpu_baseline"]["same_config_ratio"]["outer_fgmres_refine3"] = (
+                cs["gmres_outer_iter_per_s"] / out["cpu_baseline"]["outer"]["value"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

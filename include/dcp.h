@@ -447,6 +447,14 @@ int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_t
  * receive count. Zeros on one GPU or before the first such solve. */
 int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]);
 
+/* Device bytes held by the buffers the CALLING host thread allocated through
+ * the library (context state, operators, Krylov pools): live now and the peak.
+ * One context per thread (one rank per process, or one rank per thread in an
+ * in-process group) makes these the context's own footprint. Diagnostic; it
+ * replaces no reference interface (deal.II's MemoryConsumption has no
+ * counterpart on this path). */
+int dcp_device_memory(int64_t* live_bytes, int64_t* peak_bytes);
+
 /* The operator form's coupling blocks of nse_matrix as scalar CSR, without
  * materialising the velocity block: which = 0 -> B^T (3 n_vnodes rows, pressure
  * columns), 1 -> B (n_p rows, velocity columns 3 n + c), the B the Schur

@@ -3,6 +3,7 @@
 #include "oracle.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -239,9 +240,167 @@ Vec3 cross(const Vec3& a, const Vec3& b) {
 // ===========================================================================
 // Element level
 
+namespace {
+// The (a, b) entries, in ddot's lexicographic order, where the symmetric
+// gradients of a component-ci and a component-cj velocity shape can both be
+// non-zero (eps of component c lives in row c and column c). Every other term
+// of ddot(eps_i, eps_j) has an exactly-zero factor.
+int eps_common(int ci, int cj, int* ab) {
+  int n = 0;
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b)
+      if ((a == ci || b == ci) && (a == cj || b == cj)) ab[n++] = 3 * a + b;
+  return n;
+}
+}  // namespace
+
+// The element matrix loops below skip the structural zeros of the FESystem
+// (a velocity shape has one non-zero component; phi_p vanishes on velocity
+// shapes and vice versa) and sum every other term in the literal loop's order,
+// so each entry is bitwise the one of the literal loop of
+// boussinesq_model.tpp:626-637 (orc_cell_nse_system_literal; only the sign of
+// an exact zero may differ). tests/test_oracle_kat.py checks this on every
+// cell of a mesh. They exist to make the refine-5 oracle affordable.
+// Local dofs grouped by component (27 per velocity component, 8 pressure);
+// Kb accumulates the element matrix in that grouped order (entry (i, j) at
+// Kb[89 * pos(i) + pos(j)]) and is permuted into K after the point loop.
+struct CompBlocks {
+  int idx[4][27], cnt[4], pos[89];
+  int ab[3][3][9], nab[3][3];
+  CompBlocks() {
+    for (int c = 0; c < 4; ++c) cnt[c] = 0;
+    int p = 0;
+    for (int c = 0; c < 4; ++c)
+      for (int k = 0; k < 89; ++k)
+        if (sysdof(k).comp == c) {
+          idx[c][cnt[c]++] = k;
+          pos[k] = p++;
+        }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) nab[a][b] = eps_common(a, b, ab[a][b]);
+  }
+};
+const CompBlocks& comp_blocks() {
+  static const CompBlocks cb;
+  return cb;
+}
+
+static void nse_K_q(const NseShapes& sh, double dt, double R2, double JxW, double* Kb) {
+  const CompBlocks& cb = comp_blocks();
+  double V[3][27], E[3][9][27], D[3][27], Pp[8];
+  for (int c = 0; c < 3; ++c)
+    for (int n = 0; n < 27; ++n) {
+      const int k = cb.idx[c][n];
+      V[c][n] = sh.phi_u[k][c];
+      D[c][n] = sh.div[k];
+      for (int e = 0; e < 9; ++e) E[c][e][n] = (&sh.eps[k][0][0])[e];
+    }
+  for (int n = 0; n < 8; ++n) Pp[n] = sh.phi_p[cb.idx[3][n]];
+  for (int ci = 0; ci < 3; ++ci)
+    for (int ii = 0; ii < 27; ++ii) {
+      double* row = Kb + 89 * (27 * ci + ii);
+      for (int cj = 0; cj < 3; ++cj) {
+        const int na = cb.nab[ci][cj];
+        const int* ab = cb.ab[ci][cj];
+        double* r = row + 27 * cj;
+        if (ci == cj) {  // na == 5
+          const double vi = V[ci][ii];
+          const double a0 = E[ci][ab[0]][ii], a1 = E[ci][ab[1]][ii], a2 = E[ci][ab[2]][ii],
+                       a3 = E[ci][ab[3]][ii], a4 = E[ci][ab[4]][ii];
+          const double *b0 = E[cj][ab[0]], *b1 = E[cj][ab[1]], *b2 = E[cj][ab[2]],
+                       *b3 = E[cj][ab[3]], *b4 = E[cj][ab[4]];
+          for (int jj = 0; jj < 27; ++jj) {
+            const double a = vi * V[cj][jj];
+            double s = 0;
+            s += a0 * b0[jj];
+            s += a1 * b1[jj];
+            s += a2 * b2[jj];
+            s += a3 * b3[jj];
+            s += a4 * b4[jj];
+            r[jj] += (a + dt * (R2 * s)) * JxW;
+          }
+        } else {  // na == 2
+          const double a0 = E[ci][ab[0]][ii], a1 = E[ci][ab[1]][ii];
+          const double *b0 = E[cj][ab[0]], *b1 = E[cj][ab[1]];
+          for (int jj = 0; jj < 27; ++jj) {
+            double s = 0;
+            s += a0 * b0[jj];
+            s += a1 * b1[jj];
+            r[jj] += (dt * (R2 * s)) * JxW;
+          }
+        }
+        (void)na;
+      }
+      for (int jp = 0; jp < 8; ++jp) row[81 + jp] += (-(D[ci][ii] * Pp[jp])) * JxW;
+    }
+  for (int ip = 0; ip < 8; ++ip) {
+    double* row = Kb + 89 * (81 + ip);
+    for (int cj = 0; cj < 3; ++cj)
+      for (int jj = 0; jj < 27; ++jj) row[27 * cj + jj] += (-(Pp[ip] * D[cj][jj])) * JxW;
+  }
+}
+
+extern "C" void orc_cell_nse_system_literal(const orc_physics* ph, const double* geom64,
+                                            const double* u_local, const double* T_local,
+                                            double* K, double* f);
+
 extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom64,
                                     const double* u_local, const double* T_local, double* K,
                                     double* f) {
+  // boussinesq_model.tpp:550-673; QGauss(nse_velocity_degree + 1) = 3 (:708)
+  CellValues cv;
+  cv.reinit(geom64, 3);
+  const int tdeg = ph->temperature_degree, ntd = T_dofs_per_cell(tdeg);
+  std::fill(K, K + 89 * 89, 0.0);
+  std::fill(f, f + 89, 0.0);
+  static thread_local NseShapes sh;
+  static thread_local std::vector<double> Kb(89 * 89);
+  std::fill(Kb.begin(), Kb.end(), 0.0);
+  for (int q = 0; q < cv.nq; ++q) {
+    sh.at(cv, q);
+    double old_temperature = 0;
+    for (int k = 0; k < ntd; ++k) old_temperature += T_local[k] * T_value(cv, tdeg, q, k);
+    Vec3 old_velocity;
+    double G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int k = 0; k < 89; ++k) {
+      const SysDof s = sysdof(k);
+      if (s.comp == 3) continue;
+      old_velocity[s.comp] += u_local[k] * sh.phi_u[k][s.comp];
+      for (int d = 0; d < 3; ++d) G[s.comp][d] += u_local[k] * sh.grad[k][s.comp][d];
+    }
+    const double density_scaling =
+        1 - ph->expansion_coefficient * (old_temperature - ph->temperature_ref);
+    Vec3 advection;
+    for (int j = 0; j < 3; ++j)
+      for (int i = 0; i < 3; ++i) advection[j] += old_velocity[i] * G[j][i];
+    Vec3 coriolis;
+    if (ph->cuboid) coriolis[2] = ph->coriolis_scale * ph->omega;
+    const double JxW = cv.JxW[q];
+    const double dt = ph->time_step;
+    nse_K_q(sh, dt, ph->one_over_reynolds * 2, JxW, Kb.data());
+    Vec3 gravity;
+    if (ph->cuboid) {
+      gravity[2] = -ph->gravity_constant;
+    } else {
+      gravity = gravity_vector(cv.xq[q], ph->gravity_constant);
+    }
+    for (int d = 0; d < 3; ++d) gravity[d] *= ph->gravity_scale;
+    const Vec3 cor_x_u = cross(coriolis, old_velocity);
+    for (int i = 0; i < 89; ++i)
+      f[i] += (dot(sh.phi_u[i], old_velocity) + dt * density_scaling * dot(gravity, sh.phi_u[i]) -
+               dt * dot(sh.phi_u[i], advection) - dt * (2 * dot(sh.phi_u[i], cor_x_u))) *
+              JxW;
+  }
+  const CompBlocks& cb = comp_blocks();
+  for (int i = 0; i < 89; ++i)
+    for (int j = 0; j < 89; ++j) K[89 * i + j] = Kb[89 * cb.pos[i] + cb.pos[j]];
+}
+
+// The literal restatement of local_assemble_nse_system (every 89 x 89 term);
+// the checker of the structural-zero loop above (tests/test_oracle_kat.py).
+extern "C" void orc_cell_nse_system_literal(const orc_physics* ph, const double* geom64,
+                                            const double* u_local, const double* T_local,
+                                            double* K, double* f) {
   // boussinesq_model.tpp:550-673; QGauss(nse_velocity_degree + 1) = 3 (:708)
   CellValues cv;
   cv.reinit(geom64, 3);
@@ -300,6 +459,47 @@ extern "C" void orc_cell_nse_system(const orc_physics* ph, const double* geom64,
 
 extern "C" void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom64,
                                             double* P) {
+  // boussinesq_model.tpp:421-464, structural zeros skipped as in nse_K_q:
+  // velocity pairs of one component (dot + (dt/Re) grad:grad over that
+  // component's gradient row) and pressure pairs (phi_p phi_p); bitwise the
+  // literal loop (orc_cell_nse_preconditioner_literal)
+  CellValues cv;
+  cv.reinit(geom64, 3);
+  std::fill(P, P + 89 * 89, 0.0);
+  static thread_local NseShapes sh;
+  const CompBlocks& cb = comp_blocks();
+  const double dtr = ph->time_step * ph->one_over_reynolds;
+  for (int q = 0; q < cv.nq; ++q) {
+    sh.at(cv, q);
+    const double JxW = cv.JxW[q];
+    for (int c = 0; c < 3; ++c) {
+      double V[27], G[3][27];
+      for (int n = 0; n < 27; ++n) {
+        const int k = cb.idx[c][n];
+        V[n] = sh.phi_u[k][c];
+        for (int b = 0; b < 3; ++b) G[b][n] = sh.grad[k][c][b];
+      }
+      for (int ii = 0; ii < 27; ++ii) {
+        double* Pi = P + 89 * cb.idx[c][ii];
+        const double vi = V[ii], g0 = G[0][ii], g1 = G[1][ii], g2 = G[2][ii];
+        for (int jj = 0; jj < 27; ++jj) {
+          const double a = vi * V[jj];
+          double s = 0;
+          s += g0 * G[0][jj];
+          s += g1 * G[1][jj];
+          s += g2 * G[2][jj];
+          Pi[cb.idx[c][jj]] += (a + dtr * s) * JxW;
+        }
+      }
+    }
+    for (int ii = 0; ii < 8; ++ii)
+      for (int jj = 0; jj < 8; ++jj)
+        P[89 * cb.idx[3][ii] + cb.idx[3][jj]] += (sh.phi_p[cb.idx[3][ii]] * sh.phi_p[cb.idx[3][jj]]) * JxW;
+  }
+}
+
+extern "C" void orc_cell_nse_preconditioner_literal(const orc_physics* ph, const double* geom64,
+                                                    double* P) {
   // boussinesq_model.tpp:421-464
   CellValues cv;
   cv.reinit(geom64, 3);
@@ -453,6 +653,20 @@ void add_sorted_unique(std::vector<int>& v) {
   v.erase(std::unique(v.begin(), v.end()), v.end());
 }
 
+// Row split of [0, n) into T ranges of about equal pattern entries.
+std::vector<int> row_split(const std::vector<int>& rowptr, int n, int T) {
+  std::vector<int> s(T + 1, n);
+  s[0] = 0;
+  const long nnz = rowptr.empty() ? n : rowptr[n];
+  int r = 0;
+  for (int t = 1; t < T; ++t) {
+    const long goal = nnz * t / T;
+    while (r < n && (rowptr.empty() ? r : rowptr[r]) < goal) ++r;
+    s[t] = r;
+  }
+  return s;
+}
+
 // Expansion of a local dof under the constraints: unconstrained -> itself,
 // constrained -> its targets with weights (AffineConstraints condensation).
 void expand(const Cons& c, int dof, std::vector<std::pair<int, double>>& out) {
@@ -470,23 +684,34 @@ void expand(const Cons& c, int dof, std::vector<std::pair<int, double>>& out) {
 template <class Coupling>
 void make_pattern(Csr& A, int n, int n_cells, int dpc, const int* cell_dofs, const Cons& cons,
                   Coupling coupling) {
+  // rows split over g_threads threads by range (the sorted unique rows do
+  // not depend on the insertion order)
   std::vector<std::vector<int>> rows(n);
-  std::vector<std::pair<int, double>> ei, ej;
-  for (int c = 0; c < n_cells; ++c) {
-    const int* d = cell_dofs + size_t(c) * dpc;
-    for (int i = 0; i < dpc; ++i) {
-      expand(cons, d[i], ei);
-      for (int j = 0; j < dpc; ++j) {
-        if (!coupling(i, j)) continue;
-        expand(cons, d[j], ej);
-        for (const auto& a : ei)
-          for (const auto& b : ej) rows[a.first].push_back(b.first);
+  const std::vector<int> split = row_split({}, n, g_threads);
+#pragma omp parallel for num_threads(g_threads) schedule(static, 1) if (g_threads > 1)
+  for (int t = 0; t < g_threads; ++t) {
+    const int r0 = split[t], r1 = split[t + 1];
+    std::vector<std::pair<int, double>> ei, ej;
+    for (int c = 0; c < n_cells; ++c) {
+      const int* d = cell_dofs + size_t(c) * dpc;
+      for (int i = 0; i < dpc; ++i) {
+        expand(cons, d[i], ei);
+        bool any_own = false;
+        for (const auto& a : ei) any_own |= a.first >= r0 && a.first < r1;
+        if (!any_own) continue;
+        for (int j = 0; j < dpc; ++j) {
+          if (!coupling(i, j)) continue;
+          expand(cons, d[j], ej);
+          for (const auto& a : ei)
+            if (a.first >= r0 && a.first < r1)
+              for (const auto& b : ej) rows[a.first].push_back(b.first);
+        }
       }
     }
-  }
-  for (int r = 0; r < n; ++r) {
-    if (cons.constrained(r)) rows[r].push_back(r);
-    add_sorted_unique(rows[r]);
+    for (int r = r0; r < r1; ++r) {
+      if (cons.constrained(r)) rows[r].push_back(r);
+      add_sorted_unique(rows[r]);
+    }
   }
   A.build(rows);
 }
@@ -496,28 +721,41 @@ void make_pattern(Csr& A, int n, int n_cells, int dpc, const int* cell_dofs, con
 // false: condensed entries C^T K C, constrained diagonals += |K_ii| (or the
 // mean |K_jj| when K_ii == 0), rhs_t += w f_i, inhomogeneities lifted into
 // unconstrained rows: rhs_r -= K_rj g_j.
+//
+// [r0, r1): only the global rows in this range are written (every entry of
+// such a row gets its contributions in the same order as with the full range).
+// Threads that own disjoint row ranges and each walk all cells in cell order
+// therefore produce bitwise the serial copier's result (assemble_ordered).
 void distribute_local_to_global(const Cons& cons, int dpc, const int* dofs, const double* K,
-                                const double* f, Csr* A, double* rhs) {
+                                const double* f, Csr* A, double* rhs, int r0 = 0,
+                                int r1 = INT32_MAX) {
   std::vector<std::pair<int, double>> ei, ej;
   bool any_constrained = false;
   for (int i = 0; i < dpc; ++i) any_constrained |= cons.constrained(dofs[i]);
+  auto own = [&](int r) { return r >= r0 && r < r1; };
   for (int i = 0; i < dpc; ++i) {
     expand(cons, dofs[i], ei);
+    bool any_own = false;
+    for (const auto& a : ei) any_own |= own(a.first);
+    if (!any_own) continue;
     if (A)
       for (int j = 0; j < dpc; ++j) {
         const double k = K[dpc * i + j];
         if (k == 0.0) continue;
         expand(cons, dofs[j], ej);
         for (const auto& a : ei)
-          for (const auto& b : ej) A->at(a.first, b.first) += a.second * b.second * k;
+          if (own(a.first))
+            for (const auto& b : ej) A->at(a.first, b.first) += a.second * b.second * k;
       }
     if (rhs && f) {
-      for (const auto& a : ei) rhs[a.first] += a.second * f[i];
+      for (const auto& a : ei)
+        if (own(a.first)) rhs[a.first] += a.second * f[i];
       // inhomogeneity of constrained columns j into the rows of i
       for (int j = 0; j < dpc; ++j) {
         const int l = cons.line_of[dofs[j]];
         if (l < 0 || cons.inhom[l] == 0.0) continue;
-        for (const auto& a : ei) rhs[a.first] -= a.second * K[dpc * i + j] * cons.inhom[l];
+        for (const auto& a : ei)
+          if (own(a.first)) rhs[a.first] -= a.second * K[dpc * i + j] * cons.inhom[l];
       }
     }
   }
@@ -526,10 +764,31 @@ void distribute_local_to_global(const Cons& cons, int dpc, const int* dofs, cons
     for (int i = 0; i < dpc; ++i) avg += std::fabs(K[dpc * i + i]);
     avg /= dpc;
     for (int i = 0; i < dpc; ++i)
-      if (cons.constrained(dofs[i])) {
+      if (cons.constrained(dofs[i]) && own(dofs[i])) {
         const double kii = std::fabs(K[dpc * i + i]);
         A->at(dofs[i], dofs[i]) += (kii != 0.0 ? kii : avg);
       }
+  }
+}
+
+// Cell loop of an assembly with WorkStream's result (boussinesq_model.tpp:712-734):
+// element work `compute(c, K, f)` on g_threads threads in chunks of cells, then
+// the copier `scatter(c, K, f, r0, r1)` by the row ranges of `split`, each thread walking the
+// chunk in cell order -- bitwise the serial cell-order copier.
+template <class Compute, class Scatter>
+void assemble_ordered(int n_cells, size_t kmat, size_t kvec, const std::vector<int>& split,
+                      Compute compute, Scatter scatter) {
+  const int T = int(split.size()) - 1, W = g_threads;
+  const int chunk = 128 * std::max(W, 1);
+  std::vector<double> K(size_t(chunk) * kmat), f(size_t(chunk) * kvec);
+  for (int c0 = 0; c0 < n_cells; c0 += chunk) {
+    const int c1 = std::min(n_cells, c0 + chunk);
+#pragma omp parallel for num_threads(W) schedule(dynamic, 2) if (W > 1)
+    for (int c = c0; c < c1; ++c) compute(c, &K[size_t(c - c0) * kmat], &f[size_t(c - c0) * kvec]);
+#pragma omp parallel for num_threads(T) schedule(static, 1) if (T > 1)
+    for (int t = 0; t < T; ++t)
+      for (int c = c0; c < c1; ++c)
+        scatter(c, &K[size_t(c - c0) * kmat], &f[size_t(c - c0) * kvec], split[t], split[t + 1]);
   }
 }
 
@@ -653,47 +912,32 @@ void orc2d_assemble_temperature_rhs(orc_model* m, const double* old_T, const dou
 
 extern "C" void orc_assemble_nse_system(orc_model* m, const double* old_nse, const double* old_T) {
   // assemble_nse_system (:691-740); the four unused block matrices of :700-704 (Q22) are not kept.
+  // WorkStream (:712-734): local_assemble_nse_system per cell, copy_local_to_global_nse_system
+  // (:677-687) in cell order; on g_threads threads bitwise the serial loop (assemble_ordered).
   if (m->dim == 2) return orc2d_assemble_nse_system(m, old_nse, old_T);
   m->nse.zero();
   std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
-  std::vector<double> K(89 * 89), f(89), ul(89), Tl(27);
-  for (int c = 0; c < m->n_cells; ++c) {
-    gather(m->cell_nse, c, 89, old_nse, ul.data());
-    gather(m->cell_T, c, m->tdpc, old_T, Tl.data());
-    orc_cell_nse_system(&m->ph, &m->geom[192 * size_t(c)], ul.data(), Tl.data(), K.data(), f.data());
-    // copy_local_to_global_nse_system (:677-687)
-    distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)], K.data(), f.data(),
-                               &m->nse, m->nse_rhs.data());
-  }
+  assemble_ordered(
+      m->n_cells, 89 * 89, 89, row_split(m->nse.rowptr, m->nse.n, g_threads),
+      [&](int c, double* K, double* f) {
+        double ul[89], Tl[27];
+        gather(m->cell_nse, c, 89, old_nse, ul);
+        gather(m->cell_T, c, m->tdpc, old_T, Tl);
+        orc_cell_nse_system(&m->ph, &m->geom[192 * size_t(c)], ul, Tl, K, f);
+      },
+      [&](int c, const double* K, const double* f, int r0, int r1) {
+        distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)], K, f, &m->nse,
+                                   m->nse_rhs.data(), r0, r1);
+      });
 }
 
 extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_nse,
                                                 const double* old_T, int threads) {
-  if (m->dim == 2) return orc2d_assemble_nse_system(m, old_nse, old_T);
-  // The same assembly as orc_assemble_nse_system with deal.II WorkStream's
-  // structure (boussinesq_model.tpp:712-734): local_assemble_nse_system on
-  // `threads` threads (per-thread scratch), copy_local_to_global serialized in
-  // cell order, so the result is bitwise the single-threaded one. Used only by
-  // bench.py's cpu_baseline (all-cores leg).
-  m->nse.zero();
-  std::fill(m->nse_rhs.begin(), m->nse_rhs.end(), 0.0);
-  const int chunk = 64 * (threads > 0 ? threads : 1);
-  std::vector<double> K(size_t(chunk) * 89 * 89), f(size_t(chunk) * 89);
-  for (int c0 = 0; c0 < m->n_cells; c0 += chunk) {
-    const int c1 = std::min(m->n_cells, c0 + chunk);
-#pragma omp parallel for num_threads(threads) schedule(dynamic, 4)
-    for (int c = c0; c < c1; ++c) {
-      double ul[89], Tl[27];
-      gather(m->cell_nse, c, 89, old_nse, ul);
-      gather(m->cell_T, c, m->tdpc, old_T, Tl);
-      orc_cell_nse_system(&m->ph, &m->geom[192 * size_t(c)], ul, Tl,
-                          &K[size_t(c - c0) * 89 * 89], &f[size_t(c - c0) * 89]);
-    }
-    for (int c = c0; c < c1; ++c)
-      distribute_local_to_global(m->cnse, 89, &m->cell_nse[89 * size_t(c)],
-                                 &K[size_t(c - c0) * 89 * 89], &f[size_t(c - c0) * 89], &m->nse,
-                                 m->nse_rhs.data());
-  }
+  // orc_assemble_nse_system on `threads` threads (bench.py's cpu_baseline legs)
+  const int keep = g_threads;
+  g_threads = threads > 1 ? threads : 1;
+  orc_assemble_nse_system(m, old_nse, old_T);
+  g_threads = keep;
 }
 
 extern "C" void orc_set_inner_max_steps(orc_model* m, int n) { m->inner_max_steps = n; }
@@ -703,48 +947,55 @@ extern "C" void orc_set_block_fixed_inner(orc_model* m, int k) { m->block_fixed_
 extern "C" void orc_build_nse_preconditioner(orc_model* m) {
   // assemble_nse_preconditioner (:479-514) + build_nse_preconditioner (:518-542).
   // Only the diagonals of block(0,0) / block(1,1) are consumed (Ifpack point
-  // Jacobi), so the condensed diagonal is accumulated directly.
+  // Jacobi), so the condensed diagonal is accumulated directly. A pair of
+  // unconstrained local dofs i != j never lands on a diagonal, so only the
+  // other pairs are walked (the same additions in the same order).
   m->A_diag.assign(m->n_u, 0.0);
   m->Mp_diag.assign(m->n_p, 0.0);
   const int npc = m->dim == 2 ? 22 : 89, ngeom = m->dim == 2 ? 32 : 192;
-  std::vector<double> P(npc * npc);
   std::vector<std::pair<int, double>> ei, ej;
-  for (int c = 0; c < m->n_cells; ++c) {
-    if (m->dim == 2)
-      orc2d_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P.data());
-    else
-      orc_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P.data());
-    const int* d = &m->cell_nse[npc * size_t(c)];
-    bool any = false;
-    for (int i = 0; i < npc; ++i) any |= m->cnse.constrained(d[i]);
-    for (int i = 0; i < npc; ++i) {
-      expand(m->cnse, d[i], ei);
-      for (int j = 0; j < npc; ++j) {
-        const double k = P[npc * i + j];
-        if (k == 0.0) continue;
-        expand(m->cnse, d[j], ej);
-        for (const auto& a : ei)
-          for (const auto& b : ej)
-            if (a.first == b.first) {
-              if (a.first < m->n_u)
-                m->A_diag[a.first] += a.second * b.second * k;
-              else
-                m->Mp_diag[a.first - m->n_u] += a.second * b.second * k;
-            }
-      }
-    }
-    if (any) {
-      double avg = 0;
-      for (int i = 0; i < npc; ++i) avg += std::fabs(P[npc * i + i]);
-      avg /= npc;
-      for (int i = 0; i < npc; ++i)
-        if (m->cnse.constrained(d[i])) {
-          const double kii = std::fabs(P[npc * i + i]);
-          const double v = kii != 0.0 ? kii : avg;
-          if (d[i] < m->n_u) m->A_diag[d[i]] += v; else m->Mp_diag[d[i] - m->n_u] += v;
+  assemble_ordered(
+      m->n_cells, size_t(npc) * npc, 0, {0, m->n_u + m->n_p},
+      [&](int c, double* P, double*) {
+        if (m->dim == 2)
+          orc2d_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P);
+        else
+          orc_cell_nse_preconditioner(&m->ph, &m->geom[ngeom * size_t(c)], P);
+      },
+      [&](int c, const double* P, const double*, int, int) {
+        const int* d = &m->cell_nse[npc * size_t(c)];
+        bool any = false;
+        for (int i = 0; i < npc; ++i) any |= m->cnse.constrained(d[i]);
+        for (int i = 0; i < npc; ++i) {
+          const bool ci = m->cnse.constrained(d[i]);
+          for (int j = 0; j < npc; ++j) {
+            const double k = P[npc * i + j];
+            if (k == 0.0) continue;
+            if (!ci && !m->cnse.constrained(d[j]) && d[i] != d[j]) continue;
+            expand(m->cnse, d[i], ei);
+            expand(m->cnse, d[j], ej);
+            for (const auto& a : ei)
+              for (const auto& b : ej)
+                if (a.first == b.first) {
+                  if (a.first < m->n_u)
+                    m->A_diag[a.first] += a.second * b.second * k;
+                  else
+                    m->Mp_diag[a.first - m->n_u] += a.second * b.second * k;
+                }
+          }
         }
-    }
-  }
+        if (any) {
+          double avg = 0;
+          for (int i = 0; i < npc; ++i) avg += std::fabs(P[npc * i + i]);
+          avg /= npc;
+          for (int i = 0; i < npc; ++i)
+            if (m->cnse.constrained(d[i])) {
+              const double kii = std::fabs(P[npc * i + i]);
+              const double v = kii != 0.0 ? kii : avg;
+              if (d[i] < m->n_u) m->A_diag[d[i]] += v; else m->Mp_diag[d[i] - m->n_u] += v;
+            }
+        }
+      });
   m->A_inv.resize(m->n_u);
   m->Mp_inv.resize(m->n_p);
   for (int i = 0; i < m->n_u; ++i) m->A_inv[i] = 1.0 / m->A_diag[i];
@@ -757,13 +1008,16 @@ extern "C" void orc_assemble_temperature_matrix(orc_model* m) {
   m->Tmass.zero();
   m->Tstiff.zero();
   const int n = m->tdpc;
-  std::vector<double> M(n * n), K(n * n);
-  for (int c = 0; c < m->n_cells; ++c) {
-    orc_cell_temperature_matrix(&m->ph, &m->geom[192 * size_t(c)], M.data(), K.data());
-    const int* d = &m->cell_T[size_t(n) * c];
-    distribute_local_to_global(m->cT, n, d, M.data(), nullptr, &m->Tmass, nullptr);
-    distribute_local_to_global(m->cT, n, d, K.data(), nullptr, &m->Tstiff, nullptr);
-  }
+  assemble_ordered(
+      m->n_cells, size_t(2 * n * n), 0, row_split(m->Tmass.rowptr, m->n_T, g_threads),
+      [&](int c, double* MK, double*) {
+        orc_cell_temperature_matrix(&m->ph, &m->geom[192 * size_t(c)], MK, MK + n * n);
+      },
+      [&](int c, const double* MK, const double*, int r0, int r1) {
+        const int* d = &m->cell_T[size_t(n) * c];
+        distribute_local_to_global(m->cT, n, d, MK, nullptr, &m->Tmass, nullptr, r0, r1);
+        distribute_local_to_global(m->cT, n, d, MK + n * n, nullptr, &m->Tstiff, nullptr, r0, r1);
+      });
 }
 
 extern "C" void orc_assemble_temperature_rhs(orc_model* m, const double* old_T,
@@ -777,17 +1031,21 @@ extern "C" void orc_assemble_temperature_rhs(orc_model* m, const double* old_T,
   std::fill(m->T_rhs.begin(), m->T_rhs.end(), 0.0);
   if (m->dim == 2) return orc2d_assemble_temperature_rhs(m, old_T, nse_solution);
   const int n = m->tdpc;
-  std::vector<double> Tl(n), ul(89), rhs(n), mfbc(n * n);
-  std::vector<int> mask(n);
-  for (int c = 0; c < m->n_cells; ++c) {
-    const int* d = &m->cell_T[size_t(n) * c];
-    gather(m->cell_T, c, n, old_T, Tl.data());
-    gather(m->cell_nse, c, 89, nse_solution, ul.data());
-    for (int i = 0; i < n; ++i) mask[i] = m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0;
-    orc_cell_temperature_rhs(&m->ph, &m->geom[192 * size_t(c)], Tl.data(), ul.data(), mask.data(),
-                             rhs.data(), mfbc.data());
-    distribute_rhs_with_bc(m->cT, n, d, rhs.data(), mfbc.data(), m->T_rhs.data());
-  }
+  assemble_ordered(
+      m->n_cells, size_t(n * n), size_t(n), {0, m->n_T},
+      [&](int c, double* mfbc, double* rhs) {
+        const int* d = &m->cell_T[size_t(n) * c];
+        double Tl[27], ul[89];
+        int mask[27];
+        gather(m->cell_T, c, n, old_T, Tl);
+        gather(m->cell_nse, c, 89, nse_solution, ul);
+        for (int i = 0; i < n; ++i)
+          mask[i] = m->cT.constrained(d[i]) && m->cT.inhom[m->cT.line_of[d[i]]] != 0.0;
+        orc_cell_temperature_rhs(&m->ph, &m->geom[192 * size_t(c)], Tl, ul, mask, rhs, mfbc);
+      },
+      [&](int c, const double* mfbc, const double* rhs, int, int) {
+        distribute_rhs_with_bc(m->cT, n, &m->cell_T[size_t(n) * c], rhs, mfbc, m->T_rhs.data());
+      });
 }
 
 extern "C" long orc_nse_matrix_nnz(const orc_model* m) { return long(m->nse.cols.size()); }
@@ -795,6 +1053,29 @@ extern "C" void orc_nse_matrix_csr(const orc_model* m, int* rowptr, int* cols, d
   std::copy(m->nse.rowptr.begin(), m->nse.rowptr.end(), rowptr);
   std::copy(m->nse.cols.begin(), m->nse.cols.end(), cols);
   std::copy(m->nse.vals.begin(), m->nse.vals.end(), vals);
+}
+// One block of nse_matrix (which: 0 = (0,0) A, 1 = (0,1) B^T, 2 = (1,0) B) as
+// CSR with block-local columns; rowptr NULL: return the block's nnz only.
+extern "C" long orc_nse_block_csr(const orc_model* m, int which, int* rowptr, int* cols,
+                                  double* vals) {
+  const int nu = m->n_u, n = m->nse.n;
+  const int r0 = which == 2 ? nu : 0, r1 = which == 2 ? n : nu;
+  const int c0 = which == 1 ? nu : 0, c1 = which == 1 ? n : nu;
+  long k = 0;
+  if (rowptr) rowptr[0] = 0;
+  for (int r = r0; r < r1; ++r) {
+    for (int e = m->nse.rowptr[r]; e < m->nse.rowptr[r + 1]; ++e) {
+      const int c = m->nse.cols[e];
+      if (c < c0 || c >= c1) continue;
+      if (rowptr) {
+        cols[k] = c - c0;
+        vals[k] = m->nse.vals[e];
+      }
+      ++k;
+    }
+    if (rowptr) rowptr[r - r0 + 1] = int(k);
+  }
+  return k;
 }
 extern "C" void orc_nse_rhs(const orc_model* m, double* out) {
   std::copy(m->nse_rhs.begin(), m->nse_rhs.end(), out);
@@ -1300,6 +1581,45 @@ extern "C" int orc_solve_nse(orc_model* m, double* sol, int* outer_it, int* inne
 // solve_NSE_block_preconditioned cut at k outer iterations (SolverControl(k)),
 // no fallback; the initial guess as the solve sets it up. Returns the
 // iterations done, inner Schur GMRES iterations to *inner_it.
+// CPU baseline sample of the inner Schur GMRES at any size, on given coupling
+// blocks: deal.II's SolverGMRES (modified Gram-Schmidt, restart 28) on
+// S = B (D_A^-1 (B^T p)) (schur_complement.hpp:143-150 with the A-Jacobi, Q9),
+// held at exactly k steps; the CSR products row-parallel on g_threads threads
+// (Epetra's row-distributed SpMV). Bt: n_u x n_p, B: n_p x n_u (block-local
+// columns), A_inv: n_u. Returns the wall seconds of the k steps; dst_p gets the
+// iterate.
+extern "C" double orc_schur_gmres_sample(int n_u, int n_p, const int* bt_ptr, const int* bt_col,
+                                         const double* bt_val, const int* b_ptr, const int* b_col,
+                                         const double* b_val, const double* A_inv,
+                                         const double* src_p, double* dst_p, int k) {
+  std::vector<double> t1(n_u), t2(n_u);
+  auto csr = [](int rows, const int* rp, const int* cl, const double* v, const double* x,
+                double* y) {
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
+    for (int r = 0; r < rows; ++r) {
+      double s = 0;
+      for (int e = rp[r]; e < rp[r + 1]; ++e) s += v[e] * x[cl[e]];
+      y[r] = s;
+    }
+  };
+  std::fill(dst_p, dst_p + n_p, 0.0);
+  Control ctl{unsigned(k), 0.0};
+  int it = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  try {
+    gmres(
+        n_p,
+        [&](const double* x, double* y) {
+          csr(n_u, bt_ptr, bt_col, bt_val, x, t1.data());
+          for (int i = 0; i < n_u; ++i) t2[i] = t1[i] * A_inv[i];
+          csr(n_p, b_ptr, b_col, b_val, t2.data(), y);
+        },
+        [&](const double* x, double* y) { std::copy(x, x + n_p, y); }, dst_p, src_p, ctl, it);
+  } catch (const NoConvergence&) {
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 extern "C" int orc_fgmres_outer(orc_model* m, const double* sol, int k, int* inner_it) {
   const int nu = m->n_u, np = m->n_p, n = nu + np;
   const double dt = m->ph.time_step;

@@ -62,6 +62,16 @@ void orc_cell_nse_system(const orc_physics* ph, const double* geom64,
                          double* K /*89x89 row-major*/, double* f /*89*/);
 /* local_assemble_nse_preconditioner (:421-464) */
 void orc_cell_nse_preconditioner(const orc_physics* ph, const double* geom64, double* P);
+/* The same two element matrices with every 89 x 89 term of the reference
+ * loops evaluated (the functions above skip the FESystem's structural zeros
+ * and are bitwise these, up to the sign of exact zeros). */
+void orc_cell_nse_system_literal(const orc_physics* ph, const double* geom64,
+                                 const double* u_local, const double* T_local, double* K,
+                                 double* f);
+void orc_cell_nse_preconditioner_literal(const orc_physics* ph, const double* geom64, double* P);
+/* Threads of the oracle's cell loops (copier by row ranges, bitwise the
+ * serial cell-order copier) and row-parallel operator applies; default 1. */
+void orc_set_threads(int n);
 /* local_assemble_temperature_matrix (:748-800) */
 void orc_cell_temperature_matrix(const orc_physics* ph, const double* geom64, double* M,
                                  double* K);
@@ -117,6 +127,9 @@ void orc_assemble_temperature_rhs(orc_model* m, const double* old_T, const doubl
 long orc_nse_matrix_nnz(const orc_model* m);
 void orc_nse_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals);
 void orc_nse_rhs(const orc_model* m, double* out);
+/* one block of nse_matrix (0: A, 1: B^T, 2: B), block-local columns; rowptr
+ * NULL: returns the block's nnz only */
+long orc_nse_block_csr(const orc_model* m, int which, int* rowptr, int* cols, double* vals);
 void orc_precond_diagonals(const orc_model* m, double* A_diag /*n_u*/, double* Mp_diag /*n_p*/);
 long orc_T_matrix_nnz(const orc_model* m);
 void orc_T_matrix_csr(const orc_model* m, int* rowptr, int* cols, double* vals);
@@ -139,6 +152,14 @@ int orc_solve_nse_schur(orc_model* m, double* nse_solution /*inout*/, int* schur
                         int* a_solves);
 /* AztecOO A-GMRES iterations of the last orc_solve_nse (do_solve_A fallback). */
 long orc_a_solve_iterations(const orc_model* m);
+
+/* CPU baseline sample: deal.II's SolverGMRES on S = B (D_A^-1 (B^T p)) from given
+ * coupling blocks (block-local CSR columns), exactly k steps on orc_set_threads
+ * threads; returns the wall seconds, dst_p the iterate. */
+double orc_schur_gmres_sample(int n_u, int n_p, const int* bt_ptr, const int* bt_col,
+                              const double* bt_val, const int* b_ptr, const int* b_col,
+                              const double* b_val, const double* A_inv, const double* src_p,
+                              double* dst_p, int k);
 
 /* Step control (get_maximal_velocity / get_cfl_number, :1023-1101). */
 double orc_max_velocity(const orc_model* m, const double* nse_solution);

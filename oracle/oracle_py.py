@@ -57,6 +57,10 @@ def lib():
         L.orc_nse_matrix_nnz.restype = C.c_long
         L.orc_nse_matrix_csr.argtypes = [P, P, P, P]
         L.orc_nse_rhs.argtypes = [P, P]
+        L.orc_nse_block_csr.argtypes = [P, I, P, P, P]
+        L.orc_nse_block_csr.restype = C.c_long
+        L.orc_cell_nse_system_literal.argtypes = [P, P, P, P, P, P]
+        L.orc_cell_nse_preconditioner_literal.argtypes = [P, P, P]
         L.orc_precond_diagonals.argtypes = [P, P, P]
         L.orc_T_matrix_nnz.argtypes = [P]
         L.orc_T_matrix_nnz.restype = C.c_long
@@ -74,6 +78,8 @@ def lib():
         L.orc_set_block_fixed_inner.argtypes = [P, I]
         L.orc_set_threads.argtypes = [I]
         L.orc_fgmres_outer.argtypes = [P, P, I, P]
+        L.orc_schur_gmres_sample.argtypes = [I, I, P, P, P, P, P, P, P, P, P, I]
+        L.orc_schur_gmres_sample.restype = D
         L.orc_a_solve_iterations.argtypes = [P]
         L.orc_a_solve_iterations.restype = C.c_long
         L.orc_max_velocity.argtypes = [P, P]
@@ -128,6 +134,39 @@ def cell_nse_system(ph, geom64, u_local, T_local):
                               _p(np.ascontiguousarray(u_local, np.float64)),
                               _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
     return K, f
+
+
+def cell_nse_system_literal(ph, geom64, u_local, T_local):
+    """The literal 89 x 89 loop of local_assemble_nse_system (checker of the
+    structural-zero loop cell_nse_system uses)."""
+    K = np.zeros((89, 89))
+    f = np.zeros(89)
+    o = physics(ph)
+    lib().orc_cell_nse_system_literal(C.byref(o), _p(np.ascontiguousarray(geom64, np.float64)),
+                                      _p(np.ascontiguousarray(u_local, np.float64)),
+                                      _p(np.ascontiguousarray(T_local, np.float64)), _p(K), _p(f))
+    return K, f
+
+
+def cell_nse_preconditioner_literal(ph, geom64):
+    P = np.zeros((89, 89))
+    o = physics(ph)
+    lib().orc_cell_nse_preconditioner_literal(C.byref(o),
+                                              _p(np.ascontiguousarray(geom64, np.float64)), _p(P))
+    return P
+
+
+def set_threads(n):
+    """Threads of the oracle's cell loops and operator applies (bitwise the
+    serial results)."""
+    lib().orc_set_threads(int(n))
+
+
+def usable_threads(cap=16):
+    """Cores this process may use, capped (the GPU box's CPU share is 16)."""
+    import os
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(cap, n))
 
 
 def cell_nse_preconditioner(ph, geom64):
@@ -231,6 +270,16 @@ class Model:
         n = self.mesh.n_u + self.mesh.n_p
         rp, cols, vals = np.zeros(n + 1, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
         lib().orc_nse_matrix_csr(self.h, _p(rp), _p(cols), _p(vals))
+        return rp, cols, vals
+
+    def nse_block_csr(self, which):
+        """One block of nse_matrix as (rowptr, cols, vals): "A" (0,0), "Bt" (0,1),
+        "B" (1,0), with block-local columns."""
+        w = {"A": 0, "Bt": 1, "B": 2}[which]
+        nnz = lib().orc_nse_block_csr(self.h, w, None, None, None)
+        nr = self.mesh.n_p if which == "B" else self.mesh.n_u
+        rp, cols, vals = np.zeros(nr + 1, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
+        lib().orc_nse_block_csr(self.h, w, _p(rp), _p(cols), _p(vals))
         return rp, cols, vals
 
     def nse_rhs(self):
@@ -405,6 +454,20 @@ class FeecModel:
         out = np.zeros(2)
         lib().orc_feec_velocity_stats(self.h, _p(np.ascontiguousarray(sol, np.float64)), _p(out))
         return out
+
+
+def schur_gmres_sample(Bt, B, A_inv, src_p, k):
+    """CPU baseline sample: k steps of deal.II's SolverGMRES on
+    S = B (D_A^-1 (B^T p)) from the CSR triples Bt (n_u x n_p) and B (n_p x n_u).
+    Returns (seconds, iterate)."""
+    (btp, btc, btv), (bp, bc, bv) = Bt, B
+    n_u, n_p = len(btp) - 1, len(bp) - 1
+    arr = [np.ascontiguousarray(a, t) for a, t in ((btp, np.int32), (btc, np.int32), (btv, np.float64),
+                                                      (bp, np.int32), (bc, np.int32), (bv, np.float64),
+                                                      (A_inv, np.float64), (src_p, np.float64))]
+    dst = np.zeros(n_p)
+    sec = lib().orc_schur_gmres_sample(n_u, n_p, *[_p(a) for a in arr], _p(dst), int(k))
+    return sec, dst
 
 
 def cuthill_mckee_nse(cell_nse_dofs, n_vnodes, n_u, n_p):

@@ -236,3 +236,62 @@ def test_shell_solve_converges_r2():
     o.build_nse_preconditioner()
     rc, x, outer, inner = o.solve_nse(u)
     assert rc == 0 and outer < 40 and inner < 2000
+
+
+@pytest.mark.parametrize("cuboid", [False, True])
+def test_structural_zero_loops_are_the_literal_loops(cuboid):
+    """orc_cell_nse_system / orc_cell_nse_preconditioner skip the FESystem's
+    structural zeros and sum every other term in the order of the literal
+    89 x 89 loops of boussinesq_model.tpp:626-637 / :421-464: every entry must
+    be bitwise the literal one (numpy equality, so +0 == -0), on every cell of
+    a mesh, with a random state."""
+    m = dcp.HostMesh(cuboid=cuboid, refine=1 if cuboid else 2)
+    ph = dcp.classic_physics()
+    ph.cuboid = int(cuboid)
+    rng = np.random.default_rng(7)
+    u = rng.uniform(-1, 1, m.n_u + m.n_p)
+    T = rng.uniform(-1, 1, m.n_T)
+    for c in range(m.n_cells):
+        g, ul, Tl = m.cell_geometry[c], u[m.cell_nse_dofs[c]], T[m.cell_T_dofs[c]]
+        K, f = oracle_py.cell_nse_system(ph, g, ul, Tl)
+        Kl, fl = oracle_py.cell_nse_system_literal(ph, g, ul, Tl)
+        assert np.array_equal(K, Kl) and np.array_equal(f, fl), c
+        assert np.array_equal(oracle_py.cell_nse_preconditioner(ph, g),
+                              oracle_py.cell_nse_preconditioner_literal(ph, g)), c
+
+
+def test_threaded_assembly_is_the_serial_assembly():
+    """The oracle's cell loops on several threads (element work in parallel, the
+    copier by row ranges in cell order) give bitwise the serial cell-order
+    copier's matrix, rhs, preconditioner diagonals and temperature system."""
+    m = dcp.HostMesh(refine=2)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(11)
+    u = rng.uniform(-1, 1, m.n_u + m.n_p)
+    T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+    out = []
+    try:
+        for th in (1, 4):
+            oracle_py.set_threads(th)
+            orc = oracle_py.Model(ph, m)
+            orc.assemble_nse_system(u, T)
+            orc.build_nse_preconditioner()
+            orc.assemble_temperature_matrix()
+            orc.assemble_temperature_rhs(T, u)
+            out.append([*orc.nse_matrix_csr(), orc.nse_rhs(), *orc.precond_diagonals(),
+                        *orc.T_matrix_csr(), orc.T_rhs(), orc.nse_vmult(u),
+                        orc.schur_vmult(u[m.n_u:])])
+    finally:
+        oracle_py.set_threads(1)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    # the block accessor is the slice of the full CSR
+    import scipy.sparse as sp
+    n = m.n_u + m.n_p
+    A = sp.csr_matrix((out[0][2], out[0][1], out[0][0]), shape=(n, n))
+    orc = oracle_py.Model(ph, m)
+    orc.assemble_nse_system(u, T)
+    for key, blk in (("Bt", A[:m.n_u, m.n_u:]), ("B", A[m.n_u:, :m.n_u]), ("A", A[:m.n_u, :m.n_u])):
+        rp, cols, vals = orc.nse_block_csr(key)
+        S = sp.csr_matrix((vals, cols, rp), shape=blk.shape)
+        assert (S != blk).nnz == 0, key

@@ -640,3 +640,54 @@ def test_handoff_timeout_reruns_on_multi_launch_kernels(gs):
     assert abs(inner - inner_o) <= 0.10 * inner_o
     assert rel2(ctx.get_state(dcp.NSE_SOLUTION), x_o) < 1e-10
     ctx.close()
+
+
+_SWITCH_CHILD = r"""
+import sys
+sys.path[:0] = sys.argv[1:3]
+import numpy as np
+import dcp, oracle_py
+m = dcp.HostMesh(refine=2)
+ph = dcp.classic_physics()
+rng = np.random.default_rng(20261015)
+u = rng.uniform(-1, 1, m.n_u + m.n_p)
+T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+ctx = dcp.Context()
+ctx.set_physics(ph)
+ctx.upload_mesh(m)
+ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+ctx.set_state(dcp.OLD_T_SOLUTION, T)
+ctx.assemble_nse_system()
+orc = oracle_py.Model(ph, m)
+orc.assemble_nse_system(u, T)
+x = rng.uniform(-1, 1, m.n_u + m.n_p)
+y, yo = ctx.nse_vmult(x), orc.nse_vmult(x)
+e = np.max(np.abs(y - yo)) / np.max(np.abs(yo))
+r, ro = ctx.get_state(dcp.NSE_RHS), orc.nse_rhs()
+er = np.max(np.abs(r - ro)) / np.max(np.abs(ro))
+ctx.close()
+print("apply", e, "rhs", er)
+assert e < 1e-12 and er < 1e-12
+"""
+
+
+@pytest.mark.parametrize("switch", ["DCP_ASM_RHS_HALFWAVE=0", "DCP_ASM_CELL_BLOCK=1"])
+def test_assembly_timing_switches_keep_constrained_diagonals(switch):
+    """The one-launch constrained-diagonal pass of the operator-form assembly
+    writes per-(cell, node) slots that only the half-wave rhs kernel fills;
+    the timing switches that pick another cell kernel for the rhs must not
+    reach that pass (they would add into con_diag across colours at once).
+    Each switch is read once per process, so the assembly runs in a child
+    process with it set; the operator (constrained rows carry con_diag) and
+    the rhs against the oracle at 1e-12."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    k, v = switch.split("=")
+    env = dict(os.environ, **{k: v})
+    out = subprocess.run([sys.executable, "-c", _SWITCH_CHILD,
+                          os.path.join(root, "3d-dycoreplanet_amd"), os.path.join(root, "oracle")],
+                         env=env, capture_output=True, text=True, timeout=300)
+    print(out.stdout, out.stderr[-2000:])
+    assert out.returncode == 0
