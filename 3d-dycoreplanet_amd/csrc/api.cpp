@@ -1,6 +1,7 @@
 // C ABI implementation (include/dcp.h): context management, the one-off
 // mesh/DoF upload (patterns, colouring, scatter maps) and the hot-path calls.
 #include <algorithm>
+#include <queue>
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -398,6 +399,112 @@ std::vector<int> partition_colour_hint(int n_cells, const int32_t* cell_nse_dofs
 
 // Host half of dcp_mesh_upload: validation, node map, node-local constraints,
 // colouring and block patterns (no device access, so it is testable on CPU).
+// The fused matrix-free apply's schedule (k_mf_fused):
+// the pencil batches keep the two-launch kernel's XCD placement (XCD x works
+// its contiguous batch range in order; workgroup id = XCD + 8 k), and every
+// gather window is placed at least `lag` ids after the last batch it reads
+// records from, so by the time an XCD dispatches it its inputs are usually
+// complete and the poll costs one load. Only meshes whose apply runs as one
+// chunk of one-wave batches (the default) get a schedule.
+void build_mf_fused(Ctx& c, int n_cells, int nv, int n_p, const std::vector<int32_t>& vptr, const std::vector<int32_t>& pptr,
+                    const std::vector<int32_t>& vslot, const std::vector<int32_t>& pslot,
+                    int32_t pbase) {
+  c.mf_fused = false;
+  c.mf_ntasks = 0;
+  // off by default: measured slower than the two launches
+  const char* env = std::getenv("DCP_MF_FUSED");
+  if (!(env && *env == '1') || c.mf_chunks != 1 || kMfGroupCells != 7 || n_cells <= 0) return;
+  const int n_pen = (n_cells + 6) / 7;
+  const int nvw = (nv + 63) / 64, npw = (n_p + 63) / 64, nw = nvw + npw;
+  // slot -> batch of the records
+  std::vector<int32_t> vb(size_t(vptr[nv]), -1), pb(size_t(pptr[n_p]), -1);
+  for (int cell = 0; cell < n_cells; ++cell) {
+    for (int t = 0; t < 27; ++t) {
+      const int32_t sl = vslot[27 * size_t(cell) + t];
+      if (sl >= 0) vb[size_t(sl / 3)] = cell / 7;
+    }
+    for (int v = 0; v < 8; ++v) pb[size_t(pslot[8 * size_t(cell) + v] - pbase)] = cell / 7;
+  }
+  // per window its distinct batches
+  std::vector<int32_t> dep_ptr(size_t(nw) + 1, 0), dep;
+  dep.reserve(size_t(nw) * 24);
+  std::vector<int32_t> tmp;
+  for (int w = 0; w < nw; ++w) {
+    tmp.clear();
+    if (w < nvw) {
+      const int n0 = 64 * w, n1 = std::min(n0 + 64, nv);
+      for (int k = vptr[n0]; k < vptr[n1]; ++k) tmp.push_back(vb[size_t(k)]);
+    } else {
+      const int j0 = 64 * (w - nvw), j1 = std::min(j0 + 64, n_p);
+      for (int k = pptr[j0]; k < pptr[j1]; ++k) tmp.push_back(pb[size_t(k)]);
+    }
+    std::sort(tmp.begin(), tmp.end());
+    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+    for (int32_t b : tmp)
+      if (b < 0) return;  // a slot no batch writes: no schedule
+    dep.insert(dep.end(), tmp.begin(), tmp.end());
+    dep_ptr[size_t(w) + 1] = int32_t(dep.size());
+  }
+  // batch -> dependent windows
+  std::vector<int32_t> rptr(size_t(n_pen) + 1, 0), rw(dep.size());
+  for (int32_t b : dep) rptr[size_t(b) + 1]++;
+  for (int b = 0; b < n_pen; ++b) rptr[b + 1] += rptr[b];
+  {
+    std::vector<int32_t> f(rptr.begin(), rptr.end() - 1);
+    for (int w = 0; w < nw; ++w)
+      for (int k = dep_ptr[w]; k < dep_ptr[w + 1]; ++k) rw[size_t(f[size_t(dep[k])]++)] = w;
+  }
+  // the two-launch kernel's XCD ranges (xcd_block)
+  const int q = n_pen >> 3, r = n_pen & 7;
+  int start[8], cnt[8], pos[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int x = 0; x < 8; ++x) {
+    cnt[x] = q + (x < r ? 1 : 0);
+    start[x] = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  }
+  const char* env_lag = std::getenv("DCP_MF_FUSED_LAG");
+  const long lag = env_lag ? std::atol(env_lag) : 3072;
+  std::vector<int32_t> left(static_cast<size_t>(nw));
+  for (int w = 0; w < nw; ++w) left[w] = dep_ptr[w + 1] - dep_ptr[w];
+  using Ready = std::pair<long, int32_t>;  // (ready id, window)
+  std::priority_queue<Ready, std::vector<Ready>, std::greater<Ready>> ready;
+  std::vector<int32_t> sched;
+  sched.reserve(size_t(n_pen) + size_t(nw) + 64);
+  int pen_done = 0, win_done = 0;
+  for (long id = 0; pen_done < n_pen || win_done < nw; ++id) {
+    const int x = int(id & 7);
+    if (!ready.empty() && ready.top().first <= id) {
+      sched.push_back((ready.top().second < nvw ? 1 << 30 : 2 << 30) |
+                      (ready.top().second < nvw ? ready.top().second : ready.top().second - nvw));
+      ready.pop();
+      ++win_done;
+    } else if (pos[x] < cnt[x]) {
+      const int b = start[x] + pos[x]++;
+      sched.push_back(b);
+      ++pen_done;
+      for (int k = rptr[b]; k < rptr[b + 1]; ++k) {
+        const int w = rw[size_t(k)];
+        if (--left[w] == 0) ready.push({id + lag, w});
+      }
+    } else if (!ready.empty()) {
+      sched.push_back((ready.top().second < nvw ? 1 << 30 : 2 << 30) |
+                      (ready.top().second < nvw ? ready.top().second : ready.top().second - nvw));
+      ready.pop();
+      ++win_done;
+    } else {
+      sched.push_back(3 << 30);  // padding: this XCD's batches are out, no window ready
+    }
+  }
+  c.mf_sched.upload(sched);
+  c.mf_dep_ptr.upload(dep_ptr);
+  c.mf_dep.upload(dep);
+  c.mf_done.alloc(size_t(n_pen));
+  c.mf_done.zero(c.stream);
+  c.mf_seq = 0;
+  c.mf_ntasks = int(sched.size());
+  c.mf_nvwin = nvw;
+  c.mf_fused = true;
+}
+
 void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
                   const int32_t* cell_T_dofs, const double* cell_geometry,
                   const double* cell_diameter, int n_u, int n_p, int n_T,
@@ -1657,6 +1764,10 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->feec_zero_mean = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_FEEC_BLOCK_PRECONDITIONER) {
+      ctx->feec_block_prec = value != 0;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_FEEC_FIXED_INNER) {
       require(value >= 0 && value <= 100, DCP_ERR_INVALID,
               "DCP_OPT_FEEC_FIXED_INNER must be in [0, 100]");
@@ -2072,6 +2183,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           DCP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         DCP_HIP_CHECK(hipEventCreateWithFlags(&c.mf_join_ev, hipEventDisableTiming));
       }
+      build_mf_fused(c, n_cells, nv, n_p, vptr, pptr, vslot, pslot, pbase);
       c.mf_cmask.upload(cmask);
       c.mf_vptr.upload(vptr);
       c.mf_vslot.upload(vslot);
@@ -2186,7 +2298,10 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
                             "B^T task: two vertices of a cell map to one entry");
                   dm |= uint64_t(dest[v]) << (FB * v);
                 }
-                rec.insert(rec.end(), {col[size_t(cell)], layer[size_t(cell)] << 16 | lex << 8 | (n - first),
+                // bit 15: the row's node is constrained (the entry lanes load its
+                // NodeConstraint only then; unconstrained rows condense by identity)
+                const int con = vc[n].type != 0 ? 1 << 15 : 0;
+                rec.insert(rec.end(), {col[size_t(cell)], layer[size_t(cell)] << 16 | con | lex << 8 | (n - first),
                                        int32_t(uint32_t(dm)), int32_t(uint32_t(dm >> 32))});
                 ++ns;
               }
@@ -2612,13 +2727,19 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     }
     if (rhs_co) {
       const MfCells mc = c.mfc();
-      for (int k = 0; k < c.mf_chunks; ++k)
-        mf_rhs_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.old_nse.p, c.old_T.p, c.ph,
-                     c.mf_buf.p, c.stream);
       MfGather g = c.mfg();
       g.cdiag = nullptr;  // condensation only
       g.pcidx = nullptr;
-      mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
+      if (c.mf_fused && c.hmapped) {
+        if (++c.mf_seq == 0) ++c.mf_seq;
+        mf_rhs_fused(mc, g, c.mff(c.hmapped + kMfErrSlot), c.mf_ntasks, c.old_nse.p, c.old_T.p,
+                     c.ph, c.mf_buf.p, c.nse_rhs.p, c.mf_seq, c.stream);
+      } else {
+        for (int k = 0; k < c.mf_chunks; ++k)
+          mf_rhs_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.old_nse.p, c.old_T.p, c.ph,
+                       c.mf_buf.p, c.nse_rhs.p, c.stream);
+        mf_gather(g, 0, c.n_vnodes, 0, 0, false, c.mf_buf.p, nullptr, c.nse_rhs.p, c.stream);
+      }
     }
     if (bt_rows && overlap != 1 && overlap != 3) launch_bt();
     if (overlap) {
@@ -2771,6 +2892,7 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     const int rc = solve_nse(c, outer, inner);
     c.time_schur = false;
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    check_mf_err(c);
     double sum = 0;
     int napp = 0;
     for (int k = 0; k < c.schur_ev_used; ++k) {
@@ -2857,6 +2979,7 @@ int dcp_nse_vmult(dcp_ctx* ctx, const double* src, double* dst) {
     require(ctx->nse_assembled, DCP_ERR_STATE, "nse_matrix not assembled");
     nse_vmult(*ctx, src, dst);
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    check_mf_err(*ctx);
     return DCP_OK;
   });
 }
@@ -2868,6 +2991,7 @@ int dcp_velocity_vmult(dcp_ctx* ctx, const double* src, double* dst) {
     require(!ctx->feec, DCP_ERR_UNSUPPORTED, "classic Q2/Q1 system only");
     velocity_vmult(*ctx, src, dst);
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    check_mf_err(*ctx);
     return DCP_OK;
   });
 }
@@ -2889,6 +3013,7 @@ int dcp_block_preconditioner_vmult(dcp_ctx* ctx, const double* src, double* dst,
     require(ctx->nse_assembled && ctx->precond_built, DCP_ERR_STATE, "operator not ready");
     const int rc = block_preconditioner_vmult(*ctx, src, dst, do_solve_A != 0, inner);
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    check_mf_err(*ctx);
     return rc;
   });
 }
@@ -3086,6 +3211,34 @@ int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]) {
     const int64_t v[8] = {m.built ? 1 : 0, m.n_ext, m.rows[1], m.rows[2], m.rows[3],
                           m.halo.nr, m.vals.nr, c.halo_p.nr};
     for (int i = 0; i < 8; ++i) info[i] = m.built || i == 7 ? v[i] : 0;
+    return DCP_OK;
+  });
+}
+
+int dcp_comm_info(dcp_ctx* ctx, int32_t info[4]) {
+  return guarded(ctx, [&] {
+    require(info != nullptr, DCP_ERR_INVALID, "NULL info");
+    int v[4] = {0, 1, 0, -1};
+    if (ctx->comm) {
+      ctx->comm->describe(v);
+    } else {
+      (void)hipGetDevice(&v[3]);
+    }
+    for (int i = 0; i < 4; ++i) info[i] = v[i];
+    return DCP_OK;
+  });
+}
+
+int dcp_local_sizes(dcp_ctx* ctx, int64_t out[8]) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(out != nullptr, DCP_ERR_INVALID, "NULL out");
+    const Ctx& c = *ctx;
+    const bool part = c.comm != nullptr;
+    const int64_t v[8] = {c.n_cells, part ? c.n_owned_cells : c.n_cells, c.n_u, c.n_p, c.n_T,
+                          part ? int64_t(c.vdim) * c.nvo : c.n_u, part ? c.npo : c.n_p,
+                          part ? c.nTo : c.n_T};
+    for (int i = 0; i < 8; ++i) out[i] = v[i];
     return DCP_OK;
   });
 }
@@ -3415,7 +3568,9 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     c.posT.upload(posT);
     c.T_inv.alloc(nT);
     c.fe_cellw.alloc(nc);
-    feec_cell_weights(c.fcd(), nc, c.fe_cellw.p, c.stream);
+    feec_cell_weights(c.fcd(), nc, c.fe_cellw.p, c.stream, 1);
+    c.fe_cellw2.alloc(nc);
+    feec_cell_weights(c.fcd(), nc, c.fe_cellw2.p, c.stream, 2);
     c.fe_dinv.alloc(nw + nu);
     for (auto* b : {&c.fe_t1, &c.fe_t2, &c.fe_t3, &c.fe_t4}) b->alloc(n);
     c.nse_sol.alloc(n);
@@ -3428,12 +3583,15 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     free_workspaces(c);
     {
       // sum of the mean-value weights over the owned cells (all ranks)
-      std::vector<double> w(nc);
+      std::vector<double> w(nc), w2(nc);
       DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
       DCP_HIP_CHECK(hipMemcpy(w.data(), c.fe_cellw.p, nc * sizeof(double), hipMemcpyDeviceToHost));
-      double ws = 0;
+      DCP_HIP_CHECK(hipMemcpy(w2.data(), c.fe_cellw2.p, nc * sizeof(double), hipMemcpyDeviceToHost));
+      double ws = 0, ws2 = 0;
       for (int k = 0; k < c.fe_npo; ++k) ws += w[k];
+      for (int k = 0; k < c.fe_npo; ++k) ws2 += w2[k];
       c.fe_wsum = ws;
+      c.fe_wsum2 = ws2;
     }
     if (dist) {
       auto one = [&](Ctx::Halo& h, std::initializer_list<std::pair<const HaloPlan*, int>> parts) {
@@ -3453,11 +3611,15 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
       DCP_HIP_CHECK(hipMemcpyAsync(d, mx, sizeof(mx), hipMemcpyHostToDevice, c.stream));
       c.comm->allreduce(d, 5, true, c.stream);
       DCP_HIP_CHECK(hipMemcpyAsync(mx, d, sizeof(mx), hipMemcpyDeviceToHost, c.stream));
-      DCP_HIP_CHECK(hipMemcpyAsync(d, &c.fe_wsum, sizeof(double), hipMemcpyHostToDevice, c.stream));
-      c.comm->allreduce(d, 1, false, c.stream);
-      DCP_HIP_CHECK(hipMemcpyAsync(&c.fe_wsum, d, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+      const double wsums[2] = {c.fe_wsum, c.fe_wsum2};
+      DCP_HIP_CHECK(hipMemcpyAsync(d, wsums, sizeof(wsums), hipMemcpyHostToDevice, c.stream));
+      c.comm->allreduce(d, 2, false, c.stream);
+      double wsum_all[2];
+      DCP_HIP_CHECK(hipMemcpyAsync(wsum_all, d, sizeof(wsum_all), hipMemcpyDeviceToHost, c.stream));
       DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
       for (int k = 0; k < 5; ++k) c.max_owned[3 + k] = int(mx[k]);
+      c.fe_wsum = wsum_all[0];
+      c.fe_wsum2 = wsum_all[1];
     }
     c.have_mesh = true;
     c.fe_assembled = c.fe_precond = c.T_matrix_ok = c.T_rhs_ok = false;

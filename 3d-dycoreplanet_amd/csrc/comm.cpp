@@ -38,10 +38,28 @@ struct RcclComm : Comm {
     nccl_check(ncclAllReduce(buf, buf, n, ncclDouble, max ? ncclMax : ncclSum, comm, s),
                "ncclAllReduce");
   }
+  void describe(int out[4]) const override {
+    int count = -1, user = -1, dev = -1;
+    nccl_check(ncclCommCount(comm, &count), "ncclCommCount");
+    nccl_check(ncclCommUserRank(comm, &user), "ncclCommUserRank");
+    nccl_check(ncclCommCuDevice(comm, &dev), "ncclCommCuDevice");
+    out[0] = 1;
+    out[1] = count;
+    out[2] = user;
+    out[3] = dev;
+  }
 };
 
 struct LocalComm : Comm {
   LocalGroup* g;
+  void describe(int out[4]) const override {
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    out[0] = 2;
+    out[1] = g->size;
+    out[2] = rank;
+    out[3] = dev;
+  }
   void exchange(int npeers, const int* peers, double* const* sbuf, const size_t* sn,
                 double* const* rbuf, const size_t* rn, hipStream_t s) override {
     LocalGroup::Post& me = g->post[rank];

@@ -34,6 +34,10 @@ struct Comm {
   // In-place element-wise sum (or max) over all ranks; identical result on
   // every rank. Collective over all ranks.
   virtual void allreduce(double* buf, size_t n, bool max, hipStream_t s) = 0;
+  // What the transport itself reports: kind (1 RCCL, 2 in-process group), its
+  // rank count, this rank, and the device it drives (RCCL: ncclCommCount /
+  // ncclCommUserRank / ncclCommCuDevice).
+  virtual void describe(int out[4]) const = 0;
 };
 
 // ncclUniqueId (128 bytes) from rank 0, passed in dcp_config.nccl_id.

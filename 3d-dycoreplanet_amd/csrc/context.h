@@ -304,6 +304,17 @@ struct Ctx {
   DBuf<int32_t> mf_col, mf_layer;
   DBuf<double> mf_colgeo, mf_laygeo, mf_colphi, mf_layR, mf_colphin, mf_layRs;
   bool mf_separable = false;
+  // the fused one-launch apply (k_mf_fused, DCP_MF_FUSED): schedule, gather
+  // window dependencies, per-batch done flags, the apply counter (flag tags)
+  DBuf<int32_t> mf_sched, mf_dep_ptr, mf_dep;
+  DBuf<uint32_t> mf_done;
+  int mf_ntasks = 0, mf_nvwin = 0;
+  unsigned mf_seq = 0;
+  bool mf_fused = false;
+  MfFused mff(double* err) const {
+    return MfFused{mf_sched.p, mf_dep_ptr.p, mf_dep.p, const_cast<uint32_t*>(mf_done.p), err,
+                   mf_nvwin, 1L << 22};
+  }
   MfCells mfc() const {
     return MfCells{n_cells,    n_u,         cell_q2.p,  cell_p.p,
                    mf_geo_tree.p, vcon.p,   mf_cmask.p, mf_vslot.p, mf_vnext.p,
@@ -412,10 +423,13 @@ struct Ctx {
   DBuf<int32_t> fe_dofs;
   DBuf<int8_t> fe_sign;
   DBuf<double> fe_X, fe_cellw;
+  DBuf<double> fe_cellw2;  // QGauss(2) cell volumes (PreconditionerBlockIdentity's mean)
   DBuf<uint8_t> fe_fixed;
   DBuf<int32_t> fe_ptr, fe_col, fe_pos, fp_ptr, fp_col, fp_pos;
   DBuf<double> fe_val, fp_val, fe_dinv;   // system, preconditioner, Jacobi of the w/u diagonal blocks
   double fe_wsum = 0;                      // sum of the mean-value weights
+  double fe_wsum2 = 0;
+  bool feec_block_prec = true;  // use_block_preconditioner_feec
   bool fe_assembled = false, fe_precond = false;
   std::vector<double*> fe_v, fe_s, fe_n;  // Krylov bases: outer, shifted Schur, nested Schur
   DBuf<double> fe_t1, fe_t2, fe_t3, fe_t4;
@@ -523,6 +537,11 @@ int solve_nse(Ctx& c, int* outer, int* inner);
 int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves);
 int solve_temperature(Ctx& c, int* iters, double* T_range);
 void nse_vmult(Ctx& c, const double* src, double* dst);
+// hmapped slot of the fused matrix-free apply's poll-timeout flag
+constexpr int kMfErrSlot = 8001;
+// a fused matrix-free apply whose gather poll timed out (k_mf_fused): throws
+// and switches the context to the two-launch apply
+void check_mf_err(Ctx& c);
 void velocity_vmult(Ctx& c, const double* src, double* dst);
 void schur_vmult(Ctx& c, const double* src_p, double* dst_p);
 int block_preconditioner_vmult(Ctx& c, const double* src, double* dst, bool do_solve_A,

@@ -233,7 +233,30 @@ struct MfGather {
 constexpr int kMfGroupCells = 7 * DCP_MF_WAVES;
 // cells [c0, c1) / gather positions [v0, v1) and [p0, p1)
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
-              double* buf, hipStream_t s);
+              double* buf, double* dst, hipStream_t s);
+// The fused apply's schedule (k_mf_fused, built at upload): per workgroup a
+// task (kind << 30 | index; kind 0 pencil batch, 1 velocity window, 2
+// pressure window, 3 padding); per gather window (velocity windows first) the
+// pencil batches whose records it reads (dep_ptr / dep); done[batch] = the
+// apply's seq once the batch's records are stored; err (host-mapped) set
+// when a poll exceeded spin_limit.
+struct MfFused {
+  const int32_t* sched;
+  const int32_t* dep_ptr;
+  const int32_t* dep;
+  unsigned* done;
+  double* err;
+  int n_vwin;
+  long spin_limit;
+};
+void mf_fused(const MfCells& mc, const MfGather& mg, const MfFused& f, int n_tasks, double nu,
+              bool stokes, const double* src, double* buf, double* dst, unsigned seq,
+              hipStream_t s);
+// the NSE rhs (mf_rhs_cells + the velocity gather with condensation only, mg.cdiag
+// null) in the same one-launch form
+void mf_rhs_fused(const MfCells& mc, const MfGather& mg, const MfFused& f, int n_tasks,
+                  const double* u_old, const double* T_old, const PhysicsDev& ph, double* buf,
+                  double* rhs, unsigned seq, hipStream_t s);
 void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, const double* buf,
                const double* src, double* dst, hipStream_t s);
 // The velocity rhs of local_assemble_nse_system (boussinesq_model.tpp:655-669)
@@ -242,7 +265,7 @@ void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, 
 // [c0, c1), one chunk of the cell-order layout), then mf_gather of the
 // velocity positions with mg.cdiag = null (condensation only) into rhs[0, n_u)
 void mf_rhs_cells(const MfCells& mc, int c0, int c1, const double* u_old, const double* T_old,
-                  const PhysicsDev& ph, double* buf, hipStream_t s);
+                  const PhysicsDev& ph, double* buf, double* rhs, hipStream_t s);
 // one colour class = positions [base, base + n): dst (+)= C^T K C src
 void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
                      const double* src, double* dst, hipStream_t s);
@@ -515,6 +538,8 @@ struct SStepArgs {
   double theta[kSStep];
   double sigma;
 };
+// co-resident workgroups of the one-launch s-step block (resident.h)
+int sstep_block_capacity();
 void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st, double* gran,
                  int nb, unsigned long long seq, double* err, hipStream_t s);
 // Several GPUs / large meshes: the same block as five launches (dots, column

@@ -54,14 +54,21 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
   if (rp->use_direct_solver)  // the reference throws at its first step (:1886-1893)
     return unsupported("Solver not implemented: MUMPS does not work on "
                        "TrilinosWrappers::MPI::BlockSparseMatrix classes.");
+  int rc0 = DCP_OK;
   if (feec) {
     if (rp->nse_velocity_degree != 1)
       return unsupported("FEEC: only nse velocity degree = 1 (Nedelec(0) / RT(0) / DGQ(0))");
     if (rp->physics.cuboid)
       return unsupported("FEEC on the periodic cuboid is not supported");
-    if (!schur && !rp->use_block_preconditioner_feec)
-      return unsupported("FEEC: use block preconditioner feec = false (identity-preconditioned "
-                         "GMRES, FEEC.tpp:1420-1431) is not implemented");
+    // use block preconditioner feec = false: the identity-preconditioned
+    // GMRES(100) branch (FEEC.tpp:1420-1431)
+    if ((rc0 = dcp_set_option(ctx, DCP_OPT_FEEC_BLOCK_PRECONDITIONER,
+                              rp->use_block_preconditioner_feec ? 1 : 0)) < 0)
+      return rc0;
+    // correct pressure to zero mean (both preconditioners' mean corrections)
+    if ((rc0 = dcp_set_option(ctx, DCP_OPT_FEEC_ZERO_MEAN,
+                              rp->correct_pressure_to_zero_mean ? 1 : 0)) < 0)
+      return rc0;
   } else if (rp->nse_velocity_degree != 2) {
     return unsupported("classic model: only nse velocity degree = 2 (Q2/Q1)");
   }

@@ -37,7 +37,8 @@ void launch_feec_T_rhs(const FeecCellData& cd, const int32_t* cells, int n, cons
                        const double* T_bc, double* rhs, hipStream_t s);
 void feec_velocity_stats(const FeecCellData& cd, int n_cells, const double* nse, double* out2,
                          hipStream_t s);
-void feec_cell_weights(const FeecCellData& cd, int n_cells, double* w, hipStream_t s);
+// npt = 1: QGauss(1) JxW (det J at the centre); 2: QGauss(2) JxW sum (the cell volume)
+void feec_cell_weights(const FeecCellData& cd, int n_cells, double* w, hipStream_t s, int npt);
 void feec_positions(const FeecCellData& cd, int n_cells, const int32_t* ptr, const int32_t* col,
                     int32_t* pos, hipStream_t s);
 

@@ -2066,6 +2066,12 @@ __device__ inline void bt_entry(const double* __restrict__ P, const double* __re
 // other (the next header / record prefetched) measured 10 / 17 % slower for 2
 // / 4 (profiles/r04l_bt_tpw_variants.json); loading the row constraints in
 // phase 1 into LDS with a packed destination scan, 20 % slower (r04m).
+// DCP_BT_PROBE (timing probes only, wrong B^T): 1 no entry stores, 2 the
+// column / layer tables replaced by register values, 3 no row-constraint
+// loads, 4 = 2 + 3
+#ifndef DCP_BT_PROBE
+#define DCP_BT_PROBE 0
+#endif
 template <int SL, int EL>
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
@@ -2105,11 +2111,17 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
           (unsigned long long)(unsigned)r[i].z | ((unsigned long long)(unsigned)r[i].w << 32);
       vof[wave][sl][int((dm >> (FB * v)) & (NE - 1))] = uint8_t(v);
       double ev[3];
-      bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 255, v, ev);
+      if (DCP_BT_PROBE == 2 || DCP_BT_PROBE == 4) {
+        ev[0] = 1e-3 * r[i].x;
+        ev[1] = 1e-3 * (r[i].y >> 16);
+        ev[2] = 1e-3 * v;
+      } else {
+        bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 31, v, ev);
+      }
       vals[wave][3 * e] = ev[0];
       vals[wave][3 * e + 1] = ev[1];
       vals[wave][3 * e + 2] = ev[2];
-      if (v == 0) rowl[wave][sl] = r[i].y & 255;
+      if (v == 0) rowl[wave][sl] = r[i].y & 0x80ff;  // row in task | constrained flag
     }
   }
   wsync();
@@ -2132,9 +2144,17 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
       }
     }
     double Ca[3][3];
-    condensation(cd.vcon[h.y + rl], Ca);
+    // unconstrained rows: identity (the same products as condensation() forms)
+    const NodeConstraint nc = ((rl & 0x8000) && DCP_BT_PROBE != 3 && DCP_BT_PROBE != 4)
+                                  ? cd.vcon[h.y + (rl & 255)]
+                                  : NodeConstraint{{0.0, 0.0, 0.0}, 0, 0};
+    condensation(nc, Ca);
 #if DCP_BT_STORE == 3
     double* dst = Bt + 3 * size_t(h.x + j);
+    if (DCP_BT_PROBE == 1) {
+      if (acc[0] == 12345.0) dst[0] = Ca[0][0];  // keeps the work alive
+      continue;
+    }
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj)
       __builtin_nontemporal_store(Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2],

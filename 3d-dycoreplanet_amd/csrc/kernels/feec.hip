@@ -388,13 +388,27 @@ __global__ __launch_bounds__(256) void k_feec_vel_stats(FeecCellData cd, int n_c
 }
 
 // per-cell weight of compute_mean_value(QGauss(1)) on MappingQ1: det J at the centre
-__global__ void k_feec_cell_weights(FeecCellData cd, int n_cells, double* w) {
+// per cell the JxW sum of compute_mean_value's quadrature on the MappingQ1
+// cell: QGauss(1) (npt = 1: det J at the centre, the nested Schur correction) or
+// QGauss(2) (npt = 2: the exact volume, PreconditionerBlockIdentity)
+__global__ void k_feec_cell_weights(FeecCellData cd, int n_cells, double* w, int npt) {
   const long cell = long(blockIdx.x) * 256 + threadIdx.x;
   if (cell >= n_cells) return;
-  const double xi[3] = {0.5, 0.5, 0.5};
   double x[3], J[3][3], Ji[3][3], det;
-  q1_map(cd.X + 24 * size_t(cell), xi, x, J, Ji, det);
-  w[cell] = det;
+  if (npt == 1) {
+    const double xi[3] = {0.5, 0.5, 0.5};
+    q1_map(cd.X + 24 * size_t(cell), xi, x, J, Ji, det);
+    w[cell] = det;
+    return;
+  }
+  const double g[2] = {0.5 - 0.5 / sqrt(3.0), 0.5 + 0.5 / sqrt(3.0)};
+  double s = 0.0;
+  for (int q = 0; q < 8; ++q) {
+    const double xi[3] = {g[q & 1], g[(q >> 1) & 1], g[q >> 2]};
+    q1_map(cd.X + 24 * size_t(cell), xi, x, J, Ji, det);
+    s += det * 0.125;
+  }
+  w[cell] = s;
 }
 
 // scatter positions of the 19x19 local entries into a sorted CSR (-1: absent)
@@ -458,10 +472,10 @@ void feec_velocity_stats(const FeecCellData& cd, int n_cells, const double* nse,
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void feec_cell_weights(const FeecCellData& cd, int n_cells, double* w, hipStream_t s) {
+void feec_cell_weights(const FeecCellData& cd, int n_cells, double* w, hipStream_t s, int npt) {
   if (n_cells <= 0) return;
   hipLaunchKernelGGL(k_feec_cell_weights, dim3((n_cells + 255) / 256), dim3(256), 0, s, cd, n_cells,
-                     w);
+                     w, npt);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

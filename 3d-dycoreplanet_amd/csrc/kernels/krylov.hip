@@ -38,6 +38,7 @@
 #include "../comm.h"
 #include "../device.h"
 #include "granule.h"
+#include "resident.h"
 
 namespace dcp {
 namespace {
@@ -546,9 +547,33 @@ void set_handoff_spin_limit(long spins) {
   DCP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &v, sizeof(v)));
 }
 
+namespace {
+// co-resident workgroups of every instance of a one-launch kernel family
+// (resident.h; the smallest over the instances the launchers may pick)
+template <class F, size_t N>
+int family_capacity(const F (&fs)[N]) {
+  int cap = 1 << 30;
+  for (const F f : fs) cap = std::min(cap, resident_capacity(reinterpret_cast<const void*>(f), kChainThreads));
+  return cap;
+}
+int cgs2_capacity() {
+  static const int cap = [] {
+    decltype(&k_cgs2_chain<4, true>) fs[] = {
+        k_cgs2_chain<4, true>, k_cgs2_chain<8, true>, k_cgs2_chain<12, true>,
+        k_cgs2_chain<16, true>, k_cgs2_chain<20, true>, k_cgs2_chain<24, true>,
+        k_cgs2_chain<28, true>, k_cgs2_chain<32, true>, k_cgs2_chain<4, false>,
+        k_cgs2_chain<8, false>, k_cgs2_chain<12, false>, k_cgs2_chain<16, false>,
+        k_cgs2_chain<20, false>, k_cgs2_chain<24, false>, k_cgs2_chain<28, false>,
+        k_cgs2_chain<32, false>};
+    return family_capacity(fs);
+  }();
+  return cap;
+}
+}  // namespace
+
 bool cgs2_chain_fits(long n, int nb, int n_cus) {
   return nb >= kGmMaxDim && nb <= n_cus && nb <= 256 &&
-         n <= long(nb) * kChainThreads * kChainEntries;
+         n <= long(nb) * kChainThreads * kChainEntries && nb <= cgs2_capacity();
 }
 
 void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, double* gran,
@@ -557,17 +582,15 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
   for (int j = d; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
   bool wide = g.n1 == g.n && g.n % 2 == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
   for (int j = 0; j < d; ++j) wide = wide && (reinterpret_cast<uintptr_t>(V.v[j]) & 15) == 0;
-  const dim3 grid(nb), block(kChainThreads);
   // KL > d: the chain's second reduction keeps its |w|^2 entry at K - 1 >= d
 #define DCP_CGS_CASE(KL)                                                                       \
   if (d < KL) {                                                                                \
     if (wide)                                                                                  \
-      hipLaunchKernelGGL((k_cgs2_chain<KL, true>), grid, block, 0, s, g, w, Vp, d, st, d - 1,  \
-                         gran, seq, err);                                                      \
+      launch_resident(k_cgs2_chain<KL, true>, nb, kChainThreads, s, g, w, Vp, d, st, d - 1,    \
+                      gran, seq, err);                                                         \
     else                                                                                       \
-      hipLaunchKernelGGL((k_cgs2_chain<KL, false>), grid, block, 0, s, g, w, Vp, d, st, d - 1, \
-                         gran, seq, err);                                                      \
-    DCP_HIP_CHECK(hipGetLastError());                                                          \
+      launch_resident(k_cgs2_chain<KL, false>, nb, kChainThreads, s, g, w, Vp, d, st, d - 1,   \
+                      gran, seq, err);                                                         \
     return;                                                                                    \
   }
   DCP_CGS_CASE(4) DCP_CGS_CASE(8) DCP_CGS_CASE(12) DCP_CGS_CASE(16) DCP_CGS_CASE(20)
@@ -1040,15 +1063,23 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
 
 }  // namespace
 
+int sstep_block_capacity() {
+  static const int cap = [] {
+    decltype(&k_sstep_block<4>) fs[] = {k_sstep_block<4>,  k_sstep_block<8>,  k_sstep_block<12>,
+                                        k_sstep_block<16>, k_sstep_block<20>, k_sstep_block<24>,
+                                        k_sstep_block<28>};
+    return family_capacity(fs);
+  }();
+  return cap;
+}
+
 void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev* st, double* gran,
                  int nb, unsigned long long seq, double* err, hipStream_t s) {
   ChainVecs Vp = V;
   for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
-  const dim3 grid(nb), block(kChainThreads);
 #define DCP_SS_CASE(KL)                                                                        \
   if (k + 1 <= KL) {                                                                           \
-    hipLaunchKernelGGL((k_sstep_block<KL>), grid, block, 0, s, g, Vp, a, k, st, gran, seq, err); \
-    DCP_HIP_CHECK(hipGetLastError());                                                          \
+    launch_resident(k_sstep_block<KL>, nb, kChainThreads, s, g, Vp, a, k, st, gran, seq, err);  \
     return;                                                                                    \
   }
   DCP_SS_CASE(4) DCP_SS_CASE(8) DCP_SS_CASE(12) DCP_SS_CASE(16) DCP_SS_CASE(20) DCP_SS_CASE(24)
@@ -1521,7 +1552,24 @@ __global__ __launch_bounds__(kBlock) void k_dcgs_update(Seg g, const double* __r
   dcgs_bookkeeping<KP>(st, hs, k, tail, c);
 }
 
-bool dcgs2_fits(long n, int nb, int n_cus) { return cgs2_chain_fits(n, nb, n_cus); }
+namespace {
+int dcgs2_capacity() {
+  static const int cap = [] {
+    decltype(&k_dcgs2_step<4, true>) fs[] = {
+        k_dcgs2_step<4, true>,   k_dcgs2_step<8, true>,   k_dcgs2_step<12, true>,
+        k_dcgs2_step<16, true>,  k_dcgs2_step<20, true>,  k_dcgs2_step<24, true>,
+        k_dcgs2_step<28, true>,  k_dcgs2_step<4, false>,  k_dcgs2_step<8, false>,
+        k_dcgs2_step<12, false>, k_dcgs2_step<16, false>, k_dcgs2_step<20, false>,
+        k_dcgs2_step<24, false>, k_dcgs2_step<28, false>};
+    return family_capacity(fs);
+  }();
+  return cap;
+}
+}  // namespace
+
+bool dcgs2_fits(long n, int nb, int n_cus) {
+  return cgs2_chain_fits(n, nb, n_cus) && nb <= dcgs2_capacity();
+}
 
 #ifdef DCP_DCGS_TIMING
 extern "C" int dcp_probe_dcgs_timestamps(unsigned long long* out) {
@@ -1544,17 +1592,15 @@ void dcgs2_step(Seg g, const double* w, const ChainVecs& V, int k, double* tnext
     bool wide = g.n1 == g.n && g.n % 2 == 0 && (reinterpret_cast<uintptr_t>(tnext) & 15) == 0 &&
                 (reinterpret_cast<uintptr_t>(w) & 15) == 0;
     for (int j = 0; j <= k; ++j) wide = wide && (reinterpret_cast<uintptr_t>(V.v[j]) & 15) == 0;
-    const dim3 grid(nb), block(kChainThreads);
     ++seq;
 #define DCP_DCGS_CASE(KL)                                                                       \
     if (k <= KL) {                                                                              \
       if (wide)                                                                                 \
-        hipLaunchKernelGGL((k_dcgs2_step<KL, true>), grid, block, 0, s, g, w, Vp, k, tnext, st, \
-                           gran, seq, err);                                                     \
+        launch_resident(k_dcgs2_step<KL, true>, nb, kChainThreads, s, g, w, Vp, k, tnext, st,   \
+                        gran, seq, err);                                                        \
       else                                                                                      \
-        hipLaunchKernelGGL((k_dcgs2_step<KL, false>), grid, block, 0, s, g, w, Vp, k, tnext,    \
-                           st, gran, seq, err);                                                 \
-      DCP_HIP_CHECK(hipGetLastError());                                                         \
+        launch_resident(k_dcgs2_step<KL, false>, nb, kChainThreads, s, g, w, Vp, k, tnext, st,  \
+                        gran, seq, err);                                                        \
       return;                                                                                   \
     }
     DCP_DCGS_CASE(4) DCP_DCGS_CASE(8) DCP_DCGS_CASE(12) DCP_DCGS_CASE(16) DCP_DCGS_CASE(20)

@@ -17,6 +17,7 @@
 #include "../comm.h"
 #include "../device.h"
 #include "granule.h"
+#include "resident.h"
 
 namespace dcp {
 namespace {
@@ -837,16 +838,16 @@ void chain_add_and_dot_ex(Seg g, double* v, const double* prev, int nb_prev, dou
 
 bool mgs_chain_fits(long n, int nb, int d, int n_cus) {
   return d >= 1 && d < kMgsMaxVecs && nb >= 1 && nb <= n_cus && nb <= kBlock &&
-         n <= long(kMgsElems) * nb * kBlock;
+         n <= long(kMgsElems) * nb * kBlock &&
+         nb <= resident_capacity(reinterpret_cast<const void*>(&k_mgs_chain), kBlock);
 }
 
 void mgs_chain(Seg g, double* w, const ChainVecs& V, int d, const double* prev, int nb_prev,
                const double* prev2, double* store2, double* coef, double* partials,
                double* partials_host, int nb, double* gran, unsigned long long seq, double* err,
                hipStream_t s) {
-  hipLaunchKernelGGL(k_mgs_chain, dim3(nb), dim3(kBlock), 0, s, g, w, V, d, prev, nb_prev, prev2,
-                     store2, coef, partials, partials_host, gran, seq, err);
-  DCP_HIP_CHECK(hipGetLastError());
+  launch_resident(k_mgs_chain, nb, kBlock, s, g, w, V, d, prev, nb_prev, prev2, store2, coef,
+                  partials, partials_host, gran, seq, err);
 }
 
 int sell_fused_blocks(int rows) { return int((long(rows) + 63) / 64); }

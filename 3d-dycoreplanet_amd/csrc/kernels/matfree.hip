@@ -503,12 +503,44 @@ __device__ __forceinline__ void rhs_flux(const PhysicsDev& ph, const double u[3]
 // F = (u + dt rho g' - dt (u.grad) u - 2 dt Omega x u) JxW of
 // local_assemble_nse_system (boussinesq_model.tpp:655-669) against the test
 // function values only
-template <bool STOKES, bool SEP, bool RHS = false>
-__global__ __launch_bounds__(64 * kPenWaves, DCP_MF_WAVES_PER_EU)
-void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict__ src,
-                 double* __restrict__ buf, const double* __restrict__ T_old, PhysicsDev ph) {
+// record stores of the fused apply (k_mf_fused): agent-scope (sc1) stores, so a
+// gather task on any XCD reads them after the batch's done flag
+// timing switches: DCP_MF_FUSED_SC1=0 plain record stores / loads in the fused
+// kernel (wrong across XCDs: probes only); DCP_MF_REC_SC1=1 agent-coherent
+// record stores in the two-launch kernel too (the cost of write-through alone)
+#ifndef DCP_MF_FUSED_SC1
+#define DCP_MF_FUSED_SC1 1
+#endif
+#ifndef DCP_MF_REC_SC1
+#define DCP_MF_REC_SC1 0
+#endif
+__device__ __forceinline__ void rec_store(double* p, double v, bool fused) {
+  if ((fused && DCP_MF_FUSED_SC1) || DCP_MF_REC_SC1)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                       (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+__device__ __forceinline__ double rec_load(const double* p, bool fused) {
+  if (fused && DCP_MF_FUSED_SC1)
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return *p;
+}
+
+// The pencil kernel's work for cell batch `blk` (k_mf_pencil: the block's
+// XCD-contiguous batch; k_mf_fused: the batch of its schedule entry). FUSED:
+// records stored agent-coherent and, once they are complete, the batch's done
+// flag (done[blk] = seq) for the gather tasks waiting on it.
+template <bool STOKES, bool SEP, bool RHS, bool FUSED>
+__device__ __forceinline__ void pencil_body(const MfCells& mc, int blk, int c0, int c1, double nu,
+                                            const double* __restrict__ src,
+                                            double* __restrict__ buf, double* __restrict__ dst,
+                                            const double* __restrict__ T_old,
+                                            const PhysicsDev& ph, double (*lds)[kPenFields],
+                                            unsigned* done, unsigned seq) {
   static_assert(!(RHS && STOKES), "the rhs pass has no pressure");
-  __shared__ double lds[kPenWaves][kPenFields];
 #if !DCP_MF_LDS_ALIAS
   __shared__ double aux[kPenWaves][kPenSlots][kPenAux];
   __shared__ MfLink nxt_own[kPenWaves * kPenCells * 27];  // chain links of the group partial sums
@@ -525,10 +557,6 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   const int cs = DCP_MF_SHADOW && dummy ? kPenCells - 1 : lane / 9;
   const int p = DCP_MF_SHADOW && dummy ? (lane - 9 * (lane / 9)) % 9 : lane - 9 * cs;
   const int pa = p % 3, pb = p / 3;
-#ifndef DCP_MF_XCD
-#define DCP_MF_XCD 1
-#endif
-  const int blk = DCP_MF_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x);
   double* S = lds[wave] + (DCP_MF_FIELD_MAJOR ? 27 * cs : 243 * cs);
 #if DCP_MF_LDS_ALIAS
   // P (vertex values): field 8 of the slot, read before the forward y pass
@@ -948,7 +976,7 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   if (live && !DCP_MF_NOSTORE) {
 #pragma unroll
     for (int n = 0; n < 3; ++n) {
-      if (Ic.slot[n] < 0) continue;
+      if (Ic.slot[n] < 0) continue;  // not the node's first occurrence in the group
       double s0 = y[n][0], s1 = y[n][1], s2 = y[n][2];
       // links point forward inside the group (at most kMfGroupCells - 1 hops)
       int k = Ic.next[n];
@@ -964,11 +992,11 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
         s2 += Sw[2 * kFS + idx];
       }
       double* out = buf + Ic.slot[n];
-      out[0] = s0;
-      out[1] = s1;
-      out[2] = s2;
+      rec_store(out, s0, FUSED);
+      rec_store(out + 1, s1, FUSED);
+      rec_store(out + 2, s2, FUSED);
     }
-    if (STOKES && p < 8) buf[Ic.pslot] = yp;
+    if (STOKES && p < 8) rec_store(buf + Ic.pslot, yp, FUSED);
   }
   // the next batch overwrites the slabs this one just read
   if (kPenWaves > 1)
@@ -979,6 +1007,27 @@ void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict
   In = Inn;
   if (DCP_MF_PREFETCH_NODES) Nc = Nn;
   }
+  if (FUSED) {
+    // every record store of the batch acknowledged, then its flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kPenWaves > 1) __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(done + blk, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+#ifndef DCP_MF_XCD
+#define DCP_MF_XCD 1
+#endif
+template <bool STOKES, bool SEP, bool RHS = false>
+__global__ __launch_bounds__(64 * kPenWaves, DCP_MF_WAVES_PER_EU)
+void k_mf_pencil(MfCells mc, int c0, int c1, double nu, const double* __restrict__ src,
+                 double* __restrict__ buf, double* __restrict__ dst,
+                 const double* __restrict__ T_old, PhysicsDev ph) {
+  __shared__ double lds[kPenWaves][kPenFields];
+  const int blk = DCP_MF_XCD ? xcd_block(blockIdx.x, gridDim.x) : int(blockIdx.x);
+  pencil_body<STOKES, SEP, RHS, false>(mc, blk, c0, c1, nu, src, buf, dst, T_old, ph, lds, nullptr,
+                                       0);
 }
 
 // Every dof sums its contiguous run of slots in slot (= ascending cell) order,
@@ -993,17 +1042,15 @@ constexpr int kGatherWaves = DCP_MF_GWAVES;
 #define DCP_MF_GSPAN 512  // 64 nodes x ~2.1 wave partials x 3 (r=5: 768 -> 512, 34.8 -> 32.0 us)
 #endif
 constexpr int kGvSpan = DCP_MF_GSPAN;  // doubles per wave window (longer spans: direct reads)
-template <bool STOKES>
-__global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int v0, int v1,
-                                                                  int p0, int p1,
-                                                                  const double* __restrict__ buf,
-                                                                  const double* __restrict__ src,
-                                                                  double* __restrict__ dst) {
-  __shared__ double win[kGatherWaves][kGvSpan];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int w = blockIdx.x * kGatherWaves + wave;
+// Gather wave w (velocity windows first, then pressure windows); W: the
+// wave's LDS window (kGvSpan doubles). FUSED: records read agent-coherent.
+template <bool STOKES, bool FUSED>
+__device__ __forceinline__ void gather_body(const MfGather& g, int w, int v0, int v1, int p0,
+                                            int p1, const double* __restrict__ buf,
+                                            const double* __restrict__ src,
+                                            double* __restrict__ dst, double* W) {
+  const int lane = threadIdx.x & 63;
   const int nvw = (v1 - v0 + 63) >> 6;
-  double* W = win[wave];
   if (w < nvw) {
     const int n0 = v0 + 64 * w, n1 = min(n0 + 64, v1);  // gather positions
     const int s0 = g.vptr[n0];
@@ -1011,7 +1058,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     const double* b = buf + 3 * size_t(s0);
     const bool fits = len <= kGvSpan;
     if (fits)
-      for (int i = lane; i < len; i += 64) W[i] = b[i];
+      for (int i = lane; i < len; i += 64) W[i] = rec_load(b + i, FUSED);
     wsync();
     const int pos = n0 + lane;
     if (pos >= n1) return;
@@ -1026,9 +1073,9 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
       }
     } else {
       for (int k = k0; k < k1; ++k) {
-        s[0] += b[3 * k];
-        s[1] += b[3 * k + 1];
-        s[2] += b[3 * k + 2];
+        s[0] += rec_load(b + 3 * k, FUSED);
+        s[1] += rec_load(b + 3 * k + 1, FUSED);
+        s[2] += rec_load(b + 3 * k + 2, FUSED);
       }
     }
     // the cidx lookup only where the wave's positions hold a constrained node
@@ -1058,7 +1105,7 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     const double* b = buf + g.pbase + s0;
     const bool fits = len <= kGvSpan;
     if (fits)
-      for (int i = lane; i < len; i += 64) W[i] = b[i];
+      for (int i = lane; i < len; i += 64) W[i] = rec_load(b + i, FUSED);
     wsync();
     const int pos = j0 + lane;
     if (pos >= j1) return;
@@ -1068,10 +1115,69 @@ __global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int
     if (fits)
       for (int k = k0; k < k1; ++k) s += W[k];
     else
-      for (int k = k0; k < k1; ++k) s += b[k];
+      for (int k = k0; k < k1; ++k) s += rec_load(b + k, FUSED);
     if (g.pcidx && g.pcidx[j] >= 0) s = g.pcdiag[g.pcidx[j]] * src[g.n_u + j];  // periodic image
     dst[g.n_u + j] = s;
   }
+}
+
+template <bool STOKES>
+__global__ __launch_bounds__(64 * kGatherWaves) void k_mf_gather(MfGather g, int v0, int v1,
+                                                                  int p0, int p1,
+                                                                  const double* __restrict__ buf,
+                                                                  const double* __restrict__ src,
+                                                                  double* __restrict__ dst) {
+  __shared__ double win[kGatherWaves][kGvSpan];
+  const int wave = threadIdx.x >> 6;
+  gather_body<STOKES, false>(g, int(blockIdx.x) * kGatherWaves + wave, v0, v1, p0, p1, buf, src,
+                             dst, win[wave]);
+}
+
+// One launch for the whole apply (DCP_MF_FUSED): pencil batches and gather
+// windows in one grid, in the order of the schedule built at upload
+// (api.cpp): every gather window after all the batches that write its
+// records. A gather task polls those batches' done flags (agent-coherent,
+// tag = this apply's seq) before it reads. It waits only on tasks of lower
+// workgroup ids, and an XCD dispatches its workgroups in id order, so the
+// lowest unfinished task always has its inputs: no deadlock whatever the
+// residency. A poll that exceeds the spin bound raises f.err (host-mapped)
+// and reads anyway; the host then refuses the result. The same sums in the
+// same order as the two launches: bitwise their result.
+static_assert(kPenWaves == 1 && kMfBatches == 1, "k_mf_fused: one-wave pencil batches");
+static_assert(kGvSpan <= kPenFields, "the gather window aliases the pencil slab");
+template <bool STOKES, bool SEP, bool RHS>
+__global__ __launch_bounds__(64, DCP_MF_WAVES_PER_EU) void k_mf_fused(
+    MfCells mc, MfGather g, MfFused f, double nu, const double* __restrict__ src,
+    double* __restrict__ buf, double* __restrict__ dst, unsigned seq,
+    const double* __restrict__ T_old, PhysicsDev ph) {
+  __shared__ double lds[1][kPenFields];
+  const int task = f.sched[blockIdx.x];
+  const int kind = (task >> 30) & 3, idx = task & 0x3fffffff;
+  if (kind == 0) {
+    pencil_body<STOKES, SEP, RHS, true>(mc, idx, 0, mc.n_cells, nu, src, buf, dst, T_old, ph,
+                                        lds, f.done, seq);
+    return;
+  }
+  // padding; pressure windows of a velocity-only pass (A x, the rhs)
+  if (kind == 3 || (kind == 2 && !STOKES)) return;
+  const int lane = threadIdx.x & 63;
+  const int win = kind == 1 ? idx : f.n_vwin + idx;
+  const int d0 = f.dep_ptr[win], d1 = f.dep_ptr[win + 1];
+  bool late = false;
+  for (int i = d0 + lane; i < d1; i += 64) {
+    const unsigned* flag = f.done + f.dep[i];
+    long spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
+      if (++spins > f.spin_limit) {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  if (__any(late) && lane == 0) *f.err = 1.0;
+  gather_body<STOKES, true>(g, kind == 1 ? idx : ((g.n_vnodes + 63) >> 6) + idx, 0, g.n_vnodes, 0,
+                            g.n_p, buf, src, dst, lds[0]);
 }
 
 // constrained velocity dofs: dst = (assembled diagonal) * src
@@ -1106,7 +1212,7 @@ void mf_apply_colour(const MfData& md, int base, int n, double nu, bool stokes,
 }
 
 void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const double* src,
-              double* buf, hipStream_t s) {
+              double* buf, double* dst, hipStream_t s) {
   if (c1 <= c0) return;
   const dim3 grid((kMfBatchTotal(c1 - c0) + kMfBatches - 1) / kMfBatches);
 #ifndef DCP_MF_SEP
@@ -1115,18 +1221,19 @@ void mf_cells(const MfCells& mc, int c0, int c1, double nu, bool stokes, const d
   const bool sep = DCP_MF_SEP && mc.col != nullptr;
   auto k = stokes ? (sep ? k_mf_pencil<true, true> : k_mf_pencil<true, false>)
                   : (sep ? k_mf_pencil<false, true> : k_mf_pencil<false, false>);
-  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, nu, src, buf, nullptr,
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, nu, src, buf, dst, nullptr,
                      PhysicsDev{});
   DCP_HIP_CHECK(hipGetLastError());
 }
 
 void mf_rhs_cells(const MfCells& mc, int c0, int c1, const double* u_old, const double* T_old,
-                  const PhysicsDev& ph, double* buf, hipStream_t s) {
+                  const PhysicsDev& ph, double* buf, double* rhs, hipStream_t s) {
   if (c1 <= c0) return;
   const dim3 grid((kMfBatchTotal(c1 - c0) + kMfBatches - 1) / kMfBatches);
   const bool sep = DCP_MF_SEP && mc.col != nullptr;
   auto k = sep ? k_mf_pencil<false, true, true> : k_mf_pencil<false, false, true>;
-  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, 0.0, u_old, buf, T_old, ph);
+  hipLaunchKernelGGL(k, grid, dim3(64 * kPenWaves), 0, s, mc, c0, c1, 0.0, u_old, buf, rhs, T_old,
+                     ph);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
@@ -1139,6 +1246,29 @@ void mf_gather(const MfGather& mg, int v0, int v1, int p0, int p1, bool stokes, 
     hipLaunchKernelGGL(k_mf_gather<true>, grid, block, 0, s, mg, v0, v1, p0, p1, buf, src, dst);
   else
     hipLaunchKernelGGL(k_mf_gather<false>, grid, block, 0, s, mg, v0, v1, p0, p1, buf, src, dst);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_fused(const MfCells& mc, const MfGather& mg, const MfFused& f, int n_tasks, double nu,
+              bool stokes, const double* src, double* buf, double* dst, unsigned seq,
+              hipStream_t s) {
+  if (n_tasks <= 0) return;
+  const bool sep = DCP_MF_SEP && mc.col != nullptr;
+  auto k = stokes ? (sep ? k_mf_fused<true, true, false> : k_mf_fused<true, false, false>)
+                  : (sep ? k_mf_fused<false, true, false> : k_mf_fused<false, false, false>);
+  hipLaunchKernelGGL(k, dim3(n_tasks), dim3(64), 0, s, mc, mg, f, nu, src, buf, dst, seq, nullptr,
+                     PhysicsDev{});
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void mf_rhs_fused(const MfCells& mc, const MfGather& mg, const MfFused& f, int n_tasks,
+                  const double* u_old, const double* T_old, const PhysicsDev& ph, double* buf,
+                  double* rhs, unsigned seq, hipStream_t s) {
+  if (n_tasks <= 0) return;
+  const bool sep = DCP_MF_SEP && mc.col != nullptr;
+  auto k = sep ? k_mf_fused<false, true, true> : k_mf_fused<false, false, true>;
+  hipLaunchKernelGGL(k, dim3(n_tasks), dim3(64), 0, s, mc, mg, f, 0.0, u_old, buf, rhs, seq, T_old,
+                     ph);
   DCP_HIP_CHECK(hipGetLastError());
 }
 

@@ -172,6 +172,7 @@ double block_sum_host(const double* p, int nb) {
 // One-launch chains (k_mgs_chain): one GPU, every workgroup resident, w in
 // registers. The timeout flag lives in mapped host memory and is sticky.
 constexpr int kChainErr = 8000;
+constexpr int kMfErr = kMfErrSlot;  // k_mf_fused poll timeout flag (hmapped)
 static_assert(kStepBlock + kStepBlockLen <= kChainErr && kChainErr < kNumSlots, "slot layout");
 bool fused_chain_ok(const Ctx& c, Seg g, int nb, int dim) {
   return !c.comm && c.fused_chain && c.hmapped && mgs_chain_fits(g.n, nb, dim, c.n_cus);
@@ -772,7 +773,8 @@ State gmres_schur_cgs2(Ctx& c, double* x, const double* b, Control& ctl, std::ve
 bool sstep_fits(const Ctx& c, long n, int nb) {
   constexpr int nG = kSStep * (kSStep + 1) / 2;
   const int max_cols = kSStep * (kGmMaxDim - 1 - kSStep + 1) + nG;
-  return !c.comm && c.fused_chain && c.hmapped && nb >= max_cols && cgs2_chain_fits(n, nb, c.n_cus);
+  return !c.comm && c.fused_chain && c.hmapped && nb >= max_cols && cgs2_chain_fits(n, nb, c.n_cus) &&
+         nb <= sstep_block_capacity();
 }
 
 double schur_lambda(Ctx& c) {
@@ -966,7 +968,12 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
   if (c.time_schur && c.mf_ev_used[v] < Ctx::kMfEvents) e = &c.mf_ev[v][c.mf_ev_used[v]++];
   if (c.time_schur) c.mf_calls[v]++;
   if (e) DCP_HIP_CHECK(hipEventRecord(e->a, c.stream));
-  if (c.matrix_free == 1) {
+  if (c.matrix_free == 1 && c.mf_fused && c.hmapped) {
+    // one launch: pencil batches and gather windows in the upload's schedule
+    if (++c.mf_seq == 0) ++c.mf_seq;  // 0 is the flags' initial value
+    mf_fused(c.mfc(), c.mfg(), c.mff(c.hmapped + kMfErr), c.mf_ntasks, c.nse_ph.nu_sys, stokes,
+             src, c.mf_buf.p, dst, c.mf_seq, c.stream);
+  } else if (c.matrix_free == 1) {
     // chunk k's pencil launch, then (on mf_stream) the gather of the dofs whose
     // last cell is in chunk k, overlapping chunk k + 1's pencil launch
     const MfCells mc = c.mfc();
@@ -975,7 +982,7 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
     hipStream_t gs = one_stream ? c.stream : c.mf_stream;
     for (int k = 0; k < c.mf_chunks; ++k) {
       mf_cells(mc, c.mf_cell_cut[k], c.mf_cell_cut[k + 1], c.nse_ph.nu_sys, stokes, src, c.mf_buf.p,
-               c.stream);
+               dst, c.stream);
       if (!one_stream) {
         DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[k], c.stream));
         DCP_HIP_CHECK(hipStreamWaitEvent(gs, c.mf_chunk_ev[k], 0));
@@ -1693,7 +1700,8 @@ int feec_solve_nse(Ctx& c, int* iterations) {
   copy(n, c.nse_sol.p, x.p, c.stream);
   scale(np, DScal{nullptr, c.ph.dt}, x.p + o.op, c.stream);  // :1345 block(2) *= dt
   const double tol = 1e-8 * std::sqrt(dot_host(c, c.seg_fe(), c.nse_rhs.p, c.nse_rhs.p, kSlotA));
-  Control ctl{500, tol};
+  // n_max_iter: 500 with the block preconditioner, 15000 with the identity (:1386-1391)
+  Control ctl{c.feec_block_prec ? 500u : 15000u, tol};
   // SolverGMRES(AdditionalData(100)): fresh (zero) temporary vectors per solve;
   // the preconditioner's output vector is the initial guess of its inner solves
   ensure_pool(c.fe_v, 100, size_t(n));
@@ -1702,7 +1710,21 @@ int feec_solve_nse(Ctx& c, int* iterations) {
     halo_exchange(c, c.halo_nse, const_cast<double*>(xx));
     spmv_csr(n, c.fe_ptr.p, c.fe_col.p, c.fe_val.p, xx, y, false, c.stream);
   };
-  Op P = [&](const double* s, double* d) { feec_precondition(c, o, s, d); };
+  Op P = [&](const double* s, double* d) {
+    if (c.feec_block_prec) {
+      feec_precondition(c, o, s, d);
+      return;
+    }
+    // PreconditionerBlockIdentity::vmult (preconditioner_block_identity.hpp:31-53):
+    // dst = src, then the pressure block minus compute_mean_value(QGauss(2)) of it
+    copy(n, s, d, c.stream);
+    if (c.feec_zero_mean) {
+      gdot(c, c.seg_fp(), c.fe_cellw2.p, d + o.op, kSlotC);
+      fill(1, c.fe_wsum2, slot(c, kSlotD), c.stream);
+      scalar_div(slot(c, kSlotC), slot(c, kSlotD), slot(c, kSlotA), c.stream);
+      shift(np, DScal{slot(c, kSlotA), -1.0}, d + o.op, c.stream);
+    }
+  };
   const State st = gmres(c, n, c.seg_fe(), A, &P, x.p, c.nse_rhs.p, ctl, c.fe_v, 100);
   zero_fixed(n, c.fe_fixed.p, x.p, c.stream);                // constraints.distribute (:1440)
   scale(np, DScal{nullptr, 1.0 / c.ph.dt}, x.p + o.op, c.stream);  // :1446 block(2) /= dt
@@ -1778,6 +1800,16 @@ int solve_temperature(Ctx& c, int* iters, double* T_range) {
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
   if (iters) *iters = int(ctl.last_step);
   return conv == kSuccess ? DCP_OK : DCP_NOT_CONVERGED;
+}
+
+void check_mf_err(Ctx& c) {
+  if (c.hmapped && c.hmapped[kMfErr] != 0.0) {
+    c.hmapped[kMfErr] = 0.0;
+    c.mf_fused = false;
+    throw std::runtime_error(
+        "matrix-free fused apply: a gather window timed out waiting for its cell batches; "
+        "the context now uses the two-launch apply");
+  }
 }
 
 }  // namespace dcp

@@ -40,6 +40,7 @@ OPT_SCHUR_FIXED_INNER = 12
 OPT_HANDOFF_SPIN_LIMIT = 13
 OPT_BLOCK_FIXED_INNER = 14
 OPT_MATRIX_POWERS = 15
+OPT_FEEC_BLOCK_PRECONDITIONER = 16
 ABI_VERSION = 5            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
@@ -67,6 +68,7 @@ EXPORTED = [
     "dcp_mesh_upload_distributed", "dcp_dist_partition_info", "dcp_dist_partition_info_field",
     "dcp_partition_info_field", "dcp_state_set_owned",
     "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_device_memory",
+    "dcp_comm_info", "dcp_local_sizes",
     "dcp_nse_coupling_export",
     "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
@@ -258,6 +260,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_scatter_info.argtypes = [P, P, P, P]
     lib.dcp_matrix_powers_info.argtypes = [P, P]
     lib.dcp_device_memory.argtypes = [P, P]
+    lib.dcp_comm_info.argtypes = [P, P]
+    lib.dcp_local_sizes.argtypes = [P, P]
     lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
@@ -1105,6 +1109,11 @@ class Context:
     def set_feec_zero_mean(self, on: bool):
         self._check(lib().dcp_set_option(self._h, OPT_FEEC_ZERO_MEAN, int(bool(on))))
 
+    def set_feec_block_preconditioner(self, on: bool):
+        """DCP_OPT_FEEC_BLOCK_PRECONDITIONER (use_block_preconditioner_feec): off
+        runs the identity-preconditioned GMRES(100) branch (FEEC.tpp:1420-1431)."""
+        self._check(lib().dcp_set_option(self._h, OPT_FEEC_BLOCK_PRECONDITIONER, int(bool(on))))
+
     def set_feec_fixed_inner(self, k: int):
         """DCP_OPT_FEEC_FIXED_INNER (test hook): both inner GMRES of the FEEC
         preconditioner run exactly k steps (0 = the reference's rule)."""
@@ -1269,6 +1278,20 @@ class Context:
         self._check(lib().dcp_matrix_powers_info(self._h, _ptr(v)))
         return {"built": bool(v[0]), "n_ext": int(v[1]), "rows": [int(x) for x in v[2:5]],
                 "halo_recv": int(v[5]), "value_recv": int(v[6]), "spmv_halo_recv": int(v[7])}
+
+    def comm_info(self) -> dict:
+        """dcp_comm_info: the communicator as its transport reports it."""
+        v = np.zeros(4, np.int32)
+        self._check(lib().dcp_comm_info(self._h, _ptr(v)))
+        return {"transport": {0: "none", 1: "rccl", 2: "in-process"}[int(v[0])],
+                "ranks": int(v[1]), "rank": int(v[2]), "device": int(v[3])}
+
+    def local_sizes(self) -> dict:
+        """dcp_local_sizes: the rank's local / owned cells and dofs."""
+        v = np.zeros(8, np.int64)
+        self._check(lib().dcp_local_sizes(self._h, _ptr(v)))
+        keys = ("cells", "owned_cells", "n_u", "n_p", "n_T", "owned_u", "owned_p", "owned_T")
+        return {k: int(x) for k, x in zip(keys, v)}
 
     @staticmethod
     def device_memory() -> dict:

@@ -447,6 +447,17 @@ int dcp_scatter_info(dcp_ctx* ctx, int64_t* touched, int64_t* nnzb, int* first_t
  * receive count. Zeros on one GPU or before the first such solve. */
 int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]);
 
+/* The context's communicator as the transport reports it: info[0] = 0 (none,
+ * one GPU), 1 (RCCL: [1] ncclCommCount, [2] ncclCommUserRank, [3]
+ * ncclCommCuDevice) or 2 (in-process group: size, rank, current device). */
+int dcp_comm_info(dcp_ctx* ctx, int32_t info[4]);
+
+/* Local sizes of the context's mesh: [0] local cells (owned + ghost layers),
+ * [1] owned cells, [2] local velocity dofs, [3] local pressure dofs, [4] local
+ * temperature dofs, [5] owned velocity dofs, [6] owned pressure dofs, [7]
+ * owned temperature dofs (one GPU: local = owned = global). */
+int dcp_local_sizes(dcp_ctx* ctx, int64_t out[8]);
+
 /* Device bytes held by the buffers the CALLING host thread allocated through
  * the library (context state, operators, Krylov pools): live now and the peak.
  * One context per thread (one rank per process, or one rank per thread in an
@@ -517,7 +528,8 @@ int dcp_feec_assemble_nse_system(dcp_ctx* ctx);
 /* assemble_nse_preconditioner / build_nse_preconditioner (FEEC.tpp:509-660) */
 int dcp_feec_build_nse_preconditioner(dcp_ctx* ctx);
 /* solve_NSE_block_preconditioned (FEEC.tpp:1268-1477): GMRES(100) <= 500 with
- * BlockSchurPreconditionerFEEC; DCP_NOT_CONVERGED if it does not converge. */
+ * BlockSchurPreconditionerFEEC (or, DCP_OPT_FEEC_BLOCK_PRECONDITIONER = 0,
+ * <= 15000 with the block identity); DCP_NOT_CONVERGED if it does not converge. */
 int dcp_feec_solve_nse(dcp_ctx* ctx, int* iterations);
 /* DCP_OPT_FEEC_ZERO_MEAN (default 1): parameters.correct_pressure_to_zero_mean */
 enum { DCP_OPT_FEEC_ZERO_MEAN = 2 };
@@ -527,6 +539,13 @@ enum { DCP_OPT_FEEC_ZERO_MEAN = 2 };
  *   preconditioner is a smooth map of its input with no early-stop decisions
  *   for rounding to flip; the oracle has the same switch. */
 enum { DCP_OPT_FEEC_FIXED_INNER = 8 };
+/* DCP_OPT_FEEC_BLOCK_PRECONDITIONER (default 1): parameters.use_block_preconditioner_feec.
+ *   0: dcp_feec_solve_nse runs the reference's other branch
+ *   (boussineq_model_FEEC.tpp:1420-1431): SolverGMRES(100) <= 15000 iterations,
+ *   tol 1e-8 |rhs|, with PreconditionerBlockIdentity (dst = src, then the pressure
+ *   block minus its QGauss(2) mean value if correct_pressure_to_zero_mean,
+ *   preconditioner_block_identity.hpp:31-53); no preconditioner build needed. */
+enum { DCP_OPT_FEEC_BLOCK_PRECONDITIONER = 16 };
 /* element matrices / rhs of cells [first, first+n): K [n][19][19], f [n][19] */
 int dcp_feec_cell_system(dcp_ctx* ctx, int first, int n, double* K, double* f);
 /* which = 0: nse_matrix, 1: nse_preconditioner_matrix (CSR, n_w+n_u+n_p rows) */

@@ -2144,6 +2144,7 @@ struct orc_feec {
   std::vector<double> rhs, T_rhs, T_inv;
   bool zero_mean = true;
   int fixed_inner = 0;  // test hook: both inner GMRES run exactly this many steps
+  bool block_prec = true;  // parameters.use_block_preconditioner_feec
 };
 
 extern "C" orc_feec* orc_feec_create(const orc_physics* ph, int n_cells, const int* cell_dofs19,
@@ -2379,13 +2380,39 @@ extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
       for (int i = 0; i < np; ++i) dst[op + i] += -mean;
     }
   };
+  // PreconditionerBlockIdentity::vmult (preconditioner_block_identity.hpp:31-53):
+  // dst = src; with correct_pressure_mean_value the pressure block minus
+  // VectorTools::compute_mean_value(dof_handler, QGauss<3>(2), dst, 6): per
+  // cell, per point, mean += p_K JxW, area += JxW (the DGQ0 value is p_K)
+  auto identity_block = [&](const double* src, double* dst) {
+    std::copy(src, src + n, dst);
+    if (!m->zero_mean) return;
+    const double g[2] = {0.5 - 0.5 / std::sqrt(3.0), 0.5 + 0.5 / std::sqrt(3.0)};
+    double mean = 0, area = 0;
+    for (int c = 0; c < m->n_cells; ++c)
+      for (int q = 0; q < 8; ++q) {
+        const double xi[3] = {g[q & 1], g[(q >> 1) & 1], g[q >> 2]};
+        double J[3][3];
+        Vec3 xq;
+        map_q1(&m->X[24 * size_t(c)], xi, J, xq);
+        const double JxW = det3(J) * 0.125;
+        mean += dst[op + c] * JxW;
+        area += JxW;
+      }
+    mean /= area;
+    for (int i = 0; i < np; ++i) dst[op + i] += -mean;
+  };
   auto Aop = [&](const double* x, double* y) { csr_block(A, 0, n, 0, n, x, y, false); };
   std::vector<double> x(sol, sol + n);
   for (int i = op; i < n; ++i) x[i] *= dt;  // :1345
-  Control ctl{500, 1e-8 * norm2(m->rhs, 0, n)};
+  // n_max_iter 500 with the block preconditioner, 15000 without (:1386-1391)
+  Control ctl{m->block_prec ? 500u : 15000u, 1e-8 * norm2(m->rhs, 0, n)};
   int its = 0, rc = 0;
   try {
-    gmres(n, Aop, precondition, x.data(), m->rhs.data(), ctl, its, 100);
+    if (m->block_prec)
+      gmres(n, Aop, precondition, x.data(), m->rhs.data(), ctl, its, 100);
+    else
+      gmres(n, Aop, identity_block, x.data(), m->rhs.data(), ctl, its, 100);  // :1420-1431
   } catch (const NoConvergence&) {
     rc = 1;
   }
@@ -2395,6 +2422,8 @@ extern "C" int orc_feec_solve_nse(orc_feec* m, double* sol, int* iterations) {
   if (iterations) *iterations = int(ctl.last_step);
   return rc;
 }
+
+extern "C" void orc_feec_set_block_preconditioner(orc_feec* m, int on) { m->block_prec = on != 0; }
 
 extern "C" int orc_feec_solve_temperature(orc_feec* m, double* T, int* iterations) {
   // solve_temperature: same CG + Jacobi as the classic model (:1417-1476)

@@ -181,6 +181,8 @@ void orc_feec_destroy(orc_feec* m);
 void orc_feec_set_zero_mean(orc_feec* m, int on);
 /* test hook: both inner GMRES of the FEEC preconditioner run exactly k steps */
 void orc_feec_set_fixed_inner(orc_feec* m, int k);
+/* use_block_preconditioner_feec (default 1); 0: identity-preconditioned GMRES(100) */
+void orc_feec_set_block_preconditioner(orc_feec* m, int on);
 void orc_feec_assemble_nse_system(orc_feec* m, const double* old_nse, const double* old_T);
 void orc_feec_assemble_preconditioner(orc_feec* m);
 long orc_feec_matrix_nnz(const orc_feec* m, int which);

@@ -93,6 +93,7 @@ def lib():
         L.orc_feec_destroy.argtypes = [P]
         L.orc_feec_set_zero_mean.argtypes = [P, I]
         L.orc_feec_set_fixed_inner.argtypes = [P, I]
+        L.orc_feec_set_block_preconditioner.argtypes = [P, I]
         L.orc_feec_assemble_nse_system.argtypes = [P, P, P]
         L.orc_feec_assemble_preconditioner.argtypes = [P]
         L.orc_feec_matrix_nnz.argtypes = [P, I]
@@ -437,6 +438,10 @@ class FeecModel:
     def set_fixed_inner(self, k):
         """Test hook (DCP_OPT_FEEC_FIXED_INNER): both inner GMRES run exactly k steps."""
         lib().orc_feec_set_fixed_inner(self.h, int(k))
+
+    def set_block_preconditioner(self, on):
+        """use_block_preconditioner_feec; off: identity-preconditioned GMRES(100)."""
+        lib().orc_feec_set_block_preconditioner(self.h, int(bool(on)))
 
     def solve_nse(self, sol):
         x = np.array(sol, dtype=np.float64, copy=True)

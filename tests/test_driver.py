@@ -208,15 +208,42 @@ def test_run_feec_with_schur_complement_solver_is_the_reference_no_op():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["feec-degree-2", "classic-degree-1", "direct-solver",
-                                  "feec-identity-preconditioner"])
+def test_run_feec_without_block_preconditioner():
+    """use block preconditioner feec = false (FEEC.tpp:1420-1431): run() skips
+    build_nse_preconditioner (:2264-2276) and the solve is the identity-
+    preconditioned GMRES(100); one step against the step-by-step calls with the
+    option set directly (bitwise)."""
+    rp = dcp.load_prm(FEEC_PRM)
+    rp.initial_global_refinement = 1
+    rp.use_block_preconditioner_feec = 0
+    rp.use_schur_complement_solver = 0
+    m = dcp.HostMesh(refine=1, feec=True, R0=rp.R0, R1=rp.R1, length=rp.length)
+    ctx = fresh_feec(rp, m)
+    rc, rep, steps = ctx.run(rp, max_steps=1)
+    x_run = ctx.get_state(dcp.NSE_SOLUTION)
+    n_prec = _calls(ctx, "   Build NSE FEEC preconditioner")
+    ctx.close()
+    assert rc == dcp.DCP_OK and rep.fgmres_outer > 0 and n_prec == 0
+    ctx = fresh_feec(rp, m)
+    ctx.set_feec_block_preconditioner(False)
+    ctx.set_feec_zero_mean(bool(rp.correct_pressure_to_zero_mean))
+    ctx.set_time_step(rp.physics.time_step)
+    ctx.cfl_number()
+    ctx.feec_assemble_nse_system()
+    rc2, it = ctx.feec_solve_nse()
+    assert rc2 == dcp.DCP_OK and it == rep.fgmres_outer
+    assert np.array_equal(ctx.get_state(dcp.NSE_SOLUTION), x_run)
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["feec-degree-2", "classic-degree-1", "direct-solver"])
 def test_run_rejects_what_the_device_path_does_not_implement(case):
     """dcp_run refuses up front (DCP_ERR_UNSUPPORTED, nothing stepped) instead
     of silently running another discretisation: FEEC with nse velocity degree
     != 1 (FE_Nedelec/RT/DGQ(degree - 1), FEEC.tpp:21-30), the classic model
-    with degree != 2, the MUMPS branch the reference itself throws on
-    (:1886-1893), and FEEC without its block preconditioner (the identity-
-    preconditioned GMRES branch, FEEC.tpp:1420-1431)."""
+    with degree != 2, and the MUMPS branch the reference itself throws on
+    (:1886-1893)."""
     feec = case.startswith("feec")
     rp = dcp.load_prm(FEEC_PRM if feec else PRM)
     rp.initial_global_refinement = 1
@@ -224,11 +251,8 @@ def test_run_rejects_what_the_device_path_does_not_implement(case):
         rp.nse_velocity_degree = 2
     elif case == "classic-degree-1":
         rp.nse_velocity_degree = 1
-    elif case == "direct-solver":
-        rp.use_direct_solver = 1
     else:
-        rp.use_block_preconditioner_feec = 0
-        rp.use_schur_complement_solver = 0
+        rp.use_direct_solver = 1
     m = dcp.HostMesh(refine=1, feec=feec, R0=rp.R0, R1=rp.R1, length=rp.length)
     ctx = fresh_feec(rp, m) if feec else fresh(rp, m)
     with pytest.raises(dcp.DcpError) as e:

@@ -280,3 +280,40 @@ def test_feec_time_step_fixed_inner(feec_setup):
     assert it == ito
     xg = ctx.get_state(dcp.NSE_SOLUTION)
     assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("zero_mean", [True, False])
+def test_feec_identity_preconditioned_gmres(zero_mean):
+    """use_block_preconditioner_feec = false (boussineq_model_FEEC.tpp:1420-1431):
+    SolverGMRES(100) <= 15000 on nse_matrix with PreconditionerBlockIdentity
+    (dst = src, the pressure block minus its QGauss(2) mean value when
+    correct_pressure_to_zero_mean; preconditioner_block_identity.hpp:31-53),
+    config 4's physics at r = 2 (242 GMRES iterations in the oracle): equal
+    iteration count, iterate at 1e-10."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    rp = dcp.load_prm("configs/aqua_planet_shell_test_3d-feec.prm")
+    ph = dcp.physics_from_params(rp)
+    f = m.feec
+    rng = np.random.default_rng(SEED + 7)
+    x0 = np.zeros(f.n)
+    T0 = m.T0 + 0.05 * rng.uniform(-1, 1, m.n_T)
+    ctx = dcp.Context()
+    ctx.set_physics(ph)
+    ctx.upload_feec_mesh(m)
+    ctx.set_feec_zero_mean(zero_mean)
+    ctx.set_feec_block_preconditioner(False)
+    for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
+                   (dcp.T_SOLUTION, T0)):
+        ctx.set_state(fld, v)
+    ctx.feec_assemble_nse_system()
+    rc, it = ctx.feec_solve_nse()
+    xg = ctx.get_state(dcp.NSE_SOLUTION)
+    ctx.close()
+    orc = oracle_py.FeecModel(ph, m, zero_mean=zero_mean)
+    orc.set_block_preconditioner(False)
+    orc.assemble_nse_system(x0, T0)
+    rco, xo, ito = orc.solve_nse(x0)
+    print("identity-preconditioned GMRES(100):", it, ito)
+    assert rc == rco == 0 and it == ito and it > 30
+    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)

@@ -691,3 +691,43 @@ def test_assembly_timing_switches_keep_constrained_diagonals(switch):
                          env=env, capture_output=True, text=True, timeout=300)
     print(out.stdout, out.stderr[-2000:])
     assert out.returncode == 0
+
+
+@pytest.mark.parametrize("kind,lag", [("shell-r3", None), ("shell-r3", "0"), ("shell-r2", "1000000000"),
+                                      ("warped-r2", None)])
+def test_fused_matrix_free_apply_is_the_two_launch_apply(monkeypatch, kind, lag):
+    """DCP_MF_FUSED (default): the matrix-free apply as ONE launch (k_mf_fused:
+    pencil batches and gather windows in the upload's schedule, each window
+    polling the done flags of the batches it reads) against the two launches
+    (pencil kernel, then the gather kernel): the same sums in the same order,
+    so [A B^T; B 0] x and A x must be bitwise equal, repeatable, and within
+    1e-13 of the assembled operator. lag = 0 puts each window right after its
+    last batch (the polls wait), a huge lag puts every window after all the
+    batches (padding where an XCD runs out of batches); warped: the streamed
+    (non-separable) geometry."""
+    m = dcp.HostMesh(refine=int(kind[-1]))
+    if kind.startswith("warped"):
+        X = m.cell_geometry.reshape(-1, 3)
+        X += 0.02 * np.sin(3.0 * X[:, [1, 2, 0]]) * np.cos(2.0 * X[:, [2, 0, 1]])
+    if lag is not None:
+        monkeypatch.setenv("DCP_MF_FUSED_LAG", lag)
+    x = np.random.default_rng(SEED + 31).uniform(-1, 1, m.n_u + m.n_p)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DCP_MF_FUSED", fused)
+        ctx = dcp.Context()
+        ctx.set_physics(dcp.classic_physics())
+        ctx.upload_mesh(m)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, np.zeros(m.n_u + m.n_p))
+        ctx.set_state(dcp.OLD_T_SOLUTION, m.T0)
+        ctx.assemble_nse_system()
+        y = ctx.nse_vmult(x)
+        out[fused] = (y, ctx.nse_vmult(x), ctx.velocity_vmult(x[:m.n_u]))
+        if fused == "1":
+            ctx.set_matrix_free(False)
+            out["assembled"] = ctx.nse_vmult(x)
+        ctx.close()
+    (y1, y1b, v1), (y0, _, v0) = out["1"], out["0"]
+    assert np.array_equal(y1, y1b)
+    assert np.array_equal(y1, y0) and np.array_equal(v1, v0)
+    assert rel_max(y1, out["assembled"]) < 1e-13

@@ -13,7 +13,8 @@ import dcp  # noqa: E402
 R = int(os.environ.get("R", "5"))
 m = dcp.HostMesh(refine=R)
 ref = None
-for path in sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__), "build/var/libdcp_*.so"))):
+for path in sorted(glob.glob(os.path.join(os.path.dirname(dcp.__file__),
+                                         "build/var/libdcp_%s.so" % os.environ.get("VAR", "*")))):
     dcp._lib = dcp.load_library(path)
     ctx = dcp.Context(device=0)
     ctx.set_physics(dcp.classic_physics())
