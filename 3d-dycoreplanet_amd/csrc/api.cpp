@@ -3417,16 +3417,51 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     std::vector<uint8_t> fixed(n, 0);
     for (int e = 0; e < nw; ++e) fixed[e] = m->w_fixed[e] != 0;
     for (int u = 0; u < nu; ++u) fixed[nw + u] = m->u_fixed[u] != 0;
-    // temperature constraints: Dirichlet lines
+    // temperature constraints: Dirichlet lines and, on the cuboid, the
+    // periodic identities of make_periodicity_constraints (FEEC.tpp:435-455).
+    // An image is folded into its partner in the cell maps (the partner's row
+    // receives the image's cell contributions, as distribute_local_to_global
+    // does) and keeps a diagonal-only row, copied from the partner after the
+    // solve; the same treatment as the classic upload (prepare_host above).
     std::vector<uint8_t> Tfix(nT, 0);
     std::vector<double> Tbc(nT, 0.0);
+    std::vector<int32_t> tmaster(nT, -1);
+    int n_timg = 0;
     for (int l = 0; l < m->T.n_lines; ++l) {
       const int d = m->T.line_dof[l];
       require(d >= 0 && d < nT, DCP_ERR_INVALID, "temperature constraint out of range");
+      const int b = m->T.entry_ptr[l];
+      if (m->T.entry_ptr[l + 1] - b == 1 && m->T.entry_w[b] == 1.0 && m->T.inhomogeneity[l] == 0.0 &&
+          m->T.entry_dof[b] != d) {
+        require(m->T.entry_dof[b] >= 0 && m->T.entry_dof[b] < nT, DCP_ERR_INVALID,
+                "temperature constraint out of range");
+        tmaster[d] = m->T.entry_dof[b];
+        ++n_timg;
+        continue;
+      }
       require(m->T.entry_ptr[l] == m->T.entry_ptr[l + 1], DCP_ERR_UNSUPPORTED,
-              "temperature constraints must be Dirichlet lines");
+              "temperature constraints must be Dirichlet lines or periodic identities");
       Tfix[d] = 1;
       Tbc[d] = m->T.inhomogeneity[l];
+    }
+    for (int t = 0; t < nT; ++t)
+      require(tmaster[t] < 0 || (tmaster[tmaster[t]] < 0 && !Tfix[tmaster[t]]), DCP_ERR_UNSUPPORTED,
+              "periodic temperature chain not closed");
+    require(!dist || n_timg == 0, DCP_ERR_UNSUPPORTED,
+            "periodic FEEC temperature runs on one GPU (the cuboid is not partitioned)");
+    const std::vector<int32_t> tdo = td;
+    if (n_timg)
+      for (auto& t : td)
+        if (tmaster[t] >= 0) t = tmaster[t];
+    // one global dof per local dof of a cell: the scatter kernels add a
+    // cell's entries concurrently
+    for (int cell = 0; cell < nc; ++cell) {
+      const int32_t* d = &dofs[19 * size_t(cell)];
+      const int32_t* t = &td[8 * size_t(cell)];
+      for (int i = 0; i < 19; ++i)
+        for (int j = 0; j < i; ++j)
+          require(d[i] != d[j] && (i >= 8 || t[i] != t[j]), DCP_ERR_UNSUPPORTED,
+                  "a cell holds a global dof twice (periodic box with one cell across?)");
     }
     // patterns: system (w:{w,u}, u:{w,u,p}, p:{u}), preconditioner (w:{w,u}, u:{w,u}, p:{w,p})
     std::vector<int32_t> Sp, Sc, Pp, Pc;
@@ -3447,12 +3482,29 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     for (int cell = 0; cell < nc; ++cell)
       for (int i = 0; i < 8; ++i)
         for (int j = 0; j < 8; ++j) trows[td[8 * size_t(cell) + i]].push_back(td[8 * size_t(cell) + j]);
+    for (int t = 0; t < nT; ++t)
+      if (tmaster[t] >= 0) trows[t].push_back(t);  // an image: its diagonal only
     for (auto& r : trows) {
       std::sort(r.begin(), r.end());
       r.erase(std::unique(r.begin(), r.end()), r.end());
     }
     std::vector<int32_t> Tp, Tc;
     build_csr(trows, Tp, Tc);
+    // position of an image's diagonal per (cell, vertex), -1 if not an image
+    std::vector<int32_t> posTs(n_timg ? size_t(nc) * 8 : 0, -1);
+    std::vector<int32_t> iT, mT;
+    if (n_timg) {
+      for (size_t k = 0; k < posTs.size(); ++k)
+        if (tdo[k] != td[k]) {
+          const int o = tdo[k];
+          posTs[k] = int32_t(std::lower_bound(Tc.begin() + Tp[o], Tc.begin() + Tp[o + 1], o) - Tc.begin());
+        }
+      for (int t = 0; t < nT; ++t)
+        if (tmaster[t] >= 0) {
+          iT.push_back(t);
+          mT.push_back(tmaster[t]);
+        }
+    }
     std::vector<int32_t> posT(size_t(nc) * 64);
     for (int cell = 0; cell < nc; ++cell)
       for (int i = 0; i < 8; ++i)
@@ -3566,6 +3618,14 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     c.Tstiff.alloc(Tc.size());
     c.Tmat.alloc(Tc.size());
     c.posT.upload(posT);
+    c.periodic = n_timg > 0;
+    c.n_img_u = c.n_img_p = c.n_img_node = 0;
+    c.n_img_T = n_timg;
+    if (c.periodic) {
+      c.posTs.upload(posTs);
+      c.img_T.upload(iT);
+      c.mst_T.upload(mT);
+    }
     c.T_inv.alloc(nT);
     c.fe_cellw.alloc(nc);
     feec_cell_weights(c.fcd(), nc, c.fe_cellw.p, c.stream, 1);
@@ -3879,11 +3939,11 @@ int dcp_host_mesh_view_get(const dcp_host_mesh* h, dcp_host_mesh_view* out) {
 
 int dcp_host_feec_view_get(dcp_host_mesh* h, dcp_feec_mesh* out) {
   if (!h || !out) return DCP_ERR_INVALID;
-  if (h->mesh.cuboid) {
-    // the cuboid's x/y periodicity (planet_geometry.tpp:44-56) would need
-    // periodic identification of the Nedelec / RT / DGQ0 dofs, which
-    // feec_dofs does not do: periodic faces would silently become boundary faces
-    g_last_error = "FEEC on the periodic cuboid is not supported (no periodic FEEC dofs)";
+  // the cuboid's x/y periodicity is in the topology (feec_mesh.cpp) and in
+  // the temperature constraints' identity lines (folded at upload)
+  if (h->mesh.cuboid && h->mesh.N < 2) {
+    // one cell across: a cell would hold the same edge / face dof twice
+    g_last_error = "FEEC on the periodic cuboid needs refinement >= 1 (two cells per direction)";
     return DCP_ERR_UNSUPPORTED;
   }
   try {

@@ -58,8 +58,6 @@ extern "C" int dcp_run(dcp_ctx* ctx, const dcp_run_params* rp, int max_steps,
   if (feec) {
     if (rp->nse_velocity_degree != 1)
       return unsupported("FEEC: only nse velocity degree = 1 (Nedelec(0) / RT(0) / DGQ(0))");
-    if (rp->physics.cuboid)
-      return unsupported("FEEC on the periodic cuboid is not supported");
     // use block preconditioner feec = false: the identity-preconditioned
     // GMRES(100) branch (FEEC.tpp:1420-1431)
     if ((rc0 = dcp_set_option(ctx, DCP_OPT_FEEC_BLOCK_PRECONDITIONER,

@@ -819,6 +819,7 @@ def main():
         # what each rank's communicator reports, its sizes and bytes per apply
         # (the traffic of N > 1 lines is this per-rank byte model: no PMC there)
         mine = {"rank": rank, "comm": ctx.comm_info(), "sizes": ls,
+                "device_memory": ctx.device_memory(),
                 "schur_bytes": sbytes, "schur_apply_ms": schur_ms,
                 "assembly_bytes": asm_bytes, "assemble_ms": float(np.mean(
                     [r[4]["assemble_nse_ms"] for r in recs]))}

@@ -513,8 +513,15 @@ typedef struct {
   const int32_t* cell_T_dofs;     /* [n_cells][8] */
   const uint8_t* w_fixed;         /* [n_w] boundary edge: w = 0 (FEEC.tpp:311-350) */
   const uint8_t* u_fixed;         /* [n_u] boundary face: u.n = 0 */
-  dcp_constraints T;              /* temperature constraints */
+  dcp_constraints T;              /* temperature constraints: Dirichlet lines and
+                                   * periodic identities (one entry, weight 1, no
+                                   * inhomogeneity: the image is folded into its
+                                   * partner, one GPU) */
 } dcp_feec_mesh;
+/* On the periodic cuboid (FEEC.tpp:313-333) the x = 1 / y = 1 edges and faces
+ * ARE their x = 0 / y = 0 partners in cell_w / cell_u (make_periodicity_
+ * constraints with unit weights, condensed): no NSE constraint lines beyond
+ * the fixed flags of the z faces. A cell must not hold a dof twice. */
 int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* m);
 /* Host-only summary of rank's FEEC partition (no GPU): info[11] = {n_cells
  * local, n_owned_cells, nwo, nwg, nuo, nug, nTo, nTg, n_peers, n_send,

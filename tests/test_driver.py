@@ -260,3 +260,58 @@ def test_run_rejects_what_the_device_path_does_not_implement(case):
     assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
     assert _calls(ctx, "   Assemble NSE system") == 0
     ctx.close()
+
+
+CUBE_PRM = os.path.join(ROOT, "configs", "aqua_planet_cube_test_3d.prm")
+
+
+@pytest.mark.gpu
+def test_run_feec_cube_prm_against_the_oracle():
+    """data/aqua_planet_cube_test_3d.prm: FEEC on the periodic cuboid with the
+    Schur-complement switch, i.e. run() reassembles the NSE system every step
+    and leaves nse_solution as it is (FEEC.tpp:1480-1500), and the temperature
+    (periodic in x, y: identity lines folded at upload, FEEC.tpp:435-463)
+    diffuses and advects with the given RT velocity. Three dcp_run steps
+    against the oracle's assemble / CG step by step: equal CG counts,
+    temperature at 1e-10, periodic images equal to their partners."""
+    import oracle_py
+    rp = dcp.load_prm(CUBE_PRM)
+    rp.initial_global_refinement = 2
+    m = dcp.HostMesh(cuboid=True, refine=2, feec=True, length=rp.length)
+    f = m.feec
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(f.n)
+    x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
+    x0[f.fixed.astype(bool)] = 0
+    ctx = fresh_feec(rp, m)
+    ctx.set_state(dcp.NSE_SOLUTION, x0)
+    ctx.set_state(dcp.OLD_NSE_SOLUTION, x0)
+    nsteps = 3
+    rc, rep, steps = ctx.run(rp, max_steps=nsteps)
+    assert rc == dcp.DCP_OK and rep.steps == nsteps
+    T_run = ctx.get_state(dcp.T_SOLUTION)
+    assert np.array_equal(ctx.get_state(dcp.NSE_SOLUTION), x0)
+    assert _calls(ctx, "   Assemble NSE system") == nsteps
+    ctx.close()
+    orc = oracle_py.FeecModel(dcp.physics_from_params(rp), m)
+    T = m.T0.copy()
+    for n in range(nsteps):
+        orc.assemble_nse_system(x0, T)
+        orc.assemble_temperature(T, x0)
+        rcT, T, itT = orc.solve_temperature(T)
+        assert rcT == 0 and itT == steps[n].T_cg
+    assert np.linalg.norm(T_run - T) <= 1e-10 * np.linalg.norm(T)
+    cs = m.T_constraints
+    for l, d in enumerate(cs.line_dof):
+        b, e = cs.entry_ptr[l], cs.entry_ptr[l + 1]
+        if e - b == 1 and cs.entry_w[b] == 1.0:
+            assert T_run[d] == T_run[cs.entry_dof[b]]
+
+
+@pytest.mark.gpu
+def test_executable_runs_the_cube_prm():
+    exe = os.path.join(ROOT, "3d-dycoreplanet_amd", "dcp_aquaplanet")
+    out = subprocess.run([exe, "-p", CUBE_PRM, "--refine", "2", "--max-steps", "3"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.count("Time step ") == 3

@@ -9,6 +9,8 @@ theorem per cell; block identities of the assembled system).
 GPU: the HIP kernels and solver chain against the oracle through the C ABI
 (element matrices and assembled entries at 1e-12 of the largest entry,
 solver iterates at 1e-10, same iteration counts)."""
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -17,6 +19,7 @@ import dcp
 import oracle_py
 
 SEED = 20261015
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def cube_cell(shear=0.3):
@@ -61,6 +64,72 @@ def test_face_and_edge_signs_conform():
         v = m.cell_T_dofs[c]  # Q1 temperature dofs are the vertices
         for l, (a, b) in enumerate(LINE_VTX):
             assert f.sign_w[c, l] == (1 if v[a] < v[b] else -1)
+
+
+CUBE_PRM = os.path.join(ROOT, "configs", "aqua_planet_cube_test_3d.prm")
+FEEC_PRM = os.path.join(ROOT, "configs", "aqua_planet_shell_test_3d-feec.prm")
+
+
+def test_cuboid_topology_is_periodic():
+    """The cuboid (FEEC.tpp:313-333: periodic in x and y, boundary ids 4 / 5
+    at z = 0 / 1): edges and faces on x = 1 (y = 1) are their partners on
+    x = 0 (y = 0), so V - E + F - C = chi(T^2 x I) = 0, every side face has two
+    cells, only the z faces are fixed, and the edges all point along +axis."""
+    for r in (1, 2, 3):
+        m = dcp.HostMesh(cuboid=True, refine=r, feec=True)
+        f, N = m.feec, 2 ** r
+        assert (f.n_w, f.n_u, f.n_p) == (2 * N * N * (N + 1) + N ** 3, 2 * N ** 3 + N * N * (N + 1),
+                                         N ** 3)
+        V = N * N * (N + 1)  # periodic vertices
+        assert V - f.n_w + f.n_u - f.n_p == 0
+        assert f.u_fixed.sum() == 2 * N * N and f.w_fixed.sum() == 4 * N * N
+        assert np.all(f.sign_w == 1)
+        seen = np.zeros(f.n_u, int)
+        flux = {}
+        for c in range(f.n_cells):
+            for q in range(6):
+                g = f.cell_u[c, q]
+                seen[g] += 1
+                flux.setdefault(g, []).append(f.sign_u[c, q] * (1 if q % 2 else -1))
+        assert np.all((seen == 2) | f.u_fixed.astype(bool)) and seen.max() == 2
+        assert all(s[0] == -s[1] for s in flux.values() if len(s) == 2)
+        # a fixed face is a z face: its four vertices share z = 0 or z = 1
+        for c in range(f.n_cells):
+            for q in range(6):
+                if f.u_fixed[f.cell_u[c, q]]:
+                    z = f.cell_vertices[c][list(FACE_VTX[q]), 2]
+                    assert q >= 4 and np.ptp(z) == 0
+
+
+def test_cuboid_oracle_identities_and_solve():
+    """On the cuboid with its own physics (vertical gravity, Coriolis on z):
+    B = B^T, the dt/Re curl coupling identity, the temperature's periodic
+    identity lines resolve to their partners after the oracle's solve."""
+    rp = dcp.load_prm(CUBE_PRM)
+    ph = dcp.physics_from_params(rp)
+    m = dcp.HostMesh(cuboid=True, refine=1, feec=True, length=rp.length)
+    f = m.feec
+    M = oracle_py.FeecModel(ph, m)
+    M.assemble_nse_system(np.zeros(f.n), m.T0)
+    rp_, cols, vals = M.matrix_csr(0)
+    A = sp.csr_matrix((vals, cols, rp_), shape=(f.n, f.n))
+    nw, nu = f.n_w, f.n_u
+    Bt = A[nw:nw + nu, nw + nu:].toarray()
+    B = A[nw + nu:, nw:nw + nu].toarray()
+    assert np.array_equal(B, Bt.T)
+    M.assemble_preconditioner()
+    rc, x, it = M.solve_nse(np.zeros(f.n))
+    assert rc == 0 and 0 < it < 500 and np.all(x[f.fixed.astype(bool)] == 0)
+    M.assemble_temperature(m.T0, x)
+    rcT, T, itT = M.solve_temperature(m.T0)
+    cs = m.T_constraints
+    n_id = 0
+    for l, d in enumerate(cs.line_dof):
+        b, e = cs.entry_ptr[l], cs.entry_ptr[l + 1]
+        if e - b == 1 and cs.entry_w[b] == 1.0:
+            assert T[d] == T[cs.entry_dof[b]]
+            n_id += 1
+    assert rcT == 0 and n_id > 0
 
 
 def test_element_interpolants_of_constants_are_exact():
@@ -171,10 +240,28 @@ def rel(a, b):
     return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
 
 
-@pytest.fixture(scope="module")
-def feec_setup():
-    m = dcp.HostMesh(refine=2, feec=True)
-    ph = dcp.classic_physics()
+def periodic(m, T):
+    """T with its periodic images set to their partners (the reference's
+    old_temperature_solution is always distributed)."""
+    T = T.copy()
+    cs = m.T_constraints
+    for l, d in enumerate(cs.line_dof):
+        b, e = cs.entry_ptr[l], cs.entry_ptr[l + 1]
+        if e - b == 1 and cs.entry_w[b] == 1.0 and cs.inhomogeneity[l] == 0.0:
+            T[d] = T[cs.entry_dof[b]]
+    return T
+
+
+@pytest.fixture(scope="module", params=["shell", "cube"])
+def feec_setup(request):
+    if request.param == "cube":
+        # aqua_planet_cube_test_3d.prm: FEEC on the periodic cuboid
+        rp = dcp.load_prm(CUBE_PRM)
+        m = dcp.HostMesh(cuboid=True, refine=2, feec=True, length=rp.length)
+        ph = dcp.physics_from_params(rp)
+    else:
+        m = dcp.HostMesh(refine=2, feec=True)
+        ph = dcp.classic_physics()
     ctx = dcp.Context()
     ctx.set_physics(ph)
     ctx.upload_feec_mesh(m)
@@ -192,7 +279,7 @@ def test_feec_element_and_assembly(feec_setup, state):
     else:
         x = rng.uniform(-1, 1, f.n)
         x[f.fixed.astype(bool)] = 0
-        T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+        T = periodic(m, m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T))
     ctx.set_state(dcp.OLD_NSE_SOLUTION, x)
     ctx.set_state(dcp.OLD_T_SOLUTION, T)
     K, fl = ctx.feec_cell_system(0, f.n_cells)
@@ -219,7 +306,7 @@ def test_feec_element_and_assembly(feec_setup, state):
 def test_feec_time_step(feec_setup):
     m, ph, ctx = feec_setup
     f = m.feec
-    x0, T0 = np.zeros(f.n), m.T0.copy()
+    x0, T0 = np.zeros(f.n), periodic(m, m.T0)
     for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
                    (dcp.T_SOLUTION, T0)):
         ctx.set_state(fld, v)
@@ -260,7 +347,7 @@ def test_feec_time_step_fixed_inner(feec_setup):
     iterates agree at 1e-10 with equal outer counts."""
     m, ph, ctx = feec_setup
     f = m.feec
-    x0, T0 = np.zeros(f.n), m.T0.copy()
+    x0, T0 = np.zeros(f.n), periodic(m, m.T0)
     for fld, v in ((dcp.OLD_NSE_SOLUTION, x0), (dcp.NSE_SOLUTION, x0), (dcp.OLD_T_SOLUTION, T0),
                    (dcp.T_SOLUTION, T0)):
         ctx.set_state(fld, v)
@@ -276,28 +363,46 @@ def test_feec_time_step_fixed_inner(feec_setup):
     orc.assemble_nse_system(x0, T0)
     orc.assemble_preconditioner()
     rco, xo, ito = orc.solve_nse(x0)
+    # the oracle's own rounding envelope: the same solve from a pressure guess
+    # perturbed by 1e-16. On the shell it moves nothing (< 1e-12, equal
+    # counts); the cuboid's step ends at the tolerance boundary (21 vs 20
+    # outer steps, 1e-6 apart), so there the GPU may take either count
+    x1 = x0.copy()
+    x1[f.n_w + f.n_u:] = 1e-16 * np.random.default_rng(1).uniform(-1, 1, f.n_p)
+    _, xo1, ito1 = orc.solve_nse(x1)
+    spread = np.linalg.norm(xo1 - xo) / np.linalg.norm(xo)
     assert rc == rco == 0
-    assert it == ito
+    assert it in (ito, ito1)
     xg = ctx.get_state(dcp.NSE_SOLUTION)
-    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+    if ito == ito1:
+        assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+    else:
+        xr = xo if it == ito else xo1
+        assert np.linalg.norm(xg - xr) <= max(1e-10, 10 * spread) * np.linalg.norm(xr)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("geometry", ["shell", "cube"])
 @pytest.mark.parametrize("zero_mean", [True, False])
-def test_feec_identity_preconditioned_gmres(zero_mean):
+def test_feec_identity_preconditioned_gmres(zero_mean, geometry):
     """use_block_preconditioner_feec = false (boussineq_model_FEEC.tpp:1420-1431):
     SolverGMRES(100) <= 15000 on nse_matrix with PreconditionerBlockIdentity
     (dst = src, the pressure block minus its QGauss(2) mean value when
     correct_pressure_to_zero_mean; preconditioner_block_identity.hpp:31-53),
     config 4's physics at r = 2 (242 GMRES iterations in the oracle): equal
-    iteration count, iterate at 1e-10."""
-    m = dcp.HostMesh(refine=2, feec=True)
-    rp = dcp.load_prm("configs/aqua_planet_shell_test_3d-feec.prm")
+    iteration count, iterate at 1e-10. The cuboid (60 iterations): its
+    pressure without the mean correction is fixed only up to the Krylov
+    iterate, and a 1e-16 perturbation of the oracle's own guess moves it by
+    2.7e-10, so there the iterate is compared at 1e-8."""
+    cube = geometry == "cube"
+    rp = dcp.load_prm(CUBE_PRM if cube else FEEC_PRM)
+    m = (dcp.HostMesh(cuboid=True, refine=2, feec=True, length=rp.length) if cube
+         else dcp.HostMesh(refine=2, feec=True))
     ph = dcp.physics_from_params(rp)
     f = m.feec
     rng = np.random.default_rng(SEED + 7)
     x0 = np.zeros(f.n)
-    T0 = m.T0 + 0.05 * rng.uniform(-1, 1, m.n_T)
+    T0 = periodic(m, m.T0 + 0.05 * rng.uniform(-1, 1, m.n_T))
     ctx = dcp.Context()
     ctx.set_physics(ph)
     ctx.upload_feec_mesh(m)
@@ -316,4 +421,4 @@ def test_feec_identity_preconditioned_gmres(zero_mean):
     rco, xo, ito = orc.solve_nse(x0)
     print("identity-preconditioned GMRES(100):", it, ito)
     assert rc == rco == 0 and it == ito and it > 30
-    assert np.linalg.norm(xg - xo) <= 1e-10 * np.linalg.norm(xo)
+    assert np.linalg.norm(xg - xo) <= (1e-8 if cube else 1e-10) * np.linalg.norm(xo)

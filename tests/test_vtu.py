@@ -138,12 +138,14 @@ def test_feec_vtu_on_the_shell(tmp_path):
     assert 'Name="vorticity"' in txt and 'Name="velocity"' in txt and "feec-00001.0000.vtu" in txt
 
 
-def test_periodic_feec_is_rejected():
-    """FEEC on the cuboid (data/aqua_planet_cube_test_3d.prm selects it) would
-    need periodic Nedelec / RT / DGQ0 dofs (planet_geometry.tpp:44-56), which
-    the FEEC numbering does not build: refused instead of silently treating
-    periodic faces as boundary faces."""
+def test_periodic_feec_one_cell_across_is_rejected():
+    """FEEC on the cuboid identifies the x = 1 / y = 1 edges and faces with
+    their x = 0 / y = 0 partners (feec_mesh.cpp); with one cell across
+    (refinement 0) a cell would hold the same dof twice, which the concurrent
+    scatter cannot take: refused up front."""
     import pytest
     with pytest.raises(dcp.DcpError) as e:
-        dcp.HostMesh(cuboid=True, refine=1, feec=True)
+        dcp.HostMesh(cuboid=True, refine=0, feec=True)
     assert e.value.code == dcp.DCP_ERR_UNSUPPORTED
+    m = dcp.HostMesh(cuboid=True, refine=1, feec=True)
+    assert m.feec.n_p == 8
