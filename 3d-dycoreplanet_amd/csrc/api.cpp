@@ -559,7 +559,6 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
       td[size_t(cell) * tdpc + (tdpc == 27 ? kQ2HierToLex[v] : v)] = t;
     }
   }
-  for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
   // ---- periodic identification. An identity line "dof = partner" (one
   // entry, weight 1, homogeneous: a closed make_periodicity_constraints line)
   // makes the dof an image of its partner. A velocity node is an image of node
@@ -630,10 +629,14 @@ void prepare_mesh(HostPrep& h, int n_cells, const int32_t* cell_nse_dofs,
     for (int n = 0; n < nv; ++n)
       require(h.vmaster[n] < 0 || h.vmaster[h.vmaster[n]] < 0, DCP_ERR_UNSUPPORTED,
               "periodic chain not closed");
+    // a rank's local mesh may hold a partner only through its images' cells
+    for (int n = 0; n < nv; ++n)
+      if (h.vmaster[n] >= 0 && seen[n]) seen[h.vmaster[n]] = 1;
     for (int p = 0; p < n_p; ++p)
       require(h.pmaster[p] < 0 || h.pmaster[h.pmaster[p]] < 0, DCP_ERR_UNSUPPORTED,
               "periodic chain not closed");
   }
+  for (int k = 0; k < nv; ++k) require(seen[k], DCP_ERR_INVALID, "velocity node without a cell");
   // ---- constraints -> node-local form. A line without entries is a fixed
   // component; three of them on one node form a no-slip node; a single one is
   // a no-normal-flux line whose weights all vanished (normal along an axis).
@@ -2456,8 +2459,6 @@ int dcp_mesh_upload(dcp_ctx* ctx, int n_cells, const int32_t* cell_nse_dofs,
       cell_diameter = L.diameter.data();
       prepare_mesh(h, n_cells, L.cell_nse_dofs.data(), L.cell_T_dofs.data(), L.geometry.data(),
                    cell_diameter, n_u, n_p, n_T, &lnc, &ltc, &hint);
-      require(!(h.n_vslave || h.n_pslave || h.n_tslave), DCP_ERR_UNSUPPORTED,
-              "periodic constraints on several GPUs are not supported");
     } else {
       prepare_mesh(h, n_cells, cell_nse_dofs, cell_T_dofs, cell_geometry, cell_diameter, n_u,
                    n_p, n_T, nse_c, T_c);
@@ -2868,7 +2869,7 @@ int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves) {
     require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     require(c.nse_assembled, DCP_ERR_STATE, "assemble_nse_system must run first");
-    require(!c.comm, DCP_ERR_UNSUPPORTED, "the Schur-complement solver runs on one GPU");
+    require(!c.comm || !c.dim2, DCP_ERR_UNSUPPORTED, "the 2D model runs on one GPU");
     SectionScope sec(c, "   Solve NSE system");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     return solve_nse_schur(c, schur_iterations, a_solves);

@@ -27,7 +27,12 @@ struct Global {
   int n_u;
   std::vector<int64_t> start;                 // cell range of each rank
   std::vector<int32_t> vown, pown, Town;      // owner rank per entity
-  std::vector<int32_t> pc_ptr, pc_cells;      // pressure dof (vertex) -> cells
+  std::vector<int32_t> pc_ptr, pc_cells;      // pressure dof (partner) -> cells
+  // periodic partner per entity (itself if none): make_periodicity_constraints'
+  // identity lines. Ghost layers grow across them (the partner's cells are
+  // neighbours, as p4est's periodic ghost layer has them) and every local
+  // image brings its partner, so each rank's constraint lines stay local.
+  std::vector<int32_t> vfold, pfold, Tfold;
 
   int rank_of(int c) const {
     return int(std::upper_bound(start.begin(), start.end(), int64_t(c)) - start.begin()) - 1;
@@ -48,7 +53,7 @@ std::vector<int32_t> local_cells(const Global& g, int s, std::vector<int>& stamp
       for (int k = 0; k < 89; ++k) {
         const int d = g.nse[size_t(c) * 89 + k];
         if (d < g.n_u) continue;
-        const int p = d - g.n_u;
+        const int p = g.pfold[d - g.n_u];
         for (int j = g.pc_ptr[p]; j < g.pc_ptr[p + 1]; ++j) {
           const int o = g.pc_cells[j];
           if (stamp[o] != token) {
@@ -126,6 +131,58 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
       if (g.Town[t] < 0) g.Town[t] = rc;
     }
   }
+  // periodic partners: lines "dof = partner" (one entry, weight 1, homogeneous)
+  auto identity = [](const dcp_constraints* cs, int l) {
+    const int b = cs->entry_ptr[l];
+    return (cs->entry_ptr[l + 1] - b == 1 && cs->entry_w[b] == 1.0 && cs->inhomogeneity[l] == 0.0)
+               ? cs->entry_dof[b]
+               : -1;
+  };
+  g.vfold.resize(g.nv);
+  g.pfold.resize(n_p);
+  g.Tfold.resize(n_T);
+  for (int i = 0; i < g.nv; ++i) g.vfold[i] = i;
+  for (int i = 0; i < n_p; ++i) g.pfold[i] = i;
+  for (int i = 0; i < n_T; ++i) g.Tfold[i] = i;
+  if (nse_c)
+    for (int l = 0; l < nse_c->n_lines; ++l) {
+      const int d = nse_c->line_dof[l], t = identity(nse_c, l);
+      if (d < 0 || d >= n_u + n_p || t < 0 || t >= n_u + n_p || t == d) continue;
+      if (d < n_u && t < n_u && t / 3 != d / 3 && t % 3 == d % 3) g.vfold[d / 3] = t / 3;
+      if (d >= n_u && t >= n_u) g.pfold[d - n_u] = t - n_u;
+    }
+  // Q1 temperature: the partner vertex's dof (via the pressure partner of
+  // the same vertex, local dof 4v + 3), also where the image's identity line
+  // was closed into a Dirichlet line: local T and p then cover the same
+  // vertices, as prepare_mesh requires
+  if (tdpc == 8) {
+    std::vector<int32_t> pT(n_p, -1);
+    for (int c = 0; c < n_cells; ++c)
+      for (int v = 0; v < 8; ++v) {
+        const int d = cell_nse_dofs[size_t(c) * 89 + 4 * v + 3];
+        if (d >= n_u && d < n_u + n_p) pT[d - n_u] = cell_T_dofs[size_t(c) * 8 + v];
+      }
+    for (int c = 0; c < n_cells; ++c)
+      for (int v = 0; v < 8; ++v) {
+        const int d = cell_nse_dofs[size_t(c) * 89 + 4 * v + 3];
+        const int t = cell_T_dofs[size_t(c) * 8 + v];
+        if (d < n_u || d >= n_u + n_p || t < 0 || t >= n_T) continue;
+        const int pf = g.pfold[d - n_u];
+        if (pf != d - n_u && pT[pf] >= 0) g.Tfold[t] = pT[pf];
+      }
+  }
+  if (T_c)
+    for (int l = 0; l < T_c->n_lines; ++l) {
+      const int d = T_c->line_dof[l], t = identity(T_c, l);
+      if (d >= 0 && d < n_T && t >= 0 && t < n_T && t != d) g.Tfold[d] = t;
+    }
+  // cells per pressure partner (a periodic image's cells join its partner's)
+  std::fill(cnt.begin(), cnt.end(), 0);
+  for (int c = 0; c < n_cells; ++c)
+    for (int k = 0; k < 89; ++k) {
+      const int d = cell_nse_dofs[size_t(c) * 89 + k];
+      if (d >= n_u) cnt[g.pfold[d - n_u] + 1]++;
+    }
   for (int p = 0; p < n_p; ++p) cnt[p + 1] += cnt[p];
   g.pc_ptr = cnt;
   g.pc_cells.resize(size_t(cnt[n_p]));
@@ -134,25 +191,36 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
     for (int c = 0; c < n_cells; ++c)
       for (int k = 0; k < 89; ++k) {
         const int d = cell_nse_dofs[size_t(c) * 89 + k];
-        if (d >= n_u) g.pc_cells[f[d - n_u]++] = c;
+        if (d >= n_u) g.pc_cells[f[g.pfold[d - n_u]]++] = c;
       }
   }
   std::vector<int> cstamp(n_cells, -1), vstamp(g.nv, -1), pstamp(n_p, -1), Tstamp(n_T, -1);
   int token = 0;
+  // a cell's entities and their periodic partners
   auto vnodes_of = [&](int c, auto&& emit) {
     for (int k = 0; k < 89; ++k) {
       const int d = cell_nse_dofs[size_t(c) * 89 + k];
-      if (d < n_u && d % 3 == 0) emit(d / 3);
+      if (d < n_u && d % 3 == 0) {
+        emit(d / 3);
+        if (g.vfold[d / 3] != d / 3) emit(g.vfold[d / 3]);
+      }
     }
   };
   auto pdofs_of = [&](int c, auto&& emit) {
     for (int k = 0; k < 89; ++k) {
       const int d = cell_nse_dofs[size_t(c) * 89 + k];
-      if (d >= n_u) emit(d - n_u);
+      if (d >= n_u) {
+        emit(d - n_u);
+        if (g.pfold[d - n_u] != d - n_u) emit(g.pfold[d - n_u]);
+      }
     }
   };
   auto Tdofs_of = [&](int c, auto&& emit) {
-    for (int v = 0; v < tdpc; ++v) emit(cell_T_dofs[size_t(c) * tdpc + v]);
+    for (int v = 0; v < tdpc; ++v) {
+      const int t = cell_T_dofs[size_t(c) * tdpc + v];
+      emit(t);
+      if (g.Tfold[t] != t) emit(g.Tfold[t]);
+    }
   };
 
   LocalMesh L;
@@ -201,9 +269,16 @@ LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cel
     for (int l = 0; l < nse_c->n_lines; ++l) {
       const int d = nse_c->line_dof[l];
       if (d >= n_u || vl[d / 3] < 0) {
-        if (d >= n_u && pl[d - n_u] >= 0) {  // keep pressure lines: upload rejects them
+        if (d >= n_u && pl[d - n_u] >= 0) {  // pressure lines (periodic identities)
           L.nse_line.push_back(nu_loc + pl[d - n_u]);
           L.nse_inh.push_back(nse_c->inhomogeneity[l]);
+          for (int k = nse_c->entry_ptr[l]; k < nse_c->entry_ptr[l + 1]; ++k) {
+            const int e = nse_c->entry_dof[k];
+            const int le = e >= n_u && e < n_u + n_p && pl[e - n_u] >= 0 ? nu_loc + pl[e - n_u] : -1;
+            if (le < 0) throw std::runtime_error("localize: constraint entry outside the local mesh");
+            L.nse_edof.push_back(le);
+            L.nse_w.push_back(nse_c->entry_w[k]);
+          }
           L.nse_ptr.push_back(int(L.nse_edof.size()));
         }
         continue;

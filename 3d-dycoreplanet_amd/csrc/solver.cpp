@@ -1341,7 +1341,8 @@ int solve_nse(Ctx& c, int* outer, int* inner_out) {
     distribute_nse_2d(c, x.p);                                 // :1233
   else
     distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);  // :1233
-  if (c.periodic) {  // periodic images = their partners
+  if (c.periodic) {  // periodic images = their partners (fresh ghosts first)
+    halo_exchange(c, c.halo_nse, x.p);
     copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
     copy_images(c.n_img_p, c.img_p.p, c.mst_p.p, x.p, c.stream);
   }
@@ -1437,6 +1438,9 @@ void build_ilu(Ctx& c) {
         for (int k = bp[r]; k < bp[r + 1]; ++k)
           for (int cj = 0; cj < 3; ++cj) {
             const int j = 3 * bc[k] + cj;
+            // several GPUs: the rank's owned block only (Ifpack's ILU under
+            // TrilinosWrappers::PreconditionILU, overlap 0: block Jacobi)
+            if (j >= n) continue;
             if (j == i) diag[i] = int(col.size());
             col.push_back(j);
             pos.push_back(9 * k + 3 * ci + cj);
@@ -1499,8 +1503,12 @@ void build_ilu(Ctx& c) {
 }  // namespace
 
 int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
-  // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414), one GPU
-  if (c.comm) throw std::runtime_error("the Schur-complement solver runs on one GPU");
+  // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414). Several GPUs
+  // (3D): each rank factors the ILU of its owned diagonal block (the
+  // reference's Trilinos ILU with zero overlap, i.e. block Jacobi over the
+  // ranks, so the preconditioner depends on the partition as it does there);
+  // every block product refreshes its source's ghost entries first
+  if (c.comm && c.dim2) throw std::runtime_error("the 2D model runs on one GPU");
   const int nu = c.n_u, np = c.n_p, n = nu + np;
   const double dt = c.ph.dt;
   if (!c.dim2) {
@@ -1514,18 +1522,22 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   ilu_factor(iv, c.dim2 ? c.m2_val.p : c.A_val.p, f.lf_host.data(), f.lu.p, f.max_row, c.stream);
   // the blocks of nse_matrix: A, B^T (velocity rows), B (pressure rows)
   auto Ablk = [&](const double* x, double* y) {
-    if (c.dim2) c.m2_block(0, nu, 0, nu, x, y, false);
-    else spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
+    if (c.dim2) return c.m2_block(0, nu, 0, nu, x, y, false);
+    halo_exchange(c, c.halo_v, const_cast<double*>(x));
+    spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
   };
   auto Btblk = [&](const double* p, double* y) {
-    if (c.dim2) c.m2_block(0, nu, nu, n, p, y, false);
-    else spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, p, y, false, c.stream);
+    if (c.dim2) return c.m2_block(0, nu, nu, n, p, y, false);
+    halo_exchange(c, c.halo_p, const_cast<double*>(p));
+    spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, p, y, false, c.stream);
   };
   auto Bblk = [&](const double* u, double* y) {
-    if (c.dim2) c.m2_block(nu, n, 0, nu, u, y, false);
-    else spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, u, y, false, c.stream);
+    if (c.dim2) return c.m2_block(nu, n, 0, nu, u, y, false);
+    halo_exchange(c, c.halo_v, const_cast<double*>(u));
+    spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, u, y, false, c.stream);
   };
-  const Seg gu = Seg::all(nu), gp = Seg::all(np);
+  // owned entries (one GPU: all of them)
+  const Seg gu = c.dim2 ? Seg::all(nu) : c.seg_v(), gp = c.dim2 ? Seg::all(np) : c.seg_p();
   ensure_pool(c.sc_v, 8, size_t(nu));
   double* const cg_u[3] = {c.sc_v[0], c.sc_v[1], c.sc_v[2]};
   double *tmp = c.sc_v[3], *t1 = c.sc_v[4], *t2 = c.sc_v[5];
@@ -1586,6 +1598,8 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
     }
     distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);
     if (c.periodic) {
+      // several GPUs: a partner may be a ghost, fresh only after the exchange
+      halo_exchange(c, c.halo_nse, x.p);
       copy_images(c.n_img_u, c.img_u.p, c.mst_u.p, x.p, c.stream);
       copy_images(c.n_img_p, c.img_p.p, c.mst_p.p, x.p, c.stream);
     }
@@ -1601,6 +1615,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   sec_u.stop();
   scale(np, DScal{nullptr, 1.0 / dt}, x.p + nu, c.stream);           // :1384
   copy(n, x.p, c.nse_sol.p, c.stream);
+  halo_exchange(c, c.halo_nse, c.nse_sol.p);                          // ghosted copy
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
   if (schur_iterations) *schur_iterations = int(ctl.last_step);
   if (a_solves) *a_solves = n_inv;
@@ -1785,7 +1800,10 @@ int solve_temperature(Ctx& c, int* iters, double* T_range) {
     }
   }
   distribute_temperature(n, c.T_fixed.p, c.T_bc.p, x, c.stream);
-  if (c.periodic) copy_images(c.n_img_T, c.img_T.p, c.mst_T.p, x, c.stream);
+  if (c.periodic) {
+    halo_exchange(c, c.halo_T, x);
+    copy_images(c.n_img_T, c.img_T.p, c.mst_T.p, x, c.stream);
+  }
   halo_exchange(c, c.halo_T, x);
   if (T_range) {
     // min over ranks as max of -min

@@ -862,6 +862,9 @@ struct orc_model {
   long a_solve_iterations = 0;  // AztecOO A-GMRES iterations of the last solve (do_solve_A)
   int inner_max_steps = 5000;   // SolverControl(5000) of the inner Schur GMRES (timing hook)
   int schur_fixed_inner = 0;    // parity hook: the Schur solver's inner CGs run exactly k steps
+  // the Schur solver's ILU on P MPI ranks: Trilinos' ILU with zero overlap
+  // factors each rank's owned diagonal block (block Jacobi); empty: one rank
+  std::vector<int> ilu_block;   // [n_u] rank owning each velocity dof
   int block_fixed_inner = 0;    // parity hook: the block preconditioner's inner GMRES runs exactly k steps
 };
 
@@ -942,6 +945,10 @@ extern "C" void orc_assemble_nse_system_threads(orc_model* m, const double* old_
 
 extern "C" void orc_set_inner_max_steps(orc_model* m, int n) { m->inner_max_steps = n; }
 extern "C" void orc_set_schur_fixed_inner(orc_model* m, int k) { m->schur_fixed_inner = k; }
+extern "C" void orc_set_ilu_blocks(orc_model* m, const int* owner) {
+  if (owner) m->ilu_block.assign(owner, owner + m->n_u);
+  else m->ilu_block.clear();
+}
 extern "C" void orc_set_block_fixed_inner(orc_model* m, int k) { m->block_fixed_inner = k; }
 
 extern "C" void orc_build_nse_preconditioner(orc_model* m) {
@@ -1676,14 +1683,17 @@ struct Ilu0 {
   int n = 0;
   std::vector<int> ptr, col, diag;
   std::vector<double> val;
-  void factor(const Csr& A, int rows) {
+  // block: optional [rows] block id; entries between blocks are dropped (the
+  // factor of each diagonal block, TrilinosWrappers::PreconditionILU with
+  // overlap 0 on several ranks)
+  void factor(const Csr& A, int rows, const std::vector<int>* block = nullptr) {
     n = rows;
     ptr.assign(n + 1, 0);
     col.clear();
     val.clear();
     for (int r = 0; r < n; ++r) {
       for (int k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
-        if (A.cols[k] < n) {
+        if (A.cols[k] < n && (!block || (*block)[A.cols[k]] == (*block)[r])) {
           col.push_back(A.cols[k]);
           val.push_back(A.vals[k]);
         }
@@ -1765,7 +1775,8 @@ extern "C" int orc_solve_nse_schur(orc_model* m, double* sol, int* schur_iterati
   const double dt = m->ph.time_step;
   const Csr& M = m->nse;
   Ilu0 ilu;
-  ilu.factor(M, nu);  // inner_schur_preconditioner->initialize(block(0,0))
+  // inner_schur_preconditioner->initialize(block(0,0))
+  ilu.factor(M, nu, m->ilu_block.empty() ? nullptr : &m->ilu_block);
   auto A = [&](const double* x, double* y) { csr_block(M, 0, nu, 0, nu, x, y, false); };
   auto P = [&](const double* x, double* y) { ilu.apply(x, y); };
   int n_inv = 0;

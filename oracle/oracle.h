@@ -86,6 +86,9 @@ typedef struct orc_model orc_model;
 /* parity hook: the Schur-complement solver's A^-1 and preconditioner CGs run
  * exactly k steps (0 = the reference's 1e-6 relative rule) */
 void orc_set_schur_fixed_inner(orc_model* m, int k);
+/* the Schur solver's ILU as on P ranks: owner[n_u] = the rank owning each
+ * velocity dof, couplings between ranks dropped (block Jacobi); NULL: one rank */
+void orc_set_ilu_blocks(orc_model* m, const int* owner);
 /* Standard::BoussinesqModel<2>: element level (22 NSE dofs, 16 support points
  * per cell as [16][2]) and a 2D model whose other orc_* calls (schur solver,
  * temperature solve, exports, cfl) work as for the 3D one. */

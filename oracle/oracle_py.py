@@ -75,6 +75,7 @@ def lib():
         L.orc_assemble_nse_system_threads.argtypes = [P, P, P, I]
         L.orc_set_inner_max_steps.argtypes = [P, I]
         L.orc_set_schur_fixed_inner.argtypes = [P, I]
+        L.orc_set_ilu_blocks.argtypes = [P, P]
         L.orc_set_block_fixed_inner.argtypes = [P, I]
         L.orc_set_threads.argtypes = [I]
         L.orc_fgmres_outer.argtypes = [P, P, I, P]
@@ -255,6 +256,16 @@ class Model:
     def set_schur_fixed_inner(self, k):
         """Parity hook: the Schur solver's inner CGs run exactly k steps (0 = off)."""
         lib().orc_set_schur_fixed_inner(self.h, int(k))
+
+    def set_ilu_blocks(self, owner):
+        """The Schur solver's ILU as on P ranks (Trilinos ILU, overlap 0): owner
+        = the rank of every velocity dof; None restores the one-rank factor."""
+        if owner is None:
+            self._ilu_owner = None
+            lib().orc_set_ilu_blocks(self.h, None)
+            return
+        self._ilu_owner = np.ascontiguousarray(owner, np.int32)
+        lib().orc_set_ilu_blocks(self.h, _p(self._ilu_owner))
 
     def build_nse_preconditioner(self):
         lib().orc_build_nse_preconditioner(self.h)

@@ -18,12 +18,12 @@ import torch.multiprocessing as mp
 import dcp
 
 
-def _gloo_worker(rank, world, port, refine, q):
+def _gloo_worker(rank, world, port, refine, q, cuboid=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        m = dcp.HostMesh(refine=refine)
+        m = dcp.HostMesh(refine=refine, cuboid=cuboid)
         info = dcp.partition_info(m, rank, world)
         mine = {"rank": rank, "nvo": info["nvo"], "npo": info["npo"], "nTo": info["nTo"],
                 "cells": info["n_owned_cells"],
@@ -43,13 +43,16 @@ def _gloo_worker(rank, world, port, refine, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("refine", [2, 3])
-def test_partition_halo_consistency_gloo(refine):
+@pytest.mark.parametrize("refine,cuboid", [(2, False), (3, False), (2, True)])
+def test_partition_halo_consistency_gloo(refine, cuboid):
+    """cuboid: the periodic cube, whose ghost layers cross the x / y periodic
+    boundary (each image's partner local too)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29611 + refine
-    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, refine, q)) for r in range(world)]
+    port = 29611 + refine + 4 * cuboid
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, refine, q, cuboid))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(world))
@@ -115,6 +118,32 @@ def test_partition_covers_and_matches(refine, world):
             assert np.array_equal(ids, infos[s]["recv"][r])
         # every partition keeps the whole shell's 8-colour layout
         assert i["n_colors"] == 8
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_cube_partition_holds_every_local_images_partner(world):
+    """The periodic cube on several ranks: every rank's local mesh passes the
+    upload's periodic checks (each local image's partner is local, chains
+    closed), ownership covers every dof once and halos pair up."""
+    m = dcp.HostMesh(cuboid=True, refine=3)
+    infos = [dcp.partition_info(m, r, world) for r in range(world)]
+    assert sum(i["n_owned_cells"] for i in infos) == m.n_cells
+    assert sum(i["nvo"] for i in infos) == m.n_u // 3
+    assert sum(i["npo"] for i in infos) == m.n_p
+    assert sum(i["nTo"] for i in infos) == m.n_T
+    for r, i in enumerate(infos):
+        for s, ids in i["send"].items():
+            assert np.array_equal(ids, infos[s]["recv"][r])
+
+
+def periodic_state(m, v, cs):
+    """v with every periodic image set to its partner (identity lines)."""
+    v = v.copy()
+    for l, d in enumerate(cs.line_dof):
+        b, e = cs.entry_ptr[l], cs.entry_ptr[l + 1]
+        if e - b == 1 and cs.entry_w[b] == 1.0 and cs.inhomogeneity[l] == 0.0:
+            v[d] = v[cs.entry_dof[b]]
+    return v
 
 
 def _time_step(ctx, m, u, T):
@@ -649,3 +678,77 @@ def test_group_matrix_powers_bitwise(world, refine, fixed_inner):
         for key in ("x", "Tx", "rhs"):
             assert np.array_equal(a[key].view(np.int64), b[key].view(np.int64)), (r, key)
     print("matrix powers", world, refine, [x["extra"] for x in on[:2]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,gs,fixed_inner", [(2, "modified", 0), (3, "sstep", 0),
+                                                  (4, "sstep", 24)])
+def test_group_cube_time_step_matches_single_gpu(world, gs, fixed_inner):
+    """BASELINE C2's periodic cube (classic Q2/Q1, Coriolis and vertical
+    gravity on) as an in-process group: the x / y periodic identities cross
+    rank boundaries (ghost layers grow across them, every local image's
+    partner is local), against the one-GPU run: rhs and T rhs at 1e-12, the
+    solve at 1e-10 with equal FGMRES counts, T at 1e-10."""
+    rp = dcp.load_prm(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "configs", "aqua_planet_cube_test_3d.prm"))
+    ph = dcp.physics_from_params(rp)
+    m = dcp.HostMesh(cuboid=True, refine=2, length=rp.length)
+    rng = np.random.default_rng(17)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    u = periodic_state(m, u, m.nse_constraints)
+    T = periodic_state(m, m.T0.copy(), m.T_constraints)
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(ph)
+    ref_ctx.upload_mesh(m)
+    ref_ctx.set_gram_schmidt(gs)
+    ref_ctx.set_block_fixed_inner(fixed_inner)
+    ref = _time_step(ref_ctx, m, u, T)
+    ref_ctx.close()
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(ph)
+            ctx.upload_mesh(m)
+            ctx.set_gram_schmidt(gs)
+            ctx.set_block_fixed_inner(fixed_inner)
+            results[rank] = _time_step(ctx, m, u, T)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+
+    def merged(key):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        return v
+    rel = lambda a, b: np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)  # noqa: E731
+    assert rel(merged("rhs"), ref["rhs"]) < 1e-12
+    assert rel(merged("T_rhs"), ref["T_rhs"]) < 1e-12
+    x = merged("x")
+    print("cube group", world, gs, "outer", ref["nse"][1], "inner", ref["nse"][2],
+          [r["nse"][2] for r in results], "x rel2",
+          np.linalg.norm(x - ref["x"]) / np.linalg.norm(ref["x"]))
+    assert np.linalg.norm(x - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
+    assert rel(merged("Tx"), ref["Tx"]) < 1e-10
+    for r in results:
+        assert r["nse"][0] == ref["nse"][0] == 0
+        assert r["nse"][1] == ref["nse"][1]
+        if fixed_inner:
+            assert r["nse"][2] == ref["nse"][2]
+        assert abs(r["nse"][2] - ref["nse"][2]) <= 0.15 * ref["nse"][2]
+        assert abs(r["T"][1] - ref["T"][1]) <= 1
+        assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-10)
+
