@@ -915,7 +915,8 @@ std::vector<int64_t> global_positions(const Ctx& c, int field) {
       g[size_t(nw + nu) + i] = int64_t(c.fe_nw_g) + c.fe_nu_g + c.p_g[i];
   } else {
     g.resize(size_t(c.n_u) + c.n_p);
-    for (int i = 0; i < c.n_u; ++i) g[i] = 3 * int64_t(c.vnode_g[i / 3]) + i % 3;
+    const int vd = c.vdim;
+    for (int i = 0; i < c.n_u; ++i) g[i] = vd * int64_t(c.vnode_g[i / vd]) + i % vd;
     for (int i = 0; i < c.n_p; ++i) g[size_t(c.n_u) + i] = int64_t(c.n_u_g) + c.p_g[i];
   }
   return g;
@@ -931,7 +932,7 @@ bool owned_entry(const Ctx& c, int field, size_t i) {
     if (k < c.fe_nw + c.fe_nu) return k - c.fe_nw < c.fe_nuo;
     return k - c.fe_nw - c.fe_nu < c.fe_npo;
   }
-  if (int(i) < c.n_u) return int(i) < 3 * c.nvo;
+  if (int(i) < c.n_u) return int(i) < c.vdim * c.nvo;
   return int(i) - c.n_u < c.npo;
 }
 
@@ -2638,6 +2639,8 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     SectionScope sec(c, "   Assemble NSE system");
     PhaseTimer t(c, &c.timings.assemble_nse_ms);
     if (c.dim2) {
+      if (!c.old_nse_ghosted) halo_exchange(c, c.halo_nse, c.old_nse.p);
+      if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
       assemble_nse_2d(c, flags);
       t.stop();
       return DCP_OK;
@@ -2869,7 +2872,6 @@ int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves) {
     require(!ctx->feec, DCP_ERR_STATE, "FEEC mesh uploaded: use the dcp_feec_* calls");
     Ctx& c = *ctx;
     require(c.nse_assembled, DCP_ERR_STATE, "assemble_nse_system must run first");
-    require(!c.comm || !c.dim2, DCP_ERR_UNSUPPORTED, "the 2D model runs on one GPU");
     SectionScope sec(c, "   Solve NSE system");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
     return solve_nse_schur(c, schur_iterations, a_solves);
@@ -3448,8 +3450,6 @@ int dcp_feec_mesh_upload(dcp_ctx* ctx, const dcp_feec_mesh* gm) {
     for (int t = 0; t < nT; ++t)
       require(tmaster[t] < 0 || (tmaster[tmaster[t]] < 0 && !Tfix[tmaster[t]]), DCP_ERR_UNSUPPORTED,
               "periodic temperature chain not closed");
-    require(!dist || n_timg == 0, DCP_ERR_UNSUPPORTED,
-            "periodic FEEC temperature runs on one GPU (the cuboid is not partitioned)");
     const std::vector<int32_t> tdo = td;
     if (n_timg)
       for (auto& t : td)
@@ -4054,8 +4054,85 @@ int dcp_host_mesh2d_view_get(const dcp_host_mesh* h, dcp_mesh2d* out, const doub
 
 int dcp_mesh2d_upload(dcp_ctx* ctx, const dcp_mesh2d* m) {
   return guarded(ctx, [&] {
-    require(ctx != nullptr, DCP_ERR_INVALID, "NULL context");
-    mesh2d_upload(*ctx, m);
+    require(ctx != nullptr && m != nullptr, DCP_ERR_INVALID, "NULL argument");
+    Ctx& c = *ctx;
+    if (!c.comm) {
+      mesh2d_upload(c, m);
+      return DCP_OK;
+    }
+    // several GPUs: this rank's cells + two ghost layers (partition.h), the
+    // velocity as scalar dofs (vdim 1: the support points' two components
+    // are two owned-or-ghost entries of their own)
+    Local2D L;
+    try {
+      L = localize_2d(*m, c.cfg.rank, c.cfg.world_size);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    const dcp_mesh2d lv = L.view();
+    mesh2d_upload(c, &lv);
+    c.have_mesh = false;
+    c.vdim = 1;
+    c.n_owned_cells = L.n_owned_cells;
+    c.n_vnodes = L.n_u();
+    c.nvo = L.nuo;
+    c.npo = L.npo;
+    c.nTo = L.nTo;
+    c.n_u_g = m->n_u;
+    c.n_p_g = m->n_p;
+    c.n_T_g = m->n_T;
+    c.vnode_g = L.u_g;
+    c.p_g = L.p_g;
+    c.T_g = L.T_g;
+    auto one = [&](Ctx::Halo& h, std::initializer_list<std::pair<const HaloPlan*, int>> parts) {
+      std::vector<int> peers;
+      std::vector<std::vector<int32_t>> sp, rp;
+      for (auto& pr : parts) plan_positions(*pr.first, pr.second, peers, sp, rp);
+      make_halo(h, peers, sp, rp);
+    };
+    one(c.halo_v, {{&L.hu, 0}});
+    one(c.halo_p, {{&L.hp, 0}});
+    one(c.halo_nse, {{&L.hu, 0}, {&L.hp, c.n_u}});
+    one(c.halo_T, {{&L.hT, 0}});
+    double mx[4] = {double(c.nvo + c.npo), double(c.npo), double(c.nvo), double(c.nTo)};
+    double* d = c.dscal.p + 3500;
+    DCP_HIP_CHECK(hipMemcpyAsync(d, mx, sizeof(mx), hipMemcpyHostToDevice, c.stream));
+    c.comm->allreduce(d, 4, true, c.stream);
+    DCP_HIP_CHECK(hipMemcpyAsync(mx, d, sizeof(mx), hipMemcpyDeviceToHost, c.stream));
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    for (int k = 0; k < 4; ++k) c.max_owned[k] = int(mx[k]);
+    c.old_nse_ghosted = c.old_T_ghosted = false;
+    c.have_mesh = true;
+    return DCP_OK;
+  });
+}
+
+int dcp_mesh2d_partition_info(const dcp_mesh2d* m, int rank, int world, int field, int64_t* info,
+                              int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                              int32_t* recv_ptr, int64_t* recv_gid) {
+  return guarded(nullptr, [&] {
+    require(m != nullptr && info != nullptr, DCP_ERR_INVALID, "NULL argument");
+    require(field >= 0 && field < 3, DCP_ERR_INVALID, "field must be 0..2");
+    Local2D L;
+    try {
+      L = localize_2d(*m, rank, world);
+    } catch (const std::runtime_error& e) {
+      fail(DCP_ERR_INVALID, e.what());
+    }
+    // the local mesh passes the upload's own checks
+    int n_colors = 0;
+    const dcp_mesh2d lv = L.view();
+    mesh2d_check(&lv, &n_colors);
+    const HaloPlan& h = field == 0 ? L.hu : field == 1 ? L.hp : L.hT;
+    const int64_t v[11] = {L.n_cells, L.n_owned_cells, L.nuo, L.nug, L.npo, L.npg, L.nTo, L.nTg,
+                           int64_t(h.peers.size()), int64_t(h.send_idx.size()),
+                           int64_t(h.recv_idx.size())};
+    std::copy(v, v + 11, info);
+    if (peers) std::copy(h.peers.begin(), h.peers.end(), peers);
+    if (send_ptr) std::copy(h.send_ptr.begin(), h.send_ptr.end(), send_ptr);
+    if (recv_ptr) std::copy(h.recv_ptr.begin(), h.recv_ptr.end(), recv_ptr);
+    if (send_gid) std::copy(h.send_gid.begin(), h.send_gid.end(), send_gid);
+    if (recv_gid) std::copy(h.recv_gid.begin(), h.recv_gid.end(), recv_gid);
     return DCP_OK;
   });
 }

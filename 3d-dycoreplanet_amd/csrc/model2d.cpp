@@ -227,7 +227,8 @@ void mesh2d_check(const dcp_mesh2d* m, int* n_colors) {
 }
 
 void mesh2d_upload(Ctx& c, const dcp_mesh2d* m) {
-  need(!c.comm, DCP_ERR_UNSUPPORTED, "the 2D model runs on one GPU");
+  // several GPUs: m is the rank's local mesh (localize_2d) and the caller
+  // (dcp_mesh2d_upload) then sets the owned sizes, global ids and halos
   Prep2D h;
   prepare2d(m, h);
   DCP_HIP_CHECK(hipSetDevice(c.cfg.device));

@@ -416,7 +416,19 @@ FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
       if (Town[t] < 0) Town[t] = rc;
     }
   }
-  // vertex (T dof) -> cells, for the vertex-neighbour ghost layers
+  // periodic temperature partners (the cuboid's identity lines): a local
+  // image brings its partner, so the rank's constraint lines stay local
+  std::vector<int32_t> Tfold(m.n_T);
+  for (int t = 0; t < m.n_T; ++t) Tfold[t] = t;
+  for (int l = 0; l < m.T.n_lines; ++l) {
+    const int d = m.T.line_dof[l], b = m.T.entry_ptr[l];
+    if (d >= 0 && d < m.n_T && m.T.entry_ptr[l + 1] - b == 1 && m.T.entry_w[b] == 1.0 &&
+        m.T.inhomogeneity[l] == 0.0 && m.T.entry_dof[b] >= 0 && m.T.entry_dof[b] < m.n_T)
+      Tfold[d] = m.T.entry_dof[b];
+  }
+  // vertex (T dof) -> cells and edge -> cells, for the ghost layers: cells
+  // sharing a vertex or an edge are neighbours (the periodic cuboid's edges are
+  // identified across x = 0 / 1, y = 0 / 1, so its layers cross them)
   std::vector<int32_t> vptr(size_t(m.n_T) + 1, 0), vcells;
   for (int c = 0; c < nc; ++c)
     for (int v = 0; v < 8; ++v) vptr[m.cell_T_dofs[8 * size_t(c) + v] + 1]++;
@@ -426,6 +438,16 @@ FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
     std::vector<int32_t> f(vptr.begin(), vptr.end() - 1);
     for (int c = 0; c < nc; ++c)
       for (int v = 0; v < 8; ++v) vcells[f[m.cell_T_dofs[8 * size_t(c) + v]]++] = c;
+  }
+  std::vector<int32_t> eptr(size_t(m.n_w) + 1, 0), ecells;
+  for (int c = 0; c < nc; ++c)
+    for (int l = 0; l < 12; ++l) eptr[m.cell_w[12 * size_t(c) + l] + 1]++;
+  for (int e = 0; e < m.n_w; ++e) eptr[e + 1] += eptr[e];
+  ecells.resize(size_t(eptr[m.n_w]));
+  {
+    std::vector<int32_t> f(eptr.begin(), eptr.end() - 1);
+    for (int c = 0; c < nc; ++c)
+      for (int l = 0; l < 12; ++l) ecells[f[m.cell_w[12 * size_t(c) + l]]++] = c;
   }
   std::vector<int> cstamp(nc, -1), wstamp(m.n_w, -1), ustamp(m.n_u, -1), Tstamp(m.n_T, -1);
   int token = 0;
@@ -439,15 +461,22 @@ FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
     frontier = owned;
     for (int layer = 0; layer < 2; ++layer) {
       next.clear();
-      for (int32_t c : frontier)
+      auto visit = [&](int o) {
+        if (cstamp[o] != tok) {
+          cstamp[o] = tok;
+          next.push_back(o);
+        }
+      };
+      for (int32_t c : frontier) {
         for (int v = 0; v < 8; ++v) {
           const int t = m.cell_T_dofs[8 * size_t(c) + v];
-          for (int j = vptr[t]; j < vptr[t + 1]; ++j)
-            if (cstamp[vcells[j]] != tok) {
-              cstamp[vcells[j]] = tok;
-              next.push_back(vcells[j]);
-            }
+          for (int j = vptr[t]; j < vptr[t + 1]; ++j) visit(vcells[j]);
         }
+        for (int l = 0; l < 12; ++l) {
+          const int e = m.cell_w[12 * size_t(c) + l];
+          for (int j = eptr[e]; j < eptr[e + 1]; ++j) visit(ecells[j]);
+        }
+      }
       ghosts.insert(ghosts.end(), next.begin(), next.end());
       frontier.swap(next);
     }
@@ -462,7 +491,11 @@ FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
     for (int f = 0; f < 6; ++f) emit(m.cell_u[6 * size_t(c) + f]);
   };
   auto T_of = [&](int c, auto&& emit) {
-    for (int v = 0; v < 8; ++v) emit(m.cell_T_dofs[8 * size_t(c) + v]);
+    for (int v = 0; v < 8; ++v) {
+      const int t = m.cell_T_dofs[8 * size_t(c) + v];
+      emit(t);
+      if (Tfold[t] != t) emit(Tfold[t]);
+    }
   };
   FeecLocal L;
   L.rank = rank;
@@ -560,6 +593,224 @@ FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world) {
     }
   }
   for (int f = 0; f < 4; ++f) {
+    const Field& F = fields[f];
+    std::vector<std::vector<int32_t>> recv(world);
+    for (size_t i = size_t(F.no); i < F.ents->size(); ++i) {
+      const int32_t e = (*F.ents)[i];
+      recv[(*F.own)[e]].push_back(e);
+    }
+    HaloPlan& h = *F.plan;
+    h.send_ptr.push_back(0);
+    h.recv_ptr.push_back(0);
+    for (int s = 0; s < world; ++s) {
+      if (s == rank || (sends[f][s].empty() && recv[s].empty())) continue;
+      h.peers.push_back(s);
+      for (int32_t e : sends[f][s]) {
+        h.send_idx.push_back((*F.lidx)[e]);
+        h.send_gid.push_back(e);
+      }
+      for (int32_t e : recv[s]) {
+        h.recv_idx.push_back((*F.lidx)[e]);
+        h.recv_gid.push_back(e);
+      }
+      h.send_ptr.push_back(int32_t(h.send_idx.size()));
+      h.recv_ptr.push_back(int32_t(h.recv_idx.size()));
+    }
+  }
+  return L;
+}
+
+dcp_mesh2d Local2D::view() const {
+  dcp_mesh2d v{};
+  v.n_cells = n_cells;
+  v.n_u = n_u();
+  v.n_p = n_p();
+  v.n_T = n_T();
+  v.temperature_degree = tdpc == 9 ? 2 : 1;
+  v.cell_nse_dofs = cell_dofs.data();
+  v.cell_T_dofs = cell_T.data();
+  v.cell_geometry = geometry.data();
+  v.cell_diameter = diameter.data();
+  v.nse = dcp_constraints{int(nse_line.size()), nse_line.data(), nse_ptr.data(), nse_edof.data(),
+                          nse_w.data(), nse_inh.data()};
+  v.T = dcp_constraints{int(T_line.size()), T_line.data(), T_ptr.data(), T_edof.data(), T_w.data(),
+                        T_inh.data()};
+  return v;
+}
+
+Local2D localize_2d(const dcp_mesh2d& m, int rank, int world) {
+  const int nc = m.n_cells, nu = m.n_u, np = m.n_p, nT = m.n_T;
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("localize: bad rank/world");
+  if (nc < world) throw std::runtime_error("localize: fewer cells than ranks");
+  if (!m.cell_nse_dofs || !m.cell_T_dofs || !m.cell_geometry || !m.cell_diameter)
+    throw std::runtime_error("localize: NULL array");
+  if (m.temperature_degree != 1 && m.temperature_degree != 2)
+    throw std::runtime_error("localize: 2D temperature degree must be 1 or 2");
+  const int tdpc = m.temperature_degree == 1 ? 4 : 9;
+  // FESystem(FE_Q(2)^2, FE_Q(1)) local dof: pressure at 2, 5, 8, 11 (the vertices)
+  auto is_p = [](int i) { return i < 12 && i % 3 == 2; };
+  std::vector<int64_t> start(size_t(world) + 1);
+  for (int r = 0; r <= world; ++r) start[r] = int64_t(r) * nc / world;
+  auto rank_of = [&](int c) {
+    return int(std::upper_bound(start.begin(), start.end(), int64_t(c)) - start.begin()) - 1;
+  };
+  std::vector<int32_t> uown(nu, -1), pown(np, -1), Town(nT, -1);
+  std::vector<int32_t> pptr(size_t(np) + 1, 0), pcells;
+  for (int c = 0; c < nc; ++c) {
+    const int rc = rank_of(c);
+    for (int i = 0; i < 22; ++i) {
+      const int d = m.cell_nse_dofs[22 * size_t(c) + i];
+      if (is_p(i)) {
+        if (d < nu || d >= nu + np) throw std::runtime_error("localize: pressure dof out of range");
+        if (pown[d - nu] < 0) pown[d - nu] = rc;
+        pptr[d - nu + 1]++;
+      } else {
+        if (d < 0 || d >= nu) throw std::runtime_error("localize: velocity dof out of range");
+        if (uown[d] < 0) uown[d] = rc;
+      }
+    }
+    for (int v = 0; v < tdpc; ++v) {
+      const int t = m.cell_T_dofs[size_t(tdpc) * c + v];
+      if (t < 0 || t >= nT) throw std::runtime_error("localize: T dof out of range");
+      if (Town[t] < 0) Town[t] = rc;
+    }
+  }
+  for (int p = 0; p < np; ++p) pptr[p + 1] += pptr[p];
+  pcells.resize(size_t(pptr[np]));
+  {
+    std::vector<int32_t> f(pptr.begin(), pptr.end() - 1);
+    for (int c = 0; c < nc; ++c)
+      for (int i = 2; i < 12; i += 3) pcells[f[m.cell_nse_dofs[22 * size_t(c) + i] - nu]++] = c;
+  }
+  std::vector<int> cstamp(nc, -1), ustamp(nu, -1), pstamp(np, -1), Tstamp(nT, -1);
+  int token = 0;
+  auto cells_of = [&](int s) {
+    const int tok = token++;
+    std::vector<int32_t> owned, ghosts, frontier, next;
+    for (int64_t c = start[s]; c < start[s + 1]; ++c) {
+      owned.push_back(int32_t(c));
+      cstamp[c] = tok;
+    }
+    frontier = owned;
+    for (int layer = 0; layer < 2; ++layer) {
+      next.clear();
+      for (int32_t c : frontier)
+        for (int i = 2; i < 12; i += 3) {
+          const int p = m.cell_nse_dofs[22 * size_t(c) + i] - nu;
+          for (int j = pptr[p]; j < pptr[p + 1]; ++j)
+            if (cstamp[pcells[j]] != tok) {
+              cstamp[pcells[j]] = tok;
+              next.push_back(pcells[j]);
+            }
+        }
+      ghosts.insert(ghosts.end(), next.begin(), next.end());
+      frontier.swap(next);
+    }
+    std::sort(ghosts.begin(), ghosts.end());
+    owned.insert(owned.end(), ghosts.begin(), ghosts.end());
+    return owned;
+  };
+  auto u_of = [&](int c, auto&& emit) {
+    for (int i = 0; i < 22; ++i)
+      if (!is_p(i)) emit(m.cell_nse_dofs[22 * size_t(c) + i]);
+  };
+  auto p_of = [&](int c, auto&& emit) {
+    for (int i = 2; i < 12; i += 3) emit(m.cell_nse_dofs[22 * size_t(c) + i] - nu);
+  };
+  auto T_of = [&](int c, auto&& emit) {
+    for (int v = 0; v < tdpc; ++v) emit(m.cell_T_dofs[size_t(tdpc) * c + v]);
+  };
+  Local2D L;
+  L.rank = rank;
+  L.world = world;
+  L.tdpc = tdpc;
+  L.cells_g = cells_of(rank);
+  L.n_cells = int(L.cells_g.size());
+  L.n_owned_cells = int(start[rank + 1] - start[rank]);
+  auto order = [&](std::vector<int32_t>& ents, const std::vector<int32_t>& own, int& no, int& ng) {
+    std::stable_partition(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; });
+    no = int(std::count_if(ents.begin(), ents.end(), [&](int32_t e) { return own[e] == rank; }));
+    ng = int(ents.size()) - no;
+  };
+  collect(L.cells_g, u_of, ustamp, token++, L.u_g);
+  collect(L.cells_g, p_of, pstamp, token++, L.p_g);
+  collect(L.cells_g, T_of, Tstamp, token++, L.T_g);
+  order(L.u_g, uown, L.nuo, L.nug);
+  order(L.p_g, pown, L.npo, L.npg);
+  order(L.T_g, Town, L.nTo, L.nTg);
+  std::vector<int32_t> ul(nu, -1), pl(np, -1), Tl(nT, -1);
+  for (size_t i = 0; i < L.u_g.size(); ++i) ul[L.u_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.p_g.size(); ++i) pl[L.p_g[i]] = int32_t(i);
+  for (size_t i = 0; i < L.T_g.size(); ++i) Tl[L.T_g[i]] = int32_t(i);
+  const int nul = L.n_u();
+  auto local_nse = [&](int d) { return d < nu ? ul[d] : (pl[d - nu] < 0 ? -1 : nul + pl[d - nu]); };
+  L.cell_dofs.resize(size_t(L.n_cells) * 22);
+  L.cell_T.resize(size_t(L.n_cells) * tdpc);
+  L.geometry.resize(size_t(L.n_cells) * 32);
+  L.diameter.resize(L.n_cells);
+  for (int lc = 0; lc < L.n_cells; ++lc) {
+    const size_t c = size_t(L.cells_g[lc]);
+    for (int i = 0; i < 22; ++i) L.cell_dofs[22 * size_t(lc) + i] = local_nse(m.cell_nse_dofs[22 * c + i]);
+    for (int v = 0; v < tdpc; ++v) L.cell_T[size_t(tdpc) * lc + v] = Tl[m.cell_T_dofs[tdpc * c + v]];
+    std::copy(m.cell_geometry + 32 * c, m.cell_geometry + 32 * c + 32, L.geometry.begin() + 32 * size_t(lc));
+    L.diameter[lc] = m.cell_diameter[c];
+  }
+  // constraint lines of the local dofs (entries must be local: node-local lines)
+  L.nse_ptr.push_back(0);
+  for (int l = 0; l < m.nse.n_lines; ++l) {
+    const int d = m.nse.line_dof[l];
+    if (d < 0 || d >= nu + np || local_nse(d) < 0) continue;
+    L.nse_line.push_back(local_nse(d));
+    L.nse_inh.push_back(m.nse.inhomogeneity[l]);
+    for (int k = m.nse.entry_ptr[l]; k < m.nse.entry_ptr[l + 1]; ++k) {
+      const int e = m.nse.entry_dof[k];
+      const int le = e >= 0 && e < nu + np ? local_nse(e) : -1;
+      if (le < 0) throw std::runtime_error("localize: constraint entry outside the local mesh");
+      L.nse_edof.push_back(le);
+      L.nse_w.push_back(m.nse.entry_w[k]);
+    }
+    L.nse_ptr.push_back(int(L.nse_edof.size()));
+  }
+  L.T_ptr.push_back(0);
+  for (int l = 0; l < m.T.n_lines; ++l) {
+    const int d = m.T.line_dof[l];
+    if (d < 0 || d >= nT || Tl[d] < 0) continue;
+    L.T_line.push_back(Tl[d]);
+    L.T_inh.push_back(m.T.inhomogeneity[l]);
+    for (int k = m.T.entry_ptr[l]; k < m.T.entry_ptr[l + 1]; ++k) {
+      const int e = m.T.entry_dof[k];
+      if (e < 0 || e >= nT || Tl[e] < 0)
+        throw std::runtime_error("localize: constraint entry outside the local mesh");
+      L.T_edof.push_back(Tl[e]);
+      L.T_w.push_back(m.T.entry_w[k]);
+    }
+    L.T_ptr.push_back(int(L.T_edof.size()));
+  }
+  // halo plans: my ghosts grouped by owner; my owned entities in other ranks' cells
+  struct Field {
+    HaloPlan* plan;
+    const std::vector<int32_t>* ents;
+    const std::vector<int32_t>* own;
+    const std::vector<int32_t>* lidx;
+    int no;
+  };
+  Field fields[3] = {{&L.hu, &L.u_g, &uown, &ul, L.nuo},
+                     {&L.hp, &L.p_g, &pown, &pl, L.npo},
+                     {&L.hT, &L.T_g, &Town, &Tl, L.nTo}};
+  std::vector<std::vector<std::vector<int32_t>>> sends(3, std::vector<std::vector<int32_t>>(world));
+  for (int s = 0; s < world; ++s) {
+    if (s == rank) continue;
+    const std::vector<int32_t> cs = cells_of(s);
+    for (int f = 0; f < 3; ++f) {
+      std::vector<int32_t> ents;
+      if (f == 0) collect(cs, u_of, ustamp, token++, ents);
+      else if (f == 1) collect(cs, p_of, pstamp, token++, ents);
+      else collect(cs, T_of, Tstamp, token++, ents);
+      for (int32_t e : ents)
+        if ((*fields[f].own)[e] == rank) sends[f][s].push_back(e);
+    }
+  }
+  for (int f = 0; f < 3; ++f) {
     const Field& F = fields[f];
     std::vector<std::vector<int32_t>> recv(world);
     for (size_t i = size_t(F.no); i < F.ents->size(); ++i) {

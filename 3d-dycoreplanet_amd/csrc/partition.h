@@ -83,6 +83,27 @@ struct FeecLocal {
 };
 FeecLocal localize_feec(const dcp_feec_mesh& m, int rank, int world);
 
+// The 2D model (Standard::BoussinesqModel<2>): the same split and two ghost
+// layers (cells sharing a vertex = a pressure dof); fields u (scalar velocity
+// dofs), p, T, each numbered owned first then ghosts, ascending global id.
+// The local NSE vector is [u_l | p_l].
+struct Local2D {
+  int rank = 0, world = 1, tdpc = 4;
+  int n_cells = 0, n_owned_cells = 0;
+  int nuo = 0, nug = 0, npo = 0, npg = 0, nTo = 0, nTg = 0;
+  std::vector<int32_t> cells_g, u_g, p_g, T_g;  // local -> global id per field
+  std::vector<int32_t> cell_dofs, cell_T;       // [n][22] (u local, n_u_l + p local), [n][tdpc]
+  std::vector<double> geometry, diameter;       // [n][16][2], [n]
+  std::vector<int> nse_line, nse_ptr, nse_edof, T_line, T_ptr, T_edof;
+  std::vector<double> nse_w, nse_inh, T_w, T_inh;
+  HaloPlan hu, hp, hT;
+  int n_u() const { return nuo + nug; }
+  int n_p() const { return npo + npg; }
+  int n_T() const { return nTo + nTg; }
+  dcp_mesh2d view() const;  // points into this object
+};
+Local2D localize_2d(const dcp_mesh2d& m, int rank, int world);
+
 // Builds rank `rank`'s local mesh of a `world`-way split of the global mesh
 // (arguments as dcp_mesh_upload). Throws std::runtime_error on bad input.
 LocalMesh localize(int n_cells, const int32_t* cell_nse_dofs, const int32_t* cell_T_dofs,

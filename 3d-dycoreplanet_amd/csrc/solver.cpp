@@ -1006,11 +1006,11 @@ void mf_apply(Ctx& c, const double* src, double* dst, bool stokes) {
 
 // A (velocity-velocity block) on a velocity vector [u_own u_ghost]
 void a_vmult(Ctx& c, const double* src, double* dst) {
+  halo_exchange(c, c.halo_v, const_cast<double*>(src));
   if (c.dim2) {
     c.m2_block(0, c.n_u, 0, c.n_u, src, dst, false);
     return;
   }
-  halo_exchange(c, c.halo_v, const_cast<double*>(src));
   if (c.matrix_free) {
     mf_apply(c, src, dst, false);
     return;
@@ -1209,12 +1209,12 @@ void velocity_vmult(Ctx& c, const double* src, double* dst) { a_vmult(c, src, ds
 
 void nse_vmult(Ctx& c, const double* src, double* dst) {
   // BlockSparseMatrix::vmult: block(0,0), then vmult_add block(0,1); block(1,0)
+  halo_exchange(c, c.halo_nse, const_cast<double*>(src));
   if (c.dim2) {
     const int n = c.n_u + c.n_p;
     c.m2_block(0, n, 0, n, src, dst, false);
     return;
   }
-  halo_exchange(c, c.halo_nse, const_cast<double*>(src));
   if (c.matrix_free) {
     mf_apply(c, src, dst, true);
     return;
@@ -1229,10 +1229,12 @@ void schur_vmult(Ctx& c, const double* src, double* dst) {
   if (c.dim2) {
     // SchurComplement::vmult (schur_complement.hpp:143-150) with the Jacobi A^-1
     const int nu = c.n_u, n = c.n_u + c.n_p;
+    halo_exchange(c, c.halo_p, const_cast<double*>(src));
     Timer* ev = schur_sample(c);
     if (ev) DCP_HIP_CHECK(hipEventRecord(ev->a, c.stream));
     c.m2_block(0, nu, nu, n, src, c.schur_tmp1.p, false);
     mul(nu, c.A_inv.p, c.schur_tmp1.p, c.schur_tmp2.p, c.stream);
+    halo_exchange(c, c.halo_v, c.schur_tmp2.p);
     c.m2_block(nu, n, 0, nu, c.schur_tmp2.p, dst, false);
     if (ev) DCP_HIP_CHECK(hipEventRecord(ev->b, c.stream));
     return;
@@ -1406,7 +1408,7 @@ State pcg(Ctx& c, int n, Seg g, const Op& A, const Op& P, double* x, const doubl
 void build_ilu(Ctx& c) {
   Ctx::Ilu& f = c.ilu;
   if (f.ptr.p) return;  // reset by every mesh upload (free_workspaces)
-  const int n = c.dim2 ? c.n_u : 3 * c.nvo;
+  const int n = c.vdim * c.nvo;  // owned velocity dofs (one GPU: all)
   std::vector<int32_t> ptr(n + 1, 0), col, pos, diag(n, -1);
   if (c.dim2) {
     // the velocity window (rows and columns < n_u) of the scalar 2D nse_matrix;
@@ -1504,11 +1506,10 @@ void build_ilu(Ctx& c) {
 
 int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414). Several GPUs
-  // (3D): each rank factors the ILU of its owned diagonal block (the
+  // (3D and 2D): each rank factors the ILU of its owned diagonal block (the
   // reference's Trilinos ILU with zero overlap, i.e. block Jacobi over the
   // ranks, so the preconditioner depends on the partition as it does there);
   // every block product refreshes its source's ghost entries first
-  if (c.comm && c.dim2) throw std::runtime_error("the 2D model runs on one GPU");
   const int nu = c.n_u, np = c.n_p, n = nu + np;
   const double dt = c.ph.dt;
   if (!c.dim2) {
@@ -1522,22 +1523,22 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   ilu_factor(iv, c.dim2 ? c.m2_val.p : c.A_val.p, f.lf_host.data(), f.lu.p, f.max_row, c.stream);
   // the blocks of nse_matrix: A, B^T (velocity rows), B (pressure rows)
   auto Ablk = [&](const double* x, double* y) {
-    if (c.dim2) return c.m2_block(0, nu, 0, nu, x, y, false);
     halo_exchange(c, c.halo_v, const_cast<double*>(x));
+    if (c.dim2) return c.m2_block(0, nu, 0, nu, x, y, false);
     spmv_bsr33(c.nvo, c.A_ptr.p, c.A_col.p, c.A_val.p, x, y, false, c.stream);
   };
   auto Btblk = [&](const double* p, double* y) {
-    if (c.dim2) return c.m2_block(0, nu, nu, n, p, y, false);
     halo_exchange(c, c.halo_p, const_cast<double*>(p));
+    if (c.dim2) return c.m2_block(0, nu, nu, n, p, y, false);
     spmv_bsr31(c.nvo, c.Bt_ptr.p, c.Bt_col.p, c.Bt_val.p, p, y, false, c.stream);
   };
   auto Bblk = [&](const double* u, double* y) {
-    if (c.dim2) return c.m2_block(nu, n, 0, nu, u, y, false);
     halo_exchange(c, c.halo_v, const_cast<double*>(u));
+    if (c.dim2) return c.m2_block(nu, n, 0, nu, u, y, false);
     spmv_bsr13(c.npo, c.B_ptr.p, c.B_col.p, c.B_val.p, u, y, false, c.stream);
   };
   // owned entries (one GPU: all of them)
-  const Seg gu = c.dim2 ? Seg::all(nu) : c.seg_v(), gp = c.dim2 ? Seg::all(np) : c.seg_p();
+  const Seg gu = c.seg_v(), gp = c.seg_p();
   ensure_pool(c.sc_v, 8, size_t(nu));
   double* const cg_u[3] = {c.sc_v[0], c.sc_v[1], c.sc_v[2]};
   double *tmp = c.sc_v[3], *t1 = c.sc_v[4], *t2 = c.sc_v[5];
@@ -1594,6 +1595,7 @@ int solve_nse_schur(Ctx& c, int* schur_iterations, int* a_solves) {
   auto distribute = [&] {
     if (c.dim2) {
       distribute_nse_2d(c, x.p);
+      halo_exchange(c, c.halo_nse, x.p);
       return;
     }
     distribute_velocity(c.n_vnodes, c.vcon.p, x.p, c.stream);

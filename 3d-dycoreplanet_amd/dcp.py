@@ -62,6 +62,7 @@ EXPORTED = [
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
     "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
+    "dcp_mesh2d_partition_info",
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
@@ -265,6 +266,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
+    lib.dcp_mesh2d_partition_info.argtypes = [C.POINTER(Mesh2DView), I, I, I, P, P, P, P, P, P]
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_renumber_cuthill_mckee.argtypes = [P]
@@ -899,6 +901,32 @@ def feec_partition_info(m, rank, world, field):
     if rc != DCP_OK:
         raise DcpError(rc, lib().dcp_last_error(None).decode())
     keys = ("n_cells", "n_owned_cells", "nwo", "nwg", "nuo", "nug", "nTo", "nTg", "n_peers",
+            "n_send", "n_recv")
+    out = {k: int(v) for k, v in zip(keys, info)}
+    out["send"] = {int(p): sg[sp[i]:sp[i + 1]].copy() for i, p in enumerate(peers[:npeer])}
+    out["recv"] = {int(p): rg[rp[i]:rp[i + 1]].copy() for i, p in enumerate(peers[:npeer])}
+    return out
+
+
+def mesh2d_partition_info(m, rank, world, field):
+    """Host-only summary of rank's 2D partition (dcp_mesh2d_partition_info) and
+    the halo lists (global ids) per peer of `field` ("u", "p", "T")."""
+    fid = {"u": 0, "p": 1, "T": 2}[field]
+    view = m.as_struct()
+    info = np.zeros(11, np.int64)
+    rc = lib().dcp_mesh2d_partition_info(C.byref(view), rank, world, fid, _ptr(info), None, None,
+                                         None, None, None)
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    npeer, ns, nr = int(info[8]), int(info[9]), int(info[10])
+    peers = np.zeros(max(npeer, 1), np.int32)
+    sp, rp = np.zeros(npeer + 1, np.int32), np.zeros(npeer + 1, np.int32)
+    sg, rg = np.zeros(max(ns, 1), np.int64), np.zeros(max(nr, 1), np.int64)
+    rc = lib().dcp_mesh2d_partition_info(C.byref(view), rank, world, fid, _ptr(info), _ptr(peers),
+                                         _ptr(sp), _ptr(sg), _ptr(rp), _ptr(rg))
+    if rc != DCP_OK:
+        raise DcpError(rc, lib().dcp_last_error(None).decode())
+    keys = ("n_cells", "n_owned_cells", "nuo", "nug", "npo", "npg", "nTo", "nTg", "n_peers",
             "n_send", "n_recv")
     out = {k: int(v) for k, v in zip(keys, info)}
     out["send"] = {int(p): sg[sp[i]:sp[i + 1]].copy() for i, p in enumerate(peers[:npeer])}

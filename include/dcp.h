@@ -570,7 +570,8 @@ int dcp_feec_matrix_export(dcp_ctx* ctx, int which, int64_t* nnz, int32_t* rowpt
  * ([n][16][2], 4 x 4 Gauss-Lobatto, x fastest). The NSE constraint lines must
  * be homogeneous with at most one entry on a dof of the same cells (the
  * no-slip / no-normal-flux lines of the shell are), the temperature lines
- * Dirichlet. One GPU. After the upload the hot-path calls above (assemble,
+ * Dirichlet. Several GPUs: every rank passes the global mesh and keeps its
+ * cells + two ghost layers (as dcp_mesh_upload). After the upload the hot-path calls above (assemble,
  * preconditioner, dcp_solve_nse / dcp_solve_nse_schur, temperature, CFL,
  * state, vmults, exports; dcp_cell_nse_system returns [n][22][22] / [n][22])
  * act on the 2D model. */
@@ -586,6 +587,15 @@ typedef struct {
 int dcp_mesh2d_upload(dcp_ctx* ctx, const dcp_mesh2d* m);
 /* Host-only dry run of dcp_mesh2d_upload's validation, patterns and colouring. */
 int dcp_mesh2d_check(const dcp_mesh2d* m, int* n_colors);
+/* Host-only summary of rank's 2D partition (no GPU; several GPUs take the
+ * global mesh in dcp_mesh2d_upload and keep their cells + two ghost layers):
+ * info[11] = {n_cells, n_owned_cells, owned / ghost velocity dofs, owned /
+ * ghost pressure, owned / ghost temperature, peers, send, recv} and the halo
+ * lists (global ids) of field 0 (velocity), 1 (pressure), 2 (temperature);
+ * the local mesh is run through dcp_mesh2d_check's validation as well. */
+int dcp_mesh2d_partition_info(const dcp_mesh2d* m, int rank, int world, int field, int64_t* info,
+                              int32_t* peers, int32_t* send_ptr, int64_t* send_gid,
+                              int32_t* recv_ptr, int64_t* recv_gid);
 
 /* Host setup helpers (mesh generator, .prm) ----------------------------- */
 typedef struct dcp_host_mesh dcp_host_mesh;

@@ -272,7 +272,10 @@ def test_run_feec_cube_prm_against_the_oracle():
     and leaves nse_solution as it is (FEEC.tpp:1480-1500), and the temperature
     (periodic in x, y: identity lines folded at upload, FEEC.tpp:435-463)
     diffuses and advects with the given RT velocity. Three dcp_run steps
-    against the oracle's assemble / CG step by step: equal CG counts,
+    against the oracle's assemble / CG step by step: CG counts within one
+    (the second step's CG ends at its 1e-12 threshold: a 1e-15 perturbation of
+    the oracle's own old temperature moves it between 25 and 26 steps,
+    test_feec.py::test_cube_temperature_cg_count_is_rounding_sensitive),
     temperature at 1e-10, periodic images equal to their partners."""
     import oracle_py
     rp = dcp.load_prm(CUBE_PRM)
@@ -299,7 +302,7 @@ def test_run_feec_cube_prm_against_the_oracle():
         orc.assemble_nse_system(x0, T)
         orc.assemble_temperature(T, x0)
         rcT, T, itT = orc.solve_temperature(T)
-        assert rcT == 0 and itT == steps[n].T_cg
+        assert rcT == 0 and abs(itT - steps[n].T_cg) <= 1
     assert np.linalg.norm(T_run - T) <= 1e-10 * np.linalg.norm(T)
     cs = m.T_constraints
     for l, d in enumerate(cs.line_dof):

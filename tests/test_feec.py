@@ -230,6 +230,29 @@ def test_oracle_fixed_inner_count_is_not_rounding_sensitive():
     assert np.linalg.norm(x2 - x) < 1e-12 * np.linalg.norm(x)
 
 
+def test_cube_temperature_cg_count_is_rounding_sensitive():
+    """Documents the CG-count bar of test_driver.py's cube run: with the cube
+    prm's physics and a random RT velocity, the second step's temperature CG
+    (tol 1e-12 |rhs|) ends at its threshold, so a 1e-15 relative perturbation
+    of the old temperature moves the oracle's own count by one."""
+    rp = dcp.load_prm(CUBE_PRM)
+    m = dcp.HostMesh(cuboid=True, refine=2, feec=True, length=rp.length)
+    f = m.feec
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(f.n)
+    x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
+    x0[f.fixed.astype(bool)] = 0
+    orc = oracle_py.FeecModel(dcp.physics_from_params(rp), m)
+    orc.assemble_temperature(m.T0, x0)
+    _, T1, _ = orc.solve_temperature(m.T0.copy())
+    counts = set()
+    for s in range(6):
+        Tp = T1 * (1 + (1e-15 if s else 0.0) * np.random.default_rng(s).uniform(-1, 1, T1.size))
+        orc.assemble_temperature(Tp, x0)
+        counts.add(orc.solve_temperature(Tp)[2])
+    assert len(counts) == 2 and max(counts) - min(counts) == 1
+
+
 # ------------------------------------------------------------------ GPU parity
 
 def csr(rp, cols, vals, n):

@@ -61,12 +61,12 @@ def test_partition_halo_consistency_gloo(refine, cuboid):
     assert res == {0: True, 1: True}
 
 
-def _gloo_feec_worker(rank, world, port, refine, q):
+def _gloo_feec_worker(rank, world, port, refine, q, cuboid=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        m = dcp.HostMesh(refine=refine, feec=True)
+        m = dcp.HostMesh(refine=refine, feec=True, cuboid=cuboid)
         ok = True
         mine = {}
         for fld in ("w", "u", "p", "T"):
@@ -89,14 +89,15 @@ def _gloo_feec_worker(rank, world, port, refine, q):
         dist.destroy_process_group()
 
 
-def test_feec_partition_halo_consistency_gloo():
-    """FEEC (config 4) partition across two gloo processes: every halo send
-    list of edges, faces, cells and vertices matches the peer's receive list;
-    ownership covers every dof once."""
+@pytest.mark.parametrize("cuboid", [False, True])
+def test_feec_partition_halo_consistency_gloo(cuboid):
+    """FEEC (config 4; cuboid: the cube prm's periodic FEEC) partition across
+    two gloo processes: every halo send list of edges, faces, cells and
+    vertices matches the peer's receive list; ownership covers every dof once."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_feec_worker, args=(r, world, 29631, 2, q))
+    procs = [ctx.Process(target=_gloo_feec_worker, args=(r, world, 29631 + cuboid, 2, q, cuboid))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -263,19 +264,27 @@ def _feec_time_step(ctx, m, x0, T0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_group_feec_time_step_matches_single_gpu(world):
+@pytest.mark.parametrize("world,geometry", [(2, "shell"), (3, "shell"), (2, "cube"), (3, "cube")])
+def test_group_feec_time_step_matches_single_gpu(world, geometry):
     """Config 4 (FEEC, SURVEY §8e: 2 GPUs with a ghost-DoF halo) as an
     in-process group: same outer GMRES count as one GPU; iterates at 1e-6
-    (the FEEC chain's rounding sensitivity, tests/test_feec.py)."""
-    m = dcp.HostMesh(refine=2, feec=True)
+    (the FEEC chain's rounding sensitivity, tests/test_feec.py). cube: the cube
+    prm's periodic FEEC (edges / faces identified across x / y, ghost layers
+    across them, the temperature's periodic images folded on every rank)."""
+    if geometry == "cube":
+        rp = dcp.load_prm(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                       "configs", "aqua_planet_cube_test_3d.prm"))
+        m = dcp.HostMesh(cuboid=True, refine=2, feec=True, length=rp.length)
+        ph = dcp.physics_from_params(rp)
+    else:
+        m = dcp.HostMesh(refine=2, feec=True)
+        ph = dcp.classic_physics()
     f = m.feec
-    ph = dcp.classic_physics()
     rng = np.random.default_rng(11)
     x0 = np.zeros(f.n)
     x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
     x0[f.fixed.astype(bool)] = 0
-    T0 = m.T0.copy()
+    T0 = periodic_state(m, m.T0.copy(), m.T_constraints)
     ref_ctx = dcp.Context()
     ref_ctx.set_physics(ph)
     ref_ctx.upload_feec_mesh(m)
