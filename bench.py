@@ -779,7 +779,18 @@ def main():
         "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
         "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None,
-        "traffic": pmc_asm_traffic(args.refine) if world == 1 else asm_bytes}
+        # HBM bytes per assembly, 2 x FETCH_SIZE + WRITE_SIZE (the gfx950
+        # correction, as for every other roofline here); the counts as taken
+        # in traffic_detail
+        "traffic": None, "traffic_detail": None}
+    if world == 1:
+        t_asm = pmc_asm_traffic(args.refine)
+        if t_asm:
+            out["roofline_assembly"]["traffic"] = t_asm["two_fetch_plus_write"]
+            out["roofline_assembly"]["traffic_detail"] = t_asm
+            out["roofline_assembly"]["traffic_over_output"] = t_asm["two_fetch_plus_write"] / asm_bytes
+    else:
+        out["roofline_assembly"]["traffic"] = asm_bytes
     if args.schur == "explicit" and world == 1:
         out["roofline_chain"] = chain_roofline(args.refine, m.n_p, args.gram_schmidt)
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
