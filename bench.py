@@ -56,7 +56,7 @@ CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
                (5, "sstep"): "profiles/r04i_inner_r5_structured_kernel_stats.csv"}
 # the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
 # launches per assembly (the rhs kernel once per colour class)
-PMC_ASM = {5: ("profiles/r04s_pmc_asm_r5.json",
+PMC_ASM = {5: ("profiles/r05/r05i_pmc_asm_r5.json",
                {"k_bt_tasks": 1, "k_mf_pencil": 1, "k_mf_gather": 1, "k_nse_rhs_halfwave": 1,
                 "k_con_gather": 1})}  # (k_bt_coltab runs once at upload)
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather)
