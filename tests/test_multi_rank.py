@@ -264,7 +264,8 @@ def _feec_time_step(ctx, m, x0, T0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,geometry", [(2, "shell"), (3, "shell"), (2, "cube"), (3, "cube")])
+@pytest.mark.parametrize("world,geometry", [(2, "shell"), (3, "shell"), (2, "cube"), (3, "cube"),
+                                            (8, "cube")])
 def test_group_feec_time_step_matches_single_gpu(world, geometry):
     """Config 4 (FEEC, SURVEY §8e: 2 GPUs with a ghost-DoF halo) as an
     in-process group: same outer GMRES count as one GPU; iterates at 1e-6
@@ -690,9 +691,10 @@ def test_group_matrix_powers_bitwise(world, refine, fixed_inner):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,gs,fixed_inner", [(2, "modified", 0), (3, "sstep", 0),
-                                                  (4, "sstep", 24)])
-def test_group_cube_time_step_matches_single_gpu(world, gs, fixed_inner):
+@pytest.mark.parametrize("world,gs,fixed_inner,refine", [(2, "modified", 0, 2), (3, "sstep", 0, 2),
+                                                         (4, "sstep", 24, 2),
+                                                         (8, "sstep", 24, 3)])
+def test_group_cube_time_step_matches_single_gpu(world, gs, fixed_inner, refine):
     """BASELINE C2's periodic cube (classic Q2/Q1, Coriolis and vertical
     gravity on) as an in-process group: the x / y periodic identities cross
     rank boundaries (ghost layers grow across them, every local image's
@@ -701,7 +703,7 @@ def test_group_cube_time_step_matches_single_gpu(world, gs, fixed_inner):
     rp = dcp.load_prm(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                    "configs", "aqua_planet_cube_test_3d.prm"))
     ph = dcp.physics_from_params(rp)
-    m = dcp.HostMesh(cuboid=True, refine=2, length=rp.length)
+    m = dcp.HostMesh(cuboid=True, refine=refine, length=rp.length)
     rng = np.random.default_rng(17)
     u = np.zeros(m.n_u + m.n_p)
     u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)

@@ -135,7 +135,7 @@ def merged(results, key, like):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_group_2d_block_preconditioned_step_matches_single_gpu(world):
     m = make_mesh(2, cm=False)
     ph = physics()
@@ -184,7 +184,7 @@ def test_group_2d_block_preconditioned_step_matches_single_gpu(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_group_2d_schur_solver_block_jacobi_ilu_matches_oracle(world):
     m = make_mesh(2, cm=True)
     ph = physics()

@@ -57,7 +57,8 @@ def test_velocity_owner_rule_matches_the_partition(name, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,world,k", [("cube", 2, 8), ("cube", 3, 8), ("shell", 2, 40)])
+@pytest.mark.parametrize("name,world,k", [("cube", 2, 8), ("cube", 3, 8), ("shell", 2, 40),
+                                          ("shell", 8, 40)])
 def test_group_schur_solver_block_jacobi_ilu_matches_oracle(name, world, k):
     m, ph = case(name)
     rng = np.random.default_rng(23)
