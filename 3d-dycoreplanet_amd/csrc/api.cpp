@@ -2999,6 +2999,41 @@ int dcp_velocity_vmult(dcp_ctx* ctx, const double* src, double* dst) {
   });
 }
 
+int dcp_time_operator(dcp_ctx* ctx, int which, int reps, int nvec, const double* src,
+                      double* dst, double* ms_per_apply) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    Ctx& c = *ctx;
+    require(src && dst && ms_per_apply && reps > 0 && nvec > 0 && which >= 0 && which <= 2,
+            DCP_ERR_INVALID, "bad arguments");
+    require(c.nse_assembled && !c.feec, DCP_ERR_STATE, "nse_matrix not assembled");
+    require(which != 2 || c.precond_built, DCP_ERR_STATE, "build_nse_preconditioner first");
+    const size_t len = which == 0 ? size_t(c.n_u) + c.n_p : which == 1 ? size_t(c.n_u) : size_t(c.n_p);
+    auto apply = [&](int k) {
+      const double* s = src + len * size_t(k % nvec);
+      double* d = dst + len * size_t(k % nvec);
+      if (which == 0) nse_vmult(c, s, d);
+      else if (which == 1) velocity_vmult(c, s, d);
+      else schur_vmult(c, s, d);
+    };
+    apply(0);  // the first apply may build tables (B^T transpose map, S layout)
+    hipEvent_t a, b;
+    DCP_HIP_CHECK(hipEventCreate(&a));
+    DCP_HIP_CHECK(hipEventCreate(&b));
+    DCP_HIP_CHECK(hipEventRecord(a, c.stream));
+    for (int k = 0; k < reps; ++k) apply(k + 1);
+    DCP_HIP_CHECK(hipEventRecord(b, c.stream));
+    DCP_HIP_CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    DCP_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    check_mf_err(c);
+    *ms_per_apply = double(ms) / reps;
+    return DCP_OK;
+  });
+}
+
 int dcp_schur_vmult(dcp_ctx* ctx, const double* src, double* dst) {
   return guarded(ctx, [&] {
     need_ready(*ctx);

@@ -62,7 +62,7 @@ EXPORTED = [
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
     "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
-    "dcp_mesh2d_partition_info",
+    "dcp_mesh2d_partition_info", "dcp_time_operator",
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
     "dcp_mesh2d_upload", "dcp_mesh2d_check", "dcp_host_mesh2d_create", "dcp_host_mesh2d_view_get",
@@ -267,6 +267,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
     lib.dcp_mesh2d_partition_info.argtypes = [C.POINTER(Mesh2DView), I, I, I, P, P, P, P, P, P]
+    lib.dcp_time_operator.argtypes = [P, I, I, I, C.c_void_p, C.c_void_p, D]
     lib.dcp_host_mesh_create.argtypes = [I, I, C.c_double, C.c_double, C.c_double, I, I, I]
     lib.dcp_host_mesh_create.restype = P
     lib.dcp_host_mesh_renumber_cuthill_mckee.argtypes = [P]
@@ -1363,6 +1364,16 @@ class Context:
             rc = fn(C.c_void_p(d_src.ptr), C.c_void_p(d_dst.ptr))
             out = d_dst.download() if rc in (DCP_OK, DCP_NOT_CONVERGED) else None
         return rc, out
+
+    def time_operator(self, which, reps, d_src, d_dst, nvec=1):
+        """dcp_time_operator: ms per apply of `reps` back-to-back applies on
+        device buffers (which: "nse", "velocity", "schur"), one HIP event pair;
+        apply k uses vector k mod nvec of d_src / d_dst."""
+        ms = C.c_double(0.0)
+        w = {"nse": 0, "velocity": 1, "schur": 2}[which]
+        self._check(lib().dcp_time_operator(self._h, w, int(reps), int(nvec), C.c_void_p(d_src),
+                                            C.c_void_p(d_dst), C.byref(ms)))
+        return ms.value
 
     def nse_vmult(self, src):
         n = self.mesh.n_u + self.mesh.n_p

@@ -398,6 +398,16 @@ int dcp_nse_vmult(dcp_ctx* ctx, const double* d_src, double* d_dst);          /*
  * GMRES (block_schur_preconditioner.hpp:59-67). */
 int dcp_velocity_vmult(dcp_ctx* ctx, const double* d_src_u, double* d_dst_u);
 int dcp_schur_vmult(dcp_ctx* ctx, const double* d_src_p, double* d_dst_p);    /* schur_complement.hpp:143-150 */
+/* Diagnostic (no reference counterpart): `reps` back-to-back applies of an
+ * operator on the context's stream between one pair of HIP events, device
+ * vectors only; *ms_per_apply = elapsed / reps. which: 0 nse_matrix (the
+ * matrix-free [A B^T; B 0] when DCP_OPT_MATRIX_FREE), 1 its velocity block,
+ * 2 the Schur complement. Apply k reads vector k mod nvec of d_src and writes
+ * the same of d_dst (nvec consecutive vectors of the operator's length each):
+ * nvec vectors larger together than the 256 MB Infinity Cache keep every
+ * source cold, as the Krylov vectors of a solve are. */
+int dcp_time_operator(dcp_ctx* ctx, int which, int reps, int nvec, const double* d_src,
+                      double* d_dst, double* ms_per_apply);
 /* BlockSchurPreconditioner::vmult (block_schur_preconditioner.hpp:42-70).
  * As there, d_dst's pressure block is the inner Schur GMRES's initial guess
  * (and its velocity block the A-GMRES's when do_solve_A): pass it zeroed, or
