@@ -6,6 +6,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "lanes.h"
+
 namespace dcp {
 
 typedef unsigned int mgs_u4 __attribute__((ext_vector_type(4)));
@@ -91,9 +93,7 @@ __device__ inline double granule_coef(const double* gran, int nb, unsigned long 
   double v[4] = {l < nb ? granule_value(q0) : 0.0, l + 64 < nb ? granule_value(q1) : 0.0,
                  l + 128 < nb ? granule_value(q2) : 0.0, l + 192 < nb ? granule_value(q3) : 0.0};
 #pragma unroll
-  for (int w = 0; w < 4; ++w)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[w] += __shfl_xor(v[w], off, 64);
+  for (int w = 0; w < 4; ++w) v[w] = wave_allsum(v[w]);
   return v[0] + v[1] + v[2] + v[3];
 }
 

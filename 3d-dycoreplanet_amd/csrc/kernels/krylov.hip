@@ -57,9 +57,7 @@ __device__ inline double block_sums(double (&s)[K], int d, double* sm) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     if (j < d) {
-      double v = s[j];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      const double v = wave_allsum(s[j]);
       if (l == 0) sm[w * K + j] = v;
     }
   }
@@ -292,48 +290,52 @@ constexpr int kChainWaves = kChainThreads / 64;
 constexpr int kChainEntries = 2;   // vector entries per thread (registers: 2 x d basis entries)
 constexpr int kCgsRes = 2 * kGmMaxDim * 256;  // result granules after the partial area
 
-// Reduce-scatter of the K products v[j] * x over the 64 lanes of a wave:
-// log2 K halving exchanges (the first one forms the products, so only K / 2
-// accumulators are live next to v) then full butterflies over the remaining
-// lane bits; lane l ends with the wave sum of value l >> (6 - log2 K).
-// Fixed tree, deterministic.
-// The products of one thread are v[0][j] x[0] + v[1][j] x[1] (its two entries).
+template <int C, int O>
+__device__ inline void rs_step(double* s, int l) {
+  // C live accumulators -> C / 2: lanes with bit O clear keep [0, C/2), the
+  // others [C/2, C)
+  if constexpr (O >= 16) {
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) {
+      double a = s[i], b = s[i + C / 2];
+      xch_swap<O>(a, b);
+      s[i] = a + b;
+    }
+  } else {
+    const bool up = (l & O) != 0;
+#pragma unroll
+    for (int i = 0; i < C / 2; ++i) {
+      const double send = up ? s[i] : s[i + C / 2];
+      const double keep = up ? s[i + C / 2] : s[i];
+      s[i] = keep + xch_xor<O>(send);
+    }
+  }
+}
+template <int C, int O>
+__device__ inline void rs_steps(double* s, int l) {
+  if constexpr (C > 1) {
+    rs_step<C, O>(s, l);
+    rs_steps<C / 2, O / 2>(s, l);
+  }
+}
 template <int K>
 __device__ inline double wave_reduce_scatter(const double (&v)[kChainEntries][K],
                                              const double (&x)[kChainEntries]) {
   const int l = threadIdx.x & 63;
   if constexpr (K == 1) {
-    double r = v[0][0] * x[0] + v[1][0] * x[1];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-    return r;
+    return butterfly_from<32>(v[0][0] * x[0] + v[1][0] * x[1]);
   } else {
     double s[K / 2];
-    {
-      const bool up = (l & 32) != 0;
 #pragma unroll
-      for (int i = 0; i < K / 2; ++i) {
-        const double lo = v[0][i] * x[0] + v[1][i] * x[1];
-        const double hi = v[0][i + K / 2] * x[0] + v[1][i + K / 2] * x[1];
-        const double send = up ? lo : hi;
-        const double keep = up ? hi : lo;
-        s[i] = keep + __shfl_xor(send, 32, 64);
-      }
+    for (int i = 0; i < K / 2; ++i) {
+      double lo = v[0][i] * x[0] + v[1][i] * x[1];
+      double hi = v[0][i + K / 2] * x[0] + v[1][i + K / 2] * x[1];
+      xch_swap<32>(lo, hi);
+      s[i] = lo + hi;
     }
-    int o = 16;
-#pragma unroll
-    for (int c = K / 2; c > 1; c >>= 1, o >>= 1) {
-      const bool up = (l & o) != 0;
-#pragma unroll
-      for (int i = 0; i < c / 2; ++i) {
-        const double send = up ? s[i] : s[i + c / 2];
-        const double keep = up ? s[i + c / 2] : s[i];
-        s[i] = keep + __shfl_xor(send, o, 64);
-      }
-    }
-    double r = s[0];
-    for (; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-    return r;
+    // K / 2 live at lane bit 16, down to one value, then butterflies below
+    rs_steps<K / 2, 16>(s, l);
+    return butterfly_from<32 / K>(s[0]);  // the lane bits below the halving steps
   }
 }
 template <int K>
@@ -341,18 +343,29 @@ constexpr int log2i() { return K <= 1 ? 0 : 1 + log2i<K / 2>(); }
 
 // d <= K block sums of v[j] * x over the 16 waves (wave reduce-scatter, then
 // the wave sums in wave order): thread j < d returns sum j. sm: [kChainWaves][K].
+// (in two halves, chain_wave_sums / chain_sum_waves around the caller's
+// barrier, so several reductions share one)
 template <int K>
-__device__ inline double chain_block_sums(const double (&v)[kChainEntries][K],
-                                          const double (&x)[kChainEntries], int d, double* sm) {
+__device__ inline void chain_wave_sums(const double (&v)[kChainEntries][K],
+                                       const double (&x)[kChainEntries], double* sm) {
   const double r = wave_reduce_scatter<K>(v, x);
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int sh = 6 - log2i<K>();
   if ((l & ((1 << sh) - 1)) == 0) sm[w * K + (l >> sh)] = r;
-  __syncthreads();
+}
+template <int K>
+__device__ inline double chain_sum_waves(int d, const double* sm) {
   double t = 0.0;
   if (int(threadIdx.x) < d)
     for (int i = 0; i < kChainWaves; ++i) t += sm[i * K + threadIdx.x];
   return t;
+}
+template <int K>
+__device__ inline double chain_block_sums(const double (&v)[kChainEntries][K],
+                                          const double (&x)[kChainEntries], int d, double* sm) {
+  chain_wave_sums<K>(v, x, sm);
+  __syncthreads();
+  return chain_sum_waves<K>(d, sm);
 }
 
 template <int KL>
@@ -608,32 +621,60 @@ void cgs2_chain_step(Seg g, double* w, const ChainVecs& V, int d, GmresDev* st, 
 //   2. C2 = Q^T W and G = W^T W, W -= Q C2, G' = G - C2^T C2      (reduction 2)
 //   3. R = chol(G'), q_{k+1..k+s} = W R^-1 (block Gram-Schmidt twice, then
 //      Cholesky QR; no further reduction)
-// and workgroup 0 turns the change of basis into the s new Hessenberg columns
+// and one workgroup (an idle one when the grid has one) turns the change of
+// basis into the s new Hessenberg columns
 // k..k+s-1 (A [w_0..w_{s-1}] = [w_0..w_s] B, B = theta on the diagonal, sigma
 // below it; H_new = (Rhat B - H_old T_top) U^-1) and runs SolverGMRES's Givens
 // step and SolverControl check column by column, so the iteration count and
 // the stopping column are those of the one-vector-per-step Arnoldi process.
 // Two reductions per s steps instead of two per step; the same registers /
 // granule hand-off scheme as k_cgs2_chain (nb resident 512-thread workgroups,
-// two entries per thread).
+// two entries per thread). The wave reductions run on lane swaps / DPP
+// (lanes.h), the four (eight) block sums of a pass share one barrier, and the
+// Gram corrections run one thread per entry: the same arithmetic in the same
+// order as before, bit for bit.
 namespace {
 
 constexpr int kSsRes = 2 * 128 * 256;  // result granules after the partial area
 
+// DCP_SS_PROBE bit 32 (timing probe): thread 0 of the s-step block's
+// Hessenberg workgroup stamps the wall clock (100 MHz) at the phase boundaries
+// and prints every 64th launch
+#ifndef DCP_SS_PROBE
+#define DCP_SS_PROBE 0
+#endif
+#if DCP_SS_PROBE & 32
+#define SS_STAMP(i) \
+  if (ss_ts && threadIdx.x == 0) ss_ts[i] = wall_clock64()
+#else
+#define SS_STAMP(i)
+#endif
+
 
 // G' = G - C2^T C2 (G: pass-2 Gram sums after C2's d * S coefficients at
-// c2[ncol1..]) and R = chol(G') upper triangular; false if G' is not
-// positive definite (the block lost rank)
-__device__ bool sstep_chol(const double* c2, int d, int ncol1, double (*Rm)[kSStep]) {
+// c2[ncol1..]), upper-triangle entry p = (i, l >= i) in row order, one thread
+// per entry
+__device__ inline double sstep_gram_entry(const double* c2, int d, int ncol1, int p) {
+  constexpr int S = kSStep;
+  int i = 0, l = p;
+  while (l >= S - i) {
+    l -= S - i;
+    ++i;
+  }
+  l += i;
+  double gv = c2[ncol1 + p];
+  for (int j = 0; j < d; ++j) gv -= c2[i * d + j] * c2[l * d + j];
+  return gv;
+}
+
+// R = chol(G') upper triangular from the packed entries of sstep_gram_entry;
+// false if G' is not positive definite (the block lost rank)
+__device__ bool sstep_chol(const double* Gp, double (*Rm)[kSStep]) {
   constexpr int S = kSStep;
   double G[S][S];
   int p = 0;
   for (int i = 0; i < S; ++i)
-    for (int l = i; l < S; ++l) {
-      double gv = c2[ncol1 + p++];
-      for (int j = 0; j < d; ++j) gv -= c2[i * d + j] * c2[l * d + j];
-      G[i][l] = G[l][i] = gv;
-    }
+    for (int l = i; l < S; ++l, ++p) G[i][l] = G[l][i] = Gp[p];
   bool ok = true;
   for (int i = 0; i < S; ++i) {
     double dd = G[i][i];
@@ -653,35 +694,65 @@ __device__ bool sstep_chol(const double* c2, int d, int ncol1, double (*Rm)[kSSt
   return ok;
 }
 
+// G' entries (threads < nG) and R (thread 0) into the workgroup's LDS; every
+// thread of the workgroup calls it, ends with a barrier
+__device__ inline void sstep_factor(const double* c2, int d, int ncol1, double* Gp,
+                                    double (*Rm)[kSStep], int* bad) {
+  constexpr int nG = kSStep * (kSStep + 1) / 2;
+  if (threadIdx.x < nG) Gp[threadIdx.x] = sstep_gram_entry(c2, d, ncol1, threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) *bad = !sstep_chol(Gp, Rm);
+  __syncthreads();
+}
+
+// The Hessenberg state workgroup 0 reads (old raw columns, rotations, gamma_k,
+// step count, tolerance), staged in LDS by sstep_hess_stage at the start of the
+// launch so the global-memory latency overlaps the block's reductions (only
+// workgroup 0 of the launch writes these fields, at its very end)
+struct SsHess {
+  double Hs[kGmMaxDim + 1][kGmMaxDim];
+  double cs[kGmMaxDim], sn[kGmMaxDim], gam[kGmMaxDim + 1];
+  double tol;
+  int acc0, max_steps;
+};
+__device__ inline void sstep_hess_stage(SsHess& h, const GmresDev* st, int k) {
+  const int d = k + 1, t = threadIdx.x, nt = blockDim.x;
+  for (int e = t; e < d * k; e += nt) h.Hs[e / k][e % k] = st->Hr[e / k][e % k];
+  for (int i = t; i < k; i += nt) {
+    h.cs[i] = st->ci[i];
+    h.sn[i] = st->si[i];
+  }
+  if (t == 0) {
+    h.gam[k] = st->gamma[k];
+    h.acc0 = st->accumulated;
+    h.tol = st->tol;
+    h.max_steps = st->max_steps;
+  }
+}
+
 // Hessenberg columns k..k+s-1 from the block's change of basis (c1 + c2 the
 // coefficients on q_0..q_k, Rm the Cholesky factor) into Hr, then their
 // Givens steps / checks. Called by every thread of one workgroup: the old
-// columns, rotations and gamma are staged in LDS; X (old columns weighted by
+// columns, rotations and gamma are staged in LDS (SsHess, staged and synchronised by the caller); X (old columns weighted by
 // the change of basis) one thread per entry, the triangular solve
 // H_new U = X one thread per row, the k earlier rotations one thread per new
 // column, and one thread the block's own rotations and checks column by
 // column (a column after the converged one is never used).
-__device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const double* c1,
-                                 const double* c2, const double (*Rm)[kSStep]) {
+__device__ void sstep_hessenberg(GmresDev* st, SsHess& h, const SStepArgs& a, int k,
+                                 const double* c1, const double* c2, const double (*Rm)[kSStep],
+                                 long long* ss_ts = nullptr) {
   constexpr int S = kSStep;
-  __shared__ double Hs[kGmMaxDim + 1][kGmMaxDim];
   __shared__ double Hn[kGmMaxDim + 1][S];
-  __shared__ double cs[kGmMaxDim], sn[kGmMaxDim], gam[kGmMaxDim + 1];
   __shared__ double Hrot[kGmMaxDim + 1][S];
-  __shared__ int last_col, acc0;
+  __shared__ int last_col;
+  auto& Hs = h.Hs;
+  double* cs = h.cs;
+  double* sn = h.sn;
+  double* gam = h.gam;
   const int d = k + 1;
   const int rows = k + S + 1;
   const int t = threadIdx.x, nt = blockDim.x;
-  for (int e = t; e < d * k; e += nt) Hs[e / k][e % k] = st->Hr[e / k][e % k];
-  for (int i = t; i < k; i += nt) {
-    cs[i] = st->ci[i];
-    sn[i] = st->si[i];
-  }
-  if (t == 0) {
-    gam[k] = st->gamma[k];
-    acc0 = st->accumulated;
-  }
-  __syncthreads();
+  SS_STAMP(8);
   auto rhat = [&](int r, int c) -> double {  // Rhat (rows x (S+1)): [e_k | [C; R]]
     if (c == 0) return r == k ? 1.0 : 0.0;
     if (r <= k) return c1[(c - 1) * d + r] + c2[(c - 1) * d + r];
@@ -698,6 +769,7 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     Xs[r][c] = x;
   }
   __syncthreads();
+  SS_STAMP(9);
   // H_new U = X with U[l][c] = Rhat[k + l][c] (upper triangular), row by row
   if (t < rows) {
     const int r = t;
@@ -711,6 +783,7 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     }
   }
   __syncthreads();
+  SS_STAMP(10);
   // the k rotations of the earlier columns, one thread per new column
   if (t < S) {
     const int c = t;
@@ -724,10 +797,11 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     hk[c] = hi;
   }
   __syncthreads();
+  SS_STAMP(11);
   if (t == 0) {
-    int acc = acc0;
-    const double tol = st->tol;
-    const int max_steps = st->max_steps;
+    int acc = h.acc0;
+    const double tol = h.tol;
+    const int max_steps = h.max_steps;
     last_col = S - 1;
     for (int c = 0; c < S; ++c) {
       const int kk = k + c;
@@ -761,6 +835,7 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     }
   }
   __syncthreads();
+  SS_STAMP(12);
   const int nc = last_col + 1;
   // write back: raw and rotated columns, rotations, gamma
   for (int e = t; e < rows * nc; e += nt) {
@@ -773,6 +848,18 @@ __device__ void sstep_hessenberg(GmresDev* st, const SStepArgs& a, int k, const 
     st->si[k + c] = sn[k + c];
   }
   for (int i = t; i <= nc; i += nt) st->gamma[k + i] = gam[k + i];
+  SS_STAMP(13);
+#if DCP_SS_PROBE & 32
+  if (t == 0 && ss_ts) {
+    const unsigned ph = unsigned(ss_ts[15]) & 63;
+    if (ph == 0)
+      printf("ssprobe k=%d %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", k,
+             ss_ts[1] - ss_ts[0], ss_ts[2] - ss_ts[1], ss_ts[3] - ss_ts[2], ss_ts[4] - ss_ts[3],
+             ss_ts[5] - ss_ts[4], ss_ts[6] - ss_ts[5], ss_ts[7] - ss_ts[6], ss_ts[8] - ss_ts[7],
+             ss_ts[9] - ss_ts[8], ss_ts[10] - ss_ts[9], ss_ts[11] - ss_ts[10],
+             ss_ts[12] - ss_ts[11], ss_ts[13] - ss_ts[12]);
+  }
+#endif
 }
 
 // DCP_SS_NT (timing variant): the block's basis (1) and basis + W (2) loads
@@ -790,7 +877,19 @@ __device__ inline double ss_ldw(const double* p) {
   if (DCP_SS_NT >= 2) return __builtin_nontemporal_load(p);
   return *p;
 }
-template <int KL>
+typedef double ss_d2 __attribute__((ext_vector_type(2)));
+__device__ inline ss_d2 ss_ldv2(const double* p) {
+  if (DCP_SS_NT >= 1) return __builtin_nontemporal_load(reinterpret_cast<const ss_d2*>(p));
+  return *reinterpret_cast<const ss_d2*>(p);
+}
+__device__ inline ss_d2 ss_ldw2(const double* p) {
+  if (DCP_SS_NT >= 2) return __builtin_nontemporal_load(reinterpret_cast<const ss_d2*>(p));
+  return *reinterpret_cast<const ss_d2*>(p);
+}
+// WIDE (one segment, n even, 16-byte aligned vectors): a thread owns the
+// adjacent entries b * 1024 + 2 t, + 1 and reads / writes each vector with one
+// 16-byte access, else entries b * 1024 + e * 512 + t
+template <int KL, bool WIDE>
 __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs V, SStepArgs a,
                                                                int k, GmresDev* st, double* gran,
                                                                unsigned long long seq, double* err) {
@@ -801,39 +900,75 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   __shared__ double sm16[kChainWaves * 16];
   __shared__ double c1[S * 32], c2[S * 32 + 16];
   __shared__ double Rm[S][S];
+  __shared__ double Gp[S * (S + 1) / 2];
+  __shared__ SsHess hs;
   __shared__ int bad;
-  if (st->status) return;
   const int nb = gridDim.x, b = blockIdx.x;
+  // the Hessenberg workgroup: the last one when it owns no vector entries (a
+  // grid of min(CUs, 256) workgroups covers n <= 256 Ki with idle ones at the
+  // end), so the Hessenberg columns and Givens steps overlap the other
+  // workgroups' last update and q stores; else workgroup 0
+  const int hb = long(nb - 1) * (kChainThreads * kChainEntries) >= g.n ? nb - 1 : 0;
+#if DCP_SS_PROBE & 32
+  __shared__ long long ss_buf[16];
+  long long* ss_ts = b == hb ? ss_buf : nullptr;
+  if (threadIdx.x == 0) ss_buf[15] = (long long)seq;
+#else
+  long long* ss_ts = nullptr;
+#endif
+  SS_STAMP(0);
+  if (st->status) return;
   const int d = k + 1;              // basis vectors q_0..q_k
   const int ncol1 = S * d;          // C columns (i * d + j)
   constexpr int nG = S * (S + 1) / 2;
-  // entries b * 1024 + e * 512 + t of the vectors (two per thread)
+  // two entries per thread (WIDE: adjacent)
   double v[kChainEntries][K], w[kChainEntries][S];
   unsigned pos[kChainEntries];
   bool live[kChainEntries];
   const long kb = long(b) * (kChainThreads * kChainEntries);
+  if (WIDE) {
+    const long k0 = kb + 2 * long(threadIdx.x);
+    live[0] = live[1] = k0 < g.n;  // n even: a pair is all in or all out
+    pos[0] = live[0] ? unsigned(k0) : 0u;
+    pos[1] = pos[0] + 1;
 #pragma unroll
-  for (int e = 0; e < kChainEntries; ++e) {
-    const long kk = kb + e * kChainThreads + threadIdx.x;
-    live[e] = kk < g.n;
-    pos[e] = live[e] ? unsigned(seg_pos(g, kk)) : 0u;
+    for (int i = 0; i < S; ++i) {
+      const ss_d2 t = live[0] ? ss_ldw2(a.w[i] + pos[0]) : ss_d2{0.0, 0.0};
+      w[0][i] = t.x;
+      w[1][i] = t.y;
+    }
 #pragma unroll
-    for (int i = 0; i < S; ++i) w[e][i] = live[e] ? ss_ldw(a.w[i] + pos[e]) : 0.0;
+    for (int j = 0; j < K; ++j) {
+      const ss_d2 t = (j < KL && j < d && live[0]) ? ss_ldv2(V.v[j] + pos[0]) : ss_d2{0.0, 0.0};
+      v[0][j] = t.x;
+      v[1][j] = t.y;
+    }
+  } else {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-      v[e][j] = (j < KL && j < d && live[e]) ? ss_ldv(V.v[j] + pos[e]) : 0.0;
+    for (int e = 0; e < kChainEntries; ++e) {
+      const long kk = kb + e * kChainThreads + threadIdx.x;
+      live[e] = kk < g.n;
+      pos[e] = live[e] ? unsigned(seg_pos(g, kk)) : 0u;
+#pragma unroll
+      for (int i = 0; i < S; ++i) w[e][i] = live[e] ? ss_ldw(a.w[i] + pos[e]) : 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        v[e][j] = (j < KL && j < d && live[e]) ? ss_ldv(V.v[j] + pos[e]) : 0.0;
+    }
   }
+  if (b == hb) sstep_hess_stage(hs, st, k);  // synchronised by the passes' barriers
   double* part = gran;
   double* res = gran + kSsRes;
   for (int pass = 0; pass < 2; ++pass) {
     const unsigned long long tag = seq * 256 + 2 * unsigned(pass);
     const int ncol = pass == 0 ? ncol1 : ncol1 + nG;
-    // block sums of V^T w_i (and, pass 1, of w_a w_b)
+    if (pass == 1) SS_STAMP(3);
+    // block sums of V^T w_i (and, pass 1, of w_a w_b): the wave sums of all
+    // of them, one barrier, then the sums over the waves
 #pragma unroll
     for (int i = 0; i < S; ++i) {
       const double x[kChainEntries] = {w[0][i], w[1][i]};
-      const double r = chain_block_sums<K>(v, x, d, sm[i]);
-      if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
+      chain_wave_sums<K>(v, x, sm[i]);
     }
     if (pass == 1) {
       // Gram sums w_i . w_l (l >= i): row i of W^T W as a 4-wide block sum,
@@ -841,13 +976,26 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
 #pragma unroll
       for (int i = 0; i < S; ++i) {
         const double x[kChainEntries] = {w[0][i], w[1][i]};
-        const double r = chain_block_sums<S>(w, x, S, sm16 + (i & 1) * kChainWaves * S);
+        chain_wave_sums<S>(w, x, sm16 + i * kChainWaves * S);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const double r = chain_sum_waves<K>(d, sm[i]);
+      if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
+    }
+    if (pass == 1) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const double r = chain_sum_waves<S>(S, sm16 + i * kChainWaves * S);
         const int l = threadIdx.x;
         if (l >= i && l < S)
           granule_store(part + 2 * (size_t(ncol1 + i * S - i * (i - 1) / 2 + (l - i)) * nb + b), r,
                         tag);
       }
     }
+    SS_STAMP(pass == 0 ? 1 : 4);
     // workgroup c reduces column c and publishes the total
     if (b < ncol && threadIdx.x < 64) {
       const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err, &st->status, g_spin_limit);
@@ -868,6 +1016,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
       else c2[c] = granule_value(q);
     }
     __syncthreads();
+    SS_STAMP(pass == 0 ? 2 : 5);
     const double* h = pass == 0 ? c1 : c2;
     // basis vector by basis vector: the compiler barrier keeps the LDS loads of
     // the 4 coefficients of vector j next to their use (hoisting all 4 KL of
@@ -889,8 +1038,8 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   }
   // G' = G - C2^T C2 and its Cholesky factor (every workgroup, the same
   // arithmetic in the same order)
-  if (threadIdx.x == 0) bad = !sstep_chol(c2, d, ncol1, Rm);
-  __syncthreads();
+  sstep_factor(c2, d, ncol1, Gp, Rm, &bad);
+  SS_STAMP(6);
   // q_{k+1+i} = (w_i - sum_{l<i} q_{k+1+l} R[l][i]) / R[i][i]
 #pragma unroll
   for (int e = 0; e < kChainEntries; ++e) {
@@ -900,10 +1049,15 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
 #pragma unroll
       for (int l = 0; l < i; ++l) q -= w[e][l] * Rm[l][i];
       w[e][i] = q / Rm[i][i];
-      if (live[e]) a.q[i][pos[e]] = w[e][i];
+      if (!WIDE && live[e]) a.q[i][pos[e]] = w[e][i];
     }
   }
-  if (b != 0) return;
+  if (WIDE && live[0])
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      *reinterpret_cast<ss_d2*>(a.q[i] + pos[0]) = ss_d2{w[0][i], w[1][i]};
+  SS_STAMP(7);
+  if (b != hb) return;
   if (bad) {  // the block lost rank: a breakdown the one-vector process would not see
     if (threadIdx.x == 0) {
       atomicMax(&st->status, 2);
@@ -911,7 +1065,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     }
     return;
   }
-  sstep_hessenberg(st, a, k, c1, c2, Rm);
+  sstep_hessenberg(st, hs, a, k, c1, c2, Rm, ss_ts);
 }
 
 // Several GPUs / large meshes: the same block as five launches around two
@@ -1017,16 +1171,18 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
   constexpr int S = kSStep;
   __shared__ double c1[S * 32], c2[S * 32 + 16];
   __shared__ double Rm[S][S];
+  __shared__ double Gp[S * (S + 1) / 2];
+  __shared__ SsHess hs;
   __shared__ int bad;
   if (st->status) return;
   const int d = k + 1, ncol1 = S * d;
+  if (blockIdx.x == 0) sstep_hess_stage(hs, st, k);
   for (int c = threadIdx.x; c < ncol1 + S * (S + 1) / 2; c += kBlock) {
     if (c < ncol1) c1[c] = c1g[c];
     c2[c] = c2g[c];
   }
   __syncthreads();
-  if (threadIdx.x == 0) bad = !sstep_chol(c2, d, ncol1, Rm);
-  __syncthreads();
+  sstep_factor(c2, d, ncol1, Gp, Rm, &bad);
   const long k0 = long(blockIdx.x) * (kBlock * kCgsElems) + threadIdx.x;
 #pragma unroll
   for (int e = 0; e < kCgsElems; ++e) {
@@ -1058,16 +1214,19 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
     }
     return;
   }
-  sstep_hessenberg(st, a, k, c1, c2, Rm);
+  sstep_hessenberg(st, hs, a, k, c1, c2, Rm);
 }
 
 }  // namespace
 
 int sstep_block_capacity() {
   static const int cap = [] {
-    decltype(&k_sstep_block<4>) fs[] = {k_sstep_block<4>,  k_sstep_block<8>,  k_sstep_block<12>,
-                                        k_sstep_block<16>, k_sstep_block<20>, k_sstep_block<24>,
-                                        k_sstep_block<28>};
+    decltype(&k_sstep_block<4, true>) fs[] = {
+        k_sstep_block<4, true>,   k_sstep_block<8, true>,   k_sstep_block<12, true>,
+        k_sstep_block<16, true>,  k_sstep_block<20, true>,  k_sstep_block<24, true>,
+        k_sstep_block<28, true>,  k_sstep_block<4, false>,  k_sstep_block<8, false>,
+        k_sstep_block<12, false>, k_sstep_block<16, false>, k_sstep_block<20, false>,
+        k_sstep_block<24, false>, k_sstep_block<28, false>};
     return family_capacity(fs);
   }();
   return cap;
@@ -1077,10 +1236,19 @@ void sstep_block(Seg g, const ChainVecs& V, const SStepArgs& a, int k, GmresDev*
                  int nb, unsigned long long seq, double* err, hipStream_t s) {
   ChainVecs Vp = V;
   for (int j = k + 1; j < kGmMaxDim; ++j) Vp.v[j] = V.v[0];
-#define DCP_SS_CASE(KL)                                                                        \
-  if (k + 1 <= KL) {                                                                           \
-    launch_resident(k_sstep_block<KL>, nb, kChainThreads, s, g, Vp, a, k, st, gran, seq, err);  \
-    return;                                                                                    \
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  bool wide = g.n1 == g.n && g.n % 2 == 0;
+  for (int j = 0; j <= k; ++j) wide = wide && al16(V.v[j]);
+  for (int i = 0; i < kSStep; ++i) wide = wide && al16(a.w[i]) && al16(a.q[i]);
+#define DCP_SS_CASE(KL)                                                                          \
+  if (k + 1 <= KL) {                                                                             \
+    if (wide)                                                                                    \
+      launch_resident(k_sstep_block<KL, true>, nb, kChainThreads, s, g, Vp, a, k, st, gran, seq,  \
+                      err);                                                                      \
+    else                                                                                         \
+      launch_resident(k_sstep_block<KL, false>, nb, kChainThreads, s, g, Vp, a, k, st, gran, seq, \
+                      err);                                                                      \
+    return;                                                                                      \
   }
   DCP_SS_CASE(4) DCP_SS_CASE(8) DCP_SS_CASE(12) DCP_SS_CASE(16) DCP_SS_CASE(20) DCP_SS_CASE(24)
   DCP_SS_CASE(28)
@@ -1197,28 +1365,14 @@ template <int K, class F>
 __device__ inline double wave_rs(F prod) {
   const int l = threadIdx.x & 63;
   double s[K / 2];
-  {
-    const bool up = (l & 32) != 0;
 #pragma unroll
-    for (int i = 0; i < K / 2; ++i) {
-      const double lo = prod(i), hi = prod(i + K / 2);
-      s[i] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, 64);
-    }
+  for (int i = 0; i < K / 2; ++i) {
+    double lo = prod(i), hi = prod(i + K / 2);
+    xch_swap<32>(lo, hi);
+    s[i] = lo + hi;
   }
-  int o = 16;
-#pragma unroll
-  for (int c = K / 2; c > 1; c >>= 1, o >>= 1) {
-    const bool up = (l & o) != 0;
-#pragma unroll
-    for (int i = 0; i < c / 2; ++i) {
-      const double send = up ? s[i] : s[i + c / 2];
-      const double keep = up ? s[i + c / 2] : s[i];
-      s[i] = keep + __shfl_xor(send, o, 64);
-    }
-  }
-  double r = s[0];
-  for (; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-  return r;
+  rs_steps<K / 2, 16>(s, l);
+  return butterfly_from<32 / K>(s[0]);
 }
 
 // The scalars of the step from the reduced slots r[] (every workgroup computes

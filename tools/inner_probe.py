@@ -3,6 +3,7 @@ buffers) at refine R for every build/var/libdcp_*.so: one JSON line per
 variant with microseconds per inner iteration (median of 4 calls)."""
 import ctypes as C
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -45,6 +46,8 @@ for path in libs or [dcp.LIB_PATH]:
             dt = time.perf_counter() - t0
             if rep:
                 per.append(dt / max(it.value, 1) * 1e6)
+        digest = hashlib.sha1(dd.download().tobytes()).hexdigest()[:12]
     print(json.dumps({"variant": os.path.basename(path), "inner_its": it.value,
-                      "us_per_inner_it": float(np.median(per))}), flush=True)
+                      "us_per_inner_it": float(np.median(per)), "result_sha1": digest}),
+          flush=True)
     ctx.close()
