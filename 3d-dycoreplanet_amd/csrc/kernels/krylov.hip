@@ -802,27 +802,43 @@ __device__ void sstep_hessenberg(GmresDev* st, SsHess& h, const SStepArgs& a, in
     int acc = h.acc0;
     const double tol = h.tol;
     const int max_steps = h.max_steps;
+    // the block's S x S corner of new columns, hk and gamma_k in registers up
+    // front, the block's own rotations kept in registers (the loop is fully
+    // unrolled; LDS round trips on the serial chain were its cost)
+    double hnr[S][S], hkr[S], csr[S], snr[S];
+#pragma unroll
+    for (int c = 0; c < S; ++c) {
+      hkr[c] = hk[c];
+#pragma unroll
+      for (int i = 0; i < S; ++i) hnr[i][c] = Hn[k + 1 + i][c];  // Hn[kk + 1] for kk = k + i
+    }
+    double g0 = gam[k];
     last_col = S - 1;
+#pragma unroll
     for (int c = 0; c < S; ++c) {
       const int kk = k + c;
       // then the block's own rotations, carrying h[i+1] in a register
-      double hi = hk[c];
-      for (int i = k; i < kk; i++) {
-        const double hn = Hn[i + 1][c];
-        Hrot[i][c] = cs[i] * hi + sn[i] * hn;
-        hi = -sn[i] * hi + cs[i] * hn;
+      double hi = hkr[c];
+#pragma unroll
+      for (int i = 0; i < c; i++) {
+        const double hn = hnr[i][c];
+        Hrot[k + i][c] = csr[i] * hi + snr[i] * hn;
+        hi = -snr[i] * hi + csr[i] * hn;
       }
-      const double hk1 = Hn[kk + 1][c];
+      const double hk1 = hnr[c][c];
       const double r = 1. / sqrt(hi * hi + hk1 * hk1);
       const double s_ = hk1 * r, c_ = hi * r;
+      snr[c] = s_;
+      csr[c] = c_;
       sn[kk] = s_;
       cs[kk] = c_;
       Hrot[kk][c] = c_ * hi + s_ * hk1;
-      const double g0 = gam[kk];
-      gam[kk + 1] = -s_ * g0;
+      const double g1 = -s_ * g0;
+      gam[kk + 1] = g1;
       gam[kk] = g0 * c_;
+      g0 = g1;
       ++acc;
-      const double rho = fabs(gam[kk + 1]);
+      const double rho = fabs(g1);
       const int status = rho <= tol ? 1 : ((acc >= max_steps || isnan(rho)) ? 2 : 0);
       if (status || c == S - 1) {
         st->accumulated = acc;
@@ -957,6 +973,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     }
   }
   if (b == hb) sstep_hess_stage(hs, st, k);  // synchronised by the passes' barriers
+  const bool idle = kb >= g.n;  // the workgroup owns no entries
   double* part = gran;
   double* res = gran + kSsRes;
   for (int pass = 0; pass < 2; ++pass) {
@@ -964,31 +981,35 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     const int ncol = pass == 0 ? ncol1 : ncol1 + nG;
     if (pass == 1) SS_STAMP(3);
     // block sums of V^T w_i (and, pass 1, of w_a w_b): the wave sums of all
-    // of them, one barrier, then the sums over the waves
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      const double x[kChainEntries] = {w[0][i], w[1][i]};
-      chain_wave_sums<K>(v, x, sm[i]);
-    }
-    if (pass == 1) {
-      // Gram sums w_i . w_l (l >= i): row i of W^T W as a 4-wide block sum,
-      // so only the 4 w entries are live next to the basis
+    // of them, one barrier, then the sums over the waves. A workgroup that
+    // owns no entries publishes +0.0, what those reductions give over its zero
+    // entries, without running them.
+    if (!idle) {
 #pragma unroll
       for (int i = 0; i < S; ++i) {
         const double x[kChainEntries] = {w[0][i], w[1][i]};
-        chain_wave_sums<S>(w, x, sm16 + i * kChainWaves * S);
+        chain_wave_sums<K>(v, x, sm[i]);
       }
+      if (pass == 1) {
+        // Gram sums w_i . w_l (l >= i): row i of W^T W as a 4-wide block sum,
+        // so only the 4 w entries are live next to the basis
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const double x[kChainEntries] = {w[0][i], w[1][i]};
+          chain_wave_sums<S>(w, x, sm16 + i * kChainWaves * S);
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
 #pragma unroll
     for (int i = 0; i < S; ++i) {
-      const double r = chain_sum_waves<K>(d, sm[i]);
+      const double r = idle ? 0.0 : chain_sum_waves<K>(d, sm[i]);
       if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
     }
     if (pass == 1) {
 #pragma unroll
       for (int i = 0; i < S; ++i) {
-        const double r = chain_sum_waves<S>(S, sm16 + i * kChainWaves * S);
+        const double r = idle ? 0.0 : chain_sum_waves<S>(S, sm16 + i * kChainWaves * S);
         const int l = threadIdx.x;
         if (l >= i && l < S)
           granule_store(part + 2 * (size_t(ncol1 + i * S - i * (i - 1) / 2 + (l - i)) * nb + b), r,
@@ -1001,6 +1022,10 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
       const double tot = granule_coef(part + 2 * size_t(b) * nb, nb, tag, err, &st->status, g_spin_limit);
       if (threadIdx.x == 0) granule_store(res + 2 * b, tot, tag + 1);
     }
+    // an idle workgroup other than the Hessenberg one is done after its last
+    // publications (it read the first pass's results, so every reducer of that
+    // pass had read the partials its second-pass granules overwrite)
+    if (pass == 1 && idle && b != hb) return;
     for (int c = threadIdx.x; c < ncol; c += kChainThreads) {
       const double* p = res + 2 * c;
       mgs_u4 q = granule_load(p);
@@ -1017,6 +1042,7 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     }
     __syncthreads();
     SS_STAMP(pass == 0 ? 2 : 5);
+    if (idle) continue;  // no entries to update
     const double* h = pass == 0 ? c1 : c2;
     // basis vector by basis vector: the compiler barrier keeps the LDS loads of
     // the 4 coefficients of vector j next to their use (hoisting all 4 KL of
@@ -1037,7 +1063,9 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     __syncthreads();
   }
   // G' = G - C2^T C2 and its Cholesky factor (every workgroup, the same
-  // arithmetic in the same order)
+  // arithmetic in the same order); the idle Hessenberg workgroup gets here
+  // straight from the second hand-off, so its Hessenberg columns overlap the
+  // others' update and stores
   sstep_factor(c2, d, ncol1, Gp, Rm, &bad);
   SS_STAMP(6);
   // q_{k+1+i} = (w_i - sum_{l<i} q_{k+1+l} R[l][i]) / R[i][i]
