@@ -338,6 +338,23 @@ __device__ inline double wave_reduce_scatter(const double (&v)[kChainEntries][K]
     return butterfly_from<32 / K>(s[0]);  // the lane bits below the halving steps
   }
 }
+// Reduce-scatter over a wave of the K products prod(j) (j compile-time after
+// unrolling), as wave_reduce_scatter: lane l ends with the wave sum of slot
+// l >> (6 - log2 K).
+template <int K, class F>
+__device__ inline double wave_rs(F prod) {
+  const int l = threadIdx.x & 63;
+  double s[K / 2];
+#pragma unroll
+  for (int i = 0; i < K / 2; ++i) {
+    double lo = prod(i), hi = prod(i + K / 2);
+    xch_swap<32>(lo, hi);
+    s[i] = lo + hi;
+  }
+  rs_steps<K / 2, 16>(s, l);
+  return butterfly_from<32 / K>(s[0]);
+}
+
 template <int K>
 constexpr int log2i() { return K <= 1 ? 0 : 1 + log2i<K / 2>(); }
 
@@ -912,7 +929,8 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
   constexpr int K = pow2_at_least<KL>();
   constexpr int S = kSStep;
   static_assert(kChainEntries == 2, "two entries per thread");
-  __shared__ double sm[S][kChainWaves * K];
+  constexpr int G = (KL + 7) / 8;  // slot groups: basis vectors 8 g .. 8 g + 7
+  __shared__ double smg[G][kChainWaves * 32];
   __shared__ double sm16[kChainWaves * 16];
   __shared__ double c1[S * 32], c2[S * 32 + 16];
   __shared__ double Rm[S][S];
@@ -981,40 +999,51 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     const int ncol = pass == 0 ? ncol1 : ncol1 + nG;
     if (pass == 1) SS_STAMP(3);
     // block sums of V^T w_i (and, pass 1, of w_a w_b): the wave sums of all
-    // of them, one barrier, then the sums over the waves. A workgroup that
-    // owns no entries publishes +0.0, what those reductions give over its zero
-    // entries, without running them.
+    // of them, one barrier, then the sums over the waves. The products are
+    // reduced in groups of 32 slots (w_i . q_j for i < 4 and 8 consecutive j),
+    // so group g needs only basis vectors 8 g .. 8 g + 7 and starts while the
+    // later ones are still loading; the 10 Gram sums are one 16-slot group.
+    // A workgroup that owns no entries publishes +0.0, what those reductions
+    // give over its zero entries, without running them.
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (!idle) {
 #pragma unroll
-      for (int i = 0; i < S; ++i) {
-        const double x[kChainEntries] = {w[0][i], w[1][i]};
-        chain_wave_sums<K>(v, x, sm[i]);
+      for (int gr = 0; gr < G; ++gr) {
+        if (8 * gr < d) {
+          const double r = wave_rs<32>([&](int sl) {
+            const int i = sl >> 3, j = 8 * gr + (sl & 7);
+            return j < KL ? v[0][j] * w[0][i] + v[1][j] * w[1][i] : 0.0;
+          });
+          if ((lane & 1) == 0) smg[gr][wv * 32 + (lane >> 1)] = r;
+        }
       }
       if (pass == 1) {
-        // Gram sums w_i . w_l (l >= i): row i of W^T W as a 4-wide block sum,
-        // so only the 4 w entries are live next to the basis
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          const double x[kChainEntries] = {w[0][i], w[1][i]};
-          chain_wave_sums<S>(w, x, sm16 + i * kChainWaves * S);
-        }
+        const double r = wave_rs<16>([&](int p) {
+          int i = 0, l = p;  // p -> (i, l >= i), row-major upper triangle
+          while (l >= S - i) {
+            l -= S - i;
+            ++i;
+          }
+          l += i;
+          return p < nG ? w[0][i] * w[0][l] + w[1][i] * w[1][l] : 0.0;
+        });
+        if ((lane & 3) == 0) sm16[wv * 16 + (lane >> 2)] = r;
       }
       __syncthreads();
     }
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      const double r = idle ? 0.0 : chain_sum_waves<K>(d, sm[i]);
-      if (int(threadIdx.x) < d) granule_store(part + 2 * (size_t(i * d + threadIdx.x) * nb + b), r, tag);
+    for (int c = threadIdx.x; c < ncol1; c += kChainThreads) {
+      const int i = c / d, j = c - i * d;
+      const double* sp = &smg[j >> 3][i * 8 + (j & 7)];
+      double t = 0.0;
+      if (!idle)
+        for (int q = 0; q < kChainWaves; ++q) t += sp[q * 32];
+      granule_store(part + 2 * (size_t(c) * nb + b), t, tag);
     }
-    if (pass == 1) {
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        const double r = idle ? 0.0 : chain_sum_waves<S>(S, sm16 + i * kChainWaves * S);
-        const int l = threadIdx.x;
-        if (l >= i && l < S)
-          granule_store(part + 2 * (size_t(ncol1 + i * S - i * (i - 1) / 2 + (l - i)) * nb + b), r,
-                        tag);
-      }
+    if (pass == 1 && int(threadIdx.x) < nG) {
+      double t = 0.0;
+      if (!idle)
+        for (int q = 0; q < kChainWaves; ++q) t += sm16[q * 16 + threadIdx.x];
+      granule_store(part + 2 * (size_t(ncol1 + threadIdx.x) * nb + b), t, tag);
     }
     SS_STAMP(pass == 0 ? 1 : 4);
     // workgroup c reduces column c and publishes the total
@@ -1384,23 +1413,6 @@ template <int KP>
 __device__ inline bool dcgs_used(int j, int k, bool tail) {
   if (j < KP) return j < k || j == KP - 1;
   return !tail && (j - KP < k || j >= 2 * KP - 2);
-}
-
-// Reduce-scatter over a wave of the K products prod(j) (j compile-time after
-// unrolling), as wave_reduce_scatter: lane l ends with the wave sum of slot
-// l >> (6 - log2 K).
-template <int K, class F>
-__device__ inline double wave_rs(F prod) {
-  const int l = threadIdx.x & 63;
-  double s[K / 2];
-#pragma unroll
-  for (int i = 0; i < K / 2; ++i) {
-    double lo = prod(i), hi = prod(i + K / 2);
-    xch_swap<32>(lo, hi);
-    s[i] = lo + hi;
-  }
-  rs_steps<K / 2, 16>(s, l);
-  return butterfly_from<32 / K>(s[0]);
 }
 
 // The scalars of the step from the reduced slots r[] (every workgroup computes
