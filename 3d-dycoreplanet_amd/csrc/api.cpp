@@ -1796,6 +1796,11 @@ int dcp_set_option(dcp_ctx* ctx, int option, int value) {
       ctx->element_mfma = value != 0;
       return DCP_OK;
     }
+    if (option == DCP_OPT_T_FIXED_CG) {
+      require(value >= 0, DCP_ERR_INVALID, "DCP_OPT_T_FIXED_CG must be >= 0");
+      ctx->T_fixed_cg = value;
+      return DCP_OK;
+    }
     if (option == DCP_OPT_SCHUR_FIXED_INNER) {
       require(value >= 0, DCP_ERR_INVALID, "DCP_OPT_SCHUR_FIXED_INNER must be >= 0");
       ctx->schur_fixed_inner = value;

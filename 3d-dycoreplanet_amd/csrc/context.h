@@ -430,6 +430,7 @@ struct Ctx {
   double fe_wsum = 0;                      // sum of the mean-value weights
   double fe_wsum2 = 0;
   bool feec_block_prec = true;  // use_block_preconditioner_feec
+  int T_fixed_cg = 0;            // DCP_OPT_T_FIXED_CG (test hook of solve_temperature)
   bool fe_assembled = false, fe_precond = false;
   std::vector<double*> fe_v, fe_s, fe_n;  // Krylov bases: outer, shifted Schur, nested Schur
   DBuf<double> fe_t1, fe_t2, fe_t3, fe_t4;

@@ -1756,7 +1756,8 @@ int solve_temperature(Ctx& c, int* iters, double* T_range) {
   const int n = c.n_T;
   const Seg g = c.seg_T();
   const double rhs_norm = std::sqrt(dot_host(c, g, c.T_rhs.p, c.T_rhs.p, kSlotA));
-  Control ctl{unsigned(c.n_T_g), 1e-12 * rhs_norm};
+  const int fk = c.T_fixed_cg;  // > 0: exactly fk steps (test hook)
+  Control ctl{fk > 0 ? unsigned(fk) : unsigned(c.n_T_g), fk > 0 ? 0.0 : 1e-12 * rhs_norm};
   if (c.cg_g.n < size_t(n)) {
     c.cg_g.alloc(n);
     c.cg_d.alloc(n);
@@ -1819,7 +1820,7 @@ int solve_temperature(Ctx& c, int* iters, double* T_range) {
   }
   DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
   if (iters) *iters = int(ctl.last_step);
-  return conv == kSuccess ? DCP_OK : DCP_NOT_CONVERGED;
+  return conv == kSuccess || (fk > 0 && int(ctl.last_step) == fk) ? DCP_OK : DCP_NOT_CONVERGED;
 }
 
 void check_mf_err(Ctx& c) {

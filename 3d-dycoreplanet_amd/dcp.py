@@ -41,6 +41,7 @@ OPT_HANDOFF_SPIN_LIMIT = 13
 OPT_BLOCK_FIXED_INNER = 14
 OPT_MATRIX_POWERS = 15
 OPT_FEEC_BLOCK_PRECONDITIONER = 16
+OPT_T_FIXED_CG = 17
 ABI_VERSION = 5            # include/dcp.h DCP_ABI_VERSION
 CELL_SUPPORT_POINTS = 64   # include/dcp.h DCP_CELL_SUPPORT_POINTS
 
@@ -1142,6 +1143,11 @@ class Context:
         """DCP_OPT_FEEC_BLOCK_PRECONDITIONER (use_block_preconditioner_feec): off
         runs the identity-preconditioned GMRES(100) branch (FEEC.tpp:1420-1431)."""
         self._check(lib().dcp_set_option(self._h, OPT_FEEC_BLOCK_PRECONDITIONER, int(bool(on))))
+
+    def set_T_fixed_cg(self, k: int):
+        """DCP_OPT_T_FIXED_CG (test hook): the temperature CG runs exactly k
+        steps (0 = the reference's 1e-12 |rhs| rule)."""
+        self._check(lib().dcp_set_option(self._h, OPT_T_FIXED_CG, int(k)))
 
     def set_feec_fixed_inner(self, k: int):
         """DCP_OPT_FEEC_FIXED_INNER (test hook): both inner GMRES of the FEEC

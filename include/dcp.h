@@ -299,6 +299,11 @@ enum { DCP_OPT_BLOCK_FIXED_INNER = 14 };
  * instead of 4. Bitwise the same iterates; 0 = one exchange per SpMV. No
  * effect on one GPU or with another DCP_OPT_GRAM_SCHMIDT. */
 enum { DCP_OPT_MATRIX_POWERS = 15 };
+/* DCP_OPT_T_FIXED_CG (test hook, default 0 = the reference's rule): k > 0 runs
+ *   the temperature CG (dcp_solve_temperature) for exactly k steps (tolerance
+ *   0, counted as converged at k), so partitioned sums cannot move its stopping
+ *   step; k below the CG's convergence (steps past it divide round-off). */
+enum { DCP_OPT_T_FIXED_CG = 17 };
 int dcp_set_option(dcp_ctx* ctx, int option, int value);
 
 /* The SolverControl log of the last dcp_solve_nse (DCP_OPT_LOG_HISTORY):

@@ -336,6 +336,65 @@ def test_group_feec_time_step_matches_single_gpu(world, geometry):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_feec_time_step_fixed_inner_1e10(world):
+    """The FEEC group step of the test above with both inner GMRES held at 3
+    steps (DCP_OPT_FEEC_FIXED_INNER) on every rank and on the one-GPU
+    reference: no inner stopping decision can follow the partitioned
+    summation order, so the iterate meets the north-star 1e-10 with equal
+    outer counts (shell; the temperature CG still stops on its tolerance)."""
+    m = dcp.HostMesh(refine=2, feec=True)
+    ph = dcp.classic_physics()
+    f = m.feec
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(f.n)
+    x0[:f.n_w + f.n_u] = 0.05 * rng.uniform(-1, 1, f.n_w + f.n_u)
+    x0[f.fixed.astype(bool)] = 0
+    T0 = m.T0.copy()
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(ph)
+    ref_ctx.upload_feec_mesh(m)
+    ref_ctx.set_feec_fixed_inner(3)
+    ref = _feec_time_step(ref_ctx, m, x0, T0)
+    ref_ctx.close()
+
+    g = dcp.Group(world)
+    results, errors = [None] * world, []
+
+    def run(rank):
+        try:
+            ctx = dcp.Context(rank=rank, world_size=world, group=g)
+            ctx.set_physics(ph)
+            ctx.upload_feec_mesh(m)
+            ctx.set_feec_fixed_inner(3)
+            results[rank] = _feec_time_step(ctx, m, x0, T0)
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append((rank, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    g.close()
+    assert not errors, errors
+
+    def merged(key):
+        v = np.zeros_like(ref[key])
+        for r in results:
+            nz = r[key] != 0
+            v[nz] = r[key][nz]
+        return v
+    x = merged("x")
+    assert np.linalg.norm(x - ref["x"]) <= 1e-10 * np.linalg.norm(ref["x"])
+    for r in results:
+        assert r["nse"][0] == ref["nse"][0] == 0
+        assert r["nse"][1] == ref["nse"][1]
+        assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-10)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("gs", ["classical2", "sstep"])
 def test_one_rank_rccl_time_step_matches_single_gpu(gs):
     """The multi-GPU code path on a one-rank RCCL communicator (dcp_config
@@ -763,3 +822,47 @@ def test_group_cube_time_step_matches_single_gpu(world, gs, fixed_inner, refine)
         assert abs(r["T"][1] - ref["T"][1]) <= 1
         assert np.isclose(r["vmax"], ref["vmax"], rtol=1e-10)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,geometry", [(2, "shell"), (3, "shell"), (2, "cube"), (3, "cube")])
+def test_group_temperature_fixed_cg_exact_count(world, geometry):
+    """The temperature CG on a group against one GPU with DCP_OPT_T_FIXED_CG:
+    the group tests above allow its count ±1 (CG to 1e-12 |b| stops on either
+    side of the threshold with partitioned sums); with both held at 6 steps
+    (below convergence at r = 2) the counts are equal and T agrees at 1e-12
+    (shell, and the periodic cube with its images copied after the solve)."""
+    k = 6
+    if geometry == "cube":
+        rp = dcp.load_prm(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                       "configs", "aqua_planet_cube_test_3d.prm"))
+        ph = dcp.physics_from_params(rp)
+        m = dcp.HostMesh(cuboid=True, refine=2, length=rp.length)
+    else:
+        ph = dcp.classic_physics()
+        m = dcp.HostMesh(refine=2)
+    rng = np.random.default_rng(23)
+    u = np.zeros(m.n_u + m.n_p)
+    u[:m.n_u] = 0.05 * rng.uniform(-1, 1, m.n_u)
+    u = periodic_state(m, u, m.nse_constraints)
+    T = periodic_state(m, m.T0 + 0.02 * rng.uniform(-1, 1, m.n_T), m.T_constraints)
+
+    def setup(ctx):
+        ctx.set_T_fixed_cg(k)
+        ctx.set_block_fixed_inner(8)
+
+    ref_ctx = dcp.Context()
+    ref_ctx.set_physics(ph)
+    ref_ctx.upload_mesh(m)
+    setup(ref_ctx)
+    ref = _time_step(ref_ctx, m, u, T)
+    ref_ctx.close()
+    results = _group_run(world, m, ph, u, T, setup)
+    Tx = np.zeros_like(ref["Tx"])
+    for r in results:
+        nz = r["Tx"] != 0
+        Tx[nz] = r["Tx"][nz]
+    assert ref["T"][:2] == (0, k)
+    for r in results:
+        assert r["T"][:2] == (0, k)
+    assert np.max(np.abs(Tx - ref["Tx"])) <= 1e-12 * np.max(np.abs(ref["Tx"]))
