@@ -244,8 +244,8 @@ def test_threaded_host_comm_localisation_matches_global(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_upload_group_time_step_matches_single_gpu(world):
+@pytest.mark.parametrize("world,t_fixed", [(2, 0), (3, 0), (2, 6), (3, 6)])
+def test_distributed_upload_group_time_step_matches_single_gpu(world, t_fixed):
     """The distributed entry point on several ranks (in-process group, one
     thread per rank, ThreadHostComms as the caller's communicator): one full
     time step -- assembly, preconditioner, the s-step inner GMRES with the
@@ -253,7 +253,8 @@ def test_distributed_upload_group_time_step_matches_single_gpu(world):
     every rank's owned entries. The inner solves run 28 fixed steps
     (DCP_OPT_BLOCK_FIXED_INNER) so both take the same control decisions:
     rhs 1e-12, iterates 1e-10, equal outer counts; temperature 1e-9 (its CG
-    keeps the reference's stopping rule)."""
+    keeps the reference's stopping rule), or with t_fixed (DCP_OPT_T_FIXED_CG:
+    the CG held at that many steps on both sides) equal counts and 1e-12."""
     m = dcp.HostMesh(refine=2)
     ph = dcp.classic_physics()
     rng = np.random.default_rng(17)
@@ -264,6 +265,7 @@ def test_distributed_upload_group_time_step_matches_single_gpu(world):
     def step(ctx, setv):
         ctx.set_gram_schmidt("sstep")
         ctx.set_block_fixed_inner(28)
+        ctx.set_T_fixed_cg(t_fixed)
         for f, v in ((dcp.OLD_NSE_SOLUTION, u), (dcp.NSE_SOLUTION, u), (dcp.OLD_T_SOLUTION, T),
                      (dcp.T_SOLUTION, T)):
             setv(f, v)
@@ -310,5 +312,9 @@ def test_distributed_upload_group_time_step_matches_single_gpu(world):
         assert rel(x, dm.owned_nse(ref_x)) < 1e-10
         # temperature CG to 1e-12 under the reference's rule: partitioned dot
         # products may move its stop by one iteration (2.7e-10 measured on 3 ranks)
-        assert abs(counts[1][1] - ref_counts[1][1]) <= 1
-        assert rel(Tx, dm.owned_T(ref_T)) < 1e-9
+        if t_fixed:
+            assert counts[1][:2] == ref_counts[1][:2] == (0, t_fixed)
+            assert rel(Tx, dm.owned_T(ref_T)) < 1e-12
+        else:
+            assert abs(counts[1][1] - ref_counts[1][1]) <= 1
+            assert rel(Tx, dm.owned_T(ref_T)) < 1e-9
