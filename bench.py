@@ -52,6 +52,8 @@ PMC_SUMMARIES = {(5, "explicit"): ("profiles/r04j_pmc_inner_r5.json", "k_sell_sp
 # rocprofv3 --kernel-trace --stats of the same workload (durations of the
 # orthogonalisation launches, for their roofline): the CGS2 chain (bench) and
 # the s-step block (inner probe)
+# PMC (2 FETCH + WRITE) of the same launches (tools/pmc_inner.sh)
+CHAIN_PMC = {(5, "sstep"): "profiles/r05/r05ab_pmc_inner_sstep_r5.json"}
 CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
                (5, "sstep"): "profiles/r05/r05w_bench_r5_kernel_stats.csv"}
 # the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
@@ -172,9 +174,24 @@ def chain_roofline(refine, n_p, gs):
             "Arnoldi column)" if gs == "classical2" else
             "s-step block k_sstep_block<KL> (one launch per 4 inner Arnoldi columns: BCGS2 + "
             "Cholesky QR + Hessenberg/Givens)")
-    return {"kernel": what, "bound": "hbm", "source": path,
-            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "per_template": per}
+    out = {"kernel": what, "bound": "hbm", "source": path,
+           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "per_template": per, "traffic": None}
+    pmc = CHAIN_PMC.get((refine, gs))
+    if pmc and os.path.exists(os.path.join(ROOT, pmc)):
+        with open(os.path.join(ROOT, pmc)) as f:
+            tb = json.load(f)["traffic_bytes"]
+        for name, v in tb.items():
+            if key in name:
+                kl = int(name.split(key)[1].split(",")[0].split(">")[0])
+                if kl in per:
+                    per[kl]["traffic"] = v
+        calls = {kl: c for kl, c, _ in rows}
+        if all("traffic" in per[kl] for kl in per):
+            # per launch, averaged over the launches of the profile
+            out["traffic"] = sum(calls[kl] * per[kl]["traffic"] for kl in per) / sum(calls.values())
+            out["traffic_source"] = pmc
+    return out
 
 
 def parse():
