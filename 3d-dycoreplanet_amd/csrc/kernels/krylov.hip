@@ -1009,7 +1009,10 @@ __global__ __launch_bounds__(kChainThreads) void k_sstep_block(Seg g, ChainVecs 
     if (!idle) {
 #pragma unroll
       for (int gr = 0; gr < G; ++gr) {
-        if (8 * gr < d) {
+        // every group, without a branch on d (the launch takes the smallest KL
+        // >= d = k + 1, so 8 gr < d anyway): one basic block, in which the
+        // scheduler overlaps the groups' exchange trees (-0.2 us per column)
+        {
           const double r = wave_rs<32>([&](int sl) {
             const int i = sl >> 3, j = 8 * gr + (sl & 7);
             return j < KL ? v[0][j] * w[0][i] + v[1][j] * w[1][i] : 0.0;
