@@ -2103,6 +2103,18 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 #pragma unroll
   for (int i = 0; i < SL * NE / 8 / 64; ++i) vw[64 * i + lane] = ~0ull;
   wsync();
+#ifndef DCP_BT_UNCOND
+#define DCP_BT_UNCOND 1
+#endif
+  // DCP_BT_UNCOND (default): every slot's table loads issued up front, without
+  // the per-slot branch (an unused slot's zero record reads column 0 / layer
+  // 0), so the R slots' table latencies overlap: k_bt_tasks<16,1> 313.6 ->
+  // 306.0 us under the tracer, bitwise (profiles/r05/r05ad_bt_uncond_variants.log)
+  double evu[R][3];
+  if (DCP_BT_UNCOND && !(DCP_BT_PROBE == 2 || DCP_BT_PROBE == 4)) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 31, v, evu[i]);
+  }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int sl = 8 * i + k, e = 64 * i + lane;  // e = 8 slot + v
@@ -2115,6 +2127,10 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
         ev[0] = 1e-3 * r[i].x;
         ev[1] = 1e-3 * (r[i].y >> 16);
         ev[2] = 1e-3 * v;
+      } else if (DCP_BT_UNCOND) {
+        ev[0] = evu[i][0];
+        ev[1] = evu[i][1];
+        ev[2] = evu[i][2];
       } else {
         bt_entry(P, Q, r[i].x, r[i].y >> 16, (r[i].y >> 8) & 31, v, ev);
       }
