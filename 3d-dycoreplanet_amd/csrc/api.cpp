@@ -1266,6 +1266,9 @@ bool build_sell_structured(Ctx& c, const std::vector<int32_t>& Sp, const std::ve
   for (double r : ur)
     if (lev.empty() || r > lev.back() * (1 + 1e-10)) lev.push_back(r);
   const int nl = int(lev.size());
+  // the structured SpMV steps through a row's slots with at most 3 wraps per
+  // step (linalg.hip SlotPos), which needs >= 3 levels in reach of every row
+  if (nl < 3) return false;
   std::vector<int32_t> level(static_cast<size_t>(n));
   for (int p = 0; p < n; ++p)
     level[p] = int32_t(std::lower_bound(lev.begin(), lev.end(), rad[p] * (1 - 1e-10)) - lev.begin());

@@ -343,10 +343,15 @@ __device__ inline double2 sell_ld(const double2* p) {
 struct SlotPos {  // entry k = nd j + d of a structured row (nd levels in reach)
   int j, d, nd;
   __device__ void step(int n) {  // k += n, 0 <= n <= 8
+    // nd >= 3 and d <= 6 before a step, so at most 3 wraps: three selects
+    // (a while loop here put a branch between the slice's address
+    // computations and cost 0.7 us per S apply, profiles/r05/r05ae_*)
     d += n;
-    while (d >= nd) {
-      d -= nd;
-      ++j;
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const bool wr = d >= nd;
+      d = wr ? d - nd : d;
+      j = wr ? j + 1 : j;
     }
   }
 };
