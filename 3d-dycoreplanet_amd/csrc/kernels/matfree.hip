@@ -1044,6 +1044,31 @@ constexpr int kGatherWaves = DCP_MF_GWAVES;
 constexpr int kGvSpan = DCP_MF_GSPAN;  // doubles per wave window (longer spans: direct reads)
 // Gather wave w (velocity windows first, then pressure windows); W: the
 // wave's LDS window (kGvSpan doubles). FUSED: records read agent-coherent.
+// the wave's record window into LDS: DCP_MF_WIN_UNROLL (default) issues all of
+// a lane's window loads (kGvSpan / 64 of them, clamped to the window) before
+// the LDS writes, instead of one load-wait-write per loop trip (r=5 Stokes
+// apply 156.6-160.9 -> 152.8-153.0 us in tools/mf_probe.py, bitwise;
+// profiles/r05/r05af_mf_window_variants.log)
+#ifndef DCP_MF_WIN_UNROLL
+#define DCP_MF_WIN_UNROLL 1
+#endif
+template <bool FUSED>
+__device__ __forceinline__ void load_window(const double* __restrict__ b, int len, double* W,
+                                            int lane) {
+  if (DCP_MF_WIN_UNROLL) {
+    if (len <= 0) return;
+    constexpr int U = kGvSpan / 64;
+    double t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = rec_load(b + min(lane + 64 * u, len - 1), FUSED);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (lane + 64 * u < len) W[lane + 64 * u] = t[u];
+  } else {
+    for (int i = lane; i < len; i += 64) W[i] = rec_load(b + i, FUSED);
+  }
+}
+
 template <bool STOKES, bool FUSED>
 __device__ __forceinline__ void gather_body(const MfGather& g, int w, int v0, int v1, int p0,
                                             int p1, const double* __restrict__ buf,
@@ -1057,8 +1082,7 @@ __device__ __forceinline__ void gather_body(const MfGather& g, int w, int v0, in
     const int len = 3 * (g.vptr[n1] - s0);
     const double* b = buf + 3 * size_t(s0);
     const bool fits = len <= kGvSpan;
-    if (fits)
-      for (int i = lane; i < len; i += 64) W[i] = rec_load(b + i, FUSED);
+    if (fits) load_window<FUSED>(b, len, W, lane);
     wsync();
     const int pos = n0 + lane;
     if (pos >= n1) return;
@@ -1104,8 +1128,7 @@ __device__ __forceinline__ void gather_body(const MfGather& g, int w, int v0, in
     const int len = g.pptr[j1] - s0;
     const double* b = buf + g.pbase + s0;
     const bool fits = len <= kGvSpan;
-    if (fits)
-      for (int i = lane; i < len; i += 64) W[i] = rec_load(b + i, FUSED);
+    if (fits) load_window<FUSED>(b, len, W, lane);
     wsync();
     const int pos = j0 + lane;
     if (pos >= j1) return;
