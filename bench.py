@@ -55,7 +55,7 @@ PMC_SUMMARIES = {(5, "explicit"): ("profiles/r04j_pmc_inner_r5.json", "k_sell_sp
 # PMC (2 FETCH + WRITE) of the same launches (tools/pmc_inner.sh)
 CHAIN_PMC = {(5, "sstep"): "profiles/r05/r05ab_pmc_inner_sstep_r5.json"}
 CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
-               (5, "sstep"): "profiles/r05/r05w_bench_r5_kernel_stats.csv"}
+               (5, "sstep"): "profiles/r05/r05zd_bench_r5_kernel_stats.csv"}
 # the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
 # launches per assembly (the rhs kernel once per colour class)
 PMC_ASM = {5: ("profiles/r05/r05i_pmc_asm_r5.json",
