@@ -411,9 +411,13 @@ void build_mf_fused(Ctx& c, int n_cells, int nv, int n_p, const std::vector<int3
                     int32_t pbase) {
   c.mf_fused = false;
   c.mf_ntasks = 0;
-  // off by default: measured slower than the two launches
+  // off by default: measured slower than the two launches;
+  // tested on one-GPU shells only, so partitioned and periodic meshes keep the
+  // two launches
   const char* env = std::getenv("DCP_MF_FUSED");
-  if (!(env && *env == '1') || c.mf_chunks != 1 || kMfGroupCells != 7 || n_cells <= 0) return;
+  if (!(env && *env == '1') || c.mf_chunks != 1 || kMfGroupCells != 7 || n_cells <= 0 ||
+      c.comm || c.periodic)
+    return;
   const int n_pen = (n_cells + 6) / 7;
   const int nvw = (nv + 63) / 64, npw = (n_p + 63) / 64, nw = nvw + npw;
   // slot -> batch of the records
@@ -1888,6 +1892,8 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
     c.dim2 = false;
     c.vdim = 3;
     c.tdpc3 = h.tdpc;
+    c.tsep = false;
+    c.ts_tmat_valid = false;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -2232,6 +2238,11 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           for (size_t i = 0; i < layR.size(); ++i) rs[i] = std::sqrt(layR[i]);
           c.mf_colphin.upload(pn);
           c.mf_layRs.upload(rs);
+          // the temperature system in Kronecker form (kernels/temperature_sep.hip);
+          // DCP_T_SEPARABLE=0 keeps the colour kernels
+          const char* env_ts = std::getenv("DCP_T_SEPARABLE");
+          if (!c.periodic && h.tdpc == 8 && !(env_ts && *env_ts == '0'))
+            build_tsep(c, n_cells, td, col, layer, layR, Tfix, Tp, Tc, n_T);
         } else {
           // general mesh: J^-1 / JxW per Gauss point, tree order (2160 B per cell)
           c.mf_geo_tree.alloc(size_t(n_cells) * 270);
@@ -2762,6 +2773,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       image_diagonal_blocks(c.n_img_node, c.img_node.p, c.img_blk.p, c.mf_cidx.p, c.con_diag.p,
                             c.A_val.p, c.stream);
     t.stop();
+    if (rhs_co && c.mf_fused && c.hmapped) {
+      // the fused rhs's poll-timeout flag belongs to this call, not a later one
+      DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+      check_mf_err(c);
+    }
     if (matrix) {
       // else B = (B^T)^T, materialised when read
       c.B_current = out.B != nullptr;
@@ -2826,11 +2842,21 @@ int dcp_assemble_temperature_matrix(dcp_ctx* ctx) {
       c.T_matrix_ok = true;
       return DCP_OK;
     }
-    c.Tmass.zero(c.stream);
-    c.Tstiff.zero(c.stream);
-    for (int k = 0; k < c.n_colors(); ++k)
-      launch_T_matrix(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.ph, c.Tmass.p,
-                      c.Tstiff.p, c.periodic ? c.posTs.p : nullptr, c.stream);
+    c.ts_tmat_valid = false;
+    if (c.tsep && !c.feec) {
+      // Kronecker form: M, K, and T_matrix = M + dt K with its Jacobi inverse
+      // (the first lines of assemble_temperature_rhs, :975-986) in one pass
+      tsep_matrix(c.tsd(), long(c.Tmat.n), c.ph, c.Tmass.p, c.Tstiff.p, c.Tmat.p, c.T_inv.p,
+                  c.stream);
+      c.ts_tmat_valid = true;
+      c.ts_tmat_dt = c.ph.dt_T;
+    } else {
+      c.Tmass.zero(c.stream);
+      c.Tstiff.zero(c.stream);
+      for (int k = 0; k < c.n_colors(); ++k)
+        launch_T_matrix(c.cd(), c.maps(), c.color_begin(k), c.color_size(k), c.ph, c.Tmass.p,
+                        c.Tstiff.p, c.periodic ? c.posTs.p : nullptr, c.stream);
+    }
     t.stop();
     c.T_matrix_ok = true;
     return DCP_OK;
@@ -2844,12 +2870,21 @@ int dcp_assemble_temperature_rhs(dcp_ctx* ctx) {
     require(c.T_matrix_ok, DCP_ERR_STATE, "assemble the temperature matrices first");
     SectionScope sec(c, "   Assemble temperature RHS");
     PhaseTimer t(c, &c.timings.assemble_T_rhs_ms);
-    // T_matrix = M + dt/interval K ; Jacobi rebuilt (:975-986)
-    lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
-    csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
-    c.T_rhs.zero(c.stream);
+    // T_matrix = M + dt/interval K ; Jacobi rebuilt (:975-986), unless the
+    // separable matrix assembly formed both with this dt
+    if (!(c.ts_tmat_valid && c.ts_tmat_dt == c.ph.dt_T)) {
+      lincomb(int(c.Tmat.n), c.Tmass.p, c.ph.dt_T, c.Tstiff.p, c.Tmat.p, c.stream);
+      csr_diag_inverse(c.n_T, c.T_ptr.p, c.T_col.p, c.Tmat.p, c.T_inv.p, c.stream);
+    }
     if (!c.old_T_ghosted) halo_exchange(c, c.halo_T, c.old_T.p);
     halo_exchange(c, c.halo_nse, c.nse_sol.p);
+    if (c.tsep && !c.feec && !c.dim2) {
+      tsep_rhs(c.tsd(), c.cd(), c.n_T, c.old_T.p, c.nse_sol.p, c.ph, c.T_rhs.p, c.stream);
+      t.stop();
+      c.T_rhs_ok = true;
+      return DCP_OK;
+    }
+    c.T_rhs.zero(c.stream);
     if (c.dim2) {
       assemble_T_rhs_2d(c);
       t.stop();
@@ -2882,7 +2917,12 @@ int dcp_solve_nse_schur(dcp_ctx* ctx, int* schur_iterations, int* a_solves) {
     require(c.nse_assembled, DCP_ERR_STATE, "assemble_nse_system must run first");
     SectionScope sec(c, "   Solve NSE system");
     PhaseTimer t(c, &c.timings.solve_nse_ms);
-    return solve_nse_schur(c, schur_iterations, a_solves);
+    const int rc = solve_nse_schur(c, schur_iterations, a_solves);
+    if (c.mf_fused) {
+      DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+      check_mf_err(c);
+    }
+    return rc;
   });
 }
 
@@ -3048,6 +3088,7 @@ int dcp_schur_vmult(dcp_ctx* ctx, const double* src, double* dst) {
     require(ctx->nse_assembled && ctx->precond_built, DCP_ERR_STATE, "operator not ready");
     schur_vmult(*ctx, src, dst);
     DCP_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    check_mf_err(*ctx);
     return DCP_OK;
   });
 }
@@ -3351,6 +3392,19 @@ int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permute
     if (col_bytes) *col_bytes = c.S_nbr.p ? 0 : c.S_sell_c16.p ? 2 : 4;
     if (stored) *stored = int64_t(c.S_val.n);
     if (permuted) *permuted = c.S_perm.p != nullptr;
+    return DCP_OK;
+  });
+}
+
+int dcp_temperature_layout(dcp_ctx* ctx, int64_t info[6]) {
+  return guarded(ctx, [&] {
+    need_ready(*ctx);
+    require(info != nullptr, DCP_ERR_INVALID, "NULL info");
+    const Ctx& c = *ctx;
+    const bool on = c.tsep && !c.feec && !c.dim2;
+    const int64_t v[6] = {on ? 1 : 0, on ? c.ts_n_colids : 0, on ? c.ts_n_layers : 0,
+                          on ? c.ts_n_kinds : 0, on ? c.ts_n_latnnz : 0, 0};
+    for (int i = 0; i < 6; ++i) info[i] = v[i];
     return DCP_OK;
   });
 }

@@ -7,6 +7,9 @@
 #include <vector>
 
 #include <memory>
+#include <mutex>
+#include <thread>
+#include <utility>
 
 #include "../../include/dcp.h"
 #include "comm.h"
@@ -21,27 +24,46 @@ struct ApiError {
   std::string msg;
 };
 
-// Device bytes held by the buffers the calling host thread allocated (one
-// rank = one thread in an in-process group): dcp_device_memory.
+// Device bytes held by the buffers each host thread allocated (one rank = one
+// thread in an in-process group): dcp_device_memory reports the calling
+// thread's. One process-wide table behind a mutex, each buffer remembering its
+// allocating thread, so a buffer freed on another thread (e.g. a context closed
+// by Python's GC) is still taken off its owner's count.
 struct DevMemTrack {
   int64_t live = 0, peak = 0;
-  std::unordered_map<const void*, int64_t> sizes;
 };
-inline DevMemTrack& dev_mem() {
-  static thread_local DevMemTrack t;
-  return t;
+struct DevMemTable {
+  std::mutex mu;
+  std::unordered_map<std::thread::id, DevMemTrack> per_thread;
+  std::unordered_map<const void*, std::pair<int64_t, std::thread::id>> sizes;
+};
+inline DevMemTable& dev_mem_table() {
+  static DevMemTable* t = new DevMemTable;  // never destroyed: frees may run during exit
+  return *t;
+}
+inline DevMemTrack dev_mem() {
+  DevMemTable& t = dev_mem_table();
+  std::lock_guard<std::mutex> lock(t.mu);
+  auto it = t.per_thread.find(std::this_thread::get_id());
+  return it == t.per_thread.end() ? DevMemTrack{} : it->second;
 }
 inline void dev_mem_alloc(const void* p, size_t bytes) {
-  DevMemTrack& t = dev_mem();
-  t.sizes[p] = int64_t(bytes);
-  t.live += int64_t(bytes);
-  if (t.live > t.peak) t.peak = t.live;
+  DevMemTable& t = dev_mem_table();
+  const auto me = std::this_thread::get_id();
+  std::lock_guard<std::mutex> lock(t.mu);
+  auto old = t.sizes.find(p);
+  if (old != t.sizes.end()) t.per_thread[old->second.second].live -= old->second.first;
+  t.sizes[p] = {int64_t(bytes), me};
+  DevMemTrack& m = t.per_thread[me];
+  m.live += int64_t(bytes);
+  if (m.live > m.peak) m.peak = m.live;
 }
 inline void dev_mem_free(const void* p) {
-  DevMemTrack& t = dev_mem();
+  DevMemTable& t = dev_mem_table();
+  std::lock_guard<std::mutex> lock(t.mu);
   auto it = t.sizes.find(p);
-  if (it == t.sizes.end()) return;  // allocated on another thread
-  t.live -= it->second;
+  if (it == t.sizes.end()) return;
+  t.per_thread[it->second.second].live -= it->second.first;
   t.sizes.erase(it);
 }
 
@@ -333,6 +355,41 @@ struct Ctx {
   MfData mfd() const {
     return MfData{n_u, mf_q2.p, mf_p.p, vcon.p, mf_geo.p, mf_first.p};
   }
+  // separable temperature assembly (tsep.cpp, kernels/temperature_sep.hip): set at upload
+  // when the local cells are the full column x layer product of a separable
+  // shell with FE_Q(1) temperature and no periodic identification
+  bool tsep = false;
+  int ts_n_colids = 0, ts_n_layers = 0, ts_n_kinds = 0, ts_n_latnnz = 0;
+  DBuf<int32_t> ts_ord2lay, ts_lay2ord, ts_kind, ts_kc, ts_lptr, ts_lcon, ts_sptr, ts_slot;
+  DBuf<uint32_t> ts_code;
+  DBuf<double> ts_loc, ts_rad, ts_A, ts_rec;
+  bool ts_tmat_valid = false;  // Tmat / T_inv of the last matrix assembly, made with ts_tmat_dt
+  double ts_tmat_dt = 0.0;
+  TSepDev tsd() const {
+    TSepDev t;
+    t.n_colids = ts_n_colids;
+    t.n_layers = ts_n_layers;
+    t.n_kinds = ts_n_kinds;
+    t.n_latnnz = ts_n_latnnz;
+    t.colgeo = mf_colgeo.p;
+    t.laygeo = mf_laygeo.p;
+    t.layR = mf_layR.p;
+    t.ord2lay = ts_ord2lay.p;
+    t.lay2ord = ts_lay2ord.p;
+    t.kind = ts_kind.p;
+    t.kc = ts_kc.p;
+    t.lptr = ts_lptr.p;
+    t.lcon = ts_lcon.p;
+    t.code = ts_code.p;
+    t.T_col = T_col.p;
+    t.sptr = ts_sptr.p;
+    t.slot = ts_slot.p;
+    t.loc = ts_loc.p;
+    t.rad = ts_rad.p;
+    t.A = ts_A.p;
+    t.rec = ts_rec.p;
+    return t;
+  }
   // state
   DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;
   DBuf<double> A_diag, Mp_diag, A_inv, Mp_inv, T_inv;
@@ -532,6 +589,11 @@ void assemble_T_rhs_2d(Ctx& c);
 void distribute_nse_2d(Ctx& c, double* x);
 void nse_matrix_export_2d(Ctx& c, int64_t* nnz, int32_t* rowptr, int32_t* cols, double* vals);
 void cell_nse_system_2d(Ctx& c, int first, int n, double* K, double* f);
+// tsep.cpp: the separable temperature tables (false: keep the colour kernels)
+bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td, const std::vector<int32_t>& col,
+                const std::vector<int32_t>& layer, const std::vector<double>& layR,
+                const std::vector<uint8_t>& Tfix, const std::vector<int32_t>& Tp,
+                const std::vector<int32_t>& Tc, int n_T);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
 // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414)

@@ -309,6 +309,39 @@ void launch_T2_rhs(const CellData& cd, const int32_t* cells, int n, const double
                    const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
 void launch_T_rhs(const CellData& cd, const int32_t* cells, int n, const double* T_old,
                   const double* u_cur, const PhysicsDev& ph, double* rhs, hipStream_t s);
+
+// Temperature system on a radially separable mesh that is the full product of
+// columns and layers (kernels/temperature_sep.hip: Kronecker-form assembly; tsep.cpp
+// builds the tables at upload).
+struct TSepDev {
+  int n_colids = 0;   // column ids of the separable geometry (mapping kinds apart)
+  int n_layers = 0;   // radial layers; levels 0..n_layers
+  int n_kinds = 0;    // mapping kinds of the layers
+  int n_latnnz = 0;   // entries of the lateral pattern
+  const double* colgeo = nullptr;   // separable tables (CellData::sep_*)
+  const double* laygeo = nullptr;
+  const double* layR = nullptr;
+  const int32_t* ord2lay = nullptr;  // [n_layers] layer id of radial ordinal o
+  const int32_t* lay2ord = nullptr;  // [layer ids] ordinal
+  const int32_t* kind = nullptr;     // [n_layers] mapping kind of ordinal o
+  const int32_t* kc = nullptr;       // [lateral columns][n_kinds] column id
+  const int32_t* lptr = nullptr;     // [n_latnnz + 1]
+  const int32_t* lcon = nullptr;     // lateral column << 4 | alpha << 2 | beta
+  const uint32_t* code = nullptr;    // [nnz of T] (k_tsep_matrix)
+  const int32_t* T_col = nullptr;
+  const int32_t* sptr = nullptr;     // [n_T + 1] records of each T dof
+  const int32_t* slot = nullptr;     // 8 cell + a, ascending cell
+  double* loc = nullptr;             // [n_colids][64] lateral tables
+  double* rad = nullptr;             // [n_layers][16] radial tables
+  double* A = nullptr;               // [n_kinds][n_latnnz][5]
+  double* rec = nullptr;             // [n_cells][8] rhs records
+};
+// M, K, T_matrix = M + dt_T K and its Jacobi inverse (every entry written)
+void tsep_matrix(const TSepDev& t, long nnz, const PhysicsDev& ph, double* M, double* K,
+                 double* Tmat, double* Tinv, hipStream_t s);
+// the temperature rhs (overwritten; needs tsep_matrix's tables)
+void tsep_rhs(const TSepDev& t, const CellData& cd, int n_T, const double* T_old,
+              const double* u, const PhysicsDev& ph, double* rhs, hipStream_t s);
 // Builds posA/posBt/posB/posT by binary search in the sorted patterns.
 void launch_build_scatter_maps(const CellData& cd, const int32_t* A_ptr, const int32_t* A_col,
                                const int32_t* Bt_ptr, const int32_t* Bt_col, const int32_t* B_ptr,

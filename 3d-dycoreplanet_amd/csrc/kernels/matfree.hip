@@ -1009,10 +1009,12 @@ __device__ __forceinline__ void pencil_body(const MfCells& mc, int blk, int c0, 
   }
   if (FUSED) {
     // every record store of the batch acknowledged, then its flag
+    // (release: the record stores are ordered before the flag by the memory
+    // model, not only by this wait)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (kPenWaves > 1) __syncthreads();
     if (threadIdx.x == 0)
-      __hip_atomic_store(done + blk, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done + blk, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1190,7 +1192,7 @@ __global__ __launch_bounds__(64, DCP_MF_WAVES_PER_EU) void k_mf_fused(
   for (int i = d0 + lane; i < d1; i += 64) {
     const unsigned* flag = f.done + f.dep[i];
     long spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq) {
       if (++spins > f.spin_limit) {
         late = true;
         break;
@@ -1198,6 +1200,9 @@ __global__ __launch_bounds__(64, DCP_MF_WAVES_PER_EU) void k_mf_fused(
       __builtin_amdgcn_s_sleep(1);
     }
   }
+  // acquire for the whole wave: every lane's polled flags happen-before the
+  // window reads of gather_body, whichever lane observed them
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (__any(late) && lane == 0) *f.err = 1.0;
   gather_body<STOKES, true>(g, kind == 1 ? idx : ((g.n_vnodes + 63) >> 6) + idx, 0, g.n_vnodes, 0,
                             g.n_p, buf, src, dst, lds[0]);

@@ -62,7 +62,8 @@ EXPORTED = [
     "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
-    "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_feec_partition_info",
+    "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_temperature_layout",
+    "dcp_feec_partition_info",
     "dcp_mesh2d_partition_info", "dcp_time_operator",
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
     "dcp_timer_section", "dcp_timer_record", "dcp_timer_reset",
@@ -259,6 +260,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 5
     lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int)]
+    lib.dcp_temperature_layout.argtypes = [P, P]
     lib.dcp_scatter_info.argtypes = [P, P, P, P]
     lib.dcp_matrix_powers_info.argtypes = [P, P]
     lib.dcp_device_memory.argtypes = [P, P]
@@ -1356,6 +1358,13 @@ class Context:
         cb, st, pm = C.c_int(), C.c_int64(), C.c_int()
         self._check(lib().dcp_schur_layout(self._h, C.byref(cb), C.byref(st), C.byref(pm)))
         return {"col_bytes": cb.value, "stored": st.value, "permuted": bool(pm.value)}
+
+    def temperature_layout(self) -> dict:
+        """dcp_temperature_layout: which temperature assembly runs."""
+        v = np.zeros(6, np.int64)
+        self._check(lib().dcp_temperature_layout(self._h, _ptr(v)))
+        return {"separable": bool(v[0]), "column_ids": int(v[1]), "layers": int(v[2]),
+                "kinds": int(v[3]), "lateral_entries": int(v[4])}
 
     def timings(self) -> dict:
         t = Timings()

@@ -221,6 +221,9 @@ def parse():
                     help="rehearsal: every rank on device 0 (one-GPU box), gloo bootstrap")
     ap.add_argument("--probe-schur", type=int, default=0,
                     help="PMC probe: only N Schur-complement applies after one assembly")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launch rehearsal: every rank sets up torch.distributed (gloo) and the "
+                         "communicator id broadcast, reports its env and stops before any GPU call")
     args = ap.parse_args()
     argv = sys.argv[1:]
     args.refine_set = any(a.startswith("--refine") for a in argv)
@@ -426,34 +429,140 @@ def converging_leg(make_ctx, args, refine=3):
             "schur_apply_ms_avg": t["schur_apply_ms_avg"]}
 
 
+def free_port():
+    """A free TCP port on 127.0.0.1 for the ranks' rendezvous."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without a launcher: start the N rank processes here,
+    one per GPU, as torch.distributed.run would (the reference's `mpirun -np N`
+    of source/main.cxx:64-65, one MPI rank per p::d::Triangulation part,
+    planet_geometry.tpp:13-20). The parent touches neither HIP nor torch: it
+    only sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT for
+    each child (the same script and arguments), lets them write to its own
+    stdout / stderr (rank 0 prints the one JSON line), waits, and exits with the
+    first non-zero child status. No exec: the children are new processes. A
+    rank that fails leaves the others up to 120 s to finish before they are
+    killed, so a rank stuck in a collective cannot hang the job."""
+    import subprocess
+    n = args.gpus
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": port, "DCP_BENCH_CHILD": "1"})
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)]
+                                      + sys.argv[1:], env=env))
+    rc, failed_at = 0, None
+    while any(p.poll() is None for p in procs):
+        for p in procs:
+            if p.returncode not in (None, 0) and rc == 0:
+                rc, failed_at = p.returncode, time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > 120:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    for p in procs:
+        if p.returncode != 0 and rc == 0:
+            rc = p.returncode
+    if rc != 0:
+        print(f"[bench] launch of {n} ranks failed: exit statuses "
+              f"{[p.returncode for p in procs]}", file=sys.stderr, flush=True)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def init_dist(args):
-    """One process per GPU (torchrun env); the library's own RCCL communicator
-    is created from rank 0's unique id broadcast through torch.distributed."""
+    """One process per GPU (torchrun env, or launch_ranks); the library's own
+    RCCL communicator is created from rank 0's unique id broadcast through
+    torch.distributed. dry: gloo and a random id, nothing touches a GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dry = args.dry_launch
+    host_only = args.shared_device or dry
     dist = None
     if args.shared_device:
         local_rank = 0
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         import torch
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("gloo" if args.shared_device else "nccl")
-    tdev = "cpu" if args.shared_device else "cuda"
-    import dcp
+        if not host_only:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo" if host_only else "nccl")
+        assert dist.get_world_size() == world and dist.get_rank() == rank
+    tdev = "cpu" if host_only else "cuda"
     nccl_id = None
     if world > 1:
         import torch
         idt = torch.zeros(128, dtype=torch.uint8, device=tdev)
         if rank == 0:
-            idt.copy_(torch.frombuffer(bytearray(dcp.nccl_unique_id()), dtype=torch.uint8))
+            raw = os.urandom(128) if dry else __import__("dcp").nccl_unique_id()
+            idt.copy_(torch.frombuffer(bytearray(raw), dtype=torch.uint8))
         dist.broadcast(idt, 0)
         nccl_id = bytes(idt.cpu().numpy().tobytes())
+    if dry:
+        return world, rank, dist, tdev, nccl_id
+
+    import dcp
 
     def make_ctx():
         return dcp.Context(device=local_rank, rank=rank, world_size=world, nccl_id=nccl_id)
     return world, rank, dist, tdev, make_ctx
+
+
+def dry_launch(args):
+    """--dry-launch: the N>1 launch up to the communicator id, no GPU. Every
+    rank reports what it got; rank 0 prints them as one JSON line."""
+    import hashlib
+    world, rank, dist, _, nccl_id = init_dist(args)
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "world_size": world, "pid": os.getpid(),
+            "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+            "backend": dist.get_backend() if dist is not None else None,
+            "nccl_id_sha": hashlib.sha256(nccl_id).hexdigest()[:16] if nccl_id else None,
+            "gpu_touched": "dcp" in sys.modules or (
+                "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized())}
+    gathered = [mine]
+    if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "n_gpus": args.gpus, "world_size": world,
+                          "ranks": gathered}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    if os.environ.get("DCP_BENCH_DRY_FAIL_RANK") == str(rank):
+        sys.exit(3)  # test hook: a rank that fails after the rendezvous
+
+
+def check_comm(ctx, args, world, rank, dist):
+    """Every rank's communicator must span the N ranks with one device per
+    rank (the reference's one MPI rank per process): a SCALE line that is
+    really N single-GPU runs, or N ranks on one device, is refused."""
+    info = ctx.comm_info()
+    if world == 1:
+        return [info]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, info)
+    counts = sorted({g["ranks"] for g in gathered})
+    devices = [g["device"] for g in gathered]
+    bad = []
+    if counts != [world]:
+        bad.append(f"communicator sizes {counts} != [{world}]")
+    if [g["rank"] for g in gathered] != list(range(world)):
+        bad.append(f"communicator ranks {[g['rank'] for g in gathered]}")
+    if not args.shared_device and len(set(devices)) != world:
+        bad.append(f"devices {devices} are not distinct")
+    if bad:
+        raise SystemExit(f"[bench rank {rank}] bad multi-GPU launch: " + "; ".join(bad))
+    return gathered
 
 
 def run_feec(args):
@@ -475,6 +584,7 @@ def run_feec(args):
                      temperature_degree=ph.temperature_degree, feec=True)
     f = m.feec
     ctx = make_ctx()
+    check_comm(ctx, args, world, rank, dist)
     ctx.set_physics(ph)
     ctx.upload_feec_mesh(m)
     ctx.set_feec_zero_mean(bool(rp.correct_pressure_to_zero_mean))
@@ -549,6 +659,11 @@ def progress(msg):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_launch:
+        dry_launch(args)
+        return
     if args.variant == "feec":
         run_feec(args)
         return
@@ -562,6 +677,7 @@ def main():
                      temperature_degree=ph.temperature_degree)
     progress(f"host mesh refine {args.refine}: {m.n_cells} cells")
     ctx = make_ctx()
+    comm_seen = check_comm(ctx, args, world, rank, dist)
     ctx.set_physics(ph)
     ctx.set_schur_explicit(args.schur == "explicit")
     ctx.set_gram_schmidt(args.gram_schmidt)
@@ -902,6 +1018,11 @@ def main():
         dist.all_gather_object(gathered, mine)
         out["ranks"] = gathered
         out["comm_ranks_reported"] = sorted({g["comm"]["ranks"] for g in gathered})
+        out["comm_devices"] = [g["device"] for g in comm_seen]
+        out["launcher"] = ("bench.py --gpus (launch_ranks)" if os.environ.get("DCP_BENCH_CHILD")
+                           else "external (torch.distributed.run)")
+        if out["comm_ranks_reported"] != [world]:
+            raise SystemExit(f"comm_ranks_reported {out['comm_ranks_reported']} != [{world}]")
         # DESIGN.md section 6 "Cost at P=8, r=5": the expected strong-scaling
         # efficiency of each phase (budgeted, not measured)
         out["design_expectation"] = {
@@ -927,5 +1048,19 @@ def main():
         dist.destroy_process_group()
 
 
+def print_maps():
+    """DCP_BENCH_MAPS=1: the executable mappings of this process on stderr, to
+    place the frames of a crash at exit (their libraries) after the fact."""
+    if os.environ.get("DCP_BENCH_MAPS") != "1":
+        return
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and "x" in parts[1]:
+                print("[maps] " + parts[0] + " " + parts[5], file=sys.stderr)
+    sys.stderr.flush()
+
+
 if __name__ == "__main__":
     main()
+    print_maps()

@@ -696,7 +696,8 @@ def test_assembly_timing_switches_keep_constrained_diagonals(switch):
 @pytest.mark.parametrize("kind,lag", [("shell-r3", None), ("shell-r3", "0"), ("shell-r2", "1000000000"),
                                       ("warped-r2", None)])
 def test_fused_matrix_free_apply_is_the_two_launch_apply(monkeypatch, kind, lag):
-    """DCP_MF_FUSED (default): the matrix-free apply as ONE launch (k_mf_fused:
+    """DCP_MF_FUSED=1 (opt-in; off by default, slower than the two launches,
+    and refused on partitioned or periodic meshes): the matrix-free apply as ONE launch (k_mf_fused:
     pencil batches and gather windows in the upload's schedule, each window
     polling the done flags of the batches it reads) against the two launches
     (pencil kernel, then the gather kernel): the same sums in the same order,
