@@ -2242,7 +2242,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
           // DCP_T_SEPARABLE=0 keeps the colour kernels
           const char* env_ts = std::getenv("DCP_T_SEPARABLE");
           if (!c.periodic && h.tdpc == 8 && !(env_ts && *env_ts == '0'))
-            build_tsep(c, n_cells, td, col, layer, layR, Tfix, Tp, Tc, n_T);
+            build_tsep(c, n_cells, td, col, layer, layR, Tfix, Tbc, Tp, Tc, n_T);
         } else {
           // general mesh: J^-1 / JxW per Gauss point, tree order (2160 B per cell)
           c.mf_geo_tree.alloc(size_t(n_cells) * 270);

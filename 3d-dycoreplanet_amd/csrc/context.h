@@ -1,6 +1,7 @@
 // Device-resident state of one dcp_ctx (one GPU / rank).
 #pragma once
 #include <chrono>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <unordered_map>
@@ -359,8 +360,9 @@ struct Ctx {
   // when the local cells are the full column x layer product of a separable
   // shell with FE_Q(1) temperature and no periodic identification
   bool tsep = false;
-  int ts_n_colids = 0, ts_n_layers = 0, ts_n_kinds = 0, ts_n_latnnz = 0;
-  DBuf<int32_t> ts_ord2lay, ts_lay2ord, ts_kind, ts_kc, ts_lptr, ts_lcon, ts_sptr, ts_slot;
+  int ts_n_colids = 0, ts_n_layers = 0, ts_n_kinds = 0, ts_n_latnnz = 0, ts_n_con = 0;
+  DBuf<int32_t> ts_ord2lay, ts_lay2ord, ts_kind, ts_lptr, ts_lcon, ts_sptr, ts_slot;
+  DBuf<uint16_t> ts_cmask;
   DBuf<uint32_t> ts_code;
   DBuf<double> ts_loc, ts_rad, ts_A, ts_rec;
   bool ts_tmat_valid = false;  // Tmat / T_inv of the last matrix assembly, made with ts_tmat_dt
@@ -377,7 +379,10 @@ struct Ctx {
     t.ord2lay = ts_ord2lay.p;
     t.lay2ord = ts_lay2ord.p;
     t.kind = ts_kind.p;
-    t.kc = ts_kc.p;
+    t.n_con = ts_n_con;
+    const char* pr = std::getenv("DCP_TSEP_PROBE");
+    t.probe = pr ? std::atoi(pr) : 0;
+    t.cmask = ts_cmask.p;
     t.lptr = ts_lptr.p;
     t.lcon = ts_lcon.p;
     t.code = ts_code.p;
@@ -592,7 +597,8 @@ void cell_nse_system_2d(Ctx& c, int first, int n, double* K, double* f);
 // tsep.cpp: the separable temperature tables (false: keep the colour kernels)
 bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td, const std::vector<int32_t>& col,
                 const std::vector<int32_t>& layer, const std::vector<double>& layR,
-                const std::vector<uint8_t>& Tfix, const std::vector<int32_t>& Tp,
+                const std::vector<uint8_t>& Tfix, const std::vector<double>& Tbc,
+                const std::vector<int32_t>& Tp,
                 const std::vector<int32_t>& Tc, int n_T);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);

@@ -324,18 +324,23 @@ struct TSepDev {
   const int32_t* ord2lay = nullptr;  // [n_layers] layer id of radial ordinal o
   const int32_t* lay2ord = nullptr;  // [layer ids] ordinal
   const int32_t* kind = nullptr;     // [n_layers] mapping kind of ordinal o
-  const int32_t* kc = nullptr;       // [lateral columns][n_kinds] column id
+  int n_con = 0;                     // lateral contributions (per kind)
+  int probe = 0;                     // DCP_TSEP_PROBE timing variants (0: the real kernels)
   const int32_t* lptr = nullptr;     // [n_latnnz + 1]
-  const int32_t* lcon = nullptr;     // lateral column << 4 | alpha << 2 | beta
+  const int32_t* lcon = nullptr;     // [n_kinds][n_con] column id << 4 | alpha << 2 | beta
+  const uint16_t* cmask = nullptr;   // [n_cells] fixed vertices | lifted vertices << 8
   const uint32_t* code = nullptr;    // [nnz of T] (k_tsep_matrix)
   const int32_t* T_col = nullptr;
   const int32_t* sptr = nullptr;     // [n_T + 1] records of each T dof
   const int32_t* slot = nullptr;     // 8 cell + a, ascending cell
   double* loc = nullptr;             // [n_colids][64] lateral tables
   double* rad = nullptr;             // [n_layers][16] radial tables
-  double* A = nullptr;               // [n_kinds][n_latnnz][5]
+  double* A = nullptr;               // [n_kinds][n_latnnz][6] (M, ll, x, x^T, 22, pad)
   double* rec = nullptr;             // [n_cells][8] rhs records
 };
+// the lateral / radial tables of the column ids and layers (mesh geometry,
+// formed once at upload like the B^T column / layer factors)
+void tsep_tables(const TSepDev& t, hipStream_t s);
 // M, K, T_matrix = M + dt_T K and its Jacobi inverse (every entry written)
 void tsep_matrix(const TSepDev& t, long nnz, const PhysicsDev& ph, double* M, double* K,
                  double* Tmat, double* Tinv, hipStream_t s);

@@ -2072,10 +2072,16 @@ __device__ inline void bt_entry(const double* __restrict__ P, const double* __re
 #ifndef DCP_BT_PROBE
 #define DCP_BT_PROBE 0
 #endif
+// mode (DCP_BT_MODE, default 3): bit 0: the doubles of the task's first and
+// last 128-byte line stored plainly (the rest nontemporal), so the two tasks
+// sharing a line meet in one L2 instead of each writing the partial line to
+// HBM; bit 1: each XCD a contiguous range of workgroups (neighbouring tasks,
+// hence the shared lines, on the same XCD)
 template <int SL, int EL>
 __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
     CellData cd, int n_tasks, const int4* __restrict__ hdr, const int4* __restrict__ rec,
-    const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ Bt) {
+    const double* __restrict__ P, const double* __restrict__ Q, double* __restrict__ Bt,
+    int mode) {
   constexpr int R = SL / 8;             // slot records per lane
   constexpr int NE = 64 * EL;           // task entries (EL per lane)
   constexpr int FB = EL == 1 ? 6 : 7;   // bits per destination field of a record
@@ -2086,7 +2092,8 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
   __shared__ uint8_t vof[kBtRowWaves][SL][NE];
   __shared__ int rowl[kBtRowWaves][SL];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int task = int(blockIdx.x) * kBtRowWaves + wave;
+  const int blk = (mode & 2) ? xcd_block(int(blockIdx.x), int(gridDim.x)) : int(blockIdx.x);
+  const int task = blk * kBtRowWaves + wave;
   if (task >= n_tasks) return;
   const int k = lane >> 3, v = lane & 7;
   // records at SL task + slot (unused slots zero): header and record loads
@@ -2171,10 +2178,24 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
       if (acc[0] == 12345.0) dst[0] = Ca[0][0];  // keeps the work alive
       continue;
     }
+    if (mode & 1) {
+      // the task's piece spans doubles [3 h.x, 3 (h.x + ne)); its first and
+      // last 128-byte lines may be shared with the neighbouring tasks
+      const size_t first_line = (3 * size_t(h.x)) >> 4;
+      const size_t last_line = (3 * size_t(h.x + ne) - 1) >> 4;
 #pragma unroll
-    for (int jj = 0; jj < 3; ++jj)
-      __builtin_nontemporal_store(Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2],
-                                  dst + jj);
+      for (int jj = 0; jj < 3; ++jj) {
+        const double val = Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2];
+        const size_t line = (3 * size_t(h.x + j) + jj) >> 4;
+        if (line == first_line || line == last_line) dst[jj] = val;
+        else __builtin_nontemporal_store(val, dst + jj);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj)
+        __builtin_nontemporal_store(Ca[0][jj] * acc[0] + Ca[1][jj] * acc[1] + Ca[2][jj] * acc[2],
+                                    dst + jj);
+    }
 #elif DCP_BT_STORE
     out[q][0] = Ca[0][0] * acc[0] + Ca[1][0] * acc[1] + Ca[2][0] * acc[2];
     out[q][1] = Ca[0][1] * acc[0] + Ca[1][1] * acc[1] + Ca[2][1] * acc[2];
@@ -2396,10 +2417,12 @@ void launch_bt_rows(const CellData& cd, int n_cols, int n_layers, double* P, dou
     DCP_HIP_CHECK(hipGetLastError());
   }
   if (n_tasks > 0) {
+    const char* env = std::getenv("DCP_BT_MODE");
+    const int mode = env ? std::atoi(env) : 3;
     hipLaunchKernelGGL((slots == 32 ? k_bt_tasks<32, 2> : slots == 16 ? k_bt_tasks<16, 1> : k_bt_tasks<8, 1>),
                        dim3((n_tasks + kBtRowWaves - 1) / kBtRowWaves), dim3(64 * kBtRowWaves), 0,
                        s, cd, n_tasks, reinterpret_cast<const int4*>(task_hdr),
-                       reinterpret_cast<const int4*>(slot_rec), P, Q, Bt);
+                       reinterpret_cast<const int4*>(slot_rec), P, Q, Bt, mode);
     DCP_HIP_CHECK(hipGetLastError());
   }
 }

@@ -41,7 +41,8 @@ int find_root(std::vector<int32_t>& par, int x) {
 bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
                 const std::vector<int32_t>& col, const std::vector<int32_t>& layer,
                 const std::vector<double>& layR, const std::vector<uint8_t>& Tfix,
-                const std::vector<int32_t>& Tp, const std::vector<int32_t>& Tc, int n_T) {
+                const std::vector<double>& Tbc, const std::vector<int32_t>& Tp,
+                const std::vector<int32_t>& Tc, int n_T) {
   c.tsep = false;
   c.ts_tmat_valid = false;
   if (n_cells <= 0 || n_T <= 0 || td.size() != size_t(n_cells) * 8 || col.size() != size_t(n_cells) ||
@@ -156,7 +157,15 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
       lcolv.push_back(cons[k].w);
       lrow[size_t(cons[k].v) + 1]++;
     }
-    lcon.push_back((cons[k].C << 4) | cons[k].ab);
+    lcon.push_back(k);  // filled per kind below
+  }
+  // contributions as (column id of the kind) << 4 | alpha << 2 | beta, per kind
+  {
+    const size_t ncon = cons.size();
+    lcon.assign(ncon * NK, 0);
+    for (int k = 0; k < NK; ++k)
+      for (size_t j = 0; j < ncon; ++j)
+        lcon[k * ncon + j] = (kc[size_t(cons[j].C) * NK + k] << 4) | cons[j].ab;
   }
   lptr.push_back(int32_t(cons.size()));
   const int NLAT = int(lcolv.size());
@@ -193,15 +202,24 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
     for (int cell = 0; cell < n_cells; ++cell)
       for (int a = 0; a < 8; ++a) slot[fill[td[8 * size_t(cell) + a]]++] = 8 * cell + a;
   }
-  if (int64_t(n_cells) * 8 >= (int64_t(1) << 31)) return false;
+  if (int64_t(n_cells) * 8 >= (int64_t(1) << 31) || n_colids >= (1 << 27)) return false;
+  // per cell: bit a = vertex a fixed, bit 8 + a = fixed with a nonzero value (lifted)
+  std::vector<uint16_t> cmask(n_cells, 0);
+  for (int cell = 0; cell < n_cells; ++cell)
+    for (int a = 0; a < 8; ++a) {
+      const int i = td[8 * size_t(cell) + a];
+      if (Tfix[i]) cmask[cell] |= uint16_t(1u << a);
+      if (Tfix[i] && Tbc[i] != 0.0) cmask[cell] |= uint16_t(1u << (8 + a));
+    }
   c.ts_n_colids = n_colids;
   c.ts_n_layers = NL;
   c.ts_n_kinds = NK;
   c.ts_n_latnnz = NLAT;
+  c.ts_n_con = int(cons.size());
+  c.ts_cmask.upload(cmask);
   c.ts_ord2lay.upload(ord2lay);
   c.ts_lay2ord.upload(lay2ord);
   c.ts_kind.upload(kind);
-  c.ts_kc.upload(kc);
   c.ts_lptr.upload(lptr);
   c.ts_lcon.upload(lcon);
   c.ts_code.upload(code);
@@ -209,9 +227,10 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
   c.ts_slot.upload(slot);
   c.ts_loc.alloc(size_t(n_colids) * 64);
   c.ts_rad.alloc(size_t(NL) * 16);
-  c.ts_A.alloc(size_t(NK) * NLAT * 5);
+  c.ts_A.alloc(size_t(NK) * NLAT * 6);
   c.ts_rec.alloc(size_t(n_cells) * 8);
   c.tsep = true;
+  tsep_tables(c.tsd(), c.stream);
   return true;
 }
 

@@ -61,8 +61,34 @@ CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
 PMC_ASM = {5: ("profiles/r05/r05i_pmc_asm_r5.json",
                {"k_bt_tasks": 1, "k_mf_pencil": 1, "k_mf_gather": 1, "k_nse_rhs_halfwave": 1,
                 "k_con_gather": 1})}  # (k_bt_coltab runs once at upload)
-# the same for the matrix-free Stokes apply (pencil kernel + dof gather)
-PMC_MF = {5: ("profiles/r04j_pmc_mf_r5.json", ("k_mf_pencil<true", "k_mf_gather<true>"))}
+# the same for the matrix-free Stokes apply (pencil kernel + dof gather); the
+# kernel names must be found in the summary (no stale profile of other kernels)
+PMC_MF = {5: ("profiles/r06/r06_pmc_mf_r5.json", ("k_mf_pencil<true, true, false>",
+                                                  "k_mf_gather<true>"))}
+# rocprofv3 --kernel-trace of the default refine-5 step alone (bench.py
+# --no-converging-leg --no-other-gs --no-cpu-baseline), per-kernel durations
+# with the early-exit launches of stopped Krylov cycles split off
+# (tools/trace_summary.py): the source of roofline_chain and of the trace
+# cross-checks of the in-step HIP-event rooflines
+TRACE = {(5, "sstep"): "profiles/r06/r06_trace_r5.json"}
+
+
+def trace_summary(refine, gs):
+    path = TRACE.get((refine, gs))
+    if path is None or not os.path.exists(os.path.join(ROOT, path)):
+        return None
+    with open(os.path.join(ROOT, path)) as f:
+        d = json.load(f)
+    d["path"] = path
+    return d
+
+
+def trace_kernel(tr, key):
+    """The one kernel of the trace summary whose name contains key, or None."""
+    if tr is None:
+        return None
+    hits = [(k, v) for k, v in tr["kernels"].items() if key in k]
+    return hits[0] if len(hits) == 1 else None
 
 
 def pmc_asm_traffic(refine):
@@ -89,14 +115,19 @@ def pmc_asm_traffic(refine):
 
 def pmc_mf_traffic(refine):
     """HBM bytes of one matrix-free Stokes apply (both launches) from the
-    committed PMC summary, or None."""
+    committed PMC summary: (bytes, None), or (None, why)."""
     ent = PMC_MF.get(refine)
     if ent is None or not os.path.exists(os.path.join(ROOT, ent[0])):
-        return None
+        return None, "no PMC summary for this refinement"
     with open(os.path.join(ROOT, ent[0])) as f:
         tb = json.load(f)["traffic_bytes"]
-    parts = [sum(v for k, v in tb.items() if key in k) for key in ent[1]]
-    return sum(parts) if all(parts) else None
+    parts = []
+    for key in ent[1]:
+        hits = [v for k, v in tb.items() if key in k]
+        if len(hits) != 1:
+            return None, f"{ent[0]}: kernel {key!r} found {len(hits)} times (stale profile?)"
+        parts.append(hits[0])
+    return sum(parts), None
 
 
 def pmc_traffic(refine, mode, n_p):
@@ -137,6 +168,49 @@ def back_to_back_applies(ctx, ls, nvec=8, reps=48, batches=8, warm=3):
                    "one HIP event pair per batch, sources rotating over %d vectors of %d MB"
                    % (batches - warm, warm, reps, nvec, 8 * n // 1000000))
     return res
+
+
+def chain_roofline_trace(refine, n_p, gs):
+    """roofline_chain from the committed kernel trace of the default step
+    alone (TRACE): per k_sstep_block<KL> template the average over its working
+    launches (early exits of stopped cycles split off), bytes (KL + 5) 8 n_p."""
+    tr = trace_summary(refine, gs)
+    if tr is None or gs != "sstep":
+        return None
+    key = "k_sstep_block<"
+    rows = []
+    for name, v in tr["kernels"].items():
+        if key not in name:
+            continue
+        kl = int(name.split(key)[1].split(",")[0].split(">")[0])
+        rows.append((kl, v["full_calls"], v["avg_ns_full"], v["early_exit_calls"]))
+    if not rows:
+        return None
+    per = {kl: {"bytes": (kl + 5.0) * 8 * n_p, "avg_us": ns * 1e-3, "launches": c,
+                "early_exits_dropped": ee,
+                "achieved": (kl + 5.0) * 8 * n_p / (ns * 1e-9) / 1e9} for kl, c, ns, ee in rows}
+    tot_b = sum(c * (kl + 5.0) * 8 * n_p for kl, c, _, _ in rows)
+    tot_t = sum(c * ns * 1e-9 for _, c, ns, _ in rows)
+    ach = tot_b / tot_t / 1e9
+    out = {"kernel": "s-step block k_sstep_block<KL> (one launch per 4 inner Arnoldi columns: "
+                     "BCGS2 + Cholesky QR + Hessenberg/Givens)",
+           "bound": "hbm", "source": tr["path"], "rule": tr.get("early_exit_rule"),
+           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "per_template": per, "traffic": None}
+    pmc = CHAIN_PMC.get((refine, gs))
+    if pmc and os.path.exists(os.path.join(ROOT, pmc)):
+        with open(os.path.join(ROOT, pmc)) as f:
+            tb = json.load(f)["traffic_bytes"]
+        for name, v in tb.items():
+            if key in name:
+                kl = int(name.split(key)[1].split(",")[0].split(">")[0])
+                if kl in per:
+                    per[kl]["traffic"] = v
+        if all("traffic" in per[kl] for kl in per):
+            calls = {kl: c for kl, c, _, _ in rows}
+            out["traffic"] = sum(calls[kl] * per[kl]["traffic"] for kl in per) / sum(calls.values())
+            out["traffic_source"] = pmc
+    return out
 
 
 def chain_roofline(refine, n_p, gs):
@@ -207,6 +281,9 @@ def parse():
                     help="skip the back-to-back matrix-free apply timing after the steps")
     ap.add_argument("--no-converging-leg", action="store_true",
                     help="skip the converging refine-3 step (GMRES outer iter/s)")
+    ap.add_argument("--no-other-gs", action="store_true",
+                    help="skip the one-step legs of the other Gram-Schmidt variants (a kernel "
+                         "trace of the default step alone)")
     ap.add_argument("--schur", choices=["explicit", "composite"], default="explicit",
                     help="explicit: formed S = B D^-1 B^T (default); composite: B^T, Jacobi, B")
     ap.add_argument("--gram-schmidt", choices=["modified", "classical2", "dcgs2", "sstep"],
@@ -780,6 +857,8 @@ def main():
     # on several GPUs likewise (d + 1 all-reduces per column: seconds per step)
     other = []
     for other_gs in ("modified", "classical2", "dcgs2", "sstep"):
+        if args.no_other_gs:
+            break
         if other_gs == args.gram_schmidt or (other_gs == "modified" and
                                              (args.refine >= 6 or world > 1)):
             continue
@@ -952,7 +1031,19 @@ def main():
     else:
         out["roofline_assembly"]["traffic"] = asm_bytes
     if args.schur == "explicit" and world == 1:
-        out["roofline_chain"] = chain_roofline(args.refine, m.n_p, args.gram_schmidt)
+        out["roofline_chain"] = (chain_roofline_trace(args.refine, m.n_p, args.gram_schmidt)
+                                 or chain_roofline(args.refine, m.n_p, args.gram_schmidt))
+    # the headline roofline against the committed trace of the same step: the
+    # S SpMV's average over its working launches there
+    tk = trace_kernel(trace_summary(args.refine, args.gram_schmidt), "k_sell_spmv<true, 2>")
+    if tk and world == 1 and args.schur == "explicit":
+        t_ms = tk[1]["avg_ns_full"] * 1e-6
+        out["roofline"]["trace_check"] = {
+            "source": TRACE[(args.refine, args.gram_schmidt)], "kernel": tk[0].split("(")[0],
+            "launches": tk[1]["full_calls"], "early_exits_dropped": tk[1]["early_exit_calls"],
+            "avg_apply_ms": t_ms, "achieved": sbytes / (t_ms * 1e-3) / 1e9,
+            "frac": sbytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "line_over_trace": (achieved / (sbytes / (t_ms * 1e-3) / 1e9)) if t_ms > 0 else None}
     # matrix-free operator apply (north-star target, SURVEY §8d byte count):
     # src read + dst write per dof, int32 cell->dof map, J^-1 + JxW per point
     # (SURVEY's unit of work; the kernel recomputes the geometry instead of
@@ -964,10 +1055,13 @@ def main():
         nc = ls["cells"]  # the apply runs over every local cell (owned + ghost layers)
         st_bytes = 16 * (ls["n_u"] + ls["n_p"]) + 4 * 89 * nc + 80 * 27 * nc
         ve_bytes = 16 * ls["n_u"] + 4 * 27 * nc + 80 * 27 * nc
+        mf_traffic, mf_traffic_why = pmc_mf_traffic(args.refine) if world == 1 else (st_bytes, None)
         mf = {"kernel": "matrix-free [A B^T; B 0] x (k_mf_pencil<true> cell-order sum "
                         "factorisation + k_mf_gather dof gather)",
               "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
-              "traffic": pmc_mf_traffic(args.refine) if world == 1 else st_bytes,
+              "traffic": mf_traffic, "traffic_source": PMC_MF.get(args.refine, (None,))[0]
+              if world == 1 else "per-rank byte model",
+              "traffic_missing": mf_traffic_why,
               "bytes_per_apply": st_bytes, "avg_apply_ms": st_ms,
               "applies_per_step": recs[-1][4]["stokes_applies"],
               "achieved": st_bytes / (st_ms * 1e-3) / 1e9 if st_ms > 0 else None,
@@ -998,6 +1092,14 @@ def main():
                 mf["timing"] = b2b["what"]
         if ceil and mf["achieved"]:
             mf["frac_measured_read_ceiling"] = mf["achieved"] / ceil["read_GBps"]
+        tr = trace_summary(args.refine, args.gram_schmidt)
+        tp, tg = trace_kernel(tr, "k_mf_pencil<true, true, false>"), trace_kernel(tr, "k_mf_gather<true>")
+        if tp and tg and world == 1:
+            t_ms = (tp[1]["avg_ns_full"] + tg[1]["avg_ns_full"]) * 1e-6
+            mf["trace_check"] = {"source": tr["path"], "pencil_us": tp[1]["avg_ns_full"] * 1e-3,
+                                 "gather_us": tg[1]["avg_ns_full"] * 1e-3,
+                                 "avg_apply_ms": t_ms,
+                                 "frac": st_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         # the bytes the apply actually moves (PMC; the geometry is recomputed,
         # not read) over the same apply time
         mf["frac_actual_traffic"] = (mf["traffic"] / (mf["avg_apply_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
