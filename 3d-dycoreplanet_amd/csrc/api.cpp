@@ -1894,6 +1894,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
     c.tdpc3 = h.tdpc;
     c.tsep = false;
     c.ts_tmat_valid = false;
+    c.btk = false;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -2402,6 +2403,12 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             launch_bt_rows(c.cd(), c.bt_ncols, nlay, c.bt_P.p, c.bt_Q, 0, c.bt_slots, nullptr,
                            nullptr, nullptr, c.stream);
             c.bt_rows = true;
+            // one GPU: B^T in Kronecker form instead of the tasks
+            // (kernels/bt_kron.hip; DCP_BT_KRON=0 keeps the tasks)
+            const char* env_bk = std::getenv("DCP_BT_KRON");
+            c.btk = false;
+            if (!dist && nrows == nv && c.B_transpose && !(env_bk && *env_bk == '0'))
+              build_btk(c, n_cells, q2, pd, col, layer, layR, vc, Btp, Btc, nv, n_p);
           }
         }
       }
@@ -2716,8 +2723,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     const hipStream_t bt_stream = overlap == 1 || overlap == 2 ? c.mf_stream : c.stream;
     const hipStream_t con_stream = overlap == 3 ? c.mf_stream : c.stream;
     auto launch_bt = [&] {
-      launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
-                     c.bt_slot_rec.p, c.Bt_val.p, bt_stream);
+      if (c.btk)
+        btk_assemble(c.btkd(), long(c.Bt_val.n / 3), c.vcon.p, c.Bt_val.p, bt_stream);
+      else
+        launch_bt_rows(c.cd(), 0, 0, c.bt_P.p, c.bt_Q, c.bt_ntasks, c.bt_slots, c.bt_task_hdr.p,
+                       c.bt_slot_rec.p, c.Bt_val.p, bt_stream);
     };
     if (overlap) {
       DCP_HIP_CHECK(hipEventRecord(c.mf_chunk_ev[0], c.stream));
@@ -3396,15 +3406,17 @@ int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permute
   });
 }
 
-int dcp_temperature_layout(dcp_ctx* ctx, int64_t info[6]) {
+int dcp_assembly_layout(dcp_ctx* ctx, int64_t info[8]) {
   return guarded(ctx, [&] {
     need_ready(*ctx);
     require(info != nullptr, DCP_ERR_INVALID, "NULL info");
     const Ctx& c = *ctx;
     const bool on = c.tsep && !c.feec && !c.dim2;
-    const int64_t v[6] = {on ? 1 : 0, on ? c.ts_n_colids : 0, on ? c.ts_n_layers : 0,
-                          on ? c.ts_n_kinds : 0, on ? c.ts_n_latnnz : 0, 0};
-    for (int i = 0; i < 6; ++i) info[i] = v[i];
+    const bool bk = c.btk && !c.feec && !c.dim2;
+    const int64_t v[8] = {on ? 1 : 0, on ? c.ts_n_colids : 0, on ? c.ts_n_layers : 0,
+                          on ? c.ts_n_kinds : 0, on ? c.ts_n_latnnz : 0, bk ? 1 : 0,
+                          bk ? c.btk_n_pairs : 0, bk ? c.btk_n_conent : 0};
+    for (int i = 0; i < 8; ++i) info[i] = v[i];
     return DCP_OK;
   });
 }

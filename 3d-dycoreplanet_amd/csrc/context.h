@@ -395,6 +395,35 @@ struct Ctx {
     t.rec = ts_rec.p;
     return t;
   }
+  // B^T in Kronecker form (btkron.cpp, kernels/bt_kron.hip): set at upload on
+  // the one-GPU layered shell; then every assembly (operator form or full)
+  // takes B^T from it and B as its transpose
+  bool btk = false;
+  int btk_n_layers = 0, btk_n_kinds = 0, btk_n_pairs = 0, btk_n_con = 0, btk_n_conent = 0;
+  DBuf<int32_t> btk_ord2lay, btk_kind, btk_lptr, btk_lcon, btk_con_entry, btk_con_row;
+  DBuf<uint32_t> btk_code;
+  DBuf<double> btk_A;
+  BtkDev btkd() const {
+    BtkDev b;
+    b.n_layers = btk_n_layers;
+    b.n_kinds = btk_n_kinds;
+    b.n_pairs = btk_n_pairs;
+    b.n_con = btk_n_con;
+    b.n_conent = btk_n_conent;
+    const char* pr = std::getenv("DCP_BTK_PROBE");
+    b.probe = pr ? std::atoi(pr) : 0;
+    b.P = bt_P.p;
+    b.Q = bt_Q;
+    b.ord2lay = btk_ord2lay.p;
+    b.kind = btk_kind.p;
+    b.lptr = btk_lptr.p;
+    b.lcon = btk_lcon.p;
+    b.code = btk_code.p;
+    b.con_entry = btk_con_entry.p;
+    b.con_row = btk_con_row.p;
+    b.A = btk_A.p;
+    return b;
+  }
   // state
   DBuf<double> nse_sol, old_nse, T_sol, old_T, nse_rhs, T_rhs;
   DBuf<double> A_diag, Mp_diag, A_inv, Mp_inv, T_inv;
@@ -600,6 +629,11 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td, const std::
                 const std::vector<uint8_t>& Tfix, const std::vector<double>& Tbc,
                 const std::vector<int32_t>& Tp,
                 const std::vector<int32_t>& Tc, int n_T);
+// btkron.cpp: the Kronecker B^T tables (false: keep the B^T tasks)
+bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::vector<int32_t>& pd,
+               const std::vector<int32_t>& col, const std::vector<int32_t>& layer,
+               const std::vector<double>& layR, const std::vector<NodeConstraint>& vc,
+               const std::vector<int32_t>& Btp, const std::vector<int32_t>& Btc, int nv, int n_p);
 // solver.cpp
 int solve_nse(Ctx& c, int* outer, int* inner);
 // solve_NSE_Schur_complement (boussinesq_model.tpp:1248-1414)

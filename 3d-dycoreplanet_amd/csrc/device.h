@@ -341,6 +341,23 @@ struct TSepDev {
 // the lateral / radial tables of the column ids and layers (mesh geometry,
 // formed once at upload like the B^T column / layer factors)
 void tsep_tables(const TSepDev& t, hipStream_t s);
+// B^T in Kronecker form (kernels/bt_kron.hip; btkron.cpp builds the tables)
+struct BtkDev {
+  int n_layers = 0, n_kinds = 0, n_pairs = 0, n_con = 0, n_conent = 0;
+  int probe = 0;                     // DCP_BTK_PROBE timing variants (0: the real kernels)
+  const double* P = nullptr;         // column factors (k_bt_coltab)
+  const double* Q = nullptr;         // layer factors by layer id (k_bt_laytab)
+  const int32_t* ord2lay = nullptr;  // [n_layers]
+  const int32_t* kind = nullptr;     // [n_layers] mapping kind of ordinal layer
+  const int32_t* lptr = nullptr;     // [n_pairs + 1] lateral (node, vertex) pairs
+  const int32_t* lcon = nullptr;     // [n_kinds][n_con] offset of the pair's P entry
+  const uint32_t* code = nullptr;    // [nnz of B^T]
+  const int32_t* con_entry = nullptr;  // entries of constrained rows
+  const int32_t* con_row = nullptr;    // and their rows
+  double* A = nullptr;               // [n_kinds][n_pairs][6]
+};
+void btk_assemble(const BtkDev& b, long nnz, const NodeConstraint* vcon, double* Bt,
+                  hipStream_t s);
 // M, K, T_matrix = M + dt_T K and its Jacobi inverse (every entry written)
 void tsep_matrix(const TSepDev& t, long nnz, const PhysicsDev& ph, double* M, double* K,
                  double* Tmat, double* Tinv, hipStream_t s);

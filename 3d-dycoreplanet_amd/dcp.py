@@ -62,7 +62,7 @@ EXPORTED = [
     "dcp_nccl_unique_id", "dcp_group_create", "dcp_group_destroy", "dcp_partition_info",
     "dcp_feec_mesh_upload", "dcp_feec_assemble_nse_system", "dcp_feec_build_nse_preconditioner",
     "dcp_feec_solve_nse", "dcp_feec_cell_system", "dcp_feec_matrix_export",
-    "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_temperature_layout",
+    "dcp_host_feec_view_get", "dcp_schur_layout", "dcp_assembly_layout",
     "dcp_feec_partition_info",
     "dcp_mesh2d_partition_info", "dcp_time_operator",
     "dcp_write_vtu", "dcp_write_pvtu_record", "dcp_solver_history", "dcp_timer_summary",
@@ -260,7 +260,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_pattern_info.argtypes = [P] + [C.POINTER(C.c_int64)] * 5
     lib.dcp_schur_layout.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int)]
-    lib.dcp_temperature_layout.argtypes = [P, P]
+    lib.dcp_assembly_layout.argtypes = [P, P]
     lib.dcp_scatter_info.argtypes = [P, P, P, P]
     lib.dcp_matrix_powers_info.argtypes = [P, P]
     lib.dcp_device_memory.argtypes = [P, P]
@@ -1359,12 +1359,17 @@ class Context:
         self._check(lib().dcp_schur_layout(self._h, C.byref(cb), C.byref(st), C.byref(pm)))
         return {"col_bytes": cb.value, "stored": st.value, "permuted": bool(pm.value)}
 
-    def temperature_layout(self) -> dict:
-        """dcp_temperature_layout: which temperature assembly runs."""
-        v = np.zeros(6, np.int64)
-        self._check(lib().dcp_temperature_layout(self._h, _ptr(v)))
+    def assembly_layout(self) -> dict:
+        """dcp_assembly_layout: which forms the temperature and B^T assembly run in."""
+        v = np.zeros(8, np.int64)
+        self._check(lib().dcp_assembly_layout(self._h, _ptr(v)))
         return {"separable": bool(v[0]), "column_ids": int(v[1]), "layers": int(v[2]),
-                "kinds": int(v[3]), "lateral_entries": int(v[4])}
+                "kinds": int(v[3]), "lateral_entries": int(v[4]), "bt_kronecker": bool(v[5]),
+                "bt_lateral_pairs": int(v[6]), "bt_constrained_entries": int(v[7])}
+
+    def temperature_layout(self) -> dict:
+        """The temperature part of assembly_layout."""
+        return self.assembly_layout()
 
     def timings(self) -> dict:
         t = Timings()

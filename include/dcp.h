@@ -441,13 +441,16 @@ int dcp_pattern_info(dcp_ctx* ctx, int64_t* nnzb_A, int64_t* nnzb_Bt, int64_t* n
  * Cuthill-McKee). */
 int dcp_schur_layout(dcp_ctx* ctx, int* col_bytes, int64_t* stored, int* permuted);
 
-/* The temperature assembly's form (assemble_temperature_matrix / _rhs,
- * boussinesq_model.tpp:748-1020): info[0] = 1 when the separable Kronecker
- * form runs (the layered shell, one product of columns and layers, FE_Q(1),
- * no periodic identity; DCP_T_SEPARABLE=0 disables it), 0 for the colour
- * kernels; [1] column ids, [2] radial layers, [3] layer kinds, [4] lateral
- * pattern entries, [5] reserved (0). */
-int dcp_temperature_layout(dcp_ctx* ctx, int64_t info[6]);
+/* The forms the assembly runs in. Temperature (assemble_temperature_matrix /
+ * _rhs, boussinesq_model.tpp:748-1020): info[0] = 1 when the separable
+ * Kronecker form runs (the layered shell, one product of columns and layers,
+ * FE_Q(1), no periodic identity; DCP_T_SEPARABLE=0 disables it), 0 for the
+ * colour kernels; [1] column ids, [2] radial layers, [3] layer kinds, [4]
+ * lateral pattern entries. B^T of nse_matrix (:626-637, :677-687): [5] = 1
+ * when the operator-form assembly writes it in Kronecker form (one GPU,
+ * layered shell; DCP_BT_KRON=0 keeps the row tasks), [6] lateral
+ * (node, vertex) pairs, [7] entries of constrained rows. */
+int dcp_assembly_layout(dcp_ctx* ctx, int64_t info[8]);
 
 /* Communicator self-test (no mesh needed): the solver's forward halo (gather
  * of vec[send_pos], grouped send/recv, scatter into vec[recv_pos]) with every
