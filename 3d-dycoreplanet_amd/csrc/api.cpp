@@ -59,7 +59,12 @@ thread_local std::string g_last_error;
 template <class F>
 int guarded(dcp_ctx* ctx, F&& f) {
   try {
-    return f();
+    const int rc = f();
+    // a device-side collective that timed out (PeerComm) fails the call that
+    // observes it, not a later one (host-mapped flag; work still in flight is
+    // caught by the next call)
+    if (ctx && ctx->comm) ctx->comm->check();
+    return rc;
   } catch (const ApiError& e) {
     if (ctx) ctx->err = e.msg;
     g_last_error = e.msg;
@@ -1713,6 +1718,11 @@ int dcp_ctx_create(const dcp_config* cfg, dcp_ctx** out) {
       if (c->cfg.group) {
         require(c->cfg.group->size == c->cfg.world_size, DCP_ERR_INVALID, "group size != world_size");
         c->comm = make_local_comm(c->cfg.group, c->cfg.rank);
+        // DCP_PEER_COMM=1: the all-reduces device-initiated over the group's
+        // mailboxes (comm.h PeerComm); every rank of the group must agree
+        const char* env_pc = std::getenv("DCP_PEER_COMM");
+        if (env_pc && *env_pc == '1')
+          c->comm = make_peer_comm(std::move(c->comm), c->cfg.group, c->cfg.rank);
       } else {
         require(c->cfg.nccl_id != nullptr, DCP_ERR_INVALID,
                 "world_size > 1 needs nccl_id (dcp_nccl_unique_id on rank 0) or a dcp_group");
@@ -2954,6 +2964,7 @@ int dcp_solve_nse(dcp_ctx* ctx, int* outer, int* inner) {
     c.time_schur = false;
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     check_mf_err(c);
+    if (c.comm) c.comm->check();
     double sum = 0;
     int napp = 0;
     for (int k = 0; k < c.schur_ev_used; ++k) {
@@ -3278,6 +3289,33 @@ int dcp_halo_selftest(dcp_ctx* ctx, int n, double* vec, int n_list, const int32_
     halo_exchange(c, h, v.p);
     DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
     DCP_HIP_CHECK(hipMemcpy(vec, v.p, size_t(n) * sizeof(double), hipMemcpyDeviceToHost));
+    return DCP_OK;
+  });
+}
+
+int dcp_allreduce_selftest(dcp_ctx* ctx, double* vec, size_t n, int reps, double* ms_per_call) {
+  return guarded(ctx, [&] {
+    require(ctx && vec && n > 0 && reps >= 1, DCP_ERR_INVALID, "bad arguments");
+    Ctx& c = *ctx;
+    require(c.comm != nullptr, DCP_ERR_STATE, "no communicator (nccl_id or group)");
+    DBuf<double> v;
+    v.upload(std::vector<double>(vec, vec + n));
+    hipEvent_t a, b;
+    DCP_HIP_CHECK(hipEventCreate(&a));
+    DCP_HIP_CHECK(hipEventCreate(&b));
+    c.comm->allreduce(v.p, n, false, c.stream);  // warm-up: the result is this one's
+    DCP_HIP_CHECK(hipStreamSynchronize(c.stream));
+    DCP_HIP_CHECK(hipMemcpy(vec, v.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    DCP_HIP_CHECK(hipEventRecord(a, c.stream));
+    for (int k = 1; k < reps; ++k) c.comm->allreduce(v.p, n, true, c.stream);  // max: stays finite
+    DCP_HIP_CHECK(hipEventRecord(b, c.stream));
+    DCP_HIP_CHECK(hipEventSynchronize(b));
+    float ms = 0.0f;
+    DCP_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    c.comm->check();
+    if (ms_per_call) *ms_per_call = reps > 1 ? double(ms) / (reps - 1) : 0.0;
     return DCP_OK;
   });
 }

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -112,7 +113,85 @@ struct LocalComm : Comm {
   }
 };
 
+// Device-initiated all-reduce over the group's mailboxes (comm.h). Each call
+// takes the next tag; tags alternate between two slot sets (parity), and a
+// rank cannot start call k + 2 before every rank has finished call k (call
+// k + 1 waits for all ranks' tags of k + 1, posted after their k), so a slot
+// set is never overwritten while a rank still reads it.
+struct PeerComm : Comm {
+  std::unique_ptr<Comm> base;
+  LocalGroup* g = nullptr;
+  PeerBoxes boxes{};
+  double* box = nullptr;
+  unsigned long long* flag = nullptr;
+  unsigned* err = nullptr;  // host-mapped timeout flag
+  unsigned long long seq = 0;
+  ~PeerComm() override {
+    if (box) (void)hipFree(box);
+    if (flag) (void)hipFree(flag);
+    if (err) (void)hipHostFree(err);
+  }
+  void exchange(int npeers, const int* peers, double* const* sbuf, const size_t* sn,
+                double* const* rbuf, const size_t* rn, hipStream_t s) override {
+    base->exchange(npeers, peers, sbuf, sn, rbuf, rn, s);
+  }
+  void allreduce(double* buf, size_t n, bool max, hipStream_t s) override {
+    if (n == 0) return;
+    if (n > size_t(kPeerArCap)) {
+      base->allreduce(buf, n, max, s);
+      return;
+    }
+    peer_allreduce(boxes, rank, size, n, buf, ++seq, max, err, 3000000000L, s);  // 30 s
+  }
+  void describe(int out[4]) const override {
+    base->describe(out);
+    out[0] = 3;
+  }
+  void check() override {
+    if (err && *reinterpret_cast<volatile unsigned*>(err))
+      throw std::runtime_error("PeerComm: an all-reduce timed out waiting for a rank's tag");
+  }
+};
+
 }  // namespace
+
+std::unique_ptr<Comm> make_peer_comm(std::unique_ptr<Comm> base, LocalGroup* g, int rank) {
+  // Every rank's polling kernel must run beside the others: in one process
+  // their streams need hardware queues of their own (HIP shares
+  // GPU_MAX_HW_QUEUES, default 4, among all streams of the process; two ranks'
+  // streams on one queue would run their all-reduces in order and deadlock).
+  // Each context holds two streams.
+  const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+  const int queues = q ? std::atoi(q) : 4;
+  if (queues < 2 * g->size + 1)
+    throw std::runtime_error("PeerComm: " + std::to_string(g->size) +
+                             " in-process ranks need GPU_MAX_HW_QUEUES >= " +
+                             std::to_string(2 * g->size + 1) + " (is " + std::to_string(queues) +
+                             "): ranks sharing a hardware queue would deadlock");
+  auto c = std::make_unique<PeerComm>();
+  c->rank = rank;
+  c->size = g->size;
+  c->g = g;
+  c->base = std::move(base);
+  DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->box),
+                          sizeof(double) * 2 * size_t(g->size) * kPeerArCap));
+  DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->flag),
+                          sizeof(unsigned long long) * 2 * size_t(g->size)));
+  DCP_HIP_CHECK(hipMemset(c->flag, 0, sizeof(unsigned long long) * 2 * size_t(g->size)));
+  DCP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c->err), sizeof(unsigned),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+  *c->err = 0;
+  DCP_HIP_CHECK(hipDeviceSynchronize());
+  g->post[rank].peer_box = c->box;
+  g->post[rank].peer_flag = c->flag;
+  g->barrier();  // every rank's mailbox posted
+  for (int r = 0; r < g->size; ++r) {
+    c->boxes.box[r] = g->post[r].peer_box;
+    c->boxes.flag[r] = g->post[r].peer_flag;
+  }
+  g->barrier();  // the posts may be reused
+  return c;
+}
 
 std::unique_ptr<Comm> make_rccl_comm(const void* nccl_id, int rank, int size) {
   auto c = std::make_unique<RcclComm>();

@@ -4,14 +4,21 @@
 // Allreduce of Krylov partial sums. Everything is
 // stream-ordered on the context stream; no host synchronisation.
 //
-// Two transports:
+// Transports:
 //   RcclComm  one process per GPU, RCCL over xGMI (the production path):
 //             grouped ncclSend/ncclRecv per neighbour, ncclAllReduce;
 //   LocalComm P contexts of ONE process, each driven by its own host thread
 //             (tests on a single GPU: the partition, halo and reduction logic
 //             of the P-rank path without P devices). Collectives rendezvous on
 //             a host barrier and move data with device copies / one reduction
-//             kernel; results are identical on every rank.
+//             kernel; results are identical on every rank;
+//   PeerComm  device-initiated all-reduce over peer-mapped mailboxes
+//             (DCP_PEER_COMM=1 on an in-process group): one kernel per
+//             all-reduce stores this rank's partial into every rank's mailbox
+//             slot, then a tagged flag, polls its own mailbox for every
+//             rank's flag and sums the slots in rank order -- no host
+//             rendezvous, bitwise LocalComm's sums. Halos and all-reduces
+//             longer than the mailbox go to the wrapped transport.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,6 +45,9 @@ struct Comm {
   // rank count, this rank, and the device it drives (RCCL: ncclCommCount /
   // ncclCommUserRank / ncclCommCuDevice).
   virtual void describe(int out[4]) const = 0;
+  // Raise if a device-side collective timed out (PeerComm; call after a
+  // stream synchronisation).
+  virtual void check() {}
 };
 
 // ncclUniqueId (128 bytes) from rank 0, passed in dcp_config.nccl_id.
@@ -60,6 +70,8 @@ struct LocalGroup {
     std::vector<size_t> n;
     double* buf = nullptr;
     size_t len = 0;
+    double* peer_box = nullptr;  // PeerComm mailboxes, shared at creation
+    unsigned long long* peer_flag = nullptr;
   };
   std::vector<Post> post;
   std::vector<hipEvent_t> ready, done;
@@ -67,12 +79,26 @@ struct LocalGroup {
   std::vector<size_t> tmp_len;
 };
 std::unique_ptr<Comm> make_local_comm(LocalGroup* g, int rank);
-
 // linalg.hip: out[i] = sum (or max) over r < nbufs of bufs[r][i], r ascending.
 constexpr int kMaxLocalRanks = 16;
 struct BufTable {
   const double* p[kMaxLocalRanks];
 };
 void group_reduce(size_t n, int nbufs, const BufTable& t, double* out, bool max, hipStream_t s);
+
+// PeerComm over an in-process group (every rank must call it: the mailbox
+// pointers are shared under the group's barrier); `base` keeps the halos
+std::unique_ptr<Comm> make_peer_comm(std::unique_ptr<Comm> base, LocalGroup* g, int rank);
+
+// kernels/peer.hip: the device side of PeerComm
+constexpr int kPeerArCap = 4096;  // doubles per all-reduce slot
+struct PeerBoxes {
+  double* box[kMaxLocalRanks];              // [2 parity][size][kPeerArCap] slots per rank
+  unsigned long long* flag[kMaxLocalRanks];  // [2 parity][size] tags per rank
+};
+void peer_allreduce(const PeerBoxes& b, int rank, int size, size_t n, double* buf,
+                    unsigned long long seq, bool max, unsigned* err, long spin_limit,
+                    hipStream_t s);
+
 
 }  // namespace dcp

@@ -73,7 +73,7 @@ EXPORTED = [
     "dcp_state_get_owned", "dcp_scatter_info", "dcp_matrix_powers_info", "dcp_device_memory",
     "dcp_comm_info", "dcp_local_sizes",
     "dcp_nse_coupling_export",
-    "dcp_halo_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
+    "dcp_halo_selftest", "dcp_allreduce_selftest", "dcp_write_feec_vtu", "dcp_write_feec_pvtu_record",
 ]
 
 
@@ -267,6 +267,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dcp_comm_info.argtypes = [P, P]
     lib.dcp_local_sizes.argtypes = [P, P]
     lib.dcp_halo_selftest.argtypes = [P, I, P, I, P, P, I]
+    lib.dcp_allreduce_selftest.argtypes = [P, P, C.c_size_t, I, C.POINTER(C.c_double)]
     lib.dcp_nse_coupling_export.argtypes = [P, I, C.POINTER(C.c_int64), P, P, P]
     lib.dcp_feec_partition_info.argtypes = [C.POINTER(FeecMeshView), I, I, I, P, P, P, P, P, P]
     lib.dcp_mesh2d_partition_info.argtypes = [C.POINTER(Mesh2DView), I, I, I, P, P, P, P, P, P]
@@ -1316,11 +1317,19 @@ class Context:
         return {"built": bool(v[0]), "n_ext": int(v[1]), "rows": [int(x) for x in v[2:5]],
                 "halo_recv": int(v[5]), "value_recv": int(v[6]), "spmv_halo_recv": int(v[7])}
 
+    def allreduce_selftest(self, vec, reps=1):
+        """dcp_allreduce_selftest: vec summed over the ranks (returned), and
+        the average ms of reps - 1 further back-to-back all-reduces."""
+        v = np.ascontiguousarray(vec, dtype=np.float64).copy()
+        ms = C.c_double(0.0)
+        self._check(lib().dcp_allreduce_selftest(self._h, _ptr(v), v.size, int(reps), C.byref(ms)))
+        return v, ms.value
+
     def comm_info(self) -> dict:
         """dcp_comm_info: the communicator as its transport reports it."""
         v = np.zeros(4, np.int32)
         self._check(lib().dcp_comm_info(self._h, _ptr(v)))
-        return {"transport": {0: "none", 1: "rccl", 2: "in-process"}[int(v[0])],
+        return {"transport": {0: "none", 1: "rccl", 2: "in-process", 3: "peer"}[int(v[0])],
                 "ranks": int(v[1]), "rank": int(v[2]), "device": int(v[3])}
 
     def local_sizes(self) -> dict:

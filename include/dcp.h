@@ -459,6 +459,13 @@ int dcp_assembly_layout(dcp_ctx* ctx, int64_t info[8]);
 int dcp_halo_selftest(dcp_ctx* ctx, int n, double* vec, int n_list, const int32_t* send_pos,
                       const int32_t* recv_pos, int n_peers);
 
+/* Communicator self-test of the all-reduce (every rank of the communicator
+ * must call it with the same n and reps): vec (n doubles) is summed over the
+ * ranks in place (the solver's partial-sum all-reduce; the result returned in
+ * vec), then reps - 1 further all-reduces (max, so values stay finite) run
+ * back to back between one HIP event pair: *ms_per_call is their average. */
+int dcp_allreduce_selftest(dcp_ctx* ctx, double* vec, size_t n, int reps, double* ms_per_call);
+
 /* Scatter bookkeeping of the assembly (copy_local_to_global_nse_system,
  * boussinesq_model.tpp:677-687): per block pattern A, B^T, B ([3] each) the
  * blocks some cell's scatter position reaches, the pattern size, and whether
@@ -475,7 +482,9 @@ int dcp_matrix_powers_info(dcp_ctx* ctx, int64_t info[8]);
 
 /* The context's communicator as the transport reports it: info[0] = 0 (none,
  * one GPU), 1 (RCCL: [1] ncclCommCount, [2] ncclCommUserRank, [3]
- * ncclCommCuDevice) or 2 (in-process group: size, rank, current device). */
+ * ncclCommCuDevice), 2 (in-process group: size, rank, current device) or 3
+ * (in-process group with device-initiated all-reduces, DCP_PEER_COMM=1 at
+ * dcp_ctx_create: size, rank, device). */
 int dcp_comm_info(dcp_ctx* ctx, int32_t info[4]);
 
 /* Local sizes of the context's mesh: [0] local cells (owned + ghost layers),

@@ -311,10 +311,13 @@ def test_distributed_upload_group_time_step_matches_single_gpu(world, t_fixed):
         assert rel(rhs, dm.owned_nse(ref_rhs)) < 1e-12
         assert rel(x, dm.owned_nse(ref_x)) < 1e-10
         # temperature CG to 1e-12 under the reference's rule: partitioned dot
-        # products may move its stop by one iteration (2.7e-10 measured on 3 ranks)
+        # products may move its stop by one iteration (2.7e-10 measured on 3
+        # ranks; 1.5e-9 on 2 since the one-GPU reference assembles T in
+        # Kronecker form, another summation order than the ranks' colour
+        # kernels); the fixed-count companion holds the iterate to 1e-12
         if t_fixed:
             assert counts[1][:2] == ref_counts[1][:2] == (0, t_fixed)
             assert rel(Tx, dm.owned_T(ref_T)) < 1e-12
         else:
             assert abs(counts[1][1] - ref_counts[1][1]) <= 1
-            assert rel(Tx, dm.owned_T(ref_T)) < 1e-9
+            assert rel(Tx, dm.owned_T(ref_T)) < 1e-8
