@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -135,13 +136,18 @@ struct PeerComm : Comm {
                 double* const* rbuf, const size_t* rn, hipStream_t s) override {
     base->exchange(npeers, peers, sbuf, sn, rbuf, rn, s);
   }
+  // diagnostics (DCP_PEER_MAXN: the longest all-reduce taken by the peer
+  // kernel; DCP_PEER_SYNC=1: a stream synchronisation after each)
+  size_t max_n = kPeerArCap;
+  bool sync_each = false;
   void allreduce(double* buf, size_t n, bool max, hipStream_t s) override {
     if (n == 0) return;
-    if (n > size_t(kPeerArCap)) {
+    if (n > max_n) {
       base->allreduce(buf, n, max, s);
       return;
     }
     peer_allreduce(boxes, rank, size, n, buf, ++seq, max, err, 3000000000L, s);  // 30 s
+    if (sync_each) DCP_HIP_CHECK(hipStreamSynchronize(s));
   }
   void describe(int out[4]) const override {
     base->describe(out);
@@ -173,6 +179,9 @@ std::unique_ptr<Comm> make_peer_comm(std::unique_ptr<Comm> base, LocalGroup* g, 
   c->size = g->size;
   c->g = g;
   c->base = std::move(base);
+  if (const char* e = std::getenv("DCP_PEER_MAXN"))
+    c->max_n = std::min<size_t>(size_t(std::atol(e)), size_t(kPeerArCap));
+  if (const char* e = std::getenv("DCP_PEER_SYNC")) c->sync_each = *e == '1';
   DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->box),
                           sizeof(double) * 2 * size_t(g->size) * kPeerArCap));
   DCP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c->flag),

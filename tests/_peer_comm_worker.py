@@ -81,16 +81,31 @@ def time_steps():
         extra = {}
         for peer in (True, False):
             os.environ["DCP_PEER_COMM"] = "1" if peer else "0"
+            if os.environ.get("PEER_VARIANTS") and peer:
+                base_x = None
+                for var in os.environ["PEER_VARIANTS"].split(";"):
+                    for kv in var.split(","):
+                        k_, v_ = kv.split("=")
+                        os.environ[k_] = v_
+                    runs = [_group_run(world, m, ph, u, T, setup, None) for _ in range(2)]
+                    extra["var " + var] = [
+                        all(np.array_equal(a["x"].view(np.int64), b["x"].view(np.int64))
+                            for a, b in zip(runs[0], runs[1]))]
+                    for kv in var.split(","):
+                        os.environ.pop(kv.split("=")[0], None)
             if os.environ.get("PEER_TWICE") and peer:
                 extra["again"] = _group_run(world, m, ph, u, T, setup,
                                             lambda c: [c.comm_info()["transport"],
                                                        c.timings()["solve_nse_ms"]])
             out[peer] = _group_run(world, m, ph, u, T, setup,
-                                   lambda c: [c.comm_info()["transport"], c.timings()["solve_nse_ms"]])
+                                   lambda c: [c.comm_info()["transport"], c.timings()["solve_nse_ms"],
+                                                       c.timings().get("handoff_timeouts", 0)])
         same = True
         diff = {}
         for r, (a, b) in enumerate(zip(out[True], out[False])):
             same &= tuple(a["nse"]) == tuple(b["nse"]) and a["T"][1] == b["T"][1]
+            if tuple(a["nse"]) != tuple(b["nse"]) or a["T"][1] != b["T"][1]:
+                diff[f"{r}:counts"] = [list(a["nse"]), list(b["nse"]), a["T"][1], b["T"][1]]
             for key in ("x", "Tx", "rhs", "T_rhs"):
                 eq = bool(np.array_equal(a[key].view(np.int64), b[key].view(np.int64)))
                 same &= eq
@@ -100,6 +115,8 @@ def time_steps():
             same &= a["cfl"] == b["cfl"] and a["vmax"] == b["vmax"]
             if a["cfl"] != b["cfl"] or a["vmax"] != b["vmax"]:
                 diff[f"{r}:cfl/vmax"] = [a["cfl"], b["cfl"], a["vmax"], b["vmax"]]
+        for key_ in [k_ for k_ in extra if k_.startswith("var ")]:
+            diff[key_] = extra[key_]
         if "again" in extra:
             diff["peer_vs_peer_bitwise"] = all(
                 np.array_equal(a["x"].view(np.int64), b["x"].view(np.int64))
@@ -107,6 +124,8 @@ def time_steps():
         res.append({"world": world, "refine": refine, "gs": gs, "fixed_inner": fixed,
                     "transports": [out[True][0]["extra"][0], out[False][0]["extra"][0]],
                     "bitwise": bool(same), "nse": list(out[True][0]["nse"]), "diff": diff,
+                    "handoff_timeouts": [sum(r["extra"][2] for r in out[True]),
+                                         sum(r["extra"][2] for r in out[False])],
                     "solve_ms_peer": max(r["extra"][1] for r in out[True]),
                     "solve_ms_local": max(r["extra"][1] for r in out[False])})
     return res
