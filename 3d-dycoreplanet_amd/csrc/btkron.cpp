@@ -13,8 +13,12 @@
 //     kind of every layer (tsep.cpp's rule);
 //   * the lateral (node, vertex) pairs with their contributions (column,
 //     a b, i j), per kind as offsets into P;
-//   * one 32-bit code per B^T entry, and the list of entries whose row is a
-//     constrained (no-normal-flux) node.
+//   * per block of kBtkBlock consecutive B^T entries (one workgroup of
+//     k_btk_entries) the sorted list of the distinct A records (kind, pair)
+//     its entries read, and one 32-bit code per entry: the slots of its one or
+//     two terms in that list, the node level and the level step;
+//   * the list of entries whose row is a constrained (no-normal-flux) node,
+//     with their codes in the global form (pair, level, level step).
 // Anything that does not fit returns false and the B^T tasks stay in use.
 #include <algorithm>
 #include <array>
@@ -213,12 +217,64 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
     }
   if (bad) return false;
   std::vector<int32_t> con_entry, con_row;
+  std::vector<uint32_t> con_code;
   for (int n = 0; n < nv; ++n)
     if (vc[n].type != 0)
       for (int e = Btp[n]; e < Btp[n + 1]; ++e) {
         con_entry.push_back(e);
         con_row.push_back(n);
+        con_code.push_back(code[e] & 0x3FFFFFFFu);
       }
+  // the records of an entry's terms, in the order of btk_terms (bt_kron.hip)
+  auto terms = [&](uint32_t cd, int32_t rec[2]) {
+    const int p = int(cd & 0xFFFFFu), lam = int((cd >> 20) & 0xFFu), dl = int((cd >> 28) & 3u);
+    const int m = lam >> 1;
+    int L0 = -1, L1 = -1;
+    if (lam & 1)
+      L0 = m;
+    else if (dl == 0)
+      L0 = m >= 1 ? m - 1 : -1;
+    else if (dl == 2)
+      L0 = m;
+    else {
+      L0 = m >= 1 ? m - 1 : -1;
+      L1 = m < NL ? m : -1;
+    }
+    rec[0] = L0 >= 0 && L0 < NL ? kind[L0] * NPAIR + p : -1;
+    rec[1] = L1 >= 0 ? kind[L1] * NPAIR + p : -1;
+  };
+  const long nnz = long(Btc.size());
+  const long nblk = (nnz + kBtkBlock - 1) / kBtkBlock;
+  if (int64_t(NK) * NPAIR >= (int64_t(1) << 31) || nblk >= (1L << 31)) return false;
+  std::vector<std::vector<int32_t>> blk_list(nblk);
+  int worst = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(max : worst)
+  for (long bi = 0; bi < nblk; ++bi) {
+    const long e0 = bi * kBtkBlock, e1 = std::min(nnz, e0 + kBtkBlock);
+    std::vector<int32_t>& L = blk_list[bi];
+    for (long e = e0; e < e1; ++e) {
+      int32_t r[2];
+      terms(code[e], r);
+      for (int t = 0; t < 2; ++t)
+        if (r[t] >= 0) L.push_back(r[t]);
+    }
+    std::sort(L.begin(), L.end());
+    L.erase(std::unique(L.begin(), L.end()), L.end());
+    worst = std::max(worst, int(L.size()));
+    for (long e = e0; e < e1; ++e) {
+      int32_t r[2];
+      terms(code[e], r);
+      uint32_t slot[2] = {0, 0};
+      for (int t = 0; t < 2; ++t)
+        if (r[t] >= 0) slot[t] = uint32_t(std::lower_bound(L.begin(), L.end(), r[t]) - L.begin());
+      code[e] = (slot[0] & 1023u) | ((slot[1] & 1023u) << 10) | (code[e] & 0x7FF00000u);
+    }
+  }
+  if (worst > kBtkMaxRec) return false;
+  std::vector<int32_t> blk_ptr(size_t(nblk) + 1, 0), blk_rec;
+  for (long bi = 0; bi < nblk; ++bi) blk_ptr[bi + 1] = blk_ptr[bi] + int32_t(blk_list[bi].size());
+  blk_rec.reserve(size_t(blk_ptr[nblk]));
+  for (long bi = 0; bi < nblk; ++bi) blk_rec.insert(blk_rec.end(), blk_list[bi].begin(), blk_list[bi].end());
   c.btk_n_layers = NL;
   c.btk_n_kinds = NK;
   c.btk_n_pairs = NPAIR;
@@ -229,6 +285,10 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
   c.btk_lptr.upload(lptr);
   c.btk_lcon.upload(lcon);
   c.btk_code.upload(code);
+  c.btk_con_code.upload(con_code);
+  c.btk_blk_ptr.upload(blk_ptr);
+  c.btk_blk_rec.upload(blk_rec);
+  c.btk_max_rec = worst;
   c.btk_con_entry.upload(con_entry);
   c.btk_con_row.upload(con_row);
   c.btk_A.alloc(size_t(NK) * NPAIR * 6);

@@ -400,8 +400,10 @@ struct Ctx {
   // takes B^T from it and B as its transpose
   bool btk = false;
   int btk_n_layers = 0, btk_n_kinds = 0, btk_n_pairs = 0, btk_n_con = 0, btk_n_conent = 0;
+  int btk_max_rec = 0;
   DBuf<int32_t> btk_ord2lay, btk_kind, btk_lptr, btk_lcon, btk_con_entry, btk_con_row;
-  DBuf<uint32_t> btk_code;
+  DBuf<int32_t> btk_blk_ptr, btk_blk_rec;
+  DBuf<uint32_t> btk_code, btk_con_code;
   DBuf<double> btk_A;
   BtkDev btkd() const {
     BtkDev b;
@@ -410,6 +412,7 @@ struct Ctx {
     b.n_pairs = btk_n_pairs;
     b.n_con = btk_n_con;
     b.n_conent = btk_n_conent;
+    b.max_rec = btk_max_rec;
     const char* pr = std::getenv("DCP_BTK_PROBE");
     b.probe = pr ? std::atoi(pr) : 0;
     b.P = bt_P.p;
@@ -419,6 +422,9 @@ struct Ctx {
     b.lptr = btk_lptr.p;
     b.lcon = btk_lcon.p;
     b.code = btk_code.p;
+    b.blk_ptr = btk_blk_ptr.p;
+    b.blk_rec = btk_blk_rec.p;
+    b.con_code = btk_con_code.p;
     b.con_entry = btk_con_entry.p;
     b.con_row = btk_con_row.p;
     b.A = btk_A.p;

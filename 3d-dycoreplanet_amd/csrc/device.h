@@ -341,9 +341,20 @@ struct TSepDev {
 // the lateral / radial tables of the column ids and layers (mesh geometry,
 // formed once at upload like the B^T column / layer factors)
 void tsep_tables(const TSepDev& t, hipStream_t s);
-// B^T in Kronecker form (kernels/bt_kron.hip; btkron.cpp builds the tables)
+// B^T in Kronecker form (kernels/bt_kron.hip; btkron.cpp builds the tables).
+// k_btk_entries: one workgroup of kBtkTB threads per kBtkPT * kBtkTB
+// consecutive entries; btkron.cpp lists each such block's distinct lateral
+// records (kind, pair), staged into LDS, and codes the entries by slot.
+#ifndef DCP_BTK_PT
+#define DCP_BTK_PT 8
+#endif
+constexpr int kBtkTB = 256;
+constexpr int kBtkPT = DCP_BTK_PT;
+constexpr long kBtkBlock = long(kBtkPT) * kBtkTB;
+constexpr int kBtkMaxRec = 1023;  // slots per block (10-bit slot fields of the code)
 struct BtkDev {
   int n_layers = 0, n_kinds = 0, n_pairs = 0, n_con = 0, n_conent = 0;
+  int max_rec = 0;                   // largest record list of a block
   int probe = 0;                     // DCP_BTK_PROBE timing variants (0: the real kernels)
   const double* P = nullptr;         // column factors (k_bt_coltab)
   const double* Q = nullptr;         // layer factors by layer id (k_bt_laytab)
@@ -351,7 +362,12 @@ struct BtkDev {
   const int32_t* kind = nullptr;     // [n_layers] mapping kind of ordinal layer
   const int32_t* lptr = nullptr;     // [n_pairs + 1] lateral (node, vertex) pairs
   const int32_t* lcon = nullptr;     // [n_kinds][n_con] offset of the pair's P entry
-  const uint32_t* code = nullptr;    // [nnz of B^T]
+  // per entry: slot of the first term (bits 0-9), of the second (10-19),
+  // node level lambda (20-27), l - lambda / 2 + 1 (28-29), constrained row (30)
+  const uint32_t* code = nullptr;      // [nnz of B^T]
+  const int32_t* blk_ptr = nullptr;    // [blocks + 1] record lists
+  const int32_t* blk_rec = nullptr;    // records kind n_pairs + pair
+  const uint32_t* con_code = nullptr;  // per constrained entry: pair (bits 0-19), lambda, dl
   const int32_t* con_entry = nullptr;  // entries of constrained rows
   const int32_t* con_row = nullptr;    // and their rows
   double* A = nullptr;               // [n_kinds][n_pairs][6]

@@ -16,11 +16,17 @@
 // A_t^kind(nu, v) = sum over the (one to four) columns holding nu and v of
 // that kind's P_t: the lateral matrices. Per assembly:
 //   k_btk_lateral  A^kind from P (2 kinds x ~154 k lateral pairs at r=5),
-//   k_btk_entries  one thread per B^T entry (4 per thread, kTB apart, each XCD
-//                  a contiguous range): the one or two layer terms, written
-//                  once (no zero fill, no colouring, no atomics),
+//   k_btk_entries  one workgroup per kBtkPT x 256 consecutive B^T entries:
+//                  the block's distinct lateral records (kind, pair; ~160 of
+//                  them per 1024 entries at r=5, listed at upload) staged from
+//                  A into LDS with coalesced loads, then per entry the one or
+//                  two layer terms from LDS, written once (no zero fill, no
+//                  colouring, no atomics) through an LDS stage so each store
+//                  instruction writes 512 contiguous bytes,
 //   k_btk_con      the entries of constrained rows (no-normal-flux nodes):
 //                  the same value condensed with the row's constraint C^T.
+// (Reading A per entry from L2 instead -- 3 16-byte loads per term at 64
+// scattered lines per wave instruction -- cost 150 of the kernel's 270 us.)
 #include <hip/hip_runtime.h>
 
 #include "../device.h"
@@ -28,11 +34,8 @@
 namespace dcp {
 namespace {
 
-constexpr int kTB = 256;
-#ifndef DCP_BTK_PT
-#define DCP_BTK_PT 4
-#endif
-constexpr int kPT = DCP_BTK_PT;  // entries per thread
+constexpr int kTB = kBtkTB;
+constexpr int kPT = kBtkPT;  // entries per thread
 
 // A[(kind n_pairs + pair) 6 + (t 3 + d)], t = 01, 2
 __global__ __launch_bounds__(kTB) void k_btk_lateral(BtkDev b) {
@@ -54,23 +57,15 @@ __global__ __launch_bounds__(kTB) void k_btk_lateral(BtkDev b) {
   for (int i = 0; i < 6; ++i) a[i] = s[i];
 }
 
-// code: bits 0-19 lateral pair, 20-27 node level lambda, 28-29 l - lambda / 2 + 1,
-// 30 constrained row (k_btk_con writes it)
-__device__ __forceinline__ void btk_value(const BtkDev& b, const int* skind, const double* sq,
-                                          uint32_t code, double v[3]) {
-  int p = int(code & 0xFFFFFu);
-  const int lam = int((code >> 20) & 0xFFu), dl = int((code >> 28) & 3u);
-  if (b.probe & 1) p &= 4095;  // probe: a 4096-pair window of A (L2-resident)
-  if (b.probe & 2) {           // probe: no A / Q reads
-    v[0] = double(p);
-    v[1] = double(lam);
-    v[2] = double(dl);
-    return;
-  }
+// The one or two layer terms of an entry (node level lambda, l - lambda / 2 + 1
+// = dl): rec(t, L) is the A record of term t (0, 1) in layer L.
+template <class Rec>
+__device__ __forceinline__ void btk_terms(const BtkDev& b, const double* sq, int lam, int dl,
+                                          Rec rec, double v[3]) {
   const int m = lam >> 1;
   v[0] = v[1] = v[2] = 0.0;
-  auto add = [&](int L, int c, int k) {
-    const double2* a2 = reinterpret_cast<const double2*>(b.A + 6 * (size_t(skind[L]) * b.n_pairs + p));
+  auto add = [&](int t, int L, int c, int k) {
+    const double2* a2 = rec(t, L);
     const double2 A0 = a2[0], A1 = a2[1], A2 = a2[2];
     const double q01 = sq[12 * L + 4 * c + 2 * k], q2 = sq[12 * L + 4 * c + 2 * k + 1];
     v[0] -= A0.x * q01 + A1.y * q2;
@@ -78,15 +73,26 @@ __device__ __forceinline__ void btk_value(const BtkDev& b, const int* skind, con
     v[2] -= A1.x * q01 + A2.y * q2;
   };
   if (lam & 1) {
-    add(m, 1, dl - 1);
+    add(0, m, 1, dl - 1);
   } else if (dl == 0) {
-    if (m >= 1) add(m - 1, 2, 0);
+    if (m >= 1) add(0, m - 1, 2, 0);
   } else if (dl == 2) {
-    add(m, 0, 1);
+    add(0, m, 0, 1);
   } else {
-    if (m >= 1) add(m - 1, 2, 1);
-    if (m < b.n_layers) add(m, 0, 0);
+    if (m >= 1) add(0, m - 1, 2, 1);
+    if (m < b.n_layers) add(1, m, 0, 0);
   }
+}
+
+// con_code: bits 0-19 lateral pair, 20-27 lambda, 28-29 dl; A from global memory
+__device__ __forceinline__ void btk_value_global(const BtkDev& b, const int* skind,
+                                                 const double* sq, uint32_t code, double v[3]) {
+  const int p = int(code & 0xFFFFFu);
+  btk_terms(b, sq, int((code >> 20) & 0xFFu), int((code >> 28) & 3u),
+            [&](int, int L) {
+              return reinterpret_cast<const double2*>(b.A + 6 * (size_t(skind[L]) * b.n_pairs + p));
+            },
+            v);
 }
 
 __device__ __forceinline__ void btk_stage(const BtkDev& b, double* sq, int* skind) {
@@ -95,29 +101,66 @@ __device__ __forceinline__ void btk_stage(const BtkDev& b, double* sq, int* skin
   for (int i = threadIdx.x; i < b.n_layers; i += kTB) skind[i] = b.kind[i];
 }
 
-// The 64 entries of a wave (per u) are 192 consecutive doubles of B^T: staged
-// in LDS so each store instruction writes 512 contiguous bytes. Entries of
-// constrained rows are written unconstrained here and overwritten by k_btk_con
-// (same stream, after).
+// The block's records are staged into LDS first. The 64 entries of a wave (per u) are 192 consecutive
+// doubles of B^T: staged in LDS so each store instruction writes 512
+// contiguous bytes. Entries of constrained rows are written unconstrained here
+// and overwritten by k_btk_con (same stream, after).
 __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double* __restrict__ Bt) {
   extern __shared__ __attribute__((aligned(16))) double sq[];
-  int* skind = reinterpret_cast<int*>(sq + 12 * b.n_layers);
+  double2* srec = reinterpret_cast<double2*>(sq + 12 * b.n_layers);
   __shared__ double stage[kTB / 64][192];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long base = long(xcd_block(int(blockIdx.x), int(gridDim.x))) * (kPT * kTB) + threadIdx.x;
+  const int blk = xcd_block(int(blockIdx.x), int(gridDim.x));
+  const long base = long(blk) * kBtkBlock + threadIdx.x;
+  // the block's records into LDS, 3 double2 each, consecutive threads on
+  // consecutive double2 (coalesced, the records are sorted): every global
+  // load issued up front and unpredicated (indices clamped; predicated loads
+  // each got a wait of their own), so the staging costs two dependent
+  // latencies (record id, record), not two per trip. Measured at r=5
+  // (profiles/r06/r06ae_btk_probe.log): a loop over the doubles 384 us per
+  // assembly, this 370 us, a thread per record (48-byte strided loads) 532 us.
+  const int r0 = b.blk_ptr[blk], nr = b.blk_ptr[blk + 1] - r0;  // nr >= 1
+  const double2* A2 = reinterpret_cast<const double2*>(b.A);
+  constexpr int kU = 4;  // 4 kTB double2 = 341 records without the loop below
+  int rid[kU];
+#pragma unroll
+  for (int q = 0; q < kU; ++q) rid[q] = b.blk_rec[r0 + min((int(threadIdx.x) + q * kTB) / 3, nr - 1)];
   uint32_t code[kPT];
 #pragma unroll
-  for (int u = 0; u < kPT; ++u) {
-    const long e = base + long(u) * kTB;
-    code[u] = e < nnz ? __builtin_nontemporal_load(b.code + e) : 0u;
+  for (int u = 0; u < kPT; ++u)
+    code[u] = __builtin_nontemporal_load(b.code + min(base + long(u) * kTB, nnz - 1));
+  double2 ra[kU];
+#pragma unroll
+  for (int q = 0; q < kU; ++q) {
+    const int i = int(threadIdx.x) + q * kTB;
+    ra[q] = A2[3 * size_t(rid[q]) + (i - 3 * (i / 3))];
   }
-  btk_stage(b, sq, skind);
+#pragma unroll
+  for (int q = 0; q < kU; ++q) {
+    const int i = int(threadIdx.x) + q * kTB;
+    if (i < 3 * nr) srec[i] = ra[q];
+  }
+  for (int i = threadIdx.x + kU * kTB; i < 3 * nr; i += kTB) {  // blocks of > 341 records
+    const int j = i / 3;
+    srec[i] = A2[3 * size_t(b.blk_rec[r0 + j]) + (i - 3 * j)];
+  }
+  for (int i = threadIdx.x; i < 12 * b.n_layers; i += kTB)
+    sq[i] = b.Q[12 * size_t(b.ord2lay[i / 12]) + i % 12];
   __syncthreads();
-  // every entry's A loads issued before the first LDS hand-off (the fences of
-  // the hand-off would keep the next entry's loads behind this one's stores)
   double v[kPT][3];
 #pragma unroll
-  for (int u = 0; u < kPT; ++u) btk_value(b, skind, sq, code[u], v[u]);
+  for (int u = 0; u < kPT; ++u) {
+    const uint32_t cu = code[u];
+    if (b.probe & 2) {  // probe: no A / Q reads
+      v[u][0] = double(cu & 1023u);
+      v[u][1] = double((cu >> 10) & 1023u);
+      v[u][2] = double(cu >> 20);
+      continue;
+    }
+    const int s0 = int(cu & 1023u), s1 = int((cu >> 10) & 1023u);
+    btk_terms(b, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u),
+              [&](int t, int) { return srec + 3 * (t ? s1 : s0); }, v[u]);
+  }
 #pragma unroll
   for (int u = 0; u < kPT; ++u) {
     stage[wave][3 * lane] = v[u][0];
@@ -153,7 +196,7 @@ __global__ __launch_bounds__(kTB) void k_btk_con(BtkDev b, const NodeConstraint*
   if (i >= b.n_conent) return;
   const long e = b.con_entry[i];
   double v[3];
-  btk_value(b, skind, sq, b.code[e], v);
+  btk_value_global(b, skind, sq, b.con_code[i], v);
   const NodeConstraint nc = vcon[b.con_row[i]];
   double C[3][3];
 #pragma unroll
@@ -180,10 +223,11 @@ __global__ __launch_bounds__(kTB) void k_btk_con(BtkDev b, const NodeConstraint*
 void btk_assemble(const BtkDev& b, long nnz, const NodeConstraint* vcon, double* Bt,
                   hipStream_t s) {
   const size_t lds = sizeof(double) * 12 * size_t(b.n_layers) + sizeof(int) * size_t(b.n_layers);
+  const size_t lds_e = sizeof(double) * 12 * size_t(b.n_layers) + 48 * size_t(b.max_rec);
   hipLaunchKernelGGL(k_btk_lateral, dim3((b.n_kinds * b.n_pairs + kTB - 1) / kTB), dim3(kTB), 0, s,
                      b);
-  hipLaunchKernelGGL(k_btk_entries, dim3(unsigned((nnz + long(kPT) * kTB - 1) / (long(kPT) * kTB))),
-                     dim3(kTB), lds, s, b, nnz, Bt);
+  hipLaunchKernelGGL(k_btk_entries, dim3(unsigned((nnz + kBtkBlock - 1) / kBtkBlock)), dim3(kTB),
+                     lds_e, s, b, nnz, Bt);
   if (b.n_conent > 0)
     hipLaunchKernelGGL(k_btk_con, dim3((b.n_conent + kTB - 1) / kTB), dim3(kTB), lds, s, b, vcon,
                        Bt);

@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdcp.so")
+# DCP_LIBRARY: another build of the same sources (tools/ probes of compile-time variants)
+LIB_PATH = os.environ.get("DCP_LIBRARY") or os.path.join(_HERE, "libdcp.so")
 
 DCP_OK, DCP_NOT_CONVERGED = 0, 1
 DCP_ERR_INVALID, DCP_ERR_UNSUPPORTED, DCP_ERR_DEVICE, DCP_ERR_STATE = -1, -2, -3, -4

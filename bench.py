@@ -58,9 +58,10 @@ CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
                (5, "sstep"): "profiles/r05/r05zd_bench_r5_kernel_stats.csv"}
 # the operator-form assembly's kernels (tools/bt_rows_probe.py) and their
 # launches per assembly (the rhs kernel once per colour class)
-PMC_ASM = {5: ("profiles/r05/r05i_pmc_asm_r5.json",
-               {"k_bt_tasks": 1, "k_mf_pencil": 1, "k_mf_gather": 1, "k_nse_rhs_halfwave": 1,
-                "k_con_gather": 1})}  # (k_bt_coltab runs once at upload)
+PMC_ASM = {5: ("profiles/r06/r06_pmc_asm_r5.json",
+               {"k_btk_lateral": 1, "k_btk_entries": 1, "k_btk_con": 1, "k_mf_pencil": 1,
+                "k_mf_gather": 1, "k_nse_rhs_halfwave": 1, "k_con_gather": 1})}
+# (k_bt_coltab / k_bt_laytab run once at upload)
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather); the
 # kernel names must be found in the summary (no stale profile of other kernels)
 PMC_MF = {5: ("profiles/r06/r06_pmc_mf_r5.json", ("k_mf_pencil<true, true, false>",
@@ -105,7 +106,7 @@ def pmc_asm_traffic(refine):
     for key, launches in ent[1].items():
         fk = [v["mean_kB"] for k, v in ctr["FETCH_SIZE"].items() if key in k]
         wk = [v["mean_kB"] for k, v in ctr["WRITE_SIZE"].items() if key in k]
-        if not fk or not wk:
+        if len(fk) != 1 or len(wk) != 1:  # missing or ambiguous: no stale numbers
             return None
         fetch += launches * fk[0] * 1e3
         write += launches * wk[0] * 1e3
@@ -1012,9 +1013,10 @@ def main():
     asm_bytes = 24.0 * pinfo["nnzb_Bt"] + 16.0 * ls["n_u"] + 8.0 * ls["n_T"]
     asm_ach = asm_bytes / (asm_ms * 1e-3) / 1e9
     out["roofline_assembly"] = {
-        "kernel": "operator-form assemble_nse_system (B^T by row tasks k_bt_tasks, the rhs "
-                  "by the pencil kernel + velocity gather, the constrained diagonals by "
-                  "k_nse_rhs_halfwave over the constrained cells + k_con_gather)",
+        "kernel": "operator-form assemble_nse_system (B^T in Kronecker form: k_btk_lateral "
+                  "+ k_btk_entries + k_btk_con; the rhs by the pencil kernel + velocity gather, "
+                  "the constrained diagonals by k_nse_rhs_halfwave over the constrained cells "
+                  "+ k_con_gather)",
         "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
         "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None,
