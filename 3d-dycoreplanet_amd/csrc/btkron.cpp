@@ -17,8 +17,7 @@
 //     k_btk_entries) the sorted list of the distinct A records (kind, pair)
 //     its entries read, and one 32-bit code per entry: the slots of its one or
 //     two terms in that list, the node level and the level step;
-//   * the list of entries whose row is a constrained (no-normal-flux) node,
-//     with their codes in the global form (pair, level, level step).
+//   * the list of entries whose row is a constrained (no-normal-flux) node.
 // Anything that does not fit returns false and the B^T tasks stay in use.
 #include <algorithm>
 #include <array>
@@ -217,13 +216,11 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
     }
   if (bad) return false;
   std::vector<int32_t> con_entry, con_row;
-  std::vector<uint32_t> con_code;
   for (int n = 0; n < nv; ++n)
     if (vc[n].type != 0)
       for (int e = Btp[n]; e < Btp[n + 1]; ++e) {
         con_entry.push_back(e);
         con_row.push_back(n);
-        con_code.push_back(code[e] & 0x3FFFFFFFu);
       }
   // the records of an entry's terms, in the order of btk_terms (bt_kron.hip)
   auto terms = [&](uint32_t cd, int32_t rec[2]) {
@@ -285,7 +282,6 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
   c.btk_lptr.upload(lptr);
   c.btk_lcon.upload(lcon);
   c.btk_code.upload(code);
-  c.btk_con_code.upload(con_code);
   c.btk_blk_ptr.upload(blk_ptr);
   c.btk_blk_rec.upload(blk_rec);
   c.btk_max_rec = worst;

@@ -403,7 +403,7 @@ struct Ctx {
   int btk_max_rec = 0;
   DBuf<int32_t> btk_ord2lay, btk_kind, btk_lptr, btk_lcon, btk_con_entry, btk_con_row;
   DBuf<int32_t> btk_blk_ptr, btk_blk_rec;
-  DBuf<uint32_t> btk_code, btk_con_code;
+  DBuf<uint32_t> btk_code;
   DBuf<double> btk_A;
   BtkDev btkd() const {
     BtkDev b;
@@ -424,7 +424,6 @@ struct Ctx {
     b.code = btk_code.p;
     b.blk_ptr = btk_blk_ptr.p;
     b.blk_rec = btk_blk_rec.p;
-    b.con_code = btk_con_code.p;
     b.con_entry = btk_con_entry.p;
     b.con_row = btk_con_row.p;
     b.A = btk_A.p;

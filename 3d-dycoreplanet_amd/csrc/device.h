@@ -367,7 +367,6 @@ struct BtkDev {
   const uint32_t* code = nullptr;      // [nnz of B^T]
   const int32_t* blk_ptr = nullptr;    // [blocks + 1] record lists
   const int32_t* blk_rec = nullptr;    // records kind n_pairs + pair
-  const uint32_t* con_code = nullptr;  // per constrained entry: pair (bits 0-19), lambda, dl
   const int32_t* con_entry = nullptr;  // entries of constrained rows
   const int32_t* con_row = nullptr;    // and their rows
   double* A = nullptr;               // [n_kinds][n_pairs][6]

@@ -24,7 +24,8 @@
 //                  colouring, no atomics) through an LDS stage so each store
 //                  instruction writes 512 contiguous bytes,
 //   k_btk_con      the entries of constrained rows (no-normal-flux nodes):
-//                  the same value condensed with the row's constraint C^T.
+//                  the value k_btk_entries wrote, condensed with the row's
+//                  constraint C^T.
 // (Reading A per entry from L2 instead -- 3 16-byte loads per term at 64
 // scattered lines per wave instruction -- cost 150 of the kernel's 270 us.)
 #include <hip/hip_runtime.h>
@@ -82,23 +83,6 @@ __device__ __forceinline__ void btk_terms(const BtkDev& b, const double* sq, int
     if (m >= 1) add(0, m - 1, 2, 1);
     if (m < b.n_layers) add(1, m, 0, 0);
   }
-}
-
-// con_code: bits 0-19 lateral pair, 20-27 lambda, 28-29 dl; A from global memory
-__device__ __forceinline__ void btk_value_global(const BtkDev& b, const int* skind,
-                                                 const double* sq, uint32_t code, double v[3]) {
-  const int p = int(code & 0xFFFFFu);
-  btk_terms(b, sq, int((code >> 20) & 0xFFu), int((code >> 28) & 3u),
-            [&](int, int L) {
-              return reinterpret_cast<const double2*>(b.A + 6 * (size_t(skind[L]) * b.n_pairs + p));
-            },
-            v);
-}
-
-__device__ __forceinline__ void btk_stage(const BtkDev& b, double* sq, int* skind) {
-  for (int i = threadIdx.x; i < 12 * b.n_layers; i += kTB)
-    sq[i] = b.Q[12 * size_t(b.ord2lay[i / 12]) + i % 12];
-  for (int i = threadIdx.x; i < b.n_layers; i += kTB) skind[i] = b.kind[i];
 }
 
 // The block's records are staged into LDS first. The 64 entries of a wave (per u) are 192 consecutive
@@ -184,20 +168,18 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
   }
 }
 
-// entries of constrained rows: out = C^T v (condensation(), type 2: the
-// normal component eliminated; types 1 / 3: zero rows)
-__global__ __launch_bounds__(kTB) void k_btk_con(BtkDev b, const NodeConstraint* __restrict__ vcon,
+// entries of constrained rows: out = C^T v, v the value k_btk_entries wrote
+// (condensation(), type 2: the normal component eliminated; types 1 / 3: zero
+// rows)
+__global__ __launch_bounds__(kTB) void k_btk_con(int n_conent, const int32_t* __restrict__ con_entry,
+                                                 const int32_t* __restrict__ con_row,
+                                                 const NodeConstraint* __restrict__ vcon,
                                                  double* __restrict__ Bt) {
-  extern __shared__ __attribute__((aligned(16))) double sq[];
-  int* skind = reinterpret_cast<int*>(sq + 12 * b.n_layers);
-  btk_stage(b, sq, skind);
-  __syncthreads();
   const int i = int(blockIdx.x) * kTB + int(threadIdx.x);
-  if (i >= b.n_conent) return;
-  const long e = b.con_entry[i];
-  double v[3];
-  btk_value_global(b, skind, sq, b.con_code[i], v);
-  const NodeConstraint nc = vcon[b.con_row[i]];
+  if (i >= n_conent) return;
+  double* dst = Bt + 3 * size_t(con_entry[i]);
+  const double v[3] = {dst[0], dst[1], dst[2]};
+  const NodeConstraint nc = vcon[con_row[i]];
   double C[3][3];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -213,7 +195,6 @@ __global__ __launch_bounds__(kTB) void k_btk_con(BtkDev b, const NodeConstraint*
         C[nc.k][d] = nc.w[d];
       }
   }
-  double* dst = Bt + 3 * e;
 #pragma unroll
   for (int jj = 0; jj < 3; ++jj) dst[jj] = C[0][jj] * v[0] + C[1][jj] * v[1] + C[2][jj] * v[2];
 }
@@ -222,15 +203,14 @@ __global__ __launch_bounds__(kTB) void k_btk_con(BtkDev b, const NodeConstraint*
 
 void btk_assemble(const BtkDev& b, long nnz, const NodeConstraint* vcon, double* Bt,
                   hipStream_t s) {
-  const size_t lds = sizeof(double) * 12 * size_t(b.n_layers) + sizeof(int) * size_t(b.n_layers);
   const size_t lds_e = sizeof(double) * 12 * size_t(b.n_layers) + 48 * size_t(b.max_rec);
   hipLaunchKernelGGL(k_btk_lateral, dim3((b.n_kinds * b.n_pairs + kTB - 1) / kTB), dim3(kTB), 0, s,
                      b);
   hipLaunchKernelGGL(k_btk_entries, dim3(unsigned((nnz + kBtkBlock - 1) / kBtkBlock)), dim3(kTB),
                      lds_e, s, b, nnz, Bt);
   if (b.n_conent > 0)
-    hipLaunchKernelGGL(k_btk_con, dim3((b.n_conent + kTB - 1) / kTB), dim3(kTB), lds, s, b, vcon,
-                       Bt);
+    hipLaunchKernelGGL(k_btk_con, dim3((b.n_conent + kTB - 1) / kTB), dim3(kTB), 0, s, b.n_conent,
+                       b.con_entry, b.con_row, vcon, Bt);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
