@@ -1905,6 +1905,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
     c.tsep = false;
     c.ts_tmat_valid = false;
     c.btk = false;
+    c.cdk = false;
     const int nv = h.nv;
     c.color_ptr = h.color_ptr;
     const auto &q2 = h.q2, &pd = h.pd, &td = h.td;
@@ -2372,6 +2373,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.con_color_ptr.clear();
             c.con_color_cells.release();
             c.rhs_cell_order = h.tdpc == 8 && !(env_rhs && *env_rhs == '0');
+            std::vector<int32_t> cdk_rec;  // per slot: cell 27 + local node
             if (c.rhs_cell_order) {
               std::vector<int32_t> sub;
               c.con_color_ptr.assign(1, 0);
@@ -2403,6 +2405,10 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
               c.con_cptr.upload(cptr);
               c.con_cslot.upload(cslot);
               c.con_cbuf.alloc(3 * size_t(std::max(cptr[n_con], 1)));
+              cdk_rec.assign(size_t(cptr[n_con]), 0);
+              for (size_t k = 0; k < sub.size(); ++k)
+                for (int t = 0; t < 27; ++t)
+                  if (cslot[27 * k + t] >= 0) cdk_rec[size_t(cslot[27 * k + t])] = 27 * sub[k] + t;
             }
             // the column factors P of the B^T entries are mesh geometry
             // (the column tables, reference functions): formed once here
@@ -2419,6 +2425,17 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.btk = false;
             if (!dist && nrows == nv && c.B_transpose && !(env_bk && *env_bk == '0'))
               build_btk(c, n_cells, q2, pd, col, layer, layR, vc, Btp, Btc, nv, n_p);
+            // with it the constrained diagonals in Kronecker form (k_cdk_*;
+            // DCP_CDIAG_KRON=0 keeps the cell pass + con_gather)
+            const char* env_cd = std::getenv("DCP_CDIAG_KRON");
+            if (c.btk && c.rhs_cell_order && !cdk_rec.empty() && !(env_cd && *env_cd == '0')) {
+              c.cdk_rec.upload(cdk_rec);
+              c.cdk_L.alloc(size_t(90) * c.bt_ncols);
+              c.cdk_R.alloc(size_t(12) * nlay);
+              cdk_tables(c.mf_colgeo.p, c.bt_ncols, c.mf_laygeo.p, nlay, c.cdk_L.p, c.cdk_R.p,
+                         c.stream);
+              c.cdk = true;
+            }
           }
         }
       }
@@ -2745,7 +2762,11 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       if (overlap == 1) launch_bt();
     }
     if (overlap == 3 && !out.cdiag) launch_bt();  // nothing to overlap: B^T first anyway
-    if (rhs_co && out.cdiag) {
+    if (rhs_co && out.cdiag && c.cdk) {
+      cdk_diag(c.n_con, c.con_cptr.p, c.cdk_rec.p, c.cd(), c.cdk_L.p, c.cdk_R.p, c.ph.nu_sys,
+               c.con_diag.p, con_stream);
+      if (overlap == 3) launch_bt();
+    } else if (rhs_co && out.cdiag) {
       // the constrained-row diagonals only: the cells with a constrained node
       // in one launch, per (cell, node) slots, summed per node in colour order
       NseOut oc = out;

@@ -106,6 +106,14 @@ struct NseOut {
 };
 // cdiag[3 i + c] = sum over slots [cptr[i], cptr[i + 1]) of cbuf[3 slot + c]
 void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdiag, hipStream_t s);
+// the constrained-row diagonals in Kronecker form (kernels/assembly.hip,
+// k_cdk_*): the lateral (10 per column id and lateral node) and radial (4 per
+// layer and radial node) tables at upload; per assembly the sums over each
+// constrained node's slots rec[cptr[i] .. cptr[i + 1]) (cell 27 + local node)
+void cdk_tables(const double* colgeo, int n_cols, const double* laygeo, int n_layers, double* L,
+                double* R, hipStream_t s);
+void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const CellData& cd,
+              const double* L, const double* R, double nu, double* cdiag, hipStream_t s);
 
 // ---- assembly2d.hip -----------------------------------------------------------
 // Two-dimensional model (Standard::BoussinesqModel<2>): 22-dof cells over a

@@ -2237,7 +2237,116 @@ __global__ __launch_bounds__(64 * kBtRowWaves) void k_bt_tasks(
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// The constrained-row diagonals in Kronecker form (one GPU, layered shell).
+// A constrained node's diagonal sums, over the cells holding it, the cell's
+// |K_ii| per component (local_assemble_nse_system :626-637 restricted to the
+// diagonal, the value AffineConstraints puts on a constrained row):
+//   K_ii[d] = M + nu (g[0] + g[1] + g[2]) + nu g[d],  nu = dt / Re,
+//   M = sum_q JxW phi^2,  g[d] = sum_q JxW (d_d phi)^2.
+// With J^-1 rows m0 / R, m1 / R, m2 / R', JxW = R^2 R' D2 w and phi =
+// psi_ab(x, y) chi_c(z), d_d phi = (A_d chi_c) / R + (B_d chi'_c) / R' with
+// A_d = psi'_a psi_b m0[d] + psi_a psi'_b m1[d], B_d = psi_a psi_b m2[d], so
+// every term is a lateral 9-point sum times a radial 3-point sum:
+//   M = LM RM,  g[d] = L1[d] R1 + L2[d] R2 + L3[d] R3.
+// k_cdk_lateral / k_cdk_radial form the tables at upload (mesh geometry, like
+// the B^T column / layer factors); per assembly k_cdk_diag sums a node's cells
+// in the slot order of k_nse_rhs_halfwave + k_con_gather, which it replaces.
+// K_ii > 0 (the mass term), so the |.| and the zero-diagonal average rule of
+// the cell kernel never change a value here.
+__global__ void k_cdk_lateral(const double* __restrict__ colgeo, int n_cols, double* __restrict__ L) {
+  const int i = int(blockIdx.x) * blockDim.x + int(threadIdx.x);
+  if (i >= 9 * n_cols) return;
+  const int col = i / 9, ab = i - 9 * col, na = ab % 3, nb = ab / 3;
+  double lm = 0, l1[3] = {0, 0, 0}, l2[3] = {0, 0, 0}, l3[3] = {0, 0, 0};
+  for (int q1 = 0; q1 < 3; ++q1)
+    for (int q0 = 0; q0 < 3; ++q0) {
+      const double* m = colgeo + 90 * size_t(col) + 10 * (q0 + 3 * q1);
+      const double xa = sel_gauss(q0), xb = sel_gauss(q1);
+      const double la = ce_l2(na, xa), lb = ce_l2(nb, xb), da = ce_dl2(na, xa), db = ce_dl2(nb, xb);
+      const double w = cW[q0] * cW[q1] * m[9];
+      lm += w * (la * lb) * (la * lb);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const double A = da * lb * m[d] + la * db * m[3 + d], B = la * lb * m[6 + d];
+        l1[d] += w * A * A;
+        l2[d] += 2 * w * A * B;
+        l3[d] += w * B * B;
+      }
+    }
+  double* o = L + 10 * size_t(i);
+  o[0] = lm;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    o[1 + d] = l1[d];
+    o[4 + d] = l2[d];
+    o[7 + d] = l3[d];
+  }
+}
+
+__global__ void k_cdk_radial(const double* __restrict__ laygeo, int n_layers, double* __restrict__ R) {
+  const int i = int(blockIdx.x) * blockDim.x + int(threadIdx.x);
+  if (i >= 3 * n_layers) return;
+  const int lay = i / 3, c = i - 3 * lay;
+  double rm = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (int q2 = 0; q2 < 3; ++q2) {
+    const double* lg = laygeo + 9 * size_t(lay) + 3 * q2;
+    const double x = sel_gauss(q2), lc = ce_l2(c, x), dc = ce_dl2(c, x);
+    const double W = cW[q2] * lg[2], iR = lg[0], iRp = lg[1];
+    rm += W * lc * lc;
+    r1 += W * (iR * lc) * (iR * lc);
+    r2 += W * (iR * lc) * (iRp * dc);
+    r3 += W * (iRp * dc) * (iRp * dc);
+  }
+  double* o = R + 4 * size_t(i);
+  o[0] = rm;
+  o[1] = r1;
+  o[2] = r2;
+  o[3] = r3;
+}
+
+__global__ void k_cdk_diag(int n_con, const int32_t* __restrict__ cptr, const int32_t* __restrict__ rec,
+                           CellData cd, const double* __restrict__ L, const double* __restrict__ R,
+                           double nu, double* __restrict__ cdiag) {
+  const int ci = int(blockIdx.x) * blockDim.x + int(threadIdx.x);
+  if (ci >= n_con) return;
+  double s[3] = {0, 0, 0};
+  int node = 0;
+  for (int k = cptr[ci]; k < cptr[ci + 1]; ++k) {
+    const int r = rec[k], cell = r / 27, t = r - 27 * cell;
+    const double* l = L + 10 * (9 * size_t(cd.sep_col[cell]) + t % 9);
+    const double* rr = R + 4 * (3 * size_t(cd.sep_layer[cell]) + t / 9);
+    double g[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g[d] = l[1 + d] * rr[1] + l[4 + d] * rr[2] + l[7 + d] * rr[3];
+    const double M = l[0] * rr[0], G = g[0] + g[1] + g[2];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) s[d] += fabs(M + nu * G + nu * g[d]);
+    node = cd.cell_q2[r];
+  }
+  const NodeConstraint nc = cd.vcon[node];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+    cdiag[3 * size_t(ci) + d] = nc.type == 1 || nc.type == 3 || d == nc.k ? s[d] : 0.0;
+}
+
 }  // namespace
+
+void cdk_tables(const double* colgeo, int n_cols, const double* laygeo, int n_layers, double* L,
+                double* R, hipStream_t s) {
+  hipLaunchKernelGGL(k_cdk_lateral, dim3((9 * n_cols + 255) / 256), dim3(256), 0, s, colgeo, n_cols, L);
+  hipLaunchKernelGGL(k_cdk_radial, dim3((3 * n_layers + 255) / 256), dim3(256), 0, s, laygeo,
+                     n_layers, R);
+  DCP_HIP_CHECK(hipGetLastError());
+}
+
+void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const CellData& cd,
+              const double* L, const double* R, double nu, double* cdiag, hipStream_t s) {
+  if (n_con <= 0) return;
+  hipLaunchKernelGGL(k_cdk_diag, dim3((n_con + 255) / 256), dim3(256), 0, s, n_con, cptr, rec, cd, L,
+                     R, nu, cdiag);
+  DCP_HIP_CHECK(hipGetLastError());
+}
 
 void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdiag, hipStream_t s) {
   if (n_con <= 0) return;

@@ -73,6 +73,53 @@ def test_kronecker_bt_matches_oracle_and_row_tasks(monkeypatch, refine):
     old.close()
 
 
+@pytest.mark.parametrize("refine", [2, 3])
+def test_kronecker_constrained_diagonals(monkeypatch, refine):
+    """The constrained-row diagonals (no-normal-flux nodes: the |K_ii| of the
+    cells holding the node, what AffineConstraints puts on a constrained row)
+    in Kronecker form (k_cdk_diag, assembly.hip) against the cell pass +
+    con_gather (DCP_CDIAG_KRON=0): the velocity apply and the Stokes apply at
+    1e-13, the velocity apply against the oracle's assembled nse_matrix at
+    1e-12, bitwise repeatable, and a time
+    step change (dt / Re in K_ii) followed by the next assembly."""
+    m = dcp.HostMesh(refine=refine)
+    ph = dcp.classic_physics()
+    rng = np.random.default_rng(SEED + 40 + refine)
+    u = rng.uniform(-1, 1, m.n_u + m.n_p)
+    T = m.T0 + 0.1 * rng.uniform(-1, 1, m.n_T)
+    x = rng.uniform(-1, 1, m.n_u + m.n_p)
+    out = {}
+    for kron in ("1", "0"):
+        monkeypatch.setenv("DCP_CDIAG_KRON", kron)
+        ctx = make_ctx(m, ph, True, monkeypatch)
+        monkeypatch.delenv("DCP_CDIAG_KRON", raising=False)
+        ctx.set_state(dcp.OLD_NSE_SOLUTION, u)
+        ctx.set_state(dcp.OLD_T_SOLUTION, T)
+        ctx.assemble_nse_system()
+        r = [ctx.velocity_vmult(x[:m.n_u]), ctx.nse_vmult(x), None]
+        ctx.assemble_nse_system()
+        r.append(ctx.velocity_vmult(x[:m.n_u]))
+        ctx.set_time_step(0.5 * ph.time_step)
+        ctx.assemble_nse_system()
+        r.append(ctx.velocity_vmult(x[:m.n_u]))
+        out[kron] = r
+        ctx.close()
+    k, c = out["1"], out["0"]
+    for a, b in zip(k[:2], c[:2]):
+        assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(b))
+    assert np.array_equal(k[0], k[3])
+    assert np.max(np.abs(k[4] - c[4])) <= 1e-13 * np.max(np.abs(c[4]))
+    assert not np.allclose(k[4], k[0], rtol=1e-6)  # dt entered K_ii
+    # the velocity apply, constrained rows included, against the oracle's
+    # assembled nse_matrix (velocity block) times x
+    orc = oracle_py.Model(ph, m)
+    orc.assemble_nse_system(u, T)
+    xv = x.copy()
+    xv[m.n_u:] = 0.0
+    yo = orc.nse_vmult(xv)[:m.n_u]
+    assert np.max(np.abs(k[0] - yo)) <= 1e-12 * np.max(np.abs(yo))
+
+
 def test_kronecker_bt_solve_matches_row_tasks(monkeypatch):
     """The block-preconditioned solve on either B^T: equal FGMRES / inner
     counts, iterates at 1e-10 (the inner GMRES held at a fixed step count, so

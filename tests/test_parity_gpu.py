@@ -106,7 +106,8 @@ def test_operator_form_assembly_is_the_full_assembly(monkeypatch, bt_kron):
     (DCP_BT_KRON=0) everything the solve reads must be bitwise what the full
     distribute_local_to_global scatter produces (the rhs, summed in another
     order, to 1e-13); the Kronecker-form B^T (default on one GPU) sums the
-    same products over lateral columns and layers instead of cells: 1e-13.
+    same products over lateral columns and layers instead of cells, and the
+    constrained-row diagonals likewise: 1e-13.
     The block materialised on export must be the one of the assembly's time
     step."""
     monkeypatch.setenv("DCP_BT_KRON", bt_kron)
@@ -142,7 +143,9 @@ def test_operator_form_assembly_is_the_full_assembly(monkeypatch, bt_kron):
         assert np.array_equal(y0, y1) and np.array_equal(yv0, yv1)
         assert (K0 != K1).nnz == 0
     else:
-        assert rel_max(y0, y1) < 1e-13 and np.array_equal(yv0, yv1)
+        # (the constrained-row diagonals in Kronecker form too, k_cdk_diag: the
+        # same |K_ii| sums, each cell's term as lateral x radial sums)
+        assert rel_max(y0, y1) < 1e-13 and rel_max(yv0, yv1) < 1e-13
         assert abs(K0 - K1).max() <= 1e-13 * abs(K1).max()
     assert np.array_equal(y0, y20) and np.array_equal(y1, y21)
     # the materialised operator is the one the matrix-free apply evaluates
