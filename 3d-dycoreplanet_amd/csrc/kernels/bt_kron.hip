@@ -85,10 +85,12 @@ __device__ __forceinline__ void btk_terms(const BtkDev& b, const double* sq, int
   }
 }
 
-// The block's records are staged into LDS first. The 64 entries of a wave (per u) are 192 consecutive
-// doubles of B^T: staged in LDS so each store instruction writes 512
-// contiguous bytes. Entries of constrained rows are written unconstrained here
-// and overwritten by k_btk_con (same stream, after).
+// The block's records are staged into LDS first. The 64 entries of a wave
+// (per u) are 192 consecutive doubles of B^T: staged in LDS so each store
+// instruction writes 512 contiguous bytes (every lane storing its own 24 bytes
+// instead: 392 against 382 us per assembly, profiles/r06/r06al_direct_store.log).
+// Entries of constrained rows are written unconstrained here and overwritten
+// by k_btk_con (same stream, after).
 __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double* __restrict__ Bt) {
   extern __shared__ __attribute__((aligned(16))) double sq[];
   double2* srec = reinterpret_cast<double2*>(sq + 12 * b.n_layers);
