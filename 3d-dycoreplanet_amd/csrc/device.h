@@ -590,6 +590,10 @@ struct GmresDev {
   // and the pending scale nu_k / beta_k of that correction
   double Hr[kGmMaxDim + 1][kGmMaxDim];
   double c_pend;
+  // status as the launch before a multi-launch step's last kernel saw it: that
+  // kernel's block 0 may stop the cycle (Givens step) while its other blocks
+  // still have their rows to write, so they test this copy, not status
+  int status_in;
 };
 // What the host reads after a cycle (pinned, written by gmres_cycle_end)
 struct GmresReport {

@@ -1203,8 +1203,10 @@ __global__ __launch_bounds__(kBlock) void k_ss_dots(Seg g, ChainVecs V, SStepArg
 // reducing workgroup reads ~6 MB at refine 6 and is load-latency bound).
 __global__ __launch_bounds__(kBlock) void k_ss_colsum(const double* __restrict__ gran, int nb,
                                                       double* out, unsigned long long seq,
-                                                      double* err, const int* __restrict__ status) {
+                                                      double* err, const int* __restrict__ status,
+                                                      int* status_in) {
   __shared__ double sm[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *status_in = *status;  // for k_ss_final
   if (*status) return;
   const int c = blockIdx.x;
   const unsigned long long tag = seq * 256 + 1;
@@ -1234,7 +1236,9 @@ __global__ __launch_bounds__(kBlock) void k_ss_final(Seg g, ChainVecs V, SStepAr
   __shared__ double Gp[S * (S + 1) / 2];
   __shared__ SsHess hs;
   __shared__ int bad;
-  if (st->status) return;
+  // not st->status: block 0 sets it below (a stop at this block) while other
+  // blocks may not have started; every block must still write its rows of q
+  if (st->status_in) return;
   const int d = k + 1, ncol1 = S * d;
   if (blockIdx.x == 0) sstep_hess_stage(hs, st, k);
   for (int c = threadIdx.x; c < ncol1 + S * (S + 1) / 2; c += kBlock) {
@@ -1334,14 +1338,14 @@ void sstep_block_multi(Seg g, const ChainVecs& V, const SStepArgs& a, int k, Gmr
                        gran, ++seq, status);                                                     \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     hipLaunchKernelGGL(k_ss_colsum, dim3(ncol1), dim3(kBlock), 0, s, gran, nb, c1, seq, err,     \
-                       status);                                                                  \
+                       status, &st->status_in);                                                  \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     if (comm) comm->allreduce(c1, size_t(ncol1), false, s);                                      \
     hipLaunchKernelGGL((k_ss_dots<KL, 1>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, gran, \
                        ++seq, status);                                                           \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     hipLaunchKernelGGL(k_ss_colsum, dim3(ncol2), dim3(kBlock), 0, s, gran, nb, c2, seq, err,     \
-                       status);                                                                  \
+                       status, &st->status_in);                                                  \
     DCP_HIP_CHECK(hipGetLastError());                                                            \
     if (comm) comm->allreduce(c2, size_t(ncol2), false, s);                                      \
     hipLaunchKernelGGL((k_ss_final<KL>), dim3(nb), dim3(kBlock), 0, s, g, Vp, a, k, c1, c2, st); \
@@ -1659,6 +1663,7 @@ __global__ __launch_bounds__(kBlock) void k_dcgs_partials(Seg g, const double* _
   constexpr int K = 2 * KP;
   __shared__ double sm[4 * K];
   __shared__ int is_last;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->status_in = st->status;  // for k_dcgs_update
   if (st->status) return;
   double s[K];
 #pragma unroll
@@ -1722,7 +1727,9 @@ __global__ __launch_bounds__(kBlock) void k_dcgs_update(Seg g, const double* __r
   constexpr int KP = dcgs_kp<KL>();
   constexpr int K = 2 * KP;
   __shared__ double hs[K];
-  if (st->status) return;
+  // not st->status: block 0's bookkeeping may stop the cycle while other
+  // blocks have not started; every block must still write its rows
+  if (st->status_in) return;
   const bool tail = tnext == nullptr;
   if (int(threadIdx.x) < K) hs[threadIdx.x] = st->coef[threadIdx.x];
   __syncthreads();

@@ -76,6 +76,8 @@ def time_steps():
         def setup(ctx):
             ctx.set_gram_schmidt(gs)
             ctx.set_block_fixed_inner(fixed)
+            if os.environ.get("WORKER_MP") == "0":  # diagnostics: per-SpMV halo exchanges
+                ctx.set_matrix_powers(False)
 
         out = {}
         extra = {}
@@ -97,6 +99,8 @@ def time_steps():
                 extra["again"] = _group_run(world, m, ph, u, T, setup,
                                             lambda c: [c.comm_info()["transport"],
                                                        c.timings()["solve_nse_ms"]])
+            if os.environ.get("LOCAL_TWICE") and not peer:
+                extra["local_again"] = _group_run(world, m, ph, u, T, setup, None)
             out[peer] = _group_run(world, m, ph, u, T, setup,
                                    lambda c: [c.comm_info()["transport"], c.timings()["solve_nse_ms"],
                                                        c.timings().get("handoff_timeouts", 0)])
@@ -117,6 +121,10 @@ def time_steps():
                 diff[f"{r}:cfl/vmax"] = [a["cfl"], b["cfl"], a["vmax"], b["vmax"]]
         for key_ in [k_ for k_ in extra if k_.startswith("var ")]:
             diff[key_] = extra[key_]
+        if "local_again" in extra:
+            diff["local_vs_local_bitwise"] = all(
+                np.array_equal(a["x"].view(np.int64), b["x"].view(np.int64))
+                for a, b in zip(extra["local_again"], out[False]))
         if "again" in extra:
             diff["peer_vs_peer_bitwise"] = all(
                 np.array_equal(a["x"].view(np.int64), b["x"].view(np.int64))

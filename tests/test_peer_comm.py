@@ -40,25 +40,15 @@ def test_peer_allreduce_sums_in_rank_order():
 
 
 def test_peer_group_time_step_is_bitwise_local():
-    """2 and 3 ranks: bitwise. 8 in-process ranks on one GPU: equal counts,
-    the rhs, T rhs and the temperature bitwise, the NSE iterate within 1e-13
-    (a run-to-run difference of ~1e-15 in that solve with the peer
-    all-reduce, which a stream synchronisation after each all-reduce removes;
-    the peer sums themselves are exact: the CG through them is bitwise)."""
+    """Bitwise on 2, 3 and 8 ranks. (The 8-rank s-step case found a race in
+    the multi-launch s-step and DCGS2 steps: k_ss_final / k_dcgs_update tested
+    st->status, which their block 0 sets when the cycle stops there, so blocks
+    scheduled after it skipped their rows of the last basis vectors; they now
+    test the copy the previous launch took, GmresDev::status_in. DESIGN 12b.)"""
     for r in _worker("time_steps"):
         print(r)
         assert r["transports"] == ["peer", "in-process"], r
-        if r["world"] <= 3:
-            assert r["bitwise"], r
-        else:
-            bad = {k: v for k, v in r["diff"].items()
-                   if not k.endswith(":x") and not k.endswith(":cfl/vmax")}
-            assert not bad, r
-            assert all(v < 1e-13 for k, v in r["diff"].items() if k.endswith(":x")), r
-            for k, v in r["diff"].items():
-                if k.endswith(":cfl/vmax"):
-                    assert abs(v[0] - v[1]) <= 1e-12 * abs(v[1]), r
-                    assert abs(v[2] - v[3]) <= 1e-12 * abs(v[3]), r
+        assert r["bitwise"], r
 
 
 def test_peer_comm_refuses_shared_hardware_queues(monkeypatch):
