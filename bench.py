@@ -60,7 +60,7 @@ CHAIN_STATS = {(5, "classical2"): "profiles/r03a_bench_r5_kernel_stats.csv",
 # launches per assembly (the rhs kernel once per colour class)
 PMC_ASM = {5: ("profiles/r06/r06_pmc_asm_r5.json",
                {"k_btk_lateral": 1, "k_btk_entries": 1, "k_btk_con": 1, "k_mf_pencil": 1,
-                "k_mf_gather": 1, "k_nse_rhs_halfwave": 1, "k_con_gather": 1})}
+                "k_mf_gather": 1, "k_cdk_diag": 1})}
 # (k_bt_coltab / k_bt_laytab run once at upload)
 # the same for the matrix-free Stokes apply (pencil kernel + dof gather); the
 # kernel names must be found in the summary (no stale profile of other kernels)
@@ -1014,9 +1014,8 @@ def main():
     asm_ach = asm_bytes / (asm_ms * 1e-3) / 1e9
     out["roofline_assembly"] = {
         "kernel": "operator-form assemble_nse_system (B^T in Kronecker form: k_btk_lateral "
-                  "+ k_btk_entries + k_btk_con; the rhs by the pencil kernel + velocity gather, "
-                  "the constrained diagonals by k_nse_rhs_halfwave over the constrained cells "
-                  "+ k_con_gather)",
+                  "+ k_btk_entries + k_btk_con; the rhs by the pencil kernel + velocity gather; "
+                  "the constrained diagonals in Kronecker form, k_cdk_diag)",
         "bound": "hbm", "achieved": asm_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": asm_ach / HBM_PEAK_GBS, "bytes_per_assembly": asm_bytes, "ms": asm_ms,
         "frac_measured_copy_ceiling": asm_ach / ceil["copy_GBps"] if ceil else None,
