@@ -2373,7 +2373,8 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             c.con_color_ptr.clear();
             c.con_color_cells.release();
             c.rhs_cell_order = h.tdpc == 8 && !(env_rhs && *env_rhs == '0');
-            std::vector<int32_t> cdk_rec;  // per slot: cell 27 + local node
+            // per slot: (lateral, radial) table indices; per node: constrained components
+            std::vector<int32_t> cdk_rec, cdk_mask;
             if (c.rhs_cell_order) {
               std::vector<int32_t> sub;
               c.con_color_ptr.assign(1, 0);
@@ -2405,10 +2406,19 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
               c.con_cptr.upload(cptr);
               c.con_cslot.upload(cslot);
               c.con_cbuf.alloc(3 * size_t(std::max(cptr[n_con], 1)));
-              cdk_rec.assign(size_t(cptr[n_con]), 0);
+              cdk_rec.assign(2 * size_t(cptr[n_con]), 0);
+              cdk_mask.assign(size_t(n_con), 0);
               for (size_t k = 0; k < sub.size(); ++k)
-                for (int t = 0; t < 27; ++t)
-                  if (cslot[27 * k + t] >= 0) cdk_rec[size_t(cslot[27 * k + t])] = 27 * sub[k] + t;
+                for (int t = 0; t < 27; ++t) {
+                  const int sl = cslot[27 * k + t];
+                  if (sl < 0) continue;
+                  cdk_rec[2 * size_t(sl)] = 9 * col[size_t(sub[k])] + t % 9;
+                  cdk_rec[2 * size_t(sl) + 1] = 3 * layer[size_t(sub[k])] + t / 9;
+                  const int nd = q2[27 * size_t(sub[k]) + t];
+                  const NodeConstraint& nc = vc[size_t(nd)];
+                  cdk_mask[size_t(cidx[size_t(nd)])] =
+                      nc.type == 1 || nc.type == 3 ? 7 : (nc.type == 2 ? 1 << nc.k : 0);
+                }
             }
             // the column factors P of the B^T entries are mesh geometry
             // (the column tables, reference functions): formed once here
@@ -2430,6 +2440,7 @@ void upload_prepared(Ctx& c, HostPrep& h, const LocalMesh& L, bool dist, int n_c
             const char* env_cd = std::getenv("DCP_CDIAG_KRON");
             if (c.btk && c.rhs_cell_order && !cdk_rec.empty() && !(env_cd && *env_cd == '0')) {
               c.cdk_rec.upload(cdk_rec);
+              c.cdk_mask.upload(cdk_mask);
               c.cdk_L.alloc(size_t(90) * c.bt_ncols);
               c.cdk_R.alloc(size_t(12) * nlay);
               cdk_tables(c.mf_colgeo.p, c.bt_ncols, c.mf_laygeo.p, nlay, c.cdk_L.p, c.cdk_R.p,
@@ -2763,8 +2774,8 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
     }
     if (overlap == 3 && !out.cdiag) launch_bt();  // nothing to overlap: B^T first anyway
     if (rhs_co && out.cdiag && c.cdk) {
-      cdk_diag(c.n_con, c.con_cptr.p, c.cdk_rec.p, c.cd(), c.cdk_L.p, c.cdk_R.p, c.ph.nu_sys,
-               c.con_diag.p, con_stream);
+      cdk_diag(c.n_con, c.con_cptr.p, c.cdk_rec.p, c.cdk_mask.p, c.cdk_L.p, c.cdk_R.p,
+               c.ph.nu_sys, c.con_diag.p, con_stream);
       if (overlap == 3) launch_bt();
     } else if (rhs_co && out.cdiag) {
       // the constrained-row diagonals only: the cells with a constrained node

@@ -197,9 +197,10 @@ struct Ctx {
   DBuf<int32_t> con_cptr, con_cslot;  // slots of the constrained diagonals (con_gather)
   DBuf<double> con_cbuf;
   // the same diagonals in Kronecker form (k_cdk_*, one GPU, layered shell):
-  // per slot its (cell 27 + local node), and the lateral / radial tables
+  // per slot its (lateral, radial) table indices, per node its constrained
+  // components, and the lateral / radial tables
   bool cdk = false;
-  DBuf<int32_t> cdk_rec;
+  DBuf<int32_t> cdk_rec, cdk_mask;
   DBuf<double> cdk_L, cdk_R;
   DBuf<double> bt_P;  // [n_cols][216] column factors, then [n_layers][12] layer factors (upload)
   double* bt_Q = nullptr;

@@ -109,10 +109,12 @@ void con_gather(int n_con, const int32_t* cptr, const double* cbuf, double* cdia
 // the constrained-row diagonals in Kronecker form (kernels/assembly.hip,
 // k_cdk_*): the lateral (10 per column id and lateral node) and radial (4 per
 // layer and radial node) tables at upload; per assembly the sums over each
-// constrained node's slots rec[cptr[i] .. cptr[i + 1]) (cell 27 + local node)
+// constrained node's slots [cptr[i], cptr[i + 1]), rec holding per slot the
+// pair (lateral table index, radial table index), mask[i] the node's
+// constrained components (bit d)
 void cdk_tables(const double* colgeo, int n_cols, const double* laygeo, int n_layers, double* L,
                 double* R, hipStream_t s);
-void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const CellData& cd,
+void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const int32_t* mask,
               const double* L, const double* R, double nu, double* cdiag, hipStream_t s);
 
 // ---- assembly2d.hip -----------------------------------------------------------

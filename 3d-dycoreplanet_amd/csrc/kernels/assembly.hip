@@ -2305,29 +2305,26 @@ __global__ void k_cdk_radial(const double* __restrict__ laygeo, int n_layers, do
   o[3] = r3;
 }
 
-__global__ void k_cdk_diag(int n_con, const int32_t* __restrict__ cptr, const int32_t* __restrict__ rec,
-                           CellData cd, const double* __restrict__ L, const double* __restrict__ R,
-                           double nu, double* __restrict__ cdiag) {
+__global__ void k_cdk_diag(int n_con, const int32_t* __restrict__ cptr, const int2* __restrict__ rec,
+                           const int32_t* __restrict__ mask, const double* __restrict__ L,
+                           const double* __restrict__ R, double nu, double* __restrict__ cdiag) {
   const int ci = int(blockIdx.x) * blockDim.x + int(threadIdx.x);
   if (ci >= n_con) return;
   double s[3] = {0, 0, 0};
-  int node = 0;
   for (int k = cptr[ci]; k < cptr[ci + 1]; ++k) {
-    const int r = rec[k], cell = r / 27, t = r - 27 * cell;
-    const double* l = L + 10 * (9 * size_t(cd.sep_col[cell]) + t % 9);
-    const double* rr = R + 4 * (3 * size_t(cd.sep_layer[cell]) + t / 9);
+    const int2 r = rec[k];  // lateral table (column id 9 + ab), radial table (layer 3 + c)
+    const double* l = L + 10 * size_t(r.x);
+    const double* rr = R + 4 * size_t(r.y);
     double g[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) g[d] = l[1 + d] * rr[1] + l[4 + d] * rr[2] + l[7 + d] * rr[3];
     const double M = l[0] * rr[0], G = g[0] + g[1] + g[2];
 #pragma unroll
     for (int d = 0; d < 3; ++d) s[d] += fabs(M + nu * G + nu * g[d]);
-    node = cd.cell_q2[r];
   }
-  const NodeConstraint nc = cd.vcon[node];
+  const int on = mask[ci];  // the row's constrained components (condensation)
 #pragma unroll
-  for (int d = 0; d < 3; ++d)
-    cdiag[3 * size_t(ci) + d] = nc.type == 1 || nc.type == 3 || d == nc.k ? s[d] : 0.0;
+  for (int d = 0; d < 3; ++d) cdiag[3 * size_t(ci) + d] = (on >> d) & 1 ? s[d] : 0.0;
 }
 
 }  // namespace
@@ -2340,11 +2337,11 @@ void cdk_tables(const double* colgeo, int n_cols, const double* laygeo, int n_la
   DCP_HIP_CHECK(hipGetLastError());
 }
 
-void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const CellData& cd,
+void cdk_diag(int n_con, const int32_t* cptr, const int32_t* rec, const int32_t* mask,
               const double* L, const double* R, double nu, double* cdiag, hipStream_t s) {
   if (n_con <= 0) return;
-  hipLaunchKernelGGL(k_cdk_diag, dim3((n_con + 255) / 256), dim3(256), 0, s, n_con, cptr, rec, cd, L,
-                     R, nu, cdiag);
+  hipLaunchKernelGGL(k_cdk_diag, dim3((n_con + 255) / 256), dim3(256), 0, s, n_con, cptr,
+                     reinterpret_cast<const int2*>(rec), mask, L, R, nu, cdiag);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
