@@ -137,12 +137,6 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
 #pragma unroll
   for (int u = 0; u < kPT; ++u) {
     const uint32_t cu = code[u];
-    if (b.probe & 2) {  // probe: no A / Q reads
-      v[u][0] = double(cu & 1023u);
-      v[u][1] = double((cu >> 10) & 1023u);
-      v[u][2] = double(cu >> 20);
-      continue;
-    }
     const int s0 = int(cu & 1023u), s1 = int((cu >> 10) & 1023u);
     btk_terms(b, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u),
               [&](int t, int) { return srec + 3 * (t ? s1 : s0); }, v[u]);
@@ -158,11 +152,17 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
     const long e0 = base - lane + long(u) * kTB;  // the wave's first entry
     const long left = 3 * (nnz - e0);             // doubles of B^T left from there
     double* dst = Bt + 3 * e0;
+    // the three LDS reads before the stores: one wait, not one per store
+    double o[3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int k = lane + 64 * r;
-      if (k < left && !(b.probe & 4)) __builtin_nontemporal_store(stage[wave][k], dst + k);
-      if (k < left && (b.probe & 4) && stage[wave][k] == 12345.0) dst[k] = 0.0;  // probe: no stores
+    for (int r = 0; r < 3; ++r) o[r] = stage[wave][lane + 64 * r];
+    if (left >= 192) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) __builtin_nontemporal_store(o[r], dst + lane + 64 * r);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        if (lane + 64 * r < left) __builtin_nontemporal_store(o[r], dst + lane + 64 * r);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
