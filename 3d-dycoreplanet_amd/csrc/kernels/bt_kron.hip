@@ -59,30 +59,36 @@ __global__ __launch_bounds__(kTB) void k_btk_lateral(BtkDev b) {
 }
 
 // The one or two layer terms of an entry (node level lambda, l - lambda / 2 + 1
-// = dl): rec(t, L) is the A record of term t (0, 1) in layer L.
-template <class Rec>
-__device__ __forceinline__ void btk_terms(const BtkDev& b, const double* sq, int lam, int dl,
-                                          Rec rec, double v[3]) {
+// = dl), records r0 / r1 of terms 0 / 1:
+//   lambda odd         term 0: layer m, c 1, k dl - 1
+//   dl = 0             term 0: layer m - 1, c 2, k 0          (m >= 1)
+//   dl = 2             term 0: layer m, c 0, k 1
+//   dl = 1             term 0: layer m - 1, c 2, k 1 (m >= 1); term 1: layer m, c 0, k 0 (m < NL)
+// Branch-free (the lanes of a wave hold every case; as branches each case
+// took its own pass of LDS reads): both terms always, an absent one with
+// factors q = 0, which leaves v bitwise as without it (v - (A 0 + A 0) = v).
+__device__ __forceinline__ void btk_terms(int n_layers, const double* sq, int lam, int dl,
+                                          const double2* r0, const double2* r1, double v[3]) {
   const int m = lam >> 1;
-  v[0] = v[1] = v[2] = 0.0;
-  auto add = [&](int t, int L, int c, int k) {
-    const double2* a2 = rec(t, L);
-    const double2 A0 = a2[0], A1 = a2[1], A2 = a2[2];
-    const double q01 = sq[12 * L + 4 * c + 2 * k], q2 = sq[12 * L + 4 * c + 2 * k + 1];
-    v[0] -= A0.x * q01 + A1.y * q2;
-    v[1] -= A0.y * q01 + A2.x * q2;
-    v[2] -= A1.x * q01 + A2.y * q2;
-  };
-  if (lam & 1) {
-    add(0, m, 1, dl - 1);
-  } else if (dl == 0) {
-    if (m >= 1) add(0, m - 1, 2, 0);
-  } else if (dl == 2) {
-    add(0, m, 0, 1);
-  } else {
-    if (m >= 1) add(0, m - 1, 2, 1);
-    if (m < b.n_layers) add(1, m, 0, 0);
-  }
+  const bool odd = lam & 1;
+  const int L0 = odd || dl == 2 ? m : m - 1;
+  const int c0 = odd ? 1 : (dl == 2 ? 0 : 2);
+  const int k0 = odd ? dl - 1 : (dl == 0 ? 0 : 1);
+  const bool p0 = L0 >= 0;
+  const bool p1 = !odd && dl == 1 && m < n_layers;
+  const int i0 = 12 * (p0 ? L0 : 0) + 4 * c0 + 2 * k0, i1 = 12 * (p1 ? m : 0);
+  const double2 Q0 = *reinterpret_cast<const double2*>(sq + i0);
+  const double2 Q1 = *reinterpret_cast<const double2*>(sq + i1);
+  const double q01a = p0 ? Q0.x : 0.0, q2a = p0 ? Q0.y : 0.0;
+  const double q01b = p1 ? Q1.x : 0.0, q2b = p1 ? Q1.y : 0.0;
+  const double2 A0 = r0[0], A1 = r0[1], A2 = r0[2];
+  const double2 B0 = r1[0], B1 = r1[1], B2 = r1[2];
+  v[0] = 0.0 - (A0.x * q01a + A1.y * q2a);
+  v[1] = 0.0 - (A0.y * q01a + A2.x * q2a);
+  v[2] = 0.0 - (A1.x * q01a + A2.y * q2a);
+  v[0] -= B0.x * q01b + B1.y * q2b;
+  v[1] -= B0.y * q01b + B2.x * q2b;
+  v[2] -= B1.x * q01b + B2.y * q2b;
 }
 
 // The block's records are staged into LDS first. The 64 entries of a wave
@@ -133,19 +139,18 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
   for (int i = threadIdx.x; i < 12 * b.n_layers; i += kTB)
     sq[i] = b.Q[12 * size_t(b.ord2lay[i / 12]) + i % 12];
   __syncthreads();
-  double v[kPT][3];
+  // per u: the entry from LDS, then straight through the stage to the stores
+  // (all kPT entries first held 8 x 12 double2 of records: 252 VGPRs)
 #pragma unroll
   for (int u = 0; u < kPT; ++u) {
     const uint32_t cu = code[u];
     const int s0 = int(cu & 1023u), s1 = int((cu >> 10) & 1023u);
-    btk_terms(b, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u),
-              [&](int t, int) { return srec + 3 * (t ? s1 : s0); }, v[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < kPT; ++u) {
-    stage[wave][3 * lane] = v[u][0];
-    stage[wave][3 * lane + 1] = v[u][1];
-    stage[wave][3 * lane + 2] = v[u][2];
+    double v[3];
+    btk_terms(b.n_layers, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u), srec + 3 * s0,
+              srec + 3 * s1, v);
+    stage[wave][3 * lane] = v[0];
+    stage[wave][3 * lane + 1] = v[1];
+    stage[wave][3 * lane + 2] = v[2];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
