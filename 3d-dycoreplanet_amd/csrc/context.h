@@ -369,7 +369,9 @@ struct Ctx {
   int ts_n_colids = 0, ts_n_layers = 0, ts_n_kinds = 0, ts_n_latnnz = 0, ts_n_con = 0;
   DBuf<int32_t> ts_ord2lay, ts_lay2ord, ts_kind, ts_lptr, ts_lcon, ts_sptr, ts_slot;
   DBuf<uint16_t> ts_cmask;
-  DBuf<uint32_t> ts_code;
+  DBuf<uint32_t> ts_code, ts_rcode;
+  DBuf<int32_t> ts_blk_ptr, ts_blk_rec;
+  int ts_blk_pt = 0, ts_max_rec = 0;
   DBuf<double> ts_loc, ts_rad, ts_A, ts_rec;
   bool ts_tmat_valid = false;  // Tmat / T_inv of the last matrix assembly, made with ts_tmat_dt
   double ts_tmat_dt = 0.0;
@@ -392,6 +394,11 @@ struct Ctx {
     t.lptr = ts_lptr.p;
     t.lcon = ts_lcon.p;
     t.code = ts_code.p;
+    t.blk_pt = ts_blk_pt;
+    t.max_rec = ts_max_rec;
+    t.blk_ptr = ts_blk_ptr.p;
+    t.blk_rec = ts_blk_rec.p;
+    t.rcode = ts_rcode.p;
     t.T_col = T_col.p;
     t.sptr = ts_sptr.p;
     t.slot = ts_slot.p;

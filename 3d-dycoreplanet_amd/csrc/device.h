@@ -340,6 +340,14 @@ struct TSepDev {
   const int32_t* lcon = nullptr;     // [n_kinds][n_con] column id << 4 | alpha << 2 | beta
   const uint16_t* cmask = nullptr;   // [n_cells] fixed vertices | lifted vertices << 8
   const uint32_t* code = nullptr;    // [nnz of T] (k_tsep_matrix)
+  // k_tsep_matrix_lds: per block of blk_pt x 256 consecutive entries its
+  // distinct A records (kind n_latnnz + p), staged in LDS; the entries coded
+  // by slot (bits 0-9 term a, 10-19 term b, 20-27 l, 28-29 dl, 30 zero, 31
+  // diagonal) in rcode. blk_pt 0: no lists (k_tsep_matrix reads A per entry)
+  int blk_pt = 0, max_rec = 0;
+  const int32_t* blk_ptr = nullptr;
+  const int32_t* blk_rec = nullptr;
+  const uint32_t* rcode = nullptr;
   const int32_t* T_col = nullptr;
   const int32_t* sptr = nullptr;     // [n_T + 1] records of each T dof
   const int32_t* slot = nullptr;     // 8 cell + a, ascending cell

@@ -243,6 +243,86 @@ __global__ __launch_bounds__(kTB) void k_tsep_matrix(TSepDev t, long nnz, double
   }
 }
 
+// The same entries from per-block records (tsep.cpp): the block's distinct A
+// records staged into LDS with coalesced loads (the per-entry A loads above
+// are 3 scattered 16-byte reads per term, bound by the vector memory pipe's
+// line rate, as k_btk_entries was), then both terms of every entry from LDS,
+// branch-free: an absent term (or a zero entry) with radial factors 0, which
+// leaves mm / kk bitwise as without it (x + A 0 = x).
+template <int PT>
+__global__ __launch_bounds__(kTB) void k_tsep_matrix_lds(TSepDev t, long nnz, double one_over_pe,
+                                                         double dt_T, double* __restrict__ M,
+                                                         double* __restrict__ K,
+                                                         double* __restrict__ Tmat,
+                                                         double* __restrict__ Tinv) {
+  extern __shared__ __attribute__((aligned(16))) double srad[];
+  double2* srec = reinterpret_cast<double2*>(srad + 16 * t.n_layers);
+  const int blk = xcd_block(int(blockIdx.x), int(gridDim.x));
+  const long base = long(blk) * (PT * kTB) + threadIdx.x;
+  const int r0 = t.blk_ptr[blk], nr = t.blk_ptr[blk + 1] - r0;  // nr >= 1
+  constexpr int kU = 4;  // 4 kTB double2 = 341 records without the loop below
+  int rid[kU];
+#pragma unroll
+  for (int q = 0; q < kU; ++q) rid[q] = t.blk_rec[r0 + min((int(threadIdx.x) + q * kTB) / 3, nr - 1)];
+  uint32_t code[PT];
+#pragma unroll
+  for (int u = 0; u < PT; ++u)
+    code[u] = __builtin_nontemporal_load(t.rcode + min(base + long(u) * kTB, nnz - 1));
+  const double2* A2 = reinterpret_cast<const double2*>(t.A);
+  double2 ra[kU];
+#pragma unroll
+  for (int q = 0; q < kU; ++q) {
+    const int i = int(threadIdx.x) + q * kTB;
+    ra[q] = A2[3 * size_t(rid[q]) + (i - 3 * (i / 3))];
+  }
+#pragma unroll
+  for (int q = 0; q < kU; ++q) {
+    const int i = int(threadIdx.x) + q * kTB;
+    if (i < 3 * nr) srec[i] = ra[q];
+  }
+  for (int i = threadIdx.x + kU * kTB; i < 3 * nr; i += kTB) {
+    const int j = i / 3;
+    srec[i] = A2[3 * size_t(t.blk_rec[r0 + j]) + (i - 3 * j)];
+  }
+  for (int i = threadIdx.x; i < 16 * t.n_layers; i += kTB) srad[i] = t.rad[i];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < PT; ++u) {
+    const long e = base + long(u) * kTB;
+    const uint32_t c = code[u];
+    const int sa = int(c & 1023u), sb = int((c >> 10) & 1023u);
+    const int l = int((c >> 20) & 0xFFu), dl = int((c >> 28) & 3u);
+    const bool zero = (c >> 30) & 1u;
+    const int oa = dl == 2 ? l : l - 1;
+    const int ra_ = dl == 2 ? 1 : (dl == 0 ? 2 : 3);
+    const int rt = ((ra_ & 1) << 1) | (ra_ >> 1);
+    const bool has_a = !zero && oa >= 0;
+    const bool has_b = !zero && dl == 1 && l < t.n_layers;
+    const double* qa = srad + 16 * (oa >= 0 ? oa : 0);
+    const double* qb = srad + 16 * (l < t.n_layers ? l : 0);
+    const double fa0 = has_a ? qa[ra_] : 0.0, fa1 = has_a ? qa[4 + ra_] : 0.0;
+    const double fa2 = has_a ? qa[8 + ra_] : 0.0, fa3 = has_a ? qa[8 + rt] : 0.0;
+    const double fa4 = has_a ? qa[12 + ra_] : 0.0;
+    const double fb0 = has_b ? qb[0] : 0.0, fb1 = has_b ? qb[4] : 0.0;
+    const double fb2 = has_b ? qb[8] : 0.0, fb4 = has_b ? qb[12] : 0.0;
+    const double2 A0 = srec[3 * sa], A1 = srec[3 * sa + 1], A2v = srec[3 * sa + 2];
+    const double2 B0 = srec[3 * sb], B1 = srec[3 * sb + 1], B2 = srec[3 * sb + 2];
+    double mm = 0.0, kk = 0.0;
+    mm += A0.x * fa0;
+    kk += A0.y * fa1 + A1.x * fa2 + A1.y * fa3 + A2v.x * fa4;
+    mm += B0.x * fb0;
+    kk += B0.y * fb1 + B1.x * fb2 + B1.y * fb2 + B2.x * fb4;
+    const double m = mm, k = kk * one_over_pe;
+    if (e < nnz) {
+      const double tm = m + dt_T * k;
+      __builtin_nontemporal_store(m, M + e);
+      __builtin_nontemporal_store(k, K + e);
+      __builtin_nontemporal_store(tm, Tmat + e);
+      if (c >> 31) Tinv[t.T_col[e]] = 1.0 / tm;
+    }
+  }
+}
+
 // wave-level LDS hand-off (the two cells of a wave never leave it)
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -446,6 +526,19 @@ void tsep_matrix(const TSepDev& t, long nnz, const PhysicsDev& ph, double* M, do
                  double* Tmat, double* Tinv, hipStream_t s) {
   hipLaunchKernelGGL(k_tsep_lateral, dim3(blocks(long(t.n_kinds) * t.n_latnnz)), dim3(kTB), 0, s,
                      t);
+  if (t.blk_pt && !(t.probe & 64)) {  // records staged in LDS (probe 64: per-entry A loads)
+    const size_t lds_r = sizeof(double) * 16 * size_t(t.n_layers) + 48 * size_t(t.max_rec);
+    const long B = long(t.blk_pt) * kTB;
+    const unsigned nb = unsigned((nnz + B - 1) / B);
+    if (t.blk_pt == 8)
+      hipLaunchKernelGGL(k_tsep_matrix_lds<8>, dim3(nb), dim3(kTB), lds_r, s, t, nnz,
+                         ph.one_over_peclet, ph.dt_T, M, K, Tmat, Tinv);
+    else
+      hipLaunchKernelGGL(k_tsep_matrix_lds<4>, dim3(nb), dim3(kTB), lds_r, s, t, nnz,
+                         ph.one_over_peclet, ph.dt_T, M, K, Tmat, Tinv);
+    DCP_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const size_t lds = sizeof(double) * 16 * size_t(t.n_layers) + sizeof(int) * size_t(t.n_layers);
   // CSR entries per thread (DCP_TSEP_PT: 4 or 8; default 4)
   const char* env = std::getenv("DCP_TSEP_PT");

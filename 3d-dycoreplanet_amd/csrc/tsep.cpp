@@ -192,6 +192,60 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
                 (i == j ? 1u << 31 : 0u);
     }
   if (bad) return false;
+  // per block of pt x 256 entries (k_tsep_matrix_lds) the sorted distinct A
+  // records (kind n_latnnz + p) of its terms, the entries coded by slot; the
+  // larger block when every list fits the 10-bit slots
+  auto terms = [&](uint32_t cd, int32_t rec[2]) {
+    rec[0] = rec[1] = -1;
+    if ((cd >> 30) & 1u) return;
+    const int p = int(cd & 0xFFFFFu), l = int((cd >> 20) & 0xFFu), dl = int((cd >> 28) & 3u);
+    const int oa = dl == 2 ? l : l - 1;
+    if (oa >= 0) rec[0] = kind[oa] * NLAT + p;
+    if (dl == 1 && l < NL) rec[1] = kind[l] * NLAT + p;
+  };
+  const long nnz = long(Tc.size());
+  std::vector<uint32_t> rcode;
+  std::vector<int32_t> blk_ptr, blk_rec;
+  int blk_pt = 0, max_rec = 0;
+  for (const int pt : {8, 4}) {
+    if (int64_t(NK) * NLAT >= (int64_t(1) << 31)) break;
+    const long B = long(pt) * 256, nblk = (nnz + B - 1) / B;
+    std::vector<std::vector<int32_t>> lists(static_cast<size_t>(nblk));
+    std::vector<uint32_t> rc(code.size());
+    int worst = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(max : worst)
+    for (long bi = 0; bi < nblk; ++bi) {
+      const long e0 = bi * B, e1 = std::min(nnz, e0 + B);
+      std::vector<int32_t>& L = lists[size_t(bi)];
+      for (long e = e0; e < e1; ++e) {
+        int32_t r[2];
+        terms(code[e], r);
+        for (int t = 0; t < 2; ++t)
+          if (r[t] >= 0) L.push_back(r[t]);
+      }
+      std::sort(L.begin(), L.end());
+      L.erase(std::unique(L.begin(), L.end()), L.end());
+      if (L.empty()) L.push_back(0);  // every block stages at least one record
+      worst = std::max(worst, int(L.size()));
+      for (long e = e0; e < e1; ++e) {
+        int32_t r[2];
+        terms(code[e], r);
+        uint32_t sl[2] = {0, 0};
+        for (int t = 0; t < 2; ++t)
+          if (r[t] >= 0) sl[t] = uint32_t(std::lower_bound(L.begin(), L.end(), r[t]) - L.begin());
+        rc[e] = (sl[0] & 1023u) | ((sl[1] & 1023u) << 10) | (code[e] & 0xFFF00000u);
+      }
+    }
+    if (worst > 1023) continue;
+    blk_ptr.assign(size_t(nblk) + 1, 0);
+    for (long bi = 0; bi < nblk; ++bi) blk_ptr[bi + 1] = blk_ptr[bi] + int32_t(lists[bi].size());
+    blk_rec.clear();
+    for (const auto& L : lists) blk_rec.insert(blk_rec.end(), L.begin(), L.end());
+    rcode.swap(rc);
+    blk_pt = pt;
+    max_rec = worst;
+    break;
+  }
   // rhs records per dof, ascending cell
   std::vector<int32_t> sptr(size_t(n_T) + 1, 0), slot(size_t(n_cells) * 8);
   for (int cell = 0; cell < n_cells; ++cell)
@@ -223,6 +277,13 @@ bool build_tsep(Ctx& c, int n_cells, const std::vector<int32_t>& td,
   c.ts_lptr.upload(lptr);
   c.ts_lcon.upload(lcon);
   c.ts_code.upload(code);
+  c.ts_blk_pt = blk_pt;
+  c.ts_max_rec = max_rec;
+  if (blk_pt) {
+    c.ts_rcode.upload(rcode);
+    c.ts_blk_ptr.upload(blk_ptr);
+    c.ts_blk_rec.upload(blk_rec);
+  }
   c.ts_sptr.upload(sptr);
   c.ts_slot.upload(slot);
   c.ts_loc.alloc(size_t(n_colids) * 64);
