@@ -2311,8 +2311,7 @@ __global__ void k_cdk_diag(int n_con, const int32_t* __restrict__ cptr, const in
   const int ci = int(blockIdx.x) * blockDim.x + int(threadIdx.x);
   if (ci >= n_con) return;
   double s[3] = {0, 0, 0};
-  for (int k = cptr[ci]; k < cptr[ci + 1]; ++k) {
-    const int2 r = rec[k];  // lateral table (column id 9 + ab), radial table (layer 3 + c)
+  auto add = [&](int2 r, bool on) {  // r: lateral table (column id 9 + ab), radial (layer 3 + c)
     const double* l = L + 10 * size_t(r.x);
     const double* rr = R + 4 * size_t(r.y);
     double g[3];
@@ -2320,8 +2319,17 @@ __global__ void k_cdk_diag(int n_con, const int32_t* __restrict__ cptr, const in
     for (int d = 0; d < 3; ++d) g[d] = l[1 + d] * rr[1] + l[4 + d] * rr[2] + l[7 + d] * rr[3];
     const double M = l[0] * rr[0], G = g[0] + g[1] + g[2];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) s[d] += fabs(M + nu * G + nu * g[d]);
-  }
+    for (int d = 0; d < 3; ++d) s[d] += on ? fabs(M + nu * G + nu * g[d]) : 0.0;
+  };
+  // a surface node lies in at most 4 cells of its layer: those records loaded
+  // together (clamped, unpredicated), a longer list (none on the shell) after
+  const int k0 = cptr[ci], n = cptr[ci + 1] - k0;
+  int2 r4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r4[j] = rec[k0 + min(j, n - 1)];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) add(r4[j], j < n);
+  for (int k = k0 + 4; k < k0 + n; ++k) add(rec[k], true);
   const int on = mask[ci];  // the row's constrained components (condensation)
 #pragma unroll
   for (int d = 0; d < 3; ++d) cdiag[3 * size_t(ci) + d] = (on >> d) & 1 ? s[d] : 0.0;
