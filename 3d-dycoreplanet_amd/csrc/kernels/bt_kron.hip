@@ -45,20 +45,14 @@ __global__ __launch_bounds__(kTB) void k_btk_lateral(BtkDev b) {
   const int k = gid / b.n_pairs, p = gid - k * b.n_pairs;
   const int32_t* con = b.lcon + size_t(k) * b.n_con;
   double s[6] = {0, 0, 0, 0, 0, 0};
-  auto add = [&](int j, bool on) {
+  for (int j = b.lptr[p]; j < b.lptr[p + 1]; ++j) {
     const double* P = b.P + con[j];  // colid 216 + a 36 + b 12 + i 6 + j 3
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      s[d] += on ? P[d] : 0.0;
-      s[3 + d] += on ? P[108 + d] : 0.0;
+      s[d] += P[d];
+      s[3 + d] += P[108 + d];
     }
-  };
-  // a pair lies in at most 4 columns: those loaded together (clamped,
-  // unpredicated; adding 0.0 for the absent ones leaves the sums bitwise)
-  const int j0 = b.lptr[p], n = b.lptr[p + 1] - j0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) add(j0 + min(q, n - 1), q < n);
-  for (int j = j0 + 4; j < j0 + n; ++j) add(j, true);
+  }
   double* a = b.A + 6 * size_t(gid);
 #pragma unroll
   for (int i = 0; i < 6; ++i) a[i] = s[i];
