@@ -17,7 +17,8 @@
 //     k_btk_entries) the sorted list of the distinct A records (kind, pair)
 //     its entries read, and one 32-bit code per entry: the slots of its one or
 //     two terms in that list, the node level and the level step;
-//   * the list of entries whose row is a constrained (no-normal-flux) node.
+//   * per block the constrained (no-normal-flux) rows its entries lie in, the
+//     entries of such rows carrying the row's local index in the free slot.
 // Anything that does not fit returns false and the B^T tasks stay in use.
 #include <algorithm>
 #include <array>
@@ -215,12 +216,14 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
                 (vc[n].type != 0 ? 1u << 30 : 0u);
     }
   if (bad) return false;
-  std::vector<int32_t> con_entry, con_row;
+  // the row of every entry of a constrained row (-1 elsewhere)
+  std::vector<int32_t> erow(Btc.size(), -1);
+  long n_conent = 0;
   for (int n = 0; n < nv; ++n)
     if (vc[n].type != 0)
       for (int e = Btp[n]; e < Btp[n + 1]; ++e) {
-        con_entry.push_back(e);
-        con_row.push_back(n);
+        erow[size_t(e)] = n;
+        ++n_conent;
       }
   // the records of an entry's terms, in the order of btk_terms (bt_kron.hip)
   auto terms = [&](uint32_t cd, int32_t rec[2]) {
@@ -243,12 +246,21 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
   const long nnz = long(Btc.size());
   const long nblk = (nnz + kBtkBlock - 1) / kBtkBlock;
   if (int64_t(NK) * NPAIR >= (int64_t(1) << 31) || nblk >= (1L << 31)) return false;
-  std::vector<std::vector<int32_t>> blk_list(nblk);
-  int worst = 0;
-#pragma omp parallel for schedule(dynamic, 64) reduction(max : worst)
+  std::vector<std::vector<int32_t>> blk_list(nblk), blk_cons(nblk);
+  int worst = 0, worst_con = 0, bad_con = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(max : worst, worst_con) reduction(+ : bad_con)
   for (long bi = 0; bi < nblk; ++bi) {
     const long e0 = bi * kBtkBlock, e1 = std::min(nnz, e0 + kBtkBlock);
     std::vector<int32_t>& L = blk_list[bi];
+    // the block's constrained rows (their NodeConstraints staged beside the
+    // records); an entry of such a row carries its local index in the slot
+    // field its terms leave free (one of the two on the shell's boundary levels)
+    std::vector<int32_t>& CR = blk_cons[bi];
+    for (long e = e0; e < e1; ++e)
+      if (erow[size_t(e)] >= 0) CR.push_back(erow[size_t(e)]);
+    std::sort(CR.begin(), CR.end());
+    CR.erase(std::unique(CR.begin(), CR.end()), CR.end());
+    worst_con = std::max(worst_con, int(CR.size()));
     for (long e = e0; e < e1; ++e) {
       int32_t r[2];
       terms(code[e], r);
@@ -264,10 +276,23 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
       uint32_t slot[2] = {0, 0};
       for (int t = 0; t < 2; ++t)
         if (r[t] >= 0) slot[t] = uint32_t(std::lower_bound(L.begin(), L.end(), r[t]) - L.begin());
+      if (erow[size_t(e)] >= 0) {
+        const int free_t = r[0] < 0 ? 0 : (r[1] < 0 ? 1 : -1);
+        if (free_t < 0) {
+          ++bad_con;
+        } else {
+          slot[free_t] = uint32_t(std::lower_bound(CR.begin(), CR.end(), erow[size_t(e)]) - CR.begin());
+        }
+      }
       code[e] = (slot[0] & 1023u) | ((slot[1] & 1023u) << 10) | (code[e] & 0x7FF00000u);
     }
   }
-  if (worst > kBtkMaxRec) return false;
+  if (worst > kBtkMaxRec || worst_con > 1023 || bad_con) return false;
+  std::vector<int32_t> blk_cptr(size_t(nblk) + 1, 0), blk_crow;
+  for (long bi = 0; bi < nblk; ++bi) blk_cptr[bi + 1] = blk_cptr[bi] + int32_t(blk_cons[bi].size());
+  blk_crow.reserve(size_t(blk_cptr[nblk]));
+  for (long bi = 0; bi < nblk; ++bi) blk_crow.insert(blk_crow.end(), blk_cons[bi].begin(), blk_cons[bi].end());
+  if (blk_crow.empty()) blk_crow.push_back(0);
   std::vector<int32_t> blk_ptr(size_t(nblk) + 1, 0), blk_rec;
   for (long bi = 0; bi < nblk; ++bi) blk_ptr[bi + 1] = blk_ptr[bi] + int32_t(blk_list[bi].size());
   blk_rec.reserve(size_t(blk_ptr[nblk]));
@@ -276,7 +301,7 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
   c.btk_n_kinds = NK;
   c.btk_n_pairs = NPAIR;
   c.btk_n_con = int(ncon);
-  c.btk_n_conent = int(con_entry.size());
+  c.btk_n_conent = int(n_conent);
   c.btk_ord2lay.upload(ord2lay);
   c.btk_kind.upload(kind);
   c.btk_lptr.upload(lptr);
@@ -285,8 +310,9 @@ bool build_btk(Ctx& c, int n_cells, const std::vector<int32_t>& q2, const std::v
   c.btk_blk_ptr.upload(blk_ptr);
   c.btk_blk_rec.upload(blk_rec);
   c.btk_max_rec = worst;
-  c.btk_con_entry.upload(con_entry);
-  c.btk_con_row.upload(con_row);
+  c.btk_blk_cptr.upload(blk_cptr);
+  c.btk_blk_crow.upload(blk_crow);
+  c.btk_max_con = worst_con;
   c.btk_A.alloc(size_t(NK) * NPAIR * 6);
   c.btk = true;
   return true;

@@ -414,7 +414,8 @@ struct Ctx {
   bool btk = false;
   int btk_n_layers = 0, btk_n_kinds = 0, btk_n_pairs = 0, btk_n_con = 0, btk_n_conent = 0;
   int btk_max_rec = 0;
-  DBuf<int32_t> btk_ord2lay, btk_kind, btk_lptr, btk_lcon, btk_con_entry, btk_con_row;
+  DBuf<int32_t> btk_ord2lay, btk_kind, btk_lptr, btk_lcon, btk_blk_cptr, btk_blk_crow;
+  int btk_max_con = 0;
   DBuf<int32_t> btk_blk_ptr, btk_blk_rec;
   DBuf<uint32_t> btk_code;
   DBuf<double> btk_A;
@@ -437,8 +438,9 @@ struct Ctx {
     b.code = btk_code.p;
     b.blk_ptr = btk_blk_ptr.p;
     b.blk_rec = btk_blk_rec.p;
-    b.con_entry = btk_con_entry.p;
-    b.con_row = btk_con_row.p;
+    b.blk_cptr = btk_blk_cptr.p;
+    b.blk_crow = btk_blk_crow.p;
+    b.max_con = btk_max_con;
     b.A = btk_A.p;
     return b;
   }

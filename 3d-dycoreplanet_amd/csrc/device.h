@@ -381,12 +381,15 @@ struct BtkDev {
   const int32_t* lptr = nullptr;     // [n_pairs + 1] lateral (node, vertex) pairs
   const int32_t* lcon = nullptr;     // [n_kinds][n_con] offset of the pair's P entry
   // per entry: slot of the first term (bits 0-9), of the second (10-19),
-  // node level lambda (20-27), l - lambda / 2 + 1 (28-29), constrained row (30)
+  // node level lambda (20-27), l - lambda / 2 + 1 (28-29), constrained row
+  // (30; then the slot field of the absent term holds the row's index in the
+  // block's constrained rows)
   const uint32_t* code = nullptr;      // [nnz of B^T]
   const int32_t* blk_ptr = nullptr;    // [blocks + 1] record lists
   const int32_t* blk_rec = nullptr;    // records kind n_pairs + pair
-  const int32_t* con_entry = nullptr;  // entries of constrained rows
-  const int32_t* con_row = nullptr;    // and their rows
+  const int32_t* blk_cptr = nullptr;  // [blocks + 1] constrained rows of each block
+  const int32_t* blk_crow = nullptr;  // their row (velocity node) ids
+  int max_con = 0;                    // largest such list
   double* A = nullptr;               // [n_kinds][n_pairs][6]
 };
 void btk_assemble(const BtkDev& b, long nnz, const NodeConstraint* vcon, double* Bt,

@@ -23,9 +23,9 @@
 //                  two layer terms from LDS, written once (no zero fill, no
 //                  colouring, no atomics) through an LDS stage so each store
 //                  instruction writes 512 contiguous bytes,
-//   k_btk_con      the entries of constrained rows (no-normal-flux nodes):
-//                  the value k_btk_entries wrote, condensed with the row's
-//                  constraint C^T.
+//                  An entry of a constrained row (no-normal-flux node) is
+//                  condensed with the row's constraint C^T before its store
+//                  (the block's constraints staged in LDS beside the records).
 // (Reading A per entry from L2 instead -- 3 16-byte loads per term at 64
 // scattered lines per wave instruction -- cost 150 of the kernel's 270 us.)
 #include <hip/hip_runtime.h>
@@ -67,8 +67,8 @@ __global__ __launch_bounds__(kTB) void k_btk_lateral(BtkDev b) {
 // Branch-free (the lanes of a wave hold every case; as branches each case
 // took its own pass of LDS reads): both terms always, an absent one with
 // factors q = 0, which leaves v bitwise as without it (v - (A 0 + A 0) = v).
-__device__ __forceinline__ void btk_terms(int n_layers, const double* sq, int lam, int dl,
-                                          const double2* r0, const double2* r1, double v[3]) {
+__device__ __forceinline__ bool btk_terms(int n_layers, const double* sq, int lam, int dl,
+                                          const double2* srec, int s0, int s1, double v[3]) {
   const int m = lam >> 1;
   const bool odd = lam & 1;
   const int L0 = odd || dl == 2 ? m : m - 1;
@@ -81,6 +81,9 @@ __device__ __forceinline__ void btk_terms(int n_layers, const double* sq, int la
   const double2 Q1 = *reinterpret_cast<const double2*>(sq + i1);
   const double q01a = p0 ? Q0.x : 0.0, q2a = p0 ? Q0.y : 0.0;
   const double q01b = p1 ? Q1.x : 0.0, q2b = p1 ? Q1.y : 0.0;
+  // an absent term's slot may hold a constrained-row index: read record 0
+  const double2* r0 = srec + 3 * (p0 ? s0 : 0);
+  const double2* r1 = srec + 3 * (p1 ? s1 : 0);
   const double2 A0 = r0[0], A1 = r0[1], A2 = r0[2];
   const double2 B0 = r1[0], B1 = r1[1], B2 = r1[2];
   v[0] = 0.0 - (A0.x * q01a + A1.y * q2a);
@@ -89,15 +92,43 @@ __device__ __forceinline__ void btk_terms(int n_layers, const double* sq, int la
   v[0] -= B0.x * q01b + B1.y * q2b;
   v[1] -= B0.y * q01b + B2.x * q2b;
   v[2] -= B1.x * q01b + B2.y * q2b;
+  return p0;
+}
+
+// an entry of a constrained row: C^T v (condensation(); type 2: the normal
+// component k eliminated, C[d][d] = 1 and C[k][d] = w[d] for d != k; types 1 /
+// 3: zero rows), the sums in the order of the former k_btk_con
+__device__ __forceinline__ void btk_condense(const NodeConstraint& nc, double v[3]) {
+  double C[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C[r][c] = 0.0;
+  if (nc.type == 0) {
+    C[0][0] = C[1][1] = C[2][2] = 1.0;
+  } else if (nc.type == 2) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+      if (d != nc.k) {
+        C[d][d] = 1.0;
+        C[nc.k][d] = nc.w[d];
+      }
+  }
+  double o[3];
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) o[jj] = C[0][jj] * v[0] + C[1][jj] * v[1] + C[2][jj] * v[2];
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) v[jj] = o[jj];
 }
 
 // The block's records are staged into LDS first. The 64 entries of a wave
 // (per u) are 192 consecutive doubles of B^T: staged in LDS so each store
 // instruction writes 512 contiguous bytes (every lane storing its own 24 bytes
 // instead: 392 against 382 us per assembly, profiles/r06/r06al_direct_store.log).
-// Entries of constrained rows are written unconstrained here and overwritten
-// by k_btk_con (same stream, after).
-__global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double* __restrict__ Bt) {
+// Entries of constrained rows are condensed before the store.
+__global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz,
+                                                     const NodeConstraint* __restrict__ vcon,
+                                                     double* __restrict__ Bt) {
   extern __shared__ __attribute__((aligned(16))) double sq[];
   double2* srec = reinterpret_cast<double2*>(sq + 12 * b.n_layers);
   __shared__ double stage[kTB / 64][192];
@@ -136,6 +167,12 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
     const int j = i / 3;
     srec[i] = A2[3 * size_t(b.blk_rec[r0 + j]) + (i - 3 * j)];
   }
+  // the block's constrained rows (k_btk_con folded in: 11 us at r=5)
+  NodeConstraint* scon = reinterpret_cast<NodeConstraint*>(srec + 3 * size_t(b.max_rec));
+  {
+    const int c0 = b.blk_cptr[blk], nc = b.blk_cptr[blk + 1] - c0;
+    for (int i = threadIdx.x; i < nc; i += kTB) scon[i] = vcon[b.blk_crow[c0 + i]];
+  }
   for (int i = threadIdx.x; i < 12 * b.n_layers; i += kTB)
     sq[i] = b.Q[12 * size_t(b.ord2lay[i / 12]) + i % 12];
   __syncthreads();
@@ -146,8 +183,9 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
     const uint32_t cu = code[u];
     const int s0 = int(cu & 1023u), s1 = int((cu >> 10) & 1023u);
     double v[3];
-    btk_terms(b.n_layers, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u), srec + 3 * s0,
-              srec + 3 * s1, v);
+    const bool p0 = btk_terms(b.n_layers, sq, int((cu >> 20) & 0xFFu), int((cu >> 28) & 3u), srec,
+                              s0, s1, v);
+    if ((cu >> 30) & 1u) btk_condense(scon[p0 ? s1 : s0], v);
     stage[wave][3 * lane] = v[0];
     stage[wave][3 * lane + 1] = v[1];
     stage[wave][3 * lane + 2] = v[2];
@@ -175,49 +213,16 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz, double*
   }
 }
 
-// entries of constrained rows: out = C^T v, v the value k_btk_entries wrote
-// (condensation(), type 2: the normal component eliminated; types 1 / 3: zero
-// rows)
-__global__ __launch_bounds__(kTB) void k_btk_con(int n_conent, const int32_t* __restrict__ con_entry,
-                                                 const int32_t* __restrict__ con_row,
-                                                 const NodeConstraint* __restrict__ vcon,
-                                                 double* __restrict__ Bt) {
-  const int i = int(blockIdx.x) * kTB + int(threadIdx.x);
-  if (i >= n_conent) return;
-  double* dst = Bt + 3 * size_t(con_entry[i]);
-  const double v[3] = {dst[0], dst[1], dst[2]};
-  const NodeConstraint nc = vcon[con_row[i]];
-  double C[3][3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int s = 0; s < 3; ++s) C[r][s] = 0.0;
-  if (nc.type == 0) {
-    C[0][0] = C[1][1] = C[2][2] = 1.0;
-  } else if (nc.type == 2) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-      if (d != nc.k) {
-        C[d][d] = 1.0;
-        C[nc.k][d] = nc.w[d];
-      }
-  }
-#pragma unroll
-  for (int jj = 0; jj < 3; ++jj) dst[jj] = C[0][jj] * v[0] + C[1][jj] * v[1] + C[2][jj] * v[2];
-}
-
 }  // namespace
 
 void btk_assemble(const BtkDev& b, long nnz, const NodeConstraint* vcon, double* Bt,
                   hipStream_t s) {
-  const size_t lds_e = sizeof(double) * 12 * size_t(b.n_layers) + 48 * size_t(b.max_rec);
+  const size_t lds_e = sizeof(double) * 12 * size_t(b.n_layers) + 48 * size_t(b.max_rec) +
+                       sizeof(NodeConstraint) * size_t(b.max_con);
   hipLaunchKernelGGL(k_btk_lateral, dim3((b.n_kinds * b.n_pairs + kTB - 1) / kTB), dim3(kTB), 0, s,
                      b);
   hipLaunchKernelGGL(k_btk_entries, dim3(unsigned((nnz + kBtkBlock - 1) / kBtkBlock)), dim3(kTB),
-                     lds_e, s, b, nnz, Bt);
-  if (b.n_conent > 0)
-    hipLaunchKernelGGL(k_btk_con, dim3((b.n_conent + kTB - 1) / kTB), dim3(kTB), 0, s, b.n_conent,
-                       b.con_entry, b.con_row, vcon, Bt);
+                     lds_e, s, b, nnz, vcon, Bt);
   DCP_HIP_CHECK(hipGetLastError());
 }
 
