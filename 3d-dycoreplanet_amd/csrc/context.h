@@ -427,8 +427,6 @@ struct Ctx {
     b.n_con = btk_n_con;
     b.n_conent = btk_n_conent;
     b.max_rec = btk_max_rec;
-    const char* pr = std::getenv("DCP_BTK_PROBE");
-    b.probe = pr ? std::atoi(pr) : 0;
     b.P = bt_P.p;
     b.Q = bt_Q;
     b.ord2lay = btk_ord2lay.p;

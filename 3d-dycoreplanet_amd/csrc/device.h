@@ -373,7 +373,6 @@ constexpr int kBtkMaxRec = 1023;  // slots per block (10-bit slot fields of the 
 struct BtkDev {
   int n_layers = 0, n_kinds = 0, n_pairs = 0, n_con = 0, n_conent = 0;
   int max_rec = 0;                   // largest record list of a block
-  int probe = 0;                     // DCP_BTK_PROBE timing variants (0: the real kernels)
   const double* P = nullptr;         // column factors (k_bt_coltab)
   const double* Q = nullptr;         // layer factors by layer id (k_bt_laytab)
   const int32_t* ord2lay = nullptr;  // [n_layers]

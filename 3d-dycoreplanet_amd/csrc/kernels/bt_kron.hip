@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kTB) void k_btk_entries(BtkDev b, long nnz,
   // load issued up front and unpredicated (indices clamped; predicated loads
   // each got a wait of their own), so the staging costs two dependent
   // latencies (record id, record), not two per trip. Measured at r=5
-  // (profiles/r06/r06ae_btk_probe.log): a loop over the doubles 384 us per
+  // (profiles/r06/r06ae_btk_staging_variants.log): a loop over the doubles 384 us per
   // assembly, this 370 us, a thread per record (48-byte strided loads) 532 us.
   const int r0 = b.blk_ptr[blk], nr = b.blk_ptr[blk + 1] - r0;  // nr >= 1
   const double2* A2 = reinterpret_cast<const double2*>(b.A);

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """assemble_nse_system at refine R with the Kronecker-form B^T (default) and
 with the B^T row tasks (DCP_BT_KRON=0): medians over alternating rounds, and
-the largest relative B^T difference between the two."""
+the largest relative B^T difference between the two. PROBES sets
+DCP_BTK_PROBE per timing row; the probe variants of round 6 (no A reads, no
+stores, direct stores, staging forms) were measured and then removed from the
+kernel, so today every value times the real kernels (the logs under
+profiles/r06/ keep those measurements)."""
 import os
 import sys
 
