@@ -2725,7 +2725,10 @@ int dcp_assemble_nse_system(dcp_ctx* ctx, int flags) {
       bt_rows = c.bt_rows && !full;
       if (!bt_rows && !c.first_touch_Bt) c.Bt_val.zero(c.stream);
       if (!bt_rows && scatter_B && !c.first_touch_B) c.B_val.zero(c.stream);
-      c.con_diag.zero(c.stream);
+      // k_cdk_diag (below) assigns every constrained diagonal: no zero fill
+      const bool cdk_all = c.cdk && bt_rows && c.rhs_cell_order && (flags & DCP_ASSEMBLE_RHS) &&
+                           c.con_diag.n == 3 * size_t(c.n_con);
+      if (!cdk_all) c.con_diag.zero(c.stream);
       out.A = full ? c.A_val.p : nullptr;
       out.Bt = bt_rows ? nullptr : c.Bt_val.p;
       out.B = scatter_B && !bt_rows ? c.B_val.p : nullptr;
